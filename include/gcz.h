@@ -1,0 +1,137 @@
+/*
+ * gcz.h — C ABI of the MI355X-native shared_tree construction engine (libgcz).
+ *
+ * This is the drop-in boundary for the reference's hot path.  The reference
+ * (Quinten-van-Woerkom/genome-compression) has no FFI of its own: its
+ * replaceable engine is `tree_constructor` behind the `shared_tree`
+ * constructors (include/shared_tree.h:158-162, src/shared_tree.cpp:207-215,
+ * called from compress.cpp:183 and tests/test.cpp:240,274,298,339,395).  The
+ * entry points below are what a binding of that engine needs: plain pointers
+ * and sizes, no C++/torch types.  include/shared_tree.h (this repo) rebuilds the
+ * reference's C++ surface on top of them; INTEGRATION.md shows the ctypes /
+ * C++ bindings a maintainer adds.
+ *
+ * Word layout (reference in-memory `pointer`, include/shared_tree.h:73-76):
+ *   bits 0-28 index, bit 29 mirror, bit 30 transpose, bit 31 invariant.
+ * A node is two words (left, right); the null child is 0x9fffffff.
+ * Leaves are nibble-packed `dna` values (include/dna.h:20-32,73-74).
+ */
+#ifndef GCZ_H
+#define GCZ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(GCZ_BUILDING)
+#define GCZ_API __attribute__((visibility("default")))
+#else
+#define GCZ_API
+#endif
+
+/* Status codes.  The reference never returns errors: it prints and exits
+ * (src/dna.cpp:44-47 unknown symbol -> exit(1); src/fasta_reader.cpp:15-18,109-112
+ * I/O -> exit(1)).  The C++ wrapper maps these codes back to that behaviour. */
+enum {
+  GCZ_OK = 0,
+  GCZ_ERR_SYMBOL = 1,   /* unknown nucleotide symbol; see gcz_info.error_offset */
+  GCZ_ERR_IO = 2,       /* file could not be opened/read */
+  GCZ_ERR_CAPACITY = 3, /* more than 2^29-1 unique items in one layer */
+  GCZ_ERR_DEVICE = 4,   /* HIP runtime error */
+  GCZ_ERR_ARG = 5,      /* invalid argument (L outside 1..16, null pointer, ...) */
+  GCZ_ERR_EMPTY = 6     /* fewer than L bases: the reference has no tree to build */
+};
+
+#define GCZ_NULL_WORD 0x9fffffffu
+#define GCZ_MAX_LAYERS 64
+
+typedef struct gcz_ctx gcz_ctx;     /* one device + stream + workspace */
+typedef struct gcz_tree gcz_tree;   /* host-resident shared tree */
+
+/* Summary of the last build (shared_tree::depth/leaf_count/node_count, shared_tree.h:164-170). */
+typedef struct {
+  int status;                        /* GCZ_* of the last build */
+  int L;                             /* leaf length dna::size() */
+  int n_layers;                      /* node layers; depth() = n_layers + 1 */
+  uint32_t root;                     /* root pointer word (keeps m/t bits) */
+  uint64_t n_strands;                /* S = width() of the tree */
+  uint64_t n_leaves;                 /* unique canonical leaves */
+  uint64_t layer_size[GCZ_MAX_LAYERS];
+  uint64_t error_offset;             /* GCZ_ERR_SYMBOL: byte offset into the bases */
+  int error_symbol;                  /* the offending byte */
+  double build_ms;                   /* device time of the build (hipEvents) */
+} gcz_info;
+
+/* ---- device context ---------------------------------------------------- */
+GCZ_API int gcz_ctx_create(int device, gcz_ctx **out);
+GCZ_API void gcz_ctx_destroy(gcz_ctx *ctx);
+/* Launch on a caller stream (hipStream_t); NULL restores the context's own stream. */
+GCZ_API int gcz_ctx_set_stream(gcz_ctx *ctx, void *hip_stream);
+GCZ_API void *gcz_ctx_stream(gcz_ctx *ctx);
+GCZ_API const char *gcz_ctx_last_error(gcz_ctx *ctx);
+
+/* ---- builds ------------------------------------------------------------ *
+ * Replace tree_constructor::reduce (src/shared_tree.cpp:719-763).  The result
+ * stays resident in HBM inside ctx until the next build; fetch it with
+ * gcz_info_get / gcz_copy_leaves / gcz_copy_layer / gcz_tree_fetch.
+ * All builds are asynchronous on the context stream except that they return
+ * after validating results (one small D2H of the level counts). */
+
+/* bases: device pointer to raw nucleotide bytes (no FASTA line structure);
+ * the tail beyond a multiple of L is ignored (src/fasta_reader.cpp:60-61). */
+GCZ_API int gcz_build_device_bases(gcz_ctx *ctx, const void *d_bases, uint64_t nbases, int L);
+/* leaves: device pointer to S nibble-packed strands (shared_tree(std::vector<dna>&),
+ * src/shared_tree.cpp:212-215). */
+GCZ_API int gcz_build_device_leaves(gcz_ctx *ctx, const uint64_t *d_leaves, uint64_t S, int L);
+/* Host conveniences: FASTA bytes (line structure per src/fasta_reader.cpp:40-68)
+ * or host leaves; copied to the device, then built. */
+GCZ_API int gcz_build_host_fasta(gcz_ctx *ctx, const void *fasta, uint64_t nbytes, int L);
+GCZ_API int gcz_build_host_leaves(gcz_ctx *ctx, const uint64_t *leaves, uint64_t S, int L);
+
+GCZ_API int gcz_info_get(gcz_ctx *ctx, gcz_info *out);
+GCZ_API int gcz_copy_leaves(gcz_ctx *ctx, uint64_t *host_out);                /* n_leaves u64 */
+GCZ_API int gcz_copy_layer(gcz_ctx *ctx, int layer, uint32_t *host_out);      /* 2*layer_size words */
+
+/* Device pointers of the last build (valid until the next build). */
+GCZ_API const uint64_t *gcz_device_leaves(gcz_ctx *ctx);
+GCZ_API const uint32_t *gcz_device_layer(gcz_ctx *ctx, int layer);
+
+/* ---- per-kernel timing (hipEvents on the launch stream) ---------------- */
+GCZ_API int gcz_profile_enable(gcz_ctx *ctx, int on);
+/* Kernel `k` of the profile table: name, launches, total ms.  Returns 0, or -1 past the end. */
+GCZ_API int gcz_profile_entry(gcz_ctx *ctx, int k, const char **name, uint64_t *launches, double *total_ms);
+GCZ_API void gcz_profile_reset(gcz_ctx *ctx);
+
+/* ---- host tree (shared_tree container operations) ---------------------- */
+GCZ_API gcz_tree *gcz_tree_new(void);
+GCZ_API void gcz_tree_free(gcz_tree *t);
+GCZ_API int gcz_tree_fetch(gcz_ctx *ctx, gcz_tree *t);          /* D2H of the last build */
+GCZ_API int gcz_tree_n_layers(const gcz_tree *t);
+GCZ_API uint64_t gcz_tree_n_leaves(const gcz_tree *t);
+GCZ_API uint64_t gcz_tree_layer_size(const gcz_tree *t, int layer);
+GCZ_API uint32_t gcz_tree_root(const gcz_tree *t);
+GCZ_API int gcz_tree_L(const gcz_tree *t);
+GCZ_API const uint64_t *gcz_tree_leaves(const gcz_tree *t);
+GCZ_API const uint32_t *gcz_tree_layer(const gcz_tree *t, int layer);
+/* Frequency sort (src/shared_tree.cpp:316-483), bytes() (:488-496),
+ * serialize() (:504-513), width() (shared_tree.h:165). */
+GCZ_API void gcz_tree_sort(gcz_tree *t);
+GCZ_API uint64_t gcz_tree_bytes(const gcz_tree *t);
+GCZ_API uint64_t gcz_tree_serialize(const gcz_tree *t, uint8_t *buf, uint64_t cap);
+GCZ_API uint64_t gcz_tree_width(const gcz_tree *t);
+
+/* ---- host utilities ---------------------------------------------------- */
+/* FASTA line contract of src/fasta_reader.cpp:40-68 (headers, blank lines);
+ * writes the concatenated bases to out (capacity >= n) and returns their count. */
+GCZ_API uint64_t gcz_fasta_extract(const uint8_t *file, uint64_t n, uint8_t *out);
+/* Synthetic genomes (genome-compression_amd/csrc/synth.h), multi-threaded. */
+GCZ_API void gcz_synth_fill(char *out, int kind, uint64_t seed, uint64_t begin, uint64_t end);
+GCZ_API uint64_t gcz_synth_default_seed(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

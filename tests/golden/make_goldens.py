@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors of the shared_tree build from the COMPILED REFERENCE.
+
+Runs only in the build container (needs /root/reference and `make -C oracle ref`).
+Every expected value committed under tests/golden/ comes from
+oracle/_ref/ref_harness, i.e. from the reference's own src/*.cpp:
+
+  corpus/    the 13 bundled DNA files (data files the reference's tests hold), L=12
+  lsweep/    chmpxx at every leaf length L = 1..16
+  fasta/     FASTA line-structure edge cases (inputs written here, tiny)
+  vectors/   shared_tree(std::vector<dna>&) inputs (u64 leaves), incl. the reference
+             tests' dna::random() vectors (tests/test.cpp:234-291,361-409)
+  synth/     synthetic genomes of genome-compression_amd/csrc/synth.h (hashes only)
+  full/      complete dumps (gzip) of chmpxx and hehcmv for debugging
+
+manifest.json maps every case to its inputs and the reference's outputs
+(sha256 of leaves.bin / layers.bin / unsorted.dag / dag, counts, root, ratio).
+
+usage: python tests/golden/make_goldens.py [--synth-large]
+"""
+import gzip
+import hashlib
+import json
+import os
+import random
+import shutil
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+HARNESS = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+GEN = os.path.join(REPO, "oracle", "_ref", "gen_synth")
+DATA = os.path.join(HERE, "data")
+CORPUS = ["chmpxx", "chntxx", "edited", "hehcmv", "humdyst", "humghcs", "humhbb",
+          "humhdab", "humprtb", "merged", "mpomtcg", "mtpacga", "vaccg"]
+
+MASK64 = (1 << 64) - 1
+
+
+def sha(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 22), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def run_dump(mode, inp, L, tmp, name):
+    prefix = os.path.join(tmp, name)
+    p = subprocess.run([HARNESS, mode, inp, str(L), prefix], capture_output=True, text=True)
+    if p.returncode != 0:
+        return {"exit": p.returncode, "stderr": p.stderr.strip()}
+    with open(prefix + ".json") as f:
+        meta = json.load(f)
+    meta.pop("build_ms", None)
+    meta["exit"] = 0
+    for ext in ("leaves.bin", "layers.bin", "unsorted.dag", "dag"):
+        meta["sha_" + ext.replace(".", "_")] = sha(prefix + "." + ext)
+    return meta
+
+
+# --- leaf helpers (restated for input generation only) ---------------------
+def transposed(v):
+    v = ((v >> 1) & 0x5555555555555555) | ((v & 0x5555555555555555) << 1)
+    v = ((v >> 2) & 0x3333333333333333) | ((v & 0x3333333333333333) << 2)
+    return v & MASK64
+
+
+def mirrored(v, L):
+    r = 0
+    for i in range(L):
+        r |= ((v >> (4 * (L - 1 - i))) & 0xF) << (4 * i)
+    return r
+
+
+def ref_random(seed):
+    return int(subprocess.run([HARNESS, "random", str(seed)], capture_output=True,
+                              text=True, check=True).stdout)
+
+
+def write_leaves(path, vals):
+    with open(path, "wb") as f:
+        for v in vals:
+            f.write(int(v & MASK64).to_bytes(8, "little"))
+
+
+def fasta_cases():
+    """Tiny FASTA inputs exercising fasta_reader.cpp:40-68."""
+    rnd = random.Random(7)
+    acgt = lambda n: "".join(rnd.choice("ACGT") for _ in range(n))
+    c = {}
+    c["multi_record"] = ">seq1 some description\n" + acgt(61) + "\n" + acgt(60) + "\n>seq2\n" + acgt(77) + "\n"
+    c["blank_lines"] = acgt(30) + "\n\n" + acgt(40) + "\n\n\n" + acgt(41) + "\n"
+    c["mixed_case_iupac"] = "".join(rnd.choice("ACGTRYKMBVDHSWN-acgtrykmbvdhswn") for _ in range(600))
+    c["crlf"] = ">h\r\n" + acgt(30) + "\r\n" + acgt(30) + "\r\n"
+    c["two_headers"] = ">h1\n>h2\n" + acgt(48) + "\n"
+    c["blank_then_header"] = acgt(24) + "\n\n>h\n" + acgt(24) + "\n"
+    c["bad_tail_ok"] = acgt(24) + "U"
+    c["bad_symbol"] = acgt(30) + "U" + acgt(30)
+    c["exactly_L"] = acgt(12)
+    c["no_trailing_newline"] = ">x\n" + acgt(50) + "\n" + acgt(50)
+    c["trailing_newlines"] = acgt(100) + "\n\n\n\n"
+    c["header_no_newline_at_eof"] = acgt(100) + "\n>tail"
+    c["header_skip_then_data"] = ">a\n" + acgt(13) + "\n>b\n" + acgt(35) + "\n>c\n" + acgt(36)
+    c["long_lines"] = ">x\n" + "\n".join(acgt(1000) for _ in range(20)) + "\n"
+    # IUPAC stress: palindromes, complements, mirrors, self-transposed S/W/N/- runs
+    syms = "ACGTRYKMBVDHSWN-"
+    parts = []
+    for _ in range(900):
+        k = rnd.randrange(7)
+        s = "".join(rnd.choice(syms) for _ in range(12))
+        if k == 0:
+            half = "".join(rnd.choice(syms) for _ in range(6)); s = half + half[::-1]
+        elif k == 1:
+            s = "".join(rnd.choice("SWN-") for _ in range(12))
+        elif k == 2 and parts:
+            s = parts[rnd.randrange(len(parts))]
+        elif k == 3 and parts:
+            comp = {"A": "T", "T": "A", "C": "G", "G": "C", "R": "Y", "Y": "R", "K": "M", "M": "K",
+                    "B": "V", "V": "B", "D": "H", "H": "D", "S": "S", "W": "W", "N": "N", "-": "-"}
+            s = "".join(comp[x] for x in parts[rnd.randrange(len(parts))])
+        elif k == 4 and parts:
+            s = parts[rnd.randrange(len(parts))][::-1]
+        parts.append(s)
+    seq = "".join(parts)
+    seq = "".join(ch.lower() if rnd.random() < 0.3 else ch for ch in seq)
+    c["iupac_stress"] = ">iupac stress\n" + "\n".join(seq[i:i + 60] for i in range(0, len(seq), 60)) + "\n"
+    return c
+
+
+def vector_cases():
+    rnd = random.Random(11)
+    v = {}
+    a = ref_random(0)
+    t = transposed(a)
+    v["ref_tree_transposition"] = (12, [a, a, t, a, a, t, t, t])          # tests/test.cpp:234-264
+    a1, b2, c3 = ref_random(1), ref_random(2), ref_random(3)
+    m = {"a": a1, "b": b2, "c": c3}
+    v["ref_frequency_sort"] = (12, [m[x] for x in "bbbacbacbabacacacabcaaaaaaaaaaaaaa"])  # :266-291
+    v["ref_serialization"] = (12, [ref_random(0), ref_random(1), ref_random(1), ref_random(0),
+                                   ref_random(2), ref_random(0)])                     # :361-409
+    base = [rnd.getrandbits(48) for _ in range(6)]
+    pool = []
+    for x in base:
+        pool += [x, transposed(x), mirrored(x, 12), mirrored(transposed(x), 12)]
+    for S in (1, 2, 3, 4, 5, 6, 7, 8, 9, 15, 16, 17, 31, 32, 33, 100, 1000, 4097):
+        v[f"pool_S{S}"] = (12, [rnd.choice(pool) for _ in range(S)])
+    v["random48_S10000"] = (12, [rnd.getrandbits(48) for _ in range(10000)])
+    pal = []
+    for _ in range(300):
+        h = [rnd.randrange(16) for _ in range(6)]
+        nib = h + h[::-1]
+        pal.append(sum(n << (4 * i) for i, n in enumerate(nib)))
+    v["palindromes_S3000"] = (12, [rnd.choice(pal + pool) for _ in range(3000)])
+    full = [MASK64, MASK64 - 1, 0, 1, 1 << 63, 0x0123456789ABCDEF, 0xFEDCBA9876543210]
+    full += [rnd.getrandbits(64) for _ in range(20)]
+    v["L16_edges_S5000"] = (16, [rnd.choice(full + [transposed(x) for x in full]) for _ in range(5000)])
+    for L in (1, 2, 5):
+        v[f"L{L}_small_alphabet"] = (L, [rnd.getrandbits(4 * L) for _ in range(3000)])
+    return v
+
+
+def main():
+    synth_large = "--synth-large" in sys.argv
+    if not os.path.exists(HARNESS):
+        sys.exit("build the reference harness first: make -C oracle ref")
+    if not os.path.exists(GEN):
+        subprocess.run(["gcc", "-O2", "-pthread", "-o", GEN,
+                        os.path.join(REPO, "genome-compression_amd", "csrc", "gen_synth.c")], check=True)
+    manifest_path = os.path.join(HERE, "manifest.json")
+    manifest = {}
+    if os.path.exists(manifest_path):
+        with open(manifest_path) as f:
+            manifest = json.load(f)
+    tmp = tempfile.mkdtemp(prefix="gcz_golden_")
+    try:
+        for name in CORPUS:
+            manifest[f"corpus/{name}"] = {"kind": "fasta", "input": f"data/{name}", "L": 12,
+                                          "expect": run_dump("dump", os.path.join(DATA, name), 12, tmp, name)}
+        for L in range(1, 17):
+            manifest[f"lsweep/chmpxx_L{L}"] = {"kind": "fasta", "input": "data/chmpxx", "L": L,
+                                               "expect": run_dump("dump", os.path.join(DATA, "chmpxx"), L, tmp, f"c{L}")}
+        os.makedirs(os.path.join(HERE, "fasta"), exist_ok=True)
+        for name, text in fasta_cases().items():
+            path = os.path.join(HERE, "fasta", name + ".fa")
+            with open(path, "wb") as f:
+                f.write(text.encode())
+            manifest[f"fasta/{name}"] = {"kind": "fasta", "input": f"fasta/{name}.fa", "L": 12,
+                                         "expect": run_dump("dump", path, 12, tmp, name)}
+        os.makedirs(os.path.join(HERE, "vectors"), exist_ok=True)
+        for name, (L, vals) in vector_cases().items():
+            path = os.path.join(HERE, "vectors", name + ".u64")
+            write_leaves(path, vals)
+            manifest[f"vectors/{name}"] = {"kind": "leaves", "input": f"vectors/{name}.u64", "L": L,
+                                           "expect": run_dump("dumpleaves", path, L, tmp, name)}
+        synth = [(0, 1_000_000), (0, 10_000_000), (1, 10_000_000), (0, 100_000_003)]
+        if synth_large:
+            synth += [(1, 100_000_000), (0, 1_000_000_000)]
+        for kind, n in synth:
+            key = f"synth/{'uniform' if kind == 0 else 'tandem'}_{n}"
+            if key in manifest and not synth_large:
+                continue
+            path = os.path.join(tmp, "synth.txt")
+            subprocess.run([GEN, str(kind), str(n), path], check=True)
+            manifest[key] = {"kind": "synth", "synth_kind": kind, "nbases": n, "L": 12,
+                             "expect": run_dump("dump", path, 12, tmp, "synth")}
+            os.remove(path)
+        os.makedirs(os.path.join(HERE, "full"), exist_ok=True)
+        for name in ("chmpxx", "hehcmv"):
+            for ext in ("leaves.bin", "layers.bin", "unsorted.dag", "dag"):
+                with open(os.path.join(tmp, f"{name}.{ext}"), "rb") as src, \
+                        open(os.path.join(HERE, "full", f"{name}.{ext}.gz"), "wb") as raw, \
+                        gzip.GzipFile(fileobj=raw, mode="wb", mtime=0) as dst:
+                    shutil.copyfileobj(src, dst)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    with open(manifest_path, "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+        f.write("\n")
+    print(f"wrote {len(manifest)} cases to {manifest_path}")
+
+
+if __name__ == "__main__":
+    main()
