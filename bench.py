@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""Benchmark: shared_tree build throughput (bases/s) on MI355X.
+
+One step = one full device build (leaf pack -> every level's hash-cons ->
+unique nodes/leaves + root resident in HBM) of the configured synthetic genome,
+with the ASCII bases already resident in HBM (SURVEY §8(d) timing scope).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config uniform_1g]
+
+N > 1 is launched by torch.distributed.run (one process per GPU).  Each rank
+then builds its own shard genome (a different seed, same size): the per-GPU
+work is fixed, so the scaling mode is "weak"; no collective is on the data
+path (multi-GPU).
+
+Printed (rank 0): ONE JSON line with value, roofline of the dominant kernel,
+the CPU baseline (compiled reference on this host, bounded sample) and the
+parity verdict against the reference goldens.
+"""
+import argparse
+import hashlib
+import importlib.util
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+METRIC = "bases/sec shared_tree build, 1 Gbase synthetic, 1/2/4/8 MI355X; ratio bit-exact"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+CONFIGS = {
+    "uniform_1g": {"kind": 0, "nbases": 1_000_000_000, "golden": "synth/uniform_1000000000"},
+    "uniform_100m": {"kind": 0, "nbases": 100_000_003, "golden": "synth/uniform_100000003"},
+    "tandem_100m": {"kind": 1, "nbases": 100_000_000, "golden": "synth/tandem_100000000"},
+    "tandem_3g2": {"kind": 1, "nbases": 3_200_000_000, "golden": None},
+}
+
+
+def load_gcz():
+    path = os.path.join(REPO, "genome-compression_amd", "gcz.py")
+    spec = importlib.util.spec_from_file_location("gcz", path)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["gcz"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes):
+    """Algorithmic HBM bytes of all launches of `kernel` in one build:
+    streamed bytes + one 64-B sector per random table/group access."""
+    pk = []
+    n = S
+    while True:
+        p = (n + 1) // 2
+        pk.append(p)
+        if p == 1:
+            break
+        n = p
+    if kernel == "leaf_insert":     # ASCII in, provisional word out, one table sector per strand
+        return S * L + 4 * S + 64 * S
+    if kernel == "node_insert":     # pair in, word out, one table sector per pair
+        return sum(8 * p + 4 * p + 64 * p for p in pk)
+    if kernel == "flagscan_leaf":   # word in/out, slot read, group record, unique leaves out
+        return 4 * S + 64 * S + 4 * S + 16 * ((S + 63) // 64) + 8 * n_leaves
+    if kernel == "flagscan_node":
+        return sum(4 * p + 64 * p + 4 * p + 16 * ((p + 63) // 64) for p in pk) + 8 * sum(layer_sizes)
+    if kernel == "resolve":         # word in; non-first: group sector read + word out
+        nf = (S - n_leaves) + sum(p - u for p, u in zip(pk, layer_sizes))
+        return 4 * (S + sum(pk)) + 16 * ((S + sum(pk) + 63) // 64) + 68 * nf
+    return 0
+
+
+def build_bytes(L, S, n_leaves, layer_sizes):
+    """Whole-build algorithmic bytes, SURVEY §8(d): B_stream + B_table."""
+    pk = []
+    n = S
+    while True:
+        p = (n + 1) // 2
+        pk.append(p)
+        if p == 1:
+            break
+        n = p
+    b_stream = S * L + 4 * S + 8 * n_leaves + sum(4 * 2 * p + 4 * p + 8 * u for p, u in zip(pk, layer_sizes))
+    b_table = 64 * (S + sum(pk))
+    return b_stream, b_table
+
+
+def cpu_baseline(sample_bases):
+    """Compiled reference (oracle/_ref/ref_harness, built from /root/reference sources)
+    timed on this host: pack + shared_tree(std::vector<dna>&) build, 1 thread."""
+    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    if os.path.exists(harness):
+        try:
+            out = subprocess.run([harness, "time", "0", str(sample_bases), "12"], capture_output=True,
+                                 text=True, timeout=600, check=True).stdout
+            r = json.loads(out)
+            return {"value": r["bases_per_s"], "unit": "bases/s", "cores": 1, "kind": "reference",
+                    "sample": f"synthetic uniform ACGT, first {sample_bases} bases of the bench genome "
+                              f"(csrc/synth.h), pack+build, {os.cpu_count()} host CPUs visible, 1 used",
+                    "build_ms": r["build_ms"], "pack_ms": r["pack_ms"]}
+        except Exception as e:  # noqa: BLE001
+            return {"value": None, "unit": "bases/s", "cores": 1, "kind": "reference", "error": str(e)}
+    # port: the C restatement (test infrastructure) as the checker-side CPU timing
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # noqa: E402
+    gcz = sys.modules["gcz"]
+    data = gcz.synth(0, sample_bases).tobytes()
+    t0 = time.perf_counter()
+    oracle.build_leaves(oracle.pack(data, 12), 12)
+    dt = time.perf_counter() - t0
+    return {"value": (len(data) // 12 * 12) / dt, "unit": "bases/s", "cores": 1, "kind": "port",
+            "sample": f"synthetic uniform ACGT, {sample_bases} bases, oracle/gcz_oracle.c"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="uniform_1g", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-sample", type=int, default=120_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    gcz = load_gcz()
+    cfg = CONFIGS[args.config]
+    L = 12
+    nbases = cfg["nbases"]
+    seed = gcz._lib.gcz_synth_default_seed() ^ (0 if rank == 0 else (0x5851F42D4C957F2D * rank) & ((1 << 64) - 1))
+    host = gcz.synth(cfg["kind"], nbases, seed)
+    dev = torch.from_numpy(host).to(f"cuda:{local}")
+    ctx = gcz.Context(local)
+    stream = torch.cuda.Stream(device=local)
+    ctx.set_stream(stream.cuda_stream)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        ctx.build_device_bases(dev.data_ptr(), nbases, L)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        info = ctx.build_device_bases(dev.data_ptr(), nbases, L)
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    S = nbases // L
+    ms_per_step = dt / args.steps * 1e3
+    value = world * S * L * args.steps / dt
+
+    # per-kernel device time (hipEvents on the library's launch stream), one extra build
+    ctx.profile(True)
+    ctx.profile_reset()
+    info = ctx.build_device_bases(dev.data_ptr(), nbases, L)
+    prof = ctx.profile_table()
+    ctx.profile(False)
+    kernels = {}
+    for name, p in prof.items():
+        if p["launches"] == 0:
+            continue
+        b = algorithmic_bytes(name, L, S, info["n_leaves"], info["layer_size"])
+        kernels[name] = {"launches": p["launches"], "total_ms": round(p["total_ms"], 4),
+                         "avg_ms": p["total_ms"] / p["launches"], "alg_bytes": b,
+                         "gbs": b / (p["total_ms"] * 1e-3) / 1e9 if p["total_ms"] > 0 else None}
+    dom = max((k for k in kernels if k != "table_clear"), key=lambda k: kernels[k]["total_ms"])
+    dk = kernels[dom]
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            traffic = json.load(f).get(dom)
+    roofline = {"bound": "hbm", "kernel": dom,
+                "achieved": round(dk["alg_bytes"] / dk["launches"] / (dk["avg_ms"] * 1e-3) / 1e9, 2),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(dk["alg_bytes"] / (dk["total_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                "traffic": traffic, "avg_launch_ms": round(dk["avg_ms"], 4),
+                "alg_bytes_per_launch": dk["alg_bytes"] // dk["launches"]}
+    b_stream, b_table = build_bytes(L, S, info["n_leaves"], info["layer_size"])
+    build_frac = (b_stream + b_table) / (info["build_ms"] * 1e-3) / (HBM_PEAK_GBS * 1e9)
+
+    parity = None
+    if not args.no_parity and rank == 0 and cfg["golden"]:
+        with open(os.path.join(REPO, "tests", "golden", "manifest.json")) as f:
+            exp = json.load(f)[cfg["golden"]]["expect"]
+        tree = ctx.tree()
+        d = gcz.digest(tree)
+        ratio = f"{nbases / d['bytes']:.6g}"
+        parity = {"golden": cfg["golden"],
+                  "dag_sha256_match": d["sha_dag"] == exp["sha_dag"],
+                  "unsorted_sha256_match": d["sha_unsorted_dag"] == exp["sha_unsorted_dag"],
+                  "layers_sha256_match": d["sha_layers_bin"] == exp["sha_layers_bin"],
+                  "ratio": ratio, "ratio_ref": exp["ratio"]}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_sample)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "bases/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": args.config, "nbases_per_gpu": nbases, "L": L, "strands_per_gpu": S,
+                       "parallelism": f"independent shard genome per GPU x{world}"},
+            "roofline": roofline,
+            "build": {"device_ms": info["build_ms"], "b_stream": b_stream, "b_table": b_table,
+                      "hbm_frac_survey_formula": round(build_frac, 5), "n_leaves": info["n_leaves"],
+                      "n_layers": info["n_layers"]},
+            "kernels": kernels,
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,270 @@
+// Host-side operations of libgcz: the shared_tree container operations that sit
+// after the build (frequency sort, bytes(), serialize(), width()), the FASTA
+// line contract, and the synthetic genome generator.  No HIP calls here, so
+// these entry points work on machines without a GPU.
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <thread>
+
+#include "gcz_internal.h"
+#include "synth.h"
+
+using gcz::kIndexMask;
+using gcz::kNullIndex;
+using gcz::ul;
+
+namespace {
+
+// Stable permutation of `n` children by descending reference count, ties by old
+// index (std::stable_sort in sort_leaves/sort_nodes, src/shared_tree.cpp:409-436).
+// Returns newpos[old] (invert_indices, :360-365).  Counting sort when the count
+// range is small, which it is for every real tree.
+std::vector<uint32_t> frequency_order(const std::vector<uint32_t>& parent, size_t n) {
+  std::vector<uint32_t> cnt(n, 0);
+  for (uint32_t w : parent)                                  // histogram, :316-326
+    if (ul(w) != kNullIndex) ++cnt[w & kIndexMask];
+  uint32_t maxc = 0;
+  for (uint32_t c : cnt) maxc = std::max(maxc, c);
+  std::vector<uint32_t> newpos(n);
+  if (maxc <= (1u << 22)) {
+    std::vector<uint64_t> start(size_t(maxc) + 2, 0);
+    for (uint32_t c : cnt) ++start[maxc - c + 1];            // bucket 0 = largest count
+    for (size_t b = 1; b < start.size(); ++b) start[b] += start[b - 1];
+    for (size_t i = 0; i < n; ++i) newpos[i] = uint32_t(start[maxc - cnt[i]]++);
+  } else {
+    std::vector<uint32_t> idx(n);
+    std::iota(idx.begin(), idx.end(), 0u);
+    std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return cnt[a] > cnt[b]; });
+    for (size_t i = 0; i < n; ++i) newpos[idx[i]] = uint32_t(i);
+  }
+  return newpos;
+}
+
+// rewire_nodes (src/shared_tree.cpp:383-403): new index, m/t/v bits kept, null untouched.
+void rewire(std::vector<uint32_t>& parent, const std::vector<uint32_t>& newpos) {
+  for (uint32_t& w : parent)
+    if (ul(w) != kNullIndex) w = (w & gcz::kFlagMask) | newpos[w & kIndexMask];
+}
+
+// Pointer compression (src/shared_tree.cpp:25-67,122-142).
+int segment(uint32_t idx) {
+  if (idx == kNullIndex) return 3;
+  if (idx < 16u) return 0;
+  if (idx < 16u + 4096u) return 1;
+  if (idx < 16u + 4096u + 1048576u) return 2;
+  return 3;
+}
+constexpr uint32_t kSegBits[4] = {4, 12, 20, 28};
+constexpr uint32_t kSegStart[4] = {0, 16, 16 + 4096, 16 + 4096 + 1048576};
+
+inline uint64_t ptr_bytes(uint32_t w) { return (4 + kSegBits[segment(w & kIndexMask)]) / 8; }
+
+uint8_t* put_be(uint8_t* o, uint64_t v, int nbytes) {       // binary_write, utility.h:178-184
+  for (int i = nbytes - 1; i >= 0; --i) *o++ = uint8_t(v >> (8 * i));
+  return o;
+}
+
+uint8_t* put_ptr(uint8_t* o, uint32_t w) {                   // pointer::serialize, :133-142
+  const uint32_t idx = w & kIndexMask;
+  const int seg = segment(idx);
+  const uint32_t off = idx == kNullIndex ? 0xfffffffu : idx - kSegStart[seg];
+  int sh = int(kSegBits[seg]) - 4;
+  *o++ = uint8_t((off >> sh) | (((w >> 29) & 1) << 4) | (((w >> 30) & 1) << 5) | (seg << 6));
+  for (sh -= 8; sh >= 0; sh -= 8) *o++ = uint8_t(off >> sh);
+  return o;
+}
+
+}  // namespace
+
+extern "C" {
+
+gcz_tree* gcz_tree_new(void) { return new gcz_tree(); }
+void gcz_tree_free(gcz_tree* t) { delete t; }
+int gcz_tree_n_layers(const gcz_tree* t) { return int(t->layers.size()); }
+uint64_t gcz_tree_n_leaves(const gcz_tree* t) { return t->leaves.size(); }
+uint64_t gcz_tree_layer_size(const gcz_tree* t, int k) {
+  return (k >= 0 && size_t(k) < t->layers.size()) ? t->layers[k].size() / 2 : 0;
+}
+uint32_t gcz_tree_root(const gcz_tree* t) { return t->root; }
+int gcz_tree_L(const gcz_tree* t) { return t->L; }
+const uint64_t* gcz_tree_leaves(const gcz_tree* t) { return t->leaves.data(); }
+const uint32_t* gcz_tree_layer(const gcz_tree* t, int k) {
+  return (k >= 0 && size_t(k) < t->layers.size()) ? t->layers[k].data() : nullptr;
+}
+
+// shared_tree::sort_tree (src/shared_tree.cpp:443-483).  The reference's two
+// std::async batches touch disjoint layers and a parent's reordering does not
+// change its children's counts, so the net effect is: leaves and node layers
+// 0..D-2 each permuted independently by their parent's histogram (the top
+// layer and the root are unchanged).  Layers are processed in parallel.
+void gcz_tree_sort(gcz_tree* t) {
+  const size_t D = t->layers.size();
+  if (D == 0) return;
+  // permutation of child layer c (c = 0: leaves, c = l+1: node layer l) from parent
+  std::vector<std::vector<uint32_t>> perm(D);
+  {
+    std::vector<std::thread> th;
+    for (size_t c = 0; c < D; ++c) {
+      const size_t n = c == 0 ? t->leaves.size() : t->layers[c - 1].size() / 2;
+      th.emplace_back([&, c, n] { perm[c] = frequency_order(t->layers[c], n); });
+    }
+    for (auto& x : th) x.join();
+  }
+  std::vector<std::thread> th;
+  th.emplace_back([&] {
+    std::vector<uint64_t> nl(t->leaves.size());
+    for (size_t i = 0; i < nl.size(); ++i) nl[perm[0][i]] = t->leaves[i];   // reorder_layer :371-377
+    t->leaves.swap(nl);
+  });
+  for (size_t l = 0; l + 1 < D; ++l) {
+    th.emplace_back([&, l] {
+      const auto& np = perm[l + 1];
+      std::vector<uint32_t> w(t->layers[l].size());
+      for (size_t i = 0; i < np.size(); ++i) {
+        w[2 * size_t(np[i])] = t->layers[l][2 * i];
+        w[2 * size_t(np[i]) + 1] = t->layers[l][2 * i + 1];
+      }
+      t->layers[l].swap(w);
+    });
+  }
+  for (auto& x : th) x.join();
+  th.clear();
+  for (size_t c = 0; c < D; ++c) th.emplace_back([&, c] { rewire(t->layers[c], perm[c]); });
+  for (auto& x : th) x.join();
+}
+
+// shared_tree::bytes (src/shared_tree.cpp:488-496).
+uint64_t gcz_tree_bytes(const gcz_tree* t) {
+  uint64_t b = ptr_bytes(t->root) + 8 + t->leaves.size() * uint64_t((t->L + 1) / 2);
+  for (const auto& layer : t->layers) {
+    b += 8;
+    for (uint32_t w : layer) b += ptr_bytes(w);
+  }
+  return b;
+}
+
+// shared_tree::serialize (src/shared_tree.cpp:504-513).  0 when cap is too small.
+uint64_t gcz_tree_serialize(const gcz_tree* t, uint8_t* buf, uint64_t cap) {
+  const uint64_t need = gcz_tree_bytes(t);
+  if (cap < need) return 0;
+  uint8_t* o = put_ptr(buf, t->root);
+  o = put_be(o, t->leaves.size(), 8);
+  const int lb = (t->L + 1) / 2;
+  for (uint64_t v : t->leaves) o = put_be(o, v, lb);
+  for (const auto& layer : t->layers) {
+    o = put_be(o, layer.size() / 2, 8);
+    for (uint32_t w : layer) o = put_ptr(o, w);
+  }
+  return uint64_t(o - buf);
+}
+
+// shared_tree::width via children() (include/shared_tree.h:165,
+// src/shared_tree.cpp:252-259), bottom-up.
+uint64_t gcz_tree_width(const gcz_tree* t) {
+  if (t->layers.empty()) return 0;
+  std::vector<uint64_t> below;
+  for (size_t l = 0; l < t->layers.size(); ++l) {
+    const auto& layer = t->layers[l];
+    std::vector<uint64_t> cur(layer.size() / 2);
+    for (size_t i = 0; i < cur.size(); ++i) {
+      uint64_t s = 0;
+      for (int c = 0; c < 2; ++c) {
+        const uint32_t w = layer[2 * i + c];
+        if (ul(w) == kNullIndex) continue;
+        s += l == 0 ? 1 : below[w & kIndexMask];
+      }
+      cur[i] = s;
+    }
+    below.swap(cur);
+  }
+  return ul(t->root) == kNullIndex ? 0 : below[t->root & kIndexMask];
+}
+
+void gcz_tree_set_leaves(gcz_tree* t, int L, const uint64_t* leaves, uint64_t n) {
+  t->L = L;
+  t->leaves.assign(leaves, leaves + n);
+  t->layers.clear();
+}
+
+void gcz_tree_push_layer(gcz_tree* t, const uint32_t* words, uint64_t n_nodes) {
+  t->layers.emplace_back(words, words + 2 * n_nodes);
+}
+
+void gcz_tree_set_root(gcz_tree* t, uint32_t root) { t->root = root; }
+
+// pointer::deserialize (src/shared_tree.cpp:147-163) + shared_tree::deserialize
+// (:520-538): root, u64 leaf count, leaves of ceil(L/2) bytes, then layers
+// (u64 count + pointer pairs) until the input ends.  invariant = false.
+int gcz_tree_deserialize(gcz_tree* t, int L, const uint8_t* buf, uint64_t n) {
+  uint64_t pos = 0;
+  bool ok = true;
+  auto get_be = [&](int nbytes) -> uint64_t {
+    uint64_t v = 0;
+    if (pos + uint64_t(nbytes) > n) { ok = false; return 0; }
+    for (int i = 0; i < nbytes; ++i) v = (v << 8) | buf[pos++];
+    return v;
+  };
+  auto get_ptr = [&]() -> uint32_t {
+    const uint32_t first = uint32_t(get_be(1));
+    const int seg = (first >> 6) & 3;
+    const uint32_t t_bit = (first >> 5) & 1, m_bit = (first >> 4) & 1;
+    uint64_t off = uint64_t(first & 0xf) << (kSegBits[seg] - 4);
+    for (int sh = int(kSegBits[seg]) - 12; sh >= 0; sh -= 8) off |= get_be(1) << sh;
+    const uint32_t idx = (seg == 3 && off == 0xfffffffu) ? kNullIndex : uint32_t(kSegStart[seg] + off);
+    return idx | (m_bit << 29) | (t_bit << 30);   // pointer{data, m, t, false}
+  };
+  gcz_tree nt;
+  nt.L = L;
+  nt.root = get_ptr();
+  const uint64_t nl = get_be(8);
+  if (!ok || nl > n) return GCZ_ERR_ARG;
+  nt.leaves.resize(nl);
+  for (uint64_t i = 0; i < nl && ok; ++i) nt.leaves[i] = get_be((L + 1) / 2);
+  while (ok && pos < n) {
+    const uint64_t cnt = get_be(8);
+    if (!ok || cnt > n) return GCZ_ERR_ARG;
+    std::vector<uint32_t> w(2 * cnt);
+    for (uint64_t i = 0; i < 2 * cnt && ok; ++i) w[i] = get_ptr();
+    nt.layers.push_back(std::move(w));
+  }
+  if (!ok) return GCZ_ERR_ARG;
+  *t = std::move(nt);
+  return GCZ_OK;
+}
+
+// fasta_reader::load_buffer line contract (src/fasta_reader.cpp:40-68): at each
+// line start a '>' or '\n' skips ONE line, the next line is data without a
+// second peek; data line bodies are concatenated.
+uint64_t gcz_fasta_extract(const uint8_t* f, uint64_t n, uint8_t* out) {
+  uint64_t pos = 0, j = 0;
+  while (pos < n) {
+    if (f[pos] == '>' || f[pos] == '\n') {
+      const void* nl = std::memchr(f + pos, '\n', n - pos);
+      pos = nl ? uint64_t(static_cast<const uint8_t*>(nl) - f) + 1 : n;
+      if (pos >= n) break;
+    }
+    const void* nl = std::memchr(f + pos, '\n', n - pos);
+    const uint64_t end = nl ? uint64_t(static_cast<const uint8_t*>(nl) - f) : n;
+    if (out + j != f + pos) std::memmove(out + j, f + pos, end - pos);
+    j += end - pos;
+    pos = nl ? end + 1 : n;
+  }
+  return j;
+}
+
+void gcz_synth_fill(char* out, int kind, uint64_t seed, uint64_t begin, uint64_t end) {
+  const uint64_t n = end > begin ? end - begin : 0;
+  unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (n < (1u << 22)) T = 1;
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < T; ++t) {
+    const uint64_t a = begin + n * t / T, b = begin + n * (t + 1) / T;
+    th.emplace_back([=] { gcz_synth_fill_range(out + (a - begin), kind, seed, a, b); });
+  }
+  for (auto& x : th) x.join();
+}
+
+uint64_t gcz_synth_default_seed(void) { return GCZ_SYNTH_SEED; }
+
+}  // extern "C"

@@ -13,7 +13,7 @@ typedef struct { char *buf; int kind; uint64_t seed, begin, end; } job_t;
 
 static void *run(void *p) {
   job_t *j = (job_t *)p;
-  gcz_synth_fill(j->buf + j->begin, j->kind, j->seed, j->begin, j->end);
+  gcz_synth_fill_range(j->buf + j->begin, j->kind, j->seed, j->begin, j->end);
   return NULL;
 }
 

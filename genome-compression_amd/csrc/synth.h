@@ -71,7 +71,7 @@ static inline void gcz_synth_tandem(char *out, uint64_t seed, uint64_t begin, ui
   }
 }
 
-static inline void gcz_synth_fill(char *out, int kind, uint64_t seed, uint64_t begin, uint64_t end) {
+static inline void gcz_synth_fill_range(char *out, int kind, uint64_t seed, uint64_t begin, uint64_t end) {
   if (kind == 1) gcz_synth_tandem(out, seed, begin, end);
   else gcz_synth_uniform(out, seed, begin, end);
 }

@@ -1,0 +1,304 @@
+"""ctypes binding of libgcz (include/gcz.h) — the MI355X shared_tree build.
+
+Python mirror of the reference's construction surface for tests and the bench:
+`Context.build_fasta` corresponds to ``shared_tree{path}`` (compress.cpp:183),
+`Context.build_leaves` to ``shared_tree(std::vector<dna>&)``
+(src/shared_tree.cpp:212-215), and `Tree` to the container operations that
+follow (sort_tree, bytes, serialize, width; src/shared_tree.cpp:316-513).
+
+The library is the only compute path: if libgcz.so is missing this module
+raises at import time (there is no CPU fallback).
+"""
+import ctypes
+import hashlib
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgcz.so")
+
+GCZ_OK, GCZ_ERR_SYMBOL, GCZ_ERR_IO, GCZ_ERR_CAPACITY, GCZ_ERR_DEVICE, GCZ_ERR_ARG, GCZ_ERR_EMPTY = range(7)
+NULL_WORD = 0x9FFFFFFF
+MAX_LAYERS = 64
+
+
+class GczError(RuntimeError):
+    def __init__(self, code, msg, info=None):
+        super().__init__(f"libgcz error {code}: {msg}")
+        self.code = code
+        self.info = info
+
+
+class _Info(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int), ("L", ctypes.c_int), ("n_layers", ctypes.c_int),
+                ("root", ctypes.c_uint32), ("n_strands", ctypes.c_uint64), ("n_leaves", ctypes.c_uint64),
+                ("layer_size", ctypes.c_uint64 * MAX_LAYERS), ("error_offset", ctypes.c_uint64),
+                ("error_symbol", ctypes.c_int), ("build_ms", ctypes.c_double)]
+
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} not built: run `make -C genome-compression_amd` "
+                      "(or __graft_entry__.build()); there is no fallback path")
+_lib = ctypes.CDLL(LIB_PATH)
+
+_P = ctypes.c_void_p
+_U64 = ctypes.c_uint64
+_SIGS = {
+    "gcz_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_P)]),
+    "gcz_ctx_destroy": (None, [_P]),
+    "gcz_ctx_set_stream": (ctypes.c_int, [_P, _P]),
+    "gcz_ctx_stream": (_P, [_P]),
+    "gcz_ctx_last_error": (ctypes.c_char_p, [_P]),
+    "gcz_build_device_bases": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
+    "gcz_build_device_leaves": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
+    "gcz_build_host_fasta": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
+    "gcz_build_host_leaves": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
+    "gcz_info_get": (ctypes.c_int, [_P, ctypes.POINTER(_Info)]),
+    "gcz_copy_leaves": (ctypes.c_int, [_P, _P]),
+    "gcz_copy_layer": (ctypes.c_int, [_P, ctypes.c_int, _P]),
+    "gcz_device_leaves": (_P, [_P]),
+    "gcz_device_layer": (_P, [_P, ctypes.c_int]),
+    "gcz_profile_enable": (ctypes.c_int, [_P, ctypes.c_int]),
+    "gcz_profile_entry": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                          ctypes.POINTER(_U64), ctypes.POINTER(ctypes.c_double)]),
+    "gcz_profile_reset": (None, [_P]),
+    "gcz_tree_new": (_P, []),
+    "gcz_tree_free": (None, [_P]),
+    "gcz_tree_fetch": (ctypes.c_int, [_P, _P]),
+    "gcz_tree_n_layers": (ctypes.c_int, [_P]),
+    "gcz_tree_n_leaves": (_U64, [_P]),
+    "gcz_tree_layer_size": (_U64, [_P, ctypes.c_int]),
+    "gcz_tree_root": (ctypes.c_uint32, [_P]),
+    "gcz_tree_L": (ctypes.c_int, [_P]),
+    "gcz_tree_leaves": (_P, [_P]),
+    "gcz_tree_layer": (_P, [_P, ctypes.c_int]),
+    "gcz_tree_sort": (None, [_P]),
+    "gcz_tree_bytes": (_U64, [_P]),
+    "gcz_tree_serialize": (_U64, [_P, _P, _U64]),
+    "gcz_tree_width": (_U64, [_P]),
+    "gcz_tree_set_leaves": (None, [_P, ctypes.c_int, _P, _U64]),
+    "gcz_tree_push_layer": (None, [_P, _P, _U64]),
+    "gcz_tree_set_root": (None, [_P, ctypes.c_uint32]),
+    "gcz_tree_deserialize": (ctypes.c_int, [_P, ctypes.c_int, _P, _U64]),
+    "gcz_fasta_extract": (_U64, [_P, _U64, _P]),
+    "gcz_synth_fill": (None, [_P, ctypes.c_int, _U64, _U64, _U64]),
+    "gcz_synth_default_seed": (_U64, []),
+}
+for _name, (_res, _args) in _SIGS.items():
+    _f = getattr(_lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+EXPORTED = tuple(_SIGS)
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a.size else ctypes.c_void_p(0)
+
+
+# ---- host utilities ---------------------------------------------------------
+def fasta_extract(data: bytes) -> bytes:
+    """Concatenated bases under the reference reader's line contract."""
+    buf = np.frombuffer(data, dtype=np.uint8)
+    out = np.empty(max(len(data), 1), dtype=np.uint8)
+    n = _lib.gcz_fasta_extract(_ptr(buf), len(data), _ptr(out))
+    return out[:n].tobytes()
+
+
+def synth(kind: int, nbases: int, seed: int = None) -> np.ndarray:
+    """Synthetic genome (csrc/synth.h): kind 0 uniform ACGT, kind 1 tandem repeats."""
+    if seed is None:
+        seed = _lib.gcz_synth_default_seed()
+    out = np.empty(max(nbases, 1), dtype=np.uint8)
+    _lib.gcz_synth_fill(_ptr(out), kind, seed, 0, nbases)
+    return out[:nbases]
+
+
+# ---- host tree ----------------------------------------------------------------
+class Tree:
+    """Host-resident shared tree (leaves, per-layer node words, root)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _lib.gcz_tree_free(self._h)
+            self._h = None
+
+    @property
+    def L(self):
+        return _lib.gcz_tree_L(self._h)
+
+    @property
+    def n_layers(self):
+        return _lib.gcz_tree_n_layers(self._h)
+
+    @property
+    def depth(self):
+        return self.n_layers + 1
+
+    @property
+    def root(self):
+        return _lib.gcz_tree_root(self._h)
+
+    @classmethod
+    def from_arrays(cls, L, leaves, layers, root):
+        """Host tree from raw arrays (no GPU involved)."""
+        t = cls(_lib.gcz_tree_new())
+        lv = np.ascontiguousarray(leaves, dtype=np.uint64)
+        _lib.gcz_tree_set_leaves(t._h, L, _ptr(lv), lv.size)
+        for w in layers:
+            w = np.ascontiguousarray(w, dtype=np.uint32)
+            _lib.gcz_tree_push_layer(t._h, _ptr(w), w.size // 2)
+        _lib.gcz_tree_set_root(t._h, int(root))
+        return t
+
+    @classmethod
+    def deserialize(cls, data: bytes, L=12):
+        t = cls(_lib.gcz_tree_new())
+        buf = np.frombuffer(data, dtype=np.uint8)
+        rc = _lib.gcz_tree_deserialize(t._h, L, _ptr(buf), len(data))
+        if rc != GCZ_OK:
+            raise GczError(rc, "malformed .dag")
+        return t
+
+    def leaves(self) -> np.ndarray:
+        n = _lib.gcz_tree_n_leaves(self._h)
+        if n == 0:
+            return np.zeros(0, dtype=np.uint64)
+        p = _lib.gcz_tree_leaves(self._h)
+        return np.ctypeslib.as_array((ctypes.c_uint64 * n).from_address(p)).copy()
+
+    def layer(self, k) -> np.ndarray:
+        n = 2 * _lib.gcz_tree_layer_size(self._h, k)
+        if n == 0:
+            return np.zeros(0, dtype=np.uint32)
+        p = _lib.gcz_tree_layer(self._h, k)
+        return np.ctypeslib.as_array((ctypes.c_uint32 * n).from_address(p)).copy()
+
+    def layer_sizes(self):
+        return [int(_lib.gcz_tree_layer_size(self._h, k)) for k in range(self.n_layers)]
+
+    def sort(self):
+        _lib.gcz_tree_sort(self._h)
+
+    def bytes(self):
+        return int(_lib.gcz_tree_bytes(self._h))
+
+    def width(self):
+        return int(_lib.gcz_tree_width(self._h))
+
+    def serialize(self) -> bytes:
+        n = self.bytes()
+        buf = np.empty(max(n, 1), dtype=np.uint8)
+        got = _lib.gcz_tree_serialize(self._h, _ptr(buf), n)
+        assert got == n
+        return buf[:n].tobytes()
+
+    # dump format of oracle/ref_harness.cpp
+    def leaves_bin(self) -> bytes:
+        return self.leaves().astype("<u8").tobytes()
+
+    def layers_bin(self) -> bytes:
+        out = []
+        for k in range(self.n_layers):
+            w = self.layer(k)
+            out.append(np.uint64(len(w) // 2).astype("<u8").tobytes())
+            out.append(w.astype("<u4").tobytes())
+        return b"".join(out)
+
+
+def _sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+def digest(tree: Tree) -> dict:
+    """Hashes in the format of tests/golden/manifest.json (sorts the tree!)."""
+    d = {"n_leaves": int(_lib.gcz_tree_n_leaves(tree._h)), "depth": tree.depth, "root": tree.root,
+         "width": tree.width(), "layer_sizes": tree.layer_sizes(),
+         "sha_leaves_bin": _sha(tree.leaves_bin()), "sha_layers_bin": _sha(tree.layers_bin()),
+         "unsorted_bytes": tree.bytes(), "sha_unsorted_dag": _sha(tree.serialize())}
+    tree.sort()
+    d["bytes"] = tree.bytes()
+    d["sha_dag"] = _sha(tree.serialize())
+    return d
+
+
+# ---- device context -----------------------------------------------------------
+class Context:
+    """One GPU, one stream, a reusable workspace (gcz_ctx)."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        rc = _lib.gcz_ctx_create(device, ctypes.byref(h))
+        if rc != GCZ_OK:
+            raise GczError(rc, f"gcz_ctx_create(device={device}) failed")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.gcz_ctx_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def _check(self, rc):
+        if rc != GCZ_OK:
+            raise GczError(rc, _lib.gcz_ctx_last_error(self._h).decode(), self.info())
+        return self.info()
+
+    def set_stream(self, stream_ptr: int):
+        _lib.gcz_ctx_set_stream(self._h, ctypes.c_void_p(stream_ptr))
+
+    @property
+    def stream(self):
+        return _lib.gcz_ctx_stream(self._h)
+
+    def info(self) -> dict:
+        i = _Info()
+        _lib.gcz_info_get(self._h, ctypes.byref(i))
+        return {"status": i.status, "L": i.L, "n_layers": i.n_layers, "root": i.root,
+                "n_strands": i.n_strands, "n_leaves": i.n_leaves,
+                "layer_size": [int(i.layer_size[k]) for k in range(i.n_layers)],
+                "error_offset": i.error_offset, "error_symbol": i.error_symbol, "build_ms": i.build_ms}
+
+    def build_fasta(self, data: bytes, L: int = 12) -> dict:
+        buf = np.frombuffer(data, dtype=np.uint8)
+        return self._check(_lib.gcz_build_host_fasta(self._h, _ptr(buf), len(data), L))
+
+    def build_leaves(self, leaves: np.ndarray, L: int = 12) -> dict:
+        a = np.ascontiguousarray(leaves, dtype=np.uint64)
+        return self._check(_lib.gcz_build_host_leaves(self._h, _ptr(a), a.size, L))
+
+    def build_device_bases(self, dev_ptr: int, nbases: int, L: int = 12) -> dict:
+        return self._check(_lib.gcz_build_device_bases(self._h, ctypes.c_void_p(dev_ptr), nbases, L))
+
+    def build_device_leaves(self, dev_ptr: int, S: int, L: int = 12) -> dict:
+        return self._check(_lib.gcz_build_device_leaves(self._h, ctypes.c_void_p(dev_ptr), S, L))
+
+    def tree(self) -> Tree:
+        t = _lib.gcz_tree_new()
+        rc = _lib.gcz_tree_fetch(self._h, t)
+        if rc != GCZ_OK:
+            _lib.gcz_tree_free(t)
+            raise GczError(rc, "gcz_tree_fetch failed")
+        return Tree(t)
+
+    def profile(self, on=True):
+        _lib.gcz_profile_enable(self._h, int(on))
+
+    def profile_reset(self):
+        _lib.gcz_profile_reset(self._h)
+
+    def profile_table(self) -> dict:
+        out = {}
+        k = 0
+        name = ctypes.c_char_p()
+        n = ctypes.c_uint64()
+        ms = ctypes.c_double()
+        while _lib.gcz_profile_entry(self._h, k, ctypes.byref(name), ctypes.byref(n), ctypes.byref(ms)) == 0:
+            out[name.value.decode()] = {"launches": int(n.value), "total_ms": float(ms.value)}
+            k += 1
+        return out

@@ -122,6 +122,15 @@ GCZ_API void gcz_tree_sort(gcz_tree *t);
 GCZ_API uint64_t gcz_tree_bytes(const gcz_tree *t);
 GCZ_API uint64_t gcz_tree_serialize(const gcz_tree *t, uint8_t *buf, uint64_t cap);
 GCZ_API uint64_t gcz_tree_width(const gcz_tree *t);
+/* Fill a host tree from raw arrays (e.g. a tree built elsewhere): leaves, then
+ * layers bottom-up (2 words per node), then the root word. */
+GCZ_API void gcz_tree_set_leaves(gcz_tree *t, int L, const uint64_t *leaves, uint64_t n);
+GCZ_API void gcz_tree_push_layer(gcz_tree *t, const uint32_t *words, uint64_t n_nodes);
+GCZ_API void gcz_tree_set_root(gcz_tree *t, uint32_t root);
+/* shared_tree::deserialize (src/shared_tree.cpp:520-538): the .dag format
+ * drops the invariant bit, so every loaded pointer has bit 31 clear.
+ * Returns GCZ_OK or GCZ_ERR_ARG on a truncated buffer. */
+GCZ_API int gcz_tree_deserialize(gcz_tree *t, int L, const uint8_t *buf, uint64_t n);
 
 /* ---- host utilities ---------------------------------------------------- */
 /* FASTA line contract of src/fasta_reader.cpp:40-68 (headers, blank lines);

@@ -143,7 +143,7 @@ int main(int argc, char** argv) {
     dna::size(std::atoi(argv[4]));
     int reps = argc > 5 ? std::atoi(argv[5]) : 1;
     std::vector<char> ascii(nbases);
-    gcz_synth_fill(ascii.data(), kind, GCZ_SYNTH_SEED, 0, nbases);
+    gcz_synth_fill_range(ascii.data(), kind, GCZ_SYNTH_SEED, 0, nbases);
     const uint64_t L = dna::size();
     const uint64_t S = nbases / L;
     double best_pack = 1e30, best_build = 1e30;

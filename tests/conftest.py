@@ -1,0 +1,76 @@
+import importlib.util
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(REPO, "tests", "golden")
+PKG = os.path.join(REPO, "genome-compression_amd")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+    config.addinivalue_line("markers", "slow: large inputs (>= 100 Mbase)")
+
+
+def _load(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def load_gcz():
+    if "gcz" in sys.modules:
+        return sys.modules["gcz"]
+    lib = os.path.join(PKG, "libgcz.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-s", "-C", PKG], check=True)
+    return _load("gcz", os.path.join(PKG, "gcz.py"))
+
+
+def load_oracle():
+    if "gcz_oracle" in sys.modules:
+        return sys.modules["gcz_oracle"]
+    return _load("gcz_oracle", os.path.join(REPO, "oracle", "oracle.py"))
+
+
+@pytest.fixture(scope="session")
+def gcz():
+    return load_gcz()
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    return load_oracle()
+
+
+@pytest.fixture(scope="session")
+def manifest():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)
+
+
+def case_input(case, gcz_mod):
+    """(kind, payload, L): payload is FASTA bytes or a u64 leaf array."""
+    L = case["L"]
+    if case["kind"] == "fasta":
+        with open(os.path.join(GOLDEN, case["input"]), "rb") as f:
+            return "fasta", f.read(), L
+    if case["kind"] == "leaves":
+        return "leaves", np.fromfile(os.path.join(GOLDEN, case["input"]), dtype="<u8"), L
+    if case["kind"] == "synth":
+        return "fasta", gcz_mod.synth(case["synth_kind"], case["nbases"]).tobytes(), L
+    raise ValueError(case["kind"])
+
+
+def compare_digest(got, exp):
+    keys = ["n_leaves", "depth", "root", "width", "layer_sizes", "sha_leaves_bin", "sha_layers_bin",
+            "unsorted_bytes", "sha_unsorted_dag", "bytes", "sha_dag"]
+    diffs = {k: (got.get(k), exp.get(k)) for k in keys if got.get(k) != exp.get(k)}
+    return diffs

@@ -1,0 +1,115 @@
+"""Parity of the HIP build (libgcz, gfx950) with the compiled reference's goldens
+and with the C oracle.  Every test here runs the MI355X kernels through the C ABI."""
+import gzip
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, case_input, compare_digest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx(gcz):
+    c = gcz.Context(0)
+    yield c
+    c.close()
+
+
+def _names(max_bases):
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        m = json.load(f)
+    return [n for n, c in sorted(m.items()) if not (c["kind"] == "synth" and c["nbases"] > max_bases)]
+
+
+def _build(ctx, kind, payload, L):
+    return ctx.build_fasta(payload, L) if kind == "fasta" else ctx.build_leaves(payload, L)
+
+
+@pytest.mark.parametrize("name", _names(12_000_000))
+def test_gpu_matches_reference_goldens(name, ctx, gcz, manifest):
+    case = manifest[name]
+    exp = case["expect"]
+    kind, payload, L = case_input(case, gcz)
+    if exp["exit"] != 0:
+        with pytest.raises(gcz.GczError) as ei:
+            _build(ctx, kind, payload, L)
+        assert ei.value.code == gcz.GCZ_ERR_SYMBOL
+        sym = ei.value.info["error_symbol"]
+        sym = sym - 32 if 97 <= sym <= 122 else sym
+        assert f"Encountered unknown symbol: {sym} (ASCII code {sym})" == exp["stderr"]
+        return
+    info = _build(ctx, kind, payload, L)
+    assert info["n_strands"] == exp["width"]
+    got = gcz.digest(ctx.tree())
+    assert compare_digest(got, exp) == {}
+
+
+@pytest.mark.parametrize("name", ["chmpxx", "hehcmv"])
+def test_gpu_full_dump(name, ctx, gcz):
+    with open(os.path.join(GOLDEN, "data", name), "rb") as f:
+        ctx.build_fasta(f.read(), 12)
+    t = ctx.tree()
+    with gzip.open(os.path.join(GOLDEN, "full", f"{name}.leaves.bin.gz")) as f:
+        assert t.leaves_bin() == f.read()
+    with gzip.open(os.path.join(GOLDEN, "full", f"{name}.layers.bin.gz")) as f:
+        assert t.layers_bin() == f.read()
+
+
+def test_gpu_matches_oracle_random_iupac(ctx, gcz, oracle):
+    """Random leaves over every nibble value, many sizes (tails, tiny trees)."""
+    rng = np.random.default_rng(5)
+    for S in [1, 2, 3, 5, 63, 64, 65, 2047, 2048, 2049, 4097, 100_003]:
+        pool = rng.integers(0, 1 << 48, size=max(4, S // 7), dtype=np.uint64)
+        leaves = pool[rng.integers(0, pool.size, size=S)]
+        ctx.build_leaves(leaves, 12)
+        g = ctx.tree()
+        o = oracle.build_leaves(leaves, 12)
+        assert g.leaves_bin() == o.leaves_bin(), S
+        assert g.layers_bin() == o.layers_bin(), S
+        assert g.root == o.root, S
+
+
+def test_gpu_deterministic(ctx, gcz):
+    data = gcz.synth(1, 3_000_000).tobytes()
+    ctx.build_fasta(data, 12)
+    a = ctx.tree()
+    ctx.build_fasta(data, 12)
+    b = ctx.tree()
+    assert a.layers_bin() == b.layers_bin() and a.leaves_bin() == b.leaves_bin()
+
+
+def test_gpu_device_pointer_path(ctx, gcz):
+    """gcz_build_device_bases on a device buffer (the bench path), incl. a misaligned pointer."""
+    import torch
+    data = gcz.synth(0, 1_000_000)
+    ref = gcz.digest((ctx.build_fasta(data.tobytes(), 12), ctx.tree())[1])
+    dev = torch.from_numpy(np.concatenate([np.zeros(1, np.uint8), data])).to("cuda")
+    torch.cuda.synchronize()
+    ctx.build_device_bases(dev.data_ptr() + 1, data.size, 12)
+    assert compare_digest(gcz.digest(ctx.tree()), ref) == {}
+
+
+def test_gpu_empty_and_bad_L(ctx, gcz):
+    with pytest.raises(gcz.GczError) as ei:
+        ctx.build_fasta(b"ACGTACGTAC", 12)
+    assert ei.value.code == gcz.GCZ_ERR_EMPTY
+    with pytest.raises(gcz.GczError) as ei:
+        ctx.build_fasta(b"ACGT" * 100, 17)
+    assert ei.value.code == gcz.GCZ_ERR_ARG
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", ["synth/uniform_100000003", "synth/tandem_100000000",
+                                  "synth/uniform_1000000000"])
+def test_gpu_large_synth_goldens(name, ctx, gcz, manifest):
+    case = manifest[name]
+    kind, payload, L = case_input(case, gcz)
+    info = _build(ctx, kind, payload, L)
+    exp = case["expect"]
+    assert info["n_leaves"] == exp["n_leaves"]
+    assert info["layer_size"] == exp["layer_sizes"]
+    assert compare_digest(gcz.digest(ctx.tree()), exp) == {}
