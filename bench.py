@@ -126,17 +126,17 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     args = ap.parse_args()
 
-    import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
+        # CPU-side rendezvous only (barrier, max-over-ranks).  torch is imported
+        # before libgcz so the process holds a single HIP runtime; no GPU tensor
+        # or collective is on the build path.
+        import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
 
     gcz = load_gcz()
     cfg = CONFIGS[args.config]
@@ -144,27 +144,26 @@ def main():
     nbases = cfg["nbases"]
     seed = gcz._lib.gcz_synth_default_seed() ^ (0 if rank == 0 else (0x5851F42D4C957F2D * rank) & ((1 << 64) - 1))
     host = gcz.synth(cfg["kind"], nbases, seed)
-    dev = torch.from_numpy(host).to(f"cuda:{local}")
     ctx = gcz.Context(local)
-    stream = torch.cuda.Stream(device=local)
-    ctx.set_stream(stream.cuda_stream)
+    dev = ctx.upload(host)
+    del host
 
     def barrier():
-        torch.cuda.synchronize()
+        ctx.sync()
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize()
+        ctx.sync()
 
     for _ in range(args.warmup):
-        ctx.build_device_bases(dev.data_ptr(), nbases, L)
+        ctx.build_device_bases(dev.ptr, nbases, L)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        info = ctx.build_device_bases(dev.data_ptr(), nbases, L)
+        info = ctx.build_device_bases(dev.ptr, nbases, L)
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     S = nbases // L
@@ -174,7 +173,7 @@ def main():
     # per-kernel device time (hipEvents on the library's launch stream), one extra build
     ctx.profile(True)
     ctx.profile_reset()
-    info = ctx.build_device_bases(dev.data_ptr(), nbases, L)
+    info = ctx.build_device_bases(dev.ptr, nbases, L)
     prof = ctx.profile_table()
     ctx.profile(False)
     kernels = {}
@@ -234,6 +233,7 @@ def main():
             "parity": parity,
         }
         print(json.dumps(line), flush=True)
+    dev.free()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -720,6 +720,38 @@ int gcz_ctx_set_stream(gcz_ctx* c, void* s) {
 void* gcz_ctx_stream(gcz_ctx* c) { return c ? c->stream : nullptr; }
 const char* gcz_ctx_last_error(gcz_ctx* c) { return c ? c->last_error.c_str() : "null context"; }
 
+void* gcz_dev_alloc(gcz_ctx* c, uint64_t bytes) {
+  if (!c || hipSetDevice(c->device) != hipSuccess) return nullptr;
+  void* p = nullptr;
+  return hipMalloc(&p, bytes ? bytes : 1) == hipSuccess ? p : nullptr;
+}
+
+int gcz_dev_free(gcz_ctx* c, void* p) {
+  if (!c) return GCZ_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  (void)hipStreamSynchronize(c->stream);
+  return hipFree(p) == hipSuccess ? GCZ_OK : GCZ_ERR_DEVICE;
+}
+
+int gcz_memcpy_h2d(gcz_ctx* c, void* dst, const void* src, uint64_t bytes) {
+  if (!c) return GCZ_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  if (hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return GCZ_ERR_DEVICE;
+  return hipStreamSynchronize(c->stream) == hipSuccess ? GCZ_OK : GCZ_ERR_DEVICE;
+}
+
+int gcz_memcpy_d2h(gcz_ctx* c, void* dst, const void* src, uint64_t bytes) {
+  if (!c) return GCZ_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess) return GCZ_ERR_DEVICE;
+  return hipStreamSynchronize(c->stream) == hipSuccess ? GCZ_OK : GCZ_ERR_DEVICE;
+}
+
+int gcz_ctx_sync(gcz_ctx* c) {
+  if (!c) return GCZ_ERR_ARG;
+  return hipStreamSynchronize(c->stream) == hipSuccess ? GCZ_OK : GCZ_ERR_DEVICE;
+}
+
 int gcz_build_device_bases(gcz_ctx* c, const void* d_bases, uint64_t nbases, int L) {
   if (!c || (!d_bases && nbases)) return GCZ_ERR_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;

@@ -50,6 +50,11 @@ _SIGS = {
     "gcz_ctx_set_stream": (ctypes.c_int, [_P, _P]),
     "gcz_ctx_stream": (_P, [_P]),
     "gcz_ctx_last_error": (ctypes.c_char_p, [_P]),
+    "gcz_dev_alloc": (_P, [_P, _U64]),
+    "gcz_dev_free": (ctypes.c_int, [_P, _P]),
+    "gcz_memcpy_h2d": (ctypes.c_int, [_P, _P, _P, _U64]),
+    "gcz_memcpy_d2h": (ctypes.c_int, [_P, _P, _P, _U64]),
+    "gcz_ctx_sync": (ctypes.c_int, [_P]),
     "gcz_build_device_bases": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
     "gcz_build_device_leaves": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
     "gcz_build_host_fasta": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
@@ -227,6 +232,25 @@ def digest(tree: Tree) -> dict:
 
 
 # ---- device context -----------------------------------------------------------
+class DeviceBuffer:
+    """Device allocation made through libgcz (no other GPU runtime needed)."""
+
+    def __init__(self, ctx, nbytes):
+        self._ctx = ctx
+        self.nbytes = nbytes
+        self.ptr = _lib.gcz_dev_alloc(ctx._h, nbytes)
+        if not self.ptr:
+            raise GczError(GCZ_ERR_DEVICE, f"gcz_dev_alloc({nbytes}) failed")
+
+    def free(self):
+        if getattr(self, "ptr", None) and getattr(self._ctx, "_h", None):
+            _lib.gcz_dev_free(self._ctx._h, ctypes.c_void_p(self.ptr))
+        self.ptr = None
+
+    __del__ = free
+
+
+
 class Context:
     """One GPU, one stream, a reusable workspace (gcz_ctx)."""
 
@@ -255,6 +279,20 @@ class Context:
     @property
     def stream(self):
         return _lib.gcz_ctx_stream(self._h)
+
+    def upload(self, host: np.ndarray) -> "DeviceBuffer":
+        """Copy a host array into a new device buffer owned by this context."""
+        a = np.ascontiguousarray(host)
+        buf = DeviceBuffer(self, a.nbytes)
+        rc = _lib.gcz_memcpy_h2d(self._h, ctypes.c_void_p(buf.ptr), _ptr(a), a.nbytes)
+        if rc != GCZ_OK:
+            raise GczError(rc, "H2D copy failed")
+        return buf
+
+    def sync(self):
+        rc = _lib.gcz_ctx_sync(self._h)
+        if rc != GCZ_OK:
+            raise GczError(rc, "stream synchronize failed")
 
     def info(self) -> dict:
         i = _Info()

@@ -73,6 +73,14 @@ GCZ_API int gcz_ctx_set_stream(gcz_ctx *ctx, void *hip_stream);
 GCZ_API void *gcz_ctx_stream(gcz_ctx *ctx);
 GCZ_API const char *gcz_ctx_last_error(gcz_ctx *ctx);
 
+/* Device memory helpers on the context's device/stream, so FFI callers need no
+ * other GPU runtime for staging inputs. */
+GCZ_API void *gcz_dev_alloc(gcz_ctx *ctx, uint64_t bytes);
+GCZ_API int gcz_dev_free(gcz_ctx *ctx, void *ptr);
+GCZ_API int gcz_memcpy_h2d(gcz_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+GCZ_API int gcz_memcpy_d2h(gcz_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+GCZ_API int gcz_ctx_sync(gcz_ctx *ctx);
+
 /* ---- builds ------------------------------------------------------------ *
  * Replace tree_constructor::reduce (src/shared_tree.cpp:719-763).  The result
  * stays resident in HBM inside ctx until the next build; fetch it with

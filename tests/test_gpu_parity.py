@@ -84,13 +84,17 @@ def test_gpu_deterministic(ctx, gcz):
 
 def test_gpu_device_pointer_path(ctx, gcz):
     """gcz_build_device_bases on a device buffer (the bench path), incl. a misaligned pointer."""
-    import torch
     data = gcz.synth(0, 1_000_000)
     ref = gcz.digest((ctx.build_fasta(data.tobytes(), 12), ctx.tree())[1])
-    dev = torch.from_numpy(np.concatenate([np.zeros(1, np.uint8), data])).to("cuda")
-    torch.cuda.synchronize()
-    ctx.build_device_bases(dev.data_ptr() + 1, data.size, 12)
+    dev = ctx.upload(np.concatenate([np.zeros(1, np.uint8), data]))
+    ctx.build_device_bases(dev.ptr + 1, data.size, 12)
     assert compare_digest(gcz.digest(ctx.tree()), ref) == {}
+    with pytest.raises(gcz.GczError) as ei:          # aligned path; byte 0 is not a base
+        ctx.build_device_bases(dev.ptr, data.size + 1, 12)
+    assert ei.value.code == gcz.GCZ_ERR_SYMBOL and ei.value.info["error_offset"] == 0
+    leaves = ctx.upload(np.frombuffer(bytes(range(256)) * 8, dtype=np.uint64))
+    ctx.build_device_leaves(leaves.ptr, leaves.nbytes // 8, 16)
+    dev.free(); leaves.free()
 
 
 def test_gpu_empty_and_bad_L(ctx, gcz):
