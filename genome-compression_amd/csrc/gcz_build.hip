@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -137,68 +138,156 @@ __device__ __forceinline__ u64 leaf_canonical(u64 x, int L, u32& m, u32& t, u32&
   return best;
 }
 
-// ---- hash table ------------------------------------------------------------
-// Insert-or-find; the slot's pos becomes the minimum position of the key.
-// A plain 16-B probe load may be stale (L1/L2 of this CU/XCD), but keys only
-// go EMPTY -> key and pos only decreases, so a stale read can only cause an
-// extra CAS or an extra atomicMin, never a wrong answer.
-template <bool kCount>
-__device__ __forceinline__ u32 tab_insert(Slot* __restrict__ tab, u32 mask, u64 skey, u32 pos,
-                                          Header* __restrict__ hdr) {
-  u32 s = slot_hash(skey) & mask;
-  for (u32 probe = 0; probe < kMaxProbe; ++probe) {
-    const Slot cur = tab[s];
-    u64 k = cur.key;
-    if (k == kEmpty) {
-      k = atomicCAS(&tab[s].key, kEmpty, skey);
-      if (k == kEmpty) {
-        if (kCount) atomicAdd(&hdr->inserts, 1u);
-        atomicMin(&tab[s].pos, pos);
+// ---- hash tables -------------------------------------------------------------
+// Both tables map a canonical key to (slot, minimum position).  The slot index
+// is what the insert pass records per element; flagscan reads the slot back.
+//
+// PackedTab (default): one 8-B word per slot,
+//     word = quotient(h) << (D+P) | displacement << P | pos
+// where h = mix(key) is a bijection on K key bits, the home slot is h's low c
+// bits and the quotient its high K-c bits.  The CAS that claims a slot also
+// stores the position, so a new key costs ONE memory-side atomic; repeats of a
+// key carry identical high bits and lower pos with a 64-bit atomicMin.  The
+// key is recovered exactly from (slot, word) by inverting the mix.
+// Used when quotient + displacement + position bits fit in 64.
+//
+// WideTab (fallback, e.g. L = 16 leaves): 16-B slots {key ^ 1, pos}; CAS on
+// the key then atomicMin on pos.
+//
+// Both probe linearly with a plain load first.  The load may be stale (this
+// CU's L1 / this XCD's L2), but slots only go EMPTY -> claimed and positions
+// only decrease, so staleness costs at most an extra CAS/atomicMin.
+
+__device__ __forceinline__ u32 enc_child(u32 w, u32 B) {      // pointer word -> B+3 bits
+  const u32 idx = w & kIdx;
+  const u32 code = idx == kIdx ? ((1u << B) - 1u) : idx;      // null index -> all-ones code
+  return (code << 3) | (((w >> 29) & 1u) << 2) | (((w >> 30) & 1u) << 1) | (w >> 31);
+}
+__device__ __forceinline__ u32 dec_child(u32 e, u32 B) {
+  const u32 code = e >> 3;
+  if (code == (1u << B) - 1u) return kNullWord;
+  return code | (((e >> 2) & 1u) << 29) | (((e >> 1) & 1u) << 30) | ((e & 1u) << 31);
+}
+
+struct WideTab {
+  Slot* tab;
+  u32 mask;
+  u32 limit;
+  u32 B;   // unused
+
+  __device__ __forceinline__ u64 node_key(u32 cl, u32 cr) const { return (u64(cl) << 32) | cr; }
+  __device__ __forceinline__ void node_words(u64 key, u32& cl, u32& cr) const {
+    cl = u32(key >> 32); cr = u32(key);
+  }
+  __device__ __forceinline__ u32 insert(u64 key, u32 pos, Header* __restrict__ hdr) const {
+    const u64 skey = key ^ 1ull;
+    u32 s = slot_hash(skey) & mask;
+    for (u32 probe = 0; probe < limit; ++probe) {
+      const Slot cur = tab[s];
+      u64 k = cur.key;
+      if (k == kEmpty) k = atomicCAS(&tab[s].key, kEmpty, skey);
+      if (k == kEmpty || k == skey) {
+        if (cur.pos > pos) atomicMin(&tab[s].pos, pos);
         return s;
       }
+      s = (s + 1) & mask;
     }
-    if (k == skey) {
-      if (cur.pos > pos) atomicMin(&tab[s].pos, pos);
-      return s;
-    }
-    s = (s + 1) & mask;
+    atomicOr(&hdr->overflow, 1u);
+    return 0;
   }
-  atomicOr(&hdr->overflow, 1u);
-  return 0;
-}
+  __device__ __forceinline__ void read(u32 s, u64& key, u32& pos) const {
+    const Slot sl = tab[s];
+    key = sl.key ^ 1ull;
+    pos = sl.pos;
+  }
+};
+
+struct PackedTab {
+  u64* tab;
+  u32 mask;
+  u32 limit;   // <= 2^D - 2 probes
+  u32 B;       // child index bits (node levels)
+  u32 c, P, D, sh;
+  u64 kmask, c1, c2, c1i, c2i;
+
+  __device__ __forceinline__ u64 node_key(u32 cl, u32 cr) const {
+    return (u64(enc_child(cl, B)) << (B + 3)) | enc_child(cr, B);
+  }
+  __device__ __forceinline__ void node_words(u64 key, u32& cl, u32& cr) const {
+    cl = dec_child(u32(key >> (B + 3)), B);
+    cr = dec_child(u32(key & ((1ull << (B + 3)) - 1)), B);
+  }
+  __device__ __forceinline__ u64 mix(u64 x) const {
+    x ^= x >> sh; x = (x * c1) & kmask;
+    x ^= x >> sh; x = (x * c2) & kmask;
+    x ^= x >> sh;
+    return x;
+  }
+  __device__ __forceinline__ u64 unmix(u64 h) const {
+    h ^= h >> sh; h = (h * c2i) & kmask;
+    h ^= h >> sh; h = (h * c1i) & kmask;
+    h ^= h >> sh;
+    return h;
+  }
+  __device__ __forceinline__ u32 insert(u64 key, u32 pos, Header* __restrict__ hdr) const {
+    const u64 h = mix(key);
+    u32 s = u32(h) & mask;
+    const u64 qd = (h >> c) << D;             // quotient, displacement bits free
+    const u64 pmask = (1ull << P) - 1;
+    for (u32 d = 0; d < limit; ++d) {
+      const u64 mine = ((qd | d) << P) | pos;
+      u64 cur = tab[s];
+      if (cur == kEmpty) {
+        cur = atomicCAS(&tab[s], kEmpty, mine);
+        if (cur == kEmpty) return s;
+      }
+      if ((cur >> P) == (mine >> P)) {
+        if ((cur & pmask) > pos) atomicMin(&tab[s], mine);
+        return s;
+      }
+      s = (s + 1) & mask;
+    }
+    atomicOr(&hdr->overflow, 1u);
+    return 0;
+  }
+  __device__ __forceinline__ void read(u32 s, u64& key, u32& pos) const {
+    const u64 w = tab[s];
+    pos = u32(w & ((1ull << P) - 1));
+    const u32 d = u32((w >> P) & ((1ull << D) - 1));
+    const u64 q = w >> (P + D);
+    const u64 home = (s - d) & mask;
+    key = unmix((q << c) | home);
+  }
+};
 
 // ---- kernels -----------------------------------------------------------------
 
+// nac codes of an ASCII byte, include/dna.h:20-32 (to_nac, src/dna.cpp:25-49); -1 unknown
+__device__ __forceinline__ int nac_code(int c) {
+  const int u = (c >= 'a' && c <= 'z') ? c - 32 : c;
+  switch (u) {
+    case 'A': return 1;  case 'C': return 2;  case 'G': return 4;  case 'T': return 8;
+    case 'R': return 3;  case 'Y': return 12; case 'K': return 7;  case 'M': return 14;
+    case 'B': return 5;  case 'V': return 10; case 'D': return 11; case 'H': return 13;
+    case 'S': return 0;  case 'W': return 9;  case 'N': return 6;  case '-': return 15;
+    default: return -1;
+  }
+}
+
 // Leaf level from raw bases: pack L symbols (dna::dna(string_view) +
-// dna::set, dna.cpp:79-84,187-197; to_nac :25-49), canonicalise, insert.
+// dna::set, dna.cpp:79-84,187-197), canonicalise (dna.cpp:135-143), insert.
 // Bases for the block are staged through LDS with coalesced 4-B loads.
-template <int L, bool kCount>
-__global__ __launch_bounds__(kBlock) void k_leaf_bases(const unsigned char* __restrict__ bases,
-                                                      u64 S, Slot* __restrict__ tab, u32 mask,
+template <int L, class Tab>
+__global__ __launch_bounds__(kBlock) void k_leaf_bases(const unsigned char* __restrict__ bases, u64 S, Tab T,
                                                       u32* __restrict__ rec, Header* __restrict__ hdr) {
   __shared__ signed char lut[256];
   __shared__ __align__(16) unsigned char buf[kBlock * L + 16];
   const int tid = threadIdx.x;
-  {
-    // nac codes, include/dna.h:20-32; -1 = unknown symbol
-    int c = tid;
-    int code = -1;
-    const int u = (c >= 'a' && c <= 'z') ? c - 32 : c;
-    switch (u) {
-      case 'A': code = 1; break;  case 'C': code = 2; break;  case 'G': code = 4; break;
-      case 'T': code = 8; break;  case 'R': code = 3; break;  case 'Y': code = 12; break;
-      case 'K': code = 7; break;  case 'M': code = 14; break; case 'B': code = 5; break;
-      case 'V': code = 10; break; case 'D': code = 11; break; case 'H': code = 13; break;
-      case 'S': code = 0; break;  case 'W': code = 9; break;  case 'N': code = 6; break;
-      case '-': code = 15; break; default: break;
-    }
-    lut[c] = (signed char)code;
-  }
+  lut[tid] = (signed char)nac_code(tid);
   const u64 first = u64(blockIdx.x) * kBlock;
   const u64 nstr = (S - first) < u64(kBlock) ? (S - first) : u64(kBlock);
-  const u64 byte0 = first * L;
+  const u64 byte0 = first * L;                 // multiple of 4 (kBlock = 256)
   const u64 nbytes = nstr * L;
-  // byte0 is a multiple of 4 when L*kBlock is (always: kBlock = 256)
   const u32* src = reinterpret_cast<const u32*>(bases + byte0);
   u32* dst = reinterpret_cast<u32*>(buf);
   const u32 nwords = u32(nbytes / 4);
@@ -218,28 +307,27 @@ __global__ __launch_bounds__(kBlock) void k_leaf_bases(const unsigned char* __re
   if (bad >= 0) atomicMin(&hdr->err_offset, i * L + u64(bad));
   u32 m, t, v;
   const u64 key = leaf_canonical(x, L, m, t, v);
-  const u32 s = tab_insert<kCount>(tab, mask, key ^ 1ull, u32(i), hdr);
+  const u32 s = T.insert(key, u32(i), hdr);
   rec[i] = make_word(s, m, t, v);
 }
 
 // Leaf level from packed strands (shared_tree(std::vector<dna>&)).
-template <bool kCount>
-__global__ __launch_bounds__(kBlock) void k_leaf_packed(const u64* __restrict__ leaves, u64 S, int L,
-                                                       Slot* __restrict__ tab, u32 mask,
+template <class Tab>
+__global__ __launch_bounds__(kBlock) void k_leaf_packed(const u64* __restrict__ leaves, u64 S, int L, Tab T,
                                                        u32* __restrict__ rec, Header* __restrict__ hdr) {
   const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (i >= S) return;
   u32 m, t, v;
   const u64 key = leaf_canonical(leaves[i], L, m, t, v);
-  const u32 s = tab_insert<kCount>(tab, mask, key ^ 1ull, u32(i), hdr);
+  const u32 s = T.insert(key, u32(i), hdr);
   rec[i] = make_word(s, m, t, v);
 }
 
 // Node level: pair (2j, 2j+1) of the previous level's final words; the odd
 // tail pairs with the null pointer (foreach_pair, include/utility.h:17-29).
 // tree_constructor::emplace_node, src/shared_tree.cpp:662-672.
-__global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ in, u64 n, u64 p,
-                                                       Slot* __restrict__ tab, u32 mask,
+template <class Tab>
+__global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ in, u64 n, u64 p, Tab T,
                                                        u32* __restrict__ rec, Header* __restrict__ hdr) {
   const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (j >= p) return;
@@ -253,8 +341,7 @@ __global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ 
   u32 cl, cr, m, t;
   node_canonical(l, r, cl, cr, m, t);
   const u32 v = ulw(l) == ulw(xf(r, 1, 0));      // left == right.mirrored() (:670)
-  const u64 key = (u64(cl) << 32) | cr;
-  const u32 s = tab_insert<false>(tab, mask, key ^ 1ull, u32(j), hdr);
+  const u32 s = T.insert(T.node_key(cl, cr), u32(j), hdr);
   rec[j] = make_word(s, m, t, v);
 }
 
@@ -270,9 +357,8 @@ constexpr u64 kValMask = (1ull << 62) - 1;
 
 // First-occurrence flags + device-wide scan (decoupled look-back) + emission.
 // kLeaf: unique output is u64 leaves, else uint2 {left,right} node words.
-template <bool kLeaf>
-__global__ __launch_bounds__(kBlock) void k_flagscan(u32* __restrict__ words, u64 p,
-                                                    const Slot* __restrict__ tab,
+template <bool kLeaf, class Tab>
+__global__ __launch_bounds__(kBlock) void k_flagscan(u32* __restrict__ words, u64 p, Tab T,
                                                     Group* __restrict__ grp, u64* __restrict__ desc,
                                                     u32* __restrict__ ticket, void* __restrict__ out,
                                                     u64* __restrict__ count_out) {
@@ -295,9 +381,7 @@ __global__ __launch_bounds__(kBlock) void k_flagscan(u32* __restrict__ words, u6
   for (int e = 0; e < kItems; ++e) {
     const u64 j = base + u64(e) * kBlock + tid;
     if (j < p) {
-      const Slot sl = tab[rec[e] & kIdx];
-      key[e] = sl.key;
-      pos[e] = sl.pos;
+      T.read(rec[e] & kIdx, key[e], pos[e]);
     } else {
       key[e] = 0; pos[e] = ~0u;
     }
@@ -359,11 +443,11 @@ __global__ __launch_bounds__(kBlock) void k_flagscan(u32* __restrict__ words, u6
     if (j >= p) continue;
     if ((mask[e] >> lane) & 1ull) {
       const u32 id = gpre + u32(__popcll(mask[e] & lt));
-      const u64 k = key[e] ^ 1ull;
       if (kLeaf) {
-        reinterpret_cast<u64*>(out)[id] = k;
+        reinterpret_cast<u64*>(out)[id] = key[e];
       } else {
-        uint2 w; w.x = u32(k >> 32); w.y = u32(k);
+        uint2 w;
+        T.node_words(key[e], w.x, w.y);
         reinterpret_cast<uint2*>(out)[id] = w;
       }
       words[j] = id | (rec[e] & kBits);
@@ -408,6 +492,64 @@ struct DevBuf {
   size_t bytes = 0;
 };
 
+u64 inv64(u64 a) {                 // inverse of an odd number mod 2^64 (Newton)
+  u64 x = a;
+  for (int i = 0; i < 6; ++i) x *= 2 - a * x;
+  return x;
+}
+
+u32 bit_width(u64 x) {
+  u32 b = 0;
+  while (x) { ++b; x >>= 1; }
+  return b;
+}
+
+u32 log2_exact(u64 x) { return bit_width(x) - 1; }
+
+constexpr u32 kAdaptiveProbeLimit = 256;
+constexpr u64 kMixC1 = 0x9E3779B97F4A7C15ull;
+constexpr u64 kMixC2 = 0xD6E8FEB86659FD93ull;
+
+// A level's table: packed 8-B words when quotient+displacement+position fit
+// in 64 bits, else 16-B wide slots.
+struct LevelTab {
+  bool packed = false;
+  PackedTab pt{};
+  WideTab wt{};
+  u64 cap = 0;
+  u64 bytes() const { return cap * (packed ? 8 : 16); }
+};
+
+LevelTab plan_table(void* buf, u64 cap, u32 K, u64 npos, u32 B, bool allow_packed, u32 wide_limit) {
+  LevelTab lt;
+  lt.cap = cap;
+  const u32 c = log2_exact(cap);
+  const u32 Q = K > c ? K - c : 0;
+  const u32 P = std::max<u32>(1, bit_width(npos - 1));
+  const int room = 64 - int(Q) - int(P);
+  if (allow_packed && K <= 64 && room >= 6) {
+    lt.packed = true;
+    PackedTab& t = lt.pt;
+    t.tab = static_cast<u64*>(buf);
+    t.mask = u32(cap - 1);
+    t.D = u32(std::min(room, 8));
+    t.limit = (1u << t.D) - 2;
+    t.B = B;
+    t.c = c;
+    t.P = P;
+    t.sh = (K + 1) / 2;
+    t.kmask = K >= 64 ? ~0ull : ((1ull << K) - 1);
+    t.c1 = kMixC1; t.c2 = kMixC2;
+    t.c1i = inv64(kMixC1); t.c2i = inv64(kMixC2);
+  } else {
+    lt.wt.tab = static_cast<Slot*>(buf);
+    lt.wt.mask = u32(cap - 1);
+    lt.wt.limit = wide_limit;
+    lt.wt.B = B;
+  }
+  return lt;
+}
+
 enum KernelId { KID_LEAF, KID_NODE, KID_FLAGSCAN_LEAF, KID_FLAGSCAN_NODE, KID_RESOLVE, KID_MEMSET, KID_COUNT };
 const char* kKernelNames[KID_COUNT] = {"leaf_insert", "node_insert", "flagscan_leaf", "flagscan_node",
                                        "resolve", "table_clear"};
@@ -427,6 +569,7 @@ struct gcz_ctx {
   u64 leaf_cap_hint = 0;
   // profiling
   bool profile = false;
+  bool force_wide = false;   // GCZ_TABLE=wide: always use 16-B slots (testing)
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> event_pool;
   size_t event_used = 0;
@@ -489,19 +632,12 @@ struct gcz_ctx {
 
 namespace {
 
-template <int L>
-void launch_leaf_bases_L(bool count, dim3 g, hipStream_t st, const unsigned char* b, u64 S, Slot* tab,
-                         u32 mask, u32* rec, Header* hdr) {
-  if (count)
-    hipLaunchKernelGGL((k_leaf_bases<L, true>), g, dim3(kBlock), 0, st, b, S, tab, mask, rec, hdr);
-  else
-    hipLaunchKernelGGL((k_leaf_bases<L, false>), g, dim3(kBlock), 0, st, b, S, tab, mask, rec, hdr);
-}
-
-void launch_leaf_bases(int L, bool count, dim3 g, hipStream_t st, const unsigned char* b, u64 S, Slot* tab,
-                       u32 mask, u32* rec, Header* hdr) {
+template <class Tab>
+void launch_leaf_bases(int L, dim3 g, hipStream_t st, const unsigned char* b, u64 S, const Tab& T, u32* rec,
+                       Header* hdr) {
   switch (L) {
-#define GCZ_CASE(X) case X: launch_leaf_bases_L<X>(count, g, st, b, S, tab, mask, rec, hdr); break;
+#define GCZ_CASE(X) \
+  case X: hipLaunchKernelGGL((k_leaf_bases<X, Tab>), g, dim3(kBlock), 0, st, b, S, T, rec, hdr); break;
     GCZ_CASE(1) GCZ_CASE(2) GCZ_CASE(3) GCZ_CASE(4) GCZ_CASE(5) GCZ_CASE(6) GCZ_CASE(7) GCZ_CASE(8)
     GCZ_CASE(9) GCZ_CASE(10) GCZ_CASE(11) GCZ_CASE(12) GCZ_CASE(13) GCZ_CASE(14) GCZ_CASE(15) GCZ_CASE(16)
 #undef GCZ_CASE
@@ -542,27 +678,26 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   }
 
   // leaf table: big enough for S when S is small; otherwise start at 2^23 slots
-  // (every ACGT 12-mer class fits) and grow if the unique count overflows it.
+  // (every ACGT 12-mer class fits) and grow if the probe bound overflows.
   const u64 full_cap = std::max<u64>(256, next_pow2(2 * S));
   u64 leaf_cap = full_cap;
   if (S > (1ull << 22)) leaf_cap = std::min(full_cap, std::max<u64>(1ull << 23, leaf_cap_hint));
   const u64 node_cap0 = std::max<u64>(256, next_pow2(2 * pk[0]));
 
+  u32* in = nullptr;
   int rc;
   if ((rc = ensure(wa, S * 4 + 16))) return rc;
   if ((rc = ensure(wb, ((S + 1) / 2) * 4 + 16))) return rc;
   if ((rc = ensure(grp, ((S + 63) / 64 + kGroupsPerTile) * sizeof(Group)))) return rc;
   if ((rc = ensure(desc, ntiles_total * 8 + 64))) return rc;
-  if ((rc = ensure(tab, std::max(leaf_cap, node_cap0) * sizeof(Slot)))) return rc;
   if ((rc = ensure(leaves_out, S * 8 + 16))) return rc;
   if ((rc = ensure(nodes_out, layer_off[D] * 8 + 16))) return rc;
   if ((rc = ensure(hdr, sizeof(Header)))) return rc;
   if (!h_hdr) HIP_TRY(hipHostMalloc((void**)&h_hdr, sizeof(Header), hipHostMallocDefault));
 
   Header* d_hdr = static_cast<Header*>(hdr.ptr);
-  Slot* d_tab = static_cast<Slot*>(tab.ptr);
   u32* A = static_cast<u32*>(wa.ptr);
-  u32* B = static_cast<u32*>(wb.ptr);
+  u32* Bw = static_cast<u32*>(wb.ptr);
   Group* d_grp = static_cast<Group*>(grp.ptr);
   u64* d_desc = static_cast<u64*>(desc.ptr);
 
@@ -570,97 +705,118 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     HIP_TRY(hipEventCreate(&ev_start));
     HIP_TRY(hipEventCreate(&ev_stop));
   }
-  HIP_TRY(hipEventRecord(ev_start, stream));
-  HIP_TRY(hipMemsetAsync(d_hdr, 0, sizeof(Header), stream));
-  HIP_TRY(hipMemsetAsync(&d_hdr->err_offset, 0xff, 8, stream));
-  HIP_TRY(hipMemsetAsync(d_desc, 0, ntiles_total * 8, stream));
 
-  // ---- leaf level ----
-  for (;;) {
-    const bool count = leaf_cap < 2 * S;
-    hipEvent_t e0{};
-    prof_begin(KID_MEMSET, e0);
-    HIP_TRY(hipMemsetAsync(d_tab, 0xff, leaf_cap * sizeof(Slot), stream));
-    prof_end(KID_MEMSET, e0);
-    const dim3 g(unsigned((S + kBlock - 1) / kBlock));
-    prof_begin(KID_LEAF, e0);
-    if (d_bases) {
-      launch_leaf_bases(L, count, g, stream, static_cast<const unsigned char*>(d_bases), S, d_tab,
-                        u32(leaf_cap - 1), A, d_hdr);
-    } else if (count) {
-      hipLaunchKernelGGL((k_leaf_packed<true>), g, dim3(kBlock), 0, stream, d_leaves, S, L, d_tab,
-                         u32(leaf_cap - 1), A, d_hdr);
-    } else {
-      hipLaunchKernelGGL((k_leaf_packed<false>), g, dim3(kBlock), 0, stream, d_leaves, S, L, d_tab,
-                         u32(leaf_cap - 1), A, d_hdr);
-    }
-    HIP_TRY(hipGetLastError());
-    prof_end(KID_LEAF, e0);
-    if (!count) break;
-    HIP_TRY(hipMemcpyAsync(h_hdr, d_hdr, sizeof(Header), hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    if (!h_hdr->overflow && u64(h_hdr->inserts) * 4 <= leaf_cap * 3) break;
-    leaf_cap = std::min(full_cap, leaf_cap * 8);
-    if ((rc = ensure(tab, std::max(leaf_cap, node_cap0) * sizeof(Slot)))) return rc;
-    d_tab = static_cast<Slot*>(tab.ptr);
+  for (bool allow_packed : {!force_wide, false}) {
+    HIP_TRY(hipEventRecord(ev_start, stream));
     HIP_TRY(hipMemsetAsync(d_hdr, 0, sizeof(Header), stream));
     HIP_TRY(hipMemsetAsync(&d_hdr->err_offset, 0xff, 8, stream));
-  }
-  leaf_cap_hint = leaf_cap;
-  {
-    const dim3 gs(unsigned((S + kTile - 1) / kTile));
-    hipEvent_t e0{};
-    prof_begin(KID_FLAGSCAN_LEAF, e0);
-    hipLaunchKernelGGL((k_flagscan<true>), gs, dim3(kBlock), 0, stream, A, S, d_tab, d_grp,
-                       d_desc + desc_off[0], &d_hdr->ticket[0], leaves_out.ptr, &d_hdr->count[0]);
-    HIP_TRY(hipGetLastError());
-    prof_end(KID_FLAGSCAN_LEAF, e0);
-    prof_begin(KID_RESOLVE, e0);
-    hipLaunchKernelGGL(k_resolve, dim3(unsigned((S + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, A, S,
-                       d_grp);
-    HIP_TRY(hipGetLastError());
-    prof_end(KID_RESOLVE, e0);
-  }
+    HIP_TRY(hipMemsetAsync(d_desc, 0, ntiles_total * 8, stream));
+    if ((rc = ensure(tab, std::max(leaf_cap, node_cap0) * 16))) return rc;
 
-  // ---- node layers ----
-  u32* in = A;
-  u32* outw = B;
-  u64 n = S;
-  for (int k = 0; k < D; ++k) {
-    const u64 p = pk[k];
-    const u64 cap = std::max<u64>(256, next_pow2(2 * p));
-    hipEvent_t e0{};
-    prof_begin(KID_MEMSET, e0);
-    HIP_TRY(hipMemsetAsync(d_tab, 0xff, cap * sizeof(Slot), stream));
-    prof_end(KID_MEMSET, e0);
-    prof_begin(KID_NODE, e0);
-    hipLaunchKernelGGL(k_node_insert, dim3(unsigned((p + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, in, n,
-                       p, d_tab, u32(cap - 1), outw, d_hdr);
+    // ---- leaf level ----
+    LevelTab lt;
+    for (;;) {
+      const bool adaptive = leaf_cap < 2 * S;
+      const u32 limit = adaptive ? kAdaptiveProbeLimit : kMaxProbe;
+      // packed leaves only from bases (< 2^4L by construction); user leaves may carry any bits
+      lt = plan_table(tab.ptr, leaf_cap, d_bases ? 4 * u32(L) : 64, S, 0, allow_packed && d_bases, limit);
+      if (lt.packed && lt.pt.limit > limit) lt.pt.limit = limit;
+      hipEvent_t e0{};
+      prof_begin(KID_MEMSET, e0);
+      HIP_TRY(hipMemsetAsync(tab.ptr, 0xff, lt.bytes(), stream));
+      prof_end(KID_MEMSET, e0);
+      const dim3 g(unsigned((S + kBlock - 1) / kBlock));
+      prof_begin(KID_LEAF, e0);
+      if (d_bases) {
+        if (lt.packed) launch_leaf_bases(L, g, stream, static_cast<const unsigned char*>(d_bases), S, lt.pt, A, d_hdr);
+        else launch_leaf_bases(L, g, stream, static_cast<const unsigned char*>(d_bases), S, lt.wt, A, d_hdr);
+      } else {
+        hipLaunchKernelGGL((k_leaf_packed<WideTab>), g, dim3(kBlock), 0, stream, d_leaves, S, L, lt.wt, A, d_hdr);
+      }
+      HIP_TRY(hipGetLastError());
+      prof_end(KID_LEAF, e0);
+      if (!adaptive) break;
+      HIP_TRY(hipMemcpyAsync(h_hdr, d_hdr, sizeof(Header), hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      if (!h_hdr->overflow) break;
+      leaf_cap = std::min(full_cap, leaf_cap * 8);
+      if ((rc = ensure(tab, std::max(leaf_cap, node_cap0) * 16))) return rc;
+      HIP_TRY(hipMemsetAsync(d_hdr, 0, sizeof(Header), stream));
+      HIP_TRY(hipMemsetAsync(&d_hdr->err_offset, 0xff, 8, stream));
+    }
+    leaf_cap_hint = leaf_cap;
+    {
+      const dim3 gs(unsigned((S + kTile - 1) / kTile));
+      hipEvent_t e0{};
+      prof_begin(KID_FLAGSCAN_LEAF, e0);
+      if (lt.packed)
+        hipLaunchKernelGGL((k_flagscan<true, PackedTab>), gs, dim3(kBlock), 0, stream, A, S, lt.pt, d_grp,
+                           d_desc + desc_off[0], &d_hdr->ticket[0], leaves_out.ptr, &d_hdr->count[0]);
+      else
+        hipLaunchKernelGGL((k_flagscan<true, WideTab>), gs, dim3(kBlock), 0, stream, A, S, lt.wt, d_grp,
+                           d_desc + desc_off[0], &d_hdr->ticket[0], leaves_out.ptr, &d_hdr->count[0]);
+      HIP_TRY(hipGetLastError());
+      prof_end(KID_FLAGSCAN_LEAF, e0);
+      prof_begin(KID_RESOLVE, e0);
+      hipLaunchKernelGGL(k_resolve, dim3(unsigned((S + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, A, S,
+                         d_grp);
+      HIP_TRY(hipGetLastError());
+      prof_end(KID_RESOLVE, e0);
+    }
+
+    // ---- node layers ----
+    in = A;
+    u32* outw = Bw;
+    u64 n = S;
+    u64 bound = std::min(S, leaf_cap);        // child ids of layer 0 are leaf ids < #slots
+    for (int k = 0; k < D; ++k) {
+      const u64 p = pk[k];
+      const u64 cap = std::max<u64>(256, next_pow2(2 * p));
+      const u32 Bk = std::max<u32>(1, bit_width(bound));
+      const LevelTab nt = plan_table(tab.ptr, cap, 2 * (Bk + 3), p, Bk, allow_packed, kMaxProbe);
+      hipEvent_t e0{};
+      prof_begin(KID_MEMSET, e0);
+      HIP_TRY(hipMemsetAsync(tab.ptr, 0xff, nt.bytes(), stream));
+      prof_end(KID_MEMSET, e0);
+      prof_begin(KID_NODE, e0);
+      const dim3 gi(unsigned((p + kBlock - 1) / kBlock));
+      if (nt.packed)
+        hipLaunchKernelGGL((k_node_insert<PackedTab>), gi, dim3(kBlock), 0, stream, in, n, p, nt.pt, outw, d_hdr);
+      else
+        hipLaunchKernelGGL((k_node_insert<WideTab>), gi, dim3(kBlock), 0, stream, in, n, p, nt.wt, outw, d_hdr);
+      HIP_TRY(hipGetLastError());
+      prof_end(KID_NODE, e0);
+      prof_begin(KID_FLAGSCAN_NODE, e0);
+      const dim3 gs(unsigned((p + kTile - 1) / kTile));
+      uint2* out_k = static_cast<uint2*>(nodes_out.ptr) + layer_off[k];
+      if (nt.packed)
+        hipLaunchKernelGGL((k_flagscan<false, PackedTab>), gs, dim3(kBlock), 0, stream, outw, p, nt.pt, d_grp,
+                           d_desc + desc_off[k + 1], &d_hdr->ticket[k + 1], out_k, &d_hdr->count[k + 1]);
+      else
+        hipLaunchKernelGGL((k_flagscan<false, WideTab>), gs, dim3(kBlock), 0, stream, outw, p, nt.wt, d_grp,
+                           d_desc + desc_off[k + 1], &d_hdr->ticket[k + 1], out_k, &d_hdr->count[k + 1]);
+      HIP_TRY(hipGetLastError());
+      prof_end(KID_FLAGSCAN_NODE, e0);
+      prof_begin(KID_RESOLVE, e0);
+      hipLaunchKernelGGL(k_resolve, gi, dim3(kBlock), 0, stream, outw, p, d_grp);
+      HIP_TRY(hipGetLastError());
+      prof_end(KID_RESOLVE, e0);
+      std::swap(in, outw);
+      n = p;
+      bound = p;
+    }
+    hipLaunchKernelGGL(k_root, dim3(1), dim3(1), 0, stream, in, d_hdr);
     HIP_TRY(hipGetLastError());
-    prof_end(KID_NODE, e0);
-    prof_begin(KID_FLAGSCAN_NODE, e0);
-    hipLaunchKernelGGL((k_flagscan<false>), dim3(unsigned((p + kTile - 1) / kTile)), dim3(kBlock), 0, stream,
-                       outw, p, d_tab, d_grp, d_desc + desc_off[k + 1], &d_hdr->ticket[k + 1],
-                       static_cast<uint2*>(nodes_out.ptr) + layer_off[k], &d_hdr->count[k + 1]);
-    HIP_TRY(hipGetLastError());
-    prof_end(KID_FLAGSCAN_NODE, e0);
-    prof_begin(KID_RESOLVE, e0);
-    hipLaunchKernelGGL(k_resolve, dim3(unsigned((p + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, outw, p,
-                       d_grp);
-    HIP_TRY(hipGetLastError());
-    prof_end(KID_RESOLVE, e0);
-    std::swap(in, outw);
-    n = p;
+    HIP_TRY(hipEventRecord(ev_stop, stream));
+    HIP_TRY(hipMemcpyAsync(h_hdr, d_hdr, sizeof(Header), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, ev_start, ev_stop));
+    info.build_ms = ms;
+    if (profile) prof_collect();
+    // a packed table whose displacement field overflowed: rebuild with wide slots
+    if (!(h_hdr->overflow && allow_packed)) break;
   }
-  hipLaunchKernelGGL(k_root, dim3(1), dim3(1), 0, stream, in, d_hdr);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(ev_stop, stream));
-  HIP_TRY(hipMemcpyAsync(h_hdr, d_hdr, sizeof(Header), hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipStreamSynchronize(stream));
-  float ms = 0.f;
-  HIP_TRY(hipEventElapsedTime(&ms, ev_start, ev_stop));
-  info.build_ms = ms;
-  if (profile) prof_collect();
 
   if (h_hdr->err_offset != ~0ull) {
     info.error_offset = h_hdr->err_offset;
@@ -673,6 +829,8 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   if (h_hdr->overflow) return fail(GCZ_ERR_CAPACITY, "build", "hash table probe limit exceeded");
   info.n_layers = D;
   info.n_leaves = h_hdr->count[0];
+  // keep the next build's adaptive leaf table at load <= 1/2 (speed only)
+  leaf_cap_hint = std::max(leaf_cap_hint, next_pow2(2 * info.n_leaves));
   for (int k = 0; k < D; ++k) info.layer_size[k] = h_hdr->count[k + 1];
   info.root = h_hdr->root;
   return GCZ_OK;
@@ -694,6 +852,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
     return GCZ_ERR_DEVICE;
   }
   c->stream = c->own_stream;
+  if (const char* t = std::getenv("GCZ_TABLE")) c->force_wide = std::strcmp(t, "wide") == 0;
   *out = c;
   return GCZ_OK;
 }

@@ -19,6 +19,18 @@ def ctx(gcz):
     c.close()
 
 
+@pytest.fixture(scope="module")
+def ctx_wide(gcz):
+    """A context forced onto the 16-B wide table (the fallback path)."""
+    os.environ["GCZ_TABLE"] = "wide"
+    try:
+        c = gcz.Context(0)
+    finally:
+        del os.environ["GCZ_TABLE"]
+    yield c
+    c.close()
+
+
 def _names(max_bases):
     with open(os.path.join(GOLDEN, "manifest.json")) as f:
         m = json.load(f)
@@ -46,6 +58,15 @@ def test_gpu_matches_reference_goldens(name, ctx, gcz, manifest):
     assert info["n_strands"] == exp["width"]
     got = gcz.digest(ctx.tree())
     assert compare_digest(got, exp) == {}
+
+
+@pytest.mark.parametrize("name", ["corpus/chmpxx", "corpus/merged", "fasta/iupac_stress", "lsweep/chmpxx_L16",
+                                  "lsweep/chmpxx_L3", "vectors/L16_edges_S5000", "synth/tandem_10000000"])
+def test_gpu_wide_table_path(name, ctx_wide, gcz, manifest):
+    case = manifest[name]
+    kind, payload, L = case_input(case, gcz)
+    _build(ctx_wide, kind, payload, L)
+    assert compare_digest(gcz.digest(ctx_wide.tree()), case["expect"]) == {}
 
 
 @pytest.mark.parametrize("name", ["chmpxx", "hehcmv"])
