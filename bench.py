@@ -59,17 +59,19 @@ def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes):
         if p == 1:
             break
         n = p
+    U = n_leaves
     if kernel == "leaf_insert":     # ASCII in, provisional word out, one table sector per strand
         return S * L + 4 * S + 64 * S
     if kernel == "node_insert":     # pair in, word out, one table sector per pair
         return sum(8 * p + 4 * p + 64 * p for p in pk)
-    if kernel == "flagscan_leaf":   # word in/out, slot read, group record, unique leaves out
-        return 4 * S + 64 * S + 4 * S + 16 * ((S + 63) // 64) + 8 * n_leaves
-    if kernel == "flagscan_node":
-        return sum(4 * p + 64 * p + 4 * p + 16 * ((p + 63) // 64) for p in pk) + 8 * sum(layer_sizes)
-    if kernel == "resolve":         # word in; non-first: group sector read + word out
-        nf = (S - n_leaves) + sum(p - u for p, u in zip(pk, layer_sizes))
-        return 4 * (S + sum(pk)) + 16 * ((S + sum(pk) + 63) // 64) + 68 * nf
+    if kernel == "flagscan_leaf":   # not-first marks; firsts: word, slot sector, leaf out, slot->id sector
+        return S + U * (4 + 64 + 8 + 64 + 4)
+    if kernel == "flagscan_node":   # not-first marks, group records; firsts: pair re-read, node out, word
+        return sum(p + 16 * ((p + 63) // 64) + u * (8 + 8 + 4 + 4) for p, u in zip(pk, layer_sizes))
+    if kernel == "resolve_leaf":    # marks; non-first: word, slot->id sector, word
+        return S + (S - U) * (4 + 64 + 4)
+    if kernel == "resolve_node":    # marks; non-first: word, slot sector, group sector, word
+        return sum(p + (p - u) * (4 + 64 + 64 + 4) for p, u in zip(pk, layer_sizes))
     return 0
 
 

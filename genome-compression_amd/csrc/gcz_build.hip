@@ -1,23 +1,5 @@
-// MI355X (gfx950) shared_tree construction: leaf packing, per-level
-// canonicalise + hash-cons, first-occurrence ID assignment, unique emission.
-//
-// Replaces tree_constructor (reference include/shared_tree.h:245-316,
-// src/shared_tree.cpp:621-763).  One global level-by-level build; the
-// reference's 2^22/2^25-strand segmentation is output-invisible.
-//
-// Per level (n input words -> p = ceil(n/2) pairs; the leaf level has p = S):
-//   insert    canonical key of each pair/leaf -> open-addressing table in HBM:
-//             CAS on the 64-bit key, atomicMin of the position.  Writes the
-//             provisional word rec[j] = slot | m<<29 | t<<30 | v<<31.
-//   flagscan  first occurrence <=> slot.pos == j.  Wave ballot -> 64-element
-//             group masks; in-tile scan + decoupled look-back across tiles ->
-//             group prefixes; first occurrences get id = first-occurrence rank,
-//             emit the unique node/leaf at out[id] and their final word.
-//             Others keep minpos in place of the slot index.
-//   resolve   non-first occurrences: id = rank of minpos from its group's
-//             {mask, prefix} (one 16-B read into a p/4-byte array).
-// The next level reads the final words directly (coalesced); no per-element
-// id table lookups remain.
+// MI355X (gfx950) shared_tree construction: host orchestration and the C ABI.
+// Device code and the algorithm description: gcz_device.h.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -27,451 +9,11 @@
 #include <string>
 #include <vector>
 
-#include "gcz_internal.h"
+#include "gcz_device.h"
 
 namespace {
 
-using u32 = uint32_t;
-using u64 = unsigned long long;
-
-constexpr u32 kNullWord = 0x9fffffffu;
-constexpr u32 kIdx = 0x1fffffffu;
-constexpr u32 kBits = 0xe0000000u;
-constexpr u64 kEmpty = ~0ull;              // stored key; stored = key ^ 1 (see kEmpty note below)
-constexpr int kBlock = 256;
-constexpr int kItems = 8;                  // flagscan elements per thread
-constexpr int kTile = kBlock * kItems;     // 2048 elements per look-back tile
-constexpr int kGroupsPerTile = kTile / 64; // 32
-constexpr u32 kMaxProbe = 1u << 16;
-
-// kEmpty note: table keys are stored as key ^ 1, so a stored ~0 means key
-// 0xffff_ffff_ffff_fffe.  That value is never a key: as a leaf its transpose
-// (..fff7) is smaller so it is never canonical (dna.cpp:135-143); as a node
-// its left word would carry both the mirror and invariant bits, which the
-// pointer ctor forbids (shared_tree.cpp:85-86).  memset(0xff) clears a table.
-
-struct __align__(16) Slot {
-  u64 key;
-  u32 pos;
-  u32 pad;
-};
-struct __align__(16) Group {
-  u64 mask;    // first-occurrence flags of 64 consecutive elements
-  u32 prefix;  // first occurrences before this group (global, this level)
-  u32 pad;
-};
-
-struct Header {
-  u64 count[GCZ_MAX_LAYERS + 1];  // [0] unique leaves, [1+k] unique nodes of layer k
-  u64 err_offset;                 // first unknown symbol (min), ~0 if none
-  u32 overflow;
-  u32 inserts;                    // new keys in an adaptively sized leaf table
-  u32 ticket[GCZ_MAX_LAYERS + 1]; // look-back tile tickets per level
-  u32 root;
-  u32 pad;
-};
-
-__device__ __forceinline__ u32 slot_hash(u64 k) {
-  k ^= k >> 31;
-  k *= 0x7fb5d329728ea185ull;
-  k ^= k >> 27;
-  k *= 0x81dadef4bc2dd44dull;
-  k ^= k >> 33;
-  return u32(k);
-}
-
-// ---- word algebra: reference src/shared_tree.cpp:76-107 -------------------
-__device__ __forceinline__ u32 ulw(u32 w) { return w & 0x7fffffffu; }
-// transform ctor (shared_tree.cpp:76-80): m' = (M != m) && !v ; t' = (T != t) && !null
-__device__ __forceinline__ u32 xf(u32 w, u32 M, u32 T) {
-  const u32 v = w >> 31, m = (w >> 29) & 1u, t = (w >> 30) & 1u;
-  const u32 nm = (M ^ m) & (v ^ 1u);
-  const u32 nt = (T ^ t) & u32(ulw(w) != kIdx);
-  return (w & 0x9fffffffu) | (nm << 29) | (nt << 30);
-}
-__device__ __forceinline__ u32 make_word(u32 idx, u32 m, u32 t, u32 v) {
-  return idx | ((m & (v ^ 1u)) << 29) | (t << 30) | (v << 31);
-}
-
-// node::canonical (include/shared_tree.h:115-126): min over (key, m, t).
-// Candidates id=(l,r) mir=(M(r),M(l)) tra=(T(l),T(r)) inv=(I(r),I(l)).
-__device__ __forceinline__ void node_canonical(u32 l, u32 r, u32& cl, u32& cr, u32& cm, u32& ct) {
-  const u32 ml = xf(l, 1, 0), mr = xf(r, 1, 0);
-  const u32 tl = xf(l, 0, 1), tr = xf(r, 0, 1);
-  const u32 il = xf(l, 1, 1), ir = xf(r, 1, 1);
-  // key with (m,t) appended below it: lexicographic (key, m, t) in one 66-bit compare.
-  // key fits in 62 bits, so (key << 2 | m << 1 | t) is exact in 64 bits.
-  auto k = [](u32 a, u32 b, u32 m, u32 t) -> u64 {
-    return ((u64(ulw(a)) << 31 | ulw(b)) << 2) | (m << 1) | t;
-  };
-  u64 best = k(l, r, 0, 0);
-  cl = l; cr = r; cm = 0; ct = 0;
-  u64 c = k(mr, ml, 1, 0);
-  if (c < best) { best = c; cl = mr; cr = ml; cm = 1; ct = 0; }
-  c = k(tl, tr, 0, 1);
-  if (c < best) { best = c; cl = tl; cr = tr; cm = 0; ct = 1; }
-  c = k(ir, il, 1, 1);
-  if (c < best) { best = c; cl = ir; cr = il; cm = 1; ct = 1; }
-}
-
-// ---- leaf codec: reference src/dna.cpp:104-143 -----------------------------
-__device__ __forceinline__ u64 leaf_transposed(u64 v) {
-  v = ((v >> 1) & 0x5555555555555555ull) | ((v & 0x5555555555555555ull) << 1);
-  v = ((v >> 2) & 0x3333333333333333ull) | ((v & 0x3333333333333333ull) << 2);
-  return v;
-}
-// reverse the low L nibbles (higher nibbles dropped), dna::mirrored :116-121
-__device__ __forceinline__ u64 leaf_mirrored(u64 v, int L) {
-  u64 y = __builtin_bswap64(v);
-  y = ((y >> 4) & 0x0f0f0f0f0f0f0f0full) | ((y & 0x0f0f0f0f0f0f0f0full) << 4);
-  return L == 16 ? y : (y >> (64 - 4 * L));
-}
-__device__ __forceinline__ u64 leaf_canonical(u64 x, int L, u32& m, u32& t, u32& v) {
-  const u64 tx = leaf_transposed(x);
-  const u64 mx = leaf_mirrored(x, L);
-  const u64 ix = leaf_mirrored(tx, L);
-  v = x == mx;
-  u64 best = x; m = 0; t = 0;
-  if (tx < best) { best = tx; m = 0; t = 1; }
-  if (mx < best) { best = mx; m = 1; t = 0; }
-  if (ix < best) { best = ix; m = 1; t = 1; }
-  return best;
-}
-
-// ---- hash tables -------------------------------------------------------------
-// Both tables map a canonical key to (slot, minimum position).  The slot index
-// is what the insert pass records per element; flagscan reads the slot back.
-//
-// PackedTab (default): one 8-B word per slot,
-//     word = quotient(h) << (D+P) | displacement << P | pos
-// where h = mix(key) is a bijection on K key bits, the home slot is h's low c
-// bits and the quotient its high K-c bits.  The CAS that claims a slot also
-// stores the position, so a new key costs ONE memory-side atomic; repeats of a
-// key carry identical high bits and lower pos with a 64-bit atomicMin.  The
-// key is recovered exactly from (slot, word) by inverting the mix.
-// Used when quotient + displacement + position bits fit in 64.
-//
-// WideTab (fallback, e.g. L = 16 leaves): 16-B slots {key ^ 1, pos}; CAS on
-// the key then atomicMin on pos.
-//
-// Both probe linearly with a plain load first.  The load may be stale (this
-// CU's L1 / this XCD's L2), but slots only go EMPTY -> claimed and positions
-// only decrease, so staleness costs at most an extra CAS/atomicMin.
-
-__device__ __forceinline__ u32 enc_child(u32 w, u32 B) {      // pointer word -> B+3 bits
-  const u32 idx = w & kIdx;
-  const u32 code = idx == kIdx ? ((1u << B) - 1u) : idx;      // null index -> all-ones code
-  return (code << 3) | (((w >> 29) & 1u) << 2) | (((w >> 30) & 1u) << 1) | (w >> 31);
-}
-__device__ __forceinline__ u32 dec_child(u32 e, u32 B) {
-  const u32 code = e >> 3;
-  if (code == (1u << B) - 1u) return kNullWord;
-  return code | (((e >> 2) & 1u) << 29) | (((e >> 1) & 1u) << 30) | ((e & 1u) << 31);
-}
-
-struct WideTab {
-  Slot* tab;
-  u32 mask;
-  u32 limit;
-  u32 B;   // unused
-
-  __device__ __forceinline__ u64 node_key(u32 cl, u32 cr) const { return (u64(cl) << 32) | cr; }
-  __device__ __forceinline__ void node_words(u64 key, u32& cl, u32& cr) const {
-    cl = u32(key >> 32); cr = u32(key);
-  }
-  __device__ __forceinline__ u32 insert(u64 key, u32 pos, Header* __restrict__ hdr) const {
-    const u64 skey = key ^ 1ull;
-    u32 s = slot_hash(skey) & mask;
-    for (u32 probe = 0; probe < limit; ++probe) {
-      const Slot cur = tab[s];
-      u64 k = cur.key;
-      if (k == kEmpty) k = atomicCAS(&tab[s].key, kEmpty, skey);
-      if (k == kEmpty || k == skey) {
-        if (cur.pos > pos) atomicMin(&tab[s].pos, pos);
-        return s;
-      }
-      s = (s + 1) & mask;
-    }
-    atomicOr(&hdr->overflow, 1u);
-    return 0;
-  }
-  __device__ __forceinline__ void read(u32 s, u64& key, u32& pos) const {
-    const Slot sl = tab[s];
-    key = sl.key ^ 1ull;
-    pos = sl.pos;
-  }
-};
-
-struct PackedTab {
-  u64* tab;
-  u32 mask;
-  u32 limit;   // <= 2^D - 2 probes
-  u32 B;       // child index bits (node levels)
-  u32 c, P, D, sh;
-  u64 kmask, c1, c2, c1i, c2i;
-
-  __device__ __forceinline__ u64 node_key(u32 cl, u32 cr) const {
-    return (u64(enc_child(cl, B)) << (B + 3)) | enc_child(cr, B);
-  }
-  __device__ __forceinline__ void node_words(u64 key, u32& cl, u32& cr) const {
-    cl = dec_child(u32(key >> (B + 3)), B);
-    cr = dec_child(u32(key & ((1ull << (B + 3)) - 1)), B);
-  }
-  __device__ __forceinline__ u64 mix(u64 x) const {
-    x ^= x >> sh; x = (x * c1) & kmask;
-    x ^= x >> sh; x = (x * c2) & kmask;
-    x ^= x >> sh;
-    return x;
-  }
-  __device__ __forceinline__ u64 unmix(u64 h) const {
-    h ^= h >> sh; h = (h * c2i) & kmask;
-    h ^= h >> sh; h = (h * c1i) & kmask;
-    h ^= h >> sh;
-    return h;
-  }
-  __device__ __forceinline__ u32 insert(u64 key, u32 pos, Header* __restrict__ hdr) const {
-    const u64 h = mix(key);
-    u32 s = u32(h) & mask;
-    const u64 qd = (h >> c) << D;             // quotient, displacement bits free
-    const u64 pmask = (1ull << P) - 1;
-    for (u32 d = 0; d < limit; ++d) {
-      const u64 mine = ((qd | d) << P) | pos;
-      u64 cur = tab[s];
-      if (cur == kEmpty) {
-        cur = atomicCAS(&tab[s], kEmpty, mine);
-        if (cur == kEmpty) return s;
-      }
-      if ((cur >> P) == (mine >> P)) {
-        if ((cur & pmask) > pos) atomicMin(&tab[s], mine);
-        return s;
-      }
-      s = (s + 1) & mask;
-    }
-    atomicOr(&hdr->overflow, 1u);
-    return 0;
-  }
-  __device__ __forceinline__ void read(u32 s, u64& key, u32& pos) const {
-    const u64 w = tab[s];
-    pos = u32(w & ((1ull << P) - 1));
-    const u32 d = u32((w >> P) & ((1ull << D) - 1));
-    const u64 q = w >> (P + D);
-    const u64 home = (s - d) & mask;
-    key = unmix((q << c) | home);
-  }
-};
-
-// ---- kernels -----------------------------------------------------------------
-
-// nac codes of an ASCII byte, include/dna.h:20-32 (to_nac, src/dna.cpp:25-49); -1 unknown
-__device__ __forceinline__ int nac_code(int c) {
-  const int u = (c >= 'a' && c <= 'z') ? c - 32 : c;
-  switch (u) {
-    case 'A': return 1;  case 'C': return 2;  case 'G': return 4;  case 'T': return 8;
-    case 'R': return 3;  case 'Y': return 12; case 'K': return 7;  case 'M': return 14;
-    case 'B': return 5;  case 'V': return 10; case 'D': return 11; case 'H': return 13;
-    case 'S': return 0;  case 'W': return 9;  case 'N': return 6;  case '-': return 15;
-    default: return -1;
-  }
-}
-
-// Leaf level from raw bases: pack L symbols (dna::dna(string_view) +
-// dna::set, dna.cpp:79-84,187-197), canonicalise (dna.cpp:135-143), insert.
-// Bases for the block are staged through LDS with coalesced 4-B loads.
-template <int L, class Tab>
-__global__ __launch_bounds__(kBlock) void k_leaf_bases(const unsigned char* __restrict__ bases, u64 S, Tab T,
-                                                      u32* __restrict__ rec, Header* __restrict__ hdr) {
-  __shared__ signed char lut[256];
-  __shared__ __align__(16) unsigned char buf[kBlock * L + 16];
-  const int tid = threadIdx.x;
-  lut[tid] = (signed char)nac_code(tid);
-  const u64 first = u64(blockIdx.x) * kBlock;
-  const u64 nstr = (S - first) < u64(kBlock) ? (S - first) : u64(kBlock);
-  const u64 byte0 = first * L;                 // multiple of 4 (kBlock = 256)
-  const u64 nbytes = nstr * L;
-  const u32* src = reinterpret_cast<const u32*>(bases + byte0);
-  u32* dst = reinterpret_cast<u32*>(buf);
-  const u32 nwords = u32(nbytes / 4);
-  for (u32 w = tid; w < nwords; w += kBlock) dst[w] = src[w];
-  for (u32 b = nwords * 4 + tid; b < nbytes; b += kBlock) buf[b] = bases[byte0 + b];
-  __syncthreads();
-  if (u64(tid) >= nstr) return;
-  u64 x = 0;
-  int bad = -1;
-#pragma unroll
-  for (int c = 0; c < L; ++c) {
-    const int code = lut[buf[tid * L + c]];
-    if (code < 0 && bad < 0) bad = c;
-    x |= u64(code & 15) << (4 * c);
-  }
-  const u64 i = first + tid;
-  if (bad >= 0) atomicMin(&hdr->err_offset, i * L + u64(bad));
-  u32 m, t, v;
-  const u64 key = leaf_canonical(x, L, m, t, v);
-  const u32 s = T.insert(key, u32(i), hdr);
-  rec[i] = make_word(s, m, t, v);
-}
-
-// Leaf level from packed strands (shared_tree(std::vector<dna>&)).
-template <class Tab>
-__global__ __launch_bounds__(kBlock) void k_leaf_packed(const u64* __restrict__ leaves, u64 S, int L, Tab T,
-                                                       u32* __restrict__ rec, Header* __restrict__ hdr) {
-  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (i >= S) return;
-  u32 m, t, v;
-  const u64 key = leaf_canonical(leaves[i], L, m, t, v);
-  const u32 s = T.insert(key, u32(i), hdr);
-  rec[i] = make_word(s, m, t, v);
-}
-
-// Node level: pair (2j, 2j+1) of the previous level's final words; the odd
-// tail pairs with the null pointer (foreach_pair, include/utility.h:17-29).
-// tree_constructor::emplace_node, src/shared_tree.cpp:662-672.
-template <class Tab>
-__global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ in, u64 n, u64 p, Tab T,
-                                                       u32* __restrict__ rec, Header* __restrict__ hdr) {
-  const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (j >= p) return;
-  u32 l, r;
-  if (2 * j + 1 < n) {
-    const uint2 w = reinterpret_cast<const uint2*>(in)[j];
-    l = w.x; r = w.y;
-  } else {
-    l = in[2 * j]; r = kNullWord;
-  }
-  u32 cl, cr, m, t;
-  node_canonical(l, r, cl, cr, m, t);
-  const u32 v = ulw(l) == ulw(xf(r, 1, 0));      // left == right.mirrored() (:670)
-  const u32 s = T.insert(T.node_key(cl, cr), u32(j), hdr);
-  rec[j] = make_word(s, m, t, v);
-}
-
-__device__ __forceinline__ u64 wave_sum(u64 v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-constexpr u64 kStA = 1ull << 62;   // tile aggregate published
-constexpr u64 kStP = 2ull << 62;   // tile inclusive prefix published
-constexpr u64 kValMask = (1ull << 62) - 1;
-
-// First-occurrence flags + device-wide scan (decoupled look-back) + emission.
-// kLeaf: unique output is u64 leaves, else uint2 {left,right} node words.
-template <bool kLeaf, class Tab>
-__global__ __launch_bounds__(kBlock) void k_flagscan(u32* __restrict__ words, u64 p, Tab T,
-                                                    Group* __restrict__ grp, u64* __restrict__ desc,
-                                                    u32* __restrict__ ticket, void* __restrict__ out,
-                                                    u64* __restrict__ count_out) {
-  __shared__ u32 s_tile;
-  __shared__ u32 s_cnt[kGroupsPerTile];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) s_tile = atomicAdd(ticket, 1u);
-  __syncthreads();
-  const u64 tile = s_tile;
-  const u64 base = tile * kTile;
-
-  u32 rec[kItems], pos[kItems];
-  u64 key[kItems], mask[kItems];
-#pragma unroll
-  for (int e = 0; e < kItems; ++e) {
-    const u64 j = base + u64(e) * kBlock + tid;
-    rec[e] = j < p ? words[j] : 0u;
-  }
-#pragma unroll
-  for (int e = 0; e < kItems; ++e) {
-    const u64 j = base + u64(e) * kBlock + tid;
-    if (j < p) {
-      T.read(rec[e] & kIdx, key[e], pos[e]);
-    } else {
-      key[e] = 0; pos[e] = ~0u;
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < kItems; ++e) {
-    const u64 j = base + u64(e) * kBlock + tid;
-    mask[e] = __ballot(j < p && u64(pos[e]) == j);
-    if (lane == 0) s_cnt[e * 4 + wave] = u32(__popcll(mask[e]));
-  }
-  __syncthreads();
-  if (wave == 0) {
-    const u32 c = lane < kGroupsPerTile ? s_cnt[lane] : 0u;
-    u32 incl = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const u32 y = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += y;
-    }
-    const u64 agg = __shfl(incl, 63, 64);
-    u64 prefix = 0;
-    if (tile == 0) {
-      if (lane == 0) __hip_atomic_store(&desc[0], kStP | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      if (lane == 0) __hip_atomic_store(&desc[tile], kStA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      long long look = (long long)tile - 1;
-      for (;;) {
-        const long long idx = look - lane;
-        const u64 d = idx >= 0 ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-        const u64 st = d >> 62;
-        const u64 pm = __ballot(st == 2);
-        const u64 zm = __ballot(st == 0);
-        const int firstP = pm ? __ffsll((long long)pm) - 1 : 64;
-        const u64 need = firstP >= 63 ? ~0ull : ((1ull << (firstP + 1)) - 1);
-        if (zm & need) {
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        prefix += wave_sum(lane <= firstP ? (d & kValMask) : 0ull);
-        if (firstP < 64) break;
-        look -= 64;
-      }
-      if (lane == 0) __hip_atomic_store(&desc[tile], kStP | (prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (lane < kGroupsPerTile) s_cnt[lane] = u32(prefix + incl - c);
-    if (lane == 0 && (tile + 1) * kTile >= p) *count_out = prefix + agg;
-  }
-  __syncthreads();
-  const u64 lt = (1ull << lane) - 1;
-#pragma unroll
-  for (int e = 0; e < kItems; ++e) {
-    const u64 j = base + u64(e) * kBlock + tid;
-    const u32 gpre = s_cnt[e * 4 + wave];
-    if (lane == 0) {
-      Group g;
-      g.mask = mask[e]; g.prefix = gpre; g.pad = 0;
-      grp[(base >> 6) + e * 4 + wave] = g;
-    }
-    if (j >= p) continue;
-    if ((mask[e] >> lane) & 1ull) {
-      const u32 id = gpre + u32(__popcll(mask[e] & lt));
-      if (kLeaf) {
-        reinterpret_cast<u64*>(out)[id] = key[e];
-      } else {
-        uint2 w;
-        T.node_words(key[e], w.x, w.y);
-        reinterpret_cast<uint2*>(out)[id] = w;
-      }
-      words[j] = id | (rec[e] & kBits);
-    } else {
-      words[j] = pos[e] | (rec[e] & kBits);
-    }
-  }
-}
-
-// Non-first occurrences: id = rank of the first occurrence (minpos).
-__global__ __launch_bounds__(kBlock) void k_resolve(u32* __restrict__ words, u64 p,
-                                                   const Group* __restrict__ grp) {
-  const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (j >= p) return;
-  const Group g = grp[j >> 6];
-  if ((g.mask >> (j & 63)) & 1ull) return;
-  const u32 w = words[j];
-  const u32 q = w & kIdx;
-  const Group h = grp[q >> 6];
-  const u32 id = h.prefix + u32(__popcll(h.mask & ((1ull << (q & 63)) - 1)));
-  words[j] = id | (w & kBits);
-}
-
-__global__ void k_root(const u32* __restrict__ words, Header* __restrict__ hdr) { hdr->root = words[0]; }
+using namespace gcz_dev;
 
 // ---- host side -----------------------------------------------------------------
 
@@ -550,9 +92,11 @@ LevelTab plan_table(void* buf, u64 cap, u32 K, u64 npos, u32 B, bool allow_packe
   return lt;
 }
 
-enum KernelId { KID_LEAF, KID_NODE, KID_FLAGSCAN_LEAF, KID_FLAGSCAN_NODE, KID_RESOLVE, KID_MEMSET, KID_COUNT };
+enum KernelId {
+  KID_LEAF, KID_NODE, KID_FLAGSCAN_LEAF, KID_FLAGSCAN_NODE, KID_RESOLVE_LEAF, KID_RESOLVE_NODE, KID_MEMSET, KID_COUNT
+};
 const char* kKernelNames[KID_COUNT] = {"leaf_insert", "node_insert", "flagscan_leaf", "flagscan_node",
-                                       "resolve", "table_clear"};
+                                       "resolve_leaf", "resolve_node", "clear"};
 
 }  // namespace
 
@@ -561,7 +105,7 @@ struct gcz_ctx {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   std::string last_error;
-  DevBuf wa, wb, grp, desc, tab, leaves_out, nodes_out, hdr, input;
+  DevBuf wa, wb, grp, desc, tab, leaves_out, nodes_out, hdr, input, nf, ids;
   Header* h_hdr = nullptr;   // pinned
   // last build
   gcz_info info{};
@@ -634,10 +178,10 @@ namespace {
 
 template <class Tab>
 void launch_leaf_bases(int L, dim3 g, hipStream_t st, const unsigned char* b, u64 S, const Tab& T, u32* rec,
-                       Header* hdr) {
+                       unsigned char* nf, Header* hdr) {
   switch (L) {
 #define GCZ_CASE(X) \
-  case X: hipLaunchKernelGGL((k_leaf_bases<X, Tab>), g, dim3(kBlock), 0, st, b, S, T, rec, hdr); break;
+  case X: hipLaunchKernelGGL((k_leaf_bases<X, Tab>), g, dim3(kBlock), 0, st, b, S, T, rec, nf, hdr); break;
     GCZ_CASE(1) GCZ_CASE(2) GCZ_CASE(3) GCZ_CASE(4) GCZ_CASE(5) GCZ_CASE(6) GCZ_CASE(7) GCZ_CASE(8)
     GCZ_CASE(9) GCZ_CASE(10) GCZ_CASE(11) GCZ_CASE(12) GCZ_CASE(13) GCZ_CASE(14) GCZ_CASE(15) GCZ_CASE(16)
 #undef GCZ_CASE
@@ -693,6 +237,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   if ((rc = ensure(leaves_out, S * 8 + 16))) return rc;
   if ((rc = ensure(nodes_out, layer_off[D] * 8 + 16))) return rc;
   if ((rc = ensure(hdr, sizeof(Header)))) return rc;
+  if ((rc = ensure(nf, S + 16))) return rc;
   if (!h_hdr) HIP_TRY(hipHostMalloc((void**)&h_hdr, sizeof(Header), hipHostMallocDefault));
 
   Header* d_hdr = static_cast<Header*>(hdr.ptr);
@@ -700,6 +245,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   u32* Bw = static_cast<u32*>(wb.ptr);
   Group* d_grp = static_cast<Group*>(grp.ptr);
   u64* d_desc = static_cast<u64*>(desc.ptr);
+  unsigned char* d_nf = static_cast<unsigned char*>(nf.ptr);
 
   if (!ev_start) {
     HIP_TRY(hipEventCreate(&ev_start));
@@ -724,14 +270,17 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       hipEvent_t e0{};
       prof_begin(KID_MEMSET, e0);
       HIP_TRY(hipMemsetAsync(tab.ptr, 0xff, lt.bytes(), stream));
+      HIP_TRY(hipMemsetAsync(d_nf, 0, S, stream));
       prof_end(KID_MEMSET, e0);
       const dim3 g(unsigned((S + kBlock - 1) / kBlock));
       prof_begin(KID_LEAF, e0);
       if (d_bases) {
-        if (lt.packed) launch_leaf_bases(L, g, stream, static_cast<const unsigned char*>(d_bases), S, lt.pt, A, d_hdr);
-        else launch_leaf_bases(L, g, stream, static_cast<const unsigned char*>(d_bases), S, lt.wt, A, d_hdr);
+        const auto* b = static_cast<const unsigned char*>(d_bases);
+        if (lt.packed) launch_leaf_bases(L, g, stream, b, S, lt.pt, A, d_nf, d_hdr);
+        else launch_leaf_bases(L, g, stream, b, S, lt.wt, A, d_nf, d_hdr);
       } else {
-        hipLaunchKernelGGL((k_leaf_packed<WideTab>), g, dim3(kBlock), 0, stream, d_leaves, S, L, lt.wt, A, d_hdr);
+        hipLaunchKernelGGL((k_leaf_packed<WideTab>), g, dim3(kBlock), 0, stream, d_leaves, S, L, lt.wt, A, d_nf,
+                           d_hdr);
       }
       HIP_TRY(hipGetLastError());
       prof_end(KID_LEAF, e0);
@@ -745,23 +294,26 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       HIP_TRY(hipMemsetAsync(&d_hdr->err_offset, 0xff, 8, stream));
     }
     leaf_cap_hint = leaf_cap;
+    if ((rc = ensure(ids, leaf_cap * 4))) return rc;
     {
+      u32* d_ids = static_cast<u32*>(ids.ptr);
       const dim3 gs(unsigned((S + kTile - 1) / kTile));
       hipEvent_t e0{};
       prof_begin(KID_FLAGSCAN_LEAF, e0);
+      u64* lo = static_cast<u64*>(leaves_out.ptr);
       if (lt.packed)
-        hipLaunchKernelGGL((k_flagscan<true, PackedTab>), gs, dim3(kBlock), 0, stream, A, S, lt.pt, d_grp,
-                           d_desc + desc_off[0], &d_hdr->ticket[0], leaves_out.ptr, &d_hdr->count[0]);
+        hipLaunchKernelGGL((k_flagscan_leaf<PackedTab>), gs, dim3(kBlock), 0, stream, A, S, lt.pt, d_nf,
+                           d_desc + desc_off[0], &d_hdr->ticket[0], lo, d_ids, &d_hdr->count[0]);
       else
-        hipLaunchKernelGGL((k_flagscan<true, WideTab>), gs, dim3(kBlock), 0, stream, A, S, lt.wt, d_grp,
-                           d_desc + desc_off[0], &d_hdr->ticket[0], leaves_out.ptr, &d_hdr->count[0]);
+        hipLaunchKernelGGL((k_flagscan_leaf<WideTab>), gs, dim3(kBlock), 0, stream, A, S, lt.wt, d_nf,
+                           d_desc + desc_off[0], &d_hdr->ticket[0], lo, d_ids, &d_hdr->count[0]);
       HIP_TRY(hipGetLastError());
       prof_end(KID_FLAGSCAN_LEAF, e0);
-      prof_begin(KID_RESOLVE, e0);
-      hipLaunchKernelGGL(k_resolve, dim3(unsigned((S + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, A, S,
-                         d_grp);
+      prof_begin(KID_RESOLVE_LEAF, e0);
+      hipLaunchKernelGGL(k_resolve_leaf, dim3(unsigned((S + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, A, S,
+                         d_nf, d_ids);
       HIP_TRY(hipGetLastError());
-      prof_end(KID_RESOLVE, e0);
+      prof_end(KID_RESOLVE_LEAF, e0);
     }
 
     // ---- node layers ----
@@ -777,30 +329,32 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       hipEvent_t e0{};
       prof_begin(KID_MEMSET, e0);
       HIP_TRY(hipMemsetAsync(tab.ptr, 0xff, nt.bytes(), stream));
+      HIP_TRY(hipMemsetAsync(d_nf, 0, p, stream));
       prof_end(KID_MEMSET, e0);
       prof_begin(KID_NODE, e0);
       const dim3 gi(unsigned((p + kBlock - 1) / kBlock));
       if (nt.packed)
-        hipLaunchKernelGGL((k_node_insert<PackedTab>), gi, dim3(kBlock), 0, stream, in, n, p, nt.pt, outw, d_hdr);
+        hipLaunchKernelGGL((k_node_insert<PackedTab>), gi, dim3(kBlock), 0, stream, in, n, p, nt.pt, outw, d_nf,
+                           d_hdr);
       else
-        hipLaunchKernelGGL((k_node_insert<WideTab>), gi, dim3(kBlock), 0, stream, in, n, p, nt.wt, outw, d_hdr);
+        hipLaunchKernelGGL((k_node_insert<WideTab>), gi, dim3(kBlock), 0, stream, in, n, p, nt.wt, outw, d_nf,
+                           d_hdr);
       HIP_TRY(hipGetLastError());
       prof_end(KID_NODE, e0);
       prof_begin(KID_FLAGSCAN_NODE, e0);
       const dim3 gs(unsigned((p + kTile - 1) / kTile));
       uint2* out_k = static_cast<uint2*>(nodes_out.ptr) + layer_off[k];
-      if (nt.packed)
-        hipLaunchKernelGGL((k_flagscan<false, PackedTab>), gs, dim3(kBlock), 0, stream, outw, p, nt.pt, d_grp,
-                           d_desc + desc_off[k + 1], &d_hdr->ticket[k + 1], out_k, &d_hdr->count[k + 1]);
-      else
-        hipLaunchKernelGGL((k_flagscan<false, WideTab>), gs, dim3(kBlock), 0, stream, outw, p, nt.wt, d_grp,
-                           d_desc + desc_off[k + 1], &d_hdr->ticket[k + 1], out_k, &d_hdr->count[k + 1]);
+      hipLaunchKernelGGL(k_flagscan_node, gs, dim3(kBlock), 0, stream, outw, p, in, n, d_nf, d_grp,
+                         d_desc + desc_off[k + 1], &d_hdr->ticket[k + 1], out_k, &d_hdr->count[k + 1]);
       HIP_TRY(hipGetLastError());
       prof_end(KID_FLAGSCAN_NODE, e0);
-      prof_begin(KID_RESOLVE, e0);
-      hipLaunchKernelGGL(k_resolve, gi, dim3(kBlock), 0, stream, outw, p, d_grp);
+      prof_begin(KID_RESOLVE_NODE, e0);
+      if (nt.packed)
+        hipLaunchKernelGGL((k_resolve_node<PackedTab>), gi, dim3(kBlock), 0, stream, outw, p, nt.pt, d_nf, d_grp);
+      else
+        hipLaunchKernelGGL((k_resolve_node<WideTab>), gi, dim3(kBlock), 0, stream, outw, p, nt.wt, d_nf, d_grp);
       HIP_TRY(hipGetLastError());
-      prof_end(KID_RESOLVE, e0);
+      prof_end(KID_RESOLVE_NODE, e0);
       std::swap(in, outw);
       n = p;
       bound = p;
@@ -861,7 +415,8 @@ void gcz_ctx_destroy(gcz_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&c->wa, &c->wb, &c->grp, &c->desc, &c->tab, &c->leaves_out, &c->nodes_out, &c->hdr, &c->input})
+  for (DevBuf* b : {&c->wa, &c->wb, &c->grp, &c->desc, &c->tab, &c->leaves_out, &c->nodes_out, &c->hdr, &c->input,
+                    &c->nf, &c->ids})
     if (b->ptr) (void)hipFree(b->ptr);
   if (c->h_hdr) (void)hipHostFree(c->h_hdr);
   for (auto e : c->event_pool) (void)hipEventDestroy(e);

@@ -1,0 +1,547 @@
+// Device code of the MI355X (gfx950) shared_tree construction.
+// Included by gcz_build.hip only.
+//
+// Replaces tree_constructor (reference include/shared_tree.h:245-316,
+// src/shared_tree.cpp:621-763) with one global level-by-level build; the
+// reference's 2^22 / 2^25-strand segmentation is output-invisible.
+//
+// Per level (n input words -> p = ceil(n/2) pairs; the leaf level has p = S):
+//
+//   insert    canonical key of each leaf/pair -> open-addressing table in HBM
+//             (hash-consing, tree_constructor::emplace_leaf/emplace_node).
+//             Records the provisional word rec[j] = slot | m<<29 | t<<30 | v<<31
+//             and marks nf[j] = 1 ("not first") for every element that is
+//             provably not its key's first occurrence (see Tables below).
+//   flagscan  first occurrence <=> nf[j] == 0.  Wave ballot -> 64-element group
+//             masks, in-tile scan, decoupled look-back across tiles -> ids are
+//             the dense first-occurrence ranks (the reference's parent.node_count
+//             at emplace time, shared_tree.cpp:632,666).  First occurrences emit
+//             the unique leaf/node at out[id] and write their final word.
+//   resolve   non-first occurrences get the id of their key's first occurrence:
+//             leaves through a slot -> id array written by flagscan, nodes
+//             through the slot's minimum position -> its group's {mask, prefix}.
+//
+// The next level reads the final words directly (coalesced 8-B pairs).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gcz_internal.h"
+
+namespace gcz_dev {
+
+using u32 = uint32_t;
+using u64 = unsigned long long;
+
+constexpr u32 kNullWord = 0x9fffffffu;
+constexpr u32 kIdx = 0x1fffffffu;
+constexpr u32 kBits = 0xe0000000u;
+constexpr u64 kEmpty = ~0ull;
+constexpr int kBlock = 256;
+constexpr int kItems = 8;                  // flagscan elements per thread
+constexpr int kTile = kBlock * kItems;     // 2048 elements per look-back tile
+constexpr int kGroupsPerTile = kTile / 64; // 32
+constexpr u32 kMaxProbe = 1u << 16;
+
+struct __align__(16) Slot {   // WideTab slot; key stored as key ^ 1 (see WideTab)
+  u64 key;
+  u32 pos;
+  u32 pad;
+};
+
+struct __align__(16) Group {
+  u64 mask;    // first-occurrence flags of 64 consecutive elements
+  u32 prefix;  // first occurrences before this group (global, this level)
+  u32 pad;
+};
+
+struct Header {
+  u64 count[GCZ_MAX_LAYERS + 1];  // [0] unique leaves, [1+k] unique nodes of layer k
+  u64 err_offset;                 // first unknown symbol (min), ~0 if none
+  u32 overflow;
+  u32 pad0;
+  u32 ticket[GCZ_MAX_LAYERS + 1]; // look-back tile tickets per level
+  u32 root;
+  u32 pad1;
+};
+
+// ---- word algebra: reference src/shared_tree.cpp:76-107 --------------------
+__device__ __forceinline__ u32 ulw(u32 w) { return w & 0x7fffffffu; }   // to_ulong
+// transform ctor (shared_tree.cpp:76-80): m' = (M != m) && !v ; t' = (T != t) && !null
+__device__ __forceinline__ u32 xf(u32 w, u32 M, u32 T) {
+  const u32 v = w >> 31, m = (w >> 29) & 1u, t = (w >> 30) & 1u;
+  const u32 nm = (M ^ m) & (v ^ 1u);
+  const u32 nt = (T ^ t) & u32(ulw(w) != kIdx);
+  return (w & 0x9fffffffu) | (nm << 29) | (nt << 30);
+}
+__device__ __forceinline__ u32 make_word(u32 idx, u32 m, u32 t, u32 v) {   // ctor :85-86
+  return idx | ((m & (v ^ 1u)) << 29) | (t << 30) | (v << 31);
+}
+
+// node::canonical (include/shared_tree.h:115-126): min over (key, m, t) of
+// id=(l,r) mir=(M(r),M(l)) tra=(T(l),T(r)) inv=(I(r),I(l)); key = to_ulong pair.
+__device__ __forceinline__ void node_canonical(u32 l, u32 r, u32& cl, u32& cr, u32& cm, u32& ct) {
+  const u32 ml = xf(l, 1, 0), mr = xf(r, 1, 0);
+  const u32 tl = xf(l, 0, 1), tr = xf(r, 0, 1);
+  const u32 il = xf(l, 1, 1), ir = xf(r, 1, 1);
+  // (key << 2 | m << 1 | t): the 62-bit key with (m,t) appended is one compare
+  auto k = [](u32 a, u32 b, u32 m, u32 t) -> u64 {
+    return ((u64(ulw(a)) << 31 | ulw(b)) << 2) | (m << 1) | t;
+  };
+  u64 best = k(l, r, 0, 0);
+  cl = l; cr = r; cm = 0; ct = 0;
+  u64 c = k(mr, ml, 1, 0);
+  if (c < best) { best = c; cl = mr; cr = ml; cm = 1; ct = 0; }
+  c = k(tl, tr, 0, 1);
+  if (c < best) { best = c; cl = tl; cr = tr; cm = 0; ct = 1; }
+  c = k(ir, il, 1, 1);
+  if (c < best) { cl = ir; cr = il; cm = 1; ct = 1; }
+}
+
+// ---- leaf codec: reference src/dna.cpp:104-143 ------------------------------
+__device__ __forceinline__ u64 leaf_transposed(u64 v) {
+  v = ((v >> 1) & 0x5555555555555555ull) | ((v & 0x5555555555555555ull) << 1);
+  v = ((v >> 2) & 0x3333333333333333ull) | ((v & 0x3333333333333333ull) << 2);
+  return v;
+}
+// reverse the low L nibbles, higher nibbles dropped (dna::mirrored :116-121)
+__device__ __forceinline__ u64 leaf_mirrored(u64 v, int L) {
+  u64 y = __builtin_bswap64(v);
+  y = ((y >> 4) & 0x0f0f0f0f0f0f0f0full) | ((y & 0x0f0f0f0f0f0f0f0full) << 4);
+  return L == 16 ? y : (y >> (64 - 4 * L));
+}
+__device__ __forceinline__ u64 leaf_canonical(u64 x, int L, u32& m, u32& t, u32& v) {
+  const u64 tx = leaf_transposed(x);
+  const u64 mx = leaf_mirrored(x, L);
+  const u64 ix = leaf_mirrored(tx, L);
+  v = x == mx;
+  u64 best = x; m = 0; t = 0;
+  if (tx < best) { best = tx; m = 0; t = 1; }
+  if (mx < best) { best = mx; m = 1; t = 0; }
+  if (ix < best) { best = ix; m = 1; t = 1; }
+  return best;
+}
+
+// nac code of an ASCII byte, include/dna.h:20-32 (to_nac, src/dna.cpp:25-49); -1 unknown
+__device__ __forceinline__ int nac_code(int c) {
+  const int u = (c >= 'a' && c <= 'z') ? c - 32 : c;
+  switch (u) {
+    case 'A': return 1;  case 'C': return 2;  case 'G': return 4;  case 'T': return 8;
+    case 'R': return 3;  case 'Y': return 12; case 'K': return 7;  case 'M': return 14;
+    case 'B': return 5;  case 'V': return 10; case 'D': return 11; case 'H': return 13;
+    case 'S': return 0;  case 'W': return 9;  case 'N': return 6;  case '-': return 15;
+    default: return -1;
+  }
+}
+
+// ---- hash tables ---------------------------------------------------------------
+// Both tables map a canonical key to (slot, minimum position) and, as a side
+// effect of the insert, mark every element that is provably NOT the first
+// occurrence of its key:
+//   * an element that sees its key already holding a smaller position marks
+//     itself;
+//   * an element that lowers the slot's position marks the element it
+//     displaced (the returning atomicMin tells which);
+// the slot's position sequence is decreasing, so exactly the final minimum
+// (the first occurrence) stays unmarked.  Unique keys cost one CAS.
+//
+// PackedTab (default): one 8-B word per slot,
+//     word = quotient(h) << (D+P) | displacement << P | pos
+// h = mix(key) is a bijection on the K key bits; the home slot is h's low c
+// bits, the quotient its high K-c bits.  The claiming CAS also stores the
+// position; repeats share the high bits, so a 64-bit atomicMin lowers pos.
+// The key is recovered exactly from (slot, word) by inverting the mix.
+//
+// WideTab (fallback: keys that do not pack, e.g. L = 16 leaves): 16-B slots
+// {key ^ 1, pos}; CAS on the key then atomicMin on pos.  key ^ 1 == ~0 would
+// need key 0xffff_ffff_ffff_fffe, which is never canonical (its transpose
+// ..fff7 is smaller, dna.cpp:135-143) and never a node key (left word with
+// both mirror and invariant bits, which the pointer ctor forbids).
+//
+// Probes read the slot with a plain load first; it may be stale (this CU's L1
+// or this XCD's L2), but slots only go EMPTY -> claimed and positions only
+// decrease, so staleness costs at most an extra CAS / atomicMin.
+
+__device__ __forceinline__ u32 slot_hash(u64 k) {
+  k ^= k >> 31;
+  k *= 0x7fb5d329728ea185ull;
+  k ^= k >> 27;
+  k *= 0x81dadef4bc2dd44dull;
+  k ^= k >> 33;
+  return u32(k);
+}
+
+__device__ __forceinline__ u32 enc_child(u32 w, u32 B) {      // pointer word -> B+3 bits
+  const u32 idx = w & kIdx;
+  const u32 code = idx == kIdx ? ((1u << B) - 1u) : idx;      // null index -> all-ones code
+  return (code << 3) | (((w >> 29) & 1u) << 2) | (((w >> 30) & 1u) << 1) | (w >> 31);
+}
+__device__ __forceinline__ u32 dec_child(u32 e, u32 B) {
+  const u32 code = e >> 3;
+  if (code == (1u << B) - 1u) return kNullWord;
+  return code | (((e >> 2) & 1u) << 29) | (((e >> 1) & 1u) << 30) | ((e & 1u) << 31);
+}
+
+__device__ __forceinline__ void mark(unsigned char* nf, u32 pos) { nf[pos] = 1; }
+
+struct WideTab {
+  Slot* tab;
+  u32 mask;
+  u32 limit;
+  u32 B;   // unused
+
+  __device__ __forceinline__ u64 node_key(u32 cl, u32 cr) const { return (u64(cl) << 32) | cr; }
+  __device__ __forceinline__ u32 insert(u64 key, u32 pos, unsigned char* __restrict__ nf,
+                                        Header* __restrict__ hdr) const {
+    const u64 skey = key ^ 1ull;
+    u32 s = slot_hash(skey) & mask;
+    for (u32 probe = 0; probe < limit; ++probe) {
+      const Slot cur = tab[s];
+      u64 k = cur.key;
+      if (k == kEmpty) {
+        k = atomicCAS(&tab[s].key, kEmpty, skey);
+        if (k == kEmpty) {                       // claimed: now lower pos from EMPTY
+          const u32 old = atomicMin(&tab[s].pos, pos);
+          if (old < pos) mark(nf, pos);
+          else if (old != ~0u) mark(nf, old);
+          return s;
+        }
+      }
+      if (k == skey) {
+        if (cur.pos < pos) { mark(nf, pos); return s; }
+        const u32 old = atomicMin(&tab[s].pos, pos);
+        if (old < pos) mark(nf, pos);
+        else if (old != ~0u) mark(nf, old);
+        return s;
+      }
+      s = (s + 1) & mask;
+    }
+    atomicOr(&hdr->overflow, 1u);
+    return 0;
+  }
+  __device__ __forceinline__ void read(u32 s, u64& key, u32& pos) const {
+    const Slot sl = tab[s];
+    key = sl.key ^ 1ull;
+    pos = sl.pos;
+  }
+};
+
+struct PackedTab {
+  u64* tab;
+  u32 mask;
+  u32 limit;   // <= 2^D - 2 probes
+  u32 B;       // child index bits (node levels)
+  u32 c, P, D, sh;
+  u64 kmask, c1, c2, c1i, c2i;
+
+  __device__ __forceinline__ u64 node_key(u32 cl, u32 cr) const {
+    return (u64(enc_child(cl, B)) << (B + 3)) | enc_child(cr, B);
+  }
+  __device__ __forceinline__ u64 mix(u64 x) const {
+    x ^= x >> sh; x = (x * c1) & kmask;
+    x ^= x >> sh; x = (x * c2) & kmask;
+    x ^= x >> sh;
+    return x;
+  }
+  __device__ __forceinline__ u64 unmix(u64 h) const {
+    h ^= h >> sh; h = (h * c2i) & kmask;
+    h ^= h >> sh; h = (h * c1i) & kmask;
+    h ^= h >> sh;
+    return h;
+  }
+  __device__ __forceinline__ u32 insert(u64 key, u32 pos, unsigned char* __restrict__ nf,
+                                        Header* __restrict__ hdr) const {
+    const u64 h = mix(key);
+    u32 s = u32(h) & mask;
+    const u64 qd = (h >> c) << D;             // quotient; displacement bits below
+    const u64 pmask = (1ull << P) - 1;
+    for (u32 d = 0; d < limit; ++d) {
+      const u64 mine = ((qd | d) << P) | pos;
+      u64 cur = tab[s];
+      if (cur == kEmpty) {
+        cur = atomicCAS(&tab[s], kEmpty, mine);
+        if (cur == kEmpty) return s;            // new key: one atomic, nothing to mark
+      }
+      if ((cur >> P) == (mine >> P)) {
+        if (u32(cur & pmask) < pos) { mark(nf, pos); return s; }
+        const u64 old = atomicMin(&tab[s], mine);
+        const u32 op = u32(old & pmask);
+        mark(nf, op < pos ? pos : op);
+        return s;
+      }
+      s = (s + 1) & mask;
+    }
+    atomicOr(&hdr->overflow, 1u);
+    return 0;
+  }
+  __device__ __forceinline__ void read(u32 s, u64& key, u32& pos) const {
+    const u64 w = tab[s];
+    pos = u32(w & ((1ull << P) - 1));
+    const u32 d = u32((w >> P) & ((1ull << D) - 1));
+    const u64 q = w >> (P + D);
+    const u64 home = (s - d) & mask;
+    key = unmix((q << c) | home);
+  }
+};
+
+// ---- insert kernels -----------------------------------------------------------
+
+// Leaf level from raw bases: pack L symbols (dna::dna(string_view) + dna::set,
+// dna.cpp:79-84,187-197), canonicalise (:135-143), hash-cons (emplace_leaf,
+// shared_tree.cpp:630-637).  The block's bases are staged through LDS with
+// coalesced 4-B loads.
+template <int L, class Tab>
+__global__ __launch_bounds__(kBlock) void k_leaf_bases(const unsigned char* __restrict__ bases, u64 S, Tab T,
+                                                      u32* __restrict__ rec, unsigned char* __restrict__ nf,
+                                                      Header* __restrict__ hdr) {
+  __shared__ signed char lut[256];
+  __shared__ __align__(16) unsigned char buf[kBlock * L + 16];
+  const int tid = threadIdx.x;
+  lut[tid] = (signed char)nac_code(tid);
+  const u64 first = u64(blockIdx.x) * kBlock;
+  const u64 nstr = (S - first) < u64(kBlock) ? (S - first) : u64(kBlock);
+  const u64 byte0 = first * L;                 // multiple of 4 (kBlock = 256)
+  const u64 nbytes = nstr * L;
+  const u32* src = reinterpret_cast<const u32*>(bases + byte0);
+  u32* dst = reinterpret_cast<u32*>(buf);
+  const u32 nwords = u32(nbytes / 4);
+  for (u32 w = tid; w < nwords; w += kBlock) dst[w] = src[w];
+  for (u32 b = nwords * 4 + tid; b < nbytes; b += kBlock) buf[b] = bases[byte0 + b];
+  __syncthreads();
+  if (u64(tid) >= nstr) return;
+  u64 x = 0;
+  int bad = -1;
+#pragma unroll
+  for (int c = 0; c < L; ++c) {
+    const int code = lut[buf[tid * L + c]];
+    if (code < 0 && bad < 0) bad = c;
+    x |= u64(code & 15) << (4 * c);
+  }
+  const u64 i = first + tid;
+  if (bad >= 0) atomicMin(&hdr->err_offset, i * L + u64(bad));
+  u32 m, t, v;
+  const u64 key = leaf_canonical(x, L, m, t, v);
+  const u32 s = T.insert(key, u32(i), nf, hdr);
+  rec[i] = make_word(s, m, t, v);
+}
+
+// Leaf level from packed strands (shared_tree(std::vector<dna>&), :212-215).
+template <class Tab>
+__global__ __launch_bounds__(kBlock) void k_leaf_packed(const u64* __restrict__ leaves, u64 S, int L, Tab T,
+                                                       u32* __restrict__ rec, unsigned char* __restrict__ nf,
+                                                       Header* __restrict__ hdr) {
+  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= S) return;
+  u32 m, t, v;
+  const u64 key = leaf_canonical(leaves[i], L, m, t, v);
+  const u32 s = T.insert(key, u32(i), nf, hdr);
+  rec[i] = make_word(s, m, t, v);
+}
+
+// Pair (2j, 2j+1) of the previous level's final words; the odd tail pairs with
+// the null pointer (foreach_pair, include/utility.h:17-29).
+__device__ __forceinline__ void load_pair(const u32* __restrict__ in, u64 n, u64 j, u32& l, u32& r) {
+  if (2 * j + 1 < n) {
+    const uint2 w = reinterpret_cast<const uint2*>(in)[j];
+    l = w.x; r = w.y;
+  } else {
+    l = in[2 * j]; r = kNullWord;
+  }
+}
+
+// Node level, tree_constructor::emplace_node (src/shared_tree.cpp:662-672).
+template <class Tab>
+__global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ in, u64 n, u64 p, Tab T,
+                                                       u32* __restrict__ rec, unsigned char* __restrict__ nf,
+                                                       Header* __restrict__ hdr) {
+  const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= p) return;
+  u32 l, r, cl, cr, m, t;
+  load_pair(in, n, j, l, r);
+  node_canonical(l, r, cl, cr, m, t);
+  const u32 v = ulw(l) == ulw(xf(r, 1, 0));      // left == right.mirrored() (:670)
+  const u32 s = T.insert(T.node_key(cl, cr), u32(j), nf, hdr);
+  rec[j] = make_word(s, m, t, v);
+}
+
+// ---- flag scan ------------------------------------------------------------------
+
+__device__ __forceinline__ u64 wave_sum(u64 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+constexpr u64 kStA = 1ull << 62;   // tile aggregate published
+constexpr u64 kStP = 2ull << 62;   // tile inclusive prefix published
+constexpr u64 kValMask = (1ull << 62) - 1;
+
+// Shared part of both flagscan kernels: takes a tile ticket (tiles are
+// processed in ticket order, so every predecessor is resident), reads the
+// not-first marks, ballots 64-element groups, scans them within the tile and
+// across tiles by decoupled look-back.  On return s_pre[g] holds the number
+// of first occurrences before group g of the tile (global), mask[e] the
+// group masks of this thread's wave, and the level total is in *count_out.
+// The look-back descriptor is one 64-bit word (status | value), so it needs
+// no separate payload and no fences (relaxed agent-scope atomics).
+struct TileScan {
+  u64 base;
+  u64 mask[kItems];
+};
+
+__device__ __forceinline__ void tile_scan(TileScan& ts, u32* s_tile, u32* s_pre,
+                                          const unsigned char* __restrict__ nf, u64 p,
+                                          u64* __restrict__ desc, u32* __restrict__ ticket,
+                                          u64* __restrict__ count_out) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) *s_tile = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const u64 tile = *s_tile;
+  ts.base = tile * kTile;
+#pragma unroll
+  for (int e = 0; e < kItems; ++e) {
+    const u64 j = ts.base + u64(e) * kBlock + tid;
+    const bool first = j < p && nf[j] == 0;
+    ts.mask[e] = __ballot(first);
+    if (lane == 0) s_pre[e * 4 + wave] = u32(__popcll(ts.mask[e]));
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const u32 c = lane < kGroupsPerTile ? s_pre[lane] : 0u;
+    u32 incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const u32 y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    const u64 agg = __shfl(incl, 63, 64);
+    u64 prefix = 0;
+    if (tile == 0) {
+      if (lane == 0) __hip_atomic_store(&desc[0], kStP | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0) __hip_atomic_store(&desc[tile], kStA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      long long look = (long long)tile - 1;
+      for (;;) {
+        const long long idx = look - lane;
+        const u64 d =
+            idx >= 0 ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        const u64 st = d >> 62;
+        const u64 pm = __ballot(st == 2);
+        const u64 zm = __ballot(st == 0);
+        const int firstP = pm ? __ffsll((long long)pm) - 1 : 64;
+        const u64 need = firstP >= 63 ? ~0ull : ((1ull << (firstP + 1)) - 1);
+        if (zm & need) {
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        prefix += wave_sum(lane <= firstP ? (d & kValMask) : 0ull);
+        if (firstP < 64) break;
+        look -= 64;
+      }
+      if (lane == 0)
+        __hip_atomic_store(&desc[tile], kStP | (prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane < kGroupsPerTile) s_pre[lane] = u32(prefix + incl - c);
+    if (lane == 0 && (tile + 1) * kTile >= p) *count_out = prefix + agg;
+  }
+  __syncthreads();
+}
+
+// Leaves: first occurrences read their slot to recover the canonical leaf,
+// emit it, and publish slot -> id for resolve_leaf.
+template <class Tab>
+__global__ __launch_bounds__(kBlock) void k_flagscan_leaf(u32* __restrict__ words, u64 p, Tab T,
+                                                         const unsigned char* __restrict__ nf,
+                                                         u64* __restrict__ desc, u32* __restrict__ ticket,
+                                                         u64* __restrict__ out, u32* __restrict__ ids,
+                                                         u64* __restrict__ count_out) {
+  __shared__ u32 s_tile;
+  __shared__ u32 s_pre[kGroupsPerTile];
+  TileScan ts;
+  tile_scan(ts, &s_tile, s_pre, nf, p, desc, ticket, count_out);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const u64 lt = (1ull << lane) - 1;
+#pragma unroll
+  for (int e = 0; e < kItems; ++e) {
+    const u64 j = ts.base + u64(e) * kBlock + tid;
+    if (j < p && ((ts.mask[e] >> lane) & 1ull)) {
+      const u32 id = s_pre[e * 4 + wave] + u32(__popcll(ts.mask[e] & lt));
+      const u32 rec = words[j];
+      u64 key;
+      u32 pos;
+      T.read(rec & kIdx, key, pos);
+      out[id] = key;
+      ids[rec & kIdx] = id;
+      words[j] = id | (rec & kBits);
+    }
+  }
+}
+
+// Nodes: first occurrences recompute their canonical pair from the input
+// (coalesced) instead of reading the table, emit it, and publish the group
+// records that resolve_node uses.
+__global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ words, u64 p,
+                                                         const u32* __restrict__ in, u64 n,
+                                                         const unsigned char* __restrict__ nf,
+                                                         Group* __restrict__ grp, u64* __restrict__ desc,
+                                                         u32* __restrict__ ticket, uint2* __restrict__ out,
+                                                         u64* __restrict__ count_out) {
+  __shared__ u32 s_tile;
+  __shared__ u32 s_pre[kGroupsPerTile];
+  TileScan ts;
+  tile_scan(ts, &s_tile, s_pre, nf, p, desc, ticket, count_out);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const u64 lt = (1ull << lane) - 1;
+#pragma unroll
+  for (int e = 0; e < kItems; ++e) {
+    const u64 j = ts.base + u64(e) * kBlock + tid;
+    const u32 gpre = s_pre[e * 4 + wave];
+    if (lane == 0) {
+      Group g;
+      g.mask = ts.mask[e]; g.prefix = gpre; g.pad = 0;
+      grp[(ts.base >> 6) + e * 4 + wave] = g;
+    }
+    if (j < p && ((ts.mask[e] >> lane) & 1ull)) {
+      const u32 id = gpre + u32(__popcll(ts.mask[e] & lt));
+      u32 l, r, cl, cr, m, t;
+      load_pair(in, n, j, l, r);
+      node_canonical(l, r, cl, cr, m, t);
+      uint2 w;
+      w.x = cl; w.y = cr;
+      out[id] = w;
+      words[j] = id | (words[j] & kBits);
+    }
+  }
+}
+
+// ---- resolve ----------------------------------------------------------------------
+
+__global__ __launch_bounds__(kBlock) void k_resolve_leaf(u32* __restrict__ words, u64 p,
+                                                        const unsigned char* __restrict__ nf,
+                                                        const u32* __restrict__ ids) {
+  const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= p || nf[j] == 0) return;
+  const u32 w = words[j];
+  words[j] = ids[w & kIdx] | (w & kBits);
+}
+
+template <class Tab>
+__global__ __launch_bounds__(kBlock) void k_resolve_node(u32* __restrict__ words, u64 p, Tab T,
+                                                        const unsigned char* __restrict__ nf,
+                                                        const Group* __restrict__ grp) {
+  const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= p || nf[j] == 0) return;
+  const u32 w = words[j];
+  u64 key;
+  u32 q;
+  T.read(w & kIdx, key, q);                     // q = the key's first position
+  const Group h = grp[q >> 6];
+  const u32 id = h.prefix + u32(__popcll(h.mask & ((1ull << (q & 63)) - 1)));
+  words[j] = id | (w & kBits);
+}
+
+__global__ void k_root(const u32* __restrict__ words, Header* __restrict__ hdr) { hdr->root = words[0]; }
+
+}  // namespace gcz_dev
