@@ -177,11 +177,11 @@ struct gcz_ctx {
 namespace {
 
 template <class Tab>
-void launch_leaf_bases(int L, dim3 g, hipStream_t st, const unsigned char* b, u64 S, const Tab& T, u32* rec,
-                       unsigned char* nf, Header* hdr) {
+void launch_leaf_bases(int L, dim3 g, hipStream_t st, const unsigned char* b, u64 i0, u64 i1, const Tab& T,
+                       u32* rec, unsigned char* nf, Header* hdr) {
   switch (L) {
 #define GCZ_CASE(X) \
-  case X: hipLaunchKernelGGL((k_leaf_bases<X, Tab>), g, dim3(kBlock), 0, st, b, S, T, rec, nf, hdr); break;
+  case X: hipLaunchKernelGGL((k_leaf_bases<X, Tab>), g, dim3(kBlock), 0, st, b, i0, i1, T, rec, nf, hdr); break;
     GCZ_CASE(1) GCZ_CASE(2) GCZ_CASE(3) GCZ_CASE(4) GCZ_CASE(5) GCZ_CASE(6) GCZ_CASE(7) GCZ_CASE(8)
     GCZ_CASE(9) GCZ_CASE(10) GCZ_CASE(11) GCZ_CASE(12) GCZ_CASE(13) GCZ_CASE(14) GCZ_CASE(15) GCZ_CASE(16)
 #undef GCZ_CASE
@@ -201,7 +201,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   if (S > u64(kIdx)) return fail(GCZ_ERR_CAPACITY, "build", "more than 2^29-1 strands");
   info.n_strands = S;
 
-  // level plan
+  // ---- plan: node layers, leaf chunks, scan descriptor regions ----
   std::vector<u64> pk;                     // pairs per node layer
   for (u64 n = S;;) {
     const u64 p = (n + 1) / 2;
@@ -213,22 +213,32 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   const int D = int(pk.size());
   layer_off.assign(D + 1, 0);
   for (int k = 0; k < D; ++k) layer_off[k + 1] = layer_off[k] + pk[k];
-  u64 ntiles_total = (S + kTile - 1) / kTile;
-  std::vector<u64> desc_off(D + 1);
-  desc_off[0] = 0;
+  // leaf chunks: up to 8, each a multiple of the scan tile
+  const u64 nchunks = std::max<u64>(1, std::min<u64>(8, S >> 21));
+  u64 csize = (S + nchunks - 1) / nchunks;
+  csize = (csize + kTile - 1) / kTile * kTile;
+  std::vector<u64> chunk_start;
+  for (u64 i = 0; i < S; i += csize) chunk_start.push_back(i);
+  chunk_start.push_back(S);
+  const int C = int(chunk_start.size()) - 1;
+  std::vector<u64> desc_off;
+  u64 ntiles_total = 0;
+  for (int c = 0; c < C; ++c) {
+    desc_off.push_back(ntiles_total);
+    ntiles_total += (chunk_start[c + 1] - chunk_start[c] + kTile - 1) / kTile;
+  }
   for (int k = 0; k < D; ++k) {
-    desc_off[k + 1] = ntiles_total;
+    desc_off.push_back(ntiles_total);
     ntiles_total += (pk[k] + kTile - 1) / kTile;
   }
 
   // leaf table: big enough for S when S is small; otherwise start at 2^23 slots
-  // (every ACGT 12-mer class fits) and grow if the probe bound overflows.
+  // (every ACGT 12-mer class fits) and grow after an overflow.
   const u64 full_cap = std::max<u64>(256, next_pow2(2 * S));
   u64 leaf_cap = full_cap;
   if (S > (1ull << 22)) leaf_cap = std::min(full_cap, std::max<u64>(1ull << 23, leaf_cap_hint));
   const u64 node_cap0 = std::max<u64>(256, next_pow2(2 * pk[0]));
 
-  u32* in = nullptr;
   int rc;
   if ((rc = ensure(wa, S * 4 + 16))) return rc;
   if ((rc = ensure(wb, ((S + 1) / 2) * 4 + 16))) return rc;
@@ -252,66 +262,63 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     HIP_TRY(hipEventCreate(&ev_stop));
   }
 
-  for (bool allow_packed : {!force_wide, false}) {
+  bool allow_packed = !force_wide;
+  u32* in = nullptr;
+  for (;;) {
+    if ((rc = ensure(tab, std::max(leaf_cap, node_cap0) * 16))) return rc;
     HIP_TRY(hipEventRecord(ev_start, stream));
     HIP_TRY(hipMemsetAsync(d_hdr, 0, sizeof(Header), stream));
     HIP_TRY(hipMemsetAsync(&d_hdr->err_offset, 0xff, 8, stream));
     HIP_TRY(hipMemsetAsync(d_desc, 0, ntiles_total * 8, stream));
-    if ((rc = ensure(tab, std::max(leaf_cap, node_cap0) * 16))) return rc;
 
-    // ---- leaf level ----
-    LevelTab lt;
-    for (;;) {
-      const bool adaptive = leaf_cap < 2 * S;
-      const u32 limit = adaptive ? kAdaptiveProbeLimit : kMaxProbe;
-      // packed leaves only from bases (< 2^4L by construction); user leaves may carry any bits
-      lt = plan_table(tab.ptr, leaf_cap, d_bases ? 4 * u32(L) : 64, S, 0, allow_packed && d_bases, limit);
-      if (lt.packed && lt.pt.limit > limit) lt.pt.limit = limit;
-      hipEvent_t e0{};
-      prof_begin(KID_MEMSET, e0);
-      HIP_TRY(hipMemsetAsync(tab.ptr, 0xff, lt.bytes(), stream));
-      HIP_TRY(hipMemsetAsync(d_nf, 0, S, stream));
-      prof_end(KID_MEMSET, e0);
-      const dim3 g(unsigned((S + kBlock - 1) / kBlock));
+    // ---- leaf level, in chunks ----
+    const bool adaptive = leaf_cap < 2 * S;
+    const u32 limit = adaptive ? kAdaptiveProbeLimit : kMaxProbe;
+    // packed leaves only from bases (< 2^4L by construction); user leaves may carry any bits.
+    // Chunked settling needs one spare bit in the packed word, hence K + 1.
+    LevelTab lt = plan_table(tab.ptr, leaf_cap, d_bases ? 4 * u32(L) + 1 : 64, S, 0, allow_packed && d_bases,
+                             limit);
+    if (lt.packed) {
+      lt.pt.limit = std::min(lt.pt.limit, limit);
+      lt.pt.kmask >>= 1;                   // the key itself has 4L bits
+      lt.pt.sh = (4 * u32(L) + 1) / 2;
+    }
+    hipEvent_t e0{};
+    prof_begin(KID_MEMSET, e0);
+    HIP_TRY(hipMemsetAsync(tab.ptr, 0xff, lt.bytes(), stream));
+    HIP_TRY(hipMemsetAsync(d_nf, 0, S, stream));
+    prof_end(KID_MEMSET, e0);
+    u64* lo = static_cast<u64*>(leaves_out.ptr);
+    for (int c = 0; c < C; ++c) {
+      const u64 i0 = chunk_start[c], i1 = chunk_start[c + 1];
+      const dim3 g(unsigned((i1 - i0 + kBlock - 1) / kBlock));
       prof_begin(KID_LEAF, e0);
       if (d_bases) {
         const auto* b = static_cast<const unsigned char*>(d_bases);
-        if (lt.packed) launch_leaf_bases(L, g, stream, b, S, lt.pt, A, d_nf, d_hdr);
-        else launch_leaf_bases(L, g, stream, b, S, lt.wt, A, d_nf, d_hdr);
+        if (lt.packed) launch_leaf_bases(L, g, stream, b, i0, i1, lt.pt, A, d_nf, d_hdr);
+        else launch_leaf_bases(L, g, stream, b, i0, i1, lt.wt, A, d_nf, d_hdr);
       } else {
-        hipLaunchKernelGGL((k_leaf_packed<WideTab>), g, dim3(kBlock), 0, stream, d_leaves, S, L, lt.wt, A, d_nf,
-                           d_hdr);
+        hipLaunchKernelGGL((k_leaf_packed<WideTab>), g, dim3(kBlock), 0, stream, d_leaves, i0, i1, L, lt.wt, A,
+                           d_nf, d_hdr);
       }
       HIP_TRY(hipGetLastError());
       prof_end(KID_LEAF, e0);
-      if (!adaptive) break;
-      HIP_TRY(hipMemcpyAsync(h_hdr, d_hdr, sizeof(Header), hipMemcpyDeviceToHost, stream));
-      HIP_TRY(hipStreamSynchronize(stream));
-      if (!h_hdr->overflow) break;
-      leaf_cap = std::min(full_cap, leaf_cap * 8);
-      if ((rc = ensure(tab, std::max(leaf_cap, node_cap0) * 16))) return rc;
-      HIP_TRY(hipMemsetAsync(d_hdr, 0, sizeof(Header), stream));
-      HIP_TRY(hipMemsetAsync(&d_hdr->err_offset, 0xff, 8, stream));
-    }
-    leaf_cap_hint = leaf_cap;
-    if ((rc = ensure(ids, leaf_cap * 4))) return rc;
-    {
-      u32* d_ids = static_cast<u32*>(ids.ptr);
-      const dim3 gs(unsigned((S + kTile - 1) / kTile));
-      hipEvent_t e0{};
+      const dim3 gs(unsigned((i1 - i0 + kTile - 1) / kTile));
+      const u64* id0 = c == 0 ? nullptr : &d_hdr->count[c - 1];
       prof_begin(KID_FLAGSCAN_LEAF, e0);
-      u64* lo = static_cast<u64*>(leaves_out.ptr);
       if (lt.packed)
-        hipLaunchKernelGGL((k_flagscan_leaf<PackedTab>), gs, dim3(kBlock), 0, stream, A, S, lt.pt, d_nf,
-                           d_desc + desc_off[0], &d_hdr->ticket[0], lo, d_ids, &d_hdr->count[0]);
+        hipLaunchKernelGGL((k_flagscan_leaf<PackedTab>), gs, dim3(kBlock), 0, stream, A, i0, i1, lt.pt, d_nf,
+                           d_desc + desc_off[c], &d_hdr->ticket[c], lo, id0, &d_hdr->count[c]);
       else
-        hipLaunchKernelGGL((k_flagscan_leaf<WideTab>), gs, dim3(kBlock), 0, stream, A, S, lt.wt, d_nf,
-                           d_desc + desc_off[0], &d_hdr->ticket[0], lo, d_ids, &d_hdr->count[0]);
+        hipLaunchKernelGGL((k_flagscan_leaf<WideTab>), gs, dim3(kBlock), 0, stream, A, i0, i1, lt.wt, d_nf,
+                           d_desc + desc_off[c], &d_hdr->ticket[c], lo, id0, &d_hdr->count[c]);
       HIP_TRY(hipGetLastError());
       prof_end(KID_FLAGSCAN_LEAF, e0);
       prof_begin(KID_RESOLVE_LEAF, e0);
-      hipLaunchKernelGGL(k_resolve_leaf, dim3(unsigned((S + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, A, S,
-                         d_nf, d_ids);
+      if (lt.packed)
+        hipLaunchKernelGGL((k_resolve_leaf<PackedTab>), g, dim3(kBlock), 0, stream, A, i0, i1, lt.pt, d_nf);
+      else
+        hipLaunchKernelGGL((k_resolve_leaf<WideTab>), g, dim3(kBlock), 0, stream, A, i0, i1, lt.wt, d_nf);
       HIP_TRY(hipGetLastError());
       prof_end(KID_RESOLVE_LEAF, e0);
     }
@@ -326,7 +333,6 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       const u64 cap = std::max<u64>(256, next_pow2(2 * p));
       const u32 Bk = std::max<u32>(1, bit_width(bound));
       const LevelTab nt = plan_table(tab.ptr, cap, 2 * (Bk + 3), p, Bk, allow_packed, kMaxProbe);
-      hipEvent_t e0{};
       prof_begin(KID_MEMSET, e0);
       HIP_TRY(hipMemsetAsync(tab.ptr, 0xff, nt.bytes(), stream));
       HIP_TRY(hipMemsetAsync(d_nf, 0, p, stream));
@@ -345,7 +351,8 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       const dim3 gs(unsigned((p + kTile - 1) / kTile));
       uint2* out_k = static_cast<uint2*>(nodes_out.ptr) + layer_off[k];
       hipLaunchKernelGGL(k_flagscan_node, gs, dim3(kBlock), 0, stream, outw, p, in, n, d_nf, d_grp,
-                         d_desc + desc_off[k + 1], &d_hdr->ticket[k + 1], out_k, &d_hdr->count[k + 1]);
+                         d_desc + desc_off[C + k], &d_hdr->ticket[kLayerSlot + k], out_k,
+                         &d_hdr->count[kLayerSlot + k]);
       HIP_TRY(hipGetLastError());
       prof_end(KID_FLAGSCAN_NODE, e0);
       prof_begin(KID_RESOLVE_NODE, e0);
@@ -368,8 +375,15 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     HIP_TRY(hipEventElapsedTime(&ms, ev_start, ev_stop));
     info.build_ms = ms;
     if (profile) prof_collect();
-    // a packed table whose displacement field overflowed: rebuild with wide slots
-    if (!(h_hdr->overflow && allow_packed)) break;
+    if (h_hdr->leaf_overflow && adaptive) {    // leaf table too small: grow and rebuild
+      leaf_cap = std::min(full_cap, leaf_cap * 8);
+      continue;
+    }
+    if ((h_hdr->overflow || h_hdr->leaf_overflow) && allow_packed) {   // displacement field overflow
+      allow_packed = false;
+      continue;
+    }
+    break;
   }
 
   if (h_hdr->err_offset != ~0ull) {
@@ -380,12 +394,13 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     info.error_symbol = sym;
     return fail(GCZ_ERR_SYMBOL, "build", "unknown nucleotide symbol");
   }
-  if (h_hdr->overflow) return fail(GCZ_ERR_CAPACITY, "build", "hash table probe limit exceeded");
+  if (h_hdr->overflow || h_hdr->leaf_overflow)
+    return fail(GCZ_ERR_CAPACITY, "build", "hash table probe limit exceeded");
   info.n_layers = D;
-  info.n_leaves = h_hdr->count[0];
-  // keep the next build's adaptive leaf table at load <= 1/2 (speed only)
-  leaf_cap_hint = std::max(leaf_cap_hint, next_pow2(2 * info.n_leaves));
-  for (int k = 0; k < D; ++k) info.layer_size[k] = h_hdr->count[k + 1];
+  info.n_leaves = h_hdr->count[C - 1];
+  // next build of this size starts its adaptive leaf table at load <= 3/4 (speed only)
+  leaf_cap_hint = next_pow2(std::max<u64>(1, info.n_leaves * 4 / 3));
+  for (int k = 0; k < D; ++k) info.layer_size[k] = h_hdr->count[kLayerSlot + k];
   info.root = h_hdr->root;
   return GCZ_OK;
 }

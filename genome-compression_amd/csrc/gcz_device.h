@@ -18,8 +18,13 @@
 //             at emplace time, shared_tree.cpp:632,666).  First occurrences emit
 //             the unique leaf/node at out[id] and write their final word.
 //   resolve   non-first occurrences get the id of their key's first occurrence:
-//             leaves through a slot -> id array written by flagscan, nodes
+//             leaves through the slot, which flagscan settled with the id; nodes
 //             through the slot's minimum position -> its group's {mask, prefix}.
+//
+// The leaf level runs in chunks of strands (insert, flagscan, resolve per
+// chunk): a strand whose key was settled by an earlier chunk gets its final
+// word straight from the insert probe, so only keys new to a chunk pay for the
+// scan and the resolve read.
 //
 // The next level reads the final words directly (coalesced 8-B pairs).
 #pragma once
@@ -57,14 +62,19 @@ struct __align__(16) Group {
   u32 pad;
 };
 
+// Scan slots: leaf chunk c uses slot c, node layer k uses slot kLayerSlot + k.
+constexpr int kMaxChunks = 64;
+constexpr int kLayerSlot = kMaxChunks;
+constexpr int kScanSlots = kMaxChunks + GCZ_MAX_LAYERS;
+
 struct Header {
-  u64 count[GCZ_MAX_LAYERS + 1];  // [0] unique leaves, [1+k] unique nodes of layer k
-  u64 err_offset;                 // first unknown symbol (min), ~0 if none
-  u32 overflow;
-  u32 pad0;
-  u32 ticket[GCZ_MAX_LAYERS + 1]; // look-back tile tickets per level
+  u64 count[kScanSlots];   // leaf chunk c: unique leaves after chunk c (cumulative); layer k: its uniques
+  u32 ticket[kScanSlots];  // look-back tile tickets
+  u64 err_offset;          // first unknown symbol (min), ~0 if none
+  u32 overflow;            // a node-level probe bound was exceeded
+  u32 leaf_overflow;       // the (adaptively sized) leaf table was too small
   u32 root;
-  u32 pad1;
+  u32 pad;
 };
 
 // ---- word algebra: reference src/shared_tree.cpp:76-107 --------------------
@@ -184,7 +194,17 @@ __device__ __forceinline__ u32 dec_child(u32 e, u32 B) {
   return code | (((e >> 2) & 1u) << 29) | (((e >> 1) & 1u) << 30) | ((e & 1u) << 31);
 }
 
-__device__ __forceinline__ void mark(unsigned char* nf, u32 pos) { nf[pos] = 1; }
+// not-first marks: 0 = maybe first, 1 = not first (resolve through the slot),
+// 2 = key settled by an earlier leaf chunk (final word already written)
+constexpr unsigned char kNfMaybe = 0, kNfNot = 1, kNfDone = 2;
+__device__ __forceinline__ void mark(unsigned char* nf, u32 pos) { nf[pos] = kNfNot; }
+
+// Result of a leaf-chunk insert: the slot, or the settled id of the key.
+struct Ins {
+  u32 slot;
+  u32 id;      // valid when settled
+  bool settled;
+};
 
 struct WideTab {
   Slot* tab;
@@ -194,7 +214,7 @@ struct WideTab {
 
   __device__ __forceinline__ u64 node_key(u32 cl, u32 cr) const { return (u64(cl) << 32) | cr; }
   __device__ __forceinline__ u32 insert(u64 key, u32 pos, unsigned char* __restrict__ nf,
-                                        Header* __restrict__ hdr) const {
+                                        u32* __restrict__ ovf) const {
     const u64 skey = key ^ 1ull;
     u32 s = slot_hash(skey) & mask;
     for (u32 probe = 0; probe < limit; ++probe) {
@@ -218,7 +238,7 @@ struct WideTab {
       }
       s = (s + 1) & mask;
     }
-    atomicOr(&hdr->overflow, 1u);
+    atomicOr(ovf, 1u);
     return 0;
   }
   __device__ __forceinline__ void read(u32 s, u64& key, u32& pos) const {
@@ -226,6 +246,23 @@ struct WideTab {
     key = sl.key ^ 1ull;
     pos = sl.pos;
   }
+  // Leaf chunks: a slot whose key's first occurrence lies in an earlier chunk
+  // carries its final id in pad (0xffffffff until settled).
+  __device__ __forceinline__ Ins insert_chunk(u64 key, u32 pos, unsigned char* __restrict__ nf,
+                                              u32* __restrict__ ovf) const {
+    const u64 skey = key ^ 1ull;
+    u32 s = slot_hash(skey) & mask;
+    for (u32 probe = 0; probe < limit; ++probe) {
+      const Slot cur = tab[s];
+      if (cur.key == skey && cur.pad != ~0u) return {s, cur.pad, true};
+      if (cur.key == kEmpty || cur.key == skey) return {insert(key, pos, nf, ovf), 0, false};
+      s = (s + 1) & mask;
+    }
+    atomicOr(ovf, 1u);
+    return {0, 0, false};
+  }
+  __device__ __forceinline__ void settle(u32 s, u32 id) const { tab[s].pad = id; }
+  __device__ __forceinline__ u32 settled_id(u32 s) const { return tab[s].pad; }
 };
 
 struct PackedTab {
@@ -252,7 +289,7 @@ struct PackedTab {
     return h;
   }
   __device__ __forceinline__ u32 insert(u64 key, u32 pos, unsigned char* __restrict__ nf,
-                                        Header* __restrict__ hdr) const {
+                                        u32* __restrict__ ovf) const {
     const u64 h = mix(key);
     u32 s = u32(h) & mask;
     const u64 qd = (h >> c) << D;             // quotient; displacement bits below
@@ -273,17 +310,50 @@ struct PackedTab {
       }
       s = (s + 1) & mask;
     }
-    atomicOr(&hdr->overflow, 1u);
+    atomicOr(ovf, 1u);
     return 0;
   }
   __device__ __forceinline__ void read(u32 s, u64& key, u32& pos) const {
-    const u64 w = tab[s];
+    const u64 w = tab[s] & ~kSettled;
     pos = u32(w & ((1ull << P) - 1));
     const u32 d = u32((w >> P) & ((1ull << D) - 1));
     const u64 q = w >> (P + D);
     const u64 home = (s - d) & mask;
     key = unmix((q << c) | home);
   }
+  // Leaf chunks (needs Q + D + P <= 63): a settled slot keeps its key bits and
+  // holds the final id in the position field, with bit 63 set.
+  static constexpr u64 kSettled = 1ull << 63;
+  __device__ __forceinline__ Ins insert_chunk(u64 key, u32 pos, unsigned char* __restrict__ nf,
+                                              u32* __restrict__ ovf) const {
+    const u64 h = mix(key);
+    u32 s = u32(h) & mask;
+    const u64 qd = (h >> c) << D;
+    const u64 pmask = (1ull << P) - 1;
+    for (u32 d = 0; d < limit; ++d) {
+      const u64 mine = ((qd | d) << P) | pos;
+      u64 cur = tab[s];
+      if (cur == kEmpty) {
+        cur = atomicCAS(&tab[s], kEmpty, mine);
+        if (cur == kEmpty) return {s, 0, false};
+      }
+      if (((cur & ~kSettled) >> P) == (mine >> P)) {
+        if (cur & kSettled) return {s, u32(cur & pmask), true};
+        if (u32(cur & pmask) < pos) { mark(nf, pos); return {s, 0, false}; }
+        const u64 old = atomicMin(&tab[s], mine);
+        const u32 op = u32(old & pmask);
+        mark(nf, op < pos ? pos : op);
+        return {s, 0, false};
+      }
+      s = (s + 1) & mask;
+    }
+    atomicOr(ovf, 1u);
+    return {0, 0, false};
+  }
+  __device__ __forceinline__ void settle(u32 s, u32 id) const {
+    tab[s] = kSettled | (tab[s] & ~((1ull << P) - 1)) | id;
+  }
+  __device__ __forceinline__ u32 settled_id(u32 s) const { return u32(tab[s] & ((1ull << P) - 1)); }
 };
 
 // ---- insert kernels -----------------------------------------------------------
@@ -292,16 +362,17 @@ struct PackedTab {
 // dna.cpp:79-84,187-197), canonicalise (:135-143), hash-cons (emplace_leaf,
 // shared_tree.cpp:630-637).  The block's bases are staged through LDS with
 // coalesced 4-B loads.
+// Strands [i0, i1) of the current leaf chunk; i0 is a multiple of kBlock.
 template <int L, class Tab>
-__global__ __launch_bounds__(kBlock) void k_leaf_bases(const unsigned char* __restrict__ bases, u64 S, Tab T,
-                                                      u32* __restrict__ rec, unsigned char* __restrict__ nf,
+__global__ __launch_bounds__(kBlock) void k_leaf_bases(const unsigned char* __restrict__ bases, u64 i0, u64 i1,
+                                                      Tab T, u32* __restrict__ rec, unsigned char* __restrict__ nf,
                                                       Header* __restrict__ hdr) {
   __shared__ signed char lut[256];
   __shared__ __align__(16) unsigned char buf[kBlock * L + 16];
   const int tid = threadIdx.x;
   lut[tid] = (signed char)nac_code(tid);
-  const u64 first = u64(blockIdx.x) * kBlock;
-  const u64 nstr = (S - first) < u64(kBlock) ? (S - first) : u64(kBlock);
+  const u64 first = i0 + u64(blockIdx.x) * kBlock;
+  const u64 nstr = (i1 - first) < u64(kBlock) ? (i1 - first) : u64(kBlock);
   const u64 byte0 = first * L;                 // multiple of 4 (kBlock = 256)
   const u64 nbytes = nstr * L;
   const u32* src = reinterpret_cast<const u32*>(bases + byte0);
@@ -323,21 +394,23 @@ __global__ __launch_bounds__(kBlock) void k_leaf_bases(const unsigned char* __re
   if (bad >= 0) atomicMin(&hdr->err_offset, i * L + u64(bad));
   u32 m, t, v;
   const u64 key = leaf_canonical(x, L, m, t, v);
-  const u32 s = T.insert(key, u32(i), nf, hdr);
-  rec[i] = make_word(s, m, t, v);
+  const Ins r = T.insert_chunk(key, u32(i), nf, &hdr->leaf_overflow);
+  if (r.settled) nf[i] = kNfDone;
+  rec[i] = make_word(r.settled ? r.id : r.slot, m, t, v);
 }
 
 // Leaf level from packed strands (shared_tree(std::vector<dna>&), :212-215).
 template <class Tab>
-__global__ __launch_bounds__(kBlock) void k_leaf_packed(const u64* __restrict__ leaves, u64 S, int L, Tab T,
-                                                       u32* __restrict__ rec, unsigned char* __restrict__ nf,
+__global__ __launch_bounds__(kBlock) void k_leaf_packed(const u64* __restrict__ leaves, u64 i0, u64 i1, int L,
+                                                       Tab T, u32* __restrict__ rec, unsigned char* __restrict__ nf,
                                                        Header* __restrict__ hdr) {
-  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (i >= S) return;
+  const u64 i = i0 + u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= i1) return;
   u32 m, t, v;
   const u64 key = leaf_canonical(leaves[i], L, m, t, v);
-  const u32 s = T.insert(key, u32(i), nf, hdr);
-  rec[i] = make_word(s, m, t, v);
+  const Ins r = T.insert_chunk(key, u32(i), nf, &hdr->leaf_overflow);
+  if (r.settled) nf[i] = kNfDone;
+  rec[i] = make_word(r.settled ? r.id : r.slot, m, t, v);
 }
 
 // Pair (2j, 2j+1) of the previous level's final words; the odd tail pairs with
@@ -362,7 +435,7 @@ __global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ 
   load_pair(in, n, j, l, r);
   node_canonical(l, r, cl, cr, m, t);
   const u32 v = ulw(l) == ulw(xf(r, 1, 0));      // left == right.mirrored() (:670)
-  const u32 s = T.insert(T.node_key(cl, cr), u32(j), nf, hdr);
+  const u32 s = T.insert(T.node_key(cl, cr), u32(j), nf, &hdr->overflow);
   rec[j] = make_word(s, m, t, v);
 }
 
@@ -391,19 +464,21 @@ struct TileScan {
   u64 mask[kItems];
 };
 
+// Elements are positions [j0, p) of the level (j0 > 0 for later leaf chunks);
+// ids start at id0.  ts.base is the first position of the tile.
 __device__ __forceinline__ void tile_scan(TileScan& ts, u32* s_tile, u32* s_pre,
-                                          const unsigned char* __restrict__ nf, u64 p,
+                                          const unsigned char* __restrict__ nf, u64 j0, u64 p, u64 id0,
                                           u64* __restrict__ desc, u32* __restrict__ ticket,
                                           u64* __restrict__ count_out) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid == 0) *s_tile = atomicAdd(ticket, 1u);
   __syncthreads();
   const u64 tile = *s_tile;
-  ts.base = tile * kTile;
+  ts.base = j0 + tile * kTile;
 #pragma unroll
   for (int e = 0; e < kItems; ++e) {
     const u64 j = ts.base + u64(e) * kBlock + tid;
-    const bool first = j < p && nf[j] == 0;
+    const bool first = j < p && nf[j] == kNfMaybe;
     ts.mask[e] = __ballot(first);
     if (lane == 0) s_pre[e * 4 + wave] = u32(__popcll(ts.mask[e]));
   }
@@ -417,9 +492,9 @@ __device__ __forceinline__ void tile_scan(TileScan& ts, u32* s_tile, u32* s_pre,
       if (lane >= o) incl += y;
     }
     const u64 agg = __shfl(incl, 63, 64);
-    u64 prefix = 0;
+    u64 prefix = tile == 0 ? id0 : 0;   // descriptors' P values already include id0
     if (tile == 0) {
-      if (lane == 0) __hip_atomic_store(&desc[0], kStP | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) __hip_atomic_store(&desc[0], kStP | (id0 + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       if (lane == 0) __hip_atomic_store(&desc[tile], kStA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       long long look = (long long)tile - 1;
@@ -444,23 +519,26 @@ __device__ __forceinline__ void tile_scan(TileScan& ts, u32* s_tile, u32* s_pre,
         __hip_atomic_store(&desc[tile], kStP | (prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (lane < kGroupsPerTile) s_pre[lane] = u32(prefix + incl - c);
-    if (lane == 0 && (tile + 1) * kTile >= p) *count_out = prefix + agg;
+    if (lane == 0 && ts.base + kTile >= p) *count_out = prefix + agg;
   }
   __syncthreads();
 }
 
-// Leaves: first occurrences read their slot to recover the canonical leaf,
-// emit it, and publish slot -> id for resolve_leaf.
+// Leaves (one launch per leaf chunk, positions [j0, p), ids from id0 =
+// uniques of earlier chunks): first occurrences read their slot to recover the
+// canonical leaf, emit it, and settle the slot with their id, which both the
+// chunk's resolve and later chunks' inserts read.
 template <class Tab>
-__global__ __launch_bounds__(kBlock) void k_flagscan_leaf(u32* __restrict__ words, u64 p, Tab T,
+__global__ __launch_bounds__(kBlock) void k_flagscan_leaf(u32* __restrict__ words, u64 j0, u64 p, Tab T,
                                                          const unsigned char* __restrict__ nf,
                                                          u64* __restrict__ desc, u32* __restrict__ ticket,
-                                                         u64* __restrict__ out, u32* __restrict__ ids,
+                                                         u64* __restrict__ out, const u64* __restrict__ id0_p,
                                                          u64* __restrict__ count_out) {
   __shared__ u32 s_tile;
   __shared__ u32 s_pre[kGroupsPerTile];
   TileScan ts;
-  tile_scan(ts, &s_tile, s_pre, nf, p, desc, ticket, count_out);
+  const u64 id0 = id0_p ? *id0_p : 0;
+  tile_scan(ts, &s_tile, s_pre, nf, j0, p, id0, desc, ticket, count_out);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const u64 lt = (1ull << lane) - 1;
 #pragma unroll
@@ -473,7 +551,7 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_leaf(u32* __restrict__ word
       u32 pos;
       T.read(rec & kIdx, key, pos);
       out[id] = key;
-      ids[rec & kIdx] = id;
+      T.settle(rec & kIdx, id);
       words[j] = id | (rec & kBits);
     }
   }
@@ -491,7 +569,7 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
   __shared__ u32 s_tile;
   __shared__ u32 s_pre[kGroupsPerTile];
   TileScan ts;
-  tile_scan(ts, &s_tile, s_pre, nf, p, desc, ticket, count_out);
+  tile_scan(ts, &s_tile, s_pre, nf, 0, p, 0, desc, ticket, count_out);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const u64 lt = (1ull << lane) - 1;
 #pragma unroll
@@ -518,13 +596,15 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
 
 // ---- resolve ----------------------------------------------------------------------
 
-__global__ __launch_bounds__(kBlock) void k_resolve_leaf(u32* __restrict__ words, u64 p,
-                                                        const unsigned char* __restrict__ nf,
-                                                        const u32* __restrict__ ids) {
-  const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (j >= p || nf[j] == 0) return;
+// Non-first leaves of a chunk: their key's first occurrence is in this chunk
+// and has settled the slot.
+template <class Tab>
+__global__ __launch_bounds__(kBlock) void k_resolve_leaf(u32* __restrict__ words, u64 j0, u64 p, Tab T,
+                                                        const unsigned char* __restrict__ nf) {
+  const u64 j = j0 + u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= p || nf[j] != kNfNot) return;
   const u32 w = words[j];
-  words[j] = ids[w & kIdx] | (w & kBits);
+  words[j] = T.settled_id(w & kIdx) | (w & kBits);
 }
 
 template <class Tab>
@@ -532,7 +612,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve_node(u32* __restrict__ words
                                                         const unsigned char* __restrict__ nf,
                                                         const Group* __restrict__ grp) {
   const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (j >= p || nf[j] == 0) return;
+  if (j >= p || nf[j] != kNfNot) return;
   const u32 w = words[j];
   u64 key;
   u32 q;
