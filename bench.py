@@ -48,7 +48,7 @@ def load_gcz():
     return mod
 
 
-def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes):
+def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None):
     """Algorithmic HBM bytes of all launches of `kernel` in one build:
     streamed bytes + one 64-B sector per random table/group access."""
     pk = []
@@ -62,8 +62,9 @@ def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes):
     U = n_leaves
     if kernel == "leaf_insert":     # ASCII in, provisional word out, one table sector per strand
         return S * L + 4 * S + 64 * S
-    if kernel == "node_insert":     # pair in, word out, one table sector per pair
-        return sum(8 * p + 4 * p + 64 * p for p in pk)
+    if kernel == "node_insert":     # pair + child marks in, word out; table sector per hashed pair
+        hashed = hashed_pairs if hashed_pairs is not None else sum(pk)
+        return sum(8 * p + 4 * p + 4 * p for p in pk) + 64 * hashed
     if kernel == "flagscan_leaf":   # not-first marks; firsts: word, slot sector, leaf out, slot->id sector
         return S + U * (4 + 64 + 8 + 64 + 4)
     if kernel == "flagscan_node":   # not-first marks, group records; firsts: pair re-read, node out, word
@@ -182,7 +183,7 @@ def main():
     for name, p in prof.items():
         if p["launches"] == 0:
             continue
-        b = algorithmic_bytes(name, L, S, info["n_leaves"], info["layer_size"])
+        b = algorithmic_bytes(name, L, S, info["n_leaves"], info["layer_size"], info["hashed_pairs"])
         kernels[name] = {"launches": p["launches"], "total_ms": round(p["total_ms"], 4),
                          "avg_ms": p["total_ms"] / p["launches"], "alg_bytes": b,
                          "gbs": b / (p["total_ms"] * 1e-3) / 1e9 if p["total_ms"] > 0 else None}
@@ -227,7 +228,7 @@ def main():
             "config": {"workload": args.config, "nbases_per_gpu": nbases, "L": L, "strands_per_gpu": S,
                        "parallelism": f"independent shard genome per GPU x{world}"},
             "roofline": roofline,
-            "build": {"device_ms": info["build_ms"], "b_stream": b_stream, "b_table": b_table,
+            "build": {"device_ms": info["build_ms"], "hashed_pairs": info["hashed_pairs"], "b_stream": b_stream, "b_table": b_table,
                       "hbm_frac_survey_formula": round(build_frac, 5), "n_leaves": info["n_leaves"],
                       "n_layers": info["n_layers"]},
             "kernels": kernels,

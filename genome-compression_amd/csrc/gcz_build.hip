@@ -105,7 +105,7 @@ struct gcz_ctx {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   std::string last_error;
-  DevBuf wa, wb, grp, desc, tab, leaves_out, nodes_out, hdr, input, nf, ids;
+  DevBuf wa, wb, grp, desc, tab, leaves_out, nodes_out, hdr, input, nf, multi;
   Header* h_hdr = nullptr;   // pinned
   // last build
   gcz_info info{};
@@ -114,6 +114,8 @@ struct gcz_ctx {
   // profiling
   bool profile = false;
   bool force_wide = false;   // GCZ_TABLE=wide: always use 16-B slots (testing)
+  int node_cap_shift = 1;    // node table capacity = next_pow2(p << shift)   (GCZ_NODE_CAP_SHIFT)
+  int leaf_cap_log2 = 0;     // force the adaptive leaf table size            (GCZ_LEAF_CAP_LOG2)
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> event_pool;
   size_t event_used = 0;
@@ -237,7 +239,12 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   const u64 full_cap = std::max<u64>(256, next_pow2(2 * S));
   u64 leaf_cap = full_cap;
   if (S > (1ull << 22)) leaf_cap = std::min(full_cap, std::max<u64>(1ull << 23, leaf_cap_hint));
-  const u64 node_cap0 = std::max<u64>(256, next_pow2(2 * pk[0]));
+  if (leaf_cap_log2 > 0 && S > (1ull << 22)) leaf_cap = std::min(full_cap, 1ull << leaf_cap_log2);
+  // load <= 2/3 (shift 0), 1/2 (shift 1, default) or 1/4 (shift 2)
+  auto node_cap = [&](u64 p) {
+    return std::max<u64>(256, next_pow2(node_cap_shift <= 0 ? p + p / 2 + 1 : p << node_cap_shift));
+  };
+  const u64 node_cap0 = node_cap(pk[0]);
 
   int rc;
   if ((rc = ensure(wa, S * 4 + 16))) return rc;
@@ -247,7 +254,9 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   if ((rc = ensure(leaves_out, S * 8 + 16))) return rc;
   if ((rc = ensure(nodes_out, layer_off[D] * 8 + 16))) return rc;
   if ((rc = ensure(hdr, sizeof(Header)))) return rc;
-  if ((rc = ensure(nf, S + 16))) return rc;
+  const u64 full_b = (S + 16 + 255) / 256 * 256, half = ((S + 1) / 2 + 16 + 255) / 256 * 256;
+  if ((rc = ensure(nf, full_b + half))) return rc;       // [leaf / even layers: S][odd layers: S/2]
+  if ((rc = ensure(multi, 2 * half))) return rc;         // [even layers][odd layers]
   if (!h_hdr) HIP_TRY(hipHostMalloc((void**)&h_hdr, sizeof(Header), hipHostMallocDefault));
 
   Header* d_hdr = static_cast<Header*>(hdr.ptr);
@@ -256,6 +265,8 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   Group* d_grp = static_cast<Group*>(grp.ptr);
   u64* d_desc = static_cast<u64*>(desc.ptr);
   unsigned char* d_nf = static_cast<unsigned char*>(nf.ptr);
+  unsigned char* nf_set[2] = {d_nf, d_nf + full_b};
+  unsigned char* multi_set[2] = {static_cast<unsigned char*>(multi.ptr), static_cast<unsigned char*>(multi.ptr) + half};
 
   if (!ev_start) {
     HIP_TRY(hipEventCreate(&ev_start));
@@ -330,36 +341,42 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     u64 bound = std::min(S, leaf_cap);        // child ids of layer 0 are leaf ids < #slots
     for (int k = 0; k < D; ++k) {
       const u64 p = pk[k];
-      const u64 cap = std::max<u64>(256, next_pow2(2 * p));
+      const u64 cap = node_cap(p);
       const u32 Bk = std::max<u32>(1, bit_width(bound));
       const LevelTab nt = plan_table(tab.ptr, cap, 2 * (Bk + 3), p, Bk, allow_packed, kMaxProbe);
+      const int cur = (k + 1) & 1, prev = k & 1;
+      unsigned char* knf = nf_set[cur];
+      const Marks mk{knf, multi_set[cur]};
+      const unsigned char* pnf = k == 0 ? nullptr : nf_set[prev];
+      const unsigned char* pmu = k == 0 ? nullptr : multi_set[prev];
       prof_begin(KID_MEMSET, e0);
       HIP_TRY(hipMemsetAsync(tab.ptr, 0xff, nt.bytes(), stream));
-      HIP_TRY(hipMemsetAsync(d_nf, 0, p, stream));
+      HIP_TRY(hipMemsetAsync(knf, 0, p, stream));
+      HIP_TRY(hipMemsetAsync(mk.multi, 0, p, stream));
       prof_end(KID_MEMSET, e0);
       prof_begin(KID_NODE, e0);
       const dim3 gi(unsigned((p + kBlock - 1) / kBlock));
       if (nt.packed)
-        hipLaunchKernelGGL((k_node_insert<PackedTab>), gi, dim3(kBlock), 0, stream, in, n, p, nt.pt, outw, d_nf,
-                           d_hdr);
+        hipLaunchKernelGGL((k_node_insert<PackedTab>), gi, dim3(kBlock), 0, stream, in, n, p, nt.pt, pnf, pmu, outw,
+                           mk, d_hdr);
       else
-        hipLaunchKernelGGL((k_node_insert<WideTab>), gi, dim3(kBlock), 0, stream, in, n, p, nt.wt, outw, d_nf,
-                           d_hdr);
+        hipLaunchKernelGGL((k_node_insert<WideTab>), gi, dim3(kBlock), 0, stream, in, n, p, nt.wt, pnf, pmu, outw,
+                           mk, d_hdr);
       HIP_TRY(hipGetLastError());
       prof_end(KID_NODE, e0);
       prof_begin(KID_FLAGSCAN_NODE, e0);
       const dim3 gs(unsigned((p + kTile - 1) / kTile));
       uint2* out_k = static_cast<uint2*>(nodes_out.ptr) + layer_off[k];
-      hipLaunchKernelGGL(k_flagscan_node, gs, dim3(kBlock), 0, stream, outw, p, in, n, d_nf, d_grp,
+      hipLaunchKernelGGL(k_flagscan_node, gs, dim3(kBlock), 0, stream, outw, p, in, n, knf, d_grp,
                          d_desc + desc_off[C + k], &d_hdr->ticket[kLayerSlot + k], out_k,
                          &d_hdr->count[kLayerSlot + k]);
       HIP_TRY(hipGetLastError());
       prof_end(KID_FLAGSCAN_NODE, e0);
       prof_begin(KID_RESOLVE_NODE, e0);
       if (nt.packed)
-        hipLaunchKernelGGL((k_resolve_node<PackedTab>), gi, dim3(kBlock), 0, stream, outw, p, nt.pt, d_nf, d_grp);
+        hipLaunchKernelGGL((k_resolve_node<PackedTab>), gi, dim3(kBlock), 0, stream, outw, p, nt.pt, knf, d_grp);
       else
-        hipLaunchKernelGGL((k_resolve_node<WideTab>), gi, dim3(kBlock), 0, stream, outw, p, nt.wt, d_nf, d_grp);
+        hipLaunchKernelGGL((k_resolve_node<WideTab>), gi, dim3(kBlock), 0, stream, outw, p, nt.wt, knf, d_grp);
       HIP_TRY(hipGetLastError());
       prof_end(KID_RESOLVE_NODE, e0);
       std::swap(in, outw);
@@ -402,6 +419,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   leaf_cap_hint = next_pow2(std::max<u64>(1, info.n_leaves * 4 / 3));
   for (int k = 0; k < D; ++k) info.layer_size[k] = h_hdr->count[kLayerSlot + k];
   info.root = h_hdr->root;
+  for (int i = 0; i < 64; ++i) info.hashed_pairs += h_hdr->hashed[i];
   return GCZ_OK;
 }
 
@@ -422,6 +440,8 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   }
   c->stream = c->own_stream;
   if (const char* t = std::getenv("GCZ_TABLE")) c->force_wide = std::strcmp(t, "wide") == 0;
+  if (const char* t = std::getenv("GCZ_NODE_CAP_SHIFT")) c->node_cap_shift = std::atoi(t);
+  if (const char* t = std::getenv("GCZ_LEAF_CAP_LOG2")) c->leaf_cap_log2 = std::atoi(t);
   *out = c;
   return GCZ_OK;
 }
@@ -431,7 +451,7 @@ void gcz_ctx_destroy(gcz_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->wa, &c->wb, &c->grp, &c->desc, &c->tab, &c->leaves_out, &c->nodes_out, &c->hdr, &c->input,
-                    &c->nf, &c->ids})
+                    &c->nf, &c->multi})
     if (b->ptr) (void)hipFree(b->ptr);
   if (c->h_hdr) (void)hipHostFree(c->h_hdr);
   for (auto e : c->event_pool) (void)hipEventDestroy(e);

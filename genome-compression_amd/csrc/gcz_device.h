@@ -71,6 +71,7 @@ struct Header {
   u64 count[kScanSlots];   // leaf chunk c: unique leaves after chunk c (cumulative); layer k: its uniques
   u32 ticket[kScanSlots];  // look-back tile tickets
   u64 err_offset;          // first unknown symbol (min), ~0 if none
+  u64 hashed[64];          // node pairs that went through the table (statistics, sharded)
   u32 overflow;            // a node-level probe bound was exceeded
   u32 leaf_overflow;       // the (adaptively sized) leaf table was too small
   u32 root;
@@ -199,6 +200,26 @@ __device__ __forceinline__ u32 dec_child(u32 e, u32 B) {
 constexpr unsigned char kNfMaybe = 0, kNfNot = 1, kNfDone = 2;
 __device__ __forceinline__ void mark(unsigned char* nf, u32 pos) { nf[pos] = kNfNot; }
 
+// Marks of one level: nf (not first) and, on node levels, multi (the key has
+// more than one occurrence).  When an insert learns of another occurrence
+// `other` of its key, the later of the two positions is not first and the
+// earlier one is multi.  The final minimum is always marked multi when its
+// key repeats: either it lowered the slot from another position (and marks
+// itself), or it claimed the slot and every later occurrence finds it there.
+struct Marks {
+  unsigned char* nf;
+  unsigned char* multi;   // null on the leaf level (not tracked)
+};
+__device__ __forceinline__ void mark_dup(const Marks& mk, u32 self, u32 other) {
+  if (other < self) {
+    mk.nf[self] = kNfNot;
+    if (mk.multi) mk.multi[other] = 1;
+  } else {
+    mk.nf[other] = kNfNot;
+    if (mk.multi) mk.multi[self] = 1;
+  }
+}
+
 // Result of a leaf-chunk insert: the slot, or the settled id of the key.
 struct Ins {
   u32 slot;
@@ -213,8 +234,7 @@ struct WideTab {
   u32 B;   // unused
 
   __device__ __forceinline__ u64 node_key(u32 cl, u32 cr) const { return (u64(cl) << 32) | cr; }
-  __device__ __forceinline__ u32 insert(u64 key, u32 pos, unsigned char* __restrict__ nf,
-                                        u32* __restrict__ ovf) const {
+  __device__ __forceinline__ u32 insert(u64 key, u32 pos, const Marks& mk, u32* __restrict__ ovf) const {
     const u64 skey = key ^ 1ull;
     u32 s = slot_hash(skey) & mask;
     for (u32 probe = 0; probe < limit; ++probe) {
@@ -224,16 +244,14 @@ struct WideTab {
         k = atomicCAS(&tab[s].key, kEmpty, skey);
         if (k == kEmpty) {                       // claimed: now lower pos from EMPTY
           const u32 old = atomicMin(&tab[s].pos, pos);
-          if (old < pos) mark(nf, pos);
-          else if (old != ~0u) mark(nf, old);
+          if (old != ~0u) mark_dup(mk, pos, old);
           return s;
         }
       }
       if (k == skey) {
-        if (cur.pos < pos) { mark(nf, pos); return s; }
+        if (cur.pos < pos) { mark_dup(mk, pos, cur.pos); return s; }
         const u32 old = atomicMin(&tab[s].pos, pos);
-        if (old < pos) mark(nf, pos);
-        else if (old != ~0u) mark(nf, old);
+        if (old != ~0u) mark_dup(mk, pos, old);
         return s;
       }
       s = (s + 1) & mask;
@@ -248,14 +266,14 @@ struct WideTab {
   }
   // Leaf chunks: a slot whose key's first occurrence lies in an earlier chunk
   // carries its final id in pad (0xffffffff until settled).
-  __device__ __forceinline__ Ins insert_chunk(u64 key, u32 pos, unsigned char* __restrict__ nf,
+  __device__ __forceinline__ Ins insert_chunk(u64 key, u32 pos, const Marks& mk,
                                               u32* __restrict__ ovf) const {
     const u64 skey = key ^ 1ull;
     u32 s = slot_hash(skey) & mask;
     for (u32 probe = 0; probe < limit; ++probe) {
       const Slot cur = tab[s];
       if (cur.key == skey && cur.pad != ~0u) return {s, cur.pad, true};
-      if (cur.key == kEmpty || cur.key == skey) return {insert(key, pos, nf, ovf), 0, false};
+      if (cur.key == kEmpty || cur.key == skey) return {insert(key, pos, mk, ovf), 0, false};
       s = (s + 1) & mask;
     }
     atomicOr(ovf, 1u);
@@ -288,8 +306,7 @@ struct PackedTab {
     h ^= h >> sh;
     return h;
   }
-  __device__ __forceinline__ u32 insert(u64 key, u32 pos, unsigned char* __restrict__ nf,
-                                        u32* __restrict__ ovf) const {
+  __device__ __forceinline__ u32 insert(u64 key, u32 pos, const Marks& mk, u32* __restrict__ ovf) const {
     const u64 h = mix(key);
     u32 s = u32(h) & mask;
     const u64 qd = (h >> c) << D;             // quotient; displacement bits below
@@ -302,10 +319,9 @@ struct PackedTab {
         if (cur == kEmpty) return s;            // new key: one atomic, nothing to mark
       }
       if ((cur >> P) == (mine >> P)) {
-        if (u32(cur & pmask) < pos) { mark(nf, pos); return s; }
+        if (u32(cur & pmask) < pos) { mark_dup(mk, pos, u32(cur & pmask)); return s; }
         const u64 old = atomicMin(&tab[s], mine);
-        const u32 op = u32(old & pmask);
-        mark(nf, op < pos ? pos : op);
+        mark_dup(mk, pos, u32(old & pmask));
         return s;
       }
       s = (s + 1) & mask;
@@ -324,7 +340,7 @@ struct PackedTab {
   // Leaf chunks (needs Q + D + P <= 63): a settled slot keeps its key bits and
   // holds the final id in the position field, with bit 63 set.
   static constexpr u64 kSettled = 1ull << 63;
-  __device__ __forceinline__ Ins insert_chunk(u64 key, u32 pos, unsigned char* __restrict__ nf,
+  __device__ __forceinline__ Ins insert_chunk(u64 key, u32 pos, const Marks& mk,
                                               u32* __restrict__ ovf) const {
     const u64 h = mix(key);
     u32 s = u32(h) & mask;
@@ -339,10 +355,9 @@ struct PackedTab {
       }
       if (((cur & ~kSettled) >> P) == (mine >> P)) {
         if (cur & kSettled) return {s, u32(cur & pmask), true};
-        if (u32(cur & pmask) < pos) { mark(nf, pos); return {s, 0, false}; }
+        if (u32(cur & pmask) < pos) { mark_dup(mk, pos, u32(cur & pmask)); return {s, 0, false}; }
         const u64 old = atomicMin(&tab[s], mine);
-        const u32 op = u32(old & pmask);
-        mark(nf, op < pos ? pos : op);
+        mark_dup(mk, pos, u32(old & pmask));
         return {s, 0, false};
       }
       s = (s + 1) & mask;
@@ -394,7 +409,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_bases(const unsigned char* __re
   if (bad >= 0) atomicMin(&hdr->err_offset, i * L + u64(bad));
   u32 m, t, v;
   const u64 key = leaf_canonical(x, L, m, t, v);
-  const Ins r = T.insert_chunk(key, u32(i), nf, &hdr->leaf_overflow);
+  const Ins r = T.insert_chunk(key, u32(i), Marks{nf, nullptr}, &hdr->leaf_overflow);
   if (r.settled) nf[i] = kNfDone;
   rec[i] = make_word(r.settled ? r.id : r.slot, m, t, v);
 }
@@ -408,7 +423,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_packed(const u64* __restrict__ 
   if (i >= i1) return;
   u32 m, t, v;
   const u64 key = leaf_canonical(leaves[i], L, m, t, v);
-  const Ins r = T.insert_chunk(key, u32(i), nf, &hdr->leaf_overflow);
+  const Ins r = T.insert_chunk(key, u32(i), Marks{nf, nullptr}, &hdr->leaf_overflow);
   if (r.settled) nf[i] = kNfDone;
   rec[i] = make_word(r.settled ? r.id : r.slot, m, t, v);
 }
@@ -425,18 +440,48 @@ __device__ __forceinline__ void load_pair(const u32* __restrict__ in, u64 n, u64
 }
 
 // Node level, tree_constructor::emplace_node (src/shared_tree.cpp:662-672).
+//
+// Singleton propagation: a previous-level element that is the only occurrence
+// of its key (first, not multi) is referenced by exactly one input word, so
+// every symmetry variant of a pair containing it contains that one word: the
+// pair's key cannot occur anywhere else.  Such pairs skip the table entirely
+// (first occurrence, only occurrence); only pairs of two repeated children
+// are hash-consed.  prev_nf/prev_multi are null when the children are leaves
+// (not tracked).
 template <class Tab>
 __global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ in, u64 n, u64 p, Tab T,
-                                                       u32* __restrict__ rec, unsigned char* __restrict__ nf,
+                                                       const unsigned char* __restrict__ prev_nf,
+                                                       const unsigned char* __restrict__ prev_multi,
+                                                       u32* __restrict__ rec, Marks mk,
                                                        Header* __restrict__ hdr) {
+  __shared__ u32 s_hashed;
+  if (threadIdx.x == 0) s_hashed = 0;
+  __syncthreads();
   const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (j >= p) return;
+  bool single = true;
+  if (j < p) {
   u32 l, r, cl, cr, m, t;
   load_pair(in, n, j, l, r);
   node_canonical(l, r, cl, cr, m, t);
   const u32 v = ulw(l) == ulw(xf(r, 1, 0));      // left == right.mirrored() (:670)
-  const u32 s = T.insert(T.node_key(cl, cr), u32(j), nf, &hdr->overflow);
+  single = false;
+  if (prev_nf) {
+    if (2 * j + 1 < n) {
+      const uchar2 f = reinterpret_cast<const uchar2*>(prev_nf)[j];
+      const uchar2 g = reinterpret_cast<const uchar2*>(prev_multi)[j];
+      single = (f.x == 0 && g.x == 0) || (f.y == 0 && g.y == 0);
+    } else {
+      single = prev_nf[2 * j] == 0 && prev_multi[2 * j] == 0;
+    }
+  }
+  const u32 s = single ? 0u : T.insert(T.node_key(cl, cr), u32(j), mk, &hdr->overflow);
   rec[j] = make_word(s, m, t, v);
+  }
+  // statistics: pairs hashed, one LDS add per wave, one sharded global add per block
+  const u64 hb = __ballot(!single);
+  if ((threadIdx.x & 63) == 0 && hb) atomicAdd(&s_hashed, u32(__popcll(hb)));
+  __syncthreads();
+  if (threadIdx.x == 0 && s_hashed) atomicAdd(&hdr->hashed[blockIdx.x & 63], u64(s_hashed));
 }
 
 // ---- flag scan ------------------------------------------------------------------

@@ -63,6 +63,7 @@ typedef struct {
   uint64_t error_offset;             /* GCZ_ERR_SYMBOL: byte offset into the bases */
   int error_symbol;                  /* the offending byte */
   double build_ms;                   /* device time of the build (hipEvents) */
+  uint64_t hashed_pairs;             /* node pairs hash-consed (others skipped as provably unique) */
 } gcz_info;
 
 /* ---- device context ---------------------------------------------------- */
