@@ -349,34 +349,41 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       const Marks mk{knf, multi_set[cur]};
       const unsigned char* pnf = k == 0 ? nullptr : nf_set[prev];
       const unsigned char* pmu = k == 0 ? nullptr : multi_set[prev];
+      const u64* pcount = k == 0 ? &d_hdr->count[C - 1] : &d_hdr->count[kLayerSlot + k - 1];
+      uint2* out_k = static_cast<uint2*>(nodes_out.ptr) + layer_off[k];
+      u64* count_k = &d_hdr->count[kLayerSlot + k];
       prof_begin(KID_MEMSET, e0);
-      HIP_TRY(hipMemsetAsync(tab.ptr, 0xff, nt.bytes(), stream));
-      HIP_TRY(hipMemsetAsync(knf, 0, p, stream));
-      HIP_TRY(hipMemsetAsync(mk.multi, 0, p, stream));
+      {
+        const u64 tab16 = nt.bytes() / 16, p16 = (p + 15) / 16;
+        const u64 blocks = std::min<u64>(4096, (std::max(tab16, p16) + kBlock - 1) / kBlock);
+        hipLaunchKernelGGL(k_clear, dim3(unsigned(blocks)), dim3(kBlock), 0, stream, static_cast<uint4*>(tab.ptr),
+                           tab16, reinterpret_cast<uint4*>(knf), reinterpret_cast<uint4*>(mk.multi), p16, pcount, n);
+        HIP_TRY(hipGetLastError());
+      }
       prof_end(KID_MEMSET, e0);
       prof_begin(KID_NODE, e0);
       const dim3 gi(unsigned((p + kBlock - 1) / kBlock));
       if (nt.packed)
         hipLaunchKernelGGL((k_node_insert<PackedTab>), gi, dim3(kBlock), 0, stream, in, n, p, nt.pt, pnf, pmu, outw,
-                           mk, d_hdr);
+                           mk, d_hdr, pcount, out_k, count_k);
       else
         hipLaunchKernelGGL((k_node_insert<WideTab>), gi, dim3(kBlock), 0, stream, in, n, p, nt.wt, pnf, pmu, outw,
-                           mk, d_hdr);
+                           mk, d_hdr, pcount, out_k, count_k);
       HIP_TRY(hipGetLastError());
       prof_end(KID_NODE, e0);
       prof_begin(KID_FLAGSCAN_NODE, e0);
       const dim3 gs(unsigned((p + kTile - 1) / kTile));
-      uint2* out_k = static_cast<uint2*>(nodes_out.ptr) + layer_off[k];
       hipLaunchKernelGGL(k_flagscan_node, gs, dim3(kBlock), 0, stream, outw, p, in, n, knf, d_grp,
-                         d_desc + desc_off[C + k], &d_hdr->ticket[kLayerSlot + k], out_k,
-                         &d_hdr->count[kLayerSlot + k]);
+                         d_desc + desc_off[C + k], &d_hdr->ticket[kLayerSlot + k], out_k, count_k, pcount);
       HIP_TRY(hipGetLastError());
       prof_end(KID_FLAGSCAN_NODE, e0);
       prof_begin(KID_RESOLVE_NODE, e0);
       if (nt.packed)
-        hipLaunchKernelGGL((k_resolve_node<PackedTab>), gi, dim3(kBlock), 0, stream, outw, p, nt.pt, knf, d_grp);
+        hipLaunchKernelGGL((k_resolve_node<PackedTab>), gi, dim3(kBlock), 0, stream, outw, p, nt.pt, knf, d_grp,
+                           pcount, n);
       else
-        hipLaunchKernelGGL((k_resolve_node<WideTab>), gi, dim3(kBlock), 0, stream, outw, p, nt.wt, knf, d_grp);
+        hipLaunchKernelGGL((k_resolve_node<WideTab>), gi, dim3(kBlock), 0, stream, outw, p, nt.wt, knf, d_grp,
+                           pcount, n);
       HIP_TRY(hipGetLastError());
       prof_end(KID_RESOLVE_NODE, e0);
       std::swap(in, outw);

@@ -448,12 +448,36 @@ __device__ __forceinline__ void load_pair(const u32* __restrict__ in, u64 n, u64
 // (first occurrence, only occurrence); only pairs of two repeated children
 // are hash-consed.  prev_nf/prev_multi are null when the children are leaves
 // (not tracked).
+//
+// Direct levels: when every element of the previous level is the only
+// occurrence of its key (its unique count equals its size), every pair of
+// this level is too, so ids are positions: the insert writes the final word
+// and the unique node itself, and flagscan/resolve/clear of the level exit.
+__device__ __forceinline__ bool level_direct(const u64* prev_count, u64 prev_n) {
+  return prev_count && *prev_count == prev_n;
+}
+
 template <class Tab>
 __global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ in, u64 n, u64 p, Tab T,
                                                        const unsigned char* __restrict__ prev_nf,
                                                        const unsigned char* __restrict__ prev_multi,
                                                        u32* __restrict__ rec, Marks mk,
-                                                       Header* __restrict__ hdr) {
+                                                       Header* __restrict__ hdr, const u64* prev_count,
+                                                       uint2* __restrict__ out, u64* __restrict__ count_out) {
+  if (level_direct(prev_count, n)) {
+    const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
+    if (j == 0) *count_out = p;
+    if (j >= p) return;
+    u32 l, r, cl, cr, m, t;
+    load_pair(in, n, j, l, r);
+    node_canonical(l, r, cl, cr, m, t);
+    const u32 v = ulw(l) == ulw(xf(r, 1, 0));
+    uint2 w;
+    w.x = cl; w.y = cr;
+    out[j] = w;
+    rec[j] = make_word(u32(j), m, t, v);
+    return;
+  }
   __shared__ u32 s_hashed;
   if (threadIdx.x == 0) s_hashed = 0;
   __syncthreads();
@@ -610,7 +634,8 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
                                                          const unsigned char* __restrict__ nf,
                                                          Group* __restrict__ grp, u64* __restrict__ desc,
                                                          u32* __restrict__ ticket, uint2* __restrict__ out,
-                                                         u64* __restrict__ count_out) {
+                                                         u64* __restrict__ count_out, const u64* prev_count) {
+  if (level_direct(prev_count, n)) return;
   __shared__ u32 s_tile;
   __shared__ u32 s_pre[kGroupsPerTile];
   TileScan ts;
@@ -655,7 +680,9 @@ __global__ __launch_bounds__(kBlock) void k_resolve_leaf(u32* __restrict__ words
 template <class Tab>
 __global__ __launch_bounds__(kBlock) void k_resolve_node(u32* __restrict__ words, u64 p, Tab T,
                                                         const unsigned char* __restrict__ nf,
-                                                        const Group* __restrict__ grp) {
+                                                        const Group* __restrict__ grp, const u64* prev_count,
+                                                        u64 n) {
+  if (level_direct(prev_count, n)) return;
   const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (j >= p || nf[j] != kNfNot) return;
   const u32 w = words[j];
@@ -668,5 +695,19 @@ __global__ __launch_bounds__(kBlock) void k_resolve_node(u32* __restrict__ words
 }
 
 __global__ void k_root(const u32* __restrict__ words, Header* __restrict__ hdr) { hdr->root = words[0]; }
+
+// Clear a node level's table (all ones) and marks (zero) unless the level is direct.
+__global__ __launch_bounds__(kBlock) void k_clear(uint4* __restrict__ tab, u64 tab16, uint4* __restrict__ nf,
+                                                 uint4* __restrict__ multi, u64 p16, const u64* prev_count,
+                                                 u64 prev_n) {
+  if (level_direct(prev_count, prev_n)) return;
+  const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u), zero = make_uint4(0, 0, 0, 0);
+  const u64 stride = u64(gridDim.x) * kBlock;
+  for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < tab16; i += stride) tab[i] = ones;
+  for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < p16; i += stride) {
+    nf[i] = zero;
+    multi[i] = zero;
+  }
+}
 
 }  // namespace gcz_dev
