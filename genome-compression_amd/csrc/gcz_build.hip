@@ -215,19 +215,31 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   const int D = int(pk.size());
   layer_off.assign(D + 1, 0);
   for (int k = 0; k < D; ++k) layer_off[k + 1] = layer_off[k] + pk[k];
-  // leaf chunks: up to 8, each a multiple of the scan tile
-  const u64 nchunks = std::max<u64>(1, std::min<u64>(8, S >> 21));
-  u64 csize = (S + nchunks - 1) / nchunks;
-  csize = (csize + kTile - 1) / kTile * kTile;
-  std::vector<u64> chunk_start;
-  for (u64 i = 0; i < S; i += csize) chunk_start.push_back(i);
-  chunk_start.push_back(S);
+  // leaf chunks, geometric: S/64, S/64, S/32, ... S/2 (multiples of the leaf tile);
+  // the first small chunks discover most keys, the big later ones mostly hit
+  // settled slots.  Small inputs are one chunk.
+  std::vector<u64> chunk_start{0};
+  {
+    const u64 tile = kLeafTile;
+    u64 next = std::max<u64>(tile, (S / 64 + tile - 1) / tile * tile);
+    if (S <= (1ull << 21)) next = S;
+    bool first = true;
+    while (chunk_start.back() < S && int(chunk_start.size()) < kMaxChunks) {
+      const u64 c0 = chunk_start.back();
+      u64 c1 = std::min(S, c0 + next);
+      if (S - c1 < tile) c1 = S;
+      chunk_start.push_back(c1);
+      if (!first) next *= 2;
+      first = false;
+    }
+    chunk_start.back() = S;
+  }
   const int C = int(chunk_start.size()) - 1;
   std::vector<u64> desc_off;
   u64 ntiles_total = 0;
   for (int c = 0; c < C; ++c) {
     desc_off.push_back(ntiles_total);
-    ntiles_total += (chunk_start[c + 1] - chunk_start[c] + kTile - 1) / kTile;
+    ntiles_total += (chunk_start[c + 1] - chunk_start[c] + kLeafTile - 1) / kLeafTile;
   }
   for (int k = 0; k < D; ++k) {
     desc_off.push_back(ntiles_total);
@@ -238,7 +250,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   // (every ACGT 12-mer class fits) and grow after an overflow.
   const u64 full_cap = std::max<u64>(256, next_pow2(2 * S));
   u64 leaf_cap = full_cap;
-  if (S > (1ull << 22)) leaf_cap = std::min(full_cap, std::max<u64>(1ull << 23, leaf_cap_hint));
+  if (S > (1ull << 22)) leaf_cap = std::min(full_cap, std::max<u64>(1ull << 24, leaf_cap_hint));
   if (leaf_cap_log2 > 0 && S > (1ull << 22)) leaf_cap = std::min(full_cap, 1ull << leaf_cap_log2);
   // load <= 2/3 (shift 0), 1/2 (shift 1, default) or 1/4 (shift 2)
   auto node_cap = [&](u64 p) {
@@ -314,7 +326,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       }
       HIP_TRY(hipGetLastError());
       prof_end(KID_LEAF, e0);
-      const dim3 gs(unsigned((i1 - i0 + kTile - 1) / kTile));
+      const dim3 gs(unsigned((i1 - i0 + kLeafTile - 1) / kLeafTile));
       const u64* id0 = c == 0 ? nullptr : &d_hdr->count[c - 1];
       prof_begin(KID_FLAGSCAN_LEAF, e0);
       if (lt.packed)
@@ -422,8 +434,8 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     return fail(GCZ_ERR_CAPACITY, "build", "hash table probe limit exceeded");
   info.n_layers = D;
   info.n_leaves = h_hdr->count[C - 1];
-  // next build of this size starts its adaptive leaf table at load <= 3/4 (speed only)
-  leaf_cap_hint = next_pow2(std::max<u64>(1, info.n_leaves * 4 / 3));
+  // next build starts its adaptive leaf table at load <= 1/4..1/2 (speed only)
+  leaf_cap_hint = next_pow2(std::max<u64>(1, info.n_leaves * 2));
   for (int k = 0; k < D; ++k) info.layer_size[k] = h_hdr->count[kLayerSlot + k];
   info.root = h_hdr->root;
   for (int i = 0; i < 64; ++i) info.hashed_pairs += h_hdr->hashed[i];

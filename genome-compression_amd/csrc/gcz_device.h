@@ -45,9 +45,11 @@ constexpr u32 kIdx = 0x1fffffffu;
 constexpr u32 kBits = 0xe0000000u;
 constexpr u64 kEmpty = ~0ull;
 constexpr int kBlock = 256;
-constexpr int kItems = 8;                  // flagscan elements per thread
+constexpr int kItems = 8;                  // node flagscan elements per thread
 constexpr int kTile = kBlock * kItems;     // 2048 elements per look-back tile
 constexpr int kGroupsPerTile = kTile / 64; // 32
+constexpr int kLeafItems = 16;             // leaf flagscan: most strands are already settled
+constexpr int kLeafTile = kBlock * kLeafItems;
 constexpr u32 kMaxProbe = 1u << 16;
 
 struct __align__(16) Slot {   // WideTab slot; key stored as key ^ 1 (see WideTab)
@@ -528,14 +530,16 @@ constexpr u64 kValMask = (1ull << 62) - 1;
 // group masks of this thread's wave, and the level total is in *count_out.
 // The look-back descriptor is one 64-bit word (status | value), so it needs
 // no separate payload and no fences (relaxed agent-scope atomics).
+template <int ITEMS>
 struct TileScan {
   u64 base;
-  u64 mask[kItems];
+  u64 mask[ITEMS];
 };
 
 // Elements are positions [j0, p) of the level (j0 > 0 for later leaf chunks);
 // ids start at id0.  ts.base is the first position of the tile.
-__device__ __forceinline__ void tile_scan(TileScan& ts, u32* s_tile, u32* s_pre,
+template <int ITEMS>
+__device__ __forceinline__ void tile_scan(TileScan<ITEMS>& ts, u32* s_tile, u32* s_pre,
                                           const unsigned char* __restrict__ nf, u64 j0, u64 p, u64 id0,
                                           u64* __restrict__ desc, u32* __restrict__ ticket,
                                           u64* __restrict__ count_out) {
@@ -543,9 +547,9 @@ __device__ __forceinline__ void tile_scan(TileScan& ts, u32* s_tile, u32* s_pre,
   if (tid == 0) *s_tile = atomicAdd(ticket, 1u);
   __syncthreads();
   const u64 tile = *s_tile;
-  ts.base = j0 + tile * kTile;
+  ts.base = j0 + tile * (kBlock * ITEMS);
 #pragma unroll
-  for (int e = 0; e < kItems; ++e) {
+  for (int e = 0; e < ITEMS; ++e) {
     const u64 j = ts.base + u64(e) * kBlock + tid;
     const bool first = j < p && nf[j] == kNfMaybe;
     ts.mask[e] = __ballot(first);
@@ -553,7 +557,7 @@ __device__ __forceinline__ void tile_scan(TileScan& ts, u32* s_tile, u32* s_pre,
   }
   __syncthreads();
   if (wave == 0) {
-    const u32 c = lane < kGroupsPerTile ? s_pre[lane] : 0u;
+    const u32 c = lane < 4 * ITEMS ? s_pre[lane] : 0u;
     u32 incl = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -587,8 +591,8 @@ __device__ __forceinline__ void tile_scan(TileScan& ts, u32* s_tile, u32* s_pre,
       if (lane == 0)
         __hip_atomic_store(&desc[tile], kStP | (prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (lane < kGroupsPerTile) s_pre[lane] = u32(prefix + incl - c);
-    if (lane == 0 && ts.base + kTile >= p) *count_out = prefix + agg;
+    if (lane < 4 * ITEMS) s_pre[lane] = u32(prefix + incl - c);
+    if (lane == 0 && ts.base + kBlock * ITEMS >= p) *count_out = prefix + agg;
   }
   __syncthreads();
 }
@@ -604,14 +608,14 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_leaf(u32* __restrict__ word
                                                          u64* __restrict__ out, const u64* __restrict__ id0_p,
                                                          u64* __restrict__ count_out) {
   __shared__ u32 s_tile;
-  __shared__ u32 s_pre[kGroupsPerTile];
-  TileScan ts;
+  __shared__ u32 s_pre[4 * kLeafItems];
+  TileScan<kLeafItems> ts;
   const u64 id0 = id0_p ? *id0_p : 0;
   tile_scan(ts, &s_tile, s_pre, nf, j0, p, id0, desc, ticket, count_out);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const u64 lt = (1ull << lane) - 1;
 #pragma unroll
-  for (int e = 0; e < kItems; ++e) {
+  for (int e = 0; e < kLeafItems; ++e) {
     const u64 j = ts.base + u64(e) * kBlock + tid;
     if (j < p && ((ts.mask[e] >> lane) & 1ull)) {
       const u32 id = s_pre[e * 4 + wave] + u32(__popcll(ts.mask[e] & lt));
@@ -638,7 +642,7 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
   if (level_direct(prev_count, n)) return;
   __shared__ u32 s_tile;
   __shared__ u32 s_pre[kGroupsPerTile];
-  TileScan ts;
+  TileScan<kItems> ts;
   tile_scan(ts, &s_tile, s_pre, nf, 0, p, 0, desc, ticket, count_out);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const u64 lt = (1ull << lane) - 1;
