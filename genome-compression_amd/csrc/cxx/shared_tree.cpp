@@ -1,0 +1,351 @@
+// shared_tree container (include/shared_tree.h) on top of libgcz.
+// Construction: the HIP build (gcz_build.hip) replaces tree_constructor
+// (reference src/shared_tree.cpp:621-763); everything after the build restates
+// the reference container: pointer compression :25-67,122-163, node :169-196,
+// access/indexing :231-291, histogram/sort :316-483, bytes/serialize/deserialize
+// :488-546, iterator :553-614.
+#include "shared_tree.h"
+
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <mutex>
+#include <numeric>
+#include <sstream>
+
+#include "gcz.h"
+#include "../gcz_internal.h"
+
+namespace {
+
+// One libgcz context per process (device GCZ_DEVICE, default 0), created on
+// first use.  Builds are serialised, matching the reference's single build thread.
+struct Engine {
+  gcz_ctx* ctx = nullptr;
+  std::mutex mu;
+  Engine() {
+    const char* d = std::getenv("GCZ_DEVICE");
+    const int rc = gcz_ctx_create(d ? std::atoi(d) : 0, &ctx);
+    if (rc != GCZ_OK) {
+      std::cerr << "libgcz: no usable MI355X device (code " << rc << "), aborting...\n";
+      std::exit(1);
+    }
+  }
+  ~Engine() { gcz_ctx_destroy(ctx); }
+};
+
+Engine& engine() {
+  static Engine e;
+  return e;
+}
+
+void check_build(int rc, gcz_ctx* ctx) {
+  if (rc == GCZ_OK) return;
+  gcz_info info{};
+  gcz_info_get(ctx, &info);
+  if (rc == GCZ_ERR_SYMBOL) {   // to_nac, src/dna.cpp:44-47
+    int c = info.error_symbol;
+    if (c >= 'a' && c <= 'z') c -= 32;
+    std::cerr << "Encountered unknown symbol: " << c << " (ASCII code " << c << ")\n";
+  } else if (rc == GCZ_ERR_EMPTY) {
+    std::cerr << "Genome shorter than one strand of " << dna::size() << " nucleotides, aborting...\n";
+  } else {
+    std::cerr << "libgcz build failed (code " << rc << "): " << gcz_ctx_last_error(ctx) << '\n';
+  }
+  std::exit(1);
+}
+
+// pointer compression, src/shared_tree.cpp:25-67
+int segment(std::uint32_t idx) {
+  if (idx == 0x1fffffffu) return 3;
+  if (idx < 16u) return 0;
+  if (idx < 16u + 4096u) return 1;
+  if (idx < 16u + 4096u + 1048576u) return 2;
+  return 3;
+}
+constexpr std::uint32_t kSegStart[4] = {0, 16, 16 + 4096, 16 + 4096 + 1048576};
+
+gcz::TreeView view(const std::vector<std::vector<node>>& nodes, const std::vector<dna>& leaves, pointer root) {
+  gcz::TreeView v;
+  v.L = int(dna::size());
+  v.leaves = const_cast<std::uint64_t*>(reinterpret_cast<const std::uint64_t*>(leaves.data()));
+  v.n_leaves = leaves.size();
+  for (const auto& layer : nodes) {
+    v.layer.push_back(const_cast<std::uint32_t*>(reinterpret_cast<const std::uint32_t*>(layer.data())));
+    v.layer_n.push_back(layer.size());
+  }
+  v.root = root.raw();
+  return v;
+}
+
+}  // namespace
+
+// ---- pointer -----------------------------------------------------------------
+// transform ctor, src/shared_tree.cpp:76-80
+pointer::pointer(const pointer& other, bool mirror, bool transpose) noexcept {
+  const std::uint32_t w = other.word;
+  const bool m = (w >> 29) & 1u, t = (w >> 30) & 1u, v = w >> 31;
+  const bool nm = (mirror != m) && !v;
+  const bool nt = (transpose != t) && other != nullptr;
+  word = (w & 0x9fffffffu) | (std::uint32_t(nm) << 29) | (std::uint32_t(nt) << 30);
+}
+
+auto pointer::bytes() const noexcept -> std::size_t {
+  return (4 + address_bits[segment(word & 0x1fffffffu)]) / 8;
+}
+
+void pointer::serialize(std::ostream& os) const {
+  const std::uint32_t idx = word & 0x1fffffffu;
+  const int seg = segment(idx);
+  const std::uint32_t off = idx == 0x1fffffffu ? 0xfffffffu : idx - kSegStart[seg];
+  int sh = address_bits[seg] - 4;
+  os.put(char((off >> sh) | (((word >> 29) & 1u) << 4) | (((word >> 30) & 1u) << 5) | (seg << 6)));
+  for (sh -= 8; sh >= 0; sh -= 8) os.put(char(off >> sh));
+}
+
+auto pointer::deserialize(std::istream& is) -> pointer {
+  const std::uint32_t first = static_cast<unsigned char>(is.get());
+  const int seg = (first >> 6) & 3;
+  std::uint64_t off = std::uint64_t(first & 0xf) << (address_bits[seg] - 4);
+  for (int sh = address_bits[seg] - 12; sh >= 0; sh -= 8) off |= std::uint64_t(static_cast<unsigned char>(is.get())) << sh;
+  const std::size_t idx = (seg == 3 && off == 0xfffffff) ? 0x1fffffffu : kSegStart[seg] + off;
+  return pointer{idx, bool((first >> 4) & 1), bool((first >> 5) & 1), false};
+}
+
+// ---- node ----------------------------------------------------------------------
+// node::canonical, include/shared_tree.h:119-126 (lexicographic min of (node, m, t))
+auto node::canonical() const noexcept -> std::tuple<node, bool, bool> {
+  std::tuple<node, bool, bool> best{*this, false, false};
+  const std::tuple<node, bool, bool> cand[3] = {{mirrored(), true, false}, {transposed(), false, true},
+                                                {inverted(), true, true}};
+  for (const auto& c : cand)
+    if (c < best) best = c;
+  return best;
+}
+
+void node::serialize(std::ostream& os) const {
+  children[0].serialize(os);
+  children[1].serialize(os);
+}
+
+auto node::deserialize(std::istream& is) -> node {
+  auto l = pointer::deserialize(is);
+  auto r = pointer::deserialize(is);
+  return node{l, r};
+}
+
+// ---- construction (libgcz) -------------------------------------------------------
+shared_tree::shared_tree(fasta_reader file, bool verbose) {
+  auto& e = engine();
+  std::lock_guard<std::mutex> lock(e.mu);
+  const auto& raw = file.raw();
+  check_build(gcz_build_host_fasta(e.ctx, raw.data(), raw.size(), int(dna::size())), e.ctx);
+  build_from_gpu();
+  if (verbose) std::cout << "\rConstructing subtrees: done.\n\rCombining subtrees: done.\n";
+}
+
+shared_tree::shared_tree(std::vector<dna>& data, bool verbose) {
+  static_assert(sizeof(dna) == 8, "dna is one 64-bit word");
+  auto& e = engine();
+  std::lock_guard<std::mutex> lock(e.mu);
+  check_build(gcz_build_host_leaves(e.ctx, reinterpret_cast<const std::uint64_t*>(data.data()), data.size(),
+                                    int(dna::size())),
+              e.ctx);
+  build_from_gpu();
+  if (verbose) std::cout << "\rConstructing subtrees: done.\n\rCombining subtrees: done.\n";
+}
+
+void shared_tree::build_from_gpu() {
+  gcz_ctx* ctx = engine().ctx;
+  gcz_info info{};
+  gcz_info_get(ctx, &info);
+  leaves.resize(info.n_leaves);
+  if (info.n_leaves) check_build(gcz_copy_leaves(ctx, reinterpret_cast<std::uint64_t*>(leaves.data())), ctx);
+  nodes.assign(info.n_layers, {});
+  for (int k = 0; k < info.n_layers; ++k) {
+    nodes[k].resize(info.layer_size[k], node{pointer{}});
+    check_build(gcz_copy_layer(ctx, k, reinterpret_cast<std::uint32_t*>(nodes[k].data())), ctx);
+  }
+  root = pointer::from_word(info.root);
+}
+
+// ---- accessors -----------------------------------------------------------------
+auto shared_tree::width() const -> std::size_t {
+  assert(nodes.back().size() == 1);
+  return gcz::view_width(view(nodes, leaves, root));
+}
+
+auto shared_tree::children(std::size_t layer, pointer p) const -> std::size_t {   // :252-259
+  if (p.empty()) return 0;
+  const auto n = access_node(layer, p);
+  if (layer == 0) return !n.left().empty() + !n.right().empty();
+  return children(layer - 1, n.left()) + children(layer - 1, n.right());
+}
+
+auto shared_tree::node_count() const -> std::size_t {
+  std::size_t sum = 0;
+  for (const auto& layer : nodes) sum += layer.size();
+  return sum;
+}
+
+auto shared_tree::access_leaf(pointer p) const -> dna {   // :231-236
+  auto leaf = leaves[p.index()];
+  if (p.is_mirrored()) leaf = leaf.mirrored();
+  if (p.is_transposed()) leaf = leaf.transposed();
+  return leaf;
+}
+
+auto shared_tree::operator[](std::uint64_t index) const -> dna {   // :268-291
+  auto current = root;
+  for (int layer = int(nodes.size()) - 1; layer >= 0; --layer) {
+    const auto n = access_node(std::size_t(layer), current);
+    const auto size = std::uint64_t(1) << layer;
+    const bool mirror = current.is_mirrored(), transpose = current.is_transposed();
+    const pointer first = mirror ? n.right() : n.left();
+    const pointer second = mirror ? n.left() : n.right();
+    if (index < size) {
+      current = pointer{first, mirror, transpose};
+    } else {
+      index -= size;
+      current = pointer{second, mirror, transpose};
+    }
+  }
+  return access_leaf(current);
+}
+
+// ---- frequency sort (:316-483) ------------------------------------------------------
+auto shared_tree::histogram(std::size_t layer) const -> std::vector<std::size_t> {
+  assert(layer < nodes.size());
+  std::vector<std::size_t> result(layer == 0 ? leaves.size() : nodes[layer - 1].size(), 0);
+  for (const auto& n : nodes[layer]) {
+    if (auto l = n.left(); l) ++result[l.index()];
+    if (auto r = n.right(); r) ++result[r.index()];
+  }
+  return result;
+}
+
+void shared_tree::store_histogram(std::filesystem::path path) const {
+  std::ofstream file{path};
+  for (std::size_t layer = 0; layer < nodes.size(); ++layer) {
+    auto freq = histogram(layer);
+    std::sort(freq.begin(), freq.end(), std::greater<>());
+    for (std::size_t i = 0; i < freq.size(); i += 1000) {
+      for (std::size_t j = i; j < std::min(freq.size(), i + 1000); ++j) file << freq[j] << ',';
+      file << '\n';
+    }
+    file << '\n';
+  }
+}
+
+void shared_tree::rewire_nodes(std::size_t layer, const std::vector<std::size_t>& indices) {
+  auto rewire = [&](pointer old) {
+    if (old.empty()) return old;
+    return pointer{indices[old.index()], old.is_mirrored(), old.is_transposed(), old.is_invariant()};
+  };
+  for (auto& n : nodes[layer]) n = node{rewire(n.left()), rewire(n.right())};
+}
+
+namespace {
+std::vector<std::size_t> sorted_positions(const std::vector<std::size_t>& freq) {
+  std::vector<std::size_t> idx(freq.size());
+  std::iota(idx.begin(), idx.end(), 0);
+  std::stable_sort(idx.begin(), idx.end(), [&](auto a, auto b) { return freq[a] > freq[b]; });
+  std::vector<std::size_t> inv(idx.size());
+  for (std::size_t i = 0; i < idx.size(); ++i) inv[idx[i]] = i;
+  return inv;
+}
+}  // namespace
+
+void shared_tree::sort_leaves() {
+  const auto pos = sorted_positions(histogram(0));
+  std::vector<dna> r(leaves.size());
+  for (std::size_t i = 0; i < pos.size(); ++i) r[pos[i]] = leaves[i];
+  leaves.swap(r);
+  rewire_nodes(0, pos);
+}
+
+void shared_tree::sort_nodes(std::size_t layer) {
+  const auto pos = sorted_positions(histogram(layer + 1));
+  std::vector<node> r(nodes[layer].size(), node{pointer{}});
+  for (std::size_t i = 0; i < pos.size(); ++i) r[pos[i]] = nodes[layer][i];
+  nodes[layer].swap(r);
+  rewire_nodes(layer + 1, pos);
+}
+
+void shared_tree::sort_tree(bool verbose) {
+  auto v = view(nodes, leaves, root);   // all layers at once, in parallel (same net effect)
+  gcz::view_sort(v);
+  if (verbose) std::cout << "\rSorting nodes: done.\n";
+}
+
+// ---- persistence (:488-546) ------------------------------------------------------------
+auto shared_tree::bytes() const noexcept -> std::size_t { return gcz::view_bytes(view(nodes, leaves, root)); }
+
+void shared_tree::serialize(std::ostream& os) const {
+  const auto v = view(nodes, leaves, root);
+  std::vector<std::uint8_t> buf(gcz::view_bytes(v));
+  gcz::view_serialize(v, buf.data(), buf.size());
+  os.write(reinterpret_cast<const char*>(buf.data()), std::streamsize(buf.size()));
+}
+
+auto shared_tree::deserialize(std::istream& is) -> shared_tree {
+  shared_tree result;
+  result.root = pointer::deserialize(is);
+  std::uint64_t size = 0;
+  auto read_u64 = [&](std::uint64_t& v) {
+    v = 0;
+    for (int i = 0; i < 8; ++i) {
+      const int c = is.get();
+      if (c == EOF) return false;
+      v = (v << 8) | std::uint64_t(c);
+    }
+    return true;
+  };
+  read_u64(size);
+  for (std::uint64_t i = 0; i < size; ++i) result.leaves.emplace_back(dna::deserialize(is));
+  while (read_u64(size)) {
+    result.nodes.emplace_back();
+    result.nodes.back().reserve(size);
+    for (std::uint64_t i = 0; i < size; ++i) result.nodes.back().emplace_back(node::deserialize(is));
+  }
+  return result;
+}
+
+void shared_tree::save(std::filesystem::path path) const {
+  std::ofstream file{path, std::ios::binary};
+  serialize(file);
+}
+
+// ---- iterator (:553-614) ----------------------------------------------------------------
+shared_tree::iterator::iterator(const shared_tree& parent, std::size_t layer, pointer root) : parent{parent} {
+  if (root) {
+    stack.emplace_back(layer, root);
+    next_leaf();
+  }
+}
+
+auto shared_tree::iterator::operator*() const noexcept -> dna { return parent.access_leaf(stack.back().current); }
+
+auto shared_tree::iterator::operator++() -> iterator& {
+  stack.pop_back();
+  next_leaf();
+  return *this;
+}
+
+void shared_tree::iterator::next_leaf() {
+  while (!stack.empty()) {
+    const auto st = stack.back();
+    if (st.layer == std::size_t(-1)) return;
+    const auto top = st.current;
+    const auto n = parent.access_node(st.layer, top);
+    stack.pop_back();
+    auto push = [&](pointer next) { stack.emplace_back(st.layer - 1, pointer{next, top.is_mirrored(), top.is_transposed()}); };
+    if (top.is_mirrored()) {
+      if (n.left()) push(n.left());
+      if (n.right()) push(n.right());
+    } else {
+      if (n.right()) push(n.right());
+      if (n.left()) push(n.left());
+    }
+  }
+}

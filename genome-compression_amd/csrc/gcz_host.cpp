@@ -20,10 +20,10 @@ namespace {
 // index (std::stable_sort in sort_leaves/sort_nodes, src/shared_tree.cpp:409-436).
 // Returns newpos[old] (invert_indices, :360-365).  Counting sort when the count
 // range is small, which it is for every real tree.
-std::vector<uint32_t> frequency_order(const std::vector<uint32_t>& parent, size_t n) {
+std::vector<uint32_t> frequency_order(const uint32_t* parent, size_t nwords, size_t n) {
   std::vector<uint32_t> cnt(n, 0);
-  for (uint32_t w : parent)                                  // histogram, :316-326
-    if (ul(w) != kNullIndex) ++cnt[w & kIndexMask];
+  for (size_t i = 0; i < nwords; ++i)                        // histogram, :316-326
+    if (ul(parent[i]) != kNullIndex) ++cnt[parent[i] & kIndexMask];
   uint32_t maxc = 0;
   for (uint32_t c : cnt) maxc = std::max(maxc, c);
   std::vector<uint32_t> newpos(n);
@@ -42,9 +42,9 @@ std::vector<uint32_t> frequency_order(const std::vector<uint32_t>& parent, size_
 }
 
 // rewire_nodes (src/shared_tree.cpp:383-403): new index, m/t/v bits kept, null untouched.
-void rewire(std::vector<uint32_t>& parent, const std::vector<uint32_t>& newpos) {
-  for (uint32_t& w : parent)
-    if (ul(w) != kNullIndex) w = (w & gcz::kFlagMask) | newpos[w & kIndexMask];
+void rewire(uint32_t* parent, size_t nwords, const std::vector<uint32_t>& newpos) {
+  for (size_t i = 0; i < nwords; ++i)
+    if (ul(parent[i]) != kNullIndex) parent[i] = (parent[i] & gcz::kFlagMask) | newpos[parent[i] & kIndexMask];
 }
 
 // Pointer compression (src/shared_tree.cpp:25-67,122-142).
@@ -75,6 +75,113 @@ uint8_t* put_ptr(uint8_t* o, uint32_t w) {                   // pointer::seriali
   return o;
 }
 
+
+}  // namespace
+
+namespace gcz {
+
+TreeView view_of(gcz_tree* t) {
+  TreeView v;
+  v.L = t->L;
+  v.leaves = t->leaves.data();
+  v.n_leaves = t->leaves.size();
+  for (auto& layer : t->layers) {
+    v.layer.push_back(layer.data());
+    v.layer_n.push_back(layer.size() / 2);
+  }
+  v.root = t->root;
+  return v;
+}
+
+// shared_tree::sort_tree (src/shared_tree.cpp:443-483).  The reference's two
+// std::async batches touch disjoint layers and a parent's reordering does not
+// change its children's counts, so the net effect is: leaves and node layers
+// 0..D-2 each permuted independently by their parent's histogram (the top
+// layer and the root are unchanged).  Layers are processed in parallel.
+void view_sort(TreeView& t) {
+  const size_t D = t.layer.size();
+  if (D == 0) return;
+  auto parent_words = [&](size_t c) { return std::vector<uint32_t>(t.layer[c], t.layer[c] + 2 * t.layer_n[c]); };
+  std::vector<std::vector<uint32_t>> perm(D);
+  {
+    std::vector<std::thread> th;
+    for (size_t c = 0; c < D; ++c) {
+      const size_t n = c == 0 ? t.n_leaves : t.layer_n[c - 1];
+      th.emplace_back([&, c, n] { perm[c] = frequency_order(t.layer[c], 2 * t.layer_n[c], n); });
+    }
+    for (auto& x : th) x.join();
+  }
+  (void)parent_words;
+  std::vector<std::thread> th;
+  th.emplace_back([&] {
+    std::vector<uint64_t> nl(t.leaves, t.leaves + t.n_leaves);
+    for (size_t i = 0; i < nl.size(); ++i) t.leaves[perm[0][i]] = nl[i];   // reorder_layer :371-377
+  });
+  for (size_t l = 0; l + 1 < D; ++l) {
+    th.emplace_back([&, l] {
+      const auto& np = perm[l + 1];
+      std::vector<uint32_t> w(t.layer[l], t.layer[l] + 2 * t.layer_n[l]);
+      for (size_t i = 0; i < np.size(); ++i) {
+        t.layer[l][2 * size_t(np[i])] = w[2 * i];
+        t.layer[l][2 * size_t(np[i]) + 1] = w[2 * i + 1];
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  th.clear();
+  for (size_t c = 0; c < D; ++c) th.emplace_back([&, c] { rewire(t.layer[c], 2 * t.layer_n[c], perm[c]); });
+  for (auto& x : th) x.join();
+}
+
+// shared_tree::bytes (src/shared_tree.cpp:488-496).
+uint64_t view_bytes(const TreeView& t) {
+  uint64_t b = ptr_bytes(t.root) + 8 + t.n_leaves * uint64_t((t.L + 1) / 2);
+  for (size_t l = 0; l < t.layer.size(); ++l) {
+    b += 8;
+    for (size_t i = 0; i < 2 * t.layer_n[l]; ++i) b += ptr_bytes(t.layer[l][i]);
+  }
+  return b;
+}
+
+// shared_tree::serialize (src/shared_tree.cpp:504-513).  0 when cap is too small.
+uint64_t view_serialize(const TreeView& t, uint8_t* buf, uint64_t cap) {
+  const uint64_t need = view_bytes(t);
+  if (cap < need) return 0;
+  uint8_t* o = put_ptr(buf, t.root);
+  o = put_be(o, t.n_leaves, 8);
+  const int lb = (t.L + 1) / 2;
+  for (size_t i = 0; i < t.n_leaves; ++i) o = put_be(o, t.leaves[i], lb);
+  for (size_t l = 0; l < t.layer.size(); ++l) {
+    o = put_be(o, t.layer_n[l], 8);
+    for (size_t i = 0; i < 2 * t.layer_n[l]; ++i) o = put_ptr(o, t.layer[l][i]);
+  }
+  return uint64_t(o - buf);
+}
+
+// shared_tree::width via children() (include/shared_tree.h:165,
+// src/shared_tree.cpp:252-259), bottom-up.
+uint64_t view_width(const TreeView& t) {
+  if (t.layer.empty()) return 0;
+  std::vector<uint64_t> below;
+  for (size_t l = 0; l < t.layer.size(); ++l) {
+    std::vector<uint64_t> cur(t.layer_n[l]);
+    for (size_t i = 0; i < cur.size(); ++i) {
+      uint64_t s = 0;
+      for (int c = 0; c < 2; ++c) {
+        const uint32_t w = t.layer[l][2 * i + c];
+        if (ul(w) == kNullIndex) continue;
+        s += l == 0 ? 1 : below[w & kIndexMask];
+      }
+      cur[i] = s;
+    }
+    below.swap(cur);
+  }
+  return ul(t.root) == kNullIndex ? 0 : below[t.root & kIndexMask];
+}
+
+}  // namespace gcz
+
+namespace {
 }  // namespace
 
 extern "C" {
@@ -93,93 +200,18 @@ const uint32_t* gcz_tree_layer(const gcz_tree* t, int k) {
   return (k >= 0 && size_t(k) < t->layers.size()) ? t->layers[k].data() : nullptr;
 }
 
-// shared_tree::sort_tree (src/shared_tree.cpp:443-483).  The reference's two
-// std::async batches touch disjoint layers and a parent's reordering does not
-// change its children's counts, so the net effect is: leaves and node layers
-// 0..D-2 each permuted independently by their parent's histogram (the top
-// layer and the root are unchanged).  Layers are processed in parallel.
 void gcz_tree_sort(gcz_tree* t) {
-  const size_t D = t->layers.size();
-  if (D == 0) return;
-  // permutation of child layer c (c = 0: leaves, c = l+1: node layer l) from parent
-  std::vector<std::vector<uint32_t>> perm(D);
-  {
-    std::vector<std::thread> th;
-    for (size_t c = 0; c < D; ++c) {
-      const size_t n = c == 0 ? t->leaves.size() : t->layers[c - 1].size() / 2;
-      th.emplace_back([&, c, n] { perm[c] = frequency_order(t->layers[c], n); });
-    }
-    for (auto& x : th) x.join();
-  }
-  std::vector<std::thread> th;
-  th.emplace_back([&] {
-    std::vector<uint64_t> nl(t->leaves.size());
-    for (size_t i = 0; i < nl.size(); ++i) nl[perm[0][i]] = t->leaves[i];   // reorder_layer :371-377
-    t->leaves.swap(nl);
-  });
-  for (size_t l = 0; l + 1 < D; ++l) {
-    th.emplace_back([&, l] {
-      const auto& np = perm[l + 1];
-      std::vector<uint32_t> w(t->layers[l].size());
-      for (size_t i = 0; i < np.size(); ++i) {
-        w[2 * size_t(np[i])] = t->layers[l][2 * i];
-        w[2 * size_t(np[i]) + 1] = t->layers[l][2 * i + 1];
-      }
-      t->layers[l].swap(w);
-    });
-  }
-  for (auto& x : th) x.join();
-  th.clear();
-  for (size_t c = 0; c < D; ++c) th.emplace_back([&, c] { rewire(t->layers[c], perm[c]); });
-  for (auto& x : th) x.join();
+  gcz::TreeView v = gcz::view_of(t);
+  gcz::view_sort(v);
 }
 
-// shared_tree::bytes (src/shared_tree.cpp:488-496).
-uint64_t gcz_tree_bytes(const gcz_tree* t) {
-  uint64_t b = ptr_bytes(t->root) + 8 + t->leaves.size() * uint64_t((t->L + 1) / 2);
-  for (const auto& layer : t->layers) {
-    b += 8;
-    for (uint32_t w : layer) b += ptr_bytes(w);
-  }
-  return b;
-}
+uint64_t gcz_tree_bytes(const gcz_tree* t) { return gcz::view_bytes(gcz::view_of(const_cast<gcz_tree*>(t))); }
 
-// shared_tree::serialize (src/shared_tree.cpp:504-513).  0 when cap is too small.
 uint64_t gcz_tree_serialize(const gcz_tree* t, uint8_t* buf, uint64_t cap) {
-  const uint64_t need = gcz_tree_bytes(t);
-  if (cap < need) return 0;
-  uint8_t* o = put_ptr(buf, t->root);
-  o = put_be(o, t->leaves.size(), 8);
-  const int lb = (t->L + 1) / 2;
-  for (uint64_t v : t->leaves) o = put_be(o, v, lb);
-  for (const auto& layer : t->layers) {
-    o = put_be(o, layer.size() / 2, 8);
-    for (uint32_t w : layer) o = put_ptr(o, w);
-  }
-  return uint64_t(o - buf);
+  return gcz::view_serialize(gcz::view_of(const_cast<gcz_tree*>(t)), buf, cap);
 }
 
-// shared_tree::width via children() (include/shared_tree.h:165,
-// src/shared_tree.cpp:252-259), bottom-up.
-uint64_t gcz_tree_width(const gcz_tree* t) {
-  if (t->layers.empty()) return 0;
-  std::vector<uint64_t> below;
-  for (size_t l = 0; l < t->layers.size(); ++l) {
-    const auto& layer = t->layers[l];
-    std::vector<uint64_t> cur(layer.size() / 2);
-    for (size_t i = 0; i < cur.size(); ++i) {
-      uint64_t s = 0;
-      for (int c = 0; c < 2; ++c) {
-        const uint32_t w = layer[2 * i + c];
-        if (ul(w) == kNullIndex) continue;
-        s += l == 0 ? 1 : below[w & kIndexMask];
-      }
-      cur[i] = s;
-    }
-    below.swap(cur);
-  }
-  return ul(t->root) == kNullIndex ? 0 : below[t->root & kIndexMask];
-}
+uint64_t gcz_tree_width(const gcz_tree* t) { return gcz::view_width(gcz::view_of(const_cast<gcz_tree*>(t))); }
 
 void gcz_tree_set_leaves(gcz_tree* t, int L, const uint64_t* leaves, uint64_t n) {
   t->L = L;

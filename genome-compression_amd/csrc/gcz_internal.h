@@ -1,6 +1,7 @@
 // Internal definitions shared by the libgcz translation units.
 #pragma once
 
+#include <cstddef>
 #include <cstdint>
 #include <vector>
 
@@ -16,6 +17,23 @@ constexpr uint32_t kFlagMask = 0xe0000000u;
 
 inline uint32_t ul(uint32_t w) { return w & 0x7fffffffu; }   // pointer::to_ulong, :103-107
 
+}  // namespace gcz
+
+namespace gcz {
+// Raw view of a shared tree (used by both the C ABI's gcz_tree and the C++
+// shared_tree): leaves, per-layer node words (2 per node), root.
+struct TreeView {
+  int L = 12;
+  uint64_t* leaves = nullptr;
+  size_t n_leaves = 0;
+  std::vector<uint32_t*> layer;
+  std::vector<size_t> layer_n;
+  uint32_t root = kNullWord;
+};
+void view_sort(TreeView& t);
+uint64_t view_bytes(const TreeView& t);
+uint64_t view_serialize(const TreeView& t, uint8_t* buf, uint64_t cap);
+uint64_t view_width(const TreeView& t);
 }  // namespace gcz
 
 // Host-resident shared tree: the three members of the reference's shared_tree

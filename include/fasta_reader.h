@@ -1,0 +1,52 @@
+/*
+ * fasta_reader.h — FASTA ingest of the shared_tree construction.
+ *
+ * Drop-in for the reference's include/fasta_reader.h (same names, same
+ * line contract, src/fasta_reader.cpp:40-68): at each line start a '>' or an
+ * empty line skips ONE line, the following line is read as data; data line
+ * bodies are concatenated; the tail beyond a multiple of dna::size() is
+ * dropped unvalidated; an unknown symbol prints the reference's message and
+ * exits(1).  read_into() hands out consecutive buffers of buffer_size strands.
+ *
+ * shared_tree{path} / shared_tree{fasta_reader} do NOT go through these
+ * buffers: they hand the raw file to libgcz, which applies the same contract
+ * on the host and packs the strands on the GPU.
+ * Implementation: genome-compression_amd/csrc/cxx/fasta_reader.cpp.
+ */
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <filesystem>
+#include <vector>
+
+#include "dna.h"
+
+class fasta_reader {
+ public:
+  using value_type = dna;
+
+  fasta_reader(std::filesystem::path path, std::size_t buffer_size = (1 << 22));
+  fasta_reader(const fasta_reader&) = delete;
+  fasta_reader(fasta_reader&&) noexcept = default;
+
+  auto eof() const -> bool { return next >= strands; }
+  auto read_into(std::vector<dna>& vector) -> bool;
+  auto size() const -> std::size_t;      // file size in bytes (upper bound on bases)
+  auto buffers() const -> std::size_t;   // approximate number of buffers
+  auto path() const -> const std::filesystem::path& { return file_path; }
+
+  // Raw file bytes and the concatenated bases (FASTA contract applied).
+  auto raw() const -> const std::vector<std::uint8_t>& { return bytes; }
+  auto bases() const -> const std::vector<std::uint8_t>& { return seq; }
+
+ private:
+  std::filesystem::path file_path;
+  std::size_t buffer_size;
+  std::vector<std::uint8_t> bytes;
+  std::vector<std::uint8_t> seq;
+  std::size_t strands = 0;
+  std::size_t next = 0;
+};
+
+auto read_genome(const std::filesystem::path path) -> std::vector<dna>;

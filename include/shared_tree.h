@@ -1,0 +1,223 @@
+/*
+ * shared_tree.h — balanced shared tree (node DAG) built on MI355X.
+ *
+ * Drop-in for the reference's include/shared_tree.h.  Same classes, names,
+ * member functions and semantics:
+ *   pointer   29-bit index + mirror/transpose/invariant bits (:36-77); the
+ *             in-memory word layout bits 0-28 / 29 / 30 / 31 is also libgcz's
+ *   node      two pointers (:99-134)
+ *   shared_tree  constructors, accessors, frequency sort, bytes/serialize/
+ *             deserialize/save, DFS iterator (:154-237)
+ * The construction engine (the reference's tree_constructor, :245-316) is
+ * replaced by the libgcz HIP build (include/gcz.h): the constructors hand the
+ * genome to the GPU and copy the finished DAG back into the containers.
+ *
+ * Device selection: GCZ_DEVICE (default 0).  Errors behave like the
+ * reference: an unknown nucleotide prints "Encountered unknown symbol: ..."
+ * and exits(1); a device failure prints the libgcz error and exits(1).
+ * Implementation: genome-compression_amd/csrc/cxx/shared_tree.cpp.
+ */
+#pragma once
+
+#include <array>
+#include <cassert>
+#include <cstddef>
+#include <cstdint>
+#include <filesystem>
+#include <iostream>
+#include <tuple>
+#include <vector>
+
+#include "dna.h"
+#include "fasta_reader.h"
+
+class pointer {
+ public:
+  static constexpr auto address_bits = std::array{4, 12, 20, 28};
+
+  pointer(std::nullptr_t = nullptr) noexcept : word{0x9fffffffu} {}
+  pointer(const pointer& other, bool mirror = false, bool transpose = false) noexcept;
+  pointer(std::size_t index, bool mirror, bool transpose, bool invariant) noexcept
+      : word{std::uint32_t(index) | (std::uint32_t(mirror && !invariant) << 29) | (std::uint32_t(transpose) << 30) |
+             (std::uint32_t(invariant) << 31)} {}
+  pointer(pointer&&) noexcept = default;
+  pointer& operator=(const pointer&) noexcept = default;
+  pointer& operator=(pointer&&) noexcept = default;
+
+  static auto from_word(std::uint32_t w) noexcept -> pointer {
+    pointer p;
+    p.word = w;
+    return p;
+  }
+  auto raw() const noexcept -> std::uint32_t { return word; }
+
+  bool empty() const noexcept { return *this == nullptr; }
+  auto canonical() const noexcept { return word & 0x1fffffffu; }
+  auto index() const noexcept -> std::size_t {
+    assert(!empty());
+    return word & 0x1fffffffu;
+  }
+
+  bool operator==(const pointer& o) const noexcept { return to_ulong() == o.to_ulong(); }
+  bool operator!=(const pointer& o) const noexcept { return to_ulong() != o.to_ulong(); }
+  bool operator<(const pointer& o) const noexcept { return to_ulong() < o.to_ulong(); }
+  auto to_ulong() const noexcept -> unsigned long { return word & 0x7fffffffu; }
+  operator bool() const noexcept { return *this != nullptr; }
+
+  auto bytes() const noexcept -> std::size_t;
+  void serialize(std::ostream& os) const;
+  static auto deserialize(std::istream& is) -> pointer;
+
+  bool is_mirrored() const noexcept { return (word >> 29) & 1u; }
+  bool is_transposed() const noexcept { return (word >> 30) & 1u; }
+  bool is_inverted() const noexcept { return is_mirrored() && is_transposed(); }
+  bool is_invariant() const noexcept { return word >> 31; }
+
+  auto mirrored() const noexcept { return pointer{*this, true, false}; }
+  auto transposed() const noexcept { return pointer{*this, false, true}; }
+  auto inverted() const noexcept { return pointer{*this, true, true}; }
+
+ private:
+  std::uint32_t word;
+};
+static_assert(sizeof(pointer) == 4, "pointer is one 32-bit word");
+
+inline auto& operator<<(std::ostream& os, const pointer& p) {
+  if (p.empty()) return os << "empty";
+  return os << '(' << p.index() << ": " << p.is_mirrored() << p.is_transposed() << p.is_invariant() << ')';
+}
+
+namespace std {
+template <>
+struct hash<pointer> {
+  auto operator()(const pointer& p) const noexcept -> std::size_t {
+    std::uint64_t x = p.to_ulong() * 0x9E3779B97F4A7C15ull;
+    return std::size_t(x ^ (x >> 29));
+  }
+};
+}  // namespace std
+
+class node {
+ public:
+  node(pointer left, pointer right = nullptr) : children{left, right} {}
+  node(const node&) noexcept = default;
+  node(node&&) noexcept = default;
+  node& operator=(const node&) noexcept = default;
+  node& operator=(node&&) noexcept = default;
+
+  bool operator==(const node& o) const noexcept { return children == o.children; }
+  bool operator!=(const node& o) const noexcept { return !(*this == o); }
+  bool operator<(const node& o) const noexcept { return children < o.children; }
+
+  auto left() const noexcept { return children[0]; }
+  auto right() const noexcept { return children[1]; }
+
+  auto mirrored() const noexcept { return node{children[1].mirrored(), children[0].mirrored()}; }
+  auto transposed() const noexcept { return node{children[0].transposed(), children[1].transposed()}; }
+  auto inverted() const noexcept { return node{children[1].inverted(), children[0].inverted()}; }
+  auto canonical() const noexcept -> std::tuple<node, bool, bool>;
+
+  auto bytes() const noexcept { return left().bytes() + right().bytes(); }
+  void serialize(std::ostream& os) const;
+  static auto deserialize(std::istream& is) -> node;
+
+ private:
+  std::array<pointer, 2> children;
+};
+static_assert(sizeof(node) == 8, "node is two 32-bit words");
+
+inline auto& operator<<(std::ostream& os, const node& n) {
+  return os << "node<" << n.left() << ", " << n.right() << '>';
+}
+
+namespace std {
+template <>
+struct hash<node> {
+  auto operator()(const node& n) const noexcept -> std::size_t {
+    auto h = std::hash<pointer>();
+    return 5 * h(n.left()) + 3 * h(n.right());
+  }
+};
+}  // namespace std
+
+class shared_tree {
+ public:
+  shared_tree() = default;
+  shared_tree(std::filesystem::path path) : shared_tree{fasta_reader{path}} {}
+  shared_tree(fasta_reader file, bool verbose = false);
+  shared_tree(std::vector<dna>& data, bool verbose = false);
+
+  auto depth() const { return nodes.size() + 1; }
+  auto width() const -> std::size_t;
+
+  auto children(std::size_t layer, pointer p) const -> std::size_t;
+  auto node_count() const -> std::size_t;
+  auto node_count(std::size_t layer) const { return nodes[layer].size(); }
+  auto leaf_count() const noexcept { return leaves.size(); }
+
+  auto access_leaf(pointer p) const -> dna;
+  auto access_node(std::size_t layer, pointer p) const -> node { return nodes[layer][p.index()]; }
+  auto operator[](std::uint64_t index) const -> dna;
+
+  void add_layer() { nodes.emplace_back(); }
+  void emplace_node(std::size_t layer, node n) { nodes[layer].emplace_back(n); }
+  void emplace_leaf(dna leaf) { leaves.emplace_back(leaf); }
+
+  auto histogram(std::size_t layer) const -> std::vector<std::size_t>;
+  void store_histogram(std::filesystem::path) const;
+
+  void rewire_nodes(std::size_t layer, const std::vector<std::size_t>& indices);
+  void sort_leaves();
+  void sort_nodes(std::size_t layer);
+  void sort_tree(bool verbose = false);
+
+  auto bytes() const noexcept -> std::size_t;
+  void serialize(std::ostream& os) const;
+  static auto deserialize(std::istream& is) -> shared_tree;
+  void save(std::filesystem::path) const;
+
+  auto root_pointer() const noexcept -> pointer { return root; }
+
+  friend inline auto operator<<(std::ostream& os, const shared_tree& tree) -> std::ostream&;
+
+  struct iterator {
+    struct status {
+      status(std::size_t layer, pointer current) : layer{layer}, current{current} {}
+      std::size_t layer;  // leaf level is the maximum std::size_t value
+      pointer current;
+    };
+
+    iterator(const shared_tree& nodes, std::size_t layer, pointer root);
+
+    auto operator*() const noexcept -> dna;
+    auto operator++() -> iterator&;
+    auto operator!=(const iterator&) const { return !stack.empty(); }
+    void next_leaf();
+
+    const shared_tree& parent;
+    std::vector<status> stack;
+  };
+  using const_iterator = iterator;
+
+  auto begin() const { return iterator{*this, nodes.size() - 1, root}; }
+  auto end() const { return iterator{*this, 0, nullptr}; }
+
+ private:
+  void build_from_gpu();   // copies the last libgcz build of this thread into the containers
+
+  std::vector<std::vector<node>> nodes;
+  std::vector<dna> leaves;
+  pointer root;
+};
+
+inline auto operator<<(std::ostream& os, const shared_tree& tree) -> std::ostream& {
+  os << "Leaves (" << tree.leaves.size() << "):";
+  for (const auto& leaf : tree.leaves) os << ' ' << leaf;
+  os << '\n';
+  for (const auto& layer : tree.nodes) {
+    os << "Layer (" << layer.size() << "):";
+    for (const auto& n : layer) os << ' ' << n;
+    os << '\n';
+  }
+  return os;
+}

@@ -1,0 +1,163 @@
+// C++ drop-in surface tests (include/dna.h, fasta_reader.h, shared_tree.h).
+// Mirrors the behaviours the reference's own tests pin (tests/test.cpp:33-409):
+// symmetry ops, pointer bits, FASTA reading, canonical invariance, round-trip
+// decompression after build / sort / (de)serialization.
+//
+// usage: test_dropin <golden-dir> [gpu]
+//   without "gpu" only host-side groups run (no device needed)
+#include <cstdio>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "dna.h"
+#include "fasta_reader.h"
+#include "shared_tree.h"
+
+static int failures = 0;
+#define CHECK(cond, msg)                                                   \
+  do {                                                                     \
+    if (!(cond)) {                                                         \
+      ++failures;                                                          \
+      std::cout << "FAIL " << __func__ << ": " << msg << '\n';             \
+    }                                                                      \
+  } while (0)
+
+static std::string dir;
+
+static void dna_ops() {
+  const dna a{std::string_view{"AAAAAAAAAAAA"}};
+  const dna t{std::string_view{"TTTTTTTTTTTT"}};
+  CHECK(a.transposed() == t, "A transposes to T");
+  const dna p{std::string_view{"ACTGACTGACTG"}};
+  const dna q{std::string_view{"GTCAGTCAGTCA"}};
+  CHECK(p.mirrored() == q, "mirror reverses");
+  CHECK(p.inverted() == p.transposed().mirrored(), "inverted = mirrored(transposed)");
+  const dna pal{std::string_view{"ACGTTAATTGCA"}};
+  CHECK(pal.invariant(), "palindrome is mirror invariant");
+  std::ostringstream os;
+  os << dna{std::string_view{"acgtrykmbvdh"}};
+  CHECK(os.str() == "ACGTRYKMBVDH", "case-insensitive parse + print: " << os.str());
+  // canonical is the minimum over the four variants
+  const auto [c, m, tr, inv] = p.canonical();
+  CHECK(!(p.transposed() < c) && !(p.mirrored() < c) && !(p.inverted() < c) && !(p < c), "canonical is min");
+  (void)m; (void)tr; (void)inv;
+  std::stringstream ss;
+  p.serialize(ss);
+  CHECK(dna::deserialize(ss) == p, "dna serialize round trip");
+}
+
+static void pointer_ops() {
+  const pointer basis{3280, false, false, false};
+  CHECK(basis != basis.transposed(), "transposed non-null pointer differs");
+  CHECK(basis != basis.mirrored(), "mirrored non-invariant pointer differs");
+  CHECK(basis.index() == 3280, "index round trip");
+  const pointer inv{7, true, false, true};
+  CHECK(!inv.is_mirrored(), "mirror bit cleared for invariant pointers");
+  CHECK(inv.mirrored() == inv, "invariant pointer is its own mirror");
+  const pointer null{};
+  CHECK(null.empty() && null.transposed().empty() && null.inverted().empty(), "null stays null");
+  for (std::size_t idx : {0ul, 15ul, 16ul, 4111ul, 4112ul, 1052687ul, 1052688ul, 123456789ul}) {
+    const pointer p{idx, bool(idx & 1), bool(idx & 2), false};
+    std::stringstream ss;
+    p.serialize(ss);
+    CHECK(std::size_t(ss.str().size()) == p.bytes(), "bytes() = serialized size");
+    CHECK(pointer::deserialize(ss) == p, "pointer round trip " << idx);
+  }
+  std::stringstream ss;
+  null.serialize(ss);
+  CHECK(pointer::deserialize(ss).empty(), "null round trip");
+}
+
+static void canonical_invariance() {
+  const pointer l{0, false, false, false}, r{1, true, false, false};
+  const auto a = std::get<0>(node{l, r}.canonical());
+  CHECK(a == std::get<0>(a.mirrored().canonical()), "mirror");
+  CHECK(a == std::get<0>(a.transposed().canonical()), "transpose");
+  CHECK(a == std::get<0>(a.inverted().canonical()), "invert");
+}
+
+static void file_reader() {
+  // multi-line file with blank lines reads like the single-line original
+  fasta_reader edited{dir + "/data/edited"};
+  std::ifstream f(dir + "/data/chmpxx", std::ios::binary);
+  std::string direct((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  std::vector<dna> buf;
+  std::size_t i = 0;
+  bool same = true;
+  while (edited.read_into(buf))
+    for (const auto& b : buf) {
+      same &= b == dna{std::string_view{&direct[i * dna::size()], dna::size()}};
+      ++i;
+    }
+  CHECK(same, "edited == chmpxx strand by strand");
+  CHECK(i == direct.size() / dna::size(), "strand count " << i);
+  CHECK(read_genome(dir + "/data/chmpxx").size() == i, "read_genome");
+}
+
+template <class T>
+static bool same_sequence(const shared_tree& tree, const T& data) {
+  std::size_t i = 0;
+  bool ok = true;
+  for (auto it = tree.begin(); it != tree.end(); ++it) ok &= i < data.size() && *it == data[i++];
+  for (std::size_t k = 0; k < data.size() && ok; k += 97) ok &= tree[k] == data[k];
+  return ok && i == data.size();
+}
+
+static void gpu_transposition() {
+  const auto a = dna::random(0);
+  const auto t = a.transposed();
+  std::vector<dna> data{a, a, t, a, a, t, t, t};
+  shared_tree tree{data};
+  CHECK(tree.width() == data.size(), "width");
+  CHECK(tree.leaf_count() == 1, "a and its transpose share one leaf");
+  CHECK(same_sequence(tree, data), "decompression");
+}
+
+static void gpu_frequency_sort() {
+  const auto a = dna::random(1), b = dna::random(2), c = dna::random(3);
+  std::vector<dna> data;
+  for (char x : std::string("bbbacbacbabacacacabcaaaaaaaaaaaaaa")) data.push_back(x == 'a' ? a : x == 'b' ? b : c);
+  shared_tree tree{data};
+  shared_tree old = tree;
+  tree.sort_tree();
+  CHECK(same_sequence(tree, data) && same_sequence(old, data), "sort keeps the sequence");
+}
+
+static void gpu_file_build() {
+  const auto data = read_genome(dir + "/data/chmpxx");
+  shared_tree from_vector{const_cast<std::vector<dna>&>(data)};
+  shared_tree from_file{std::filesystem::path{dir + "/data/chmpxx"}};
+  CHECK(from_vector.width() == data.size(), "width");
+  CHECK(same_sequence(from_file, data), "file build decompresses");
+  CHECK(same_sequence(from_vector, data), "vector build decompresses");
+  std::stringstream a, b;
+  from_vector.serialize(a);
+  from_file.serialize(b);
+  CHECK(a.str() == b.str(), "file and vector builds serialize identically");
+  from_file.sort_tree();
+  CHECK(from_file.bytes() == 104990, "sorted bytes() = reference 104990, got " << from_file.bytes());
+  std::stringstream s;
+  from_file.serialize(s);
+  auto load = shared_tree::deserialize(s);
+  CHECK(load.width() == from_file.width() && load.leaf_count() == from_file.leaf_count(), "deserialize dims");
+  CHECK(same_sequence(load, data), "deserialized tree decompresses");
+}
+
+int main(int argc, char** argv) {
+  dir = argc > 1 ? argv[1] : "tests/golden";
+  const bool gpu = argc > 2 && std::string(argv[2]) == "gpu";
+  dna_ops();
+  pointer_ops();
+  canonical_invariance();
+  file_reader();
+  if (gpu) {
+    gpu_transposition();
+    gpu_frequency_sort();
+    gpu_file_build();
+  }
+  std::cout << (failures ? "FAILED " : "OK ") << failures << '\n';
+  return failures ? 1 : 0;
+}
