@@ -1,180 +1,12 @@
 // MI355X (gfx950) shared_tree construction: host orchestration and the C ABI.
-// Device code and the algorithm description: gcz_device.h.
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <string>
-#include <vector>
-
-#include "gcz_device.h"
-
-namespace {
+// Device code and the algorithm description: gcz_device.h; the multi-rank
+// build: gcz_dist.hip.
+#include "gcz_ctx.h"
 
 using namespace gcz_dev;
+using namespace gcz_host;
 
-// ---- host side -----------------------------------------------------------------
-
-#define HIP_TRY(x)                                                          \
-  do {                                                                      \
-    hipError_t e_ = (x);                                                    \
-    if (e_ != hipSuccess) return fail(GCZ_ERR_DEVICE, #x, hipGetErrorString(e_)); \
-  } while (0)
-
-u64 next_pow2(u64 x) {
-  u64 p = 1;
-  while (p < x) p <<= 1;
-  return p;
-}
-
-struct DevBuf {
-  void* ptr = nullptr;
-  size_t bytes = 0;
-};
-
-u64 inv64(u64 a) {                 // inverse of an odd number mod 2^64 (Newton)
-  u64 x = a;
-  for (int i = 0; i < 6; ++i) x *= 2 - a * x;
-  return x;
-}
-
-u32 bit_width(u64 x) {
-  u32 b = 0;
-  while (x) { ++b; x >>= 1; }
-  return b;
-}
-
-u32 log2_exact(u64 x) { return bit_width(x) - 1; }
-
-constexpr u32 kAdaptiveProbeLimit = 256;
-constexpr u64 kMixC1 = 0x9E3779B97F4A7C15ull;
-constexpr u64 kMixC2 = 0xD6E8FEB86659FD93ull;
-
-// A level's table: packed 8-B words when quotient+displacement+position fit
-// in 64 bits, else 16-B wide slots.
-struct LevelTab {
-  bool packed = false;
-  PackedTab pt{};
-  WideTab wt{};
-  u64 cap = 0;
-  u64 bytes() const { return cap * (packed ? 8 : 16); }
-};
-
-LevelTab plan_table(void* buf, u64 cap, u32 K, u64 npos, u32 B, bool allow_packed, u32 wide_limit) {
-  LevelTab lt;
-  lt.cap = cap;
-  const u32 c = log2_exact(cap);
-  const u32 Q = K > c ? K - c : 0;
-  const u32 P = std::max<u32>(1, bit_width(npos - 1));
-  const int room = 64 - int(Q) - int(P);
-  if (allow_packed && K <= 64 && room >= 6) {
-    lt.packed = true;
-    PackedTab& t = lt.pt;
-    t.tab = static_cast<u64*>(buf);
-    t.mask = u32(cap - 1);
-    t.D = u32(std::min(room, 8));
-    t.limit = (1u << t.D) - 2;
-    t.B = B;
-    t.c = c;
-    t.P = P;
-    t.sh = (K + 1) / 2;
-    t.kmask = K >= 64 ? ~0ull : ((1ull << K) - 1);
-    t.c1 = kMixC1; t.c2 = kMixC2;
-    t.c1i = inv64(kMixC1); t.c2i = inv64(kMixC2);
-  } else {
-    lt.wt.tab = static_cast<Slot*>(buf);
-    lt.wt.mask = u32(cap - 1);
-    lt.wt.limit = wide_limit;
-    lt.wt.B = B;
-  }
-  return lt;
-}
-
-enum KernelId {
-  KID_LEAF, KID_NODE, KID_FLAGSCAN_LEAF, KID_FLAGSCAN_NODE, KID_RESOLVE_LEAF, KID_RESOLVE_NODE, KID_MEMSET, KID_COUNT
-};
-const char* kKernelNames[KID_COUNT] = {"leaf_insert", "node_insert", "flagscan_leaf", "flagscan_node",
-                                       "resolve_leaf", "resolve_node", "clear"};
-
-}  // namespace
-
-struct gcz_ctx {
-  int device = 0;
-  hipStream_t own_stream = nullptr;
-  hipStream_t stream = nullptr;
-  std::string last_error;
-  DevBuf wa, wb, grp, desc, tab, leaves_out, nodes_out, hdr, input, nf, multi;
-  Header* h_hdr = nullptr;   // pinned
-  // last build
-  gcz_info info{};
-  std::vector<u64> layer_off;  // node offsets (in nodes) per layer within nodes_out
-  u64 leaf_cap_hint = 0;
-  // profiling
-  bool profile = false;
-  bool force_wide = false;   // GCZ_TABLE=wide: always use 16-B slots (testing)
-  int node_cap_shift = 1;    // node table capacity = next_pow2(p << shift)   (GCZ_NODE_CAP_SHIFT)
-  int leaf_cap_log2 = 0;     // force the adaptive leaf table size            (GCZ_LEAF_CAP_LOG2)
-  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
-  std::vector<hipEvent_t> event_pool;
-  size_t event_used = 0;
-  u64 prof_launches[KID_COUNT] = {};
-  double prof_ms[KID_COUNT] = {};
-  hipEvent_t ev_start = nullptr, ev_stop = nullptr;
-
-  int fail(int code, const char* what, const char* detail) {
-    last_error = std::string(what) + ": " + detail;
-    info.status = code;
-    return code;
-  }
-
-  int ensure(DevBuf& b, size_t bytes) {
-    if (b.bytes >= bytes && b.ptr) return GCZ_OK;
-    if (b.ptr) {
-      HIP_TRY(hipStreamSynchronize(stream));
-      HIP_TRY(hipFree(b.ptr));
-      b.ptr = nullptr; b.bytes = 0;
-    }
-    HIP_TRY(hipMalloc(&b.ptr, bytes));
-    b.bytes = bytes;
-    return GCZ_OK;
-  }
-
-  hipEvent_t next_event() {
-    if (event_used == event_pool.size()) {
-      hipEvent_t e;
-      (void)hipEventCreate(&e);
-      event_pool.push_back(e);
-    }
-    return event_pool[event_used++];
-  }
-
-  void prof_begin(int kid, hipEvent_t& a) {
-    if (!profile) return;
-    a = next_event();
-    (void)hipEventRecord(a, stream);
-    (void)kid;
-  }
-  void prof_end(int kid, hipEvent_t a) {
-    if (!profile) return;
-    hipEvent_t b = next_event();
-    (void)hipEventRecord(b, stream);
-    pending.push_back({kid, {a, b}});
-  }
-  void prof_collect() {
-    for (auto& pe : pending) {
-      float ms = 0.f;
-      (void)hipEventElapsedTime(&ms, pe.second.first, pe.second.second);
-      prof_ms[pe.first] += ms;
-      prof_launches[pe.first] += 1;
-    }
-    pending.clear();
-    event_used = 0;
-  }
-
-  int build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, int L);
-};
+void gcz_dist_state_free(gcz_ctx* c);   // gcz_dist.hip
 
 namespace {
 
@@ -192,6 +24,145 @@ void launch_leaf_bases(int L, dim3 g, hipStream_t st, const unsigned char* b, u6
 }
 
 }  // namespace
+
+// leaf chunks, geometric: S/64, S/64, S/32, ... S/2 (multiples of the leaf tile);
+// the first small chunks discover most keys, the big later ones mostly hit
+// settled slots.  Small inputs are one chunk.
+std::vector<u64> gcz_host::leaf_chunks(u64 S) {
+  std::vector<u64> chunk_start{0};
+  const u64 tile = kLeafTile;
+  u64 next = std::max<u64>(tile, (S / 64 + tile - 1) / tile * tile);
+  if (S <= (1ull << 21)) next = S;
+  bool first = true;
+  while (chunk_start.back() < S && int(chunk_start.size()) < kMaxChunks) {
+    const u64 c0 = chunk_start.back();
+    u64 c1 = std::min(S, c0 + next);
+    if (S - c1 < tile) c1 = S;
+    chunk_start.push_back(c1);
+    if (!first) next *= 2;
+    first = false;
+  }
+  chunk_start.back() = S;
+  if (chunk_start.size() == 1) chunk_start.push_back(S);   // S == 0: one empty chunk
+  return chunk_start;
+}
+
+int gcz_ctx::ensure_marks(u64 S) {
+  const u64 full_b = (S + 16 + 255) / 256 * 256, half = ((S + 1) / 2 + 16 + 255) / 256 * 256;
+  if (int rc = ensure(nf, full_b + half)) return rc;       // [leaf / even layers: S][odd layers: S/2]
+  if (int rc = ensure(multi, 2 * half)) return rc;         // [even layers][odd layers]
+  nf_set[0] = nf.as<unsigned char>();
+  nf_set[1] = nf.as<unsigned char>() + full_b;
+  multi_set[0] = multi.as<unsigned char>();
+  multi_set[1] = multi.as<unsigned char>() + half;
+  return GCZ_OK;
+}
+
+int gcz_ctx::leaf_level(const LeafLevel& a, Header* d_hdr) {
+  if (a.S == 0) return GCZ_OK;
+  const u32 limit = a.adaptive ? kAdaptiveProbeLimit : kMaxProbe;
+  const int L = a.L;
+  // packed leaves only from bases (< 2^4L by construction); user leaves may carry any bits.
+  // Chunked settling needs one spare bit in the packed word, hence K + 1.
+  LevelTab lt = plan_table(tab.ptr, a.cap, a.bases ? 4 * u32(L) + 1 : 64, a.S, 0, allow_packed && a.bases, limit);
+  if (lt.packed) {
+    lt.pt.limit = std::min(lt.pt.limit, limit);
+    lt.pt.kmask >>= 1;                   // the key itself has 4L bits
+    lt.pt.sh = (4 * u32(L) + 1) / 2;
+  }
+  unsigned char* d_nf = nf_set[0];
+  hipEvent_t e0{};
+  prof_begin(KID_MEMSET, e0);
+  HIP_TRY(hipMemsetAsync(tab.ptr, 0xff, lt.bytes(), stream));
+  HIP_TRY(hipMemsetAsync(d_nf, 0, a.S, stream));
+  prof_end(KID_MEMSET, e0);
+  u32* A = a.words;
+  const int C = int(a.chunk_start.size()) - 1;
+  for (int c = 0; c < C; ++c) {
+    const u64 i0 = a.chunk_start[c], i1 = a.chunk_start[c + 1];
+    const dim3 g(unsigned((i1 - i0 + kBlock - 1) / kBlock));
+    prof_begin(KID_LEAF, e0);
+    if (a.bases) {
+      const auto* b = static_cast<const unsigned char*>(a.bases);
+      if (lt.packed) launch_leaf_bases(L, g, stream, b, i0, i1, lt.pt, A, d_nf, d_hdr);
+      else launch_leaf_bases(L, g, stream, b, i0, i1, lt.wt, A, d_nf, d_hdr);
+    } else {
+      hipLaunchKernelGGL((k_leaf_packed<WideTab>), g, dim3(kBlock), 0, stream, a.leaves, i0, i1, L, lt.wt, A,
+                         d_nf, d_hdr);
+    }
+    HIP_TRY(hipGetLastError());
+    prof_end(KID_LEAF, e0);
+    const dim3 gs(unsigned((i1 - i0 + kLeafTile - 1) / kLeafTile));
+    const u64* id0 = c == 0 ? nullptr : &a.count[c - 1];
+    prof_begin(KID_FLAGSCAN_LEAF, e0);
+    if (lt.packed)
+      hipLaunchKernelGGL((k_flagscan_leaf<PackedTab>), gs, dim3(kBlock), 0, stream, A, i0, i1, lt.pt, d_nf,
+                         a.desc + a.desc_off[c], &a.ticket[c], a.out, id0, &a.count[c]);
+    else
+      hipLaunchKernelGGL((k_flagscan_leaf<WideTab>), gs, dim3(kBlock), 0, stream, A, i0, i1, lt.wt, d_nf,
+                         a.desc + a.desc_off[c], &a.ticket[c], a.out, id0, &a.count[c]);
+    HIP_TRY(hipGetLastError());
+    prof_end(KID_FLAGSCAN_LEAF, e0);
+    prof_begin(KID_RESOLVE_LEAF, e0);
+    if (lt.packed)
+      hipLaunchKernelGGL((k_resolve_leaf<PackedTab>), g, dim3(kBlock), 0, stream, A, i0, i1, lt.pt, d_nf);
+    else
+      hipLaunchKernelGGL((k_resolve_leaf<WideTab>), g, dim3(kBlock), 0, stream, A, i0, i1, lt.wt, d_nf);
+    HIP_TRY(hipGetLastError());
+    prof_end(KID_RESOLVE_LEAF, e0);
+  }
+  return GCZ_OK;
+}
+
+int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
+  const u64 p = a.p, n = a.n;
+  if (p == 0) return GCZ_OK;
+  const u64 cap = node_cap(p);
+  const u32 Bk = std::max<u32>(1, bit_width(a.bound));
+  const LevelTab nt = plan_table(tab.ptr, cap, 2 * (Bk + 3), p, Bk, allow_packed, kMaxProbe);
+  const int cur = (a.k + 1) & 1, prev = a.k & 1;
+  unsigned char* knf = nf_set[cur];
+  const Marks mk{knf, multi_set[cur]};
+  const unsigned char* pnf = a.prev_marks ? nf_set[prev] : nullptr;
+  const unsigned char* pmu = a.prev_marks ? multi_set[prev] : nullptr;
+  Group* d_grp = grp.as<Group>();
+  hipEvent_t e0{};
+  prof_begin(KID_MEMSET, e0);
+  {
+    const u64 tab16 = nt.bytes() / 16, p16 = (p + 15) / 16;
+    const u64 blocks = std::min<u64>(4096, (std::max(tab16, p16) + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_clear, dim3(unsigned(blocks)), dim3(kBlock), 0, stream, static_cast<uint4*>(tab.ptr),
+                       tab16, reinterpret_cast<uint4*>(knf), reinterpret_cast<uint4*>(mk.multi), p16, a.pcount, n);
+    HIP_TRY(hipGetLastError());
+  }
+  prof_end(KID_MEMSET, e0);
+  prof_begin(KID_NODE, e0);
+  const dim3 gi(unsigned((p + kBlock - 1) / kBlock));
+  if (nt.packed)
+    hipLaunchKernelGGL((k_node_insert<PackedTab>), gi, dim3(kBlock), 0, stream, a.in, n, p, nt.pt, pnf, pmu,
+                       a.words, mk, d_hdr, a.pcount, a.out, a.count, a.id_off);
+  else
+    hipLaunchKernelGGL((k_node_insert<WideTab>), gi, dim3(kBlock), 0, stream, a.in, n, p, nt.wt, pnf, pmu,
+                       a.words, mk, d_hdr, a.pcount, a.out, a.count, a.id_off);
+  HIP_TRY(hipGetLastError());
+  prof_end(KID_NODE, e0);
+  prof_begin(KID_FLAGSCAN_NODE, e0);
+  const dim3 gs(unsigned((p + kTile - 1) / kTile));
+  hipLaunchKernelGGL(k_flagscan_node, gs, dim3(kBlock), 0, stream, a.words, p, a.in, n, knf, d_grp, a.desc,
+                     a.ticket, a.out, a.count, a.pcount);
+  HIP_TRY(hipGetLastError());
+  prof_end(KID_FLAGSCAN_NODE, e0);
+  prof_begin(KID_RESOLVE_NODE, e0);
+  if (nt.packed)
+    hipLaunchKernelGGL((k_resolve_node<PackedTab>), gi, dim3(kBlock), 0, stream, a.words, p, nt.pt, knf, d_grp,
+                       a.pcount, n);
+  else
+    hipLaunchKernelGGL((k_resolve_node<WideTab>), gi, dim3(kBlock), 0, stream, a.words, p, nt.wt, knf, d_grp,
+                       a.pcount, n);
+  HIP_TRY(hipGetLastError());
+  prof_end(KID_RESOLVE_NODE, e0);
+  return GCZ_OK;
+}
 
 int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, int L) {
   info = gcz_info{};
@@ -215,25 +186,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   const int D = int(pk.size());
   layer_off.assign(D + 1, 0);
   for (int k = 0; k < D; ++k) layer_off[k + 1] = layer_off[k] + pk[k];
-  // leaf chunks, geometric: S/64, S/64, S/32, ... S/2 (multiples of the leaf tile);
-  // the first small chunks discover most keys, the big later ones mostly hit
-  // settled slots.  Small inputs are one chunk.
-  std::vector<u64> chunk_start{0};
-  {
-    const u64 tile = kLeafTile;
-    u64 next = std::max<u64>(tile, (S / 64 + tile - 1) / tile * tile);
-    if (S <= (1ull << 21)) next = S;
-    bool first = true;
-    while (chunk_start.back() < S && int(chunk_start.size()) < kMaxChunks) {
-      const u64 c0 = chunk_start.back();
-      u64 c1 = std::min(S, c0 + next);
-      if (S - c1 < tile) c1 = S;
-      chunk_start.push_back(c1);
-      if (!first) next *= 2;
-      first = false;
-    }
-    chunk_start.back() = S;
-  }
+  const std::vector<u64> chunk_start = leaf_chunks(S);
   const int C = int(chunk_start.size()) - 1;
   std::vector<u64> desc_off;
   u64 ntiles_total = 0;
@@ -246,16 +199,12 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     ntiles_total += (pk[k] + kTile - 1) / kTile;
   }
 
-  // leaf table: big enough for S when S is small; otherwise start at 2^23 slots
+  // leaf table: big enough for S when S is small; otherwise start at 2^24 slots
   // (every ACGT 12-mer class fits) and grow after an overflow.
   const u64 full_cap = std::max<u64>(256, next_pow2(2 * S));
   u64 leaf_cap = full_cap;
   if (S > (1ull << 22)) leaf_cap = std::min(full_cap, std::max<u64>(1ull << 24, leaf_cap_hint));
   if (leaf_cap_log2 > 0 && S > (1ull << 22)) leaf_cap = std::min(full_cap, 1ull << leaf_cap_log2);
-  // load <= 2/3 (shift 0), 1/2 (shift 1, default) or 1/4 (shift 2)
-  auto node_cap = [&](u64 p) {
-    return std::max<u64>(256, next_pow2(node_cap_shift <= 0 ? p + p / 2 + 1 : p << node_cap_shift));
-  };
   const u64 node_cap0 = node_cap(pk[0]);
 
   int rc;
@@ -266,27 +215,20 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   if ((rc = ensure(leaves_out, S * 8 + 16))) return rc;
   if ((rc = ensure(nodes_out, layer_off[D] * 8 + 16))) return rc;
   if ((rc = ensure(hdr, sizeof(Header)))) return rc;
-  const u64 full_b = (S + 16 + 255) / 256 * 256, half = ((S + 1) / 2 + 16 + 255) / 256 * 256;
-  if ((rc = ensure(nf, full_b + half))) return rc;       // [leaf / even layers: S][odd layers: S/2]
-  if ((rc = ensure(multi, 2 * half))) return rc;         // [even layers][odd layers]
+  if ((rc = ensure_marks(S))) return rc;
   if (!h_hdr) HIP_TRY(hipHostMalloc((void**)&h_hdr, sizeof(Header), hipHostMallocDefault));
 
-  Header* d_hdr = static_cast<Header*>(hdr.ptr);
-  u32* A = static_cast<u32*>(wa.ptr);
-  u32* Bw = static_cast<u32*>(wb.ptr);
-  Group* d_grp = static_cast<Group*>(grp.ptr);
-  u64* d_desc = static_cast<u64*>(desc.ptr);
-  unsigned char* d_nf = static_cast<unsigned char*>(nf.ptr);
-  unsigned char* nf_set[2] = {d_nf, d_nf + full_b};
-  unsigned char* multi_set[2] = {static_cast<unsigned char*>(multi.ptr), static_cast<unsigned char*>(multi.ptr) + half};
+  Header* d_hdr = hdr.as<Header>();
+  u32* A = wa.as<u32>();
+  u32* Bw = wb.as<u32>();
+  u64* d_desc = desc.as<u64>();
 
   if (!ev_start) {
     HIP_TRY(hipEventCreate(&ev_start));
     HIP_TRY(hipEventCreate(&ev_stop));
   }
 
-  bool allow_packed = !force_wide;
-  u32* in = nullptr;
+  allow_packed = !force_wide;
   for (;;) {
     if ((rc = ensure(tab, std::max(leaf_cap, node_cap0) * 16))) return rc;
     HIP_TRY(hipEventRecord(ev_start, stream));
@@ -295,112 +237,40 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     HIP_TRY(hipMemsetAsync(d_desc, 0, ntiles_total * 8, stream));
 
     // ---- leaf level, in chunks ----
-    const bool adaptive = leaf_cap < 2 * S;
-    const u32 limit = adaptive ? kAdaptiveProbeLimit : kMaxProbe;
-    // packed leaves only from bases (< 2^4L by construction); user leaves may carry any bits.
-    // Chunked settling needs one spare bit in the packed word, hence K + 1.
-    LevelTab lt = plan_table(tab.ptr, leaf_cap, d_bases ? 4 * u32(L) + 1 : 64, S, 0, allow_packed && d_bases,
-                             limit);
-    if (lt.packed) {
-      lt.pt.limit = std::min(lt.pt.limit, limit);
-      lt.pt.kmask >>= 1;                   // the key itself has 4L bits
-      lt.pt.sh = (4 * u32(L) + 1) / 2;
-    }
-    hipEvent_t e0{};
-    prof_begin(KID_MEMSET, e0);
-    HIP_TRY(hipMemsetAsync(tab.ptr, 0xff, lt.bytes(), stream));
-    HIP_TRY(hipMemsetAsync(d_nf, 0, S, stream));
-    prof_end(KID_MEMSET, e0);
-    u64* lo = static_cast<u64*>(leaves_out.ptr);
-    for (int c = 0; c < C; ++c) {
-      const u64 i0 = chunk_start[c], i1 = chunk_start[c + 1];
-      const dim3 g(unsigned((i1 - i0 + kBlock - 1) / kBlock));
-      prof_begin(KID_LEAF, e0);
-      if (d_bases) {
-        const auto* b = static_cast<const unsigned char*>(d_bases);
-        if (lt.packed) launch_leaf_bases(L, g, stream, b, i0, i1, lt.pt, A, d_nf, d_hdr);
-        else launch_leaf_bases(L, g, stream, b, i0, i1, lt.wt, A, d_nf, d_hdr);
-      } else {
-        hipLaunchKernelGGL((k_leaf_packed<WideTab>), g, dim3(kBlock), 0, stream, d_leaves, i0, i1, L, lt.wt, A,
-                           d_nf, d_hdr);
-      }
-      HIP_TRY(hipGetLastError());
-      prof_end(KID_LEAF, e0);
-      const dim3 gs(unsigned((i1 - i0 + kLeafTile - 1) / kLeafTile));
-      const u64* id0 = c == 0 ? nullptr : &d_hdr->count[c - 1];
-      prof_begin(KID_FLAGSCAN_LEAF, e0);
-      if (lt.packed)
-        hipLaunchKernelGGL((k_flagscan_leaf<PackedTab>), gs, dim3(kBlock), 0, stream, A, i0, i1, lt.pt, d_nf,
-                           d_desc + desc_off[c], &d_hdr->ticket[c], lo, id0, &d_hdr->count[c]);
-      else
-        hipLaunchKernelGGL((k_flagscan_leaf<WideTab>), gs, dim3(kBlock), 0, stream, A, i0, i1, lt.wt, d_nf,
-                           d_desc + desc_off[c], &d_hdr->ticket[c], lo, id0, &d_hdr->count[c]);
-      HIP_TRY(hipGetLastError());
-      prof_end(KID_FLAGSCAN_LEAF, e0);
-      prof_begin(KID_RESOLVE_LEAF, e0);
-      if (lt.packed)
-        hipLaunchKernelGGL((k_resolve_leaf<PackedTab>), g, dim3(kBlock), 0, stream, A, i0, i1, lt.pt, d_nf);
-      else
-        hipLaunchKernelGGL((k_resolve_leaf<WideTab>), g, dim3(kBlock), 0, stream, A, i0, i1, lt.wt, d_nf);
-      HIP_TRY(hipGetLastError());
-      prof_end(KID_RESOLVE_LEAF, e0);
-    }
+    LeafLevel la;
+    la.bases = d_bases; la.leaves = d_leaves; la.S = S; la.L = L;
+    la.cap = leaf_cap;
+    la.adaptive = leaf_cap < 2 * S;
+    la.words = A;
+    la.out = leaves_out.as<u64>();
+    la.chunk_start = chunk_start;
+    la.desc = d_desc;
+    la.desc_off = desc_off;
+    la.count = d_hdr->count;
+    la.ticket = d_hdr->ticket;
+    if ((rc = leaf_level(la, d_hdr))) return rc;
 
     // ---- node layers ----
-    in = A;
+    u32* in = A;
     u32* outw = Bw;
     u64 n = S;
     u64 bound = std::min(S, leaf_cap);        // child ids of layer 0 are leaf ids < #slots
     for (int k = 0; k < D; ++k) {
-      const u64 p = pk[k];
-      const u64 cap = node_cap(p);
-      const u32 Bk = std::max<u32>(1, bit_width(bound));
-      const LevelTab nt = plan_table(tab.ptr, cap, 2 * (Bk + 3), p, Bk, allow_packed, kMaxProbe);
-      const int cur = (k + 1) & 1, prev = k & 1;
-      unsigned char* knf = nf_set[cur];
-      const Marks mk{knf, multi_set[cur]};
-      const unsigned char* pnf = k == 0 ? nullptr : nf_set[prev];
-      const unsigned char* pmu = k == 0 ? nullptr : multi_set[prev];
-      const u64* pcount = k == 0 ? &d_hdr->count[C - 1] : &d_hdr->count[kLayerSlot + k - 1];
-      uint2* out_k = static_cast<uint2*>(nodes_out.ptr) + layer_off[k];
-      u64* count_k = &d_hdr->count[kLayerSlot + k];
-      prof_begin(KID_MEMSET, e0);
-      {
-        const u64 tab16 = nt.bytes() / 16, p16 = (p + 15) / 16;
-        const u64 blocks = std::min<u64>(4096, (std::max(tab16, p16) + kBlock - 1) / kBlock);
-        hipLaunchKernelGGL(k_clear, dim3(unsigned(blocks)), dim3(kBlock), 0, stream, static_cast<uint4*>(tab.ptr),
-                           tab16, reinterpret_cast<uint4*>(knf), reinterpret_cast<uint4*>(mk.multi), p16, pcount, n);
-        HIP_TRY(hipGetLastError());
-      }
-      prof_end(KID_MEMSET, e0);
-      prof_begin(KID_NODE, e0);
-      const dim3 gi(unsigned((p + kBlock - 1) / kBlock));
-      if (nt.packed)
-        hipLaunchKernelGGL((k_node_insert<PackedTab>), gi, dim3(kBlock), 0, stream, in, n, p, nt.pt, pnf, pmu, outw,
-                           mk, d_hdr, pcount, out_k, count_k);
-      else
-        hipLaunchKernelGGL((k_node_insert<WideTab>), gi, dim3(kBlock), 0, stream, in, n, p, nt.wt, pnf, pmu, outw,
-                           mk, d_hdr, pcount, out_k, count_k);
-      HIP_TRY(hipGetLastError());
-      prof_end(KID_NODE, e0);
-      prof_begin(KID_FLAGSCAN_NODE, e0);
-      const dim3 gs(unsigned((p + kTile - 1) / kTile));
-      hipLaunchKernelGGL(k_flagscan_node, gs, dim3(kBlock), 0, stream, outw, p, in, n, knf, d_grp,
-                         d_desc + desc_off[C + k], &d_hdr->ticket[kLayerSlot + k], out_k, count_k, pcount);
-      HIP_TRY(hipGetLastError());
-      prof_end(KID_FLAGSCAN_NODE, e0);
-      prof_begin(KID_RESOLVE_NODE, e0);
-      if (nt.packed)
-        hipLaunchKernelGGL((k_resolve_node<PackedTab>), gi, dim3(kBlock), 0, stream, outw, p, nt.pt, knf, d_grp,
-                           pcount, n);
-      else
-        hipLaunchKernelGGL((k_resolve_node<WideTab>), gi, dim3(kBlock), 0, stream, outw, p, nt.wt, knf, d_grp,
-                           pcount, n);
-      HIP_TRY(hipGetLastError());
-      prof_end(KID_RESOLVE_NODE, e0);
+      NodeLevel na;
+      na.k = k;
+      na.in = in; na.n = n; na.p = pk[k];
+      na.words = outw;
+      na.out = nodes_out.as<uint2>() + layer_off[k];
+      na.count = &d_hdr->count[kLayerSlot + k];
+      na.bound = bound;
+      na.prev_marks = k > 0;
+      na.pcount = k == 0 ? &d_hdr->count[C - 1] : &d_hdr->count[kLayerSlot + k - 1];
+      na.desc = d_desc + desc_off[C + k];
+      na.ticket = &d_hdr->ticket[kLayerSlot + k];
+      if ((rc = node_level(na, d_hdr))) return rc;
       std::swap(in, outw);
-      n = p;
-      bound = p;
+      n = pk[k];
+      bound = pk[k];
     }
     hipLaunchKernelGGL(k_root, dim3(1), dim3(1), 0, stream, in, d_hdr);
     HIP_TRY(hipGetLastError());
@@ -411,7 +281,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     HIP_TRY(hipEventElapsedTime(&ms, ev_start, ev_stop));
     info.build_ms = ms;
     if (profile) prof_collect();
-    if (h_hdr->leaf_overflow && adaptive) {    // leaf table too small: grow and rebuild
+    if (h_hdr->leaf_overflow && la.adaptive) {    // leaf table too small: grow and rebuild
       leaf_cap = std::min(full_cap, leaf_cap * 8);
       continue;
     }
@@ -469,6 +339,7 @@ void gcz_ctx_destroy(gcz_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  gcz_dist_state_free(c);
   for (DevBuf* b : {&c->wa, &c->wb, &c->grp, &c->desc, &c->tab, &c->leaves_out, &c->nodes_out, &c->hdr, &c->input,
                     &c->nf, &c->multi})
     if (b->ptr) (void)hipFree(b->ptr);
@@ -622,7 +493,7 @@ int gcz_profile_enable(gcz_ctx* c, int on) {
 }
 int gcz_profile_entry(gcz_ctx* c, int k, const char** name, uint64_t* launches, double* total_ms) {
   if (!c || k < 0 || k >= KID_COUNT) return -1;
-  if (name) *name = kKernelNames[k];
+  if (name) *name = kernel_name(k);
   if (launches) *launches = c->prof_launches[k];
   if (total_ms) *total_ms = c->prof_ms[k];
   return 0;

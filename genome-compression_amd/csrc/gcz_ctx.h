@@ -1,0 +1,232 @@
+// Host-side build context shared by the single-device build (gcz_build.hip)
+// and the multi-rank build (gcz_dist.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gcz_device.h"
+
+#define HIP_TRY(x)                                                                    \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess) return fail(GCZ_ERR_DEVICE, #x, hipGetErrorString(e_));    \
+  } while (0)
+
+namespace gcz_host {
+
+using gcz_dev::u32;
+using gcz_dev::u64;
+
+inline u64 next_pow2(u64 x) {
+  u64 p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+inline u64 inv64(u64 a) {                 // inverse of an odd number mod 2^64 (Newton)
+  u64 x = a;
+  for (int i = 0; i < 6; ++i) x *= 2 - a * x;
+  return x;
+}
+
+inline u32 bit_width(u64 x) {
+  u32 b = 0;
+  while (x) { ++b; x >>= 1; }
+  return b;
+}
+
+inline u32 log2_exact(u64 x) { return bit_width(x) - 1; }
+
+constexpr u32 kAdaptiveProbeLimit = 256;
+constexpr u64 kMixC1 = 0x9E3779B97F4A7C15ull;
+constexpr u64 kMixC2 = 0xD6E8FEB86659FD93ull;
+
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  template <class T> T* as() const { return static_cast<T*>(ptr); }
+};
+
+// A level's table: packed 8-B words when quotient+displacement+position fit
+// in 64 bits, else 16-B wide slots.
+struct LevelTab {
+  bool packed = false;
+  gcz_dev::PackedTab pt{};
+  gcz_dev::WideTab wt{};
+  u64 cap = 0;
+  u64 bytes() const { return cap * (packed ? 8 : 16); }
+};
+
+inline LevelTab plan_table(void* buf, u64 cap, u32 K, u64 npos, u32 B, bool allow_packed, u32 wide_limit) {
+  LevelTab lt;
+  lt.cap = cap;
+  const u32 c = log2_exact(cap);
+  const u32 Q = K > c ? K - c : 0;
+  const u32 P = std::max<u32>(1, bit_width(npos - 1));
+  const int room = 64 - int(Q) - int(P);
+  if (allow_packed && K <= 64 && room >= 6) {
+    lt.packed = true;
+    gcz_dev::PackedTab& t = lt.pt;
+    t.tab = static_cast<u64*>(buf);
+    t.mask = u32(cap - 1);
+    t.D = u32(std::min(room, 8));
+    t.limit = (1u << t.D) - 2;
+    t.B = B;
+    t.c = c;
+    t.P = P;
+    t.sh = (K + 1) / 2;
+    t.kmask = K >= 64 ? ~0ull : ((1ull << K) - 1);
+    t.c1 = kMixC1; t.c2 = kMixC2;
+    t.c1i = inv64(kMixC1); t.c2i = inv64(kMixC2);
+  } else {
+    lt.wt.tab = static_cast<gcz_dev::Slot*>(buf);
+    lt.wt.mask = u32(cap - 1);
+    lt.wt.limit = wide_limit;
+    lt.wt.B = B;
+  }
+  return lt;
+}
+
+enum KernelId {
+  KID_LEAF, KID_NODE, KID_FLAGSCAN_LEAF, KID_FLAGSCAN_NODE, KID_RESOLVE_LEAF, KID_RESOLVE_NODE, KID_MEMSET,
+  KID_EXCHANGE, KID_DIST, KID_COUNT
+};
+inline const char* kernel_name(int k) {
+  static const char* names[KID_COUNT] = {"leaf_insert", "node_insert", "flagscan_leaf", "flagscan_node",
+                                         "resolve_leaf", "resolve_node", "clear", "exchange", "dist_local"};
+  return names[k];
+}
+
+// Leaf chunk plan (strands [chunk_start[c], chunk_start[c+1])).
+std::vector<u64> leaf_chunks(u64 S);
+
+// One node level of the build.
+struct NodeLevel {
+  int k = 0;                        // layer index (marks parity)
+  const u32* in = nullptr;          // n final words of the previous level
+  u64 n = 0, p = 0;                 // p = ceil(n / 2) pairs
+  u32* words = nullptr;             // p output words
+  uint2* out = nullptr;             // unique nodes, indexed by id
+  u64* count = nullptr;             // unique count (device)
+  u64 bound = 0;                    // child ids < bound
+  bool prev_marks = false;          // previous level's marks valid (singleton propagation)
+  const u64* pcount = nullptr;      // direct iff *pcount == n
+  u32 id_off = 0;                   // direct ids are id_off + j
+  u64* desc = nullptr;              // look-back descriptors (ceil(p / kTile))
+  u32* ticket = nullptr;
+};
+
+// One leaf level (all chunks).
+struct LeafLevel {
+  const void* bases = nullptr;      // ASCII (4-B aligned) or null
+  const u64* leaves = nullptr;      // packed strands or null
+  u64 S = 0;
+  int L = 12;
+  u64 cap = 0;                      // table slots
+  bool adaptive = false;            // probe-limited: overflow -> grow and rebuild
+  u32* words = nullptr;             // S words (local ids)
+  u64* out = nullptr;               // unique leaves, indexed by id
+  std::vector<u64> chunk_start;
+  u64* desc = nullptr;              // descriptors, chunk c at desc + desc_off[c]
+  std::vector<u64> desc_off;
+  u64* count = nullptr;             // count[c] = uniques after chunk c (cumulative, device)
+  u32* ticket = nullptr;            // one per chunk
+};
+
+}  // namespace gcz_host
+
+struct gcz_dist_state;   // gcz_dist.hip
+
+struct gcz_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string last_error;
+  gcz_host::DevBuf wa, wb, grp, desc, tab, leaves_out, nodes_out, hdr, input, nf, multi;
+  gcz_dev::Header* h_hdr = nullptr;   // pinned
+  unsigned char* nf_set[2] = {nullptr, nullptr};      // marks, even / odd layers
+  unsigned char* multi_set[2] = {nullptr, nullptr};
+  // last build
+  gcz_info info{};
+  std::vector<gcz_host::u64> layer_off;  // node offsets (in nodes) per layer within nodes_out
+  gcz_host::u64 leaf_cap_hint = 0;
+  bool allow_packed = true;
+  // profiling
+  bool profile = false;
+  bool force_wide = false;   // GCZ_TABLE=wide: always use 16-B slots (testing)
+  int node_cap_shift = 1;    // node table capacity = next_pow2(p << shift)   (GCZ_NODE_CAP_SHIFT)
+  int leaf_cap_log2 = 0;     // force the adaptive leaf table size            (GCZ_LEAF_CAP_LOG2)
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+  std::vector<hipEvent_t> event_pool;
+  size_t event_used = 0;
+  gcz_host::u64 prof_launches[gcz_host::KID_COUNT] = {};
+  double prof_ms[gcz_host::KID_COUNT] = {};
+  hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+  gcz_dist_state* dist = nullptr;   // multi-rank build state (gcz_dist.hip)
+
+  int fail(int code, const char* what, const char* detail) {
+    last_error = std::string(what) + ": " + detail;
+    info.status = code;
+    return code;
+  }
+
+  int ensure(gcz_host::DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes && b.ptr) return GCZ_OK;
+    if (b.ptr) {
+      HIP_TRY(hipStreamSynchronize(stream));
+      HIP_TRY(hipFree(b.ptr));
+      b.ptr = nullptr; b.bytes = 0;
+    }
+    HIP_TRY(hipMalloc(&b.ptr, bytes ? bytes : 16));
+    b.bytes = bytes ? bytes : 16;
+    return GCZ_OK;
+  }
+
+  hipEvent_t next_event() {
+    if (event_used == event_pool.size()) {
+      hipEvent_t e;
+      (void)hipEventCreate(&e);
+      event_pool.push_back(e);
+    }
+    return event_pool[event_used++];
+  }
+  void prof_begin(int, hipEvent_t& a) {
+    if (!profile) return;
+    a = next_event();
+    (void)hipEventRecord(a, stream);
+  }
+  void prof_end(int kid, hipEvent_t a) {
+    if (!profile) return;
+    hipEvent_t b = next_event();
+    (void)hipEventRecord(b, stream);
+    pending.push_back({kid, {a, b}});
+  }
+  void prof_collect() {
+    for (auto& pe : pending) {
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, pe.second.first, pe.second.second);
+      prof_ms[pe.first] += ms;
+      prof_launches[pe.first] += 1;
+    }
+    pending.clear();
+    event_used = 0;
+  }
+
+  gcz_host::u64 node_cap(gcz_host::u64 p) const {   // load <= 2/3 (shift 0), 1/2 (1, default), 1/4 (2)
+    using gcz_host::next_pow2;
+    return std::max<gcz_host::u64>(256, next_pow2(node_cap_shift <= 0 ? p + p / 2 + 1 : p << node_cap_shift));
+  }
+  // Marks buffers for levels of up to S elements (sets aligned for uchar2 loads).
+  int ensure_marks(gcz_host::u64 S);
+
+  int leaf_level(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr);
+  int node_level(const gcz_host::NodeLevel& a, gcz_dev::Header* d_hdr);
+  int build(const void* d_bases, const gcz_host::u64* d_leaves, gcz_host::u64 nbases, gcz_host::u64 S, int L);
+};

@@ -465,7 +465,8 @@ __global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ 
                                                        const unsigned char* __restrict__ prev_multi,
                                                        u32* __restrict__ rec, Marks mk,
                                                        Header* __restrict__ hdr, const u64* prev_count,
-                                                       uint2* __restrict__ out, u64* __restrict__ count_out) {
+                                                       uint2* __restrict__ out, u64* __restrict__ count_out,
+                                                       u32 id_off) {
   if (level_direct(prev_count, n)) {
     const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
     if (j == 0) *count_out = p;
@@ -477,7 +478,7 @@ __global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ 
     uint2 w;
     w.x = cl; w.y = cr;
     out[j] = w;
-    rec[j] = make_word(u32(j), m, t, v);
+    rec[j] = make_word(u32(j) + id_off, m, t, v);   // id_off: first pair of this rank (multi-rank build)
     return;
   }
   __shared__ u32 s_hashed;
@@ -633,7 +634,7 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_leaf(u32* __restrict__ word
 // Nodes: first occurrences recompute their canonical pair from the input
 // (coalesced) instead of reading the table, emit it, and publish the group
 // records that resolve_node uses.
-__global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ words, u64 p,
+[[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ words, u64 p,
                                                          const u32* __restrict__ in, u64 n,
                                                          const unsigned char* __restrict__ nf,
                                                          Group* __restrict__ grp, u64* __restrict__ desc,
@@ -698,10 +699,10 @@ __global__ __launch_bounds__(kBlock) void k_resolve_node(u32* __restrict__ words
   words[j] = id | (w & kBits);
 }
 
-__global__ void k_root(const u32* __restrict__ words, Header* __restrict__ hdr) { hdr->root = words[0]; }
+[[maybe_unused]] static __global__ void k_root(const u32* __restrict__ words, Header* __restrict__ hdr) { hdr->root = words[0]; }
 
 // Clear a node level's table (all ones) and marks (zero) unless the level is direct.
-__global__ __launch_bounds__(kBlock) void k_clear(uint4* __restrict__ tab, u64 tab16, uint4* __restrict__ nf,
+[[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_clear(uint4* __restrict__ tab, u64 tab16, uint4* __restrict__ nf,
                                                  uint4* __restrict__ multi, u64 p16, const u64* prev_count,
                                                  u64 prev_n) {
   if (level_direct(prev_count, prev_n)) return;

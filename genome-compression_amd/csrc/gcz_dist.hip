@@ -1,0 +1,1031 @@
+// Multi-rank shared_tree construction: one rank per GPU (RCCL over xGMI), or R
+// virtual ranks sharing one device (testing).  Algorithm: gcz_dist_device.h.
+//
+// Partition: rank r owns strands [r*B, (r+1)*B) clipped to S,
+// where B = ceil(S/R) rounded up to a multiple of 2^G.  Node level k < G pairs
+// elements (2j, 2j+1) that then lie on one rank, so levels 0..G-1 run
+// distributed; the n_G < ~R*1024 words left are gathered to rank 0, which
+// finishes the top layers alone.  Rank r's uniques of every distributed level
+// are the contiguous id range [off_r, off_r + c_r) of that layer, so the
+// layers are the rank-ordered concatenation of the slices — byte-identical to
+// the single-device (and the reference's) build.
+#include <dlfcn.h>
+#include <rccl/rccl.h>   // types only: the functions are resolved with dlsym
+
+#include "gcz_ctx.h"
+#include "gcz_dist_device.h"
+
+using namespace gcz_dev;
+using namespace gcz_host;
+
+struct gcz_dist_state {
+  DevBuf scratch, gnf, gmul, gid, blockcnt, skey, sidx, sflag, scval, sdval;   // sender side
+  DevBuf rkey, oslot, rflag, rcval, rdval, owntab;                            // owner side
+  DevBuf dhdr, gath, gath2, gathf, ddesc, tail_in;
+  u64* h_gath = nullptr;    // pinned mirrors of the gathered vectors
+  u64* h_gath2 = nullptr;
+  u64* h_gathf = nullptr;
+};
+
+void gcz_dist_state_free(gcz_ctx* c) {
+  gcz_dist_state* d = c->dist;
+  if (!d) return;
+  for (DevBuf* b : {&d->scratch, &d->gnf, &d->gmul, &d->gid, &d->blockcnt, &d->skey, &d->sidx, &d->sflag,
+                    &d->scval, &d->sdval, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab,
+                    &d->dhdr, &d->gath, &d->gath2, &d->gathf, &d->ddesc, &d->tail_in})
+    if (b->ptr) (void)hipFree(b->ptr);
+  for (u64* h : {d->h_gath, d->h_gath2, d->h_gathf})
+    if (h) (void)hipHostFree(h);
+  delete d;
+  c->dist = nullptr;
+}
+
+namespace {
+
+// ---- transports ------------------------------------------------------------------
+
+struct Transport {
+  int world = 1;
+  std::string err;
+  virtual ~Transport() = default;
+  // counts: M[s * world + d] elements from rank s to rank d (reverse: from d to s).
+  // send[i]: local rank i's buffer, segments in destination order; recv[i]: segments in source order.
+  virtual int alltoallv(const std::vector<u64>& M, bool reverse, size_t elem, const std::vector<const void*>& send,
+                        const std::vector<void*>& recv) = 0;
+  virtual int allgather(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) = 0;
+  // rank 0 receives cnt[r] elements from every rank r, concatenated in rank order
+  virtual int gather0(const std::vector<u64>& cnt, size_t elem, const std::vector<const void*>& send,
+                      void* recv0) = 0;
+};
+
+u64 mcount(const std::vector<u64>& M, int R, bool reverse, int s, int d) {
+  return reverse ? M[size_t(d) * R + s] : M[size_t(s) * R + d];
+}
+u64 send_displ(const std::vector<u64>& M, int R, bool rev, int s, int d) {
+  u64 o = 0;
+  for (int q = 0; q < d; ++q) o += mcount(M, R, rev, s, q);
+  return o;
+}
+u64 recv_displ(const std::vector<u64>& M, int R, bool rev, int d, int s) {
+  u64 o = 0;
+  for (int q = 0; q < s; ++q) o += mcount(M, R, rev, q, d);
+  return o;
+}
+
+// All ranks in this process on one stream: exchanges are device copies.
+struct LocalTransport : Transport {
+  hipStream_t stream = nullptr;
+  int copy(void* dst, const void* src, size_t bytes) {
+    if (!bytes) return GCZ_OK;
+    if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream) != hipSuccess) {
+      err = "local transport copy failed";
+      return GCZ_ERR_DEVICE;
+    }
+    return GCZ_OK;
+  }
+  int alltoallv(const std::vector<u64>& M, bool rev, size_t elem, const std::vector<const void*>& send,
+                const std::vector<void*>& recv) override {
+    for (int s = 0; s < world; ++s)
+      for (int d = 0; d < world; ++d)
+        if (int rc = copy(static_cast<char*>(recv[d]) + recv_displ(M, world, rev, d, s) * elem,
+                          static_cast<const char*>(send[s]) + send_displ(M, world, rev, s, d) * elem,
+                          mcount(M, world, rev, s, d) * elem))
+          return rc;
+    return GCZ_OK;
+  }
+  int allgather(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) override {
+    for (int s = 0; s < world; ++s)
+      for (int d = 0; d < world; ++d)
+        if (int rc = copy(static_cast<char*>(recv[d]) + size_t(s) * bytes, send[s], bytes)) return rc;
+    return GCZ_OK;
+  }
+  int gather0(const std::vector<u64>& cnt, size_t elem, const std::vector<const void*>& send,
+              void* recv0) override {
+    u64 o = 0;
+    for (int s = 0; s < world; ++s) {
+      if (int rc = copy(static_cast<char*>(recv0) + o * elem, send[s], cnt[s] * elem)) return rc;
+      o += cnt[s];
+    }
+    return GCZ_OK;
+  }
+};
+
+struct RcclApi {
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+  bool ok = false;
+};
+
+// RCCL is loaded on first use; a process that already holds torch's RCCL
+// (same SONAME) shares it.
+RcclApi& rccl() {
+  static RcclApi api = [] {
+    RcclApi a;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return a;
+#define GCZ_SYM(field, name) a.field = reinterpret_cast<decltype(a.field)>(dlsym(h, name))
+    GCZ_SYM(GetUniqueId, "ncclGetUniqueId");
+    GCZ_SYM(CommInitRank, "ncclCommInitRank");
+    GCZ_SYM(CommDestroy, "ncclCommDestroy");
+    GCZ_SYM(GroupStart, "ncclGroupStart");
+    GCZ_SYM(GroupEnd, "ncclGroupEnd");
+    GCZ_SYM(Send, "ncclSend");
+    GCZ_SYM(Recv, "ncclRecv");
+    GCZ_SYM(AllGather, "ncclAllGather");
+    GCZ_SYM(GetErrorString, "ncclGetErrorString");
+#undef GCZ_SYM
+    a.ok = a.GetUniqueId && a.CommInitRank && a.CommDestroy && a.GroupStart && a.GroupEnd && a.Send && a.Recv &&
+           a.AllGather && a.GetErrorString;
+    return a;
+  }();
+  return api;
+}
+
+// One rank of this process on its own GPU; peers are other processes.
+struct RcclTransport : Transport {
+  int me = 0;
+  ncclComm_t comm = nullptr;
+  hipStream_t stream = nullptr;
+  ~RcclTransport() override {
+    if (comm) (void)rccl().CommDestroy(comm);
+  }
+  int check(ncclResult_t r, const char* what) {
+    if (r == ncclSuccess) return GCZ_OK;
+    err = std::string(what) + ": " + rccl().GetErrorString(r);
+    return GCZ_ERR_DEVICE;
+  }
+  int self_copy(void* dst, const void* src, size_t bytes) {
+    if (bytes && hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream) != hipSuccess) {
+      err = "rccl transport self copy failed";
+      return GCZ_ERR_DEVICE;
+    }
+    return GCZ_OK;
+  }
+  int alltoallv(const std::vector<u64>& M, bool rev, size_t elem, const std::vector<const void*>& send,
+                const std::vector<void*>& recv) override {
+    const auto* sb = static_cast<const char*>(send[0]);
+    auto* rb = static_cast<char*>(recv[0]);
+    if (int rc = self_copy(rb + recv_displ(M, world, rev, me, me) * elem,
+                           sb + send_displ(M, world, rev, me, me) * elem, mcount(M, world, rev, me, me) * elem))
+      return rc;
+    RcclApi& a = rccl();
+    if (int rc = check(a.GroupStart(), "ncclGroupStart")) return rc;
+    for (int q = 0; q < world; ++q) {
+      if (q == me) continue;
+      const u64 sc = mcount(M, world, rev, me, q), rcnt = mcount(M, world, rev, q, me);
+      if (sc) {
+        const ncclResult_t r =
+            a.Send(sb + send_displ(M, world, rev, me, q) * elem, sc * elem, ncclUint8, q, comm, stream);
+        if (r != ncclSuccess) { (void)a.GroupEnd(); return check(r, "ncclSend"); }
+      }
+      if (rcnt) {
+        const ncclResult_t r =
+            a.Recv(rb + recv_displ(M, world, rev, me, q) * elem, rcnt * elem, ncclUint8, q, comm, stream);
+        if (r != ncclSuccess) { (void)a.GroupEnd(); return check(r, "ncclRecv"); }
+      }
+    }
+    return check(a.GroupEnd(), "ncclGroupEnd");
+  }
+  int allgather(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) override {
+    return check(rccl().AllGather(send[0], recv[0], bytes, ncclUint8, comm, stream), "ncclAllGather");
+  }
+  int gather0(const std::vector<u64>& cnt, size_t elem, const std::vector<const void*>& send,
+              void* recv0) override {
+    RcclApi& a = rccl();
+    if (me != 0) {
+      if (!cnt[me]) return GCZ_OK;
+      return check(a.Send(send[0], cnt[me] * elem, ncclUint8, 0, comm, stream), "ncclSend");
+    }
+    if (int rc = self_copy(recv0, send[0], cnt[0] * elem)) return rc;
+    if (int rc = check(a.GroupStart(), "ncclGroupStart")) return rc;
+    u64 o = cnt[0];
+    for (int q = 1; q < world; ++q) {
+      if (cnt[q]) {
+        const ncclResult_t r = a.Recv(static_cast<char*>(recv0) + o * elem, cnt[q] * elem, ncclUint8, q, comm, stream);
+        if (r != ncclSuccess) { (void)a.GroupEnd(); return check(r, "ncclRecv"); }
+      }
+      o += cnt[q];
+    }
+    return check(a.GroupEnd(), "ncclGroupEnd");
+  }
+};
+
+// ---- partition -----------------------------------------------------------------
+
+struct DistPlan {
+  u64 S = 0;
+  int R = 1, G = 0, D = 0;
+  u64 B = 0;
+  std::vector<u64> nk;   // global input count of node level k (nk[0] = S); pairs of level k = nk[k+1]
+
+  void make(u64 S_, int R_) {
+    S = S_;
+    R = R_;
+    nk.assign(1, S);
+    while (nk.back() > 1 || nk.size() == 1) nk.push_back((nk.back() + 1) / 2);
+    D = int(nk.size()) - 1;
+    const u64 T = (S + R - 1) / R;
+    G = T < 1024 ? 0 : int(bit_width(T)) - 1 - 9;   // >= 512 elements per rank after G levels
+    G = std::min(G, 20);
+    G = std::min(G, D - 1);
+    if (G < 0) G = 0;
+    const u64 g = 1ull << G;
+    B = (T + g - 1) / g * g;
+  }
+  // element range of rank r at the input of node level k (k = 0: strands), k <= G
+  u64 start(int r, int k) const { return std::min((u64(r) * B) >> k, nk[k]); }
+  u64 end(int r, int k) const { return std::min((u64(r + 1) * B) >> k, nk[k]); }
+  u64 count(int r, int k) const { return end(r, k) - start(r, k); }
+};
+
+}  // namespace
+
+namespace {
+// Per local rank, the level being reconciled (see gcz_dist_device.h).
+struct RankLevel {
+  RecSrc src{};
+  u64 grid_elems = 0;       // bucket grid: leaves -> capacity, nodes -> p
+  const u64* ucount = nullptr;
+  u32* w = nullptr;         // words to remap
+  unsigned char* nf = nullptr;
+  unsigned char* multi = nullptr;
+  void* out = nullptr;      // rank's slice of the output layer
+  bool leaves = false;
+  const unsigned char* bases = nullptr;   // leaf level: for the bad-symbol report
+};
+}  // namespace
+
+struct gcz_group {
+  int world = 1;
+  std::vector<gcz_ctx*> ctx;   // local ranks
+  std::vector<int> rank;       // their global ranks
+  bool owns_ctx = false;
+  Transport* tr = nullptr;
+  std::string last_error;
+  // last build
+  gcz_info info{};
+  DistPlan plan;
+  std::vector<std::vector<u64>> slice_off, slice_cnt;   // [layer + 1][global rank]
+  std::vector<std::vector<u64>> node_base;              // [local][layer]: node offset within nodes_out
+  bool allow_packed = true;
+
+  int fail(int code, const std::string& what) {
+    last_error = what;
+    info.status = code;
+    for (gcz_ctx* c : ctx) c->fail(code, "group build", what.c_str());
+    return code;
+  }
+  int dev_fail(const char* what) {
+    return fail(GCZ_ERR_DEVICE, std::string(what) + (tr && !tr->err.empty() ? ": " + tr->err : ""));
+  }
+  int build(const void* const* d_bases, const u64* const* d_leaves, u64 S, int L);
+  int alloc(int i, int L, u64 leaf_cap);
+  int exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, std::vector<u64>& c,
+               std::vector<u64>& off, u64& total, u64* err_global, int* err_sym, int* ovf_bits);
+};
+
+#define G_HIP(x)                                                   \
+  do {                                                             \
+    if ((x) != hipSuccess) return dev_fail(#x);                    \
+  } while (0)
+#define G_RC(x)                                                    \
+  do {                                                             \
+    int rc_ = (x);                                                 \
+    if (rc_) return rc_ == GCZ_ERR_DEVICE ? dev_fail(#x) : rc_;    \
+  } while (0)
+
+namespace {
+constexpr int kRetry = -1000;   // internal: some rank overflowed a table, rebuild
+}
+
+int gcz_group::alloc(int i, int L, u64 leaf_cap) {
+  gcz_ctx* c = ctx[i];
+  const int r = rank[i];
+  const DistPlan& P = plan;
+  const u64 S_r = P.count(r, 0);
+  const u64 nG = r == 0 ? P.nk[P.G] : 0;
+  const u64 wmax = std::max(S_r, nG);
+  if (!c->dist) c->dist = new gcz_dist_state();
+  gcz_dist_state& d = *c->dist;
+  // node storage: local slices of the distributed layers, then (rank 0) the tail layers
+  node_base[i].assign(P.D + 1, 0);
+  u64 nodes = 0;
+  for (int k = 0; k < P.D; ++k) {
+    node_base[i][k] = nodes;
+    if (k < P.G) nodes += P.count(r, k + 1);
+    else if (r == 0) nodes += P.nk[k + 1];
+  }
+  node_base[i][P.D] = nodes;
+  const auto chunks = leaf_chunks(S_r);
+  u64 tiles = 0;
+  for (size_t q = 0; q + 1 < chunks.size(); ++q) tiles += (chunks[q + 1] - chunks[q] + kLeafTile - 1) / kLeafTile;
+  for (int k = 0; k < P.D; ++k) {
+    const u64 pl = k < P.G ? P.count(r, k + 1) : (r == 0 ? P.nk[k + 1] : 0);
+    tiles += (pl + kTile - 1) / kTile;
+  }
+  int rc;
+  if ((rc = c->ensure(c->wa, wmax * 4 + 16))) return rc;
+  if ((rc = c->ensure(c->wb, wmax * 4 + 16))) return rc;
+  if ((rc = c->ensure(c->grp, ((wmax + 63) / 64 + kGroupsPerTile) * sizeof(Group)))) return rc;
+  if ((rc = c->ensure(c->desc, tiles * 8 + 64))) return rc;
+  if ((rc = c->ensure(c->leaves_out, S_r * 8 + 16))) return rc;
+  if ((rc = c->ensure(c->nodes_out, nodes * 8 + 16))) return rc;
+  if ((rc = c->ensure(c->hdr, sizeof(Header)))) return rc;
+  if ((rc = c->ensure_marks(wmax))) return rc;
+  const u64 pmax = std::max<u64>(P.G > 0 ? P.count(r, 1) : 0, nG > 1 ? (nG + 1) / 2 : 1);
+  if ((rc = c->ensure(c->tab, std::max(leaf_cap, c->node_cap(pmax)) * 16))) return rc;
+  if (!c->h_hdr && hipHostMalloc((void**)&c->h_hdr, sizeof(Header), hipHostMallocDefault) != hipSuccess)
+    return GCZ_ERR_DEVICE;
+  const u64 u = S_r + 16;
+  if ((rc = c->ensure(d.scratch, u * 8))) return rc;
+  if ((rc = c->ensure(d.gnf, u))) return rc;
+  if ((rc = c->ensure(d.gmul, u))) return rc;
+  if ((rc = c->ensure(d.gid, u * 4))) return rc;
+  if ((rc = c->ensure(d.blockcnt, (u64(world) * ((u + kTile - 1) / kTile + 1)) * 4 + 64))) return rc;
+  if ((rc = c->ensure(d.skey, u * 8))) return rc;
+  if ((rc = c->ensure(d.sidx, u * 4))) return rc;
+  if ((rc = c->ensure(d.sflag, u))) return rc;
+  if ((rc = c->ensure(d.scval, u * 4))) return rc;
+  if ((rc = c->ensure(d.sdval, u * 4))) return rc;
+  if ((rc = c->ensure(d.dhdr, sizeof(DistHdr)))) return rc;
+  if ((rc = c->ensure(d.gath, size_t(world) * kSyncWords * 8))) return rc;
+  if ((rc = c->ensure(d.gath2, size_t(world) * 8))) return rc;
+  if ((rc = c->ensure(d.gathf, size_t(world) * kFinalWords * 8))) return rc;
+  if ((rc = c->ensure(d.ddesc, ((u + kTile - 1) / kTile) * 8 + 64))) return rc;
+  if ((rc = c->ensure(d.tail_in, nG * 4 + 16))) return rc;
+  if (!d.h_gath) {
+    if (hipHostMalloc((void**)&d.h_gath, size_t(kMaxRanks) * kSyncWords * 8, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&d.h_gath2, size_t(kMaxRanks) * 8, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&d.h_gathf, size_t(kMaxRanks) * kFinalWords * 8, hipHostMallocDefault) != hipSuccess)
+      return GCZ_ERR_DEVICE;
+  }
+  return GCZ_OK;
+}
+
+
+int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, std::vector<u64>& c,
+                        std::vector<u64>& off, u64& total, u64* err_global, int* err_sym, int* ovf_bits) {
+  const int R = world, NL = int(ctx.size());
+  // 1. bucket the records by owner, pack the sync vector
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    gcz_dist_state& d = *cx->dist;
+    RankLevel& L = lv[i];
+    L.src.R = u32(R);
+    DistHdr* dh = d.dhdr.as<DistHdr>();
+    G_HIP(hipMemsetAsync(dh, 0, offsetof(DistHdr, cell), cx->stream));
+    const u32 nb = u32(std::max<u64>(1, (L.grid_elems + kTile - 1) / kTile));
+    hipLaunchKernelGGL(k_bucket_count, dim3(nb), dim3(kBlock), 0, cx->stream, L.src, d.blockcnt.as<u32>(), nb);
+    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(1024), 0, cx->stream, d.blockcnt.as<u32>(), u64(R) * nb, u32(R),
+                       nb, dh->sync);
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(nb), dim3(kBlock), 0, cx->stream, L.src, d.blockcnt.as<u32>(), nb,
+                       d.skey.as<u64>(), d.sidx.as<u32>());
+    hipLaunchKernelGGL(k_dist_pack, dim3(1), dim3(1), 0, cx->stream, cx->hdr.as<Header>(), L.ucount, L.bases, dh,
+                       u32(R));
+    G_HIP(hipGetLastError());
+  }
+  {
+    std::vector<const void*> s;
+    std::vector<void*> r;
+    for (gcz_ctx* cx : ctx) {
+      s.push_back(cx->dist->dhdr.as<DistHdr>()->sync);
+      r.push_back(cx->dist->gath.ptr);
+    }
+    G_RC(tr->allgather(kSyncWords * 8, s, r));
+  }
+  gcz_dist_state& d0 = *ctx[0]->dist;
+  G_HIP(hipMemcpyAsync(d0.h_gath, d0.gath.ptr, size_t(R) * kSyncWords * 8, hipMemcpyDeviceToHost, ctx[0]->stream));
+  for (gcz_ctx* cx : ctx) G_HIP(hipStreamSynchronize(cx->stream));
+  const u64* gv = d0.h_gath;
+  std::vector<u64> M(size_t(R) * R), u(R);
+  u64 records = 0;
+  *ovf_bits = 0;
+  *err_global = ~0ull;
+  *err_sym = 0;
+  for (int s = 0; s < R; ++s) {
+    const u64* v = gv + size_t(s) * kSyncWords;
+    for (int q = 0; q < R; ++q) { M[size_t(s) * R + q] = v[q]; records += v[q]; }
+    *ovf_bits |= int(v[R]);
+    u[s] = v[R + 1];
+    if (v[R + 2] != ~0ull) {
+      const u64 g = v[R + 2] + plan.start(s, 0) * u64(info.L);   // local byte offset -> genome offset
+      if (g < *err_global) { *err_global = g; *err_sym = int(v[R + 3]); }
+    }
+  }
+  if (*ovf_bits) return kRetry;
+  if (*err_global != ~0ull) return GCZ_ERR_SYMBOL;
+
+  auto sent = [&](int r) { u64 t = 0; for (int q = 0; q < R; ++q) t += M[size_t(r) * R + q]; return t; };
+  auto recvd = [&](int r) { u64 t = 0; for (int q = 0; q < R; ++q) t += M[size_t(q) * R + r]; return t; };
+  auto blocks = [](u64 n) { return dim3(unsigned(std::max<u64>(1, (n + kBlock - 1) / kBlock))); };
+  auto displ_of = [&](int r) {   // source segments of rank r's receive buffer
+    Displ D{};
+    u64 o = 0;
+    for (int q = 0; q < R; ++q) { D.d[q] = o; o += M[size_t(q) * R + r]; }
+    for (int q = R; q <= kMaxRanks; ++q) D.d[q] = o;
+    return D;
+  };
+  std::vector<OwnTab> otab(NL);
+
+  // 2. owners decide first rank and repetition (A, B)
+  if (records) {
+    std::vector<const void*> s;
+    std::vector<void*> rv;
+    for (int i = 0; i < NL; ++i) {
+      gcz_ctx* cx = ctx[i];
+      gcz_dist_state& d = *cx->dist;
+      const u64 nr = recvd(rank[i]);
+      int rc;
+      if ((rc = cx->ensure(d.rkey, nr * 8 + 16)) || (rc = cx->ensure(d.oslot, nr * 4 + 16)) ||
+          (rc = cx->ensure(d.rflag, nr + 16)) || (rc = cx->ensure(d.rcval, nr * 4 + 16)) ||
+          (rc = cx->ensure(d.rdval, nr * 4 + 16)))
+        return dev_fail("exchange buffers");
+      const u64 cap = std::max<u64>(256, next_pow2(2 * nr));
+      if ((rc = cx->ensure(d.owntab, cap * 16))) return dev_fail("owner table");
+      otab[i].tab = d.owntab.as<Slot>();
+      otab[i].mask = u32(cap - 1);
+      s.push_back(d.skey.ptr);
+      rv.push_back(d.rkey.ptr);
+    }
+    G_RC(tr->alltoallv(M, false, 8, s, rv));
+    s.clear();
+    rv.clear();
+    for (int i = 0; i < NL; ++i) {
+      gcz_ctx* cx = ctx[i];
+      gcz_dist_state& d = *cx->dist;
+      const u64 nr = recvd(rank[i]);
+      G_HIP(hipMemsetAsync(d.owntab.ptr, 0xff, size_t(otab[i].mask + 1) * 16, cx->stream));
+      const Displ D = displ_of(rank[i]);
+      hipLaunchKernelGGL(k_own_insert, blocks(nr), dim3(kBlock), 0, cx->stream, d.rkey.as<u64>(), nr, D, u32(R),
+                         int(lv[i].leaves), otab[i], d.oslot.as<u32>(), &d.dhdr.as<DistHdr>()->final_vec[3]);
+      hipLaunchKernelGGL(k_own_reply, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr, D, u32(R),
+                         otab[i], d.rflag.as<unsigned char>());
+      G_HIP(hipGetLastError());
+      s.push_back(d.rflag.ptr);
+      rv.push_back(d.sflag.ptr);
+    }
+    G_RC(tr->alltoallv(M, true, 1, s, rv));
+  }
+  // 3. globally-first ranks in local order
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    gcz_dist_state& d = *cx->dist;
+    const u64 ur = u[rank[i]];
+    G_HIP(hipMemsetAsync(d.gnf.ptr, 0, ur + 1, cx->stream));
+    G_HIP(hipMemsetAsync(d.gmul.ptr, 0, ur + 1, cx->stream));
+    if (records) {
+      const u64 ns = sent(rank[i]);
+      hipLaunchKernelGGL(k_dist_flags, blocks(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
+                         d.sflag.as<unsigned char>(), d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>());
+    }
+    const u64 tiles = std::max<u64>(1, (ur + kTile - 1) / kTile);
+    G_HIP(hipMemsetAsync(d.ddesc.ptr, 0, tiles * 8, cx->stream));
+    DistHdr* dh = d.dhdr.as<DistHdr>();
+    hipLaunchKernelGGL(k_dist_rank, dim3(unsigned(tiles)), dim3(kBlock), 0, cx->stream, d.gnf.as<unsigned char>(),
+                       lv[i].ucount, d.gid.as<u32>(), d.ddesc.as<u64>(), &dh->ticket, &dh->cfirst);
+    G_HIP(hipGetLastError());
+  }
+  c.assign(R, 0);
+  if (records) {
+    std::vector<const void*> s;
+    std::vector<void*> rv;
+    for (gcz_ctx* cx : ctx) {
+      s.push_back(&cx->dist->dhdr.as<DistHdr>()->cfirst);
+      rv.push_back(cx->dist->gath2.ptr);
+    }
+    G_RC(tr->allgather(8, s, rv));
+    G_HIP(hipMemcpyAsync(d0.h_gath2, d0.gath2.ptr, size_t(R) * 8, hipMemcpyDeviceToHost, ctx[0]->stream));
+    for (gcz_ctx* cx : ctx) G_HIP(hipStreamSynchronize(cx->stream));
+    for (int s2 = 0; s2 < R; ++s2) c[s2] = d0.h_gath2[s2];
+  } else {
+    c = u;   // nothing crossed ranks: every local first is globally first
+  }
+  off.assign(R + 1, 0);
+  for (int s2 = 0; s2 < R; ++s2) off[s2 + 1] = off[s2] + c[s2];
+  total = off[R];
+  if (total > u64(kIdx)) return fail(GCZ_ERR_CAPACITY, "more than 2^29-1 uniques in one layer");
+  // 4. compact globally-first uniques into the slice; ids of the others (C, D)
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    gcz_dist_state& d = *cx->dist;
+    const u64 ur = u[rank[i]];
+    if (lv[i].leaves)
+      hipLaunchKernelGGL((k_dist_finalize<u64>), blocks(ur), dim3(kBlock), 0, cx->stream, lv[i].ucount,
+                         d.gnf.as<unsigned char>(), d.gid.as<u32>(), u32(off[rank[i]]), d.scratch.as<u64>(),
+                         static_cast<u64*>(lv[i].out));
+    else
+      hipLaunchKernelGGL((k_dist_finalize<uint2>), blocks(ur), dim3(kBlock), 0, cx->stream, lv[i].ucount,
+                         d.gnf.as<unsigned char>(), d.gid.as<u32>(), u32(off[rank[i]]), d.scratch.as<uint2>(),
+                         static_cast<uint2*>(lv[i].out));
+    G_HIP(hipGetLastError());
+  }
+  if (records) {
+    std::vector<const void*> s;
+    std::vector<void*> rv;
+    for (int i = 0; i < NL; ++i) {
+      gcz_ctx* cx = ctx[i];
+      gcz_dist_state& d = *cx->dist;
+      const u64 ns = sent(rank[i]);
+      hipLaunchKernelGGL(k_dist_cvals, blocks(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
+                         d.gnf.as<unsigned char>(), d.gid.as<u32>(), d.scval.as<u32>());
+      G_HIP(hipGetLastError());
+      s.push_back(d.scval.ptr);
+      rv.push_back(d.rcval.ptr);
+    }
+    G_RC(tr->alltoallv(M, false, 4, s, rv));
+    s.clear();
+    rv.clear();
+    for (int i = 0; i < NL; ++i) {
+      gcz_ctx* cx = ctx[i];
+      gcz_dist_state& d = *cx->dist;
+      const u64 nr = recvd(rank[i]);
+      hipLaunchKernelGGL(k_own_setid, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr,
+                         d.rcval.as<u32>(), otab[i]);
+      hipLaunchKernelGGL(k_own_getid, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr, otab[i],
+                         d.rdval.as<u32>());
+      G_HIP(hipGetLastError());
+      s.push_back(d.rdval.ptr);
+      rv.push_back(d.sdval.ptr);
+    }
+    G_RC(tr->alltoallv(M, true, 4, s, rv));
+    for (int i = 0; i < NL; ++i) {
+      gcz_ctx* cx = ctx[i];
+      gcz_dist_state& d = *cx->dist;
+      const u64 ns = sent(rank[i]);
+      hipLaunchKernelGGL(k_dist_dvals, blocks(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
+                         d.gnf.as<unsigned char>(), d.sdval.as<u32>(), d.gid.as<u32>());
+      G_HIP(hipGetLastError());
+    }
+  }
+  // 5. local words -> global ids
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    gcz_dist_state& d = *cx->dist;
+    const u64 nw = nwords[i];
+    hipLaunchKernelGGL(k_dist_remap, blocks(nw), dim3(kBlock), 0, cx->stream, lv[i].w, nw, lv[i].nf, lv[i].multi,
+                       d.gid.as<u32>(), d.gmul.as<unsigned char>());
+    G_HIP(hipGetLastError());
+  }
+  return GCZ_OK;
+}
+
+int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64 S, int L) {
+  info = gcz_info{};
+  info.L = L;
+  info.status = GCZ_OK;
+  last_error.clear();
+  const int R = world, NL = int(ctx.size());
+  if (L < 1 || L > 16) return fail(GCZ_ERR_ARG, "leaf length L must be in 1..16");
+  if (S == 0) return fail(GCZ_ERR_EMPTY, "fewer than L bases: nothing to build");
+  if (S > u64(kIdx)) return fail(GCZ_ERR_CAPACITY, "more than 2^29-1 strands");
+  if (R > kMaxRanks) return fail(GCZ_ERR_ARG, "at most 31 ranks");
+  info.n_strands = S;
+  plan.make(S, R);
+  const DistPlan& P = plan;
+  const int G = P.G, D = P.D;
+  if (D > GCZ_MAX_LAYERS) return fail(GCZ_ERR_CAPACITY, "too many layers");
+  node_base.assign(NL, {});
+
+  std::vector<u64> leaf_cap(NL);
+  for (int i = 0; i < NL; ++i) {
+    const u64 S_r = P.count(rank[i], 0);
+    const u64 full = std::max<u64>(256, next_pow2(2 * S_r));
+    leaf_cap[i] = S_r > (1ull << 22) ? std::min(full, std::max<u64>(1ull << 24, ctx[i]->leaf_cap_hint)) : full;
+  }
+  allow_packed = true;
+  for (gcz_ctx* cx : ctx) allow_packed = allow_packed && !cx->force_wide;
+
+  // bases: 4-B aligned copies where needed (the leaf kernel stages with 4-B loads)
+  std::vector<const unsigned char*> bases(NL, nullptr);
+  for (int i = 0; d_bases && i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    const u64 nb = P.count(rank[i], 0) * u64(L);
+    bases[i] = static_cast<const unsigned char*>(d_bases[i]);
+    if (nb && (reinterpret_cast<uintptr_t>(d_bases[i]) & 3)) {
+      if (cx->ensure(cx->input, nb + 16)) return dev_fail("realign buffer");
+      G_HIP(hipMemcpyAsync(cx->input.ptr, d_bases[i], nb, hipMemcpyDeviceToDevice, cx->stream));
+      bases[i] = cx->input.as<unsigned char>();
+    }
+  }
+
+  std::vector<RankLevel> lv(NL);
+  for (int attempt = 0;; ++attempt) {
+    if (attempt > 8) return fail(GCZ_ERR_CAPACITY, "hash table overflow persists");
+    for (int i = 0; i < NL; ++i) {
+      gcz_ctx* cx = ctx[i];
+      cx->allow_packed = allow_packed;
+      if (int rc = alloc(i, L, leaf_cap[i])) return rc == GCZ_ERR_DEVICE ? dev_fail("allocation") : rc;
+      if (!cx->ev_start) {
+        G_HIP(hipEventCreate(&cx->ev_start));
+        G_HIP(hipEventCreate(&cx->ev_stop));
+      }
+      G_HIP(hipEventRecord(cx->ev_start, cx->stream));
+      Header* h = cx->hdr.as<Header>();
+      G_HIP(hipMemsetAsync(h, 0, sizeof(Header), cx->stream));
+      G_HIP(hipMemsetAsync(&h->err_offset, 0xff, 8, cx->stream));
+      G_HIP(hipMemsetAsync(cx->desc.ptr, 0, cx->desc.bytes, cx->stream));
+    }
+    // per-rank descriptor cursors
+    std::vector<u64> dcur(NL, 0);
+
+    // ---- leaves ----
+    std::vector<int> C(NL);
+    for (int i = 0; i < NL; ++i) {
+      gcz_ctx* cx = ctx[i];
+      Header* h = cx->hdr.as<Header>();
+      const u64 S_r = P.count(rank[i], 0);
+      LeafLevel la;
+      la.bases = bases[i];
+      la.leaves = d_leaves ? d_leaves[i] : nullptr;
+      la.S = S_r;
+      la.L = L;
+      la.cap = leaf_cap[i];
+      la.adaptive = leaf_cap[i] < 2 * S_r;
+      la.words = cx->wa.as<u32>();
+      la.out = cx->dist->scratch.as<u64>();
+      la.chunk_start = leaf_chunks(S_r);
+      C[i] = int(la.chunk_start.size()) - 1;
+      for (int q = 0; q < C[i]; ++q) {
+        la.desc_off.push_back(dcur[i]);
+        dcur[i] += (la.chunk_start[q + 1] - la.chunk_start[q] + kLeafTile - 1) / kLeafTile;
+      }
+      la.desc = cx->desc.as<u64>();
+      la.count = h->count;
+      la.ticket = h->ticket;
+      if (cx->leaf_level(la, h)) return dev_fail("leaf level");
+      RankLevel& rl = lv[i];
+      rl = RankLevel{};
+      rl.src.leaves = cx->dist->scratch.as<u64>();
+      rl.src.ucount = &h->count[C[i] - 1];
+      rl.grid_elems = S_r;
+      rl.ucount = &h->count[C[i] - 1];
+      rl.w = cx->wa.as<u32>();
+      rl.out = cx->leaves_out.ptr;
+      rl.leaves = true;
+      rl.bases = bases[i];
+    }
+    std::vector<u64> c, off;
+    u64 total = 0, err_global = 0;
+    int err_sym = 0, ovf = 0;
+    {
+      std::vector<u64> nw(NL);
+      for (int i = 0; i < NL; ++i) nw[i] = P.count(rank[i], 0);
+      const int rc = exchange(lv, nw, c, off, total, &err_global, &err_sym, &ovf);
+      if (rc == kRetry) {   // every rank sees the same bits and takes the same decision
+        if (ovf & 2) {
+          for (int i = 0; i < NL; ++i)
+            leaf_cap[i] = std::min(std::max<u64>(256, next_pow2(2 * P.count(rank[i], 0))), leaf_cap[i] * 8);
+          if (attempt >= 1) allow_packed = false;
+        }
+        if (ovf & 1) allow_packed = false;
+        continue;
+      }
+      if (rc == GCZ_ERR_SYMBOL) {
+        info.error_offset = err_global;
+        info.error_symbol = err_sym;
+        for (gcz_ctx* cx : ctx) { cx->info.error_offset = err_global; cx->info.error_symbol = err_sym; }
+        return fail(GCZ_ERR_SYMBOL, "unknown nucleotide symbol");
+      }
+      if (rc) return rc;
+    }
+    slice_off.assign(D + 1, std::vector<u64>(R, 0));
+    slice_cnt.assign(D + 1, std::vector<u64>(R, 0));
+    for (int s = 0; s < R; ++s) { slice_off[0][s] = off[s]; slice_cnt[0][s] = c[s]; }
+    info.n_leaves = total;
+    for (int i = 0; i < NL; ++i) ctx[i]->leaf_cap_hint = next_pow2(std::max<u64>(1, 2 * total));
+
+    // ---- distributed node levels ----
+    u64 prev_total = total;        // uniques of the previous level (child id bound)
+    bool direct = total == P.nk[0];
+    bool retry = false;
+    std::vector<u32*> cur_in(NL), cur_out(NL);
+    for (int i = 0; i < NL; ++i) { cur_in[i] = ctx[i]->wa.as<u32>(); cur_out[i] = ctx[i]->wb.as<u32>(); }
+    for (int k = 0; k < G && !retry; ++k) {
+      for (int i = 0; i < NL; ++i) {
+        gcz_ctx* cx = ctx[i];
+        Header* h = cx->hdr.as<Header>();
+        DistHdr* dh = cx->dist->dhdr.as<DistHdr>();
+        const int r = rank[i];
+        const u64 n = P.count(r, k), p = P.count(r, k + 1);
+        hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, cx->stream, &dh->cell[k], direct ? n : ~0ull);
+        NodeLevel na;
+        na.k = k;
+        na.in = cur_in[i];
+        na.n = n;
+        na.p = p;
+        na.words = cur_out[i];
+        na.out = direct ? cx->nodes_out.as<uint2>() + node_base[i][k] : cx->dist->scratch.as<uint2>();
+        na.count = &h->count[kLayerSlot + k];
+        na.bound = prev_total;
+        na.prev_marks = k > 0;
+        na.pcount = &dh->cell[k];
+        na.id_off = u32(P.start(r, k + 1));
+        na.desc = cx->desc.as<u64>() + dcur[i];
+        dcur[i] += (p + kTile - 1) / kTile;
+        na.ticket = &h->ticket[kLayerSlot + k];
+        if (cx->node_level(na, h)) return dev_fail("node level");
+        RankLevel& rl = lv[i];
+        rl = RankLevel{};
+        rl.src.in = cur_in[i];
+        rl.src.n = n;
+        rl.src.p = p;
+        rl.src.words = cur_out[i];
+        const int cs = (k + 1) & 1, ps = k & 1;
+        rl.src.nf = cx->nf_set[cs];
+        rl.src.multi = cx->multi_set[cs];
+        rl.src.prev_nf = k > 0 ? cx->nf_set[ps] : nullptr;
+        rl.src.prev_multi = k > 0 ? cx->multi_set[ps] : nullptr;
+        rl.grid_elems = p;
+        rl.ucount = &h->count[kLayerSlot + k];
+        rl.w = cur_out[i];
+        rl.nf = cx->nf_set[cs];
+        rl.multi = cx->multi_set[cs];
+        rl.out = cx->nodes_out.as<uint2>() + node_base[i][k];
+      }
+      if (direct) {
+        for (int s = 0; s < R; ++s) { slice_off[k + 1][s] = P.start(s, k + 1); slice_cnt[k + 1][s] = P.count(s, k + 1); }
+        info.layer_size[k] = P.nk[k + 1];
+        prev_total = P.nk[k + 1];
+      } else {
+        std::vector<u64> nw(NL);
+        for (int i = 0; i < NL; ++i) nw[i] = P.count(rank[i], k + 1);
+        const int rc = exchange(lv, nw, c, off, total, &err_global, &err_sym, &ovf);
+        if (rc == kRetry) {
+          allow_packed = false;
+          retry = true;
+          break;
+        }
+        if (rc) return rc;
+        for (int s = 0; s < R; ++s) { slice_off[k + 1][s] = off[s]; slice_cnt[k + 1][s] = c[s]; }
+        info.layer_size[k] = total;
+        direct = total == P.nk[k + 1];
+        prev_total = total;
+      }
+      for (int i = 0; i < NL; ++i) std::swap(cur_in[i], cur_out[i]);
+    }
+    if (retry) continue;
+
+    // ---- gather the last distributed level to rank 0, finish the top there ----
+    {
+      std::vector<u64> cnt(R);
+      for (int s = 0; s < R; ++s) cnt[s] = P.count(s, G);
+      std::vector<const void*> sv;
+      void* recv0 = nullptr;
+      for (int i = 0; i < NL; ++i) {
+        sv.push_back(cur_in[i]);
+        if (rank[i] == 0) recv0 = ctx[i]->dist->tail_in.ptr;
+      }
+      if (!recv0) recv0 = ctx[0]->dist->tail_in.ptr;   // not used off rank 0
+      G_RC(tr->gather0(cnt, 4, sv, recv0));
+    }
+    for (int i = 0; i < NL; ++i) {
+      gcz_ctx* cx = ctx[i];
+      Header* h = cx->hdr.as<Header>();
+      DistHdr* dh = cx->dist->dhdr.as<DistHdr>();
+      const bool tail = rank[i] == 0;
+      if (tail) {
+        u32* in = cx->dist->tail_in.as<u32>();
+        u32* bufs[2] = {cx->wa.as<u32>(), cx->wb.as<u32>()};
+        int nb = 0;
+        u64 n = P.nk[G];
+        hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, cx->stream, &dh->cell[G], direct ? n : ~0ull);
+        u64 bound = prev_total;
+        for (int k = G; k < D; ++k) {
+          NodeLevel na;
+          na.k = k;
+          na.in = in;
+          na.n = n;
+          na.p = P.nk[k + 1];
+          na.words = bufs[nb];
+          na.out = cx->nodes_out.as<uint2>() + node_base[i][k];
+          na.count = &h->count[kLayerSlot + k];
+          na.bound = bound;
+          na.prev_marks = k > G;
+          na.pcount = k == G ? &dh->cell[G] : &h->count[kLayerSlot + k - 1];
+          na.desc = cx->desc.as<u64>() + dcur[i];
+          dcur[i] += (na.p + kTile - 1) / kTile;
+          na.ticket = &h->ticket[kLayerSlot + k];
+          if (cx->node_level(na, h)) return dev_fail("tail level");
+          in = bufs[nb];
+          nb ^= 1;
+          n = na.p;
+          bound = na.p;
+        }
+        hipLaunchKernelGGL(k_root, dim3(1), dim3(1), 0, cx->stream, in, h);
+      }
+      hipLaunchKernelGGL(k_dist_final, dim3(1), dim3(1), 0, cx->stream, h, dh, G, D, int(tail));
+      G_HIP(hipGetLastError());
+      G_HIP(hipEventRecord(cx->ev_stop, cx->stream));
+    }
+    {
+      std::vector<const void*> s;
+      std::vector<void*> rv;
+      for (gcz_ctx* cx : ctx) {
+        s.push_back(cx->dist->dhdr.as<DistHdr>()->final_vec);
+        rv.push_back(cx->dist->gathf.ptr);
+      }
+      G_RC(tr->allgather(kFinalWords * 8, s, rv));
+    }
+    gcz_dist_state& d0 = *ctx[0]->dist;
+    G_HIP(hipMemcpyAsync(d0.h_gathf, d0.gathf.ptr, size_t(R) * kFinalWords * 8, hipMemcpyDeviceToHost,
+                         ctx[0]->stream));
+    for (gcz_ctx* cx : ctx) G_HIP(hipStreamSynchronize(cx->stream));
+    int fo = 0;
+    for (int s = 0; s < R; ++s) fo |= int(d0.h_gathf[size_t(s) * kFinalWords]);
+    if (fo) {
+      allow_packed = false;
+      continue;
+    }
+    const u64* f0 = d0.h_gathf;   // rank 0's vector
+    info.root = u32(f0[1]);
+    for (int k = G; k < D; ++k) {
+      info.layer_size[k] = f0[4 + k];
+      slice_off[k + 1][0] = 0;
+      slice_cnt[k + 1][0] = f0[4 + k];
+    }
+    break;
+  }
+  info.n_layers = D;
+  double ms = 0;
+  for (gcz_ctx* cx : ctx) {
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, cx->ev_start, cx->ev_stop) == hipSuccess) ms = std::max(ms, double(t));
+  }
+  info.build_ms = ms;
+  for (gcz_ctx* cx : ctx) {
+    cx->info = info;
+    cx->info.status = GCZ_OK;
+  }
+  return GCZ_OK;
+}
+
+extern "C" {
+
+int gcz_dist_unique_id(void* out, uint64_t cap) {
+  if (!out || cap < NCCL_UNIQUE_ID_BYTES) return GCZ_ERR_ARG;
+  RcclApi& a = rccl();
+  if (!a.ok) return GCZ_ERR_DEVICE;
+  ncclUniqueId id;
+  if (a.GetUniqueId(&id) != ncclSuccess) return GCZ_ERR_DEVICE;
+  std::memcpy(out, &id, NCCL_UNIQUE_ID_BYTES);
+  return GCZ_OK;
+}
+
+int gcz_group_create_local(int device, int world, gcz_group** out) {
+  if (!out || world < 1 || world > kMaxRanks) return GCZ_ERR_ARG;
+  *out = nullptr;
+  auto* g = new gcz_group();
+  g->world = world;
+  g->owns_ctx = true;
+  auto* t = new LocalTransport();
+  t->world = world;
+  g->tr = t;
+  for (int r = 0; r < world; ++r) {
+    gcz_ctx* c = nullptr;
+    if (int rc = gcz_ctx_create(device, &c)) {
+      gcz_group_destroy(g);
+      return rc;
+    }
+    if (r > 0) c->stream = g->ctx[0]->stream;   // one stream: the copies order the ranks
+    g->ctx.push_back(c);
+    g->rank.push_back(r);
+  }
+  t->stream = g->ctx[0]->stream;
+  *out = g;
+  return GCZ_OK;
+}
+
+int gcz_group_create_rccl(gcz_ctx* ctx, int rank, int world, const void* unique_id, gcz_group** out) {
+  if (!ctx || !out || !unique_id || world < 1 || world > kMaxRanks || rank < 0 || rank >= world) return GCZ_ERR_ARG;
+  *out = nullptr;
+  RcclApi& a = rccl();
+  if (!a.ok) {
+    ctx->last_error = "librccl.so.1 could not be loaded";
+    return GCZ_ERR_DEVICE;
+  }
+  if (hipSetDevice(ctx->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  auto* t = new RcclTransport();
+  t->world = world;
+  t->me = rank;
+  t->stream = ctx->stream;
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id, NCCL_UNIQUE_ID_BYTES);
+  const ncclResult_t r = a.CommInitRank(&t->comm, world, id, rank);
+  if (r != ncclSuccess) {
+    ctx->last_error = std::string("ncclCommInitRank: ") + a.GetErrorString(r);
+    t->comm = nullptr;
+    delete t;
+    return GCZ_ERR_DEVICE;
+  }
+  auto* g = new gcz_group();
+  g->world = world;
+  g->tr = t;
+  g->ctx.push_back(ctx);
+  g->rank.push_back(rank);
+  *out = g;
+  return GCZ_OK;
+}
+
+void gcz_group_destroy(gcz_group* g) {
+  if (!g) return;
+  for (gcz_ctx* c : g->ctx) (void)hipStreamSynchronize(c->stream);
+  delete g->tr;
+  if (g->owns_ctx) {
+    // virtual ranks > 0 borrowed rank 0's stream
+    for (size_t i = 1; i < g->ctx.size(); ++i) g->ctx[i]->stream = g->ctx[i]->own_stream;
+    for (gcz_ctx* c : g->ctx) gcz_ctx_destroy(c);
+  }
+  delete g;
+}
+
+int gcz_group_n_local(const gcz_group* g) { return g ? int(g->ctx.size()) : 0; }
+int gcz_group_rank(const gcz_group* g, int i) { return g && i >= 0 && i < int(g->ctx.size()) ? g->rank[i] : -1; }
+int gcz_group_world(const gcz_group* g) { return g ? g->world : 0; }
+gcz_ctx* gcz_group_ctx(gcz_group* g, int i) { return g && i >= 0 && i < int(g->ctx.size()) ? g->ctx[i] : nullptr; }
+const char* gcz_group_last_error(const gcz_group* g) { return g ? g->last_error.c_str() : "null group"; }
+
+int gcz_dist_plan(uint64_t S, int world, int rank, uint64_t* s0, uint64_t* s1, int* G) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world) return GCZ_ERR_ARG;
+  if (S == 0) {
+    if (s0) *s0 = 0;
+    if (s1) *s1 = 0;
+    if (G) *G = 0;
+    return GCZ_OK;
+  }
+  DistPlan p;
+  p.make(S, world);
+  if (s0) *s0 = p.start(rank, 0);
+  if (s1) *s1 = p.end(rank, 0);
+  if (G) *G = p.G;
+  return GCZ_OK;
+}
+
+int gcz_group_build_device_bases(gcz_group* g, const void* const* d_bases, uint64_t S, int L) {
+  if (!g || !d_bases) return GCZ_ERR_ARG;
+  if (hipSetDevice(g->ctx[0]->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  return g->build(d_bases, nullptr, S, L);
+}
+
+int gcz_group_build_device_leaves(gcz_group* g, const uint64_t* const* d_leaves, uint64_t S, int L) {
+  if (!g || !d_leaves) return GCZ_ERR_ARG;
+  if (hipSetDevice(g->ctx[0]->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  return g->build(nullptr, reinterpret_cast<const u64* const*>(d_leaves), S, L);
+}
+
+int gcz_group_info(const gcz_group* g, gcz_info* out) {
+  if (!g || !out) return GCZ_ERR_ARG;
+  *out = g->info;
+  return GCZ_OK;
+}
+
+int gcz_group_slice(const gcz_group* g, int i, int layer, uint64_t* offset, uint64_t* count) {
+  if (!g || i < 0 || i >= int(g->ctx.size()) || g->info.status != GCZ_OK) return GCZ_ERR_ARG;
+  if (layer < -1 || layer >= g->info.n_layers) return GCZ_ERR_ARG;
+  const int r = g->rank[i];
+  if (offset) *offset = g->slice_off[layer + 1][r];
+  if (count) *count = g->slice_cnt[layer + 1][r];
+  return GCZ_OK;
+}
+
+int gcz_group_copy_slice(gcz_group* g, int i, int layer, void* host_out) {
+  uint64_t off = 0, cnt = 0;
+  if (int rc = gcz_group_slice(g, i, layer, &off, &cnt)) return rc;
+  if (!cnt) return GCZ_OK;
+  if (!host_out) return GCZ_ERR_ARG;
+  gcz_ctx* c = g->ctx[i];
+  if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  const void* src = layer < 0 ? c->leaves_out.ptr
+                              : static_cast<const void*>(c->nodes_out.as<uint2>() + g->node_base[i][layer]);
+  if (hipMemcpyAsync(host_out, src, cnt * 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess) return GCZ_ERR_DEVICE;
+  return hipStreamSynchronize(c->stream) == hipSuccess ? GCZ_OK : GCZ_ERR_DEVICE;
+}
+
+int gcz_group_fetch(gcz_group* g, gcz_tree* t) {
+  if (!g || !t || g->info.status != GCZ_OK || int(g->ctx.size()) != g->world) return GCZ_ERR_ARG;
+  t->L = g->info.L;
+  t->root = g->info.root;
+  t->leaves.assign(g->info.n_leaves, 0);
+  t->layers.assign(g->info.n_layers, {});
+  for (int k = 0; k < g->info.n_layers; ++k) t->layers[k].assign(2 * g->info.layer_size[k], 0);
+  for (int i = 0; i < g->world; ++i) {
+    for (int layer = -1; layer < g->info.n_layers; ++layer) {
+      uint64_t off = 0, cnt = 0;
+      if (int rc = gcz_group_slice(g, i, layer, &off, &cnt)) return rc;
+      if (!cnt) continue;
+      void* dst = layer < 0 ? static_cast<void*>(t->leaves.data() + off)
+                            : static_cast<void*>(t->layers[layer].data() + 2 * off);
+      if (int rc = gcz_group_copy_slice(g, i, layer, dst)) return rc;
+    }
+  }
+  return GCZ_OK;
+}
+
+}  // extern "C"

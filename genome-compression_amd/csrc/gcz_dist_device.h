@@ -1,0 +1,340 @@
+// Device code of the multi-rank build (gcz_dist.hip).
+//
+// R ranks own contiguous strand ranges (rank order = position order).  Every
+// hash-consed level runs the single-device kernels on the rank's own elements
+// (local ids = local first-occurrence ranks), then reconciles keys across
+// ranks through their owner rank (owner = mix(key) mod R):
+//
+//   A  every locally-first element that went through the table sends its key
+//      (bit 63: "repeats locally", node levels) to the owner;
+//   B  the owner replies per record: not-globally-first (another rank with a
+//      smaller rank id has the key) and globally-repeated;
+//   -  each rank ranks its globally-first keys in local order; an allgather of
+//      those counts gives every rank its id offset (rank order = position
+//      order, so offset + local rank = global first-occurrence rank);
+//   C  ranks send the global id of each record they own the first occurrence of;
+//   D  the owner returns the id for every record;
+//   -  local words are remapped to global ids, and globally-first uniques are
+//      compacted into the rank's slice of the output layer.
+//
+// Elements whose pair holds a child that occurs once globally (singleton
+// propagation, gcz_device.h) are unique everywhere and send nothing.
+#pragma once
+
+#include "gcz_device.h"
+
+namespace gcz_dev {
+
+constexpr int kMaxRanks = 31;              // owner slot state: one bit per rank + local-multi bit
+constexpr int kSyncWords = kMaxRanks + 4;  // per-rank sync vector (see DistHdr)
+constexpr int kFinalWords = 4 + GCZ_MAX_LAYERS;
+
+struct DistHdr {
+  // per-level sync vector: [0, R) records per owner, [R] overflow, [R+1] local uniques,
+  // [R+2] first bad symbol offset (local bytes), [R+3] that symbol
+  u64 sync[kSyncWords];
+  u64 cfirst;                           // globally-first local uniques of the level
+  u32 ticket;                           // look-back tickets of k_dist_rank
+  u32 pad;
+  u64 cell[GCZ_MAX_LAYERS + 1];         // direct flags: n_local when the layer is direct, else ~0
+  u64 final_vec[kFinalWords];           // [0] overflow, [1] root, [2] tail first layer, [4 + k] tail counts
+};
+
+struct Displ {   // segment starts of the R source (or destination) ranks in a buffer, plus the end
+  u64 d[kMaxRanks + 1];
+};
+
+__device__ __forceinline__ u32 seg_of(const Displ& D, u32 R, u64 k) {
+  u32 s = 0;
+  while (s + 1 < R && k >= D.d[s + 1]) ++s;
+  return s;
+}
+
+__device__ __forceinline__ u32 owner_of(u64 key, u32 R) {
+  u64 h = key * 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ull;
+  h ^= h >> 29;
+  return u32(((h >> 32) * u64(R)) >> 32);
+}
+
+constexpr u64 kLocalMulti = 1ull << 63;
+
+// The elements of a level that send a record.
+struct RecSrc {
+  // leaf levels: local unique ids [0, *ucount), key = leaves[lid]
+  const u64* leaves;
+  const u64* ucount;
+  // node levels: positions [0, p)
+  const u32* in;
+  u64 n, p;
+  const u32* words;                    // final local words
+  const unsigned char* nf;
+  const unsigned char* multi;
+  const unsigned char* prev_nf;        // null: every locally-first pair sends
+  const unsigned char* prev_multi;
+  u32 R;
+};
+
+__device__ __forceinline__ bool rec_get(const RecSrc& s, u64 e, u64& key, u32& lid) {
+  if (s.leaves) {
+    if (e >= *s.ucount) return false;
+    key = s.leaves[e];
+    lid = u32(e);
+    return true;
+  }
+  if (e >= s.p || s.nf[e] != kNfMaybe) return false;
+  if (s.prev_nf) {
+    bool single;
+    if (2 * e + 1 < s.n) {
+      const uchar2 f = reinterpret_cast<const uchar2*>(s.prev_nf)[e];
+      const uchar2 g = reinterpret_cast<const uchar2*>(s.prev_multi)[e];
+      single = (f.x == 0 && g.x == 0) || (f.y == 0 && g.y == 0);
+    } else {
+      single = s.prev_nf[2 * e] == 0 && s.prev_multi[2 * e] == 0;
+    }
+    if (single) return false;
+  }
+  u32 l, r, cl, cr, m, t;
+  load_pair(s.in, s.n, e, l, r);
+  node_canonical(l, r, cl, cr, m, t);
+  key = ((u64(ulw(cl)) << 31) | ulw(cr)) | (s.multi[e] ? kLocalMulti : 0ull);
+  lid = s.words[e] & kIdx;
+  return true;
+}
+
+__device__ __forceinline__ u64 rec_key(const RecSrc& s, u64 key) { return s.leaves ? key : (key & ~kLocalMulti); }
+
+// Bucketing by owner, deterministic two-pass: per-block counts, one scan, scatter.
+static __global__ __launch_bounds__(kBlock) void k_bucket_count(RecSrc s, u32* __restrict__ blockcnt, u32 nb) {
+  __shared__ u32 h[kMaxRanks];
+  const int tid = threadIdx.x;
+  if (tid < int(s.R)) h[tid] = 0;
+  __syncthreads();
+#pragma unroll 4
+  for (int e = 0; e < kItems; ++e) {
+    const u64 idx = u64(blockIdx.x) * kTile + u64(e) * kBlock + tid;
+    u64 key;
+    u32 lid;
+    if (rec_get(s, idx, key, lid)) atomicAdd(&h[owner_of(rec_key(s, key), s.R)], 1u);
+  }
+  __syncthreads();
+  if (tid < int(s.R)) blockcnt[u64(tid) * nb + blockIdx.x] = h[tid];
+}
+
+// One block: exclusive scan of blockcnt[R * nb] (destination-major) in place;
+// per-destination totals into tot[0..R).
+static __global__ __launch_bounds__(1024) void k_bucket_scan(u32* __restrict__ a, u64 N, u32 R, u32 nb,
+                                                             u64* __restrict__ tot) {
+  __shared__ u32 part[1024];
+  const int tid = threadIdx.x;
+  const u64 per = (N + 1023) / 1024;
+  const u64 b0 = u64(tid) * per, b1 = b0 + per < N ? b0 + per : N;
+  u32 sum = 0;
+  for (u64 i = b0; i < b1; ++i) sum += a[i];
+  part[tid] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {   // Hillis-Steele inclusive scan
+    const u32 v = tid >= o ? part[tid - o] : 0u;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  u32 run = part[tid] - sum;
+  for (u64 i = b0; i < b1; ++i) {
+    const u32 v = a[i];
+    a[i] = run;
+    run += v;
+  }
+  __syncthreads();
+  if (tid < int(R)) {
+    const u64 i0 = u64(tid) * nb, i1 = u64(tid + 1) * nb;
+    const u32 start = i0 < N ? a[i0] : part[1023];
+    const u32 end = i1 < N ? a[i1] : part[1023];
+    tot[tid] = u64(end - start);
+  }
+}
+
+static __global__ __launch_bounds__(kBlock) void k_bucket_scatter(RecSrc s, const u32* __restrict__ boff, u32 nb,
+                                                                  u64* __restrict__ skey, u32* __restrict__ sidx) {
+  __shared__ u32 cur[kMaxRanks];
+  const int tid = threadIdx.x;
+  if (tid < int(s.R)) cur[tid] = boff[u64(tid) * nb + blockIdx.x];
+  __syncthreads();
+#pragma unroll 4
+  for (int e = 0; e < kItems; ++e) {
+    const u64 idx = u64(blockIdx.x) * kTile + u64(e) * kBlock + tid;
+    u64 key;
+    u32 lid;
+    if (rec_get(s, idx, key, lid)) {
+      const u32 o = atomicAdd(&cur[owner_of(rec_key(s, key), s.R)], 1u);
+      skey[o] = key;
+      sidx[o] = lid;
+    }
+  }
+}
+
+// ---- owner side ----------------------------------------------------------------
+// Slot = {key ^ 1, ~state, id}: state bit r = rank r holds the key, bit 31 = some
+// rank holds it more than once.  memset 0xff clears (EMPTY key, state 0, id ~0).
+struct OwnTab {
+  Slot* tab;
+  u32 mask;
+};
+
+static __global__ __launch_bounds__(kBlock) void k_own_insert(const u64* __restrict__ rkey, u64 nrecv, Displ D,
+                                                              u32 R, int leaves, OwnTab T, u32* __restrict__ oslot,
+                                                              u64* __restrict__ ovf) {
+  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= nrecv) return;
+  const u32 src = seg_of(D, R, k);
+  const u64 raw = rkey[k];
+  const u64 key = leaves ? raw : (raw & ~kLocalMulti);
+  const u32 lm = leaves ? 0u : u32(raw >> 63);
+  const u64 skey = key ^ 1ull;
+  u32 s = slot_hash(skey) & T.mask;
+  for (u32 probe = 0; probe <= T.mask; ++probe) {
+    u64 cur = T.tab[s].key;
+    if (cur == kEmpty) cur = atomicCAS(&T.tab[s].key, kEmpty, skey);
+    if (cur == kEmpty || cur == skey) {
+      atomicAnd(&T.tab[s].pos, ~((1u << src) | (lm << 31)));
+      oslot[k] = s;
+      return;
+    }
+    s = (s + 1) & T.mask;
+  }
+  atomicOr(ovf, 1ull);
+  oslot[k] = 0;
+}
+
+// reply bit 0: another rank before this one holds the key; bit 1: the key repeats globally
+static __global__ __launch_bounds__(kBlock) void k_own_reply(const u32* __restrict__ oslot, u64 nrecv, Displ D,
+                                                             u32 R, OwnTab T, unsigned char* __restrict__ rflag) {
+  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= nrecv) return;
+  const u32 src = seg_of(D, R, k);
+  const u32 st = ~T.tab[oslot[k]].pos;
+  const u32 ranks = st & 0x7fffffffu;
+  const u32 minr = u32(__ffs(ranks) - 1);
+  const u32 gm = (__popc(ranks) > 1) | (st >> 31);
+  rflag[k] = (unsigned char)((minr != src) | (gm << 1));
+}
+
+static __global__ __launch_bounds__(kBlock) void k_own_setid(const u32* __restrict__ oslot, u64 nrecv,
+                                                             const u32* __restrict__ cval, OwnTab T) {
+  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= nrecv) return;
+  const u32 v = cval[k];
+  if (v != ~0u) T.tab[oslot[k]].pad = v;
+}
+
+static __global__ __launch_bounds__(kBlock) void k_own_getid(const u32* __restrict__ oslot, u64 nrecv, OwnTab T,
+                                                             u32* __restrict__ dval) {
+  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= nrecv) return;
+  dval[k] = T.tab[oslot[k]].pad;
+}
+
+// ---- sender side ---------------------------------------------------------------
+
+static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restrict__ sidx, u64 nsent,
+                                                              const unsigned char* __restrict__ sflag,
+                                                              unsigned char* __restrict__ gnf,
+                                                              unsigned char* __restrict__ gmul) {
+  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= nsent) return;
+  const u32 lid = sidx[k];
+  const unsigned char f = sflag[k];
+  gnf[lid] = f & 1;
+  gmul[lid] = (f >> 1) & 1;
+}
+
+// Rank of each globally-first local unique among them (local order); total -> *count_out.
+static __global__ __launch_bounds__(kBlock) void k_dist_rank(const unsigned char* __restrict__ gnf,
+                                                             const u64* __restrict__ ucount,
+                                                             u32* __restrict__ gid, u64* __restrict__ desc,
+                                                             u32* __restrict__ ticket, u64* __restrict__ count_out) {
+  __shared__ u32 s_tile;
+  __shared__ u32 s_pre[kGroupsPerTile];
+  const u64 u = *ucount;
+  if (u64(blockIdx.x) * kTile >= u) {          // grid sized for the capacity: surplus tiles leave
+    return;
+  }
+  TileScan<kItems> ts;
+  tile_scan(ts, &s_tile, s_pre, gnf, 0, u, 0, desc, ticket, count_out);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const u64 lt = (1ull << lane) - 1;
+#pragma unroll
+  for (int e = 0; e < kItems; ++e) {
+    const u64 j = ts.base + u64(e) * kBlock + tid;
+    if (j < u && ((ts.mask[e] >> lane) & 1ull)) gid[j] = s_pre[e * 4 + wave] + u32(__popcll(ts.mask[e] & lt));
+  }
+}
+
+// Globally-first uniques: compact into the rank's output slice, globalise their ids.
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_dist_finalize(const u64* __restrict__ ucount,
+                                                          const unsigned char* __restrict__ gnf,
+                                                          u32* __restrict__ gid, u32 off,
+                                                          const T* __restrict__ scratch, T* __restrict__ out) {
+  const u64 lid = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (lid >= *ucount || gnf[lid]) return;
+  const u32 r = gid[lid];
+  out[r] = scratch[lid];
+  gid[lid] = off + r;
+}
+
+static __global__ __launch_bounds__(kBlock) void k_dist_cvals(const u32* __restrict__ sidx, u64 nsent,
+                                                              const unsigned char* __restrict__ gnf,
+                                                              const u32* __restrict__ gid, u32* __restrict__ cval) {
+  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= nsent) return;
+  const u32 lid = sidx[k];
+  cval[k] = gnf[lid] ? ~0u : gid[lid];
+}
+
+static __global__ __launch_bounds__(kBlock) void k_dist_dvals(const u32* __restrict__ sidx, u64 nsent,
+                                                              const unsigned char* __restrict__ gnf,
+                                                              const u32* __restrict__ dval, u32* __restrict__ gid) {
+  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= nsent) return;
+  const u32 lid = sidx[k];
+  if (gnf[lid]) gid[lid] = dval[k];
+}
+
+// Local words -> global ids; locally-first elements whose key repeats on
+// another rank are marked multi (the next level's singleton test).
+static __global__ __launch_bounds__(kBlock) void k_dist_remap(u32* __restrict__ words, u64 p,
+                                                              const unsigned char* __restrict__ nf,
+                                                              unsigned char* __restrict__ multi,
+                                                              const u32* __restrict__ gid,
+                                                              const unsigned char* __restrict__ gmul) {
+  const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= p) return;
+  const u32 w = words[j];
+  const u32 lid = w & kIdx;
+  words[j] = gid[lid] | (w & kBits);
+  if (multi && nf[j] == kNfMaybe && gmul[lid]) multi[j] = 1;
+}
+
+static __global__ void k_dist_pack(const Header* __restrict__ h, const u64* __restrict__ ucount,
+                                   const unsigned char* __restrict__ bases, DistHdr* __restrict__ dh, u32 R) {
+  dh->sync[R] = u64(h->overflow | h->leaf_overflow);
+  dh->sync[R + 1] = ucount ? *ucount : 0ull;
+  const u64 e = h->err_offset;
+  dh->sync[R + 2] = e;
+  dh->sync[R + 3] = (e != ~0ull && bases) ? u64(bases[e]) : 0ull;
+}
+
+static __global__ void k_dist_final(const Header* __restrict__ h, DistHdr* __restrict__ dh, int tail0, int D,
+                                    int has_tail) {
+  dh->final_vec[0] = u64(h->overflow | h->leaf_overflow);
+  dh->final_vec[1] = has_tail ? u64(h->root) : 0ull;
+  dh->final_vec[2] = u64(tail0);
+  for (int k = 0; k < GCZ_MAX_LAYERS; ++k)
+    dh->final_vec[4 + k] = (has_tail && k >= tail0 && k < D) ? h->count[kLayerSlot + k] : 0ull;
+}
+
+static __global__ void k_set_u64(u64* p, u64 v) { *p = v; }
+
+}  // namespace gcz_dev

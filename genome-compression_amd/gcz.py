@@ -89,6 +89,23 @@ _SIGS = {
     "gcz_fasta_extract": (_U64, [_P, _U64, _P]),
     "gcz_synth_fill": (None, [_P, ctypes.c_int, _U64, _U64, _U64]),
     "gcz_synth_default_seed": (_U64, []),
+    "gcz_dist_unique_id": (ctypes.c_int, [_P, _U64]),
+    "gcz_group_create_rccl": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _P, ctypes.POINTER(_P)]),
+    "gcz_group_create_local": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
+    "gcz_group_destroy": (None, [_P]),
+    "gcz_group_world": (ctypes.c_int, [_P]),
+    "gcz_group_n_local": (ctypes.c_int, [_P]),
+    "gcz_group_rank": (ctypes.c_int, [_P, ctypes.c_int]),
+    "gcz_group_ctx": (_P, [_P, ctypes.c_int]),
+    "gcz_group_last_error": (ctypes.c_char_p, [_P]),
+    "gcz_dist_plan": (ctypes.c_int, [_U64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_U64), ctypes.POINTER(_U64),
+                                      ctypes.POINTER(ctypes.c_int)]),
+    "gcz_group_build_device_bases": (ctypes.c_int, [_P, ctypes.POINTER(_P), _U64, ctypes.c_int]),
+    "gcz_group_build_device_leaves": (ctypes.c_int, [_P, ctypes.POINTER(_P), _U64, ctypes.c_int]),
+    "gcz_group_info": (ctypes.c_int, [_P, ctypes.POINTER(_Info)]),
+    "gcz_group_slice": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
+    "gcz_group_copy_slice": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _P]),
+    "gcz_group_fetch": (ctypes.c_int, [_P, _P]),
 }
 for _name, (_res, _args) in _SIGS.items():
     _f = getattr(_lib, _name)
@@ -215,6 +232,31 @@ class Tree:
         return b"".join(out)
 
 
+def dist_plan(S: int, world: int, rank: int):
+    """Strands [s0, s1) owned by `rank` and the number G of distributed node levels."""
+    s0, s1, g = _U64(), _U64(), ctypes.c_int()
+    rc = _lib.gcz_dist_plan(S, world, rank, ctypes.byref(s0), ctypes.byref(s1), ctypes.byref(g))
+    if rc != GCZ_OK:
+        raise GczError(rc, "gcz_dist_plan: bad arguments")
+    return int(s0.value), int(s1.value), int(g.value)
+
+
+def dist_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    rc = _lib.gcz_dist_unique_id(buf, 128)
+    if rc != GCZ_OK:
+        raise GczError(rc, "gcz_dist_unique_id failed (RCCL not loadable)")
+    return buf.raw
+
+
+def _info_dict(i):
+    return {"status": i.status, "L": i.L, "n_layers": i.n_layers, "root": i.root,
+            "n_strands": i.n_strands, "n_leaves": i.n_leaves,
+            "layer_size": [int(i.layer_size[k]) for k in range(i.n_layers)],
+            "error_offset": i.error_offset, "error_symbol": i.error_symbol, "build_ms": i.build_ms,
+            "hashed_pairs": i.hashed_pairs}
+
+
 def _sha(b):
     return hashlib.sha256(b).hexdigest()
 
@@ -254,7 +296,11 @@ class DeviceBuffer:
 class Context:
     """One GPU, one stream, a reusable workspace (gcz_ctx)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, _borrowed=None):
+        self._owned = _borrowed is None
+        if _borrowed is not None:
+            self._h = ctypes.c_void_p(_borrowed)
+            return
         h = ctypes.c_void_p()
         rc = _lib.gcz_ctx_create(device, ctypes.byref(h))
         if rc != GCZ_OK:
@@ -262,9 +308,9 @@ class Context:
         self._h = h
 
     def close(self):
-        if getattr(self, "_h", None):
+        if getattr(self, "_h", None) and getattr(self, "_owned", True):
             _lib.gcz_ctx_destroy(self._h)
-            self._h = None
+        self._h = None
 
     __del__ = close
 
@@ -297,11 +343,7 @@ class Context:
     def info(self) -> dict:
         i = _Info()
         _lib.gcz_info_get(self._h, ctypes.byref(i))
-        return {"status": i.status, "L": i.L, "n_layers": i.n_layers, "root": i.root,
-                "n_strands": i.n_strands, "n_leaves": i.n_leaves,
-                "layer_size": [int(i.layer_size[k]) for k in range(i.n_layers)],
-                "error_offset": i.error_offset, "error_symbol": i.error_symbol, "build_ms": i.build_ms,
-                "hashed_pairs": i.hashed_pairs}
+        return _info_dict(i)
 
     def build_fasta(self, data: bytes, L: int = 12) -> dict:
         buf = np.frombuffer(data, dtype=np.uint8)
@@ -341,3 +383,94 @@ class Context:
             out[name.value.decode()] = {"launches": int(n.value), "total_ms": float(ms.value)}
             k += 1
         return out
+
+
+# ---- multi-rank build -----------------------------------------------------------
+class Group:
+    """Ranks of a multi-rank build (gcz_group): `Group.local(world)` runs `world`
+    virtual ranks on one device (tests); `Group.rccl(ctx, rank, world, uid)` is one
+    rank per process and GPU (bench).  Rank r owns strands dist_plan(S, world, r)."""
+
+    def __init__(self, handle, keep=None):
+        self._h = handle
+        self._keep = keep
+
+    @classmethod
+    def local(cls, world: int, device: int = 0):
+        h = ctypes.c_void_p()
+        rc = _lib.gcz_group_create_local(device, world, ctypes.byref(h))
+        if rc != GCZ_OK:
+            raise GczError(rc, f"gcz_group_create_local(world={world}) failed")
+        return cls(h)
+
+    @classmethod
+    def rccl(cls, ctx: Context, rank: int, world: int, unique_id: bytes):
+        h = ctypes.c_void_p()
+        uid = ctypes.create_string_buffer(unique_id, 128)
+        rc = _lib.gcz_group_create_rccl(ctx._h, rank, world, uid, ctypes.byref(h))
+        if rc != GCZ_OK:
+            raise GczError(rc, "gcz_group_create_rccl failed: " + _lib.gcz_ctx_last_error(ctx._h).decode())
+        return cls(h, keep=ctx)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.gcz_group_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    @property
+    def world(self):
+        return _lib.gcz_group_world(self._h)
+
+    @property
+    def n_local(self):
+        return _lib.gcz_group_n_local(self._h)
+
+    def rank(self, i=0):
+        return _lib.gcz_group_rank(self._h, i)
+
+    def ctx(self, i=0) -> Context:
+        return Context(_borrowed=_lib.gcz_group_ctx(self._h, i))
+
+    def build_device_bases(self, dev_ptrs, S: int, L: int = 12) -> dict:
+        arr = (ctypes.c_void_p * len(dev_ptrs))(*[ctypes.c_void_p(p) for p in dev_ptrs])
+        rc = _lib.gcz_group_build_device_bases(self._h, arr, S, L)
+        if rc != GCZ_OK:
+            raise GczError(rc, _lib.gcz_group_last_error(self._h).decode(), self.info())
+        return self.info()
+
+    def build_device_leaves(self, dev_ptrs, S: int, L: int = 12) -> dict:
+        arr = (ctypes.c_void_p * len(dev_ptrs))(*[ctypes.c_void_p(p) for p in dev_ptrs])
+        rc = _lib.gcz_group_build_device_leaves(self._h, arr, S, L)
+        if rc != GCZ_OK:
+            raise GczError(rc, _lib.gcz_group_last_error(self._h).decode(), self.info())
+        return self.info()
+
+    def info(self) -> dict:
+        i = _Info()
+        _lib.gcz_group_info(self._h, ctypes.byref(i))
+        return _info_dict(i)
+
+    def slice(self, i: int, layer: int):
+        off, cnt = _U64(), _U64()
+        rc = _lib.gcz_group_slice(self._h, i, layer, ctypes.byref(off), ctypes.byref(cnt))
+        if rc != GCZ_OK:
+            raise GczError(rc, "gcz_group_slice failed")
+        return int(off.value), int(cnt.value)
+
+    def copy_slice(self, i: int, layer: int) -> np.ndarray:
+        _, cnt = self.slice(i, layer)
+        out = np.empty(cnt if layer < 0 else 2 * cnt, dtype=np.uint64 if layer < 0 else np.uint32)
+        rc = _lib.gcz_group_copy_slice(self._h, i, layer, _ptr(out))
+        if rc != GCZ_OK:
+            raise GczError(rc, "gcz_group_copy_slice failed")
+        return out
+
+    def tree(self) -> Tree:
+        t = _lib.gcz_tree_new()
+        rc = _lib.gcz_group_fetch(self._h, t)
+        if rc != GCZ_OK:
+            _lib.gcz_tree_free(t)
+            raise GczError(rc, "gcz_group_fetch failed")
+        return Tree(t)

@@ -149,6 +149,39 @@ GCZ_API uint64_t gcz_fasta_extract(const uint8_t *file, uint64_t n, uint8_t *out
 GCZ_API void gcz_synth_fill(char *out, int kind, uint64_t seed, uint64_t begin, uint64_t end);
 GCZ_API uint64_t gcz_synth_default_seed(void);
 
+/* ---- multi-rank build ---------------------
+ * R ranks own contiguous strand ranges; every hash-consed level is reconciled
+ * through key owners (all-to-all), ids stay the global first-occurrence ranks,
+ * so rank r holds a contiguous slice [offset, offset + count) of every layer
+ * and the layers are the rank-ordered concatenation of the slices (identical
+ * to gcz_build_*).  Rank order = position order.  Replaces the same
+ * tree_constructor::reduce as gcz_build_device_bases, spread over GPUs. */
+typedef struct gcz_group gcz_group;
+/* 128-byte RCCL unique id (rank 0 creates it, every rank passes it to create). */
+GCZ_API int gcz_dist_unique_id(void *out, uint64_t cap);
+/* One rank of a `world`-rank job on ctx's device (one process per GPU, RCCL). */
+GCZ_API int gcz_group_create_rccl(gcz_ctx *ctx, int rank, int world, const void *unique_id, gcz_group **out);
+/* `world` virtual ranks sharing one device, exchanges as device copies (testing). */
+GCZ_API int gcz_group_create_local(int device, int world, gcz_group **out);
+GCZ_API void gcz_group_destroy(gcz_group *g);
+GCZ_API int gcz_group_world(const gcz_group *g);
+GCZ_API int gcz_group_n_local(const gcz_group *g);          /* ranks driven by this process */
+GCZ_API int gcz_group_rank(const gcz_group *g, int local);
+GCZ_API gcz_ctx *gcz_group_ctx(gcz_group *g, int local);
+GCZ_API const char *gcz_group_last_error(const gcz_group *g);
+/* Strands [s0, s1) of `rank` for an S-strand genome; G = distributed node levels. */
+GCZ_API int gcz_dist_plan(uint64_t S, int world, int rank, uint64_t *s0, uint64_t *s1, int *G);
+/* d_bases[i]: device ASCII bases of local rank i's strands ((s1 - s0) * L bytes). */
+GCZ_API int gcz_group_build_device_bases(gcz_group *g, const void *const *d_bases, uint64_t S, int L);
+/* d_leaves[i]: device packed strands [s0, s1) of local rank i (shared_tree(std::vector<dna>&)). */
+GCZ_API int gcz_group_build_device_leaves(gcz_group *g, const uint64_t *const *d_leaves, uint64_t S, int L);
+GCZ_API int gcz_group_info(const gcz_group *g, gcz_info *out);   /* whole-tree summary */
+/* Slice of local rank i in layer (-1 = leaves): ids [offset, offset + count). */
+GCZ_API int gcz_group_slice(const gcz_group *g, int local, int layer, uint64_t *offset, uint64_t *count);
+GCZ_API int gcz_group_copy_slice(gcz_group *g, int local, int layer, void *host_out);
+/* Whole tree to the host (every rank local, i.e. gcz_group_create_local). */
+GCZ_API int gcz_group_fetch(gcz_group *g, gcz_tree *t);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,167 @@
+"""Multi-rank build (gcz_group) against the reference goldens.
+
+The GPU tests run R virtual ranks on one MI355X (gcz_group_create_local): every
+kernel of the distributed path (bucketing, owner tables, id scan, compaction,
+remap, gather, tail) runs exactly as with one rank per GPU; only the exchange is
+a device copy instead of an RCCL send/recv.  The rank-ordered concatenation of
+the slices must equal the reference's tree byte for byte.
+
+The CPU tests check the partition (gcz_dist_plan) properties the algorithm
+relies on.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, case_input, compare_digest
+
+
+# ---- partition (host logic, no GPU) ----------------------------------------------
+@pytest.mark.parametrize("S", [1, 2, 7, 9, 100, 1023, 4096, 10085, 1 << 20, 83_333_333, 266_666_666])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_dist_plan_partition(gcz, S, world):
+    parts = [gcz.dist_plan(S, world, r) for r in range(world)]
+    G = parts[0][2]
+    assert all(p[2] == G for p in parts)
+    # contiguous, rank order = position order, covers [0, S)
+    assert parts[0][0] == 0 and parts[-1][1] == S
+    for a, b in zip(parts, parts[1:]):
+        assert a[1] == b[0]
+    # every nonempty rank boundary is a multiple of 2^G: levels < G pair within a rank
+    for s0, s1, _ in parts:
+        if s0 < S:
+            assert s0 % (1 << G) == 0
+    # after G levels each nonempty rank still holds >= 256 elements (except tiny inputs)
+    if G > 0:
+        sizes = [s1 - s0 for s0, s1, _ in parts if s1 > s0]
+        assert min(sizes[:-1] or sizes) >> G >= 256
+
+
+# ---- GPU: virtual ranks vs the reference ----------------------------------------------
+def _cases(max_bases, kinds=("fasta", "synth", "leaves")):
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        m = json.load(f)
+    out = []
+    for n, c in sorted(m.items()):
+        if c["kind"] not in kinds or c["expect"]["exit"] != 0:
+            continue
+        if c["kind"] == "synth" and c["nbases"] > max_bases:
+            continue
+        out.append(n)
+    return out
+
+
+def _dist_build(gcz, group, kind, payload, L):
+    """Upload the whole input once, hand every virtual rank a pointer to its strands."""
+    ctx0 = group.ctx(0)
+    if kind == "fasta":
+        bases = np.frombuffer(gcz.fasta_extract(payload), dtype=np.uint8)
+        S = len(bases) // L
+        buf = ctx0.upload(bases if len(bases) else np.zeros(1, np.uint8))
+        ptrs = [buf.ptr + gcz.dist_plan(max(S, 1), group.world, r)[0] * L for r in range(group.world)]
+        try:
+            return group.build_device_bases(ptrs, S, L)
+        finally:
+            buf.free()
+    leaves = np.ascontiguousarray(payload, dtype=np.uint64)
+    S = leaves.size
+    buf = ctx0.upload(leaves if S else np.zeros(1, np.uint64))
+    ptrs = [buf.ptr + gcz.dist_plan(max(S, 1), group.world, r)[0] * 8 for r in range(group.world)]
+    try:
+        return group.build_device_leaves(ptrs, S, L)
+    finally:
+        buf.free()
+
+
+@pytest.fixture(scope="module")
+def groups(gcz):
+    gs = {}
+    yield lambda w: gs.setdefault(w, gcz.Group.local(w))
+    for g in gs.values():
+        g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("name", _cases(12_000_000))
+def test_dist_matches_reference_goldens(name, world, gcz, manifest, groups):
+    case = manifest[name]
+    exp = case["expect"]
+    kind, payload, L = case_input(case, gcz)
+    g = groups(world)
+    info = _dist_build(gcz, g, kind, payload, L)
+    assert info["n_strands"] == exp["width"]
+    got = gcz.digest(g.tree())
+    assert compare_digest(got, exp) == {}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 5, 16])
+def test_dist_random_iupac_vs_oracle(world, gcz, oracle, groups):
+    """Random IUPAC genomes with planted repeats: every rank holds repeats of the others' keys."""
+    rng = np.random.default_rng(7 + world)
+    alphabet = np.frombuffer(b"ACGTRYKMBVDHSWN-acgt", dtype=np.uint8)
+    for L, n in [(12, 300_000), (5, 77_777), (16, 123_456), (3, 50_001)]:
+        base = alphabet[rng.integers(0, 6, size=n)]
+        # plant copies of early segments late in the genome (cross-rank repeats)
+        for _ in range(20):
+            a = int(rng.integers(0, n // 2))
+            b = int(rng.integers(n // 2, n - 2000))
+            base[b:b + 2000] = base[a:a + 2000]
+        data = base.tobytes()
+        ref = oracle.build_fasta(data, L)
+        info = _dist_build(gcz, groups(world), "fasta", data, L)
+        t = groups(world).tree()
+        assert info["n_leaves"] == len(ref.leaves())
+        assert np.array_equal(t.leaves(), ref.leaves())
+        for k in range(ref.n_layers):
+            assert np.array_equal(t.layer(k), ref.layer(k)), (L, k)
+        assert t.root == ref.root
+
+
+@pytest.mark.gpu
+def test_dist_bad_symbol_reports_first_offset(gcz, groups):
+    g = groups(3)
+    data = bytearray(gcz.synth(0, 1_200_000).tobytes())
+    data[900_001] = ord("x")     # on the last rank
+    data[700_005] = ord("!")     # earlier, on rank 1 or 2: this one is reported
+    with pytest.raises(gcz.GczError) as ei:
+        _dist_build(gcz, g, "fasta", bytes(data), 12)
+    assert ei.value.code == gcz.GCZ_ERR_SYMBOL
+    assert ei.value.info["error_offset"] == 700_005
+    assert ei.value.info["error_symbol"] == ord("!")
+    # the group is reusable after an error
+    info = _dist_build(gcz, g, "fasta", gcz.synth(0, 100_000).tobytes(), 12)
+    assert info["status"] == 0
+
+
+@pytest.mark.gpu
+def test_dist_equals_single_device_tandem(gcz, groups):
+    """Tandem repeats (hot keys on every rank): 4 ranks == one device, all layers."""
+    data = gcz.synth(1, 20_000_000).tobytes()
+    ctx = gcz.Context(0)
+    try:
+        ctx.build_fasta(data, 12)
+        single = ctx.tree()
+        _dist_build(gcz, groups(4), "fasta", data, 12)
+        multi = groups(4).tree()
+        assert np.array_equal(single.leaves(), multi.leaves())
+        assert single.n_layers == multi.n_layers
+        for k in range(single.n_layers):
+            assert np.array_equal(single.layer(k), multi.layer(k)), k
+        assert single.root == multi.root
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+@pytest.mark.parametrize("world", [2, 8])
+def test_dist_synth_100m(world, gcz, manifest, groups):
+    for name in ("synth/uniform_100000003", "synth/tandem_100000000"):
+        case = manifest[name]
+        kind, payload, L = case_input(case, gcz)
+        _dist_build(gcz, groups(world), kind, payload, L)
+        assert compare_digest(gcz.digest(groups(world).tree()), case["expect"]) == {}
