@@ -7,10 +7,15 @@ with the ASCII bases already resident in HBM (SURVEY §8(d) timing scope).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config uniform_1g]
 
-N > 1 is launched by torch.distributed.run (one process per GPU).  Each rank
-then builds its own shard genome (a different seed, same size): the per-GPU
-work is fixed, so the scaling mode is "weak"; no collective is on the data
-path (multi-GPU).
+N > 1 is launched by torch.distributed.run (one process per GPU).  Default
+(--mode dist): the ONE 1 Gbase genome is partitioned over the ranks
+(gcz_dist_plan: contiguous strand ranges, rank order = position order); each
+rank generates only its own bases, and every hash-consed level reconciles keys
+through their owner rank with RCCL all-to-all over xGMI (gcz_group, DESIGN.md
+§7).  Total work is fixed: "scaling": "strong".  --mode replicas runs N
+independent builds of N different genomes (weak scaling, no data-path
+collective) for comparison.  --virtual R (one GPU) runs the distributed path
+with R virtual ranks on one device, to measure its overhead.
 
 Printed (rank 0): ONE JSON line with value, roofline of the dominant kernel,
 the CPU baseline (compiled reference on this host, bounded sample) and the
@@ -118,6 +123,34 @@ def cpu_baseline(sample_bases):
             "sample": f"synthetic uniform ACGT, {sample_bases} bases, oracle/gcz_oracle.c"}
 
 
+def gather_tree(gcz, group, dist, rank, world, L):
+    """Rank slices -> rank 0 (gloo point-to-point): the whole tree for the parity check."""
+    info = group.info()
+    if world == 1:
+        return group.tree()
+    import torch   # already imported before libgcz when world > 1 (one HIP runtime)
+    layers = list(range(-1, info["n_layers"]))
+    if rank != 0:
+        for layer in layers:
+            a = group.copy_slice(0, layer)
+            dist.send(torch.tensor([a.size], dtype=torch.int64), 0)
+            if a.size:
+                dist.send(torch.from_numpy(a.view(np.int64) if layer < 0 else a.view(np.int32)), 0)
+        return None
+    parts = {layer: [group.copy_slice(0, layer)] for layer in layers}
+    for src in range(1, world):
+        for layer in layers:
+            n = torch.zeros(1, dtype=torch.int64)
+            dist.recv(n, src)
+            n = int(n.item())
+            if n:
+                t = torch.empty(n, dtype=torch.int64 if layer < 0 else torch.int32)
+                dist.recv(t, src)
+                parts[layer].append(t.numpy().view(np.uint64 if layer < 0 else np.uint32))
+    leaves = np.concatenate(parts[-1])
+    return gcz.Tree.from_arrays(L, leaves, [np.concatenate(parts[k]) for k in layers[1:]], info["root"])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -127,6 +160,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=120_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--mode", choices=["dist", "replicas"], default="dist", help="N > 1: one genome or N genomes")
+    ap.add_argument("--virtual", type=int, default=0, help="N = 1: distributed path with R virtual ranks")
+    ap.add_argument("--rccl-world1", action="store_true", help="N = 1: the RCCL group path with one rank")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -145,53 +181,90 @@ def main():
     cfg = CONFIGS[args.config]
     L = 12
     nbases = cfg["nbases"]
-    seed = gcz._lib.gcz_synth_default_seed() ^ (0 if rank == 0 else (0x5851F42D4C957F2D * rank) & ((1 << 64) - 1))
-    host = gcz.synth(cfg["kind"], nbases, seed)
+    S = nbases // L
+    mode = ("dist" if args.mode == "dist" else "replicas") if world > 1 else ("virtual" if args.virtual else "single")
+    if world == 1 and args.rccl_world1:
+        mode = "dist"
+    seed = gcz._lib.gcz_synth_default_seed()
     ctx = gcz.Context(local)
-    dev = ctx.upload(host)
+    group = None
+    if mode == "dist":
+        s0, s1, G = gcz.dist_plan(S, world, rank)
+        host = np.empty(max((s1 - s0) * L, 1), dtype=np.uint8)
+        gcz._lib.gcz_synth_fill(gcz._ptr(host), cfg["kind"], seed, s0 * L, s1 * L)
+        dev = ctx.upload(host)
+        uid = [gcz.dist_unique_id() if rank == 0 else None]
+        if dist is not None:
+            dist.broadcast_object_list(uid, src=0)
+        group = gcz.Group.rccl(ctx, rank, world, uid[0])
+        prof_ctx = ctx
+        run = lambda: group.build_device_bases([dev.ptr], S, L)  # noqa: E731
+    elif mode == "virtual":
+        group = gcz.Group.local(args.virtual, local)
+        prof_ctx = group.ctx(0)
+        host = gcz.synth(cfg["kind"], nbases, seed)
+        dev = prof_ctx.upload(host)
+        ptrs = [dev.ptr + gcz.dist_plan(S, args.virtual, r)[0] * L for r in range(args.virtual)]
+        run = lambda: group.build_device_bases(ptrs, S, L)  # noqa: E731
+    else:
+        if mode == "replicas":   # a different genome per rank, same size
+            seed ^= 0 if rank == 0 else (0x5851F42D4C957F2D * rank) & ((1 << 64) - 1)
+        host = gcz.synth(cfg["kind"], nbases, seed)
+        dev = ctx.upload(host)
+        prof_ctx = ctx
+        run = lambda: ctx.build_device_bases(dev.ptr, nbases, L)  # noqa: E731
     del host
 
     def barrier():
-        ctx.sync()
+        prof_ctx.sync()
         if dist is not None:
             dist.barrier()
-        ctx.sync()
+        prof_ctx.sync()
 
     for _ in range(args.warmup):
-        ctx.build_device_bases(dev.ptr, nbases, L)
+        run()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        info = ctx.build_device_bases(dev.ptr, nbases, L)
+        info = run()
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    S = nbases // L
     ms_per_step = dt / args.steps * 1e3
-    value = world * S * L * args.steps / dt
+    units = world * S * L if mode == "replicas" else S * L
+    value = units * args.steps / dt
 
     # per-kernel device time (hipEvents on the library's launch stream), one extra build
-    ctx.profile(True)
-    ctx.profile_reset()
-    info = ctx.build_device_bases(dev.ptr, nbases, L)
-    prof = ctx.profile_table()
-    ctx.profile(False)
+    pctxs = [group.ctx(i) for i in range(group.n_local)] if mode == "virtual" else [prof_ctx]
+    for c in pctxs:
+        c.profile(True)
+        c.profile_reset()
+    info = run()
+    tables = [c.profile_table() for c in pctxs]
+    for c in pctxs:
+        c.profile(False)
+    prof = tables[0]
+    rank_ms = [round(sum(v["total_ms"] for k, v in t.items() if k != "exchange"), 3) for t in tables]
+    share = world if mode == "dist" else (args.virtual if mode == "virtual" else 1)
     kernels = {}
     for name, p in prof.items():
         if p["launches"] == 0:
             continue
-        b = algorithmic_bytes(name, L, S, info["n_leaves"], info["layer_size"], info["hashed_pairs"])
+        # per-rank share of the algorithmic bytes (rank 0 profiled); exchange/dist phases carry none
+        b = algorithmic_bytes(name, L, S, info["n_leaves"], info["layer_size"],
+                              info["hashed_pairs"] if mode in ("single", "replicas") else None) // share
         kernels[name] = {"launches": p["launches"], "total_ms": round(p["total_ms"], 4),
                          "avg_ms": p["total_ms"] / p["launches"], "alg_bytes": b,
                          "gbs": b / (p["total_ms"] * 1e-3) / 1e9 if p["total_ms"] > 0 else None}
-    dom = max((k for k in kernels if k != "table_clear"), key=lambda k: kernels[k]["total_ms"])
+    dom = max((k for k in kernels if k not in ("clear", "exchange", "dist_local")),
+              key=lambda k: kernels[k]["total_ms"])
     dk = kernels[dom]
     traffic = None
     tpath = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
-    if os.path.exists(tpath):
+    if os.path.exists(tpath) and mode in ("single", "replicas"):
         with open(tpath) as f:
             traffic = json.load(f).get(dom)
     roofline = {"bound": "hbm", "kernel": dom,
@@ -204,10 +277,15 @@ def main():
     build_frac = (b_stream + b_table) / (info["build_ms"] * 1e-3) / (HBM_PEAK_GBS * 1e9)
 
     parity = None
-    if not args.no_parity and rank == 0 and cfg["golden"]:
+    tree = None
+    if not args.no_parity and cfg["golden"]:
+        if mode == "dist":
+            tree = gather_tree(gcz, group, dist, rank, world, L)   # every rank sends its slices
+        elif rank == 0:                                            # replicas: rank 0 built the golden genome
+            tree = group.tree() if mode == "virtual" else ctx.tree()
+    if tree is not None and rank == 0:
         with open(os.path.join(REPO, "tests", "golden", "manifest.json")) as f:
             exp = json.load(f)[cfg["golden"]]["expect"]
-        tree = ctx.tree()
         d = gcz.digest(tree)
         ratio = f"{nbases / d['bytes']:.6g}"
         parity = {"golden": cfg["golden"],
@@ -223,20 +301,28 @@ def main():
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "bases/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "scaling": "weak" if mode == "replicas" else "strong",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": args.config, "nbases_per_gpu": nbases, "L": L, "strands_per_gpu": S,
-                       "parallelism": f"independent shard genome per GPU x{world}"},
+            "config": {"workload": args.config, "nbases": nbases * (world if mode == "replicas" else 1), "L": L,
+                       "strands": S * (world if mode == "replicas" else 1),
+                       "parallelism": {"single": "1 GPU",
+                                       "dist": f"dist{world}: strand ranges per GPU, owner-hashed RCCL all-to-all per level",
+                                       "replicas": f"{world} independent genomes, one per GPU",
+                                       "virtual": f"{args.virtual} virtual ranks on 1 GPU (overhead probe)"}[mode]},
             "roofline": roofline,
             "build": {"device_ms": info["build_ms"], "hashed_pairs": info["hashed_pairs"], "b_stream": b_stream, "b_table": b_table,
                       "hbm_frac_survey_formula": round(build_frac, 5), "n_leaves": info["n_leaves"],
                       "n_layers": info["n_layers"]},
             "kernels": kernels,
+            "rank_kernel_ms": rank_ms,
             "cpu_baseline": cpu,
             "parity": parity,
         }
         print(json.dumps(line), flush=True)
     dev.free()
+    if group is not None:
+        group.close()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -96,11 +96,12 @@ inline LevelTab plan_table(void* buf, u64 cap, u32 K, u64 npos, u32 B, bool allo
 
 enum KernelId {
   KID_LEAF, KID_NODE, KID_FLAGSCAN_LEAF, KID_FLAGSCAN_NODE, KID_RESOLVE_LEAF, KID_RESOLVE_NODE, KID_MEMSET,
-  KID_EXCHANGE, KID_DIST, KID_COUNT
+  KID_EXCHANGE, KID_DIST, KID_OWNER, KID_IDS, KID_REMAP, KID_COUNT
 };
 inline const char* kernel_name(int k) {
   static const char* names[KID_COUNT] = {"leaf_insert", "node_insert", "flagscan_leaf", "flagscan_node",
-                                         "resolve_leaf", "resolve_node", "clear", "exchange", "dist_local"};
+                                         "resolve_leaf", "resolve_node", "clear", "exchange", "dist_bucket",
+                                         "dist_owner", "dist_ids", "dist_remap"};
   return names[k];
 }
 
@@ -229,4 +230,13 @@ struct gcz_ctx {
   int leaf_level(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr);
   int node_level(const gcz_host::NodeLevel& a, gcz_dev::Header* d_hdr);
   int build(const void* d_bases, const gcz_host::u64* d_leaves, gcz_host::u64 nbases, gcz_host::u64 S, int L);
+};
+
+// Times the launches of one scope on the context's stream (when profiling).
+struct ProfScope {
+  gcz_ctx* c;
+  int kid;
+  hipEvent_t e{};
+  ProfScope(gcz_ctx* c_, int kid_) : c(c_), kid(kid_) { c->prof_begin(kid, e); }
+  ~ProfScope() { c->prof_end(kid, e); }
 };

@@ -383,6 +383,8 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     DistHdr* dh = d.dhdr.as<DistHdr>();
     G_HIP(hipMemsetAsync(dh, 0, offsetof(DistHdr, cell), cx->stream));
     const u32 nb = u32(std::max<u64>(1, (L.grid_elems + kTile - 1) / kTile));
+    hipEvent_t eb{};
+    cx->prof_begin(KID_DIST, eb);
     hipLaunchKernelGGL(k_bucket_count, dim3(nb), dim3(kBlock), 0, cx->stream, L.src, d.blockcnt.as<u32>(), nb);
     hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(1024), 0, cx->stream, d.blockcnt.as<u32>(), u64(R) * nb, u32(R),
                        nb, dh->sync);
@@ -391,6 +393,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     hipLaunchKernelGGL(k_dist_pack, dim3(1), dim3(1), 0, cx->stream, cx->hdr.as<Header>(), L.ucount, L.bases, dh,
                        u32(R));
     G_HIP(hipGetLastError());
+    cx->prof_end(KID_DIST, eb);
   }
   {
     std::vector<const void*> s;
@@ -399,7 +402,10 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       s.push_back(cx->dist->dhdr.as<DistHdr>()->sync);
       r.push_back(cx->dist->gath.ptr);
     }
+    hipEvent_t e0{};
+    ctx[0]->prof_begin(KID_EXCHANGE, e0);
     G_RC(tr->allgather(kSyncWords * 8, s, r));
+    ctx[0]->prof_end(KID_EXCHANGE, e0);
   }
   gcz_dist_state& d0 = *ctx[0]->dist;
   G_HIP(hipMemcpyAsync(d0.h_gath, d0.gath.ptr, size_t(R) * kSyncWords * 8, hipMemcpyDeviceToHost, ctx[0]->stream));
@@ -455,13 +461,19 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       s.push_back(d.skey.ptr);
       rv.push_back(d.rkey.ptr);
     }
-    G_RC(tr->alltoallv(M, false, 8, s, rv));
+    {
+      hipEvent_t e0{};
+      ctx[0]->prof_begin(KID_EXCHANGE, e0);
+      G_RC(tr->alltoallv(M, false, 8, s, rv));
+      ctx[0]->prof_end(KID_EXCHANGE, e0);
+    }
     s.clear();
     rv.clear();
     for (int i = 0; i < NL; ++i) {
       gcz_ctx* cx = ctx[i];
       gcz_dist_state& d = *cx->dist;
       const u64 nr = recvd(rank[i]);
+      ProfScope ps_(cx, KID_OWNER);
       G_HIP(hipMemsetAsync(d.owntab.ptr, 0xff, size_t(otab[i].mask + 1) * 16, cx->stream));
       const Displ D = displ_of(rank[i]);
       hipLaunchKernelGGL(k_own_insert, blocks(nr), dim3(kBlock), 0, cx->stream, d.rkey.as<u64>(), nr, D, u32(R),
@@ -472,13 +484,19 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       s.push_back(d.rflag.ptr);
       rv.push_back(d.sflag.ptr);
     }
-    G_RC(tr->alltoallv(M, true, 1, s, rv));
+    {
+      hipEvent_t e0{};
+      ctx[0]->prof_begin(KID_EXCHANGE, e0);
+      G_RC(tr->alltoallv(M, true, 1, s, rv));
+      ctx[0]->prof_end(KID_EXCHANGE, e0);
+    }
   }
   // 3. globally-first ranks in local order
   for (int i = 0; i < NL; ++i) {
     gcz_ctx* cx = ctx[i];
     gcz_dist_state& d = *cx->dist;
     const u64 ur = u[rank[i]];
+    ProfScope ps_(cx, KID_IDS);
     G_HIP(hipMemsetAsync(d.gnf.ptr, 0, ur + 1, cx->stream));
     G_HIP(hipMemsetAsync(d.gmul.ptr, 0, ur + 1, cx->stream));
     if (records) {
@@ -501,7 +519,12 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       s.push_back(&cx->dist->dhdr.as<DistHdr>()->cfirst);
       rv.push_back(cx->dist->gath2.ptr);
     }
-    G_RC(tr->allgather(8, s, rv));
+    {
+      hipEvent_t e0{};
+      ctx[0]->prof_begin(KID_EXCHANGE, e0);
+      G_RC(tr->allgather(8, s, rv));
+      ctx[0]->prof_end(KID_EXCHANGE, e0);
+    }
     G_HIP(hipMemcpyAsync(d0.h_gath2, d0.gath2.ptr, size_t(R) * 8, hipMemcpyDeviceToHost, ctx[0]->stream));
     for (gcz_ctx* cx : ctx) G_HIP(hipStreamSynchronize(cx->stream));
     for (int s2 = 0; s2 < R; ++s2) c[s2] = d0.h_gath2[s2];
@@ -517,6 +540,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     gcz_ctx* cx = ctx[i];
     gcz_dist_state& d = *cx->dist;
     const u64 ur = u[rank[i]];
+    ProfScope ps_(cx, KID_IDS);
     if (lv[i].leaves)
       hipLaunchKernelGGL((k_dist_finalize<u64>), blocks(ur), dim3(kBlock), 0, cx->stream, lv[i].ucount,
                          d.gnf.as<unsigned char>(), d.gid.as<u32>(), u32(off[rank[i]]), d.scratch.as<u64>(),
@@ -534,19 +558,26 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       gcz_ctx* cx = ctx[i];
       gcz_dist_state& d = *cx->dist;
       const u64 ns = sent(rank[i]);
+      ProfScope ps_(cx, KID_IDS);
       hipLaunchKernelGGL(k_dist_cvals, blocks(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
                          d.gnf.as<unsigned char>(), d.gid.as<u32>(), d.scval.as<u32>());
       G_HIP(hipGetLastError());
       s.push_back(d.scval.ptr);
       rv.push_back(d.rcval.ptr);
     }
-    G_RC(tr->alltoallv(M, false, 4, s, rv));
+    {
+      hipEvent_t e0{};
+      ctx[0]->prof_begin(KID_EXCHANGE, e0);
+      G_RC(tr->alltoallv(M, false, 4, s, rv));
+      ctx[0]->prof_end(KID_EXCHANGE, e0);
+    }
     s.clear();
     rv.clear();
     for (int i = 0; i < NL; ++i) {
       gcz_ctx* cx = ctx[i];
       gcz_dist_state& d = *cx->dist;
       const u64 nr = recvd(rank[i]);
+      ProfScope ps_(cx, KID_OWNER);
       hipLaunchKernelGGL(k_own_setid, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr,
                          d.rcval.as<u32>(), otab[i]);
       hipLaunchKernelGGL(k_own_getid, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr, otab[i],
@@ -555,11 +586,17 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       s.push_back(d.rdval.ptr);
       rv.push_back(d.sdval.ptr);
     }
-    G_RC(tr->alltoallv(M, true, 4, s, rv));
+    {
+      hipEvent_t e0{};
+      ctx[0]->prof_begin(KID_EXCHANGE, e0);
+      G_RC(tr->alltoallv(M, true, 4, s, rv));
+      ctx[0]->prof_end(KID_EXCHANGE, e0);
+    }
     for (int i = 0; i < NL; ++i) {
       gcz_ctx* cx = ctx[i];
       gcz_dist_state& d = *cx->dist;
       const u64 ns = sent(rank[i]);
+      ProfScope ps_(cx, KID_IDS);
       hipLaunchKernelGGL(k_dist_dvals, blocks(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
                          d.gnf.as<unsigned char>(), d.sdval.as<u32>(), d.gid.as<u32>());
       G_HIP(hipGetLastError());
@@ -570,6 +607,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     gcz_ctx* cx = ctx[i];
     gcz_dist_state& d = *cx->dist;
     const u64 nw = nwords[i];
+    ProfScope ps_(cx, KID_REMAP);
     hipLaunchKernelGGL(k_dist_remap, blocks(nw), dim3(kBlock), 0, cx->stream, lv[i].w, nw, lv[i].nf, lv[i].multi,
                        d.gid.as<u32>(), d.gmul.as<unsigned char>());
     G_HIP(hipGetLastError());
@@ -863,6 +901,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
   for (gcz_ctx* cx : ctx) {
     cx->info = info;
     cx->info.status = GCZ_OK;
+    if (cx->profile) cx->prof_collect();
   }
   return GCZ_OK;
 }

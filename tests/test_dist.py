@@ -165,3 +165,24 @@ def test_dist_synth_100m(world, gcz, manifest, groups):
         kind, payload, L = case_input(case, gcz)
         _dist_build(gcz, groups(world), kind, payload, L)
         assert compare_digest(gcz.digest(groups(world).tree()), case["expect"]) == {}
+
+
+@pytest.mark.gpu
+def test_dist_rccl_world1(gcz, manifest):
+    """The RCCL transport (dlopen'd librccl, communicator, allgather, group calls) with one rank."""
+    ctx = gcz.Context(0)
+    try:
+        g = gcz.Group.rccl(ctx, 0, 1, gcz.dist_unique_id())
+        for name in ("corpus/chmpxx", "corpus/merged"):
+            case = manifest[name]
+            kind, payload, L = case_input(case, gcz)
+            bases = np.frombuffer(gcz.fasta_extract(payload), dtype=np.uint8)
+            buf = ctx.upload(bases)
+            try:
+                g.build_device_bases([buf.ptr], len(bases) // L, L)
+            finally:
+                buf.free()
+            assert compare_digest(gcz.digest(g.tree()), case["expect"]) == {}
+        g.close()
+    finally:
+        ctx.close()
