@@ -122,6 +122,16 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   const LevelTab nt = plan_table(tab.ptr, cap, 2 * (Bk + 3), p, Bk, allow_packed, kMaxProbe);
   const int cur = (a.k + 1) & 1, prev = a.k & 1;
   unsigned char* knf = nf_set[cur];
+  if (a.direct_known) {   // *pcount == n is set: the insert writes words and nodes, nothing else runs
+    hipEvent_t e0{};
+    prof_begin(KID_NODE, e0);
+    const dim3 gi(unsigned((p + kBlock - 1) / kBlock));
+    hipLaunchKernelGGL((k_node_insert<WideTab>), gi, dim3(kBlock), 0, stream, a.in, n, p, WideTab{}, nullptr, nullptr,
+                       a.words, Marks{knf, multi_set[cur]}, d_hdr, a.pcount, a.out, a.count, a.id_off);
+    HIP_TRY(hipGetLastError());
+    prof_end(KID_NODE, e0);
+    return GCZ_OK;
+  }
   const Marks mk{knf, multi_set[cur]};
   const unsigned char* pnf = a.prev_marks ? nf_set[prev] : nullptr;
   const unsigned char* pmu = a.prev_marks ? multi_set[prev] : nullptr;
@@ -161,6 +171,19 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
                        a.pcount, n);
   HIP_TRY(hipGetLastError());
   prof_end(KID_RESOLVE_NODE, e0);
+  return GCZ_OK;
+}
+
+int gcz_ctx::tail_levels(const u32* in, u64 n0, const u64* pcount, int k0, int D, const std::vector<u64>& layer_off_,
+                         Header* d_hdr) {
+  TailOut to{};
+  for (int k = k0; k < D; ++k) to.layer_off[k] = layer_off_[k];
+  hipEvent_t e0{};
+  prof_begin(KID_TAIL, e0);
+  hipLaunchKernelGGL(k_tail, dim3(1), dim3(kTailThreads), 0, stream, in, n0, pcount, k0, D, nodes_out.as<uint2>(), to,
+                     d_hdr);
+  HIP_TRY(hipGetLastError());
+  prof_end(KID_TAIL, e0);
   return GCZ_OK;
 }
 
@@ -255,7 +278,14 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     u32* outw = Bw;
     u64 n = S;
     u64 bound = std::min(S, leaf_cap);        // child ids of layer 0 are leaf ids < #slots
+    bool tail_done = false;
     for (int k = 0; k < D; ++k) {
+      if (n <= u64(kTailMaxN) && use_tail) {   // the rest fits one workgroup: one launch
+        const u64* pc = k == 0 ? &d_hdr->count[C - 1] : &d_hdr->count[kLayerSlot + k - 1];
+        if ((rc = tail_levels(in, n, pc, k, D, layer_off, d_hdr))) return rc;
+        tail_done = true;
+        break;
+      }
       NodeLevel na;
       na.k = k;
       na.in = in; na.n = n; na.p = pk[k];
@@ -272,8 +302,10 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       n = pk[k];
       bound = pk[k];
     }
-    hipLaunchKernelGGL(k_root, dim3(1), dim3(1), 0, stream, in, d_hdr);
-    HIP_TRY(hipGetLastError());
+    if (!tail_done) {
+      hipLaunchKernelGGL(k_root, dim3(1), dim3(1), 0, stream, in, d_hdr);
+      HIP_TRY(hipGetLastError());
+    }
     HIP_TRY(hipEventRecord(ev_stop, stream));
     HIP_TRY(hipMemcpyAsync(h_hdr, d_hdr, sizeof(Header), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
@@ -331,6 +363,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   if (const char* t = std::getenv("GCZ_TABLE")) c->force_wide = std::strcmp(t, "wide") == 0;
   if (const char* t = std::getenv("GCZ_NODE_CAP_SHIFT")) c->node_cap_shift = std::atoi(t);
   if (const char* t = std::getenv("GCZ_LEAF_CAP_LOG2")) c->leaf_cap_log2 = std::atoi(t);
+  if (const char* t = std::getenv("GCZ_TAIL")) c->use_tail = std::atoi(t) != 0;
   *out = c;
   return GCZ_OK;
 }

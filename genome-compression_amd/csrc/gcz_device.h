@@ -699,6 +699,106 @@ __global__ __launch_bounds__(kBlock) void k_resolve_node(u32* __restrict__ words
   words[j] = id | (w & kBits);
 }
 
+// ---- fused top levels -------------------------------------------------------------
+// Once a level's input fits one workgroup (n <= kTailMaxN), all remaining
+// levels run in ONE launch: words ping-pong in LDS, each level is either
+// direct (previous level all unique: ids are positions) or hash-consed in an
+// LDS table (CAS claims, atomicMin keeps the first position, a block scan
+// ranks the first occurrences) -- the same ids, nodes and words as the
+// per-level kernels, without ~4 launches per level.
+constexpr int kTailMaxN = 2048;
+constexpr int kTailThreads = 1024;
+constexpr int kTailSlots = 2 * kTailThreads;
+
+struct TailOut {
+  u64 layer_off[GCZ_MAX_LAYERS];   // node offset of each layer within `nodes`
+};
+
+[[maybe_unused]] static __global__ __launch_bounds__(kTailThreads) void k_tail(
+    const u32* __restrict__ in, u64 n0, const u64* prev_count, int k0, int D, uint2* __restrict__ nodes, TailOut to,
+    Header* __restrict__ hdr) {
+  __shared__ u32 wbuf[2][kTailMaxN];
+  __shared__ unsigned long long tkey[kTailSlots];
+  __shared__ u32 tpos[kTailSlots];
+  __shared__ u32 tid_of[kTailSlots];
+  __shared__ u32 wsum[kTailThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (u64 i = tid; i < n0; i += kTailThreads) wbuf[0][i] = in[i];
+  u32 n = u32(n0);
+  bool direct = prev_count && *prev_count == n0;
+  int cur = 0;
+  __syncthreads();
+  for (int k = k0; k < D; ++k) {
+    const u32 p = (n + 1) / 2;
+    const u32* win = wbuf[cur];
+    u32* wout = wbuf[cur ^ 1];
+    uint2* out = nodes + to.layer_off[k];
+    const u32 j = u32(tid);
+    u32 l = kNullWord, r = kNullWord, cl = 0, cr = 0, m = 0, t = 0, v = 0;
+    if (j < p) {
+      l = win[2 * j];
+      r = 2 * j + 1 < n ? win[2 * j + 1] : kNullWord;
+      node_canonical(l, r, cl, cr, m, t);
+      v = ulw(l) == ulw(xf(r, 1, 0));
+    }
+    u32 count;
+    if (direct) {
+      if (j < p) {
+        out[j] = make_uint2(cl, cr);
+        wout[j] = make_word(j, m, t, v);
+      }
+      count = p;
+    } else {
+      u32 mask = 1;
+      while (mask < 2 * p) mask <<= 1;
+      mask -= 1;
+      for (u32 s = tid; s <= mask; s += kTailThreads) {
+        tkey[s] = kEmpty;
+        tpos[s] = ~0u;
+      }
+      __syncthreads();
+      u32 slot = 0;
+      if (j < p) {
+        const unsigned long long key = (u64(ulw(cl)) << 31) | ulw(cr);
+        u32 s = slot_hash(key) & mask;
+        for (;;) {
+          unsigned long long c = tkey[s];
+          if (c == kEmpty) c = atomicCAS(&tkey[s], kEmpty, key);
+          if (c == kEmpty || c == key) break;
+          s = (s + 1) & mask;
+        }
+        atomicMin(&tpos[s], j);
+        slot = s;
+      }
+      __syncthreads();
+      const bool first = j < p && tpos[slot] == j;
+      const u64 bal = __ballot(first);
+      if (lane == 0) wsum[wave] = u32(__popcll(bal));
+      __syncthreads();
+      u32 before = 0, total = 0;
+      for (int w = 0; w < kTailThreads / 64; ++w) {
+        const u32 c = wsum[w];
+        before += w < wave ? c : 0u;
+        total += c;
+      }
+      if (first) {
+        const u32 id = before + u32(__popcll(bal & ((1ull << lane) - 1)));
+        tid_of[slot] = id;
+        out[id] = make_uint2(cl, cr);
+      }
+      __syncthreads();
+      if (j < p) wout[j] = make_word(tid_of[slot], m, t, v);
+      count = total;
+    }
+    if (tid == 0) hdr->count[kLayerSlot + k] = count;
+    direct = count == p;
+    n = p;
+    cur ^= 1;
+    __syncthreads();
+  }
+  if (tid == 0) hdr->root = wbuf[cur][0];
+}
+
 [[maybe_unused]] static __global__ void k_root(const u32* __restrict__ words, Header* __restrict__ hdr) { hdr->root = words[0]; }
 
 // Clear a node level's table (all ones) and marks (zero) unless the level is direct.

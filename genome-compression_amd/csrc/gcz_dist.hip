@@ -21,6 +21,7 @@ using namespace gcz_host;
 struct gcz_dist_state {
   DevBuf scratch, gnf, gmul, gid, blockcnt, skey, sidx, sflag, scval, sdval;   // sender side
   DevBuf rkey, oslot, rflag, rcval, rdval, owntab;                            // owner side
+  DevBuf s_selc, s_seld, s_prec, s_pred, o_selc, o_seld, o_prec, o_pred, sdesc;  // C/D compaction
   DevBuf dhdr, gath, gath2, gathf, ddesc, tail_in;
   u64* h_gath = nullptr;    // pinned mirrors of the gathered vectors
   u64* h_gath2 = nullptr;
@@ -32,6 +33,8 @@ void gcz_dist_state_free(gcz_ctx* c) {
   if (!d) return;
   for (DevBuf* b : {&d->scratch, &d->gnf, &d->gmul, &d->gid, &d->blockcnt, &d->skey, &d->sidx, &d->sflag,
                     &d->scval, &d->sdval, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab,
+                    &d->s_selc, &d->s_seld, &d->s_prec, &d->s_pred, &d->o_selc, &d->o_seld, &d->o_prec,
+                    &d->o_pred, &d->sdesc,
                     &d->dhdr, &d->gath, &d->gath2, &d->gathf, &d->ddesc, &d->tail_in})
     if (b->ptr) (void)hipFree(b->ptr);
   for (u64* h : {d->h_gath, d->h_gath2, d->h_gathf})
@@ -357,13 +360,18 @@ int gcz_group::alloc(int i, int L, u64 leaf_cap) {
   if ((rc = c->ensure(d.sdval, u * 4))) return rc;
   if ((rc = c->ensure(d.dhdr, sizeof(DistHdr)))) return rc;
   if ((rc = c->ensure(d.gath, size_t(world) * kSyncWords * 8))) return rc;
-  if ((rc = c->ensure(d.gath2, size_t(world) * 8))) return rc;
+  if ((rc = c->ensure(d.gath2, size_t(world) * (1 + 2 * kMaxRanks) * 8))) return rc;
+  if ((rc = c->ensure(d.s_selc, u))) return rc;
+  if ((rc = c->ensure(d.s_seld, u))) return rc;
+  if ((rc = c->ensure(d.s_prec, u * 4))) return rc;
+  if ((rc = c->ensure(d.s_pred, u * 4))) return rc;
   if ((rc = c->ensure(d.gathf, size_t(world) * kFinalWords * 8))) return rc;
   if ((rc = c->ensure(d.ddesc, ((u + kTile - 1) / kTile) * 8 + 64))) return rc;
   if ((rc = c->ensure(d.tail_in, nG * 4 + 16))) return rc;
   if (!d.h_gath) {
     if (hipHostMalloc((void**)&d.h_gath, size_t(kMaxRanks) * kSyncWords * 8, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&d.h_gath2, size_t(kMaxRanks) * 8, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&d.h_gath2, size_t(kMaxRanks) * (1 + 2 * kMaxRanks) * 8, hipHostMallocDefault) !=
+            hipSuccess ||
         hipHostMalloc((void**)&d.h_gathf, size_t(kMaxRanks) * kFinalWords * 8, hipHostMallocDefault) != hipSuccess)
       return GCZ_ERR_DEVICE;
   }
@@ -441,19 +449,43 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
   };
   std::vector<OwnTab> otab(NL);
 
-  // 2. owners decide first rank and repetition (A, B)
+  auto send_displ_of = [&](int r) {   // destination segments of rank r's send buffer
+    Displ D{};
+    u64 o = 0;
+    for (int q = 0; q < R; ++q) { D.d[q] = o; o += M[size_t(r) * R + q]; }
+    for (int q = R; q <= kMaxRanks; ++q) D.d[q] = o;
+    return D;
+  };
+  auto tiles_of = [](u64 n) { return (n + kTile - 1) / kTile; };
+  // selected-record scans: sender C, sender D, owner C, owner D (descriptor regions of sdesc)
+  auto sel_scan = [&](gcz_ctx* cx, int which, const unsigned char* sel, u64 n, u32* pre, u64 region) -> int {
+    gcz_dist_state& d = *cx->dist;
+    DistHdr* dh = d.dhdr.as<DistHdr>();
+    if (n == 0) return GCZ_OK;   // tot[which] stays 0
+    hipLaunchKernelGGL(k_sel_scan, dim3(unsigned(tiles_of(n))), dim3(kBlock), 0, cx->stream, sel, n, pre,
+                       d.sdesc.as<u64>() + region * which, &dh->tick[which], &dh->tot[which]);
+    return hipGetLastError() == hipSuccess ? GCZ_OK : GCZ_ERR_DEVICE;
+  };
+  std::vector<u64> region(NL, 0);
+
+  // 2. owners decide first rank, repetition and sharing (A, B)
   if (records) {
     std::vector<const void*> s;
     std::vector<void*> rv;
     for (int i = 0; i < NL; ++i) {
       gcz_ctx* cx = ctx[i];
       gcz_dist_state& d = *cx->dist;
-      const u64 nr = recvd(rank[i]);
+      const u64 nr = recvd(rank[i]), ns = sent(rank[i]);
       int rc;
       if ((rc = cx->ensure(d.rkey, nr * 8 + 16)) || (rc = cx->ensure(d.oslot, nr * 4 + 16)) ||
           (rc = cx->ensure(d.rflag, nr + 16)) || (rc = cx->ensure(d.rcval, nr * 4 + 16)) ||
-          (rc = cx->ensure(d.rdval, nr * 4 + 16)))
+          (rc = cx->ensure(d.rdval, nr * 4 + 16)) || (rc = cx->ensure(d.o_selc, nr + 16)) ||
+          (rc = cx->ensure(d.o_seld, nr + 16)) || (rc = cx->ensure(d.o_prec, nr * 4 + 16)) ||
+          (rc = cx->ensure(d.o_pred, nr * 4 + 16)))
         return dev_fail("exchange buffers");
+      region[i] = tiles_of(std::max(nr, ns)) + 1;
+      if ((rc = cx->ensure(d.sdesc, 4 * region[i] * 8))) return dev_fail("scan descriptors");
+      G_HIP(hipMemsetAsync(d.sdesc.ptr, 0, 4 * region[i] * 8, cx->stream));
       const u64 cap = std::max<u64>(256, next_pow2(2 * nr));
       if ((rc = cx->ensure(d.owntab, cap * 16))) return dev_fail("owner table");
       otab[i].tab = d.owntab.as<Slot>();
@@ -480,7 +512,12 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
                          int(lv[i].leaves), otab[i], d.oslot.as<u32>(), &d.dhdr.as<DistHdr>()->final_vec[3]);
       hipLaunchKernelGGL(k_own_reply, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr, D, u32(R),
                          otab[i], d.rflag.as<unsigned char>());
+      // the owner's view of the C / D compactions (same records, same order as the senders')
+      hipLaunchKernelGGL(k_sel, blocks(nr), dim3(kBlock), 0, cx->stream, d.rflag.as<unsigned char>(), nr,
+                         d.o_selc.as<unsigned char>(), d.o_seld.as<unsigned char>());
       G_HIP(hipGetLastError());
+      if (sel_scan(cx, 2, d.o_selc.as<unsigned char>(), nr, d.o_prec.as<u32>(), region[i])) return dev_fail("scan");
+      if (sel_scan(cx, 3, d.o_seld.as<unsigned char>(), nr, d.o_pred.as<u32>(), region[i])) return dev_fail("scan");
       s.push_back(d.rflag.ptr);
       rv.push_back(d.sflag.ptr);
     }
@@ -491,11 +528,12 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       ctx[0]->prof_end(KID_EXCHANGE, e0);
     }
   }
-  // 3. globally-first ranks in local order
+  // 3. globally-first ranks in local order; C / D record counts per owner
   for (int i = 0; i < NL; ++i) {
     gcz_ctx* cx = ctx[i];
     gcz_dist_state& d = *cx->dist;
     const u64 ur = u[rank[i]];
+    DistHdr* dh = d.dhdr.as<DistHdr>();
     ProfScope ps_(cx, KID_IDS);
     G_HIP(hipMemsetAsync(d.gnf.ptr, 0, ur + 1, cx->stream));
     G_HIP(hipMemsetAsync(d.gmul.ptr, 0, ur + 1, cx->stream));
@@ -503,31 +541,52 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       const u64 ns = sent(rank[i]);
       hipLaunchKernelGGL(k_dist_flags, blocks(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
                          d.sflag.as<unsigned char>(), d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>());
+      hipLaunchKernelGGL(k_sel, blocks(ns), dim3(kBlock), 0, cx->stream, d.sflag.as<unsigned char>(), ns,
+                         d.s_selc.as<unsigned char>(), d.s_seld.as<unsigned char>());
+      G_HIP(hipGetLastError());
+      if (sel_scan(cx, 0, d.s_selc.as<unsigned char>(), ns, d.s_prec.as<u32>(), region[i])) return dev_fail("scan");
+      if (sel_scan(cx, 1, d.s_seld.as<unsigned char>(), ns, d.s_pred.as<u32>(), region[i])) return dev_fail("scan");
+      const Displ SD = send_displ_of(rank[i]);
+      hipLaunchKernelGGL(k_seg_counts, dim3(1), dim3(64), 0, cx->stream, d.s_prec.as<u32>(), &dh->tot[0], ns, SD,
+                         u32(R), &dh->sync2[1]);
+      hipLaunchKernelGGL(k_seg_counts, dim3(1), dim3(64), 0, cx->stream, d.s_pred.as<u32>(), &dh->tot[1], ns, SD,
+                         u32(R), &dh->sync2[1 + R]);
     }
-    const u64 tiles = std::max<u64>(1, (ur + kTile - 1) / kTile);
+    const u64 tiles = std::max<u64>(1, tiles_of(ur));
     G_HIP(hipMemsetAsync(d.ddesc.ptr, 0, tiles * 8, cx->stream));
-    DistHdr* dh = d.dhdr.as<DistHdr>();
     hipLaunchKernelGGL(k_dist_rank, dim3(unsigned(tiles)), dim3(kBlock), 0, cx->stream, d.gnf.as<unsigned char>(),
-                       lv[i].ucount, d.gid.as<u32>(), d.ddesc.as<u64>(), &dh->ticket, &dh->cfirst);
+                       lv[i].ucount, d.gid.as<u32>(), d.ddesc.as<u64>(), &dh->ticket, &dh->sync2[0]);
     G_HIP(hipGetLastError());
   }
   c.assign(R, 0);
+  std::vector<u64> MC(size_t(R) * R, 0), MD(size_t(R) * R, 0);
+  u64 nc = 0, nd = 0;
   if (records) {
+    const size_t W = 1 + 2 * size_t(R);
     std::vector<const void*> s;
     std::vector<void*> rv;
     for (gcz_ctx* cx : ctx) {
-      s.push_back(&cx->dist->dhdr.as<DistHdr>()->cfirst);
+      s.push_back(cx->dist->dhdr.as<DistHdr>()->sync2);
       rv.push_back(cx->dist->gath2.ptr);
     }
     {
       hipEvent_t e0{};
       ctx[0]->prof_begin(KID_EXCHANGE, e0);
-      G_RC(tr->allgather(8, s, rv));
+      G_RC(tr->allgather(W * 8, s, rv));
       ctx[0]->prof_end(KID_EXCHANGE, e0);
     }
-    G_HIP(hipMemcpyAsync(d0.h_gath2, d0.gath2.ptr, size_t(R) * 8, hipMemcpyDeviceToHost, ctx[0]->stream));
+    G_HIP(hipMemcpyAsync(d0.h_gath2, d0.gath2.ptr, size_t(R) * W * 8, hipMemcpyDeviceToHost, ctx[0]->stream));
     for (gcz_ctx* cx : ctx) G_HIP(hipStreamSynchronize(cx->stream));
-    for (int s2 = 0; s2 < R; ++s2) c[s2] = d0.h_gath2[s2];
+    for (int s2 = 0; s2 < R; ++s2) {
+      const u64* v = d0.h_gath2 + size_t(s2) * W;
+      c[s2] = v[0];
+      for (int q = 0; q < R; ++q) {
+        MC[size_t(s2) * R + q] = v[1 + q];
+        MD[size_t(s2) * R + q] = v[1 + R + q];
+        nc += v[1 + q];
+        nd += v[1 + R + q];
+      }
+    }
   } else {
     c = u;   // nothing crossed ranks: every local first is globally first
   }
@@ -535,7 +594,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
   for (int s2 = 0; s2 < R; ++s2) off[s2 + 1] = off[s2] + c[s2];
   total = off[R];
   if (total > u64(kIdx)) return fail(GCZ_ERR_CAPACITY, "more than 2^29-1 uniques in one layer");
-  // 4. compact globally-first uniques into the slice; ids of the others (C, D)
+  // 4. compact globally-first uniques into the slice; ids of shared keys (C, D)
   for (int i = 0; i < NL; ++i) {
     gcz_ctx* cx = ctx[i];
     gcz_dist_state& d = *cx->dist;
@@ -551,7 +610,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
                          static_cast<uint2*>(lv[i].out));
     G_HIP(hipGetLastError());
   }
-  if (records) {
+  if (nc) {
     std::vector<const void*> s;
     std::vector<void*> rv;
     for (int i = 0; i < NL; ++i) {
@@ -560,7 +619,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       const u64 ns = sent(rank[i]);
       ProfScope ps_(cx, KID_IDS);
       hipLaunchKernelGGL(k_dist_cvals, blocks(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
-                         d.gnf.as<unsigned char>(), d.gid.as<u32>(), d.scval.as<u32>());
+                         d.sflag.as<unsigned char>(), d.s_prec.as<u32>(), d.gid.as<u32>(), d.scval.as<u32>());
       G_HIP(hipGetLastError());
       s.push_back(d.scval.ptr);
       rv.push_back(d.rcval.ptr);
@@ -568,20 +627,29 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     {
       hipEvent_t e0{};
       ctx[0]->prof_begin(KID_EXCHANGE, e0);
-      G_RC(tr->alltoallv(M, false, 4, s, rv));
+      G_RC(tr->alltoallv(MC, false, 4, s, rv));
       ctx[0]->prof_end(KID_EXCHANGE, e0);
     }
-    s.clear();
-    rv.clear();
     for (int i = 0; i < NL; ++i) {
       gcz_ctx* cx = ctx[i];
       gcz_dist_state& d = *cx->dist;
       const u64 nr = recvd(rank[i]);
       ProfScope ps_(cx, KID_OWNER);
       hipLaunchKernelGGL(k_own_setid, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr,
-                         d.rcval.as<u32>(), otab[i]);
-      hipLaunchKernelGGL(k_own_getid, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr, otab[i],
-                         d.rdval.as<u32>());
+                         d.rflag.as<unsigned char>(), d.o_prec.as<u32>(), d.rcval.as<u32>(), otab[i]);
+      G_HIP(hipGetLastError());
+    }
+  }
+  if (nd) {
+    std::vector<const void*> s;
+    std::vector<void*> rv;
+    for (int i = 0; i < NL; ++i) {
+      gcz_ctx* cx = ctx[i];
+      gcz_dist_state& d = *cx->dist;
+      const u64 nr = recvd(rank[i]);
+      ProfScope ps_(cx, KID_OWNER);
+      hipLaunchKernelGGL(k_own_getid, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr,
+                         d.rflag.as<unsigned char>(), d.o_pred.as<u32>(), otab[i], d.rdval.as<u32>());
       G_HIP(hipGetLastError());
       s.push_back(d.rdval.ptr);
       rv.push_back(d.sdval.ptr);
@@ -589,7 +657,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     {
       hipEvent_t e0{};
       ctx[0]->prof_begin(KID_EXCHANGE, e0);
-      G_RC(tr->alltoallv(M, true, 4, s, rv));
+      G_RC(tr->alltoallv(MD, true, 4, s, rv));
       ctx[0]->prof_end(KID_EXCHANGE, e0);
     }
     for (int i = 0; i < NL; ++i) {
@@ -598,7 +666,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       const u64 ns = sent(rank[i]);
       ProfScope ps_(cx, KID_IDS);
       hipLaunchKernelGGL(k_dist_dvals, blocks(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
-                         d.gnf.as<unsigned char>(), d.sdval.as<u32>(), d.gid.as<u32>());
+                         d.sflag.as<unsigned char>(), d.s_pred.as<u32>(), d.sdval.as<u32>(), d.gid.as<u32>());
       G_HIP(hipGetLastError());
     }
   }
@@ -766,6 +834,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         na.prev_marks = k > 0;
         na.pcount = &dh->cell[k];
         na.id_off = u32(P.start(r, k + 1));
+        na.direct_known = direct;
         na.desc = cx->desc.as<u64>() + dcur[i];
         dcur[i] += (p + kTile - 1) / kTile;
         na.ticket = &h->ticket[kLayerSlot + k];
@@ -836,7 +905,14 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         u64 n = P.nk[G];
         hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, cx->stream, &dh->cell[G], direct ? n : ~0ull);
         u64 bound = prev_total;
+        bool tail_done = false;
         for (int k = G; k < D; ++k) {
+          if (n <= u64(kTailMaxN) && cx->use_tail) {   // the rest in one launch
+            const u64* pc = k == G ? &dh->cell[G] : &h->count[kLayerSlot + k - 1];
+            if (cx->tail_levels(in, n, pc, k, D, node_base[i], h)) return dev_fail("tail levels");
+            tail_done = true;
+            break;
+          }
           NodeLevel na;
           na.k = k;
           na.in = in;
@@ -857,7 +933,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
           n = na.p;
           bound = na.p;
         }
-        hipLaunchKernelGGL(k_root, dim3(1), dim3(1), 0, cx->stream, in, h);
+        if (!tail_done) hipLaunchKernelGGL(k_root, dim3(1), dim3(1), 0, cx->stream, in, h);
       }
       hipLaunchKernelGGL(k_dist_final, dim3(1), dim3(1), 0, cx->stream, h, dh, G, D, int(tail));
       G_HIP(hipGetLastError());

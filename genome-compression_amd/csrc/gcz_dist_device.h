@@ -8,12 +8,14 @@
 //   A  every locally-first element that went through the table sends its key
 //      (bit 63: "repeats locally", node levels) to the owner;
 //   B  the owner replies per record: not-globally-first (another rank with a
-//      smaller rank id has the key) and globally-repeated;
+//      smaller rank id has the key), globally-repeated, held by >= 2 ranks;
 //   -  each rank ranks its globally-first keys in local order; an allgather of
 //      those counts gives every rank its id offset (rank order = position
 //      order, so offset + local rank = global first-occurrence rank);
-//   C  ranks send the global id of each record they own the first occurrence of;
-//   D  the owner returns the id for every record;
+//   C  the first holder of every key held by >= 2 ranks sends its global id;
+//   D  the owner returns that id to every other holder
+//      (C and D carry only those records, compacted in record order on both
+//      sides, so a layer of mostly rank-unique keys moves almost nothing);
 //   -  local words are remapped to global ids, and globally-first uniques are
 //      compacted into the rank's slice of the output layer.
 //
@@ -33,9 +35,13 @@ struct DistHdr {
   // per-level sync vector: [0, R) records per owner, [R] overflow, [R+1] local uniques,
   // [R+2] first bad symbol offset (local bytes), [R+3] that symbol
   u64 sync[kSyncWords];
-  u64 cfirst;                           // globally-first local uniques of the level
+  // second sync vector: [0] globally-first local uniques, [1, 1+R) C records per owner,
+  // [1+R, 1+2R) D records per owner (see exchange)
+  u64 sync2[1 + 2 * kMaxRanks];
+  u64 tot[4];                           // selected counts of the four compaction scans
   u32 ticket;                           // look-back tickets of k_dist_rank
-  u32 pad;
+  u32 tick[4];                          // ... of the compaction scans
+  u32 pad[3];
   u64 cell[GCZ_MAX_LAYERS + 1];         // direct flags: n_local when the layer is direct, else ~0
   u64 final_vec[kFinalWords];           // [0] overflow, [1] root, [2] tail first layer, [4 + k] tail counts
 };
@@ -216,23 +222,71 @@ static __global__ __launch_bounds__(kBlock) void k_own_reply(const u32* __restri
   const u32 st = ~T.tab[oslot[k]].pos;
   const u32 ranks = st & 0x7fffffffu;
   const u32 minr = u32(__ffs(ranks) - 1);
-  const u32 gm = (__popc(ranks) > 1) | (st >> 31);
-  rflag[k] = (unsigned char)((minr != src) | (gm << 1));
+  const u32 shared = __popc(ranks) > 1;
+  const u32 gm = shared | (st >> 31);
+  rflag[k] = (unsigned char)((minr != src) | (gm << 1) | (shared << 2));
+}
+
+// Per-record flags (reply bits): 1 not globally first, 2 repeats globally, 4 held by >= 2 ranks.
+// C: the first holder of a shared key sends its id; D: every other holder receives it.
+__device__ __forceinline__ bool want_c(unsigned char f) { return (f & 1) == 0 && (f & 4); }
+__device__ __forceinline__ bool want_d(unsigned char f) { return (f & 1) != 0; }
+
+// Selection bytes for the C and D compactions (0 = selected: the tile scan's convention).
+static __global__ __launch_bounds__(kBlock) void k_sel(const unsigned char* __restrict__ flag, u64 n,
+                                                       unsigned char* __restrict__ selc,
+                                                       unsigned char* __restrict__ seld) {
+  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= n) return;
+  const unsigned char f = flag[k];
+  selc[k] = want_c(f) ? 0 : 1;
+  seld[k] = want_d(f) ? 0 : 1;
+}
+
+// pre[k] = selected records before k (records keep their order, so the
+// compacted buffer keeps the per-rank segments in order); total -> *total.
+static __global__ __launch_bounds__(kBlock) void k_sel_scan(const unsigned char* __restrict__ sel, u64 n,
+                                                            u32* __restrict__ pre, u64* __restrict__ desc,
+                                                            u32* __restrict__ ticket, u64* __restrict__ total) {
+  __shared__ u32 s_tile;
+  __shared__ u32 s_pre[kGroupsPerTile];
+  TileScan<kItems> ts;
+  tile_scan(ts, &s_tile, s_pre, sel, 0, n, 0, desc, ticket, total);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const u64 lt = (1ull << lane) - 1;
+#pragma unroll
+  for (int e = 0; e < kItems; ++e) {
+    const u64 j = ts.base + u64(e) * kBlock + tid;
+    if (j < n) pre[j] = s_pre[e * 4 + wave] + u32(__popcll(ts.mask[e] & lt));
+  }
+}
+
+// Selected records per segment [D.d[q], D.d[q+1]).
+static __global__ void k_seg_counts(const u32* __restrict__ pre, const u64* __restrict__ total, u64 n, Displ D,
+                                    u32 R, u64* __restrict__ out) {
+  const u32 q = threadIdx.x;
+  if (q >= R) return;
+  const u64 a = D.d[q], b = D.d[q + 1];
+  const u64 pa = a < n ? pre[a] : *total, pb = b < n ? pre[b] : *total;
+  out[q] = pb - pa;
 }
 
 static __global__ __launch_bounds__(kBlock) void k_own_setid(const u32* __restrict__ oslot, u64 nrecv,
+                                                             const unsigned char* __restrict__ rflag,
+                                                             const u32* __restrict__ prec,
                                                              const u32* __restrict__ cval, OwnTab T) {
   const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (k >= nrecv) return;
-  const u32 v = cval[k];
-  if (v != ~0u) T.tab[oslot[k]].pad = v;
+  if (k >= nrecv || !want_c(rflag[k])) return;
+  T.tab[oslot[k]].pad = cval[prec[k]];
 }
 
-static __global__ __launch_bounds__(kBlock) void k_own_getid(const u32* __restrict__ oslot, u64 nrecv, OwnTab T,
+static __global__ __launch_bounds__(kBlock) void k_own_getid(const u32* __restrict__ oslot, u64 nrecv,
+                                                             const unsigned char* __restrict__ rflag,
+                                                             const u32* __restrict__ pred, OwnTab T,
                                                              u32* __restrict__ dval) {
   const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (k >= nrecv) return;
-  dval[k] = T.tab[oslot[k]].pad;
+  if (k >= nrecv || !want_d(rflag[k])) return;
+  dval[pred[k]] = T.tab[oslot[k]].pad;
 }
 
 // ---- sender side ---------------------------------------------------------------
@@ -285,21 +339,21 @@ __global__ __launch_bounds__(kBlock) void k_dist_finalize(const u64* __restrict_
 }
 
 static __global__ __launch_bounds__(kBlock) void k_dist_cvals(const u32* __restrict__ sidx, u64 nsent,
-                                                              const unsigned char* __restrict__ gnf,
+                                                              const unsigned char* __restrict__ sflag,
+                                                              const u32* __restrict__ prec,
                                                               const u32* __restrict__ gid, u32* __restrict__ cval) {
   const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (k >= nsent) return;
-  const u32 lid = sidx[k];
-  cval[k] = gnf[lid] ? ~0u : gid[lid];
+  if (k >= nsent || !want_c(sflag[k])) return;
+  cval[prec[k]] = gid[sidx[k]];
 }
 
 static __global__ __launch_bounds__(kBlock) void k_dist_dvals(const u32* __restrict__ sidx, u64 nsent,
-                                                              const unsigned char* __restrict__ gnf,
+                                                              const unsigned char* __restrict__ sflag,
+                                                              const u32* __restrict__ pred,
                                                               const u32* __restrict__ dval, u32* __restrict__ gid) {
   const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (k >= nsent) return;
-  const u32 lid = sidx[k];
-  if (gnf[lid]) gid[lid] = dval[k];
+  if (k >= nsent || !want_d(sflag[k])) return;
+  gid[sidx[k]] = dval[pred[k]];
 }
 
 // Local words -> global ids; locally-first elements whose key repeats on
