@@ -294,6 +294,23 @@ def main():
                   "layers_sha256_match": d["sha_layers_bin"] == exp["sha_layers_bin"],
                   "ratio": ratio, "ratio_ref": exp["ratio"]}
 
+    # ratio path on the device: frequency sort + bytes() + .dag writer
+    ratio_path = None
+    if mode in ("single", "replicas") and rank == 0:
+        ctx.sync()
+        t0 = time.perf_counter()
+        ctx.sort_device()
+        t1 = time.perf_counter()
+        n = gcz._U64()
+        dptr = gcz._lib.gcz_device_dag(ctx._h, gcz.ctypes.byref(n))
+        t2 = time.perf_counter()
+        ratio_path = {"device_sort_ms": round((t1 - t0) * 1e3, 3), "device_dag_ms": round((t2 - t1) * 1e3, 3),
+                      "dag_bytes": int(n.value), "ratio": f"{nbases / max(int(n.value), 1):.6g}"}
+        if parity is not None:
+            dag = ctx.serialize_device()
+            parity["device_dag_sha256_match"] = hashlib.sha256(dag).hexdigest() == exp["sha_dag"]
+        del dptr
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_sample)
@@ -316,6 +333,7 @@ def main():
                       "n_layers": info["n_layers"]},
             "kernels": kernels,
             "rank_kernel_ms": rank_ms,
+            "ratio_path": ratio_path,
             "cpu_baseline": cpu,
             "parity": parity,
         }

@@ -7,6 +7,7 @@ using namespace gcz_dev;
 using namespace gcz_host;
 
 void gcz_dist_state_free(gcz_ctx* c);   // gcz_dist.hip
+void gcz_sort_state_free(gcz_ctx* c);   // gcz_sort.hip
 
 namespace {
 
@@ -373,6 +374,7 @@ void gcz_ctx_destroy(gcz_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   gcz_dist_state_free(c);
+  gcz_sort_state_free(c);
   for (DevBuf* b : {&c->wa, &c->wb, &c->grp, &c->desc, &c->tab, &c->leaves_out, &c->nodes_out, &c->hdr, &c->input,
                     &c->nf, &c->multi})
     if (b->ptr) (void)hipFree(b->ptr);

@@ -96,12 +96,12 @@ inline LevelTab plan_table(void* buf, u64 cap, u32 K, u64 npos, u32 B, bool allo
 
 enum KernelId {
   KID_LEAF, KID_NODE, KID_FLAGSCAN_LEAF, KID_FLAGSCAN_NODE, KID_RESOLVE_LEAF, KID_RESOLVE_NODE, KID_MEMSET,
-  KID_EXCHANGE, KID_DIST, KID_OWNER, KID_IDS, KID_REMAP, KID_TAIL, KID_COUNT
+  KID_EXCHANGE, KID_DIST, KID_OWNER, KID_IDS, KID_REMAP, KID_TAIL, KID_SORT, KID_DAG, KID_COUNT
 };
 inline const char* kernel_name(int k) {
   static const char* names[KID_COUNT] = {"leaf_insert", "node_insert", "flagscan_leaf", "flagscan_node",
                                          "resolve_leaf", "resolve_node", "clear", "exchange", "dist_bucket",
-                                         "dist_owner", "dist_ids", "dist_remap", "tail"};
+                                         "dist_owner", "dist_ids", "dist_remap", "tail", "sort", "dag_write"};
   return names[k];
 }
 
@@ -145,6 +145,7 @@ struct LeafLevel {
 }  // namespace gcz_host
 
 struct gcz_dist_state;   // gcz_dist.hip
+struct gcz_sort_state;   // gcz_sort.hip
 
 struct gcz_ctx {
   int device = 0;
@@ -173,6 +174,7 @@ struct gcz_ctx {
   double prof_ms[gcz_host::KID_COUNT] = {};
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
   gcz_dist_state* dist = nullptr;   // multi-rank build state (gcz_dist.hip)
+  gcz_sort_state* sortst = nullptr; // device sort / .dag writer state (gcz_sort.hip)
 
   int fail(int code, const char* what, const char* detail) {
     last_error = std::string(what) + ": " + detail;

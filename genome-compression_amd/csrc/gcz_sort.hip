@@ -1,0 +1,388 @@
+// Frequency sort, bytes() and the .dag writer on the device (SURVEY §8(f)
+// rows 1-2).  Reference: shared_tree::histogram / sort_leaves / sort_nodes /
+// sort_tree / rewire_nodes (src/shared_tree.cpp:316-483), bytes (:488-496),
+// serialize (:504-513), pointer::serialize (:122-142); spec: SURVEY App. C.
+//
+// Net effect of sort_tree: every child layer (the leaves and node layers
+// 0..D-2) is permuted independently by the reference counts its parent layer
+// holds, descending, ties by the old index (std::stable_sort); parents are
+// rewired with the m/t/v bits kept; the top layer and the root stay.  On the
+// device: one histogram pass per parent layer (atomicAdd), per child layer a
+// stable descending radix sort of (count, index) over the count's bits only
+// (skipped when every count is equal: the order is then the identity), one
+// gather/scatter pass that rewires and permutes every node layer at once.
+// The .dag is written by an exclusive scan of per-node byte sizes and one
+// byte-scatter pass.
+#include <hipcub/hipcub.hpp>
+
+#include "gcz_ctx.h"
+
+using namespace gcz_dev;
+using namespace gcz_host;
+
+struct gcz_sort_state {
+  DevBuf cnt, keys2, vals, vals2, newpos, mm, tmp, sizes, pos, acc, dag, nodes2, leaves2;
+  u32* h_mm = nullptr;
+};
+
+void gcz_sort_state_free(gcz_ctx* c) {
+  gcz_sort_state* s = c->sortst;
+  if (!s) return;
+  for (DevBuf* b : {&s->cnt, &s->keys2, &s->vals, &s->vals2, &s->newpos, &s->mm, &s->tmp, &s->sizes, &s->pos,
+                    &s->acc, &s->dag, &s->nodes2, &s->leaves2})
+    if (b->ptr) (void)hipFree(b->ptr);
+  if (s->h_mm) (void)hipHostFree(s->h_mm);
+  delete s;
+  c->sortst = nullptr;
+}
+
+namespace {
+
+constexpr u32 kSegStart1 = 16, kSegStart2 = 16 + 4096, kSegStart3 = 16 + 4096 + 1048576;
+
+__device__ __forceinline__ bool is_null(u32 w) { return ulw(w) == kIdx; }
+
+__device__ __forceinline__ u32 ptr_bytes(u32 w) {   // pointer::bytes, src/shared_tree.cpp:122-125
+  const u32 i = w & kIdx;
+  if (i == kIdx) return 4;
+  return i < kSegStart1 ? 1 : i < kSegStart2 ? 2 : i < kSegStart3 ? 3 : 4;
+}
+
+// pointer::serialize (src/shared_tree.cpp:133-142)
+__device__ __forceinline__ void put_ptr(unsigned char* o, u32 w) {
+  const u32 idx = w & kIdx;
+  u32 seg, off;
+  if (idx == kIdx) { seg = 3; off = 0xfffffffu; }
+  else if (idx < kSegStart1) { seg = 0; off = idx; }
+  else if (idx < kSegStart2) { seg = 1; off = idx - kSegStart1; }
+  else if (idx < kSegStart3) { seg = 2; off = idx - kSegStart2; }
+  else { seg = 3; off = idx - kSegStart3; }
+  const int bits = 4 + 8 * int(seg);
+  int sh = bits - 4;
+  *o++ = (unsigned char)((off >> sh) | (((w >> 29) & 1u) << 4) | (((w >> 30) & 1u) << 5) | (seg << 6));
+  for (sh -= 8; sh >= 0; sh -= 8) *o++ = (unsigned char)(off >> sh);
+}
+
+__device__ __forceinline__ void put_be(unsigned char* o, u64 v, int nbytes) {   // binary_write, utility.h:178-184
+  for (int i = nbytes - 1; i >= 0; --i) *o++ = (unsigned char)(v >> (8 * i));
+}
+
+// histogram (src/shared_tree.cpp:316-326): references of each child from the parent layer
+__global__ __launch_bounds__(kBlock) void k_hist(const u32* __restrict__ parent, u64 nwords, u32* __restrict__ cnt) {
+  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= nwords) return;
+  const u32 w = parent[i];
+  if (!is_null(w)) atomicAdd(&cnt[w & kIdx], 1u);
+}
+
+__global__ __launch_bounds__(kBlock) void k_minmax(const u32* __restrict__ cnt, u64 n, u32* __restrict__ mm) {
+  __shared__ u32 smin[kBlock / 64], smax[kBlock / 64];
+  u32 lo = ~0u, hi = 0;
+  for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < n; i += u64(gridDim.x) * kBlock) {
+    const u32 c = cnt[i];
+    lo = min(lo, c);
+    hi = max(hi, c);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, u32(__shfl_xor(int(lo), o, 64)));
+    hi = max(hi, u32(__shfl_xor(int(hi), o, 64)));
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) { smin[wave] = lo; smax[wave] = hi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kBlock / 64; ++w) { lo = min(lo, smin[w]); hi = max(hi, smax[w]); }
+    atomicMin(&mm[0], lo);
+    atomicMax(&mm[1], hi);
+  }
+}
+
+__global__ void k_mm_init(u32* mm, int D) {
+  for (int i = threadIdx.x; i < D; i += blockDim.x) { mm[2 * i] = ~0u; mm[2 * i + 1] = 0u; }
+}
+
+__global__ __launch_bounds__(kBlock) void k_iota(u32* __restrict__ v, u64 n) {
+  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i < n) v[i] = u32(i);
+}
+
+// invert_indices (src/shared_tree.cpp:360-365): newpos[old] = new
+__global__ __launch_bounds__(kBlock) void k_invert(const u32* __restrict__ sorted_old, u64 n,
+                                                   u32* __restrict__ newpos) {
+  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i < n) newpos[sorted_old[i]] = u32(i);
+}
+
+__global__ __launch_bounds__(kBlock) void k_perm_leaves(const u64* __restrict__ in, u64 n,
+                                                        const u32* __restrict__ newpos, u64* __restrict__ out) {
+  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i < n) out[newpos[i]] = in[i];
+}
+
+// rewire_nodes (:383-403) with the child permutation, reorder_layer (:371-377) with the own one
+__global__ __launch_bounds__(kBlock) void k_perm_nodes(const uint2* __restrict__ in, u64 n,
+                                                       const u32* __restrict__ child_newpos,
+                                                       const u32* __restrict__ own_newpos, uint2* __restrict__ out) {
+  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  uint2 w = in[i];
+  if (child_newpos) {
+    if (!is_null(w.x)) w.x = (w.x & kBits) | child_newpos[w.x & kIdx];
+    if (!is_null(w.y)) w.y = (w.y & kBits) | child_newpos[w.y & kIdx];
+  }
+  out[own_newpos ? own_newpos[i] : i] = w;
+}
+
+struct LayerStarts {
+  u64 node[GCZ_MAX_LAYERS + 1];   // storage start of each layer within the node buffer (+ the end)
+  u64 count[GCZ_MAX_LAYERS];      // nodes of each layer (storage holds ceil(n/2) slots, count <= that)
+};
+
+__device__ __forceinline__ int layer_of(const LayerStarts& ls, int D, u64 g) {
+  int k = 0;
+  while (k + 1 < D && g >= ls.node[k + 1]) ++k;
+  return k;
+}
+
+// Byte size of every storage slot (0 past a layer's node count) and their sum.
+__global__ __launch_bounds__(kBlock) void k_node_sizes(const uint2* __restrict__ nodes, u64 n, LayerStarts ls, int D,
+                                                       u32* __restrict__ sz, unsigned long long* __restrict__ acc) {
+  __shared__ u32 part[kBlock / 64];
+  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
+  u32 b = 0;
+  if (i < n) {
+    const int k = layer_of(ls, D, i);
+    if (i - ls.node[k] < ls.count[k]) {
+      const uint2 w = nodes[i];
+      b = ptr_bytes(w.x) + ptr_bytes(w.y);
+    }
+    if (sz) sz[i] = b;
+  }
+  for (int o = 32; o > 0; o >>= 1) b += u32(__shfl_xor(int(b), o, 64));
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = b;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u32 t = 0;
+    for (int w = 0; w < kBlock / 64; ++w) t += part[w];
+    atomicAdd(acc, (unsigned long long)t);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_write_nodes(const uint2* __restrict__ nodes, u64 n,
+                                                        const u64* __restrict__ pos, LayerStarts ls, int D, u64 hdr,
+                                                        unsigned char* __restrict__ out) {
+  const u64 g = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (g >= n) return;
+  const int k = layer_of(ls, D, g);
+  if (g - ls.node[k] >= ls.count[k]) return;
+  unsigned char* o = out + hdr + 8 * u64(k + 1) + pos[g];
+  const uint2 w = nodes[g];
+  put_ptr(o, w.x);
+  put_ptr(o + ptr_bytes(w.x), w.y);
+}
+
+__global__ __launch_bounds__(kBlock) void k_write_leaves(const u64* __restrict__ leaves, u64 n, int lb, u64 base,
+                                                         unsigned char* __restrict__ out) {
+  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i < n) put_be(out + base + i * u64(lb), leaves[i], lb);
+}
+
+// root pointer, leaf count and every layer's count (its position needs the scan)
+__global__ void k_write_headers(u32 root, u64 n_leaves, LayerStarts ls, int D, u64 hdr,
+                                const u64* __restrict__ pos, const u32* __restrict__ sz, unsigned char* __restrict__ out) {
+  put_ptr(out, root);
+  put_be(out + ptr_bytes(root), n_leaves, 8);
+  for (int k = 0; k < D; ++k) {
+    const u64 g = ls.node[k];
+    const u64 before = g < ls.node[D] ? pos[g] : (pos[ls.node[D] - 1] + sz[ls.node[D] - 1]);
+    put_be(out + hdr + 8 * u64(k) + before, ls.count[k], 8);
+  }
+}
+
+dim3 grid_of(u64 n) { return dim3(unsigned(std::max<u64>(1, (n + kBlock - 1) / kBlock))); }
+
+LayerStarts layer_starts(const gcz_ctx* c) {
+  LayerStarts ls{};
+  const int D = c->info.n_layers;
+  for (int k = 0; k <= D; ++k) ls.node[k] = c->layer_off[k];
+  for (int k = 0; k < D; ++k) ls.count[k] = c->info.layer_size[k];
+  return ls;
+}
+
+u32 host_ptr_bytes(u32 w) {
+  const u32 i = w & kIdx;
+  if (i == kIdx) return 4;
+  return i < kSegStart1 ? 1 : i < kSegStart2 ? 2 : i < kSegStart3 ? 3 : 4;
+}
+
+}  // namespace
+
+#define S_HIP(x)                                                                         \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) return c->fail(GCZ_ERR_DEVICE, #x, hipGetErrorString(e_));     \
+  } while (0)
+
+extern "C" {
+
+int gcz_sort_device(gcz_ctx* c) {
+  if (!c || c->info.status != GCZ_OK || c->info.n_layers < 1) return GCZ_ERR_ARG;
+  S_HIP(hipSetDevice(c->device));
+  if (!c->sortst) c->sortst = new gcz_sort_state();
+  gcz_sort_state& s = *c->sortst;
+  const int D = c->info.n_layers;
+  const u64 nl = c->info.n_leaves;
+  // child layer cl: 0 = leaves (parent: node layer 0), cl = k + 1 = node layer k (parent: layer k + 1)
+  std::vector<u64> n_of(D), coff(D + 1, 0);
+  for (int cl = 0; cl < D; ++cl) {
+    n_of[cl] = cl == 0 ? nl : c->info.layer_size[cl - 1];
+    coff[cl + 1] = coff[cl] + n_of[cl];
+  }
+  u64 nmax = 0;
+  for (u64 v : n_of) nmax = std::max(nmax, v);
+  const u64 N = c->layer_off[D];
+  int rc;
+  if ((rc = c->ensure(s.cnt, coff[D] * 4 + 16)) || (rc = c->ensure(s.newpos, coff[D] * 4 + 16)) ||
+      (rc = c->ensure(s.keys2, nmax * 4 + 16)) || (rc = c->ensure(s.vals, nmax * 4 + 16)) ||
+      (rc = c->ensure(s.vals2, nmax * 4 + 16)) || (rc = c->ensure(s.mm, size_t(D) * 8 + 16)) ||
+      (rc = c->ensure(s.nodes2, N * 8 + 16)) || (rc = c->ensure(s.leaves2, nl * 8 + 16)))
+    return rc;
+  if (!s.h_mm) S_HIP(hipHostMalloc((void**)&s.h_mm, size_t(GCZ_MAX_LAYERS) * 8, hipHostMallocDefault));
+  hipEvent_t e0{};
+  c->prof_begin(KID_SORT, e0);
+  u32* cnt = s.cnt.as<u32>();
+  u32* mm = s.mm.as<u32>();
+  S_HIP(hipMemsetAsync(cnt, 0, coff[D] * 4, c->stream));
+  hipLaunchKernelGGL(k_mm_init, dim3(1), dim3(64), 0, c->stream, mm, D);   // [min, max] per child layer
+  const uint2* nodes = c->nodes_out.as<uint2>();
+  for (int cl = 0; cl < D; ++cl) {
+    const u64 np = c->info.layer_size[cl];   // parent layer cl
+    hipLaunchKernelGGL(k_hist, grid_of(2 * np), dim3(kBlock), 0, c->stream,
+                       reinterpret_cast<const u32*>(nodes + c->layer_off[cl]), 2 * np, cnt + coff[cl]);
+    if (n_of[cl])
+      hipLaunchKernelGGL(k_minmax, dim3(unsigned(std::min<u64>(1024, (n_of[cl] + kBlock - 1) / kBlock))),
+                         dim3(kBlock), 0, c->stream, cnt + coff[cl], n_of[cl], mm + 2 * cl);
+  }
+  S_HIP(hipGetLastError());
+  S_HIP(hipMemcpyAsync(s.h_mm, mm, size_t(D) * 8, hipMemcpyDeviceToHost, c->stream));
+  S_HIP(hipStreamSynchronize(c->stream));
+  std::vector<bool> ident(D);
+  for (int cl = 0; cl < D; ++cl) ident[cl] = n_of[cl] <= 1 || s.h_mm[2 * cl] == s.h_mm[2 * cl + 1];
+  // stable descending sort of (count, index) per non-trivial child layer
+  for (int cl = 0; cl < D; ++cl) {
+    if (ident[cl]) continue;
+    const u64 n = n_of[cl];
+    const int bits = std::max<int>(1, int(bit_width(s.h_mm[2 * cl + 1])));
+    hipLaunchKernelGGL(k_iota, grid_of(n), dim3(kBlock), 0, c->stream, s.vals.as<u32>(), n);
+    size_t tmp_bytes = 0;
+    S_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp_bytes, cnt + coff[cl], s.keys2.as<u32>(),
+                                                       s.vals.as<u32>(), s.vals2.as<u32>(), n, 0, bits, c->stream));
+    if ((rc = c->ensure(s.tmp, tmp_bytes + 16))) return rc;
+    S_HIP(hipcub::DeviceRadixSort::SortPairsDescending(s.tmp.ptr, tmp_bytes, cnt + coff[cl], s.keys2.as<u32>(),
+                                                       s.vals.as<u32>(), s.vals2.as<u32>(), n, 0, bits, c->stream));
+    hipLaunchKernelGGL(k_invert, grid_of(n), dim3(kBlock), 0, c->stream, s.vals2.as<u32>(), n,
+                       s.newpos.as<u32>() + coff[cl]);
+  }
+  // apply: leaves, then every node layer (rewire children, permute itself)
+  if (!ident[0] && nl) {
+    hipLaunchKernelGGL(k_perm_leaves, grid_of(nl), dim3(kBlock), 0, c->stream, c->leaves_out.as<u64>(), nl,
+                       s.newpos.as<u32>(), s.leaves2.as<u64>());
+    std::swap(c->leaves_out, s.leaves2);
+  }
+  for (int k = 0; k < D; ++k) {
+    const u64 n = c->info.layer_size[k];
+    const u32* child = ident[k] ? nullptr : s.newpos.as<u32>() + coff[k];
+    const u32* own = (k + 1 < D && !ident[k + 1]) ? s.newpos.as<u32>() + coff[k + 1] : nullptr;
+    hipLaunchKernelGGL(k_perm_nodes, grid_of(n), dim3(kBlock), 0, c->stream, nodes + c->layer_off[k], n, child, own,
+                       s.nodes2.as<uint2>() + c->layer_off[k]);
+  }
+  S_HIP(hipGetLastError());
+  std::swap(c->nodes_out, s.nodes2);
+  c->prof_end(KID_SORT, e0);
+  S_HIP(hipStreamSynchronize(c->stream));
+  return GCZ_OK;
+}
+
+int gcz_bytes_device(gcz_ctx* c, uint64_t* out) {
+  if (!c || !out || c->info.status != GCZ_OK) return GCZ_ERR_ARG;
+  S_HIP(hipSetDevice(c->device));
+  if (!c->sortst) c->sortst = new gcz_sort_state();
+  gcz_sort_state& s = *c->sortst;
+  if (int rc = c->ensure(s.acc, 16)) return rc;
+  S_HIP(hipMemsetAsync(s.acc.ptr, 0, 8, c->stream));
+  const int D = c->info.n_layers;
+  const u64 N = c->layer_off[D];
+  const LayerStarts ls = layer_starts(c);
+  hipLaunchKernelGGL(k_node_sizes, grid_of(N), dim3(kBlock), 0, c->stream, c->nodes_out.as<uint2>(), N, ls, D,
+                     nullptr, s.acc.as<unsigned long long>());
+  S_HIP(hipGetLastError());
+  u64 nb = 0;
+  S_HIP(hipMemcpyAsync(&nb, s.acc.ptr, 8, hipMemcpyDeviceToHost, c->stream));
+  S_HIP(hipStreamSynchronize(c->stream));
+  *out = host_ptr_bytes(c->info.root) + 8 + c->info.n_leaves * u64((c->info.L + 1) / 2) +
+         8 * u64(c->info.n_layers) + nb;
+  return GCZ_OK;
+}
+
+// The .dag bytes into device memory (d_out == null: a context buffer); *written = size.
+static int serialize_on_device(gcz_ctx* c, unsigned char** d_dag, uint64_t* written) {
+  if (!c->sortst) c->sortst = new gcz_sort_state();
+  gcz_sort_state& s = *c->sortst;
+  uint64_t total = 0;
+  if (int rc = gcz_bytes_device(c, &total)) return rc;
+  const int D = c->info.n_layers;
+  const u64 N = c->layer_off[D];
+  int rc;
+  if ((rc = c->ensure(s.sizes, N * 4 + 16)) || (rc = c->ensure(s.pos, N * 8 + 16)) ||
+      (rc = c->ensure(s.dag, total + 16)))
+    return rc;
+  hipEvent_t e0{};
+  c->prof_begin(KID_DAG, e0);
+  S_HIP(hipMemsetAsync(s.acc.ptr, 0, 8, c->stream));
+  const LayerStarts ls = layer_starts(c);
+  hipLaunchKernelGGL(k_node_sizes, grid_of(N), dim3(kBlock), 0, c->stream, c->nodes_out.as<uint2>(), N, ls, D,
+                     s.sizes.as<u32>(), s.acc.as<unsigned long long>());
+  size_t tmp_bytes = 0;
+  S_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, s.sizes.as<u32>(), s.pos.as<u64>(), N, c->stream));
+  if ((rc = c->ensure(s.tmp, tmp_bytes + 16))) return rc;
+  S_HIP(hipcub::DeviceScan::ExclusiveSum(s.tmp.ptr, tmp_bytes, s.sizes.as<u32>(), s.pos.as<u64>(), N, c->stream));
+  const int lb = (c->info.L + 1) / 2;
+  const u64 hdr = host_ptr_bytes(c->info.root) + 8 + c->info.n_leaves * u64(lb);
+  unsigned char* out = s.dag.as<unsigned char>();
+  hipLaunchKernelGGL(k_write_headers, dim3(1), dim3(1), 0, c->stream, c->info.root, c->info.n_leaves, ls, D, hdr,
+                     s.pos.as<u64>(), s.sizes.as<u32>(), out);
+  hipLaunchKernelGGL(k_write_leaves, grid_of(c->info.n_leaves), dim3(kBlock), 0, c->stream,
+                     c->leaves_out.as<u64>(), c->info.n_leaves, lb, host_ptr_bytes(c->info.root) + 8, out);
+  hipLaunchKernelGGL(k_write_nodes, grid_of(N), dim3(kBlock), 0, c->stream, c->nodes_out.as<uint2>(), N,
+                     s.pos.as<u64>(), ls, D, hdr, out);
+  S_HIP(hipGetLastError());
+  c->prof_end(KID_DAG, e0);
+  *d_dag = out;
+  *written = total;
+  return GCZ_OK;
+}
+
+int gcz_serialize_device(gcz_ctx* c, uint8_t* host_buf, uint64_t cap, uint64_t* written) {
+  if (!c || !written || c->info.status != GCZ_OK) return GCZ_ERR_ARG;
+  S_HIP(hipSetDevice(c->device));
+  unsigned char* d = nullptr;
+  uint64_t n = 0;
+  if (int rc = serialize_on_device(c, &d, &n)) return rc;
+  *written = n;
+  if (!host_buf || cap < n) {
+    S_HIP(hipStreamSynchronize(c->stream));
+    return GCZ_ERR_ARG;
+  }
+  S_HIP(hipMemcpyAsync(host_buf, d, n, hipMemcpyDeviceToHost, c->stream));
+  S_HIP(hipStreamSynchronize(c->stream));
+  return GCZ_OK;
+}
+
+const uint8_t* gcz_device_dag(gcz_ctx* c, uint64_t* written) {
+  if (!c || !written || c->info.status != GCZ_OK || hipSetDevice(c->device) != hipSuccess) return nullptr;
+  unsigned char* d = nullptr;
+  if (serialize_on_device(c, &d, written)) return nullptr;
+  return hipStreamSynchronize(c->stream) == hipSuccess ? d : nullptr;
+}
+
+}  // extern "C"

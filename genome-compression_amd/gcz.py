@@ -89,6 +89,10 @@ _SIGS = {
     "gcz_fasta_extract": (_U64, [_P, _U64, _P]),
     "gcz_synth_fill": (None, [_P, ctypes.c_int, _U64, _U64, _U64]),
     "gcz_synth_default_seed": (_U64, []),
+    "gcz_sort_device": (ctypes.c_int, [_P]),
+    "gcz_bytes_device": (ctypes.c_int, [_P, ctypes.POINTER(_U64)]),
+    "gcz_serialize_device": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
+    "gcz_device_dag": (_P, [_P, ctypes.POINTER(_U64)]),
     "gcz_dist_unique_id": (ctypes.c_int, [_P, _U64]),
     "gcz_group_create_rccl": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _P, ctypes.POINTER(_P)]),
     "gcz_group_create_local": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
@@ -366,6 +370,30 @@ class Context:
             _lib.gcz_tree_free(t)
             raise GczError(rc, "gcz_tree_fetch failed")
         return Tree(t)
+
+    # ---- ratio path on the device (frequency sort, bytes(), .dag) ----
+    def sort_device(self):
+        """shared_tree::sort_tree on the device, in place on the last build."""
+        rc = _lib.gcz_sort_device(self._h)
+        if rc != GCZ_OK:
+            raise GczError(rc, "gcz_sort_device: " + _lib.gcz_ctx_last_error(self._h).decode())
+
+    def bytes_device(self) -> int:
+        out = _U64()
+        rc = _lib.gcz_bytes_device(self._h, ctypes.byref(out))
+        if rc != GCZ_OK:
+            raise GczError(rc, "gcz_bytes_device failed")
+        return int(out.value)
+
+    def serialize_device(self) -> bytes:
+        """The .dag bytes written on the device (shared_tree::serialize)."""
+        n = _U64()
+        _lib.gcz_serialize_device(self._h, None, 0, ctypes.byref(n))
+        buf = np.empty(max(int(n.value), 1), dtype=np.uint8)
+        rc = _lib.gcz_serialize_device(self._h, _ptr(buf), buf.size, ctypes.byref(n))
+        if rc != GCZ_OK:
+            raise GczError(rc, "gcz_serialize_device failed")
+        return buf[:int(n.value)].tobytes()
 
     def profile(self, on=True):
         _lib.gcz_profile_enable(self._h, int(on))

@@ -149,6 +149,17 @@ GCZ_API uint64_t gcz_fasta_extract(const uint8_t *file, uint64_t n, uint8_t *out
 GCZ_API void gcz_synth_fill(char *out, int kind, uint64_t seed, uint64_t begin, uint64_t end);
 GCZ_API uint64_t gcz_synth_default_seed(void);
 
+/* ---- frequency sort, bytes(), .dag on the device ----------
+ * Act on the last build of ctx, in place: the same result as gcz_tree_sort /
+ * gcz_tree_bytes / gcz_tree_serialize on the fetched tree (reference
+ * shared_tree::sort_tree, bytes, serialize: src/shared_tree.cpp:443-513). */
+GCZ_API int gcz_sort_device(gcz_ctx *ctx);
+GCZ_API int gcz_bytes_device(gcz_ctx *ctx, uint64_t *out);
+/* .dag bytes into host_buf (cap >= *written, else GCZ_ERR_ARG with *written set). */
+GCZ_API int gcz_serialize_device(gcz_ctx *ctx, uint8_t *host_buf, uint64_t cap, uint64_t *written);
+/* .dag bytes left in device memory owned by ctx (valid until the next call). */
+GCZ_API const uint8_t *gcz_device_dag(gcz_ctx *ctx, uint64_t *written);
+
 /* ---- multi-rank build ---------------------
  * R ranks own contiguous strand ranges; every hash-consed level is reconciled
  * through key owners (all-to-all), ids stay the global first-occurrence ranks,
