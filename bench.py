@@ -310,6 +310,18 @@ def main():
             dag = ctx.serialize_device()
             parity["device_dag_sha256_match"] = hashlib.sha256(dag).hexdigest() == exp["sha_dag"]
         del dptr
+        # decompression on the device (operator[] for every index) and the round trip
+        text = ctx.upload(np.zeros(S * L, dtype=np.uint8))
+        ctx.sync()
+        t0 = time.perf_counter()
+        rc = gcz._lib.gcz_decompress_device(ctx._h, gcz.ctypes.c_void_p(text.ptr), S * L)
+        ratio_path["device_decompress_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+        if rc == 0 and not args.no_parity:
+            got = np.empty(S * L, dtype=np.uint8)
+            gcz._lib.gcz_memcpy_d2h(ctx._h, gcz._ptr(got), gcz.ctypes.c_void_p(text.ptr), S * L)
+            ref = gcz.synth(cfg["kind"], S * L, seed)
+            ratio_path["roundtrip_match"] = bool(np.array_equal(got, np.where(ref >= 97, ref - 32, ref)))
+        text.free()
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -21,7 +21,7 @@ using namespace gcz_dev;
 using namespace gcz_host;
 
 struct gcz_sort_state {
-  DevBuf cnt, keys2, vals, vals2, newpos, mm, tmp, sizes, pos, acc, dag, nodes2, leaves2;
+  DevBuf cnt, keys2, vals, vals2, newpos, mm, tmp, sizes, pos, acc, dag, nodes2, leaves2, dw1, dw2, text;
   u32* h_mm = nullptr;
 };
 
@@ -29,7 +29,7 @@ void gcz_sort_state_free(gcz_ctx* c) {
   gcz_sort_state* s = c->sortst;
   if (!s) return;
   for (DevBuf* b : {&s->cnt, &s->keys2, &s->vals, &s->vals2, &s->newpos, &s->mm, &s->tmp, &s->sizes, &s->pos,
-                    &s->acc, &s->dag, &s->nodes2, &s->leaves2})
+                    &s->acc, &s->dag, &s->nodes2, &s->leaves2, &s->dw1, &s->dw2, &s->text})
     if (b->ptr) (void)hipFree(b->ptr);
   if (s->h_mm) (void)hipHostFree(s->h_mm);
   delete s;
@@ -197,6 +197,47 @@ __global__ void k_write_headers(u32 root, u64 n_leaves, LayerStarts ls, int D, u
     const u64 before = g < ls.node[D] ? pos[g] : (pos[ls.node[D] - 1] + sz[ls.node[D] - 1]);
     put_be(out + hdr + 8 * u64(k) + before, ls.count[k], 8);
   }
+}
+
+// ---- decompression ---------------------------------------------
+// shared_tree::operator[] (src/shared_tree.cpp:268-291) for every index at once,
+// top-down one layer per launch: a word w referencing node (l, r) of layer k
+// stands for (M(r), M(l)) with w's transpose bit applied when w is mirrored,
+// else (l, r) with it (the transform ctor, :76-80); access_leaf (:230-235)
+// applies mirror / transpose to the canonical leaf.
+__global__ __launch_bounds__(kBlock) void k_expand(const u32* __restrict__ w_in, u64 pw,
+                                                   const uint2* __restrict__ layer, u32* __restrict__ w_out,
+                                                   u64 nout) {
+  const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (j >= pw) return;
+  const u32 w = w_in[j];
+  const uint2 nd = layer[w & kIdx];
+  const u32 m = (w >> 29) & 1u, t = (w >> 30) & 1u;
+  const u32 a = m ? xf(nd.y, 1, t) : xf(nd.x, 0, t);
+  const u32 b = m ? xf(nd.x, 1, t) : xf(nd.y, 0, t);
+  w_out[2 * j] = a;
+  if (2 * j + 1 < nout) w_out[2 * j + 1] = b;
+}
+
+__constant__ char kSym[16] = {'S', 'A', 'C', 'R', 'G', 'B', 'N', 'K', 'T', 'W', 'V', 'D', 'Y', 'H', 'M', '-'};
+
+// One strand per thread, staged through LDS so the text is stored coalesced.
+__global__ __launch_bounds__(kBlock) void k_leaves_text(const u32* __restrict__ words, u64 S,
+                                                        const u64* __restrict__ leaves, int L,
+                                                        unsigned char* __restrict__ out) {
+  __shared__ unsigned char buf[kBlock * 16];
+  const u64 s0 = u64(blockIdx.x) * kBlock;
+  const u64 s = s0 + threadIdx.x;
+  if (s < S) {
+    const u32 w = words[s];
+    u64 v = leaves[w & kIdx];
+    if ((w >> 29) & 1u) v = leaf_mirrored(v, L);
+    if ((w >> 30) & 1u) v = leaf_transposed(v);
+    for (int i = 0; i < L; ++i) buf[threadIdx.x * L + i] = (unsigned char)kSym[(v >> (4 * i)) & 15];
+  }
+  __syncthreads();
+  const u64 nstr = S - s0 < u64(kBlock) ? S - s0 : u64(kBlock);
+  for (u64 b = threadIdx.x; b < nstr * u64(L); b += kBlock) out[s0 * L + b] = buf[b];
 }
 
 dim3 grid_of(u64 n) { return dim3(unsigned(std::max<u64>(1, (n + kBlock - 1) / kBlock))); }
@@ -375,6 +416,49 @@ int gcz_serialize_device(gcz_ctx* c, uint8_t* host_buf, uint64_t cap, uint64_t* 
   }
   S_HIP(hipMemcpyAsync(host_buf, d, n, hipMemcpyDeviceToHost, c->stream));
   S_HIP(hipStreamSynchronize(c->stream));
+  return GCZ_OK;
+}
+
+int gcz_decompress_device(gcz_ctx* c, void* d_out, uint64_t cap) {
+  if (!c || !d_out || c->info.status != GCZ_OK || c->info.n_layers < 1) return GCZ_ERR_ARG;
+  const u64 S = c->info.n_strands;
+  const int L = c->info.L;
+  if (cap < S * u64(L)) return GCZ_ERR_ARG;
+  S_HIP(hipSetDevice(c->device));
+  if (!c->sortst) c->sortst = new gcz_sort_state();
+  gcz_sort_state& s = *c->sortst;
+  if (int rc = c->ensure(s.dw1, S * 4 + 16)) return rc;
+  if (int rc = c->ensure(s.dw2, S * 4 + 16)) return rc;
+  const int D = c->info.n_layers;
+  // element counts: the input of node layer k has n[k] words (n[0] = S), its output n[k + 1]
+  std::vector<u64> n(D + 1);
+  n[0] = S;
+  for (int k = 0; k < D; ++k) n[k + 1] = (n[k] + 1) / 2;
+  u32* cur = s.dw1.as<u32>();
+  u32* nxt = s.dw2.as<u32>();
+  S_HIP(hipMemcpyAsync(cur, &c->info.root, 4, hipMemcpyHostToDevice, c->stream));
+  S_HIP(hipStreamSynchronize(c->stream));   // the root came from a host variable
+  for (int k = D - 1; k >= 0; --k) {
+    hipLaunchKernelGGL(k_expand, grid_of(n[k + 1]), dim3(kBlock), 0, c->stream, cur, n[k + 1],
+                       c->nodes_out.as<uint2>() + c->layer_off[k], nxt, n[k]);
+    std::swap(cur, nxt);
+  }
+  hipLaunchKernelGGL(k_leaves_text, grid_of(S), dim3(kBlock), 0, c->stream, cur, S, c->leaves_out.as<u64>(), L,
+                     static_cast<unsigned char*>(d_out));
+  S_HIP(hipGetLastError());
+  S_HIP(hipStreamSynchronize(c->stream));
+  return GCZ_OK;
+}
+
+int gcz_decompress(gcz_ctx* c, uint8_t* host_out, uint64_t cap) {
+  if (!c || !host_out || c->info.status != GCZ_OK) return GCZ_ERR_ARG;
+  const u64 n = c->info.n_strands * u64(c->info.L);
+  if (cap < n) return GCZ_ERR_ARG;
+  S_HIP(hipSetDevice(c->device));
+  if (!c->sortst) c->sortst = new gcz_sort_state();
+  if (int rc = c->ensure(c->sortst->text, n + 16)) return rc;
+  if (int rc = gcz_decompress_device(c, c->sortst->text.ptr, n)) return rc;
+  S_HIP(hipMemcpy(host_out, c->sortst->text.ptr, n, hipMemcpyDeviceToHost));
   return GCZ_OK;
 }
 

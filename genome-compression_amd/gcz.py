@@ -93,6 +93,8 @@ _SIGS = {
     "gcz_bytes_device": (ctypes.c_int, [_P, ctypes.POINTER(_U64)]),
     "gcz_serialize_device": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
     "gcz_device_dag": (_P, [_P, ctypes.POINTER(_U64)]),
+    "gcz_decompress_device": (ctypes.c_int, [_P, _P, _U64]),
+    "gcz_decompress": (ctypes.c_int, [_P, _P, _U64]),
     "gcz_dist_unique_id": (ctypes.c_int, [_P, _U64]),
     "gcz_group_create_rccl": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _P, ctypes.POINTER(_P)]),
     "gcz_group_create_local": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
@@ -394,6 +396,16 @@ class Context:
         if rc != GCZ_OK:
             raise GczError(rc, "gcz_serialize_device failed")
         return buf[:int(n.value)].tobytes()
+
+    def decompress(self) -> bytes:
+        """The genome the last build represents (upper-case IUPAC, S*L symbols), decoded on the device."""
+        i = self.info()
+        n = i["n_strands"] * i["L"]
+        buf = np.empty(max(n, 1), dtype=np.uint8)
+        rc = _lib.gcz_decompress(self._h, _ptr(buf), n)
+        if rc != GCZ_OK:
+            raise GczError(rc, "gcz_decompress failed")
+        return buf[:n].tobytes()
 
     def profile(self, on=True):
         _lib.gcz_profile_enable(self._h, int(on))

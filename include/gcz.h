@@ -160,6 +160,11 @@ GCZ_API int gcz_serialize_device(gcz_ctx *ctx, uint8_t *host_buf, uint64_t cap, 
 /* .dag bytes left in device memory owned by ctx (valid until the next call). */
 GCZ_API const uint8_t *gcz_device_dag(gcz_ctx *ctx, uint64_t *written);
 
+/* Decompression of the last build (shared_tree::operator[] / iterator for every
+ * index, src/shared_tree.cpp:268-291,553-614): S*L upper-case IUPAC symbols. */
+GCZ_API int gcz_decompress_device(gcz_ctx *ctx, void *d_out, uint64_t cap);
+GCZ_API int gcz_decompress(gcz_ctx *ctx, uint8_t *host_out, uint64_t cap);
+
 /* ---- multi-rank build ---------------------
  * R ranks own contiguous strand ranges; every hash-consed level is reconciled
  * through key owners (all-to-all), ids stay the global first-occurrence ranks,

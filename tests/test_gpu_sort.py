@@ -74,3 +74,39 @@ def test_device_sort_1g(ctx, gcz, manifest):
     ctx.sort_device()
     dag = ctx.serialize_device()
     assert hashlib.sha256(dag).hexdigest() == exp["sha_dag"]
+
+
+# ---- decompression: operator[] for every index, on the device ----
+SYM = np.frombuffer(b"SACRGBNKTWVDYHM-", dtype=np.uint8)
+
+
+def _expected_text(kind, payload, L, gcz):
+    if kind == "fasta":
+        b = np.frombuffer(gcz.fasta_extract(payload), dtype=np.uint8)
+        b = b[:len(b) // L * L]
+        return np.where((b >= 97) & (b <= 122), b - 32, b).astype(np.uint8).tobytes()
+    lv = np.asarray(payload, dtype=np.uint64)
+    nib = (lv[:, None] >> (4 * np.arange(L, dtype=np.uint64))[None, :]) & np.uint64(15)
+    return SYM[nib.astype(np.int64)].tobytes()
+
+
+@pytest.mark.parametrize("name", _names(12_000_000))
+def test_device_decompress_round_trip(name, ctx, gcz, manifest):
+    case = manifest[name]
+    kind, payload, L = case_input(case, gcz)
+    _build(ctx, kind, payload, L)
+    expect = _expected_text(kind, payload, L, gcz)
+    assert ctx.decompress() == expect
+    ctx.sort_device()                      # a permuted tree still spells the same genome
+    assert ctx.decompress() == expect
+
+
+@pytest.mark.slow
+def test_device_decompress_1g(ctx, gcz):
+    data = gcz.synth(0, 1_000_000_000)
+    buf = ctx.upload(data)
+    ctx.build_device_bases(buf.ptr, data.size, 12)
+    buf.free()
+    text = np.frombuffer(ctx.decompress(), dtype=np.uint8)
+    up = data[:text.size]
+    assert np.array_equal(text, np.where(up >= 97, up - 32, up))
