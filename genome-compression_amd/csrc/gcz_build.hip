@@ -8,6 +8,7 @@ using namespace gcz_host;
 
 void gcz_dist_state_free(gcz_ctx* c);   // gcz_dist.hip
 void gcz_sort_state_free(gcz_ctx* c);   // gcz_sort.hip
+void gcz_ingest_state_free(gcz_ctx* c); // gcz_ingest.hip
 
 namespace {
 
@@ -375,6 +376,7 @@ void gcz_ctx_destroy(gcz_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   gcz_dist_state_free(c);
   gcz_sort_state_free(c);
+  gcz_ingest_state_free(c);
   for (DevBuf* b : {&c->wa, &c->wb, &c->grp, &c->desc, &c->tab, &c->leaves_out, &c->nodes_out, &c->hdr, &c->input,
                     &c->nf, &c->multi})
     if (b->ptr) (void)hipFree(b->ptr);
@@ -456,22 +458,16 @@ int gcz_build_host_leaves(gcz_ctx* c, const uint64_t* leaves, uint64_t S, int L)
 int gcz_build_host_fasta(gcz_ctx* c, const void* fasta, uint64_t nbytes, int L) {
   if (!c || (!fasta && nbytes)) return GCZ_ERR_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  // the raw file goes to the device; headers / line breaks are removed there (gcz_ingest.hip)
   const auto* f = static_cast<const uint8_t*>(fasta);
   const bool plain = nbytes == 0 || (f[0] != '>' && f[0] != '\n' && !std::memchr(f, '\n', nbytes));
-  std::vector<uint8_t> tmp;
-  const uint8_t* bases = f;
-  uint64_t nb = nbytes;
-  if (!plain) {
-    tmp.resize(nbytes);
-    nb = gcz_fasta_extract(f, nbytes, tmp.data());
-    bases = tmp.data();
-  }
-  if (int rc = c->ensure(c->input, nb + 16)) return rc;
-  if (nb && hipMemcpyAsync(c->input.ptr, bases, nb, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+  if (int rc = c->ensure(c->input, nbytes + 16)) return rc;
+  if (nbytes && hipMemcpyAsync(c->input.ptr, f, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess)
     return c->fail(GCZ_ERR_DEVICE, "gcz_build_host_fasta", "H2D copy failed");
   if (hipStreamSynchronize(c->stream) != hipSuccess)
     return c->fail(GCZ_ERR_DEVICE, "gcz_build_host_fasta", "sync failed");
-  return c->build(c->input.ptr, nullptr, nb, 0, L);
+  if (!plain) return gcz_build_device_fasta(c, c->input.ptr, nbytes, L);
+  return c->build(c->input.ptr, nullptr, nbytes, 0, L);
 }
 
 int gcz_info_get(gcz_ctx* c, gcz_info* out) {

@@ -146,6 +146,7 @@ struct LeafLevel {
 
 struct gcz_dist_state;   // gcz_dist.hip
 struct gcz_sort_state;   // gcz_sort.hip
+struct gcz_ingest_state; // gcz_ingest.hip
 
 struct gcz_ctx {
   int device = 0;
@@ -175,6 +176,7 @@ struct gcz_ctx {
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
   gcz_dist_state* dist = nullptr;   // multi-rank build state (gcz_dist.hip)
   gcz_sort_state* sortst = nullptr; // device sort / .dag writer state (gcz_sort.hip)
+  gcz_ingest_state* ingest = nullptr; // device FASTA ingest state (gcz_ingest.hip)
 
   int fail(int code, const char* what, const char* detail) {
     last_error = std::string(what) + ": " + detail;

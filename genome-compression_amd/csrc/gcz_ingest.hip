@@ -1,0 +1,236 @@
+// FASTA ingest on the device: the fasta_reader line
+// contract (src/fasta_reader.cpp:40-68) over a file already in
+// HBM, producing the concatenated bases the build consumes.
+//
+// At a line start the reader peeks once: '>' or '\n' skips that line, and the
+// line after a skipped one is data without a second peek.  So in a run of
+// consecutive marker lines (header or empty) the 1st, 3rd, ... are skipped and
+// the 2nd, 4th, ... are data; every other line is data.  On the device:
+//   1. newline positions (stream compaction),
+//   2. per line: marker flag, the last non-marker line before it (max-scan),
+//      hence skip / data and the data length; an exclusive sum gives each
+//      data line's output offset,
+//   3. a byte-parallel copy: each block stages the line boundaries of its
+//      2 KiB input window in LDS and every byte finds its line there.
+#include <hipcub/hipcub.hpp>
+
+#include "gcz_ctx.h"
+
+using namespace gcz_dev;
+using namespace gcz_host;
+
+struct gcz_ingest_state {
+  DevBuf nlpos, nsel, lastnm, len, off, tmp, bases;
+};
+
+void gcz_ingest_state_free(gcz_ctx* c) {
+  gcz_ingest_state* s = c->ingest;
+  if (!s) return;
+  for (DevBuf* b : {&s->nlpos, &s->nsel, &s->lastnm, &s->len, &s->off, &s->tmp, &s->bases})
+    if (b->ptr) (void)hipFree(b->ptr);
+  delete s;
+  c->ingest = nullptr;
+}
+
+namespace {
+
+constexpr int kWin = 2048;   // input bytes per copy block (LDS: 2 x 16 KiB line tables)
+
+struct IsNewline {
+  const unsigned char* f;
+  __device__ __forceinline__ bool operator()(const u64& i) const { return f[i] == '\n'; }
+};
+
+struct NewlineCount {
+  const unsigned char* f;
+  __device__ __forceinline__ u64 operator()(const u64& i) const { return f[i] == '\n' ? 1 : 0; }
+};
+
+// Line i spans [st, en): st = 0 or one past newline i-1, en = newline i or n.
+struct Lines {
+  const unsigned char* f;
+  const u64* nl;   // newline positions
+  u64 nnl, n, nlines;
+  __device__ __forceinline__ u64 st(u64 i) const { return i == 0 ? 0 : nl[i - 1] + 1; }
+  __device__ __forceinline__ u64 en(u64 i) const { return i < nnl ? nl[i] : n; }
+  __device__ __forceinline__ bool marker(u64 i) const {
+    const unsigned char c = f[st(i)];
+    return c == '>' || c == '\n';
+  }
+};
+
+// value for the max-scan: own index for a data-by-content line, -1 for a marker line
+struct NonMarkerIndex {
+  Lines ln;
+  __device__ __forceinline__ long long operator()(const u64& i) const { return ln.marker(i) ? -1ll : (long long)i; }
+};
+
+struct MaxOp {
+  __device__ __forceinline__ long long operator()(const long long& a, const long long& b) const { return a > b ? a : b; }
+};
+
+__device__ __forceinline__ bool skipped(const Lines& ln, const long long* lastnm, u64 i) {
+  if (!ln.marker(i)) return false;
+  const long long run0 = lastnm[i] + 1;            // first line of this run of marker lines
+  return ((long long)i - run0) % 2 == 0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_line_len(Lines ln, const long long* __restrict__ lastnm,
+                                                     u64* __restrict__ len) {
+  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= ln.nlines) return;
+  len[i] = skipped(ln, lastnm, i) ? 0 : ln.en(i) - ln.st(i);
+}
+
+// first line whose end is >= pos (the line containing pos, or starting at it)
+__device__ __forceinline__ u64 line_at(const Lines& ln, u64 pos) {
+  u64 lo = 0, hi = ln.nnl;   // newlines nl[0..nnl): line i ends at nl[i]
+  while (lo < hi) {
+    const u64 mid = (lo + hi) / 2;
+    if (ln.nl[mid] < pos) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(kBlock) void k_copy_lines(Lines ln, const long long* __restrict__ lastnm,
+                                                       const u64* __restrict__ off, unsigned char* __restrict__ out) {
+  __shared__ u64 s_st[kWin + 1];
+  __shared__ u64 s_off[kWin + 1];
+  __shared__ unsigned char s_data[kWin + 1];
+  __shared__ u64 s_l0;
+  __shared__ u32 s_cnt;
+  const u64 b0 = u64(blockIdx.x) * kWin;
+  const u64 b1 = b0 + kWin < ln.n ? b0 + kWin : ln.n;
+  if (threadIdx.x == 0) {
+    const u64 l0 = line_at(ln, b0);
+    const u64 l1 = line_at(ln, b1 == 0 ? 0 : b1 - 1);
+    s_l0 = l0;
+    s_cnt = u32(l1 - l0 + 1);
+  }
+  __syncthreads();
+  const u64 l0 = s_l0;
+  const u32 cnt = s_cnt;
+  for (u32 k = threadIdx.x; k < cnt; k += kBlock) {
+    const u64 i = l0 + k;
+    s_st[k] = ln.st(i);
+    const bool data = !skipped(ln, lastnm, i);
+    s_off[k] = off[i];
+    s_data[k] = data;
+  }
+  __syncthreads();
+  for (u64 p = b0 + threadIdx.x; p < b1; p += kBlock) {
+    const unsigned char c = ln.f[p];
+    if (c == '\n') continue;
+    u32 lo = 0, hi = cnt - 1;   // last local line with st <= p
+    while (lo < hi) {
+      const u32 mid = (lo + hi + 1) / 2;
+      if (s_st[mid] <= p) lo = mid;
+      else hi = mid - 1;
+    }
+    if (s_data[lo]) out[s_off[lo] + (p - s_st[lo])] = c;
+  }
+}
+
+dim3 grid_of(u64 n) { return dim3(unsigned(std::max<u64>(1, (n + kBlock - 1) / kBlock))); }
+
+}  // namespace
+
+#define I_HIP(x)                                                                         \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) return c->fail(GCZ_ERR_DEVICE, #x, hipGetErrorString(e_));     \
+  } while (0)
+
+// Bases of a FASTA file in device memory -> ctx-owned device buffer; returns the count.
+int gcz_fasta_extract_on_device(gcz_ctx* c, const unsigned char* d_file, u64 n, const unsigned char** d_bases,
+                                u64* nbases) {
+  if (!c->ingest) c->ingest = new gcz_ingest_state();
+  gcz_ingest_state& s = *c->ingest;
+  *nbases = 0;
+  *d_bases = nullptr;
+  int rc;
+  if ((rc = c->ensure(s.nsel, 16)) || (rc = c->ensure(s.bases, n + 16))) return rc;
+  *d_bases = s.bases.as<unsigned char>();
+  if (n == 0) return GCZ_OK;
+  // 1. newline positions (counted first, so the position array is exact)
+  hipcub::CountingInputIterator<u64> idx(0);
+  hipcub::TransformInputIterator<u64, NewlineCount, hipcub::CountingInputIterator<u64>> isnl(idx,
+                                                                                           NewlineCount{d_file});
+  size_t tmp_bytes = 0;
+  I_HIP(hipcub::DeviceReduce::Sum(nullptr, tmp_bytes, isnl, s.nsel.as<u64>(), n, c->stream));
+  if ((rc = c->ensure(s.tmp, tmp_bytes + 16))) return rc;
+  I_HIP(hipcub::DeviceReduce::Sum(s.tmp.ptr, tmp_bytes, isnl, s.nsel.as<u64>(), n, c->stream));
+  u64 nnl0 = 0;
+  I_HIP(hipMemcpyAsync(&nnl0, s.nsel.ptr, 8, hipMemcpyDeviceToHost, c->stream));
+  I_HIP(hipStreamSynchronize(c->stream));
+  if ((rc = c->ensure(s.nlpos, nnl0 * 8 + 16))) return rc;
+  tmp_bytes = 0;
+  I_HIP(hipcub::DeviceSelect::If(nullptr, tmp_bytes, idx, s.nlpos.as<u64>(), s.nsel.as<u64>(), n,
+                                 IsNewline{d_file}, c->stream));
+  if ((rc = c->ensure(s.tmp, tmp_bytes + 16))) return rc;
+  I_HIP(hipcub::DeviceSelect::If(s.tmp.ptr, tmp_bytes, idx, s.nlpos.as<u64>(), s.nsel.as<u64>(), n,
+                                 IsNewline{d_file}, c->stream));
+  u64 nnl = 0;
+  unsigned char last = 0;
+  I_HIP(hipMemcpyAsync(&nnl, s.nsel.ptr, 8, hipMemcpyDeviceToHost, c->stream));
+  I_HIP(hipMemcpyAsync(&last, d_file + n - 1, 1, hipMemcpyDeviceToHost, c->stream));
+  I_HIP(hipStreamSynchronize(c->stream));
+  Lines ln{d_file, s.nlpos.as<u64>(), nnl, n, nnl + (last != '\n' ? 1 : 0)};
+  const u64 L = ln.nlines;
+  // 2. skip / data per line, output offsets
+  if ((rc = c->ensure(s.lastnm, L * 8 + 16)) || (rc = c->ensure(s.len, L * 8 + 16)) ||
+      (rc = c->ensure(s.off, L * 8 + 16)))
+    return rc;
+  hipcub::TransformInputIterator<long long, NonMarkerIndex, hipcub::CountingInputIterator<u64>> nm(idx,
+                                                                                                 NonMarkerIndex{ln});
+  tmp_bytes = 0;
+  I_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tmp_bytes, nm, s.lastnm.as<long long>(), MaxOp{}, L, c->stream));
+  if ((rc = c->ensure(s.tmp, tmp_bytes + 16))) return rc;
+  I_HIP(hipcub::DeviceScan::InclusiveScan(s.tmp.ptr, tmp_bytes, nm, s.lastnm.as<long long>(), MaxOp{}, L,
+                                          c->stream));
+  hipLaunchKernelGGL(k_line_len, grid_of(L), dim3(kBlock), 0, c->stream, ln, s.lastnm.as<long long>(),
+                     s.len.as<u64>());
+  tmp_bytes = 0;
+  I_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, s.len.as<u64>(), s.off.as<u64>(), L, c->stream));
+  if ((rc = c->ensure(s.tmp, tmp_bytes + 16))) return rc;
+  I_HIP(hipcub::DeviceScan::ExclusiveSum(s.tmp.ptr, tmp_bytes, s.len.as<u64>(), s.off.as<u64>(), L, c->stream));
+  u64 tail[2] = {0, 0};
+  I_HIP(hipMemcpyAsync(&tail[0], s.off.as<u64>() + L - 1, 8, hipMemcpyDeviceToHost, c->stream));
+  I_HIP(hipMemcpyAsync(&tail[1], s.len.as<u64>() + L - 1, 8, hipMemcpyDeviceToHost, c->stream));
+  // 3. copy
+  hipLaunchKernelGGL(k_copy_lines, dim3(unsigned((n + kWin - 1) / kWin)), dim3(kBlock), 0, c->stream, ln,
+                     s.lastnm.as<long long>(), s.off.as<u64>(), s.bases.as<unsigned char>());
+  I_HIP(hipGetLastError());
+  I_HIP(hipStreamSynchronize(c->stream));
+  *nbases = tail[0] + tail[1];
+  return GCZ_OK;
+}
+
+extern "C" {
+
+int gcz_build_device_fasta(gcz_ctx* c, const void* d_file, uint64_t n, int L) {
+  if (!c || (!d_file && n)) return GCZ_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  const unsigned char* b = nullptr;
+  u64 nb = 0;
+  if (int rc = gcz_fasta_extract_on_device(c, static_cast<const unsigned char*>(d_file), n, &b, &nb)) return rc;
+  return c->build(b, nullptr, nb, 0, L);
+}
+
+int gcz_fasta_extract_device(gcz_ctx* c, const void* d_file, uint64_t n, void* d_out, uint64_t cap,
+                             uint64_t* nbases) {
+  if (!c || (!d_file && n) || !nbases) return GCZ_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  const unsigned char* b = nullptr;
+  u64 nb = 0;
+  if (int rc = gcz_fasta_extract_on_device(c, static_cast<const unsigned char*>(d_file), n, &b, &nb)) return rc;
+  *nbases = nb;
+  if (!d_out) return GCZ_OK;
+  if (cap < nb) return GCZ_ERR_ARG;
+  I_HIP(hipMemcpyAsync(d_out, b, nb, hipMemcpyDeviceToDevice, c->stream));
+  I_HIP(hipStreamSynchronize(c->stream));
+  return GCZ_OK;
+}
+
+}  // extern "C"

@@ -59,6 +59,8 @@ _SIGS = {
     "gcz_build_device_leaves": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
     "gcz_build_host_fasta": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
     "gcz_build_host_leaves": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
+    "gcz_build_device_fasta": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
+    "gcz_fasta_extract_device": (ctypes.c_int, [_P, _P, _U64, _P, _U64, ctypes.POINTER(_U64)]),
     "gcz_info_get": (ctypes.c_int, [_P, ctypes.POINTER(_Info)]),
     "gcz_copy_leaves": (ctypes.c_int, [_P, _P]),
     "gcz_copy_layer": (ctypes.c_int, [_P, ctypes.c_int, _P]),
@@ -361,6 +363,28 @@ class Context:
 
     def build_device_bases(self, dev_ptr: int, nbases: int, L: int = 12) -> dict:
         return self._check(_lib.gcz_build_device_bases(self._h, ctypes.c_void_p(dev_ptr), nbases, L))
+
+    def build_device_fasta(self, dev_ptr: int, nbytes: int, L: int = 12) -> dict:
+        """FASTA file bytes already in device memory: line contract + build on the device."""
+        return self._check(_lib.gcz_build_device_fasta(self._h, ctypes.c_void_p(dev_ptr), nbytes, L))
+
+    def fasta_extract_device(self, data: bytes) -> bytes:
+        """The device line contract on `data` (uploaded), bases back to the host."""
+        buf = self.upload(np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, np.uint8))
+        try:
+            n = _U64()
+            out = DeviceBuffer(self, max(len(data), 1))
+            rc = _lib.gcz_fasta_extract_device(self._h, ctypes.c_void_p(buf.ptr), len(data),
+                                               ctypes.c_void_p(out.ptr), max(len(data), 1), ctypes.byref(n))
+            if rc != GCZ_OK:
+                raise GczError(rc, "gcz_fasta_extract_device failed")
+            host = np.empty(max(int(n.value), 1), dtype=np.uint8)
+            if n.value:
+                _lib.gcz_memcpy_d2h(self._h, _ptr(host), ctypes.c_void_p(out.ptr), int(n.value))
+            out.free()
+            return host[:int(n.value)].tobytes()
+        finally:
+            buf.free()
 
     def build_device_leaves(self, dev_ptr: int, S: int, L: int = 12) -> dict:
         return self._check(_lib.gcz_build_device_leaves(self._h, ctypes.c_void_p(dev_ptr), S, L))

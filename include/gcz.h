@@ -99,6 +99,12 @@ GCZ_API int gcz_build_device_leaves(gcz_ctx *ctx, const uint64_t *d_leaves, uint
  * or host leaves; copied to the device, then built. */
 GCZ_API int gcz_build_host_fasta(gcz_ctx *ctx, const void *fasta, uint64_t nbytes, int L);
 GCZ_API int gcz_build_host_leaves(gcz_ctx *ctx, const uint64_t *leaves, uint64_t S, int L);
+/* A FASTA file already in device memory: the line contract (headers, blank lines;
+ * src/fasta_reader.cpp:40-68) runs on the device, then the build. */
+GCZ_API int gcz_build_device_fasta(gcz_ctx *ctx, const void *d_file, uint64_t n, int L);
+/* The device line contract alone: bases of d_file into d_out (cap bytes; null: count only). */
+GCZ_API int gcz_fasta_extract_device(gcz_ctx *ctx, const void *d_file, uint64_t n, void *d_out, uint64_t cap,
+                                     uint64_t *nbases);
 
 GCZ_API int gcz_info_get(gcz_ctx *ctx, gcz_info *out);
 GCZ_API int gcz_copy_leaves(gcz_ctx *ctx, uint64_t *host_out);                /* n_leaves u64 */
