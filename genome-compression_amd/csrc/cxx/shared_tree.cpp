@@ -23,6 +23,7 @@ namespace {
 struct Engine {
   gcz_ctx* ctx = nullptr;
   std::mutex mu;
+  std::uint64_t gen = 0;   // generation of the tree the device arrays hold (bumped by builds and device sorts)
   Engine() {
     const char* d = std::getenv("GCZ_DEVICE");
     const int rc = gcz_ctx_create(d ? std::atoi(d) : 0, &ctx);
@@ -167,7 +168,10 @@ void shared_tree::build_from_gpu() {
     check_build(gcz_copy_layer(ctx, k, reinterpret_cast<std::uint32_t*>(nodes[k].data())), ctx);
   }
   root = pointer::from_word(info.root);
+  device_gen = ++engine().gen;
 }
+
+bool shared_tree::on_device() const { return device_gen != 0 && device_gen == engine().gen; }
 
 // ---- accessors -----------------------------------------------------------------
 auto shared_tree::width() const -> std::size_t {
@@ -238,6 +242,7 @@ void shared_tree::store_histogram(std::filesystem::path path) const {
 }
 
 void shared_tree::rewire_nodes(std::size_t layer, const std::vector<std::size_t>& indices) {
+  device_gen = 0;
   auto rewire = [&](pointer old) {
     if (old.empty()) return old;
     return pointer{indices[old.index()], old.is_mirrored(), old.is_transposed(), old.is_invariant()};
@@ -273,15 +278,38 @@ void shared_tree::sort_nodes(std::size_t layer) {
 }
 
 void shared_tree::sort_tree(bool verbose) {
-  auto v = view(nodes, leaves, root);   // all layers at once, in parallel (same net effect)
-  gcz::view_sort(v);
+  if (on_device()) {   // the arrays are still in HBM: sort there, copy the result back
+    auto& e = engine();
+    std::lock_guard<std::mutex> lock(e.mu);
+    check_build(gcz_sort_device(e.ctx), e.ctx);
+    build_from_gpu();
+  } else {
+    auto v = view(nodes, leaves, root);   // all layers at once, in parallel (same net effect)
+    gcz::view_sort(v);
+  }
   if (verbose) std::cout << "\rSorting nodes: done.\n";
 }
 
 // ---- persistence (:488-546) ------------------------------------------------------------
-auto shared_tree::bytes() const noexcept -> std::size_t { return gcz::view_bytes(view(nodes, leaves, root)); }
+auto shared_tree::bytes() const noexcept -> std::size_t {
+  if (on_device()) {
+    std::uint64_t b = 0;
+    if (gcz_bytes_device(engine().ctx, &b) == GCZ_OK) return b;
+  }
+  return gcz::view_bytes(view(nodes, leaves, root));
+}
 
 void shared_tree::serialize(std::ostream& os) const {
+  if (on_device()) {   // the .dag is written on the device
+    std::uint64_t n = 0;
+    if (gcz_bytes_device(engine().ctx, &n) == GCZ_OK) {
+      std::vector<std::uint8_t> buf(n);
+      if (gcz_serialize_device(engine().ctx, buf.data(), n, &n) == GCZ_OK) {
+        os.write(reinterpret_cast<const char*>(buf.data()), std::streamsize(n));
+        return;
+      }
+    }
+  }
   const auto v = view(nodes, leaves, root);
   std::vector<std::uint8_t> buf(gcz::view_bytes(v));
   gcz::view_serialize(v, buf.data(), buf.size());

@@ -204,10 +204,12 @@ class shared_tree {
 
  private:
   void build_from_gpu();   // copies the last libgcz build of this thread into the containers
+  bool on_device() const;  // the engine's device arrays still hold exactly this tree
 
   std::vector<std::vector<node>> nodes;
   std::vector<dna> leaves;
   pointer root;
+  std::uint64_t device_gen = 0;   // engine build generation mirrored here (0: host only)
 };
 
 inline auto operator<<(std::ostream& os, const shared_tree& tree) -> std::ostream& {

@@ -15,7 +15,9 @@ BIN = os.path.join(REPO, "tests", "cxx", "test_dropin")
 def build_test_binary():
     load_gcz()   # makes sure libgcz.so exists
     src = os.path.join(REPO, "tests", "cxx", "test_dropin.cpp")
-    if not os.path.exists(BIN) or os.path.getmtime(BIN) < os.path.getmtime(src):
+    deps = [src, os.path.join(PKG, "libgcz.so")] + [os.path.join(REPO, "include", h)
+                                                    for h in ("dna.h", "fasta_reader.h", "shared_tree.h", "gcz.h")]
+    if not os.path.exists(BIN) or os.path.getmtime(BIN) < max(os.path.getmtime(d) for d in deps):
         subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-I" + os.path.join(REPO, "include"), src,
                         "-o", BIN, "-L" + PKG, "-lgcz", "-Wl,-rpath," + PKG], check=True)
     return BIN
