@@ -76,7 +76,7 @@ inline LevelTab plan_table(void* buf, u64 cap, u32 K, u64 npos, u32 B, bool allo
     gcz_dev::PackedTab& t = lt.pt;
     t.tab = static_cast<u64*>(buf);
     t.mask = u32(cap - 1);
-    t.D = u32(std::min(room, 8));
+    t.D = u32(std::min(room, 16));   // displacement bits: probe limit 2^D - 2
     t.limit = (1u << t.D) - 2;
     t.B = B;
     t.c = c;

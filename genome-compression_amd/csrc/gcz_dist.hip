@@ -20,7 +20,7 @@ using namespace gcz_host;
 
 struct gcz_dist_state {
   DevBuf scratch, gnf, gmul, gid, blockcnt, skey, sidx, sflag, scval, sdval;   // sender side
-  DevBuf rkey, oslot, rflag, rcval, rdval, owntab;                            // owner side
+  DevBuf rkey, oslot, rflag, rcval, rdval, owntab, oids;                      // owner side
   DevBuf s_selc, s_seld, s_prec, s_pred, o_selc, o_seld, o_prec, o_pred, sdesc;  // C/D compaction
   DevBuf dhdr, gath, gath2, gathf, ddesc, tail_in;
   u64* h_gath = nullptr;    // pinned mirrors of the gathered vectors
@@ -32,7 +32,7 @@ void gcz_dist_state_free(gcz_ctx* c) {
   gcz_dist_state* d = c->dist;
   if (!d) return;
   for (DevBuf* b : {&d->scratch, &d->gnf, &d->gmul, &d->gid, &d->blockcnt, &d->skey, &d->sidx, &d->sflag,
-                    &d->scval, &d->sdval, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab,
+                    &d->scval, &d->sdval, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab, &d->oids,
                     &d->s_selc, &d->s_seld, &d->s_prec, &d->s_pred, &d->o_selc, &d->o_seld, &d->o_prec,
                     &d->o_pred, &d->sdesc,
                     &d->dhdr, &d->gath, &d->gath2, &d->gathf, &d->ddesc, &d->tail_in})
@@ -291,8 +291,9 @@ struct gcz_group {
   }
   int build(const void* const* d_bases, const u64* const* d_leaves, u64 S, int L);
   int alloc(int i, int L, u64 leaf_cap);
-  int exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, std::vector<u64>& c,
-               std::vector<u64>& off, u64& total, u64* err_global, int* err_sym, int* ovf_bits);
+  int exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, u32 key_bits, u32 child_bits,
+               std::vector<u64>& c, std::vector<u64>& off, u64& total, u64* err_global, int* err_sym,
+               int* ovf_bits);
 };
 
 #define G_HIP(x)                                                   \
@@ -379,8 +380,11 @@ int gcz_group::alloc(int i, int L, u64 leaf_cap) {
 }
 
 
-int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, std::vector<u64>& c,
-                        std::vector<u64>& off, u64& total, u64* err_global, int* err_sym, int* ovf_bits) {
+// key_bits: bits of the owner-table key (leaves 4L, nodes 2 (child_bits + 2)); packed slots when
+// key_bits + R + 2 <= 64, else wide.
+int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, u32 key_bits, u32 child_bits,
+                        std::vector<u64>& c, std::vector<u64>& off, u64& total, u64* err_global, int* err_sym,
+                        int* ovf_bits) {
   const int R = world, NL = int(ctx.size());
   // 1. bucket the records by owner, pack the sync vector
   for (int i = 0; i < NL; ++i) {
@@ -487,9 +491,18 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       if ((rc = cx->ensure(d.sdesc, 4 * region[i] * 8))) return dev_fail("scan descriptors");
       G_HIP(hipMemsetAsync(d.sdesc.ptr, 0, 4 * region[i] * 8, cx->stream));
       const u64 cap = std::max<u64>(256, next_pow2(2 * nr));
-      if ((rc = cx->ensure(d.owntab, cap * 16))) return dev_fail("owner table");
+      const bool packed = key_bits + u32(R) + 2 <= 64 && !cx->force_wide;
+      if ((rc = cx->ensure(d.owntab, cap * (packed ? 8 : 16)))) return dev_fail("owner table");
+      if (packed && (rc = cx->ensure(d.oids, cap * 4))) return dev_fail("owner ids");
+      otab[i] = OwnTab{};
       otab[i].tab = d.owntab.as<Slot>();
+      otab[i].ptab = d.owntab.as<u64>();
+      otab[i].ids = d.oids.as<u32>();
       otab[i].mask = u32(cap - 1);
+      otab[i].packed = packed;
+      otab[i].R = u32(R);
+      otab[i].B = child_bits;
+      otab[i].sh = u32(R) + 2;
       s.push_back(d.skey.ptr);
       rv.push_back(d.rkey.ptr);
     }
@@ -506,7 +519,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       gcz_dist_state& d = *cx->dist;
       const u64 nr = recvd(rank[i]);
       ProfScope ps_(cx, KID_OWNER);
-      G_HIP(hipMemsetAsync(d.owntab.ptr, 0xff, size_t(otab[i].mask + 1) * 16, cx->stream));
+      G_HIP(hipMemsetAsync(d.owntab.ptr, 0xff, size_t(otab[i].mask + 1) * (otab[i].packed ? 8 : 16), cx->stream));
       const Displ D = displ_of(rank[i]);
       hipLaunchKernelGGL(k_own_insert, blocks(nr), dim3(kBlock), 0, cx->stream, d.rkey.as<u64>(), nr, D, u32(R),
                          int(lv[i].leaves), otab[i], d.oslot.as<u32>(), &d.dhdr.as<DistHdr>()->final_vec[3]);
@@ -784,7 +797,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     {
       std::vector<u64> nw(NL);
       for (int i = 0; i < NL; ++i) nw[i] = P.count(rank[i], 0);
-      const int rc = exchange(lv, nw, c, off, total, &err_global, &err_sym, &ovf);
+      const int rc = exchange(lv, nw, d_leaves ? 64u : 4 * u32(L), 0, c, off, total, &err_global, &err_sym, &ovf);
       if (rc == kRetry) {   // every rank sees the same bits and takes the same decision
         if (ovf & 2) {
           for (int i = 0; i < NL; ++i)
@@ -864,7 +877,8 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
       } else {
         std::vector<u64> nw(NL);
         for (int i = 0; i < NL; ++i) nw[i] = P.count(rank[i], k + 1);
-        const int rc = exchange(lv, nw, c, off, total, &err_global, &err_sym, &ovf);
+        const u32 cb = std::max<u32>(1, bit_width(prev_total));
+        const int rc = exchange(lv, nw, 2 * (cb + 2), cb, c, off, total, &err_global, &err_sym, &ovf);
         if (rc == kRetry) {
           allow_packed = false;
           retry = true;

@@ -181,12 +181,50 @@ static __global__ __launch_bounds__(kBlock) void k_bucket_scatter(RecSrc s, cons
 }
 
 // ---- owner side ----------------------------------------------------------------
-// Slot = {key ^ 1, ~state, id}: state bit r = rank r holds the key, bit 31 = some
-// rank holds it more than once.  memset 0xff clears (EMPTY key, state 0, id ~0).
+// Packed (default when it fits): one 8-B word per slot,
+//     word = key << (R + 2) | state << 1      (bit 0 = 0: occupied; EMPTY = ~0)
+// with the key re-encoded in K bits (leaves: the 4L-bit value; nodes: per child
+// B-bit index + mirror + transpose) and state bit r = rank r holds the key,
+// bit R = some rank holds it more than once.  A new key costs one CAS, a key
+// already claimed one atomicOr (skipped when its bits are set).  The ids of
+// C / D live beside it in ids[slot].
+// Wide (fallback): Slot = {key ^ 1, ~state, id}, state bit 31 = repeats locally.
+// memset 0xff clears both.
 struct OwnTab {
-  Slot* tab;
+  Slot* tab;     // wide
+  u64* ptab;     // packed
+  u32* ids;      // packed: id per slot
   u32 mask;
+  u32 packed;
+  u32 R;
+  u32 B;         // packed node keys: child index bits
+  u32 sh;        // packed: R + 2
 };
+
+__device__ __forceinline__ u64 own_pack_key(u64 key, int leaves, u32 B) {
+  if (leaves) return key;
+  auto enc = [B](u32 u) -> u64 {
+    const u32 idx = u & kIdx;
+    const u32 code = idx == kIdx ? ((1u << B) - 1u) : idx;
+    return (u64(code) << 2) | (((u >> 29) & 1u) << 1) | ((u >> 30) & 1u);
+  };
+  return (enc(u32(key >> 31)) << (B + 2)) | enc(u32(key & 0x7fffffffu));
+}
+
+// state of a slot: bits [0, R) ranks holding the key, bit 31 repeats locally
+__device__ __forceinline__ u32 own_state(const OwnTab& T, u32 s) {
+  if (T.packed) {
+    const u64 w = T.ptab[s];
+    const u32 st = u32(w >> 1) & ((1u << (T.R + 1)) - 1u);
+    return (st & ((1u << T.R) - 1u)) | ((st >> T.R) << 31);
+  }
+  return ~T.tab[s].pos;
+}
+__device__ __forceinline__ void own_set_id(const OwnTab& T, u32 s, u32 id) {
+  if (T.packed) T.ids[s] = id;
+  else T.tab[s].pad = id;
+}
+__device__ __forceinline__ u32 own_id(const OwnTab& T, u32 s) { return T.packed ? T.ids[s] : T.tab[s].pad; }
 
 static __global__ __launch_bounds__(kBlock) void k_own_insert(const u64* __restrict__ rkey, u64 nrecv, Displ D,
                                                               u32 R, int leaves, OwnTab T, u32* __restrict__ oslot,
@@ -197,17 +235,40 @@ static __global__ __launch_bounds__(kBlock) void k_own_insert(const u64* __restr
   const u64 raw = rkey[k];
   const u64 key = leaves ? raw : (raw & ~kLocalMulti);
   const u32 lm = leaves ? 0u : u32(raw >> 63);
-  const u64 skey = key ^ 1ull;
-  u32 s = slot_hash(skey) & T.mask;
-  for (u32 probe = 0; probe <= T.mask; ++probe) {
-    u64 cur = T.tab[s].key;
-    if (cur == kEmpty) cur = atomicCAS(&T.tab[s].key, kEmpty, skey);
-    if (cur == kEmpty || cur == skey) {
-      atomicAnd(&T.tab[s].pos, ~((1u << src) | (lm << 31)));
-      oslot[k] = s;
-      return;
+  if (T.packed) {
+    const u64 pk = own_pack_key(key, leaves, T.B);
+    const u64 bits = (u64((1u << src) | (lm << R))) << 1;
+    const u64 mine = (pk << T.sh) | bits;
+    u32 s = slot_hash(pk) & T.mask;
+    for (u32 probe = 0; probe <= T.mask; ++probe) {
+      u64 cur = T.ptab[s];
+      if (cur == kEmpty) {
+        cur = atomicCAS(&T.ptab[s], kEmpty, mine);
+        if (cur == kEmpty) {
+          oslot[k] = s;
+          return;
+        }
+      }
+      if ((cur >> T.sh) == pk) {
+        if ((cur & bits) != bits) atomicOr(&T.ptab[s], bits);
+        oslot[k] = s;
+        return;
+      }
+      s = (s + 1) & T.mask;
     }
-    s = (s + 1) & T.mask;
+  } else {
+    const u64 skey = key ^ 1ull;
+    u32 s = slot_hash(skey) & T.mask;
+    for (u32 probe = 0; probe <= T.mask; ++probe) {
+      u64 cur = T.tab[s].key;
+      if (cur == kEmpty) cur = atomicCAS(&T.tab[s].key, kEmpty, skey);
+      if (cur == kEmpty || cur == skey) {
+        atomicAnd(&T.tab[s].pos, ~((1u << src) | (lm << 31)));
+        oslot[k] = s;
+        return;
+      }
+      s = (s + 1) & T.mask;
+    }
   }
   atomicOr(ovf, 1ull);
   oslot[k] = 0;
@@ -219,7 +280,7 @@ static __global__ __launch_bounds__(kBlock) void k_own_reply(const u32* __restri
   const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (k >= nrecv) return;
   const u32 src = seg_of(D, R, k);
-  const u32 st = ~T.tab[oslot[k]].pos;
+  const u32 st = own_state(T, oslot[k]);
   const u32 ranks = st & 0x7fffffffu;
   const u32 minr = u32(__ffs(ranks) - 1);
   const u32 shared = __popc(ranks) > 1;
@@ -277,7 +338,7 @@ static __global__ __launch_bounds__(kBlock) void k_own_setid(const u32* __restri
                                                              const u32* __restrict__ cval, OwnTab T) {
   const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (k >= nrecv || !want_c(rflag[k])) return;
-  T.tab[oslot[k]].pad = cval[prec[k]];
+  own_set_id(T, oslot[k], cval[prec[k]]);
 }
 
 static __global__ __launch_bounds__(kBlock) void k_own_getid(const u32* __restrict__ oslot, u64 nrecv,
@@ -286,7 +347,7 @@ static __global__ __launch_bounds__(kBlock) void k_own_getid(const u32* __restri
                                                              u32* __restrict__ dval) {
   const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (k >= nrecv || !want_d(rflag[k])) return;
-  dval[pred[k]] = T.tab[oslot[k]].pad;
+  dval[pred[k]] = own_id(T, oslot[k]);
 }
 
 // ---- sender side ---------------------------------------------------------------
