@@ -40,7 +40,7 @@ CONFIGS = {
     "uniform_1g": {"kind": 0, "nbases": 1_000_000_000, "golden": "synth/uniform_1000000000"},
     "uniform_100m": {"kind": 0, "nbases": 100_000_003, "golden": "synth/uniform_100000003"},
     "tandem_100m": {"kind": 1, "nbases": 100_000_000, "golden": "synth/tandem_100000000"},
-    "tandem_3g2": {"kind": 1, "nbases": 3_200_000_000, "golden": None},
+    "tandem_3g2": {"kind": 1, "nbases": 3_200_000_000, "golden": "synth/tandem_3200000000"},
 }
 
 

@@ -16,7 +16,7 @@ oracle/_ref/ref_harness, i.e. from the reference's own src/*.cpp:
 manifest.json maps every case to its inputs and the reference's outputs
 (sha256 of leaves.bin / layers.bin / unsorted.dag / dag, counts, root, ratio).
 
-usage: python tests/golden/make_goldens.py [--synth-large]
+usage: python tests/golden/make_goldens.py [--synth-large | --synth-huge]
 """
 import gzip
 import hashlib
@@ -198,6 +198,9 @@ def main():
         synth = [(0, 1_000_000), (0, 10_000_000), (1, 10_000_000), (0, 100_000_003)]
         if synth_large:
             synth += [(1, 100_000_000), (0, 1_000_000_000)]
+        if "--synth-huge" in sys.argv:   # BASELINE config 5: 3.2 Gbase, 50 % tandem repeats (~3 min, ~25 GB)
+            synth = [(1, 3_200_000_000)]
+            synth_large = True
         for kind, n in synth:
             key = f"synth/{'uniform' if kind == 0 else 'tandem'}_{n}"
             if key in manifest and not synth_large:

@@ -158,9 +158,11 @@ def test_dist_equals_single_device_tandem(gcz, groups):
 
 @pytest.mark.gpu
 @pytest.mark.slow
-@pytest.mark.parametrize("world", [2, 8])
-def test_dist_synth_100m(world, gcz, manifest, groups):
-    for name in ("synth/uniform_100000003", "synth/tandem_100000000"):
+@pytest.mark.parametrize("world,names", [(2, ("synth/uniform_100000003", "synth/tandem_100000000")),
+                                         (8, ("synth/uniform_100000003", "synth/tandem_100000000",
+                                              "synth/uniform_1000000000", "synth/tandem_3200000000"))])
+def test_dist_synth_large(world, names, gcz, manifest, groups):
+    for name in names:
         case = manifest[name]
         kind, payload, L = case_input(case, gcz)
         _dist_build(gcz, groups(world), kind, payload, L)

@@ -129,7 +129,7 @@ def test_gpu_empty_and_bad_L(ctx, gcz):
 
 @pytest.mark.slow
 @pytest.mark.parametrize("name", ["synth/uniform_100000003", "synth/tandem_100000000",
-                                  "synth/uniform_1000000000"])
+                                  "synth/uniform_1000000000", "synth/tandem_3200000000"])
 def test_gpu_large_synth_goldens(name, ctx, gcz, manifest):
     case = manifest[name]
     kind, payload, L = case_input(case, gcz)

@@ -64,8 +64,9 @@ def test_device_sort_idempotent_and_unsorted_dag(ctx, gcz, manifest):
 
 
 @pytest.mark.slow
-def test_device_sort_1g(ctx, gcz, manifest):
-    case = manifest["synth/uniform_1000000000"]
+@pytest.mark.parametrize("name", ["synth/uniform_1000000000", "synth/tandem_3200000000"])
+def test_device_sort_large(name, ctx, gcz, manifest):
+    case = manifest[name]
     exp = case["expect"]
     kind, payload, L = case_input(case, gcz)
     buf = ctx.upload(np.frombuffer(payload, dtype=np.uint8))
