@@ -216,9 +216,11 @@ struct gcz_ctx {
     pending.push_back({kid, {a, b}});
   }
   void prof_collect() {
+    static const bool verbose = std::getenv("GCZ_PROFILE_VERBOSE") != nullptr;
     for (auto& pe : pending) {
       float ms = 0.f;
       (void)hipEventElapsedTime(&ms, pe.second.first, pe.second.second);
+      if (verbose) std::fprintf(stderr, "gcz-prof %s %.4f\n", gcz_host::kernel_name(pe.first), double(ms));
       prof_ms[pe.first] += ms;
       prof_launches[pe.first] += 1;
     }

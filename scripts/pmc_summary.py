@@ -23,7 +23,8 @@ def short(name):
 
 NAMES = {"k_leaf_bases": "leaf_insert", "k_leaf_packed": "leaf_insert", "k_node_insert": "node_insert",
          "k_flagscan_leaf": "flagscan_leaf", "k_flagscan_node": "flagscan_node", "k_resolve_leaf": "resolve_leaf",
-         "k_resolve_node": "resolve_node", "k_clear": "clear", "__amd_rocclr_fillBufferAligned": "clear"}
+         "k_resolve_node": "resolve_node", "k_clear": "clear", "__amd_rocclr_fillBufferAligned": "clear",
+         "k_tail": "tail"}
 
 
 def load(d, counter):
