@@ -176,6 +176,17 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   return GCZ_OK;
 }
 
+int gcz_ctx::direct_levels(const u32* in, int k0, int nlev, const DirectPlan& dp, u32* out, Header* d_hdr) {
+  hipEvent_t e0{};
+  prof_begin(KID_DIRECT, e0);
+  const u64 blocks = (dp.n[0] + kDirectChunk - 1) / kDirectChunk;
+  hipLaunchKernelGGL(k_direct_levels, dim3(unsigned(blocks)), dim3(kBlock), 0, stream, in, k0, nlev,
+                     nodes_out.as<uint2>(), dp, out, d_hdr);
+  HIP_TRY(hipGetLastError());
+  prof_end(KID_DIRECT, e0);
+  return GCZ_OK;
+}
+
 int gcz_ctx::tail_levels(const u32* in, u64 n0, const u64* pcount, int k0, int D, const std::vector<u64>& layer_off_,
                          Header* d_hdr) {
   TailOut to{};
@@ -280,13 +291,30 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     u32* outw = Bw;
     u64 n = S;
     u64 bound = std::min(S, leaf_cap);        // child ids of layer 0 are leaf ids < #slots
-    bool tail_done = false;
+    bool tail_done = false, direct = false;
     for (int k = 0; k < D; ++k) {
       if (n <= u64(kTailMaxN) && use_tail) {   // the rest fits one workgroup: one launch
         const u64* pc = k == 0 ? &d_hdr->count[C - 1] : &d_hdr->count[kLayerSlot + k - 1];
         if ((rc = tail_levels(in, n, pc, k, D, layer_off, d_hdr))) return rc;
         tail_done = true;
         break;
+      }
+      if (direct) {   // host-known: up to kDirectLog levels per launch, ids = positions
+        DirectPlan dp{};
+        int nlev = 0;
+        u64 m = n;
+        dp.n[0] = n;
+        while (nlev < kDirectLog && k + nlev < D && m > u64(kTailMaxN)) {
+          dp.layer_off[k + nlev] = layer_off[k + nlev];
+          m = pk[k + nlev];
+          dp.n[++nlev] = m;
+        }
+        if ((rc = direct_levels(in, k, nlev, dp, outw, d_hdr))) return rc;
+        std::swap(in, outw);
+        n = m;
+        bound = m;
+        k += nlev - 1;
+        continue;
       }
       NodeLevel na;
       na.k = k;
@@ -303,6 +331,14 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       std::swap(in, outw);
       n = pk[k];
       bound = pk[k];
+      // one look at the device after layer 1: if it is all unique, every later level is
+      // direct and runs as direct subtrees (saves ~4 launches per level)
+      if (k == 1 && use_direct && n > u64(kTailMaxN)) {
+        u64 cnt = 0;
+        HIP_TRY(hipMemcpyAsync(&cnt, &d_hdr->count[kLayerSlot + 1], 8, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        direct = cnt == n;
+      }
     }
     if (!tail_done) {
       hipLaunchKernelGGL(k_root, dim3(1), dim3(1), 0, stream, in, d_hdr);
@@ -366,6 +402,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   if (const char* t = std::getenv("GCZ_NODE_CAP_SHIFT")) c->node_cap_shift = std::atoi(t);
   if (const char* t = std::getenv("GCZ_LEAF_CAP_LOG2")) c->leaf_cap_log2 = std::atoi(t);
   if (const char* t = std::getenv("GCZ_TAIL")) c->use_tail = std::atoi(t) != 0;
+  if (const char* t = std::getenv("GCZ_DIRECT")) c->use_direct = std::atoi(t) != 0;
   *out = c;
   return GCZ_OK;
 }

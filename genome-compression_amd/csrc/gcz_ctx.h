@@ -96,12 +96,12 @@ inline LevelTab plan_table(void* buf, u64 cap, u32 K, u64 npos, u32 B, bool allo
 
 enum KernelId {
   KID_LEAF, KID_NODE, KID_FLAGSCAN_LEAF, KID_FLAGSCAN_NODE, KID_RESOLVE_LEAF, KID_RESOLVE_NODE, KID_MEMSET,
-  KID_EXCHANGE, KID_DIST, KID_OWNER, KID_IDS, KID_REMAP, KID_TAIL, KID_SORT, KID_DAG, KID_COUNT
+  KID_EXCHANGE, KID_DIST, KID_OWNER, KID_IDS, KID_REMAP, KID_TAIL, KID_SORT, KID_DAG, KID_DIRECT, KID_COUNT
 };
 inline const char* kernel_name(int k) {
   static const char* names[KID_COUNT] = {"leaf_insert", "node_insert", "flagscan_leaf", "flagscan_node",
                                          "resolve_leaf", "resolve_node", "clear", "exchange", "dist_bucket",
-                                         "dist_owner", "dist_ids", "dist_remap", "tail", "sort", "dag_write"};
+                                         "dist_owner", "dist_ids", "dist_remap", "tail", "sort", "dag_write", "direct_levels"};
   return names[k];
 }
 
@@ -168,6 +168,7 @@ struct gcz_ctx {
   int node_cap_shift = 1;    // node table capacity = next_pow2(p << shift)   (GCZ_NODE_CAP_SHIFT)
   int leaf_cap_log2 = 0;     // force the adaptive leaf table size            (GCZ_LEAF_CAP_LOG2)
   bool use_tail = true;      // fuse the top levels into one launch           (GCZ_TAIL=0 disables)
+  bool use_direct = true;    // direct subtrees after a host check at layer 1 (GCZ_DIRECT=0 disables)
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> event_pool;
   size_t event_used = 0;
@@ -237,6 +238,9 @@ struct gcz_ctx {
 
   int leaf_level(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr);
   int node_level(const gcz_host::NodeLevel& a, gcz_dev::Header* d_hdr);
+  // Known-direct levels k0..k0+nlev-1 in one launch (gcz_device.h k_direct_levels).
+  int direct_levels(const gcz_host::u32* in, int k0, int nlev, const gcz_dev::DirectPlan& dp, gcz_host::u32* out,
+                    gcz_dev::Header* d_hdr);
   // Levels k0..D-1 in one launch (n0 <= kTailMaxN input words); writes counts and the root.
   int tail_levels(const gcz_host::u32* in, gcz_host::u64 n0, const gcz_host::u64* pcount, int k0, int D,
                   const std::vector<gcz_host::u64>& layer_off, gcz_dev::Header* d_hdr);

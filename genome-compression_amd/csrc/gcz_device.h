@@ -699,6 +699,54 @@ __global__ __launch_bounds__(kBlock) void k_resolve_node(u32* __restrict__ words
   words[j] = id | (w & kBits);
 }
 
+// ---- direct subtrees ----------------------------------------------------------------
+// Once level k0 is known to be direct (every element of level k0-1 unique), every
+// later level is too and ids are positions.  Each workgroup takes an aligned chunk
+// of kDirectChunk input words and computes up to kDirectLog levels of its subtree in
+// LDS -- one launch instead of 4 per level.  Only the chunk holding the global tail
+// is partial, so an odd local count there is the global odd tail (null right child).
+constexpr int kDirectLog = 12;
+constexpr int kDirectChunk = 1 << kDirectLog;
+
+struct DirectPlan {
+  u64 layer_off[GCZ_MAX_LAYERS];   // node offset of each layer's (rank-local) slice
+  u64 n[GCZ_MAX_LAYERS + 1];       // n[i]: input words of level k0 + i (rank-local)
+  u32 id_off[GCZ_MAX_LAYERS];      // id of local pair 0 of each level (multi-rank: the rank's first position)
+};
+
+[[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_direct_levels(
+    const u32* __restrict__ in, int k0, int nlev, uint2* __restrict__ nodes, DirectPlan dp, u32* __restrict__ words_out,
+    Header* __restrict__ hdr) {
+  __shared__ u32 buf[2][kDirectChunk];
+  const u64 base0 = u64(blockIdx.x) * kDirectChunk;
+  u32 c = u32(dp.n[0] - base0 < u64(kDirectChunk) ? dp.n[0] - base0 : u64(kDirectChunk));
+  for (u32 e = threadIdx.x; e < c; e += kBlock) buf[0][e] = in[base0 + e];
+  __syncthreads();
+  int cur = 0;
+  for (int i = 0; i < nlev; ++i) {
+    const int k = k0 + i;
+    const u32 p = (c + 1) / 2;
+    const u64 base_out = base0 >> (i + 1);
+    uint2* out = nodes + dp.layer_off[k];
+    for (u32 j = threadIdx.x; j < p; j += kBlock) {
+      const u32 l = buf[cur][2 * j];
+      const u32 r = 2 * j + 1 < c ? buf[cur][2 * j + 1] : kNullWord;
+      u32 cl, cr, m, t;
+      node_canonical(l, r, cl, cr, m, t);
+      const u32 v = ulw(l) == ulw(xf(r, 1, 0));
+      out[base_out + j] = make_uint2(cl, cr);
+      buf[cur ^ 1][j] = make_word(u32(base_out + j) + dp.id_off[k], m, t, v);
+    }
+    __syncthreads();
+    cur ^= 1;
+    c = p;
+  }
+  const u64 base_last = base0 >> nlev;
+  for (u32 e = threadIdx.x; e < c; e += kBlock) words_out[base_last + e] = buf[cur][e];
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (int i = 0; i < nlev; ++i) hdr->count[kLayerSlot + k0 + i] = dp.n[i + 1];
+}
+
 // ---- fused top levels -------------------------------------------------------------
 // Once a level's input fits one workgroup (n <= kTailMaxN), all remaining
 // levels run in ONE launch: words ping-pong in LDS, each level is either
