@@ -553,8 +553,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     if (records) {
       const u64 ns = sent(rank[i]);
       hipLaunchKernelGGL(k_dist_flags, blocks(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
-                         d.sflag.as<unsigned char>(), d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>());
-      hipLaunchKernelGGL(k_sel, blocks(ns), dim3(kBlock), 0, cx->stream, d.sflag.as<unsigned char>(), ns,
+                         d.sflag.as<unsigned char>(), d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(),
                          d.s_selc.as<unsigned char>(), d.s_seld.as<unsigned char>());
       G_HIP(hipGetLastError());
       if (sel_scan(cx, 0, d.s_selc.as<unsigned char>(), ns, d.s_prec.as<u32>(), region[i])) return dev_fail("scan");
@@ -828,6 +827,32 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     std::vector<u32*> cur_in(NL), cur_out(NL);
     for (int i = 0; i < NL; ++i) { cur_in[i] = ctx[i]->wa.as<u32>(); cur_out[i] = ctx[i]->wb.as<u32>(); }
     for (int k = 0; k < G && !retry; ++k) {
+      if (direct) {   // host-known: direct subtrees, up to kDirectLog levels per launch, no exchange
+        const int nlev = std::min(kDirectLog, G - k);
+        for (int i = 0; i < NL; ++i) {
+          const int r = rank[i];
+          if (P.count(r, k) == 0) continue;
+          DirectPlan dp{};
+          for (int q = 0; q <= nlev; ++q) dp.n[q] = P.count(r, k + q);
+          for (int q = 0; q < nlev; ++q) {
+            dp.layer_off[k + q] = node_base[i][k + q];
+            dp.id_off[k + q] = u32(P.start(r, k + q + 1));
+          }
+          if (ctx[i]->direct_levels(cur_in[i], k, nlev, dp, cur_out[i], ctx[i]->hdr.as<Header>()))
+            return dev_fail("direct levels");
+        }
+        for (int q = 0; q < nlev; ++q) {
+          for (int s = 0; s < R; ++s) {
+            slice_off[k + q + 1][s] = P.start(s, k + q + 1);
+            slice_cnt[k + q + 1][s] = P.count(s, k + q + 1);
+          }
+          info.layer_size[k + q] = P.nk[k + q + 1];
+        }
+        prev_total = P.nk[k + nlev];
+        for (int i = 0; i < NL; ++i) std::swap(cur_in[i], cur_out[i]);
+        k += nlev - 1;
+        continue;
+      }
       for (int i = 0; i < NL; ++i) {
         gcz_ctx* cx = ctx[i];
         Header* h = cx->hdr.as<Header>();

@@ -250,7 +250,11 @@ static __global__ __launch_bounds__(kBlock) void k_own_insert(const u64* __restr
         }
       }
       if ((cur >> T.sh) == pk) {
-        if ((cur & bits) != bits) atomicOr(&T.ptab[s], bits);
+        // the reply only needs: the lowest rank, >= 2 ranks, repeats anywhere.  Once the
+        // word shows two ranks with a lower one than src, this record changes none of them.
+        const u32 ranks = u32(cur >> 1) & ((1u << R) - 1u);
+        const bool settled = __popc(ranks) >= 2 && (ranks & ((1u << src) - 1u)) != 0;
+        if (!settled && (cur & bits) != bits) atomicOr(&T.ptab[s], bits);
         oslot[k] = s;
         return;
       }
@@ -352,16 +356,22 @@ static __global__ __launch_bounds__(kBlock) void k_own_getid(const u32* __restri
 
 // ---- sender side ---------------------------------------------------------------
 
+// Reply flags -> per local unique (gnf: not globally first, gmul: repeats globally), and
+// the selection bytes of the C / D compactions (see k_sel).
 static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restrict__ sidx, u64 nsent,
                                                               const unsigned char* __restrict__ sflag,
                                                               unsigned char* __restrict__ gnf,
-                                                              unsigned char* __restrict__ gmul) {
+                                                              unsigned char* __restrict__ gmul,
+                                                              unsigned char* __restrict__ selc,
+                                                              unsigned char* __restrict__ seld) {
   const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (k >= nsent) return;
   const u32 lid = sidx[k];
   const unsigned char f = sflag[k];
   gnf[lid] = f & 1;
   gmul[lid] = (f >> 1) & 1;
+  selc[k] = want_c(f) ? 0 : 1;
+  seld[k] = want_d(f) ? 0 : 1;
 }
 
 // Rank of each globally-first local unique among them (local order); total -> *count_out.
