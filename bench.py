@@ -41,7 +41,21 @@ CONFIGS = {
     "uniform_100m": {"kind": 0, "nbases": 100_000_003, "golden": "synth/uniform_100000003"},
     "tandem_100m": {"kind": 1, "nbases": 100_000_000, "golden": "synth/tandem_100000000"},
     "tandem_3g2": {"kind": 1, "nbases": 3_200_000_000, "golden": "synth/tandem_3200000000"},
+    # BASELINE configs 2 and 3: the bundled corpus files (FASTA; headers stripped on the host)
+    "hehcmv": {"kind": "file", "path": "tests/golden/data/hehcmv", "golden": "corpus/hehcmv"},
+    "merged": {"kind": "file", "path": "tests/golden/data/merged", "golden": "corpus/merged"},
 }
+
+
+def genome(gcz, cfg, seed, begin, end):
+    """Bases [begin, end) of the configured genome (synthetic, or a corpus file's bases)."""
+    if cfg["kind"] == "file":
+        with open(os.path.join(REPO, cfg["path"]), "rb") as f:
+            b = np.frombuffer(gcz.fasta_extract(f.read()), dtype=np.uint8)
+        return b[begin:end].copy()
+    out = np.empty(max(end - begin, 1), dtype=np.uint8)
+    gcz._lib.gcz_synth_fill(gcz._ptr(out), cfg["kind"], seed, begin, end)
+    return out[:end - begin]
 
 
 def load_gcz():
@@ -180,6 +194,10 @@ def main():
     gcz = load_gcz()
     cfg = CONFIGS[args.config]
     L = 12
+    if cfg["kind"] == "file":
+        with open(os.path.join(REPO, cfg["path"]), "rb") as f:
+            raw = f.read()
+        cfg = dict(cfg, nbases=len(gcz.fasta_extract(raw)), file_size=len(raw))
     nbases = cfg["nbases"]
     S = nbases // L
     mode = ("dist" if args.mode == "dist" else "replicas") if world > 1 else ("virtual" if args.virtual else "single")
@@ -190,9 +208,8 @@ def main():
     group = None
     if mode == "dist":
         s0, s1, G = gcz.dist_plan(S, world, rank)
-        host = np.empty(max((s1 - s0) * L, 1), dtype=np.uint8)
-        gcz._lib.gcz_synth_fill(gcz._ptr(host), cfg["kind"], seed, s0 * L, s1 * L)
-        dev = ctx.upload(host)
+        host = genome(gcz, cfg, seed, s0 * L, s1 * L)
+        dev = ctx.upload(host if host.size else np.zeros(1, np.uint8))
         uid = [gcz.dist_unique_id() if rank == 0 else None]
         if dist is not None:
             dist.broadcast_object_list(uid, src=0)
@@ -202,14 +219,14 @@ def main():
     elif mode == "virtual":
         group = gcz.Group.local(args.virtual, local)
         prof_ctx = group.ctx(0)
-        host = gcz.synth(cfg["kind"], nbases, seed)
+        host = genome(gcz, cfg, seed, 0, nbases)
         dev = prof_ctx.upload(host)
         ptrs = [dev.ptr + gcz.dist_plan(S, args.virtual, r)[0] * L for r in range(args.virtual)]
         run = lambda: group.build_device_bases(ptrs, S, L)  # noqa: E731
     else:
         if mode == "replicas":   # a different genome per rank, same size
             seed ^= 0 if rank == 0 else (0x5851F42D4C957F2D * rank) & ((1 << 64) - 1)
-        host = gcz.synth(cfg["kind"], nbases, seed)
+        host = genome(gcz, cfg, seed, 0, nbases)
         dev = ctx.upload(host)
         prof_ctx = ctx
         run = lambda: ctx.build_device_bases(dev.ptr, nbases, L)  # noqa: E731
@@ -287,7 +304,7 @@ def main():
         with open(os.path.join(REPO, "tests", "golden", "manifest.json")) as f:
             exp = json.load(f)[cfg["golden"]]["expect"]
         d = gcz.digest(tree)
-        ratio = f"{nbases / d['bytes']:.6g}"
+        ratio = f"{cfg.get('file_size', nbases) / d['bytes']:.6g}"   # compress reports file size / bytes()
         parity = {"golden": cfg["golden"],
                   "dag_sha256_match": d["sha_dag"] == exp["sha_dag"],
                   "unsorted_sha256_match": d["sha_unsorted_dag"] == exp["sha_unsorted_dag"],
@@ -305,7 +322,7 @@ def main():
         dptr = gcz._lib.gcz_device_dag(ctx._h, gcz.ctypes.byref(n))
         t2 = time.perf_counter()
         ratio_path = {"device_sort_ms": round((t1 - t0) * 1e3, 3), "device_dag_ms": round((t2 - t1) * 1e3, 3),
-                      "dag_bytes": int(n.value), "ratio": f"{nbases / max(int(n.value), 1):.6g}"}
+                      "dag_bytes": int(n.value), "ratio": f"{cfg.get('file_size', nbases) / max(int(n.value), 1):.6g}"}
         if parity is not None:
             dag = ctx.serialize_device()
             parity["device_dag_sha256_match"] = hashlib.sha256(dag).hexdigest() == exp["sha_dag"]
@@ -319,7 +336,7 @@ def main():
         if rc == 0 and not args.no_parity:
             got = np.empty(S * L, dtype=np.uint8)
             gcz._lib.gcz_memcpy_d2h(ctx._h, gcz._ptr(got), gcz.ctypes.c_void_p(text.ptr), S * L)
-            ref = gcz.synth(cfg["kind"], S * L, seed)
+            ref = genome(gcz, cfg, seed, 0, S * L)
             ratio_path["roundtrip_match"] = bool(np.array_equal(got, np.where(ref >= 97, ref - 32, ref)))
         text.free()
 
