@@ -376,4 +376,11 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except Exception as e:  # noqa: BLE001 -- report a failed run as a result line, not silence
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "bases/s",
+                              "n_gpus": int(os.environ.get("WORLD_SIZE", "1")), "higher_is_better": True,
+                              "error": f"{type(e).__name__}: {e}"}), flush=True)
+        raise
