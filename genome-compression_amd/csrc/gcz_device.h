@@ -45,10 +45,10 @@ constexpr u32 kIdx = 0x1fffffffu;
 constexpr u32 kBits = 0xe0000000u;
 constexpr u64 kEmpty = ~0ull;
 constexpr int kBlock = 256;
-constexpr int kItems = 8;                  // node flagscan elements per thread
+constexpr int kItems = 32;                 // node flagscan elements per thread (look-back tiles of 8192)
 constexpr int kTile = kBlock * kItems;     // 2048 elements per look-back tile
 constexpr int kGroupsPerTile = kTile / 64; // 32
-constexpr int kLeafItems = 16;             // leaf flagscan: most strands are already settled
+constexpr int kLeafItems = 32;             // leaf flagscan: most strands are already settled
 constexpr int kLeafTile = kBlock * kLeafItems;
 constexpr u32 kMaxProbe = 1u << 16;
 
@@ -557,8 +557,17 @@ __device__ __forceinline__ void tile_scan(TileScan<ITEMS>& ts, u32* s_tile, u32*
     if (lane == 0) s_pre[e * 4 + wave] = u32(__popcll(ts.mask[e]));
   }
   __syncthreads();
+  constexpr int NG = 4 * ITEMS;             // 64-element groups per tile
+  constexpr int PER = (NG + 63) / 64;        // groups per lane of the scanning wave
   if (wave == 0) {
-    const u32 c = lane < 4 * ITEMS ? s_pre[lane] : 0u;
+    u32 cs[PER];
+    u32 c = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int g = lane * PER + q;
+      cs[q] = g < NG ? s_pre[g] : 0u;
+      c += cs[q];
+    }
     u32 incl = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -592,7 +601,13 @@ __device__ __forceinline__ void tile_scan(TileScan<ITEMS>& ts, u32* s_tile, u32*
       if (lane == 0)
         __hip_atomic_store(&desc[tile], kStP | (prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (lane < 4 * ITEMS) s_pre[lane] = u32(prefix + incl - c);
+    u32 run = u32(prefix + incl - c);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int g = lane * PER + q;
+      if (g < NG) s_pre[g] = run;
+      run += cs[q];
+    }
     if (lane == 0 && ts.base + kBlock * ITEMS >= p) *count_out = prefix + agg;
   }
   __syncthreads();
