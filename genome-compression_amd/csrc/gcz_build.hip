@@ -161,16 +161,16 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   prof_begin(KID_FLAGSCAN_NODE, e0);
   const dim3 gs(unsigned((p + kTile - 1) / kTile));
   hipLaunchKernelGGL(k_flagscan_node, gs, dim3(kBlock), 0, stream, a.words, p, a.in, n, knf, d_grp, a.desc,
-                     a.ticket, a.out, a.count, a.pcount);
+                     a.ticket, a.out, a.count, a.pcount, mk.multi, a.hashed_next);
   HIP_TRY(hipGetLastError());
   prof_end(KID_FLAGSCAN_NODE, e0);
   prof_begin(KID_RESOLVE_NODE, e0);
   if (nt.packed)
     hipLaunchKernelGGL((k_resolve_node<PackedTab>), gi, dim3(kBlock), 0, stream, a.words, p, nt.pt, knf, d_grp,
-                       a.pcount, n);
+                       a.pcount, n, a.count, a.hashed_next, a.gate);
   else
     hipLaunchKernelGGL((k_resolve_node<WideTab>), gi, dim3(kBlock), 0, stream, a.words, p, nt.wt, knf, d_grp,
-                       a.pcount, n);
+                       a.pcount, n, a.count, a.hashed_next, a.gate);
   HIP_TRY(hipGetLastError());
   prof_end(KID_RESOLVE_NODE, e0);
   return GCZ_OK;
@@ -292,9 +292,11 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     u64 n = S;
     u64 bound = std::min(S, leaf_cap);        // child ids of layer 0 are leaf ids < #slots
     bool tail_done = false, direct = false;
+    bool prev_regular = false;   // the previous level ran node_level (its gate is written)
     for (int k = 0; k < D; ++k) {
       if (n <= u64(kTailMaxN) && use_tail) {   // the rest fits one workgroup: one launch
-        const u64* pc = k == 0 ? &d_hdr->count[C - 1] : &d_hdr->count[kLayerSlot + k - 1];
+        const u64* pc = k == 0 ? &d_hdr->count[C - 1] : prev_regular ? &d_hdr->gate[k - 1]
+                                                                       : &d_hdr->count[kLayerSlot + k - 1];
         if ((rc = tail_levels(in, n, pc, k, D, layer_off, d_hdr))) return rc;
         tail_done = true;
         break;
@@ -310,6 +312,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
           dp.n[++nlev] = m;
         }
         if ((rc = direct_levels(in, k, nlev, dp, outw, d_hdr))) return rc;
+        prev_regular = false;
         std::swap(in, outw);
         n = m;
         bound = m;
@@ -324,10 +327,13 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       na.count = &d_hdr->count[kLayerSlot + k];
       na.bound = bound;
       na.prev_marks = k > 0;
-      na.pcount = k == 0 ? &d_hdr->count[C - 1] : &d_hdr->count[kLayerSlot + k - 1];
+      na.pcount = k == 0 ? &d_hdr->count[C - 1] : &d_hdr->gate[k - 1];
       na.desc = d_desc + desc_off[C + k];
       na.ticket = &d_hdr->ticket[kLayerSlot + k];
+      na.hashed_next = &d_hdr->hashed_next[k];   // look-ahead for layer k + 1 (its pairs' children are here)
+      na.gate = &d_hdr->gate[k];
       if ((rc = node_level(na, d_hdr))) return rc;
+      prev_regular = true;
       std::swap(in, outw);
       n = pk[k];
       bound = pk[k];

@@ -123,6 +123,8 @@ struct NodeLevel {
   bool direct_known = false;        // host knows the level is direct: launch the insert only
   u64* desc = nullptr;              // look-back descriptors (ceil(p / kTile))
   u32* ticket = nullptr;
+  u32* hashed_next = nullptr;       // single-device build: look ahead for the next level (null: off)
+  u64* gate = nullptr;              // ... and open its gate (the next level's pcount)
 };
 
 // One leaf level (all chunks).

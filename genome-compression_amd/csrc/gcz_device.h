@@ -74,6 +74,8 @@ struct Header {
   u32 ticket[kScanSlots];  // look-back tile tickets
   u64 err_offset;          // first unknown symbol (min), ~0 if none
   u64 hashed[64];          // node pairs that went through the table (statistics, sharded)
+  u64 gate[GCZ_MAX_LAYERS];  // gate[k] == size of layer k  =>  layer k+1 is direct (see k_resolve_node)
+  u32 hashed_next[GCZ_MAX_LAYERS];  // some pair of layer k (k >= 1) has two repeated children
   u32 overflow;            // a node-level probe bound was exceeded
   u32 leaf_overflow;       // the (adaptively sized) leaf table was too small
   u32 root;
@@ -649,22 +651,37 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_leaf(u32* __restrict__ word
 // Nodes: first occurrences recompute their canonical pair from the input
 // (coalesced) instead of reading the table, emit it, and publish the group
 // records that resolve_node uses.
+//
+// With `multi` and `hashed_next` given it also looks one level ahead: a pair of
+// the next level goes through the table only if both its children repeat
+// (singleton propagation); if no such pair exists, every pair of the next level
+// is a first occurrence and that level is direct (k_resolve_node opens its gate).
 [[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ words, u64 p,
                                                          const u32* __restrict__ in, u64 n,
                                                          const unsigned char* __restrict__ nf,
                                                          Group* __restrict__ grp, u64* __restrict__ desc,
                                                          u32* __restrict__ ticket, uint2* __restrict__ out,
-                                                         u64* __restrict__ count_out, const u64* prev_count) {
+                                                         u64* __restrict__ count_out, const u64* prev_count,
+                                                         const unsigned char* __restrict__ multi,
+                                                         u32* __restrict__ hashed_next) {
   if (level_direct(prev_count, n)) return;
   __shared__ u32 s_tile;
   __shared__ u32 s_pre[kGroupsPerTile];
+  __shared__ u32 s_hashed;
   TileScan<kItems> ts;
+  if (threadIdx.x == 0) s_hashed = 0;
   tile_scan(ts, &s_tile, s_pre, nf, 0, p, 0, desc, ticket, count_out);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const u64 lt = (1ull << lane) - 1;
+  bool hashed = false;
 #pragma unroll
   for (int e = 0; e < kItems; ++e) {
     const u64 j = ts.base + u64(e) * kBlock + tid;
+    if (hashed_next) {   // next-level pair (j, j+1): both children repeat?  (first <=> mask bit)
+      const bool rep = j < p && (((ts.mask[e] >> lane) & 1ull) == 0 || multi[j] != 0);
+      const bool partner = __shfl_xor(int(rep), 1, 64) != 0;
+      if ((lane & 1) == 0 && rep && (j + 1 < p ? partner : true)) hashed = true;
+    }
     const u32 gpre = s_pre[e * 4 + wave];
     if (lane == 0) {
       Group g;
@@ -682,6 +699,11 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_leaf(u32* __restrict__ word
       words[j] = id | (words[j] & kBits);
     }
   }
+  if (hashed_next) {
+    if (__ballot(hashed) && lane == 0) s_hashed = 1;
+    __syncthreads();
+    if (threadIdx.x == 0 && s_hashed) *hashed_next = 1;
+  }
 }
 
 // ---- resolve ----------------------------------------------------------------------
@@ -697,11 +719,16 @@ __global__ __launch_bounds__(kBlock) void k_resolve_leaf(u32* __restrict__ words
   words[j] = T.settled_id(w & kIdx) | (w & kBits);
 }
 
+// Block 0 also opens the next level's gate: gate = p (the next level is direct)
+// when this level is all unique or none of the next level's pairs hashes.
 template <class Tab>
 __global__ __launch_bounds__(kBlock) void k_resolve_node(u32* __restrict__ words, u64 p, Tab T,
                                                         const unsigned char* __restrict__ nf,
                                                         const Group* __restrict__ grp, const u64* prev_count,
-                                                        u64 n) {
+                                                        u64 n, const u64* __restrict__ count,
+                                                        const u32* __restrict__ hashed_next, u64* __restrict__ gate) {
+  if (gate && blockIdx.x == 0 && threadIdx.x == 0)
+    *gate = (*count == p || (hashed_next && *hashed_next == 0)) ? p : ~0ull;
   if (level_direct(prev_count, n)) return;
   const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (j >= p || nf[j] != kNfNot) return;
