@@ -337,13 +337,13 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       std::swap(in, outw);
       n = pk[k];
       bound = pk[k];
-      // one look at the device after layer 1: if it is all unique, every later level is
-      // direct and runs as direct subtrees (saves ~4 launches per level)
-      if (k == 1 && use_direct && n > u64(kTailMaxN)) {
-        u64 cnt = 0;
-        HIP_TRY(hipMemcpyAsync(&cnt, &d_hdr->count[kLayerSlot + 1], 8, hipMemcpyDeviceToHost, stream));
+      // a look at the device after layers 0 and 1: once a gate is open every later
+      // level is direct and runs as direct subtrees (saves ~4 launches per level)
+      if (k <= 1 && use_direct && n > u64(kTailMaxN)) {
+        u64 g = 0;
+        HIP_TRY(hipMemcpyAsync(&g, &d_hdr->gate[k], 8, hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
-        direct = cnt == n;
+        direct = g == n;
       }
     }
     if (!tail_done) {
