@@ -138,3 +138,28 @@ def test_gpu_large_synth_goldens(name, ctx, gcz, manifest):
     assert info["n_leaves"] == exp["n_leaves"]
     assert info["layer_size"] == exp["layer_sizes"]
     assert compare_digest(gcz.digest(ctx.tree()), exp) == {}
+
+
+@pytest.mark.parametrize("env", [{"GCZ_DIRECT": "0"}, {"GCZ_TAIL": "0"}, {"GCZ_DIRECT": "0", "GCZ_TAIL": "0"},
+                                 {"GCZ_NODE_CAP_SHIFT": "0"}, {"GCZ_LEAF_CAP_LOG2": "20"}])
+def test_gpu_schedule_knobs_same_tree(env, gcz, manifest):
+    """The per-level fallbacks (no direct subtrees, no fused top, tight tables, a leaf
+    table that overflows and regrows) build the same tree as the default schedule."""
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        c = gcz.Context(0)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    try:
+        for name in ("synth/uniform_10000000", "synth/tandem_10000000", "corpus/merged"):
+            case = manifest[name]
+            kind, payload, L = case_input(case, gcz)
+            _build(c, kind, payload, L)
+            assert compare_digest(gcz.digest(c.tree()), case["expect"]) == {}, (env, name)
+    finally:
+        c.close()
