@@ -93,6 +93,10 @@ int gcz_ctx::leaf_level(const LeafLevel& a, Header* d_hdr) {
                          d_nf, d_hdr);
     }
     HIP_TRY(hipGetLastError());
+    if (c == 0) {   // repetitive data? (switches the node inserts' LDS pre-dedupe)
+      hipLaunchKernelGGL(k_dup_probe, g, dim3(kBlock), 0, stream, A, i0, i1, d_hdr);
+      hipLaunchKernelGGL(k_dup_decide, dim3(1), dim3(1), 0, stream, d_hdr, i1 - i0, u32(predup_mode));
+    }
     prof_end(KID_LEAF, e0);
     const dim3 gs(unsigned((i1 - i0 + kLeafTile - 1) / kLeafTile));
     const u64* id0 = c == 0 ? nullptr : &a.count[c - 1];
@@ -306,11 +310,12 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
         int nlev = 0;
         u64 m = n;
         dp.n[0] = n;
-        while (nlev < kDirectLog && k + nlev < D && m > u64(kTailMaxN)) {
+        while (nlev < kDirectLog && k + nlev < D && (m > u64(kTailMaxN) || !use_tail)) {
           dp.layer_off[k + nlev] = layer_off[k + nlev];
           m = pk[k + nlev];
           dp.n[++nlev] = m;
         }
+        if (nlev == 0) return fail(GCZ_ERR_ARG, "build", "internal: empty direct step");
         if ((rc = direct_levels(in, k, nlev, dp, outw, d_hdr))) return rc;
         prev_regular = false;
         std::swap(in, outw);
@@ -409,6 +414,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   if (const char* t = std::getenv("GCZ_LEAF_CAP_LOG2")) c->leaf_cap_log2 = std::atoi(t);
   if (const char* t = std::getenv("GCZ_TAIL")) c->use_tail = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_DIRECT")) c->use_direct = std::atoi(t) != 0;
+  if (const char* t = std::getenv("GCZ_PREDUP")) c->predup_mode = std::atoi(t);   // 1 on, 2 off, 0 auto
   *out = c;
   return GCZ_OK;
 }

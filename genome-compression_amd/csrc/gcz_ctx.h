@@ -171,6 +171,7 @@ struct gcz_ctx {
   int leaf_cap_log2 = 0;     // force the adaptive leaf table size            (GCZ_LEAF_CAP_LOG2)
   bool use_tail = true;      // fuse the top levels into one launch           (GCZ_TAIL=0 disables)
   bool use_direct = true;    // direct subtrees after a host check at layer 1 (GCZ_DIRECT=0 disables)
+  int predup_mode = 0;       // node-insert LDS pre-dedupe: 0 auto, 1 on, 2 off  (GCZ_PREDUP)
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> event_pool;
   size_t event_used = 0;

@@ -76,6 +76,8 @@ struct Header {
   u64 hashed[64];          // node pairs that went through the table (statistics, sharded)
   u64 gate[GCZ_MAX_LAYERS];  // gate[k] == size of layer k  =>  layer k+1 is direct (see k_resolve_node)
   u32 hashed_next[GCZ_MAX_LAYERS];  // some pair of layer k (k >= 1) has two repeated children
+  u64 dupstat[64];         // in-block repeats among the first leaf chunk's strands (sharded)
+  u32 predup;              // node inserts pre-dedupe each block in LDS (repetitive data)
   u32 overflow;            // a node-level probe bound was exceeded
   u32 leaf_overflow;       // the (adaptively sized) leaf table was too small
   u32 root;
@@ -418,6 +420,37 @@ __global__ __launch_bounds__(kBlock) void k_leaf_bases(const unsigned char* __re
   rec[i] = make_word(r.settled ? r.id : r.slot, m, t, v);
 }
 
+// In-block repeats of the first leaf chunk (equal provisional slot words mean equal
+// keys): the statistic that switches the node inserts' LDS pre-dedupe on.
+[[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_dup_probe(const u32* __restrict__ rec, u64 i0,
+                                                                              u64 i1, Header* __restrict__ hdr) {
+  __shared__ u32 s_k[2 * kBlock];
+  __shared__ u32 s_n;
+  for (int q = threadIdx.x; q < 2 * kBlock; q += kBlock) s_k[q] = ~0u;
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  const u64 i = i0 + u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i < i1) {
+    const u32 w = rec[i] & kIdx;
+    u32 h = (w * 2654435761u) >> 23;   // 9 bits
+    for (;;) {
+      u32 c = s_k[h];
+      if (c == ~0u) c = atomicCAS(&s_k[h], ~0u, w);
+      if (c == w && c != ~0u) { atomicAdd(&s_n, 1u); break; }
+      if (c == ~0u) break;
+      h = (h + 1) & (2 * kBlock - 1);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && s_n) atomicAdd(&hdr->dupstat[blockIdx.x & 63], u64(s_n));
+}
+
+[[maybe_unused]] static __global__ void k_dup_decide(Header* __restrict__ hdr, u64 sampled, u32 force) {
+  u64 d = 0;
+  for (int q = 0; q < 64; ++q) d += hdr->dupstat[q];
+  hdr->predup = force == 1 ? 1u : force == 2 ? 0u : u32(d * 20 > sampled);   // > 5 % in-block repeats
+}
+
 // Leaf level from packed strands (shared_tree(std::vector<dna>&), :212-215).
 template <class Tab>
 __global__ __launch_bounds__(kBlock) void k_leaf_packed(const u64* __restrict__ leaves, u64 i0, u64 i1, int L,
@@ -483,31 +516,77 @@ __global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ 
     rec[j] = make_word(u32(j) + id_off, m, t, v);   // id_off: first pair of this rank (multi-rank build)
     return;
   }
+  // Repetitive data (hdr->predup, decided from the first leaf chunk): repeats of a
+  // key inside the block collapse onto its earliest position first, in an LDS
+  // table; only that representative touches the HBM table, the others are not
+  // first (an earlier position holds their key) and take its slot, and the
+  // representative is marked multi.  Output-invisible: the same marks and slots
+  // the global inserts would have produced.
   __shared__ u32 s_hashed;
+  __shared__ unsigned long long s_key[2 * kBlock];
+  __shared__ u32 s_pos[2 * kBlock];
+  __shared__ u32 s_slot[2 * kBlock];
+  __shared__ u32 s_dup[2 * kBlock];
+  const bool pre = hdr->predup != 0;
   if (threadIdx.x == 0) s_hashed = 0;
+  if (pre)
+    for (int q = threadIdx.x; q < 2 * kBlock; q += kBlock) {
+      s_key[q] = kEmpty;
+      s_pos[q] = ~0u;
+      s_dup[q] = 0;
+    }
   __syncthreads();
   const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
   bool single = true;
+  u32 m = 0, t = 0, v = 0, ls = 0;
+  u64 key = 0;
   if (j < p) {
-  u32 l, r, cl, cr, m, t;
-  load_pair(in, n, j, l, r);
-  node_canonical(l, r, cl, cr, m, t);
-  const u32 v = ulw(l) == ulw(xf(r, 1, 0));      // left == right.mirrored() (:670)
-  single = false;
-  if (prev_nf) {
-    if (2 * j + 1 < n) {
-      const uchar2 f = reinterpret_cast<const uchar2*>(prev_nf)[j];
-      const uchar2 g = reinterpret_cast<const uchar2*>(prev_multi)[j];
-      single = (f.x == 0 && g.x == 0) || (f.y == 0 && g.y == 0);
-    } else {
-      single = prev_nf[2 * j] == 0 && prev_multi[2 * j] == 0;
+    u32 l, r, cl, cr;
+    load_pair(in, n, j, l, r);
+    node_canonical(l, r, cl, cr, m, t);
+    v = ulw(l) == ulw(xf(r, 1, 0));      // left == right.mirrored() (:670)
+    single = false;
+    if (prev_nf) {
+      if (2 * j + 1 < n) {
+        const uchar2 f = reinterpret_cast<const uchar2*>(prev_nf)[j];
+        const uchar2 g = reinterpret_cast<const uchar2*>(prev_multi)[j];
+        single = (f.x == 0 && g.x == 0) || (f.y == 0 && g.y == 0);
+      } else {
+        single = prev_nf[2 * j] == 0 && prev_multi[2 * j] == 0;
+      }
+    }
+    key = T.node_key(cl, cr);
+    if (pre && !single) {
+      u32 h = slot_hash(key) & (2 * kBlock - 1);
+      for (;;) {
+        unsigned long long c = s_key[h];
+        if (c == kEmpty) c = atomicCAS(&s_key[h], kEmpty, (unsigned long long)key);
+        if (c == key) s_dup[h] = 1;                 // another position of the block holds it
+        if (c == kEmpty || c == key) break;
+        h = (h + 1) & (2 * kBlock - 1);
+      }
+      atomicMin(&s_pos[h], u32(j));
+      ls = h;
     }
   }
-  const u32 s = single ? 0u : T.insert(T.node_key(cl, cr), u32(j), mk, &hdr->overflow);
-  rec[j] = make_word(s, m, t, v);
+  if (pre) __syncthreads();
+  const bool rep = !pre || single || s_pos[ls] == u32(j);
+  u32 s = 0;
+  if (j < p && !single && rep) {
+    s = T.insert(key, u32(j), mk, &hdr->overflow);
+    if (pre) {
+      s_slot[ls] = s;
+      if (s_dup[ls]) mk.multi[j] = 1;
+    }
   }
+  if (pre) __syncthreads();
+  if (j < p && !single && !rep) {
+    s = s_slot[ls];
+    mk.nf[j] = kNfNot;
+  }
+  if (j < p) rec[j] = make_word(s, m, t, v);
   // statistics: pairs hashed, one LDS add per wave, one sharded global add per block
-  const u64 hb = __ballot(!single);
+  const u64 hb = __ballot(j < p && !single && rep);
   if ((threadIdx.x & 63) == 0 && hb) atomicAdd(&s_hashed, u32(__popcll(hb)));
   __syncthreads();
   if (threadIdx.x == 0 && s_hashed) atomicAdd(&hdr->hashed[blockIdx.x & 63], u64(s_hashed));

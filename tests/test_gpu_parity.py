@@ -141,7 +141,8 @@ def test_gpu_large_synth_goldens(name, ctx, gcz, manifest):
 
 
 @pytest.mark.parametrize("env", [{"GCZ_DIRECT": "0"}, {"GCZ_TAIL": "0"}, {"GCZ_DIRECT": "0", "GCZ_TAIL": "0"},
-                                 {"GCZ_NODE_CAP_SHIFT": "0"}, {"GCZ_LEAF_CAP_LOG2": "20"}])
+                                 {"GCZ_NODE_CAP_SHIFT": "0"}, {"GCZ_LEAF_CAP_LOG2": "20"},
+                                 {"GCZ_PREDUP": "1"}, {"GCZ_PREDUP": "2"}, {"GCZ_PREDUP": "1", "GCZ_TABLE": "wide"}])
 def test_gpu_schedule_knobs_same_tree(env, gcz, manifest):
     """The per-level fallbacks (no direct subtrees, no fused top, tight tables, a leaf
     table that overflows and regrows) build the same tree as the default schedule."""
