@@ -98,15 +98,21 @@ int gcz_ctx::leaf_level(const LeafLevel& a, Header* d_hdr) {
       hipLaunchKernelGGL(k_dup_decide, dim3(1), dim3(1), 0, stream, d_hdr, i1 - i0, u32(predup_mode));
     }
     prof_end(KID_LEAF, e0);
-    const dim3 gs(unsigned((i1 - i0 + kLeafTile - 1) / kLeafTile));
+    const u64 tile = scan_tile(i1 - i0);
+    const dim3 gs(unsigned((i1 - i0 + tile - 1) / tile));
     const u64* id0 = c == 0 ? nullptr : &a.count[c - 1];
     prof_begin(KID_FLAGSCAN_LEAF, e0);
-    if (lt.packed)
-      hipLaunchKernelGGL((k_flagscan_leaf<PackedTab>), gs, dim3(kBlock), 0, stream, A, i0, i1, lt.pt, d_nf,
-                         a.desc + a.desc_off[c], &a.ticket[c], a.out, id0, &a.count[c]);
-    else
-      hipLaunchKernelGGL((k_flagscan_leaf<WideTab>), gs, dim3(kBlock), 0, stream, A, i0, i1, lt.wt, d_nf,
-                         a.desc + a.desc_off[c], &a.ticket[c], a.out, id0, &a.count[c]);
+#define GCZ_FLAGSCAN_LEAF(TAB, TV, IT)                                                                   \
+  hipLaunchKernelGGL((k_flagscan_leaf<TAB, IT>), gs, dim3(kBlock), 0, stream, A, i0, i1, TV, d_nf,      \
+                     a.desc + a.desc_off[c], &a.ticket[c], a.out, id0, &a.count[c])
+    if (lt.packed) {
+      if (tile == u64(kTile)) GCZ_FLAGSCAN_LEAF(PackedTab, lt.pt, kItems);
+      else GCZ_FLAGSCAN_LEAF(PackedTab, lt.pt, kItemsSmall);
+    } else {
+      if (tile == u64(kTile)) GCZ_FLAGSCAN_LEAF(WideTab, lt.wt, kItems);
+      else GCZ_FLAGSCAN_LEAF(WideTab, lt.wt, kItemsSmall);
+    }
+#undef GCZ_FLAGSCAN_LEAF
     HIP_TRY(hipGetLastError());
     prof_end(KID_FLAGSCAN_LEAF, e0);
     prof_begin(KID_RESOLVE_LEAF, e0);
@@ -163,9 +169,14 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   HIP_TRY(hipGetLastError());
   prof_end(KID_NODE, e0);
   prof_begin(KID_FLAGSCAN_NODE, e0);
-  const dim3 gs(unsigned((p + kTile - 1) / kTile));
-  hipLaunchKernelGGL(k_flagscan_node, gs, dim3(kBlock), 0, stream, a.words, p, a.in, n, knf, d_grp, a.desc,
-                     a.ticket, a.out, a.count, a.pcount, mk.multi, a.hashed_next);
+  const u64 tile = scan_tile(p);
+  const dim3 gs(unsigned((p + tile - 1) / tile));
+  if (tile == u64(kTile))
+    hipLaunchKernelGGL((k_flagscan_node<kItems>), gs, dim3(kBlock), 0, stream, a.words, p, a.in, n, knf, d_grp,
+                       a.desc, a.ticket, a.out, a.count, a.pcount, mk.multi, a.hashed_next);
+  else
+    hipLaunchKernelGGL((k_flagscan_node<kItemsSmall>), gs, dim3(kBlock), 0, stream, a.words, p, a.in, n, knf, d_grp,
+                       a.desc, a.ticket, a.out, a.count, a.pcount, mk.multi, a.hashed_next);
   HIP_TRY(hipGetLastError());
   prof_end(KID_FLAGSCAN_NODE, e0);
   prof_begin(KID_RESOLVE_NODE, e0);
@@ -232,11 +243,12 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   u64 ntiles_total = 0;
   for (int c = 0; c < C; ++c) {
     desc_off.push_back(ntiles_total);
-    ntiles_total += (chunk_start[c + 1] - chunk_start[c] + kLeafTile - 1) / kLeafTile;
+    const u64 len = chunk_start[c + 1] - chunk_start[c];
+    ntiles_total += (len + scan_tile(len) - 1) / scan_tile(len);
   }
   for (int k = 0; k < D; ++k) {
     desc_off.push_back(ntiles_total);
-    ntiles_total += (pk[k] + kTile - 1) / kTile;
+    ntiles_total += (pk[k] + scan_tile(pk[k]) - 1) / scan_tile(pk[k]);
   }
 
   // leaf table: big enough for S when S is small; otherwise start at 2^24 slots

@@ -45,11 +45,16 @@ constexpr u32 kIdx = 0x1fffffffu;
 constexpr u32 kBits = 0xe0000000u;
 constexpr u64 kEmpty = ~0ull;
 constexpr int kBlock = 256;
-constexpr int kItems = 32;                 // node flagscan elements per thread (look-back tiles of 8192)
-constexpr int kTile = kBlock * kItems;     // 2048 elements per look-back tile
-constexpr int kGroupsPerTile = kTile / 64; // 32
-constexpr int kLeafItems = 32;             // leaf flagscan: most strands are already settled
+constexpr int kItems = 32;                 // flagscan elements per thread on large levels
+constexpr int kTile = kBlock * kItems;     // 8192 elements per look-back tile
+constexpr int kGroupsPerTile = kTile / 64; // 128
+constexpr int kItemsSmall = 8;             // ... on levels below 2^20 elements: more tiles, shorter ones
+constexpr int kTileSmall = kBlock * kItemsSmall;
+constexpr int kLeafItems = kItems;         // leaf flagscan: most strands are already settled
 constexpr int kLeafTile = kBlock * kLeafItems;
+// Look-back tile of a scan over n elements: long tiles keep the look-back chain short
+// on big levels, short ones keep enough tiles in flight on small ones.
+__host__ __device__ inline u64 scan_tile(u64 n) { return n >= (1ull << 20) ? u64(kTile) : u64(kTileSmall); }
 constexpr u32 kMaxProbe = 1u << 16;
 
 struct __align__(16) Slot {   // WideTab slot; key stored as key ^ 1 (see WideTab)
@@ -698,21 +703,21 @@ __device__ __forceinline__ void tile_scan(TileScan<ITEMS>& ts, u32* s_tile, u32*
 // uniques of earlier chunks): first occurrences read their slot to recover the
 // canonical leaf, emit it, and settle the slot with their id, which both the
 // chunk's resolve and later chunks' inserts read.
-template <class Tab>
+template <class Tab, int ITEMS>
 __global__ __launch_bounds__(kBlock) void k_flagscan_leaf(u32* __restrict__ words, u64 j0, u64 p, Tab T,
                                                          const unsigned char* __restrict__ nf,
                                                          u64* __restrict__ desc, u32* __restrict__ ticket,
                                                          u64* __restrict__ out, const u64* __restrict__ id0_p,
                                                          u64* __restrict__ count_out) {
   __shared__ u32 s_tile;
-  __shared__ u32 s_pre[4 * kLeafItems];
-  TileScan<kLeafItems> ts;
+  __shared__ u32 s_pre[4 * ITEMS];
+  TileScan<ITEMS> ts;
   const u64 id0 = id0_p ? *id0_p : 0;
   tile_scan(ts, &s_tile, s_pre, nf, j0, p, id0, desc, ticket, count_out);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const u64 lt = (1ull << lane) - 1;
 #pragma unroll
-  for (int e = 0; e < kLeafItems; ++e) {
+  for (int e = 0; e < ITEMS; ++e) {
     const u64 j = ts.base + u64(e) * kBlock + tid;
     if (j < p && ((ts.mask[e] >> lane) & 1ull)) {
       const u32 id = s_pre[e * 4 + wave] + u32(__popcll(ts.mask[e] & lt));
@@ -735,7 +740,8 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_leaf(u32* __restrict__ word
 // the next level goes through the table only if both its children repeat
 // (singleton propagation); if no such pair exists, every pair of the next level
 // is a first occurrence and that level is direct (k_resolve_node opens its gate).
-[[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ words, u64 p,
+template <int ITEMS>
+__global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ words, u64 p,
                                                          const u32* __restrict__ in, u64 n,
                                                          const unsigned char* __restrict__ nf,
                                                          Group* __restrict__ grp, u64* __restrict__ desc,
@@ -745,16 +751,16 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_leaf(u32* __restrict__ word
                                                          u32* __restrict__ hashed_next) {
   if (level_direct(prev_count, n)) return;
   __shared__ u32 s_tile;
-  __shared__ u32 s_pre[kGroupsPerTile];
+  __shared__ u32 s_pre[4 * ITEMS];
   __shared__ u32 s_hashed;
-  TileScan<kItems> ts;
+  TileScan<ITEMS> ts;
   if (threadIdx.x == 0) s_hashed = 0;
   tile_scan(ts, &s_tile, s_pre, nf, 0, p, 0, desc, ticket, count_out);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const u64 lt = (1ull << lane) - 1;
   bool hashed = false;
 #pragma unroll
-  for (int e = 0; e < kItems; ++e) {
+  for (int e = 0; e < ITEMS; ++e) {
     const u64 j = ts.base + u64(e) * kBlock + tid;
     if (hashed_next) {   // next-level pair (j, j+1): both children repeat?  (first <=> mask bit)
       const bool rep = j < p && (((ts.mask[e] >> lane) & 1ull) == 0 || multi[j] != 0);

@@ -330,11 +330,9 @@ int gcz_group::alloc(int i, int L, u64 leaf_cap) {
   node_base[i][P.D] = nodes;
   const auto chunks = leaf_chunks(S_r);
   u64 tiles = 0;
-  for (size_t q = 0; q + 1 < chunks.size(); ++q) tiles += (chunks[q + 1] - chunks[q] + kLeafTile - 1) / kLeafTile;
-  for (int k = 0; k < P.D; ++k) {
-    const u64 pl = k < P.G ? P.count(r, k + 1) : (r == 0 ? P.nk[k + 1] : 0);
-    tiles += (pl + kTile - 1) / kTile;
-  }
+  auto ntiles = [](u64 n) { return (n + scan_tile(n) - 1) / scan_tile(n); };
+  for (size_t q = 0; q + 1 < chunks.size(); ++q) tiles += ntiles(chunks[q + 1] - chunks[q]);
+  for (int k = 0; k < P.D; ++k) tiles += ntiles(k < P.G ? P.count(r, k + 1) : (r == 0 ? P.nk[k + 1] : 0));
   int rc;
   if ((rc = c->ensure(c->wa, wmax * 4 + 16))) return rc;
   if ((rc = c->ensure(c->wb, wmax * 4 + 16))) return rc;
@@ -773,7 +771,8 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
       C[i] = int(la.chunk_start.size()) - 1;
       for (int q = 0; q < C[i]; ++q) {
         la.desc_off.push_back(dcur[i]);
-        dcur[i] += (la.chunk_start[q + 1] - la.chunk_start[q] + kLeafTile - 1) / kLeafTile;
+        const u64 len = la.chunk_start[q + 1] - la.chunk_start[q];
+        dcur[i] += (len + scan_tile(len) - 1) / scan_tile(len);
       }
       la.desc = cx->desc.as<u64>();
       la.count = h->count;
@@ -874,7 +873,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         na.id_off = u32(P.start(r, k + 1));
         na.direct_known = direct;
         na.desc = cx->desc.as<u64>() + dcur[i];
-        dcur[i] += (p + kTile - 1) / kTile;
+        dcur[i] += (p + scan_tile(p) - 1) / scan_tile(p);
         na.ticket = &h->ticket[kLayerSlot + k];
         if (cx->node_level(na, h)) return dev_fail("node level");
         RankLevel& rl = lv[i];
@@ -964,7 +963,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
           na.prev_marks = k > G;
           na.pcount = k == G ? &dh->cell[G] : &h->count[kLayerSlot + k - 1];
           na.desc = cx->desc.as<u64>() + dcur[i];
-          dcur[i] += (na.p + kTile - 1) / kTile;
+          dcur[i] += (na.p + scan_tile(na.p) - 1) / scan_tile(na.p);
           na.ticket = &h->ticket[kLayerSlot + k];
           if (cx->node_level(na, h)) return dev_fail("tail level");
           in = bufs[nb];
