@@ -290,7 +290,7 @@ struct gcz_group {
     return fail(GCZ_ERR_DEVICE, std::string(what) + (tr && !tr->err.empty() ? ": " + tr->err : ""));
   }
   int build(const void* const* d_bases, const u64* const* d_leaves, u64 S, int L);
-  int alloc(int i, int L, u64 leaf_cap);
+  int alloc(int i, u64 leaf_cap);
   int exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, u32 key_bits, u32 child_bits,
                std::vector<u64>& c, std::vector<u64>& off, u64& total, u64* err_global, int* err_sym,
                int* ovf_bits);
@@ -310,7 +310,7 @@ namespace {
 constexpr int kRetry = -1000;   // internal: some rank overflowed a table, rebuild
 }
 
-int gcz_group::alloc(int i, int L, u64 leaf_cap) {
+int gcz_group::alloc(int i, u64 leaf_cap) {
   gcz_ctx* c = ctx[i];
   const int r = rank[i];
   const DistPlan& P = plan;
@@ -738,7 +738,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     for (int i = 0; i < NL; ++i) {
       gcz_ctx* cx = ctx[i];
       cx->allow_packed = allow_packed;
-      if (int rc = alloc(i, L, leaf_cap[i])) return rc == GCZ_ERR_DEVICE ? dev_fail("allocation") : rc;
+      if (int rc = alloc(i, leaf_cap[i])) return rc == GCZ_ERR_DEVICE ? dev_fail("allocation") : rc;
       if (!cx->ev_start) {
         G_HIP(hipEventCreate(&cx->ev_start));
         G_HIP(hipEventCreate(&cx->ev_stop));
