@@ -2,29 +2,59 @@
 // The file is read once; the line contract is libgcz's gcz_fasta_extract.
 #include "fasta_reader.h"
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <cstdlib>
-#include <fstream>
+#include <cstring>
 #include <iostream>
 
 #include "gcz.h"
 
 fasta_reader::fasta_reader(std::filesystem::path path, std::size_t buffer_size)
     : file_path{std::move(path)}, buffer_size{buffer_size ? buffer_size : 1} {
-  std::ifstream f(file_path, std::ios::binary);
-  if (!f.is_open()) {   // fasta_reader.cpp:15-18
+  const int fd = ::open(file_path.c_str(), O_RDONLY);
+  struct stat st {};
+  if (fd < 0 || ::fstat(fd, &st) != 0) {   // fasta_reader.cpp:15-18
     std::cerr << "Unable to open file, aborting...\n";
     std::exit(1);
   }
-  f.seekg(0, std::ios::end);
-  bytes.resize(std::size_t(f.tellg()));
-  f.seekg(0, std::ios::beg);
-  if (!bytes.empty()) f.read(reinterpret_cast<char*>(bytes.data()), std::streamsize(bytes.size()));
-  seq.resize(bytes.size());
-  seq.resize(gcz_fasta_extract(bytes.data(), bytes.size(), seq.data()));
+  nbytes = std::size_t(st.st_size);
+  if (nbytes) {
+    void* m = ::mmap(nullptr, nbytes, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+    if (m == MAP_FAILED) {
+      std::cerr << "Unable to open file, aborting...\n";
+      std::exit(1);
+    }
+    const std::size_t n = nbytes;
+    bytes = std::shared_ptr<const std::uint8_t>(static_cast<const std::uint8_t*>(m),
+                                                [n](const std::uint8_t* q) { ::munmap(const_cast<std::uint8_t*>(q), n); });
+  }
+  ::close(fd);
+}
+
+void fasta_reader::extract() const {
+  if (extracted) return;
+  seq.resize(nbytes);
+  seq.resize(gcz_fasta_extract(bytes.get(), nbytes, seq.data()));
   strands = seq.size() / dna::size();
+  extracted = true;
+}
+
+auto fasta_reader::bases() const -> const std::vector<std::uint8_t>& {
+  extract();
+  return seq;
+}
+
+auto fasta_reader::eof() const -> bool {
+  extract();
+  return next >= strands;
 }
 
 auto fasta_reader::read_into(std::vector<dna>& vector) -> bool {
+  extract();
   if (next >= strands) return false;
   const std::size_t n = std::min(buffer_size, strands - next);
   const std::size_t L = dna::size();
@@ -35,7 +65,7 @@ auto fasta_reader::read_into(std::vector<dna>& vector) -> bool {
   return true;
 }
 
-auto fasta_reader::size() const -> std::size_t { return bytes.size(); }
+auto fasta_reader::size() const -> std::size_t { return nbytes; }
 
 auto fasta_reader::buffers() const -> std::size_t { return size() / (buffer_size * dna::size()); }
 

@@ -6,12 +6,17 @@
 // :488-546, iterator :553-614.
 #include "shared_tree.h"
 
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <memory>
 #include <mutex>
 #include <numeric>
 #include <sstream>
+#include <thread>
+
+#include <unistd.h>
 
 #include "gcz.h"
 #include "../gcz_internal.h"
@@ -40,6 +45,19 @@ Engine& engine() {
   return e;
 }
 
+// GCZ_TIMING=1: host wall-clock of the construction phases on stderr ("gcz-time phase ms").
+struct PhaseTimer {
+  const char* name;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  explicit PhaseTimer(const char* n) : name{n} {}
+  ~PhaseTimer() {
+    static const bool on = std::getenv("GCZ_TIMING") != nullptr;
+    if (on)
+      std::cerr << "gcz-time " << name << ' '
+                << std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() << '\n';
+  }
+};
+
 void check_build(int rc, gcz_ctx* ctx) {
   if (rc == GCZ_OK) return;
   gcz_info info{};
@@ -66,7 +84,8 @@ int segment(std::uint32_t idx) {
 }
 constexpr std::uint32_t kSegStart[4] = {0, 16, 16 + 4096, 16 + 4096 + 1048576};
 
-gcz::TreeView view(const std::vector<std::vector<node>>& nodes, const std::vector<dna>& leaves, pointer root) {
+template <class Layers, class Leaves>
+gcz::TreeView view(const Layers& nodes, const Leaves& leaves, pointer root) {
   gcz::TreeView v;
   v.L = int(dna::size());
   v.leaves = const_cast<std::uint64_t*>(reinterpret_cast<const std::uint64_t*>(leaves.data()));
@@ -136,11 +155,27 @@ auto node::deserialize(std::istream& is) -> node {
 }
 
 // ---- construction (libgcz) -------------------------------------------------------
+namespace {
+// The device context comes up (HIP runtime + code objects, ~0.1 s) while the file is mapped.
+fasta_reader open_with_engine(const std::filesystem::path& path) {
+  if (::access(path.c_str(), R_OK) != 0) return fasta_reader{path};   // prints the reference's error
+  PhaseTimer t{"open"};
+  std::thread init([] { PhaseTimer t{"context"}; engine(); });
+  fasta_reader f = [&] { PhaseTimer t{"map"}; return fasta_reader{path}; }();
+  init.join();
+  return f;
+}
+}  // namespace
+
+shared_tree::shared_tree(std::filesystem::path path) : shared_tree{open_with_engine(path)} {}
+
 shared_tree::shared_tree(fasta_reader file, bool verbose) {
   auto& e = engine();
   std::lock_guard<std::mutex> lock(e.mu);
-  const auto& raw = file.raw();
-  check_build(gcz_build_host_fasta(e.ctx, raw.data(), raw.size(), int(dna::size())), e.ctx);
+  {
+    PhaseTimer t{"upload+build"};
+    check_build(gcz_build_host_fasta(e.ctx, file.raw_data(), file.raw_size(), int(dna::size())), e.ctx);
+  }
   build_from_gpu();
   if (verbose) std::cout << "\rConstructing subtrees: done.\n\rCombining subtrees: done.\n";
 }
@@ -157,14 +192,15 @@ shared_tree::shared_tree(std::vector<dna>& data, bool verbose) {
 }
 
 void shared_tree::build_from_gpu() {
+  PhaseTimer t{"fetch"};
   gcz_ctx* ctx = engine().ctx;
   gcz_info info{};
   gcz_info_get(ctx, &info);
   leaves.resize(info.n_leaves);
   if (info.n_leaves) check_build(gcz_copy_leaves(ctx, reinterpret_cast<std::uint64_t*>(leaves.data())), ctx);
-  nodes.assign(info.n_layers, {});
+  nodes.resize(info.n_layers);   // keeps each layer's storage when a device sort refetches the same sizes
   for (int k = 0; k < info.n_layers; ++k) {
-    nodes[k].resize(info.layer_size[k], node{pointer{}});
+    nodes[k].resize(info.layer_size[k]);
     check_build(gcz_copy_layer(ctx, k, reinterpret_cast<std::uint32_t*>(nodes[k].data())), ctx);
   }
   root = pointer::from_word(info.root);
@@ -263,7 +299,7 @@ std::vector<std::size_t> sorted_positions(const std::vector<std::size_t>& freq) 
 
 void shared_tree::sort_leaves() {
   const auto pos = sorted_positions(histogram(0));
-  std::vector<dna> r(leaves.size());
+  leaf_vector r(leaves.size());
   for (std::size_t i = 0; i < pos.size(); ++i) r[pos[i]] = leaves[i];
   leaves.swap(r);
   rewire_nodes(0, pos);
@@ -271,7 +307,7 @@ void shared_tree::sort_leaves() {
 
 void shared_tree::sort_nodes(std::size_t layer) {
   const auto pos = sorted_positions(histogram(layer + 1));
-  std::vector<node> r(nodes[layer].size(), node{pointer{}});
+  layer_vector r(nodes[layer].size());
   for (std::size_t i = 0; i < pos.size(); ++i) r[pos[i]] = nodes[layer][i];
   nodes[layer].swap(r);
   rewire_nodes(layer + 1, pos);
@@ -281,7 +317,10 @@ void shared_tree::sort_tree(bool verbose) {
   if (on_device()) {   // the arrays are still in HBM: sort there, copy the result back
     auto& e = engine();
     std::lock_guard<std::mutex> lock(e.mu);
-    check_build(gcz_sort_device(e.ctx), e.ctx);
+    {
+      PhaseTimer t{"device-sort"};
+      check_build(gcz_sort_device(e.ctx), e.ctx);
+    }
     build_from_gpu();
   } else {
     auto v = view(nodes, leaves, root);   // all layers at once, in parallel (same net effect)
@@ -303,9 +342,9 @@ void shared_tree::serialize(std::ostream& os) const {
   if (on_device()) {   // the .dag is written on the device
     std::uint64_t n = 0;
     if (gcz_bytes_device(engine().ctx, &n) == GCZ_OK) {
-      std::vector<std::uint8_t> buf(n);
-      if (gcz_serialize_device(engine().ctx, buf.data(), n, &n) == GCZ_OK) {
-        os.write(reinterpret_cast<const char*>(buf.data()), std::streamsize(n));
+      std::unique_ptr<std::uint8_t[]> buf(new std::uint8_t[n]);   // left uninitialised: the D2H copy fills it
+      if (gcz_serialize_device(engine().ctx, buf.get(), n, &n) == GCZ_OK) {
+        os.write(reinterpret_cast<const char*>(buf.get()), std::streamsize(n));
         return;
       }
     }
@@ -340,6 +379,7 @@ auto shared_tree::deserialize(std::istream& is) -> shared_tree {
 }
 
 void shared_tree::save(std::filesystem::path path) const {
+  PhaseTimer t{"save"};
   std::ofstream file{path, std::ios::binary};
   serialize(file);
 }

@@ -9,8 +9,9 @@
  * exits(1).  read_into() hands out consecutive buffers of buffer_size strands.
  *
  * shared_tree{path} / shared_tree{fasta_reader} do NOT go through these
- * buffers: they hand the raw file to libgcz, which applies the same contract
- * on the host and packs the strands on the GPU.
+ * buffers: they hand the raw file (memory-mapped, never copied on the host) to
+ * libgcz, which applies the same contract and packs the strands on the GPU.
+ * The host-side extraction behind read_into()/bases() runs on first use only.
  * Implementation: genome-compression_amd/csrc/cxx/fasta_reader.cpp.
  */
 #pragma once
@@ -18,6 +19,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <filesystem>
+#include <memory>
 #include <vector>
 
 #include "dna.h"
@@ -30,22 +32,27 @@ class fasta_reader {
   fasta_reader(const fasta_reader&) = delete;
   fasta_reader(fasta_reader&&) noexcept = default;
 
-  auto eof() const -> bool { return next >= strands; }
+  auto eof() const -> bool;
   auto read_into(std::vector<dna>& vector) -> bool;
   auto size() const -> std::size_t;      // file size in bytes (upper bound on bases)
   auto buffers() const -> std::size_t;   // approximate number of buffers
   auto path() const -> const std::filesystem::path& { return file_path; }
 
-  // Raw file bytes and the concatenated bases (FASTA contract applied).
-  auto raw() const -> const std::vector<std::uint8_t>& { return bytes; }
-  auto bases() const -> const std::vector<std::uint8_t>& { return seq; }
+  // Raw file bytes (read-only mapping) and the concatenated bases (FASTA contract applied).
+  auto raw_data() const -> const std::uint8_t* { return bytes.get(); }
+  auto raw_size() const -> std::size_t { return nbytes; }
+  auto bases() const -> const std::vector<std::uint8_t>&;
 
  private:
+  void extract() const;
+
   std::filesystem::path file_path;
   std::size_t buffer_size;
-  std::vector<std::uint8_t> bytes;
-  std::vector<std::uint8_t> seq;
-  std::size_t strands = 0;
+  std::shared_ptr<const std::uint8_t> bytes;
+  std::size_t nbytes = 0;
+  mutable std::vector<std::uint8_t> seq;
+  mutable std::size_t strands = 0;
+  mutable bool extracted = false;
   std::size_t next = 0;
 };
 

@@ -25,7 +25,10 @@
 #include <cstdint>
 #include <filesystem>
 #include <iostream>
+#include <memory>
 #include <tuple>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "dna.h"
@@ -140,10 +143,34 @@ struct hash<node> {
 };
 }  // namespace std
 
+// Allocator of the tree's containers: resize() without a value leaves the
+// elements (plain 32/64-bit words with trivial destructors) uninitialised,
+// because a device copy or a full permutation fills them right after -- 0.6 GB
+// of value-initialisation and page faults otherwise.
+template <class T>
+struct gcz_uninit_allocator : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = gcz_uninit_allocator<U>;
+  };
+  gcz_uninit_allocator() = default;
+  template <class U>
+  gcz_uninit_allocator(const gcz_uninit_allocator<U>&) noexcept {}
+  template <class U>
+  void construct(U*) noexcept {
+    static_assert(std::is_trivially_destructible_v<U> && std::is_standard_layout_v<U>,
+                  "uninitialised construction needs a plain word type");
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
+};
+
 class shared_tree {
  public:
   shared_tree() = default;
-  shared_tree(std::filesystem::path path) : shared_tree{fasta_reader{path}} {}
+  shared_tree(std::filesystem::path path);
   shared_tree(fasta_reader file, bool verbose = false);
   shared_tree(std::vector<dna>& data, bool verbose = false);
 
@@ -206,8 +233,10 @@ class shared_tree {
   void build_from_gpu();   // copies the last libgcz build of this thread into the containers
   bool on_device() const;  // the engine's device arrays still hold exactly this tree
 
-  std::vector<std::vector<node>> nodes;
-  std::vector<dna> leaves;
+  using layer_vector = std::vector<node, gcz_uninit_allocator<node>>;
+  using leaf_vector = std::vector<dna, gcz_uninit_allocator<dna>>;
+  std::vector<layer_vector> nodes;
+  leaf_vector leaves;
   pointer root;
   std::uint64_t device_gen = 0;   // engine build generation mirrored here (0: host only)
 };
