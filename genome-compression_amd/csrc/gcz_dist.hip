@@ -20,7 +20,7 @@ using namespace gcz_host;
 
 struct gcz_dist_state {
   DevBuf scratch, gnf, gmul, gid, blockcnt, skey, sidx, sflag, scval, sdval;   // sender side
-  DevBuf rkey, oslot, rflag, rcval, rdval, owntab, oids;                      // owner side
+  DevBuf rkey, oslot, rflag, rcval, rdval, owntab, oids, omin;                // owner side
   DevBuf s_selc, s_seld, s_prec, s_pred, o_selc, o_seld, o_prec, o_pred, sdesc;  // C/D compaction
   DevBuf dhdr, gath, gath2, gathf, ddesc, tail_in;
   u64* h_gath = nullptr;    // pinned mirrors of the gathered vectors
@@ -33,7 +33,7 @@ void gcz_dist_state_free(gcz_ctx* c) {
   if (!d) return;
   for (DevBuf* b : {&d->scratch, &d->gnf, &d->gmul, &d->gid, &d->blockcnt, &d->skey, &d->sidx, &d->sflag,
                     &d->scval, &d->sdval, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab, &d->oids,
-                    &d->s_selc, &d->s_seld, &d->s_prec, &d->s_pred, &d->o_selc, &d->o_seld, &d->o_prec,
+                    &d->omin, &d->s_selc, &d->s_seld, &d->s_prec, &d->s_pred, &d->o_selc, &d->o_seld, &d->o_prec,
                     &d->o_pred, &d->sdesc,
                     &d->dhdr, &d->gath, &d->gath2, &d->gathf, &d->ddesc, &d->tail_in})
     if (b->ptr) (void)hipFree(b->ptr);
@@ -279,6 +279,9 @@ struct gcz_group {
   std::vector<std::vector<u64>> slice_off, slice_cnt;   // [layer + 1][global rank]
   std::vector<std::vector<u64>> node_base;              // [local][layer]: node offset within nodes_out
   bool allow_packed = true;
+  // node levels: 0 auto (local dedupe only on repetitive data), 1 always, 2 never (GCZ_DIST_LOCAL)
+  int dist_local = std::getenv("GCZ_DIST_LOCAL") ? std::atoi(std::getenv("GCZ_DIST_LOCAL")) : 0;
+  bool any_predup = false;   // some rank's leaf probe found repetitive data (set by the leaf exchange)
 
   int fail(int code, const std::string& what) {
     last_error = what;
@@ -293,7 +296,7 @@ struct gcz_group {
   int alloc(int i, u64 leaf_cap);
   int exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, u32 key_bits, u32 child_bits,
                std::vector<u64>& c, std::vector<u64>& off, u64& total, u64* err_global, int* err_sym,
-               int* ovf_bits);
+               int* ovf_bits, bool nolocal = false);
 };
 
 #define G_HIP(x)                                                   \
@@ -380,9 +383,11 @@ int gcz_group::alloc(int i, u64 leaf_cap) {
 
 // key_bits: bits of the owner-table key (leaves 4L, nodes 2 (child_bits + 2)); packed slots when
 // key_bits + R + 2 <= 64, else wide.
+// nolocal: the senders skipped the local dedupe of this level (k_node_keys), the owners
+// find the first occurrence from the receive order (stable bucketing).
 int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, u32 key_bits, u32 child_bits,
                         std::vector<u64>& c, std::vector<u64>& off, u64& total, u64* err_global, int* err_sym,
-                        int* ovf_bits) {
+                        int* ovf_bits, bool nolocal) {
   const int R = world, NL = int(ctx.size());
   // 1. bucket the records by owner, pack the sync vector
   for (int i = 0; i < NL; ++i) {
@@ -431,6 +436,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     for (int q = 0; q < R; ++q) { M[size_t(s) * R + q] = v[q]; records += v[q]; }
     *ovf_bits |= int(v[R]);
     u[s] = v[R + 1];
+    if (v[R + 4]) any_predup = true;
     if (v[R + 2] != ~0ull) {
       const u64 g = v[R + 2] + plan.start(s, 0) * u64(info.L);   // local byte offset -> genome offset
       if (g < *err_global) { *err_global = g; *err_sym = int(v[R + 3]); }
@@ -492,6 +498,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       const bool packed = key_bits + u32(R) + 2 <= 64 && !cx->force_wide;
       if ((rc = cx->ensure(d.owntab, cap * (packed ? 8 : 16)))) return dev_fail("owner table");
       if (packed && (rc = cx->ensure(d.oids, cap * 4))) return dev_fail("owner ids");
+      if (nolocal && (rc = cx->ensure(d.omin, cap * 4))) return dev_fail("owner first index");
       otab[i] = OwnTab{};
       otab[i].tab = d.owntab.as<Slot>();
       otab[i].ptab = d.owntab.as<u64>();
@@ -501,6 +508,8 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       otab[i].R = u32(R);
       otab[i].B = child_bits;
       otab[i].sh = u32(R) + 2;
+      otab[i].nolocal = nolocal;
+      otab[i].omin = nolocal ? d.omin.as<u32>() : nullptr;
       s.push_back(d.skey.ptr);
       rv.push_back(d.rkey.ptr);
     }
@@ -518,11 +527,15 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       const u64 nr = recvd(rank[i]);
       ProfScope ps_(cx, KID_OWNER);
       G_HIP(hipMemsetAsync(d.owntab.ptr, 0xff, size_t(otab[i].mask + 1) * (otab[i].packed ? 8 : 16), cx->stream));
+      if (nolocal) G_HIP(hipMemsetAsync(d.omin.ptr, 0xff, size_t(otab[i].mask + 1) * 4, cx->stream));
       const Displ D = displ_of(rank[i]);
       hipLaunchKernelGGL(k_own_insert, blocks(nr), dim3(kBlock), 0, cx->stream, d.rkey.as<u64>(), nr, D, u32(R),
                          int(lv[i].leaves), otab[i], d.oslot.as<u32>(), &d.dhdr.as<DistHdr>()->final_vec[3]);
       hipLaunchKernelGGL(k_own_reply, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr, D, u32(R),
                          otab[i], d.rflag.as<unsigned char>());
+      if (nolocal)
+        hipLaunchKernelGGL(k_own_first, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr, otab[i],
+                           d.rflag.as<unsigned char>());
       // the owner's view of the C / D compactions (same records, same order as the senders')
       hipLaunchKernelGGL(k_sel, blocks(nr), dim3(kBlock), 0, cx->stream, d.rflag.as<unsigned char>(), nr,
                          d.o_selc.as<unsigned char>(), d.o_seld.as<unsigned char>());
@@ -751,6 +764,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     }
     // per-rank descriptor cursors
     std::vector<u64> dcur(NL, 0);
+    any_predup = false;
 
     // ---- leaves ----
     std::vector<int> C(NL);
@@ -820,6 +834,9 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     for (int i = 0; i < NL; ++i) ctx[i]->leaf_cap_hint = next_pow2(std::max<u64>(1, 2 * total));
 
     // ---- distributed node levels ----
+    // Without repetitive data the local dedupe of a node level finds almost nothing and
+    // only doubles the hashing: the pairs go straight to their owners.
+    const bool nolocal = dist_local == 2 || (dist_local == 0 && !any_predup);
     u64 prev_total = total;        // uniques of the previous level (child id bound)
     bool direct = total == P.nk[0];
     bool retry = false;
@@ -875,7 +892,16 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         na.desc = cx->desc.as<u64>() + dcur[i];
         dcur[i] += (p + scan_tile(p) - 1) / scan_tile(p);
         na.ticket = &h->ticket[kLayerSlot + k];
-        if (cx->node_level(na, h)) return dev_fail("node level");
+        if (nolocal && !direct) {
+          const int cs = (k + 1) & 1;
+          ProfScope ps_(cx, KID_NODE);
+          hipLaunchKernelGGL(k_node_keys, dim3(unsigned(std::max<u64>(1, (p + kBlock - 1) / kBlock))), dim3(kBlock), 0,
+                             cx->stream, cur_in[i], n, p, cur_out[i], cx->dist->scratch.as<uint2>(), cx->nf_set[cs],
+                             cx->multi_set[cs], na.count);
+          G_HIP(hipGetLastError());
+        } else if (cx->node_level(na, h)) {
+          return dev_fail("node level");
+        }
         RankLevel& rl = lv[i];
         rl = RankLevel{};
         rl.src.in = cur_in[i];
@@ -902,7 +928,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         std::vector<u64> nw(NL);
         for (int i = 0; i < NL; ++i) nw[i] = P.count(rank[i], k + 1);
         const u32 cb = std::max<u32>(1, bit_width(prev_total));
-        const int rc = exchange(lv, nw, 2 * (cb + 2), cb, c, off, total, &err_global, &err_sym, &ovf);
+        const int rc = exchange(lv, nw, 2 * (cb + 2), cb, c, off, total, &err_global, &err_sym, &ovf, nolocal);
         if (rc == kRetry) {
           allow_packed = false;
           retry = true;

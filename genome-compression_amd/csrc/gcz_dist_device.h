@@ -28,12 +28,13 @@
 namespace gcz_dev {
 
 constexpr int kMaxRanks = 31;              // owner slot state: one bit per rank + local-multi bit
-constexpr int kSyncWords = kMaxRanks + 4;  // per-rank sync vector (see DistHdr)
+constexpr int kSyncWords = kMaxRanks + 5;  // per-rank sync vector (see DistHdr)
 constexpr int kFinalWords = 4 + GCZ_MAX_LAYERS;
 
 struct DistHdr {
   // per-level sync vector: [0, R) records per owner, [R] overflow, [R+1] local uniques,
-  // [R+2] first bad symbol offset (local bytes), [R+3] that symbol
+  // [R+2] first bad symbol offset (local bytes), [R+3] that symbol, [R+4] repetitive
+  // data (the leaf probe's pre-dedupe decision)
   u64 sync[kSyncWords];
   // second sync vector: [0] globally-first local uniques, [1, 1+R) C records per owner,
   // [1+R, 1+2R) D records per owner (see exchange)
@@ -161,22 +162,50 @@ static __global__ __launch_bounds__(1024) void k_bucket_scan(u32* __restrict__ a
   }
 }
 
+// Stable: a block's records keep their order inside each destination segment (rounds
+// in order, waves in order within a round, lanes in order within a wave), so every
+// owner receives each source's records in the source's order.  Owners of levels that
+// skip the local dedupe rely on it: the first record of a key is its first occurrence.
 static __global__ __launch_bounds__(kBlock) void k_bucket_scatter(RecSrc s, const u32* __restrict__ boff, u32 nb,
                                                                   u64* __restrict__ skey, u32* __restrict__ sidx) {
+  constexpr int kWaves = kBlock / 64;
   __shared__ u32 cur[kMaxRanks];
-  const int tid = threadIdx.x;
+  __shared__ u32 wcnt[kWaves][kMaxRanks];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid < int(s.R)) cur[tid] = boff[u64(tid) * nb + blockIdx.x];
+  for (int q = tid; q < kWaves * kMaxRanks; q += kBlock) (&wcnt[0][0])[q] = 0;
   __syncthreads();
-#pragma unroll 4
+  const u64 lt = (1ull << lane) - 1;
   for (int e = 0; e < kItems; ++e) {
     const u64 idx = u64(blockIdx.x) * kTile + u64(e) * kBlock + tid;
-    u64 key;
-    u32 lid;
-    if (rec_get(s, idx, key, lid)) {
-      const u32 o = atomicAdd(&cur[owner_of(rec_key(s, key), s.R)], 1u);
+    u64 key = 0;
+    u32 lid = 0;
+    const bool ok = rec_get(s, idx, key, lid);
+    const u32 d = ok ? owner_of(rec_key(s, key), s.R) : 0u;
+    u32 before = 0;
+    u64 left = __ballot(ok);
+    while (left) {                                  // one ballot per distinct destination in the wave
+      const int leader = __ffsll((long long)left) - 1;
+      const u32 dl = __shfl(d, leader, 64);
+      const u64 m = __ballot(ok && d == dl);
+      if (ok && d == dl) before = __popcll(m & lt);
+      if (lane == leader) wcnt[wave][dl] = u32(__popcll(m));
+      left &= ~m;
+    }
+    __syncthreads();
+    if (ok) {
+      u32 o = cur[d] + before;
+      for (int w = 0; w < wave; ++w) o += wcnt[w][d];
       skey[o] = key;
       sidx[o] = lid;
     }
+    __syncthreads();
+    if (tid < int(s.R)) {
+      u32 t = 0;
+      for (int w = 0; w < kWaves; ++w) { t += wcnt[w][tid]; wcnt[w][tid] = 0; }
+      cur[tid] += t;
+    }
+    __syncthreads();
   }
 }
 
@@ -199,6 +228,8 @@ struct OwnTab {
   u32 R;
   u32 B;         // packed node keys: child index bits
   u32 sh;        // packed: R + 2
+  u32 nolocal;   // the senders skipped the local dedupe: a key may arrive twice from one rank
+  u32* omin;     // nolocal: first (lowest) receive index of the key in each slot
 };
 
 __device__ __forceinline__ u64 own_pack_key(u64 key, int leaves, u32 B) {
@@ -250,11 +281,16 @@ static __global__ __launch_bounds__(kBlock) void k_own_insert(const u64* __restr
         }
       }
       if ((cur >> T.sh) == pk) {
-        // the reply only needs: the lowest rank, >= 2 ranks, repeats anywhere.  Once the
-        // word shows two ranks with a lower one than src, this record changes none of them.
-        const u32 ranks = u32(cur >> 1) & ((1u << R) - 1u);
-        const bool settled = __popc(ranks) >= 2 && (ranks & ((1u << src) - 1u)) != 0;
-        if (!settled && (cur & bits) != bits) atomicOr(&T.ptab[s], bits);
+        if (T.nolocal) {   // a second record: the key repeats (first found by k_own_reply / k_own_first)
+          const u64 b2 = bits | (u64(1u << R) << 1);
+          if ((cur & b2) != b2) atomicOr(&T.ptab[s], b2);
+        } else {
+          // the reply only needs: the lowest rank, >= 2 ranks, repeats anywhere.  Once the
+          // word shows two ranks with a lower one than src, this record changes none of them.
+          const u32 ranks = u32(cur >> 1) & ((1u << R) - 1u);
+          const bool settled = __popc(ranks) >= 2 && (ranks & ((1u << src) - 1u)) != 0;
+          if (!settled && (cur & bits) != bits) atomicOr(&T.ptab[s], bits);
+        }
         oslot[k] = s;
         return;
       }
@@ -267,7 +303,8 @@ static __global__ __launch_bounds__(kBlock) void k_own_insert(const u64* __restr
       u64 cur = T.tab[s].key;
       if (cur == kEmpty) cur = atomicCAS(&T.tab[s].key, kEmpty, skey);
       if (cur == kEmpty || cur == skey) {
-        atomicAnd(&T.tab[s].pos, ~((1u << src) | (lm << 31)));
+        const u32 rep = T.nolocal && cur == skey ? 1u : lm;
+        atomicAnd(&T.tab[s].pos, ~((1u << src) | (rep << 31)));
         oslot[k] = s;
         return;
       }
@@ -284,12 +321,28 @@ static __global__ __launch_bounds__(kBlock) void k_own_reply(const u32* __restri
   const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (k >= nrecv) return;
   const u32 src = seg_of(D, R, k);
-  const u32 st = own_state(T, oslot[k]);
+  const u32 s = oslot[k];
+  const u32 st = own_state(T, s);
   const u32 ranks = st & 0x7fffffffu;
   const u32 minr = u32(__ffs(ranks) - 1);
   const u32 shared = __popc(ranks) > 1;
   const u32 gm = shared | (st >> 31);
-  rflag[k] = (unsigned char)((minr != src) | (gm << 1) | (shared << 2));
+  if (T.nolocal) {
+    // first = lowest receive index among the key's records (k_own_first settles the
+    // repeated keys, marked 0x80 here); C / D run whenever the key repeats
+    if (gm) atomicMin(&T.omin[s], u32(k));
+    rflag[k] = gm ? (unsigned char)(0x80 | 6) : (unsigned char)0;
+  } else {
+    rflag[k] = (unsigned char)((minr != src) | (gm << 1) | (shared << 2));
+  }
+}
+
+static __global__ __launch_bounds__(kBlock) void k_own_first(const u32* __restrict__ oslot, u64 nrecv, OwnTab T,
+                                                             unsigned char* __restrict__ rflag) {
+  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= nrecv) return;
+  const unsigned char f = rflag[k];
+  if (f & 0x80) rflag[k] = (unsigned char)((f & 6) | (T.omin[oslot[k]] != u32(k) ? 1 : 0));
 }
 
 // Per-record flags (reply bits): 1 not globally first, 2 repeats globally, 4 held by >= 2 ranks.
@@ -449,6 +502,29 @@ static __global__ void k_dist_pack(const Header* __restrict__ h, const u64* __re
   const u64 e = h->err_offset;
   dh->sync[R + 2] = e;
   dh->sync[R + 3] = (e != ~0ull && bases) ? u64(bases[e]) : 0ull;
+  dh->sync[R + 4] = u64(h->predup);
+}
+
+// A node level without the local dedupe: every pair is its own local unique (local id =
+// position), so the owners alone hash-cons it.  Writes what node_level would leave
+// behind for the exchange: local words, canonical pairs (the finalize source), marks
+// (all locally first, none known to repeat) and the local unique count.
+static __global__ __launch_bounds__(kBlock) void k_node_keys(const u32* __restrict__ in, u64 n, u64 p,
+                                                             u32* __restrict__ words, uint2* __restrict__ pairs,
+                                                             unsigned char* __restrict__ nf,
+                                                             unsigned char* __restrict__ multi,
+                                                             u64* __restrict__ count_out) {
+  const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (j == 0) *count_out = p;
+  if (j >= p) return;
+  u32 l, r, cl, cr, m, t;
+  load_pair(in, n, j, l, r);
+  node_canonical(l, r, cl, cr, m, t);
+  const u32 v = ulw(l) == ulw(xf(r, 1, 0));
+  pairs[j] = make_uint2(cl, cr);
+  words[j] = make_word(u32(j), m, t, v);
+  nf[j] = kNfMaybe;
+  multi[j] = 0;
 }
 
 static __global__ void k_dist_final(const Header* __restrict__ h, DistHdr* __restrict__ dh, int tail0, int D,

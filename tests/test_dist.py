@@ -188,3 +188,49 @@ def test_dist_rccl_world1(gcz, manifest):
         g.close()
     finally:
         ctx.close()
+
+
+def _group_with_env(gcz, world, env):
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return gcz.Group.local(world)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_dist_local_dedupe_modes(mode, world, gcz, manifest, oracle):
+    """Node levels with (GCZ_DIST_LOCAL=1) and without (=2) the local dedupe: without it a
+    key reaches its owner once per occurrence, several times from one rank, and the owner
+    takes the first record in receive order (stable bucketing) as the first occurrence."""
+    g = _group_with_env(gcz, world, {"GCZ_DIST_LOCAL": mode})
+    try:
+        for name in ("corpus/chmpxx", "corpus/merged", "synth/uniform_10000000", "synth/tandem_10000000"):
+            case = manifest[name]
+            kind, payload, L = case_input(case, gcz)
+            _dist_build(gcz, g, kind, payload, L)
+            assert compare_digest(gcz.digest(g.tree()), case["expect"]) == {}, name
+        rng = np.random.default_rng(world)
+        alphabet = np.frombuffer(b"ACGTRYKMBVDHSWN-", dtype=np.uint8)
+        base = alphabet[rng.integers(0, 4, size=400_000)]
+        for _ in range(30):     # repeats inside one rank and across ranks
+            a = int(rng.integers(0, 390_000))
+            b = int(rng.integers(0, 390_000))
+            base[b:b + 5000] = base[a:a + 5000]
+        data = base.tobytes()
+        ref = oracle.build_fasta(data, 6)
+        _dist_build(gcz, g, "fasta", data, 6)
+        t = g.tree()
+        assert np.array_equal(t.leaves(), ref.leaves())
+        for k in range(ref.n_layers):
+            assert np.array_equal(t.layer(k), ref.layer(k)), k
+        assert t.root == ref.root
+    finally:
+        g.close()
