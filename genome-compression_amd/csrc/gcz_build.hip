@@ -139,7 +139,7 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     prof_begin(KID_NODE, e0);
     const dim3 gi(unsigned((p + kBlock - 1) / kBlock));
     hipLaunchKernelGGL((k_node_insert<WideTab>), gi, dim3(kBlock), 0, stream, a.in, n, p, WideTab{}, nullptr, nullptr,
-                       a.words, Marks{knf, multi_set[cur]}, d_hdr, a.pcount, a.out, a.count, a.id_off);
+                       a.words, Marks{knf, multi_set[cur]}, d_hdr, a.pcount, a.out, a.count, a.id_off, stats.as<u64>());
     HIP_TRY(hipGetLastError());
     prof_end(KID_NODE, e0);
     return GCZ_OK;
@@ -162,10 +162,10 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   const dim3 gi(unsigned((p + kBlock - 1) / kBlock));
   if (nt.packed)
     hipLaunchKernelGGL((k_node_insert<PackedTab>), gi, dim3(kBlock), 0, stream, a.in, n, p, nt.pt, pnf, pmu,
-                       a.words, mk, d_hdr, a.pcount, a.out, a.count, a.id_off);
+                       a.words, mk, d_hdr, a.pcount, a.out, a.count, a.id_off, stats.as<u64>());
   else
     hipLaunchKernelGGL((k_node_insert<WideTab>), gi, dim3(kBlock), 0, stream, a.in, n, p, nt.wt, pnf, pmu,
-                       a.words, mk, d_hdr, a.pcount, a.out, a.count, a.id_off);
+                       a.words, mk, d_hdr, a.pcount, a.out, a.count, a.id_off, stats.as<u64>());
   HIP_TRY(hipGetLastError());
   prof_end(KID_NODE, e0);
   prof_begin(KID_FLAGSCAN_NODE, e0);
@@ -267,6 +267,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   if ((rc = ensure(leaves_out, S * 8 + 16))) return rc;
   if ((rc = ensure(nodes_out, layer_off[D] * 8 + 16))) return rc;
   if ((rc = ensure(hdr, sizeof(Header)))) return rc;
+  if ((rc = ensure(stats, kStatBytes))) return rc;
   if ((rc = ensure_marks(S))) return rc;
   if (!h_hdr) HIP_TRY(hipHostMalloc((void**)&h_hdr, sizeof(Header), hipHostMallocDefault));
 
@@ -287,6 +288,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     HIP_TRY(hipMemsetAsync(d_hdr, 0, sizeof(Header), stream));
     HIP_TRY(hipMemsetAsync(&d_hdr->err_offset, 0xff, 8, stream));
     HIP_TRY(hipMemsetAsync(d_desc, 0, ntiles_total * 8, stream));
+    HIP_TRY(hipMemsetAsync(stats.ptr, 0, kStatBytes, stream));
 
     // ---- leaf level, in chunks ----
     LeafLevel la;
@@ -367,6 +369,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       hipLaunchKernelGGL(k_root, dim3(1), dim3(1), 0, stream, in, d_hdr);
       HIP_TRY(hipGetLastError());
     }
+    hipLaunchKernelGGL(k_stats_sum, dim3(1), dim3(1024), 0, stream, stats.as<u64>(), &d_hdr->hashed[0]);
     HIP_TRY(hipEventRecord(ev_stop, stream));
     HIP_TRY(hipMemcpyAsync(h_hdr, d_hdr, sizeof(Header), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
@@ -439,7 +442,7 @@ void gcz_ctx_destroy(gcz_ctx* c) {
   gcz_sort_state_free(c);
   gcz_ingest_state_free(c);
   for (DevBuf* b : {&c->wa, &c->wb, &c->grp, &c->desc, &c->tab, &c->leaves_out, &c->nodes_out, &c->hdr, &c->input,
-                    &c->nf, &c->multi})
+                    &c->nf, &c->multi, &c->stats})
     if (b->ptr) (void)hipFree(b->ptr);
   if (c->h_hdr) (void)hipHostFree(c->h_hdr);
   for (auto e : c->event_pool) (void)hipEventDestroy(e);

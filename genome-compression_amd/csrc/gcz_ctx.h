@@ -156,6 +156,7 @@ struct gcz_ctx {
   hipStream_t stream = nullptr;
   std::string last_error;
   gcz_host::DevBuf wa, wb, grp, desc, tab, leaves_out, nodes_out, hdr, input, nf, multi;
+  gcz_host::DevBuf stats;   // hashed-pair counter shards (k_node_insert), summed into hdr->hashed[0]
   gcz_dev::Header* h_hdr = nullptr;   // pinned
   unsigned char* nf_set[2] = {nullptr, nullptr};      // marks, even / odd layers
   unsigned char* multi_set[2] = {nullptr, nullptr};

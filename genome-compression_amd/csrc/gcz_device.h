@@ -499,6 +499,25 @@ __device__ __forceinline__ bool level_direct(const u64* prev_count, u64 prev_n) 
   return prev_count && *prev_count == prev_n;
 }
 
+// Hashed-pair statistics: one atomic per block into 1024 shards, one 64-B line each
+// (a handful of shared counters serialises ~10^5 block atomics: +0.3 ms on layer 0).
+constexpr int kStatShards = 1024, kStatStride = 8;
+constexpr size_t kStatBytes = size_t(kStatShards) * kStatStride * 8;
+
+[[maybe_unused]] static __global__ __launch_bounds__(1024) void k_stats_sum(const u64* __restrict__ shards, u64* __restrict__ out) {
+  __shared__ u64 s_sum[1024 / 64];
+  u64 v = shards[threadIdx.x * kStatStride];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 t = 0;
+    for (int w = 0; w < 1024 / 64; ++w) t += s_sum[w];
+    *out = t;
+  }
+}
+
 template <class Tab>
 __global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ in, u64 n, u64 p, Tab T,
                                                        const unsigned char* __restrict__ prev_nf,
@@ -506,7 +525,7 @@ __global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ 
                                                        u32* __restrict__ rec, Marks mk,
                                                        Header* __restrict__ hdr, const u64* prev_count,
                                                        uint2* __restrict__ out, u64* __restrict__ count_out,
-                                                       u32 id_off) {
+                                                       u32 id_off, u64* __restrict__ stats) {
   if (level_direct(prev_count, n)) {
     const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
     if (j == 0) *count_out = p;
@@ -594,7 +613,7 @@ __global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ 
   const u64 hb = __ballot(j < p && !single && rep);
   if ((threadIdx.x & 63) == 0 && hb) atomicAdd(&s_hashed, u32(__popcll(hb)));
   __syncthreads();
-  if (threadIdx.x == 0 && s_hashed) atomicAdd(&hdr->hashed[blockIdx.x & 63], u64(s_hashed));
+  if (threadIdx.x == 0 && s_hashed) atomicAdd(&stats[(blockIdx.x & (kStatShards - 1)) * kStatStride], u64(s_hashed));
 }
 
 // ---- flag scan ------------------------------------------------------------------

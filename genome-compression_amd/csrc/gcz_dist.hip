@@ -344,6 +344,7 @@ int gcz_group::alloc(int i, u64 leaf_cap) {
   if ((rc = c->ensure(c->leaves_out, S_r * 8 + 16))) return rc;
   if ((rc = c->ensure(c->nodes_out, nodes * 8 + 16))) return rc;
   if ((rc = c->ensure(c->hdr, sizeof(Header)))) return rc;
+  if ((rc = c->ensure(c->stats, kStatBytes))) return rc;
   if ((rc = c->ensure_marks(wmax))) return rc;
   const u64 pmax = std::max<u64>(P.G > 0 ? P.count(r, 1) : 0, nG > 1 ? (nG + 1) / 2 : 1);
   if ((rc = c->ensure(c->tab, std::max(leaf_cap, c->node_cap(pmax)) * 16))) return rc;
