@@ -38,7 +38,6 @@ void gcz_sort_state_free(gcz_ctx* c) {
 
 namespace {
 
-constexpr int kAccShards = 256;   // k_node_sizes partial sums
 constexpr u32 kSegStart1 = 16, kSegStart2 = 16 + 4096, kSegStart3 = 16 + 4096 + 1048576;
 
 __device__ __forceinline__ bool is_null(u32 w) { return ulw(w) == kIdx; }
@@ -162,10 +161,10 @@ __global__ __launch_bounds__(kBlock) void k_node_sizes(const uint2* __restrict__
   for (int o = 32; o > 0; o >>= 1) b += u32(__shfl_xor(int(b), o, 64));
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = b;
   __syncthreads();
-  if (threadIdx.x == 0) {   // sharded partial sums: one address for every block would serialise
+  if (threadIdx.x == 0) {   // line-padded shards (k_stats_sum): a few shared addresses would serialise
     u32 t = 0;
     for (int w = 0; w < kBlock / 64; ++w) t += part[w];
-    if (t) atomicAdd(&acc[blockIdx.x & (kAccShards - 1)], (unsigned long long)t);
+    if (t) atomicAdd(&acc[(blockIdx.x & (kStatShards - 1)) * kStatStride], (unsigned long long)t);
   }
 }
 
@@ -350,19 +349,19 @@ int gcz_bytes_device(gcz_ctx* c, uint64_t* out) {
   S_HIP(hipSetDevice(c->device));
   if (!c->sortst) c->sortst = new gcz_sort_state();
   gcz_sort_state& s = *c->sortst;
-  if (int rc = c->ensure(s.acc, kAccShards * 8)) return rc;
-  S_HIP(hipMemsetAsync(s.acc.ptr, 0, kAccShards * 8, c->stream));
+  if (int rc = c->ensure(s.acc, kStatBytes + 8)) return rc;
+  S_HIP(hipMemsetAsync(s.acc.ptr, 0, kStatBytes, c->stream));
   const int D = c->info.n_layers;
   const u64 N = c->layer_off[D];
   const LayerStarts ls = layer_starts(c);
   hipLaunchKernelGGL(k_node_sizes, grid_of(N), dim3(kBlock), 0, c->stream, c->nodes_out.as<uint2>(), N, ls, D,
                      nullptr, s.acc.as<unsigned long long>());
+  u64* total = s.acc.as<u64>() + kStatBytes / 8;
+  hipLaunchKernelGGL(k_stats_sum, dim3(1), dim3(1024), 0, c->stream, s.acc.as<u64>(), total);
   S_HIP(hipGetLastError());
-  u64 part[kAccShards];
-  S_HIP(hipMemcpyAsync(part, s.acc.ptr, sizeof(part), hipMemcpyDeviceToHost, c->stream));
-  S_HIP(hipStreamSynchronize(c->stream));
   u64 nb = 0;
-  for (u64 v : part) nb += v;
+  S_HIP(hipMemcpyAsync(&nb, total, 8, hipMemcpyDeviceToHost, c->stream));
+  S_HIP(hipStreamSynchronize(c->stream));
   *out = host_ptr_bytes(c->info.root) + 8 + c->info.n_leaves * u64((c->info.L + 1) / 2) +
          8 * u64(c->info.n_layers) + nb;
   return GCZ_OK;
@@ -382,7 +381,7 @@ static int serialize_on_device(gcz_ctx* c, unsigned char** d_dag, uint64_t* writ
     return rc;
   hipEvent_t e0{};
   c->prof_begin(KID_DAG, e0);
-  S_HIP(hipMemsetAsync(s.acc.ptr, 0, kAccShards * 8, c->stream));
+  S_HIP(hipMemsetAsync(s.acc.ptr, 0, kStatBytes, c->stream));
   const LayerStarts ls = layer_starts(c);
   hipLaunchKernelGGL(k_node_sizes, grid_of(N), dim3(kBlock), 0, c->stream, c->nodes_out.as<uint2>(), N, ls, D,
                      s.sizes.as<u32>(), s.acc.as<unsigned long long>());
