@@ -8,14 +8,16 @@ with the ASCII bases already resident in HBM (SURVEY §8(d) timing scope).
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config uniform_1g]
 
 N > 1 is launched by torch.distributed.run (one process per GPU).  Default
-(--mode dist): the ONE 1 Gbase genome is partitioned over the ranks
-(gcz_dist_plan: contiguous strand ranges, rank order = position order); each
-rank generates only its own bases, and every hash-consed level reconciles keys
-through their owner rank with RCCL all-to-all over xGMI (gcz_group, DESIGN.md
-§7).  Total work is fixed: "scaling": "strong".  --mode replicas runs N
-independent builds of N different genomes (weak scaling, no data-path
-collective) for comparison.  --virtual R (one GPU) runs the distributed path
-with R virtual ranks on one device, to measure its overhead.
+(--mode weak): ONE genome of N x the configured size (uniform_1g: N Gbase) is
+partitioned over the ranks (gcz_dist_plan: contiguous strand ranges, rank order =
+position order), so every GPU holds and builds 1 Gbase of it; each rank generates
+only its own bases, and every hash-consed level reconciles keys through their
+owner rank with RCCL all-to-all over xGMI (gcz_group).  Per-GPU
+work is fixed: "scaling": "weak".  --mode strong partitions the configured
+genome itself (1 Gbase over N GPUs, total work fixed); --mode replicas runs N
+independent builds of N different genomes (no data-path collective).
+--virtual R (one GPU) runs the distributed path with R virtual ranks on one
+device, to measure its overhead.
 
 Printed (rank 0): ONE JSON line with value, roofline of the dominant kernel,
 the CPU baseline (compiled reference on this host, bounded sample) and the
@@ -41,6 +43,10 @@ CONFIGS = {
     "uniform_100m": {"kind": 0, "nbases": 100_000_003, "golden": "synth/uniform_100000003"},
     "tandem_100m": {"kind": 1, "nbases": 100_000_000, "golden": "synth/tandem_100000000"},
     "tandem_3g2": {"kind": 1, "nbases": 3_200_000_000, "golden": "synth/tandem_3200000000"},
+    # the genomes of the weak-scaled runs (N x uniform_1g), for --virtual probes on one GPU
+    "uniform_2g": {"kind": 0, "nbases": 2_000_000_000, "golden": "synth/uniform_2000000000"},
+    "uniform_4g": {"kind": 0, "nbases": 4_000_000_000, "golden": "synth/uniform_4000000000"},
+    "uniform_8g": {"kind": 0, "nbases": 8_000_000_000, "golden": "synth/uniform_8000000000"},
     # BASELINE configs 2 and 3: the bundled corpus files (FASTA; headers stripped on the host)
     "hehcmv": {"kind": "file", "path": "tests/golden/data/hehcmv", "golden": "corpus/hehcmv"},
     "merged": {"kind": "file", "path": "tests/golden/data/merged", "golden": "corpus/merged"},
@@ -137,13 +143,14 @@ def cpu_baseline(sample_bases):
             "sample": f"synthetic uniform ACGT, {sample_bases} bases, oracle/gcz_oracle.c"}
 
 
-def gather_tree(gcz, group, dist, rank, world, L):
-    """Rank slices -> rank 0 (gloo point-to-point): the whole tree for the parity check."""
-    info = group.info()
-    if world == 1:
-        return group.tree()
-    import torch   # already imported before libgcz when world > 1 (one HIP runtime)
+def stream_digest(group, dist, rank, world, info):
+    """Bit identity of a distributed tree without assembling it: rank 0 hashes the
+    ref_harness dump streams (leaves.bin; layers.bin = per layer a u64 node count and
+    the raw words), taking the rank slices in rank order (rank r holds a contiguous id
+    range of every layer) -- its own from HBM, the others' over gloo point-to-point."""
     layers = list(range(-1, info["n_layers"]))
+    if world > 1:
+        import torch   # already imported before libgcz when world > 1 (one HIP runtime)
     if rank != 0:
         for layer in layers:
             a = group.copy_slice(0, layer)
@@ -151,18 +158,22 @@ def gather_tree(gcz, group, dist, rank, world, L):
             if a.size:
                 dist.send(torch.from_numpy(a.view(np.int64) if layer < 0 else a.view(np.int32)), 0)
         return None
-    parts = {layer: [group.copy_slice(0, layer)] for layer in layers}
-    for src in range(1, world):
-        for layer in layers:
+    h_leaves, h_layers = hashlib.sha256(), hashlib.sha256()
+    for layer in layers:
+        h = h_leaves if layer < 0 else h_layers
+        if layer >= 0:
+            h.update(np.uint64(info["layer_size"][layer]).astype("<u8").tobytes())
+        for i in range(group.n_local):   # virtual ranks: every slice is local
+            h.update(group.copy_slice(i, layer).tobytes())
+        for src in range(1, world):
             n = torch.zeros(1, dtype=torch.int64)
             dist.recv(n, src)
             n = int(n.item())
             if n:
                 t = torch.empty(n, dtype=torch.int64 if layer < 0 else torch.int32)
                 dist.recv(t, src)
-                parts[layer].append(t.numpy().view(np.uint64 if layer < 0 else np.uint32))
-    leaves = np.concatenate(parts[-1])
-    return gcz.Tree.from_arrays(L, leaves, [np.concatenate(parts[k]) for k in layers[1:]], info["root"])
+                h.update(t.numpy().tobytes())
+    return {"sha_leaves_bin": h_leaves.hexdigest(), "sha_layers_bin": h_layers.hexdigest()}
 
 
 def main():
@@ -174,7 +185,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=120_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
-    ap.add_argument("--mode", choices=["dist", "replicas"], default="dist", help="N > 1: one genome or N genomes")
+    ap.add_argument("--mode", choices=["weak", "strong", "dist", "replicas"], default="weak",
+                    help="N > 1: one genome of N x the config size (weak), the config genome itself over N GPUs "
+                         "(strong; 'dist' is an alias), or N independent genomes (replicas)")
     ap.add_argument("--virtual", type=int, default=0, help="N = 1: distributed path with R virtual ranks")
     ap.add_argument("--rccl-world1", action="store_true", help="N = 1: the RCCL group path with one rank")
     args = ap.parse_args()
@@ -198,9 +211,17 @@ def main():
         with open(os.path.join(REPO, cfg["path"]), "rb") as f:
             raw = f.read()
         cfg = dict(cfg, nbases=len(gcz.fasta_extract(raw)), file_size=len(raw))
+    if args.mode == "dist":
+        args.mode = "strong"
+    weak = world > 1 and args.mode == "weak"
+    if weak:   # one genome of world x the configured size, 1 config genome per GPU
+        if cfg["kind"] == "file":
+            sys.exit("--mode weak needs a synthetic config (the corpus files have a fixed size)")
+        name = "uniform" if cfg["kind"] == 0 else "tandem"
+        cfg = dict(cfg, nbases=cfg["nbases"] * world, golden=f"synth/{name}_{cfg['nbases'] * world}")
     nbases = cfg["nbases"]
     S = nbases // L
-    mode = ("dist" if args.mode == "dist" else "replicas") if world > 1 else ("virtual" if args.virtual else "single")
+    mode = ("replicas" if args.mode == "replicas" else "dist") if world > 1 else ("virtual" if args.virtual else "single")
     if world == 1 and args.rccl_world1:
         mode = "dist"
     seed = gcz._lib.gcz_synth_default_seed()
@@ -295,14 +316,32 @@ def main():
 
     parity = None
     tree = None
-    if not args.no_parity and cfg["golden"]:
-        if mode == "dist":
-            tree = gather_tree(gcz, group, dist, rank, world, L)   # every rank sends its slices
+    golden = None
+    with open(os.path.join(REPO, "tests", "golden", "manifest.json")) as f:
+        golden = json.load(f).get(cfg["golden"]) if cfg["golden"] else None
+    exp = golden["expect"] if golden else None
+    if not args.no_parity:
+        if mode in ("dist", "virtual"):   # every rank streams its slices to rank 0
+            t0 = time.perf_counter()
+            d = stream_digest(group, dist, rank, world, info)
+            if rank == 0:
+                parity = {"golden": cfg["golden"] if exp else None, "digest_s": round(time.perf_counter() - t0, 2),
+                          "layers_sha256": d["sha_layers_bin"], "leaves_sha256": d["sha_leaves_bin"]}
+                if exp:
+                    parity.update({"layers_sha256_match": d["sha_layers_bin"] == exp["sha_layers_bin"],
+                                   "leaves_sha256_match": d["sha_leaves_bin"] == exp["sha_leaves_bin"],
+                                   "root_match": info["root"] == exp["root"],
+                                   "layer_sizes_match": info["layer_size"] == exp["layer_sizes"],
+                                   "ratio_ref": exp["ratio"]})
+                else:
+                    parity["note"] = f"no reference golden for {cfg['golden']} (hashes reported)"
         elif rank == 0:                                            # replicas: rank 0 built the golden genome
-            tree = group.tree() if mode == "virtual" else ctx.tree()
-    if tree is not None and rank == 0:
-        with open(os.path.join(REPO, "tests", "golden", "manifest.json")) as f:
-            exp = json.load(f)[cfg["golden"]]["expect"]
+            tree = ctx.tree()
+    if tree is not None and (not exp or "sha_dag" not in exp):   # no golden: report the dump hashes
+        parity = {"golden": None, "note": f"no reference golden for {cfg['golden']} (hashes reported)",
+                  "leaves_sha256": hashlib.sha256(tree.leaves_bin()).hexdigest(),
+                  "layers_sha256": hashlib.sha256(tree.layers_bin()).hexdigest()}
+    elif tree is not None:
         d = gcz.digest(tree)
         ratio = f"{cfg.get('file_size', nbases) / d['bytes']:.6g}"   # compress reports file size / bytes()
         parity = {"golden": cfg["golden"],
@@ -325,7 +364,7 @@ def main():
                       "dag_bytes": int(n.value), "ratio": f"{cfg.get('file_size', nbases) / max(int(n.value), 1):.6g}"}
         if parity is not None:
             dag = ctx.serialize_device()
-            parity["device_dag_sha256_match"] = hashlib.sha256(dag).hexdigest() == exp["sha_dag"]
+            parity["device_dag_sha256_match"] = exp is not None and hashlib.sha256(dag).hexdigest() == exp["sha_dag"]
         del dptr
         # decompression on the device (operator[] for every index) and the round trip
         text = ctx.upload(np.zeros(S * L, dtype=np.uint8))
@@ -348,12 +387,15 @@ def main():
         line = {
             "metric": METRIC, "value": value, "unit": "bases/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "weak" if mode == "replicas" else "strong",
+            "scaling": "weak" if (weak or mode == "replicas") else "strong",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": args.config, "nbases": nbases * (world if mode == "replicas" else 1), "L": L,
+            "config": {"workload": args.config, "nbases": nbases * (world if mode == "replicas" else 1),
+                       "per_gpu_nbases": nbases // world if mode == "dist" else nbases, "L": L,
                        "strands": S * (world if mode == "replicas" else 1),
                        "parallelism": {"single": "1 GPU",
-                                       "dist": f"dist{world}: strand ranges per GPU, owner-hashed RCCL all-to-all per level",
+                                       "dist": f"dist{world}: one genome, strand ranges per GPU "
+                                               f"({'1 config genome per GPU' if weak else 'config genome split'}), "
+                                               "owner-hashed RCCL all-to-all per level",
                                        "replicas": f"{world} independent genomes, one per GPU",
                                        "virtual": f"{args.virtual} virtual ranks on 1 GPU (overhead probe)"}[mode]},
             "roofline": roofline,

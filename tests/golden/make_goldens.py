@@ -16,7 +16,11 @@ oracle/_ref/ref_harness, i.e. from the reference's own src/*.cpp:
 manifest.json maps every case to its inputs and the reference's outputs
 (sha256 of leaves.bin / layers.bin / unsorted.dag / dag, counts, root, ratio).
 
-usage: python tests/golden/make_goldens.py [--synth-large | --synth-huge]
+usage: python tests/golden/make_goldens.py [--synth-large | --synth-huge | --synth KIND:N ...]
+
+--synth KIND:N (repeatable) computes only those synthetic genomes (KIND 0 uniform,
+1 tandem) and merges them into the manifest, e.g. the 2 Gbase uniform genome that
+bench.py's weak-scaled 2-GPU run builds (--synth 0:2000000000, ~4 min, ~20 GB).
 """
 import gzip
 import hashlib
@@ -175,7 +179,18 @@ def main():
         with open(manifest_path) as f:
             manifest = json.load(f)
     tmp = tempfile.mkdtemp(prefix="gcz_golden_")
+    only = [tuple(int(x) for x in a.split(":")) for i, a in enumerate(sys.argv) if i and sys.argv[i - 1] == "--synth"]
     try:
+        if only:
+            for kind, n in only:
+                key = f"synth/{'uniform' if kind == 0 else 'tandem'}_{n}"
+                path = os.path.join(tmp, "synth.txt")
+                subprocess.run([GEN, str(kind), str(n), path], check=True)
+                manifest[key] = {"kind": "synth", "synth_kind": kind, "nbases": n, "L": 12,
+                                 "expect": run_dump("dump", path, 12, tmp, "synth")}
+                os.remove(path)
+                print(key, manifest[key]["expect"].get("ratio"), flush=True)
+            return
         for name in CORPUS:
             manifest[f"corpus/{name}"] = {"kind": "fasta", "input": f"data/{name}", "L": 12,
                                           "expect": run_dump("dump", os.path.join(DATA, name), 12, tmp, name)}
@@ -219,10 +234,10 @@ def main():
                     shutil.copyfileobj(src, dst)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    with open(manifest_path, "w") as f:
-        json.dump(manifest, f, indent=1, sort_keys=True)
-        f.write("\n")
-    print(f"wrote {len(manifest)} cases to {manifest_path}")
+        with open(manifest_path, "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+            f.write("\n")
+        print(f"wrote {len(manifest)} cases to {manifest_path}")
 
 
 if __name__ == "__main__":
