@@ -715,11 +715,16 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
   const int R = world, NL = int(ctx.size());
   if (L < 1 || L > 16) return fail(GCZ_ERR_ARG, "leaf length L must be in 1..16");
   if (S == 0) return fail(GCZ_ERR_EMPTY, "fewer than L bases: nothing to build");
-  if (S > u64(kIdx)) return fail(GCZ_ERR_CAPACITY, "more than 2^29-1 strands");
   if (R > kMaxRanks) return fail(GCZ_ERR_ARG, "at most 31 ranks");
   info.n_strands = S;
   plan.make(S, R);
   const DistPlan& P = plan;
+  // Positions are rank-local (29-bit words, like the single-device build), so the
+  // genome may exceed 2^29 strands as long as every rank's range fits; ids are global
+  // and bounded per layer (checked per exchanged layer; a direct layer has nk[k+1] ids).
+  for (int s = 0; s < R; ++s)
+    if (P.count(s, 0) > u64(kIdx)) return fail(GCZ_ERR_CAPACITY, "more than 2^29-1 strands on one rank");
+  if (P.nk.size() > 1 && P.nk[1] > u64(kIdx)) return fail(GCZ_ERR_CAPACITY, "more than 2^29-1 nodes in layer 0");
   const int G = P.G, D = P.D;
   if (D > GCZ_MAX_LAYERS) return fail(GCZ_ERR_CAPACITY, "too many layers");
   node_base.assign(NL, {});
