@@ -21,7 +21,6 @@ using namespace gcz_host;
 struct gcz_dist_state {
   DevBuf scratch, gnf, gmul, gid, blockcnt, skey, sidx, sflag, scval, sdval;   // sender side
   DevBuf rkey, oslot, rflag, rcval, rdval, owntab, oids, omin;                // owner side
-  DevBuf s_selc, s_seld, s_prec, s_pred, o_selc, o_seld, o_prec, o_pred, sdesc;  // C/D compaction
   DevBuf dhdr, gath, gath2, gathf, ddesc, tail_in;
   u64* h_gath = nullptr;    // pinned mirrors of the gathered vectors
   u64* h_gath2 = nullptr;
@@ -33,8 +32,7 @@ void gcz_dist_state_free(gcz_ctx* c) {
   if (!d) return;
   for (DevBuf* b : {&d->scratch, &d->gnf, &d->gmul, &d->gid, &d->blockcnt, &d->skey, &d->sidx, &d->sflag,
                     &d->scval, &d->sdval, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab, &d->oids,
-                    &d->omin, &d->s_selc, &d->s_seld, &d->s_prec, &d->s_pred, &d->o_selc, &d->o_seld, &d->o_prec,
-                    &d->o_pred, &d->sdesc,
+                    &d->omin,
                     &d->dhdr, &d->gath, &d->gath2, &d->gathf, &d->ddesc, &d->tail_in})
     if (b->ptr) (void)hipFree(b->ptr);
   for (u64* h : {d->h_gath, d->h_gath2, d->h_gathf})
@@ -55,6 +53,11 @@ struct Transport {
   // send[i]: local rank i's buffer, segments in destination order; recv[i]: segments in source order.
   virtual int alltoallv(const std::vector<u64>& M, bool reverse, size_t elem, const std::vector<const void*>& send,
                         const std::vector<void*>& recv) = 0;
+  // Same counts, explicit element displacements: sd[s * world + d] in rank s's send buffer,
+  // rd[d * world + s] in rank d's receive buffer.
+  virtual int alltoallv_at(const std::vector<u64>& M, bool reverse, size_t elem, const std::vector<u64>& sd,
+                           const std::vector<u64>& rd, const std::vector<const void*>& send,
+                           const std::vector<void*>& recv) = 0;
   virtual int allgather(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) = 0;
   // rank 0 receives cnt[r] elements from every rank r, concatenated in rank order
   virtual int gather0(const std::vector<u64>& cnt, size_t elem, const std::vector<const void*>& send,
@@ -92,6 +95,17 @@ struct LocalTransport : Transport {
       for (int d = 0; d < world; ++d)
         if (int rc = copy(static_cast<char*>(recv[d]) + recv_displ(M, world, rev, d, s) * elem,
                           static_cast<const char*>(send[s]) + send_displ(M, world, rev, s, d) * elem,
+                          mcount(M, world, rev, s, d) * elem))
+          return rc;
+    return GCZ_OK;
+  }
+  int alltoallv_at(const std::vector<u64>& M, bool rev, size_t elem, const std::vector<u64>& sd,
+                   const std::vector<u64>& rd, const std::vector<const void*>& send,
+                   const std::vector<void*>& recv) override {
+    for (int s = 0; s < world; ++s)
+      for (int d = 0; d < world; ++d)
+        if (int rc = copy(static_cast<char*>(recv[d]) + rd[size_t(d) * world + s] * elem,
+                          static_cast<const char*>(send[s]) + sd[size_t(s) * world + d] * elem,
                           mcount(M, world, rev, s, d) * elem))
           return rc;
     return GCZ_OK;
@@ -197,6 +211,31 @@ struct RcclTransport : Transport {
     }
     return check(a.GroupEnd(), "ncclGroupEnd");
   }
+  int alltoallv_at(const std::vector<u64>& M, bool rev, size_t elem, const std::vector<u64>& sd,
+                   const std::vector<u64>& rd, const std::vector<const void*>& send,
+                   const std::vector<void*>& recv) override {
+    const auto* sb = static_cast<const char*>(send[0]);
+    auto* rb = static_cast<char*>(recv[0]);
+    const size_t R = size_t(world);
+    if (int rc = self_copy(rb + rd[me * R + me] * elem, sb + sd[me * R + me] * elem,
+                           mcount(M, world, rev, me, me) * elem))
+      return rc;
+    RcclApi& a = rccl();
+    if (int rc = check(a.GroupStart(), "ncclGroupStart")) return rc;
+    for (int q = 0; q < world; ++q) {
+      if (q == me) continue;
+      const u64 sc = mcount(M, world, rev, me, q), rcnt = mcount(M, world, rev, q, me);
+      if (sc) {
+        const ncclResult_t r = a.Send(sb + sd[me * R + q] * elem, sc * elem, ncclUint8, q, comm, stream);
+        if (r != ncclSuccess) { (void)a.GroupEnd(); return check(r, "ncclSend"); }
+      }
+      if (rcnt) {
+        const ncclResult_t r = a.Recv(rb + rd[me * R + q] * elem, rcnt * elem, ncclUint8, q, comm, stream);
+        if (r != ncclSuccess) { (void)a.GroupEnd(); return check(r, "ncclRecv"); }
+      }
+    }
+    return check(a.GroupEnd(), "ncclGroupEnd");
+  }
   int allgather(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) override {
     return check(rccl().AllGather(send[0], recv[0], bytes, ncclUint8, comm, stream), "ncclAllGather");
   }
@@ -263,6 +302,7 @@ struct RankLevel {
   void* out = nullptr;      // rank's slice of the output layer
   bool leaves = false;
   const unsigned char* bases = nullptr;   // leaf level: for the bad-symbol report
+  bool defer_remap = false;               // the next level's k_node_keys translates the words
 };
 }  // namespace
 
@@ -282,6 +322,8 @@ struct gcz_group {
   // node levels: 0 auto (local dedupe only on repetitive data), 1 always, 2 never (GCZ_DIST_LOCAL)
   int dist_local = std::getenv("GCZ_DIST_LOCAL") ? std::atoi(std::getenv("GCZ_DIST_LOCAL")) : 0;
   bool any_predup = false;   // some rank's leaf probe found repetitive data (set by the leaf exchange)
+  bool leaf_deferred = false;   // the leaf words keep local ids until layer 0's k_node_keys
+  std::vector<u32> leaf_offs;   // ... and each local rank's leaf id offset
 
   int fail(int code, const std::string& what) {
     last_error = what;
@@ -359,15 +401,11 @@ int gcz_group::alloc(int i, u64 leaf_cap) {
   if ((rc = c->ensure(d.skey, u * 8))) return rc;
   if ((rc = c->ensure(d.sidx, u * 4))) return rc;
   if ((rc = c->ensure(d.sflag, u))) return rc;
-  if ((rc = c->ensure(d.scval, u * 4))) return rc;
-  if ((rc = c->ensure(d.sdval, u * 4))) return rc;
+  if ((rc = c->ensure(d.scval, u * 8))) return rc;
+  if ((rc = c->ensure(d.sdval, u * 8))) return rc;
   if ((rc = c->ensure(d.dhdr, sizeof(DistHdr)))) return rc;
   if ((rc = c->ensure(d.gath, size_t(world) * kSyncWords * 8))) return rc;
   if ((rc = c->ensure(d.gath2, size_t(world) * (1 + 2 * kMaxRanks) * 8))) return rc;
-  if ((rc = c->ensure(d.s_selc, u))) return rc;
-  if ((rc = c->ensure(d.s_seld, u))) return rc;
-  if ((rc = c->ensure(d.s_prec, u * 4))) return rc;
-  if ((rc = c->ensure(d.s_pred, u * 4))) return rc;
   if ((rc = c->ensure(d.gathf, size_t(world) * kFinalWords * 8))) return rc;
   if ((rc = c->ensure(d.ddesc, ((u + kTile - 1) / kTile) * 8 + 64))) return rc;
   if ((rc = c->ensure(d.tail_in, nG * 4 + 16))) return rc;
@@ -457,6 +495,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     return D;
   };
   std::vector<OwnTab> otab(NL);
+  std::vector<LevelTab> opos(NL);
 
   auto send_displ_of = [&](int r) {   // destination segments of rank r's send buffer
     Displ D{};
@@ -466,16 +505,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     return D;
   };
   auto tiles_of = [](u64 n) { return (n + kTile - 1) / kTile; };
-  // selected-record scans: sender C, sender D, owner C, owner D (descriptor regions of sdesc)
-  auto sel_scan = [&](gcz_ctx* cx, int which, const unsigned char* sel, u64 n, u32* pre, u64 region) -> int {
-    gcz_dist_state& d = *cx->dist;
-    DistHdr* dh = d.dhdr.as<DistHdr>();
-    if (n == 0) return GCZ_OK;   // tot[which] stays 0
-    hipLaunchKernelGGL(k_sel_scan, dim3(unsigned(tiles_of(n))), dim3(kBlock), 0, cx->stream, sel, n, pre,
-                       d.sdesc.as<u64>() + region * which, &dh->tick[which], &dh->tot[which]);
-    return hipGetLastError() == hipSuccess ? GCZ_OK : GCZ_ERR_DEVICE;
-  };
-  std::vector<u64> region(NL, 0);
+  auto tiles = [&](u64 n) { return dim3(unsigned(std::max<u64>(1, tiles_of(n)))); };
 
   // 2. owners decide first rank, repetition and sharing (A, B)
   if (records) {
@@ -484,22 +514,28 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     for (int i = 0; i < NL; ++i) {
       gcz_ctx* cx = ctx[i];
       gcz_dist_state& d = *cx->dist;
-      const u64 nr = recvd(rank[i]), ns = sent(rank[i]);
+      const u64 nr = recvd(rank[i]);
       int rc;
       if ((rc = cx->ensure(d.rkey, nr * 8 + 16)) || (rc = cx->ensure(d.oslot, nr * 4 + 16)) ||
-          (rc = cx->ensure(d.rflag, nr + 16)) || (rc = cx->ensure(d.rcval, nr * 4 + 16)) ||
-          (rc = cx->ensure(d.rdval, nr * 4 + 16)) || (rc = cx->ensure(d.o_selc, nr + 16)) ||
-          (rc = cx->ensure(d.o_seld, nr + 16)) || (rc = cx->ensure(d.o_prec, nr * 4 + 16)) ||
-          (rc = cx->ensure(d.o_pred, nr * 4 + 16)))
+          (rc = cx->ensure(d.rflag, nr + 16)) || (rc = cx->ensure(d.rcval, nr * 8 + 16)) ||
+          (rc = cx->ensure(d.rdval, nr * 8 + 16)))
         return dev_fail("exchange buffers");
-      region[i] = tiles_of(std::max(nr, ns)) + 1;
-      if ((rc = cx->ensure(d.sdesc, 4 * region[i] * 8))) return dev_fail("scan descriptors");
-      G_HIP(hipMemsetAsync(d.sdesc.ptr, 0, 4 * region[i] * 8, cx->stream));
       const u64 cap = std::max<u64>(256, next_pow2(2 * nr));
-      const bool packed = key_bits + u32(R) + 2 <= 64 && !cx->force_wide;
+      // nolocal: the records in receive order are the level's occurrences in position order,
+      // so the owner hash-conses them like a single-device level (position-packed table, the
+      // receive index as position, not-first / multi marks): one CAS per new key, no reply pass
+      opos[i] = nolocal ? plan_table(d.owntab.ptr, cap, key_bits, std::max<u64>(nr, 2), child_bits,
+                                     cx->allow_packed && !cx->force_wide, 0)
+                        : LevelTab{};
+      const bool packed = opos[i].packed || (key_bits + u32(R) + 2 <= 64 && !cx->force_wide);
       if ((rc = cx->ensure(d.owntab, cap * (packed ? 8 : 16)))) return dev_fail("owner table");
+      opos[i].pt.tab = d.owntab.as<u64>();   // (re)allocated above
       if (packed && (rc = cx->ensure(d.oids, cap * 4))) return dev_fail("owner ids");
-      if (nolocal && (rc = cx->ensure(d.omin, cap * 4))) return dev_fail("owner first index");
+      if (opos[i].packed) {
+        if ((rc = cx->ensure(d.omin, 2 * nr + 64))) return dev_fail("owner marks");
+      } else if (nolocal && (rc = cx->ensure(d.omin, cap * 4))) {
+        return dev_fail("owner first index");
+      }
       otab[i] = OwnTab{};
       otab[i].tab = d.owntab.as<Slot>();
       otab[i].ptab = d.owntab.as<u64>();
@@ -528,21 +564,27 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       const u64 nr = recvd(rank[i]);
       ProfScope ps_(cx, KID_OWNER);
       G_HIP(hipMemsetAsync(d.owntab.ptr, 0xff, size_t(otab[i].mask + 1) * (otab[i].packed ? 8 : 16), cx->stream));
-      if (nolocal) G_HIP(hipMemsetAsync(d.omin.ptr, 0xff, size_t(otab[i].mask + 1) * 4, cx->stream));
       const Displ D = displ_of(rank[i]);
-      hipLaunchKernelGGL(k_own_insert, blocks(nr), dim3(kBlock), 0, cx->stream, d.rkey.as<u64>(), nr, D, u32(R),
-                         int(lv[i].leaves), otab[i], d.oslot.as<u32>(), &d.dhdr.as<DistHdr>()->final_vec[3]);
-      hipLaunchKernelGGL(k_own_reply, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr, D, u32(R),
-                         otab[i], d.rflag.as<unsigned char>());
-      if (nolocal)
-        hipLaunchKernelGGL(k_own_first, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr, otab[i],
+      if (opos[i].packed) {
+        unsigned char* onf = d.omin.as<unsigned char>();
+        unsigned char* omul = onf + nr + 32;
+        G_HIP(hipMemsetAsync(onf, 0, 2 * nr + 64, cx->stream));
+        hipLaunchKernelGGL(k_own_insert_pos, blocks(nr), dim3(kBlock), 0, cx->stream, d.rkey.as<u64>(), nr,
+                           child_bits, opos[i].pt, Marks{onf, omul}, d.oslot.as<u32>(),
+                           &cx->hdr.as<Header>()->overflow);
+        hipLaunchKernelGGL(k_own_reply_marks, blocks(nr), dim3(kBlock), 0, cx->stream, onf, omul, nr,
                            d.rflag.as<unsigned char>());
-      // the owner's view of the C / D compactions (same records, same order as the senders')
-      hipLaunchKernelGGL(k_sel, blocks(nr), dim3(kBlock), 0, cx->stream, d.rflag.as<unsigned char>(), nr,
-                         d.o_selc.as<unsigned char>(), d.o_seld.as<unsigned char>());
+      } else {
+        if (nolocal) G_HIP(hipMemsetAsync(d.omin.ptr, 0xff, size_t(otab[i].mask + 1) * 4, cx->stream));
+        hipLaunchKernelGGL(k_own_insert, blocks(nr), dim3(kBlock), 0, cx->stream, d.rkey.as<u64>(), nr, D, u32(R),
+                           int(lv[i].leaves), otab[i], d.oslot.as<u32>(), &d.dhdr.as<DistHdr>()->final_vec[3]);
+        hipLaunchKernelGGL(k_own_reply, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr, D, u32(R),
+                           otab[i], d.rflag.as<unsigned char>());
+        if (nolocal)
+          hipLaunchKernelGGL(k_own_first, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr, otab[i],
+                             d.rflag.as<unsigned char>());
+      }
       G_HIP(hipGetLastError());
-      if (sel_scan(cx, 2, d.o_selc.as<unsigned char>(), nr, d.o_prec.as<u32>(), region[i])) return dev_fail("scan");
-      if (sel_scan(cx, 3, d.o_seld.as<unsigned char>(), nr, d.o_pred.as<u32>(), region[i])) return dev_fail("scan");
       s.push_back(d.rflag.ptr);
       rv.push_back(d.sflag.ptr);
     }
@@ -553,7 +595,8 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       ctx[0]->prof_end(KID_EXCHANGE, e0);
     }
   }
-  // 3. globally-first ranks in local order; C / D record counts per owner
+  // 3. globally-first ranks in local order (straight into the rank's output slice);
+  //    C / D record counts per owner
   for (int i = 0; i < NL; ++i) {
     gcz_ctx* cx = ctx[i];
     gcz_dist_state& d = *cx->dist;
@@ -564,22 +607,21 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     G_HIP(hipMemsetAsync(d.gmul.ptr, 0, ur + 1, cx->stream));
     if (records) {
       const u64 ns = sent(rank[i]);
-      hipLaunchKernelGGL(k_dist_flags, blocks(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
+      hipLaunchKernelGGL(k_dist_flags, tiles(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
                          d.sflag.as<unsigned char>(), d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(),
-                         d.s_selc.as<unsigned char>(), d.s_seld.as<unsigned char>());
+                         send_displ_of(rank[i]), u32(R), &dh->sync2[1]);
       G_HIP(hipGetLastError());
-      if (sel_scan(cx, 0, d.s_selc.as<unsigned char>(), ns, d.s_prec.as<u32>(), region[i])) return dev_fail("scan");
-      if (sel_scan(cx, 1, d.s_seld.as<unsigned char>(), ns, d.s_pred.as<u32>(), region[i])) return dev_fail("scan");
-      const Displ SD = send_displ_of(rank[i]);
-      hipLaunchKernelGGL(k_seg_counts, dim3(1), dim3(64), 0, cx->stream, d.s_prec.as<u32>(), &dh->tot[0], ns, SD,
-                         u32(R), &dh->sync2[1]);
-      hipLaunchKernelGGL(k_seg_counts, dim3(1), dim3(64), 0, cx->stream, d.s_pred.as<u32>(), &dh->tot[1], ns, SD,
-                         u32(R), &dh->sync2[1 + R]);
     }
     const u64 tiles = std::max<u64>(1, tiles_of(ur));
     G_HIP(hipMemsetAsync(d.ddesc.ptr, 0, tiles * 8, cx->stream));
-    hipLaunchKernelGGL(k_dist_rank, dim3(unsigned(tiles)), dim3(kBlock), 0, cx->stream, d.gnf.as<unsigned char>(),
-                       lv[i].ucount, d.gid.as<u32>(), d.ddesc.as<u64>(), &dh->ticket, &dh->sync2[0]);
+    if (lv[i].leaves)
+      hipLaunchKernelGGL((k_dist_rank<u64>), dim3(unsigned(tiles)), dim3(kBlock), 0, cx->stream,
+                         d.gnf.as<unsigned char>(), lv[i].ucount, d.gid.as<u32>(), d.ddesc.as<u64>(), &dh->ticket,
+                         &dh->sync2[0], d.scratch.as<u64>(), static_cast<u64*>(lv[i].out));
+    else
+      hipLaunchKernelGGL((k_dist_rank<uint2>), dim3(unsigned(tiles)), dim3(kBlock), 0, cx->stream,
+                         d.gnf.as<unsigned char>(), lv[i].ucount, d.gid.as<u32>(), d.ddesc.as<u64>(), &dh->ticket,
+                         &dh->sync2[0], d.scratch.as<uint2>(), static_cast<uint2*>(lv[i].out));
     G_HIP(hipGetLastError());
   }
   c.assign(R, 0);
@@ -618,22 +660,19 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
   for (int s2 = 0; s2 < R; ++s2) off[s2 + 1] = off[s2] + c[s2];
   total = off[R];
   if (total > u64(kIdx)) return fail(GCZ_ERR_CAPACITY, "more than 2^29-1 uniques in one layer");
-  // 4. compact globally-first uniques into the slice; ids of shared keys (C, D)
-  for (int i = 0; i < NL; ++i) {
-    gcz_ctx* cx = ctx[i];
-    gcz_dist_state& d = *cx->dist;
-    const u64 ur = u[rank[i]];
-    ProfScope ps_(cx, KID_IDS);
-    if (lv[i].leaves)
-      hipLaunchKernelGGL((k_dist_finalize<u64>), blocks(ur), dim3(kBlock), 0, cx->stream, lv[i].ucount,
-                         d.gnf.as<unsigned char>(), d.gid.as<u32>(), u32(off[rank[i]]), d.scratch.as<u64>(),
-                         static_cast<u64*>(lv[i].out));
-    else
-      hipLaunchKernelGGL((k_dist_finalize<uint2>), blocks(ur), dim3(kBlock), 0, cx->stream, lv[i].ucount,
-                         d.gnf.as<unsigned char>(), d.gid.as<u32>(), u32(off[rank[i]]), d.scratch.as<uint2>(),
-                         static_cast<uint2*>(lv[i].out));
-    G_HIP(hipGetLastError());
-  }
+  // 4. ids of keys held by several ranks or occurrences: C (first holder -> owner), D (owner ->
+  //    the others), as (segment index, id) pairs placed at the A layout's segment starts
+  std::vector<u64> SA(size_t(R) * R), RA(size_t(R) * R);
+  for (int s2 = 0; s2 < R; ++s2)
+    for (int q = 0; q < R; ++q) {
+      SA[size_t(s2) * R + q] = send_displ(M, R, false, s2, q);
+      RA[size_t(q) * R + s2] = recv_displ(M, R, false, q, s2);
+    }
+  auto counts_from = [&](const std::vector<u64>& X, int r, bool as_dest) {   // per peer, as a Displ
+    Displ C{};
+    for (int q = 0; q < R; ++q) C.d[q] = as_dest ? X[size_t(q) * R + r] : X[size_t(r) * R + q];
+    return C;
+  };
   if (nc) {
     std::vector<const void*> s;
     std::vector<void*> rv;
@@ -642,8 +681,9 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       gcz_dist_state& d = *cx->dist;
       const u64 ns = sent(rank[i]);
       ProfScope ps_(cx, KID_IDS);
-      hipLaunchKernelGGL(k_dist_cvals, blocks(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
-                         d.sflag.as<unsigned char>(), d.s_prec.as<u32>(), d.gid.as<u32>(), d.scval.as<u32>());
+      hipLaunchKernelGGL(k_dist_cvals, tiles(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
+                         send_displ_of(rank[i]), u32(R), d.sflag.as<unsigned char>(), d.gid.as<u32>(),
+                         u32(off[rank[i]]), d.dhdr.as<DistHdr>()->ccur, d.scval.as<u64>());
       G_HIP(hipGetLastError());
       s.push_back(d.scval.ptr);
       rv.push_back(d.rcval.ptr);
@@ -651,7 +691,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     {
       hipEvent_t e0{};
       ctx[0]->prof_begin(KID_EXCHANGE, e0);
-      G_RC(tr->alltoallv(MC, false, 4, s, rv));
+      G_RC(tr->alltoallv_at(MC, false, 8, SA, RA, s, rv));
       ctx[0]->prof_end(KID_EXCHANGE, e0);
     }
     for (int i = 0; i < NL; ++i) {
@@ -659,8 +699,8 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       gcz_dist_state& d = *cx->dist;
       const u64 nr = recvd(rank[i]);
       ProfScope ps_(cx, KID_OWNER);
-      hipLaunchKernelGGL(k_own_setid, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr,
-                         d.rflag.as<unsigned char>(), d.o_prec.as<u32>(), d.rcval.as<u32>(), otab[i]);
+      hipLaunchKernelGGL(k_own_setid, blocks(nr), dim3(kBlock), 0, cx->stream, d.rcval.as<u64>(), nr,
+                         displ_of(rank[i]), counts_from(MC, rank[i], true), u32(R), d.oslot.as<u32>(), otab[i]);
       G_HIP(hipGetLastError());
     }
   }
@@ -672,8 +712,9 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       gcz_dist_state& d = *cx->dist;
       const u64 nr = recvd(rank[i]);
       ProfScope ps_(cx, KID_OWNER);
-      hipLaunchKernelGGL(k_own_getid, blocks(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr,
-                         d.rflag.as<unsigned char>(), d.o_pred.as<u32>(), otab[i], d.rdval.as<u32>());
+      hipLaunchKernelGGL(k_own_getid, tiles(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr,
+                         displ_of(rank[i]), u32(R), d.rflag.as<unsigned char>(), otab[i],
+                         d.dhdr.as<DistHdr>()->dcur, d.rdval.as<u64>());
       G_HIP(hipGetLastError());
       s.push_back(d.rdval.ptr);
       rv.push_back(d.sdval.ptr);
@@ -681,7 +722,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     {
       hipEvent_t e0{};
       ctx[0]->prof_begin(KID_EXCHANGE, e0);
-      G_RC(tr->alltoallv(MD, true, 4, s, rv));
+      G_RC(tr->alltoallv_at(MD, true, 8, RA, SA, s, rv));
       ctx[0]->prof_end(KID_EXCHANGE, e0);
     }
     for (int i = 0; i < NL; ++i) {
@@ -690,18 +731,22 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       const u64 ns = sent(rank[i]);
       ProfScope ps_(cx, KID_IDS);
       hipLaunchKernelGGL(k_dist_dvals, blocks(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
-                         d.sflag.as<unsigned char>(), d.s_pred.as<u32>(), d.sdval.as<u32>(), d.gid.as<u32>());
+                         send_displ_of(rank[i]), counts_from(MD, rank[i], false), u32(R), d.sdval.as<u64>(),
+                         d.gid.as<u32>());
       G_HIP(hipGetLastError());
     }
   }
   // 5. local words -> global ids
+  leaf_deferred = lv[0].leaves && lv[0].defer_remap && (dist_local == 2 || (dist_local == 0 && !any_predup)) &&
+                  total != plan.nk[0];
   for (int i = 0; i < NL; ++i) {
+    if (leaf_deferred) continue;
     gcz_ctx* cx = ctx[i];
     gcz_dist_state& d = *cx->dist;
     const u64 nw = nwords[i];
     ProfScope ps_(cx, KID_REMAP);
     hipLaunchKernelGGL(k_dist_remap, blocks(nw), dim3(kBlock), 0, cx->stream, lv[i].w, nw, lv[i].nf, lv[i].multi,
-                       d.gid.as<u32>(), d.gmul.as<unsigned char>());
+                       d.gid.as<u32>(), d.gmul.as<unsigned char>(), u32(off[rank[i]]));
     G_HIP(hipGetLastError());
   }
   return GCZ_OK;
@@ -812,6 +857,10 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     std::vector<u64> c, off;
     u64 total = 0, err_global = 0;
     int err_sym = 0, ovf = 0;
+    // Without the local dedupe the leaf words are translated by layer 0's k_node_keys (one
+    // pass instead of two), unless layer 0 turns out direct or is not distributed (exchange
+    // decides once the leaf totals are known: leaf_deferred).
+    for (int i = 0; i < NL; ++i) lv[i].defer_remap = G > 0;
     {
       std::vector<u64> nw(NL);
       for (int i = 0; i < NL; ++i) nw[i] = P.count(rank[i], 0);
@@ -836,6 +885,8 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     slice_off.assign(D + 1, std::vector<u64>(R, 0));
     slice_cnt.assign(D + 1, std::vector<u64>(R, 0));
     for (int s = 0; s < R; ++s) { slice_off[0][s] = off[s]; slice_cnt[0][s] = c[s]; }
+    leaf_offs.assign(NL, 0);
+    for (int i = 0; i < NL; ++i) leaf_offs[i] = u32(off[rank[i]]);
     info.n_leaves = total;
     for (int i = 0; i < NL; ++i) ctx[i]->leaf_cap_hint = next_pow2(std::max<u64>(1, 2 * total));
 
@@ -901,9 +952,11 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         if (nolocal && !direct) {
           const int cs = (k + 1) & 1;
           ProfScope ps_(cx, KID_NODE);
+          const bool tr = k == 0 && leaf_deferred;
           hipLaunchKernelGGL(k_node_keys, dim3(unsigned(std::max<u64>(1, (p + kBlock - 1) / kBlock))), dim3(kBlock), 0,
                              cx->stream, cur_in[i], n, p, cur_out[i], cx->dist->scratch.as<uint2>(), cx->nf_set[cs],
-                             cx->multi_set[cs], na.count);
+                             cx->multi_set[cs], na.count, tr ? cx->dist->gid.as<u32>() : nullptr,
+                             tr ? leaf_offs[i] : 0u);
           G_HIP(hipGetLastError());
         } else if (cx->node_level(na, h)) {
           return dev_fail("node level");
@@ -919,6 +972,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         rl.src.multi = cx->multi_set[cs];
         rl.src.prev_nf = k > 0 ? cx->nf_set[ps] : nullptr;
         rl.src.prev_multi = k > 0 ? cx->multi_set[ps] : nullptr;
+        rl.src.canon = nolocal && !direct ? cx->dist->scratch.as<uint2>() : nullptr;
         rl.grid_elems = p;
         rl.ucount = &h->count[kLayerSlot + k];
         rl.w = cur_out[i];

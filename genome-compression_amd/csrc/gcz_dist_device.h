@@ -43,6 +43,8 @@ struct DistHdr {
   u32 ticket;                           // look-back tickets of k_dist_rank
   u32 tick[4];                          // ... of the compaction scans
   u32 pad[3];
+  u32 ccur[kMaxRanks + 1];              // append cursors: C records per owner (sender side)
+  u32 dcur[kMaxRanks + 1];              // ... D records per source (owner side)
   u64 cell[GCZ_MAX_LAYERS + 1];         // direct flags: n_local when the layer is direct, else ~0
   u64 final_vec[kFinalWords];           // [0] overflow, [1] root, [2] tail first layer, [4 + k] tail counts
 };
@@ -80,6 +82,7 @@ struct RecSrc {
   const unsigned char* multi;
   const unsigned char* prev_nf;        // null: every locally-first pair sends
   const unsigned char* prev_multi;
+  const uint2* canon;                  // levels without the local dedupe: canonical pairs (k_node_keys)
   u32 R;
 };
 
@@ -102,9 +105,16 @@ __device__ __forceinline__ bool rec_get(const RecSrc& s, u64 e, u64& key, u32& l
     }
     if (single) return false;
   }
-  u32 l, r, cl, cr, m, t;
-  load_pair(s.in, s.n, e, l, r);
-  node_canonical(l, r, cl, cr, m, t);
+  u32 cl, cr;
+  if (s.canon) {
+    const uint2 c = s.canon[e];
+    cl = c.x;
+    cr = c.y;
+  } else {
+    u32 l, r, m, t;
+    load_pair(s.in, s.n, e, l, r);
+    node_canonical(l, r, cl, cr, m, t);
+  }
   key = ((u64(ulw(cl)) << 31) | ulw(cr)) | (s.multi[e] ? kLocalMulti : 0ull);
   lid = s.words[e] & kIdx;
   return true;
@@ -345,93 +355,162 @@ static __global__ __launch_bounds__(kBlock) void k_own_first(const u32* __restri
   if (f & 0x80) rflag[k] = (unsigned char)((f & 6) | (T.omin[oslot[k]] != u32(k) ? 1 : 0));
 }
 
+// A level without the local dedupe (OwnTab::nolocal) through a position-packed table:
+// every source sends its records in position order and the sources arrive in rank
+// (= position) order, so the receive index orders a key's occurrences like their genome
+// positions.  The owner hash-conses the records exactly like a single-device level
+// (PackedTab::insert: one CAS per new key, atomicMin + marks only for repeats); the
+// reply then comes from the marks, streaming.
+static __global__ __launch_bounds__(kBlock) void k_own_insert_pos(const u64* __restrict__ rkey, u64 nrecv, u32 B,
+                                                                  PackedTab T, Marks mk, u32* __restrict__ oslot,
+                                                                  u32* __restrict__ ovf) {
+  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= nrecv) return;
+  oslot[k] = T.insert(own_pack_key(rkey[k] & ~kLocalMulti, 0, B), u32(k), mk, ovf);
+}
+
+// Reply from the marks: not first (1), repeats (2), and C / D whenever the key repeats (4),
+// like k_own_reply + k_own_first.
+static __global__ __launch_bounds__(kBlock) void k_own_reply_marks(const unsigned char* __restrict__ nf,
+                                                                   const unsigned char* __restrict__ multi,
+                                                                   u64 nrecv, unsigned char* __restrict__ rflag) {
+  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= nrecv) return;
+  rflag[k] = nf[k] ? 7 : (multi[k] ? 6 : 0);
+}
+
 // Per-record flags (reply bits): 1 not globally first, 2 repeats globally, 4 held by >= 2 ranks.
 // C: the first holder of a shared key sends its id; D: every other holder receives it.
 __device__ __forceinline__ bool want_c(unsigned char f) { return (f & 1) == 0 && (f & 4); }
 __device__ __forceinline__ bool want_d(unsigned char f) { return (f & 1) != 0; }
 
-// Selection bytes for the C and D compactions (0 = selected: the tile scan's convention).
-static __global__ __launch_bounds__(kBlock) void k_sel(const unsigned char* __restrict__ flag, u64 n,
-                                                       unsigned char* __restrict__ selc,
-                                                       unsigned char* __restrict__ seld) {
-  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (k >= n) return;
-  const unsigned char f = flag[k];
-  selc[k] = want_c(f) ? 0 : 1;
-  seld[k] = want_d(f) ? 0 : 1;
+// C and D records travel as (index within the sender->owner segment, id) pairs, so
+// neither side needs them in order: they are appended per segment with wave-aggregated
+// cursors into the segment's span of the record layout (at most every record of a
+// segment is selected) and sent from there (Transport::alltoallv_at).
+__device__ __forceinline__ u32 wave_append(u32* __restrict__ cur, u32 q, bool want) {
+  const int lane = threadIdx.x & 63;
+  const u64 lt = (1ull << lane) - 1;
+  u32 slot = 0;
+  u64 left = __ballot(want);
+  while (left) {                                   // one atomic per distinct segment in the wave
+    const int leader = __ffsll((long long)left) - 1;
+    const u32 ql = __shfl(q, leader, 64);
+    const u64 m = __ballot(want && q == ql);
+    u32 base = 0;
+    if (lane == leader) base = atomicAdd(&cur[ql], u32(__popcll(m)));
+    base = __shfl(base, leader, 64);
+    if (want && q == ql) slot = base + u32(__popcll(m & lt));
+    left &= ~m;
+  }
+  return slot;
 }
 
-// pre[k] = selected records before k (records keep their order, so the
-// compacted buffer keeps the per-rank segments in order); total -> *total.
-static __global__ __launch_bounds__(kBlock) void k_sel_scan(const unsigned char* __restrict__ sel, u64 n,
-                                                            u32* __restrict__ pre, u64* __restrict__ desc,
-                                                            u32* __restrict__ ticket, u64* __restrict__ total) {
-  __shared__ u32 s_tile;
-  __shared__ u32 s_pre[kGroupsPerTile];
-  TileScan<kItems> ts;
-  tile_scan(ts, &s_tile, s_pre, sel, 0, n, 0, desc, ticket, total);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const u64 lt = (1ull << lane) - 1;
-#pragma unroll
+// C at the owner: the first holder's global id of every shared key.  cnt.d[s] = C records
+// from source s, packed at the start of s's segment.
+static __global__ __launch_bounds__(kBlock) void k_own_setid(const u64* __restrict__ rc, u64 nrecv, Displ D,
+                                                             Displ cnt, u32 R, const u32* __restrict__ oslot,
+                                                             OwnTab T) {
+  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= nrecv) return;
+  const u32 s = seg_of(D, R, k);
+  if (k - D.d[s] >= cnt.d[s]) return;
+  const u64 v = rc[k];
+  own_set_id(T, oslot[D.d[s] + u32(v)], u32(v >> 32));
+}
+
+// Per-segment append over a tile of kTile records: pass 1 counts the selected records per
+// segment (wave ballots into LDS), one global atomic per segment reserves the block's
+// span, pass 2 recomputes the selection and writes.  `sel(k, q)` -> selected, segment q.
+template <class Sel, class Put>
+__device__ __forceinline__ void tile_append(u64 n, u32 R, u32* __restrict__ gcur, Sel sel, Put put) {
+  __shared__ u32 cnt[kMaxRanks], base[kMaxRanks];
+  const int tid = threadIdx.x;
+  if (tid < int(R)) cnt[tid] = 0;
+  __syncthreads();
+  const u64 k0 = u64(blockIdx.x) * kTile;
   for (int e = 0; e < kItems; ++e) {
-    const u64 j = ts.base + u64(e) * kBlock + tid;
-    if (j < n) pre[j] = s_pre[e * 4 + wave] + u32(__popcll(ts.mask[e] & lt));
+    const u64 k = k0 + u64(e) * kBlock + tid;
+    u32 q = 0;
+    const bool want = k < n && sel(k, q);
+    (void)wave_append(cnt, q, want);
+  }
+  __syncthreads();
+  if (tid < int(R)) {
+    base[tid] = cnt[tid] ? atomicAdd(&gcur[tid], cnt[tid]) : 0u;
+    cnt[tid] = 0;
+  }
+  __syncthreads();
+  for (int e = 0; e < kItems; ++e) {
+    const u64 k = k0 + u64(e) * kBlock + tid;
+    u32 q = 0;
+    const bool want = k < n && sel(k, q);
+    const u32 slot = wave_append(cnt, q, want);
+    if (want) put(k, q, base[q] + slot);
   }
 }
 
-// Selected records per segment [D.d[q], D.d[q+1]).
-static __global__ void k_seg_counts(const u32* __restrict__ pre, const u64* __restrict__ total, u64 n, Displ D,
-                                    u32 R, u64* __restrict__ out) {
-  const u32 q = threadIdx.x;
-  if (q >= R) return;
-  const u64 a = D.d[q], b = D.d[q + 1];
-  const u64 pa = a < n ? pre[a] : *total, pb = b < n ? pre[b] : *total;
-  out[q] = pb - pa;
-}
-
-static __global__ __launch_bounds__(kBlock) void k_own_setid(const u32* __restrict__ oslot, u64 nrecv,
-                                                             const unsigned char* __restrict__ rflag,
-                                                             const u32* __restrict__ prec,
-                                                             const u32* __restrict__ cval, OwnTab T) {
-  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (k >= nrecv || !want_c(rflag[k])) return;
-  own_set_id(T, oslot[k], cval[prec[k]]);
-}
-
-static __global__ __launch_bounds__(kBlock) void k_own_getid(const u32* __restrict__ oslot, u64 nrecv,
-                                                             const unsigned char* __restrict__ rflag,
-                                                             const u32* __restrict__ pred, OwnTab T,
-                                                             u32* __restrict__ dval) {
-  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (k >= nrecv || !want_d(rflag[k])) return;
-  dval[pred[k]] = own_id(T, oslot[k]);
+// D at the owner: every other holder's record gets the id back (appended per source).
+static __global__ __launch_bounds__(kBlock) void k_own_getid(const u32* __restrict__ oslot, u64 nrecv, Displ D,
+                                                             u32 R, const unsigned char* __restrict__ rflag,
+                                                             OwnTab T, u32* __restrict__ dcur,
+                                                             u64* __restrict__ dval) {
+  tile_append(
+      nrecv, R, dcur,
+      [&](u64 k, u32& s) {
+        if (!want_d(rflag[k])) return false;
+        s = seg_of(D, R, k);
+        return true;
+      },
+      [&](u64 k, u32 s, u32 slot) { dval[D.d[s] + slot] = u64(k - D.d[s]) | (u64(own_id(T, oslot[k])) << 32); });
 }
 
 // ---- sender side ---------------------------------------------------------------
 
 // Reply flags -> per local unique (gnf: not globally first, gmul: repeats globally), and
-// the selection bytes of the C / D compactions (see k_sel).
+// the C / D record counts per owner (cnt[q], cnt[R + q]: the sync2 vector).  One tile of
+// kTile records per block.
 static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restrict__ sidx, u64 nsent,
                                                               const unsigned char* __restrict__ sflag,
                                                               unsigned char* __restrict__ gnf,
-                                                              unsigned char* __restrict__ gmul,
-                                                              unsigned char* __restrict__ selc,
-                                                              unsigned char* __restrict__ seld) {
-  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (k >= nsent) return;
-  const u32 lid = sidx[k];
-  const unsigned char f = sflag[k];
-  gnf[lid] = f & 1;
-  gmul[lid] = (f >> 1) & 1;
-  selc[k] = want_c(f) ? 0 : 1;
-  seld[k] = want_d(f) ? 0 : 1;
+                                                              unsigned char* __restrict__ gmul, Displ SD, u32 R,
+                                                              u64* __restrict__ cnt) {
+  __shared__ u32 hc[kMaxRanks], hd[kMaxRanks];
+  const int tid = threadIdx.x;
+  if (tid < int(R)) { hc[tid] = 0; hd[tid] = 0; }
+  __syncthreads();
+  const u64 k0 = u64(blockIdx.x) * kTile;
+  for (int e = 0; e < kItems; ++e) {
+    const u64 k = k0 + u64(e) * kBlock + tid;
+    unsigned char f = 0;
+    if (k < nsent) {
+      const u32 lid = sidx[k];
+      f = sflag[k];
+      gnf[lid] = f & 1;
+      gmul[lid] = (f >> 1) & 1;
+    }
+    const u32 q = (want_c(f) || want_d(f)) ? seg_of(SD, R, k) : 0u;
+    (void)wave_append(hc, q, k < nsent && want_c(f));
+    (void)wave_append(hd, q, k < nsent && want_d(f));
+  }
+  __syncthreads();
+  if (tid < int(R)) {
+    if (hc[tid]) atomicAdd(reinterpret_cast<unsigned long long*>(&cnt[tid]), (unsigned long long)hc[tid]);
+    if (hd[tid]) atomicAdd(reinterpret_cast<unsigned long long*>(&cnt[R + tid]), (unsigned long long)hd[tid]);
+  }
 }
 
 // Rank of each globally-first local unique among them (local order); total -> *count_out.
-static __global__ __launch_bounds__(kBlock) void k_dist_rank(const unsigned char* __restrict__ gnf,
-                                                             const u64* __restrict__ ucount,
-                                                             u32* __restrict__ gid, u64* __restrict__ desc,
-                                                             u32* __restrict__ ticket, u64* __restrict__ count_out) {
+// Such a unique goes straight to its place in the rank's output slice; gid keeps its local
+// rank tagged kLocalId (the global offset is known only after the count allgather and is
+// added where the id is used: k_dist_cvals, k_dist_remap).
+constexpr u32 kLocalId = 1u << 31;
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_dist_rank(const unsigned char* __restrict__ gnf,
+                                                      const u64* __restrict__ ucount, u32* __restrict__ gid,
+                                                      u64* __restrict__ desc, u32* __restrict__ ticket,
+                                                      u64* __restrict__ count_out, const T* __restrict__ scratch,
+                                                      T* __restrict__ out) {
   __shared__ u32 s_tile;
   __shared__ u32 s_pre[kGroupsPerTile];
   const u64 u = *ucount;
@@ -445,39 +524,41 @@ static __global__ __launch_bounds__(kBlock) void k_dist_rank(const unsigned char
 #pragma unroll
   for (int e = 0; e < kItems; ++e) {
     const u64 j = ts.base + u64(e) * kBlock + tid;
-    if (j < u && ((ts.mask[e] >> lane) & 1ull)) gid[j] = s_pre[e * 4 + wave] + u32(__popcll(ts.mask[e] & lt));
+    if (j < u && ((ts.mask[e] >> lane) & 1ull)) {
+      const u32 r = s_pre[e * 4 + wave] + u32(__popcll(ts.mask[e] & lt));
+      gid[j] = r | kLocalId;
+      out[r] = scratch[j];
+    }
   }
 }
 
-// Globally-first uniques: compact into the rank's output slice, globalise their ids.
-template <class T>
-__global__ __launch_bounds__(kBlock) void k_dist_finalize(const u64* __restrict__ ucount,
-                                                          const unsigned char* __restrict__ gnf,
-                                                          u32* __restrict__ gid, u32 off,
-                                                          const T* __restrict__ scratch, T* __restrict__ out) {
-  const u64 lid = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (lid >= *ucount || gnf[lid]) return;
-  const u32 r = gid[lid];
-  out[r] = scratch[lid];
-  gid[lid] = off + r;
+// C at the sender: the first holder of a shared key sends (segment index, global id).
+static __global__ __launch_bounds__(kBlock) void k_dist_cvals(const u32* __restrict__ sidx, u64 nsent, Displ SD,
+                                                              u32 R, const unsigned char* __restrict__ sflag,
+                                                              const u32* __restrict__ gid, u32 off,
+                                                              u32* __restrict__ ccur, u64* __restrict__ cval) {
+  tile_append(
+      nsent, R, ccur,
+      [&](u64 k, u32& q) {
+        if (!want_c(sflag[k])) return false;
+        q = seg_of(SD, R, k);
+        return true;
+      },
+      [&](u64 k, u32 q, u32 slot) {
+        cval[SD.d[q] + slot] = u64(k - SD.d[q]) | (u64(off + (gid[sidx[k]] & ~kLocalId)) << 32);
+      });
 }
 
-static __global__ __launch_bounds__(kBlock) void k_dist_cvals(const u32* __restrict__ sidx, u64 nsent,
-                                                              const unsigned char* __restrict__ sflag,
-                                                              const u32* __restrict__ prec,
-                                                              const u32* __restrict__ gid, u32* __restrict__ cval) {
+// D at the sender: cnt.d[q] records from owner q, packed at the start of q's segment.
+static __global__ __launch_bounds__(kBlock) void k_dist_dvals(const u32* __restrict__ sidx, u64 nsent, Displ SD,
+                                                              Displ cnt, u32 R, const u64* __restrict__ dval,
+                                                              u32* __restrict__ gid) {
   const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (k >= nsent || !want_c(sflag[k])) return;
-  cval[prec[k]] = gid[sidx[k]];
-}
-
-static __global__ __launch_bounds__(kBlock) void k_dist_dvals(const u32* __restrict__ sidx, u64 nsent,
-                                                              const unsigned char* __restrict__ sflag,
-                                                              const u32* __restrict__ pred,
-                                                              const u32* __restrict__ dval, u32* __restrict__ gid) {
-  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (k >= nsent || !want_d(sflag[k])) return;
-  gid[sidx[k]] = dval[pred[k]];
+  if (k >= nsent) return;
+  const u32 q = seg_of(SD, R, k);
+  if (k - SD.d[q] >= cnt.d[q]) return;
+  const u64 v = dval[k];
+  gid[sidx[SD.d[q] + u32(v)]] = u32(v >> 32);
 }
 
 // Local words -> global ids; locally-first elements whose key repeats on
@@ -486,12 +567,13 @@ static __global__ __launch_bounds__(kBlock) void k_dist_remap(u32* __restrict__ 
                                                               const unsigned char* __restrict__ nf,
                                                               unsigned char* __restrict__ multi,
                                                               const u32* __restrict__ gid,
-                                                              const unsigned char* __restrict__ gmul) {
+                                                              const unsigned char* __restrict__ gmul, u32 off) {
   const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (j >= p) return;
   const u32 w = words[j];
   const u32 lid = w & kIdx;
-  words[j] = gid[lid] | (w & kBits);
+  const u32 g = gid[lid];
+  words[j] = ((g & kLocalId) ? (g & ~kLocalId) + off : g) | (w & kBits);
   if (multi && nf[j] == kNfMaybe && gmul[lid]) multi[j] = 1;
 }
 
@@ -509,16 +591,28 @@ static __global__ void k_dist_pack(const Header* __restrict__ h, const u64* __re
 // position), so the owners alone hash-cons it.  Writes what node_level would leave
 // behind for the exchange: local words, canonical pairs (the finalize source), marks
 // (all locally first, none known to repeat) and the local unique count.
+// gid != null: the input words still hold the previous level's LOCAL ids (its remap was
+// deferred to here, k_dist_remap's translation), so the pass reads each word once.
 static __global__ __launch_bounds__(kBlock) void k_node_keys(const u32* __restrict__ in, u64 n, u64 p,
                                                              u32* __restrict__ words, uint2* __restrict__ pairs,
                                                              unsigned char* __restrict__ nf,
                                                              unsigned char* __restrict__ multi,
-                                                             u64* __restrict__ count_out) {
+                                                             u64* __restrict__ count_out,
+                                                             const u32* __restrict__ gid, u32 off) {
   const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (j == 0) *count_out = p;
   if (j >= p) return;
   u32 l, r, cl, cr, m, t;
   load_pair(in, n, j, l, r);
+  if (gid) {
+    auto glob = [&](u32 w) {
+      if ((w & kIdx) == kIdx) return w;   // the odd tail's null
+      const u32 g = gid[w & kIdx];
+      return ((g & kLocalId) ? (g & ~kLocalId) + off : g) | (w & kBits);
+    };
+    l = glob(l);
+    r = glob(r);
+  }
   node_canonical(l, r, cl, cr, m, t);
   const u32 v = ulw(l) == ulw(xf(r, 1, 0));
   pairs[j] = make_uint2(cl, cr);

@@ -204,13 +204,17 @@ def _group_with_env(gcz, world, env):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("mode", ["1", "2", "2w"])
 @pytest.mark.parametrize("world", [2, 3, 8])
 def test_dist_local_dedupe_modes(mode, world, gcz, manifest, oracle):
     """Node levels with (GCZ_DIST_LOCAL=1) and without (=2) the local dedupe: without it a
     key reaches its owner once per occurrence, several times from one rank, and the owner
-    takes the first record in receive order (stable bucketing) as the first occurrence."""
-    g = _group_with_env(gcz, world, {"GCZ_DIST_LOCAL": mode})
+    takes the first record in receive order (stable bucketing) as the first occurrence --
+    through the position-packed owner table, or (2w, GCZ_TABLE=wide) the wide slots."""
+    env = {"GCZ_DIST_LOCAL": mode[0]}
+    if mode.endswith("w"):
+        env["GCZ_TABLE"] = "wide"
+    g = _group_with_env(gcz, world, env)
     try:
         for name in ("corpus/chmpxx", "corpus/merged", "synth/uniform_10000000", "synth/tandem_10000000"):
             case = manifest[name]
