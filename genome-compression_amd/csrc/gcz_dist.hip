@@ -338,7 +338,7 @@ struct gcz_group {
   int alloc(int i, u64 leaf_cap);
   int exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, u32 key_bits, u32 child_bits,
                std::vector<u64>& c, std::vector<u64>& off, u64& total, u64* err_global, int* err_sym,
-               int* ovf_bits, bool nolocal = false);
+               int* ovf_bits, bool nolocal = false, bool lookahead = false, u64* next_hashed_out = nullptr);
 };
 
 #define G_HIP(x)                                                   \
@@ -405,13 +405,13 @@ int gcz_group::alloc(int i, u64 leaf_cap) {
   if ((rc = c->ensure(d.sdval, u * 8))) return rc;
   if ((rc = c->ensure(d.dhdr, sizeof(DistHdr)))) return rc;
   if ((rc = c->ensure(d.gath, size_t(world) * kSyncWords * 8))) return rc;
-  if ((rc = c->ensure(d.gath2, size_t(world) * (1 + 2 * kMaxRanks) * 8))) return rc;
+  if ((rc = c->ensure(d.gath2, size_t(world) * (2 + 2 * kMaxRanks) * 8))) return rc;
   if ((rc = c->ensure(d.gathf, size_t(world) * kFinalWords * 8))) return rc;
   if ((rc = c->ensure(d.ddesc, ((u + kTile - 1) / kTile) * 8 + 64))) return rc;
   if ((rc = c->ensure(d.tail_in, nG * 4 + 16))) return rc;
   if (!d.h_gath) {
     if (hipHostMalloc((void**)&d.h_gath, size_t(kMaxRanks) * kSyncWords * 8, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&d.h_gath2, size_t(kMaxRanks) * (1 + 2 * kMaxRanks) * 8, hipHostMallocDefault) !=
+        hipHostMalloc((void**)&d.h_gath2, size_t(kMaxRanks) * (2 + 2 * kMaxRanks) * 8, hipHostMallocDefault) !=
             hipSuccess ||
         hipHostMalloc((void**)&d.h_gathf, size_t(kMaxRanks) * kFinalWords * 8, hipHostMallocDefault) != hipSuccess)
       return GCZ_ERR_DEVICE;
@@ -426,8 +426,10 @@ int gcz_group::alloc(int i, u64 leaf_cap) {
 // find the first occurrence from the receive order (stable bucketing).
 int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, u32 key_bits, u32 child_bits,
                         std::vector<u64>& c, std::vector<u64>& off, u64& total, u64* err_global, int* err_sym,
-                        int* ovf_bits, bool nolocal) {
+                        int* ovf_bits, bool nolocal, bool lookahead, u64* next_hashed_out) {
   const int R = world, NL = int(ctx.size());
+  u64 next_hashed = 0;
+  if (next_hashed_out) *next_hashed_out = ~0ull;
   // 1. bucket the records by owner, pack the sync vector
   for (int i = 0; i < NL; ++i) {
     gcz_ctx* cx = ctx[i];
@@ -610,6 +612,9 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       hipLaunchKernelGGL(k_dist_flags, tiles(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
                          d.sflag.as<unsigned char>(), d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(),
                          send_displ_of(rank[i]), u32(R), &dh->sync2[1]);
+      if (lookahead && nwords[i] > 0)
+        hipLaunchKernelGGL(k_lookahead, blocks((nwords[i] + 1) / 2), dim3(kBlock), 0, cx->stream,
+                           d.gmul.as<unsigned char>(), nwords[i], &dh->sync2[1 + 2 * R]);
       G_HIP(hipGetLastError());
     }
     const u64 tiles = std::max<u64>(1, tiles_of(ur));
@@ -628,7 +633,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
   std::vector<u64> MC(size_t(R) * R, 0), MD(size_t(R) * R, 0);
   u64 nc = 0, nd = 0;
   if (records) {
-    const size_t W = 1 + 2 * size_t(R);
+    const size_t W = 2 + 2 * size_t(R);
     std::vector<const void*> s;
     std::vector<void*> rv;
     for (gcz_ctx* cx : ctx) {
@@ -646,6 +651,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     for (int s2 = 0; s2 < R; ++s2) {
       const u64* v = d0.h_gath2 + size_t(s2) * W;
       c[s2] = v[0];
+      if (lookahead) next_hashed += v[1 + 2 * R];
       for (int q = 0; q < R; ++q) {
         MC[size_t(s2) * R + q] = v[1 + q];
         MD[size_t(s2) * R + q] = v[1 + R + q];
@@ -653,6 +659,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
         nd += v[1 + R + q];
       }
     }
+    if (lookahead && next_hashed_out) *next_hashed_out = next_hashed;
   } else {
     c = u;   // nothing crossed ranks: every local first is globally first
   }
@@ -988,7 +995,9 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         std::vector<u64> nw(NL);
         for (int i = 0; i < NL; ++i) nw[i] = P.count(rank[i], k + 1);
         const u32 cb = std::max<u32>(1, bit_width(prev_total));
-        const int rc = exchange(lv, nw, 2 * (cb + 2), cb, c, off, total, &err_global, &err_sym, &ovf, nolocal);
+        u64 next_hashed = ~0ull;
+        const int rc = exchange(lv, nw, 2 * (cb + 2), cb, c, off, total, &err_global, &err_sym, &ovf, nolocal,
+                                nolocal && k + 1 < G, &next_hashed);
         if (rc == kRetry) {
           allow_packed = false;
           retry = true;
@@ -997,7 +1006,8 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         if (rc) return rc;
         for (int s = 0; s < R; ++s) { slice_off[k + 1][s] = off[s]; slice_cnt[k + 1][s] = c[s]; }
         info.layer_size[k] = total;
-        direct = total == P.nk[k + 1];
+        // all unique, or (look-ahead) every pair of the next level holds a singleton
+        direct = total == P.nk[k + 1] || next_hashed == 0;
         prev_total = total;
       }
       for (int i = 0; i < NL; ++i) std::swap(cur_in[i], cur_out[i]);

@@ -37,8 +37,9 @@ struct DistHdr {
   // data (the leaf probe's pre-dedupe decision)
   u64 sync[kSyncWords];
   // second sync vector: [0] globally-first local uniques, [1, 1+R) C records per owner,
-  // [1+R, 1+2R) D records per owner (see exchange)
-  u64 sync2[1 + 2 * kMaxRanks];
+  // [1+R, 1+2R) D records per owner, [1+2R] pairs of the next level with two repeated
+  // children (look-ahead, see k_lookahead; 0 = the next level is direct)
+  u64 sync2[2 + 2 * kMaxRanks];
   u64 tot[4];                           // selected counts of the four compaction scans
   u32 ticket;                           // look-back tickets of k_dist_rank
   u32 tick[4];                          // ... of the compaction scans
@@ -498,6 +499,20 @@ static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restr
     if (hc[tid]) atomicAdd(reinterpret_cast<unsigned long long*>(&cnt[tid]), (unsigned long long)hc[tid]);
     if (hd[tid]) atomicAdd(reinterpret_cast<unsigned long long*>(&cnt[R + tid]), (unsigned long long)hd[tid]);
   }
+}
+
+// Look-ahead on a level without the local dedupe (lid = position): pairs (2j, 2j+1) of the
+// next level whose children both repeat globally (the odd tail pairs with null and goes
+// through the table when its left child repeats; rec_get's singleton test).  None on any
+// rank: every next-level pair holds a singleton, so the next level is direct.
+static __global__ __launch_bounds__(kBlock) void k_lookahead(const unsigned char* __restrict__ gmul, u64 n,
+                                                             u64* __restrict__ out) {
+  const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
+  bool hashed = false;
+  if (2 * j < n) hashed = gmul[2 * j] && (2 * j + 1 >= n || gmul[2 * j + 1]);
+  const u64 m = __ballot(hashed);
+  if ((threadIdx.x & 63) == 0 && m)
+    atomicAdd(reinterpret_cast<unsigned long long*>(out), (unsigned long long)__popcll(m));
 }
 
 // Rank of each globally-first local unique among them (local order); total -> *count_out.
