@@ -176,6 +176,42 @@ def stream_digest(group, dist, rank, world, info):
     return {"sha_leaves_bin": h_leaves.hexdigest(), "sha_layers_bin": h_layers.hexdigest()}
 
 
+def strong_run(gcz, ctx, group, dist, cfg, args, seed, L, world, rank, barrier):
+    """Weak-scaled runs also time the strong-scaled case: the configured genome itself
+    (1 Gbase) partitioned over the same ranks and group."""
+    import torch
+    try:
+        S1 = CONFIGS[args.config]["nbases"] // L
+        a0, a1, _ = gcz.dist_plan(S1, world, rank)
+        h1 = genome(gcz, cfg, seed, a0 * L, a1 * L)
+        dev1 = ctx.upload(h1 if h1.size else np.zeros(1, np.uint8))
+        del h1
+        run1 = lambda: group.build_device_bases([dev1.ptr], S1, L)  # noqa: E731
+        for _ in range(args.warmup):
+            run1()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            i1 = run1()
+        barrier()
+        dt1 = time.perf_counter() - t0
+        t = torch.tensor([dt1], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt1 = float(t.item())
+        dev1.free()
+        out = {"nbases": S1 * L, "value": S1 * L * args.steps / dt1, "ms_per_step": dt1 / args.steps * 1e3,
+               "device_ms": i1["build_ms"], "n_leaves": i1["n_leaves"]}
+        golden = CONFIGS[args.config]["golden"]
+        with open(os.path.join(REPO, "tests", "golden", "manifest.json")) as f:
+            exp = json.load(f).get(golden)
+        if exp:
+            out["layer_sizes_match"] = i1["layer_size"] == exp["expect"]["layer_sizes"]
+            out["root_match"] = i1["root"] == exp["expect"]["root"]
+        return out
+    except Exception as e:  # noqa: BLE001 -- the weak line still prints
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -185,11 +221,16 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=120_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-strong", action="store_true", help="weak runs: skip the strong-scaled 1-genome timing")
     ap.add_argument("--mode", choices=["weak", "strong", "dist", "replicas"], default="weak",
                     help="N > 1: one genome of N x the config size (weak), the config genome itself over N GPUs "
                          "(strong; 'dist' is an alias), or N independent genomes (replicas)")
     ap.add_argument("--virtual", type=int, default=0, help="N = 1: distributed path with R virtual ranks")
     ap.add_argument("--rccl-world1", action="store_true", help="N = 1: the RCCL group path with one rank")
+    ap.add_argument("--transport", choices=["rccl", "shm"], default="rccl",
+                    help="N > 1 exchanges: RCCL over xGMI, or host-staged shared memory (several ranks on one GPU, "
+                         "testing)")
+    ap.add_argument("--shm-region-mb", type=int, default=1024)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -225,16 +266,22 @@ def main():
     if world == 1 and args.rccl_world1:
         mode = "dist"
     seed = gcz._lib.gcz_synth_default_seed()
-    ctx = gcz.Context(local)
+    ctx = gcz.Context(local if args.transport == "rccl" else 0)   # shm: every rank on GPU 0
     group = None
     if mode == "dist":
         s0, s1, G = gcz.dist_plan(S, world, rank)
         host = genome(gcz, cfg, seed, s0 * L, s1 * L)
         dev = ctx.upload(host if host.size else np.zeros(1, np.uint8))
-        uid = [gcz.dist_unique_id() if rank == 0 else None]
-        if dist is not None:
-            dist.broadcast_object_list(uid, src=0)
-        group = gcz.Group.rccl(ctx, rank, world, uid[0])
+        if args.transport == "shm":   # testing: several ranks on one GPU, host-staged exchanges
+            name = [f"/gcz_bench_{os.getpid()}_{time.time_ns()}" if rank == 0 else None]
+            if dist is not None:
+                dist.broadcast_object_list(name, src=0)
+            group = gcz.Group.shm(ctx, rank, world, name[0], args.shm_region_mb << 20)
+        else:
+            uid = [gcz.dist_unique_id() if rank == 0 else None]
+            if dist is not None:
+                dist.broadcast_object_list(uid, src=0)
+            group = gcz.Group.rccl(ctx, rank, world, uid[0])
         prof_ctx = ctx
         run = lambda: group.build_device_bases([dev.ptr], S, L)  # noqa: E731
     elif mode == "virtual":
@@ -379,6 +426,10 @@ def main():
             ratio_path["roundtrip_match"] = bool(np.array_equal(got, np.where(ref >= 97, ref - 32, ref)))
         text.free()
 
+    strong = None
+    if weak and not args.no_strong:
+        strong = strong_run(gcz, ctx, group, dist, cfg, args, seed, L, world, rank, barrier)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_sample)
@@ -407,6 +458,7 @@ def main():
             "ratio_path": ratio_path,
             "cpu_baseline": cpu,
             "parity": parity,
+            "strong_scaling": strong,
         }
         print(json.dumps(line), flush=True)
     dev.free()

@@ -10,6 +10,14 @@
 // layers are the rank-ordered concatenation of the slices — byte-identical to
 // the single-device (and the reference's) build.
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <thread>
 #include <rccl/rccl.h>   // types only: the functions are resolved with dlsym
 
 #include "gcz_ctx.h"
@@ -257,6 +265,125 @@ struct RcclTransport : Transport {
       o += cnt[q];
     }
     return check(a.GroupEnd(), "ncclGroupEnd");
+  }
+};
+
+// One rank per process, host-staged through a POSIX shared-memory file: the multi-process
+// path (each process its own context, decisions from the gathered vectors, matching
+// collective sequences) on ONE GPU, where RCCL refuses two ranks per device.  Testing
+// only: every exchange is a D2H copy, a barrier, H2D copies, a barrier.
+struct ShmTransport : Transport {
+  struct Ctl {
+    std::atomic<u32> arrived;
+    std::atomic<u32> sense;
+    std::atomic<u32> failed;
+  };
+  int me = 0;
+  hipStream_t stream = nullptr;
+  size_t cap = 0;             // bytes per rank region
+  size_t map_bytes = 0;
+  char* base = nullptr;
+  u32 local_sense = 0;
+  ~ShmTransport() override {
+    if (base) munmap(base, map_bytes);
+  }
+  Ctl* ctl() { return reinterpret_cast<Ctl*>(base); }
+  char* region(int r) { return base + 4096 + size_t(r) * cap; }
+  int barrier() {
+    local_sense ^= 1u;
+    Ctl* c = ctl();
+    if (c->arrived.fetch_add(1) + 1 == u32(world)) {
+      c->arrived.store(0);
+      c->sense.store(local_sense);
+    } else {
+      const auto t0 = std::chrono::steady_clock::now();
+      while (c->sense.load() != local_sense) {
+        if (c->failed.load()) { err = "shm transport: a peer failed"; return GCZ_ERR_DEVICE; }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) {
+          err = "shm transport: barrier timeout";
+          c->failed.store(1);
+          return GCZ_ERR_DEVICE;
+        }
+        std::this_thread::yield();
+      }
+    }
+    return GCZ_OK;
+  }
+  int to_host(char* dst, const void* src, size_t bytes) {
+    if (!bytes) return GCZ_OK;
+    if (bytes > cap || hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream) != hipSuccess) {
+      err = bytes > cap ? "shm transport: region too small" : "shm transport: D2H copy failed";
+      ctl()->failed.store(1);
+      return GCZ_ERR_DEVICE;
+    }
+    return GCZ_OK;
+  }
+  int to_dev(void* dst, const char* src, size_t bytes) {
+    if (bytes && hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream) != hipSuccess) {
+      err = "shm transport: H2D copy failed";
+      return GCZ_ERR_DEVICE;
+    }
+    return GCZ_OK;
+  }
+  int drain() {
+    if (hipStreamSynchronize(stream) != hipSuccess) { err = "shm transport: stream"; return GCZ_ERR_DEVICE; }
+    return GCZ_OK;
+  }
+  int alltoallv_at(const std::vector<u64>& M, bool rev, size_t elem, const std::vector<u64>& sd,
+                   const std::vector<u64>& rd, const std::vector<const void*>& send,
+                   const std::vector<void*>& recv) override {
+    const size_t R = size_t(world);
+    if (int rc = drain()) return rc;
+    for (int d = 0; d < world; ++d) {   // my segments, at their send displacements
+      const size_t o = sd[me * R + d] * elem, n = mcount(M, world, rev, me, d) * elem;
+      if (o + n > cap) { err = "shm transport: region too small"; ctl()->failed.store(1); return GCZ_ERR_DEVICE; }
+      if (int rc = to_host(region(me) + o, static_cast<const char*>(send[0]) + o, n)) return rc;
+    }
+    if (int rc = drain()) return rc;
+    if (int rc = barrier()) return rc;
+    for (int s = 0; s < world; ++s)
+      if (int rc = to_dev(static_cast<char*>(recv[0]) + rd[me * R + s] * elem,
+                          region(s) + sd[s * R + me] * elem, mcount(M, world, rev, s, me) * elem))
+        return rc;
+    if (int rc = drain()) return rc;
+    return barrier();
+  }
+  int alltoallv(const std::vector<u64>& M, bool rev, size_t elem, const std::vector<const void*>& send,
+                const std::vector<void*>& recv) override {
+    const size_t R = size_t(world);
+    std::vector<u64> sd(R * R), rd(R * R);
+    for (int s = 0; s < world; ++s)
+      for (int d = 0; d < world; ++d) {
+        sd[s * R + d] = send_displ(M, world, rev, s, d);
+        rd[d * R + s] = recv_displ(M, world, rev, d, s);
+      }
+    return alltoallv_at(M, rev, elem, sd, rd, send, recv);
+  }
+  int allgather(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) override {
+    if (int rc = drain()) return rc;
+    if (int rc = to_host(region(me), send[0], bytes)) return rc;
+    if (int rc = drain()) return rc;
+    if (int rc = barrier()) return rc;
+    for (int s = 0; s < world; ++s)
+      if (int rc = to_dev(static_cast<char*>(recv[0]) + size_t(s) * bytes, region(s), bytes)) return rc;
+    if (int rc = drain()) return rc;
+    return barrier();
+  }
+  int gather0(const std::vector<u64>& cnt, size_t elem, const std::vector<const void*>& send,
+              void* recv0) override {
+    if (int rc = drain()) return rc;
+    if (int rc = to_host(region(me), send[0], cnt[me] * elem)) return rc;
+    if (int rc = drain()) return rc;
+    if (int rc = barrier()) return rc;
+    if (me == 0) {
+      u64 o = 0;
+      for (int s = 0; s < world; ++s) {
+        if (int rc = to_dev(static_cast<char*>(recv0) + o * elem, region(s), cnt[s] * elem)) return rc;
+        o += cnt[s];
+      }
+      if (int rc = drain()) return rc;
+    }
+    return barrier();
   }
 };
 
@@ -1174,6 +1301,66 @@ int gcz_group_create_rccl(gcz_ctx* ctx, int rank, int world, const void* unique_
     delete t;
     return GCZ_ERR_DEVICE;
   }
+  auto* g = new gcz_group();
+  g->world = world;
+  g->tr = t;
+  g->ctx.push_back(ctx);
+  g->rank.push_back(rank);
+  *out = g;
+  return GCZ_OK;
+}
+
+int gcz_group_create_shm(gcz_ctx* ctx, int rank, int world, const char* name, uint64_t region_bytes,
+                         gcz_group** out) {
+  if (!ctx || !out || !name || world < 1 || world > kMaxRanks || rank < 0 || rank >= world || region_bytes == 0)
+    return GCZ_ERR_ARG;
+  *out = nullptr;
+  const size_t cap = (region_bytes + 4095) / 4096 * 4096;
+  const size_t bytes = 4096 + cap * size_t(world);
+  // rank 0 creates and sizes the file (sparse); the others wait for its size
+  int fd = -1;
+  if (rank == 0) {
+    fd = shm_open(name, O_CREAT | O_RDWR, 0600);
+    if (fd < 0 || ftruncate(fd, off_t(bytes)) != 0) {
+      if (fd >= 0) close(fd);
+      ctx->last_error = std::string("shm_open/ftruncate failed: ") + name;
+      return GCZ_ERR_DEVICE;
+    }
+  } else {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      fd = shm_open(name, O_RDWR, 0600);
+      struct stat st{};
+      if (fd >= 0 && fstat(fd, &st) == 0 && size_t(st.st_size) == bytes) break;
+      if (fd >= 0) close(fd);
+      fd = -1;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+        ctx->last_error = std::string("shm transport: no region from rank 0: ") + name;
+        return GCZ_ERR_DEVICE;
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    }
+  }
+  void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) {
+    ctx->last_error = "shm transport: mmap failed";
+    return GCZ_ERR_DEVICE;
+  }
+  auto* t = new ShmTransport();
+  t->world = world;
+  t->me = rank;
+  t->stream = ctx->stream;
+  t->cap = cap;
+  t->map_bytes = bytes;
+  t->base = static_cast<char*>(p);
+  // every rank has mapped the region before anyone uses it (the control words start at 0)
+  if (t->barrier() != GCZ_OK) {
+    ctx->last_error = t->err;
+    delete t;
+    return GCZ_ERR_DEVICE;
+  }
+  if (rank == 0) shm_unlink(name);   // every rank holds its mapping: the name can go
   auto* g = new gcz_group();
   g->world = world;
   g->tr = t;

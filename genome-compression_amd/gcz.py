@@ -99,6 +99,8 @@ _SIGS = {
     "gcz_decompress": (ctypes.c_int, [_P, _P, _U64]),
     "gcz_dist_unique_id": (ctypes.c_int, [_P, _U64]),
     "gcz_group_create_rccl": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _P, ctypes.POINTER(_P)]),
+    "gcz_group_create_shm": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, _U64,
+                                            ctypes.POINTER(_P)]),
     "gcz_group_create_local": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
     "gcz_group_destroy": (None, [_P]),
     "gcz_group_world": (ctypes.c_int, [_P]),
@@ -474,6 +476,16 @@ class Group:
         rc = _lib.gcz_group_create_rccl(ctx._h, rank, world, uid, ctypes.byref(h))
         if rc != GCZ_OK:
             raise GczError(rc, "gcz_group_create_rccl failed: " + _lib.gcz_ctx_last_error(ctx._h).decode())
+        return cls(h, keep=ctx)
+
+    @classmethod
+    def shm(cls, ctx: Context, rank: int, world: int, name: str, region_bytes: int = 1 << 30):
+        """One rank per process on a shared device, exchanges host-staged through the
+        POSIX shared-memory object `name` (testing the multi-process path on one GPU)."""
+        h = ctypes.c_void_p()
+        rc = _lib.gcz_group_create_shm(ctx._h, rank, world, name.encode(), region_bytes, ctypes.byref(h))
+        if rc != GCZ_OK:
+            raise GczError(rc, "gcz_group_create_shm failed: " + _lib.gcz_ctx_last_error(ctx._h).decode())
         return cls(h, keep=ctx)
 
     def close(self):

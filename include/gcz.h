@@ -185,6 +185,11 @@ GCZ_API int gcz_dist_unique_id(void *out, uint64_t cap);
 GCZ_API int gcz_group_create_rccl(gcz_ctx *ctx, int rank, int world, const void *unique_id, gcz_group **out);
 /* `world` virtual ranks sharing one device, exchanges as device copies (testing). */
 GCZ_API int gcz_group_create_local(int device, int world, gcz_group **out);
+/* One rank per process, exchanges host-staged through a fresh POSIX shared-memory object
+ * `name` (region_bytes per rank, sparse; unlinked once every rank has mapped it): the
+ * multi-process path on a single GPU, where RCCL refuses two ranks per device (testing). */
+GCZ_API int gcz_group_create_shm(gcz_ctx *ctx, int rank, int world, const char *name, uint64_t region_bytes,
+                                 gcz_group **out);
 GCZ_API void gcz_group_destroy(gcz_group *g);
 GCZ_API int gcz_group_world(const gcz_group *g);
 GCZ_API int gcz_group_n_local(const gcz_group *g);          /* ranks driven by this process */

@@ -1,0 +1,49 @@
+"""The N > 1 bench path as real processes on one GPU.
+
+`python -m torch.distributed.run --nproc-per-node N bench.py` is exactly what the
+driver runs on an 8-GPU node; here every rank shares GPU 0 and the exchanges go
+through the host-staged shared-memory transport (--transport shm; RCCL refuses two
+ranks on one device).  Everything else is the production multi-rank path: one
+process and context per rank, the weak-scaled genome (N x uniform_100m), the
+per-level owner exchange, the streamed rank-slice parity digest over gloo, and the
+strong-scaled timing of the configured genome on the same group.  Both must match
+the reference goldens (synth/uniform_{200000006,300000009} and uniform_100000003).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_multiprocess_shm(world):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
+           "--transport", "shm", "--shm-region-mb", "256", "--config", "uniform_100m", "--steps", "2",
+           "--warmup", "1", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=REPO)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and lines, p.stdout[-2000:] + p.stderr[-4000:]
+    d = json.loads(lines[-1])
+    assert d["n_gpus"] == world and d["scaling"] == "weak" and d["value"] > 0
+    assert d["config"]["nbases"] == world * 100_000_003
+    par = d["parity"]
+    assert par["golden"] == f"synth/uniform_{world * 100_000_003}"
+    for k in ("layers_sha256_match", "leaves_sha256_match", "root_match", "layer_sizes_match"):
+        assert par[k] is True, (k, par)
+    st = d["strong_scaling"]
+    assert "error" not in st, st
+    assert st["nbases"] == 100_000_003 // 12 * 12
+    assert st["layer_sizes_match"] and st["root_match"], st
