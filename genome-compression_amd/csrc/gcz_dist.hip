@@ -430,6 +430,7 @@ struct RankLevel {
   bool leaves = false;
   const unsigned char* bases = nullptr;   // leaf level: for the bad-symbol report
   bool defer_remap = false;               // the next level's k_node_keys translates the words
+  bool counted = false;                   // k_node_keys wrote the bucketing's tile counts
 };
 }  // namespace
 
@@ -568,7 +569,8 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     const u32 nb = u32(std::max<u64>(1, (L.grid_elems + kTile - 1) / kTile));
     hipEvent_t eb{};
     cx->prof_begin(KID_DIST, eb);
-    hipLaunchKernelGGL(k_bucket_count, dim3(nb), dim3(kBlock), 0, cx->stream, L.src, d.blockcnt.as<u32>(), nb);
+    if (!L.counted)
+      hipLaunchKernelGGL(k_bucket_count, dim3(nb), dim3(kBlock), 0, cx->stream, L.src, d.blockcnt.as<u32>(), nb);
     hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(1024), 0, cx->stream, d.blockcnt.as<u32>(), u64(R) * nb, u32(R),
                        nb, dh->sync);
     hipLaunchKernelGGL(k_bucket_scatter, dim3(nb), dim3(kBlock), 0, cx->stream, L.src, d.blockcnt.as<u32>(), nb,
@@ -1083,18 +1085,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         na.desc = cx->desc.as<u64>() + dcur[i];
         dcur[i] += (p + scan_tile(p) - 1) / scan_tile(p);
         na.ticket = &h->ticket[kLayerSlot + k];
-        if (nolocal && !direct) {
-          const int cs = (k + 1) & 1;
-          ProfScope ps_(cx, KID_NODE);
-          const bool tr = k == 0 && leaf_deferred;
-          hipLaunchKernelGGL(k_node_keys, dim3(unsigned(std::max<u64>(1, (p + kBlock - 1) / kBlock))), dim3(kBlock), 0,
-                             cx->stream, cur_in[i], n, p, cur_out[i], cx->dist->scratch.as<uint2>(), cx->nf_set[cs],
-                             cx->multi_set[cs], na.count, tr ? cx->dist->gid.as<u32>() : nullptr,
-                             tr ? leaf_offs[i] : 0u);
-          G_HIP(hipGetLastError());
-        } else if (cx->node_level(na, h)) {
-          return dev_fail("node level");
-        }
+        if (!(nolocal && !direct) && cx->node_level(na, h)) return dev_fail("node level");
         RankLevel& rl = lv[i];
         rl = RankLevel{};
         rl.src.in = cur_in[i];
@@ -1113,6 +1104,18 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         rl.nf = cx->nf_set[cs];
         rl.multi = cx->multi_set[cs];
         rl.out = cx->nodes_out.as<uint2>() + node_base[i][k];
+        if (nolocal && !direct) {   // the pairs go straight to their owners; keys + tile counts in one pass
+          rl.src.R = u32(R);
+          rl.counted = true;
+          const u32 nb = u32(std::max<u64>(1, (p + kTile - 1) / kTile));
+          const bool tr = k == 0 && leaf_deferred;
+          ProfScope ps_(cx, KID_NODE);
+          hipLaunchKernelGGL(k_node_keys, dim3(nb), dim3(kBlock), 0, cx->stream, cur_in[i], n, p, cur_out[i],
+                             cx->dist->scratch.as<uint2>(), cx->nf_set[cs], cx->multi_set[cs], na.count,
+                             tr ? cx->dist->gid.as<u32>() : nullptr, tr ? leaf_offs[i] : 0u, rl.src,
+                             cx->dist->blockcnt.as<u32>(), nb);
+          G_HIP(hipGetLastError());
+        }
       }
       if (direct) {
         for (int s = 0; s < R; ++s) { slice_off[k + 1][s] = P.start(s, k + 1); slice_cnt[k + 1][s] = P.count(s, k + 1); }

@@ -608,32 +608,53 @@ static __global__ void k_dist_pack(const Header* __restrict__ h, const u64* __re
 // (all locally first, none known to repeat) and the local unique count.
 // gid != null: the input words still hold the previous level's LOCAL ids (its remap was
 // deferred to here, k_dist_remap's translation), so the pass reads each word once.
+// blockcnt != null: also the bucketing's per-tile owner counts (k_bucket_count over `rs`,
+// the level's record source, whose canonical pairs and marks this pass writes); one tile of
+// kTile pairs per block, like the bucketing grid.
 static __global__ __launch_bounds__(kBlock) void k_node_keys(const u32* __restrict__ in, u64 n, u64 p,
                                                              u32* __restrict__ words, uint2* __restrict__ pairs,
                                                              unsigned char* __restrict__ nf,
                                                              unsigned char* __restrict__ multi,
                                                              u64* __restrict__ count_out,
-                                                             const u32* __restrict__ gid, u32 off) {
-  const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (j == 0) *count_out = p;
-  if (j >= p) return;
-  u32 l, r, cl, cr, m, t;
-  load_pair(in, n, j, l, r);
-  if (gid) {
-    auto glob = [&](u32 w) {
-      if ((w & kIdx) == kIdx) return w;   // the odd tail's null
-      const u32 g = gid[w & kIdx];
-      return ((g & kLocalId) ? (g & ~kLocalId) + off : g) | (w & kBits);
-    };
-    l = glob(l);
-    r = glob(r);
+                                                             const u32* __restrict__ gid, u32 off, RecSrc rs,
+                                                             u32* __restrict__ blockcnt, u32 nb) {
+  __shared__ u32 h[kMaxRanks];
+  const int tid = threadIdx.x;
+  if (blockcnt) {
+    if (tid < int(rs.R)) h[tid] = 0;
+    __syncthreads();
   }
-  node_canonical(l, r, cl, cr, m, t);
-  const u32 v = ulw(l) == ulw(xf(r, 1, 0));
-  pairs[j] = make_uint2(cl, cr);
-  words[j] = make_word(u32(j), m, t, v);
-  nf[j] = kNfMaybe;
-  multi[j] = 0;
+  if (blockIdx.x == 0 && tid == 0) *count_out = p;
+  for (int e = 0; e < kItems; ++e) {
+    const u64 j = u64(blockIdx.x) * kTile + u64(e) * kBlock + tid;
+    if (j >= p) break;
+    u32 l, r, cl, cr, m, t;
+    load_pair(in, n, j, l, r);
+    if (gid) {
+      auto glob = [&](u32 w) {
+        if ((w & kIdx) == kIdx) return w;   // the odd tail's null
+        const u32 g = gid[w & kIdx];
+        return ((g & kLocalId) ? (g & ~kLocalId) + off : g) | (w & kBits);
+      };
+      l = glob(l);
+      r = glob(r);
+    }
+    node_canonical(l, r, cl, cr, m, t);
+    const u32 v = ulw(l) == ulw(xf(r, 1, 0));
+    pairs[j] = make_uint2(cl, cr);
+    words[j] = make_word(u32(j), m, t, v);
+    nf[j] = kNfMaybe;
+    multi[j] = 0;
+    if (blockcnt) {
+      u64 key;
+      u32 lid;
+      if (rec_get(rs, j, key, lid)) atomicAdd(&h[owner_of(rec_key(rs, key), rs.R)], 1u);
+    }
+  }
+  if (blockcnt) {
+    __syncthreads();
+    if (tid < int(rs.R)) blockcnt[u64(tid) * nb + blockIdx.x] = h[tid];
+  }
 }
 
 static __global__ void k_dist_final(const Header* __restrict__ h, DistHdr* __restrict__ dh, int tail0, int D,
