@@ -402,7 +402,13 @@ struct DistPlan {
     while (nk.back() > 1 || nk.size() == 1) nk.push_back((nk.back() + 1) / 2);
     D = int(nk.size()) - 1;
     const u64 T = (S + R - 1) / R;
-    G = T < 1024 ? 0 : int(bit_width(T)) - 1 - 9;   // >= 512 elements per rank after G levels
+    // >= 2^t elements per rank after G levels; rank 0 gathers the ~R * 2^t words left and
+    // finishes alone.  Every distributed hash-consed level pays an exchange round (two
+    // host syncs, four or five collectives) whatever its size, so the small levels go to
+    // rank 0: t = 23 - ceil(log2 R) (~2^23 words in the tail; GCZ_DIST_TAIL_LOG2 overrides).
+    const char* env = std::getenv("GCZ_DIST_TAIL_LOG2");
+    const int t = env ? std::atoi(env) : std::max(9, 23 - int(bit_width(u64(R) - 1)));
+    G = T < (2ull << t) ? 0 : int(bit_width(T)) - 1 - t;
     G = std::min(G, 20);
     G = std::min(G, D - 1);
     if (G < 0) G = 0;
@@ -1176,6 +1182,24 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
             if (cx->tail_levels(in, n, pc, k, D, node_base[i], h)) return dev_fail("tail levels");
             tail_done = true;
             break;
+          }
+          if (direct) {   // host-known (every later level too): direct subtrees, ids = positions
+            DirectPlan dp{};
+            int nlev = 0;
+            u64 m = n;
+            dp.n[0] = n;
+            while (nlev < kDirectLog && k + nlev < D && (m > u64(kTailMaxN) || !cx->use_tail)) {
+              dp.layer_off[k + nlev] = node_base[i][k + nlev];
+              m = P.nk[k + nlev + 1];
+              dp.n[++nlev] = m;
+            }
+            if (cx->direct_levels(in, k, nlev, dp, bufs[nb], h)) return dev_fail("tail direct levels");
+            in = bufs[nb];
+            nb ^= 1;
+            n = m;
+            bound = m;
+            k += nlev - 1;
+            continue;
           }
           NodeLevel na;
           na.k = k;

@@ -18,6 +18,15 @@ import pytest
 from conftest import GOLDEN, case_input, compare_digest
 
 
+@pytest.fixture(autouse=True)
+def deep_distribution(request, monkeypatch):
+    """Distribute node levels down to 512 elements per rank (GCZ_DIST_TAIL_LOG2=9), so that
+    the small inputs here exercise the distributed node levels; the production default
+    (a ~2^23-word tail finished by rank 0) is covered by test_dist_default_depth."""
+    if "default_depth" not in request.node.name:
+        monkeypatch.setenv("GCZ_DIST_TAIL_LOG2", "9")
+
+
 # ---- partition (host logic, no GPU) ----------------------------------------------
 @pytest.mark.parametrize("S", [1, 2, 7, 9, 100, 1023, 4096, 10085, 1 << 20, 83_333_333, 266_666_666])
 @pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
@@ -238,3 +247,16 @@ def test_dist_local_dedupe_modes(mode, world, gcz, manifest, oracle):
         assert t.root == ref.root
     finally:
         g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,name", [(3, "corpus/merged"), (8, "synth/tandem_100000000"),
+                                        (8, "synth/uniform_1000000000"), (2, "synth/uniform_100000003")])
+def test_dist_default_depth(world, name, gcz, manifest, groups):
+    """The default partition depth: distributed levels stop once ~2^23 words are left in
+    total (at R = 8: 2^20 per rank) and rank 0 finishes the top alone."""
+    assert "GCZ_DIST_TAIL_LOG2" not in os.environ
+    case = manifest[name]
+    kind, payload, L = case_input(case, gcz)
+    _dist_build(gcz, groups(world), kind, payload, L)
+    assert compare_digest(gcz.digest(groups(world).tree()), case["expect"]) == {}
