@@ -34,7 +34,9 @@ std::vector<u64> gcz_host::leaf_chunks(u64 S) {
   std::vector<u64> chunk_start{0};
   const u64 tile = kLeafTile;
   u64 next = std::max<u64>(tile, (S / 64 + tile - 1) / tile * tile);
-  if (S <= (1ull << 21)) next = S;
+  // one chunk up to 2^21 strands (GCZ_LEAF_CHUNKS_FROM overrides: tests chunk small inputs)
+  const char* env = std::getenv("GCZ_LEAF_CHUNKS_FROM");
+  if (S <= (env ? u64(std::atoll(env)) : (1ull << 21))) next = S;
   bool first = true;
   while (chunk_start.back() < S && int(chunk_start.size()) < kMaxChunks) {
     const u64 c0 = chunk_start.back();
@@ -66,21 +68,32 @@ int gcz_ctx::leaf_level(const LeafLevel& a, Header* d_hdr) {
   const int L = a.L;
   // packed leaves only from bases (< 2^4L by construction); user leaves may carry any bits.
   // Chunked settling needs one spare bit in the packed word, hence K + 1.
-  LevelTab lt = plan_table(tab.ptr, a.cap, a.bases ? 4 * u32(L) + 1 : 64, a.S, 0, allow_packed && a.bases, limit);
+  // Chunked settling needs two spare bits in the packed word (settled, seeded-global), hence K + 2.
+  LevelTab lt = plan_table(tab.ptr, a.cap, a.bases ? 4 * u32(L) + 2 : 64, std::max(a.S, a.seed_n + 1), 0,
+                           allow_packed && a.bases, limit);
   if (lt.packed) {
     lt.pt.limit = std::min(lt.pt.limit, limit);
-    lt.pt.kmask >>= 1;                   // the key itself has 4L bits
+    lt.pt.kmask >>= 2;                   // the key itself has 4L bits
     lt.pt.sh = (4 * u32(L) + 1) / 2;
   }
   unsigned char* d_nf = nf_set[0];
   hipEvent_t e0{};
-  prof_begin(KID_MEMSET, e0);
-  HIP_TRY(hipMemsetAsync(tab.ptr, 0xff, lt.bytes(), stream));
-  HIP_TRY(hipMemsetAsync(d_nf, 0, a.S, stream));
-  prof_end(KID_MEMSET, e0);
+  if (a.c_begin == 0) {
+    prof_begin(KID_MEMSET, e0);
+    HIP_TRY(hipMemsetAsync(tab.ptr, 0xff, lt.bytes(), stream));
+    HIP_TRY(hipMemsetAsync(d_nf, 0, a.S, stream));
+    prof_end(KID_MEMSET, e0);
+  }
+  if (a.seed && a.seed_n && lt.packed) {   // (a wide table just goes without: seeding only saves work)
+    prof_begin(KID_LEAF, e0);
+    hipLaunchKernelGGL(k_leaf_seed, dim3(unsigned((a.seed_n + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                       a.seed, a.seed_n, lt.pt, &d_hdr->leaf_overflow);
+    HIP_TRY(hipGetLastError());
+    prof_end(KID_LEAF, e0);
+  }
   u32* A = a.words;
-  const int C = int(a.chunk_start.size()) - 1;
-  for (int c = 0; c < C; ++c) {
+  const int C = a.c_end >= 0 ? a.c_end : int(a.chunk_start.size()) - 1;
+  for (int c = a.c_begin; c < C; ++c) {
     const u64 i0 = a.chunk_start[c], i1 = a.chunk_start[c + 1];
     const dim3 g(unsigned((i1 - i0 + kBlock - 1) / kBlock));
     prof_begin(KID_LEAF, e0);

@@ -142,6 +142,11 @@ struct LeafLevel {
   std::vector<u64> desc_off;
   u64* count = nullptr;             // count[c] = uniques after chunk c (cumulative, device)
   u32* ticket = nullptr;            // one per chunk
+  // multi-rank: chunks [c_begin, c_end) only (c_end < 0: all; table and marks are cleared
+  // when c_begin == 0), and a dictionary of seed_n keys whose ids are their indices
+  int c_begin = 0, c_end = -1;
+  const u64* seed = nullptr;
+  u64 seed_n = 0;
 };
 
 }  // namespace gcz_host

@@ -208,7 +208,9 @@ __device__ __forceinline__ u32 dec_child(u32 e, u32 B) {
 
 // not-first marks: 0 = maybe first, 1 = not first (resolve through the slot),
 // 2 = key settled by an earlier leaf chunk (final word already written)
-constexpr unsigned char kNfMaybe = 0, kNfNot = 1, kNfDone = 2;
+// 3 = multi-rank leaf level: the key was seeded with its GLOBAL id (rank 0's dictionary,
+// gcz_dist.hip), the word already holds the final id
+constexpr unsigned char kNfMaybe = 0, kNfNot = 1, kNfDone = 2, kNfGlobal = 3;
 __device__ __forceinline__ void mark(unsigned char* nf, u32 pos) { nf[pos] = kNfNot; }
 
 // Marks of one level: nf (not first) and, on node levels, multi (the key has
@@ -236,6 +238,7 @@ struct Ins {
   u32 slot;
   u32 id;      // valid when settled
   bool settled;
+  bool global = false;   // settled with a global id (seeded)
 };
 
 struct WideTab {
@@ -341,7 +344,7 @@ struct PackedTab {
     return 0;
   }
   __device__ __forceinline__ void read(u32 s, u64& key, u32& pos) const {
-    const u64 w = tab[s] & ~kSettled;
+    const u64 w = tab[s] & ~(kSettled | kGlobal);
     pos = u32(w & ((1ull << P) - 1));
     const u32 d = u32((w >> P) & ((1ull << D) - 1));
     const u64 q = w >> (P + D);
@@ -351,6 +354,7 @@ struct PackedTab {
   // Leaf chunks (needs Q + D + P <= 63): a settled slot keeps its key bits and
   // holds the final id in the position field, with bit 63 set.
   static constexpr u64 kSettled = 1ull << 63;
+  static constexpr u64 kGlobal = 1ull << 62;   // settled by seed(): the id is global (needs K + 2)
   __device__ __forceinline__ Ins insert_chunk(u64 key, u32 pos, const Marks& mk,
                                               u32* __restrict__ ovf) const {
     const u64 h = mix(key);
@@ -364,8 +368,8 @@ struct PackedTab {
         cur = atomicCAS(&tab[s], kEmpty, mine);
         if (cur == kEmpty) return {s, 0, false};
       }
-      if (((cur & ~kSettled) >> P) == (mine >> P)) {
-        if (cur & kSettled) return {s, u32(cur & pmask), true};
+      if (((cur & ~(kSettled | kGlobal)) >> P) == (mine >> P)) {
+        if (cur & kSettled) return {s, u32(cur & pmask), true, (cur & kGlobal) != 0};
         if (u32(cur & pmask) < pos) { mark_dup(mk, pos, u32(cur & pmask)); return {s, 0, false}; }
         const u64 old = atomicMin(&tab[s], mine);
         mark_dup(mk, pos, u32(old & pmask));
@@ -378,6 +382,20 @@ struct PackedTab {
   }
   __device__ __forceinline__ void settle(u32 s, u32 id) const {
     tab[s] = kSettled | (tab[s] & ~((1ull << P) - 1)) | id;
+  }
+  // Multi-rank leaf level: a key of rank 0's dictionary enters a fresh table settled with
+  // its global id, so this rank's strands of that key take the final word from the probe.
+  __device__ __forceinline__ void seed(u64 key, u32 id, u32* __restrict__ ovf) const {
+    const u64 h = mix(key);
+    u32 s = u32(h) & mask;
+    const u64 qd = (h >> c) << D;
+    for (u32 d = 0; d < limit; ++d) {
+      const u64 mine = kSettled | kGlobal | ((qd | d) << P) | id;
+      const u64 cur = atomicCAS(&tab[s], kEmpty, mine);
+      if (cur == kEmpty) return;   // dictionary keys are distinct: never found, only placed
+      s = (s + 1) & mask;
+    }
+    atomicOr(ovf, 1u);
   }
   __device__ __forceinline__ u32 settled_id(u32 s) const { return u32(tab[s] & ((1ull << P) - 1)); }
 };
@@ -421,8 +439,14 @@ __global__ __launch_bounds__(kBlock) void k_leaf_bases(const unsigned char* __re
   u32 m, t, v;
   const u64 key = leaf_canonical(x, L, m, t, v);
   const Ins r = T.insert_chunk(key, u32(i), Marks{nf, nullptr}, &hdr->leaf_overflow);
-  if (r.settled) nf[i] = kNfDone;
+  if (r.settled) nf[i] = r.global ? kNfGlobal : kNfDone;
   rec[i] = make_word(r.settled ? r.id : r.slot, m, t, v);
+}
+
+[[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_leaf_seed(const u64* __restrict__ dict, u64 n, PackedTab T,
+                                                             u32* __restrict__ ovf) {
+  const u64 d = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (d < n) T.seed(dict[d], u32(d), ovf);
 }
 
 // In-block repeats of the first leaf chunk (equal provisional slot words mean equal
@@ -466,7 +490,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_packed(const u64* __restrict__ 
   u32 m, t, v;
   const u64 key = leaf_canonical(leaves[i], L, m, t, v);
   const Ins r = T.insert_chunk(key, u32(i), Marks{nf, nullptr}, &hdr->leaf_overflow);
-  if (r.settled) nf[i] = kNfDone;
+  if (r.settled) nf[i] = r.global ? kNfGlobal : kNfDone;
   rec[i] = make_word(r.settled ? r.id : r.slot, m, t, v);
 }
 

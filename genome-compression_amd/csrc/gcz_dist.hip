@@ -28,6 +28,7 @@ using namespace gcz_host;
 
 struct gcz_dist_state {
   DevBuf scratch, gnf, gmul, gid, blockcnt, skey, sidx, sflag, scval, sdval;   // sender side
+  DevBuf dict;                                                                // rank 0's leaf dictionary
   DevBuf rkey, oslot, rflag, rcval, rdval, owntab, oids, omin;                // owner side
   DevBuf dhdr, gath, gath2, gathf, ddesc, tail_in;
   u64* h_gath = nullptr;    // pinned mirrors of the gathered vectors
@@ -38,7 +39,7 @@ struct gcz_dist_state {
 void gcz_dist_state_free(gcz_ctx* c) {
   gcz_dist_state* d = c->dist;
   if (!d) return;
-  for (DevBuf* b : {&d->scratch, &d->gnf, &d->gmul, &d->gid, &d->blockcnt, &d->skey, &d->sidx, &d->sflag,
+  for (DevBuf* b : {&d->dict, &d->scratch, &d->gnf, &d->gmul, &d->gid, &d->blockcnt, &d->skey, &d->sidx, &d->sflag,
                     &d->scval, &d->sdval, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab, &d->oids,
                     &d->omin,
                     &d->dhdr, &d->gath, &d->gath2, &d->gathf, &d->ddesc, &d->tail_in})
@@ -67,6 +68,8 @@ struct Transport {
                            const std::vector<u64>& rd, const std::vector<const void*>& send,
                            const std::vector<void*>& recv) = 0;
   virtual int allgather(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) = 0;
+  // rank 0's `bytes` at send[i of rank 0] to recv[i] of every other rank
+  virtual int bcast0(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) = 0;
   // rank 0 receives cnt[r] elements from every rank r, concatenated in rank order
   virtual int gather0(const std::vector<u64>& cnt, size_t elem, const std::vector<const void*>& send,
                       void* recv0) = 0;
@@ -124,6 +127,11 @@ struct LocalTransport : Transport {
         if (int rc = copy(static_cast<char*>(recv[d]) + size_t(s) * bytes, send[s], bytes)) return rc;
     return GCZ_OK;
   }
+  int bcast0(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) override {
+    for (int d = 1; d < world; ++d)
+      if (int rc = copy(recv[d], send[0], bytes)) return rc;
+    return GCZ_OK;
+  }
   int gather0(const std::vector<u64>& cnt, size_t elem, const std::vector<const void*>& send,
               void* recv0) override {
     u64 o = 0;
@@ -144,6 +152,7 @@ struct RcclApi {
   ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
   bool ok = false;
 };
@@ -165,10 +174,11 @@ RcclApi& rccl() {
     GCZ_SYM(Send, "ncclSend");
     GCZ_SYM(Recv, "ncclRecv");
     GCZ_SYM(AllGather, "ncclAllGather");
+    GCZ_SYM(Broadcast, "ncclBroadcast");
     GCZ_SYM(GetErrorString, "ncclGetErrorString");
 #undef GCZ_SYM
     a.ok = a.GetUniqueId && a.CommInitRank && a.CommDestroy && a.GroupStart && a.GroupEnd && a.Send && a.Recv &&
-           a.AllGather && a.GetErrorString;
+           a.AllGather && a.Broadcast && a.GetErrorString;
     return a;
   }();
   return api;
@@ -246,6 +256,11 @@ struct RcclTransport : Transport {
   }
   int allgather(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) override {
     return check(rccl().AllGather(send[0], recv[0], bytes, ncclUint8, comm, stream), "ncclAllGather");
+  }
+  int bcast0(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) override {
+    if (!bytes) return GCZ_OK;
+    void* buf = me == 0 ? const_cast<void*>(send[0]) : recv[0];   // in place on the root
+    return check(rccl().Broadcast(buf, buf, bytes, ncclUint8, 0, comm, stream), "ncclBroadcast");
   }
   int gather0(const std::vector<u64>& cnt, size_t elem, const std::vector<const void*>& send,
               void* recv0) override {
@@ -369,6 +384,18 @@ struct ShmTransport : Transport {
     if (int rc = drain()) return rc;
     return barrier();
   }
+  int bcast0(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) override {
+    if (int rc = drain()) return rc;
+    if (me == 0 && (rc_ = to_host(region(0), send[0], bytes))) return rc_;
+    if (int rc = drain()) return rc;
+    if (int rc = barrier()) return rc;
+    if (me != 0) {
+      if (int rc = to_dev(recv[0], region(0), bytes)) return rc;
+      if (int rc = drain()) return rc;
+    }
+    return barrier();
+  }
+  int rc_ = 0;
   int gather0(const std::vector<u64>& cnt, size_t elem, const std::vector<const void*>& send,
               void* recv0) override {
     if (int rc = drain()) return rc;
@@ -437,6 +464,8 @@ struct RankLevel {
   const unsigned char* bases = nullptr;   // leaf level: for the bad-symbol report
   bool defer_remap = false;               // the next level's k_node_keys translates the words
   bool counted = false;                   // k_node_keys wrote the bucketing's tile counts
+  const unsigned char* gmark = nullptr;   // leaf level: kNfGlobal strands already hold global ids
+  bool identity = false;                  // rank 0's leaf level: local ids are the global ids
 };
 }  // namespace
 
@@ -455,9 +484,14 @@ struct gcz_group {
   bool allow_packed = true;
   // node levels: 0 auto (local dedupe only on repetitive data), 1 always, 2 never (GCZ_DIST_LOCAL)
   int dist_local = std::getenv("GCZ_DIST_LOCAL") ? std::atoi(std::getenv("GCZ_DIST_LOCAL")) : 0;
+  // leaf dictionary: rank 0's first-occurrence keys of its first seed_chunks leaf chunks (0: off;
+  // GCZ_DIST_SEED)
+  int seed_chunks = std::getenv("GCZ_DIST_SEED") ? std::atoi(std::getenv("GCZ_DIST_SEED")) : 4;
   bool any_predup = false;   // some rank's leaf probe found repetitive data (set by the leaf exchange)
   bool leaf_deferred = false;   // the leaf words keep local ids until layer 0's k_node_keys
   std::vector<u32> leaf_offs;   // ... and each local rank's leaf id offset
+  std::vector<const unsigned char*> leaf_gmark;   // ... its seeded-strand marks
+  std::vector<bool> leaf_identity;                // ... and whether its ids are already global
 
   int fail(int code, const std::string& what) {
     last_error = what;
@@ -881,14 +915,22 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
   // 5. local words -> global ids
   leaf_deferred = lv[0].leaves && lv[0].defer_remap && (dist_local == 2 || (dist_local == 0 && !any_predup)) &&
                   total != plan.nk[0];
+  if (lv[0].leaves) {
+    leaf_gmark.assign(NL, nullptr);
+    leaf_identity.assign(NL, false);
+    for (int i = 0; i < NL; ++i) {
+      leaf_gmark[i] = lv[i].gmark;
+      leaf_identity[i] = lv[i].identity;
+    }
+  }
   for (int i = 0; i < NL; ++i) {
-    if (leaf_deferred) continue;
+    if (leaf_deferred || lv[i].identity) continue;   // rank 0's leaf ids are already global
     gcz_ctx* cx = ctx[i];
     gcz_dist_state& d = *cx->dist;
     const u64 nw = nwords[i];
     ProfScope ps_(cx, KID_REMAP);
     hipLaunchKernelGGL(k_dist_remap, blocks(nw), dim3(kBlock), 0, cx->stream, lv[i].w, nw, lv[i].nf, lv[i].multi,
-                       d.gid.as<u32>(), d.gmul.as<unsigned char>(), u32(off[rank[i]]));
+                       d.gid.as<u32>(), d.gmul.as<unsigned char>(), u32(off[rank[i]]), lv[i].gmark);
     G_HIP(hipGetLastError());
   }
   return GCZ_OK;
@@ -960,12 +1002,23 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     any_predup = false;
 
     // ---- leaves ----
+    // Leaf dictionary (bases input, R > 1).  Nothing precedes rank 0, so the first-occurrence
+    // keys of its first c0 chunks carry their GLOBAL ids already.  Rank 0 runs those chunks,
+    // the keys go to every rank (bcast0), and ranks > 0 seed their fresh leaf table with them
+    // before their leaf level: their strands of dictionary keys take the final word from the
+    // probe (kNfGlobal) and those keys never enter their local unique lists, so the leaf
+    // exchange and the leaf-word translation shrink to the keys rank 0's prefix has not seen.
+    // Rank 0 still sends all its keys to the owners, so any rank may go without seeding.
+    const std::vector<u64> chunks0 = leaf_chunks(P.count(0, 0));
+    const int c0 = seed_chunks;
+    const bool seeding = R > 1 && d_bases && c0 > 0 && int(chunks0.size()) - 1 > c0;
     std::vector<int> C(NL);
+    std::vector<LeafLevel> las(NL);
     for (int i = 0; i < NL; ++i) {
       gcz_ctx* cx = ctx[i];
       Header* h = cx->hdr.as<Header>();
       const u64 S_r = P.count(rank[i], 0);
-      LeafLevel la;
+      LeafLevel& la = las[i];
       la.bases = bases[i];
       la.leaves = d_leaves ? d_leaves[i] : nullptr;
       la.S = S_r;
@@ -984,7 +1037,75 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
       la.desc = cx->desc.as<u64>();
       la.count = h->count;
       la.ticket = h->ticket;
+      if (seeding) {   // every local id space must hold the dictionary's ids
+        la.seed_n = P.count(0, 0) >= chunks0[c0] ? chunks0[c0] : 0;
+        if (rank[i] != 0) continue;
+        la.c_end = c0;
+      }
       if (cx->leaf_level(la, h)) return dev_fail("leaf level");
+    }
+    if (seeding) {
+      // the dictionary size (rank 0's uniques after c0 chunks), then the keys
+      std::vector<const void*> sv;
+      std::vector<void*> rv;
+      for (int i = 0; i < NL; ++i) {
+        gcz_ctx* cx = ctx[i];
+        DistHdr* dh = cx->dist->dhdr.as<DistHdr>();
+        if (rank[i] == 0)
+          G_HIP(hipMemcpyAsync(&dh->sync[0], &cx->hdr.as<Header>()->count[c0 - 1], 8, hipMemcpyDeviceToDevice,
+                               cx->stream));
+        else
+          G_HIP(hipMemsetAsync(&dh->sync[0], 0, 8, cx->stream));
+        sv.push_back(&dh->sync[0]);
+        rv.push_back(cx->dist->gath.ptr);
+      }
+      {
+        hipEvent_t e0{};
+        ctx[0]->prof_begin(KID_EXCHANGE, e0);
+        G_RC(tr->allgather(8, sv, rv));
+        ctx[0]->prof_end(KID_EXCHANGE, e0);
+      }
+      gcz_dist_state& d0 = *ctx[0]->dist;
+      G_HIP(hipMemcpyAsync(d0.h_gath, d0.gath.ptr, 8, hipMemcpyDeviceToHost, ctx[0]->stream));
+      for (gcz_ctx* cx : ctx) G_HIP(hipStreamSynchronize(cx->stream));
+      const u64 U = std::min<u64>(d0.h_gath[0], chunks0[c0]);
+      std::vector<const void*> ks(NL, nullptr);
+      std::vector<void*> kr(NL, nullptr);
+      int i0 = -1;
+      for (int i = 0; i < NL; ++i) {
+        gcz_ctx* cx = ctx[i];
+        if (cx->ensure(cx->dist->dict, U * 8 + 16)) return dev_fail("leaf dictionary");
+        kr[i] = cx->dist->dict.ptr;
+        if (rank[i] == 0) i0 = i;
+      }
+      // LocalTransport indexes by global rank (all ranks local); RCCL / shm by local slot 0
+      if (NL == R) {
+        ks[0] = ctx[i0]->dist->scratch.ptr;
+      } else {
+        ks[0] = i0 >= 0 ? ctx[i0]->dist->scratch.ptr : nullptr;
+      }
+      {
+        hipEvent_t e0{};
+        ctx[0]->prof_begin(KID_EXCHANGE, e0);
+        G_RC(tr->bcast0(U * 8, ks, kr));
+        ctx[0]->prof_end(KID_EXCHANGE, e0);
+      }
+      for (int i = 0; i < NL; ++i) {
+        LeafLevel& la = las[i];
+        if (rank[i] == 0) {
+          la.c_begin = c0;
+          la.c_end = -1;
+        } else {
+          la.seed = ctx[i]->dist->dict.as<u64>();
+          la.seed_n = U;
+        }
+        if (ctx[i]->leaf_level(la, ctx[i]->hdr.as<Header>())) return dev_fail("leaf level");
+      }
+    }
+    for (int i = 0; i < NL; ++i) {
+      gcz_ctx* cx = ctx[i];
+      Header* h = cx->hdr.as<Header>();
+      const u64 S_r = P.count(rank[i], 0);
       RankLevel& rl = lv[i];
       rl = RankLevel{};
       rl.src.leaves = cx->dist->scratch.as<u64>();
@@ -995,6 +1116,8 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
       rl.out = cx->leaves_out.ptr;
       rl.leaves = true;
       rl.bases = bases[i];
+      rl.gmark = seeding ? cx->nf_set[0] : nullptr;
+      rl.identity = rank[i] == 0;
     }
     std::vector<u64> c, off;
     u64 total = 0, err_global = 0;
@@ -1114,12 +1237,12 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
           rl.src.R = u32(R);
           rl.counted = true;
           const u32 nb = u32(std::max<u64>(1, (p + kTile - 1) / kTile));
-          const bool tr = k == 0 && leaf_deferred;
+          const bool tr = k == 0 && leaf_deferred && !leaf_identity[i];
           ProfScope ps_(cx, KID_NODE);
           hipLaunchKernelGGL(k_node_keys, dim3(nb), dim3(kBlock), 0, cx->stream, cur_in[i], n, p, cur_out[i],
                              cx->dist->scratch.as<uint2>(), cx->nf_set[cs], cx->multi_set[cs], na.count,
                              tr ? cx->dist->gid.as<u32>() : nullptr, tr ? leaf_offs[i] : 0u, rl.src,
-                             cx->dist->blockcnt.as<u32>(), nb);
+                             cx->dist->blockcnt.as<u32>(), nb, tr ? leaf_gmark[i] : nullptr);
           G_HIP(hipGetLastError());
         }
       }

@@ -582,9 +582,11 @@ static __global__ __launch_bounds__(kBlock) void k_dist_remap(u32* __restrict__ 
                                                               const unsigned char* __restrict__ nf,
                                                               unsigned char* __restrict__ multi,
                                                               const u32* __restrict__ gid,
-                                                              const unsigned char* __restrict__ gmul, u32 off) {
+                                                              const unsigned char* __restrict__ gmul, u32 off,
+                                                              const unsigned char* __restrict__ gmark) {
   const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (j >= p) return;
+  if (gmark && gmark[j] == kNfGlobal) return;   // seeded leaf: the word holds its global id
   const u32 w = words[j];
   const u32 lid = w & kIdx;
   const u32 g = gid[lid];
@@ -617,7 +619,8 @@ static __global__ __launch_bounds__(kBlock) void k_node_keys(const u32* __restri
                                                              unsigned char* __restrict__ multi,
                                                              u64* __restrict__ count_out,
                                                              const u32* __restrict__ gid, u32 off, RecSrc rs,
-                                                             u32* __restrict__ blockcnt, u32 nb) {
+                                                             u32* __restrict__ blockcnt, u32 nb,
+                                                             const unsigned char* __restrict__ gmark) {
   __shared__ u32 h[kMaxRanks];
   const int tid = threadIdx.x;
   if (blockcnt) {
@@ -631,13 +634,14 @@ static __global__ __launch_bounds__(kBlock) void k_node_keys(const u32* __restri
     u32 l, r, cl, cr, m, t;
     load_pair(in, n, j, l, r);
     if (gid) {
-      auto glob = [&](u32 w) {
-        if ((w & kIdx) == kIdx) return w;   // the odd tail's null
+      auto glob = [&](u32 w, u64 strand) {
+        if ((w & kIdx) == kIdx) return w;                            // the odd tail's null
+        if (gmark && gmark[strand] == kNfGlobal) return w;           // seeded: already global
         const u32 g = gid[w & kIdx];
         return ((g & kLocalId) ? (g & ~kLocalId) + off : g) | (w & kBits);
       };
-      l = glob(l);
-      r = glob(r);
+      l = glob(l, 2 * j);
+      r = glob(r, 2 * j + 1);
     }
     node_canonical(l, r, cl, cr, m, t);
     const u32 v = ulw(l) == ulw(xf(r, 1, 0));

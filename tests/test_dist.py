@@ -260,3 +260,34 @@ def test_dist_default_depth(world, name, gcz, manifest, groups):
     kind, payload, L = case_input(case, gcz)
     _dist_build(gcz, groups(world), kind, payload, L)
     assert compare_digest(gcz.digest(groups(world).tree()), case["expect"]) == {}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", ["1", "4", "0"])
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_dist_leaf_dictionary(seed, world, gcz, manifest, oracle, monkeypatch):
+    """Rank 0's leaf dictionary (GCZ_DIST_SEED = its first chunks; 0 = off) on small inputs:
+    GCZ_LEAF_CHUNKS_FROM forces the chunked leaf level so rank 0 has chunks to share, and
+    ranks > 0 seed their tables (strands of dictionary keys take global ids from the probe)."""
+    monkeypatch.setenv("GCZ_LEAF_CHUNKS_FROM", "1024")
+    monkeypatch.setenv("GCZ_DIST_SEED", seed)
+    g = gcz.Group.local(world)
+    try:
+        for name in ("corpus/chmpxx", "corpus/merged", "synth/uniform_10000000", "synth/tandem_10000000",
+                     "fasta/iupac_stress", "corpus/hehcmv"):
+            case = manifest[name]
+            kind, payload, L = case_input(case, gcz)
+            _dist_build(gcz, g, kind, payload, L)
+            assert compare_digest(gcz.digest(g.tree()), case["expect"]) == {}, name
+        rng = np.random.default_rng(100 + world)
+        alphabet = np.frombuffer(b"ACGTRYKMBVDHSWN-", dtype=np.uint8)
+        base = alphabet[rng.integers(0, 16, size=300_000)]
+        data = base.tobytes()
+        ref = oracle.build_fasta(data, 4)
+        _dist_build(gcz, g, "fasta", data, 4)
+        t = g.tree()
+        assert np.array_equal(t.leaves(), ref.leaves())
+        for k in range(ref.n_layers):
+            assert np.array_equal(t.layer(k), ref.layer(k)), k
+    finally:
+        g.close()
