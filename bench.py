@@ -176,6 +176,21 @@ def stream_digest(group, dist, rank, world, info):
     return {"sha_leaves_bin": h_leaves.hexdigest(), "sha_layers_bin": h_layers.hexdigest()}
 
 
+LEAF_SCOPES = ("leaf_insert", "flagscan_leaf", "resolve_leaf")
+
+
+def rank_summary(rank, build_ms, trace):
+    """One rank's profiled build: busy kernel time, exchange scopes (transfer + wait for the
+    peers), host gaps, and when its leaf level ended (ms after the build's start event)."""
+    busy = sum(d for k, _, d in trace if k != "exchange")
+    xch = [(round(t, 3), round(d, 3)) for k, t, d in trace if k == "exchange"]
+    leaf_end = max((t + d for k, t, d in trace if k in LEAF_SCOPES), default=None)
+    x = sum(d for _, d in xch)
+    return {"rank": rank, "build_ms": round(build_ms, 3), "busy_ms": round(busy, 3), "exchange_ms": round(x, 3),
+            "gap_ms": round(build_ms - busy - x, 3),
+            "leaf_end_ms": round(leaf_end, 3) if leaf_end is not None else None, "exchanges": xch}
+
+
 def strong_run(gcz, ctx, group, dist, cfg, args, seed, L, world, rank, barrier):
     """Weak-scaled runs also time the strong-scaled case: the configured genome itself
     (1 Gbase) partitioned over the same ranks and group."""
@@ -327,8 +342,20 @@ def main():
     for c in pctxs:
         c.profile(True)
         c.profile_reset()
+    barrier()   # ranks start the profiled build together: exchange waits are the peers' lag inside it
     info = run()
     tables = [c.profile_table() for c in pctxs]
+    # N > 1: every rank's timeline of the profiled build (kernel busy time, exchanges incl. the
+    # wait for peers, host gaps) -- where a rank waits is invisible in the max-over-ranks time
+    rank_detail = None
+    if mode == "dist":
+        mine = rank_summary(rank, info["build_ms"], prof_ctx.profile_trace())
+        rank_detail = [mine]
+        if dist is not None:
+            rank_detail = [None] * world
+            dist.all_gather_object(rank_detail, mine)
+    elif mode == "virtual":
+        rank_detail = [rank_summary(r, info["build_ms"], c.profile_trace()) for r, c in enumerate(pctxs)]
     for c in pctxs:
         c.profile(False)
     prof = tables[0]
@@ -455,6 +482,7 @@ def main():
                       "n_layers": info["n_layers"]},
             "kernels": kernels,
             "rank_kernel_ms": rank_ms,
+            "rank_timeline": rank_detail,
             "ratio_path": ratio_path,
             "cpu_baseline": cpu,
             "parity": parity,

@@ -30,10 +30,10 @@ void launch_leaf_bases(int L, dim3 g, hipStream_t st, const unsigned char* b, u6
 // leaf chunks, geometric: S/64, S/64, S/32, ... S/2 (multiples of the leaf tile);
 // the first small chunks discover most keys, the big later ones mostly hit
 // settled slots.  Small inputs are one chunk.
-std::vector<u64> gcz_host::leaf_chunks(u64 S) {
+std::vector<u64> gcz_host::leaf_chunks(u64 S, int first_log2) {
   std::vector<u64> chunk_start{0};
   const u64 tile = kLeafTile;
-  u64 next = std::max<u64>(tile, (S / 64 + tile - 1) / tile * tile);
+  u64 next = std::max<u64>(tile, ((S >> first_log2) + tile - 1) / tile * tile);
   // one chunk up to 2^21 strands (GCZ_LEAF_CHUNKS_FROM overrides: tests chunk small inputs)
   const char* env = std::getenv("GCZ_LEAF_CHUNKS_FROM");
   if (S <= (env ? u64(std::atoll(env)) : (1ull << 21))) next = S;
@@ -107,8 +107,10 @@ int gcz_ctx::leaf_level(const LeafLevel& a, Header* d_hdr) {
     }
     HIP_TRY(hipGetLastError());
     if (c == 0) {   // repetitive data? (switches the node inserts' LDS pre-dedupe)
-      hipLaunchKernelGGL(k_dup_probe, g, dim3(kBlock), 0, stream, A, i0, i1, d_hdr);
-      hipLaunchKernelGGL(k_dup_decide, dim3(1), dim3(1), 0, stream, d_hdr, i1 - i0, u32(predup_mode));
+      const u64 ip = std::min(i1, i0 + (u64(1) << 21));   // a sample of up to 2^21 strands is enough
+      hipLaunchKernelGGL(k_dup_probe, dim3(unsigned((ip - i0 + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, A,
+                         i0, ip, d_hdr);
+      hipLaunchKernelGGL(k_dup_decide, dim3(1), dim3(1), 0, stream, d_hdr, ip - i0, u32(predup_mode));
     }
     prof_end(KID_LEAF, e0);
     const u64 tile = scan_tile(i1 - i0);
@@ -250,7 +252,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   const int D = int(pk.size());
   layer_off.assign(D + 1, 0);
   for (int k = 0; k < D; ++k) layer_off[k + 1] = layer_off[k] + pk[k];
-  const std::vector<u64> chunk_start = leaf_chunks(S);
+  const std::vector<u64> chunk_start = leaf_chunks(S, leaf_first_log2);
   const int C = int(chunk_start.size()) - 1;
   std::vector<u64> desc_off;
   u64 ntiles_total = 0;
@@ -443,6 +445,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   if (const char* t = std::getenv("GCZ_TAIL")) c->use_tail = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_DIRECT")) c->use_direct = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_PREDUP")) c->predup_mode = std::atoi(t);   // 1 on, 2 off, 0 auto
+  if (const char* t = std::getenv("GCZ_LEAF_FIRST_LOG2")) c->leaf_first_log2 = std::max(1, std::min(20, std::atoi(t)));
   *out = c;
   return GCZ_OK;
 }
@@ -609,6 +612,13 @@ int gcz_profile_entry(gcz_ctx* c, int k, const char** name, uint64_t* launches, 
 void gcz_profile_reset(gcz_ctx* c) {
   if (!c) return;
   for (int k = 0; k < KID_COUNT; ++k) { c->prof_launches[k] = 0; c->prof_ms[k] = 0; }
+  c->prof_trace.clear();
+}
+uint64_t gcz_profile_trace(gcz_ctx* c, float* out, uint64_t cap) {
+  if (!c) return 0;
+  const uint64_t n = c->prof_trace.size() / 3;
+  for (uint64_t i = 0; out && i < std::min(n, cap) * 3; ++i) out[i] = c->prof_trace[i];
+  return n;
 }
 
 }  // extern "C"

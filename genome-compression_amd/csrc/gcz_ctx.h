@@ -105,8 +105,9 @@ inline const char* kernel_name(int k) {
   return names[k];
 }
 
-// Leaf chunk plan (strands [chunk_start[c], chunk_start[c+1])).
-std::vector<u64> leaf_chunks(u64 S);
+// Leaf chunk plan (strands [chunk_start[c], chunk_start[c+1])): a first chunk of
+// S >> first_log2 strands, then one of the same size, then doubling.
+std::vector<u64> leaf_chunks(u64 S, int first_log2 = 6);
 
 // One node level of the build.
 struct NodeLevel {
@@ -177,12 +178,14 @@ struct gcz_ctx {
   int leaf_cap_log2 = 0;     // force the adaptive leaf table size            (GCZ_LEAF_CAP_LOG2)
   bool use_tail = true;      // fuse the top levels into one launch           (GCZ_TAIL=0 disables)
   bool use_direct = true;    // direct subtrees after a host check at layer 1 (GCZ_DIRECT=0 disables)
+  int leaf_first_log2 = 6;   // first leaf chunk = S >> this                 (GCZ_LEAF_FIRST_LOG2)
   int predup_mode = 0;       // node-insert LDS pre-dedupe: 0 auto, 1 on, 2 off  (GCZ_PREDUP)
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> event_pool;
   size_t event_used = 0;
   gcz_host::u64 prof_launches[gcz_host::KID_COUNT] = {};
   double prof_ms[gcz_host::KID_COUNT] = {};
+  std::vector<float> prof_trace;   // (kid, start ms after ev_start, duration ms) per profiled scope
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
   gcz_dist_state* dist = nullptr;   // multi-rank build state (gcz_dist.hip)
   gcz_sort_state* sortst = nullptr; // device sort / .dag writer state (gcz_sort.hip)
@@ -228,8 +231,14 @@ struct gcz_ctx {
   void prof_collect() {
     static const bool verbose = std::getenv("GCZ_PROFILE_VERBOSE") != nullptr;
     for (auto& pe : pending) {
-      float ms = 0.f;
+      float ms = 0.f, t0 = -1.f;
       (void)hipEventElapsedTime(&ms, pe.second.first, pe.second.second);
+      if (ev_start && hipEventElapsedTime(&t0, ev_start, pe.second.first) != hipSuccess) t0 = -1.f;
+      if (prof_trace.size() < (1u << 16) * 3) {
+        prof_trace.push_back(float(pe.first));
+        prof_trace.push_back(t0);
+        prof_trace.push_back(ms);
+      }
       if (verbose) std::fprintf(stderr, "gcz-prof %s %.4f\n", gcz_host::kernel_name(pe.first), double(ms));
       prof_ms[pe.first] += ms;
       prof_launches[pe.first] += 1;

@@ -27,7 +27,7 @@ using namespace gcz_dev;
 using namespace gcz_host;
 
 struct gcz_dist_state {
-  DevBuf scratch, gnf, gmul, gid, blockcnt, skey, sidx, sflag, scval, sdval;   // sender side
+  DevBuf scratch, gnf, gmul, gid, blockcnt, bchunk, skey, sidx, sflag, scval, sdval;   // sender side
   DevBuf dict;                                                                // rank 0's leaf dictionary
   DevBuf rkey, oslot, rflag, rcval, rdval, owntab, oids, omin;                // owner side
   DevBuf dhdr, gath, gath2, gathf, ddesc, tail_in;
@@ -39,7 +39,7 @@ struct gcz_dist_state {
 void gcz_dist_state_free(gcz_ctx* c) {
   gcz_dist_state* d = c->dist;
   if (!d) return;
-  for (DevBuf* b : {&d->dict, &d->scratch, &d->gnf, &d->gmul, &d->gid, &d->blockcnt, &d->skey, &d->sidx, &d->sflag,
+  for (DevBuf* b : {&d->dict, &d->scratch, &d->gnf, &d->gmul, &d->gid, &d->blockcnt, &d->bchunk, &d->skey, &d->sidx, &d->sflag,
                     &d->scval, &d->sdval, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab, &d->oids,
                     &d->omin,
                     &d->dhdr, &d->gath, &d->gath2, &d->gathf, &d->ddesc, &d->tail_in})
@@ -486,7 +486,14 @@ struct gcz_group {
   int dist_local = std::getenv("GCZ_DIST_LOCAL") ? std::atoi(std::getenv("GCZ_DIST_LOCAL")) : 0;
   // leaf dictionary: rank 0's first-occurrence keys of its first seed_chunks leaf chunks (0: off;
   // GCZ_DIST_SEED)
-  int seed_chunks = std::getenv("GCZ_DIST_SEED") ? std::atoi(std::getenv("GCZ_DIST_SEED")) : 4;
+  int seed_chunks = std::getenv("GCZ_DIST_SEED") ? std::atoi(std::getenv("GCZ_DIST_SEED")) : 1;
+  // leaf chunk plan of the ranks (first chunk S_r >> this; GCZ_DIST_LEAF_FIRST_LOG2): one
+  // chunk of S_r / 8 makes rank 0's dictionary (3.85 M of the 4.2 M distinct uniform 12-mers)
+  // in one insert / flagscan / resolve -- the other ranks wait for it -- and the seeded ranks'
+  // later chunks mostly hit settled slots, so small chunks only add launches
+  int leaf_first_log2 = std::getenv("GCZ_DIST_LEAF_FIRST_LOG2")
+                            ? std::max(1, std::min(20, std::atoi(std::getenv("GCZ_DIST_LEAF_FIRST_LOG2"))))
+                            : 3;
   bool any_predup = false;   // some rank's leaf probe found repetitive data (set by the leaf exchange)
   bool leaf_deferred = false;   // the leaf words keep local ids until layer 0's k_node_keys
   std::vector<u32> leaf_offs;   // ... and each local rank's leaf id offset
@@ -541,7 +548,7 @@ int gcz_group::alloc(int i, u64 leaf_cap) {
     else if (r == 0) nodes += P.nk[k + 1];
   }
   node_base[i][P.D] = nodes;
-  const auto chunks = leaf_chunks(S_r);
+  const auto chunks = leaf_chunks(S_r, leaf_first_log2);
   u64 tiles = 0;
   auto ntiles = [](u64 n) { return (n + scan_tile(n) - 1) / scan_tile(n); };
   for (size_t q = 0; q + 1 < chunks.size(); ++q) tiles += ntiles(chunks[q + 1] - chunks[q]);
@@ -611,8 +618,14 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     cx->prof_begin(KID_DIST, eb);
     if (!L.counted)
       hipLaunchKernelGGL(k_bucket_count, dim3(nb), dim3(kBlock), 0, cx->stream, L.src, d.blockcnt.as<u32>(), nb);
-    hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(1024), 0, cx->stream, d.blockcnt.as<u32>(), u64(R) * nb, u32(R),
-                       nb, dh->sync);
+    const u32 cpr = (nb + kScanChunk - 1) / kScanChunk;
+    if (u64(R) * cpr > 1024) return fail(GCZ_ERR_CAPACITY, "bucket scan: too many chunks");
+    if (cx->ensure(d.bchunk, u64(R) * cpr * 4 + 64)) return dev_fail("bucket scan");
+    hipLaunchKernelGGL(k_bscan_sum, dim3(R * cpr), dim3(kBlock), 0, cx->stream, d.blockcnt.as<u32>(), nb, cpr,
+                       d.bchunk.as<u32>());
+    hipLaunchKernelGGL(k_bscan_top, dim3(1), dim3(1024), 0, cx->stream, d.bchunk.as<u32>(), u32(R), cpr, dh->sync);
+    hipLaunchKernelGGL(k_bscan_down, dim3(R * cpr), dim3(kBlock), 0, cx->stream, d.blockcnt.as<u32>(), nb, cpr,
+                       d.bchunk.as<u32>());
     hipLaunchKernelGGL(k_bucket_scatter, dim3(nb), dim3(kBlock), 0, cx->stream, L.src, d.blockcnt.as<u32>(), nb,
                        d.skey.as<u64>(), d.sidx.as<u32>());
     hipLaunchKernelGGL(k_dist_pack, dim3(1), dim3(1), 0, cx->stream, cx->hdr.as<Header>(), L.ucount, L.bases, dh,
@@ -1009,7 +1022,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     // probe (kNfGlobal) and those keys never enter their local unique lists, so the leaf
     // exchange and the leaf-word translation shrink to the keys rank 0's prefix has not seen.
     // Rank 0 still sends all its keys to the owners, so any rank may go without seeding.
-    const std::vector<u64> chunks0 = leaf_chunks(P.count(0, 0));
+    const std::vector<u64> chunks0 = leaf_chunks(P.count(0, 0), leaf_first_log2);
     const int c0 = seed_chunks;
     const bool seeding = R > 1 && d_bases && c0 > 0 && int(chunks0.size()) - 1 > c0;
     std::vector<int> C(NL);
@@ -1027,7 +1040,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
       la.adaptive = leaf_cap[i] < 2 * S_r;
       la.words = cx->wa.as<u32>();
       la.out = cx->dist->scratch.as<u64>();
-      la.chunk_start = leaf_chunks(S_r);
+      la.chunk_start = leaf_chunks(S_r, leaf_first_log2);
       C[i] = int(la.chunk_start.size()) - 1;
       for (int q = 0; q < C[i]; ++q) {
         la.desc_off.push_back(dcur[i]);

@@ -140,36 +140,91 @@ static __global__ __launch_bounds__(kBlock) void k_bucket_count(RecSrc s, u32* _
   if (tid < int(s.R)) blockcnt[u64(tid) * nb + blockIdx.x] = h[tid];
 }
 
-// One block: exclusive scan of blockcnt[R * nb] (destination-major) in place;
-// per-destination totals into tot[0..R).
-static __global__ __launch_bounds__(1024) void k_bucket_scan(u32* __restrict__ a, u64 N, u32 R, u32 nb,
-                                                             u64* __restrict__ tot) {
+// Exclusive scan of blockcnt[R * nb] (destination-major) in place, per-destination totals
+// into tot[0..R): each destination row is cut into chunks of kScanChunk entries; pass 1 sums
+// every chunk, pass 2 (one block) scans the R * cpr chunk sums, pass 3 rescans each chunk from
+// its offset.  Coalesced and spread over R * cpr blocks (a one-block scan of the 81 K counts of
+// a 1 Gbase leaf level took 130 us).
+constexpr u32 kScanChunk = 16 * kBlock;
+
+__device__ __forceinline__ u32 wave_incl_scan(u32 v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u32 t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+static __global__ __launch_bounds__(kBlock) void k_bscan_sum(const u32* __restrict__ a, u32 nb, u32 cpr,
+                                                             u32* __restrict__ csum) {
+  __shared__ u32 ws[kBlock / 64];
+  const u32 row = blockIdx.x / cpr, c = blockIdx.x % cpr;
+  const u32* r = a + u64(row) * nb;
+  const u32 j1 = min((c + 1) * kScanChunk, nb);
+  u32 v = 0;
+  for (u32 j = c * kScanChunk + threadIdx.x; j < j1; j += kBlock) v += r[j];
+  const int lane = threadIdx.x & 63;
+  v = wave_incl_scan(v, lane);
+  if (lane == 63) ws[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u32 t = 0;
+    for (int w = 0; w < kBlock / 64; ++w) t += ws[w];
+    csum[blockIdx.x] = t;
+  }
+}
+
+// One block of 1024 threads, R * cpr <= 1024 chunk sums -> exclusive chunk offsets (global
+// over the destination-major order), row totals.
+static __global__ __launch_bounds__(1024) void k_bscan_top(u32* __restrict__ csum, u32 R, u32 cpr,
+                                                           u64* __restrict__ tot) {
   __shared__ u32 part[1024];
-  const int tid = threadIdx.x;
-  const u64 per = (N + 1023) / 1024;
-  const u64 b0 = u64(tid) * per, b1 = b0 + per < N ? b0 + per : N;
+  __shared__ u32 ws[1024 / 64];
+  const u32 n = R * cpr, tid = threadIdx.x;
+  const int lane = tid & 63;
+  const u32 v = tid < n ? csum[tid] : 0u;
+  const u32 inc = wave_incl_scan(v, lane);
+  if (lane == 63) ws[tid >> 6] = inc;
+  __syncthreads();
+  u32 add = 0;
+  for (u32 w = 0; w < (tid >> 6); ++w) add += ws[w];
+  part[tid] = inc + add - v;   // exclusive
+  __syncthreads();
+  if (tid < n) csum[tid] = part[tid];
+  if (tid < R) {
+    u32 all = 0;
+    for (u32 w = 0; w < 1024 / 64; ++w) all += ws[w];
+    const u32 s0 = part[tid * cpr];
+    const u32 s1 = tid + 1 < R ? part[(tid + 1) * cpr] : all;
+    tot[tid] = u64(s1 - s0);
+  }
+}
+
+static __global__ __launch_bounds__(kBlock) void k_bscan_down(u32* __restrict__ a, u32 nb, u32 cpr,
+                                                              const u32* __restrict__ coff) {
+  constexpr int kPer = kScanChunk / kBlock;
+  __shared__ u32 ws[kBlock / 64];
+  const u32 row = blockIdx.x / cpr, c = blockIdx.x % cpr;
+  u32* r = a + u64(row) * nb;
+  const u32 j0 = c * kScanChunk + threadIdx.x * kPer;
+  u32 x[kPer];
   u32 sum = 0;
-  for (u64 i = b0; i < b1; ++i) sum += a[i];
-  part[tid] = sum;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {   // Hillis-Steele inclusive scan
-    const u32 v = tid >= o ? part[tid - o] : 0u;
-    __syncthreads();
-    part[tid] += v;
-    __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    x[i] = j0 + i < nb ? r[j0 + i] : 0u;
+    sum += x[i];
   }
-  u32 run = part[tid] - sum;
-  for (u64 i = b0; i < b1; ++i) {
-    const u32 v = a[i];
-    a[i] = run;
-    run += v;
-  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const u32 inc = wave_incl_scan(sum, lane);
+  if (lane == 63) ws[wave] = inc;
   __syncthreads();
-  if (tid < int(R)) {
-    const u64 i0 = u64(tid) * nb, i1 = u64(tid + 1) * nb;
-    const u32 start = i0 < N ? a[i0] : part[1023];
-    const u32 end = i1 < N ? a[i1] : part[1023];
-    tot[tid] = u64(end - start);
+  u32 run = coff[blockIdx.x] + inc - sum;
+  for (int w = 0; w < wave; ++w) run += ws[w];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    if (j0 + i < nb) r[j0 + i] = run;
+    run += x[i];
   }
 }
 

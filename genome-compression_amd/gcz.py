@@ -70,6 +70,7 @@ _SIGS = {
     "gcz_profile_entry": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                           ctypes.POINTER(_U64), ctypes.POINTER(ctypes.c_double)]),
     "gcz_profile_reset": (None, [_P]),
+    "gcz_profile_trace": (_U64, [_P, _P, _U64]),
     "gcz_tree_new": (_P, []),
     "gcz_tree_free": (None, [_P]),
     "gcz_tree_fetch": (ctypes.c_int, [_P, _P]),
@@ -449,6 +450,15 @@ class Context:
             out[name.value.decode()] = {"launches": int(n.value), "total_ms": float(ms.value)}
             k += 1
         return out
+
+    def profile_trace(self) -> list:
+        """Profiled scopes since the last reset, in stream order: (name, start ms after the
+        build's start event, duration ms)."""
+        names = list(self.profile_table())
+        n = int(_lib.gcz_profile_trace(self._h, None, 0))
+        buf = np.empty(max(3 * n, 3), dtype=np.float32)
+        n = min(n, int(_lib.gcz_profile_trace(self._h, _ptr(buf), n)))
+        return [(names[int(buf[3 * i])], float(buf[3 * i + 1]), float(buf[3 * i + 2])) for i in range(n)]
 
 
 # ---- multi-rank build -----------------------------------------------------------

@@ -119,6 +119,10 @@ GCZ_API int gcz_profile_enable(gcz_ctx *ctx, int on);
 /* Kernel `k` of the profile table: name, launches, total ms.  Returns 0, or -1 past the end. */
 GCZ_API int gcz_profile_entry(gcz_ctx *ctx, int k, const char **name, uint64_t *launches, double *total_ms);
 GCZ_API void gcz_profile_reset(gcz_ctx *ctx);
+/* Timeline of the profiled scopes since the last reset: entry i is out[3i..3i+2] =
+ * (kernel index as in gcz_profile_entry, start in ms after the build's start event,
+ * duration in ms).  Copies min(count, cap) entries; returns the count. */
+GCZ_API uint64_t gcz_profile_trace(gcz_ctx *ctx, float *out, uint64_t cap);
 
 /* ---- host tree (shared_tree container operations) ---------------------- */
 GCZ_API gcz_tree *gcz_tree_new(void);

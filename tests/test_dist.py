@@ -263,7 +263,7 @@ def test_dist_default_depth(world, name, gcz, manifest, groups):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", ["1", "4", "0"])
+@pytest.mark.parametrize("seed", ["1", "2", "0"])
 @pytest.mark.parametrize("world", [2, 3, 8])
 def test_dist_leaf_dictionary(seed, world, gcz, manifest, oracle, monkeypatch):
     """Rank 0's leaf dictionary (GCZ_DIST_SEED = its first chunks; 0 = off) on small inputs:
