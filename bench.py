@@ -73,7 +73,7 @@ def load_gcz():
     return mod
 
 
-def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None):
+def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None, bucketed_pairs=0):
     """Algorithmic HBM bytes of all launches of `kernel` in one build:
     streamed bytes + one 64-B sector per random table/group access."""
     pk = []
@@ -88,8 +88,21 @@ def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None):
     if kernel == "leaf_insert":     # ASCII in, provisional word out, one table sector per strand
         return S * L + 4 * S + 64 * S
     if kernel == "node_insert":     # pair + child marks in, word out; table sector per hashed pair
-        hashed = hashed_pairs if hashed_pairs is not None else sum(pk)
+        hashed = (hashed_pairs if hashed_pairs is not None else sum(pk)) - bucketed_pairs
+        if hashed <= 0:             # every hashed level went through the buckets: gate-only launches
+            return 0
         return sum(8 * p + 4 * p + 4 * p for p in pk) + 64 * hashed
+    # bucketed node insert (non-repetitive data, levels of >= 2^20 pairs: layer 0 of
+    # uniform_1g): bp = hashed pairs that went through the buckets
+    bp = bucketed_pairs
+    if kernel == "bucket_count":    # pair in (and the per-chunk bucket counts out)
+        return 8 * bp + 4 * (bp // 3072 + 1) * ((bp >> 16) + 1)
+    if kernel == "bucket_scan":     # exclusive scan of the count matrix
+        return 8 * (bp // 3072 + 1) * ((bp >> 16) + 1)
+    if kernel == "bucket_scatter":  # pair in, word out, one 8-B record store (a 64-B sector) per pair
+        return 12 * bp + 64 * bp
+    if kernel == "bucket_dedupe":   # records in; repeats: mark + word sectors
+        return 8 * bp + 128 * max(0, bp - (layer_sizes[0] if layer_sizes else bp))
     if kernel == "flagscan_leaf":   # not-first marks; firsts: word, slot sector, leaf out, slot->id sector
         return S + U * (4 + 64 + 8 + 64 + 4)
     if kernel == "flagscan_node":   # not-first marks, group records; firsts: pair re-read, node out, word
@@ -367,7 +380,8 @@ def main():
             continue
         # per-rank share of the algorithmic bytes (rank 0 profiled); exchange/dist phases carry none
         b = algorithmic_bytes(name, L, S, info["n_leaves"], info["layer_size"],
-                              info["hashed_pairs"] if mode in ("single", "replicas") else None) // share
+                              info["hashed_pairs"] if mode in ("single", "replicas") else None,
+                              info.get("bucketed_pairs", 0)) // share
         kernels[name] = {"launches": p["launches"], "total_ms": round(p["total_ms"], 4),
                          "avg_ms": p["total_ms"] / p["launches"], "alg_bytes": b,
                          "gbs": b / (p["total_ms"] * 1e-3) / 1e9 if p["total_ms"] > 0 else None}
@@ -465,7 +479,7 @@ def main():
         line = {
             "metric": METRIC, "value": value, "unit": "bases/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "weak" if (weak or mode == "replicas") else "strong",
+            "scaling": "weak" if (args.mode in ("weak", "replicas") and mode != "virtual") else "strong",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "config": {"workload": args.config, "nbases": nbases * (world if mode == "replicas" else 1),
                        "per_gpu_nbases": nbases // world if mode == "dist" else nbases, "L": L,

@@ -1,6 +1,8 @@
 // MI355X (gfx950) shared_tree construction: host orchestration and the C ABI.
 // Device code and the algorithm description: gcz_device.h; the multi-rank
 // build: gcz_dist.hip.
+#include <hipcub/hipcub.hpp>
+
 #include "gcz_ctx.h"
 
 using namespace gcz_dev;
@@ -154,7 +156,8 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     prof_begin(KID_NODE, e0);
     const dim3 gi(unsigned((p + kBlock - 1) / kBlock));
     hipLaunchKernelGGL((k_node_insert<WideTab>), gi, dim3(kBlock), 0, stream, a.in, n, p, WideTab{}, nullptr, nullptr,
-                       a.words, Marks{knf, multi_set[cur]}, d_hdr, a.pcount, a.out, a.count, a.id_off, stats.as<u64>());
+                       a.words, Marks{knf, multi_set[cur]}, d_hdr, a.pcount, a.out, a.count, a.id_off, stats.as<u64>(),
+                       0u);
     HIP_TRY(hipGetLastError());
     prof_end(KID_NODE, e0);
     return GCZ_OK;
@@ -163,24 +166,67 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   const unsigned char* pnf = a.prev_marks ? nf_set[prev] : nullptr;
   const unsigned char* pmu = a.prev_marks ? multi_set[prev] : nullptr;
   Group* d_grp = grp.as<Group>();
+  // bucketed insert (decided on the device: hdr->predup == 0) when the buckets average
+  // <= 3072 pairs (the LDS dedupe holds 6144) and a record fits 8 bytes
+  BktPlan bp{};
+  bp.T = nt.pt;
+  bp.K = 2 * (Bk + 3);
+  while (bp.bb < u32(kBktMaxLog) && (p >> bp.bb) > 3072) ++bp.bb;
+  const u32 bkt = a.allow_bucket && bucket_now && nt.packed && p >= bucket_min && (p >> bp.bb) <= 3072 &&
+                  bp.K >= bp.bb && bp.K - bp.bb + kBktRP <= 64 &&
+                  p <= u64(kBktMaxG) * kBktChunk ? 1u : 0u;
+  const u32 bb = bp.bb;
+  const u64 G = (p + kBktChunk - 1) / kBktChunk;
+  const u64 ncnt = (u64(1) << bb) * G + 1;
+  size_t scan_bytes = 0;
+  if (bkt) {
+    int rc;
+    if ((rc = ensure(bkt_key, p * 8)) || (rc = ensure(bkt_cnt, ncnt * 4)) ||
+        (rc = ensure(bkt_off, ncnt * 4)))
+      return rc;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, bkt_cnt.as<u32>(), bkt_off.as<u32>(), ncnt, stream));
+    if ((rc = ensure(bkt_tmp, scan_bytes))) return rc;
+  }
   hipEvent_t e0{};
   prof_begin(KID_MEMSET, e0);
   {
     const u64 tab16 = nt.bytes() / 16, p16 = (p + 15) / 16;
     const u64 blocks = std::min<u64>(4096, (std::max(tab16, p16) + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_clear, dim3(unsigned(blocks)), dim3(kBlock), 0, stream, static_cast<uint4*>(tab.ptr),
-                       tab16, reinterpret_cast<uint4*>(knf), reinterpret_cast<uint4*>(mk.multi), p16, a.pcount, n);
+                       tab16, reinterpret_cast<uint4*>(knf), reinterpret_cast<uint4*>(mk.multi), p16, a.pcount, n,
+                       d_hdr, bkt);
     HIP_TRY(hipGetLastError());
   }
   prof_end(KID_MEMSET, e0);
-  prof_begin(KID_NODE, e0);
   const dim3 gi(unsigned((p + kBlock - 1) / kBlock));
+  if (bkt) {
+    prof_begin(KID_BKT_COUNT, e0);
+    hipLaunchKernelGGL(k_bkt_count, dim3(unsigned(G)), dim3(kBktThreads), 0, stream, a.in, n, p, pnf, pmu, bp,
+                       bkt_cnt.as<u32>(), G, d_hdr, a.pcount, stats.as<u64>());
+    HIP_TRY(hipGetLastError());
+    prof_end(KID_BKT_COUNT, e0);
+    prof_begin(KID_BKT_SCAN, e0);
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(bkt_tmp.ptr, scan_bytes, bkt_cnt.as<u32>(), bkt_off.as<u32>(), ncnt,
+                                             stream));
+    prof_end(KID_BKT_SCAN, e0);
+    prof_begin(KID_BKT_SCATTER, e0);
+    hipLaunchKernelGGL(k_bkt_scatter, dim3(unsigned(G)), dim3(kBktThreads), 0, stream, a.in, n, p, pnf, pmu, bp,
+                       bkt_off.as<u32>(), G, bkt_key.as<u64>(), a.words, d_hdr, a.pcount);
+    HIP_TRY(hipGetLastError());
+    prof_end(KID_BKT_SCATTER, e0);
+    prof_begin(KID_BKT_DEDUPE, e0);
+    hipLaunchKernelGGL(k_bkt_dedupe, dim3(1u << bb), dim3(kBktThreads), 0, stream, bkt_off.as<u32>(), G,
+                       bkt_key.as<u64>(), a.words, mk, d_hdr, a.pcount, n);
+    HIP_TRY(hipGetLastError());
+    prof_end(KID_BKT_DEDUPE, e0);
+  }
+  prof_begin(KID_NODE, e0);
   if (nt.packed)
     hipLaunchKernelGGL((k_node_insert<PackedTab>), gi, dim3(kBlock), 0, stream, a.in, n, p, nt.pt, pnf, pmu,
-                       a.words, mk, d_hdr, a.pcount, a.out, a.count, a.id_off, stats.as<u64>());
+                       a.words, mk, d_hdr, a.pcount, a.out, a.count, a.id_off, stats.as<u64>(), bkt);
   else
     hipLaunchKernelGGL((k_node_insert<WideTab>), gi, dim3(kBlock), 0, stream, a.in, n, p, nt.wt, pnf, pmu,
-                       a.words, mk, d_hdr, a.pcount, a.out, a.count, a.id_off, stats.as<u64>());
+                       a.words, mk, d_hdr, a.pcount, a.out, a.count, a.id_off, stats.as<u64>(), bkt);
   HIP_TRY(hipGetLastError());
   prof_end(KID_NODE, e0);
   prof_begin(KID_FLAGSCAN_NODE, e0);
@@ -197,10 +243,10 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   prof_begin(KID_RESOLVE_NODE, e0);
   if (nt.packed)
     hipLaunchKernelGGL((k_resolve_node<PackedTab>), gi, dim3(kBlock), 0, stream, a.words, p, nt.pt, knf, d_grp,
-                       a.pcount, n, a.count, a.hashed_next, a.gate);
+                       a.pcount, n, a.count, a.hashed_next, a.gate, d_hdr, bkt);
   else
     hipLaunchKernelGGL((k_resolve_node<WideTab>), gi, dim3(kBlock), 0, stream, a.words, p, nt.wt, knf, d_grp,
-                       a.pcount, n, a.count, a.hashed_next, a.gate);
+                       a.pcount, n, a.count, a.hashed_next, a.gate, d_hdr, bkt);
   HIP_TRY(hipGetLastError());
   prof_end(KID_RESOLVE_NODE, e0);
   return GCZ_OK;
@@ -297,6 +343,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   }
 
   allow_packed = !force_wide;
+  bucket_now = use_bucket;
   for (;;) {
     if ((rc = ensure(tab, std::max(leaf_cap, node_cap0) * 16))) return rc;
     HIP_TRY(hipEventRecord(ev_start, stream));
@@ -366,6 +413,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       na.ticket = &d_hdr->ticket[kLayerSlot + k];
       na.hashed_next = &d_hdr->hashed_next[k];   // look-ahead for layer k + 1 (its pairs' children are here)
       na.gate = &d_hdr->gate[k];
+      na.allow_bucket = true;
       if ((rc = node_level(na, d_hdr))) return rc;
       prev_regular = true;
       std::swap(in, outw);
@@ -385,6 +433,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       HIP_TRY(hipGetLastError());
     }
     hipLaunchKernelGGL(k_stats_sum, dim3(1), dim3(1024), 0, stream, stats.as<u64>(), &d_hdr->hashed[0]);
+    hipLaunchKernelGGL(k_stats_sum, dim3(1), dim3(1024), 0, stream, stats.as<u64>() + 1, &d_hdr->hashed[1]);
     HIP_TRY(hipEventRecord(ev_stop, stream));
     HIP_TRY(hipMemcpyAsync(h_hdr, d_hdr, sizeof(Header), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
@@ -392,6 +441,10 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     HIP_TRY(hipEventElapsedTime(&ms, ev_start, ev_stop));
     info.build_ms = ms;
     if (profile) prof_collect();
+    if (h_hdr->bkt_overflow && bucket_now) {      // a hot key overflowed a bucket: rebuild with the table
+      bucket_now = false;
+      continue;
+    }
     if (h_hdr->leaf_overflow && la.adaptive) {    // leaf table too small: grow and rebuild
       leaf_cap = std::min(full_cap, leaf_cap * 8);
       continue;
@@ -420,6 +473,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   for (int k = 0; k < D; ++k) info.layer_size[k] = h_hdr->count[kLayerSlot + k];
   info.root = h_hdr->root;
   for (int i = 0; i < 64; ++i) info.hashed_pairs += h_hdr->hashed[i];
+  info.bucketed_pairs = h_hdr->hashed[1];
   return GCZ_OK;
 }
 
@@ -445,6 +499,8 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   if (const char* t = std::getenv("GCZ_TAIL")) c->use_tail = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_DIRECT")) c->use_direct = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_PREDUP")) c->predup_mode = std::atoi(t);   // 1 on, 2 off, 0 auto
+  if (const char* t = std::getenv("GCZ_BUCKET")) c->use_bucket = std::atoi(t) != 0;
+  if (const char* t = std::getenv("GCZ_BUCKET_MIN")) c->bucket_min = std::strtoull(t, nullptr, 10);
   if (const char* t = std::getenv("GCZ_LEAF_FIRST_LOG2")) c->leaf_first_log2 = std::max(1, std::min(20, std::atoi(t)));
   *out = c;
   return GCZ_OK;

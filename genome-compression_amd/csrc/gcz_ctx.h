@@ -96,12 +96,14 @@ inline LevelTab plan_table(void* buf, u64 cap, u32 K, u64 npos, u32 B, bool allo
 
 enum KernelId {
   KID_LEAF, KID_NODE, KID_FLAGSCAN_LEAF, KID_FLAGSCAN_NODE, KID_RESOLVE_LEAF, KID_RESOLVE_NODE, KID_MEMSET,
-  KID_EXCHANGE, KID_DIST, KID_OWNER, KID_IDS, KID_REMAP, KID_TAIL, KID_SORT, KID_DAG, KID_DIRECT, KID_COUNT
+  KID_EXCHANGE, KID_DIST, KID_OWNER, KID_IDS, KID_REMAP, KID_TAIL, KID_SORT, KID_DAG, KID_DIRECT,
+  KID_BKT_COUNT, KID_BKT_SCAN, KID_BKT_SCATTER, KID_BKT_DEDUPE, KID_COUNT
 };
 inline const char* kernel_name(int k) {
   static const char* names[KID_COUNT] = {"leaf_insert", "node_insert", "flagscan_leaf", "flagscan_node",
                                          "resolve_leaf", "resolve_node", "clear", "exchange", "dist_bucket",
-                                         "dist_owner", "dist_ids", "dist_remap", "tail", "sort", "dag_write", "direct_levels"};
+                                         "dist_owner", "dist_ids", "dist_remap", "tail", "sort", "dag_write", "direct_levels",
+                                         "bucket_count", "bucket_scan", "bucket_scatter", "bucket_dedupe"};
   return names[k];
 }
 
@@ -126,6 +128,7 @@ struct NodeLevel {
   u32* ticket = nullptr;
   u32* hashed_next = nullptr;       // single-device build: look ahead for the next level (null: off)
   u64* gate = nullptr;              // ... and open its gate (the next level's pcount)
+  bool allow_bucket = false;        // single-device build: bucketed insert allowed (overflow -> rebuild)
 };
 
 // One leaf level (all chunks).
@@ -163,6 +166,7 @@ struct gcz_ctx {
   std::string last_error;
   gcz_host::DevBuf wa, wb, grp, desc, tab, leaves_out, nodes_out, hdr, input, nf, multi;
   gcz_host::DevBuf stats;   // hashed-pair counter shards (k_node_insert), summed into hdr->hashed[0]
+  gcz_host::DevBuf bkt_key, bkt_cnt, bkt_off, bkt_tmp;   // bucketed node insert (k_bkt_*)
   gcz_dev::Header* h_hdr = nullptr;   // pinned
   unsigned char* nf_set[2] = {nullptr, nullptr};      // marks, even / odd layers
   unsigned char* multi_set[2] = {nullptr, nullptr};
@@ -180,6 +184,9 @@ struct gcz_ctx {
   bool use_direct = true;    // direct subtrees after a host check at layer 1 (GCZ_DIRECT=0 disables)
   int leaf_first_log2 = 6;   // first leaf chunk = S >> this                 (GCZ_LEAF_FIRST_LOG2)
   int predup_mode = 0;       // node-insert LDS pre-dedupe: 0 auto, 1 on, 2 off  (GCZ_PREDUP)
+  bool use_bucket = true;    // bucketed LDS node insert on non-repetitive data  (GCZ_BUCKET=0 disables)
+  gcz_host::u64 bucket_min = 1ull << 20;   // ... on levels of at least this many pairs (GCZ_BUCKET_MIN)
+  bool bucket_now = true;    // this build (cleared after a bucket overflow: rebuild with the table)
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> event_pool;
   size_t event_used = 0;

@@ -86,7 +86,7 @@ struct Header {
   u32 overflow;            // a node-level probe bound was exceeded
   u32 leaf_overflow;       // the (adaptively sized) leaf table was too small
   u32 root;
-  u32 pad;
+  u32 bkt_overflow;         // a node-level bucket exceeded the LDS dedupe (k_bkt_dedupe)
 };
 
 // ---- word algebra: reference src/shared_tree.cpp:76-107 --------------------
@@ -549,7 +549,7 @@ __global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ 
                                                        u32* __restrict__ rec, Marks mk,
                                                        Header* __restrict__ hdr, const u64* prev_count,
                                                        uint2* __restrict__ out, u64* __restrict__ count_out,
-                                                       u32 id_off, u64* __restrict__ stats) {
+                                                       u32 id_off, u64* __restrict__ stats, u32 bkt) {
   if (level_direct(prev_count, n)) {
     const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
     if (j == 0) *count_out = p;
@@ -564,6 +564,7 @@ __global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ 
     rec[j] = make_word(u32(j) + id_off, m, t, v);   // id_off: first pair of this rank (multi-rank build)
     return;
   }
+  if (bkt && hdr->predup == 0) return;   // k_bkt_* insert this level
   // Repetitive data (hdr->predup, decided from the first leaf chunk): repeats of a
   // key inside the block collapse onto its earliest position first, in an LDS
   // table; only that representative touches the HBM table, the others are not
@@ -854,7 +855,8 @@ __global__ __launch_bounds__(kBlock) void k_resolve_node(u32* __restrict__ words
                                                         const unsigned char* __restrict__ nf,
                                                         const Group* __restrict__ grp, const u64* prev_count,
                                                         u64 n, const u64* __restrict__ count,
-                                                        const u32* __restrict__ hashed_next, u64* __restrict__ gate) {
+                                                        const u32* __restrict__ hashed_next, u64* __restrict__ gate,
+                                                        const Header* __restrict__ hdr, u32 bkt) {
   if (gate && blockIdx.x == 0 && threadIdx.x == 0)
     *gate = (*count == p || (hashed_next && *hashed_next == 0)) ? p : ~0ull;
   if (level_direct(prev_count, n)) return;
@@ -863,10 +865,220 @@ __global__ __launch_bounds__(kBlock) void k_resolve_node(u32* __restrict__ words
   const u32 w = words[j];
   u64 key;
   u32 q;
-  T.read(w & kIdx, key, q);                     // q = the key's first position
+  if (bkt && hdr->predup == 0) q = w & kIdx;    // bucketed insert: the word holds it
+  else T.read(w & kIdx, key, q);                // q = the key's first position
   const Group h = grp[q >> 6];
   const u32 id = h.prefix + u32(__popcll(h.mask & ((1ull << (q & 63)) - 1)));
   words[j] = id | (w & kBits);
+}
+
+// ---- bucketed node insert (non-repetitive data) ---------------------------------------
+// Same marks and ids as k_node_insert's table, with no HBM-resident table: the hashed
+// pairs of a level are partitioned by the top bits of a hash of their canonical key into
+// nb = 2^bb buckets (count -> column-major count matrix -> exclusive scan -> scatter), and
+// each bucket (all occurrences of its keys) is deduplicated by one workgroup in LDS.
+// Repeats get nf = not-first and their key's first position in the word (k_resolve_node
+// reads it instead of a table slot); a key's first occurrence is marked multi.  Runs only
+// when hdr->predup == 0 (a hot key would overflow its bucket: hdr->bkt_overflow, and the
+// host rebuilds with the table).  One 8-B record per hashed pair: the packed table's
+// K-bit key mix h (a bijection, so equal h <=> equal key) without its top bb bits (the
+// bucket), above the pair's 16-bit offset in its count chunk (chunk g of a record at
+// index i of bucket b: the last g with off[b * G + g] <= i); the host takes this path
+// only when K - bb + 16 <= 64.
+constexpr int kBktThreads = 1024;
+constexpr int kBktItems = 64;                        // pairs per thread of count / scatter
+constexpr u64 kBktChunk = u64(kBktThreads) * kBktItems;   // pairs per count-matrix column (2^16)
+constexpr u32 kBktRP = 16;                          // record offset bits
+constexpr int kBktMaxG = 8192;                      // count chunks (p < 2^29)
+constexpr int kBktMaxLog = 14;                       // nb <= 16384 (LDS counters, 64 KB)
+constexpr int kBktSlotsLog = 13;                     // LDS table of the dedupe: 8192 slots
+constexpr int kBktCapItems = 6;                      // ... holding a bucket of <= 6144 pairs
+constexpr int kBktCap = kBktThreads * kBktCapItems;
+
+__device__ __forceinline__ u64 bkt_hash(u64 k) {     // murmur3 fmix64
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+struct BktPlan {
+  PackedTab T;   // key encoding and mix of this level
+  u32 K, bb;     // key bits, bucket bits
+  __device__ __forceinline__ u32 bucket(u64 h) const { return bb ? u32(h >> (K - bb)) : 0u; }
+};
+
+// Pair j of a level: canonical key, word bits, and whether it goes through the dedupe
+// (a pair with a child that occurs once in the previous level is itself unique).
+__device__ __forceinline__ bool bkt_pair(const u32* __restrict__ in, u64 n, u64 j,
+                                         const unsigned char* __restrict__ prev_nf,
+                                         const unsigned char* __restrict__ prev_multi, const BktPlan& bp,
+                                         u64& key, u32& bits) {
+  u32 l, r, cl, cr, m, t;
+  load_pair(in, n, j, l, r);
+  node_canonical(l, r, cl, cr, m, t);
+  const u32 v = ulw(l) == ulw(xf(r, 1, 0));   // left == right.mirrored() (shared_tree.cpp:670)
+  bits = make_word(0, m, t, v);
+  key = bp.T.mix(bp.T.node_key(cl, cr));   // K bits
+  if (!prev_nf) return true;
+  if (2 * j + 1 < n) {
+    const uchar2 f = reinterpret_cast<const uchar2*>(prev_nf)[j];
+    const uchar2 g = reinterpret_cast<const uchar2*>(prev_multi)[j];
+    return !((f.x == 0 && g.x == 0) || (f.y == 0 && g.y == 0));
+  }
+  return !(prev_nf[2 * j] == 0 && prev_multi[2 * j] == 0);
+}
+
+// Count chunk of a workgroup: the 8 XCDs (workgroups dealt round-robin) each take a
+// contiguous run of chunks, so the neighbouring count-matrix entries and the neighbouring
+// record runs of a bucket (chunk g, then g + 1, ...) are written and read through one
+// XCD's L2 and merge there into whole lines.
+__device__ __forceinline__ u64 bkt_chunk(u64 G) {
+  const u64 b = blockIdx.x, per = G / 8;
+  return b < 8 * per ? (b % 8) * per + b / 8 : b;
+}
+
+__device__ __forceinline__ bool bkt_skip(const Header* hdr, const u64* prev_count, u64 n) {
+  return level_direct(prev_count, n) || hdr->predup != 0;
+}
+
+// Column g of the count matrix: cnt[b * G + g] = hashed pairs of chunk g in bucket b.
+[[maybe_unused]] static __global__ __launch_bounds__(kBktThreads) void k_bkt_count(const u32* __restrict__ in, u64 n, u64 p,
+                                                          const unsigned char* __restrict__ prev_nf,
+                                                          const unsigned char* __restrict__ prev_multi, BktPlan bp,
+                                                          u32* __restrict__ cnt, u64 G, const Header* __restrict__ hdr,
+                                                          const u64* prev_count, u64* __restrict__ stats) {
+  if (bkt_skip(hdr, prev_count, n)) return;
+  __shared__ u32 hist[1 << kBktMaxLog];
+  __shared__ u32 s_hashed;
+  const u32 nb = 1u << bp.bb;
+  for (u32 q = threadIdx.x; q < nb; q += kBktThreads) hist[q] = 0;
+  if (threadIdx.x == 0) s_hashed = 0;
+  __syncthreads();
+  const u64 g = bkt_chunk(G), j0 = g * kBktChunk;
+  u32 hashed = 0;
+#pragma unroll 4
+  for (int e = 0; e < kBktItems; ++e) {
+    const u64 j = j0 + u64(e) * kBktThreads + threadIdx.x;
+    if (j >= p) break;
+    u64 key;
+    u32 bits;
+    if (bkt_pair(in, n, j, prev_nf, prev_multi, bp, key, bits)) {
+      atomicAdd(&hist[bp.bucket(key)], 1u);
+      ++hashed;
+    }
+  }
+  const u64 wsum = wave_sum(u64(hashed));
+  if ((threadIdx.x & 63) == 0 && wsum) atomicAdd(&s_hashed, u32(wsum));
+  __syncthreads();
+  for (u32 q = threadIdx.x; q < nb; q += kBktThreads) cnt[u64(q) * G + g] = hist[q];
+  if (g == 0 && threadIdx.x == 0) cnt[u64(nb) * G] = 0;   // the scan's total lands here
+  if (threadIdx.x == 0 && s_hashed)   // second word of each shard line: bucketed pairs
+    atomicAdd(&stats[(blockIdx.x & (kStatShards - 1)) * kStatStride + 1], u64(s_hashed));
+}
+
+// Same chunks as k_bkt_count; off = exclusive scan of cnt.  Writes every pair's
+// provisional word (position field 0) and the hashed pairs' (key, position) records.
+[[maybe_unused]] static __global__ __launch_bounds__(kBktThreads) void k_bkt_scatter(const u32* __restrict__ in, u64 n, u64 p,
+                                                            const unsigned char* __restrict__ prev_nf,
+                                                            const unsigned char* __restrict__ prev_multi, BktPlan bp,
+                                                            const u32* __restrict__ off, u64 G, u64* __restrict__ rrec,
+                                                            u32* __restrict__ rec, const Header* __restrict__ hdr,
+                                                            const u64* prev_count) {
+  if (bkt_skip(hdr, prev_count, n)) return;
+  __shared__ u32 cur[1 << kBktMaxLog];
+  const u32 nb = 1u << bp.bb;
+  const u64 g = bkt_chunk(G), j0 = g * kBktChunk;
+  const u64 lowmask = bp.K - bp.bb >= 64 ? ~0ull : (1ull << (bp.K - bp.bb)) - 1;
+  for (u32 q = threadIdx.x; q < nb; q += kBktThreads) cur[q] = off[u64(q) * G + g];
+  __syncthreads();
+#pragma unroll 4
+  for (int e = 0; e < kBktItems; ++e) {
+    const u64 j = j0 + u64(e) * kBktThreads + threadIdx.x;
+    if (j >= p) break;
+    u64 key;
+    u32 bits;
+    if (bkt_pair(in, n, j, prev_nf, prev_multi, bp, key, bits)) {
+      const u32 d = atomicAdd(&cur[bp.bucket(key)], 1u);
+      rrec[d] = ((key & lowmask) << kBktRP) | (j - j0);
+    }
+    rec[j] = bits;
+  }
+}
+
+// One workgroup per bucket (at most kBktCap records, else hdr->bkt_overflow and the host
+// rebuilds with the table): an LDS hash-cons of its records, then marks and first
+// positions for the keys that occur more than once.
+__device__ __forceinline__ u32 bkt_pos(const u32* s_off, u64 G, u32 i, u64 r) {
+  u32 lo = 0, hi = u32(G) - 1;   // chunk of record i: the last g with s_off[g] <= i
+  while (lo < hi) {
+    const u32 mid = (lo + hi + 1) >> 1;
+    if (s_off[mid] <= i) lo = mid;
+    else hi = mid - 1;
+  }
+  return (lo << kBktRP) | u32(r & ((1u << kBktRP) - 1));
+}
+
+[[maybe_unused]] static __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe(const u32* __restrict__ off, u64 G,
+                                                           const u64* __restrict__ rrec,
+                                                           u32* __restrict__ rec, Marks mk, Header* __restrict__ hdr,
+                                                           const u64* prev_count, u64 n) {
+  if (bkt_skip(hdr, prev_count, n)) return;
+  constexpr u32 TS = 1u << kBktSlotsLog;
+  __shared__ u64 s_key[TS];
+  __shared__ u32 s_pos[TS];
+  __shared__ u32 s_dup[TS / 32];
+  __shared__ u32 s_off[kBktMaxG];
+  const u64 b = blockIdx.x;
+  const u32 start = off[b * G], end = off[(b + 1) * G];
+  if (end - start > u32(kBktCap)) {   // a hot key: the table path handles this data
+    if (threadIdx.x == 0) hdr->bkt_overflow = 1;
+    return;
+  }
+  for (u32 q = threadIdx.x; q < G; q += kBktThreads) s_off[q] = off[b * G + q];
+  for (u32 q = threadIdx.x; q < TS; q += kBktThreads) {
+    s_key[q] = kEmpty;
+    s_pos[q] = ~0u;
+  }
+  for (u32 q = threadIdx.x; q < TS / 32; q += kBktThreads) s_dup[q] = 0;
+  u64 key[kBktCapItems], raw[kBktCapItems];
+  u32 pos[kBktCapItems], slot[kBktCapItems];
+#pragma unroll
+  for (int e = 0; e < kBktCapItems; ++e) {
+    const u32 i = start + u32(e) * kBktThreads + threadIdx.x;
+    raw[e] = i < end ? rrec[i] : 0ull;
+    key[e] = i < end ? raw[e] >> kBktRP : kEmpty;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < kBktCapItems; ++e) {
+    if (key[e] == kEmpty) continue;
+    pos[e] = bkt_pos(s_off, G, start + u32(e) * kBktThreads + threadIdx.x, raw[e]);
+    u32 h = u32(bkt_hash(key[e])) & (TS - 1);
+    for (;;) {
+      unsigned long long c = s_key[h];
+      if (c == kEmpty) c = atomicCAS(&s_key[h], kEmpty, (unsigned long long)key[e]);
+      if (c == key[e]) atomicOr(&s_dup[h >> 5], 1u << (h & 31));   // another position holds it
+      if (c == kEmpty || c == key[e]) break;
+      h = (h + 1) & (TS - 1);
+    }
+    atomicMin(&s_pos[h], pos[e]);
+    slot[e] = h;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < kBktCapItems; ++e) {
+    if (key[e] == kEmpty || !((s_dup[slot[e] >> 5] >> (slot[e] & 31)) & 1u)) continue;
+    const u32 first = s_pos[slot[e]];
+    if (pos[e] != first) {
+      mk.nf[pos[e]] = kNfNot;
+      rec[pos[e]] = first | (rec[pos[e]] & kBits);
+    } else {
+      mk.multi[pos[e]] = 1;
+    }
+  }
 }
 
 // ---- direct subtrees ----------------------------------------------------------------
@@ -1022,8 +1234,9 @@ struct TailOut {
 // Clear a node level's table (all ones) and marks (zero) unless the level is direct.
 [[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_clear(uint4* __restrict__ tab, u64 tab16, uint4* __restrict__ nf,
                                                  uint4* __restrict__ multi, u64 p16, const u64* prev_count,
-                                                 u64 prev_n) {
+                                                 u64 prev_n, const Header* __restrict__ hdr, u32 bkt) {
   if (level_direct(prev_count, prev_n)) return;
+  if (bkt && hdr->predup == 0) tab16 = 0;   // bucketed insert: no table
   const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u), zero = make_uint4(0, 0, 0, 0);
   const u64 stride = u64(gridDim.x) * kBlock;
   for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < tab16; i += stride) tab[i] = ones;

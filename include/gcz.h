@@ -64,6 +64,7 @@ typedef struct {
   int error_symbol;                  /* the offending byte */
   double build_ms;                   /* device time of the build (hipEvents) */
   uint64_t hashed_pairs;             /* node pairs hash-consed (others skipped as provably unique) */
+  uint64_t bucketed_pairs;           /* ... of which through the bucketed LDS dedupe (not the table) */
 } gcz_info;
 
 /* ---- device context ---------------------------------------------------- */

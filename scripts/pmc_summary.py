@@ -25,7 +25,8 @@ NAMES = {"k_leaf_bases": "leaf_insert", "k_leaf_packed": "leaf_insert", "k_node_
          "k_flagscan_leaf": "flagscan_leaf", "k_flagscan_node": "flagscan_node", "k_resolve_leaf": "resolve_leaf",
          "k_resolve_node": "resolve_node", "k_clear": "clear", "__amd_rocclr_fillBufferAligned": "clear",
          "k_tail": "tail", "k_direct_levels": "direct_levels", "k_dup_probe": "leaf_insert",
-         "k_dup_decide": "leaf_insert"}
+         "k_dup_decide": "leaf_insert", "k_bkt_count": "bucket_count", "k_bkt_scatter": "bucket_scatter",
+         "k_bkt_dedupe": "bucket_dedupe"}
 
 
 def load(d, counter):

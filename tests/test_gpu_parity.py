@@ -31,6 +31,18 @@ def ctx_wide(gcz):
     c.close()
 
 
+@pytest.fixture(scope="module")
+def ctx_bucket(gcz):
+    """A context that takes the bucketed LDS node insert on every hashed level."""
+    os.environ["GCZ_BUCKET_MIN"] = "1"
+    try:
+        c = gcz.Context(0)
+    finally:
+        del os.environ["GCZ_BUCKET_MIN"]
+    yield c
+    c.close()
+
+
 def _names(max_bases):
     with open(os.path.join(GOLDEN, "manifest.json")) as f:
         m = json.load(f)
@@ -39,6 +51,16 @@ def _names(max_bases):
 
 def _build(ctx, kind, payload, L):
     return ctx.build_fasta(payload, L) if kind == "fasta" else ctx.build_leaves(payload, L)
+
+
+@pytest.mark.parametrize("name", [n for n in _names(12_000_000) if not n.startswith("fasta/")])
+def test_gpu_bucketed_insert_goldens(name, ctx_bucket, gcz, manifest):
+    """The bucketed node insert (k_bkt_*, forced on every hashed level) builds the
+    reference's tree bit for bit."""
+    case = manifest[name]
+    kind, payload, L = case_input(case, gcz)
+    _build(ctx_bucket, kind, payload, L)
+    assert compare_digest(gcz.digest(ctx_bucket.tree()), case["expect"]) == {}
 
 
 @pytest.mark.parametrize("name", _names(12_000_000))
@@ -142,7 +164,10 @@ def test_gpu_large_synth_goldens(name, ctx, gcz, manifest):
 
 @pytest.mark.parametrize("env", [{"GCZ_DIRECT": "0"}, {"GCZ_TAIL": "0"}, {"GCZ_DIRECT": "0", "GCZ_TAIL": "0"},
                                  {"GCZ_NODE_CAP_SHIFT": "0"}, {"GCZ_LEAF_CAP_LOG2": "20"},
-                                 {"GCZ_PREDUP": "1"}, {"GCZ_PREDUP": "2"}, {"GCZ_PREDUP": "1", "GCZ_TABLE": "wide"}])
+                                 {"GCZ_PREDUP": "1"}, {"GCZ_PREDUP": "2"}, {"GCZ_PREDUP": "1", "GCZ_TABLE": "wide"},
+                                 {"GCZ_BUCKET": "0"}, {"GCZ_BUCKET_MIN": "1"},
+                                 {"GCZ_BUCKET_MIN": "1", "GCZ_DIRECT": "0"},
+                                 {"GCZ_BUCKET_MIN": "1", "GCZ_PREDUP": "2"}])
 def test_gpu_schedule_knobs_same_tree(env, gcz, manifest):
     """The per-level fallbacks (no direct subtrees, no fused top, tight tables, a leaf
     table that overflows and regrows) build the same tree as the default schedule."""
