@@ -167,12 +167,12 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   const unsigned char* pmu = a.prev_marks ? multi_set[prev] : nullptr;
   Group* d_grp = grp.as<Group>();
   // bucketed insert (decided on the device: hdr->predup == 0) when the buckets average
-  // <= 3072 pairs (the LDS dedupe holds 6144) and a record fits 8 bytes
+  // <= 2560 pairs (the LDS dedupe holds 4608) and a record fits 8 bytes
   BktPlan bp{};
   bp.T = nt.pt;
   bp.K = 2 * (Bk + 3);
-  while (bp.bb < u32(kBktMaxLog) && (p >> bp.bb) > 3072) ++bp.bb;
-  const u32 bkt = a.allow_bucket && bucket_now && nt.packed && p >= bucket_min && (p >> bp.bb) <= 3072 &&
+  while (bp.bb < u32(kBktMaxLog) && (p >> bp.bb) > 2560) ++bp.bb;
+  const u32 bkt = a.allow_bucket && bucket_now && nt.packed && p >= bucket_min && (p >> bp.bb) <= 2560 &&
                   bp.K >= bp.bb && bp.K - bp.bb + kBktRP <= 64 &&
                   p <= u64(kBktMaxG) * kBktChunk ? 1u : 0u;
   const u32 bb = bp.bb;
@@ -215,7 +215,7 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     HIP_TRY(hipGetLastError());
     prof_end(KID_BKT_SCATTER, e0);
     prof_begin(KID_BKT_DEDUPE, e0);
-    hipLaunchKernelGGL(k_bkt_dedupe, dim3(1u << bb), dim3(kBktThreads), 0, stream, bkt_off.as<u32>(), G,
+    hipLaunchKernelGGL(k_bkt_dedupe, dim3(1u << bb), dim3(kBktThreads), size_t(G) * 4, stream, bkt_off.as<u32>(), G,
                        bkt_key.as<u64>(), a.words, mk, d_hdr, a.pcount, n);
     HIP_TRY(hipGetLastError());
     prof_end(KID_BKT_DEDUPE, e0);

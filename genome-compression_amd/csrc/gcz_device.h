@@ -889,11 +889,11 @@ constexpr int kBktThreads = 1024;
 constexpr int kBktItems = 64;                        // pairs per thread of count / scatter
 constexpr u64 kBktChunk = u64(kBktThreads) * kBktItems;   // pairs per count-matrix column (2^16)
 constexpr u32 kBktRP = 16;                          // record offset bits
-constexpr int kBktMaxG = 8192;                      // count chunks (p < 2^29)
+constexpr int kBktMaxG = 8192;                      // count chunks (p < 2^29; dedupe LDS <= 32 KB)
 constexpr int kBktMaxLog = 14;                       // nb <= 16384 (LDS counters, 64 KB)
-constexpr int kBktSlotsLog = 13;                     // LDS table of the dedupe: 8192 slots
-constexpr int kBktCapItems = 6;                      // ... holding a bucket of <= 6144 pairs
-constexpr int kBktCap = kBktThreads * kBktCapItems;
+constexpr u32 kBktSlots = 6144;                      // LDS table of the dedupe (72 KB: 2 workgroups per CU)
+constexpr int kBktCapItems = 5;
+constexpr int kBktCap = 4608;                        // ... holding a bucket of <= 4608 pairs (load <= 3/4)
 
 __device__ __forceinline__ u64 bkt_hash(u64 k) {     // murmur3 fmix64
   k ^= k >> 33;
@@ -1026,11 +1026,11 @@ __device__ __forceinline__ u32 bkt_pos(const u32* s_off, u64 G, u32 i, u64 r) {
                                                            u32* __restrict__ rec, Marks mk, Header* __restrict__ hdr,
                                                            const u64* prev_count, u64 n) {
   if (bkt_skip(hdr, prev_count, n)) return;
-  constexpr u32 TS = 1u << kBktSlotsLog;
+  constexpr u32 TS = kBktSlots;
   __shared__ u64 s_key[TS];
   __shared__ u32 s_pos[TS];
   __shared__ u32 s_dup[TS / 32];
-  __shared__ u32 s_off[kBktMaxG];
+  extern __shared__ u32 s_off[];   // G entries (dynamic)
   const u64 b = blockIdx.x;
   const u32 start = off[b * G], end = off[(b + 1) * G];
   if (end - start > u32(kBktCap)) {   // a hot key: the table path handles this data
@@ -1056,13 +1056,13 @@ __device__ __forceinline__ u32 bkt_pos(const u32* s_off, u64 G, u32 i, u64 r) {
   for (int e = 0; e < kBktCapItems; ++e) {
     if (key[e] == kEmpty) continue;
     pos[e] = bkt_pos(s_off, G, start + u32(e) * kBktThreads + threadIdx.x, raw[e]);
-    u32 h = u32(bkt_hash(key[e])) & (TS - 1);
+    u32 h = u32((u64(u32(bkt_hash(key[e]))) * TS) >> 32);
     for (;;) {
       unsigned long long c = s_key[h];
       if (c == kEmpty) c = atomicCAS(&s_key[h], kEmpty, (unsigned long long)key[e]);
       if (c == key[e]) atomicOr(&s_dup[h >> 5], 1u << (h & 31));   // another position holds it
       if (c == kEmpty || c == key[e]) break;
-      h = (h + 1) & (TS - 1);
+      h = h + 1 == TS ? 0u : h + 1;
     }
     atomicMin(&s_pos[h], pos[e]);
     slot[e] = h;
