@@ -373,6 +373,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     u64 bound = std::min(S, leaf_cap);        // child ids of layer 0 are leaf ids < #slots
     bool tail_done = false, direct = false;
     bool prev_regular = false;   // the previous level ran node_level (its gate is written)
+    bool table_only = false;     // hdr->predup seen on the host: no bucketed levels
     for (int k = 0; k < D; ++k) {
       if (n <= u64(kTailMaxN) && use_tail) {   // the rest fits one workgroup: one launch
         const u64* pc = k == 0 ? &d_hdr->count[C - 1] : prev_regular ? &d_hdr->gate[k - 1]
@@ -413,7 +414,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       na.ticket = &d_hdr->ticket[kLayerSlot + k];
       na.hashed_next = &d_hdr->hashed_next[k];   // look-ahead for layer k + 1 (its pairs' children are here)
       na.gate = &d_hdr->gate[k];
-      na.allow_bucket = true;
+      na.allow_bucket = !table_only;
       if ((rc = node_level(na, d_hdr))) return rc;
       prev_regular = true;
       std::swap(in, outw);
@@ -423,9 +424,12 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       // level is direct and runs as direct subtrees (saves ~4 launches per level)
       if (k <= 1 && use_direct && n > u64(kTailMaxN)) {
         u64 g = 0;
+        u32 pd = 0;
         HIP_TRY(hipMemcpyAsync(&g, &d_hdr->gate[k], 8, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipMemcpyAsync(&pd, &d_hdr->predup, 4, hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
         direct = g == n;
+        table_only = pd != 0;   // repetitive data: later levels skip the (gated-off) bucket launches
       }
     }
     if (!tail_done) {
