@@ -491,7 +491,8 @@ def main():
                                        "replicas": f"{world} independent genomes, one per GPU",
                                        "virtual": f"{args.virtual} virtual ranks on 1 GPU (overhead probe)"}[mode]},
             "roofline": roofline,
-            "build": {"device_ms": info["build_ms"], "hashed_pairs": info["hashed_pairs"], "b_stream": b_stream, "b_table": b_table,
+            "build": {"device_ms": info["build_ms"], "hashed_pairs": info["hashed_pairs"],
+                      "bucketed_pairs": info.get("bucketed_pairs", 0), "b_stream": b_stream, "b_table": b_table,
                       "hbm_frac_survey_formula": round(build_frac, 5), "n_leaves": info["n_leaves"],
                       "n_layers": info["n_layers"]},
             "kernels": kernels,

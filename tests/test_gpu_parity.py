@@ -189,3 +189,44 @@ def test_gpu_schedule_knobs_same_tree(env, gcz, manifest):
             assert compare_digest(gcz.digest(c.tree()), case["expect"]) == {}, (env, name)
     finally:
         c.close()
+
+
+def test_gpu_bucketed_matches_oracle_random(ctx_bucket, gcz, oracle):
+    """Bucketed insert on random leaf mixes (unique-heavy and repeat-heavy), against the oracle."""
+    rng = np.random.default_rng(11)
+    for S, pool_div in [(5, 1), (4097, 1), (100_003, 1), (100_003, 7), (300_001, 50_000)]:
+        pool = rng.integers(0, 1 << 48, size=max(4, S // pool_div), dtype=np.uint64)
+        leaves = pool[rng.integers(0, pool.size, size=S)]
+        ctx_bucket.build_leaves(leaves, 12)
+        g = ctx_bucket.tree()
+        o = oracle.build_leaves(leaves, 12)
+        assert g.leaves_bin() == o.leaves_bin(), S
+        assert g.layers_bin() == o.layers_bin(), S
+
+
+def test_gpu_bucket_overflow_rebuilds(gcz, oracle):
+    """Hot keys (more records than a bucket's LDS table holds) with the repeat probe off:
+    the bucketed insert overflows and the build reruns on the table -- same tree."""
+    saved = {k: os.environ.get(k) for k in ("GCZ_BUCKET_MIN", "GCZ_PREDUP")}
+    os.environ.update({"GCZ_BUCKET_MIN": "1", "GCZ_PREDUP": "2"})
+    try:
+        c = gcz.Context(0)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    try:
+        rng = np.random.default_rng(12)
+        pool = rng.integers(0, 1 << 48, size=3, dtype=np.uint64)
+        hot = pool[rng.integers(0, 3, size=200_000)]          # 9 pair keys, ~11 K records each
+        cold = rng.integers(0, 1 << 48, size=50_001, dtype=np.uint64)
+        leaves = np.concatenate([hot, cold])
+        info = c.build_leaves(leaves, 12)
+        o = oracle.build_leaves(leaves, 12)
+        assert c.tree().leaves_bin() == o.leaves_bin()
+        assert c.tree().layers_bin() == o.layers_bin()
+        assert info["bucketed_pairs"] == 0   # the final (table) build bucketed nothing
+    finally:
+        c.close()
