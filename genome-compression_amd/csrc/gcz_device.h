@@ -825,7 +825,7 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
       uint2 w;
       w.x = cl; w.y = cr;
       out[id] = w;
-      words[j] = id | (words[j] & kBits);
+      words[j] = make_word(id, m, t, ulw(l) == ulw(xf(r, 1, 0)));   // the insert's bits, recomputed
     }
   }
   if (hashed_next) {
