@@ -1055,7 +1055,6 @@ __device__ __forceinline__ u32 bkt_pos(const u32* s_off, u64 G, u32 i, u64 r) {
 #pragma unroll
   for (int e = 0; e < kBktCapItems; ++e) {
     if (key[e] == kEmpty) continue;
-    pos[e] = bkt_pos(s_off, G, start + u32(e) * kBktThreads + threadIdx.x, raw[e]);
     u32 h = u32((u64(u32(bkt_hash(key[e]))) * TS) >> 32);
     for (;;) {
       unsigned long long c = s_key[h];
@@ -1064,8 +1063,15 @@ __device__ __forceinline__ u32 bkt_pos(const u32* s_off, u64 G, u32 i, u64 r) {
       if (c == kEmpty || c == key[e]) break;
       h = h + 1 == TS ? 0u : h + 1;
     }
-    atomicMin(&s_pos[h], pos[e]);
     slot[e] = h;
+  }
+  __syncthreads();
+  // only keys with several records need positions (most buckets have none)
+#pragma unroll
+  for (int e = 0; e < kBktCapItems; ++e) {
+    if (key[e] == kEmpty || !((s_dup[slot[e] >> 5] >> (slot[e] & 31)) & 1u)) continue;
+    pos[e] = bkt_pos(s_off, G, start + u32(e) * kBktThreads + threadIdx.x, raw[e]);
+    atomicMin(&s_pos[slot[e]], pos[e]);
   }
   __syncthreads();
 #pragma unroll
