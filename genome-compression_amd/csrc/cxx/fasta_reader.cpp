@@ -38,7 +38,7 @@ fasta_reader::fasta_reader(std::filesystem::path path, std::size_t buffer_size)
 void fasta_reader::extract() const {
   if (extracted) return;
   seq.resize(nbytes);
-  seq.resize(gcz_fasta_extract(bytes.get(), nbytes, seq.data()));
+  seq.resize(gcz_fasta_extract(bytes.get(), nbytes, int(dna::size()), buffer_size, seq.data()));
   strands = seq.size() / dna::size();
   extracted = true;
 }

@@ -600,7 +600,13 @@ int gcz_build_host_fasta(gcz_ctx* c, const void* fasta, uint64_t nbytes, int L) 
   if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
   // the raw file goes to the device; headers / line breaks are removed there (gcz_ingest.hip)
   const auto* f = static_cast<const uint8_t*>(fasta);
-  const bool plain = nbytes == 0 || (f[0] != '>' && f[0] != '\n' && !std::memchr(f, '\n', nbytes));
+  // one line without a header needs no line contract, unless a reader buffer
+  // boundary falls on a '>' (src/fasta_reader.cpp:48-51; gcz_ingest.hip)
+  bool plain = nbytes == 0 || (f[0] != '>' && f[0] != '\n' && !std::memchr(f, '\n', nbytes));
+  if (plain && L >= 1 && L <= 16) {
+    const u64 cap = gcz::reader_buffer_bytes(nbytes, L, 0);
+    for (u64 b = cap; b < nbytes && plain; b += cap) plain = f[b] != '>';
+  }
   if (int rc = c->ensure(c->input, nbytes + 16)) return rc;
   if (nbytes && hipMemcpyAsync(c->input.ptr, f, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess)
     return c->fail(GCZ_ERR_DEVICE, "gcz_build_host_fasta", "H2D copy failed");

@@ -267,20 +267,34 @@ int gcz_tree_deserialize(gcz_tree* t, int L, const uint8_t* buf, uint64_t n) {
 
 // fasta_reader::load_buffer line contract (src/fasta_reader.cpp:40-68): at each
 // line start a '>' or '\n' skips ONE line, the next line is data without a
-// second peek; data line bodies are concatenated.
-uint64_t gcz_fasta_extract(const uint8_t* f, uint64_t n, uint8_t* out) {
+// second peek; data line bodies are concatenated.  Reader buffers hold
+// cap = min(n/L + 1, buffer_strands) * L data bytes (:22-31); a data line that
+// crosses a buffer boundary resumes with a fresh peek there (:48-51), so a '>'
+// at the boundary drops the rest of that line and makes the next line data.
+uint64_t gcz_fasta_extract(const uint8_t* f, uint64_t n, int L, uint64_t buffer_strands, uint8_t* out) {
+  if (L < 1) return 0;
+  const uint64_t cap = gcz::reader_buffer_bytes(n, L, buffer_strands);
   uint64_t pos = 0, j = 0;
+  bool forced = false;
   while (pos < n) {
-    if (f[pos] == '>' || f[pos] == '\n') {
+    if (!forced && (f[pos] == '>' || f[pos] == '\n')) {
       const void* nl = std::memchr(f + pos, '\n', n - pos);
       pos = nl ? uint64_t(static_cast<const uint8_t*>(nl) - f) + 1 : n;
-      if (pos >= n) break;
+      forced = true;
+      continue;
     }
+    forced = false;
     const void* nl = std::memchr(f + pos, '\n', n - pos);
-    const uint64_t end = nl ? uint64_t(static_cast<const uint8_t*>(nl) - f) : n;
+    uint64_t end = nl ? uint64_t(static_cast<const uint8_t*>(nl) - f) : n;
+    for (uint64_t k = j / cap + 1; k * cap < j + (end - pos); ++k)
+      if (f[pos + (k * cap - j)] == '>') {
+        end = pos + (k * cap - j);
+        forced = true;
+        break;
+      }
     if (out + j != f + pos) std::memmove(out + j, f + pos, end - pos);
     j += end - pos;
-    pos = nl ? end + 1 : n;
+    pos = nl ? uint64_t(static_cast<const uint8_t*>(nl) - f) + 1 : n;
   }
   return j;
 }

@@ -10,7 +10,15 @@
 //   2. per line: marker flag, the last non-marker line before it (max-scan),
 //      hence skip / data and the data length; an exclusive sum gives each
 //      data line's output offset,
-//   3. a byte-parallel copy: each block stages the line boundaries of its
+//   3. reader buffers: the reference fills cap = B*L data bytes per buffer
+//      (src/fasta_reader.cpp:22-31,47-64) and a line that crosses a buffer
+//      boundary resumes with a fresh peek (:48-51): a '>' there drops the rest of
+//      the line and makes the next line data.  One thread per boundary checks
+//      the byte at it; the first such boundary becomes a per-line override
+//      (cut length, forced-data next line) and steps 2-3 repeat from it.  Any
+//      '>' inside a data line is otherwise an unknown symbol, so valid FASTA
+//      never loops,
+//   4. a byte-parallel copy: each block stages the line boundaries of its
 //      2 KiB input window in LDS and every byte finds its line there.
 #include <hipcub/hipcub.hpp>
 
@@ -20,13 +28,14 @@ using namespace gcz_dev;
 using namespace gcz_host;
 
 struct gcz_ingest_state {
-  DevBuf nlpos, nsel, lastnm, len, off, tmp, bases;
+  DevBuf nlpos, nsel, lastnm, len, off, tmp, bases, cut, forced, ev;
 };
 
 void gcz_ingest_state_free(gcz_ctx* c) {
   gcz_ingest_state* s = c->ingest;
   if (!s) return;
-  for (DevBuf* b : {&s->nlpos, &s->nsel, &s->lastnm, &s->len, &s->off, &s->tmp, &s->bases})
+  for (DevBuf* b : {&s->nlpos, &s->nsel, &s->lastnm, &s->len, &s->off, &s->tmp, &s->bases, &s->cut, &s->forced,
+                    &s->ev})
     if (b->ptr) (void)hipFree(b->ptr);
   delete s;
   c->ingest = nullptr;
@@ -47,13 +56,18 @@ struct NewlineCount {
 };
 
 // Line i spans [st, en): st = 0 or one past newline i-1, en = newline i or n.
+// Overrides from reader-buffer boundaries (null until the first one): forced[i]
+// = line i is read as data without a peek; cut[i] = data bytes kept of line i.
 struct Lines {
   const unsigned char* f;
   const u64* nl;   // newline positions
   u64 nnl, n, nlines;
+  const unsigned char* forced;
+  const u64* cut;
   __device__ __forceinline__ u64 st(u64 i) const { return i == 0 ? 0 : nl[i - 1] + 1; }
   __device__ __forceinline__ u64 en(u64 i) const { return i < nnl ? nl[i] : n; }
   __device__ __forceinline__ bool marker(u64 i) const {
+    if (forced && forced[i]) return false;
     const unsigned char c = f[st(i)];
     return c == '>' || c == '\n';
   }
@@ -79,7 +93,43 @@ __global__ __launch_bounds__(kBlock) void k_line_len(Lines ln, const long long* 
                                                      u64* __restrict__ len) {
   const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (i >= ln.nlines) return;
-  len[i] = skipped(ln, lastnm, i) ? 0 : ln.en(i) - ln.st(i);
+  u64 l = skipped(ln, lastnm, i) ? 0 : ln.en(i) - ln.st(i);
+  if (ln.cut && ln.cut[i] < l) l = ln.cut[i];
+  len[i] = l;
+}
+
+// last line whose output offset is < b (off is non-decreasing)
+__device__ __forceinline__ u64 line_before(const u64* off, u64 nlines, u64 b) {
+  u64 lo = 0, hi = nlines;   // first line with off >= b
+  while (lo < hi) {
+    const u64 mid = (lo + hi) / 2;
+    if (off[mid] < b) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo - 1;   // off[0] = 0 < b
+}
+
+// Boundaries k*cap, k0 <= k <= k1 (all strictly inside the data): the smallest k
+// whose boundary splits a line at a '>' (src/fasta_reader.cpp:48-51).
+__global__ __launch_bounds__(kBlock) void k_boundary_check(Lines ln, const u64* __restrict__ off,
+                                                           const u64* __restrict__ len, u64 cap, u64 k0, u64 k1,
+                                                           u64* __restrict__ ev) {
+  const u64 k = k0 + u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (k > k1) return;
+  const u64 b = k * cap;
+  const u64 i = line_before(off, ln.nlines, b);
+  if (off[i] + len[i] > b && ln.f[ln.st(i) + (b - off[i])] == '>') atomicMin(reinterpret_cast<unsigned long long*>(ev), k);
+}
+
+// The first event found by k_boundary_check becomes line overrides.
+__global__ void k_boundary_apply(Lines ln, const u64* __restrict__ off, u64 cap, const u64* __restrict__ ev,
+                                 u64* __restrict__ cut, unsigned char* __restrict__ forced) {
+  const u64 k = *ev;
+  if (k == ~0ull) return;
+  const u64 b = k * cap;
+  const u64 i = line_before(off, ln.nlines, b);
+  cut[i] = b - off[i];
+  if (i + 1 < ln.nlines) forced[i + 1] = 1;
 }
 
 // first line whose end is >= pos (the line containing pos, or starting at it)
@@ -93,11 +143,11 @@ __device__ __forceinline__ u64 line_at(const Lines& ln, u64 pos) {
   return lo;
 }
 
-__global__ __launch_bounds__(kBlock) void k_copy_lines(Lines ln, const long long* __restrict__ lastnm,
+__global__ __launch_bounds__(kBlock) void k_copy_lines(Lines ln, const u64* __restrict__ len,
                                                        const u64* __restrict__ off, unsigned char* __restrict__ out) {
   __shared__ u64 s_st[kWin + 1];
   __shared__ u64 s_off[kWin + 1];
-  __shared__ unsigned char s_data[kWin + 1];
+  __shared__ u64 s_lim[kWin + 1];   // end of the kept bytes of the line (st when skipped)
   __shared__ u64 s_l0;
   __shared__ u32 s_cnt;
   const u64 b0 = u64(blockIdx.x) * kWin;
@@ -114,9 +164,8 @@ __global__ __launch_bounds__(kBlock) void k_copy_lines(Lines ln, const long long
   for (u32 k = threadIdx.x; k < cnt; k += kBlock) {
     const u64 i = l0 + k;
     s_st[k] = ln.st(i);
-    const bool data = !skipped(ln, lastnm, i);
     s_off[k] = off[i];
-    s_data[k] = data;
+    s_lim[k] = s_st[k] + len[i];
   }
   __syncthreads();
   for (u64 p = b0 + threadIdx.x; p < b1; p += kBlock) {
@@ -128,7 +177,7 @@ __global__ __launch_bounds__(kBlock) void k_copy_lines(Lines ln, const long long
       if (s_st[mid] <= p) lo = mid;
       else hi = mid - 1;
     }
-    if (s_data[lo]) out[s_off[lo] + (p - s_st[lo])] = c;
+    if (p < s_lim[lo]) out[s_off[lo] + (p - s_st[lo])] = c;
   }
 }
 
@@ -143,16 +192,19 @@ dim3 grid_of(u64 n) { return dim3(unsigned(std::max<u64>(1, (n + kBlock - 1) / k
   } while (0)
 
 // Bases of a FASTA file in device memory -> ctx-owned device buffer; returns the count.
-int gcz_fasta_extract_on_device(gcz_ctx* c, const unsigned char* d_file, u64 n, const unsigned char** d_bases,
-                                u64* nbases) {
+// Reader buffers of buffer_strands strands (0 = the reference default 1 << 22).
+int gcz_fasta_extract_on_device(gcz_ctx* c, const unsigned char* d_file, u64 n, int Lleaf, u64 buffer_strands,
+                                const unsigned char** d_bases, u64* nbases) {
   if (!c->ingest) c->ingest = new gcz_ingest_state();
   gcz_ingest_state& s = *c->ingest;
   *nbases = 0;
   *d_bases = nullptr;
+  if (Lleaf < 1 || Lleaf > 16) return GCZ_ERR_ARG;
   int rc;
-  if ((rc = c->ensure(s.nsel, 16)) || (rc = c->ensure(s.bases, n + 16))) return rc;
+  if ((rc = c->ensure(s.nsel, 16)) || (rc = c->ensure(s.bases, n + 16)) || (rc = c->ensure(s.ev, 16))) return rc;
   *d_bases = s.bases.as<unsigned char>();
   if (n == 0) return GCZ_OK;
+  const u64 cap = gcz::reader_buffer_bytes(n, Lleaf, buffer_strands);
   // 1. newline positions (counted first, so the position array is exact)
   hipcub::CountingInputIterator<u64> idx(0);
   hipcub::TransformInputIterator<u64, NewlineCount, hipcub::CountingInputIterator<u64>> isnl(idx,
@@ -176,34 +228,61 @@ int gcz_fasta_extract_on_device(gcz_ctx* c, const unsigned char* d_file, u64 n, 
   I_HIP(hipMemcpyAsync(&nnl, s.nsel.ptr, 8, hipMemcpyDeviceToHost, c->stream));
   I_HIP(hipMemcpyAsync(&last, d_file + n - 1, 1, hipMemcpyDeviceToHost, c->stream));
   I_HIP(hipStreamSynchronize(c->stream));
-  Lines ln{d_file, s.nlpos.as<u64>(), nnl, n, nnl + (last != '\n' ? 1 : 0)};
+  Lines ln{d_file, s.nlpos.as<u64>(), nnl, n, nnl + (last != '\n' ? 1 : 0), nullptr, nullptr};
   const u64 L = ln.nlines;
-  // 2. skip / data per line, output offsets
   if ((rc = c->ensure(s.lastnm, L * 8 + 16)) || (rc = c->ensure(s.len, L * 8 + 16)) ||
       (rc = c->ensure(s.off, L * 8 + 16)))
     return rc;
-  hipcub::TransformInputIterator<long long, NonMarkerIndex, hipcub::CountingInputIterator<u64>> nm(idx,
-                                                                                                 NonMarkerIndex{ln});
-  tmp_bytes = 0;
-  I_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tmp_bytes, nm, s.lastnm.as<long long>(), MaxOp{}, L, c->stream));
-  if ((rc = c->ensure(s.tmp, tmp_bytes + 16))) return rc;
-  I_HIP(hipcub::DeviceScan::InclusiveScan(s.tmp.ptr, tmp_bytes, nm, s.lastnm.as<long long>(), MaxOp{}, L,
-                                          c->stream));
-  hipLaunchKernelGGL(k_line_len, grid_of(L), dim3(kBlock), 0, c->stream, ln, s.lastnm.as<long long>(),
-                     s.len.as<u64>());
-  tmp_bytes = 0;
-  I_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, s.len.as<u64>(), s.off.as<u64>(), L, c->stream));
-  if ((rc = c->ensure(s.tmp, tmp_bytes + 16))) return rc;
-  I_HIP(hipcub::DeviceScan::ExclusiveSum(s.tmp.ptr, tmp_bytes, s.len.as<u64>(), s.off.as<u64>(), L, c->stream));
-  u64 tail[2] = {0, 0};
-  I_HIP(hipMemcpyAsync(&tail[0], s.off.as<u64>() + L - 1, 8, hipMemcpyDeviceToHost, c->stream));
-  I_HIP(hipMemcpyAsync(&tail[1], s.len.as<u64>() + L - 1, 8, hipMemcpyDeviceToHost, c->stream));
-  // 3. copy
+  u64 total = 0;
+  for (u64 k0 = 1;;) {
+    // 2. skip / data per line, output offsets
+    hipcub::TransformInputIterator<long long, NonMarkerIndex, hipcub::CountingInputIterator<u64>> nm(
+        idx, NonMarkerIndex{ln});
+    tmp_bytes = 0;
+    I_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tmp_bytes, nm, s.lastnm.as<long long>(), MaxOp{}, L,
+                                            c->stream));
+    if ((rc = c->ensure(s.tmp, tmp_bytes + 16))) return rc;
+    I_HIP(hipcub::DeviceScan::InclusiveScan(s.tmp.ptr, tmp_bytes, nm, s.lastnm.as<long long>(), MaxOp{}, L,
+                                            c->stream));
+    hipLaunchKernelGGL(k_line_len, grid_of(L), dim3(kBlock), 0, c->stream, ln, s.lastnm.as<long long>(),
+                       s.len.as<u64>());
+    tmp_bytes = 0;
+    I_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, s.len.as<u64>(), s.off.as<u64>(), L, c->stream));
+    if ((rc = c->ensure(s.tmp, tmp_bytes + 16))) return rc;
+    I_HIP(hipcub::DeviceScan::ExclusiveSum(s.tmp.ptr, tmp_bytes, s.len.as<u64>(), s.off.as<u64>(), L, c->stream));
+    u64 tail[2] = {0, 0};
+    I_HIP(hipMemcpyAsync(&tail[0], s.off.as<u64>() + L - 1, 8, hipMemcpyDeviceToHost, c->stream));
+    I_HIP(hipMemcpyAsync(&tail[1], s.len.as<u64>() + L - 1, 8, hipMemcpyDeviceToHost, c->stream));
+    I_HIP(hipStreamSynchronize(c->stream));
+    total = tail[0] + tail[1];
+    // 3. reader-buffer boundaries strictly inside the data, from k0 on
+    const u64 k1 = total ? (total - 1) / cap : 0;
+    if (k0 > k1) break;
+    I_HIP(hipMemsetAsync(s.ev.ptr, 0xff, 8, c->stream));
+    hipLaunchKernelGGL(k_boundary_check, grid_of(k1 - k0 + 1), dim3(kBlock), 0, c->stream, ln, s.off.as<u64>(),
+                       s.len.as<u64>(), cap, k0, k1, s.ev.as<u64>());
+    u64 ev = ~0ull;
+    I_HIP(hipMemcpyAsync(&ev, s.ev.ptr, 8, hipMemcpyDeviceToHost, c->stream));
+    I_HIP(hipStreamSynchronize(c->stream));
+    if (ev == ~0ull) break;
+    if (!ln.cut) {   // first event: the override arrays
+      if ((rc = c->ensure(s.cut, L * 8 + 16)) || (rc = c->ensure(s.forced, L + 16))) return rc;
+      I_HIP(hipMemsetAsync(s.cut.ptr, 0xff, L * 8, c->stream));
+      I_HIP(hipMemsetAsync(s.forced.ptr, 0, L, c->stream));
+      ln.cut = s.cut.as<u64>();
+      ln.forced = s.forced.as<unsigned char>();
+    }
+    hipLaunchKernelGGL(k_boundary_apply, dim3(1), dim3(1), 0, c->stream, ln, s.off.as<u64>(), cap,
+                       s.ev.as<u64>(), s.cut.as<u64>(), s.forced.as<unsigned char>());
+    I_HIP(hipGetLastError());
+    k0 = ev + 1;
+  }
+  // 4. copy
   hipLaunchKernelGGL(k_copy_lines, dim3(unsigned((n + kWin - 1) / kWin)), dim3(kBlock), 0, c->stream, ln,
-                     s.lastnm.as<long long>(), s.off.as<u64>(), s.bases.as<unsigned char>());
+                     s.len.as<u64>(), s.off.as<u64>(), s.bases.as<unsigned char>());
   I_HIP(hipGetLastError());
   I_HIP(hipStreamSynchronize(c->stream));
-  *nbases = tail[0] + tail[1];
+  *nbases = total;
   return GCZ_OK;
 }
 
@@ -214,17 +293,20 @@ int gcz_build_device_fasta(gcz_ctx* c, const void* d_file, uint64_t n, int L) {
   if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
   const unsigned char* b = nullptr;
   u64 nb = 0;
-  if (int rc = gcz_fasta_extract_on_device(c, static_cast<const unsigned char*>(d_file), n, &b, &nb)) return rc;
+  if (int rc = gcz_fasta_extract_on_device(c, static_cast<const unsigned char*>(d_file), n, L, 0, &b, &nb))
+    return rc;
   return c->build(b, nullptr, nb, 0, L);
 }
 
-int gcz_fasta_extract_device(gcz_ctx* c, const void* d_file, uint64_t n, void* d_out, uint64_t cap,
-                             uint64_t* nbases) {
+int gcz_fasta_extract_device(gcz_ctx* c, const void* d_file, uint64_t n, int L, uint64_t buffer_strands, void* d_out,
+                             uint64_t cap, uint64_t* nbases) {
   if (!c || (!d_file && n) || !nbases) return GCZ_ERR_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
   const unsigned char* b = nullptr;
   u64 nb = 0;
-  if (int rc = gcz_fasta_extract_on_device(c, static_cast<const unsigned char*>(d_file), n, &b, &nb)) return rc;
+  if (int rc = gcz_fasta_extract_on_device(c, static_cast<const unsigned char*>(d_file), n, L, buffer_strands, &b,
+                                           &nb))
+    return rc;
   *nbases = nb;
   if (!d_out) return GCZ_OK;
   if (cap < nb) return GCZ_ERR_ARG;

@@ -17,6 +17,15 @@ constexpr uint32_t kFlagMask = 0xe0000000u;
 
 inline uint32_t ul(uint32_t w) { return w & 0x7fffffffu; }   // pointer::to_ulong, :103-107
 
+// Data bytes per fasta_reader buffer (src/fasta_reader.cpp:22-31): the buffer
+// holds min(file_size/L + 1, buffer_strands) strands; 0 = default 1 << 22
+// (include/fasta_reader.h:23).
+inline uint64_t reader_buffer_bytes(uint64_t file_size, int L, uint64_t buffer_strands) {
+  if (!buffer_strands) buffer_strands = uint64_t(1) << 22;
+  const uint64_t fs = file_size / uint64_t(L) + 1;
+  return (fs < buffer_strands ? fs : buffer_strands) * uint64_t(L);
+}
+
 }  // namespace gcz
 
 namespace gcz {

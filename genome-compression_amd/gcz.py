@@ -61,7 +61,7 @@ _SIGS = {
     "gcz_build_host_fasta": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
     "gcz_build_host_leaves": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
     "gcz_build_device_fasta": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
-    "gcz_fasta_extract_device": (ctypes.c_int, [_P, _P, _U64, _P, _U64, ctypes.POINTER(_U64)]),
+    "gcz_fasta_extract_device": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int, _U64, _P, _U64, ctypes.POINTER(_U64)]),
     "gcz_info_get": (ctypes.c_int, [_P, ctypes.POINTER(_Info)]),
     "gcz_copy_leaves": (ctypes.c_int, [_P, _P]),
     "gcz_copy_layer": (ctypes.c_int, [_P, ctypes.c_int, _P]),
@@ -90,7 +90,7 @@ _SIGS = {
     "gcz_tree_push_layer": (None, [_P, _P, _U64]),
     "gcz_tree_set_root": (None, [_P, ctypes.c_uint32]),
     "gcz_tree_deserialize": (ctypes.c_int, [_P, ctypes.c_int, _P, _U64]),
-    "gcz_fasta_extract": (_U64, [_P, _U64, _P]),
+    "gcz_fasta_extract": (_U64, [_P, _U64, ctypes.c_int, _U64, _P]),
     "gcz_synth_fill": (None, [_P, ctypes.c_int, _U64, _U64, _U64]),
     "gcz_synth_default_seed": (_U64, []),
     "gcz_sort_device": (ctypes.c_int, [_P]),
@@ -132,11 +132,12 @@ def _ptr(a):
 
 
 # ---- host utilities ---------------------------------------------------------
-def fasta_extract(data: bytes) -> bytes:
-    """Concatenated bases under the reference reader's line contract."""
+def fasta_extract(data: bytes, L: int = 12, buffer_strands: int = 0) -> bytes:
+    """Concatenated bases under the reference reader's line contract, for leaves of
+    L nucleotides read through buffers of buffer_strands strands (0 = 1 << 22)."""
     buf = np.frombuffer(data, dtype=np.uint8)
     out = np.empty(max(len(data), 1), dtype=np.uint8)
-    n = _lib.gcz_fasta_extract(_ptr(buf), len(data), _ptr(out))
+    n = _lib.gcz_fasta_extract(_ptr(buf), len(data), L, buffer_strands, _ptr(out))
     return out[:n].tobytes()
 
 
@@ -372,13 +373,13 @@ class Context:
         """FASTA file bytes already in device memory: line contract + build on the device."""
         return self._check(_lib.gcz_build_device_fasta(self._h, ctypes.c_void_p(dev_ptr), nbytes, L))
 
-    def fasta_extract_device(self, data: bytes) -> bytes:
+    def fasta_extract_device(self, data: bytes, L: int = 12, buffer_strands: int = 0) -> bytes:
         """The device line contract on `data` (uploaded), bases back to the host."""
         buf = self.upload(np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, np.uint8))
         try:
             n = _U64()
             out = DeviceBuffer(self, max(len(data), 1))
-            rc = _lib.gcz_fasta_extract_device(self._h, ctypes.c_void_p(buf.ptr), len(data),
+            rc = _lib.gcz_fasta_extract_device(self._h, ctypes.c_void_p(buf.ptr), len(data), L, buffer_strands,
                                                ctypes.c_void_p(out.ptr), max(len(data), 1), ctypes.byref(n))
             if rc != GCZ_OK:
                 raise GczError(rc, "gcz_fasta_extract_device failed")

@@ -103,9 +103,10 @@ GCZ_API int gcz_build_host_leaves(gcz_ctx *ctx, const uint64_t *leaves, uint64_t
 /* A FASTA file already in device memory: the line contract (headers, blank lines;
  * src/fasta_reader.cpp:40-68) runs on the device, then the build. */
 GCZ_API int gcz_build_device_fasta(gcz_ctx *ctx, const void *d_file, uint64_t n, int L);
-/* The device line contract alone: bases of d_file into d_out (cap bytes; null: count only). */
-GCZ_API int gcz_fasta_extract_device(gcz_ctx *ctx, const void *d_file, uint64_t n, void *d_out, uint64_t cap,
-                                     uint64_t *nbases);
+/* The device line contract alone (as gcz_fasta_extract): bases of d_file into d_out
+ * (cap bytes; null: count only). */
+GCZ_API int gcz_fasta_extract_device(gcz_ctx *ctx, const void *d_file, uint64_t n, int L, uint64_t buffer_strands,
+                                     void *d_out, uint64_t cap, uint64_t *nbases);
 
 GCZ_API int gcz_info_get(gcz_ctx *ctx, gcz_info *out);
 GCZ_API int gcz_copy_leaves(gcz_ctx *ctx, uint64_t *host_out);                /* n_leaves u64 */
@@ -153,9 +154,12 @@ GCZ_API void gcz_tree_set_root(gcz_tree *t, uint32_t root);
 GCZ_API int gcz_tree_deserialize(gcz_tree *t, int L, const uint8_t *buf, uint64_t n);
 
 /* ---- host utilities ---------------------------------------------------- */
-/* FASTA line contract of src/fasta_reader.cpp:40-68 (headers, blank lines);
- * writes the concatenated bases to out (capacity >= n) and returns their count. */
-GCZ_API uint64_t gcz_fasta_extract(const uint8_t *file, uint64_t n, uint8_t *out);
+/* FASTA line contract of src/fasta_reader.cpp:40-68 (headers, blank lines, the
+ * fresh peek where a line crosses a reader buffer of buffer_strands strands;
+ * 0 = the reference default 1 << 22, include/fasta_reader.h:23) for leaves of
+ * L nucleotides; writes the concatenated bases to out (capacity >= n) and
+ * returns their count. */
+GCZ_API uint64_t gcz_fasta_extract(const uint8_t *file, uint64_t n, int L, uint64_t buffer_strands, uint8_t *out);
 /* Synthetic genomes (genome-compression_amd/csrc/synth.h), multi-threaded. */
 GCZ_API void gcz_synth_fill(char *out, int kind, uint64_t seed, uint64_t begin, uint64_t end);
 GCZ_API uint64_t gcz_synth_default_seed(void);

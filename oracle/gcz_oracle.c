@@ -124,25 +124,46 @@ ORC_API void orc_node_canonical(uint32_t l, uint32_t r, uint32_t *cl, uint32_t *
  *  - at each line start, if the byte is '>' or '\n' ONE line is skipped
  *    (fasta_reader.cpp:49-51), then the following line is read as data
  *    without a second peek (so a 2nd header line becomes data);
- *  - data line bodies are concatenated (:52-57).
+ *  - data line bodies are concatenated (:52-57);
+ *  - buffer boundaries.  load_buffer fills cap = B*L data bytes per buffer,
+ *    B = min(file_size/L + 1, buffer_strands) when file_size/L + 1 >= buffer_strands,
+ *    else file_size/L + 1 (:22-31).  A getline that fills the buffer exactly also
+ *    extracts a newline that follows (libstdc++ getline), so a line ending on a
+ *    boundary behaves as anywhere else.  A data line that CROSSES a boundary
+ *    resumes, in the next load_buffer, with a fresh peek at the byte at the
+ *    boundary (:48-51): if that byte is '>', the rest of the line is skipped and
+ *    the following line is read as data.  (Pinned against the compiled reference
+ *    at small buffer sizes by tests/test_reader_boundary.py.)
+ * buffer_strands = 0 means the reference default 1<<22 (fasta_reader.h:23).
  * Truncation to a multiple of L happens in the caller (fasta_reader.cpp:60-61).
- * Known deviation (documented in DESIGN.md): the reader's 2^22-strand buffer
- * boundaries can peek mid-line; that only matters for a '>' or blank line
- * that begins exactly at a 50,331,648-byte data boundary.
  * Returns the number of bases written to out (out must hold n bytes). */
-ORC_API uint64_t orc_fasta_extract(const uint8_t *f, uint64_t n, uint8_t *out) {
+ORC_API uint64_t orc_fasta_extract(const uint8_t *f, uint64_t n, int L, uint64_t buffer_strands, uint8_t *out) {
+  if (!buffer_strands) buffer_strands = (uint64_t)1 << 22;
+  const uint64_t fs = n / (uint64_t)L + 1;
+  const uint64_t cap = (fs < buffer_strands ? fs : buffer_strands) * (uint64_t)L;
   uint64_t pos = 0, j = 0;
+  int forced = 0;   /* the line after a skip is data without a peek */
   while (pos < n) {
-    if (f[pos] == '>' || f[pos] == '\n') {
+    if (!forced && (f[pos] == '>' || f[pos] == '\n')) {
       const uint8_t *nl = memchr(f + pos, '\n', n - pos);
       pos = nl ? (uint64_t)(nl - f) + 1 : n;
-      if (pos >= n) break;
+      forced = 1;
+      continue;
     }
+    forced = 0;
     const uint8_t *nl = memchr(f + pos, '\n', n - pos);
     uint64_t end = nl ? (uint64_t)(nl - f) : n;
+    /* boundaries strictly inside [j, j + len) */
+    for (uint64_t k = j / cap + 1; k * cap < j + (end - pos); ++k) {
+      if (f[pos + (k * cap - j)] == '>') {
+        end = pos + (k * cap - j);
+        forced = 1;
+        break;
+      }
+    }
     memcpy(out + j, f + pos, end - pos);
     j += end - pos;
-    pos = nl ? end + 1 : n;
+    pos = nl ? (uint64_t)(nl - f) + 1 : n;
   }
   return j;
 }

@@ -32,7 +32,7 @@ for name, res, args in [
     ("orc_ptr_xf", _U32, [_U32, _I, _I]),
     ("orc_node_canonical", None, [_U32, _U32, ctypes.POINTER(_U32), ctypes.POINTER(_U32),
                                   ctypes.POINTER(_I), ctypes.POINTER(_I)]),
-    ("orc_fasta_extract", _U64, [_P, _U64, _P]),
+    ("orc_fasta_extract", _U64, [_P, _U64, _I, _U64, _P]),
     ("orc_pack", ctypes.c_int64, [_P, _U64, _I, _P]),
     ("orc_build", _P, [_P, _U64, _I]),
     ("orc_free", None, [_P]),
@@ -126,10 +126,11 @@ class OracleTree:
         return b"".join(parts)
 
 
-def fasta_extract(data: bytes) -> bytes:
+def fasta_extract(data: bytes, L: int = 12, buffer_strands: int = 0) -> bytes:
+    """fasta_reader's bases (buffer_strands 0 = the reference default 1 << 22)."""
     buf = np.frombuffer(data, dtype=np.uint8)
     out = np.empty(max(len(data), 1), dtype=np.uint8)
-    n = _lib.orc_fasta_extract(_ptr(buf), len(data), _ptr(out))
+    n = _lib.orc_fasta_extract(_ptr(buf), len(data), L, buffer_strands, _ptr(out))
     return out[:n].tobytes()
 
 
@@ -155,7 +156,7 @@ def build_leaves(leaves: np.ndarray, L: int) -> OracleTree:
 
 
 def build_fasta(data: bytes, L: int) -> OracleTree:
-    return build_leaves(pack(fasta_extract(data), L), L)
+    return build_leaves(pack(fasta_extract(data, L), L), L)
 
 
 def digest(tree) -> dict:

@@ -11,6 +11,9 @@
 //   dumpleaves <u64.bin> <L> <prefix> shared_tree(std::vector<dna>&)  (shared_tree.cpp:212)
 //   time <kind> <nbases> <L> [reps]  synthetic genome (csrc/synth.h) -> vector<dna> -> build
 //   random <seed>                    prints dna::random(seed) (dna.cpp:92-96) as u64
+//   reader <fasta> <L> <buffer> <out> fasta_reader{path, buffer} (fasta_reader.cpp:13-35) read_into
+//                                    loop (:92-106): u64 strands to out, one u64 buffer size per
+//                                    read_into call to out.bufs (pins the per-buffer line contract)
 //
 // dump outputs (all little-endian):
 //   prefix.leaves.bin   u64 per leaf (first-occurrence order, before sort)
@@ -25,6 +28,7 @@
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <filesystem>
@@ -35,6 +39,7 @@
 #include <limits>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <numeric>
 #include <random>
 #include <sstream>
@@ -59,6 +64,19 @@
 #undef private
 
 #include "../genome-compression_amd/csrc/synth.h"
+
+// fasta_reader::load_buffer passes getline a count of char_buffer.size() - position + 1
+// (fasta_reader.cpp:52), so a getline that fills the buffer stores its '\0' one byte past
+// the vector.  At the default 2^22-strand buffer that byte lands in the slack of the
+// page-rounded mmap chunk; at the small buffer sizes the reader tests use, it lands in
+// the next heap chunk's header.  Every allocation gets 16 bytes of slack so the
+// reference's behaviour is defined at every buffer size (the reference is unmodified).
+void* operator new(std::size_t n) {
+  if (void* p = std::malloc(n + 16)) return p;
+  throw std::bad_alloc{};
+}
+void operator delete(void* p) noexcept { std::free(p); }
+void operator delete(void* p, std::size_t) noexcept { std::free(p); }
 
 static uint32_t word(const pointer& p) {
   return (uint32_t)p.data | ((uint32_t)p.mirror << 29) | ((uint32_t)p.transpose << 30) |
@@ -166,6 +184,21 @@ int main(int argc, char** argv) {
                 "\"n_leaves\": %llu, \"n_nodes\": %llu, \"threads\": 1}\n",
                 bases, best_pack, best_build, bases / ((best_pack + best_build) * 1e-3),
                 (unsigned long long)leaves, (unsigned long long)nodes);
+    return 0;
+  }
+  if (mode == "reader" && argc == 6) {
+    dna::size(std::atoi(argv[3]));
+    fasta_reader file{std::filesystem::path{argv[2]}, std::strtoull(argv[4], nullptr, 10)};
+    std::ofstream f(argv[5], std::ios::binary), fb(std::string(argv[5]) + ".bufs", std::ios::binary);
+    std::vector<dna> buffer;
+    while (file.read_into(buffer)) {
+      uint64_t n = buffer.size();
+      fb.write((const char*)&n, 8);
+      for (const auto& d : buffer) {
+        uint64_t v = d.to_ullong();
+        f.write((const char*)&v, 8);
+      }
+    }
     return 0;
   }
   if (mode == "random" && argc == 3) {

@@ -66,6 +66,10 @@ def case_input(case, gcz_mod):
         return "leaves", np.fromfile(os.path.join(GOLDEN, case["input"]), dtype="<u8"), L
     if case["kind"] == "synth":
         return "fasta", gcz_mod.synth(case["synth_kind"], case["nbases"]).tobytes(), L
+    if case["kind"] == "fastabig":   # regenerated (tests/golden/fasta_big.py), ~100 MB
+        sys.path.insert(0, GOLDEN)
+        import fasta_big
+        return "fasta", fasta_big.make(case["name"]), L
     raise ValueError(case["kind"])
 
 

@@ -66,7 +66,7 @@ def _dist_build(gcz, group, kind, payload, L):
     """Upload the whole input once, hand every virtual rank a pointer to its strands."""
     ctx0 = group.ctx(0)
     if kind == "fasta":
-        bases = np.frombuffer(gcz.fasta_extract(payload), dtype=np.uint8)
+        bases = np.frombuffer(gcz.fasta_extract(payload, L), dtype=np.uint8)
         S = len(bases) // L
         buf = ctx0.upload(bases if len(bases) else np.zeros(1, np.uint8))
         ptrs = [buf.ptr + gcz.dist_plan(max(S, 1), group.world, r)[0] * L for r in range(group.world)]
@@ -187,7 +187,7 @@ def test_dist_rccl_world1(gcz, manifest):
         for name in ("corpus/chmpxx", "corpus/merged"):
             case = manifest[name]
             kind, payload, L = case_input(case, gcz)
-            bases = np.frombuffer(gcz.fasta_extract(payload), dtype=np.uint8)
+            bases = np.frombuffer(gcz.fasta_extract(payload, L), dtype=np.uint8)
             buf = ctx.upload(bases)
             try:
                 g.build_device_bases([buf.ptr], len(bases) // L, L)

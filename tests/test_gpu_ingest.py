@@ -71,3 +71,45 @@ def test_device_fasta_build_matches_reference(name, ctx, gcz, manifest):
     finally:
         buf.free()
     assert compare_digest(gcz.digest(ctx.tree()), exp) == {}
+
+
+# ---- reader buffers (src/fasta_reader.cpp:22-31,47-64; tests/test_reader_boundary.py) ----
+def test_device_reader_cases_match_reference(ctx, oracle):
+    """The device ingest at reader buffers of 1-8 strands == the compiled reference's strands."""
+    with open(os.path.join(GOLDEN, "reader_cases.json")) as f:
+        cases = json.load(f)
+    for i, c in enumerate(cases):
+        data, L, buf = bytes.fromhex(c["input_hex"]), c["L"], c["buffer"]
+        bases = ctx.fasta_extract_device(data, L, buf)
+        assert bases == oracle.fasta_extract(data, L, buf), (i, data, L, buf)
+        try:
+            got = [int(v) for v in oracle.pack(bases, L)]
+        except oracle.OracleError as e:
+            got = str(e)
+        exp = c["expect"]["strands"] if c["expect"]["exit"] == 0 else c["expect"]["stderr"]
+        assert got == exp, (i, data, L, buf)
+
+
+def _big_cases():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        m = json.load(f)
+    return [n for n, c in sorted(m.items()) if c["kind"] == "fastabig"]
+
+
+@pytest.mark.parametrize("name", _big_cases())
+def test_device_fasta_big_matches_reference(name, ctx, gcz, manifest):
+    """~100 MB wrapped multi-record FASTA over two reader buffers (headers, blank
+    lines, '>' at the boundaries), uploaded and built like shared_tree{path}."""
+    case = manifest[name]
+    exp = case["expect"]
+    kind, payload, L = case_input(case, gcz)
+    if exp["exit"] != 0:
+        with pytest.raises(gcz.GczError) as ei:
+            ctx.build_fasta(payload, L)
+        assert ei.value.code == gcz.GCZ_ERR_SYMBOL
+        sym = ei.value.info["error_symbol"]
+        sym = sym - 32 if 97 <= sym <= 122 else sym
+        assert f"Encountered unknown symbol: {sym} (ASCII code {sym})" == exp["stderr"]
+        return
+    ctx.build_fasta(payload, L)
+    assert compare_digest(gcz.digest(ctx.tree()), exp) == {}

@@ -32,7 +32,7 @@ def test_fasta_extract_matches_oracle(gcz, oracle, manifest):
             continue
         with open(os.path.join(GOLDEN, case["input"]), "rb") as f:
             data = f.read()
-        assert gcz.fasta_extract(data) == oracle.fasta_extract(data), name
+        assert gcz.fasta_extract(data, case["L"]) == oracle.fasta_extract(data, case["L"]), name
 
 
 @pytest.mark.parametrize("name", ["corpus/chmpxx", "corpus/hehcmv", "corpus/merged", "corpus/edited",

@@ -12,7 +12,7 @@ SMALL_CASES = None
 def _cases(manifest, max_bases=12_000_000):
     out = []
     for name, case in sorted(manifest.items()):
-        if case["kind"] == "synth" and case["nbases"] > max_bases:
+        if (case["kind"] == "synth" and case["nbases"] > max_bases) or case["kind"] == "fastabig":
             continue
         out.append(name)
     return out
