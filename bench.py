@@ -103,6 +103,23 @@ def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None, bu
         return 12 * bp + 64 * bp
     if kernel == "bucket_dedupe":   # records in; repeats: mark + word sectors
         return 8 * bp + 128 * max(0, bp - (layer_sizes[0] if layer_sizes else bp))
+    # dense leaf level (pure ACGT, L <= 12; gcz_dense.h): streamed bytes per pass
+    nch = (S + 32767) // 32768
+    NB = min(1024, 4 ** L)
+    if kernel == "dl_pack":         # bases in, pre-word out, per-chunk bucket counts
+        return S * L + 4 * S + 4 * NB * nch
+    if kernel == "dl_scan":         # exclusive scan of the count matrix
+        return 8 * NB * nch
+    if kernel == "dl_scatter":      # pre-word in, record out
+        return 8 * S
+    if kernel == "dl_first":        # records in, first position per code out, sorted first lists, bitmap
+        return 4 * S + 4 * 4 ** L + 8 * U + S // 8
+    if kernel == "dl_fbscan":       # bitmap in, per-word prefix out
+        return S // 8 + S // 16
+    if kernel == "dl_ids":          # first positions in, two random rank reads per key, id per record out
+        return 4 * 4 ** L + 8 * S + 128 * U
+    if kernel == "dl_words":        # record, id, pre-word, bitmap in; word and the leaves out
+        return 16 * S + S // 8 + 8 * U
     if kernel == "flagscan_leaf":   # not-first marks; firsts: word, slot sector, leaf out, slot->id sector
         return S + U * (4 + 64 + 8 + 64 + 4)
     if kernel == "flagscan_node":   # not-first marks, group records; firsts: pair re-read, node out, word
@@ -189,7 +206,8 @@ def stream_digest(group, dist, rank, world, info):
     return {"sha_leaves_bin": h_leaves.hexdigest(), "sha_layers_bin": h_layers.hexdigest()}
 
 
-LEAF_SCOPES = ("leaf_insert", "flagscan_leaf", "resolve_leaf")
+LEAF_SCOPES = ("leaf_insert", "flagscan_leaf", "resolve_leaf", "dl_pack", "dl_scan", "dl_scatter", "dl_first",
+               "dl_fbscan", "dl_ids", "dl_words")
 
 
 def rank_summary(rank, build_ms, trace):

@@ -4,6 +4,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include "gcz_ctx.h"
+#include "gcz_dense.h"
+#include "gcz_scan.h"
 
 using namespace gcz_dev;
 using namespace gcz_host;
@@ -140,6 +142,131 @@ int gcz_ctx::leaf_level(const LeafLevel& a, Header* d_hdr) {
     HIP_TRY(hipGetLastError());
     prof_end(KID_RESOLVE_LEAF, e0);
   }
+  return GCZ_OK;
+}
+
+namespace {
+
+template <bool kBases>
+void launch_dl_pack(int L, dim3 g, hipStream_t st, const unsigned char* b, const u64* lv, const DensePlan& P,
+                    u32* pw, u32* cnt, Header* hdr) {
+  switch (L) {
+#define GCZ_CASE(X)                                                                                          \
+  case X:                                                                                                    \
+    hipLaunchKernelGGL((k_dl_pack<X, kBases>), g, dim3(kDThreads), 0, st, b, lv, P, pw, cnt, hdr);         \
+    break;
+    GCZ_CASE(1) GCZ_CASE(2) GCZ_CASE(3) GCZ_CASE(4) GCZ_CASE(5) GCZ_CASE(6) GCZ_CASE(7) GCZ_CASE(8)
+    GCZ_CASE(9) GCZ_CASE(10) GCZ_CASE(11) GCZ_CASE(12)
+#undef GCZ_CASE
+    default: break;
+  }
+}
+
+template <class F>
+hipError_t allow_lds(F f, int bytes) {   // dynamic LDS above the default 64 KB
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
+}  // namespace
+
+int gcz_ctx::leaf_level_dense(const LeafLevel& a, Header* d_hdr, u64* ucount, bool* used) {
+  *used = false;
+  const u64 S = a.S;
+  const u32 L = u32(a.L);
+  if (L < 1 || L > 12 || S == 0) return GCZ_OK;
+  DensePlan P{};
+  P.S = S;
+  P.L = L;
+  P.nch = u32((S + kDC - 1) / kDC);
+  P.cmask = u32((1ull << (2 * L)) - 1);
+  const u32 cbits = 2 * L;
+  // 1024 buckets: LDS tables of RB = 2^14 codes (64 KB, two workgroups per CU) at L = 12
+  P.NB = u32(std::min<u64>(kDNBMax, 1ull << cbits));
+  P.IB = cbits - log2_exact(P.NB);
+  const u32 kmul = 0x5bd1e995u;                     // odd: a bijection mod 4^L
+  u32 Ki = kmul;
+  for (int i = 0; i < 5; ++i) Ki *= 2u - kmul * Ki;   // inverse mod 2^32 (hence mod 4^L)
+  P.K = kmul & P.cmask;
+  P.Kinv = Ki & P.cmask;
+  const u64 ncnt = u64(P.NB) * P.nch;
+  const u64 nfb = (S + 63) / 64;
+  const u64 t_cnt = scan_tiles(ncnt + 1), t_fb = scan_tiles(nfb + 1);
+  int rc;
+  if ((rc = ensure(dl_pw, S * 4 + 16)) || (rc = ensure(dl_rec, S * 4 + 16)) || (rc = ensure(dl_idrec, S * 4 + 16)) ||
+      (rc = ensure(dl_cnt, ncnt * 4 + 16)) || (rc = ensure(dl_off, (ncnt + 1) * 4 + 16)) ||
+      (rc = ensure(dl_fpg, (u64(1) << cbits) * 4 + 16)) || (rc = ensure(dl_fb, nfb * 8 + 16)) ||
+      (rc = ensure(dl_wpre, (nfb + 1) * 4 + 16)) || (rc = ensure(dl_desc, (t_cnt + t_fb) * 8 + 16)) ||
+      (rc = ensure(dl_fl, (u64(1) << cbits) * 4 + 16)) || (rc = ensure(dl_fo, u64(P.NB) * (P.nch + 1) * 4 + 16)))
+    return rc;
+  u64* sdesc = dl_desc.as<u64>();
+  u32* tickets = reinterpret_cast<u32*>(sdesc + t_cnt + t_fb);
+  const int RBbytes = int((1u << P.IB) * 4);
+  const int first_bytes = int(((1u << P.IB) + P.nch + 1) * 4);
+  if (first_bytes > 160 * 1024) return GCZ_OK;   // (never at L <= 12, S < 2^29)
+  const int scat_bytes = int((kDC + 3 * kDNBMax + 1 + 16) * 4);
+  const int words_bytes = int((kDC + 2 * kDNBMax + 1 + 16) * 4);
+  HIP_TRY(allow_lds(k_dl_scatter, scat_bytes));
+  HIP_TRY(allow_lds(k_dl_first, first_bytes));
+  HIP_TRY(allow_lds(k_dl_ids, RBbytes));
+  HIP_TRY(allow_lds(k_dl_words, words_bytes));
+  hipEvent_t e0{};
+  prof_begin(KID_DL_PACK, e0);
+  HIP_TRY(hipMemsetAsync(dl_desc.ptr, 0, (t_cnt + t_fb) * 8 + 16, stream));
+  if (a.bases)
+    launch_dl_pack<true>(int(L), dim3(P.nch), stream, static_cast<const unsigned char*>(a.bases), nullptr, P,
+                         dl_pw.as<u32>(), dl_cnt.as<u32>(), d_hdr);
+  else
+    launch_dl_pack<false>(int(L), dim3(P.nch), stream, nullptr, a.leaves, P, dl_pw.as<u32>(), dl_cnt.as<u32>(),
+                          d_hdr);
+  HIP_TRY(hipGetLastError());
+  u32 dfail = 0;
+  HIP_TRY(hipMemcpyAsync(&dfail, &d_hdr->dense_fail, 4, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  prof_end(KID_DL_PACK, e0);
+  if (dfail) return GCZ_OK;
+  *used = true;
+  prof_begin(KID_DL_SCAN, e0);
+  hipLaunchKernelGGL(k_scan_excl<ScanU32>, dim3(unsigned(t_cnt)), dim3(kScanThreads), 0, stream,
+                     ScanU32{dl_cnt.as<u32>(), ncnt}, ncnt + 1, dl_off.as<u32>(), sdesc, &tickets[0],
+                     static_cast<u64*>(nullptr));
+  HIP_TRY(hipGetLastError());
+  prof_end(KID_DL_SCAN, e0);
+  prof_begin(KID_DL_SCATTER, e0);
+  hipLaunchKernelGGL(k_dl_scatter, dim3(P.nch), dim3(kDThreads), scat_bytes, stream, dl_pw.as<u32>(), P,
+                     dl_off.as<u32>(), dl_rec.as<u32>());
+  HIP_TRY(hipGetLastError());
+  prof_end(KID_DL_SCATTER, e0);
+  prof_begin(KID_DL_FIRST, e0);
+  hipLaunchKernelGGL(k_dl_first, dim3(P.NB), dim3(kDThreads), first_bytes, stream, dl_rec.as<u32>(), dl_off.as<u32>(),
+                     P, dl_fpg.as<u32>(), dl_fl.as<u32>(), dl_fo.as<u32>());
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_dl_fb, dim3(P.nch), dim3(kDThreads), 0, stream, dl_fl.as<u32>(), dl_fo.as<u32>(), P,
+                     dl_fb.as<unsigned long long>());
+  HIP_TRY(hipGetLastError());
+  prof_end(KID_DL_FIRST, e0);
+  prof_begin(KID_DL_FBSCAN, e0);
+  hipLaunchKernelGGL(k_scan_excl<ScanPopc>, dim3(unsigned(t_fb)), dim3(kScanThreads), 0, stream,
+                     ScanPopc{dl_fb.as<unsigned long long>()}, nfb, dl_wpre.as<u32>(), sdesc + t_cnt, &tickets[1],
+                     ucount);
+  HIP_TRY(hipGetLastError());
+  prof_end(KID_DL_FBSCAN, e0);
+  prof_begin(KID_DL_IDS, e0);
+  hipLaunchKernelGGL(k_dl_ids, dim3(P.NB), dim3(kDThreads), RBbytes, stream, dl_rec.as<u32>(), dl_off.as<u32>(), P,
+                     dl_fpg.as<u32>(), dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), dl_idrec.as<u32>());
+  HIP_TRY(hipGetLastError());
+  prof_end(KID_DL_IDS, e0);
+  prof_begin(KID_DL_WORDS, e0);
+  hipLaunchKernelGGL(k_dl_words, dim3(P.nch), dim3(kDThreads), words_bytes, stream, dl_pw.as<u32>(),
+                     dl_rec.as<u32>(), dl_idrec.as<u32>(), dl_off.as<u32>(), P, dl_fb.as<unsigned long long>(),
+                     a.words, a.out);
+  HIP_TRY(hipGetLastError());
+  // repetitive data? (the node inserts' LDS pre-dedupe), on the final words of a sample
+  const u64 ip = std::min<u64>(S, u64(1) << 21);
+  hipLaunchKernelGGL(k_dup_probe, dim3(unsigned((ip + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, a.words,
+                     u64(0), ip, d_hdr);
+  hipLaunchKernelGGL(k_dup_decide, dim3(1), dim3(1), 0, stream, d_hdr, ip, u32(predup_mode));
+  HIP_TRY(hipGetLastError());
+  prof_end(KID_DL_WORDS, e0);
   return GCZ_OK;
 }
 
@@ -316,7 +443,9 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   // (every ACGT 12-mer class fits) and grow after an overflow.
   const u64 full_cap = std::max<u64>(256, next_pow2(2 * S));
   u64 leaf_cap = full_cap;
-  if (S > (1ull << 22)) leaf_cap = std::min(full_cap, std::max<u64>(1ull << 24, leaf_cap_hint));
+  // (each call starts here: no state carries over between builds; a probe overflow
+  // grows the table and rebuilds, counted in info.attempts)
+  if (S > (1ull << 22)) leaf_cap = std::min(full_cap, u64(1) << 24);
   if (leaf_cap_log2 > 0 && S > (1ull << 22)) leaf_cap = std::min(full_cap, 1ull << leaf_cap_log2);
   const u64 node_cap0 = node_cap(pk[0]);
 
@@ -364,7 +493,12 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     la.desc_off = desc_off;
     la.count = d_hdr->count;
     la.ticket = d_hdr->ticket;
-    if ((rc = leaf_level(la, d_hdr))) return rc;
+    dense_used = false;
+    if (dense_mode != 0 && L <= 12 && (S >= dense_min || dense_mode == 2)) {
+      if ((rc = leaf_level_dense(la, d_hdr, &d_hdr->count[C - 1], &dense_used))) return rc;
+      if (!dense_used) HIP_TRY(hipMemsetAsync(&d_hdr->dense_fail, 0, 4, stream));
+    }
+    if (!dense_used && (rc = leaf_level(la, d_hdr))) return rc;
 
     // ---- node layers ----
     u32* in = A;
@@ -444,6 +578,8 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, ev_start, ev_stop));
     info.build_ms = ms;
+    info.build_ms_all += ms;
+    info.attempts += 1;
     if (profile) prof_collect();
     if (h_hdr->bkt_overflow && bucket_now) {      // a hot key overflowed a bucket: rebuild with the table
       bucket_now = false;
@@ -472,12 +608,11 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     return fail(GCZ_ERR_CAPACITY, "build", "hash table probe limit exceeded");
   info.n_layers = D;
   info.n_leaves = h_hdr->count[C - 1];
-  // next build starts its adaptive leaf table at load <= 1/4..1/2 (speed only)
-  leaf_cap_hint = next_pow2(std::max<u64>(1, info.n_leaves * 2));
   for (int k = 0; k < D; ++k) info.layer_size[k] = h_hdr->count[kLayerSlot + k];
   info.root = h_hdr->root;
   for (int i = 0; i < 64; ++i) info.hashed_pairs += h_hdr->hashed[i];
   info.bucketed_pairs = h_hdr->hashed[1];
+  info.leaf_path = dense_used ? 1u : 0u;
   return GCZ_OK;
 }
 
@@ -505,6 +640,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   if (const char* t = std::getenv("GCZ_PREDUP")) c->predup_mode = std::atoi(t);   // 1 on, 2 off, 0 auto
   if (const char* t = std::getenv("GCZ_BUCKET")) c->use_bucket = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_BUCKET_MIN")) c->bucket_min = std::strtoull(t, nullptr, 10);
+  if (const char* t = std::getenv("GCZ_DENSE")) c->dense_mode = std::atoi(t);
   if (const char* t = std::getenv("GCZ_LEAF_FIRST_LOG2")) c->leaf_first_log2 = std::max(1, std::min(20, std::atoi(t)));
   *out = c;
   return GCZ_OK;
@@ -518,7 +654,9 @@ void gcz_ctx_destroy(gcz_ctx* c) {
   gcz_sort_state_free(c);
   gcz_ingest_state_free(c);
   for (DevBuf* b : {&c->wa, &c->wb, &c->grp, &c->desc, &c->tab, &c->leaves_out, &c->nodes_out, &c->hdr, &c->input,
-                    &c->nf, &c->multi, &c->stats})
+                    &c->nf, &c->multi, &c->stats, &c->bkt_key, &c->bkt_cnt, &c->bkt_off, &c->bkt_tmp, &c->dl_pw,
+                    &c->dl_rec, &c->dl_idrec, &c->dl_cnt, &c->dl_off, &c->dl_fpg, &c->dl_fb, &c->dl_wpre,
+                    &c->dl_desc, &c->dl_fl, &c->dl_fo})
     if (b->ptr) (void)hipFree(b->ptr);
   if (c->h_hdr) (void)hipHostFree(c->h_hdr);
   for (auto e : c->event_pool) (void)hipEventDestroy(e);

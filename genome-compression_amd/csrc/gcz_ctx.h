@@ -97,13 +97,16 @@ inline LevelTab plan_table(void* buf, u64 cap, u32 K, u64 npos, u32 B, bool allo
 enum KernelId {
   KID_LEAF, KID_NODE, KID_FLAGSCAN_LEAF, KID_FLAGSCAN_NODE, KID_RESOLVE_LEAF, KID_RESOLVE_NODE, KID_MEMSET,
   KID_EXCHANGE, KID_DIST, KID_OWNER, KID_IDS, KID_REMAP, KID_TAIL, KID_SORT, KID_DAG, KID_DIRECT,
-  KID_BKT_COUNT, KID_BKT_SCAN, KID_BKT_SCATTER, KID_BKT_DEDUPE, KID_COUNT
+  KID_BKT_COUNT, KID_BKT_SCAN, KID_BKT_SCATTER, KID_BKT_DEDUPE,
+  KID_DL_PACK, KID_DL_SCAN, KID_DL_SCATTER, KID_DL_FIRST, KID_DL_FBSCAN, KID_DL_IDS, KID_DL_WORDS, KID_COUNT
 };
 inline const char* kernel_name(int k) {
   static const char* names[KID_COUNT] = {"leaf_insert", "node_insert", "flagscan_leaf", "flagscan_node",
                                          "resolve_leaf", "resolve_node", "clear", "exchange", "dist_bucket",
                                          "dist_owner", "dist_ids", "dist_remap", "tail", "sort", "dag_write", "direct_levels",
-                                         "bucket_count", "bucket_scan", "bucket_scatter", "bucket_dedupe"};
+                                         "bucket_count", "bucket_scan", "bucket_scatter", "bucket_dedupe",
+                                         "dl_pack", "dl_scan", "dl_scatter", "dl_first", "dl_fbscan", "dl_ids",
+                                         "dl_words"};
   return names[k];
 }
 
@@ -167,6 +170,7 @@ struct gcz_ctx {
   gcz_host::DevBuf wa, wb, grp, desc, tab, leaves_out, nodes_out, hdr, input, nf, multi;
   gcz_host::DevBuf stats;   // hashed-pair counter shards (k_node_insert), summed into hdr->hashed[0]
   gcz_host::DevBuf bkt_key, bkt_cnt, bkt_off, bkt_tmp;   // bucketed node insert (k_bkt_*)
+  gcz_host::DevBuf dl_pw, dl_rec, dl_idrec, dl_cnt, dl_off, dl_fpg, dl_fb, dl_wpre, dl_desc, dl_fl, dl_fo;   // dense leaf level
   gcz_dev::Header* h_hdr = nullptr;   // pinned
   unsigned char* nf_set[2] = {nullptr, nullptr};      // marks, even / odd layers
   unsigned char* multi_set[2] = {nullptr, nullptr};
@@ -187,6 +191,9 @@ struct gcz_ctx {
   bool use_bucket = true;    // bucketed LDS node insert on non-repetitive data  (GCZ_BUCKET=0 disables)
   gcz_host::u64 bucket_min = 1ull << 20;   // ... on levels of at least this many pairs (GCZ_BUCKET_MIN)
   bool bucket_now = true;    // this build (cleared after a bucket overflow: rebuild with the table)
+  int dense_mode = 1;        // dense leaf level (gcz_dense.h): 0 off, 1 on large pure-ACGT inputs, 2 any size (GCZ_DENSE)
+  gcz_host::u64 dense_min = 1ull << 21;   // ... from this many strands (mode 1)
+  bool dense_used = false;   // the last build's leaf level ran dense
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> event_pool;
   size_t event_used = 0;
@@ -262,6 +269,10 @@ struct gcz_ctx {
   int ensure_marks(gcz_host::u64 S);
 
   int leaf_level(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr);
+  // The dense leaf level (pure-ACGT strands, L <= 12); *used = false when a strand is
+  // not pure ACGT (the caller then runs leaf_level).  Writes a.words, a.out and the
+  // unique count to *ucount.
+  int leaf_level_dense(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr, gcz_host::u64* ucount, bool* used);
   int node_level(const gcz_host::NodeLevel& a, gcz_dev::Header* d_hdr);
   // Known-direct levels k0..k0+nlev-1 in one launch (gcz_device.h k_direct_levels).
   int direct_levels(const gcz_host::u32* in, int k0, int nlev, const gcz_dev::DirectPlan& dp, gcz_host::u32* out,

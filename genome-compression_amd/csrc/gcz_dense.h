@@ -1,0 +1,488 @@
+// Dense leaf level: tree_constructor::emplace_leaf (src/shared_tree.cpp:630-637)
+// for genomes whose strands are all A/C/G/T and L <= 12, without a hash table.
+//
+// A pure-ACGT strand is a 2L-bit code (A,C,G,T -> 0..3 keeps the numeric order
+// of the nibble codes 1,2,4,8, so transposition is `x ^ mask`, mirroring a
+// 2-bit-group reverse, and the canonical choice is the same as dna::canonical,
+// src/dna.cpp:135-143).  Canonical codes live in [0, 4^L): the level is a
+// bucketed sort, all LDS-resident, with no random HBM access per strand:
+//
+//   pack     one pass over the bases: canonical code c, m/t/v, hashed code
+//            h = c*K mod 4^L (a bijection, balances the buckets); writes the
+//            pre-word (h | m t v) per strand and a per-chunk histogram of the
+//            NB buckets (h's top bits) -> count matrix, bucket-major.
+//   scan     exclusive sum of the count matrix (gcz_scan.h).
+//   scatter  per chunk of 32 Ki strands: records (h's low bits, position in
+//            the chunk) staged in LDS by bucket, written as contiguous runs.
+//   first    one workgroup per bucket: LDS table of the bucket's RB codes,
+//            atomicMin of the position -> each key's first occurrence; sets
+//            that position's bit in the first-occurrence bitmap FB.
+//   fbscan   popcount prefix of FB words: ids = first-occurrence ranks
+//            (the reference's parent.leaf_count() at emplace time).
+//   ids      per bucket: the id of every present key (FB rank of its first
+//            position) in LDS -> one id per record, bucket order.
+//   words    per chunk: the chunk's records' ids back into position order in
+//            LDS, + the pre-word's m/t/v -> final words; first occurrences
+//            (FB bit) write their leaf, whose ids are consecutive in position order.
+//
+// Strands that are not pure ACGT (IUPAC, invalid symbols, L > 12) set
+// hdr->dense_fail in the pack; the host then runs the hash-table leaf level.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "gcz_device.h"
+
+namespace gcz_dev {
+
+constexpr int kDLog = 15;
+constexpr u32 kDC = 1u << kDLog;     // strands per chunk (positions in a chunk fit 15 bits)
+constexpr int kDThreads = 1024;
+constexpr u32 kDNBMax = 1024;        // buckets (h's top bits)
+
+struct DensePlan {
+  u64 S;
+  u32 nch;     // chunks of kDC strands
+  u32 L;
+  u32 cmask;   // 4^L - 1
+  u32 NB;      // buckets, power of two <= kDNBMax
+  u32 IB;      // log2(codes per bucket) <= kDLog
+  u32 K, Kinv; // odd multiplier mod 4^L and its inverse
+};
+
+// ACGT (any case) -> 0..3; other valid IUPAC symbols -> 4; unknown -> 5
+__device__ __forceinline__ int acgt_code(int c) {
+  const int u = (c >= 'a' && c <= 'z') ? c - 32 : c;
+  switch (u) {
+    case 'A': return 0; case 'C': return 1; case 'G': return 2; case 'T': return 3;
+    default: return nac_code(c) >= 0 ? 4 : 5;
+  }
+}
+
+// reverse the L 2-bit groups of x (dna::mirrored on the 2-bit code, dna.cpp:116-121)
+__device__ __forceinline__ u32 rev2(u32 x, u32 L) {
+  u32 r = __brev(x);
+  r = ((r >> 1) & 0x55555555u) | ((r & 0x55555555u) << 1);
+  return r >> (32 - 2 * L);
+}
+
+// dna::canonical on a 2-bit code: min over (x,F,F) (T,F,T) (M,T,F) (I,T,T) (dna.cpp:135-143)
+__device__ __forceinline__ u32 canon2(u32 x, u32 L, u32 cmask, u32& m, u32& t, u32& v) {
+  const u32 tx = x ^ cmask, mx = rev2(x, L), ix = mx ^ cmask;
+  v = x == mx;
+  u32 best = x;
+  m = 0; t = 0;
+  if (tx < best) { best = tx; m = 0; t = 1; }
+  if (mx < best) { best = mx; m = 1; t = 0; }
+  if (ix < best) { best = ix; m = 1; t = 1; }
+  return best;
+}
+
+// 2-bit code -> nibble-packed dna value (A,C,G,T = 1,2,4,8 at bits 4i, include/dna.h:20-32)
+__device__ __forceinline__ u64 code2_leaf(u32 c, u32 L) {
+  u64 v = 0;
+  for (u32 i = 0; i < L; ++i) v |= u64(1u << ((c >> (2 * i)) & 3u)) << (4 * i);
+  return v;
+}
+
+// Block-wide exclusive scan of one u32 per thread (kDThreads threads); returns
+// the thread's exclusive prefix, *total = the block sum.  s_tmp: 16 u32.
+__device__ __forceinline__ u32 block_excl(u32 x, u32* s_tmp, u32* total) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  u32 incl = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u32 y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) s_tmp[wave] = incl;
+  __syncthreads();
+  u32 before = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < kDThreads / 64; ++w) {
+    const u32 v = s_tmp[w];
+    before += w < wave ? v : 0u;
+    all += v;
+  }
+  *total = all;
+  __syncthreads();
+  return before + incl - x;
+}
+
+// The runs (b, ch) of one chunk: s_base[b] = local exclusive offset (s_base[NB] = the
+// chunk's strands), s_dst[b] = the run's start in the record array.
+__device__ __forceinline__ void chunk_runs(const u32* __restrict__ off, const DensePlan& P, u32 ch, u32* s_base,
+                                           u32* s_dst, u32* s_tmp) {
+  const u32 b = threadIdx.x;   // NB <= kDThreads
+  u32 c = 0, d = 0;
+  if (b < P.NB) {
+    const u64 k = u64(b) * P.nch + ch;   // run (b, ch) = [off[k], off[k + 1]) in the flat bucket-major order
+    d = off[k];
+    c = off[k + 1] - d;
+  }
+  u32 total;
+  const u32 e = block_excl(c, s_tmp, &total);
+  if (b < P.NB) {
+    s_base[b] = e;
+    s_dst[b] = d;
+  }
+  if (b == 0) s_base[P.NB] = total;
+  __syncthreads();
+}
+
+// last bucket b with s_base[b] <= q (runs of zero length are skipped)
+__device__ __forceinline__ u32 run_of(const u32* s_base, u32 NB, u32 q) {
+  u32 lo = 0, hi = NB - 1;
+  while (lo < hi) {
+    const u32 mid = (lo + hi + 1) >> 1;
+    if (s_base[mid] <= q) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+constexpr int kDBatch = 8;   // strands / records in flight per thread
+
+// L bytes of strand s from 4-B aligned loads (no LDS staging)
+template <int L>
+__device__ __forceinline__ void load_strand(const unsigned char* __restrict__ bases, u64 s, u32 (&w)[4]) {
+  const u64 a = s * L;
+  const u32* p = reinterpret_cast<const u32*>(bases + (a & ~3ull));
+  constexpr int NW = (L + 3 + 3) / 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = i < NW ? p[i] : 0u;
+}
+
+// Pack: the strand's pre-word make_word(h, m, t, v) and the chunk's bucket histogram.
+// Bases: L bytes per strand (dna::dna(string_view), src/dna.cpp:79-84); leaves: u64.
+template <int L, bool kBases>
+__global__ __launch_bounds__(kDThreads) void k_dl_pack(const unsigned char* __restrict__ bases,
+                                                       const u64* __restrict__ leaves, DensePlan P,
+                                                       u32* __restrict__ pw, u32* __restrict__ cnt,
+                                                       Header* __restrict__ hdr) {
+  __shared__ u32 s_hist[kDNBMax];
+  __shared__ signed char s_lut[256];
+  const int tid = threadIdx.x;
+  if (tid < 256) s_lut[tid] = (signed char)acgt_code(tid);
+  for (u32 b = tid; b < P.NB; b += kDThreads) s_hist[b] = 0;
+  const u64 c0 = u64(blockIdx.x) * kDC;
+  const u32 ib = P.IB;
+  bool fail = false;
+  __syncthreads();
+  for (u32 it = 0; it < kDC / kDThreads; it += kDBatch) {
+    u32 w[kDBatch][4];
+    u64 lv[kDBatch];
+#pragma unroll
+    for (int j = 0; j < kDBatch; ++j) {
+      const u64 s = c0 + u64(it + j) * kDThreads + tid;
+      if constexpr (kBases) {
+        if (s < P.S) load_strand<L>(bases, s, w[j]);
+      } else {
+        lv[j] = s < P.S ? leaves[s] : 0ull;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kDBatch; ++j) {
+      const u64 s = c0 + u64(it + j) * kDThreads + tid;
+      if (s >= P.S) continue;
+      u32 x = 0;
+      bool ok = true;
+      if constexpr (kBases) {
+        const u32 sh = u32(s * L) & 3u;
+#pragma unroll
+        for (int c = 0; c < L; ++c) {
+          const u32 byte_i = sh + u32(c);
+          const u32 ch = (w[j][byte_i >> 2] >> (8 * (byte_i & 3))) & 0xffu;
+          const int k = s_lut[ch];
+          ok &= k < 4;
+          x |= u32(k & 3) << (2 * c);
+        }
+      } else {
+        const u64 v = lv[j];
+        if (L < 16 && (v >> (4 * L))) ok = false;
+#pragma unroll
+        for (int c = 0; c < L; ++c) {
+          const u32 nib = u32(v >> (4 * c)) & 15u;
+          ok &= nib != 0 && (nib & (nib - 1)) == 0;
+          x |= u32(__ffs(nib) - 1) << (2 * c);
+        }
+      }
+      fail |= !ok;
+      if (ok) {
+        u32 m, t, v;
+        const u32 cc = canon2(x, L, P.cmask, m, t, v);
+        const u32 h = (cc * P.K) & P.cmask;
+        pw[s] = make_word(h, m, t, v);
+        atomicAdd(&s_hist[h >> ib], 1u);
+      }
+    }
+  }
+  if (__ballot(fail) && (tid & 63) == 0) atomicOr(&hdr->dense_fail, 1u);
+  __syncthreads();
+  for (u32 b = tid; b < P.NB; b += kDThreads) cnt[u64(b) * P.nch + blockIdx.x] = s_hist[b];
+}
+
+// Scatter: records (h's low IB bits << kDLog | position in chunk) in runs
+// (chunk, bucket) at off[b * nch + chunk] of the bucket-ordered record array,
+// staged in LDS so every run is written contiguously.
+__global__ __launch_bounds__(kDThreads) void k_dl_scatter(const u32* __restrict__ pw, DensePlan P,
+                                                          const u32* __restrict__ off, u32* __restrict__ rec) {
+  extern __shared__ u32 s_dyn[];
+  u32* s_stage = s_dyn;                 // kDC records
+  u32* s_base = s_dyn + kDC;            // NB + 1: local exclusive offsets of the runs
+  u32* s_cur = s_base + kDNBMax + 1;    // NB: cursors
+  u32* s_dst = s_cur + kDNBMax;         // NB: global run starts
+  u32* s_tmp = s_dst + kDNBMax;         // 16
+  const int tid = threadIdx.x;
+  const u32 ch = blockIdx.x;
+  const u64 c0 = u64(ch) * kDC;
+  const u32 n = u32(P.S - c0 < u64(kDC) ? P.S - c0 : u64(kDC));
+  u32 h[kDC / kDThreads];
+#pragma unroll
+  for (u32 j = 0; j < kDC / kDThreads; ++j) {   // every pre-word load in flight at once
+    const u32 q = j * kDThreads + tid;
+    h[j] = q < n ? pw[c0 + q] & kIdx : 0u;
+  }
+  chunk_runs(off, P, ch, s_base, s_dst, s_tmp);
+  if (u32(tid) < P.NB) s_cur[tid] = s_base[tid];
+  __syncthreads();
+  const u32 imask = (1u << P.IB) - 1u;
+#pragma unroll
+  for (u32 j = 0; j < kDC / kDThreads; ++j) {
+    const u32 q = j * kDThreads + tid;
+    if (q < n) {
+      const u32 slot = atomicAdd(&s_cur[h[j] >> P.IB], 1u);
+      s_stage[slot] = ((h[j] & imask) << kDLog) | q;
+    }
+  }
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6;
+  for (u32 b = wave; b < P.NB; b += kDThreads / 64) {   // one run per wave step: contiguous stores
+    const u32 st = s_base[b], len = s_base[b + 1] - st, dst = s_dst[b];
+    for (u32 l = lane; l < len; l += 64) rec[dst + l] = s_stage[st + l];
+  }
+}
+
+// The records of bucket b, [off[b*nch], off[(b+1)*nch]), visited kDBatch per
+// thread at a time; f(record, position).  Each group of consecutive chunks'
+// runs is contiguous, so the chunk of a record is found among the group's run
+// starts held in registers (broadcast by shuffles).
+template <class F>
+__device__ __forceinline__ void bucket_records(const u32* __restrict__ rec, const u32* __restrict__ off,
+                                               const DensePlan& P, u32 b, F f) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int G = 16;   // chunks per wave step
+  const u64 row = u64(b) * P.nch;
+  for (u32 ch0 = u32(wave) * G; ch0 < P.nch; ch0 += (kDThreads / 64) * G) {
+    const u32 nc = P.nch - ch0 < u32(G) ? P.nch - ch0 : u32(G);
+    const u32 bnd = lane <= int(nc) ? off[row + ch0 + lane] : 0u;   // run starts of chunks ch0.., and the end
+    const u32 r0 = __shfl(bnd, 0, 64), r1 = __shfl(bnd, int(nc), 64);
+    u32 st[G];   // run starts of the group's chunks (past nc: never <= a record index)
+#pragma unroll
+    for (int g = 1; g < G; ++g) {
+      const u32 v = __shfl(bnd, g, 64);
+      st[g] = g < int(nc) ? v : ~0u;
+    }
+    for (u32 r = r0 + lane; r < r1; r += 64 * kDBatch) {
+      u32 x[kDBatch];
+#pragma unroll
+      for (int j = 0; j < kDBatch; ++j) {
+        const u32 rj = r + 64u * j;
+        x[j] = rj < r1 ? rec[rj] : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < kDBatch; ++j) {
+        const u32 rj = r + 64u * j;
+        if (rj >= r1) continue;
+        u32 c = 0;   // chunks of the group whose run starts at or before rj, minus one
+#pragma unroll
+        for (int g = 1; g < G; ++g) c += st[g] <= rj ? 1u : 0u;
+        f(x[j], rj, ((ch0 + c) << kDLog) | (x[j] & (kDC - 1)));
+      }
+    }
+  }
+}
+
+// First occurrences: one workgroup per bucket; LDS table of its 2^IB codes.
+// Writes each code's first position to fpg (~0 if absent), and the bucket's
+// first positions sorted by chunk: fl[b * RB + ...], with fo[b * (nch + 1) + ch]
+// the start of chunk ch's (a counting sort in LDS; k_dl_fb gathers them per chunk).
+__global__ __launch_bounds__(kDThreads) void k_dl_first(const u32* __restrict__ rec, const u32* __restrict__ off,
+                                                        DensePlan P, u32* __restrict__ fpg, u32* __restrict__ fl,
+                                                        u32* __restrict__ fo) {
+  extern __shared__ u32 s_dyn[];
+  u32* s_fp = s_dyn;                    // RB codes
+  u32* s_cnt = s_dyn + (1u << P.IB);    // nch + 1 chunk counters
+  __shared__ u32 s_tmp[16];
+  const int tid = threadIdx.x;
+  const u32 b = blockIdx.x, RB = 1u << P.IB;
+  for (u32 i = tid; i < RB; i += kDThreads) s_fp[i] = ~0u;
+  for (u32 c = tid; c <= P.nch; c += kDThreads) s_cnt[c] = 0;
+  __syncthreads();
+  bucket_records(rec, off, P, b, [&](u32 x, u32, u32 pos) {
+    const u32 idx = x >> kDLog;
+    if (s_fp[idx] > pos) atomicMin(&s_fp[idx], pos);
+  });
+  __syncthreads();
+  constexpr int PER = 16;   // codes per thread (RB <= 16 Ki)
+  u32 fp[PER], rk[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const u32 i = u32(k) * kDThreads + tid;
+    fp[k] = i < RB ? s_fp[i] : ~0u;
+    if (i < RB) fpg[u64(b) * RB + i] = fp[k];
+    rk[k] = fp[k] != ~0u ? atomicAdd(&s_cnt[fp[k] >> kDLog], 1u) : 0u;
+  }
+  __syncthreads();
+  // exclusive scan of the nch + 1 counters (a few per thread, in order)
+  const u32 n1 = P.nch + 1, per = (n1 + kDThreads - 1) / kDThreads, c0 = tid * per;
+  u32 loc = 0;
+  for (u32 c = c0; c < c0 + per && c < n1; ++c) loc += s_cnt[c];
+  u32 total;
+  u32 run = block_excl(loc, s_tmp, &total);
+  for (u32 c = c0; c < c0 + per && c < n1; ++c) {
+    const u32 v = s_cnt[c];
+    s_cnt[c] = run;
+    fo[u64(b) * n1 + c] = run;
+    run += v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PER; ++k)
+    if (fp[k] != ~0u) fl[u64(b) * RB + s_cnt[fp[k] >> kDLog] + rk[k]] = fp[k];
+}
+
+// First-occurrence bitmap of one chunk: its first positions from every bucket's
+// sorted list (k_dl_first), set in LDS, written as the chunk's 512 bitmap words.
+__global__ __launch_bounds__(kDThreads) void k_dl_fb(const u32* __restrict__ fl, const u32* __restrict__ fo,
+                                                     DensePlan P, unsigned long long* __restrict__ fb) {
+  __shared__ u32 s_bits[kDC / 32];
+  const int tid = threadIdx.x;
+  const u32 ch = blockIdx.x, RB = 1u << P.IB, n1 = P.nch + 1;
+  for (u32 w = tid; w < kDC / 32; w += kDThreads) s_bits[w] = 0;
+  __syncthreads();
+  for (u32 b = tid; b < P.NB; b += kDThreads) {
+    const u32 o0 = fo[u64(b) * n1 + ch], o1 = fo[u64(b) * n1 + ch + 1];
+    for (u32 k = o0; k < o1; ++k) {
+      const u32 q = fl[u64(b) * RB + k] & (kDC - 1);
+      atomicOr(&s_bits[q >> 5], 1u << (q & 31));
+    }
+  }
+  __syncthreads();
+  for (u32 w = tid; w < kDC / 64; w += kDThreads)
+    fb[u64(ch) * (kDC / 64) + w] = u64(s_bits[2 * w]) | (u64(s_bits[2 * w + 1]) << 32);
+}
+
+struct ScanPopc {   // popcount of each first-occurrence bitmap word
+  const unsigned long long* fb;
+  __device__ __forceinline__ u32 operator()(u64 i) const { return u32(__popcll(fb[i])); }
+};
+
+__device__ __forceinline__ u32 fb_rank(const unsigned long long* __restrict__ fb, const u32* __restrict__ wpre, u32 p) {
+  const unsigned long long w = fb[p >> 6];
+  return wpre[p >> 6] + u32(__popcll(w & ((1ull << (p & 63)) - 1ull)));
+}
+
+// Ids: per bucket, the id of each present code (rank of its first position)
+// in LDS, then one id per record in bucket order.
+__global__ __launch_bounds__(kDThreads) void k_dl_ids(const u32* __restrict__ rec, const u32* __restrict__ off,
+                                                      DensePlan P, const u32* __restrict__ fpg,
+                                                      const unsigned long long* __restrict__ fb,
+                                                      const u32* __restrict__ wpre, u32* __restrict__ idrec) {
+  extern __shared__ u32 s_id[];
+  const int tid = threadIdx.x;
+  const u32 b = blockIdx.x, RB = 1u << P.IB;
+  for (u32 i0 = 0; i0 < RB; i0 += kDThreads * kDBatch) {
+    u32 fp[kDBatch];
+#pragma unroll
+    for (int j = 0; j < kDBatch; ++j) {
+      const u32 i = i0 + u32(j) * kDThreads + tid;
+      fp[j] = i < RB ? fpg[u64(b) * RB + i] : ~0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kDBatch; ++j) {
+      const u32 i = i0 + u32(j) * kDThreads + tid;
+      if (i < RB) s_id[i] = fp[j] != ~0u ? fb_rank(fb, wpre, fp[j]) : 0u;
+    }
+  }
+  __syncthreads();
+  const u64 row = u64(b) * P.nch;
+  const u32 r0 = off[row], r1 = off[row + P.nch];
+  for (u32 r = r0 + tid; r < r1; r += kDThreads * kDBatch) {
+    u32 x[kDBatch];
+#pragma unroll
+    for (int j = 0; j < kDBatch; ++j) {
+      const u32 rj = r + u32(j) * kDThreads;
+      x[j] = rj < r1 ? rec[rj] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kDBatch; ++j) {
+      const u32 rj = r + u32(j) * kDThreads;
+      if (rj < r1) idrec[rj] = s_id[x[j] >> kDLog];
+    }
+  }
+}
+
+// Words: per chunk, the ids of its records back into position order (LDS), the
+// pre-word's m/t/v bits -> final words; first occurrences emit their leaf.
+__global__ __launch_bounds__(kDThreads) void k_dl_words(const u32* __restrict__ pw, const u32* __restrict__ rec,
+                                                        const u32* __restrict__ idrec, const u32* __restrict__ off,
+                                                        DensePlan P, const unsigned long long* __restrict__ fb,
+                                                        u32* __restrict__ words, u64* __restrict__ leaves_out) {
+  extern __shared__ u32 s_dyn[];
+  u32* s_w = s_dyn;                  // kDC ids by position in the chunk
+  u32* s_base = s_dyn + kDC;         // NB + 1
+  u32* s_dst = s_base + kDNBMax + 1; // NB
+  u32* s_tmp = s_dst + kDNBMax;      // 16
+  const int tid = threadIdx.x;
+  const u32 ch = blockIdx.x;
+  const u64 c0 = u64(ch) * kDC;
+  const u32 n = u32(P.S - c0 < u64(kDC) ? P.S - c0 : u64(kDC));
+  chunk_runs(off, P, ch, s_base, s_dst, s_tmp);
+  const int lane = tid & 63, wave = tid >> 6;
+  constexpr int RW = 4;   // runs per wave step (2 loads each in flight per lane)
+  for (u32 b0 = wave; b0 < P.NB; b0 += (kDThreads / 64) * RW) {
+    u32 x[RW], id[RW], dst[RW], len[RW];
+#pragma unroll
+    for (int j = 0; j < RW; ++j) {
+      const u32 b = b0 + u32(j) * (kDThreads / 64);
+      len[j] = 0; dst[j] = 0; x[j] = 0; id[j] = 0;
+      if (b < P.NB) {
+        dst[j] = s_dst[b];
+        len[j] = s_base[b + 1] - s_base[b];
+      }
+      if (u32(lane) < len[j]) {
+        x[j] = rec[dst[j] + lane];
+        id[j] = idrec[dst[j] + lane];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RW; ++j) {
+      if (u32(lane) < len[j]) s_w[x[j] & (kDC - 1)] = id[j];
+      for (u32 l = lane + 64; l < len[j]; l += 64) s_w[rec[dst[j] + l] & (kDC - 1)] = idrec[dst[j] + l];
+    }
+  }
+  __syncthreads();
+  for (u32 q0 = 0; q0 < n; q0 += kDThreads * kDBatch) {
+    u32 p[kDBatch];
+#pragma unroll
+    for (int j = 0; j < kDBatch; ++j) {
+      const u32 q = q0 + u32(j) * kDThreads + tid;
+      p[j] = q < n ? pw[c0 + q] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kDBatch; ++j) {
+      const u32 q = q0 + u32(j) * kDThreads + tid;
+      if (q >= n) continue;
+      const u64 s = c0 + q;
+      const u32 id = s_w[q];
+      words[s] = id | (p[j] & kBits);
+      if ((fb[s >> 6] >> (s & 63)) & 1ull) {
+        const u32 h = p[j] & kIdx;
+        leaves_out[id] = code2_leaf((h * P.Kinv) & P.cmask, P.L);
+      }
+    }
+  }
+}
+
+}  // namespace gcz_dev

@@ -87,6 +87,7 @@ struct Header {
   u32 leaf_overflow;       // the (adaptively sized) leaf table was too small
   u32 root;
   u32 bkt_overflow;         // a node-level bucket exceeded the LDS dedupe (k_bkt_dedupe)
+  u32 dense_fail;           // a strand is not pure ACGT: the dense leaf level does not apply (gcz_dense.h)
 };
 
 // ---- word algebra: reference src/shared_tree.cpp:76-107 --------------------

@@ -65,6 +65,10 @@ typedef struct {
   double build_ms;                   /* device time of the build (hipEvents) */
   uint64_t hashed_pairs;             /* node pairs hash-consed (others skipped as provably unique) */
   uint64_t bucketed_pairs;           /* ... of which through the bucketed LDS dedupe (not the table) */
+  uint32_t leaf_path;                /* 0: hash-table leaf level, 1: dense sort (pure ACGT, L <= 12) */
+  uint32_t attempts;                 /* device builds this call ran: > 1 after a rebuild (a bucket
+                                        overflow, leaf-table regrowth or the wide-table fallback) */
+  double build_ms_all;               /* device time of every attempt (build_ms: the last one) */
 } gcz_info;
 
 /* ---- device context ---------------------------------------------------- */

@@ -43,6 +43,18 @@ def ctx_bucket(gcz):
     c.close()
 
 
+@pytest.fixture(scope="module")
+def ctx_dense(gcz):
+    """A context that runs the dense leaf level (gcz_dense.h) at every size."""
+    os.environ["GCZ_DENSE"] = "2"
+    try:
+        c = gcz.Context(0)
+    finally:
+        del os.environ["GCZ_DENSE"]
+    yield c
+    c.close()
+
+
 def _names(max_bases):
     with open(os.path.join(GOLDEN, "manifest.json")) as f:
         m = json.load(f)
@@ -62,6 +74,43 @@ def test_gpu_bucketed_insert_goldens(name, ctx_bucket, gcz, manifest):
     kind, payload, L = case_input(case, gcz)
     _build(ctx_bucket, kind, payload, L)
     assert compare_digest(gcz.digest(ctx_bucket.tree()), case["expect"]) == {}
+
+
+@pytest.mark.parametrize("name", _names(12_000_000))
+def test_gpu_dense_leaf_goldens(name, ctx_dense, gcz, manifest):
+    """The dense leaf level forced at every size: pure-ACGT inputs with L <= 12 take
+    it, every other input falls back to the hash-table level; both give the
+    reference's tree bit for bit."""
+    case = manifest[name]
+    exp = case["expect"]
+    kind, payload, L = case_input(case, gcz)
+    if exp["exit"] != 0:
+        with pytest.raises(gcz.GczError):
+            _build(ctx_dense, kind, payload, L)
+        return
+    info = _build(ctx_dense, kind, payload, L)
+    assert compare_digest(gcz.digest(ctx_dense.tree()), exp) == {}
+    if name.startswith("synth/"):
+        assert info["leaf_path"] == 1
+
+
+def test_gpu_dense_leaf_random_acgt(ctx_dense, gcz, oracle):
+    """Pure-ACGT leaves at every L <= 12 and sizes around the 32 Ki-strand chunks."""
+    rng = np.random.default_rng(11)
+    acgt = np.array([1, 2, 4, 8], dtype=np.uint64)
+    for L, S in [(12, 1), (12, 2), (12, 1023), (12, 32767), (12, 32768), (12, 32769), (12, 100_003),
+                 (11, 70_001), (10, 65_536), (9, 5_000), (8, 40_000), (7, 3_001), (6, 777), (5, 64), (4, 4097),
+                 (3, 100), (2, 33), (1, 9), (12, 262_147)]:
+        pool = rng.integers(0, 4, size=(max(2, S // 3), L))
+        vals = (acgt[pool] << (4 * np.arange(L, dtype=np.uint64))).sum(axis=1).astype(np.uint64)
+        leaves = vals[rng.integers(0, vals.size, size=S)]
+        info = ctx_dense.build_leaves(leaves, L)
+        assert info["leaf_path"] == 1, (L, S)
+        g = ctx_dense.tree()
+        o = oracle.build_leaves(leaves, L)
+        assert g.leaves_bin() == o.leaves_bin(), (L, S)
+        assert g.layers_bin() == o.layers_bin(), (L, S)
+        assert g.root == o.root, (L, S)
 
 
 @pytest.mark.parametrize("name", _names(12_000_000))
