@@ -8,20 +8,21 @@ with the ASCII bases already resident in HBM (SURVEY §8(d) timing scope).
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config uniform_1g]
 
 N > 1 is launched by torch.distributed.run (one process per GPU).  Default
-(--mode weak): ONE genome of N x the configured size (uniform_1g: N Gbase) is
-partitioned over the ranks (gcz_dist_plan: contiguous strand ranges, rank order =
-position order), so every GPU holds and builds 1 Gbase of it; each rank generates
-only its own bases, and every hash-consed level reconciles keys through their
-owner rank with RCCL all-to-all over xGMI (gcz_group).  Per-GPU
-work is fixed: "scaling": "weak".  --mode strong partitions the configured
-genome itself (1 Gbase over N GPUs, total work fixed); --mode replicas runs N
-independent builds of N different genomes (no data-path collective).
---virtual R (one GPU) runs the distributed path with R virtual ranks on one
-device, to measure its overhead.
+(--mode strong, BASELINE's metric): the configured genome itself (uniform_1g:
+1 Gbase) is partitioned over the ranks (gcz_dist_plan: contiguous strand ranges,
+rank order = position order); each rank generates only its own bases, and every
+hash-consed level reconciles keys through their owner rank with RCCL over xGMI
+(gcz_group).  Total work is fixed: "scaling": "strong".  The same
+run times the weak-scaled case as an extra field (one genome of N x the config
+size, 1 config genome per GPU; --no-weak skips it).  --mode weak makes that the
+headline; --mode replicas runs N independent builds of N different genomes (no
+data-path collective).  --virtual R (one GPU) runs the distributed path with R
+virtual ranks on one device, to measure its per-rank cost.
 
 Printed (rank 0): ONE JSON line with value, roofline of the dominant kernel,
-the CPU baseline (compiled reference on this host, bounded sample) and the
-parity verdict against the reference goldens.
+the CPU baseline (compiled reference on this host, the same genome, run beside
+the GPU work) and the parity verdict against the reference goldens.  A parity
+mismatch exits with status 3 after the line.
 """
 import argparse
 import hashlib
@@ -146,31 +147,58 @@ def build_bytes(L, S, n_leaves, layer_sizes):
     return b_stream, b_table
 
 
-def cpu_baseline(sample_bases):
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+class CpuBaseline:
     """Compiled reference (oracle/_ref/ref_harness, built from /root/reference sources)
-    timed on this host: pack + shared_tree(std::vector<dna>&) build, 1 thread."""
-    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
-    if os.path.exists(harness):
-        try:
-            out = subprocess.run([harness, "time", "0", str(sample_bases), "12"], capture_output=True,
-                                 text=True, timeout=600, check=True).stdout
-            r = json.loads(out)
-            return {"value": r["bases_per_s"], "unit": "bases/s", "cores": 1, "kind": "reference",
-                    "sample": f"synthetic uniform ACGT, first {sample_bases} bases of the bench genome "
-                              f"(csrc/synth.h), pack+build, {os.cpu_count()} host CPUs visible, 1 used",
-                    "build_ms": r["build_ms"], "pack_ms": r["pack_ms"]}
-        except Exception as e:  # noqa: BLE001
-            return {"value": None, "unit": "bases/s", "cores": 1, "kind": "reference", "error": str(e)}
-    # port: the C restatement (test infrastructure) as the checker-side CPU timing
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle  # noqa: E402
-    gcz = sys.modules["gcz"]
-    data = gcz.synth(0, sample_bases).tobytes()
-    t0 = time.perf_counter()
-    oracle.build_leaves(oracle.pack(data, 12), 12)
-    dt = time.perf_counter() - t0
-    return {"value": (len(data) // 12 * 12) / dt, "unit": "bases/s", "cores": 1, "kind": "port",
-            "sample": f"synthetic uniform ACGT, {sample_bases} bases, oracle/gcz_oracle.c"}
+    timed on this host: pack + shared_tree(std::vector<dna>&) build of the same synthetic
+    genome, 1 thread (the reference builds single-threaded).  Started as a child process
+    before the GPU work and joined at the end, so the full config fits the bench's wall
+    time; it takes one host core of many."""
+
+    def __init__(self, kind, nbases):
+        self.kind, self.nbases, self.proc, self.t0 = kind, nbases, None, time.perf_counter()
+        harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+        if os.path.exists(harness):
+            self.proc = subprocess.Popen([harness, "time", str(kind), str(nbases), "12"], stdout=subprocess.PIPE,
+                                         stderr=subprocess.PIPE, text=True)
+
+    def result(self):
+        host = f"{cpu_model()}, {os.cpu_count()} host CPUs visible, 1 used"
+        sample = (f"synthetic {'uniform ACGT' if self.kind == 0 else 'tandem-repeat'} genome of the bench "
+                  f"config (csrc/synth.h), all {self.nbases} bases, pack + build")
+        if self.proc is not None:
+            try:
+                out, err = self.proc.communicate(timeout=900)
+                if self.proc.returncode != 0:
+                    raise RuntimeError(err.strip()[-300:])
+                r = json.loads(out)
+                return {"value": r["bases_per_s"], "unit": "bases/s", "cores": 1, "kind": "reference",
+                        "sample": sample, "host": host, "build_ms": r["build_ms"], "pack_ms": r["pack_ms"],
+                        "wall_s": round(time.perf_counter() - self.t0, 1)}
+            except Exception as e:  # noqa: BLE001
+                self.proc.kill()
+                return {"value": None, "unit": "bases/s", "cores": 1, "kind": "reference", "error": str(e)}
+        # port: the C restatement (test infrastructure) as the checker-side CPU timing, on a sample
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle  # noqa: E402
+        gcz = sys.modules["gcz"]
+        n = min(self.nbases, 120_000_000)
+        data = gcz.synth(self.kind, n).tobytes()
+        t0 = time.perf_counter()
+        oracle.build_leaves(oracle.pack(data, 12), 12)
+        dt = time.perf_counter() - t0
+        return {"value": (len(data) // 12 * 12) / dt, "unit": "bases/s", "cores": 1, "kind": "port",
+                "sample": f"first {n} bases of the bench genome, oracle/gcz_oracle.c", "host": host}
 
 
 def stream_digest(group, dist, rank, world, info):
@@ -222,12 +250,14 @@ def rank_summary(rank, build_ms, trace):
             "leaf_end_ms": round(leaf_end, 3) if leaf_end is not None else None, "exchanges": xch}
 
 
-def strong_run(gcz, ctx, group, dist, cfg, args, seed, L, world, rank, barrier):
-    """Weak-scaled runs also time the strong-scaled case: the configured genome itself
-    (1 Gbase) partitioned over the same ranks and group."""
+def weak_run(gcz, ctx, group, dist, cfg, args, seed, L, world, rank, barrier):
+    """Strong-scaled runs (the headline at N > 1) also time the weak-scaled case: one
+    genome of N x the configured size, 1 config genome per GPU, on the same group."""
     import torch
     try:
-        S1 = CONFIGS[args.config]["nbases"] // L
+        name = "uniform" if cfg["kind"] == 0 else "tandem"
+        S1 = CONFIGS[args.config]["nbases"] * world // L
+        golden = f"synth/{name}_{CONFIGS[args.config]['nbases'] * world}"
         a0, a1, _ = gcz.dist_plan(S1, world, rank)
         h1 = genome(gcz, cfg, seed, a0 * L, a1 * L)
         dev1 = ctx.upload(h1 if h1.size else np.zeros(1, np.uint8))
@@ -245,9 +275,9 @@ def strong_run(gcz, ctx, group, dist, cfg, args, seed, L, world, rank, barrier):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt1 = float(t.item())
         dev1.free()
-        out = {"nbases": S1 * L, "value": S1 * L * args.steps / dt1, "ms_per_step": dt1 / args.steps * 1e3,
-               "device_ms": i1["build_ms"], "n_leaves": i1["n_leaves"]}
-        golden = CONFIGS[args.config]["golden"]
+        out = {"nbases": S1 * L, "per_gpu_nbases": S1 * L // world, "value": S1 * L * args.steps / dt1,
+               "ms_per_step": dt1 / args.steps * 1e3, "device_ms": i1["build_ms"], "n_leaves": i1["n_leaves"],
+               "scaling": "weak", "golden": golden}
         with open(os.path.join(REPO, "tests", "golden", "manifest.json")) as f:
             exp = json.load(f).get(golden)
         if exp:
@@ -264,13 +294,12 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="uniform_1g", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-sample", type=int, default=120_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
-    ap.add_argument("--no-strong", action="store_true", help="weak runs: skip the strong-scaled 1-genome timing")
-    ap.add_argument("--mode", choices=["weak", "strong", "dist", "replicas"], default="weak",
-                    help="N > 1: one genome of N x the config size (weak), the config genome itself over N GPUs "
-                         "(strong; 'dist' is an alias), or N independent genomes (replicas)")
+    ap.add_argument("--no-weak", action="store_true", help="strong runs at N > 1: skip the weak-scaled timing")
+    ap.add_argument("--mode", choices=["weak", "strong", "dist", "replicas"], default="strong",
+                    help="N > 1: the config genome itself over N GPUs (strong, the default; 'dist' is an alias), "
+                         "one genome of N x the config size (weak), or N independent genomes (replicas)")
     ap.add_argument("--virtual", type=int, default=0, help="N = 1: distributed path with R virtual ranks")
     ap.add_argument("--rccl-world1", action="store_true", help="N = 1: the RCCL group path with one rank")
     ap.add_argument("--transport", choices=["rccl", "shm"], default="rccl",
@@ -294,6 +323,9 @@ def main():
     gcz = load_gcz()
     cfg = CONFIGS[args.config]
     L = 12
+    cpu_job = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and cfg["kind"] != "file" and not args.virtual:
+        cpu_job = CpuBaseline(cfg["kind"], cfg["nbases"])   # runs beside the GPU work
     if cfg["kind"] == "file":
         with open(os.path.join(REPO, cfg["path"]), "rb") as f:
             raw = f.read()
@@ -485,13 +517,11 @@ def main():
             ratio_path["roundtrip_match"] = bool(np.array_equal(got, np.where(ref >= 97, ref - 32, ref)))
         text.free()
 
-    strong = None
-    if weak and not args.no_strong:
-        strong = strong_run(gcz, ctx, group, dist, cfg, args, seed, L, world, rank, barrier)
+    weak_line = None
+    if mode == "dist" and args.mode == "strong" and not args.no_weak and cfg["kind"] != "file":
+        weak_line = weak_run(gcz, ctx, group, dist, cfg, args, seed, L, world, rank, barrier)
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_sample)
+    cpu = cpu_job.result() if cpu_job is not None else None
 
     if rank == 0:
         line = {
@@ -519,9 +549,16 @@ def main():
             "ratio_path": ratio_path,
             "cpu_baseline": cpu,
             "parity": parity,
-            "strong_scaling": strong,
+            "weak_scaling": weak_line,
         }
         print(json.dumps(line), flush=True)
+        bad = [k for src in (parity or {}, weak_line or {}) for k, v in src.items()
+               if k.endswith("_match") and v is False]
+        if ratio_path and ratio_path.get("roundtrip_match") is False:
+            bad.append("roundtrip_match")
+        if bad:
+            print(f"bench: parity mismatch against the reference goldens: {bad}", file=sys.stderr, flush=True)
+            exit_code[0] = 3
     dev.free()
     if group is not None:
         group.close()
@@ -530,9 +567,12 @@ def main():
         dist.destroy_process_group()
 
 
+exit_code = [0]
+
 if __name__ == "__main__":
     try:
         main()
+        sys.exit(exit_code[0])
     except Exception as e:  # noqa: BLE001 -- report a failed run as a result line, not silence
         if int(os.environ.get("RANK", "0")) == 0:
             print(json.dumps({"metric": METRIC, "value": None, "unit": "bases/s",

@@ -4,6 +4,6 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
 timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1 &&
-timeout -k 10 600 python bench.py --steps 3 --warmup 1 --cpu-sample 60000000 > gpurun_out/bench.log 2>&1 &&
+timeout -k 10 600 python bench.py --steps 3 --warmup 1 > gpurun_out/bench.log 2>&1 &&
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity > gpurun_out/prof.log 2>&1 &&
 timeout -k 10 300 python scripts/probe_torch_first.py > gpurun_out/probe_torch.log 2>&1

@@ -4,10 +4,11 @@
 driver runs on an 8-GPU node; here every rank shares GPU 0 and the exchanges go
 through the host-staged shared-memory transport (--transport shm; RCCL refuses two
 ranks on one device).  Everything else is the production multi-rank path: one
-process and context per rank, the weak-scaled genome (N x uniform_100m), the
-per-level owner exchange, the streamed rank-slice parity digest over gloo, and the
-strong-scaled timing of the configured genome on the same group.  Both must match
-the reference goldens (synth/uniform_{200000006,300000009} and uniform_100000003).
+process and context per rank, the strong-scaled headline (uniform_100m split over
+the ranks), the per-level owner exchange, the streamed rank-slice parity digest
+over gloo, and the weak-scaled timing (N x uniform_100m) on the same group.  Both
+must match the reference goldens (synth/uniform_100000003 and
+uniform_{200000006,300000009}).
 """
 import json
 import os
@@ -37,13 +38,14 @@ def test_bench_multiprocess_shm(world):
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert p.returncode == 0 and lines, p.stdout[-2000:] + p.stderr[-4000:]
     d = json.loads(lines[-1])
-    assert d["n_gpus"] == world and d["scaling"] == "weak" and d["value"] > 0
-    assert d["config"]["nbases"] == world * 100_000_003
+    assert d["n_gpus"] == world and d["scaling"] == "strong" and d["value"] > 0
+    assert d["config"]["nbases"] == 100_000_003
     par = d["parity"]
-    assert par["golden"] == f"synth/uniform_{world * 100_000_003}"
+    assert par["golden"] == "synth/uniform_100000003"
     for k in ("layers_sha256_match", "leaves_sha256_match", "root_match", "layer_sizes_match"):
         assert par[k] is True, (k, par)
-    st = d["strong_scaling"]
-    assert "error" not in st, st
-    assert st["nbases"] == 100_000_003 // 12 * 12
-    assert st["layer_sizes_match"] and st["root_match"], st
+    wk = d["weak_scaling"]
+    assert "error" not in wk, wk
+    assert wk["golden"] == f"synth/uniform_{world * 100_000_003}"
+    assert wk["nbases"] == world * 100_000_003 // 12 * 12
+    assert wk["layer_sizes_match"] and wk["root_match"], wk
