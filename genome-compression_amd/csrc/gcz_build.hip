@@ -169,12 +169,13 @@ hipError_t allow_lds(F f, int bytes) {   // dynamic LDS above the default 64 KB
 
 }  // namespace
 
-int gcz_ctx::leaf_level_dense(const LeafLevel& a, Header* d_hdr, u64* ucount, bool* used) {
+int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool check, bool list, bool* used) {
   *used = false;
   const u64 S = a.S;
   const u32 L = u32(a.L);
   if (L < 1 || L > 12 || S == 0) return GCZ_OK;
-  DensePlan P{};
+  DensePlan& P = dl_plan;
+  P = DensePlan{};
   P.S = S;
   P.L = L;
   P.nch = u32((S + kDC - 1) / kDC);
@@ -191,24 +192,23 @@ int gcz_ctx::leaf_level_dense(const LeafLevel& a, Header* d_hdr, u64* ucount, bo
   const u64 ncnt = u64(P.NB) * P.nch;
   const u64 nfb = (S + 63) / 64;
   const u64 t_cnt = scan_tiles(ncnt + 1), t_fb = scan_tiles(nfb + 1);
+  const u64 ncodes = u64(1) << cbits;
   int rc;
   if ((rc = ensure(dl_pw, S * 4 + 16)) || (rc = ensure(dl_rec, S * 4 + 16)) || (rc = ensure(dl_idrec, S * 4 + 16)) ||
       (rc = ensure(dl_cnt, ncnt * 4 + 16)) || (rc = ensure(dl_off, (ncnt + 1) * 4 + 16)) ||
-      (rc = ensure(dl_fpg, (u64(1) << cbits) * 4 + 16)) || (rc = ensure(dl_fb, nfb * 8 + 16)) ||
+      (rc = ensure(dl_fpg, ncodes * 4 + 16)) || (rc = ensure(dl_fb, nfb * 8 + 16)) ||
       (rc = ensure(dl_wpre, (nfb + 1) * 4 + 16)) || (rc = ensure(dl_desc, (t_cnt + t_fb) * 8 + 16)) ||
-      (rc = ensure(dl_fl, (u64(1) << cbits) * 4 + 16)) || (rc = ensure(dl_fo, u64(P.NB) * (P.nch + 1) * 4 + 16)))
+      (rc = ensure(dl_fl, ncodes * 4 + 16)) || (rc = ensure(dl_fo, u64(P.NB) * (P.nch + 1) * 4 + 16)))
+    return rc;
+  if (list && ((rc = ensure(dl_lh, std::min(S, ncodes) * 4 + 16)) || (rc = ensure(dl_pb, (ncodes / 64 + 1) * 8))))
     return rc;
   u64* sdesc = dl_desc.as<u64>();
   u32* tickets = reinterpret_cast<u32*>(sdesc + t_cnt + t_fb);
-  const int RBbytes = int((1u << P.IB) * 4);
   const int first_bytes = int(((1u << P.IB) + P.nch + 1) * 4);
   if (first_bytes > 160 * 1024) return GCZ_OK;   // (never at L <= 12, S < 2^29)
   const int scat_bytes = int((kDC + 3 * kDNBMax + 1 + 16) * 4);
-  const int words_bytes = int((kDC + 2 * kDNBMax + 1 + 16) * 4);
   HIP_TRY(allow_lds(k_dl_scatter, scat_bytes));
   HIP_TRY(allow_lds(k_dl_first, first_bytes));
-  HIP_TRY(allow_lds(k_dl_ids, RBbytes));
-  HIP_TRY(allow_lds(k_dl_words, words_bytes));
   hipEvent_t e0{};
   prof_begin(KID_DL_PACK, e0);
   HIP_TRY(hipMemsetAsync(dl_desc.ptr, 0, (t_cnt + t_fb) * 8 + 16, stream));
@@ -219,11 +219,23 @@ int gcz_ctx::leaf_level_dense(const LeafLevel& a, Header* d_hdr, u64* ucount, bo
     launch_dl_pack<false>(int(L), dim3(P.nch), stream, nullptr, a.leaves, P, dl_pw.as<u32>(), dl_cnt.as<u32>(),
                           d_hdr);
   HIP_TRY(hipGetLastError());
-  u32 dfail = 0;
-  HIP_TRY(hipMemcpyAsync(&dfail, &d_hdr->dense_fail, 4, hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipStreamSynchronize(stream));
+  if (check) {   // single device: fall back at once (the multi-rank caller checks every rank's flag)
+    u32 dfail = 0;
+    HIP_TRY(hipMemcpyAsync(&dfail, &d_hdr->dense_fail, 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    if (dfail) {
+      prof_end(KID_DL_PACK, e0);
+      return GCZ_OK;
+    }
+  }
+  // repetitive data? (the node inserts' LDS pre-dedupe): in-block repeats of a sample's
+  // hashed codes (equal codes <=> equal keys)
+  const u64 ip = std::min<u64>(S, u64(1) << 21);
+  hipLaunchKernelGGL(k_dup_probe, dim3(unsigned((ip + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                     dl_pw.as<u32>(), u64(0), ip, d_hdr);
+  hipLaunchKernelGGL(k_dup_decide, dim3(1), dim3(1), 0, stream, d_hdr, ip, u32(predup_mode));
+  HIP_TRY(hipGetLastError());
   prof_end(KID_DL_PACK, e0);
-  if (dfail) return GCZ_OK;
   *used = true;
   prof_begin(KID_DL_SCAN, e0);
   hipLaunchKernelGGL(k_scan_excl<ScanU32>, dim3(unsigned(t_cnt)), dim3(kScanThreads), 0, stream,
@@ -237,8 +249,10 @@ int gcz_ctx::leaf_level_dense(const LeafLevel& a, Header* d_hdr, u64* ucount, bo
   HIP_TRY(hipGetLastError());
   prof_end(KID_DL_SCATTER, e0);
   prof_begin(KID_DL_FIRST, e0);
+  if (list && (1u << P.IB) < 64) HIP_TRY(hipMemsetAsync(dl_pb.ptr, 0, (ncodes / 64 + 1) * 8, stream));
   hipLaunchKernelGGL(k_dl_first, dim3(P.NB), dim3(kDThreads), first_bytes, stream, dl_rec.as<u32>(), dl_off.as<u32>(),
-                     P, dl_fpg.as<u32>(), dl_fl.as<u32>(), dl_fo.as<u32>());
+                     P, dl_fpg.as<u32>(), dl_fl.as<u32>(), dl_fo.as<u32>(),
+                     list ? dl_pb.as<unsigned long long>() : nullptr);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_dl_fb, dim3(P.nch), dim3(kDThreads), 0, stream, dl_fl.as<u32>(), dl_fo.as<u32>(), P,
                      dl_fb.as<unsigned long long>());
@@ -249,25 +263,41 @@ int gcz_ctx::leaf_level_dense(const LeafLevel& a, Header* d_hdr, u64* ucount, bo
                      ScanPopc{dl_fb.as<unsigned long long>()}, nfb, dl_wpre.as<u32>(), sdesc + t_cnt, &tickets[1],
                      ucount);
   HIP_TRY(hipGetLastError());
+  if (list) {
+    hipLaunchKernelGGL(k_dl_lh, dim3(unsigned((nfb + 255) / 256)), dim3(256), 0, stream, dl_pw.as<u32>(),
+                       dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), nfb, dl_lh.as<u32>());
+    HIP_TRY(hipGetLastError());
+  }
   prof_end(KID_DL_FBSCAN, e0);
+  return GCZ_OK;
+}
+
+int gcz_ctx::dense_phase_b(const LeafLevel& a, Header* d_hdr, const u32* gid, u64* leaves) {
+  (void)d_hdr;
+  const DensePlan& P = dl_plan;
+  const int RBbytes = int((1u << P.IB) * 4);
+  const int words_bytes = int((kDC + 2 * kDNBMax + 1 + 16) * 4);
+  HIP_TRY(allow_lds(k_dl_ids, RBbytes));
+  HIP_TRY(allow_lds(k_dl_words, words_bytes));
+  hipEvent_t e0{};
   prof_begin(KID_DL_IDS, e0);
   hipLaunchKernelGGL(k_dl_ids, dim3(P.NB), dim3(kDThreads), RBbytes, stream, dl_rec.as<u32>(), dl_off.as<u32>(), P,
-                     dl_fpg.as<u32>(), dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), dl_idrec.as<u32>());
+                     dl_fpg.as<u32>(), dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), gid, dl_idrec.as<u32>());
   HIP_TRY(hipGetLastError());
   prof_end(KID_DL_IDS, e0);
   prof_begin(KID_DL_WORDS, e0);
   hipLaunchKernelGGL(k_dl_words, dim3(P.nch), dim3(kDThreads), words_bytes, stream, dl_pw.as<u32>(),
                      dl_rec.as<u32>(), dl_idrec.as<u32>(), dl_off.as<u32>(), P, dl_fb.as<unsigned long long>(),
-                     a.words, a.out);
-  HIP_TRY(hipGetLastError());
-  // repetitive data? (the node inserts' LDS pre-dedupe), on the final words of a sample
-  const u64 ip = std::min<u64>(S, u64(1) << 21);
-  hipLaunchKernelGGL(k_dup_probe, dim3(unsigned((ip + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, a.words,
-                     u64(0), ip, d_hdr);
-  hipLaunchKernelGGL(k_dup_decide, dim3(1), dim3(1), 0, stream, d_hdr, ip, u32(predup_mode));
+                     a.words, leaves);
   HIP_TRY(hipGetLastError());
   prof_end(KID_DL_WORDS, e0);
   return GCZ_OK;
+}
+
+int gcz_ctx::leaf_level_dense(const LeafLevel& a, Header* d_hdr, u64* ucount, bool* used) {
+  if (int rc = dense_phase_a(a, d_hdr, ucount, true, false, used)) return rc;
+  if (!*used) return GCZ_OK;
+  return dense_phase_b(a, d_hdr, nullptr, a.out);
 }
 
 int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
@@ -656,7 +686,8 @@ void gcz_ctx_destroy(gcz_ctx* c) {
   for (DevBuf* b : {&c->wa, &c->wb, &c->grp, &c->desc, &c->tab, &c->leaves_out, &c->nodes_out, &c->hdr, &c->input,
                     &c->nf, &c->multi, &c->stats, &c->bkt_key, &c->bkt_cnt, &c->bkt_off, &c->bkt_tmp, &c->dl_pw,
                     &c->dl_rec, &c->dl_idrec, &c->dl_cnt, &c->dl_off, &c->dl_fpg, &c->dl_fb, &c->dl_wpre,
-                    &c->dl_desc, &c->dl_fl, &c->dl_fo})
+                    &c->dl_desc, &c->dl_fl, &c->dl_fo, &c->dl_lh, &c->dl_pb, &c->dl_pbs, &c->dl_lower,
+                    &c->dl_pos, &c->dl_list, &c->dl_gid, &c->dl_recv, &c->dl_stage, &c->dl_seg})
     if (b->ptr) (void)hipFree(b->ptr);
   if (c->h_hdr) (void)hipHostFree(c->h_hdr);
   for (auto e : c->event_pool) (void)hipEventDestroy(e);

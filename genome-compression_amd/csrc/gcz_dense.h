@@ -51,7 +51,7 @@ struct DensePlan {
 };
 
 // ACGT (any case) -> 0..3; other valid IUPAC symbols -> 4; unknown -> 5
-__device__ __forceinline__ int acgt_code(int c) {
+static __device__ __forceinline__ int acgt_code(int c) {
   const int u = (c >= 'a' && c <= 'z') ? c - 32 : c;
   switch (u) {
     case 'A': return 0; case 'C': return 1; case 'G': return 2; case 'T': return 3;
@@ -60,14 +60,14 @@ __device__ __forceinline__ int acgt_code(int c) {
 }
 
 // reverse the L 2-bit groups of x (dna::mirrored on the 2-bit code, dna.cpp:116-121)
-__device__ __forceinline__ u32 rev2(u32 x, u32 L) {
+static __device__ __forceinline__ u32 rev2(u32 x, u32 L) {
   u32 r = __brev(x);
   r = ((r >> 1) & 0x55555555u) | ((r & 0x55555555u) << 1);
   return r >> (32 - 2 * L);
 }
 
 // dna::canonical on a 2-bit code: min over (x,F,F) (T,F,T) (M,T,F) (I,T,T) (dna.cpp:135-143)
-__device__ __forceinline__ u32 canon2(u32 x, u32 L, u32 cmask, u32& m, u32& t, u32& v) {
+static __device__ __forceinline__ u32 canon2(u32 x, u32 L, u32 cmask, u32& m, u32& t, u32& v) {
   const u32 tx = x ^ cmask, mx = rev2(x, L), ix = mx ^ cmask;
   v = x == mx;
   u32 best = x;
@@ -79,7 +79,7 @@ __device__ __forceinline__ u32 canon2(u32 x, u32 L, u32 cmask, u32& m, u32& t, u
 }
 
 // 2-bit code -> nibble-packed dna value (A,C,G,T = 1,2,4,8 at bits 4i, include/dna.h:20-32)
-__device__ __forceinline__ u64 code2_leaf(u32 c, u32 L) {
+static __device__ __forceinline__ u64 code2_leaf(u32 c, u32 L) {
   u64 v = 0;
   for (u32 i = 0; i < L; ++i) v |= u64(1u << ((c >> (2 * i)) & 3u)) << (4 * i);
   return v;
@@ -87,7 +87,7 @@ __device__ __forceinline__ u64 code2_leaf(u32 c, u32 L) {
 
 // Block-wide exclusive scan of one u32 per thread (kDThreads threads); returns
 // the thread's exclusive prefix, *total = the block sum.  s_tmp: 16 u32.
-__device__ __forceinline__ u32 block_excl(u32 x, u32* s_tmp, u32* total) {
+static __device__ __forceinline__ u32 block_excl(u32 x, u32* s_tmp, u32* total) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   u32 incl = x;
 #pragma unroll
@@ -111,7 +111,7 @@ __device__ __forceinline__ u32 block_excl(u32 x, u32* s_tmp, u32* total) {
 
 // The runs (b, ch) of one chunk: s_base[b] = local exclusive offset (s_base[NB] = the
 // chunk's strands), s_dst[b] = the run's start in the record array.
-__device__ __forceinline__ void chunk_runs(const u32* __restrict__ off, const DensePlan& P, u32 ch, u32* s_base,
+static __device__ __forceinline__ void chunk_runs(const u32* __restrict__ off, const DensePlan& P, u32 ch, u32* s_base,
                                            u32* s_dst, u32* s_tmp) {
   const u32 b = threadIdx.x;   // NB <= kDThreads
   u32 c = 0, d = 0;
@@ -131,7 +131,7 @@ __device__ __forceinline__ void chunk_runs(const u32* __restrict__ off, const De
 }
 
 // last bucket b with s_base[b] <= q (runs of zero length are skipped)
-__device__ __forceinline__ u32 run_of(const u32* s_base, u32 NB, u32 q) {
+static __device__ __forceinline__ u32 run_of(const u32* s_base, u32 NB, u32 q) {
   u32 lo = 0, hi = NB - 1;
   while (lo < hi) {
     const u32 mid = (lo + hi + 1) >> 1;
@@ -145,7 +145,7 @@ constexpr int kDBatch = 8;   // strands / records in flight per thread
 
 // L bytes of strand s from 4-B aligned loads (no LDS staging)
 template <int L>
-__device__ __forceinline__ void load_strand(const unsigned char* __restrict__ bases, u64 s, u32 (&w)[4]) {
+static __device__ __forceinline__ void load_strand(const unsigned char* __restrict__ bases, u64 s, u32 (&w)[4]) {
   const u64 a = s * L;
   const u32* p = reinterpret_cast<const u32*>(bases + (a & ~3ull));
   constexpr int NW = (L + 3 + 3) / 4;
@@ -156,7 +156,7 @@ __device__ __forceinline__ void load_strand(const unsigned char* __restrict__ ba
 // Pack: the strand's pre-word make_word(h, m, t, v) and the chunk's bucket histogram.
 // Bases: L bytes per strand (dna::dna(string_view), src/dna.cpp:79-84); leaves: u64.
 template <int L, bool kBases>
-__global__ __launch_bounds__(kDThreads) void k_dl_pack(const unsigned char* __restrict__ bases,
+[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_pack(const unsigned char* __restrict__ bases,
                                                        const u64* __restrict__ leaves, DensePlan P,
                                                        u32* __restrict__ pw, u32* __restrict__ cnt,
                                                        Header* __restrict__ hdr) {
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(kDThreads) void k_dl_pack(const unsigned char* __re
 // Scatter: records (h's low IB bits << kDLog | position in chunk) in runs
 // (chunk, bucket) at off[b * nch + chunk] of the bucket-ordered record array,
 // staged in LDS so every run is written contiguously.
-__global__ __launch_bounds__(kDThreads) void k_dl_scatter(const u32* __restrict__ pw, DensePlan P,
+[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_scatter(const u32* __restrict__ pw, DensePlan P,
                                                           const u32* __restrict__ off, u32* __restrict__ rec) {
   extern __shared__ u32 s_dyn[];
   u32* s_stage = s_dyn;                 // kDC records
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(kDThreads) void k_dl_scatter(const u32* __restrict_
 // runs is contiguous, so the chunk of a record is found among the group's run
 // starts held in registers (broadcast by shuffles).
 template <class F>
-__device__ __forceinline__ void bucket_records(const u32* __restrict__ rec, const u32* __restrict__ off,
+static __device__ __forceinline__ void bucket_records(const u32* __restrict__ rec, const u32* __restrict__ off,
                                                const DensePlan& P, u32 b, F f) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int G = 16;   // chunks per wave step
@@ -305,11 +305,12 @@ __device__ __forceinline__ void bucket_records(const u32* __restrict__ rec, cons
 
 // First occurrences: one workgroup per bucket; LDS table of its 2^IB codes.
 // Writes each code's first position to fpg (~0 if absent), and the bucket's
-// first positions sorted by chunk: fl[b * RB + ...], with fo[b * (nch + 1) + ch]
-// the start of chunk ch's (a counting sort in LDS; k_dl_fb gathers them per chunk).
-__global__ __launch_bounds__(kDThreads) void k_dl_first(const u32* __restrict__ rec, const u32* __restrict__ off,
+// first positions sorted by chunk: fl[b * RB + ...], with fo[ch * NB + b] the start
+// of chunk ch's (a counting sort in LDS; k_dl_fb gathers them per chunk).  pb
+// (multi-rank build, else null): the presence bitmap, bit h set iff hashed code h occurs.
+[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_first(const u32* __restrict__ rec, const u32* __restrict__ off,
                                                         DensePlan P, u32* __restrict__ fpg, u32* __restrict__ fl,
-                                                        u32* __restrict__ fo) {
+                                                        u32* __restrict__ fo, unsigned long long* __restrict__ pb) {
   extern __shared__ u32 s_dyn[];
   u32* s_fp = s_dyn;                    // RB codes
   u32* s_cnt = s_dyn + (1u << P.IB);    // nch + 1 chunk counters
@@ -332,6 +333,15 @@ __global__ __launch_bounds__(kDThreads) void k_dl_first(const u32* __restrict__ 
     fp[k] = i < RB ? s_fp[i] : ~0u;
     if (i < RB) fpg[u64(b) * RB + i] = fp[k];
     rk[k] = fp[k] != ~0u ? atomicAdd(&s_cnt[fp[k] >> kDLog], 1u) : 0u;
+    if (pb) {
+      const u32 h = (b << P.IB) | i;
+      if (RB >= 64) {
+        const u64 m = __ballot(fp[k] != ~0u);
+        if ((tid & 63) == 0 && i < RB) pb[h >> 6] = m;
+      } else if (fp[k] != ~0u) {
+        atomicOr(&pb[h >> 6], 1ull << (h & 63));
+      }
+    }
   }
   __syncthreads();
   // exclusive scan of the nch + 1 counters (a few per thread, in order)
@@ -343,7 +353,7 @@ __global__ __launch_bounds__(kDThreads) void k_dl_first(const u32* __restrict__ 
   for (u32 c = c0; c < c0 + per && c < n1; ++c) {
     const u32 v = s_cnt[c];
     s_cnt[c] = run;
-    fo[u64(b) * n1 + c] = run;
+    fo[u64(c) * P.NB + b] = run;
     run += v;
   }
   __syncthreads();
@@ -354,15 +364,15 @@ __global__ __launch_bounds__(kDThreads) void k_dl_first(const u32* __restrict__ 
 
 // First-occurrence bitmap of one chunk: its first positions from every bucket's
 // sorted list (k_dl_first), set in LDS, written as the chunk's 512 bitmap words.
-__global__ __launch_bounds__(kDThreads) void k_dl_fb(const u32* __restrict__ fl, const u32* __restrict__ fo,
+[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_fb(const u32* __restrict__ fl, const u32* __restrict__ fo,
                                                      DensePlan P, unsigned long long* __restrict__ fb) {
   __shared__ u32 s_bits[kDC / 32];
   const int tid = threadIdx.x;
-  const u32 ch = blockIdx.x, RB = 1u << P.IB, n1 = P.nch + 1;
+  const u32 ch = blockIdx.x, RB = 1u << P.IB;
   for (u32 w = tid; w < kDC / 32; w += kDThreads) s_bits[w] = 0;
   __syncthreads();
   for (u32 b = tid; b < P.NB; b += kDThreads) {
-    const u32 o0 = fo[u64(b) * n1 + ch], o1 = fo[u64(b) * n1 + ch + 1];
+    const u32 o0 = fo[u64(ch) * P.NB + b], o1 = fo[u64(ch + 1) * P.NB + b];
     for (u32 k = o0; k < o1; ++k) {
       const u32 q = fl[u64(b) * RB + k] & (kDC - 1);
       atomicOr(&s_bits[q >> 5], 1u << (q & 31));
@@ -378,17 +388,20 @@ struct ScanPopc {   // popcount of each first-occurrence bitmap word
   __device__ __forceinline__ u32 operator()(u64 i) const { return u32(__popcll(fb[i])); }
 };
 
-__device__ __forceinline__ u32 fb_rank(const unsigned long long* __restrict__ fb, const u32* __restrict__ wpre, u32 p) {
+static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restrict__ fb, const u32* __restrict__ wpre, u32 p) {
   const unsigned long long w = fb[p >> 6];
   return wpre[p >> 6] + u32(__popcll(w & ((1ull << (p & 63)) - 1ull)));
 }
 
 // Ids: per bucket, the id of each present code (rank of its first position)
 // in LDS, then one id per record in bucket order.
-__global__ __launch_bounds__(kDThreads) void k_dl_ids(const u32* __restrict__ rec, const u32* __restrict__ off,
+// gid (multi-rank build): the GLOBAL id of every code present on this rank,
+// indexed by hashed code; null: ids are this build's first-occurrence ranks.
+[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_ids(const u32* __restrict__ rec, const u32* __restrict__ off,
                                                       DensePlan P, const u32* __restrict__ fpg,
                                                       const unsigned long long* __restrict__ fb,
-                                                      const u32* __restrict__ wpre, u32* __restrict__ idrec) {
+                                                      const u32* __restrict__ wpre, const u32* __restrict__ gid,
+                                                      u32* __restrict__ idrec) {
   extern __shared__ u32 s_id[];
   const int tid = threadIdx.x;
   const u32 b = blockIdx.x, RB = 1u << P.IB;
@@ -397,12 +410,12 @@ __global__ __launch_bounds__(kDThreads) void k_dl_ids(const u32* __restrict__ re
 #pragma unroll
     for (int j = 0; j < kDBatch; ++j) {
       const u32 i = i0 + u32(j) * kDThreads + tid;
-      fp[j] = i < RB ? fpg[u64(b) * RB + i] : ~0u;
+      fp[j] = i < RB ? (gid ? gid : fpg)[u64(b) * RB + i] : ~0u;
     }
 #pragma unroll
     for (int j = 0; j < kDBatch; ++j) {
       const u32 i = i0 + u32(j) * kDThreads + tid;
-      if (i < RB) s_id[i] = fp[j] != ~0u ? fb_rank(fb, wpre, fp[j]) : 0u;
+      if (i < RB) s_id[i] = gid ? fp[j] : fp[j] != ~0u ? fb_rank(fb, wpre, fp[j]) : 0u;
     }
   }
   __syncthreads();
@@ -425,7 +438,7 @@ __global__ __launch_bounds__(kDThreads) void k_dl_ids(const u32* __restrict__ re
 
 // Words: per chunk, the ids of its records back into position order (LDS), the
 // pre-word's m/t/v bits -> final words; first occurrences emit their leaf.
-__global__ __launch_bounds__(kDThreads) void k_dl_words(const u32* __restrict__ pw, const u32* __restrict__ rec,
+[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_words(const u32* __restrict__ pw, const u32* __restrict__ rec,
                                                         const u32* __restrict__ idrec, const u32* __restrict__ off,
                                                         DensePlan P, const unsigned long long* __restrict__ fb,
                                                         u32* __restrict__ words, u64* __restrict__ leaves_out) {
@@ -477,12 +490,106 @@ __global__ __launch_bounds__(kDThreads) void k_dl_words(const u32* __restrict__ 
       const u64 s = c0 + q;
       const u32 id = s_w[q];
       words[s] = id | (p[j] & kBits);
-      if ((fb[s >> 6] >> (s & 63)) & 1ull) {
+      if (leaves_out && ((fb[s >> 6] >> (s & 63)) & 1ull)) {
         const u32 h = p[j] & kIdx;
         leaves_out[id] = code2_leaf((h * P.Kinv) & P.cmask, P.L);
       }
     }
   }
+}
+
+// ---- multi-rank build (gcz_dist.hip): the leaf level of one rank ----------------
+//
+// Rank r's local dense level gives its keys' local first-occurrence order.  A key's
+// global first occurrence is on the lowest rank that holds it (rank order = position
+// order), so with every rank's presence bitmap (allgather) rank r knows its "r-first"
+// keys (held by no lower rank); their global ids are off_r + their order among
+// rank r's r-first keys, off_r = the r-first counts of lower ranks.  The r-first
+// lists (hashed codes in id order) are exchanged so that every rank can look up the
+// global id of each key it holds; rank r's list is also its slice of the leaves.
+
+// Local key list: the hashed code of each first occurrence, in local-id order (the
+// ids of first occurrences increase with position, so the writes are contiguous).
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_lh(const u32* __restrict__ pw,
+                                                     const unsigned long long* __restrict__ fb,
+                                                     const u32* __restrict__ wpre, u64 nfb, u32* __restrict__ lh) {
+  const u64 w = u64(blockIdx.x) * 256 + threadIdx.x;
+  if (w >= nfb) return;
+  unsigned long long m = fb[w];
+  u32 id = wpre[w];
+  while (m) {
+    const int bit = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    lh[id++] = pw[w * 64 + bit] & kIdx;
+  }
+}
+
+// (pure-ACGT failure flag, local uniques, repetitive-data flag) for the first exchange
+[[maybe_unused]] static __global__ void k_dl_vec(const Header* __restrict__ hdr, u64* __restrict__ vec) {
+  vec[0] = hdr->dense_fail;
+  vec[1] = hdr->count[0];
+  vec[2] = hdr->predup;
+}
+
+// lower = OR of the presence bitmaps of ranks 0 .. r-1 (pbs: R bitmaps of nw words)
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_lower(const unsigned long long* __restrict__ pbs, u64 nw, int r,
+                                                  unsigned long long* __restrict__ lower) {
+  const u64 w = u64(blockIdx.x) * 256 + threadIdx.x;
+  if (w >= nw) return;
+  unsigned long long x = 0;
+  for (int q = 0; q < r; ++q) x |= pbs[u64(q) * nw + w];
+  lower[w] = x;
+}
+
+struct ScanRFirst {   // local key j is r-first: no lower rank holds it
+  const u32* lh;
+  const unsigned long long* lower;
+  u64 n;
+  __device__ __forceinline__ u32 operator()(u64 j) const {
+    if (j >= n) return 0u;
+    const u32 h = lh[j];
+    return ((lower[h >> 6] >> (h & 63)) & 1ull) ? 0u : 1u;
+  }
+};
+
+// the r-first keys in local-id order (= global-id order)
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_compact(const u32* __restrict__ lh, const unsigned long long* __restrict__ lower,
+                                                    const u32* __restrict__ pos, u64 n, u32* __restrict__ list) {
+  const u64 j = u64(blockIdx.x) * 256 + threadIdx.x;
+  if (j >= n) return;
+  const u32 h = lh[j];
+  if (!((lower[h >> 6] >> (h & 63)) & 1ull)) list[pos[j]] = h;
+}
+
+// Global ids from the gathered lists: recv holds segments (start, len, global id of
+// the first element) in any order; gid[h] = that id + index.
+struct DlSeg {
+  u64 start, len, gbase;
+};
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_gid(const u32* __restrict__ recv, const DlSeg* __restrict__ seg, int nseg,
+                                                u64 n, u32* __restrict__ gid) {
+  __shared__ u64 s_start[1024], s_base[1024];   // segments sorted by start, nonempty
+  for (int q = threadIdx.x; q < nseg; q += 256) {
+    s_start[q] = seg[q].start;
+    s_base[q] = seg[q].gbase;
+  }
+  __syncthreads();
+  const u64 e = u64(blockIdx.x) * 256 + threadIdx.x;
+  if (e >= n) return;
+  int lo = 0, hi = nseg - 1;   // last segment starting at or before e
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (s_start[mid] <= e) lo = mid;
+    else hi = mid - 1;
+  }
+  gid[recv[e]] = u32(s_base[lo] + (e - s_start[lo]));
+}
+
+// This rank's slice of the unique leaves: its r-first list as dna values
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_leaves(const u32* __restrict__ list, u64 n, DensePlan P,
+                                                   u64* __restrict__ out) {
+  const u64 k = u64(blockIdx.x) * 256 + threadIdx.x;
+  if (k < n) out[k] = code2_leaf((list[k] * P.Kinv) & P.cmask, P.L);
 }
 
 }  // namespace gcz_dev

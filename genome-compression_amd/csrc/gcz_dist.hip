@@ -22,6 +22,7 @@
 
 #include "gcz_ctx.h"
 #include "gcz_dist_device.h"
+#include "gcz_scan.h"
 
 using namespace gcz_dev;
 using namespace gcz_host;
@@ -511,6 +512,11 @@ struct gcz_group {
   }
   int build(const void* const* d_bases, const u64* const* d_leaves, u64 S, int L);
   int alloc(int i, u64 leaf_cap);
+  // The dense leaf level of every rank + the presence / r-first-list exchange
+  // (gcz_dense.h); *used = false when some strand is not pure ACGT.
+  int dense_leaves(const std::vector<const unsigned char*>& bases, const u64* const* d_leaves, int L,
+                   std::vector<u64>& c, std::vector<u64>& off, u64& total, bool* used);
+  int dense_mode = std::getenv("GCZ_DENSE") ? std::atoi(std::getenv("GCZ_DENSE")) : 1;   // 0: hash-table leaves
   int exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, u32 key_bits, u32 child_bits,
                std::vector<u64>& c, std::vector<u64>& off, u64& total, u64* err_global, int* err_sym,
                int* ovf_bits, bool nolocal = false, bool lookahead = false, u64* next_hashed_out = nullptr);
@@ -594,6 +600,182 @@ int gcz_group::alloc(int i, u64 leaf_cap) {
   return GCZ_OK;
 }
 
+
+int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, const u64* const* d_leaves, int L,
+                            std::vector<u64>& c, std::vector<u64>& off, u64& total, bool* used) {
+  *used = false;
+  const int R = world, NL = int(ctx.size());
+  const DistPlan& P = plan;
+  const u64 ncodes = u64(1) << (2 * L);
+  const u64 nw = (ncodes + 63) / 64;   // presence bitmap words
+  std::vector<LeafLevel> las(NL);
+  // A. every rank's local first occurrences, key list and presence bitmap
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    LeafLevel& la = las[i];
+    la.bases = bases[i];
+    la.leaves = d_leaves ? d_leaves[i] : nullptr;
+    la.S = P.count(rank[i], 0);
+    la.L = L;
+    la.words = cx->wa.as<u32>();
+    bool u = false;
+    Header* h = cx->hdr.as<Header>();
+    if (int rc = cx->dense_phase_a(la, h, &h->count[0], false, true, &u)) return rc == GCZ_ERR_DEVICE ? dev_fail("dense leaves") : rc;
+    if (!u) return GCZ_OK;   // L or sizes outside the dense level (the same on every rank)
+    if (cx->ensure(cx->dl_seg, size_t(64 + 3 * R) * 8 + size_t(R) * R * sizeof(DlSeg) + 64) ||
+        cx->ensure(cx->dl_pbs, size_t(R) * nw * 8 + 16) || cx->ensure(cx->dl_lower, nw * 8 + 16))
+      return dev_fail("dense leaf buffers");
+    u64* vec = cx->dl_seg.as<u64>();
+    hipLaunchKernelGGL(k_dl_vec, dim3(1), dim3(1), 0, cx->stream, h, vec);
+    G_HIP(hipGetLastError());
+  }
+  // exchange 1: (pure ACGT?, local uniques, repetitive?) and the presence bitmaps
+  {
+    std::vector<const void*> s, s2;
+    std::vector<void*> rv, rv2;
+    for (gcz_ctx* cx : ctx) {
+      s.push_back(cx->dl_seg.as<u64>());
+      rv.push_back(cx->dl_seg.as<u64>() + 8);
+      s2.push_back(cx->dl_pb.ptr);
+      rv2.push_back(cx->dl_pbs.ptr);
+    }
+    hipEvent_t e0{};
+    ctx[0]->prof_begin(KID_EXCHANGE, e0);
+    G_RC(tr->allgather(24, s, rv));
+    G_RC(tr->allgather(nw * 8, s2, rv2));
+    ctx[0]->prof_end(KID_EXCHANGE, e0);
+  }
+  std::vector<u64> hv(size_t(3) * R + 8);
+  G_HIP(hipMemcpyAsync(hv.data(), ctx[0]->dl_seg.as<u64>() + 8, size_t(3) * R * 8, hipMemcpyDeviceToHost,
+                       ctx[0]->stream));
+  for (gcz_ctx* cx : ctx) G_HIP(hipStreamSynchronize(cx->stream));
+  std::vector<u64> U(R);
+  bool pred = false;
+  for (int r = 0; r < R; ++r) {
+    if (hv[3 * r]) return GCZ_OK;   // some rank holds a non-ACGT strand: the hash-table leaf level
+    U[r] = hv[3 * r + 1];
+    pred = pred || hv[3 * r + 2] != 0;
+  }
+  any_predup = pred;
+  // r-first keys (held by no lower rank) in local-id order = global-id order
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    const int r = rank[i];
+    const u64 ur = U[r], t = scan_tiles(ur + 1);
+    ProfScope ps_(cx, KID_IDS);
+    if (cx->ensure(cx->dl_pos, (ur + 1) * 4 + t * 8 + 64) || cx->ensure(cx->dl_list, ur * 4 + 16))
+      return dev_fail("dense leaf lists");
+    u32* pos = cx->dl_pos.as<u32>();
+    u64* desc = reinterpret_cast<u64*>(pos + ((ur + 1 + 1) & ~u64(1)));
+    u32* ticket = reinterpret_cast<u32*>(desc + t);
+    G_HIP(hipMemsetAsync(desc, 0, t * 8 + 8, cx->stream));
+    hipLaunchKernelGGL(k_dl_lower, dim3(unsigned((nw + 255) / 256)), dim3(256), 0, cx->stream,
+                       cx->dl_pbs.as<unsigned long long>(), nw, r, cx->dl_lower.as<unsigned long long>());
+    hipLaunchKernelGGL(k_scan_excl<ScanRFirst>, dim3(unsigned(t)), dim3(kScanThreads), 0, cx->stream,
+                       ScanRFirst{cx->dl_lh.as<u32>(), cx->dl_lower.as<unsigned long long>(), ur}, ur + 1, pos, desc,
+                       ticket, cx->dl_seg.as<u64>() + 4);
+    if (ur)
+      hipLaunchKernelGGL(k_dl_compact, dim3(unsigned((ur + 255) / 256)), dim3(256), 0, cx->stream, cx->dl_lh.as<u32>(),
+                         cx->dl_lower.as<unsigned long long>(), pos, ur, cx->dl_list.as<u32>());
+    G_HIP(hipGetLastError());
+  }
+  // exchange 2: r-first counts -> id offsets
+  {
+    std::vector<const void*> s;
+    std::vector<void*> rv;
+    for (gcz_ctx* cx : ctx) {
+      s.push_back(cx->dl_seg.as<u64>() + 4);
+      rv.push_back(cx->dl_seg.as<u64>() + 8 + 3 * R);
+    }
+    hipEvent_t e0{};
+    ctx[0]->prof_begin(KID_EXCHANGE, e0);
+    G_RC(tr->allgather(8, s, rv));
+    ctx[0]->prof_end(KID_EXCHANGE, e0);
+  }
+  G_HIP(hipMemcpyAsync(hv.data(), ctx[0]->dl_seg.as<u64>() + 8 + 3 * R, size_t(R) * 8, hipMemcpyDeviceToHost,
+                       ctx[0]->stream));
+  for (gcz_ctx* cx : ctx) G_HIP(hipStreamSynchronize(cx->stream));
+  c.assign(R, 0);
+  off.assign(R + 1, 0);
+  for (int r = 0; r < R; ++r) {
+    c[r] = hv[r];
+    off[r + 1] = off[r] + c[r];
+  }
+  total = off[R];
+  if (total > u64(kIdx)) return fail(GCZ_ERR_CAPACITY, "more than 2^29-1 unique leaves");
+  // exchange 3: every rank gets every r-first list, relayed in two steps so no link
+  // carries rank 0's long list R - 1 times: piece q of list r goes to rank q, then each
+  // rank sends the pieces it holds to all ranks
+  auto pc = [&](int r, int q) { return c[r] * u64(q) / u64(R); };   // start of piece q of list r
+  std::vector<u64> M1(size_t(R) * R), T(R, 0), M2(size_t(R) * R), sd2(size_t(R) * R, 0), rd2(size_t(R) * R);
+  for (int r = 0; r < R; ++r)
+    for (int q = 0; q < R; ++q) {
+      M1[size_t(r) * R + q] = pc(r, q + 1) - pc(r, q);
+      T[q] += M1[size_t(r) * R + q];
+    }
+  for (int q = 0; q < R; ++q)
+    for (int d = 0; d < R; ++d) {
+      M2[size_t(q) * R + d] = T[q];
+      u64 o = 0;
+      for (int q2 = 0; q2 < q; ++q2) o += T[q2];
+      rd2[size_t(d) * R + q] = o;
+    }
+  std::vector<DlSeg> seg;   // (at most R^2 <= 961 nonempty pieces: k_dl_gid holds 1024)
+  {
+    u64 o = 0;
+    for (int q = 0; q < R; ++q)
+      for (int r = 0; r < R; ++r) {
+        const u64 len = M1[size_t(r) * R + q];
+        if (len) seg.push_back({o, len, off[r] + pc(r, q)});
+        o += len;
+      }
+  }
+  {
+    std::vector<const void*> s;
+    std::vector<void*> rv;
+    for (int i = 0; i < NL; ++i) {
+      gcz_ctx* cx = ctx[i];
+      if (cx->ensure(cx->dl_stage, T[rank[i]] * 4 + 16) || cx->ensure(cx->dl_recv, total * 4 + 16) ||
+          cx->ensure(cx->dl_gid, ncodes * 4 + 16))
+        return dev_fail("dense leaf relay");
+      s.push_back(cx->dl_list.ptr);
+      rv.push_back(cx->dl_stage.ptr);
+    }
+    hipEvent_t e0{};
+    ctx[0]->prof_begin(KID_EXCHANGE, e0);
+    G_RC(tr->alltoallv(M1, false, 4, s, rv));
+    std::vector<const void*> s2;
+    std::vector<void*> rv2;
+    for (gcz_ctx* cx : ctx) {
+      s2.push_back(cx->dl_stage.ptr);
+      rv2.push_back(cx->dl_recv.ptr);
+    }
+    G_RC(tr->alltoallv_at(M2, false, 4, sd2, rd2, s2, rv2));
+    ctx[0]->prof_end(KID_EXCHANGE, e0);
+  }
+  // global ids, then the words and this rank's slice of the leaves
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    Header* h = cx->hdr.as<Header>();
+    {
+      ProfScope ps_(cx, KID_IDS);
+      DlSeg* dseg = reinterpret_cast<DlSeg*>(cx->dl_seg.as<u64>() + 64 + 3 * R);
+      G_HIP(hipMemcpyAsync(dseg, seg.data(), seg.size() * sizeof(DlSeg), hipMemcpyHostToDevice, cx->stream));
+      if (total)
+        hipLaunchKernelGGL(k_dl_gid, dim3(unsigned((total + 255) / 256)), dim3(256), 0, cx->stream,
+                           cx->dl_recv.as<u32>(), dseg, int(seg.size()), total, cx->dl_gid.as<u32>());
+      const u64 cr = c[rank[i]];
+      if (cr)
+        hipLaunchKernelGGL(k_dl_leaves, dim3(unsigned((cr + 255) / 256)), dim3(256), 0, cx->stream,
+                           cx->dl_list.as<u32>(), cr, cx->dl_plan, cx->leaves_out.as<u64>());
+      G_HIP(hipGetLastError());
+    }
+    if (int rc = cx->dense_phase_b(las[i], h, cx->dl_gid.as<u32>(), nullptr))
+      return rc == GCZ_ERR_DEVICE ? dev_fail("dense leaves") : rc;
+  }
+  *used = true;
+  return GCZ_OK;
+}
 
 // key_bits: bits of the owner-table key (leaves 4L, nodes 2 (child_bits + 2)); packed slots when
 // key_bits + R + 2 <= 64, else wide.
@@ -975,7 +1157,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
   for (int i = 0; i < NL; ++i) {
     const u64 S_r = P.count(rank[i], 0);
     const u64 full = std::max<u64>(256, next_pow2(2 * S_r));
-    leaf_cap[i] = S_r > (1ull << 22) ? std::min(full, std::max<u64>(1ull << 24, ctx[i]->leaf_cap_hint)) : full;
+    leaf_cap[i] = S_r > (1ull << 22) ? std::min(full, u64(1) << 24) : full;   // (no state across builds)
   }
   allow_packed = true;
   for (gcz_ctx* cx : ctx) allow_packed = allow_packed && !cx->force_wide;
@@ -1014,6 +1196,21 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     std::vector<u64> dcur(NL, 0);
     any_predup = false;
 
+    std::vector<u64> c, off;
+    u64 total = 0, err_global = 0;
+    int err_sym = 0, ovf = 0;
+    // ---- leaves: the dense level (pure ACGT, L <= 12) when every rank holds strands ----
+    bool dense = false;
+    if (dense_mode != 0 && L <= 12) {
+      bool all = true;
+      for (int s2 = 0; s2 < R; ++s2) all = all && P.count(s2, 0) > 0;
+      if (all) G_RC(dense_leaves(bases, d_leaves, L, c, off, total, &dense));
+    }
+    if (dense) {
+      leaf_deferred = false;
+      leaf_identity.assign(NL, true);
+      leaf_gmark.assign(NL, nullptr);
+    }
     // ---- leaves ----
     // Leaf dictionary (bases input, R > 1).  Nothing precedes rank 0, so the first-occurrence
     // keys of its first c0 chunks carry their GLOBAL ids already.  Rank 0 runs those chunks,
@@ -1024,7 +1221,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     // Rank 0 still sends all its keys to the owners, so any rank may go without seeding.
     const std::vector<u64> chunks0 = leaf_chunks(P.count(0, 0), leaf_first_log2);
     const int c0 = seed_chunks;
-    const bool seeding = R > 1 && d_bases && c0 > 0 && int(chunks0.size()) - 1 > c0;
+    const bool seeding = !dense && R > 1 && d_bases && c0 > 0 && int(chunks0.size()) - 1 > c0;
     std::vector<int> C(NL);
     std::vector<LeafLevel> las(NL);
     for (int i = 0; i < NL; ++i) {
@@ -1050,6 +1247,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
       la.desc = cx->desc.as<u64>();
       la.count = h->count;
       la.ticket = h->ticket;
+      if (dense) continue;
       if (seeding) {   // every local id space must hold the dictionary's ids
         la.seed_n = P.count(0, 0) >= chunks0[c0] ? chunks0[c0] : 0;
         if (rank[i] != 0) continue;
@@ -1115,7 +1313,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         if (ctx[i]->leaf_level(la, ctx[i]->hdr.as<Header>())) return dev_fail("leaf level");
       }
     }
-    for (int i = 0; i < NL; ++i) {
+    for (int i = 0; i < NL && !dense; ++i) {
       gcz_ctx* cx = ctx[i];
       Header* h = cx->hdr.as<Header>();
       const u64 S_r = P.count(rank[i], 0);
@@ -1132,14 +1330,11 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
       rl.gmark = seeding ? cx->nf_set[0] : nullptr;
       rl.identity = rank[i] == 0;
     }
-    std::vector<u64> c, off;
-    u64 total = 0, err_global = 0;
-    int err_sym = 0, ovf = 0;
     // Without the local dedupe the leaf words are translated by layer 0's k_node_keys (one
     // pass instead of two), unless layer 0 turns out direct or is not distributed (exchange
     // decides once the leaf totals are known: leaf_deferred).
     for (int i = 0; i < NL; ++i) lv[i].defer_remap = G > 0;
-    {
+    if (!dense) {
       std::vector<u64> nw(NL);
       for (int i = 0; i < NL; ++i) nw[i] = P.count(rank[i], 0);
       const int rc = exchange(lv, nw, d_leaves ? 64u : 4 * u32(L), 0, c, off, total, &err_global, &err_sym, &ovf);
@@ -1166,7 +1361,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     leaf_offs.assign(NL, 0);
     for (int i = 0; i < NL; ++i) leaf_offs[i] = u32(off[rank[i]]);
     info.n_leaves = total;
-    for (int i = 0; i < NL; ++i) ctx[i]->leaf_cap_hint = next_pow2(std::max<u64>(1, 2 * total));
+    info.leaf_path = dense ? 1u : 0u;
 
     // ---- distributed node levels ----
     // Without repetitive data the local dedupe of a node level finds almost nothing and

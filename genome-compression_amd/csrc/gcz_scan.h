@@ -29,17 +29,27 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_excl(In in, u64 n, u32* _
   __shared__ u32 s_tile;
   __shared__ u32 s_wave[kScanThreads / 64];
   __shared__ u64 s_prefix;
+  __shared__ u32 s_tr[kScanTile + kScanTile / 16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid == 0) s_tile = atomicAdd(ticket, 1u);
   __syncthreads();
   const u64 tile = s_tile;
-  const u64 base = tile * kScanTile + u64(tid) * kScanItems;   // each thread: kScanItems consecutive
+  const u64 t0 = tile * kScanTile;
+  // coalesced loads (element e * 256 + tid), transposed through LDS so that each
+  // thread scans kScanItems consecutive elements
+  // LDS index of tile element j padded by j / 16: the blocked reads are conflict-free
+#pragma unroll
+  for (int e = 0; e < kScanItems; ++e) {
+    const u32 j = u32(e) * kScanThreads + tid;
+    const u64 i = t0 + j;
+    s_tr[j + (j >> 4)] = i < n ? in(i) : 0u;
+  }
+  __syncthreads();
   u32 v[kScanItems];
   u32 sum = 0;
 #pragma unroll
   for (int e = 0; e < kScanItems; ++e) {
-    const u64 i = base + e;
-    v[e] = i < n ? in(i) : 0u;
+    v[e] = s_tr[tid * (kScanItems + 1) + e];
     sum += v[e];
   }
   u32 incl = sum;   // inclusive scan over the wave
@@ -87,11 +97,18 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_excl(In in, u64 n, u32* _
   __syncthreads();
   u32 run = u32(s_prefix) + incl - sum;
   for (int w = 0; w < wave; ++w) run += s_wave[w];
+  __syncthreads();   // (every thread has read its items)
+#pragma unroll
+  for (int e = 0; e < kScanItems; ++e) {   // exclusive prefixes back through LDS, stored coalesced
+    s_tr[tid * (kScanItems + 1) + e] = run;
+    run += v[e];
+  }
+  __syncthreads();
 #pragma unroll
   for (int e = 0; e < kScanItems; ++e) {
-    const u64 i = base + e;
-    if (i < n) out[i] = run;
-    run += v[e];
+    const u32 j = u32(e) * kScanThreads + tid;
+    const u64 i = t0 + j;
+    if (i < n) out[i] = s_tr[j + (j >> 4)];
   }
 }
 
