@@ -264,8 +264,8 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
                      ucount);
   HIP_TRY(hipGetLastError());
   if (list) {
-    hipLaunchKernelGGL(k_dl_lh, dim3(unsigned((nfb + 255) / 256)), dim3(256), 0, stream, dl_pw.as<u32>(),
-                       dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), nfb, dl_lh.as<u32>());
+    hipLaunchKernelGGL(k_dl_lh, dim3(unsigned((S + 255) / 256)), dim3(256), 0, stream, dl_pw.as<u32>(),
+                       dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), S, dl_lh.as<u32>());
     HIP_TRY(hipGetLastError());
   }
   prof_end(KID_DL_FBSCAN, e0);

@@ -373,9 +373,13 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
   __syncthreads();
   for (u32 b = tid; b < P.NB; b += kDThreads) {
     const u32 o0 = fo[u64(ch) * P.NB + b], o1 = fo[u64(ch + 1) * P.NB + b];
-    for (u32 k = o0; k < o1; ++k) {
-      const u32 q = fl[u64(b) * RB + k] & (kDC - 1);
-      atomicOr(&s_bits[q >> 5], 1u << (q & 31));
+    for (u32 k0 = o0; k0 < o1; k0 += 8) {   // 8 loads in flight
+      u32 q[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[j] = k0 + j < o1 ? fl[u64(b) * RB + k0 + j] & (kDC - 1) : ~0u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (q[j] != ~0u) atomicOr(&s_bits[q[j] >> 5], 1u << (q[j] & 31));
     }
   }
   __syncthreads();
@@ -512,16 +516,11 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
 // ids of first occurrences increase with position, so the writes are contiguous).
 [[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_lh(const u32* __restrict__ pw,
                                                      const unsigned long long* __restrict__ fb,
-                                                     const u32* __restrict__ wpre, u64 nfb, u32* __restrict__ lh) {
-  const u64 w = u64(blockIdx.x) * 256 + threadIdx.x;
-  if (w >= nfb) return;
-  unsigned long long m = fb[w];
-  u32 id = wpre[w];
-  while (m) {
-    const int bit = __ffsll((long long)m) - 1;
-    m &= m - 1;
-    lh[id++] = pw[w * 64 + bit] & kIdx;
-  }
+                                                     const u32* __restrict__ wpre, u64 S, u32* __restrict__ lh) {
+  const u64 s = u64(blockIdx.x) * 256 + threadIdx.x;
+  if (s >= S) return;
+  const unsigned long long m = fb[s >> 6];
+  if ((m >> (s & 63)) & 1ull) lh[wpre[s >> 6] + u32(__popcll(m & ((1ull << (s & 63)) - 1ull)))] = pw[s] & kIdx;
 }
 
 // (pure-ACGT failure flag, local uniques, repetitive-data flag) for the first exchange

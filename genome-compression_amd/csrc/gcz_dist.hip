@@ -31,6 +31,7 @@ struct gcz_dist_state {
   DevBuf scratch, gnf, gmul, gid, blockcnt, bchunk, skey, sidx, sflag, scval, sdval;   // sender side
   DevBuf dict;                                                                // rank 0's leaf dictionary
   DevBuf rkey, oslot, rflag, rcval, rdval, owntab, oids, omin;                // owner side
+  DevBuf ob_cnt, ob_off, ob_desc, ob_rec;                                      // owner bucketed dedupe
   DevBuf dhdr, gath, gath2, gathf, ddesc, tail_in;
   u64* h_gath = nullptr;    // pinned mirrors of the gathered vectors
   u64* h_gath2 = nullptr;
@@ -42,7 +43,7 @@ void gcz_dist_state_free(gcz_ctx* c) {
   if (!d) return;
   for (DevBuf* b : {&d->dict, &d->scratch, &d->gnf, &d->gmul, &d->gid, &d->blockcnt, &d->bchunk, &d->skey, &d->sidx, &d->sflag,
                     &d->scval, &d->sdval, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab, &d->oids,
-                    &d->omin,
+                    &d->omin, &d->ob_cnt, &d->ob_off, &d->ob_desc, &d->ob_rec,
                     &d->dhdr, &d->gath, &d->gath2, &d->gathf, &d->ddesc, &d->tail_in})
     if (b->ptr) (void)hipFree(b->ptr);
   for (u64* h : {d->h_gath, d->h_gath2, d->h_gathf})
@@ -517,6 +518,8 @@ struct gcz_group {
   int dense_leaves(const std::vector<const unsigned char*>& bases, const u64* const* d_leaves, int L,
                    std::vector<u64>& c, std::vector<u64>& off, u64& total, bool* used);
   int dense_mode = std::getenv("GCZ_DENSE") ? std::atoi(std::getenv("GCZ_DENSE")) : 1;   // 0: hash-table leaves
+  // owners hash-cons levels without the local dedupe in LDS buckets (GCZ_OWNER_BUCKETS=0: the table)
+  bool owner_buckets = !std::getenv("GCZ_OWNER_BUCKETS") || std::atoi(std::getenv("GCZ_OWNER_BUCKETS")) != 0;
   int exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, u32 key_bits, u32 child_bits,
                std::vector<u64>& c, std::vector<u64>& off, u64& total, u64* err_global, int* err_sym,
                int* ovf_bits, bool nolocal = false, bool lookahead = false, u64* next_hashed_out = nullptr);
@@ -929,15 +932,49 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       gcz_dist_state& d = *cx->dist;
       const u64 nr = recvd(rank[i]);
       ProfScope ps_(cx, KID_OWNER);
-      G_HIP(hipMemsetAsync(d.owntab.ptr, 0xff, size_t(otab[i].mask + 1) * (otab[i].packed ? 8 : 16), cx->stream));
+      // owner bucketed dedupe (no table): nolocal levels whose records pack into 8 bytes
+      OwnBkt ob{};
+      bool use_ob = false;
+      if (opos[i].packed && owner_buckets && nr >= 2) {
+        ob.T = opos[i].pt;
+        ob.B = child_bits;
+        ob.K = key_bits;
+        ob.bb = 0;
+        while (ob.bb < 12 && (nr >> ob.bb) > 4096) ++ob.bb;
+        ob.nch = u32((nr + kDC - 1) / kDC);
+        ob.nr = nr;
+        use_ob = ob.K >= ob.bb && ob.K - ob.bb + kDLog <= 64 && ob.nch <= 8192;
+      }
+      if (!use_ob)
+        G_HIP(hipMemsetAsync(d.owntab.ptr, 0xff, size_t(otab[i].mask + 1) * (otab[i].packed ? 8 : 16), cx->stream));
       const Displ D = displ_of(rank[i]);
       if (opos[i].packed) {
         unsigned char* onf = d.omin.as<unsigned char>();
         unsigned char* omul = onf + nr + 32;
         G_HIP(hipMemsetAsync(onf, 0, 2 * nr + 64, cx->stream));
-        hipLaunchKernelGGL(k_own_insert_pos, blocks(nr), dim3(kBlock), 0, cx->stream, d.rkey.as<u64>(), nr,
-                           child_bits, opos[i].pt, Marks{onf, omul}, d.oslot.as<u32>(),
-                           &cx->hdr.as<Header>()->overflow);
+        if (use_ob) {
+          const u64 ncnt = (u64(1) << ob.bb) * ob.nch, t = scan_tiles(ncnt + 1);
+          if (cx->ensure(d.ob_cnt, ncnt * 4 + 16) || cx->ensure(d.ob_off, (ncnt + 1) * 4 + 16) ||
+              cx->ensure(d.ob_desc, t * 8 + 64) || cx->ensure(d.ob_rec, nr * 8 + 16))
+            return dev_fail("owner buckets");
+          G_HIP(hipMemsetAsync(d.ob_desc.ptr, 0, t * 8 + 64, cx->stream));
+          G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_ob_dedupe),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, int((ob.nch + 1) * 4)));
+          hipLaunchKernelGGL(k_ob_count, dim3(ob.nch), dim3(1024), 0, cx->stream, d.rkey.as<u64>(), ob,
+                             d.ob_cnt.as<u32>());
+          hipLaunchKernelGGL(k_scan_excl<ScanU32>, dim3(unsigned(t)), dim3(kScanThreads), 0, cx->stream,
+                             ScanU32{d.ob_cnt.as<u32>(), ncnt}, ncnt + 1, d.ob_off.as<u32>(), d.ob_desc.as<u64>(),
+                             reinterpret_cast<u32*>(d.ob_desc.as<u64>() + t), static_cast<u64*>(nullptr));
+          hipLaunchKernelGGL(k_ob_scatter, dim3(ob.nch), dim3(1024), 0, cx->stream, d.rkey.as<u64>(), ob,
+                             d.ob_off.as<u32>(), d.ob_rec.as<u64>());
+          hipLaunchKernelGGL(k_ob_dedupe, dim3(1u << ob.bb), dim3(1024), (ob.nch + 1) * 4, cx->stream,
+                             d.ob_rec.as<u64>(), d.ob_off.as<u32>(), ob, Marks{onf, omul}, d.oslot.as<u32>(),
+                             &cx->hdr.as<Header>()->overflow);
+        } else {
+          hipLaunchKernelGGL(k_own_insert_pos, blocks(nr), dim3(kBlock), 0, cx->stream, d.rkey.as<u64>(), nr,
+                             child_bits, opos[i].pt, Marks{onf, omul}, d.oslot.as<u32>(),
+                             &cx->hdr.as<Header>()->overflow);
+        }
         hipLaunchKernelGGL(k_own_reply_marks, blocks(nr), dim3(kBlock), 0, cx->stream, onf, omul, nr,
                            d.rflag.as<unsigned char>());
       } else {

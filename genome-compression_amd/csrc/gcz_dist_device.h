@@ -24,6 +24,7 @@
 #pragma once
 
 #include "gcz_device.h"
+#include "gcz_dense.h"
 
 namespace gcz_dev {
 
@@ -423,6 +424,145 @@ static __global__ __launch_bounds__(kBlock) void k_own_insert_pos(const u64* __r
   const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (k >= nrecv) return;
   oslot[k] = T.insert(own_pack_key(rkey[k] & ~kLocalMulti, 0, B), u32(k), mk, ovf);
+}
+
+// The same owner hash-cons without a table (non-repetitive levels: almost every key is
+// new): the received keys are partitioned into NB buckets by the top bits of
+// h = T.mix(key) (a bijection on the K key bits), per chunk of kDC receive indices
+// (count, scan, scatter of (h's low bits, index in chunk) records), and each bucket is
+// hash-consed by one workgroup in LDS.  Only keys with several records write anything:
+// not-first marks, the first index's multi mark, and oslot = the first index (the id
+// slot of k_own_setid / k_own_getid).  A bucket over kObCap records (a hot key) sets
+// *ovf: the level is redone through the table.
+constexpr u32 kObCap = 6144;     // records per bucket held in registers (6 per thread)
+constexpr u32 kObSlots = 8192;   // LDS table: 64 KB keys + 32 KB first indices
+
+struct OwnBkt {
+  PackedTab T;   // mix over K bits (plan_table of the level's owner keys)
+  u32 B;         // child index bits (own_pack_key)
+  u32 K, bb;     // key bits, bucket bits
+  u32 nch;       // chunks of kDC receive indices
+  u64 nr;
+  __device__ __forceinline__ u64 hash(u64 raw) const { return T.mix(own_pack_key(raw & ~kLocalMulti, 0, B)); }
+};
+
+static __global__ __launch_bounds__(1024) void k_ob_count(const u64* __restrict__ rkey, OwnBkt P,
+                                                          u32* __restrict__ cnt) {
+  __shared__ u32 hist[4096];
+  const u32 NB = 1u << P.bb;
+  for (u32 b = threadIdx.x; b < NB; b += 1024) hist[b] = 0;
+  __syncthreads();
+  const u64 k0 = u64(blockIdx.x) * kDC;
+  for (u32 q0 = 0; q0 < kDC; q0 += 1024 * 8) {
+    u64 x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const u64 k = k0 + q0 + u32(j) * 1024 + threadIdx.x;
+      x[j] = k < P.nr ? rkey[k] : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const u64 k = k0 + q0 + u32(j) * 1024 + threadIdx.x;
+      if (k < P.nr) atomicAdd(&hist[u32(P.hash(x[j]) >> (P.K - P.bb))], 1u);
+    }
+  }
+  __syncthreads();
+  for (u32 b = threadIdx.x; b < NB; b += 1024) cnt[u64(b) * P.nch + blockIdx.x] = hist[b];
+}
+
+static __global__ __launch_bounds__(1024) void k_ob_scatter(const u64* __restrict__ rkey, OwnBkt P,
+                                                            const u32* __restrict__ off, u64* __restrict__ rec) {
+  __shared__ u32 cur[4096];
+  const u32 NB = 1u << P.bb, ch = blockIdx.x;
+  for (u32 b = threadIdx.x; b < NB; b += 1024) cur[b] = off[u64(b) * P.nch + ch];
+  __syncthreads();
+  const u64 k0 = u64(ch) * kDC;
+  const u64 lowmask = (1ull << (P.K - P.bb)) - 1ull;
+  for (u32 q0 = 0; q0 < kDC; q0 += 1024 * 8) {
+    u64 x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const u64 k = k0 + q0 + u32(j) * 1024 + threadIdx.x;
+      x[j] = k < P.nr ? rkey[k] : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const u32 q = q0 + u32(j) * 1024 + threadIdx.x;
+      if (k0 + q >= P.nr) continue;
+      const u64 h = P.hash(x[j]);
+      const u32 d = atomicAdd(&cur[u32(h >> (P.K - P.bb))], 1u);
+      rec[d] = ((h & lowmask) << kDLog) | q;
+    }
+  }
+}
+
+static __global__ __launch_bounds__(1024) void k_ob_dedupe(const u64* __restrict__ rec, const u32* __restrict__ off,
+                                                           OwnBkt P, Marks mk, u32* __restrict__ oslot,
+                                                           u32* __restrict__ ovf) {
+  __shared__ unsigned long long s_key[kObSlots];
+  __shared__ u32 s_pos[kObSlots];
+  __shared__ u32 s_dup[kObSlots / 32];
+  extern __shared__ u32 s_run[];   // nch + 1 run starts of the bucket
+  constexpr int E = kObCap / 1024;
+  const u64 b = blockIdx.x;
+  const u32 start = off[b * P.nch], end = off[(b + 1) * P.nch];
+  if (end - start > kObCap) {
+    if (threadIdx.x == 0) atomicOr(ovf, 1u);
+    return;
+  }
+  for (u32 q = threadIdx.x; q <= P.nch; q += 1024) s_run[q] = off[b * P.nch + q];
+  for (u32 q = threadIdx.x; q < kObSlots; q += 1024) {
+    s_key[q] = kEmpty;
+    s_pos[q] = ~0u;
+  }
+  for (u32 q = threadIdx.x; q < kObSlots / 32; q += 1024) s_dup[q] = 0;
+  u64 x[E];
+  u32 slot[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const u32 i = start + u32(e) * 1024 + threadIdx.x;
+    x[e] = i < end ? rec[i] : kEmpty;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    if (x[e] == kEmpty) continue;
+    const u64 key = x[e] >> kDLog;
+    u32 h = u32((u64(u32(bkt_hash(key))) * kObSlots) >> 32);
+    for (;;) {
+      unsigned long long c = s_key[h];
+      if (c == kEmpty) c = atomicCAS(&s_key[h], kEmpty, (unsigned long long)key);
+      if (c == key) atomicOr(&s_dup[h >> 5], 1u << (h & 31));
+      if (c == kEmpty || c == key) break;
+      h = h + 1 == kObSlots ? 0u : h + 1;
+    }
+    slot[e] = h;
+  }
+  __syncthreads();
+  u32 pos[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {   // only keys with several records need their indices
+    pos[e] = ~0u;
+    if (x[e] == kEmpty || !((s_dup[slot[e] >> 5] >> (slot[e] & 31)) & 1u)) continue;
+    const u32 i = start + u32(e) * 1024 + threadIdx.x;
+    u32 lo = 0, hi = P.nch - 1;   // chunk: the last run starting at or before record i
+    while (lo < hi) {
+      const u32 mid = (lo + hi + 1) >> 1;
+      if (s_run[mid] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    pos[e] = (lo << kDLog) | u32(x[e] & (kDC - 1));
+    atomicMin(&s_pos[slot[e]], pos[e]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    if (pos[e] == ~0u) continue;
+    const u32 first = s_pos[slot[e]];
+    oslot[pos[e]] = first;
+    if (pos[e] != first) mk.nf[pos[e]] = kNfNot;
+    else mk.multi[pos[e]] = 1;
+  }
 }
 
 // Reply from the marks: not first (1), repeats (2), and C / D whenever the key repeats (4),

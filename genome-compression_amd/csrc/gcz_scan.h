@@ -15,9 +15,9 @@
 
 namespace gcz_dev {
 
-constexpr int kScanThreads = 256;
+constexpr int kScanThreads = 1024;
 constexpr int kScanItems = 16;
-constexpr u64 kScanTile = u64(kScanThreads) * kScanItems;   // 4096 elements
+constexpr u64 kScanTile = u64(kScanThreads) * kScanItems;   // 16 Ki elements (a short look-back chain)
 
 __host__ __device__ inline u64 scan_tiles(u64 n) { return (n + kScanTile - 1) / kScanTile; }
 
