@@ -1,8 +1,6 @@
 // MI355X (gfx950) shared_tree construction: host orchestration and the C ABI.
 // Device code and the algorithm description: gcz_device.h; the multi-rank
 // build: gcz_dist.hip.
-#include <hipcub/hipcub.hpp>
-
 #include "gcz_ctx.h"
 #include "gcz_dense.h"
 #include "gcz_scan.h"
@@ -335,14 +333,38 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   const u32 bb = bp.bb;
   const u64 G = (p + kBktChunk - 1) / kBktChunk;
   const u64 ncnt = (u64(1) << bb) * G + 1;
-  size_t scan_bytes = 0;
-  if (bkt) {
+  const u64 t_scan = scan_tiles(ncnt);   // look-back scan of the count matrix: descriptors + ticket
+  // two-pass partition (k_bkt_part / fine / dedupe2) when a record holds the key's low
+  // K - bb bits and the full position, and a chunk's coarse segment fits a fine slice
+  Bkt2Plan b2{};
+  b2.T = nt.pt;
+  b2.K = bp.K;
+  b2.b1 = std::min<u32>(bb, kPartMaxB1);
+  b2.b2 = bb - b2.b1;
+  b2.G = G;
+  const u64 mean_seg = std::min<u64>(p, kBktChunk) >> b2.b1;
+  b2.segcap = u32(2 * mean_seg + 256);
+  b2.SC = u32(std::max<u64>(1, std::min<u64>(64, u64(kFineCap / 2) / std::max<u64>(1, kBktChunk >> b2.b1))));
+  b2.P = kBktRP + log2_exact(b2.SC);   // (SC is a power of two)
+  b2.nslice = u32((G + b2.SC - 1) / b2.SC);
+  const bool two = bkt && two_pass && b2.b2 <= u32(kFineMaxB2) && bp.K - b2.b1 + kBktRP <= 64 &&
+                   bp.K - bb + b2.P <= 64 && 2 * mean_seg <= u64(kFineCap) / 2 && b2.nslice <= 512;
+  if (two) {
+    int rc;
+    const u64 nfine = (u64(1) << b2.b1) * b2.nslice;
+    if ((rc = ensure(bkt_key, G * (u64(1) << b2.b1) * b2.segcap * 8)) ||
+        (rc = ensure(bkt_cnt, G * (u64(1) << b2.b1) * 4 + 16)) ||
+        (rc = ensure(bkt_rec2, nfine * kFineCap * 8)) ||
+        (rc = ensure(bkt_off, nfine * ((u64(1) << b2.b2) + 1) * 4 + 16)))
+      return rc;
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(k_bkt_fine),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, int(kFineCap * 8)));
+  } else if (bkt) {
     int rc;
     if ((rc = ensure(bkt_key, p * 8)) || (rc = ensure(bkt_cnt, ncnt * 4)) ||
-        (rc = ensure(bkt_off, ncnt * 4)))
+        (rc = ensure(bkt_off, ncnt * 4)) || (rc = ensure(bkt_tmp, t_scan * 8 + 16)))
       return rc;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, bkt_cnt.as<u32>(), bkt_off.as<u32>(), ncnt, stream));
-    if ((rc = ensure(bkt_tmp, scan_bytes))) return rc;
+    HIP_TRY(hipMemsetAsync(bkt_tmp.ptr, 0, t_scan * 8 + 16, stream));
   }
   hipEvent_t e0{};
   prof_begin(KID_MEMSET, e0);
@@ -356,15 +378,34 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   }
   prof_end(KID_MEMSET, e0);
   const dim3 gi(unsigned((p + kBlock - 1) / kBlock));
-  if (bkt) {
+  if (two) {
+    prof_begin(KID_BKT_SCATTER, e0);
+    hipLaunchKernelGGL(k_bkt_part, dim3(unsigned(G)), dim3(kBktThreads), 0, stream, a.in, n, p, pnf, pmu, b2,
+                       bkt_key.as<u64>(), bkt_cnt.as<u32>(), a.words, d_hdr, a.pcount, stats.as<u64>());
+    HIP_TRY(hipGetLastError());
+    prof_end(KID_BKT_SCATTER, e0);
+    prof_begin(KID_BKT_FINE, e0);
+    hipLaunchKernelGGL(k_bkt_fine, dim3(unsigned((u64(1) << b2.b1) * b2.nslice)), dim3(kBktThreads),
+                       size_t(kFineCap) * 8, stream, bkt_key.as<u64>(), bkt_cnt.as<u32>(), b2, bkt_rec2.as<u64>(),
+                       bkt_off.as<u32>(), d_hdr, a.pcount, n);
+    HIP_TRY(hipGetLastError());
+    prof_end(KID_BKT_FINE, e0);
+    prof_begin(KID_BKT_DEDUPE, e0);
+    hipLaunchKernelGGL(k_bkt_dedupe2, dim3(1u << bb), dim3(kBktThreads), 0, stream, bkt_rec2.as<u64>(),
+                       bkt_off.as<u32>(), b2, a.words, mk, d_hdr, a.pcount, n);
+    HIP_TRY(hipGetLastError());
+    prof_end(KID_BKT_DEDUPE, e0);
+  } else if (bkt) {
     prof_begin(KID_BKT_COUNT, e0);
     hipLaunchKernelGGL(k_bkt_count, dim3(unsigned(G)), dim3(kBktThreads), 0, stream, a.in, n, p, pnf, pmu, bp,
                        bkt_cnt.as<u32>(), G, d_hdr, a.pcount, stats.as<u64>());
     HIP_TRY(hipGetLastError());
     prof_end(KID_BKT_COUNT, e0);
     prof_begin(KID_BKT_SCAN, e0);
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(bkt_tmp.ptr, scan_bytes, bkt_cnt.as<u32>(), bkt_off.as<u32>(), ncnt,
-                                             stream));
+    hipLaunchKernelGGL(k_scan_excl<ScanU32>, dim3(unsigned(t_scan)), dim3(kScanThreads), 0, stream,
+                       ScanU32{bkt_cnt.as<u32>(), ncnt - 1}, ncnt, bkt_off.as<u32>(), bkt_tmp.as<u64>(),
+                       reinterpret_cast<u32*>(bkt_tmp.as<u64>() + t_scan), static_cast<u64*>(nullptr));
+    HIP_TRY(hipGetLastError());
     prof_end(KID_BKT_SCAN, e0);
     prof_begin(KID_BKT_SCATTER, e0);
     hipLaunchKernelGGL(k_bkt_scatter, dim3(unsigned(G)), dim3(kBktThreads), 0, stream, a.in, n, p, pnf, pmu, bp,
@@ -670,6 +711,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   if (const char* t = std::getenv("GCZ_PREDUP")) c->predup_mode = std::atoi(t);   // 1 on, 2 off, 0 auto
   if (const char* t = std::getenv("GCZ_BUCKET")) c->use_bucket = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_BUCKET_MIN")) c->bucket_min = std::strtoull(t, nullptr, 10);
+  if (const char* t = std::getenv("GCZ_BUCKET_TWO")) c->two_pass = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_DENSE")) c->dense_mode = std::atoi(t);
   if (const char* t = std::getenv("GCZ_LEAF_FIRST_LOG2")) c->leaf_first_log2 = std::max(1, std::min(20, std::atoi(t)));
   *out = c;
@@ -684,7 +726,7 @@ void gcz_ctx_destroy(gcz_ctx* c) {
   gcz_sort_state_free(c);
   gcz_ingest_state_free(c);
   for (DevBuf* b : {&c->wa, &c->wb, &c->grp, &c->desc, &c->tab, &c->leaves_out, &c->nodes_out, &c->hdr, &c->input,
-                    &c->nf, &c->multi, &c->stats, &c->bkt_key, &c->bkt_cnt, &c->bkt_off, &c->bkt_tmp, &c->dl_pw,
+                    &c->nf, &c->multi, &c->stats, &c->bkt_key, &c->bkt_cnt, &c->bkt_off, &c->bkt_tmp, &c->bkt_rec2, &c->dl_pw,
                     &c->dl_rec, &c->dl_idrec, &c->dl_cnt, &c->dl_off, &c->dl_fpg, &c->dl_fb, &c->dl_wpre,
                     &c->dl_desc, &c->dl_fl, &c->dl_fo, &c->dl_lh, &c->dl_pb, &c->dl_pbs, &c->dl_lower,
                     &c->dl_pos, &c->dl_list, &c->dl_gid, &c->dl_recv, &c->dl_stage, &c->dl_seg})

@@ -98,14 +98,14 @@ inline LevelTab plan_table(void* buf, u64 cap, u32 K, u64 npos, u32 B, bool allo
 enum KernelId {
   KID_LEAF, KID_NODE, KID_FLAGSCAN_LEAF, KID_FLAGSCAN_NODE, KID_RESOLVE_LEAF, KID_RESOLVE_NODE, KID_MEMSET,
   KID_EXCHANGE, KID_DIST, KID_OWNER, KID_IDS, KID_REMAP, KID_TAIL, KID_SORT, KID_DAG, KID_DIRECT,
-  KID_BKT_COUNT, KID_BKT_SCAN, KID_BKT_SCATTER, KID_BKT_DEDUPE,
+  KID_BKT_COUNT, KID_BKT_SCAN, KID_BKT_SCATTER, KID_BKT_DEDUPE, KID_BKT_FINE,
   KID_DL_PACK, KID_DL_SCAN, KID_DL_SCATTER, KID_DL_FIRST, KID_DL_FBSCAN, KID_DL_IDS, KID_DL_WORDS, KID_COUNT
 };
 inline const char* kernel_name(int k) {
   static const char* names[KID_COUNT] = {"leaf_insert", "node_insert", "flagscan_leaf", "flagscan_node",
                                          "resolve_leaf", "resolve_node", "clear", "exchange", "dist_bucket",
                                          "dist_owner", "dist_ids", "dist_remap", "tail", "sort", "dag_write", "direct_levels",
-                                         "bucket_count", "bucket_scan", "bucket_scatter", "bucket_dedupe",
+                                         "bucket_count", "bucket_scan", "bucket_scatter", "bucket_dedupe", "bucket_fine",
                                          "dl_pack", "dl_scan", "dl_scatter", "dl_first", "dl_fbscan", "dl_ids",
                                          "dl_words"};
   return names[k];
@@ -170,7 +170,7 @@ struct gcz_ctx {
   std::string last_error;
   gcz_host::DevBuf wa, wb, grp, desc, tab, leaves_out, nodes_out, hdr, input, nf, multi;
   gcz_host::DevBuf stats;   // hashed-pair counter shards (k_node_insert), summed into hdr->hashed[0]
-  gcz_host::DevBuf bkt_key, bkt_cnt, bkt_off, bkt_tmp;   // bucketed node insert (k_bkt_*)
+  gcz_host::DevBuf bkt_key, bkt_cnt, bkt_off, bkt_tmp, bkt_rec2;   // bucketed node insert (k_bkt_*)
   gcz_host::DevBuf dl_pw, dl_rec, dl_idrec, dl_cnt, dl_off, dl_fpg, dl_fb, dl_wpre, dl_desc, dl_fl, dl_fo;   // dense leaf level
   gcz_host::DevBuf dl_lh, dl_pb, dl_pbs, dl_lower, dl_pos, dl_list, dl_gid, dl_recv, dl_stage, dl_seg;   // ... multi-rank
   gcz_dev::DensePlan dl_plan{};
@@ -193,6 +193,7 @@ struct gcz_ctx {
   int predup_mode = 0;       // node-insert LDS pre-dedupe: 0 auto, 1 on, 2 off  (GCZ_PREDUP)
   bool use_bucket = true;    // bucketed LDS node insert on non-repetitive data  (GCZ_BUCKET=0 disables)
   gcz_host::u64 bucket_min = 1ull << 20;   // ... on levels of at least this many pairs (GCZ_BUCKET_MIN)
+  bool two_pass = true;      // ... as the two-pass partition where records fit (GCZ_BUCKET_TWO=0: one pass)
   bool bucket_now = true;    // this build (cleared after a bucket overflow: rebuild with the table)
   int dense_mode = 1;        // dense leaf level (gcz_dense.h): 0 off, 1 on large pure-ACGT inputs, 2 any size (GCZ_DENSE)
   gcz_host::u64 dense_min = 1ull << 21;   // ... from this many strands (mode 1)

@@ -20,15 +20,16 @@
 //      never loops,
 //   4. a byte-parallel copy: each block stages the line boundaries of its
 //      2 KiB input window in LDS and every byte finds its line there.
-#include <hipcub/hipcub.hpp>
-
+// The compaction and the scans are one reduce-then-scan scheme (k_rts_*): tile
+// reductions, one workgroup scanning the tile values, and a pass that rescans
+// every tile from its carry and hands each element its prefix.
 #include "gcz_ctx.h"
 
 using namespace gcz_dev;
 using namespace gcz_host;
 
 struct gcz_ingest_state {
-  DevBuf nlpos, nsel, lastnm, len, off, tmp, bases, cut, forced, ev;
+  DevBuf nlpos, nsel, lastnm, len, off, tmp, bases, cut, forced, ev;   // tmp: tile values + carries
 };
 
 void gcz_ingest_state_free(gcz_ctx* c) {
@@ -45,14 +46,114 @@ namespace {
 
 constexpr int kWin = 2048;   // input bytes per copy block (LDS: 2 x 16 KiB line tables)
 
-struct IsNewline {
-  const unsigned char* f;
-  __device__ __forceinline__ bool operator()(const u64& i) const { return f[i] == '\n'; }
+// ---- reduce-then-scan over u64 values (Op: Sum or Max) ----
+constexpr int kRtsThreads = 1024;
+constexpr int kRtsItems = 16;
+constexpr u64 kRtsTile = u64(kRtsThreads) * kRtsItems;
+
+struct OpSum {
+  static __device__ __forceinline__ long long id() { return 0; }
+  static __device__ __forceinline__ long long op(long long a, long long b) { return a + b; }
+};
+struct OpMax {
+  static __device__ __forceinline__ long long id() { return -1; }
+  static __device__ __forceinline__ long long op(long long a, long long b) { return a > b ? a : b; }
 };
 
-struct NewlineCount {
+// exclusive block scan of one value per thread; *total = the block's reduction
+template <class Op>
+__device__ __forceinline__ long long block_excl(long long v, long long* s_w, long long* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  long long inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc = Op::op(inc, y);
+  }
+  if (lane == 63) s_w[wave] = inc;
+  __syncthreads();
+  long long pre = Op::id();
+  for (int w = 0; w < wave; ++w) pre = Op::op(pre, s_w[w]);
+  long long tot = Op::id();
+  for (int w = 0; w < kRtsThreads / 64; ++w) tot = Op::op(tot, s_w[w]);
+  __syncthreads();
+  *total = tot;
+  long long ex = __shfl_up(inc, 1, 64);
+  if (lane == 0) ex = Op::id();
+  return Op::op(pre, ex);
+}
+
+// thread t of a tile holds kRtsItems consecutive elements
+template <class In, class Op>
+__global__ __launch_bounds__(kRtsThreads) void k_rts_reduce(In in, u64 n, long long* __restrict__ part) {
+  __shared__ long long s_w[kRtsThreads / 64];
+  const u64 i0 = u64(blockIdx.x) * kRtsTile + u64(threadIdx.x) * kRtsItems;
+  long long v = Op::id();
+  for (int e = 0; e < kRtsItems; ++e)
+    if (i0 + e < n) v = Op::op(v, in(i0 + e));
+  long long tot;
+  (void)block_excl<Op>(v, s_w, &tot);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+// one workgroup: part[t] -> exclusive carry[t], carry[nt] = the total
+template <class Op>
+__global__ __launch_bounds__(kRtsThreads) void k_rts_carry(const long long* __restrict__ part, u64 nt,
+                                                           long long* __restrict__ carry) {
+  __shared__ long long s_w[kRtsThreads / 64];
+  long long run = Op::id();
+  for (u64 b = 0; b < nt; b += kRtsThreads) {
+    const u64 t = b + threadIdx.x;
+    long long tot;
+    const long long ex = block_excl<Op>(t < nt ? part[t] : Op::id(), s_w, &tot);
+    if (t < nt) carry[t] = Op::op(run, ex);
+    run = Op::op(run, tot);
+  }
+  if (threadIdx.x == 0) carry[nt] = run;
+}
+
+// sink(i, exclusive prefix, value) for every element
+template <class In, class Op, class Sink>
+__global__ __launch_bounds__(kRtsThreads) void k_rts_apply(In in, u64 n, const long long* __restrict__ carry,
+                                                           Sink sink) {
+  __shared__ long long s_w[kRtsThreads / 64];
+  const u64 i0 = u64(blockIdx.x) * kRtsTile + u64(threadIdx.x) * kRtsItems;
+  long long v[kRtsItems];
+  long long agg = Op::id();
+  for (int e = 0; e < kRtsItems; ++e) {
+    v[e] = i0 + e < n ? in(i0 + e) : Op::id();
+    agg = Op::op(agg, v[e]);
+  }
+  long long tot;
+  long long run = Op::op(carry[blockIdx.x], block_excl<Op>(agg, s_w, &tot));
+  for (int e = 0; e < kRtsItems; ++e) {
+    if (i0 + e >= n) break;
+    sink(i0 + e, run, v[e]);
+    run = Op::op(run, v[e]);
+  }
+}
+
+struct NewlineFlag {
   const unsigned char* f;
-  __device__ __forceinline__ u64 operator()(const u64& i) const { return f[i] == '\n' ? 1 : 0; }
+  __device__ __forceinline__ long long operator()(u64 i) const { return f[i] == '\n' ? 1 : 0; }
+};
+struct NewlineSink {   // compaction: newline number -> byte position
+  u64* nl;
+  __device__ __forceinline__ void operator()(u64 i, long long pre, long long v) const {
+    if (v) nl[pre] = i;
+  }
+};
+struct U64In {
+  const u64* a;
+  __device__ __forceinline__ long long operator()(u64 i) const { return (long long)a[i]; }
+};
+struct ExclSink {
+  u64* out;
+  __device__ __forceinline__ void operator()(u64 i, long long pre, long long) const { out[i] = u64(pre); }
+};
+struct InclMaxSink {
+  long long* out;
+  __device__ __forceinline__ void operator()(u64 i, long long pre, long long v) const { out[i] = pre > v ? pre : v; }
 };
 
 // Line i spans [st, en): st = 0 or one past newline i-1, en = newline i or n.
@@ -76,11 +177,7 @@ struct Lines {
 // value for the max-scan: own index for a data-by-content line, -1 for a marker line
 struct NonMarkerIndex {
   Lines ln;
-  __device__ __forceinline__ long long operator()(const u64& i) const { return ln.marker(i) ? -1ll : (long long)i; }
-};
-
-struct MaxOp {
-  __device__ __forceinline__ long long operator()(const long long& a, const long long& b) const { return a > b ? a : b; }
+  __device__ __forceinline__ long long operator()(u64 i) const { return ln.marker(i) ? -1ll : (long long)i; }
 };
 
 __device__ __forceinline__ bool skipped(const Lines& ln, const long long* lastnm, u64 i) {
@@ -205,51 +302,52 @@ int gcz_fasta_extract_on_device(gcz_ctx* c, const unsigned char* d_file, u64 n, 
   *d_bases = s.bases.as<unsigned char>();
   if (n == 0) return GCZ_OK;
   const u64 cap = gcz::reader_buffer_bytes(n, Lleaf, buffer_strands);
+  // reduce-then-scan of m elements: tile values and carries in s.tmp
+  auto rts_tiles = [](u64 m) { return std::max<u64>(1, (m + kRtsTile - 1) / kRtsTile); };
+  const u64 ntmax = rts_tiles(n + 1);   // bytes, or lines (<= n + 1)
+  if ((rc = c->ensure(s.tmp, (2 * ntmax + 2) * 8 + 16))) return rc;
+  long long* part = s.tmp.as<long long>();
+  long long* carry = part + ntmax;
   // 1. newline positions (counted first, so the position array is exact)
-  hipcub::CountingInputIterator<u64> idx(0);
-  hipcub::TransformInputIterator<u64, NewlineCount, hipcub::CountingInputIterator<u64>> isnl(idx,
-                                                                                           NewlineCount{d_file});
-  size_t tmp_bytes = 0;
-  I_HIP(hipcub::DeviceReduce::Sum(nullptr, tmp_bytes, isnl, s.nsel.as<u64>(), n, c->stream));
-  if ((rc = c->ensure(s.tmp, tmp_bytes + 16))) return rc;
-  I_HIP(hipcub::DeviceReduce::Sum(s.tmp.ptr, tmp_bytes, isnl, s.nsel.as<u64>(), n, c->stream));
-  u64 nnl0 = 0;
-  I_HIP(hipMemcpyAsync(&nnl0, s.nsel.ptr, 8, hipMemcpyDeviceToHost, c->stream));
-  I_HIP(hipStreamSynchronize(c->stream));
-  if ((rc = c->ensure(s.nlpos, nnl0 * 8 + 16))) return rc;
-  tmp_bytes = 0;
-  I_HIP(hipcub::DeviceSelect::If(nullptr, tmp_bytes, idx, s.nlpos.as<u64>(), s.nsel.as<u64>(), n,
-                                 IsNewline{d_file}, c->stream));
-  if ((rc = c->ensure(s.tmp, tmp_bytes + 16))) return rc;
-  I_HIP(hipcub::DeviceSelect::If(s.tmp.ptr, tmp_bytes, idx, s.nlpos.as<u64>(), s.nsel.as<u64>(), n,
-                                 IsNewline{d_file}, c->stream));
+  {
+    const u64 nt = rts_tiles(n);
+    hipLaunchKernelGGL((k_rts_reduce<NewlineFlag, OpSum>), dim3(unsigned(nt)), dim3(kRtsThreads), 0, c->stream,
+                       NewlineFlag{d_file}, n, part);
+    hipLaunchKernelGGL((k_rts_carry<OpSum>), dim3(1), dim3(kRtsThreads), 0, c->stream, part, nt, carry);
+    I_HIP(hipGetLastError());
+  }
   u64 nnl = 0;
   unsigned char last = 0;
-  I_HIP(hipMemcpyAsync(&nnl, s.nsel.ptr, 8, hipMemcpyDeviceToHost, c->stream));
+  I_HIP(hipMemcpyAsync(&nnl, carry + rts_tiles(n), 8, hipMemcpyDeviceToHost, c->stream));
   I_HIP(hipMemcpyAsync(&last, d_file + n - 1, 1, hipMemcpyDeviceToHost, c->stream));
   I_HIP(hipStreamSynchronize(c->stream));
+  if ((rc = c->ensure(s.nlpos, nnl * 8 + 16))) return rc;
+  hipLaunchKernelGGL((k_rts_apply<NewlineFlag, OpSum, NewlineSink>), dim3(unsigned(rts_tiles(n))),
+                     dim3(kRtsThreads), 0, c->stream, NewlineFlag{d_file}, n, carry, NewlineSink{s.nlpos.as<u64>()});
+  I_HIP(hipGetLastError());
   Lines ln{d_file, s.nlpos.as<u64>(), nnl, n, nnl + (last != '\n' ? 1 : 0), nullptr, nullptr};
   const u64 L = ln.nlines;
   if ((rc = c->ensure(s.lastnm, L * 8 + 16)) || (rc = c->ensure(s.len, L * 8 + 16)) ||
       (rc = c->ensure(s.off, L * 8 + 16)))
     return rc;
+  const u64 ntl = rts_tiles(L);
   u64 total = 0;
   for (u64 k0 = 1;;) {
-    // 2. skip / data per line, output offsets
-    hipcub::TransformInputIterator<long long, NonMarkerIndex, hipcub::CountingInputIterator<u64>> nm(
-        idx, NonMarkerIndex{ln});
-    tmp_bytes = 0;
-    I_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tmp_bytes, nm, s.lastnm.as<long long>(), MaxOp{}, L,
-                                            c->stream));
-    if ((rc = c->ensure(s.tmp, tmp_bytes + 16))) return rc;
-    I_HIP(hipcub::DeviceScan::InclusiveScan(s.tmp.ptr, tmp_bytes, nm, s.lastnm.as<long long>(), MaxOp{}, L,
-                                            c->stream));
+    // 2. skip / data per line (the last non-marker line: an inclusive max-scan), output offsets
+    hipLaunchKernelGGL((k_rts_reduce<NonMarkerIndex, OpMax>), dim3(unsigned(ntl)), dim3(kRtsThreads), 0, c->stream,
+                       NonMarkerIndex{ln}, L, part);
+    hipLaunchKernelGGL((k_rts_carry<OpMax>), dim3(1), dim3(kRtsThreads), 0, c->stream, part, ntl, carry);
+    hipLaunchKernelGGL((k_rts_apply<NonMarkerIndex, OpMax, InclMaxSink>), dim3(unsigned(ntl)), dim3(kRtsThreads), 0,
+                       c->stream, NonMarkerIndex{ln}, L, carry, InclMaxSink{s.lastnm.as<long long>()});
+    I_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_line_len, grid_of(L), dim3(kBlock), 0, c->stream, ln, s.lastnm.as<long long>(),
                        s.len.as<u64>());
-    tmp_bytes = 0;
-    I_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, s.len.as<u64>(), s.off.as<u64>(), L, c->stream));
-    if ((rc = c->ensure(s.tmp, tmp_bytes + 16))) return rc;
-    I_HIP(hipcub::DeviceScan::ExclusiveSum(s.tmp.ptr, tmp_bytes, s.len.as<u64>(), s.off.as<u64>(), L, c->stream));
+    hipLaunchKernelGGL((k_rts_reduce<U64In, OpSum>), dim3(unsigned(ntl)), dim3(kRtsThreads), 0, c->stream,
+                       U64In{s.len.as<u64>()}, L, part);
+    hipLaunchKernelGGL((k_rts_carry<OpSum>), dim3(1), dim3(kRtsThreads), 0, c->stream, part, ntl, carry);
+    hipLaunchKernelGGL((k_rts_apply<U64In, OpSum, ExclSink>), dim3(unsigned(ntl)), dim3(kRtsThreads), 0, c->stream,
+                       U64In{s.len.as<u64>()}, L, carry, ExclSink{s.off.as<u64>()});
+    I_HIP(hipGetLastError());
     u64 tail[2] = {0, 0};
     I_HIP(hipMemcpyAsync(&tail[0], s.off.as<u64>() + L - 1, 8, hipMemcpyDeviceToHost, c->stream));
     I_HIP(hipMemcpyAsync(&tail[1], s.len.as<u64>() + L - 1, 8, hipMemcpyDeviceToHost, c->stream));

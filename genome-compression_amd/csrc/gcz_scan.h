@@ -1,6 +1,8 @@
 // Single-pass exclusive prefix sum of u32 values (decoupled look-back), the
-// scan every bucketed pass of the build uses (bucket-major count matrices,
-// popcount prefixes of first-occurrence bitmaps).  Replaces the rocPRIM scan.
+// scan every bucketed pass of the build and of the ratio path uses (bucket-major
+// count matrices, popcount prefixes of first-occurrence bitmaps, .dag byte
+// offsets).  Replaces the rocPRIM scan.  Out = u32, or u64 when the total may
+// pass 2^32 (a tile's own sum, kScanTile values, must fit 32 bits).
 //
 // One launch: a tile of kScanItems x 256 elements per workgroup, tiles taken
 // in ticket order (so every predecessor is resident and the look-back cannot
@@ -22,8 +24,8 @@ constexpr u64 kScanTile = u64(kScanThreads) * kScanItems;   // 16 Ki elements (a
 __host__ __device__ inline u64 scan_tiles(u64 n) { return (n + kScanTile - 1) / kScanTile; }
 
 // In: u32 operator()(u64 i) const for i < n.
-template <class In>
-__global__ __launch_bounds__(kScanThreads) void k_scan_excl(In in, u64 n, u32* __restrict__ out,
+template <class In, class Out = u32>
+__global__ __launch_bounds__(kScanThreads) void k_scan_excl(In in, u64 n, Out* __restrict__ out,
                                                            u64* __restrict__ desc, u32* __restrict__ ticket,
                                                            u64* __restrict__ total) {
   __shared__ u32 s_tile;
@@ -95,8 +97,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_excl(In in, u64 n, u32* _
     }
   }
   __syncthreads();
-  u32 run = u32(s_prefix) + incl - sum;
+  u32 run = incl - sum;   // tile-local; the tile prefix is added at the store
   for (int w = 0; w < wave; ++w) run += s_wave[w];
+  const Out tprefix = Out(s_prefix);
   __syncthreads();   // (every thread has read its items)
 #pragma unroll
   for (int e = 0; e < kScanItems; ++e) {   // exclusive prefixes back through LDS, stored coalesced
@@ -108,7 +111,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_excl(In in, u64 n, u32* _
   for (int e = 0; e < kScanItems; ++e) {
     const u32 j = u32(e) * kScanThreads + tid;
     const u64 i = t0 + j;
-    if (i < n) out[i] = s_tr[j + (j >> 4)];
+    if (i < n) out[i] = tprefix + Out(s_tr[j + (j >> 4)]);
   }
 }
 

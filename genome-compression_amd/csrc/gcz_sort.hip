@@ -7,29 +7,38 @@
 // 0..D-2) is permuted independently by the reference counts its parent layer
 // holds, descending, ties by the old index (std::stable_sort); parents are
 // rewired with the m/t/v bits kept; the top layer and the root stay.  On the
-// device: one histogram pass per parent layer (atomicAdd), per child layer a
-// stable descending radix sort of (count, index) over the count's bits only
-// (skipped when every count is equal: the order is then the identity), one
-// gather/scatter pass that rewires and permutes every node layer at once.
+// device:
+//  * histogram per parent layer: a large layer that references each child many
+//    times (the leaves) is partitioned by child-id range (2^15 ids per bucket: count
+//    matrix, look-back scan, a scatter of 2-B records) and every bucket is counted by
+//    one workgroup in LDS, which also reduces the layer's min / max count; other
+//    layers count with global atomics (their references come in near id order);
+//  * per child layer whose counts are not all equal (else the order is the
+//    identity), a stable LSD counting sort of (hi - count) in passes of <= 8 bits:
+//    per-tile digit counts, a scan, and a scatter whose in-tile ranks come from
+//    wave ballots (a match mask per digit, so equal digits keep their order); the
+//    last pass writes each element's new position directly;
+//  * one pass over every node layer that rewires children and permutes the layer.
 // The .dag is written by an exclusive scan of per-node byte sizes and one
 // byte-scatter pass.
-#include <hipcub/hipcub.hpp>
-
 #include "gcz_ctx.h"
+#include "gcz_scan.h"
 
 using namespace gcz_dev;
 using namespace gcz_host;
 
 struct gcz_sort_state {
-  DevBuf cnt, keys2, vals, vals2, newpos, mm, tmp, sizes, pos, acc, dag, nodes2, leaves2, dw1, dw2, text;
+  DevBuf cnt, keys, keys2, vals, vals2, newpos, mm, tmp, sizes, pos, acc, dag, nodes2, leaves2, dw1, dw2, text;
+  DevBuf hmat, hoff, hrec, desc;   // partitioned histogram; scan descriptors
   u32* h_mm = nullptr;
 };
 
 void gcz_sort_state_free(gcz_ctx* c) {
   gcz_sort_state* s = c->sortst;
   if (!s) return;
-  for (DevBuf* b : {&s->cnt, &s->keys2, &s->vals, &s->vals2, &s->newpos, &s->mm, &s->tmp, &s->sizes, &s->pos,
-                    &s->acc, &s->dag, &s->nodes2, &s->leaves2, &s->dw1, &s->dw2, &s->text})
+  for (DevBuf* b : {&s->cnt, &s->keys, &s->keys2, &s->vals, &s->vals2, &s->newpos, &s->mm, &s->tmp, &s->sizes,
+                    &s->pos, &s->acc, &s->dag, &s->nodes2, &s->leaves2, &s->dw1, &s->dw2, &s->text, &s->hmat,
+                    &s->hoff, &s->hrec, &s->desc})
     if (b->ptr) (void)hipFree(b->ptr);
   if (s->h_mm) (void)hipHostFree(s->h_mm);
   delete s;
@@ -75,6 +84,180 @@ __global__ __launch_bounds__(kBlock) void k_hist(const u32* __restrict__ parent,
   if (!is_null(w)) atomicAdd(&cnt[w & kIdx], 1u);
 }
 
+// ---- partitioned histogram (parent layers of >= 2^20 words) ----
+// Buckets of 2^kHB child ids; chunks of kHChunk parent words (one count-matrix
+// column each, dealt to XCDs in contiguous runs like the build's bucket chunks).
+constexpr int kHThreads = 1024;
+constexpr int kHItems = 64;
+constexpr u64 kHChunk = u64(kHThreads) * kHItems;
+constexpr u32 kHB = 15;                 // ids per bucket: 2^15 (LDS counters, 128 KB)
+constexpr u32 kHMaxBuckets = 4096;      // child layers of <= 2^27 nodes (LDS cursors, 16 KB)
+
+__device__ __forceinline__ u64 h_chunk(u64 G) {
+  const u64 b = blockIdx.x, per = G / 8;
+  return b < 8 * per ? (b % 8) * per + b / 8 : b;
+}
+
+__global__ __launch_bounds__(kHThreads) void k_hcount(const u32* __restrict__ words, u64 nw, u32 nb, u64 G,
+                                                      u32* __restrict__ mat) {
+  __shared__ u32 hist[kHMaxBuckets];
+  for (u32 q = threadIdx.x; q < nb; q += kHThreads) hist[q] = 0;
+  __syncthreads();
+  const u64 g = h_chunk(G), j0 = g * kHChunk;
+#pragma unroll 8
+  for (int e = 0; e < kHItems; ++e) {
+    const u64 j = j0 + u64(e) * kHThreads + threadIdx.x;
+    if (j >= nw) break;
+    const u32 w = words[j];
+    if (!is_null(w)) atomicAdd(&hist[(w & kIdx) >> kHB], 1u);
+  }
+  __syncthreads();
+  for (u32 q = threadIdx.x; q < nb; q += kHThreads) mat[u64(q) * G + g] = hist[q];
+}
+
+__global__ __launch_bounds__(kHThreads) void k_hscatter(const u32* __restrict__ words, u64 nw, u32 nb, u64 G,
+                                                        const u32* __restrict__ off,
+                                                        unsigned short* __restrict__ rec) {
+  __shared__ u32 cur[kHMaxBuckets];
+  const u64 g = h_chunk(G), j0 = g * kHChunk;
+  for (u32 q = threadIdx.x; q < nb; q += kHThreads) cur[q] = off[u64(q) * G + g];
+  __syncthreads();
+#pragma unroll 8
+  for (int e = 0; e < kHItems; ++e) {
+    const u64 j = j0 + u64(e) * kHThreads + threadIdx.x;
+    if (j >= nw) break;
+    const u32 w = words[j];
+    if (is_null(w)) continue;
+    const u32 id = w & kIdx;
+    const u32 d = atomicAdd(&cur[id >> kHB], 1u);
+    rec[d] = (unsigned short)(id & ((1u << kHB) - 1));
+  }
+}
+
+// One workgroup per bucket: LDS counters for its 2^kHB ids, written coalesced, and
+// the block's min / max folded into mm[0..1].
+__global__ __launch_bounds__(kHThreads) void k_hbucket(const unsigned short* __restrict__ rec,
+                                                       const u32* __restrict__ off, u64 G, u64 nc,
+                                                       u32* __restrict__ cnt, u32* __restrict__ mm) {
+  extern __shared__ u32 c32[];   // 2^kHB counters (dynamic: 128 KB)
+  __shared__ u32 smin[kHThreads / 64], smax[kHThreads / 64];
+  const u64 b = blockIdx.x;
+  for (u32 q = threadIdx.x; q < (1u << kHB); q += kHThreads) c32[q] = 0;
+  __syncthreads();
+  const u32 r0 = off[b * G], r1 = off[(b + 1) * G];
+  for (u32 i = r0 + threadIdx.x; i < r1; i += kHThreads) atomicAdd(&c32[rec[i]], 1u);
+  __syncthreads();
+  u32 lo = ~0u, hi = 0;
+  const u64 id0 = b << kHB;
+  for (u32 q = threadIdx.x; q < (1u << kHB); q += kHThreads) {
+    if (id0 + q >= nc) break;
+    const u32 v = c32[q];
+    cnt[id0 + q] = v;
+    lo = min(lo, v);
+    hi = max(hi, v);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, u32(__shfl_xor(int(lo), o, 64)));
+    hi = max(hi, u32(__shfl_xor(int(hi), o, 64)));
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) { smin[wave] = lo; smax[wave] = hi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kHThreads / 64; ++w) { lo = min(lo, smin[w]); hi = max(hi, smax[w]); }
+    atomicMin(&mm[0], lo);
+    atomicMax(&mm[1], hi);
+  }
+}
+
+// ---- stable counting sort by count, descending (LSD passes of <= 8 bits) ----
+// key = hi - count (ascending order <=> descending counts); a tile of kCsTile
+// elements, each wave taking 1024 consecutive ones (item e of lane l: element
+// e * 64 + l, in order), so ranks follow positions.
+constexpr int kCsThreads = 256;
+constexpr int kCsItems = 16;
+constexpr u64 kCsWaveSpan = 64 * kCsItems;
+constexpr u64 kCsTile = u64(kCsThreads) * kCsItems;
+
+struct CsPass {
+  const u32* cnt;      // first pass: counts (key = hi - cnt[i], value = i)
+  const u32* keys;     // later passes: keys / values of the previous pass
+  const u32* vals;
+  u32 hi;
+  u32 shift, bits;     // digit = (key >> shift) & (2^bits - 1)
+  u64 n;
+  __device__ __forceinline__ u32 key(u64 i) const { return cnt ? hi - cnt[i] : keys[i]; }
+  __device__ __forceinline__ u32 val(u64 i) const { return cnt ? u32(i) : vals[i]; }
+  __device__ __forceinline__ u32 digit(u32 k) const { return (k >> shift) & ((1u << bits) - 1u); }
+};
+
+__global__ __launch_bounds__(kCsThreads) void k_cs_count(CsPass P, u64 ntiles, u32* __restrict__ mat) {
+  __shared__ u32 hist[256];
+  const u32 R = 1u << P.bits;
+  for (u32 q = threadIdx.x; q < R; q += kCsThreads) hist[q] = 0;
+  __syncthreads();
+  const u64 t = blockIdx.x, i0 = t * kCsTile;
+#pragma unroll
+  for (int e = 0; e < kCsItems; ++e) {
+    const u64 i = i0 + u64(e) * kCsThreads + threadIdx.x;
+    if (i < P.n) atomicAdd(&hist[P.digit(P.key(i))], 1u);
+  }
+  __syncthreads();
+  for (u32 q = threadIdx.x; q < R; q += kCsThreads) mat[u64(q) * ntiles + t] = hist[q];
+}
+
+// off = exclusive scan of the digit-major matrix.  last pass: newpos[value] = rank;
+// else keys_out / vals_out at the rank.
+__global__ __launch_bounds__(kCsThreads) void k_cs_scatter(CsPass P, u64 ntiles, const u32* __restrict__ off,
+                                                           u32* __restrict__ keys_out, u32* __restrict__ vals_out,
+                                                           u32* __restrict__ newpos) {
+  __shared__ u32 wc[kCsThreads / 64][256];
+  const u32 R = 1u << P.bits;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (u32 q = threadIdx.x; q < R * (kCsThreads / 64); q += kCsThreads) wc[q / R][q % R] = 0;
+  __syncthreads();
+  const u64 t = blockIdx.x;
+  const u64 w0 = t * kCsTile + u64(wave) * kCsWaveSpan;
+  const u64 lt = (1ull << lane) - 1;
+  u32 key[kCsItems], rank[kCsItems];
+#pragma unroll
+  for (int e = 0; e < kCsItems; ++e) {
+    const u64 i = w0 + u64(e) * 64 + lane;
+    const bool ok = i < P.n;
+    key[e] = ok ? P.key(i) : 0u;
+    const u32 d = P.digit(key[e]);
+    u64 m = __ballot(ok);
+    for (u32 b = 0; b < P.bits; ++b) {
+      const u64 bal = __ballot((d >> b) & 1u);
+      m &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    const u32 base = ok ? wc[wave][d] : 0u;
+    rank[e] = base + u32(__popcll(m & lt));
+    if (ok && (m & lt) == 0) wc[wave][d] = base + u32(__popcll(m));   // the lowest lane of the match
+  }
+  __syncthreads();
+  for (u32 q = threadIdx.x; q < R; q += kCsThreads) {   // exclusive prefix over the waves, per digit
+    u32 run = off[u64(q) * ntiles + t];
+    for (int w = 0; w < kCsThreads / 64; ++w) {
+      const u32 v = wc[w][q];
+      wc[w][q] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < kCsItems; ++e) {
+    const u64 i = w0 + u64(e) * 64 + lane;
+    if (i >= P.n) continue;
+    const u32 dst = wc[wave][P.digit(key[e])] + rank[e];
+    if (newpos) newpos[P.val(i)] = dst;
+    else {
+      keys_out[dst] = key[e];
+      vals_out[dst] = P.val(i);
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_minmax(const u32* __restrict__ cnt, u64 n, u32* __restrict__ mm) {
   __shared__ u32 smin[kBlock / 64], smax[kBlock / 64];
   u32 lo = ~0u, hi = 0;
@@ -101,36 +284,36 @@ __global__ void k_mm_init(u32* mm, int D) {
   for (int i = threadIdx.x; i < D; i += blockDim.x) { mm[2 * i] = ~0u; mm[2 * i + 1] = 0u; }
 }
 
-__global__ __launch_bounds__(kBlock) void k_iota(u32* __restrict__ v, u64 n) {
-  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (i < n) v[i] = u32(i);
-}
-
-// invert_indices (src/shared_tree.cpp:360-365): newpos[old] = new
-__global__ __launch_bounds__(kBlock) void k_invert(const u32* __restrict__ sorted_old, u64 n,
-                                                   u32* __restrict__ newpos) {
-  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (i < n) newpos[sorted_old[i]] = u32(i);
-}
-
 __global__ __launch_bounds__(kBlock) void k_perm_leaves(const u64* __restrict__ in, u64 n,
                                                         const u32* __restrict__ newpos, u64* __restrict__ out) {
   const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (i < n) out[newpos[i]] = in[i];
 }
 
-// rewire_nodes (:383-403) with the child permutation, reorder_layer (:371-377) with the own one
-__global__ __launch_bounds__(kBlock) void k_perm_nodes(const uint2* __restrict__ in, u64 n,
-                                                       const u32* __restrict__ child_newpos,
-                                                       const u32* __restrict__ own_newpos, uint2* __restrict__ out) {
-  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (i >= n) return;
-  uint2 w = in[i];
-  if (child_newpos) {
-    if (!is_null(w.x)) w.x = (w.x & kBits) | child_newpos[w.x & kIdx];
-    if (!is_null(w.y)) w.y = (w.y & kBits) | child_newpos[w.y & kIdx];
+// rewire_nodes (:383-403) with the child permutation and reorder_layer (:371-377) with
+// the own one, for every node layer in one launch (storage slot g of layer k).
+struct PermPlan {
+  u64 node[GCZ_MAX_LAYERS + 1];     // storage start of each layer (+ the end)
+  u64 count[GCZ_MAX_LAYERS];
+  long long child[GCZ_MAX_LAYERS];  // offset of the child layer's newpos, -1: identity
+  long long own[GCZ_MAX_LAYERS];    // offset of the layer's own newpos, -1: identity
+};
+
+__global__ __launch_bounds__(kBlock) void k_perm_nodes(const uint2* __restrict__ in, u64 N, int D, PermPlan pp,
+                                                       const u32* __restrict__ newpos, uint2* __restrict__ out) {
+  const u64 g = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (g >= N) return;
+  int k = 0;
+  while (k + 1 < D && g >= pp.node[k + 1]) ++k;
+  const u64 i = g - pp.node[k];
+  if (i >= pp.count[k]) return;
+  uint2 w = in[g];
+  if (pp.child[k] >= 0) {
+    const u32* cn = newpos + pp.child[k];
+    if (!is_null(w.x)) w.x = (w.x & kBits) | cn[w.x & kIdx];
+    if (!is_null(w.y)) w.y = (w.y & kBits) | cn[w.y & kIdx];
   }
-  out[own_newpos ? own_newpos[i] : i] = w;
+  out[pp.node[k] + (pp.own[k] >= 0 ? newpos[pp.own[k] + i] : i)] = w;
 }
 
 struct LayerStarts {
@@ -279,50 +462,113 @@ int gcz_sort_device(gcz_ctx* c) {
     n_of[cl] = cl == 0 ? nl : c->info.layer_size[cl - 1];
     coff[cl + 1] = coff[cl] + n_of[cl];
   }
-  u64 nmax = 0;
-  for (u64 v : n_of) nmax = std::max(nmax, v);
+  u64 nmax = 0, nwmax = 0, matmax = 0, tilemax = 0;
+  // per parent layer: partitioned histogram (nb buckets x G chunks) or global atomics (nb = 0)
+  std::vector<u32> hnb(D, 0);
+  std::vector<u64> hG(D, 0);
+  for (int cl = 0; cl < D; ++cl) {
+    nmax = std::max(nmax, n_of[cl]);
+    const u64 nw = 2 * c->info.layer_size[cl];
+    const u64 nb = (n_of[cl] + (1ull << kHB) - 1) >> kHB;
+    // partition when parents reference their children many times over in random order (the
+    // leaves: ~20 references each at 1 Gbase); a layer whose children are referenced about once
+    // is referenced in near position order (ids are first occurrences), where atomics coalesce
+    if (nw >= (1ull << 20) && nw >= 4 * n_of[cl] && nb >= 1 && nb <= kHMaxBuckets) {
+      hnb[cl] = u32(nb);
+      hG[cl] = (nw + kHChunk - 1) / kHChunk;
+      nwmax = std::max(nwmax, nw);
+      matmax = std::max(matmax, nb * hG[cl] + 1);
+    }
+  }
+  const u64 cs_tiles = (nmax + kCsTile - 1) / kCsTile;
+  matmax = std::max(matmax, 256 * cs_tiles + 1);
+  tilemax = scan_tiles(matmax);
   const u64 N = c->layer_off[D];
   int rc;
   if ((rc = c->ensure(s.cnt, coff[D] * 4 + 16)) || (rc = c->ensure(s.newpos, coff[D] * 4 + 16)) ||
-      (rc = c->ensure(s.keys2, nmax * 4 + 16)) || (rc = c->ensure(s.vals, nmax * 4 + 16)) ||
-      (rc = c->ensure(s.vals2, nmax * 4 + 16)) || (rc = c->ensure(s.mm, size_t(D) * 8 + 16)) ||
-      (rc = c->ensure(s.nodes2, N * 8 + 16)) || (rc = c->ensure(s.leaves2, nl * 8 + 16)))
+      (rc = c->ensure(s.keys, nmax * 4 + 16)) || (rc = c->ensure(s.keys2, nmax * 4 + 16)) ||
+      (rc = c->ensure(s.vals, nmax * 4 + 16)) || (rc = c->ensure(s.vals2, nmax * 4 + 16)) ||
+      (rc = c->ensure(s.mm, size_t(D) * 8 + 16)) || (rc = c->ensure(s.nodes2, N * 8 + 16)) ||
+      (rc = c->ensure(s.leaves2, nl * 8 + 16)) || (rc = c->ensure(s.hmat, matmax * 4 + 16)) ||
+      (rc = c->ensure(s.hoff, matmax * 4 + 16)) || (rc = c->ensure(s.hrec, nwmax * 2 + 16)) ||
+      (rc = c->ensure(s.desc, tilemax * 8 + 16)))
     return rc;
   if (!s.h_mm) S_HIP(hipHostMalloc((void**)&s.h_mm, size_t(GCZ_MAX_LAYERS) * 8, hipHostMallocDefault));
+  S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_hbucket), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            int((1u << kHB) * 4)));
   hipEvent_t e0{};
   c->prof_begin(KID_SORT, e0);
   u32* cnt = s.cnt.as<u32>();
   u32* mm = s.mm.as<u32>();
-  S_HIP(hipMemsetAsync(cnt, 0, coff[D] * 4, c->stream));
+  u32* mat = s.hmat.as<u32>();
+  u32* off = s.hoff.as<u32>();
+  u64* sdesc = s.desc.as<u64>();
+  // exclusive scan of m matrix entries (+ the total at off[m])
+  auto scan = [&](u64 m) -> int {
+    const u64 t = scan_tiles(m + 1);
+    S_HIP(hipMemsetAsync(sdesc, 0, t * 8 + 16, c->stream));
+    hipLaunchKernelGGL(k_scan_excl<ScanU32>, dim3(unsigned(t)), dim3(kScanThreads), 0, c->stream, ScanU32{mat, m},
+                       m + 1, off, sdesc, reinterpret_cast<u32*>(sdesc + t), static_cast<u64*>(nullptr));
+    S_HIP(hipGetLastError());
+    return GCZ_OK;
+  };
   hipLaunchKernelGGL(k_mm_init, dim3(1), dim3(64), 0, c->stream, mm, D);   // [min, max] per child layer
   const uint2* nodes = c->nodes_out.as<uint2>();
   for (int cl = 0; cl < D; ++cl) {
-    const u64 np = c->info.layer_size[cl];   // parent layer cl
-    hipLaunchKernelGGL(k_hist, grid_of(2 * np), dim3(kBlock), 0, c->stream,
-                       reinterpret_cast<const u32*>(nodes + c->layer_off[cl]), 2 * np, cnt + coff[cl]);
-    if (n_of[cl])
-      hipLaunchKernelGGL(k_minmax, dim3(unsigned(std::min<u64>(1024, (n_of[cl] + kBlock - 1) / kBlock))),
-                         dim3(kBlock), 0, c->stream, cnt + coff[cl], n_of[cl], mm + 2 * cl);
+    const u64 nw = 2 * c->info.layer_size[cl];   // words of parent layer cl
+    const u32* words = reinterpret_cast<const u32*>(nodes + c->layer_off[cl]);
+    if (hnb[cl]) {
+      const u32 nb = hnb[cl];
+      const u64 G = hG[cl];
+      hipLaunchKernelGGL(k_hcount, dim3(unsigned(G)), dim3(kHThreads), 0, c->stream, words, nw, nb, G, mat);
+      if ((rc = scan(u64(nb) * G))) return rc;
+      hipLaunchKernelGGL(k_hscatter, dim3(unsigned(G)), dim3(kHThreads), 0, c->stream, words, nw, nb, G, off,
+                         s.hrec.as<unsigned short>());
+      hipLaunchKernelGGL(k_hbucket, dim3(nb), dim3(kHThreads), (1u << kHB) * 4, c->stream,
+                         s.hrec.as<unsigned short>(), off, G, n_of[cl], cnt + coff[cl], mm + 2 * cl);
+    } else {
+      if (n_of[cl]) S_HIP(hipMemsetAsync(cnt + coff[cl], 0, n_of[cl] * 4, c->stream));
+      if (nw)
+        hipLaunchKernelGGL(k_hist, grid_of(nw), dim3(kBlock), 0, c->stream, words, nw, cnt + coff[cl]);
+      if (n_of[cl])
+        hipLaunchKernelGGL(k_minmax, dim3(unsigned(std::min<u64>(1024, (n_of[cl] + kBlock - 1) / kBlock))),
+                           dim3(kBlock), 0, c->stream, cnt + coff[cl], n_of[cl], mm + 2 * cl);
+    }
+    S_HIP(hipGetLastError());
   }
-  S_HIP(hipGetLastError());
   S_HIP(hipMemcpyAsync(s.h_mm, mm, size_t(D) * 8, hipMemcpyDeviceToHost, c->stream));
   S_HIP(hipStreamSynchronize(c->stream));
   std::vector<bool> ident(D);
   for (int cl = 0; cl < D; ++cl) ident[cl] = n_of[cl] <= 1 || s.h_mm[2 * cl] == s.h_mm[2 * cl + 1];
-  // stable descending sort of (count, index) per non-trivial child layer
+  // stable descending sort of (count, index) per non-trivial child layer: newpos[old] = new
   for (int cl = 0; cl < D; ++cl) {
     if (ident[cl]) continue;
     const u64 n = n_of[cl];
-    const int bits = std::max<int>(1, int(bit_width(s.h_mm[2 * cl + 1])));
-    hipLaunchKernelGGL(k_iota, grid_of(n), dim3(kBlock), 0, c->stream, s.vals.as<u32>(), n);
-    size_t tmp_bytes = 0;
-    S_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp_bytes, cnt + coff[cl], s.keys2.as<u32>(),
-                                                       s.vals.as<u32>(), s.vals2.as<u32>(), n, 0, bits, c->stream));
-    if ((rc = c->ensure(s.tmp, tmp_bytes + 16))) return rc;
-    S_HIP(hipcub::DeviceRadixSort::SortPairsDescending(s.tmp.ptr, tmp_bytes, cnt + coff[cl], s.keys2.as<u32>(),
-                                                       s.vals.as<u32>(), s.vals2.as<u32>(), n, 0, bits, c->stream));
-    hipLaunchKernelGGL(k_invert, grid_of(n), dim3(kBlock), 0, c->stream, s.vals2.as<u32>(), n,
-                       s.newpos.as<u32>() + coff[cl]);
+    const u32 lo = s.h_mm[2 * cl], hi = s.h_mm[2 * cl + 1];
+    const u32 bits = bit_width(u64(hi - lo));
+    const u32 npass = (bits + 7) / 8, db = (bits + npass - 1) / npass;
+    const u64 nt = (n + kCsTile - 1) / kCsTile;
+    u32 *kin = nullptr, *vin = nullptr, *kout = s.keys.as<u32>(), *vout = s.vals.as<u32>();
+    for (u32 ps = 0; ps < npass; ++ps) {
+      CsPass P{};
+      P.cnt = ps == 0 ? cnt + coff[cl] : nullptr;
+      P.keys = kin;
+      P.vals = vin;
+      P.hi = hi;
+      P.shift = ps * db;
+      P.bits = std::min(db, bits - ps * db);
+      P.n = n;
+      hipLaunchKernelGGL(k_cs_count, dim3(unsigned(nt)), dim3(kCsThreads), 0, c->stream, P, nt, mat);
+      if ((rc = scan(u64(1u << P.bits) * nt))) return rc;
+      const bool last = ps + 1 == npass;
+      hipLaunchKernelGGL(k_cs_scatter, dim3(unsigned(nt)), dim3(kCsThreads), 0, c->stream, P, nt, off, kout, vout,
+                         last ? s.newpos.as<u32>() + coff[cl] : nullptr);
+      S_HIP(hipGetLastError());
+      kin = kout;
+      vin = vout;
+      kout = kout == s.keys.as<u32>() ? s.keys2.as<u32>() : s.keys.as<u32>();
+      vout = vout == s.vals.as<u32>() ? s.vals2.as<u32>() : s.vals.as<u32>();
+    }
   }
   // apply: leaves, then every node layer (rewire children, permute itself)
   if (!ident[0] && nl) {
@@ -330,13 +576,15 @@ int gcz_sort_device(gcz_ctx* c) {
                        s.newpos.as<u32>(), s.leaves2.as<u64>());
     std::swap(c->leaves_out, s.leaves2);
   }
+  PermPlan pp{};
+  for (int k = 0; k <= D; ++k) pp.node[k] = c->layer_off[k];
   for (int k = 0; k < D; ++k) {
-    const u64 n = c->info.layer_size[k];
-    const u32* child = ident[k] ? nullptr : s.newpos.as<u32>() + coff[k];
-    const u32* own = (k + 1 < D && !ident[k + 1]) ? s.newpos.as<u32>() + coff[k + 1] : nullptr;
-    hipLaunchKernelGGL(k_perm_nodes, grid_of(n), dim3(kBlock), 0, c->stream, nodes + c->layer_off[k], n, child, own,
-                       s.nodes2.as<uint2>() + c->layer_off[k]);
+    pp.count[k] = c->info.layer_size[k];
+    pp.child[k] = ident[k] ? -1 : (long long)coff[k];
+    pp.own[k] = (k + 1 < D && !ident[k + 1]) ? (long long)coff[k + 1] : -1;
   }
+  hipLaunchKernelGGL(k_perm_nodes, grid_of(N), dim3(kBlock), 0, c->stream, nodes, N, D, pp, s.newpos.as<u32>(),
+                     s.nodes2.as<uint2>());
   S_HIP(hipGetLastError());
   std::swap(c->nodes_out, s.nodes2);
   c->prof_end(KID_SORT, e0);
@@ -385,10 +633,13 @@ static int serialize_on_device(gcz_ctx* c, unsigned char** d_dag, uint64_t* writ
   const LayerStarts ls = layer_starts(c);
   hipLaunchKernelGGL(k_node_sizes, grid_of(N), dim3(kBlock), 0, c->stream, c->nodes_out.as<uint2>(), N, ls, D,
                      s.sizes.as<u32>(), s.acc.as<unsigned long long>());
-  size_t tmp_bytes = 0;
-  S_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, s.sizes.as<u32>(), s.pos.as<u64>(), N, c->stream));
-  if ((rc = c->ensure(s.tmp, tmp_bytes + 16))) return rc;
-  S_HIP(hipcub::DeviceScan::ExclusiveSum(s.tmp.ptr, tmp_bytes, s.sizes.as<u32>(), s.pos.as<u64>(), N, c->stream));
+  const u64 t = scan_tiles(N);   // u64 byte offsets (tile sums <= 8 * kScanTile)
+  if ((rc = c->ensure(s.desc, std::max<u64>(s.desc.bytes, t * 8 + 16)))) return rc;
+  S_HIP(hipMemsetAsync(s.desc.ptr, 0, t * 8 + 16, c->stream));
+  hipLaunchKernelGGL((k_scan_excl<ScanU32, u64>), dim3(unsigned(std::max<u64>(t, 1))), dim3(kScanThreads), 0,
+                     c->stream, ScanU32{s.sizes.as<u32>(), N}, N, s.pos.as<u64>(), s.desc.as<u64>(),
+                     reinterpret_cast<u32*>(s.desc.as<u64>() + t), static_cast<u64*>(nullptr));
+  S_HIP(hipGetLastError());
   const int lb = (c->info.L + 1) / 2;
   const u64 hdr = host_ptr_bytes(c->info.root) + 8 + c->info.n_leaves * u64(lb);
   unsigned char* out = s.dag.as<unsigned char>();
