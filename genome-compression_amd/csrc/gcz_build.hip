@@ -80,7 +80,7 @@ int gcz_ctx::leaf_level(const LeafLevel& a, Header* d_hdr) {
   }
   unsigned char* d_nf = nf_set[0];
   hipEvent_t e0{};
-  if (a.c_begin == 0) {
+  if (a.c_begin == 0 && !a.precleared) {
     prof_begin(KID_MEMSET, e0);
     HIP_TRY(hipMemsetAsync(tab.ptr, 0xff, lt.bytes(), stream));
     HIP_TRY(hipMemsetAsync(d_nf, 0, a.S, stream));
@@ -119,9 +119,10 @@ int gcz_ctx::leaf_level(const LeafLevel& a, Header* d_hdr) {
     const dim3 gs(unsigned((i1 - i0 + tile - 1) / tile));
     const u64* id0 = c == 0 ? nullptr : &a.count[c - 1];
     prof_begin(KID_FLAGSCAN_LEAF, e0);
+    u64* ldesc = i1 - i0 <= kSmallScanMax && i0 % 256 == 0 ? nullptr : a.desc + a.desc_off[c];
 #define GCZ_FLAGSCAN_LEAF(TAB, TV, IT)                                                                   \
   hipLaunchKernelGGL((k_flagscan_leaf<TAB, IT>), gs, dim3(kBlock), 0, stream, A, i0, i1, TV, d_nf,      \
-                     a.desc + a.desc_off[c], &a.ticket[c], a.out, id0, &a.count[c])
+                     ldesc, &a.ticket[c], a.out, id0, &a.count[c])
     if (lt.packed) {
       if (tile == u64(kTile)) GCZ_FLAGSCAN_LEAF(PackedTab, lt.pt, kItems);
       else GCZ_FLAGSCAN_LEAF(PackedTab, lt.pt, kItemsSmall);
@@ -430,12 +431,13 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   prof_begin(KID_FLAGSCAN_NODE, e0);
   const u64 tile = scan_tile(p);
   const dim3 gs(unsigned((p + tile - 1) / tile));
+  u64* ndesc = p <= kSmallScanMax ? nullptr : a.desc;   // small levels: no look-back chain
   if (tile == u64(kTile))
     hipLaunchKernelGGL((k_flagscan_node<kItems>), gs, dim3(kBlock), 0, stream, a.words, p, a.in, n, knf, d_grp,
-                       a.desc, a.ticket, a.out, a.count, a.pcount, mk.multi, a.hashed_next);
+                       ndesc, a.ticket, a.out, a.count, a.pcount, mk.multi, a.hashed_next);
   else
     hipLaunchKernelGGL((k_flagscan_node<kItemsSmall>), gs, dim3(kBlock), 0, stream, a.words, p, a.in, n, knf, d_grp,
-                       a.desc, a.ticket, a.out, a.count, a.pcount, mk.multi, a.hashed_next);
+                       ndesc, a.ticket, a.out, a.count, a.pcount, mk.multi, a.hashed_next);
   HIP_TRY(hipGetLastError());
   prof_end(KID_FLAGSCAN_NODE, e0);
   prof_begin(KID_RESOLVE_NODE, e0);
@@ -544,107 +546,166 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
 
   allow_packed = !force_wide;
   bucket_now = use_bucket;
+  const bool try_dense = dense_mode != 0 && L <= 12 && (S >= dense_min || dense_mode == 2);
   for (;;) {
     if ((rc = ensure(tab, std::max(leaf_cap, node_cap0) * 16))) return rc;
-    HIP_TRY(hipEventRecord(ev_start, stream));
-    HIP_TRY(hipMemsetAsync(d_hdr, 0, sizeof(Header), stream));
-    HIP_TRY(hipMemsetAsync(&d_hdr->err_offset, 0xff, 8, stream));
-    HIP_TRY(hipMemsetAsync(d_desc, 0, ntiles_total * 8, stream));
-    HIP_TRY(hipMemsetAsync(stats.ptr, 0, kStatBytes, stream));
-
-    // ---- leaf level, in chunks ----
-    LeafLevel la;
-    la.bases = d_bases; la.leaves = d_leaves; la.S = S; la.L = L;
-    la.cap = leaf_cap;
-    la.adaptive = leaf_cap < 2 * S;
-    la.words = A;
-    la.out = leaves_out.as<u64>();
-    la.chunk_start = chunk_start;
-    la.desc = d_desc;
-    la.desc_off = desc_off;
-    la.count = d_hdr->count;
-    la.ticket = d_hdr->ticket;
-    dense_used = false;
-    if (dense_mode != 0 && L <= 12 && (S >= dense_min || dense_mode == 2)) {
-      if ((rc = leaf_level_dense(la, d_hdr, &d_hdr->count[C - 1], &dense_used))) return rc;
-      if (!dense_used) HIP_TRY(hipMemsetAsync(&d_hdr->dense_fail, 0, 4, stream));
-    }
-    if (!dense_used && (rc = leaf_level(la, d_hdr))) return rc;
-
-    // ---- node layers ----
-    u32* in = A;
-    u32* outw = Bw;
-    u64 n = S;
-    u64 bound = std::min(S, leaf_cap);        // child ids of layer 0 are leaf ids < #slots
-    bool tail_done = false, direct = false;
-    bool prev_regular = false;   // the previous level ran node_level (its gate is written)
-    bool table_only = false;     // hdr->predup seen on the host: no bucketed levels
-    for (int k = 0; k < D; ++k) {
-      if (n <= u64(kTailMaxN) && use_tail) {   // the rest fits one workgroup: one launch
-        const u64* pc = k == 0 ? &d_hdr->count[C - 1] : prev_regular ? &d_hdr->gate[k - 1]
-                                                                       : &d_hdr->count[kLayerSlot + k - 1];
-        if ((rc = tail_levels(in, n, pc, k, D, layer_off, d_hdr))) return rc;
-        tail_done = true;
-        break;
-      }
-      if (direct) {   // host-known: up to kDirectLog levels per launch, ids = positions
-        DirectPlan dp{};
-        int nlev = 0;
-        u64 m = n;
-        dp.n[0] = n;
-        while (nlev < kDirectLog && k + nlev < D && (m > u64(kTailMaxN) || !use_tail)) {
-          dp.layer_off[k + nlev] = layer_off[k + nlev];
-          m = pk[k + nlev];
-          dp.n[++nlev] = m;
+    // One build's launches, start event to header copy.  A build whose launch sequence
+    // has no host decision inside (no dense-level fallback check, no look at the direct
+    // gate: small genomes) is captured once as a HIP graph and replayed while the shape
+    // and buffers stay the same -- its ~30 short kernels are otherwise bound by the
+    // host's per-launch cost.
+    auto enqueue = [&]() -> int {
+      HIP_TRY(hipEventRecord(ev_start, stream));
+      {   // header, descriptors, statistics and (hash-table leaf level) its table and marks: one launch
+        InitPlan ip{};
+        ip.hdr = d_hdr;
+        ip.desc = static_cast<uint4*>(desc.ptr);
+        ip.ndesc16 = (ntiles_total * 8 + 15) / 16;
+        ip.stats = static_cast<uint4*>(stats.ptr);
+        ip.nstats16 = kStatBytes / 16;
+        if (!try_dense) {
+          const LevelTab lt = plan_table(tab.ptr, leaf_cap, d_bases ? 4 * u32(L) + 2 : 64, S, 0,
+                                         allow_packed && d_bases, leaf_cap < 2 * S ? kAdaptiveProbeLimit : kMaxProbe);
+          ip.tab = static_cast<uint4*>(tab.ptr);
+          ip.ntab16 = lt.bytes() / 16;
+          ip.nf = reinterpret_cast<uint4*>(nf_set[0]);
+          ip.nnf16 = (S + 15) / 16;
         }
-        if (nlev == 0) return fail(GCZ_ERR_ARG, "build", "internal: empty direct step");
-        if ((rc = direct_levels(in, k, nlev, dp, outw, d_hdr))) return rc;
-        prev_regular = false;
+        const u64 big = std::max<u64>({ip.ndesc16, ip.nstats16, ip.ntab16, ip.nnf16});
+        hipLaunchKernelGGL(k_build_init, dim3(unsigned(std::min<u64>(4096, (big + kBlock - 1) / kBlock))),
+                           dim3(kBlock), 0, stream, ip);
+        HIP_TRY(hipGetLastError());
+      }
+
+      // ---- leaf level, in chunks ----
+      LeafLevel la;
+      la.bases = d_bases; la.leaves = d_leaves; la.S = S; la.L = L;
+      la.cap = leaf_cap;
+      la.adaptive = leaf_cap < 2 * S;
+      la.words = A;
+      la.out = leaves_out.as<u64>();
+      la.chunk_start = chunk_start;
+      la.desc = d_desc;
+      la.desc_off = desc_off;
+      la.count = d_hdr->count;
+      la.ticket = d_hdr->ticket;
+      dense_used = false;
+      la.precleared = !try_dense;
+      if (try_dense) {
+        if ((rc = leaf_level_dense(la, d_hdr, &d_hdr->count[C - 1], &dense_used))) return rc;
+        if (!dense_used) HIP_TRY(hipMemsetAsync(&d_hdr->dense_fail, 0, 4, stream));
+      }
+      if (!dense_used && (rc = leaf_level(la, d_hdr))) return rc;
+
+      // ---- node layers ----
+      u32* in = A;
+      u32* outw = Bw;
+      u64 n = S;
+      u64 bound = std::min(S, leaf_cap);        // child ids of layer 0 are leaf ids < #slots
+      bool tail_done = false, direct = false;
+      bool prev_regular = false;   // the previous level ran node_level (its gate is written)
+      bool table_only = false;     // hdr->predup seen on the host: no bucketed levels
+      for (int k = 0; k < D; ++k) {
+        if (n <= u64(kTailMaxN) && use_tail) {   // the rest fits one workgroup: one launch
+          const u64* pc = k == 0 ? &d_hdr->count[C - 1] : prev_regular ? &d_hdr->gate[k - 1]
+                                                                         : &d_hdr->count[kLayerSlot + k - 1];
+          if ((rc = tail_levels(in, n, pc, k, D, layer_off, d_hdr))) return rc;
+          tail_done = true;
+          break;
+        }
+        if (direct) {   // host-known: up to kDirectLog levels per launch, ids = positions
+          DirectPlan dp{};
+          int nlev = 0;
+          u64 m = n;
+          dp.n[0] = n;
+          while (nlev < kDirectLog && k + nlev < D && (m > u64(kTailMaxN) || !use_tail)) {
+            dp.layer_off[k + nlev] = layer_off[k + nlev];
+            m = pk[k + nlev];
+            dp.n[++nlev] = m;
+          }
+          if (nlev == 0) return fail(GCZ_ERR_ARG, "build", "internal: empty direct step");
+          if ((rc = direct_levels(in, k, nlev, dp, outw, d_hdr))) return rc;
+          prev_regular = false;
+          std::swap(in, outw);
+          n = m;
+          bound = m;
+          k += nlev - 1;
+          continue;
+        }
+        NodeLevel na;
+        na.k = k;
+        na.in = in; na.n = n; na.p = pk[k];
+        na.words = outw;
+        na.out = nodes_out.as<uint2>() + layer_off[k];
+        na.count = &d_hdr->count[kLayerSlot + k];
+        na.bound = bound;
+        na.prev_marks = k > 0;
+        na.pcount = k == 0 ? &d_hdr->count[C - 1] : &d_hdr->gate[k - 1];
+        na.desc = d_desc + desc_off[C + k];
+        na.ticket = &d_hdr->ticket[kLayerSlot + k];
+        na.hashed_next = &d_hdr->hashed_next[k];   // look-ahead for layer k + 1 (its pairs' children are here)
+        na.gate = &d_hdr->gate[k];
+        na.allow_bucket = !table_only;
+        if ((rc = node_level(na, d_hdr))) return rc;
+        prev_regular = true;
         std::swap(in, outw);
-        n = m;
-        bound = m;
-        k += nlev - 1;
-        continue;
+        n = pk[k];
+        bound = pk[k];
+        // a look at the device after layers 0 and 1: once a gate is open every later
+        // level is direct and runs as direct subtrees (saves ~4 launches per level)
+        if (k <= 1 && use_direct && n >= kDirectCheckMin) {   // (a host round trip: only where levels are big)
+          u64 g = 0;
+          u32 pd = 0;
+          HIP_TRY(hipMemcpyAsync(&g, &d_hdr->gate[k], 8, hipMemcpyDeviceToHost, stream));
+          HIP_TRY(hipMemcpyAsync(&pd, &d_hdr->predup, 4, hipMemcpyDeviceToHost, stream));
+          HIP_TRY(hipStreamSynchronize(stream));
+          direct = g == n;
+          table_only = pd != 0;   // repetitive data: later levels skip the (gated-off) bucket launches
+        }
       }
-      NodeLevel na;
-      na.k = k;
-      na.in = in; na.n = n; na.p = pk[k];
-      na.words = outw;
-      na.out = nodes_out.as<uint2>() + layer_off[k];
-      na.count = &d_hdr->count[kLayerSlot + k];
-      na.bound = bound;
-      na.prev_marks = k > 0;
-      na.pcount = k == 0 ? &d_hdr->count[C - 1] : &d_hdr->gate[k - 1];
-      na.desc = d_desc + desc_off[C + k];
-      na.ticket = &d_hdr->ticket[kLayerSlot + k];
-      na.hashed_next = &d_hdr->hashed_next[k];   // look-ahead for layer k + 1 (its pairs' children are here)
-      na.gate = &d_hdr->gate[k];
-      na.allow_bucket = !table_only;
-      if ((rc = node_level(na, d_hdr))) return rc;
-      prev_regular = true;
-      std::swap(in, outw);
-      n = pk[k];
-      bound = pk[k];
-      // a look at the device after layers 0 and 1: once a gate is open every later
-      // level is direct and runs as direct subtrees (saves ~4 launches per level)
-      if (k <= 1 && use_direct && n > u64(kTailMaxN)) {
-        u64 g = 0;
-        u32 pd = 0;
-        HIP_TRY(hipMemcpyAsync(&g, &d_hdr->gate[k], 8, hipMemcpyDeviceToHost, stream));
-        HIP_TRY(hipMemcpyAsync(&pd, &d_hdr->predup, 4, hipMemcpyDeviceToHost, stream));
-        HIP_TRY(hipStreamSynchronize(stream));
-        direct = g == n;
-        table_only = pd != 0;   // repetitive data: later levels skip the (gated-off) bucket launches
-      }
-    }
-    if (!tail_done) {
-      hipLaunchKernelGGL(k_root, dim3(1), dim3(1), 0, stream, in, d_hdr);
+      hipLaunchKernelGGL(k_build_finish, dim3(1), dim3(1024), 0, stream, tail_done ? nullptr : in, stats.as<u64>(),
+                         d_hdr);
       HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(ev_stop, stream));
+      HIP_TRY(hipMemcpyAsync(h_hdr, d_hdr, sizeof(Header), hipMemcpyDeviceToHost, stream));
+      return GCZ_OK;
+    };
+    // (a level that may take the bucketed path can allocate inside: never captured; a
+    // shape is captured on its second build, once every buffer has its size)
+    const bool static_seq = use_graph && !profile && !try_dense && pk[0] < kDirectCheckMin &&
+                            !(use_bucket && pk[0] >= bucket_min);
+    bool launched = false;
+    if (static_seq) {
+      const GraphKey key{d_bases, d_leaves, nbases, S, L, leaf_cap, allow_packed, bucket_now, stream,
+                         tab.ptr, wa.ptr, wb.ptr, nodes_out.ptr, leaves_out.ptr, nf.ptr, desc.ptr};
+      if (graph_exec && key == graph_key) {
+        launched = hipGraphLaunch(graph_exec, stream) == hipSuccess;
+      } else if (!(key == graph_seen)) {
+        graph_seen = key;   // first build of this shape: eager
+      } else {
+        if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
+        graph_exec = nullptr;
+        if (hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+          const int crc = enqueue();
+          hipGraph_t g = nullptr;
+          const hipError_t ce = hipStreamEndCapture(stream, &g);
+          if (crc == GCZ_OK && ce == hipSuccess && g &&
+              hipGraphInstantiate(&graph_exec, g, nullptr, nullptr, 0) == hipSuccess) {
+            graph_key = key;
+            launched = hipGraphLaunch(graph_exec, stream) == hipSuccess;
+          }
+          if (g) (void)hipGraphDestroy(g);
+          if (!launched) {   // capture refused something: run it eagerly
+            if (graph_exec) (void)hipGraphExecDestroy(graph_exec);
+            graph_exec = nullptr;
+            (void)hipGetLastError();
+            info.status = GCZ_OK;
+            last_error.clear();
+          }
+        }
+      }
     }
-    hipLaunchKernelGGL(k_stats_sum, dim3(1), dim3(1024), 0, stream, stats.as<u64>(), &d_hdr->hashed[0]);
-    hipLaunchKernelGGL(k_stats_sum, dim3(1), dim3(1024), 0, stream, stats.as<u64>() + 1, &d_hdr->hashed[1]);
-    HIP_TRY(hipEventRecord(ev_stop, stream));
-    HIP_TRY(hipMemcpyAsync(h_hdr, d_hdr, sizeof(Header), hipMemcpyDeviceToHost, stream));
+    if (!launched && (rc = enqueue())) return rc;
     HIP_TRY(hipStreamSynchronize(stream));
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, ev_start, ev_stop));
@@ -656,7 +717,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       bucket_now = false;
       continue;
     }
-    if (h_hdr->leaf_overflow && la.adaptive) {    // leaf table too small: grow and rebuild
+    if (h_hdr->leaf_overflow && leaf_cap < 2 * S) {    // leaf table too small: grow and rebuild
       leaf_cap = std::min(full_cap, leaf_cap * 8);
       continue;
     }
@@ -713,6 +774,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   if (const char* t = std::getenv("GCZ_BUCKET_MIN")) c->bucket_min = std::strtoull(t, nullptr, 10);
   if (const char* t = std::getenv("GCZ_BUCKET_TWO")) c->two_pass = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_DENSE")) c->dense_mode = std::atoi(t);
+  if (const char* t = std::getenv("GCZ_GRAPH")) c->use_graph = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_LEAF_FIRST_LOG2")) c->leaf_first_log2 = std::max(1, std::min(20, std::atoi(t)));
   *out = c;
   return GCZ_OK;
@@ -732,6 +794,7 @@ void gcz_ctx_destroy(gcz_ctx* c) {
                     &c->dl_pos, &c->dl_list, &c->dl_gid, &c->dl_recv, &c->dl_stage, &c->dl_seg})
     if (b->ptr) (void)hipFree(b->ptr);
   if (c->h_hdr) (void)hipHostFree(c->h_hdr);
+  if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
   if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);

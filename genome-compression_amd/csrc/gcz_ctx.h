@@ -155,9 +155,27 @@ struct LeafLevel {
   int c_begin = 0, c_end = -1;
   const u64* seed = nullptr;
   u64 seed_n = 0;
+  bool precleared = false;          // table and marks already cleared (k_build_init)
 };
 
 }  // namespace gcz_host
+
+// What a captured build graph depends on (gcz_ctx::build): replayed only on a match.
+struct GraphKey {
+  const void* bases;
+  const void* leaves;
+  gcz_host::u64 nbases, S;
+  int L;
+  gcz_host::u64 leaf_cap;
+  bool packed, bucket;
+  hipStream_t stream;
+  void *tab, *wa, *wb, *nodes, *leaves_out, *nf, *desc;
+  bool operator==(const GraphKey& o) const {
+    return bases == o.bases && leaves == o.leaves && nbases == o.nbases && S == o.S && L == o.L &&
+           leaf_cap == o.leaf_cap && packed == o.packed && bucket == o.bucket && stream == o.stream && tab == o.tab &&
+           wa == o.wa && wb == o.wb && nodes == o.nodes && leaves_out == o.leaves_out && nf == o.nf && desc == o.desc;
+  }
+};
 
 struct gcz_dist_state;   // gcz_dist.hip
 struct gcz_sort_state;   // gcz_sort.hip
@@ -198,6 +216,9 @@ struct gcz_ctx {
   int dense_mode = 1;        // dense leaf level (gcz_dense.h): 0 off, 1 on large pure-ACGT inputs, 2 any size (GCZ_DENSE)
   gcz_host::u64 dense_min = 1ull << 21;   // ... from this many strands (mode 1)
   bool dense_used = false;   // the last build's leaf level ran dense
+  bool use_graph = true;     // small builds as a replayed HIP graph       (GCZ_GRAPH=0 disables)
+  hipGraphExec_t graph_exec = nullptr;
+  GraphKey graph_key{}, graph_seen{};
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> event_pool;
   size_t event_used = 0;

@@ -31,6 +31,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
+
 #include <cstdint>
 
 #include "gcz_internal.h"
@@ -543,6 +545,60 @@ constexpr size_t kStatBytes = size_t(kStatShards) * kStatStride * 8;
   }
 }
 
+// Build start in one launch (instead of a memset per buffer): the header (zero, the
+// error offset ~0), the look-back descriptors, the statistics shards and, when the
+// hash-table leaf level runs, its table (0xff) and not-first marks.
+struct InitPlan {
+  Header* hdr;
+  uint4* desc;  u64 ndesc16;
+  uint4* stats; u64 nstats16;
+  uint4* tab;   u64 ntab16;     // 0xff
+  uint4* nf;    u64 nnf16;
+};
+
+[[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_build_init(InitPlan ip) {
+  const u64 t = u64(blockIdx.x) * kBlock + threadIdx.x, st = u64(gridDim.x) * kBlock;
+  if (blockIdx.x == 0) {
+    u32* h = reinterpret_cast<u32*>(ip.hdr);
+    constexpr u32 nw = sizeof(Header) / 4, e0 = offsetof(Header, err_offset) / 4;
+    for (u32 i = threadIdx.x; i < nw; i += kBlock) h[i] = (i == e0 || i == e0 + 1) ? ~0u : 0u;
+  }
+  const uint4 z = make_uint4(0, 0, 0, 0), f = make_uint4(~0u, ~0u, ~0u, ~0u);
+  for (u64 i = t; i < ip.ndesc16; i += st) ip.desc[i] = z;
+  for (u64 i = t; i < ip.nstats16; i += st) ip.stats[i] = z;
+  for (u64 i = t; i < ip.ntab16; i += st) ip.tab[i] = f;
+  for (u64 i = t; i < ip.nnf16; i += st) ip.nf[i] = z;
+}
+
+// Build end in one launch: the root word (when the level loop, not k_tail, ended the
+// build) and the two hashed-pair statistics.
+[[maybe_unused]] static __global__ __launch_bounds__(1024) void k_build_finish(const u32* __restrict__ root_word,
+                                                                               const u64* __restrict__ shards,
+                                                                               Header* __restrict__ hdr) {
+  __shared__ u64 s_sum[2][1024 / 64];
+  u64 v0 = shards[threadIdx.x * kStatStride], v1 = shards[threadIdx.x * kStatStride + 1];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    v0 += __shfl_xor(v0, o, 64);
+    v1 += __shfl_xor(v1, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_sum[0][threadIdx.x >> 6] = v0;
+    s_sum[1][threadIdx.x >> 6] = v1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 a = 0, b = 0;
+    for (int w = 0; w < 1024 / 64; ++w) {
+      a += s_sum[0][w];
+      b += s_sum[1][w];
+    }
+    hdr->hashed[0] = a;
+    hdr->hashed[1] = b;
+    if (root_word) hdr->root = root_word[0];
+  }
+}
+
 template <class Tab>
 __global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ in, u64 n, u64 p, Tab T,
                                                        const unsigned char* __restrict__ prev_nf,
@@ -670,16 +726,41 @@ struct TileScan {
 
 // Elements are positions [j0, p) of the level (j0 > 0 for later leaf chunks);
 // ids start at id0.  ts.base is the first position of the tile.
+//
+// desc == null (small levels, p <= kSmallScanMax): no look-back chain; every tile
+// counts the first occurrences before it directly from the marks (16-B loads of
+// [j0, base), zero bytes counted by a SWAR test), so no tile waits for another.
+// The reads total p^2 / (2 * tile) bytes: a few MB at most.
+constexpr unsigned long long kSmallScanMax = 1ull << 17;
+
+__device__ __forceinline__ u32 zero_bytes(u32 x) {   // bytes of x equal to 0 (= kNfMaybe)
+  const u32 t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;
+  return u32(__popc(~t & 0x80808080u));
+}
+
 template <int ITEMS>
 __device__ __forceinline__ void tile_scan(TileScan<ITEMS>& ts, u32* s_tile, u32* s_pre,
                                           const unsigned char* __restrict__ nf, u64 j0, u64 p, u64 id0,
                                           u64* __restrict__ desc, u32* __restrict__ ticket,
                                           u64* __restrict__ count_out) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) *s_tile = atomicAdd(ticket, 1u);
+  const bool direct = desc == nullptr;
+  if (tid == 0) *s_tile = direct ? 0u : atomicAdd(ticket, 1u);
   __syncthreads();
-  const u64 tile = *s_tile;
+  const u64 tile = direct ? u64(blockIdx.x) : u64(*s_tile);
   ts.base = j0 + tile * (kBlock * ITEMS);
+  if (direct) {   // firsts in [j0, base): j0 and base are multiples of 256
+    const uint4* q = reinterpret_cast<const uint4*>(nf + j0);
+    const u64 nq = (ts.base - j0) / 16;
+    u32 c = 0;
+    for (u64 i = tid; i < nq; i += kBlock) {
+      const uint4 v = q[i];
+      c += zero_bytes(v.x) + zero_bytes(v.y) + zero_bytes(v.z) + zero_bytes(v.w);
+    }
+    c = u32(wave_sum(u64(c)));
+    __syncthreads();   // (every thread has read *s_tile)
+    if (lane == 0 && c) atomicAdd(s_tile, c);
+  }
 #pragma unroll
   for (int e = 0; e < ITEMS; ++e) {
     const u64 j = ts.base + u64(e) * kBlock + tid;
@@ -707,7 +788,9 @@ __device__ __forceinline__ void tile_scan(TileScan<ITEMS>& ts, u32* s_tile, u32*
     }
     const u64 agg = __shfl(incl, 63, 64);
     u64 prefix = tile == 0 ? id0 : 0;   // descriptors' P values already include id0
-    if (tile == 0) {
+    if (direct) {
+      prefix = id0 + *s_tile;
+    } else if (tile == 0) {
       if (lane == 0) __hip_atomic_store(&desc[0], kStP | (id0 + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       if (lane == 0) __hip_atomic_store(&desc[tile], kStA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1386,6 +1469,7 @@ struct DirectPlan {
 // ranks the first occurrences) -- the same ids, nodes and words as the
 // per-level kernels, without ~4 launches per level.
 constexpr int kTailMaxN = 2048;
+constexpr unsigned long long kDirectCheckMin = 1ull << 16;   // levels below: no host look at the direct gate
 constexpr int kTailThreads = 1024;
 constexpr int kTailSlots = 2 * kTailThreads;
 
