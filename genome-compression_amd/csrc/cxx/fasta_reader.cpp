@@ -50,19 +50,33 @@ auto fasta_reader::bases() const -> const std::vector<std::uint8_t>& {
 
 auto fasta_reader::eof() const -> bool {
   extract();
-  return next >= strands;
+  return next >= strands && !loaded;
 }
 
-auto fasta_reader::read_into(std::vector<dna>& vector) -> bool {
+// the next buffer of strands into the back buffer (empty at the end of the file)
+void fasta_reader::load_buffer() {
   extract();
-  if (next >= strands) return false;
-  const std::size_t n = std::min(buffer_size, strands - next);
+  const std::size_t n = next < strands ? std::min(buffer_size, strands - next) : 0;
   const std::size_t L = dna::size();
-  vector.resize(n);
+  back.resize(n);
   for (std::size_t i = 0; i < n; ++i)
-    vector[i] = dna{std::string_view{reinterpret_cast<const char*>(&seq[(next + i) * L]), L}};
+    back[i] = dna{std::string_view{reinterpret_cast<const char*>(&seq[(next + i) * L]), L}};
   next += n;
-  return true;
+  loaded = n != 0;
+}
+
+void fasta_reader::swap_buffers() {
+  std::swap(back, front);
+  loaded = !back.empty();
+}
+
+auto fasta_reader::read_into(std::vector<dna>& vector) -> bool {   // src/fasta_reader.cpp:92-106
+  if (!loaded) load_buffer();
+  if (!loaded) return false;
+  std::swap(back, vector);
+  back.clear();
+  loaded = false;
+  return !vector.empty();
 }
 
 auto fasta_reader::size() const -> std::size_t { return nbytes; }

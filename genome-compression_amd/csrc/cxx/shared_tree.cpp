@@ -191,6 +191,79 @@ shared_tree::shared_tree(std::vector<dna>& data, bool verbose) {
   if (verbose) std::cout << "\rConstructing subtrees: done.\n\rCombining subtrees: done.\n";
 }
 
+// ---- tree_constructor (src/shared_tree.cpp:617-763) ---------------------------------
+tree_constructor::tree_constructor(shared_tree& parent) : parent{parent} { nodes.reserve(64); }
+
+auto tree_constructor::emplace_leaf(dna leaf) -> pointer {   // :630-637
+  const auto [canonical, mirror, transpose, invariant] = leaf.canonical();
+  const auto ins = leaves.emplace(canonical, parent.leaf_count());
+  if (ins.second) parent.emplace_leaf(canonical);
+  return pointer{ins.first->second, mirror, transpose, invariant};
+}
+
+auto tree_constructor::emplace_leaves(dna left, dna right) -> pointer {   // :643-647
+  const auto l = emplace_leaf(left);
+  const auto r = emplace_leaf(right);
+  return emplace_node(0, l, r);
+}
+
+auto tree_constructor::emplace_leaves(dna last) -> pointer { return emplace_node(0, emplace_leaf(last)); }   // :653-656
+
+auto tree_constructor::emplace_node(std::size_t layer, pointer left, pointer right) -> pointer {   // :662-672
+  const auto [canonical, mirror, transpose] = node{left, right}.canonical();
+  const auto ins = nodes[layer].emplace(canonical, parent.node_count(layer));
+  if (ins.second) parent.emplace_node(layer, canonical);
+  const bool invariant = left == right.mirrored();
+  return pointer{ins.first->second, mirror, transpose, invariant};
+}
+
+auto tree_constructor::reduce_roots(bool verbose) -> pointer {   // :677-692
+  for (auto index = nodes.size(); roots.size() > 1; ++index) roots = reduce_nodes(roots, index);
+  if (verbose) std::cout << "\rCombining subtrees: done.\n";
+  parent.root = roots.front();   // (the reference's callers assign it; a tree built outside one needs it too)
+  return roots.front();
+}
+
+auto tree_constructor::reduce_nodes(const std::vector<pointer>& iterable, std::size_t index)
+    -> std::vector<pointer> {   // :697-712
+  auto layer = std::vector<pointer>{};
+  layer.reserve(iterable.size() / 2 + iterable.size() % 2);
+  if (parent.depth() - 2 < index) {
+    parent.add_layer();
+    nodes.emplace_back();
+  }
+  for (std::size_t i = 0; i + 1 < iterable.size(); i += 2) layer.emplace_back(emplace_node(index, iterable[i], iterable[i + 1]));
+  if (iterable.size() % 2) layer.emplace_back(emplace_node(index, iterable.back()));
+  return layer;
+}
+
+auto tree_constructor::reduce(const std::vector<dna>& data, bool verbose) -> pointer {   // :743-763, on the GPU
+  static_assert(sizeof(dna) == 8, "dna is one 64-bit word");
+  auto& e = engine();
+  {
+    std::lock_guard<std::mutex> lock(e.mu);
+    check_build(gcz_build_host_leaves(e.ctx, reinterpret_cast<const std::uint64_t*>(data.data()), data.size(),
+                                      int(dna::size())),
+                e.ctx);
+    parent.build_from_gpu();
+  }
+  if (verbose) std::cout << "\rConstructing subtrees: done.\n\rCombining subtrees: done.\n";
+  roots.assign(1, parent.root);
+  return parent.root;
+}
+
+auto tree_constructor::reduce(fasta_reader& file, bool verbose) -> pointer {   // :719-736, on the GPU
+  auto& e = engine();
+  {
+    std::lock_guard<std::mutex> lock(e.mu);
+    check_build(gcz_build_host_fasta(e.ctx, file.raw_data(), file.raw_size(), int(dna::size())), e.ctx);
+    parent.build_from_gpu();
+  }
+  if (verbose) std::cout << "\rConstructing subtrees: done.\n\rCombining subtrees: done.\n";
+  roots.assign(1, parent.root);
+  return parent.root;
+}
+
 void shared_tree::build_from_gpu() {
   PhaseTimer t{"fetch"};
   gcz_ctx* ctx = engine().ctx;

@@ -6,7 +6,12 @@
  * empty line skips ONE line, the following line is read as data; data line
  * bodies are concatenated; the tail beyond a multiple of dna::size() is
  * dropped unvalidated; an unknown symbol prints the reference's message and
- * exits(1).  read_into() hands out consecutive buffers of buffer_size strands.
+ * exits(1).  read_into() hands out consecutive buffers of buffer_size strands:
+ * load_buffer() decodes the next one into the back buffer (the reference runs it
+ * on a background thread, src/fasta_reader.cpp:40-68,92-106; here read_into calls
+ * it when the back buffer is empty), read_into() swaps it out; swap_buffers()
+ * exchanges the back buffer with the reader's front buffer (declared without a
+ * definition in the reference, include/fasta_reader.h:33).
  *
  * shared_tree{path} / shared_tree{fasta_reader} do NOT go through these
  * buffers: they hand the raw file (memory-mapped, never copied on the host) to
@@ -33,6 +38,8 @@ class fasta_reader {
   fasta_reader(fasta_reader&&) noexcept = default;
 
   auto eof() const -> bool;
+  void load_buffer();
+  void swap_buffers();
   auto read_into(std::vector<dna>& vector) -> bool;
   auto size() const -> std::size_t;      // file size in bytes (upper bound on bases)
   auto buffers() const -> std::size_t;   // approximate number of buffers
@@ -53,7 +60,9 @@ class fasta_reader {
   mutable std::vector<std::uint8_t> seq;
   mutable std::size_t strands = 0;
   mutable bool extracted = false;
-  std::size_t next = 0;
+  std::size_t next = 0;            // next strand to load
+  std::vector<dna> back, front;    // load_buffer target / swap_buffers partner
+  bool loaded = false;             // back holds a buffer read_into has not handed out
 };
 
 auto read_genome(const std::filesystem::path path) -> std::vector<dna>;

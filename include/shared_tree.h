@@ -11,6 +11,11 @@
  * The construction engine (the reference's tree_constructor, :245-316) is
  * replaced by the libgcz HIP build (include/gcz.h): the constructors hand the
  * genome to the GPU and copy the finished DAG back into the containers.
+ *   tree_constructor  the reference's class, same members: reduce() (whole
+ *             genomes) runs the HIP build; the element-at-a-time members
+ *             (emplace_*, reduce_leaves/nodes/segment/roots) keep the reference's
+ *             incremental dictionaries on the host for code that assembles a
+ *             tree piece by piece -- they are not the build path.
  *
  * Device selection: GCZ_DEVICE (default 0).  Errors behave like the
  * reference: an unknown nucleotide prints "Encountered unknown symbol: ..."
@@ -28,6 +33,7 @@
 #include <memory>
 #include <tuple>
 #include <type_traits>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -230,6 +236,7 @@ class shared_tree {
   auto end() const { return iterator{*this, 0, nullptr}; }
 
  private:
+  friend class tree_constructor;
   void build_from_gpu();   // copies the last libgcz build of this thread into the containers
   bool on_device() const;  // the engine's device arrays still hold exactly this tree
 
@@ -251,4 +258,74 @@ inline auto operator<<(std::ostream& os, const shared_tree& tree) -> std::ostrea
     os << '\n';
   }
   return os;
+}
+
+/******************************************************************************
+ * tree_constructor (reference include/shared_tree.h:245-316, src/shared_tree.cpp:617-763).
+ *
+ * reduce(data) / reduce(file): the whole genome through the libgcz HIP build; the
+ * parent receives the finished DAG (leaves, layers, root) and the root is returned.
+ * It expects a constructor that has not emplaced anything yet (as the shared_tree
+ * constructors use it); the GPU build is global, which equals the reference's
+ * segmented reduce for its power-of-two segments.
+ *
+ * The element-at-a-time members keep the reference's dictionaries on the host:
+ * emplace_leaf / emplace_leaves / emplace_node hash-cons one element (first
+ * occurrence = next index of the parent's layer), reduce_leaves / reduce_nodes
+ * pair up one layer, reduce_segment reduces a segment to one root, reduce_roots
+ * combines the roots.  Same results as the reference's, element for element.
+ */
+class tree_constructor {
+ public:
+  tree_constructor(shared_tree& parent);
+
+  auto emplace_node(std::size_t layer_index, pointer left, pointer right = nullptr) -> pointer;
+  auto emplace_leaves(dna left, dna right) -> pointer;
+  auto emplace_leaves(dna last) -> pointer;
+  auto emplace_leaf(dna leaf) -> pointer;
+
+  template <typename Iterable>
+  auto reduce_leaves(Iterable&& layer) -> std::vector<pointer>;
+  auto reduce_nodes(const std::vector<pointer>& segment, std::size_t index) -> std::vector<pointer>;
+  auto reduce_roots(bool verbose = false) -> pointer;
+  auto reduce(const std::vector<dna>& data, bool verbose = false) -> pointer;
+  auto reduce(fasta_reader& file, bool verbose = false) -> pointer;
+
+  template <typename Iterable>
+  void reduce_segment(Iterable&& layer);
+
+ private:
+  shared_tree& parent;
+  std::vector<std::unordered_map<node, std::size_t>> nodes;
+  std::unordered_map<dna, std::size_t> leaves;
+  std::vector<pointer> roots;
+};
+
+// reduce_leaves (src/shared_tree.h:287-302): pairs of strands -> layer-0 pointers
+// (foreach_pair, include/utility.h:17-29: an odd last strand pairs with null)
+template <typename Iterable>
+auto tree_constructor::reduce_leaves(Iterable&& iterable) -> std::vector<pointer> {
+  auto layer = std::vector<pointer>{};
+  const std::size_t n = std::size(iterable);
+  layer.reserve(n / 2 + n % 2);
+  if (parent.depth() == 1) {
+    parent.add_layer();
+    nodes.emplace_back();
+  }
+  auto it = std::begin(iterable);
+  for (std::size_t i = 0; i + 1 < n; i += 2) {
+    const dna left = *it++;
+    const dna right = *it++;
+    layer.emplace_back(emplace_leaves(left, right));
+  }
+  if (n % 2) layer.emplace_back(emplace_leaves(dna{*it}));
+  return layer;
+}
+
+// reduce_segment (:308-319): a segment down to one root, appended to the roots
+template <typename Iterable>
+void tree_constructor::reduce_segment(Iterable&& segment) {
+  auto layer = reduce_leaves(segment);
+  for (auto index = 1u; layer.size() > 1 || index < nodes.size(); ++index) layer = reduce_nodes(layer, index);
+  roots.emplace_back(layer.front());
 }

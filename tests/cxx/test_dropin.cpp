@@ -146,6 +146,66 @@ static void gpu_file_build() {
   CHECK(same_sequence(load, data), "deserialized tree decompresses");
 }
 
+// fasta_reader's buffer API (include/fasta_reader.h:31-33): load_buffer + read_into
+// hand out the same strands as read_genome; swap_buffers exchanges the buffers.
+static void buffer_api() {
+  const auto path = dir + "/data/chmpxx";
+  const auto all = read_genome(path);
+  fasta_reader f{path, 1000};
+  std::vector<dna> got, buf;
+  f.load_buffer();
+  CHECK(!f.eof(), "a loaded buffer is not eof");
+  while (f.read_into(buf)) {
+    CHECK(buf.size() <= 1000, "buffer size bound");
+    got.insert(got.end(), buf.begin(), buf.end());
+  }
+  CHECK(f.eof(), "eof after the last buffer");
+  CHECK(got == all, "buffers concatenate to read_genome: " << got.size() << " vs " << all.size());
+  fasta_reader g{path, 64};
+  g.load_buffer();          // back = strands [0, 64)
+  g.swap_buffers();         // front = [0, 64), back empty
+  g.load_buffer();          // back = [64, 128)
+  std::vector<dna> b;
+  CHECK(g.read_into(b) && b.size() == 64 && b.front() == all[64], "read_into after swap_buffers hands out the back buffer");
+  g.swap_buffers();         // back = [0, 64) again
+  CHECK(g.read_into(b) && b.front() == all[0], "swap_buffers brings the front buffer back");
+}
+
+static std::string dump(const shared_tree& t) {
+  std::ostringstream os;
+  os << t;
+  return os.str();
+}
+
+// tree_constructor (include/shared_tree.h:245-316): the element-at-a-time members build
+// the same DAG as the GPU build, reduce() runs the GPU build into the parent.
+static void gpu_tree_constructor() {
+  auto data = read_genome(dir + "/data/chmpxx");
+  const shared_tree gpu{data};
+  shared_tree a;
+  tree_constructor ca{a};
+  ca.reduce_segment(data);
+  const pointer ra = ca.reduce_roots();
+  CHECK(ra == gpu.root_pointer(), "element-wise root equals the GPU root");
+  CHECK(dump(a) == dump(gpu), "element-wise DAG equals the GPU DAG");
+  // two power-of-two segments then reduce_roots: the reference's segmented build
+  shared_tree b;
+  tree_constructor cb{b};
+  const std::size_t half = 4096;
+  cb.reduce_segment(std::vector<dna>(data.begin(), data.begin() + half));
+  cb.reduce_segment(std::vector<dna>(data.begin() + half, data.end()));
+  CHECK(cb.reduce_roots() == gpu.root_pointer() && dump(b) == dump(gpu), "segmented reduce equals the global build");
+  shared_tree c;
+  tree_constructor cc{c};
+  CHECK(cc.reduce(data) == gpu.root_pointer(), "reduce(data) root");
+  CHECK(dump(c) == dump(gpu), "reduce(data) DAG");
+  CHECK(c[5000] == data[5000], "reduce(data) tree decompresses");
+  shared_tree d;
+  tree_constructor cd{d};
+  fasta_reader f{dir + "/data/chmpxx"};
+  CHECK(cd.reduce(f) == gpu.root_pointer() && dump(d) == dump(gpu), "reduce(fasta_reader)");
+}
+
 int main(int argc, char** argv) {
   dir = argc > 1 ? argv[1] : "tests/golden";
   const bool gpu = argc > 2 && std::string(argv[2]) == "gpu";
@@ -153,7 +213,9 @@ int main(int argc, char** argv) {
   pointer_ops();
   canonical_invariance();
   file_reader();
+  buffer_api();
   if (gpu) {
+    gpu_tree_constructor();
     gpu_transposition();
     gpu_frequency_sort();
     gpu_file_build();
