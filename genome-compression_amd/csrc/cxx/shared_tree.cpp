@@ -160,7 +160,12 @@ namespace {
 fasta_reader open_with_engine(const std::filesystem::path& path) {
   if (::access(path.c_str(), R_OK) != 0) return fasta_reader{path};   // prints the reference's error
   PhaseTimer t{"open"};
-  std::thread init([] { PhaseTimer t{"context"}; engine(); });
+  std::error_code ec;
+  const auto fsize = std::filesystem::file_size(path, ec);
+  std::thread init([fsize] {   // the context, the input buffer and a warm upload path, while the file maps
+    PhaseTimer t{"context"};
+    (void)gcz_upload_reserve(engine().ctx, fsize);
+  });
   fasta_reader f = [&] { PhaseTimer t{"map"}; return fasta_reader{path}; }();
   init.join();
   return f;

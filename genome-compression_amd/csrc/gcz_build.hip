@@ -1,6 +1,8 @@
 // MI355X (gfx950) shared_tree construction: host orchestration and the C ABI.
 // Device code and the algorithm description: gcz_device.h; the multi-rank
 // build: gcz_dist.hip.
+#include <thread>
+
 #include "gcz_ctx.h"
 #include "gcz_dense.h"
 #include "gcz_scan.h"
@@ -748,6 +750,33 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   return GCZ_OK;
 }
 
+// ---- host -> device upload ----------------------------------------------------------
+// The runtime's pageable copy reaches the link's ~56 GB/s once warm (a pinned staging
+// ring of 1-8 worker threads measured 30-54 GB/s: tools/microbench/upload.hip,
+// profiles/r02/microbench_upload.jsonl).  What costs on a cold process is the first copy
+// (~32 GB/s: the runtime's staging path and the destination's first DMA touch), so
+// upload_reserve() warms the path with a small copy (the C++ surface runs it while the
+// file is mapped) and upload() touches a destination with a memset before the DMA.
+int gcz_ctx::upload_reserve(size_t bytes) {
+  if (int rc = ensure(input, std::max<size_t>(bytes, size_t(8) << 20) + 16)) return rc;
+  HIP_TRY(hipMemsetAsync(input.ptr, 0, input.bytes, stream));
+  if (!upload_warm) {
+    const size_t n = size_t(8) << 20;
+    std::vector<char> h(n, 0);
+    HIP_TRY(hipMemcpyAsync(input.ptr, h.data(), n, hipMemcpyHostToDevice, stream));
+    upload_warm = true;
+  }
+  HIP_TRY(hipStreamSynchronize(stream));
+  return GCZ_OK;
+}
+
+int gcz_ctx::upload(void* d_dst, const void* h_src, size_t n) {
+  if (n == 0) return GCZ_OK;
+  if (n >= (size_t(64) << 20)) HIP_TRY(hipMemsetAsync(d_dst, 0, n, stream));   // first DMA touch, ~0.2 ms/GB
+  HIP_TRY(hipMemcpyAsync(d_dst, h_src, n, hipMemcpyHostToDevice, stream));
+  return GCZ_OK;
+}
+
 extern "C" {
 
 int gcz_ctx_create(int device, gcz_ctx** out) {
@@ -826,8 +855,14 @@ int gcz_dev_free(gcz_ctx* c, void* p) {
 int gcz_memcpy_h2d(gcz_ctx* c, void* dst, const void* src, uint64_t bytes) {
   if (!c) return GCZ_ERR_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
-  if (hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return GCZ_ERR_DEVICE;
+  if (int rc = c->upload(dst, src, bytes)) return rc;
   return hipStreamSynchronize(c->stream) == hipSuccess ? GCZ_OK : GCZ_ERR_DEVICE;
+}
+
+int gcz_upload_reserve(gcz_ctx* c, uint64_t bytes) {
+  if (!c) return GCZ_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  return c->upload_reserve(bytes);
 }
 
 int gcz_memcpy_d2h(gcz_ctx* c, void* dst, const void* src, uint64_t bytes) {
@@ -864,30 +899,19 @@ int gcz_build_host_leaves(gcz_ctx* c, const uint64_t* leaves, uint64_t S, int L)
   if (!c || (!leaves && S)) return GCZ_ERR_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
   if (int rc = c->ensure(c->input, S * 8 + 16)) return rc;
-  if (S && hipMemcpyAsync(c->input.ptr, leaves, S * 8, hipMemcpyHostToDevice, c->stream) != hipSuccess)
-    return c->fail(GCZ_ERR_DEVICE, "gcz_build_host_leaves", "H2D copy failed");
+  if (S && c->upload(c->input.ptr, leaves, S * 8)) return c->fail(GCZ_ERR_DEVICE, "gcz_build_host_leaves", "H2D copy failed");
   return c->build(nullptr, static_cast<const u64*>(c->input.ptr), 0, S, L);
 }
 
 int gcz_build_host_fasta(gcz_ctx* c, const void* fasta, uint64_t nbytes, int L) {
   if (!c || (!fasta && nbytes)) return GCZ_ERR_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
-  // the raw file goes to the device; headers / line breaks are removed there (gcz_ingest.hip)
-  const auto* f = static_cast<const uint8_t*>(fasta);
-  // one line without a header needs no line contract, unless a reader buffer
-  // boundary falls on a '>' (src/fasta_reader.cpp:48-51; gcz_ingest.hip)
-  bool plain = nbytes == 0 || (f[0] != '>' && f[0] != '\n' && !std::memchr(f, '\n', nbytes));
-  if (plain && L >= 1 && L <= 16) {
-    const u64 cap = gcz::reader_buffer_bytes(nbytes, L, 0);
-    for (u64 b = cap; b < nbytes && plain; b += cap) plain = f[b] != '>';
-  }
+  // the raw file goes to the device; headers / line breaks are removed there (gcz_ingest.hip:
+  // a file of one unbroken line is built in place, without a host scan for line breaks)
   if (int rc = c->ensure(c->input, nbytes + 16)) return rc;
-  if (nbytes && hipMemcpyAsync(c->input.ptr, f, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+  if (nbytes && c->upload(c->input.ptr, fasta, nbytes))
     return c->fail(GCZ_ERR_DEVICE, "gcz_build_host_fasta", "H2D copy failed");
-  if (hipStreamSynchronize(c->stream) != hipSuccess)
-    return c->fail(GCZ_ERR_DEVICE, "gcz_build_host_fasta", "sync failed");
-  if (!plain) return gcz_build_device_fasta(c, c->input.ptr, nbytes, L);
-  return c->build(c->input.ptr, nullptr, nbytes, 0, L);
+  return gcz_build_device_fasta(c, c->input.ptr, nbytes, L);
 }
 
 int gcz_info_get(gcz_ctx* c, gcz_info* out) {

@@ -217,6 +217,9 @@ struct gcz_ctx {
   gcz_host::u64 dense_min = 1ull << 21;   // ... from this many strands (mode 1)
   bool dense_used = false;   // the last build's leaf level ran dense
   bool use_graph = true;     // small builds as a replayed HIP graph       (GCZ_GRAPH=0 disables)
+  bool upload_warm = false;   // the runtime's host -> device path has run once (upload_reserve)
+  int upload_reserve(size_t bytes);                     // input buffer of `bytes`, touched; the copy path warmed
+  int upload(void* d_dst, const void* h_src, size_t n); // stream-ordered before later work on `stream`
   hipGraphExec_t graph_exec = nullptr;
   GraphKey graph_key{}, graph_seen{};
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;

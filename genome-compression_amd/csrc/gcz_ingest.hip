@@ -375,6 +375,13 @@ int gcz_fasta_extract_on_device(gcz_ctx* c, const unsigned char* d_file, u64 n, 
     I_HIP(hipGetLastError());
     k0 = ev + 1;
   }
+  // one line without a break, read whole (no header, no reader-buffer override): the
+  // file itself is the genome, no copy
+  if (nnl == 0 && !ln.cut && total == n) {
+    *d_bases = d_file;
+    *nbases = total;
+    return GCZ_OK;
+  }
   // 4. copy
   hipLaunchKernelGGL(k_copy_lines, dim3(unsigned((n + kWin - 1) / kWin)), dim3(kBlock), 0, c->stream, ln,
                      s.len.as<u64>(), s.off.as<u64>(), s.bases.as<unsigned char>());

@@ -84,6 +84,11 @@ GCZ_API const char *gcz_ctx_last_error(gcz_ctx *ctx);
 GCZ_API void *gcz_dev_alloc(gcz_ctx *ctx, uint64_t bytes);
 GCZ_API int gcz_dev_free(gcz_ctx *ctx, void *ptr);
 GCZ_API int gcz_memcpy_h2d(gcz_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+/* Prepare the upload of a `bytes`-byte input (gcz_build_host_*): the input buffer
+ * allocated and touched, the host -> device path warmed (a cold process's first copy
+ * runs at about half the link rate).  Optional; the C++ surface runs it while the
+ * input file is mapped. */
+GCZ_API int gcz_upload_reserve(gcz_ctx *ctx, uint64_t bytes);
 GCZ_API int gcz_memcpy_d2h(gcz_ctx *ctx, void *dst, const void *src, uint64_t bytes);
 GCZ_API int gcz_ctx_sync(gcz_ctx *ctx);
 

@@ -188,12 +188,13 @@ static void gpu_tree_constructor() {
   const pointer ra = ca.reduce_roots();
   CHECK(ra == gpu.root_pointer(), "element-wise root equals the GPU root");
   CHECK(dump(a) == dump(gpu), "element-wise DAG equals the GPU DAG");
-  // two power-of-two segments then reduce_roots: the reference's segmented build
+  // segments of 2^12 strands (the last one shorter) then reduce_roots: the reference's
+  // segmented build, equal to the global one
   shared_tree b;
   tree_constructor cb{b};
-  const std::size_t half = 4096;
-  cb.reduce_segment(std::vector<dna>(data.begin(), data.begin() + half));
-  cb.reduce_segment(std::vector<dna>(data.begin() + half, data.end()));
+  const std::size_t seg = 4096;
+  for (std::size_t i = 0; i < data.size(); i += seg)
+    cb.reduce_segment(std::vector<dna>(data.begin() + i, data.begin() + std::min(data.size(), i + seg)));
   CHECK(cb.reduce_roots() == gpu.root_pointer() && dump(b) == dump(gpu), "segmented reduce equals the global build");
   shared_tree c;
   tree_constructor cc{c};
