@@ -55,6 +55,7 @@ _SIGS = {
     "gcz_dev_alloc": (_P, [_P, _U64]),
     "gcz_dev_free": (ctypes.c_int, [_P, _P]),
     "gcz_memcpy_h2d": (ctypes.c_int, [_P, _P, _P, _U64]),
+    "gcz_upload_reserve": (ctypes.c_int, [_P, _U64]),
     "gcz_memcpy_d2h": (ctypes.c_int, [_P, _P, _P, _U64]),
     "gcz_ctx_sync": (ctypes.c_int, [_P]),
     "gcz_build_device_bases": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
