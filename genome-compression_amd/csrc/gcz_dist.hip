@@ -309,6 +309,7 @@ struct ShmTransport : Transport {
   int barrier() {
     local_sense ^= 1u;
     Ctl* c = ctl();
+    if (c->failed.load()) { err = "shm transport: a peer failed"; return GCZ_ERR_DEVICE; }
     if (c->arrived.fetch_add(1) + 1 == u32(world)) {
       c->arrived.store(0);
       c->sense.store(local_sense);
@@ -335,15 +336,22 @@ struct ShmTransport : Transport {
     }
     return GCZ_OK;
   }
+  // every failure inside a collective raises `failed`, so the peers leave their barrier
+  // at once instead of at the timeout (a group is single-use after a failure)
   int to_dev(void* dst, const char* src, size_t bytes) {
     if (bytes && hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream) != hipSuccess) {
       err = "shm transport: H2D copy failed";
+      ctl()->failed.store(1);
       return GCZ_ERR_DEVICE;
     }
     return GCZ_OK;
   }
   int drain() {
-    if (hipStreamSynchronize(stream) != hipSuccess) { err = "shm transport: stream"; return GCZ_ERR_DEVICE; }
+    if (hipStreamSynchronize(stream) != hipSuccess) {
+      err = "shm transport: stream";
+      ctl()->failed.store(1);
+      return GCZ_ERR_DEVICE;
+    }
     return GCZ_OK;
   }
   int alltoallv_at(const std::vector<u64>& M, bool rev, size_t elem, const std::vector<u64>& sd,
@@ -1712,10 +1720,13 @@ int gcz_group_create_shm(gcz_ctx* ctx, int rank, int world, const char* name, ui
   *out = nullptr;
   const size_t cap = (region_bytes + 4095) / 4096 * 4096;
   const size_t bytes = 4096 + cap * size_t(world);
-  // rank 0 creates and sizes the file (sparse); the others wait for its size
+  // rank 0 creates and sizes a fresh object (a stale one of the same name is removed
+  // first; a new object reads as zeros, so the control words start at 0); the others
+  // wait for its size.  Names must be unique per job (bench.py derives them from the port).
   int fd = -1;
   if (rank == 0) {
-    fd = shm_open(name, O_CREAT | O_RDWR, 0600);
+    (void)shm_unlink(name);
+    fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
     if (fd < 0 || ftruncate(fd, off_t(bytes)) != 0) {
       if (fd >= 0) close(fd);
       ctx->last_error = std::string("shm_open/ftruncate failed: ") + name;
