@@ -338,28 +338,30 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   const u64 ncnt = (u64(1) << bb) * G + 1;
   const u64 t_scan = scan_tiles(ncnt);   // look-back scan of the count matrix: descriptors + ticket
   // two-pass partition (k_bkt_part / fine / dedupe2) when a record holds the key's low
-  // K - bb bits and the full position, and a chunk's coarse segment fits a fine slice
+  // K - bb bits and its position in a fine slice
   Bkt2Plan b2{};
   b2.T = nt.pt;
   b2.K = bp.K;
   b2.b1 = std::min<u32>(bb, kPartMaxB1);
   b2.b2 = bb - b2.b1;
-  b2.G = G;
-  const u64 mean_seg = std::min<u64>(p, kBktChunk) >> b2.b1;
-  b2.segcap = u32(2 * mean_seg + 256);
-  b2.SC = u32(std::max<u64>(1, std::min<u64>(64, u64(kFineCap / 2) / std::max<u64>(1, kBktChunk >> b2.b1))));
-  b2.P = kBktRP + log2_exact(b2.SC);   // (SC is a power of two)
-  b2.nslice = u32((G + b2.SC - 1) / b2.SC);
-  const bool two = bkt && two_pass && b2.b2 <= u32(kFineMaxB2) && bp.K - b2.b1 + kBktRP <= 64 &&
-                   bp.K - bb + b2.P <= 64 && 2 * mean_seg <= u64(kFineCap) / 2 && b2.nslice <= 512;
+  b2.G = (p + kPartChunk - 1) / kPartChunk;
+  const u64 mean_run = std::max<u64>(1, std::min<u64>(p, kPartChunk) >> b2.b1);   // records per (chunk, coarse)
+  b2.SC = u32(std::max<u64>(1, std::min<u64>(128, u64(kFineCap / 2) / mean_run)));
+  b2.SC = 1u << log2_exact(b2.SC);   // a power of two
+  b2.P = kPartLog + log2_exact(b2.SC);
+  b2.nslice = u32((b2.G + b2.SC - 1) / b2.SC);
+  const bool two = bkt && two_pass && b2.b2 <= u32(kFineMaxB2) && bp.K - b2.b1 + kPartLog <= 64 &&
+                   bp.K - bb + b2.P <= 64 && mean_run * b2.SC <= u64(kFineCap) / 2 && b2.nslice <= 512;
   if (two) {
     int rc;
     const u64 nfine = (u64(1) << b2.b1) * b2.nslice;
-    if ((rc = ensure(bkt_key, G * (u64(1) << b2.b1) * b2.segcap * 8)) ||
-        (rc = ensure(bkt_cnt, G * (u64(1) << b2.b1) * 4 + 16)) ||
+    if ((rc = ensure(bkt_key, b2.G * kPartChunk * 8)) ||
+        (rc = ensure(bkt_cnt, b2.G * ((u64(1) << b2.b1) + 1) * 4 + 16)) ||
         (rc = ensure(bkt_rec2, nfine * kFineCap * 8)) ||
         (rc = ensure(bkt_off, nfine * ((u64(1) << b2.b2) + 1) * 4 + 16)))
       return rc;
+    HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(k_bkt_part),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, int(kPartChunk * 8)));
     HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(k_bkt_fine),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, int(kFineCap * 8)));
   } else if (bkt) {
@@ -383,8 +385,9 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   const dim3 gi(unsigned((p + kBlock - 1) / kBlock));
   if (two) {
     prof_begin(KID_BKT_SCATTER, e0);
-    hipLaunchKernelGGL(k_bkt_part, dim3(unsigned(G)), dim3(kBktThreads), 0, stream, a.in, n, p, pnf, pmu, b2,
-                       bkt_key.as<u64>(), bkt_cnt.as<u32>(), a.words, d_hdr, a.pcount, stats.as<u64>());
+    hipLaunchKernelGGL(k_bkt_part, dim3(unsigned(b2.G)), dim3(kBktThreads), size_t(kPartChunk) * 8, stream, a.in,
+                       n, p, pnf, pmu, b2, bkt_key.as<u64>(), bkt_cnt.as<u32>(), a.words, d_hdr, a.pcount,
+                       stats.as<u64>());
     HIP_TRY(hipGetLastError());
     prof_end(KID_BKT_SCATTER, e0);
     prof_begin(KID_BKT_FINE, e0);

@@ -1173,103 +1173,151 @@ __device__ __forceinline__ u32 bkt_pos(const u32* s_off, u64 G, u32 i, u64 r) {
 
 // ---- two-pass partition (levels where a record can carry its full position) ----------
 // The single-pass scatter above writes ~2.5 records per bucket per chunk, so its 8-B
-// stores never fill a line.  Here the records are partitioned twice, each pass with
-// long runs per bucket:
-//   part: per chunk (kBktChunk pairs) into 2^b1 coarse buckets (~256 records each at
-//         b1 = 8), written into fixed-capacity segments [chunk][coarse] (no count pass:
-//         a segment past its capacity sets bkt_overflow, like a hot key), record =
-//         h's low K - b1 bits above the 16-bit offset in the chunk;
+// stores never fill a line.  Here the records are partitioned twice, each pass writing
+// whole runs:
+//   part: per chunk of kPartChunk pairs, the records sorted in LDS by 2^b1 coarse
+//         buckets (h's top bits; ~64 records per bucket at b1 = 8) and written back
+//         contiguously at the chunk's slot, with the chunk's run table rt[chunk][0..2^b1]
+//         (no count matrix, no scan, no capacity to overflow); record = h's low K - b1
+//         bits above the 14-bit offset in the chunk;
 //   fine: per slice of SC (a power of two) consecutive chunks of one coarse bucket
-//         (<= kFineCap records in LDS), an LDS counting sort by the next b2 bits; records
-//         become h's low K - b1 - b2 bits above the P = log2(SC) + 16-bit position within
-//         the slice, written back contiguous with the slice's fine offsets;
+//         (<= kFineCap records in LDS), its runs gathered and counting-sorted in LDS by
+//         the next b2 bits; records become h's low K - b1 - b2 bits above the
+//         P = log2(SC) + 14-bit position within the slice, written back contiguously
+//         with the slice's fine offsets;
 //   dedupe: one workgroup per fine bucket, reading its run in each slice of its coarse
 //         bucket; position = slice start + the record's field (no search).
-constexpr int kFineCap = 16384;         // records per fine-pass slice (128 KB of LDS)
+constexpr int kFineCap = 8192;          // records per fine-pass slice (64 KB of LDS: two workgroups per CU)
 constexpr int kFineItems = kFineCap / kBktThreads;
 constexpr int kFineMaxB2 = 8;           // fine buckets per coarse bucket <= 256
-constexpr u32 kPartMaxB1 = 8;           // coarse buckets <= 256 (runs of >= 256 records per chunk)
+constexpr u32 kPartMaxB1 = 8;           // coarse buckets <= 256
+constexpr u32 kPartLog = 14;
+constexpr u64 kPartChunk = u64(1) << kPartLog;   // pairs per part chunk (its records fill 128 KB of LDS)
+constexpr int kPartItems = int(kPartChunk / kBktThreads);
 
 struct Bkt2Plan {
   PackedTab T;
-  u32 K, b1, b2, P;    // key bits, coarse / fine bucket bits, position-in-slice bits (log2(SC) + 16)
-  u32 segcap;          // records per [chunk][coarse] segment
+  u32 K, b1, b2, P;    // key bits, coarse / fine bucket bits, position-in-slice bits (log2(SC) + 14)
   u32 SC, nslice;      // chunks per fine slice, slices per coarse bucket
-  u64 G;               // chunks
+  u64 G;               // part chunks
 };
 
-[[maybe_unused]] static __global__ __launch_bounds__(kBktThreads) void k_bkt_part(
-    const u32* __restrict__ in, u64 n, u64 p, const unsigned char* __restrict__ prev_nf,
-    const unsigned char* __restrict__ prev_multi, Bkt2Plan bp, u64* __restrict__ seg, u32* __restrict__ segcnt,
-    u32* __restrict__ rec, Header* __restrict__ hdr, const u64* prev_count, u64* __restrict__ stats) {
-  if (bkt_skip(hdr, prev_count, n)) return;
-  __shared__ u32 cur[1u << kPartMaxB1];
-  __shared__ u32 s_hashed;
-  const u32 nb1 = 1u << bp.b1;
-  for (u32 q = threadIdx.x; q < nb1; q += kBktThreads) cur[q] = 0;
-  if (threadIdx.x == 0) s_hashed = 0;
-  __syncthreads();
-  const u64 g = bkt_chunk(bp.G), j0 = g * kBktChunk;
-  const u32 sh1 = bp.K - bp.b1;
-  const u64 lowmask = sh1 >= 64 ? ~0ull : (1ull << sh1) - 1;
-  u64* segs = seg + g * nb1 * u64(bp.segcap);
-  BktPlan kp{bp.T, bp.K, bp.b1};
-  u32 hashed = 0;
-  bool over = false;
-#pragma unroll 4
-  for (int e = 0; e < kBktItems; ++e) {
-    const u64 j = j0 + u64(e) * kBktThreads + threadIdx.x;
-    if (j >= p) break;
-    u64 key;
-    u32 bits;
-    if (bkt_pair(in, n, j, prev_nf, prev_multi, kp, key, bits)) {
-      const u32 c = bp.b1 ? u32(key >> sh1) : 0u;
-      const u32 d = atomicAdd(&cur[c], 1u);
-      if (d < bp.segcap) segs[u64(c) * bp.segcap + d] = ((key & lowmask) << kBktRP) | (j - j0);
-      else over = true;
-      ++hashed;
-    }
-    rec[j] = bits;
-  }
-  if (over) hdr->bkt_overflow = 1;
-  const u64 wsum = wave_sum(u64(hashed));
-  if ((threadIdx.x & 63) == 0 && wsum) atomicAdd(&s_hashed, u32(wsum));
-  __syncthreads();
-  for (u32 q = threadIdx.x; q < nb1; q += kBktThreads) segcnt[g * nb1 + q] = min(cur[q], bp.segcap);
-  if (threadIdx.x == 0 && s_hashed)
-    atomicAdd(&stats[(blockIdx.x & (kStatShards - 1)) * kStatStride + 1], u64(s_hashed));
-}
-
-// One workgroup per (coarse bucket, slice): out region (c * nslice + s) * kFineCap,
-// fine offsets fo[(c * nslice + s) * (2^b2 + 1) + f].
-[[maybe_unused]] static __global__ __launch_bounds__(kBktThreads) void k_bkt_fine(
-    const u64* __restrict__ seg, const u32* __restrict__ segcnt, Bkt2Plan bp, u64* __restrict__ out,
-    u32* __restrict__ fo, Header* __restrict__ hdr, const u64* prev_count, u64 n) {
-  if (bkt_skip(hdr, prev_count, n)) return;
-  extern __shared__ u64 stage[];   // kFineCap records (dynamic)
-  __shared__ u32 s_pre[65];        // segment prefix (SC <= 64)
-  __shared__ u32 hist[1u << kFineMaxB2], base[(1u << kFineMaxB2) + 1];
-  const u32 nb1 = 1u << bp.b1, nb2 = 1u << bp.b2;
-  const u32 c = blockIdx.x / bp.nslice, sl = blockIdx.x % bp.nslice;
-  const u64 g0 = u64(sl) * bp.SC;
-  const u32 nsc = u32(g0 + bp.SC <= bp.G ? bp.SC : bp.G - g0);
-  if (threadIdx.x < 64) {   // segment counts: one per lane, a wave scan (nsc <= 64)
+// Exclusive prefix of n <= 256 LDS counters in place (one wave, 4 per lane); c[n] = the total.
+__device__ __forceinline__ void lds_excl256(u32* c, u32 n) {
+  if (threadIdx.x < 64) {
     const u32 lane = threadIdx.x;
-    const u32 v = lane < nsc ? segcnt[(g0 + lane) * nb1 + c] : 0u;
-    u32 inc = v;
+    u32 v[4], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const u32 i = lane * 4 + k;
+      v[k] = i < n ? c[i] : 0u;
+      sum += v[k];
+    }
+    u32 inc = sum;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const u32 y = __shfl_up(inc, o, 64);
       if (int(lane) >= o) inc += y;
     }
-    if (lane < nsc) s_pre[lane] = inc - v;
-    if (lane == nsc - 1) s_pre[nsc] = inc;
+    u32 run = inc - sum;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const u32 i = lane * 4 + k;
+      if (i < n) c[i] = run;
+      run += v[k];
+    }
+    if (lane == 63) c[n] = inc;
+  }
+}
+
+[[maybe_unused]] static __global__ __launch_bounds__(kBktThreads) void k_bkt_part(
+    const u32* __restrict__ in, u64 n, u64 p, const unsigned char* __restrict__ prev_nf,
+    const unsigned char* __restrict__ prev_multi, Bkt2Plan bp, u64* __restrict__ seg, u32* __restrict__ rt,
+    u32* __restrict__ rec, Header* __restrict__ hdr, const u64* prev_count, u64* __restrict__ stats) {
+  if (bkt_skip(hdr, prev_count, n)) return;
+  extern __shared__ u64 stage[];   // kPartChunk records (dynamic)
+  __shared__ u32 cur[(1u << kPartMaxB1) + 1];
+  const u32 nb1 = 1u << bp.b1;
+  for (u32 q = threadIdx.x; q <= nb1; q += kBktThreads) cur[q] = 0;
+  __syncthreads();
+  const u64 g = bkt_chunk(bp.G), j0 = g * kPartChunk;
+  const u32 sh1 = bp.K - bp.b1;
+  const u64 lowmask = sh1 >= 64 ? ~0ull : (1ull << sh1) - 1;
+  BktPlan kp{bp.T, bp.K, bp.b1};
+  u64 r[kPartItems];
+  u32 slot[kPartItems];   // coarse bucket << 16 | rank in it; ~0: not hashed
+  u32 hashed = 0;
+#pragma unroll
+  for (int e = 0; e < kPartItems; ++e) {
+    const u64 j = j0 + u64(e) * kBktThreads + threadIdx.x;
+    slot[e] = ~0u;
+    if (j >= p) continue;
+    u64 key;
+    u32 bits;
+    if (bkt_pair(in, n, j, prev_nf, prev_multi, kp, key, bits)) {
+      const u32 c = bp.b1 ? u32(key >> sh1) : 0u;
+      r[e] = ((key & lowmask) << kPartLog) | (j - j0);
+      slot[e] = (c << 16) | atomicAdd(&cur[c], 1u);
+      ++hashed;
+    }
+    rec[j] = bits;
+  }
+  __syncthreads();
+  lds_excl256(cur, nb1);
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < kPartItems; ++e)
+    if (slot[e] != ~0u) stage[cur[slot[e] >> 16] + (slot[e] & 0xffffu)] = r[e];
+  __syncthreads();
+  const u32 total = cur[nb1];
+  u64* out = seg + g * kPartChunk;
+  for (u32 i = threadIdx.x; i < total; i += kBktThreads) out[i] = stage[i];
+  u32* rts = rt + g * (nb1 + 1);
+  for (u32 q = threadIdx.x; q <= nb1; q += kBktThreads) rts[q] = cur[q];
+  const u64 wsum = wave_sum(u64(hashed));
+  if ((threadIdx.x & 63) == 0 && wsum)   // second word of each shard line: bucketed pairs
+    atomicAdd(&stats[(blockIdx.x & (kStatShards - 1)) * kStatStride + 1], wsum);
+}
+
+// One workgroup per (coarse bucket, slice): out region (c * nslice + s) * kFineCap,
+// fine offsets fo[(c * nslice + s) * (2^b2 + 1) + f].
+[[maybe_unused]] static __global__ __launch_bounds__(kBktThreads) void k_bkt_fine(
+    const u64* __restrict__ seg, const u32* __restrict__ rt, Bkt2Plan bp, u64* __restrict__ out,
+    u32* __restrict__ fo, Header* __restrict__ hdr, const u64* prev_count, u64 n) {
+  if (bkt_skip(hdr, prev_count, n)) return;
+  extern __shared__ u64 stage[];   // kFineCap records (dynamic)
+  __shared__ u32 s_pre[129], s_beg[128];   // runs of the slice's chunks (SC <= 128)
+  __shared__ u32 s_w[2];
+  __shared__ u32 hist[(1u << kFineMaxB2) + 1];
+  const u32 nb1 = 1u << bp.b1, nb2 = 1u << bp.b2;
+  const u32 c = blockIdx.x / bp.nslice, sl = blockIdx.x % bp.nslice;
+  const u64 g0 = u64(sl) * bp.SC;
+  const u32 nsc = u32(g0 + bp.SC <= bp.G ? bp.SC : bp.G - g0);
+  {   // run (chunk g0 + t, bucket c): one lane each, a two-wave scan of the lengths
+    const u32 t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    u32 len = 0;
+    if (t < nsc) {
+      const u32* q = rt + (g0 + t) * (nb1 + 1) + c;
+      s_beg[t] = q[0];
+      len = q[1] - q[0];
+    }
+    u32 inc = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const u32 y = __shfl_up(inc, o, 64);
+      if (int(lane) >= o) inc += y;
+    }
+    if (wave < 2 && lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    const u32 pre = wave == 1 ? s_w[0] : 0u;
+    if (t < nsc) s_pre[t] = pre + inc - len;
+    if (t == nsc - 1) s_pre[nsc] = pre + inc;
   }
   for (u32 q = threadIdx.x; q < nb2; q += kBktThreads) hist[q] = 0;
   __syncthreads();
   const u32 total = s_pre[nsc];
   u32* fos = fo + u64(blockIdx.x) * (nb2 + 1);
-  if (total > u32(kFineCap)) {
+  if (total > u32(kFineCap)) {   // a hot key the probe missed: the table path handles this data
     if (threadIdx.x == 0) hdr->bkt_overflow = 1;
     for (u32 q = threadIdx.x; q <= nb2; q += kBktThreads) fos[q] = 0;
     return;
@@ -1283,33 +1331,26 @@ struct Bkt2Plan {
     const u32 i = u32(e) * kBktThreads + threadIdx.x;
     slot[e] = ~0u;
     if (i >= total) continue;
-    u32 s = 0, hi = nsc - 1;   // segment of record i: the last s with s_pre[s] <= i
+    u32 s = 0, hi = nsc - 1;   // run of record i: the last s with s_pre[s] <= i
     while (s < hi) {
       const u32 mid = (s + hi + 1) >> 1;
       if (s_pre[mid] <= i) s = mid;
       else hi = mid - 1;
     }
-    const u64 v = seg[((g0 + s) * nb1 + c) * u64(bp.segcap) + (i - s_pre[s])];
-    const u64 key = v >> kBktRP;   // K - b1 bits
-    const u64 pos = (u64(s) << kBktRP) | (v & ((1u << kBktRP) - 1));   // within the slice
+    const u64 v = seg[(g0 + s) * kPartChunk + s_beg[s] + (i - s_pre[s])];
+    const u64 key = v >> kPartLog;   // K - b1 bits
+    const u64 pos = (u64(s) << kPartLog) | (v & (kPartChunk - 1));   // within the slice
     const u32 f = bp.b2 ? u32(key >> sh2) : 0u;
     r[e] = ((key & keep) << bp.P) | pos;
     slot[e] = (f << 16) | atomicAdd(&hist[f], 1u);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    u32 run = 0;
-    for (u32 f = 0; f < nb2; ++f) {
-      base[f] = run;
-      run += hist[f];
-    }
-    base[nb2] = run;
-  }
+  lds_excl256(hist, nb2);
   __syncthreads();
 #pragma unroll
   for (int e = 0; e < kFineItems; ++e)
-    if (slot[e] != ~0u) stage[base[slot[e] >> 16] + (slot[e] & 0xffffu)] = r[e];
-  for (u32 q = threadIdx.x; q <= nb2; q += kBktThreads) fos[q] = base[q];
+    if (slot[e] != ~0u) stage[hist[slot[e] >> 16] + (slot[e] & 0xffffu)] = r[e];
+  for (u32 q = threadIdx.x; q <= nb2; q += kBktThreads) fos[q] = hist[q];
   __syncthreads();
   u64* o = out + u64(blockIdx.x) * kFineCap;
   for (u32 i = threadIdx.x; i < total; i += kBktThreads) o[i] = stage[i];
@@ -1378,7 +1419,7 @@ struct Bkt2Plan {
     }
     const u64 v = recs[u64(c * ns + lo) * kFineCap + s_beg[lo] + (i - s_pre[lo])];
     key[e] = v >> bp.P;
-    pos[e] = u32(u64(lo) * bp.SC * kBktChunk + (v & pmask));
+    pos[e] = u32(u64(lo) * bp.SC * kPartChunk + (v & pmask));
   }
 #pragma unroll
   for (int e = 0; e < kBktCapItems; ++e) {
