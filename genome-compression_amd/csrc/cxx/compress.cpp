@@ -2,7 +2,9 @@
 // MI355X build.  Same flags, messages, exit codes, report and --statistics
 // CSV (dna_size,width,ratio,original,compressed,t_build_ms,t_sort_ms,t_total_ms;
 // compress.cpp:71-79); the .dag output is byte-identical to the reference's.
-// GPU selection: GCZ_DEVICE (default 0).
+// GPU selection: GCZ_DEVICE (default 0); --gpus=N spreads the build over N GPUs
+// (shared_tree_on_gpus, include/shared_tree.h).
+#include <algorithm>
 #include <array>
 #include <chrono>
 #include <cstdlib>
@@ -87,13 +89,15 @@ void print_help() {
             << "\t--no-save\t\tDo not save the compressed file\n"
             << "\t--output=<file>\t\tWrite output to <file>, default being <input>.dag\n"
             << "\t--histogram=<file>\tSave histogram of node references in tree to <file>\n"
-            << "\t--dna-size=<size>\tThe number of nucleotides stored per leaf node, default is 12\n";
+            << "\t--dna-size=<size>\tThe number of nucleotides stored per leaf node, default is 12\n"
+            << "\t--gpus=<n>\t\tBuild on n GPUs (GCZ_DEVICE onwards), default is 1\n";
 }
 
 auto parse_commands(int argc, char* argv[]) {   // compress.cpp:95-165
   std::filesystem::path input, output, histogram;
   bool verbose = false, statistics = false, save = true;
   std::size_t dna_size = 12;
+  int gpus = 1;
   if (argc == 1) {
     std::cout << "Invalid command: argument <file> required.\n";
     std::cout << "Use --help for more information\n";
@@ -114,6 +118,8 @@ auto parse_commands(int argc, char* argv[]) {   // compress.cpp:95-165
       histogram = a.substr(12);
     } else if (a == "--no-save") {
       save = false;
+    } else if (a.substr(0, 7) == "--gpus=") {
+      gpus = std::max(1, std::atoi(std::string(a.substr(7)).c_str()));
     } else if (a.substr(0, 11) == "--dna-size=") {
       a.remove_prefix(11);
       std::cout << a << '\n';
@@ -140,13 +146,13 @@ auto parse_commands(int argc, char* argv[]) {   // compress.cpp:95-165
     output = input;
     output.replace_extension(".dag");
   }
-  return std::tuple{input, output, histogram, verbose, statistics, dna_size};
+  return std::tuple{input, output, histogram, verbose, statistics, dna_size, gpus};
 }
 
 }  // namespace
 
 int main(int argc, char* argv[]) {
-  auto [input, output, histogram, verbose, statistics, dna_size] = parse_commands(argc, argv);
+  auto [input, output, histogram, verbose, statistics, dna_size, gpus] = parse_commands(argc, argv);
   dna::size(dna_size);
   if (!std::filesystem::is_regular_file(input)) {
     std::cout << "Invalid filename: " << input << '\n';
@@ -156,7 +162,7 @@ int main(int argc, char* argv[]) {
   if (verbose) print_input(input, original_size);
 
   auto start = std::chrono::high_resolution_clock::now();
-  auto compressed = shared_tree{input};
+  auto compressed = gpus > 1 ? shared_tree_on_gpus(input, gpus) : shared_tree{input};
   auto end = std::chrono::high_resolution_clock::now();
   const auto construction = std::chrono::duration_cast<std::chrono::milliseconds>(end - start);
 

@@ -16,7 +16,14 @@
 #include <sstream>
 #include <thread>
 
+#include <sys/mman.h>
+#include <sys/wait.h>
 #include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cctype>
+#include <string_view>
 
 #include "gcz.h"
 #include "../gcz_internal.h"
@@ -267,6 +274,167 @@ auto tree_constructor::reduce(fasta_reader& file, bool verbose) -> pointer {   /
   if (verbose) std::cout << "\rConstructing subtrees: done.\n\rCombining subtrees: done.\n";
   roots.assign(1, parent.root);
   return parent.root;
+}
+
+// ---- multi-GPU construction (compress --gpus=N) ------------------------------------
+namespace {
+
+struct MultiShared {            // head of the shared result region
+  std::atomic<int> status[64];  // per rank: 0 running, 1 done, 2 failed
+  gcz_info info;                // rank 0's whole-tree summary
+};
+
+// first byte of [0, n) that is not one of the 16 symbols (any case), or n; threads
+std::uint64_t first_unknown(const std::uint8_t* b, std::uint64_t n) {
+  static const auto ok = [] {
+    std::array<bool, 256> t{};
+    for (char c : std::string_view{"SACRGBNKTWVDYHM-"}) {
+      t[static_cast<unsigned char>(c)] = true;
+      t[static_cast<unsigned char>(std::tolower(c))] = true;
+    }
+    return t;
+  }();
+  const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<std::uint64_t> first(T, n);
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < T; ++t)
+    th.emplace_back([&, t] {
+      const std::uint64_t a = n * t / T, e = n * (t + 1) / T;
+      for (std::uint64_t i = a; i < e; ++i)
+        if (!ok[b[i]]) { first[t] = i; return; }
+    });
+  for (auto& x : th) x.join();
+  return *std::min_element(first.begin(), first.end());
+}
+
+[[noreturn]] void rank_fail(MultiShared* ms, int rank, const char* what, int rc, gcz_ctx* c) {
+  std::cerr << "libgcz rank " << rank << ": " << what << " failed (code " << rc << ")"
+            << (c ? std::string(": ") + gcz_ctx_last_error(c) : std::string()) << '\n';
+  ms->status[rank].store(2);
+  std::_Exit(1);
+}
+
+}  // namespace
+
+auto shared_tree_on_gpus(const std::filesystem::path& path, int gpus) -> shared_tree {
+  const int L = int(dna::size());
+  fasta_reader f{path};
+  // the FASTA contract on the host (gcz_fasta_extract), into memory the ranks share
+  const std::uint64_t fsz = f.raw_size();
+  auto* bases = static_cast<std::uint8_t*>(
+      ::mmap(nullptr, fsz + 16, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0));
+  if (bases == MAP_FAILED) { std::cerr << "libgcz: no memory for the bases\n"; std::exit(1); }
+  const std::uint64_t nb = fsz ? gcz_fasta_extract(f.raw_data(), fsz, L, 0, bases) : 0;
+  const std::uint64_t S = nb / std::uint64_t(L);
+  if (S == 0) {
+    std::cerr << "Genome shorter than one strand of " << dna::size() << " nucleotides, aborting...\n";
+    std::exit(1);
+  }
+  if (const auto bad = first_unknown(bases, S * L); bad < S * L)   // to_nac's message and exit(1)
+    (void)dna{std::string_view{reinterpret_cast<const char*>(bases + bad), 1}};
+  gpus = std::max(1, std::min(gpus, 64));
+  // layer slots: every layer's ids are < its pair count
+  std::vector<std::uint64_t> loff{0};
+  for (std::uint64_t n = S;;) {
+    const std::uint64_t p = (n + 1) / 2;
+    loff.push_back(loff.back() + p);
+    if (p == 1) break;
+    n = p;
+  }
+  const std::size_t head = (sizeof(MultiShared) + 4095) / 4096 * 4096;
+  const std::size_t rbytes = head + S * 8 + loff.back() * 8;
+  auto* region = static_cast<char*>(::mmap(nullptr, rbytes, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0));
+  if (region == MAP_FAILED) { std::cerr << "libgcz: no memory for the results\n"; std::exit(1); }
+  auto* ms = new (region) MultiShared{};
+  auto* out_leaves = reinterpret_cast<std::uint64_t*>(region + head);
+  auto* out_nodes = reinterpret_cast<std::uint32_t*>(region + head + S * 8);
+  const bool shm = [] {
+    const char* t = std::getenv("GCZ_MULTI_TRANSPORT");
+    return t && std::string_view{t} == "shm";
+  }();
+  const char* dv = std::getenv("GCZ_DEVICE");
+  const int dev0 = dv ? std::atoi(dv) : 0;
+  const std::string shm_name = "/gcz_compress_" + std::to_string(::getpid());
+  // ranks 1.. are forked before this process touches the device; the RCCL id goes over pipes
+  std::vector<int> wr(gpus, -1);
+  std::vector<pid_t> kids;
+  int rank = 0, rd = -1;
+  for (int r = 1; r < gpus; ++r) {
+    int fd[2];
+    if (::pipe(fd) != 0) { std::cerr << "libgcz: pipe failed\n"; std::exit(1); }
+    const pid_t pid = ::fork();
+    if (pid < 0) { std::cerr << "libgcz: fork failed\n"; std::exit(1); }
+    if (pid == 0) {
+      rank = r;
+      rd = fd[0];
+      ::close(fd[1]);
+      for (int q = 1; q < r; ++q) ::close(wr[q]);
+      break;
+    }
+    ::close(fd[0]);
+    wr[r] = fd[1];
+    kids.push_back(pid);
+  }
+  gcz_ctx* ctx = nullptr;
+  int rc = gcz_ctx_create(shm ? dev0 : dev0 + rank, &ctx);
+  if (rc) rank_fail(ms, rank, "device context", rc, nullptr);
+  gcz_group* g = nullptr;
+  if (shm) {
+    rc = gcz_group_create_shm(ctx, rank, gpus, shm_name.c_str(), (S / std::uint64_t(gpus) + 1) * 64 + (64u << 20), &g);
+  } else {
+    unsigned char id[128] = {};
+    if (rank == 0) {
+      if ((rc = gcz_dist_unique_id(id, sizeof id))) rank_fail(ms, 0, "RCCL unique id", rc, ctx);
+      for (int r = 1; r < gpus; ++r)
+        if (::write(wr[r], id, sizeof id) != ssize_t(sizeof id)) rank_fail(ms, 0, "id pipe", -1, ctx);
+    } else if (::read(rd, id, sizeof id) != ssize_t(sizeof id)) {
+      rank_fail(ms, rank, "id pipe", -1, ctx);
+    }
+    rc = gcz_group_create_rccl(ctx, rank, gpus, id, &g);
+  }
+  if (rc) rank_fail(ms, rank, "group", rc, ctx);
+  std::uint64_t s0 = 0, s1 = 0;
+  gcz_dist_plan(S, gpus, rank, &s0, &s1, nullptr);
+  void* d = gcz_dev_alloc(ctx, (s1 - s0) * std::uint64_t(L) + 16);
+  if (!d) rank_fail(ms, rank, "device allocation", GCZ_ERR_DEVICE, ctx);
+  if ((rc = gcz_memcpy_h2d(ctx, d, bases + s0 * std::uint64_t(L), (s1 - s0) * std::uint64_t(L))))
+    rank_fail(ms, rank, "upload", rc, ctx);
+  const void* dp = d;
+  if ((rc = gcz_group_build_device_bases(g, &dp, S, L))) rank_fail(ms, rank, "build", rc, ctx);
+  gcz_info info{};
+  gcz_group_info(g, &info);
+  for (int layer = -1; layer < info.n_layers; ++layer) {   // the rank's slices into place
+    std::uint64_t off = 0, cnt = 0;
+    gcz_group_slice(g, 0, layer, &off, &cnt);
+    void* dst = layer < 0 ? static_cast<void*>(out_leaves + off) : static_cast<void*>(out_nodes + 2 * (loff[layer] + off));
+    if (cnt && (rc = gcz_group_copy_slice(g, 0, layer, dst))) rank_fail(ms, rank, "slice copy", rc, ctx);
+  }
+  if (rank == 0) ms->info = info;
+  gcz_dev_free(ctx, d);
+  gcz_group_destroy(g);
+  gcz_ctx_destroy(ctx);
+  ms->status[rank].store(1);
+  if (rank != 0) std::_Exit(0);
+  bool ok = true;
+  for (pid_t pid : kids) {
+    int st = 0;
+    if (::waitpid(pid, &st, 0) != pid || !WIFEXITED(st) || WEXITSTATUS(st) != 0) ok = false;
+  }
+  for (int r = 1; r < gpus; ++r) ::close(wr[r]);
+  if (!ok) { std::cerr << "libgcz: a rank of the multi-GPU build failed\n"; std::exit(1); }
+  shared_tree t;
+  const gcz_info& in = ms->info;
+  t.leaves.resize(in.n_leaves);
+  std::memcpy(t.leaves.data(), out_leaves, in.n_leaves * 8);
+  t.nodes.resize(in.n_layers);
+  for (int k = 0; k < in.n_layers; ++k) {
+    t.nodes[k].resize(in.layer_size[k]);
+    std::memcpy(static_cast<void*>(t.nodes[k].data()), out_nodes + 2 * loff[k], in.layer_size[k] * 8);
+  }
+  t.root = pointer::from_word(in.root);
+  ::munmap(region, rbytes);
+  ::munmap(bases, fsz + 16);
+  return t;
 }
 
 void shared_tree::build_from_gpu() {

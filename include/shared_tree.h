@@ -237,6 +237,7 @@ class shared_tree {
 
  private:
   friend class tree_constructor;
+  friend auto shared_tree_on_gpus(const std::filesystem::path& path, int gpus) -> shared_tree;
   void build_from_gpu();   // copies the last libgcz build of this thread into the containers
   bool on_device() const;  // the engine's device arrays still hold exactly this tree
 
@@ -259,6 +260,14 @@ inline auto operator<<(std::ostream& os, const shared_tree& tree) -> std::ostrea
   }
   return os;
 }
+
+/* Beyond the reference surface (compress --gpus=N): the construction of a FASTA file
+ * spread over `gpus` devices GCZ_DEVICE .. GCZ_DEVICE + gpus - 1, one process per GPU
+ * (this process and gpus - 1 children forked before any device work), strand ranges per
+ * rank and owner-hashed exchanges over RCCL; the slices meet in
+ * shared memory and the result equals shared_tree{path}.  GCZ_MULTI_TRANSPORT=shm runs
+ * every rank on GCZ_DEVICE with host-staged exchanges (testing on one GPU). */
+auto shared_tree_on_gpus(const std::filesystem::path& path, int gpus) -> shared_tree;
 
 /******************************************************************************
  * tree_constructor (reference include/shared_tree.h:245-316, src/shared_tree.cpp:617-763).

@@ -74,3 +74,32 @@ def test_compress_cli_errors(tmp_path, manifest):
     exp = manifest["fasta/crlf"]["expect"]
     r = _compress(["--no-save", os.path.join(GOLDEN, "fasta", "crlf.fa")], str(tmp_path))
     assert r.returncode == 1 and r.stderr.strip() == exp["stderr"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gpus", [2, 3])
+@pytest.mark.parametrize("name", ["chmpxx", "merged"])
+def test_compress_cli_gpus(name, gpus, tmp_path, manifest):
+    """compress --gpus=N (shared_tree_on_gpus): N processes, one rank each; on the one-GPU
+    box every rank shares the device and exchanges host-staged (GCZ_MULTI_TRANSPORT=shm).
+    Same .dag and statistics as the reference."""
+    exp = manifest[f"corpus/{name}"]["expect"]
+    out = tmp_path / f"{name}.dag"
+    env = dict(os.environ, GCZ_MULTI_TRANSPORT="shm")
+    exe = os.path.join(PKG, "compress")
+    r = subprocess.run([exe, "--statistics", f"--gpus={gpus}", f"--output={out}", os.path.join(GOLDEN, "data", name)],
+                       capture_output=True, text=True, cwd=str(tmp_path), env=env, timeout=240)
+    assert r.returncode == 0, r.stderr
+    f = r.stdout.strip().split(",")
+    assert int(f[1]) == exp["width"] and f[2] == exp["ratio"] and int(f[4]) == exp["bytes"]
+    assert hashlib.sha256(out.read_bytes()).hexdigest() == exp["sha_dag"]
+
+
+@pytest.mark.gpu
+def test_compress_cli_gpus_errors(tmp_path, manifest):
+    exp = manifest["fasta/bad_symbol"]["expect"]
+    env = dict(os.environ, GCZ_MULTI_TRANSPORT="shm")
+    r = subprocess.run([os.path.join(PKG, "compress"), "--no-save", "--gpus=2",
+                        os.path.join(GOLDEN, "fasta", "bad_symbol.fa")], capture_output=True, text=True,
+                       cwd=str(tmp_path), env=env, timeout=240)
+    assert r.returncode == 1 and r.stderr.strip() == exp["stderr"]
