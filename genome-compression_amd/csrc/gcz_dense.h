@@ -457,7 +457,7 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
   const u32 n = u32(P.S - c0 < u64(kDC) ? P.S - c0 : u64(kDC));
   chunk_runs(off, P, ch, s_base, s_dst, s_tmp);
   const int lane = tid & 63, wave = tid >> 6;
-  constexpr int RW = 4;   // runs per wave step (2 loads each in flight per lane)
+  constexpr int RW = 8;   // runs per wave step (2 loads each in flight per lane)
   for (u32 b0 = wave; b0 < P.NB; b0 += (kDThreads / 64) * RW) {
     u32 x[RW], id[RW], dst[RW], len[RW];
 #pragma unroll

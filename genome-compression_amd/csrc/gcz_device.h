@@ -738,11 +738,17 @@ __device__ __forceinline__ u32 zero_bytes(u32 x) {   // bytes of x equal to 0 (=
   return u32(__popc(~t & 0x80808080u));
 }
 
-template <int ITEMS>
+struct NoPrefetch {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+// after_marks() runs once the tile's marks are read and before the scan waits: loads
+// issued there (e.g. the first occurrences' input pairs) overlap the look-back.
+template <int ITEMS, class AfterMarks = NoPrefetch>
 __device__ __forceinline__ void tile_scan(TileScan<ITEMS>& ts, u32* s_tile, u32* s_pre,
                                           const unsigned char* __restrict__ nf, u64 j0, u64 p, u64 id0,
                                           u64* __restrict__ desc, u32* __restrict__ ticket,
-                                          u64* __restrict__ count_out) {
+                                          u64* __restrict__ count_out, AfterMarks after_marks = {}) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool direct = desc == nullptr;
   if (tid == 0) *s_tile = direct ? 0u : atomicAdd(ticket, 1u);
@@ -768,6 +774,7 @@ __device__ __forceinline__ void tile_scan(TileScan<ITEMS>& ts, u32* s_tile, u32*
     ts.mask[e] = __ballot(first);
     if (lane == 0) s_pre[e * 4 + wave] = u32(__popcll(ts.mask[e]));
   }
+  after_marks();
   __syncthreads();
   constexpr int NG = 4 * ITEMS;             // 64-element groups per tile
   constexpr int PER = (NG + 63) / 64;        // groups per lane of the scanning wave
