@@ -80,6 +80,7 @@ int gcz_ctx::leaf_level(const LeafLevel& a, Header* d_hdr) {
     lt.pt.kmask >>= 2;                   // the key itself has 4L bits
     lt.pt.sh = (4 * u32(L) + 1) / 2;
   }
+  fused_leaf = lt;
   unsigned char* d_nf = nf_set[0];
   hipEvent_t e0{};
   if (a.c_begin == 0 && !a.precleared) {
@@ -110,10 +111,13 @@ int gcz_ctx::leaf_level(const LeafLevel& a, Header* d_hdr) {
                          d_nf, d_hdr);
     }
     HIP_TRY(hipGetLastError());
-    if (c == 0) {   // repetitive data? (switches the node inserts' LDS pre-dedupe)
+    // repetitive data? (switches the node inserts' LDS pre-dedupe; a small build's node
+    // levels gain nothing from it: no probe there, predup stays off unless forced)
+    if (c == 0 && (predup_mode != 0 || a.S >= kDupProbeMin)) {
       const u64 ip = std::min(i1, i0 + (u64(1) << 21));   // a sample of up to 2^21 strands is enough
-      hipLaunchKernelGGL(k_dup_probe, dim3(unsigned((ip - i0 + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, A,
-                         i0, ip, d_hdr);
+      if (predup_mode == 0)
+        hipLaunchKernelGGL(k_dup_probe, dim3(unsigned((ip - i0 + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                           A, i0, ip, d_hdr);
       hipLaunchKernelGGL(k_dup_decide, dim3(1), dim3(1), 0, stream, d_hdr, ip - i0, u32(predup_mode));
     }
     prof_end(KID_LEAF, e0);
@@ -127,14 +131,17 @@ int gcz_ctx::leaf_level(const LeafLevel& a, Header* d_hdr) {
                      ldesc, &a.ticket[c], a.out, id0, &a.count[c])
     if (lt.packed) {
       if (tile == u64(kTile)) GCZ_FLAGSCAN_LEAF(PackedTab, lt.pt, kItems);
-      else GCZ_FLAGSCAN_LEAF(PackedTab, lt.pt, kItemsSmall);
+      else if (tile == u64(kTileSmall)) GCZ_FLAGSCAN_LEAF(PackedTab, lt.pt, kItemsSmall);
+      else GCZ_FLAGSCAN_LEAF(PackedTab, lt.pt, kItemsTiny);
     } else {
       if (tile == u64(kTile)) GCZ_FLAGSCAN_LEAF(WideTab, lt.wt, kItems);
-      else GCZ_FLAGSCAN_LEAF(WideTab, lt.wt, kItemsSmall);
+      else if (tile == u64(kTileSmall)) GCZ_FLAGSCAN_LEAF(WideTab, lt.wt, kItemsSmall);
+      else GCZ_FLAGSCAN_LEAF(WideTab, lt.wt, kItemsTiny);
     }
 #undef GCZ_FLAGSCAN_LEAF
     HIP_TRY(hipGetLastError());
     prof_end(KID_FLAGSCAN_LEAF, e0);
+    if (a.defer_resolve && c + 1 == C) break;   // settled by level 0's insert (fused small build)
     prof_begin(KID_RESOLVE_LEAF, e0);
     if (lt.packed)
       hipLaunchKernelGGL((k_resolve_leaf<PackedTab>), g, dim3(kBlock), 0, stream, A, i0, i1, lt.pt, d_nf);
@@ -306,16 +313,17 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   if (p == 0) return GCZ_OK;
   const u64 cap = node_cap(p);
   const u32 Bk = std::max<u32>(1, bit_width(a.bound));
-  const LevelTab nt = plan_table(tab.ptr, cap, 2 * (Bk + 3), p, Bk, allow_packed, kMaxProbe);
+  const LevelTab nt = plan_table(a.fused ? a.ftab : tab.ptr, cap, 2 * (Bk + 3), p, Bk, allow_packed, kMaxProbe);
   const int cur = (a.k + 1) & 1, prev = a.k & 1;
   unsigned char* knf = nf_set[cur];
+  u32* in = const_cast<u32*>(a.in);   // (written only by a fused insert, which settles it)
   if (a.direct_known) {   // *pcount == n is set: the insert writes words and nodes, nothing else runs
     hipEvent_t e0{};
     prof_begin(KID_NODE, e0);
     const dim3 gi(unsigned((p + kBlock - 1) / kBlock));
-    hipLaunchKernelGGL((k_node_insert<WideTab>), gi, dim3(kBlock), 0, stream, a.in, n, p, WideTab{}, nullptr, nullptr,
-                       a.words, Marks{knf, multi_set[cur]}, d_hdr, a.pcount, a.out, a.count, a.id_off, stats.as<u64>(),
-                       0u);
+    hipLaunchKernelGGL((k_node_insert<WideTab, NoRes>), gi, dim3(kBlock), 0, stream, in, n, p, WideTab{}, nullptr,
+                       nullptr, a.words, Marks{knf, multi_set[cur]}, d_hdr, a.pcount, a.out, a.count, a.id_off,
+                       stats.as<u64>(), 0u, NoRes{}, FuseIn{});
     HIP_TRY(hipGetLastError());
     prof_end(KID_NODE, e0);
     return GCZ_OK;
@@ -372,16 +380,16 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     HIP_TRY(hipMemsetAsync(bkt_tmp.ptr, 0, t_scan * 8 + 16, stream));
   }
   hipEvent_t e0{};
-  prof_begin(KID_MEMSET, e0);
-  {
+  if (!a.fused) {
+    prof_begin(KID_MEMSET, e0);
     const u64 tab16 = nt.bytes() / 16, p16 = (p + 15) / 16;
     const u64 blocks = std::min<u64>(4096, (std::max(tab16, p16) + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_clear, dim3(unsigned(blocks)), dim3(kBlock), 0, stream, static_cast<uint4*>(tab.ptr),
                        tab16, reinterpret_cast<uint4*>(knf), reinterpret_cast<uint4*>(mk.multi), p16, a.pcount, n,
                        d_hdr, bkt);
     HIP_TRY(hipGetLastError());
+    prof_end(KID_MEMSET, e0);
   }
-  prof_end(KID_MEMSET, e0);
   const dim3 gi(unsigned((p + kBlock - 1) / kBlock));
   if (two) {
     prof_begin(KID_BKT_SCATTER, e0);
@@ -425,26 +433,55 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     prof_end(KID_BKT_DEDUPE, e0);
   }
   prof_begin(KID_NODE, e0);
-  if (nt.packed)
-    hipLaunchKernelGGL((k_node_insert<PackedTab>), gi, dim3(kBlock), 0, stream, a.in, n, p, nt.pt, pnf, pmu,
-                       a.words, mk, d_hdr, a.pcount, a.out, a.count, a.id_off, stats.as<u64>(), bkt);
-  else
-    hipLaunchKernelGGL((k_node_insert<WideTab>), gi, dim3(kBlock), 0, stream, a.in, n, p, nt.wt, pnf, pmu,
-                       a.words, mk, d_hdr, a.pcount, a.out, a.count, a.id_off, stats.as<u64>(), bkt);
+  FuseIn fz{};
+  u64 clr16 = 0;   // fused: marks of the next level, cleared by the flag scan
+  if (a.fused) {
+    if (a.k > 0) {
+      fz.pcount = &d_hdr->count[kLayerSlot + a.k - 1];
+      fz.phashed = &d_hdr->hashed_next[a.k - 1];
+      fz.gate_out = &d_hdr->gate[a.k - 1];
+    }
+    if (a.p_next) {
+      const u32 Bn = std::max<u32>(1, bit_width(p));
+      fz.clear = static_cast<uint4*>(a.ftab_next);
+      fz.clear16 = plan_table(a.ftab_next, node_cap(a.p_next), 2 * (Bn + 3), a.p_next, Bn, allow_packed, kMaxProbe)
+                       .bytes() / 16;
+      clr16 = (a.p_next + 15) / 16;
+    }
+  }
+  auto insert = [&](auto T, auto res) {
+    hipLaunchKernelGGL((k_node_insert<decltype(T), decltype(res)>), gi, dim3(kBlock), 0, stream, in, n, p, T, pnf,
+                       pmu, a.words, mk, d_hdr, a.pcount, a.out, a.count, a.id_off, stats.as<u64>(), bkt, res, fz);
+  };
+  auto insert_settling = [&](auto T) {   // the resolver of the previous level (fused builds)
+    if (!a.fused) insert(T, NoRes{});
+    else if (a.k == 0 && fused_leaf.packed) insert(T, LeafRes<PackedTab>{fused_leaf.pt, nf_set[prev]});
+    else if (a.k == 0) insert(T, LeafRes<WideTab>{fused_leaf.wt, nf_set[prev]});
+    else if (fused_prev.packed) insert(T, NodeRes<PackedTab>{fused_prev.pt, nf_set[prev], d_grp});
+    else insert(T, NodeRes<WideTab>{fused_prev.wt, nf_set[prev], d_grp});
+  };
+  if (nt.packed) insert_settling(nt.pt);
+  else insert_settling(nt.wt);
   HIP_TRY(hipGetLastError());
   prof_end(KID_NODE, e0);
+  if (a.fused) fused_prev = nt;
+  uint4* clr_nf = reinterpret_cast<uint4*>(nf_set[prev]);
+  uint4* clr_mu = reinterpret_cast<uint4*>(multi_set[prev]);
   prof_begin(KID_FLAGSCAN_NODE, e0);
   const u64 tile = scan_tile(p);
   const dim3 gs(unsigned((p + tile - 1) / tile));
   u64* ndesc = p <= kSmallScanMax ? nullptr : a.desc;   // small levels: no look-back chain
-  if (tile == u64(kTile))
-    hipLaunchKernelGGL((k_flagscan_node<kItems>), gs, dim3(kBlock), 0, stream, a.words, p, a.in, n, knf, d_grp,
-                       ndesc, a.ticket, a.out, a.count, a.pcount, mk.multi, a.hashed_next);
-  else
-    hipLaunchKernelGGL((k_flagscan_node<kItemsSmall>), gs, dim3(kBlock), 0, stream, a.words, p, a.in, n, knf, d_grp,
-                       ndesc, a.ticket, a.out, a.count, a.pcount, mk.multi, a.hashed_next);
+  auto flagscan = [&](auto items) {
+    hipLaunchKernelGGL((k_flagscan_node<decltype(items)::value>), gs, dim3(kBlock), 0, stream, a.words, p, a.in, n,
+                       knf, d_grp, ndesc, a.ticket, a.out, a.count, a.pcount, mk.multi, a.hashed_next, clr_nf, clr_mu,
+                       clr16);
+  };
+  if (tile == u64(kTile)) flagscan(std::integral_constant<int, kItems>{});
+  else if (tile == u64(kTileSmall)) flagscan(std::integral_constant<int, kItemsSmall>{});
+  else flagscan(std::integral_constant<int, kItemsTiny>{});
   HIP_TRY(hipGetLastError());
   prof_end(KID_FLAGSCAN_NODE, e0);
+  if (a.fused && !a.fused_last) return GCZ_OK;   // the next level's insert settles the repeats
   prof_begin(KID_RESOLVE_NODE, e0);
   if (nt.packed)
     hipLaunchKernelGGL((k_resolve_node<PackedTab>), gi, dim3(kBlock), 0, stream, a.words, p, nt.pt, knf, d_grp,
@@ -525,6 +562,11 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   // grows the table and rebuilds, counted in info.attempts)
   if (S > (1ull << 22)) leaf_cap = std::min(full_cap, u64(1) << 24);
   if (leaf_cap_log2 > 0 && S > (1ull << 22)) leaf_cap = std::min(full_cap, 1ull << leaf_cap_log2);
+  // small builds: a launch lasts as long as its longest probe chain, so their tables are
+  // sparser (a few MB at most)
+  const bool small = S <= 2 * kDirectCheckMin;
+  if (small) leaf_cap = full_cap << small_cap_shift;
+  cap_boost = small ? small_cap_shift : 0;
   const u64 node_cap0 = node_cap(pk[0]);
 
   int rc;
@@ -554,6 +596,13 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   const bool try_dense = dense_mode != 0 && L <= 12 && (S >= dense_min || dense_mode == 2);
   for (;;) {
     if ((rc = ensure(tab, std::max(leaf_cap, node_cap0) * 16))) return rc;
+    // small build, one leaf chunk, no bucketed level, no host look at a gate: two launches
+    // per node level (FuseIn, gcz_device.h), the node tables in three regions of ftab
+    const bool fused = use_fused && !try_dense && C == 1 && pk[0] < kDirectCheckMin &&
+                       !(bucket_now && pk[0] >= bucket_min) && (S > u64(kTailMaxN) || !use_tail);
+    const u64 fregion = node_cap0 * 16;
+    if (fused && (rc = ensure(ftab, 3 * fregion))) return rc;
+    auto fregion_ptr = [&](int k) { return static_cast<void*>(ftab.as<unsigned char>() + u64(k % 3) * fregion); };
     // One build's launches, start event to header copy.  A build whose launch sequence
     // has no host decision inside (no dense-level fallback check, no look at the direct
     // gate: small genomes) is captured once as a HIP graph and replayed while the shape
@@ -576,7 +625,15 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
           ip.nf = reinterpret_cast<uint4*>(nf_set[0]);
           ip.nnf16 = (S + 15) / 16;
         }
-        const u64 big = std::max<u64>({ip.ndesc16, ip.nstats16, ip.ntab16, ip.nnf16});
+        if (fused) {   // level 0's table and marks
+          const u32 B0 = std::max<u32>(1, bit_width(std::min(S, leaf_cap)));
+          ip.ftab = static_cast<uint4*>(fregion_ptr(0));
+          ip.nftab16 = plan_table(ip.ftab, node_cap0, 2 * (B0 + 3), pk[0], B0, allow_packed, kMaxProbe).bytes() / 16;
+          ip.fnf = reinterpret_cast<uint4*>(nf_set[1]);
+          ip.fmulti = reinterpret_cast<uint4*>(multi_set[1]);
+          ip.nfm16 = (pk[0] + 15) / 16;
+        }
+        const u64 big = std::max<u64>({ip.ndesc16, ip.nstats16, ip.ntab16, ip.nnf16, ip.nftab16, ip.nfm16});
         hipLaunchKernelGGL(k_build_init, dim3(unsigned(std::min<u64>(4096, (big + kBlock - 1) / kBlock))),
                            dim3(kBlock), 0, stream, ip);
         HIP_TRY(hipGetLastError());
@@ -596,6 +653,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       la.ticket = d_hdr->ticket;
       dense_used = false;
       la.precleared = !try_dense;
+      la.defer_resolve = fused;
       if (try_dense) {
         if ((rc = leaf_level_dense(la, d_hdr, &d_hdr->count[C - 1], &dense_used))) return rc;
         if (!dense_used) HIP_TRY(hipMemsetAsync(&d_hdr->dense_fail, 0, 4, stream));
@@ -650,7 +708,14 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
         na.ticket = &d_hdr->ticket[kLayerSlot + k];
         na.hashed_next = &d_hdr->hashed_next[k];   // look-ahead for layer k + 1 (its pairs' children are here)
         na.gate = &d_hdr->gate[k];
-        na.allow_bucket = !table_only;
+        na.allow_bucket = !table_only && !fused;
+        if (fused) {
+          na.fused = true;
+          na.ftab = fregion_ptr(k);
+          na.ftab_next = fregion_ptr(k + 1);
+          na.p_next = k + 1 < D ? pk[k + 1] : 0;
+          na.fused_last = k + 1 == D || (pk[k] <= u64(kTailMaxN) && use_tail);
+        }
         if ((rc = node_level(na, d_hdr))) return rc;
         prev_regular = true;
         std::swap(in, outw);
@@ -682,7 +747,8 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     bool launched = false;
     if (static_seq) {
       const GraphKey key{d_bases, d_leaves, nbases, S, L, leaf_cap, allow_packed, bucket_now, stream,
-                         tab.ptr, wa.ptr, wb.ptr, nodes_out.ptr, leaves_out.ptr, nf.ptr, desc.ptr};
+                         tab.ptr, wa.ptr, wb.ptr, nodes_out.ptr, leaves_out.ptr, nf.ptr, desc.ptr,
+                         fused ? ftab.ptr : nullptr, fused};
       if (graph_exec && key == graph_key) {
         launched = hipGraphLaunch(graph_exec, stream) == hipSuccess;
       } else if (!(key == graph_seen)) {
@@ -807,6 +873,8 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   if (const char* t = std::getenv("GCZ_BUCKET_TWO")) c->two_pass = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_DENSE")) c->dense_mode = std::atoi(t);
   if (const char* t = std::getenv("GCZ_GRAPH")) c->use_graph = std::atoi(t) != 0;
+  if (const char* t = std::getenv("GCZ_FUSED")) c->use_fused = std::atoi(t) != 0;
+  if (const char* t = std::getenv("GCZ_SMALL_CAP_SHIFT")) c->small_cap_shift = std::max(0, std::min(4, std::atoi(t)));
   if (const char* t = std::getenv("GCZ_LEAF_FIRST_LOG2")) c->leaf_first_log2 = std::max(1, std::min(20, std::atoi(t)));
   *out = c;
   return GCZ_OK;

@@ -133,6 +133,13 @@ struct NodeLevel {
   u32* hashed_next = nullptr;       // single-device build: look ahead for the next level (null: off)
   u64* gate = nullptr;              // ... and open its gate (the next level's pcount)
   bool allow_bucket = false;        // single-device build: bucketed insert allowed (overflow -> rebuild)
+  // fused small-build levels (k_node_insert with a resolver, gcz_device.h): this level's
+  // table lives in ftab region k % 3, its repeats are settled by the next level's insert
+  // unless it is the last one before the tail (resolve launched here)
+  bool fused = false, fused_last = false;
+  u64 p_next = 0;                   // the next level's pairs (its table is cleared here)
+  void* ftab = nullptr;             // region base of this level's table
+  void* ftab_next = nullptr;        // ... and of the next level's
 };
 
 // One leaf level (all chunks).
@@ -156,6 +163,7 @@ struct LeafLevel {
   const u64* seed = nullptr;
   u64 seed_n = 0;
   bool precleared = false;          // table and marks already cleared (k_build_init)
+  bool defer_resolve = false;       // fused small build: level 0's insert settles the repeats
 };
 
 }  // namespace gcz_host
@@ -169,11 +177,13 @@ struct GraphKey {
   gcz_host::u64 leaf_cap;
   bool packed, bucket;
   hipStream_t stream;
-  void *tab, *wa, *wb, *nodes, *leaves_out, *nf, *desc;
+  void *tab, *wa, *wb, *nodes, *leaves_out, *nf, *desc, *ftab;
+  bool fused;
   bool operator==(const GraphKey& o) const {
     return bases == o.bases && leaves == o.leaves && nbases == o.nbases && S == o.S && L == o.L &&
            leaf_cap == o.leaf_cap && packed == o.packed && bucket == o.bucket && stream == o.stream && tab == o.tab &&
-           wa == o.wa && wb == o.wb && nodes == o.nodes && leaves_out == o.leaves_out && nf == o.nf && desc == o.desc;
+           wa == o.wa && wb == o.wb && nodes == o.nodes && leaves_out == o.leaves_out && nf == o.nf && desc == o.desc &&
+           ftab == o.ftab && fused == o.fused;
   }
 };
 
@@ -217,6 +227,11 @@ struct gcz_ctx {
   gcz_host::u64 dense_min = 1ull << 21;   // ... from this many strands (mode 1)
   bool dense_used = false;   // the last build's leaf level ran dense
   bool use_graph = true;     // small builds as a replayed HIP graph       (GCZ_GRAPH=0 disables)
+  bool use_fused = true;     // small builds: two launches per node level  (GCZ_FUSED=0 disables)
+  int small_cap_shift = 2;   // ... and tables 2^this times the usual size: short probe chains (GCZ_SMALL_CAP_SHIFT)
+  int cap_boost = 0;         // (this build's node-table boost)
+  gcz_host::DevBuf ftab;     // ... their node tables, three rotating regions
+  gcz_host::LevelTab fused_leaf{}, fused_prev{};   // ... the tables the next insert settles through
   bool upload_warm = false;   // the runtime's host -> device path has run once (upload_reserve)
   int upload_reserve(size_t bytes);                     // input buffer of `bytes`, touched; the copy path warmed
   int upload(void* d_dst, const void* h_src, size_t n); // stream-ordered before later work on `stream`
@@ -291,7 +306,8 @@ struct gcz_ctx {
 
   gcz_host::u64 node_cap(gcz_host::u64 p) const {   // load <= 2/3 (shift 0), 1/2 (1, default), 1/4 (2)
     using gcz_host::next_pow2;
-    return std::max<gcz_host::u64>(256, next_pow2(node_cap_shift <= 0 ? p + p / 2 + 1 : p << node_cap_shift));
+    return std::max<gcz_host::u64>(256, next_pow2(node_cap_shift <= 0 ? p + p / 2 + 1 : p << node_cap_shift))
+           << cap_boost;
   }
   // Marks buffers for levels of up to S elements (sets aligned for uchar2 loads).
   int ensure_marks(gcz_host::u64 S);

@@ -34,6 +34,7 @@
 #include <cstddef>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "gcz_internal.h"
 
@@ -56,7 +57,18 @@ constexpr int kLeafItems = kItems;         // leaf flagscan: most strands are al
 constexpr int kLeafTile = kBlock * kLeafItems;
 // Look-back tile of a scan over n elements: long tiles keep the look-back chain short
 // on big levels, short ones keep enough tiles in flight on small ones.
-__host__ __device__ inline u64 scan_tile(u64 n) { return n >= (1ull << 20) ? u64(kTile) : u64(kTileSmall); }
+constexpr int kItemsTiny = 1;              // ... and one per thread up to 2^17 (direct prefix, no look-back)
+constexpr int kTileTiny = kBlock * kItemsTiny;
+inline u64 tiny_tile_max() {   // (GCZ_TINY_MAX overrides, process-wide: every caller sizes alike)
+  static const u64 v = [] {
+    const char* e = std::getenv("GCZ_TINY_MAX");
+    return e ? u64(std::strtoull(e, nullptr, 10)) : u64(1) << 17;
+  }();
+  return v;
+}
+inline u64 scan_tile(u64 n) {
+  return n >= (1ull << 20) ? u64(kTile) : n > tiny_tile_max() ? u64(kTileSmall) : u64(kTileTiny);
+}
 constexpr u32 kMaxProbe = 1u << 16;
 
 struct __align__(16) Slot {   // WideTab slot; key stored as key ^ 1 (see WideTab)
@@ -425,8 +437,23 @@ __global__ __launch_bounds__(kBlock) void k_leaf_bases(const unsigned char* __re
   const u32* src = reinterpret_cast<const u32*>(bases + byte0);
   u32* dst = reinterpret_cast<u32*>(buf);
   const u32 nwords = u32(nbytes / 4);
-  for (u32 w = tid; w < nwords; w += kBlock) dst[w] = src[w];
-  for (u32 b = nwords * 4 + tid; b < nbytes; b += kBlock) buf[b] = bases[byte0 + b];
+  if (nstr == u64(kBlock)) {   // full block: L / 4 words per thread, all loads in flight at once
+    constexpr int kW = (L + 3) / 4;
+    u32 v[kW];
+#pragma unroll
+    for (int q = 0; q < kW; ++q) {
+      const u32 w = u32(q) * kBlock + tid;
+      v[q] = w < nwords ? src[w] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < kW; ++q) {
+      const u32 w = u32(q) * kBlock + tid;
+      if (w < nwords) dst[w] = v[q];
+    }
+  } else {
+    for (u32 w = tid; w < nwords; w += kBlock) dst[w] = src[w];
+    for (u32 b = nwords * 4 + tid; b < nbytes; b += kBlock) buf[b] = bases[byte0 + b];
+  }
   __syncthreads();
   if (u64(tid) >= nstr) return;
   u64 x = 0;
@@ -554,6 +581,9 @@ struct InitPlan {
   uint4* stats; u64 nstats16;
   uint4* tab;   u64 ntab16;     // 0xff
   uint4* nf;    u64 nnf16;
+  // fused small-build levels: the first node level's table (ones) and marks (zero)
+  uint4* ftab;  u64 nftab16;
+  uint4* fnf;   uint4* fmulti; u64 nfm16;
 };
 
 [[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_build_init(InitPlan ip) {
@@ -568,6 +598,11 @@ struct InitPlan {
   for (u64 i = t; i < ip.nstats16; i += st) ip.stats[i] = z;
   for (u64 i = t; i < ip.ntab16; i += st) ip.tab[i] = f;
   for (u64 i = t; i < ip.nnf16; i += st) ip.nf[i] = z;
+  for (u64 i = t; i < ip.nftab16; i += st) ip.ftab[i] = f;
+  for (u64 i = t; i < ip.nfm16; i += st) {
+    ip.fnf[i] = z;
+    ip.fmulti[i] = z;
+  }
 }
 
 // Build end in one launch: the root word (when the level loop, not k_tail, ended the
@@ -599,20 +634,100 @@ struct InitPlan {
   }
 }
 
+// ---- fused small-build levels --------------------------------------------------------
+// Small builds (no bucketed level, no host look at the gates) run each node level as two
+// launches instead of four: the insert of level k settles level k-1's repeats itself (the
+// resolve: a not-first child word takes its key's first id) and writes the final words
+// back into its input, and the tables and marks a level needs are cleared by the
+// launches two steps before it (tables in three rotating regions, marks in the two
+// parity sets).  The previous level's gate is decided by the insert from its count and
+// look-ahead flag (block 0 stores it for the launches behind).
+struct NoRes {
+  static constexpr bool kOn = false;
+  const unsigned char* nf = nullptr;
+  __device__ __forceinline__ u32 operator()(unsigned char, u32 w) const { return w; }
+};
 template <class Tab>
-__global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ in, u64 n, u64 p, Tab T,
+struct LeafRes {   // k_resolve_leaf's rule, one leaf chunk
+  static constexpr bool kOn = true;
+  Tab T;
+  const unsigned char* nf;
+  __device__ __forceinline__ u32 operator()(unsigned char f, u32 w) const {   // f = the word's mark
+    return f == kNfNot ? T.settled_id(w & kIdx) | (w & kBits) : w;
+  }
+};
+template <class Tab>
+struct NodeRes {   // k_resolve_node's rule (table insert)
+  static constexpr bool kOn = true;
+  Tab T;
+  const unsigned char* nf;
+  const Group* grp;
+  __device__ __forceinline__ u32 operator()(unsigned char fm, u32 w) const {
+    if (fm != kNfNot) return w;
+    u64 key;
+    u32 f;
+    T.read(w & kIdx, key, f);   // f = the key's first position
+    const Group h = grp[f >> 6];
+    return (h.prefix + u32(__popcll(h.mask & ((1ull << (f & 63)) - 1)))) | (w & kBits);
+  }
+};
+struct FuseIn {
+  const u64* pcount = nullptr;     // previous level's unique count (null: not fused, use prev_count)
+  const u32* phashed = nullptr;    // ... and its look-ahead flag
+  u64* gate_out = nullptr;         // where the previous level's gate goes
+  uint4* clear = nullptr;          // the table of the level after this one: filled with ones
+  u64 clear16 = 0;
+};
+
+template <class Tab, class Res>
+__global__ __launch_bounds__(kBlock) void k_node_insert(u32* __restrict__ in, u64 n, u64 p, Tab T,
                                                        const unsigned char* __restrict__ prev_nf,
                                                        const unsigned char* __restrict__ prev_multi,
                                                        u32* __restrict__ rec, Marks mk,
                                                        Header* __restrict__ hdr, const u64* prev_count,
                                                        uint2* __restrict__ out, u64* __restrict__ count_out,
-                                                       u32 id_off, u64* __restrict__ stats, u32 bkt) {
-  if (level_direct(prev_count, n)) {
-    const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
+                                                       u32 id_off, u64* __restrict__ stats, u32 bkt, Res res,
+                                                       FuseIn fz) {
+  if (fz.clear) {
+    const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u);
+    for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < fz.clear16; i += u64(gridDim.x) * kBlock)
+      fz.clear[i] = ones;
+  }
+  if (bkt && !level_direct(prev_count, n) && hdr->predup == 0) return;   // k_bkt_* insert this level
+  // every load that depends on nothing goes out first: the pair, the previous level's
+  // marks of its two children, the gate inputs
+  const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
+  const bool two = 2 * j + 1 < n;
+  u32 l = kNullWord, r = kNullWord;
+  uchar2 f = make_uchar2(0, 0), g = make_uchar2(0, 0);   // (nf, multi) of 2j in .x, of 2j + 1 in .y
+  const unsigned char* fnf = Res::kOn ? res.nf : prev_nf;
+  if (j < p) {
+    load_pair(in, n, j, l, r);
+    if (fnf) f = two ? reinterpret_cast<const uchar2*>(fnf)[j] : make_uchar2(fnf[2 * j], 0);
+    if (prev_nf) g = two ? reinterpret_cast<const uchar2*>(prev_multi)[j] : make_uchar2(prev_multi[2 * j], 0);
+  }
+  bool direct;
+  if (fz.pcount) {
+    direct = *fz.pcount == n || *fz.phashed == 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *fz.gate_out = direct ? n : ~0ull;
+  } else {
+    direct = level_direct(prev_count, n);
+  }
+  if constexpr (Res::kOn) {   // settle the previous level's repeats; the final words go back
+    if (j < p) {
+      const u32 l2 = res(f.x, l), r2 = two ? res(f.y, r) : r;
+      if (l2 != l || r2 != r) {
+        if (two) reinterpret_cast<uint2*>(in)[j] = make_uint2(l2, r2);
+        else in[2 * j] = l2;
+      }
+      l = l2;
+      r = r2;
+    }
+  }
+  if (direct) {
     if (j == 0) *count_out = p;
     if (j >= p) return;
-    u32 l, r, cl, cr, m, t;
-    load_pair(in, n, j, l, r);
+    u32 cl, cr, m, t;
     node_canonical(l, r, cl, cr, m, t);
     const u32 v = ulw(l) == ulw(xf(r, 1, 0));
     uint2 w;
@@ -621,7 +736,6 @@ __global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ 
     rec[j] = make_word(u32(j) + id_off, m, t, v);   // id_off: first pair of this rank (multi-rank build)
     return;
   }
-  if (bkt && hdr->predup == 0) return;   // k_bkt_* insert this level
   // Repetitive data (hdr->predup, decided from the first leaf chunk): repeats of a
   // key inside the block collapse onto its earliest position first, in an LDS
   // table; only that representative touches the HBM table, the others are not
@@ -642,25 +756,15 @@ __global__ __launch_bounds__(kBlock) void k_node_insert(const u32* __restrict__ 
       s_dup[q] = 0;
     }
   __syncthreads();
-  const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
   bool single = true;
   u32 m = 0, t = 0, v = 0, ls = 0;
   u64 key = 0;
   if (j < p) {
-    u32 l, r, cl, cr;
-    load_pair(in, n, j, l, r);
+    u32 cl, cr;
     node_canonical(l, r, cl, cr, m, t);
     v = ulw(l) == ulw(xf(r, 1, 0));      // left == right.mirrored() (:670)
     single = false;
-    if (prev_nf) {
-      if (2 * j + 1 < n) {
-        const uchar2 f = reinterpret_cast<const uchar2*>(prev_nf)[j];
-        const uchar2 g = reinterpret_cast<const uchar2*>(prev_multi)[j];
-        single = (f.x == 0 && g.x == 0) || (f.y == 0 && g.y == 0);
-      } else {
-        single = prev_nf[2 * j] == 0 && prev_multi[2 * j] == 0;
-      }
-    }
+    if (prev_nf) single = (f.x == 0 && g.x == 0) || (two && f.y == 0 && g.y == 0);
     key = T.node_key(cl, cr);
     if (pre && !single) {
       u32 h = slot_hash(key) & (2 * kBlock - 1);
@@ -759,7 +863,15 @@ __device__ __forceinline__ void tile_scan(TileScan<ITEMS>& ts, u32* s_tile, u32*
     const uint4* q = reinterpret_cast<const uint4*>(nf + j0);
     const u64 nq = (ts.base - j0) / 16;
     u32 c = 0;
-    for (u64 i = tid; i < nq; i += kBlock) {
+    u64 i = tid;
+    for (; i + 7 * kBlock < nq; i += 8 * kBlock) {   // eight loads in flight per pass
+      uint4 v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = q[i + e * kBlock];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) c += zero_bytes(v[e].x) + zero_bytes(v[e].y) + zero_bytes(v[e].z) + zero_bytes(v[e].w);
+    }
+    for (; i < nq; i += kBlock) {
       const uint4 v = q[i];
       c += zero_bytes(v.x) + zero_bytes(v.y) + zero_bytes(v.z) + zero_bytes(v.w);
     }
@@ -883,15 +995,33 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
                                                          u32* __restrict__ ticket, uint2* __restrict__ out,
                                                          u64* __restrict__ count_out, const u64* prev_count,
                                                          const unsigned char* __restrict__ multi,
-                                                         u32* __restrict__ hashed_next) {
+                                                         u32* __restrict__ hashed_next, uint4* __restrict__ clr_nf,
+                                                         uint4* __restrict__ clr_multi, u64 clr16) {
+  // fused small-build levels: clear the marks of the level after this one (its parity
+  // set held the previous level's marks, last read by this level's insert)
+  for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < clr16; i += u64(gridDim.x) * kBlock) {
+    clr_nf[i] = make_uint4(0, 0, 0, 0);
+    clr_multi[i] = make_uint4(0, 0, 0, 0);
+  }
   if (level_direct(prev_count, n)) return;
   __shared__ u32 s_tile;
   __shared__ u32 s_pre[4 * ITEMS];
   __shared__ u32 s_hashed;
   TileScan<ITEMS> ts;
   if (threadIdx.x == 0) s_hashed = 0;
-  tile_scan(ts, &s_tile, s_pre, nf, 0, p, 0, desc, ticket, count_out);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  u32 pl[ITEMS], pr[ITEMS];   // the first occurrences' input pairs, read while the scan waits
+  constexpr bool kPre = ITEMS <= kItemsSmall;   // (32 items: the registers cost more than the wait)
+  auto fetch = [&]() {
+    if constexpr (kPre) {
+#pragma unroll
+      for (int e = 0; e < ITEMS; ++e) {
+        const u64 j = ts.base + u64(e) * kBlock + tid;
+        if (j < p && ((ts.mask[e] >> lane) & 1ull)) load_pair(in, n, j, pl[e], pr[e]);
+      }
+    }
+  };
+  tile_scan(ts, &s_tile, s_pre, nf, 0, p, 0, desc, ticket, count_out, fetch);
   const u64 lt = (1ull << lane) - 1;
   bool hashed = false;
 #pragma unroll
@@ -911,7 +1041,12 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
     if (j < p && ((ts.mask[e] >> lane) & 1ull)) {
       const u32 id = gpre + u32(__popcll(ts.mask[e] & lt));
       u32 l, r, cl, cr, m, t;
-      load_pair(in, n, j, l, r);
+      if constexpr (kPre) {
+        l = pl[e];
+        r = pr[e];
+      } else {
+        load_pair(in, n, j, l, r);
+      }
       node_canonical(l, r, cl, cr, m, t);
       uint2 w;
       w.x = cl; w.y = cr;
@@ -1518,6 +1653,7 @@ struct DirectPlan {
 // per-level kernels, without ~4 launches per level.
 constexpr int kTailMaxN = 2048;
 constexpr unsigned long long kDirectCheckMin = 1ull << 16;   // levels below: no host look at the direct gate
+constexpr unsigned long long kDupProbeMin = 1ull << 17;      // fewer strands: no repetitive-data probe
 constexpr int kTailThreads = 1024;
 constexpr int kTailSlots = 2 * kTailThreads;
 

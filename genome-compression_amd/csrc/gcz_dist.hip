@@ -581,6 +581,7 @@ int gcz_group::alloc(int i, u64 leaf_cap) {
   if ((rc = c->ensure(c->stats, kStatBytes))) return rc;
   if ((rc = c->ensure_marks(wmax))) return rc;
   const u64 pmax = std::max<u64>(P.G > 0 ? P.count(r, 1) : 0, nG > 1 ? (nG + 1) / 2 : 1);
+  c->cap_boost = 0;   // (the single-device small-build boost is not used here)
   if ((rc = c->ensure(c->tab, std::max(leaf_cap, c->node_cap(pmax)) * 16))) return rc;
   if (!c->h_hdr && hipHostMalloc((void**)&c->h_hdr, sizeof(Header), hipHostMallocDefault) != hipSuccess)
     return GCZ_ERR_DEVICE;

@@ -217,7 +217,8 @@ def test_gpu_large_synth_goldens(name, ctx, gcz, manifest):
                                  {"GCZ_PREDUP": "1"}, {"GCZ_PREDUP": "2"}, {"GCZ_PREDUP": "1", "GCZ_TABLE": "wide"},
                                  {"GCZ_BUCKET": "0"}, {"GCZ_BUCKET_MIN": "1"},
                                  {"GCZ_BUCKET_MIN": "1", "GCZ_DIRECT": "0"},
-                                 {"GCZ_BUCKET_MIN": "1", "GCZ_PREDUP": "2"}])
+                                 {"GCZ_BUCKET_MIN": "1", "GCZ_PREDUP": "2"}, {"GCZ_FUSED": "0"},
+                                 {"GCZ_FUSED": "0", "GCZ_GRAPH": "0"}, {"GCZ_GRAPH": "0", "GCZ_TAIL": "0"}])
 def test_gpu_schedule_knobs_same_tree(env, gcz, manifest):
     """The per-level fallbacks (no direct subtrees, no fused top, tight tables, a leaf
     table that overflows and regrows) build the same tree as the default schedule."""
@@ -278,5 +279,42 @@ def test_gpu_bucket_overflow_rebuilds(gcz, oracle):
         assert c.tree().leaves_bin() == o.leaves_bin()
         assert c.tree().layers_bin() == o.layers_bin()
         assert info["bucketed_pairs"] == 0   # the final (table) build bucketed nothing
+    finally:
+        c.close()
+
+
+def _ctx_env(gcz, env):
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return gcz.Context(0)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("env", [{}, {"GCZ_TABLE": "wide"}, {"GCZ_PREDUP": "1"}, {"GCZ_TAIL": "0"},
+                                 {"GCZ_PREDUP": "1", "GCZ_TABLE": "wide", "GCZ_TAIL": "0"}, {"GCZ_FUSED": "0"}])
+def test_gpu_fused_small_levels_random(env, gcz, oracle):
+    """Small builds run two launches per node level (the insert settles the previous
+    level's repeats, tables in rotating regions): random leaf mixes from all-unique to
+    nearly all-repeated, each built three times (eager, graph capture, graph replay),
+    against the oracle."""
+    c = _ctx_env(gcz, env)
+    rng = np.random.default_rng(23)
+    try:
+        for S, pool_div in [(3, 1), (257, 1), (2049, 3), (4099, 3), (20_001, 40), (100_003, 1), (100_003, 7),
+                            (131_071, 1000), (131_072, 50_000)]:
+            pool = rng.integers(0, 1 << 48, size=max(4, S // pool_div), dtype=np.uint64)
+            leaves = pool[rng.integers(0, pool.size, size=S)]
+            o = oracle.build_leaves(leaves, 12)
+            for rep in range(3):
+                c.build_leaves(leaves, 12)
+                g = c.tree()
+                assert g.leaves_bin() == o.leaves_bin(), (env, S, pool_div, rep)
+                assert g.layers_bin() == o.layers_bin(), (env, S, pool_div, rep)
     finally:
         c.close()
