@@ -511,7 +511,9 @@ int gcz_ctx::tail_levels(const u32* in, u64 n0, const u64* pcount, int k0, int D
   for (int k = k0; k < D; ++k) to.layer_off[k] = layer_off_[k];
   hipEvent_t e0{};
   prof_begin(KID_TAIL, e0);
-  hipLaunchKernelGGL(k_tail, dim3(1), dim3(kTailThreads), 0, stream, in, n0, pcount, k0, D, nodes_out.as<uint2>(), to,
+  HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(k_tail), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              int(kTailLds)));
+  hipLaunchKernelGGL(k_tail, dim3(1), dim3(kTailThreads), kTailLds, stream, in, n0, pcount, k0, D, nodes_out.as<uint2>(), to,
                      d_hdr);
   HIP_TRY(hipGetLastError());
   prof_end(KID_TAIL, e0);

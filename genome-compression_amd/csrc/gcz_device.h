@@ -1651,11 +1651,15 @@ struct DirectPlan {
 // LDS table (CAS claims, atomicMin keeps the first position, a block scan
 // ranks the first occurrences) -- the same ids, nodes and words as the
 // per-level kernels, without ~4 launches per level.
-constexpr int kTailMaxN = 2048;
+constexpr int kTailMaxN = 8192;
 constexpr unsigned long long kDirectCheckMin = 1ull << 16;   // levels below: no host look at the direct gate
 constexpr unsigned long long kDupProbeMin = 1ull << 17;      // fewer strands: no repetitive-data probe
 constexpr int kTailThreads = 1024;
-constexpr int kTailSlots = 2 * kTailThreads;
+constexpr int kTailItems = kTailMaxN / 2 / kTailThreads;   // pairs per thread
+constexpr int kTailSlots = kTailMaxN;                       // LDS table: load <= 1/2
+// dynamic LDS: the level's words (in place), the table keys, per slot the minimum
+// position and then the id
+constexpr size_t kTailLds = size_t(kTailMaxN) * 4 + size_t(kTailSlots) * 12;
 
 struct TailOut {
   u64 layer_off[GCZ_MAX_LAYERS];   // node offset of each layer within `nodes`
@@ -1664,35 +1668,41 @@ struct TailOut {
 [[maybe_unused]] static __global__ __launch_bounds__(kTailThreads) void k_tail(
     const u32* __restrict__ in, u64 n0, const u64* prev_count, int k0, int D, uint2* __restrict__ nodes, TailOut to,
     Header* __restrict__ hdr) {
-  __shared__ u32 wbuf[2][kTailMaxN];
-  __shared__ unsigned long long tkey[kTailSlots];
-  __shared__ u32 tpos[kTailSlots];
-  __shared__ u32 tid_of[kTailSlots];
-  __shared__ u32 wsum[kTailThreads / 64];
+  extern __shared__ __align__(16) unsigned char tail_lds[];
+  unsigned long long* tkey = reinterpret_cast<unsigned long long*>(tail_lds);
+  u32* tpos = reinterpret_cast<u32*>(tkey + kTailSlots);
+  u32* wbuf = tpos + kTailSlots;
+  __shared__ u32 wsum[kTailItems][kTailThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (u64 i = tid; i < n0; i += kTailThreads) wbuf[0][i] = in[i];
+  for (u64 i = tid; i < n0; i += kTailThreads) wbuf[i] = in[i];
   u32 n = u32(n0);
   bool direct = prev_count && *prev_count == n0;
-  int cur = 0;
   __syncthreads();
   for (int k = k0; k < D; ++k) {
     const u32 p = (n + 1) / 2;
-    const u32* win = wbuf[cur];
-    u32* wout = wbuf[cur ^ 1];
     uint2* out = nodes + to.layer_off[k];
-    const u32 j = u32(tid);
-    u32 l = kNullWord, r = kNullWord, cl = 0, cr = 0, m = 0, t = 0, v = 0;
-    if (j < p) {
-      l = win[2 * j];
-      r = 2 * j + 1 < n ? win[2 * j + 1] : kNullWord;
-      node_canonical(l, r, cl, cr, m, t);
-      v = ulw(l) == ulw(xf(r, 1, 0));
+    u32 cl[kTailItems], cr[kTailItems], mtv[kTailItems], slot[kTailItems];
+#pragma unroll
+    for (int e = 0; e < kTailItems; ++e) {   // pair j = e * kTailThreads + tid: position order is (e, tid)
+      const u32 j = u32(e * kTailThreads + tid);
+      cl[e] = cr[e] = mtv[e] = slot[e] = 0;
+      if (j < p) {
+        const u32 l = wbuf[2 * j], r = 2 * j + 1 < n ? wbuf[2 * j + 1] : kNullWord;
+        u32 m, t;
+        node_canonical(l, r, cl[e], cr[e], m, t);
+        mtv[e] = make_word(0, m, t, ulw(l) == ulw(xf(r, 1, 0)));
+      }
     }
     u32 count;
     if (direct) {
-      if (j < p) {
-        out[j] = make_uint2(cl, cr);
-        wout[j] = make_word(j, m, t, v);
+      __syncthreads();   // (every read of the level's words is done: they are rewritten in place)
+#pragma unroll
+      for (int e = 0; e < kTailItems; ++e) {
+        const u32 j = u32(e * kTailThreads + tid);
+        if (j < p) {
+          out[j] = make_uint2(cl[e], cr[e]);
+          wbuf[j] = j | mtv[e];
+        }
       }
       count = p;
     } else {
@@ -1704,46 +1714,65 @@ struct TailOut {
         tpos[s] = ~0u;
       }
       __syncthreads();
-      u32 slot = 0;
-      if (j < p) {
-        const unsigned long long key = (u64(ulw(cl)) << 31) | ulw(cr);
-        u32 s = slot_hash(key) & mask;
-        for (;;) {
-          unsigned long long c = tkey[s];
-          if (c == kEmpty) c = atomicCAS(&tkey[s], kEmpty, key);
-          if (c == kEmpty || c == key) break;
-          s = (s + 1) & mask;
+#pragma unroll
+      for (int e = 0; e < kTailItems; ++e) {
+        const u32 j = u32(e * kTailThreads + tid);
+        if (j < p) {
+          const unsigned long long key = (u64(ulw(cl[e])) << 31) | ulw(cr[e]);
+          u32 s = slot_hash(key) & mask;
+          for (;;) {
+            unsigned long long c = tkey[s];
+            if (c == kEmpty) c = atomicCAS(&tkey[s], kEmpty, key);
+            if (c == kEmpty || c == key) break;
+            s = (s + 1) & mask;
+          }
+          atomicMin(&tpos[s], j);
+          slot[e] = s;
         }
-        atomicMin(&tpos[s], j);
-        slot = s;
       }
       __syncthreads();
-      const bool first = j < p && tpos[slot] == j;
-      const u64 bal = __ballot(first);
-      if (lane == 0) wsum[wave] = u32(__popcll(bal));
-      __syncthreads();
-      u32 before = 0, total = 0;
-      for (int w = 0; w < kTailThreads / 64; ++w) {
-        const u32 c = wsum[w];
-        before += w < wave ? c : 0u;
-        total += c;
+      u64 bal[kTailItems];
+#pragma unroll
+      for (int e = 0; e < kTailItems; ++e) {
+        const u32 j = u32(e * kTailThreads + tid);
+        bal[e] = __ballot(j < p && tpos[slot[e]] == j);
+        if (lane == 0) wsum[e][wave] = u32(__popcll(bal[e]));
       }
-      if (first) {
-        const u32 id = before + u32(__popcll(bal & ((1ull << lane) - 1)));
-        tid_of[slot] = id;
-        out[id] = make_uint2(cl, cr);
+      __syncthreads();   // (every tpos read is done: firsts now overwrite theirs with the id)
+      u32 base[kTailItems], acc = 0;   // firsts before (item e, this wave): all of items < e, then waves
+#pragma unroll
+      for (int e = 0; e < kTailItems; ++e) {
+        u32 before = 0, tot = 0;
+        for (int w = 0; w < kTailThreads / 64; ++w) {
+          const u32 c = wsum[e][w];
+          before += w < wave ? c : 0u;
+          tot += c;
+        }
+        base[e] = acc + before;
+        acc += tot;
+      }
+#pragma unroll
+      for (int e = 0; e < kTailItems; ++e) {
+        if ((bal[e] >> lane) & 1ull) {
+          const u32 id = base[e] + u32(__popcll(bal[e] & ((1ull << lane) - 1)));
+          tpos[slot[e]] = id;
+          out[id] = make_uint2(cl[e], cr[e]);
+        }
       }
       __syncthreads();
-      if (j < p) wout[j] = make_word(tid_of[slot], m, t, v);
-      count = total;
+#pragma unroll
+      for (int e = 0; e < kTailItems; ++e) {
+        const u32 j = u32(e * kTailThreads + tid);
+        if (j < p) wbuf[j] = tpos[slot[e]] | mtv[e];
+      }
+      count = acc;
     }
     if (tid == 0) hdr->count[kLayerSlot + k] = count;
     direct = count == p;
     n = p;
-    cur ^= 1;
     __syncthreads();
   }
-  if (tid == 0) hdr->root = wbuf[cur][0];
+  if (tid == 0) hdr->root = wbuf[0];
 }
 
 [[maybe_unused]] static __global__ void k_root(const u32* __restrict__ words, Header* __restrict__ hdr) { hdr->root = words[0]; }
