@@ -79,6 +79,7 @@ int gcz_ctx::leaf_level(const LeafLevel& a, Header* d_hdr) {
     lt.pt.limit = std::min(lt.pt.limit, limit);
     lt.pt.kmask >>= 2;                   // the key itself has 4L bits
     lt.pt.sh = (4 * u32(L) + 1) / 2;
+    lt.pt.cas_first = cap_boost > 0;   // sparse small-build table: the home slot is mostly free
   }
   fused_leaf = lt;
   unsigned char* d_nf = nf_set[0];
@@ -313,7 +314,8 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   if (p == 0) return GCZ_OK;
   const u64 cap = node_cap(p);
   const u32 Bk = std::max<u32>(1, bit_width(a.bound));
-  const LevelTab nt = plan_table(a.fused ? a.ftab : tab.ptr, cap, 2 * (Bk + 3), p, Bk, allow_packed, kMaxProbe);
+  LevelTab nt = plan_table(a.fused ? a.ftab : tab.ptr, cap, 2 * (Bk + 3), p, Bk, allow_packed, kMaxProbe);
+  nt.pt.cas_first = cap_boost > 0;
   const int cur = (a.k + 1) & 1, prev = a.k & 1;
   unsigned char* knf = nf_set[cur];
   u32* in = const_cast<u32*>(a.in);   // (written only by a fused insert, which settles it)
@@ -457,14 +459,12 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     if (!a.fused) insert(T, NoRes{});
     else if (a.k == 0 && fused_leaf.packed) insert(T, LeafRes<PackedTab>{fused_leaf.pt, nf_set[prev]});
     else if (a.k == 0) insert(T, LeafRes<WideTab>{fused_leaf.wt, nf_set[prev]});
-    else if (fused_prev.packed) insert(T, NodeRes<PackedTab>{fused_prev.pt, nf_set[prev], d_grp});
-    else insert(T, NodeRes<WideTab>{fused_prev.wt, nf_set[prev], d_grp});
+    else insert(T, NodeRes{nf_set[prev], a.sid_prev});
   };
   if (nt.packed) insert_settling(nt.pt);
   else insert_settling(nt.wt);
   HIP_TRY(hipGetLastError());
   prof_end(KID_NODE, e0);
-  if (a.fused) fused_prev = nt;
   uint4* clr_nf = reinterpret_cast<uint4*>(nf_set[prev]);
   uint4* clr_mu = reinterpret_cast<uint4*>(multi_set[prev]);
   prof_begin(KID_FLAGSCAN_NODE, e0);
@@ -474,7 +474,7 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   auto flagscan = [&](auto items) {
     hipLaunchKernelGGL((k_flagscan_node<decltype(items)::value>), gs, dim3(kBlock), 0, stream, a.words, p, a.in, n,
                        knf, d_grp, ndesc, a.ticket, a.out, a.count, a.pcount, mk.multi, a.hashed_next, clr_nf, clr_mu,
-                       clr16);
+                       clr16, a.fused && !a.fused_last ? a.sid : nullptr);
   };
   if (tile == u64(kTile)) flagscan(std::integral_constant<int, kItems>{});
   else if (tile == u64(kTileSmall)) flagscan(std::integral_constant<int, kItemsSmall>{});
@@ -506,7 +506,7 @@ int gcz_ctx::direct_levels(const u32* in, int k0, int nlev, const DirectPlan& dp
 }
 
 int gcz_ctx::tail_levels(const u32* in, u64 n0, const u64* pcount, int k0, int D, const std::vector<u64>& layer_off_,
-                         Header* d_hdr) {
+                         Header* d_hdr, const u64* shards) {
   TailOut to{};
   for (int k = k0; k < D; ++k) to.layer_off[k] = layer_off_[k];
   hipEvent_t e0{};
@@ -514,7 +514,7 @@ int gcz_ctx::tail_levels(const u32* in, u64 n0, const u64* pcount, int k0, int D
   HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(k_tail), hipFuncAttributeMaxDynamicSharedMemorySize,
                               int(kTailLds)));
   hipLaunchKernelGGL(k_tail, dim3(1), dim3(kTailThreads), kTailLds, stream, in, n0, pcount, k0, D, nodes_out.as<uint2>(), to,
-                     d_hdr);
+                     d_hdr, shards);
   HIP_TRY(hipGetLastError());
   prof_end(KID_TAIL, e0);
   return GCZ_OK;
@@ -603,7 +603,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     const bool fused = use_fused && !try_dense && C == 1 && pk[0] < kDirectCheckMin &&
                        !(bucket_now && pk[0] >= bucket_min) && (S > u64(kTailMaxN) || !use_tail);
     const u64 fregion = node_cap0 * 16;
-    if (fused && (rc = ensure(ftab, 3 * fregion))) return rc;
+    if (fused && ((rc = ensure(ftab, 3 * fregion)) || (rc = ensure(fsid, 3 * node_cap0 * 4)))) return rc;
     auto fregion_ptr = [&](int k) { return static_cast<void*>(ftab.as<unsigned char>() + u64(k % 3) * fregion); };
     // One build's launches, start event to header copy.  A build whose launch sequence
     // has no host decision inside (no dense-level fallback check, no look at the direct
@@ -674,7 +674,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
         if (n <= u64(kTailMaxN) && use_tail) {   // the rest fits one workgroup: one launch
           const u64* pc = k == 0 ? &d_hdr->count[C - 1] : prev_regular ? &d_hdr->gate[k - 1]
                                                                          : &d_hdr->count[kLayerSlot + k - 1];
-          if ((rc = tail_levels(in, n, pc, k, D, layer_off, d_hdr))) return rc;
+          if ((rc = tail_levels(in, n, pc, k, D, layer_off, d_hdr, stats.as<u64>()))) return rc;
           tail_done = true;
           break;
         }
@@ -715,6 +715,8 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
           na.fused = true;
           na.ftab = fregion_ptr(k);
           na.ftab_next = fregion_ptr(k + 1);
+          na.sid = fsid.as<u32>() + u64(k % 3) * node_cap0;
+          na.sid_prev = k > 0 ? fsid.as<u32>() + u64((k - 1) % 3) * node_cap0 : nullptr;
           na.p_next = k + 1 < D ? pk[k + 1] : 0;
           na.fused_last = k + 1 == D || (pk[k] <= u64(kTailMaxN) && use_tail);
         }
@@ -735,9 +737,10 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
           table_only = pd != 0;   // repetitive data: later levels skip the (gated-off) bucket launches
         }
       }
-      hipLaunchKernelGGL(k_build_finish, dim3(1), dim3(1024), 0, stream, tail_done ? nullptr : in, stats.as<u64>(),
-                         d_hdr);
-      HIP_TRY(hipGetLastError());
+      if (!tail_done) {   // (the tail sums the statistics itself)
+        hipLaunchKernelGGL(k_build_finish, dim3(1), dim3(1024), 0, stream, in, stats.as<u64>(), d_hdr);
+        HIP_TRY(hipGetLastError());
+      }
       HIP_TRY(hipEventRecord(ev_stop, stream));
       HIP_TRY(hipMemcpyAsync(h_hdr, d_hdr, sizeof(Header), hipMemcpyDeviceToHost, stream));
       return GCZ_OK;
@@ -750,7 +753,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     if (static_seq) {
       const GraphKey key{d_bases, d_leaves, nbases, S, L, leaf_cap, allow_packed, bucket_now, stream,
                          tab.ptr, wa.ptr, wb.ptr, nodes_out.ptr, leaves_out.ptr, nf.ptr, desc.ptr,
-                         fused ? ftab.ptr : nullptr, fused};
+                         fused ? ftab.ptr : nullptr, fused ? fsid.ptr : nullptr, fused};
       if (graph_exec && key == graph_key) {
         launched = hipGraphLaunch(graph_exec, stream) == hipSuccess;
       } else if (!(key == graph_seen)) {

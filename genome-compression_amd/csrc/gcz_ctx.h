@@ -140,6 +140,8 @@ struct NodeLevel {
   u64 p_next = 0;                   // the next level's pairs (its table is cleared here)
   void* ftab = nullptr;             // region base of this level's table
   void* ftab_next = nullptr;        // ... and of the next level's
+  gcz_host::u32* sid = nullptr;     // ids of this level's repeated keys by slot (flag scan -> next insert)
+  const gcz_host::u32* sid_prev = nullptr;   // ... of the previous level
 };
 
 // One leaf level (all chunks).
@@ -177,13 +179,13 @@ struct GraphKey {
   gcz_host::u64 leaf_cap;
   bool packed, bucket;
   hipStream_t stream;
-  void *tab, *wa, *wb, *nodes, *leaves_out, *nf, *desc, *ftab;
+  void *tab, *wa, *wb, *nodes, *leaves_out, *nf, *desc, *ftab, *fsid;
   bool fused;
   bool operator==(const GraphKey& o) const {
     return bases == o.bases && leaves == o.leaves && nbases == o.nbases && S == o.S && L == o.L &&
            leaf_cap == o.leaf_cap && packed == o.packed && bucket == o.bucket && stream == o.stream && tab == o.tab &&
            wa == o.wa && wb == o.wb && nodes == o.nodes && leaves_out == o.leaves_out && nf == o.nf && desc == o.desc &&
-           ftab == o.ftab && fused == o.fused;
+           ftab == o.ftab && fsid == o.fsid && fused == o.fused;
   }
 };
 
@@ -231,7 +233,8 @@ struct gcz_ctx {
   int small_cap_shift = 2;   // ... and tables 2^this times the usual size: short probe chains (GCZ_SMALL_CAP_SHIFT)
   int cap_boost = 0;         // (this build's node-table boost)
   gcz_host::DevBuf ftab;     // ... their node tables, three rotating regions
-  gcz_host::LevelTab fused_leaf{}, fused_prev{};   // ... the tables the next insert settles through
+  gcz_host::DevBuf fsid;     // ... and slot -> id of each table's repeated keys, three regions
+  gcz_host::LevelTab fused_leaf{};   // ... the leaf table level 0's insert settles through
   bool upload_warm = false;   // the runtime's host -> device path has run once (upload_reserve)
   int upload_reserve(size_t bytes);                     // input buffer of `bytes`, touched; the copy path warmed
   int upload(void* d_dst, const void* h_src, size_t n); // stream-ordered before later work on `stream`
@@ -329,9 +332,11 @@ struct gcz_ctx {
   // Known-direct levels k0..k0+nlev-1 in one launch (gcz_device.h k_direct_levels).
   int direct_levels(const gcz_host::u32* in, int k0, int nlev, const gcz_dev::DirectPlan& dp, gcz_host::u32* out,
                     gcz_dev::Header* d_hdr);
-  // Levels k0..D-1 in one launch (n0 <= kTailMaxN input words); writes counts and the root.
+  // Levels k0..D-1 in one launch (n0 <= kTailMaxN input words); writes counts and the root
+  // (and, given the statistics shards, sums them: the build's last launch).
   int tail_levels(const gcz_host::u32* in, gcz_host::u64 n0, const gcz_host::u64* pcount, int k0, int D,
-                  const std::vector<gcz_host::u64>& layer_off, gcz_dev::Header* d_hdr);
+                  const std::vector<gcz_host::u64>& layer_off, gcz_dev::Header* d_hdr,
+                  const gcz_host::u64* shards = nullptr);
   int build(const void* d_bases, const gcz_host::u64* d_leaves, gcz_host::u64 nbases, gcz_host::u64 S, int L);
 };
 

@@ -318,6 +318,7 @@ struct PackedTab {
   u32 limit;   // <= 2^D - 2 probes
   u32 B;       // child index bits (node levels)
   u32 c, P, D, sh;
+  u32 cas_first;   // probe the home slot with the CAS itself (sparse small-build tables: one round trip)
   u64 kmask, c1, c2, c1i, c2i;
 
   __device__ __forceinline__ u64 node_key(u32 cl, u32 cr) const {
@@ -342,7 +343,7 @@ struct PackedTab {
     const u64 pmask = (1ull << P) - 1;
     for (u32 d = 0; d < limit; ++d) {
       const u64 mine = ((qd | d) << P) | pos;
-      u64 cur = tab[s];
+      u64 cur = d == 0 && cas_first ? kEmpty : tab[s];
       if (cur == kEmpty) {
         cur = atomicCAS(&tab[s], kEmpty, mine);
         if (cur == kEmpty) return s;            // new key: one atomic, nothing to mark
@@ -378,7 +379,7 @@ struct PackedTab {
     const u64 pmask = (1ull << P) - 1;
     for (u32 d = 0; d < limit; ++d) {
       const u64 mine = ((qd | d) << P) | pos;
-      u64 cur = tab[s];
+      u64 cur = d == 0 && cas_first ? kEmpty : tab[s];
       if (cur == kEmpty) {
         cur = atomicCAS(&tab[s], kEmpty, mine);
         if (cur == kEmpty) return {s, 0, false};
@@ -607,11 +608,10 @@ struct InitPlan {
 
 // Build end in one launch: the root word (when the level loop, not k_tail, ended the
 // build) and the two hashed-pair statistics.
-[[maybe_unused]] static __global__ __launch_bounds__(1024) void k_build_finish(const u32* __restrict__ root_word,
-                                                                               const u64* __restrict__ shards,
-                                                                               Header* __restrict__ hdr) {
+// The build's statistics shards summed into hdr->hashed by a 1024-thread block (k_build_finish,
+// or k_tail when it ends the build); v0/v1 are this thread's shard pair, loaded early.
+__device__ __forceinline__ void stats_sum(u64 v0, u64 v1, Header* __restrict__ hdr) {
   __shared__ u64 s_sum[2][1024 / 64];
-  u64 v0 = shards[threadIdx.x * kStatStride], v1 = shards[threadIdx.x * kStatStride + 1];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     v0 += __shfl_xor(v0, o, 64);
@@ -630,8 +630,14 @@ struct InitPlan {
     }
     hdr->hashed[0] = a;
     hdr->hashed[1] = b;
-    if (root_word) hdr->root = root_word[0];
   }
+}
+
+[[maybe_unused]] static __global__ __launch_bounds__(1024) void k_build_finish(const u32* __restrict__ root_word,
+                                                                               const u64* __restrict__ shards,
+                                                                               Header* __restrict__ hdr) {
+  stats_sum(shards[threadIdx.x * kStatStride], shards[threadIdx.x * kStatStride + 1], hdr);
+  if (threadIdx.x == 0 && root_word) hdr->root = root_word[0];
 }
 
 // ---- fused small-build levels --------------------------------------------------------
@@ -656,19 +662,12 @@ struct LeafRes {   // k_resolve_leaf's rule, one leaf chunk
     return f == kNfNot ? T.settled_id(w & kIdx) | (w & kBits) : w;
   }
 };
-template <class Tab>
-struct NodeRes {   // k_resolve_node's rule (table insert)
+struct NodeRes {   // k_resolve_node's rule, the ids settled by slot (k_flagscan_node's sid)
   static constexpr bool kOn = true;
-  Tab T;
   const unsigned char* nf;
-  const Group* grp;
+  const u32* sid;
   __device__ __forceinline__ u32 operator()(unsigned char fm, u32 w) const {
-    if (fm != kNfNot) return w;
-    u64 key;
-    u32 f;
-    T.read(w & kIdx, key, f);   // f = the key's first position
-    const Group h = grp[f >> 6];
-    return (h.prefix + u32(__popcll(h.mask & ((1ull << (f & 63)) - 1)))) | (w & kBits);
+    return fm == kNfNot ? sid[w & kIdx] | (w & kBits) : w;
   }
 };
 struct FuseIn {
@@ -859,21 +858,30 @@ __device__ __forceinline__ void tile_scan(TileScan<ITEMS>& ts, u32* s_tile, u32*
   __syncthreads();
   const u64 tile = direct ? u64(blockIdx.x) : u64(*s_tile);
   ts.base = j0 + tile * (kBlock * ITEMS);
+  // short tiles: the marks' loads go out before the prefix count's (long tiles read them
+  // one ballot at a time: registers)
+  constexpr bool kEarlyMarks = ITEMS <= kItemsSmall;
+  unsigned char mv[kEarlyMarks ? ITEMS : 1];
+  if constexpr (kEarlyMarks) {
+#pragma unroll
+    for (int e = 0; e < ITEMS; ++e) {
+      const u64 j = ts.base + u64(e) * kBlock + tid;
+      mv[e] = j < p ? nf[j] : kNfNot;
+    }
+  }
   if (direct) {   // firsts in [j0, base): j0 and base are multiples of 256
     const uint4* q = reinterpret_cast<const uint4*>(nf + j0);
     const u64 nq = (ts.base - j0) / 16;
     u32 c = 0;
-    u64 i = tid;
-    for (; i + 7 * kBlock < nq; i += 8 * kBlock) {   // eight loads in flight per pass
-      uint4 v[8];
+    for (u64 i0 = tid; i0 < nq; i0 += 16 * kBlock) {   // sixteen predicated loads in flight per pass
+      uint4 v[16];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = q[i + e * kBlock];
+      for (int e = 0; e < 16; ++e) {
+        const u64 i = i0 + u64(e) * kBlock;
+        v[e] = i < nq ? q[i] : make_uint4(~0u, ~0u, ~0u, ~0u);   // (no zero byte)
+      }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) c += zero_bytes(v[e].x) + zero_bytes(v[e].y) + zero_bytes(v[e].z) + zero_bytes(v[e].w);
-    }
-    for (; i < nq; i += kBlock) {
-      const uint4 v = q[i];
-      c += zero_bytes(v.x) + zero_bytes(v.y) + zero_bytes(v.z) + zero_bytes(v.w);
+      for (int e = 0; e < 16; ++e) c += zero_bytes(v[e].x) + zero_bytes(v[e].y) + zero_bytes(v[e].z) + zero_bytes(v[e].w);
     }
     c = u32(wave_sum(u64(c)));
     __syncthreads();   // (every thread has read *s_tile)
@@ -881,8 +889,13 @@ __device__ __forceinline__ void tile_scan(TileScan<ITEMS>& ts, u32* s_tile, u32*
   }
 #pragma unroll
   for (int e = 0; e < ITEMS; ++e) {
-    const u64 j = ts.base + u64(e) * kBlock + tid;
-    const bool first = j < p && nf[j] == kNfMaybe;
+    bool first;
+    if constexpr (kEarlyMarks) {
+      first = mv[e] == kNfMaybe;
+    } else {
+      const u64 j = ts.base + u64(e) * kBlock + tid;
+      first = j < p && nf[j] == kNfMaybe;
+    }
     ts.mask[e] = __ballot(first);
     if (lane == 0) s_pre[e * 4 + wave] = u32(__popcll(ts.mask[e]));
   }
@@ -996,28 +1009,55 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
                                                          u64* __restrict__ count_out, const u64* prev_count,
                                                          const unsigned char* __restrict__ multi,
                                                          u32* __restrict__ hashed_next, uint4* __restrict__ clr_nf,
-                                                         uint4* __restrict__ clr_multi, u64 clr16) {
+                                                         uint4* __restrict__ clr_multi, u64 clr16,
+                                                         u32* __restrict__ sid) {
   // fused small-build levels: clear the marks of the level after this one (its parity
   // set held the previous level's marks, last read by this level's insert)
   for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < clr16; i += u64(gridDim.x) * kBlock) {
     clr_nf[i] = make_uint4(0, 0, 0, 0);
     clr_multi[i] = make_uint4(0, 0, 0, 0);
   }
-  if (level_direct(prev_count, n)) return;
   __shared__ u32 s_tile;
   __shared__ u32 s_pre[4 * ITEMS];
   __shared__ u32 s_hashed;
   TileScan<ITEMS> ts;
-  if (threadIdx.x == 0) s_hashed = 0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  u32 pl[ITEMS], pr[ITEMS];   // the first occurrences' input pairs, read while the scan waits
-  constexpr bool kPre = ITEMS <= kItemsSmall;   // (32 items: the registers cost more than the wait)
+  // Short tiles read their whole input up front (pairs, multi marks, the insert's slot
+  // words), before the gate and the prefix count: one round trip for all of it.  Long
+  // tiles (registers) and look-back tiles (tile known late) read the pairs of their
+  // first occurrences while the scan waits.
+  constexpr bool kPre = ITEMS <= kItemsSmall;
+  const bool early = kPre && desc == nullptr;
+  u32 pl[ITEMS], pr[ITEMS], sw[ITEMS];
+  unsigned char mu[ITEMS];
+  if (kPre) {
+#pragma unroll
+    for (int e = 0; e < ITEMS; ++e) {
+      pl[e] = pr[e] = sw[e] = 0;
+      mu[e] = 0;
+    }
+  }
+  if (early) {
+#pragma unroll
+    for (int e = 0; e < ITEMS; ++e) {
+      const u64 j = u64(blockIdx.x) * (kBlock * ITEMS) + u64(e) * kBlock + tid;
+      if (j < p) {
+        load_pair(in, n, j, pl[e], pr[e]);
+        if (hashed_next || sid) mu[e] = multi[j];
+        if (sid) sw[e] = words[j];
+      }
+    }
+  }
+  if (level_direct(prev_count, n)) return;
+  if (threadIdx.x == 0) s_hashed = 0;
   auto fetch = [&]() {
     if constexpr (kPre) {
+      if (!early) {
 #pragma unroll
-      for (int e = 0; e < ITEMS; ++e) {
-        const u64 j = ts.base + u64(e) * kBlock + tid;
-        if (j < p && ((ts.mask[e] >> lane) & 1ull)) load_pair(in, n, j, pl[e], pr[e]);
+        for (int e = 0; e < ITEMS; ++e) {
+          const u64 j = ts.base + u64(e) * kBlock + tid;
+          if (j < p && ((ts.mask[e] >> lane) & 1ull)) load_pair(in, n, j, pl[e], pr[e]);
+        }
       }
     }
   };
@@ -1027,8 +1067,11 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
 #pragma unroll
   for (int e = 0; e < ITEMS; ++e) {
     const u64 j = ts.base + u64(e) * kBlock + tid;
+    const bool is_first = j < p && ((ts.mask[e] >> lane) & 1ull);
+    unsigned char me = 0;   // multi mark: needed for first occurrences only
+    if ((hashed_next || sid) && is_first) me = early ? mu[e] : multi[j];
     if (hashed_next) {   // next-level pair (j, j+1): both children repeat?  (first <=> mask bit)
-      const bool rep = j < p && (((ts.mask[e] >> lane) & 1ull) == 0 || multi[j] != 0);
+      const bool rep = j < p && (!is_first || me != 0);
       const bool partner = __shfl_xor(int(rep), 1, 64) != 0;
       if ((lane & 1) == 0 && rep && (j + 1 < p ? partner : true)) hashed = true;
     }
@@ -1038,7 +1081,7 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
       g.mask = ts.mask[e]; g.prefix = gpre; g.pad = 0;
       grp[(ts.base >> 6) + e * 4 + wave] = g;
     }
-    if (j < p && ((ts.mask[e] >> lane) & 1ull)) {
+    if (is_first) {
       const u32 id = gpre + u32(__popcll(ts.mask[e] & lt));
       u32 l, r, cl, cr, m, t;
       if constexpr (kPre) {
@@ -1047,6 +1090,9 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
       } else {
         load_pair(in, n, j, l, r);
       }
+      // fused small builds: a repeated key's id by its slot, for the next insert's resolver
+      // (only repeated keys are ever looked up, and their first occurrence is multi)
+      if (sid && me) sid[(early ? sw[e] : words[j]) & kIdx] = id;
       node_canonical(l, r, cl, cr, m, t);
       uint2 w;
       w.x = cl; w.y = cr;
@@ -1667,18 +1713,26 @@ struct TailOut {
 
 [[maybe_unused]] static __global__ __launch_bounds__(kTailThreads) void k_tail(
     const u32* __restrict__ in, u64 n0, const u64* prev_count, int k0, int D, uint2* __restrict__ nodes, TailOut to,
-    Header* __restrict__ hdr) {
+    Header* __restrict__ hdr, const u64* __restrict__ shards) {
   extern __shared__ __align__(16) unsigned char tail_lds[];
   unsigned long long* tkey = reinterpret_cast<unsigned long long*>(tail_lds);
   u32* tpos = reinterpret_cast<u32*>(tkey + kTailSlots);
   u32* wbuf = tpos + kTailSlots;
   __shared__ u32 wsum[kTailItems][kTailThreads / 64];
+  __shared__ u32 wtot;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  u64 sv0 = 0, sv1 = 0;   // shards != null: this launch ends the build (k_build_finish's sum)
+  if (shards) {
+    sv0 = shards[tid * kStatStride];
+    sv1 = shards[tid * kStatStride + 1];
+  }
   for (u64 i = tid; i < n0; i += kTailThreads) wbuf[i] = in[i];
   u32 n = u32(n0);
   bool direct = prev_count && *prev_count == n0;
+  if (shards) stats_sum(sv0, sv1, hdr);
   __syncthreads();
-  for (int k = k0; k < D; ++k) {
+  int k = k0;
+  for (; k < D && n > 128; ++k) {   // the whole block while a level has more than 64 pairs
     const u32 p = (n + 1) / 2;
     uint2* out = nodes + to.layer_off[k];
     u32 cl[kTailItems], cr[kTailItems], mtv[kTailItems], slot[kTailItems];
@@ -1739,18 +1793,26 @@ struct TailOut {
         if (lane == 0) wsum[e][wave] = u32(__popcll(bal[e]));
       }
       __syncthreads();   // (every tpos read is done: firsts now overwrite theirs with the id)
-      u32 base[kTailItems], acc = 0;   // firsts before (item e, this wave): all of items < e, then waves
+      // firsts before (item e, wave w): all of items < e, then waves < w -- one wave scans
+      // the (item, wave) counts in that order, in place
+      constexpr int kNW = kTailThreads / 64, kNC = kTailItems * kNW;
+      static_assert(kNC <= 64, "one wave scans the tail's (item, wave) counts");
+      if (wave == 0) {
+        const u32 c = lane < kNC ? wsum[lane / kNW][lane % kNW] : 0u;
+        u32 incl = c;
 #pragma unroll
-      for (int e = 0; e < kTailItems; ++e) {
-        u32 before = 0, tot = 0;
-        for (int w = 0; w < kTailThreads / 64; ++w) {
-          const u32 c = wsum[e][w];
-          before += w < wave ? c : 0u;
-          tot += c;
+        for (int o = 1; o < 64; o <<= 1) {
+          const u32 y = __shfl_up(incl, o, 64);
+          if (lane >= o) incl += y;
         }
-        base[e] = acc + before;
-        acc += tot;
+        if (lane < kNC) wsum[lane / kNW][lane % kNW] = incl - c;
+        if (lane == 63) wtot = incl;
       }
+      __syncthreads();
+      u32 base[kTailItems];
+#pragma unroll
+      for (int e = 0; e < kTailItems; ++e) base[e] = wsum[e][wave];
+      const u32 acc = wtot;
 #pragma unroll
       for (int e = 0; e < kTailItems; ++e) {
         if ((bal[e] >> lane) & 1ull) {
@@ -1772,7 +1834,41 @@ struct TailOut {
     n = p;
     __syncthreads();
   }
-  if (tid == 0) hdr->root = wbuf[0];
+  // the last levels (<= 64 pairs) in wave 0 alone, with no barriers: lane j holds pair j, a
+  // key's first occurrence is the lowest lane holding it (a uniform sweep of readlanes),
+  // ids are ranks among the first lanes
+  if (wave != 0) return;
+  for (; k < D; ++k) {
+    const u32 p = (n + 1) / 2, j = u32(lane);
+    u32 cl = 0, cr = 0, mtv = 0;
+    if (j < p) {
+      const u32 l = wbuf[2 * j], r = 2 * j + 1 < n ? wbuf[2 * j + 1] : kNullWord;
+      u32 m, t;
+      node_canonical(l, r, cl, cr, m, t);
+      mtv = make_word(0, m, t, ulw(l) == ulw(xf(r, 1, 0)));
+    }
+    u32 id = j, count = p;
+    if (!direct) {
+      const u32 ka = ulw(cl), kb = ulw(cr);
+      u32 f = 64;
+      for (u32 q = 0; q < p; ++q) {
+        const u32 qa = __builtin_amdgcn_readlane(ka, q), qb = __builtin_amdgcn_readlane(kb, q);
+        if (f == 64 && qa == ka && qb == kb) f = q;
+      }
+      const u64 bal = __ballot(j < p && f == j);
+      const u32 rank = u32(__popcll(bal & ((1ull << lane) - 1)));
+      id = u32(__shfl(int(rank), int(f & 63), 64));
+      count = u32(__popcll(bal));
+      if (j < p && f == j) nodes[to.layer_off[k] + rank] = make_uint2(cl, cr);
+    } else if (j < p) {
+      nodes[to.layer_off[k] + j] = make_uint2(cl, cr);
+    }
+    if (j < p) wbuf[j] = id | mtv;   // (every lane has read the level: LDS is in order per wave)
+    if (lane == 0) hdr->count[kLayerSlot + k] = count;
+    direct = count == p;
+    n = p;
+  }
+  if (lane == 0) hdr->root = wbuf[0];
 }
 
 [[maybe_unused]] static __global__ void k_root(const u32* __restrict__ words, Header* __restrict__ hdr) { hdr->root = words[0]; }

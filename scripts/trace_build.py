@@ -6,7 +6,7 @@ import sys
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 starts = [i for i, r in enumerate(rows) if "k_build_init" in r["Kernel_Name"]]
 b = starts[-2]
-end = next(i for i in range(b, len(rows)) if "k_build_finish" in rows[i]["Kernel_Name"])
+end = next(i for i in range(b, len(rows)) if any(x in rows[i]["Kernel_Name"] for x in ("k_tail", "k_build_finish")))
 tot = 0
 for r in rows[b:end + 1]:
     d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
