@@ -18,10 +18,10 @@ namespace {
 
 template <class Tab>
 void launch_leaf_bases(int L, dim3 g, hipStream_t st, const unsigned char* b, u64 i0, u64 i1, const Tab& T,
-                       u32* rec, unsigned char* nf, Header* hdr) {
+                       u32* rec, unsigned char* nf, Header* hdr, u64* lkey) {
   switch (L) {
 #define GCZ_CASE(X) \
-  case X: hipLaunchKernelGGL((k_leaf_bases<X, Tab>), g, dim3(kBlock), 0, st, b, i0, i1, T, rec, nf, hdr); break;
+  case X: hipLaunchKernelGGL((k_leaf_bases<X, Tab>), g, dim3(kBlock), 0, st, b, i0, i1, T, rec, nf, hdr, lkey); break;
     GCZ_CASE(1) GCZ_CASE(2) GCZ_CASE(3) GCZ_CASE(4) GCZ_CASE(5) GCZ_CASE(6) GCZ_CASE(7) GCZ_CASE(8)
     GCZ_CASE(9) GCZ_CASE(10) GCZ_CASE(11) GCZ_CASE(12) GCZ_CASE(13) GCZ_CASE(14) GCZ_CASE(15) GCZ_CASE(16)
 #undef GCZ_CASE
@@ -81,7 +81,6 @@ int gcz_ctx::leaf_level(const LeafLevel& a, Header* d_hdr) {
     lt.pt.sh = (4 * u32(L) + 1) / 2;
     lt.pt.cas_first = cap_boost > 0;   // sparse small-build table: the home slot is mostly free
   }
-  fused_leaf = lt;
   unsigned char* d_nf = nf_set[0];
   hipEvent_t e0{};
   if (a.c_begin == 0 && !a.precleared) {
@@ -105,11 +104,11 @@ int gcz_ctx::leaf_level(const LeafLevel& a, Header* d_hdr) {
     prof_begin(KID_LEAF, e0);
     if (a.bases) {
       const auto* b = static_cast<const unsigned char*>(a.bases);
-      if (lt.packed) launch_leaf_bases(L, g, stream, b, i0, i1, lt.pt, A, d_nf, d_hdr);
-      else launch_leaf_bases(L, g, stream, b, i0, i1, lt.wt, A, d_nf, d_hdr);
+      if (lt.packed) launch_leaf_bases(L, g, stream, b, i0, i1, lt.pt, A, d_nf, d_hdr, a.lkey);
+      else launch_leaf_bases(L, g, stream, b, i0, i1, lt.wt, A, d_nf, d_hdr, a.lkey);
     } else {
       hipLaunchKernelGGL((k_leaf_packed<WideTab>), g, dim3(kBlock), 0, stream, a.leaves, i0, i1, L, lt.wt, A,
-                         d_nf, d_hdr);
+                         d_nf, d_hdr, a.lkey);
     }
     HIP_TRY(hipGetLastError());
     // repetitive data? (switches the node inserts' LDS pre-dedupe; a small build's node
@@ -129,7 +128,7 @@ int gcz_ctx::leaf_level(const LeafLevel& a, Header* d_hdr) {
     u64* ldesc = i1 - i0 <= kSmallScanMax && i0 % 256 == 0 ? nullptr : a.desc + a.desc_off[c];
 #define GCZ_FLAGSCAN_LEAF(TAB, TV, IT)                                                                   \
   hipLaunchKernelGGL((k_flagscan_leaf<TAB, IT>), gs, dim3(kBlock), 0, stream, A, i0, i1, TV, d_nf,      \
-                     ldesc, &a.ticket[c], a.out, id0, &a.count[c])
+                     ldesc, &a.ticket[c], a.out, id0, &a.count[c], a.lkey, a.lsid)
     if (lt.packed) {
       if (tile == u64(kTile)) GCZ_FLAGSCAN_LEAF(PackedTab, lt.pt, kItems);
       else if (tile == u64(kTileSmall)) GCZ_FLAGSCAN_LEAF(PackedTab, lt.pt, kItemsSmall);
@@ -457,8 +456,7 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   };
   auto insert_settling = [&](auto T) {   // the resolver of the previous level (fused builds)
     if (!a.fused) insert(T, NoRes{});
-    else if (a.k == 0 && fused_leaf.packed) insert(T, LeafRes<PackedTab>{fused_leaf.pt, nf_set[prev]});
-    else if (a.k == 0) insert(T, LeafRes<WideTab>{fused_leaf.wt, nf_set[prev]});
+    else if (a.k == 0) insert(T, LeafRes{nf_set[prev], a.sid_prev});
     else insert(T, NodeRes{nf_set[prev], a.sid_prev});
   };
   if (nt.packed) insert_settling(nt.pt);
@@ -603,7 +601,8 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     const bool fused = use_fused && !try_dense && C == 1 && pk[0] < kDirectCheckMin &&
                        !(bucket_now && pk[0] >= bucket_min) && (S > u64(kTailMaxN) || !use_tail);
     const u64 fregion = node_cap0 * 16;
-    if (fused && ((rc = ensure(ftab, 3 * fregion)) || (rc = ensure(fsid, 3 * node_cap0 * 4)))) return rc;
+    if (fused && ((rc = ensure(ftab, 3 * fregion)) || (rc = ensure(fsid, 3 * node_cap0 * 4)) ||
+                  (rc = ensure(flkey, S * 8 + 16)) || (rc = ensure(flsid, leaf_cap * 4)))) return rc;
     auto fregion_ptr = [&](int k) { return static_cast<void*>(ftab.as<unsigned char>() + u64(k % 3) * fregion); };
     // One build's launches, start event to header copy.  A build whose launch sequence
     // has no host decision inside (no dense-level fallback check, no look at the direct
@@ -656,6 +655,8 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       dense_used = false;
       la.precleared = !try_dense;
       la.defer_resolve = fused;
+      la.lkey = fused ? flkey.as<u64>() : nullptr;
+      la.lsid = fused ? flsid.as<u32>() : nullptr;
       if (try_dense) {
         if ((rc = leaf_level_dense(la, d_hdr, &d_hdr->count[C - 1], &dense_used))) return rc;
         if (!dense_used) HIP_TRY(hipMemsetAsync(&d_hdr->dense_fail, 0, 4, stream));
@@ -716,7 +717,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
           na.ftab = fregion_ptr(k);
           na.ftab_next = fregion_ptr(k + 1);
           na.sid = fsid.as<u32>() + u64(k % 3) * node_cap0;
-          na.sid_prev = k > 0 ? fsid.as<u32>() + u64((k - 1) % 3) * node_cap0 : nullptr;
+          na.sid_prev = k > 0 ? fsid.as<u32>() + u64((k - 1) % 3) * node_cap0 : flsid.as<u32>();
           na.p_next = k + 1 < D ? pk[k + 1] : 0;
           na.fused_last = k + 1 == D || (pk[k] <= u64(kTailMaxN) && use_tail);
         }
@@ -753,7 +754,8 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     if (static_seq) {
       const GraphKey key{d_bases, d_leaves, nbases, S, L, leaf_cap, allow_packed, bucket_now, stream,
                          tab.ptr, wa.ptr, wb.ptr, nodes_out.ptr, leaves_out.ptr, nf.ptr, desc.ptr,
-                         fused ? ftab.ptr : nullptr, fused ? fsid.ptr : nullptr, fused};
+                         fused ? ftab.ptr : nullptr, fused ? fsid.ptr : nullptr, fused ? flkey.ptr : nullptr,
+                         fused ? flsid.ptr : nullptr, fused};
       if (graph_exec && key == graph_key) {
         launched = hipGraphLaunch(graph_exec, stream) == hipSuccess;
       } else if (!(key == graph_seen)) {

@@ -166,6 +166,8 @@ struct LeafLevel {
   u64 seed_n = 0;
   bool precleared = false;          // table and marks already cleared (k_build_init)
   bool defer_resolve = false;       // fused small build: level 0's insert settles the repeats
+  u64* lkey = nullptr;              // ... through ids by slot (lsid) the flag scan leaves, emitting
+  u32* lsid = nullptr;              //     first occurrences from the keys the insert stored (lkey)
 };
 
 }  // namespace gcz_host
@@ -179,13 +181,13 @@ struct GraphKey {
   gcz_host::u64 leaf_cap;
   bool packed, bucket;
   hipStream_t stream;
-  void *tab, *wa, *wb, *nodes, *leaves_out, *nf, *desc, *ftab, *fsid;
+  void *tab, *wa, *wb, *nodes, *leaves_out, *nf, *desc, *ftab, *fsid, *flkey, *flsid;
   bool fused;
   bool operator==(const GraphKey& o) const {
     return bases == o.bases && leaves == o.leaves && nbases == o.nbases && S == o.S && L == o.L &&
            leaf_cap == o.leaf_cap && packed == o.packed && bucket == o.bucket && stream == o.stream && tab == o.tab &&
            wa == o.wa && wb == o.wb && nodes == o.nodes && leaves_out == o.leaves_out && nf == o.nf && desc == o.desc &&
-           ftab == o.ftab && fsid == o.fsid && fused == o.fused;
+           ftab == o.ftab && fsid == o.fsid && flkey == o.flkey && flsid == o.flsid && fused == o.fused;
   }
 };
 
@@ -234,7 +236,7 @@ struct gcz_ctx {
   int cap_boost = 0;         // (this build's node-table boost)
   gcz_host::DevBuf ftab;     // ... their node tables, three rotating regions
   gcz_host::DevBuf fsid;     // ... and slot -> id of each table's repeated keys, three regions
-  gcz_host::LevelTab fused_leaf{};   // ... the leaf table level 0's insert settles through
+  gcz_host::DevBuf flkey, flsid;   // ... the leaf level's canonical keys by position, ids by slot
   bool upload_warm = false;   // the runtime's host -> device path has run once (upload_reserve)
   int upload_reserve(size_t bytes);                     // input buffer of `bytes`, touched; the copy path warmed
   int upload(void* d_dst, const void* h_src, size_t n); // stream-ordered before later work on `stream`

@@ -426,7 +426,7 @@ struct PackedTab {
 template <int L, class Tab>
 __global__ __launch_bounds__(kBlock) void k_leaf_bases(const unsigned char* __restrict__ bases, u64 i0, u64 i1,
                                                       Tab T, u32* __restrict__ rec, unsigned char* __restrict__ nf,
-                                                      Header* __restrict__ hdr) {
+                                                      Header* __restrict__ hdr, u64* __restrict__ lkey) {
   __shared__ signed char lut[256];
   __shared__ __align__(16) unsigned char buf[kBlock * L + 16];
   const int tid = threadIdx.x;
@@ -469,6 +469,7 @@ __global__ __launch_bounds__(kBlock) void k_leaf_bases(const unsigned char* __re
   if (bad >= 0) atomicMin(&hdr->err_offset, i * L + u64(bad));
   u32 m, t, v;
   const u64 key = leaf_canonical(x, L, m, t, v);
+  if (lkey) lkey[i] = key;   // (fused small build: the flag scan emits first occurrences from it)
   const Ins r = T.insert_chunk(key, u32(i), Marks{nf, nullptr}, &hdr->leaf_overflow);
   if (r.settled) nf[i] = r.global ? kNfGlobal : kNfDone;
   rec[i] = make_word(r.settled ? r.id : r.slot, m, t, v);
@@ -515,11 +516,12 @@ __global__ __launch_bounds__(kBlock) void k_leaf_bases(const unsigned char* __re
 template <class Tab>
 __global__ __launch_bounds__(kBlock) void k_leaf_packed(const u64* __restrict__ leaves, u64 i0, u64 i1, int L,
                                                        Tab T, u32* __restrict__ rec, unsigned char* __restrict__ nf,
-                                                       Header* __restrict__ hdr) {
+                                                       Header* __restrict__ hdr, u64* __restrict__ lkey) {
   const u64 i = i0 + u64(blockIdx.x) * kBlock + threadIdx.x;
   if (i >= i1) return;
   u32 m, t, v;
   const u64 key = leaf_canonical(leaves[i], L, m, t, v);
+  if (lkey) lkey[i] = key;
   const Ins r = T.insert_chunk(key, u32(i), Marks{nf, nullptr}, &hdr->leaf_overflow);
   if (r.settled) nf[i] = r.global ? kNfGlobal : kNfDone;
   rec[i] = make_word(r.settled ? r.id : r.slot, m, t, v);
@@ -653,13 +655,12 @@ struct NoRes {
   const unsigned char* nf = nullptr;
   __device__ __forceinline__ u32 operator()(unsigned char, u32 w) const { return w; }
 };
-template <class Tab>
-struct LeafRes {   // k_resolve_leaf's rule, one leaf chunk
+struct LeafRes {   // k_resolve_leaf's rule, the ids left by slot (k_flagscan_leaf's lsid)
   static constexpr bool kOn = true;
-  Tab T;
   const unsigned char* nf;
+  const u32* sid;
   __device__ __forceinline__ u32 operator()(unsigned char f, u32 w) const {   // f = the word's mark
-    return f == kNfNot ? T.settled_id(w & kIdx) | (w & kBits) : w;
+    return f == kNfNot ? sid[w & kIdx] | (w & kBits) : w;
   }
 };
 struct NodeRes {   // k_resolve_node's rule, the ids settled by slot (k_flagscan_node's sid)
@@ -968,26 +969,58 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_leaf(u32* __restrict__ word
                                                          const unsigned char* __restrict__ nf,
                                                          u64* __restrict__ desc, u32* __restrict__ ticket,
                                                          u64* __restrict__ out, const u64* __restrict__ id0_p,
-                                                         u64* __restrict__ count_out) {
+                                                         u64* __restrict__ count_out, const u64* __restrict__ lkey,
+                                                         u32* __restrict__ lsid) {
   __shared__ u32 s_tile;
   __shared__ u32 s_pre[4 * ITEMS];
   TileScan<ITEMS> ts;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // fused small build (lkey, lsid given; one chunk, direct tiles): the slot words and keys
+  // are read up front, first occurrences emit the key the insert stored and leave their
+  // id by slot for level 0's insert -- no table read, no settle
+  constexpr bool kShort = ITEMS <= kItemsSmall;
+  const bool early = kShort && lsid != nullptr && desc == nullptr;
+  u32 rw[kShort ? ITEMS : 1];
+  u64 kw[kShort ? ITEMS : 1];
+  if constexpr (kShort) {
+#pragma unroll
+    for (int e = 0; e < ITEMS; ++e) {
+      rw[e] = 0;
+      kw[e] = 0;
+      const u64 j = j0 + u64(blockIdx.x) * (kBlock * ITEMS) + u64(e) * kBlock + tid;
+      if (early && j < p) {
+        rw[e] = words[j];
+        kw[e] = lkey[j];
+      }
+    }
+  }
   const u64 id0 = id0_p ? *id0_p : 0;
   tile_scan(ts, &s_tile, s_pre, nf, j0, p, id0, desc, ticket, count_out);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const u64 lt = (1ull << lane) - 1;
 #pragma unroll
   for (int e = 0; e < ITEMS; ++e) {
     const u64 j = ts.base + u64(e) * kBlock + tid;
     if (j < p && ((ts.mask[e] >> lane) & 1ull)) {
       const u32 id = s_pre[e * 4 + wave] + u32(__popcll(ts.mask[e] & lt));
-      const u32 rec = words[j];
-      u64 key;
-      u32 pos;
-      T.read(rec & kIdx, key, pos);
-      out[id] = key;
-      T.settle(rec & kIdx, id);
-      words[j] = id | (rec & kBits);
+      bool done = false;
+      if constexpr (kShort) {
+        if (early) {
+          out[id] = kw[e];
+          lsid[rw[e] & kIdx] = id;
+          words[j] = id | (rw[e] & kBits);
+          done = true;
+        }
+      }
+      if (!done) {
+        const u32 rec = words[j];
+        u64 key;
+        u32 pos;
+        T.read(rec & kIdx, key, pos);
+        out[id] = key;
+        T.settle(rec & kIdx, id);
+        if (lsid) lsid[rec & kIdx] = id;
+        words[j] = id | (rec & kBits);
+      }
     }
   }
 }
