@@ -1736,38 +1736,63 @@ constexpr unsigned long long kDupProbeMin = 1ull << 17;      // fewer strands: n
 constexpr int kTailThreads = 1024;
 constexpr int kTailItems = kTailMaxN / 2 / kTailThreads;   // pairs per thread
 constexpr int kTailSlots = kTailMaxN;                       // LDS table: load <= 1/2
-// dynamic LDS: the level's words (in place), the table keys, per slot the minimum
-// position and then the id
-constexpr size_t kTailLds = size_t(kTailMaxN) * 4 + size_t(kTailSlots) * 12;
+// dynamic LDS: the table (one 64-bit entry per slot) and the level's words (in place)
+constexpr size_t kTailLds = size_t(kTailSlots) * 8 + size_t(kTailMaxN) * 4;
+
+// A tail level's pair key in 32 bits: child words of the tail are ids < 8192 (14 bits, the
+// null word's index field becomes 0x3fff) plus the mirror and transpose bits (ulw drops v).
+__device__ __forceinline__ u32 tail_ck(u32 w) { return (w & 0x3fffu) | ((w >> 15) & 0xc000u); }
 
 struct TailOut {
   u64 layer_off[GCZ_MAX_LAYERS];   // node offset of each layer within `nodes`
 };
 
+// Tail table entry: [level tag: 5 bits][pair key: 32 bits][position, then id: 16 bits].  An
+// entry of another level's tag is a free slot, so the table is cleared once per launch, and
+// the minimum position of a key is one 64-bit atomicMin (equal tag and key above it).
+constexpr int kTailTagShift = 59, kTailKeyShift = 16;
+
+// A workgroup barrier for LDS hand-offs only: __syncthreads() also drains every global
+// store (s_waitcnt vmcnt(0)), a memory round trip per level for the tail's node writes,
+// which nothing in the launch reads.
+__device__ __forceinline__ void tail_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 [[maybe_unused]] static __global__ __launch_bounds__(kTailThreads) void k_tail(
     const u32* __restrict__ in, u64 n0, const u64* prev_count, int k0, int D, uint2* __restrict__ nodes, TailOut to,
     Header* __restrict__ hdr, const u64* __restrict__ shards) {
   extern __shared__ __align__(16) unsigned char tail_lds[];
-  unsigned long long* tkey = reinterpret_cast<unsigned long long*>(tail_lds);
-  u32* tpos = reinterpret_cast<u32*>(tkey + kTailSlots);
-  u32* wbuf = tpos + kTailSlots;
-  __shared__ u32 wsum[kTailItems][kTailThreads / 64];
-  __shared__ u32 wtot;
+  unsigned long long* tab = reinterpret_cast<unsigned long long*>(tail_lds);
+  u32* wbuf = reinterpret_cast<u32*>(tab + kTailSlots);
+  __shared__ u32 wsum[kTailItems * (kTailThreads / 64)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   u64 sv0 = 0, sv1 = 0;   // shards != null: this launch ends the build (k_build_finish's sum)
   if (shards) {
     sv0 = shards[tid * kStatStride];
     sv1 = shards[tid * kStatStride + 1];
   }
-  for (u64 i = tid; i < n0; i += kTailThreads) wbuf[i] = in[i];
+  {   // the input words: every load in flight at once (n0 <= kTailMaxN)
+    constexpr int kW = kTailMaxN / kTailThreads;
+    u32 v[kW];
+#pragma unroll
+    for (int e = 0; e < kW; ++e) {
+      const u64 i = u64(e) * kTailThreads + tid;
+      v[e] = i < n0 ? in[i] : 0u;
+    }
+#pragma unroll
+    for (int e = 0; e < kW; ++e) {
+      const u64 i = u64(e) * kTailThreads + tid;
+      if (i < n0) wbuf[i] = v[e];
+    }
+  }
+  for (int q = tid; q < kTailSlots; q += kTailThreads) tab[q] = 0;   // tag 0: no level
   u32 n = u32(n0);
   bool direct = prev_count && *prev_count == n0;
-  if (shards) stats_sum(sv0, sv1, hdr);
   __syncthreads();
   int k = k0;
   for (; k < D && n > 128; ++k) {   // the whole block while a level has more than 64 pairs
     const u32 p = (n + 1) / 2;
     uint2* out = nodes + to.layer_off[k];
+    const u64 tag = u64(k - k0 + 1) << kTailTagShift;   // (<= 14 levels: 8192 words down to 1)
     u32 cl[kTailItems], cr[kTailItems], mtv[kTailItems], slot[kTailItems];
 #pragma unroll
     for (int e = 0; e < kTailItems; ++e) {   // pair j = e * kTailThreads + tid: position order is (e, tid)
@@ -1782,7 +1807,7 @@ struct TailOut {
     }
     u32 count;
     if (direct) {
-      __syncthreads();   // (every read of the level's words is done: they are rewritten in place)
+      tail_sync();   // (every read of the level's words is done: they are rewritten in place)
 #pragma unroll
       for (int e = 0; e < kTailItems; ++e) {
         const u32 j = u32(e * kTailThreads + tid);
@@ -1796,77 +1821,73 @@ struct TailOut {
       u32 mask = 1;
       while (mask < 2 * p) mask <<= 1;
       mask -= 1;
-      for (u32 s = tid; s <= mask; s += kTailThreads) {
-        tkey[s] = kEmpty;
-        tpos[s] = ~0u;
-      }
-      __syncthreads();
 #pragma unroll
       for (int e = 0; e < kTailItems; ++e) {
         const u32 j = u32(e * kTailThreads + tid);
         if (j < p) {
-          const unsigned long long key = (u64(ulw(cl[e])) << 31) | ulw(cr[e]);
+          const u32 key = (tail_ck(ulw(cl[e])) << 16) | tail_ck(ulw(cr[e]));
+          const unsigned long long mine = tag | (u64(key) << kTailKeyShift) | j;
           u32 s = slot_hash(key) & mask;
           for (;;) {
-            unsigned long long c = tkey[s];
-            if (c == kEmpty) c = atomicCAS(&tkey[s], kEmpty, key);
-            if (c == kEmpty || c == key) break;
+            unsigned long long c = tab[s];
+            if ((c >> kTailTagShift) != (tag >> kTailTagShift)) {   // free (an older level's entry)
+              const unsigned long long o = atomicCAS(&tab[s], c, mine);
+              if (o == c) break;
+              c = o;
+              if ((c >> kTailTagShift) != (tag >> kTailTagShift)) continue;
+            }
+            if (u32(c >> kTailKeyShift) == key) {
+              atomicMin(&tab[s], mine);
+              break;
+            }
             s = (s + 1) & mask;
           }
-          atomicMin(&tpos[s], j);
           slot[e] = s;
         }
       }
-      __syncthreads();
+      tail_sync();
       u64 bal[kTailItems];
 #pragma unroll
       for (int e = 0; e < kTailItems; ++e) {
         const u32 j = u32(e * kTailThreads + tid);
-        bal[e] = __ballot(j < p && tpos[slot[e]] == j);
-        if (lane == 0) wsum[e][wave] = u32(__popcll(bal[e]));
+        bal[e] = __ballot(j < p && u32(tab[slot[e]] & 0xffffu) == j);
+        if (lane == 0) wsum[e * (kTailThreads / 64) + wave] = u32(__popcll(bal[e]));
       }
-      __syncthreads();   // (every tpos read is done: firsts now overwrite theirs with the id)
-      // firsts before (item e, wave w): all of items < e, then waves < w -- one wave scans
-      // the (item, wave) counts in that order, in place
-      constexpr int kNW = kTailThreads / 64, kNC = kTailItems * kNW;
-      static_assert(kNC <= 64, "one wave scans the tail's (item, wave) counts");
-      if (wave == 0) {
-        const u32 c = lane < kNC ? wsum[lane / kNW][lane % kNW] : 0u;
-        u32 incl = c;
+      tail_sync();   // (every position read is done: firsts now overwrite theirs with the id)
+      // firsts before (item e, wave w): all of items < e, then waves < w -- every wave scans
+      // the 64 (item, wave) counts itself
+      constexpr int kNW = kTailThreads / 64;
+      static_assert(kTailItems * kNW == 64, "one wave-wide scan of the tail's (item, wave) counts");
+      const u32 c = wsum[lane];
+      u32 incl = c;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const u32 y = __shfl_up(incl, o, 64);
-          if (lane >= o) incl += y;
-        }
-        if (lane < kNC) wsum[lane / kNW][lane % kNW] = incl - c;
-        if (lane == 63) wtot = incl;
+      for (int o = 1; o < 64; o <<= 1) {
+        const u32 y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
       }
-      __syncthreads();
-      u32 base[kTailItems];
-#pragma unroll
-      for (int e = 0; e < kTailItems; ++e) base[e] = wsum[e][wave];
-      const u32 acc = wtot;
+      count = u32(__shfl(int(incl), 63, 64));
 #pragma unroll
       for (int e = 0; e < kTailItems; ++e) {
+        const u32 base = u32(__shfl(int(incl - c), e * kNW + wave, 64));
         if ((bal[e] >> lane) & 1ull) {
-          const u32 id = base[e] + u32(__popcll(bal[e] & ((1ull << lane) - 1)));
-          tpos[slot[e]] = id;
+          const u32 id = base + u32(__popcll(bal[e] & ((1ull << lane) - 1)));
+          tab[slot[e]] = (tab[slot[e]] & ~0xffffull) | id;
           out[id] = make_uint2(cl[e], cr[e]);
         }
       }
-      __syncthreads();
+      tail_sync();
 #pragma unroll
       for (int e = 0; e < kTailItems; ++e) {
         const u32 j = u32(e * kTailThreads + tid);
-        if (j < p) wbuf[j] = tpos[slot[e]] | mtv[e];
+        if (j < p) wbuf[j] = u32(tab[slot[e]] & 0xffffu) | mtv[e];
       }
-      count = acc;
     }
     if (tid == 0) hdr->count[kLayerSlot + k] = count;
     direct = count == p;
     n = p;
-    __syncthreads();
+    tail_sync();
   }
+  if (shards) stats_sum(sv0, sv1, hdr);   // (its loads went out at the start)
   // the last levels (<= 64 pairs) in wave 0 alone, with no barriers: lane j holds pair j, a
   // key's first occurrence is the lowest lane holding it (a uniform sweep of readlanes),
   // ids are ranks among the first lanes
