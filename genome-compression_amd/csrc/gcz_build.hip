@@ -472,14 +472,15 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   auto flagscan = [&](auto items) {
     hipLaunchKernelGGL((k_flagscan_node<decltype(items)::value>), gs, dim3(kBlock), 0, stream, a.words, p, a.in, n,
                        knf, d_grp, ndesc, a.ticket, a.out, a.count, a.pcount, mk.multi, a.hashed_next, clr_nf, clr_mu,
-                       clr16, a.fused && !a.fused_last ? a.sid : nullptr);
+                       clr16, a.fused && (!a.fused_last || a.tail_settles) ? a.sid : nullptr);
   };
   if (tile == u64(kTile)) flagscan(std::integral_constant<int, kItems>{});
   else if (tile == u64(kTileSmall)) flagscan(std::integral_constant<int, kItemsSmall>{});
   else flagscan(std::integral_constant<int, kItemsTiny>{});
   HIP_TRY(hipGetLastError());
   prof_end(KID_FLAGSCAN_NODE, e0);
-  if (a.fused && !a.fused_last) return GCZ_OK;   // the next level's insert settles the repeats
+  // the next level's insert (or the tail) settles the repeats
+  if (a.fused && (!a.fused_last || a.tail_settles)) return GCZ_OK;
   prof_begin(KID_RESOLVE_NODE, e0);
   if (nt.packed)
     hipLaunchKernelGGL((k_resolve_node<PackedTab>), gi, dim3(kBlock), 0, stream, a.words, p, nt.pt, knf, d_grp,
@@ -504,7 +505,7 @@ int gcz_ctx::direct_levels(const u32* in, int k0, int nlev, const DirectPlan& dp
 }
 
 int gcz_ctx::tail_levels(const u32* in, u64 n0, const u64* pcount, int k0, int D, const std::vector<u64>& layer_off_,
-                         Header* d_hdr, const u64* shards) {
+                         Header* d_hdr, const u64* shards, const TailSettle& st) {
   TailOut to{};
   for (int k = k0; k < D; ++k) to.layer_off[k] = layer_off_[k];
   hipEvent_t e0{};
@@ -512,7 +513,7 @@ int gcz_ctx::tail_levels(const u32* in, u64 n0, const u64* pcount, int k0, int D
   HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(k_tail), hipFuncAttributeMaxDynamicSharedMemorySize,
                               int(kTailLds)));
   hipLaunchKernelGGL(k_tail, dim3(1), dim3(kTailThreads), kTailLds, stream, in, n0, pcount, k0, D, nodes_out.as<uint2>(), to,
-                     d_hdr, shards);
+                     d_hdr, shards, st);
   HIP_TRY(hipGetLastError());
   prof_end(KID_TAIL, e0);
   return GCZ_OK;
@@ -675,7 +676,15 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
         if (n <= u64(kTailMaxN) && use_tail) {   // the rest fits one workgroup: one launch
           const u64* pc = k == 0 ? &d_hdr->count[C - 1] : prev_regular ? &d_hdr->gate[k - 1]
                                                                          : &d_hdr->count[kLayerSlot + k - 1];
-          if ((rc = tail_levels(in, n, pc, k, D, layer_off, d_hdr, stats.as<u64>()))) return rc;
+          TailSettle st{};
+          if (fused && k > 0) {   // the last fused level's repeats and gate
+            st.nf = nf_set[k & 1];
+            st.sid = fsid.as<u32>() + u64((k - 1) % 3) * node_cap0;
+            st.pcount = &d_hdr->count[kLayerSlot + k - 1];
+            st.phashed = &d_hdr->hashed_next[k - 1];
+            st.gate_out = &d_hdr->gate[k - 1];
+          }
+          if ((rc = tail_levels(in, n, pc, k, D, layer_off, d_hdr, stats.as<u64>(), st))) return rc;
           tail_done = true;
           break;
         }
@@ -720,6 +729,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
           na.sid_prev = k > 0 ? fsid.as<u32>() + u64((k - 1) % 3) * node_cap0 : flsid.as<u32>();
           na.p_next = k + 1 < D ? pk[k + 1] : 0;
           na.fused_last = k + 1 == D || (pk[k] <= u64(kTailMaxN) && use_tail);
+          na.tail_settles = k + 1 < D && pk[k] <= u64(kTailMaxN) && use_tail;
         }
         if ((rc = node_level(na, d_hdr))) return rc;
         prev_regular = true;

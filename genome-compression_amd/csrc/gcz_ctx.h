@@ -137,6 +137,7 @@ struct NodeLevel {
   // table lives in ftab region k % 3, its repeats are settled by the next level's insert
   // unless it is the last one before the tail (resolve launched here)
   bool fused = false, fused_last = false;
+  bool tail_settles = false;        // fused_last and the tail follows: it settles this level's repeats
   u64 p_next = 0;                   // the next level's pairs (its table is cleared here)
   void* ftab = nullptr;             // region base of this level's table
   void* ftab_next = nullptr;        // ... and of the next level's
@@ -338,7 +339,7 @@ struct gcz_ctx {
   // (and, given the statistics shards, sums them: the build's last launch).
   int tail_levels(const gcz_host::u32* in, gcz_host::u64 n0, const gcz_host::u64* pcount, int k0, int D,
                   const std::vector<gcz_host::u64>& layer_off, gcz_dev::Header* d_hdr,
-                  const gcz_host::u64* shards = nullptr);
+                  const gcz_host::u64* shards = nullptr, const gcz_dev::TailSettle& st = {});
   int build(const void* d_bases, const gcz_host::u64* d_leaves, gcz_host::u64 nbases, gcz_host::u64 S, int L);
 };
 

@@ -1757,9 +1757,19 @@ constexpr int kTailTagShift = 59, kTailKeyShift = 16;
 // which nothing in the launch reads.
 __device__ __forceinline__ void tail_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Fused small builds: the tail settles the last fused level's repeats itself (ids by slot,
+// k_flagscan_node's sid) and decides that level's gate from its count and look-ahead flag.
+struct TailSettle {
+  const unsigned char* nf = nullptr;   // null: the input words are final, prev_count gates
+  const u32* sid = nullptr;
+  const u64* pcount = nullptr;
+  const u32* phashed = nullptr;
+  u64* gate_out = nullptr;
+};
+
 [[maybe_unused]] static __global__ __launch_bounds__(kTailThreads) void k_tail(
     const u32* __restrict__ in, u64 n0, const u64* prev_count, int k0, int D, uint2* __restrict__ nodes, TailOut to,
-    Header* __restrict__ hdr, const u64* __restrict__ shards) {
+    Header* __restrict__ hdr, const u64* __restrict__ shards, TailSettle st) {
   extern __shared__ __align__(16) unsigned char tail_lds[];
   unsigned long long* tab = reinterpret_cast<unsigned long long*>(tail_lds);
   u32* wbuf = reinterpret_cast<u32*>(tab + kTailSlots);
@@ -1770,23 +1780,32 @@ __device__ __forceinline__ void tail_sync() { asm volatile("s_waitcnt lgkmcnt(0)
     sv0 = shards[tid * kStatStride];
     sv1 = shards[tid * kStatStride + 1];
   }
-  {   // the input words: every load in flight at once (n0 <= kTailMaxN)
+  {   // the input words (and marks): every load in flight at once (n0 <= kTailMaxN)
     constexpr int kW = kTailMaxN / kTailThreads;
     u32 v[kW];
+    unsigned char f[kW];
 #pragma unroll
     for (int e = 0; e < kW; ++e) {
       const u64 i = u64(e) * kTailThreads + tid;
       v[e] = i < n0 ? in[i] : 0u;
+      f[e] = st.nf && i < n0 ? st.nf[i] : kNfMaybe;
     }
 #pragma unroll
     for (int e = 0; e < kW; ++e) {
       const u64 i = u64(e) * kTailThreads + tid;
+      if (f[e] == kNfNot) v[e] = st.sid[v[e] & kIdx] | (v[e] & kBits);
       if (i < n0) wbuf[i] = v[e];
     }
   }
   for (int q = tid; q < kTailSlots; q += kTailThreads) tab[q] = 0;   // tag 0: no level
   u32 n = u32(n0);
-  bool direct = prev_count && *prev_count == n0;
+  bool direct;
+  if (st.nf) {
+    direct = *st.pcount == n0 || *st.phashed == 0;
+    if (tid == 0) *st.gate_out = direct ? n0 : ~0ull;
+  } else {
+    direct = prev_count && *prev_count == n0;
+  }
   __syncthreads();
   int k = k0;
   for (; k < D && n > 128; ++k) {   // the whole block while a level has more than 64 pairs
