@@ -428,42 +428,59 @@ __global__ __launch_bounds__(kBlock) void k_leaf_bases(const unsigned char* __re
                                                       Tab T, u32* __restrict__ rec, unsigned char* __restrict__ nf,
                                                       Header* __restrict__ hdr, u64* __restrict__ lkey) {
   __shared__ signed char lut[256];
-  __shared__ __align__(16) unsigned char buf[kBlock * L + 16];
+  __shared__ __align__(16) unsigned char buf[L % 4 == 0 ? 16 : kBlock * L + 16];
   const int tid = threadIdx.x;
   lut[tid] = (signed char)nac_code(tid);
   const u64 first = i0 + u64(blockIdx.x) * kBlock;
   const u64 nstr = (i1 - first) < u64(kBlock) ? (i1 - first) : u64(kBlock);
-  const u64 byte0 = first * L;                 // multiple of 4 (kBlock = 256)
-  const u64 nbytes = nstr * L;
-  const u32* src = reinterpret_cast<const u32*>(bases + byte0);
-  u32* dst = reinterpret_cast<u32*>(buf);
-  const u32 nwords = u32(nbytes / 4);
-  if (nstr == u64(kBlock)) {   // full block: L / 4 words per thread, all loads in flight at once
-    constexpr int kW = (L + 3) / 4;
-    u32 v[kW];
-#pragma unroll
-    for (int q = 0; q < kW; ++q) {
-      const u32 w = u32(q) * kBlock + tid;
-      v[q] = w < nwords ? src[w] : 0u;
-    }
-#pragma unroll
-    for (int q = 0; q < kW; ++q) {
-      const u32 w = u32(q) * kBlock + tid;
-      if (w < nwords) dst[w] = v[q];
-    }
-  } else {
-    for (u32 w = tid; w < nwords; w += kBlock) dst[w] = src[w];
-    for (u32 b = nwords * 4 + tid; b < nbytes; b += kBlock) buf[b] = bases[byte0 + b];
-  }
-  __syncthreads();
-  if (u64(tid) >= nstr) return;
   u64 x = 0;
   int bad = -1;
+  if constexpr (L % 4 == 0) {   // a strand is L / 4 aligned words: the wave's loads are contiguous
+    u32 wv[L / 4];
+    if (u64(tid) < nstr) {
+      const u32* src = reinterpret_cast<const u32*>(bases + (first + tid) * L);
 #pragma unroll
-  for (int c = 0; c < L; ++c) {
-    const int code = lut[buf[tid * L + c]];
-    if (code < 0 && bad < 0) bad = c;
-    x |= u64(code & 15) << (4 * c);
+      for (int q = 0; q < L / 4; ++q) wv[q] = src[q];
+    }
+    __syncthreads();   // (the table; the loads are in flight)
+    if (u64(tid) >= nstr) return;
+#pragma unroll
+    for (int c = 0; c < L; ++c) {
+      const int code = lut[(wv[c / 4] >> (8 * (c % 4))) & 0xffu];
+      if (code < 0 && bad < 0) bad = c;
+      x |= u64(code & 15) << (4 * c);
+    }
+  } else {   // staged through LDS (coalesced 4-B loads of the block's bytes)
+    const u64 byte0 = first * L;                 // multiple of 4 (kBlock = 256)
+    const u64 nbytes = nstr * L;
+    const u32* src = reinterpret_cast<const u32*>(bases + byte0);
+    u32* dst = reinterpret_cast<u32*>(buf);
+    const u32 nwords = u32(nbytes / 4);
+    if (nstr == u64(kBlock)) {   // full block: L / 4 words per thread, all loads in flight at once
+      constexpr int kW = (L + 3) / 4;
+      u32 v[kW];
+#pragma unroll
+      for (int q = 0; q < kW; ++q) {
+        const u32 w = u32(q) * kBlock + tid;
+        v[q] = w < nwords ? src[w] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < kW; ++q) {
+        const u32 w = u32(q) * kBlock + tid;
+        if (w < nwords) dst[w] = v[q];
+      }
+    } else {
+      for (u32 w = tid; w < nwords; w += kBlock) dst[w] = src[w];
+      for (u32 b = nwords * 4 + tid; b < nbytes; b += kBlock) buf[b] = bases[byte0 + b];
+    }
+    __syncthreads();
+    if (u64(tid) >= nstr) return;
+#pragma unroll
+    for (int c = 0; c < L; ++c) {
+      const int code = lut[buf[tid * L + c]];
+      if (code < 0 && bad < 0) bad = c;
+      x |= u64(code & 15) << (4 * c);
+    }
   }
   const u64 i = first + tid;
   if (bad >= 0) atomicMin(&hdr->err_offset, i * L + u64(bad));
