@@ -402,12 +402,12 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     prof_begin(KID_BKT_FINE, e0);
     hipLaunchKernelGGL(k_bkt_fine, dim3(unsigned((u64(1) << b2.b1) * b2.nslice)), dim3(kBktThreads),
                        size_t(kFineCap) * 8, stream, bkt_key.as<u64>(), bkt_cnt.as<u32>(), b2, bkt_rec2.as<u64>(),
-                       bkt_off.as<u32>(), d_hdr, a.pcount, n);
+                       bkt_off.as<u32>(), d_hdr, a.pcount, n, &d_hdr->bkt_overflow);
     HIP_TRY(hipGetLastError());
     prof_end(KID_BKT_FINE, e0);
     prof_begin(KID_BKT_DEDUPE, e0);
-    hipLaunchKernelGGL(k_bkt_dedupe2, dim3(1u << bb), dim3(kBktThreads), 0, stream, bkt_rec2.as<u64>(),
-                       bkt_off.as<u32>(), b2, a.words, mk, d_hdr, a.pcount, n);
+    hipLaunchKernelGGL(k_bkt_dedupe2<false>, dim3(1u << bb), dim3(kBktThreads), 0, stream, bkt_rec2.as<u64>(),
+                       bkt_off.as<u32>(), b2, a.words, mk, d_hdr, a.pcount, n, &d_hdr->bkt_overflow);
     HIP_TRY(hipGetLastError());
     prof_end(KID_BKT_DEDUPE, e0);
   } else if (bkt) {

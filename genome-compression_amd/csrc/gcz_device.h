@@ -1263,7 +1263,7 @@ __device__ __forceinline__ u64 bkt_chunk(u64 G) {
 }
 
 __device__ __forceinline__ bool bkt_skip(const Header* hdr, const u64* prev_count, u64 n) {
-  return level_direct(prev_count, n) || hdr->predup != 0;
+  return hdr && (level_direct(prev_count, n) || hdr->predup != 0);   // (null: the multi-rank owner)
 }
 
 // Column g of the count matrix: cnt[b * G + g] = hashed pairs of chunk g in bucket b.
@@ -1521,7 +1521,7 @@ __device__ __forceinline__ void lds_excl256(u32* c, u32 n) {
 // fine offsets fo[(c * nslice + s) * (2^b2 + 1) + f].
 [[maybe_unused]] static __global__ __launch_bounds__(kBktThreads) void k_bkt_fine(
     const u64* __restrict__ seg, const u32* __restrict__ rt, Bkt2Plan bp, u64* __restrict__ out,
-    u32* __restrict__ fo, Header* __restrict__ hdr, const u64* prev_count, u64 n) {
+    u32* __restrict__ fo, Header* __restrict__ hdr, const u64* prev_count, u64 n, u32* __restrict__ ovf) {
   if (bkt_skip(hdr, prev_count, n)) return;
   extern __shared__ u64 stage[];   // kFineCap records (dynamic)
   __shared__ u32 s_pre[129], s_beg[128];   // runs of the slice's chunks (SC <= 128)
@@ -1556,7 +1556,7 @@ __device__ __forceinline__ void lds_excl256(u32* c, u32 n) {
   const u32 total = s_pre[nsc];
   u32* fos = fo + u64(blockIdx.x) * (nb2 + 1);
   if (total > u32(kFineCap)) {   // a hot key the probe missed: the table path handles this data
-    if (threadIdx.x == 0) hdr->bkt_overflow = 1;
+    if (threadIdx.x == 0) *ovf = 1;
     for (u32 q = threadIdx.x; q <= nb2; q += kBktThreads) fos[q] = 0;
     return;
   }
@@ -1594,10 +1594,13 @@ __device__ __forceinline__ void lds_excl256(u32* c, u32 n) {
   for (u32 i = threadIdx.x; i < total; i += kBktThreads) o[i] = stage[i];
 }
 
-// One workgroup per fine bucket b = c * 2^b2 + f.
-[[maybe_unused]] static __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
+// One workgroup per fine bucket b = c * 2^b2 + f.  kOwner (the multi-rank owner dedupe,
+// positions = receive indices): every record of a repeated key gets the key's first index
+// in oslot (`rec`), instead of the not-first words pointing at it.
+template <bool kOwner>
+__global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
     const u64* __restrict__ recs, const u32* __restrict__ fo, Bkt2Plan bp, u32* __restrict__ rec, Marks mk,
-    Header* __restrict__ hdr, const u64* prev_count, u64 n) {
+    Header* __restrict__ hdr, const u64* prev_count, u64 n, u32* __restrict__ ovf) {
   if (bkt_skip(hdr, prev_count, n)) return;
   constexpr u32 TS = kBktSlots;
   __shared__ u64 s_key[TS];
@@ -1638,7 +1641,7 @@ __device__ __forceinline__ void lds_excl256(u32* c, u32 n) {
   __syncthreads();
   const u32 total = s_pre[ns];
   if (total > u32(kBktCap)) {   // a hot key: the table path handles this data
-    if (threadIdx.x == 0) hdr->bkt_overflow = 1;
+    if (threadIdx.x == 0) *ovf = 1;
     return;
   }
   const u64 pmask = (1ull << bp.P) - 1;
@@ -1683,9 +1686,10 @@ __device__ __forceinline__ void lds_excl256(u32* c, u32 n) {
   for (int e = 0; e < kBktCapItems; ++e) {
     if (key[e] == kEmpty || !((s_dup[slot[e] >> 5] >> (slot[e] & 31)) & 1u)) continue;
     const u32 first = s_pos[slot[e]];
+    if constexpr (kOwner) rec[pos[e]] = first;
     if (pos[e] != first) {
       mk.nf[pos[e]] = kNfNot;
-      rec[pos[e]] = first | (rec[pos[e]] & kBits);
+      if constexpr (!kOwner) rec[pos[e]] = first | (rec[pos[e]] & kBits);
     } else {
       mk.multi[pos[e]] = 1;
     }

@@ -32,6 +32,7 @@ struct gcz_dist_state {
   DevBuf dict;                                                                // rank 0's leaf dictionary
   DevBuf rkey, oslot, rflag, rcval, rdval, owntab, oids, omin;                // owner side
   DevBuf ob_cnt, ob_off, ob_desc, ob_rec;                                      // owner bucketed dedupe
+  DevBuf ob_seg, ob_rt, ob_rec2, ob_fo;                                        // ... as the two-pass partition
   DevBuf dhdr, gath, gath2, gathf, ddesc, tail_in;
   u64* h_gath = nullptr;    // pinned mirrors of the gathered vectors
   u64* h_gath2 = nullptr;
@@ -43,7 +44,8 @@ void gcz_dist_state_free(gcz_ctx* c) {
   if (!d) return;
   for (DevBuf* b : {&d->dict, &d->scratch, &d->gnf, &d->gmul, &d->gid, &d->blockcnt, &d->bchunk, &d->skey, &d->sidx, &d->sflag,
                     &d->scval, &d->sdval, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab, &d->oids,
-                    &d->omin, &d->ob_cnt, &d->ob_off, &d->ob_desc, &d->ob_rec,
+                    &d->omin, &d->ob_cnt, &d->ob_off, &d->ob_desc, &d->ob_rec, &d->ob_seg, &d->ob_rt,
+                    &d->ob_rec2, &d->ob_fo,
                     &d->dhdr, &d->gath, &d->gath2, &d->gathf, &d->ddesc, &d->tail_in})
     if (b->ptr) (void)hipFree(b->ptr);
   for (u64* h : {d->h_gath, d->h_gath2, d->h_gathf})
@@ -528,6 +530,7 @@ struct gcz_group {
   int dense_mode = std::getenv("GCZ_DENSE") ? std::atoi(std::getenv("GCZ_DENSE")) : 1;   // 0: hash-table leaves
   // owners hash-cons levels without the local dedupe in LDS buckets (GCZ_OWNER_BUCKETS=0: the table)
   bool owner_buckets = !std::getenv("GCZ_OWNER_BUCKETS") || std::atoi(std::getenv("GCZ_OWNER_BUCKETS")) != 0;
+  bool owner_two_pass = !std::getenv("GCZ_OWNER_TWO") || std::atoi(std::getenv("GCZ_OWNER_TWO")) != 0;
   int exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, u32 key_bits, u32 child_bits,
                std::vector<u64>& c, std::vector<u64>& off, u64& total, u64* err_global, int* err_sym,
                int* ovf_bits, bool nolocal = false, bool lookahead = false, u64* next_hashed_out = nullptr);
@@ -954,6 +957,25 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
         ob.nr = nr;
         use_ob = ob.K >= ob.bb && ob.K - ob.bb + kDLog <= 64 && ob.nch <= 8192;
       }
+      // ... preferably as the single-device two-pass partition (whole-run writes)
+      Bkt2Plan b2{};
+      bool use_ob2 = false;
+      if (use_ob && owner_two_pass) {
+        u32 bb = 0;
+        while (bb < u32(kBktMaxLog) && (nr >> bb) > 2560) ++bb;
+        b2.T = opos[i].pt;
+        b2.K = key_bits;
+        b2.b1 = std::min<u32>(bb, kPartMaxB1);
+        b2.b2 = bb - b2.b1;
+        b2.G = (nr + kPartChunk - 1) / kPartChunk;
+        const u64 mean_run = std::max<u64>(1, std::min<u64>(nr, kPartChunk) >> b2.b1);
+        b2.SC = u32(std::max<u64>(1, std::min<u64>(128, u64(kFineCap / 2) / mean_run)));
+        b2.SC = 1u << log2_exact(b2.SC);
+        b2.P = kPartLog + log2_exact(b2.SC);
+        b2.nslice = u32((b2.G + b2.SC - 1) / b2.SC);
+        use_ob2 = key_bits >= bb && b2.b2 <= u32(kFineMaxB2) && key_bits - b2.b1 + kPartLog <= 64 &&
+                  key_bits - bb + b2.P <= 64 && mean_run * b2.SC <= u64(kFineCap) / 2 && b2.nslice <= 512;
+      }
       if (!use_ob)
         G_HIP(hipMemsetAsync(d.owntab.ptr, 0xff, size_t(otab[i].mask + 1) * (otab[i].packed ? 8 : 16), cx->stream));
       const Displ D = displ_of(rank[i]);
@@ -961,7 +983,26 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
         unsigned char* onf = d.omin.as<unsigned char>();
         unsigned char* omul = onf + nr + 32;
         G_HIP(hipMemsetAsync(onf, 0, 2 * nr + 64, cx->stream));
-        if (use_ob) {
+        if (use_ob2) {
+          const u64 nfine = (u64(1) << b2.b1) * b2.nslice;
+          if (cx->ensure(d.ob_seg, b2.G * kPartChunk * 8) || cx->ensure(d.ob_rt, b2.G * ((u64(1) << b2.b1) + 1) * 4 + 16) ||
+              cx->ensure(d.ob_rec2, nfine * kFineCap * 8) || cx->ensure(d.ob_fo, nfine * ((u64(1) << b2.b2) + 1) * 4 + 16))
+            return dev_fail("owner partition");
+          G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_ob_part),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, int(kPartChunk * 8)));
+          G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_bkt_fine),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, int(kFineCap * 8)));
+          u32* ovf = &cx->hdr.as<Header>()->overflow;
+          hipLaunchKernelGGL(k_ob_part, dim3(unsigned(b2.G)), dim3(kBktThreads), size_t(kPartChunk) * 8, cx->stream,
+                             d.rkey.as<u64>(), nr, b2, child_bits, d.ob_seg.as<u64>(), d.ob_rt.as<u32>());
+          hipLaunchKernelGGL(k_bkt_fine, dim3(unsigned(nfine)), dim3(kBktThreads), size_t(kFineCap) * 8, cx->stream,
+                             d.ob_seg.as<u64>(), d.ob_rt.as<u32>(), b2, d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(),
+                             static_cast<Header*>(nullptr), static_cast<const u64*>(nullptr), nr, ovf);
+          hipLaunchKernelGGL(k_bkt_dedupe2<true>, dim3(unsigned(u64(1) << (b2.b1 + b2.b2))), dim3(kBktThreads), 0,
+                             cx->stream, d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(), b2, d.oslot.as<u32>(),
+                             Marks{onf, omul}, static_cast<Header*>(nullptr), static_cast<const u64*>(nullptr), nr,
+                             ovf);
+        } else if (use_ob) {
           const u64 ncnt = (u64(1) << ob.bb) * ob.nch, t = scan_tiles(ncnt + 1);
           if (cx->ensure(d.ob_cnt, ncnt * 4 + 16) || cx->ensure(d.ob_off, (ncnt + 1) * 4 + 16) ||
               cx->ensure(d.ob_desc, t * 8 + 64) || cx->ensure(d.ob_rec, nr * 8 + 16))

@@ -446,6 +446,52 @@ struct OwnBkt {
   __device__ __forceinline__ u64 hash(u64 raw) const { return T.mix(own_pack_key(raw & ~kLocalMulti, 0, B)); }
 };
 
+// The owner dedupe as the single-device two-pass partition (k_bkt_fine, k_bkt_dedupe2<true>
+// follow): pass 1 sorts each chunk of kPartChunk receive indices by the b1 coarse bits of
+// h = T.mix(packed key) in LDS and writes the records back contiguously with the chunk's
+// run table -- whole runs instead of k_ob_scatter's scattered 8-B stores.
+static __global__ __launch_bounds__(kBktThreads) void k_ob_part(const u64* __restrict__ rkey, u64 nr, Bkt2Plan bp,
+                                                                u32 B, u64* __restrict__ seg, u32* __restrict__ rt) {
+  extern __shared__ u64 stage[];   // kPartChunk records (dynamic)
+  __shared__ u32 cur[(1u << kPartMaxB1) + 1];
+  const u32 nb1 = 1u << bp.b1;
+  for (u32 q = threadIdx.x; q <= nb1; q += kBktThreads) cur[q] = 0;
+  const u64 g = blockIdx.x, j0 = g * kPartChunk;
+  u64 x[kPartItems];
+#pragma unroll
+  for (int e = 0; e < kPartItems; ++e) {
+    const u64 j = j0 + u64(e) * kBktThreads + threadIdx.x;
+    x[e] = j < nr ? rkey[j] : 0ull;
+  }
+  __syncthreads();
+  const u32 sh1 = bp.K - bp.b1;
+  const u64 lowmask = sh1 >= 64 ? ~0ull : (1ull << sh1) - 1;
+  u64 r[kPartItems];
+  u32 slot[kPartItems];   // coarse bucket << 16 | rank in it
+#pragma unroll
+  for (int e = 0; e < kPartItems; ++e) {
+    const u64 j = j0 + u64(e) * kBktThreads + threadIdx.x;
+    slot[e] = ~0u;
+    if (j >= nr) continue;
+    const u64 h = bp.T.mix(own_pack_key(x[e] & ~kLocalMulti, 0, B));
+    const u32 c = bp.b1 ? u32(h >> sh1) : 0u;
+    r[e] = ((h & lowmask) << kPartLog) | (j - j0);
+    slot[e] = (c << 16) | atomicAdd(&cur[c], 1u);
+  }
+  __syncthreads();
+  lds_excl256(cur, nb1);
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < kPartItems; ++e)
+    if (slot[e] != ~0u) stage[cur[slot[e] >> 16] + (slot[e] & 0xffffu)] = r[e];
+  __syncthreads();
+  const u32 total = cur[nb1];
+  u64* out = seg + g * kPartChunk;
+  for (u32 i = threadIdx.x; i < total; i += kBktThreads) out[i] = stage[i];
+  u32* rts = rt + g * (nb1 + 1);
+  for (u32 q = threadIdx.x; q <= nb1; q += kBktThreads) rts[q] = cur[q];
+}
+
 static __global__ __launch_bounds__(1024) void k_ob_count(const u64* __restrict__ rkey, OwnBkt P,
                                                           u32* __restrict__ cnt) {
   __shared__ u32 hist[4096];
