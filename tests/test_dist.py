@@ -291,3 +291,29 @@ def test_dist_leaf_dictionary(seed, world, gcz, manifest, oracle, monkeypatch):
             assert np.array_equal(t.layer(k), ref.layer(k)), k
     finally:
         g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+def test_dist_owner_hot_pair_overflow(world, gcz, oracle):
+    """Node levels without the local dedupe (GCZ_DIST_LOCAL=2: the owners partition their
+    records in LDS buckets) and one pair planted 30,000 times: its owner's slice overflows,
+    the build reruns on the tables -- same tree as the oracle."""
+    rng = np.random.default_rng(101 + world)
+    S = 2_600_000
+    leaves = rng.integers(0, 1 << 48, size=S, dtype=np.uint64)
+    a, b = np.uint64(0x123456789AB), np.uint64(0xBA987654321)
+    js = rng.choice(np.arange(S // 2 + 2**20, S, 2), size=30_000, replace=False)
+    leaves[js] = a
+    leaves[js + 1] = b
+    ref = oracle.build_leaves(leaves, 12)
+    g = _group_with_env(gcz, world, {"GCZ_DIST_LOCAL": "2"})
+    try:
+        _dist_build(gcz, g, "leaves", leaves, 12)
+        t = g.tree()
+        assert np.array_equal(t.leaves(), ref.leaves())
+        for k in range(ref.n_layers):
+            assert np.array_equal(t.layer(k), ref.layer(k)), k
+        assert t.root == ref.root
+    finally:
+        g.close()
