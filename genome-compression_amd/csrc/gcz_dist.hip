@@ -453,10 +453,26 @@ struct DistPlan {
     if (G < 0) G = 0;
     const u64 g = 1ull << G;
     B = (T + g - 1) / g * g;
+    // Rank 0 also gathers the top and finishes it alone (~0.1 ms at 1 Gbase over 8 ranks
+    // against ~1.1 ms per rank, most of it not proportional to the share), so it takes a
+    // smaller share: 1000 - 25 R permille of B (0.80 at R = 8, 0.95 at R = 2), the rest
+    // spread over the others (GCZ_DIST_RANK0_PERMILLE overrides; 1000 = even shares).  Only
+    // where the ranks hold >= 2^20 strands, so every share stays a multiple of 2^G far
+    // above 256.
+    const char* e0 = std::getenv("GCZ_DIST_RANK0_PERMILLE");
+    const u64 pm = e0 ? u64(std::max(500, std::min(1000, std::atoi(e0)))) : u64(std::max(700, 1000 - 25 * R));
+    B0 = B1 = B;
+    if (R > 1 && G > 0 && T >= (1ull << 20) && pm < 1000) {
+      B0 = std::max<u64>(g, B * pm / 1000 / g * g);
+      B1 = ((S - std::min(S, B0)) + u64(R - 1) - 1) / u64(R - 1);
+      B1 = (B1 + g - 1) / g * g;
+    }
   }
+  u64 B0 = 0, B1 = 0;   // rank 0's strands, every other rank's (the last: the remainder)
+  u64 first(int r) const { return r == 0 ? 0 : B0 + u64(r - 1) * B1; }
   // element range of rank r at the input of node level k (k = 0: strands), k <= G
-  u64 start(int r, int k) const { return std::min((u64(r) * B) >> k, nk[k]); }
-  u64 end(int r, int k) const { return std::min((u64(r + 1) * B) >> k, nk[k]); }
+  u64 start(int r, int k) const { return std::min(first(r) >> k, nk[k]); }
+  u64 end(int r, int k) const { return std::min(first(r + 1) >> k, nk[k]); }
   u64 count(int r, int k) const { return end(r, k) - start(r, k); }
 };
 
