@@ -456,8 +456,7 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   };
   auto insert_settling = [&](auto T) {   // the resolver of the previous level (fused builds)
     if (!a.fused) insert(T, NoRes{});
-    else if (a.k == 0) insert(T, LeafRes{nf_set[prev], a.sid_prev});
-    else insert(T, NodeRes{nf_set[prev], a.sid_prev});
+    else insert(T, SlotRes{nf_set[prev], a.sid_prev});   // (k = 0: the leaves' ids by slot)
   };
   if (nt.packed) insert_settling(nt.pt);
   else insert_settling(nt.wt);

@@ -662,30 +662,25 @@ __device__ __forceinline__ void stats_sum(u64 v0, u64 v1, Header* __restrict__ h
 // ---- fused small-build levels --------------------------------------------------------
 // Small builds (no bucketed level, no host look at the gates) run each node level as two
 // launches instead of four: the insert of level k settles level k-1's repeats itself (the
-// resolve: a not-first child word takes its key's first id) and writes the final words
-// back into its input, and the tables and marks a level needs are cleared by the
-// launches two steps before it (tables in three rotating regions, marks in the two
-// parity sets).  The previous level's gate is decided by the insert from its count and
+// resolve: a not-first child word takes its key's first id, which level k-1's flag scan
+// left by table slot) and writes the final words back into its input; the insert of
+// level k clears level k+1's table (three rotating regions: level k-1's is still read)
+// and the flag scan of level k clears level k+1's marks (the parity set level k's insert
+// read last).  The previous level's gate is decided by the insert from its count and
 // look-ahead flag (block 0 stores it for the launches behind).
 struct NoRes {
   static constexpr bool kOn = false;
   const unsigned char* nf = nullptr;
   __device__ __forceinline__ u32 operator()(unsigned char, u32 w) const { return w; }
 };
-struct LeafRes {   // k_resolve_leaf's rule, the ids left by slot (k_flagscan_leaf's lsid)
+// k_resolve_leaf's / k_resolve_node's rule with the ids by slot (k_flagscan_leaf's lsid,
+// k_flagscan_node's sid): a not-first word holds its key's slot
+struct SlotRes {
   static constexpr bool kOn = true;
-  const unsigned char* nf;
+  const unsigned char* nf;   // the previous level's not-first marks
   const u32* sid;
   __device__ __forceinline__ u32 operator()(unsigned char f, u32 w) const {   // f = the word's mark
     return f == kNfNot ? sid[w & kIdx] | (w & kBits) : w;
-  }
-};
-struct NodeRes {   // k_resolve_node's rule, the ids settled by slot (k_flagscan_node's sid)
-  static constexpr bool kOn = true;
-  const unsigned char* nf;
-  const u32* sid;
-  __device__ __forceinline__ u32 operator()(unsigned char fm, u32 w) const {
-    return fm == kNfNot ? sid[w & kIdx] | (w & kBits) : w;
   }
 };
 struct FuseIn {
