@@ -565,7 +565,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   // small builds: a launch lasts as long as its longest probe chain, so their tables are
   // sparser (a few MB at most)
   const bool small = S <= 2 * kDirectCheckMin;
-  if (small) leaf_cap = full_cap << small_cap_shift;
+  if (small) leaf_cap = full_cap << (small_leaf_shift >= 0 ? small_leaf_shift : small_cap_shift);
   cap_boost = small ? small_cap_shift : 0;
   const u64 node_cap0 = node_cap(pk[0]);
 
@@ -891,6 +891,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   if (const char* t = std::getenv("GCZ_GRAPH")) c->use_graph = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_FUSED")) c->use_fused = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_SMALL_CAP_SHIFT")) c->small_cap_shift = std::max(0, std::min(4, std::atoi(t)));
+  if (const char* t = std::getenv("GCZ_SMALL_LEAF_SHIFT")) c->small_leaf_shift = std::max(0, std::min(4, std::atoi(t)));
   if (const char* t = std::getenv("GCZ_LEAF_FIRST_LOG2")) c->leaf_first_log2 = std::max(1, std::min(20, std::atoi(t)));
   *out = c;
   return GCZ_OK;

@@ -234,6 +234,7 @@ struct gcz_ctx {
   bool use_graph = true;     // small builds as a replayed HIP graph       (GCZ_GRAPH=0 disables)
   bool use_fused = true;     // small builds: two launches per node level  (GCZ_FUSED=0 disables)
   int small_cap_shift = 2;   // ... and tables 2^this times the usual size: short probe chains (GCZ_SMALL_CAP_SHIFT)
+  int small_leaf_shift = -1; // ... the leaf table's own (GCZ_SMALL_LEAF_SHIFT; -1: small_cap_shift)
   int cap_boost = 0;         // (this build's node-table boost)
   gcz_host::DevBuf ftab;     // ... their node tables, three rotating regions
   gcz_host::DevBuf fsid;     // ... and slot -> id of each table's repeated keys, three regions
