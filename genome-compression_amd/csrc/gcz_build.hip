@@ -259,8 +259,8 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
   prof_begin(KID_DL_FIRST, e0);
   if (list && (1u << P.IB) < 64) HIP_TRY(hipMemsetAsync(dl_pb.ptr, 0, (ncodes / 64 + 1) * 8, stream));
   hipLaunchKernelGGL(k_dl_first, dim3(P.NB), dim3(kDThreads), first_bytes, stream, dl_rec.as<u32>(), dl_off.as<u32>(),
-                     P, dl_fpg.as<u32>(), dl_fl.as<u32>(), dl_fo.as<u32>(),
-                     list ? dl_pb.as<unsigned long long>() : nullptr);
+                     P, list ? nullptr : dl_fpg.as<u32>(), dl_fl.as<u32>(), dl_fo.as<u32>(),
+                     list ? dl_pb.as<unsigned long long>() : nullptr);   // (multi-rank: ids come from gid)
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_dl_fb, dim3(P.nch), dim3(kDThreads), 0, stream, dl_fl.as<u32>(), dl_fo.as<u32>(), P,
                      dl_fb.as<unsigned long long>());

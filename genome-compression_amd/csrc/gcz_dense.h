@@ -331,7 +331,7 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
   for (int k = 0; k < PER; ++k) {
     const u32 i = u32(k) * kDThreads + tid;
     fp[k] = i < RB ? s_fp[i] : ~0u;
-    if (i < RB) fpg[u64(b) * RB + i] = fp[k];
+    if (fpg && i < RB) fpg[u64(b) * RB + i] = fp[k];
     rk[k] = fp[k] != ~0u ? atomicAdd(&s_cnt[fp[k] >> kDLog], 1u) : 0u;
     if (pb) {
       const u32 h = (b << P.IB) | i;
