@@ -1783,6 +1783,14 @@ struct TailSettle {
   u64* gate_out = nullptr;
 };
 
+#ifdef GCZ_TAIL_PROBE   // (tools/microbench/tail.hip: wall-clock stamps of each tail level)
+__device__ unsigned long long gcz_tail_probe[64];
+#define GCZ_TAIL_STAMP(i) \
+  if (threadIdx.x == 0) gcz_tail_probe[(i) & 63] = wall_clock64()
+#else
+#define GCZ_TAIL_STAMP(i)
+#endif
+
 [[maybe_unused]] static __global__ __launch_bounds__(kTailThreads) void k_tail(
     const u32* __restrict__ in, u64 n0, const u64* prev_count, int k0, int D, uint2* __restrict__ nodes, TailOut to,
     Header* __restrict__ hdr, const u64* __restrict__ shards, TailSettle st) {
@@ -1824,7 +1832,9 @@ struct TailSettle {
   }
   __syncthreads();
   int k = k0;
+  GCZ_TAIL_STAMP(0);
   for (; k < D && n > 128; ++k) {   // the whole block while a level has more than 64 pairs
+    GCZ_TAIL_STAMP(k - k0 + 1);
     const u32 p = (n + 1) / 2;
     uint2* out = nodes + to.layer_off[k];
     const u64 tag = u64(k - k0 + 1) << kTailTagShift;   // (<= 14 levels: 8192 words down to 1)
@@ -1928,6 +1938,7 @@ struct TailSettle {
   // ids are ranks among the first lanes
   if (wave != 0) return;
   for (; k < D; ++k) {
+    GCZ_TAIL_STAMP(k - k0 + 1);
     const u32 p = (n + 1) / 2, j = u32(lane);
     u32 cl = 0, cr = 0, mtv = 0;
     if (j < p) {
@@ -1958,6 +1969,7 @@ struct TailSettle {
     n = p;
   }
   if (lane == 0) hdr->root = wbuf[0];
+  GCZ_TAIL_STAMP(63);
 }
 
 [[maybe_unused]] static __global__ void k_root(const u32* __restrict__ words, Header* __restrict__ hdr) { hdr->root = words[0]; }
