@@ -1746,7 +1746,10 @@ struct DirectPlan {
 // LDS table (CAS claims, atomicMin keeps the first position, a block scan
 // ranks the first occurrences) -- the same ids, nodes and words as the
 // per-level kernels, without ~4 launches per level.
-constexpr int kTailMaxN = 8192;
+#ifndef GCZ_TAIL_MAXN
+#define GCZ_TAIL_MAXN 8192   // (tools/microbench/tail.hip builds other sizes)
+#endif
+constexpr int kTailMaxN = GCZ_TAIL_MAXN;
 constexpr unsigned long long kDirectCheckMin = 1ull << 16;   // levels below: no host look at the direct gate
 constexpr unsigned long long kDupProbeMin = 1ull << 17;      // fewer strands: no repetitive-data probe
 constexpr int kTailThreads = 1024;
@@ -1798,7 +1801,9 @@ __device__ unsigned long long gcz_tail_probe[64];
   unsigned long long* tab = reinterpret_cast<unsigned long long*>(tail_lds);
   u32* wbuf = reinterpret_cast<u32*>(tab + kTailSlots);
   __shared__ u32 wsum[kTailItems * (kTailThreads / 64)];
+  __shared__ u64 s_off[GCZ_MAX_LAYERS];   // the layer offsets, read once (not per level from the arguments)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < GCZ_MAX_LAYERS) s_off[tid] = to.layer_off[tid];
   u64 sv0 = 0, sv1 = 0;   // shards != null: this launch ends the build (k_build_finish's sum)
   if (shards) {
     sv0 = shards[tid * kStatStride];
@@ -1836,7 +1841,7 @@ __device__ unsigned long long gcz_tail_probe[64];
   for (; k < D && n > 128; ++k) {   // the whole block while a level has more than 64 pairs
     GCZ_TAIL_STAMP(k - k0 + 1);
     const u32 p = (n + 1) / 2;
-    uint2* out = nodes + to.layer_off[k];
+    uint2* out = nodes + s_off[k];
     const u64 tag = u64(k - k0 + 1) << kTailTagShift;   // (<= 14 levels: 8192 words down to 1)
     u32 cl[kTailItems], cr[kTailItems], mtv[kTailItems], slot[kTailItems];
 #pragma unroll
@@ -1902,8 +1907,8 @@ __device__ unsigned long long gcz_tail_probe[64];
       // firsts before (item e, wave w): all of items < e, then waves < w -- every wave scans
       // the 64 (item, wave) counts itself
       constexpr int kNW = kTailThreads / 64;
-      static_assert(kTailItems * kNW == 64, "one wave-wide scan of the tail's (item, wave) counts");
-      const u32 c = wsum[lane];
+      static_assert(kTailItems * kNW <= 64, "one wave-wide scan of the tail's (item, wave) counts");
+      const u32 c = lane < kTailItems * kNW ? wsum[lane] : 0u;
       u32 incl = c;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
@@ -1959,9 +1964,9 @@ __device__ unsigned long long gcz_tail_probe[64];
       const u32 rank = u32(__popcll(bal & ((1ull << lane) - 1)));
       id = u32(__shfl(int(rank), int(f & 63), 64));
       count = u32(__popcll(bal));
-      if (j < p && f == j) nodes[to.layer_off[k] + rank] = make_uint2(cl, cr);
+      if (j < p && f == j) nodes[s_off[k] + rank] = make_uint2(cl, cr);
     } else if (j < p) {
-      nodes[to.layer_off[k] + j] = make_uint2(cl, cr);
+      nodes[s_off[k] + j] = make_uint2(cl, cr);
     }
     if (j < p) wbuf[j] = id | mtv;   // (every lane has read the level: LDS is in order per wave)
     if (lane == 0) hdr->count[kLayerSlot + k] = count;
