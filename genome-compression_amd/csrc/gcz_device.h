@@ -1591,7 +1591,8 @@ __device__ __forceinline__ void lds_excl256(u32* c, u32 n) {
 
 // One workgroup per fine bucket b = c * 2^b2 + f.  kOwner (the multi-rank owner dedupe,
 // positions = receive indices): every record of a repeated key gets the key's first index
-// in oslot (`rec`), instead of the not-first words pointing at it.
+// in oslot (`rec`), instead of the not-first words pointing at it, and mk.nf is the reply
+// itself (k_own_reply_marks' flags: 7 not first, 6 the first of a repeated key, 0 else).
 template <bool kOwner>
 __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
     const u64* __restrict__ recs, const u32* __restrict__ fo, Bkt2Plan bp, u32* __restrict__ rec, Marks mk,
@@ -1681,10 +1682,12 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
   for (int e = 0; e < kBktCapItems; ++e) {
     if (key[e] == kEmpty || !((s_dup[slot[e] >> 5] >> (slot[e] & 31)) & 1u)) continue;
     const u32 first = s_pos[slot[e]];
-    if constexpr (kOwner) rec[pos[e]] = first;
-    if (pos[e] != first) {
+    if constexpr (kOwner) {
+      rec[pos[e]] = first;
+      mk.nf[pos[e]] = pos[e] != first ? 7 : 6;
+    } else if (pos[e] != first) {
       mk.nf[pos[e]] = kNfNot;
-      if constexpr (!kOwner) rec[pos[e]] = first | (rec[pos[e]] & kBits);
+      rec[pos[e]] = first | (rec[pos[e]] & kBits);
     } else {
       mk.multi[pos[e]] = 1;
     }

@@ -999,7 +999,8 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       if (opos[i].packed) {
         unsigned char* onf = d.omin.as<unsigned char>();
         unsigned char* omul = onf + nr + 32;
-        G_HIP(hipMemsetAsync(onf, 0, 2 * nr + 64, cx->stream));
+        if (use_ob2) G_HIP(hipMemsetAsync(d.rflag.ptr, 0, nr + 16, cx->stream));   // (the reply, written directly)
+        else G_HIP(hipMemsetAsync(onf, 0, 2 * nr + 64, cx->stream));
         if (use_ob2) {
           const u64 nfine = (u64(1) << b2.b1) * b2.nslice;
           if (cx->ensure(d.ob_seg, b2.G * kPartChunk * 8) || cx->ensure(d.ob_rt, b2.G * ((u64(1) << b2.b1) + 1) * 4 + 16) ||
@@ -1017,8 +1018,8 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
                              static_cast<Header*>(nullptr), static_cast<const u64*>(nullptr), nr, ovf);
           hipLaunchKernelGGL(k_bkt_dedupe2<true>, dim3(unsigned(u64(1) << (b2.b1 + b2.b2))), dim3(kBktThreads), 0,
                              cx->stream, d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(), b2, d.oslot.as<u32>(),
-                             Marks{onf, omul}, static_cast<Header*>(nullptr), static_cast<const u64*>(nullptr), nr,
-                             ovf);
+                             Marks{d.rflag.as<unsigned char>(), nullptr}, static_cast<Header*>(nullptr),
+                             static_cast<const u64*>(nullptr), nr, ovf);
         } else if (use_ob) {
           const u64 ncnt = (u64(1) << ob.bb) * ob.nch, t = scan_tiles(ncnt + 1);
           if (cx->ensure(d.ob_cnt, ncnt * 4 + 16) || cx->ensure(d.ob_off, (ncnt + 1) * 4 + 16) ||
@@ -1042,8 +1043,9 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
                              child_bits, opos[i].pt, Marks{onf, omul}, d.oslot.as<u32>(),
                              &cx->hdr.as<Header>()->overflow);
         }
-        hipLaunchKernelGGL(k_own_reply_marks, blocks(nr), dim3(kBlock), 0, cx->stream, onf, omul, nr,
-                           d.rflag.as<unsigned char>());
+        if (!use_ob2)
+          hipLaunchKernelGGL(k_own_reply_marks, blocks(nr), dim3(kBlock), 0, cx->stream, onf, omul, nr,
+                             d.rflag.as<unsigned char>());
       } else {
         if (nolocal) G_HIP(hipMemsetAsync(d.omin.ptr, 0xff, size_t(otab[i].mask + 1) * 4, cx->stream));
         hipLaunchKernelGGL(k_own_insert, blocks(nr), dim3(kBlock), 0, cx->stream, d.rkey.as<u64>(), nr, D, u32(R),
