@@ -124,6 +124,18 @@ __device__ __forceinline__ bool rec_get(const RecSrc& s, u64 e, u64& key, u32& l
 
 __device__ __forceinline__ u64 rec_key(const RecSrc& s, u64 key) { return s.leaves ? key : (key & ~kLocalMulti); }
 
+// rec_get for levels without the local dedupe (canonical pairs given, no singleton
+// marks): every load of the record issued at once, none behind the not-first mark.
+__device__ __forceinline__ bool rec_get_canon(const RecSrc& s, u64 e, u64& key, u32& lid) {
+  const u64 es = e < s.p ? e : 0;   // (in bounds; used only when e < p)
+  const unsigned char f = s.nf[es], mu = s.multi[es];
+  const uint2 c = s.canon[es];
+  const u32 w = s.words[es];
+  key = ((u64(ulw(c.x)) << 31) | ulw(c.y)) | (mu ? kLocalMulti : 0ull);
+  lid = w & kIdx;
+  return e < s.p && f == kNfMaybe;
+}
+
 // Bucketing by owner, deterministic two-pass: per-block counts, one scan, scatter.
 static __global__ __launch_bounds__(kBlock) void k_bucket_count(RecSrc s, u32* __restrict__ blockcnt, u32 nb) {
   __shared__ u32 h[kMaxRanks];
@@ -243,36 +255,58 @@ static __global__ __launch_bounds__(kBlock) void k_bucket_scatter(RecSrc s, cons
   for (int q = tid; q < kWaves * kMaxRanks; q += kBlock) (&wcnt[0][0])[q] = 0;
   __syncthreads();
   const u64 lt = (1ull << lane) - 1;
-  for (int e = 0; e < kItems; ++e) {
-    const u64 idx = u64(blockIdx.x) * kTile + u64(e) * kBlock + tid;
-    u64 key = 0;
-    u32 lid = 0;
-    const bool ok = rec_get(s, idx, key, lid);
-    const u32 d = ok ? owner_of(rec_key(s, key), s.R) : 0u;
-    u32 before = 0;
-    u64 left = __ballot(ok);
-    while (left) {                                  // one ballot per distinct destination in the wave
-      const int leader = __ffsll((long long)left) - 1;
-      const u32 dl = __shfl(d, leader, 64);
-      const u64 m = __ballot(ok && d == dl);
-      if (ok && d == dl) before = __popcll(m & lt);
-      if (lane == leader) wcnt[wave][dl] = u32(__popcll(m));
-      left &= ~m;
+  // canonical-pair levels: the records of kPre items are loaded together (straight-line,
+  // in flight at once) instead of one dependent pair of loads per item
+  constexpr int kPre = 8;
+  const bool pre = s.canon != nullptr && s.prev_nf == nullptr && s.leaves == nullptr;
+  for (int e0 = 0; e0 < kItems; e0 += kPre) {
+    u64 pkey[kPre];
+    u32 plid[kPre];
+    bool pok[kPre];
+    if (pre) {
+#pragma unroll
+      for (int q = 0; q < kPre; ++q)
+        pok[q] = rec_get_canon(s, u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid, pkey[q], plid[q]);
     }
-    __syncthreads();
-    if (ok) {
-      u32 o = cur[d] + before;
-      for (int w = 0; w < wave; ++w) o += wcnt[w][d];
-      skey[o] = key;
-      sidx[o] = lid;
+#pragma unroll
+    for (int q = 0; q < kPre; ++q) {
+      const u64 idx = u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid;
+      u64 key = 0;
+      u32 lid = 0;
+      bool ok;
+      if (pre) {
+        ok = pok[q];
+        key = pkey[q];
+        lid = plid[q];
+      } else {
+        ok = rec_get(s, idx, key, lid);
+      }
+      const u32 d = ok ? owner_of(rec_key(s, key), s.R) : 0u;
+      u32 before = 0;
+      u64 left = __ballot(ok);
+      while (left) {                                  // one ballot per distinct destination in the wave
+        const int leader = __ffsll((long long)left) - 1;
+        const u32 dl = __shfl(d, leader, 64);
+        const u64 m = __ballot(ok && d == dl);
+        if (ok && d == dl) before = __popcll(m & lt);
+        if (lane == leader) wcnt[wave][dl] = u32(__popcll(m));
+        left &= ~m;
+      }
+      __syncthreads();
+      if (ok) {
+        u32 o = cur[d] + before;
+        for (int w = 0; w < wave; ++w) o += wcnt[w][d];
+        skey[o] = key;
+        sidx[o] = lid;
+      }
+      __syncthreads();
+      if (tid < int(s.R)) {
+        u32 t = 0;
+        for (int w = 0; w < kWaves; ++w) { t += wcnt[w][tid]; wcnt[w][tid] = 0; }
+        cur[tid] += t;
+      }
+      __syncthreads();
     }
-    __syncthreads();
-    if (tid < int(s.R)) {
-      u32 t = 0;
-      for (int w = 0; w < kWaves; ++w) { t += wcnt[w][tid]; wcnt[w][tid] = 0; }
-      cur[tid] += t;
-    }
-    __syncthreads();
   }
 }
 
