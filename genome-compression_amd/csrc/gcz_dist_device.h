@@ -124,16 +124,26 @@ __device__ __forceinline__ bool rec_get(const RecSrc& s, u64 e, u64& key, u32& l
 
 __device__ __forceinline__ u64 rec_key(const RecSrc& s, u64 key) { return s.leaves ? key : (key & ~kLocalMulti); }
 
-// rec_get for levels without the local dedupe (canonical pairs given, no singleton
-// marks): every load of the record issued at once, none behind the not-first mark.
+// rec_get for levels without the local dedupe (canonical pairs given): every load of the
+// record issued at once, none behind the not-first mark.
 __device__ __forceinline__ bool rec_get_canon(const RecSrc& s, u64 e, u64& key, u32& lid) {
   const u64 es = e < s.p ? e : 0;   // (in bounds; used only when e < p)
   const unsigned char f = s.nf[es], mu = s.multi[es];
   const uint2 c = s.canon[es];
   const u32 w = s.words[es];
+  bool single = false;
+  if (s.prev_nf) {
+    if (2 * es + 1 < s.n) {
+      const uchar2 pf = reinterpret_cast<const uchar2*>(s.prev_nf)[es];
+      const uchar2 pm = reinterpret_cast<const uchar2*>(s.prev_multi)[es];
+      single = (pf.x == 0 && pm.x == 0) || (pf.y == 0 && pm.y == 0);
+    } else {
+      single = s.prev_nf[2 * es] == 0 && s.prev_multi[2 * es] == 0;
+    }
+  }
   key = ((u64(ulw(c.x)) << 31) | ulw(c.y)) | (mu ? kLocalMulti : 0ull);
   lid = w & kIdx;
-  return e < s.p && f == kNfMaybe;
+  return e < s.p && f == kNfMaybe && !single;
 }
 
 // Bucketing by owner, deterministic two-pass: per-block counts, one scan, scatter.
@@ -258,7 +268,7 @@ static __global__ __launch_bounds__(kBlock) void k_bucket_scatter(RecSrc s, cons
   // canonical-pair levels: the records of kPre items are loaded together (straight-line,
   // in flight at once) instead of one dependent pair of loads per item
   constexpr int kPre = 8;
-  const bool pre = s.canon != nullptr && s.prev_nf == nullptr && s.leaves == nullptr;
+  const bool pre = s.canon != nullptr && s.leaves == nullptr;
   for (int e0 = 0; e0 < kItems; e0 += kPre) {
     u64 pkey[kPre];
     u32 plid[kPre];
@@ -903,31 +913,73 @@ static __global__ __launch_bounds__(kBlock) void k_node_keys(const u32* __restri
     __syncthreads();
   }
   if (blockIdx.x == 0 && tid == 0) *count_out = p;
-  for (int e = 0; e < kItems; ++e) {
-    const u64 j = u64(blockIdx.x) * kTile + u64(e) * kBlock + tid;
-    if (j >= p) break;
-    u32 l, r, cl, cr, m, t;
-    load_pair(in, n, j, l, r);
-    if (gid) {
-      auto glob = [&](u32 w, u64 strand) {
-        if ((w & kIdx) == kIdx) return w;                            // the odd tail's null
-        if (gmark && gmark[strand] == kNfGlobal) return w;           // seeded: already global
-        const u32 g = gid[w & kIdx];
-        return ((g & kLocalId) ? (g & ~kLocalId) + off : g) | (w & kBits);
-      };
-      l = glob(l, 2 * j);
-      r = glob(r, 2 * j + 1);
+  // kB items at a time: their pairs (and the previous level's marks) loaded together, then
+  // their leaf-id lookups together, then the work -- no dependent loads per item.  The
+  // bucketing count takes the record straight from registers (a pair with a singleton
+  // child is not sent: rec_get's rule).
+  constexpr int kB = 8;
+  auto glob = [&](u32 w, u64 strand, unsigned char gm, u32 g) {
+    if ((w & kIdx) == kIdx) return w;                            // the odd tail's null
+    if (gmark && gm == kNfGlobal) return w;                      // seeded: already global
+    (void)strand;
+    return ((g & kLocalId) ? (g & ~kLocalId) + off : g) | (w & kBits);
+  };
+  for (int e0 = 0; e0 < kItems; e0 += kB) {
+    u32 L[kB], Rw[kB];
+    uchar2 pf[kB], pm[kB];
+#pragma unroll
+    for (int q = 0; q < kB; ++q) {
+      const u64 j = u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid;
+      L[q] = Rw[q] = kNullWord;
+      pf[q] = pm[q] = make_uchar2(1, 1);
+      if (j < p) {
+        load_pair(in, n, j, L[q], Rw[q]);
+        if (blockcnt && rs.prev_nf) {
+          if (2 * j + 1 < n) {
+            pf[q] = reinterpret_cast<const uchar2*>(rs.prev_nf)[j];
+            pm[q] = reinterpret_cast<const uchar2*>(rs.prev_multi)[j];
+          } else {
+            pf[q] = make_uchar2(rs.prev_nf[2 * j], 1);
+            pm[q] = make_uchar2(rs.prev_multi[2 * j], 1);
+          }
+        }
+      }
     }
-    node_canonical(l, r, cl, cr, m, t);
-    const u32 v = ulw(l) == ulw(xf(r, 1, 0));
-    pairs[j] = make_uint2(cl, cr);
-    words[j] = make_word(u32(j), m, t, v);
-    nf[j] = kNfMaybe;
-    multi[j] = 0;
-    if (blockcnt) {
-      u64 key;
-      u32 lid;
-      if (rec_get(rs, j, key, lid)) atomicAdd(&h[owner_of(rec_key(rs, key), rs.R)], 1u);
+    if (gid) {
+      u32 gl[kB], gr[kB];
+      unsigned char ml[kB], mr[kB];
+#pragma unroll
+      for (int q = 0; q < kB; ++q) {
+        const u64 j = u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid;
+        const bool okj = j < p;
+        gl[q] = okj && (L[q] & kIdx) != kIdx ? gid[L[q] & kIdx] : 0u;
+        gr[q] = okj && (Rw[q] & kIdx) != kIdx ? gid[Rw[q] & kIdx] : 0u;
+        ml[q] = okj && gmark ? gmark[2 * j] : 0;
+        mr[q] = okj && gmark && 2 * j + 1 < n ? gmark[2 * j + 1] : 0;
+      }
+#pragma unroll
+      for (int q = 0; q < kB; ++q) {
+        const u64 j = u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid;
+        L[q] = glob(L[q], 2 * j, ml[q], gl[q]);
+        Rw[q] = glob(Rw[q], 2 * j + 1, mr[q], gr[q]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kB; ++q) {
+      const u64 j = u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid;
+      if (j >= p) continue;
+      const u32 l = L[q], r = Rw[q];
+      u32 cl, cr, m, t;
+      node_canonical(l, r, cl, cr, m, t);
+      const u32 v = ulw(l) == ulw(xf(r, 1, 0));
+      pairs[j] = make_uint2(cl, cr);
+      words[j] = make_word(u32(j), m, t, v);
+      nf[j] = kNfMaybe;
+      multi[j] = 0;
+      if (blockcnt) {
+        const bool single = rs.prev_nf && ((pf[q].x == 0 && pm[q].x == 0) || (pf[q].y == 0 && pm[q].y == 0));
+        if (!single) atomicAdd(&h[owner_of((u64(ulw(cl)) << 31) | ulw(cr), rs.R)], 1u);
+      }
     }
   }
   if (blockcnt) {
