@@ -766,18 +766,28 @@ static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restr
   if (tid < int(R)) { hc[tid] = 0; hd[tid] = 0; }
   __syncthreads();
   const u64 k0 = u64(blockIdx.x) * kTile;
-  for (int e = 0; e < kItems; ++e) {
-    const u64 k = k0 + u64(e) * kBlock + tid;
-    unsigned char f = 0;
-    if (k < nsent) {
-      const u32 lid = sidx[k];
-      f = sflag[k];
-      gnf[lid] = f & 1;
-      gmul[lid] = (f >> 1) & 1;
+  constexpr int kB = 8;   // records whose index and flag are loaded together
+  for (int e0 = 0; e0 < kItems; e0 += kB) {
+    u32 li[kB];
+    unsigned char fl[kB];
+#pragma unroll
+    for (int b = 0; b < kB; ++b) {
+      const u64 k = k0 + u64(e0 + b) * kBlock + tid;
+      li[b] = k < nsent ? sidx[k] : 0u;
+      fl[b] = k < nsent ? sflag[k] : 0;
     }
-    const u32 q = (want_c(f) || want_d(f)) ? seg_of(SD, R, k) : 0u;
-    (void)wave_append(hc, q, k < nsent && want_c(f));
-    (void)wave_append(hd, q, k < nsent && want_d(f));
+#pragma unroll
+    for (int b = 0; b < kB; ++b) {
+      const u64 k = k0 + u64(e0 + b) * kBlock + tid;
+      const unsigned char f = fl[b];
+      if (k < nsent) {
+        gnf[li[b]] = f & 1;
+        gmul[li[b]] = (f >> 1) & 1;
+      }
+      const u32 q = (want_c(f) || want_d(f)) ? seg_of(SD, R, k) : 0u;
+      (void)wave_append(hc, q, k < nsent && want_c(f));
+      (void)wave_append(hd, q, k < nsent && want_d(f));
+    }
   }
   __syncthreads();
   if (tid < int(R)) {
@@ -871,12 +881,16 @@ static __global__ __launch_bounds__(kBlock) void k_dist_remap(u32* __restrict__ 
                                                               const unsigned char* __restrict__ gmark) {
   const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
   if (j >= p) return;
-  if (gmark && gmark[j] == kNfGlobal) return;   // seeded leaf: the word holds its global id
+  // the word, its marks and the seeding mark in one round trip, then the id lookups
+  const unsigned char gm = gmark ? gmark[j] : 0;
   const u32 w = words[j];
+  const unsigned char f = multi ? nf[j] : 0;
+  if (gmark && gm == kNfGlobal) return;   // seeded leaf: the word holds its global id
   const u32 lid = w & kIdx;
   const u32 g = gid[lid];
+  const unsigned char gmu = multi && f == kNfMaybe ? gmul[lid] : 0;
   words[j] = ((g & kLocalId) ? (g & ~kLocalId) + off : g) | (w & kBits);
-  if (multi && nf[j] == kNfMaybe && gmul[lid]) multi[j] = 1;
+  if (gmu) multi[j] = 1;
 }
 
 static __global__ void k_dist_pack(const Header* __restrict__ h, const u64* __restrict__ ucount,
