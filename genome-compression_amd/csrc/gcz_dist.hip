@@ -795,7 +795,7 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
       if (total)
         hipLaunchKernelGGL(k_dl_gid, dim3(unsigned((total + 255) / 256)), dim3(256), 0, cx->stream,
                            cx->dl_recv.as<u32>(), dseg, int(seg.size()), total, cx->dl_gid.as<u32>(),
-                           cx->dl_pb.as<unsigned long long>());
+                           static_cast<const unsigned long long*>(nullptr));   // (filtering by presence: slower)
       const u64 cr = c[rank[i]];
       if (cr)
         hipLaunchKernelGGL(k_dl_leaves, dim3(unsigned((cr + 255) / 256)), dim3(256), 0, cx->stream,
