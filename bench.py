@@ -275,9 +275,10 @@ def weak_run(gcz, ctx, group, dist, cfg, args, seed, L, world, rank, barrier):
             i1 = run1()
         barrier()
         dt1 = time.perf_counter() - t0
-        t = torch.tensor([dt1], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt1 = float(t.item())
+        if dist is not None:
+            t = torch.tensor([dt1], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt1 = float(t.item())
         dev1.free()
         out = {"nbases": S1 * L, "per_gpu_nbases": S1 * L // world, "value": S1 * L * args.steps / dt1,
                "ms_per_step": dt1 / args.steps * 1e3, "device_ms": i1["build_ms"], "n_leaves": i1["n_leaves"],
@@ -350,6 +351,7 @@ def main():
     seed = gcz._lib.gcz_synth_default_seed()
     ctx = gcz.Context(local if args.transport == "rccl" else 0)   # shm: every rank on GPU 0
     group = None
+    transport_used = "rccl" if args.transport == "rccl" else "shm"
     if mode == "dist":
         s0, s1, G = gcz.dist_plan(S, world, rank)
         host = genome(gcz, cfg, seed, s0 * L, s1 * L)
@@ -363,7 +365,27 @@ def main():
             uid = [gcz.dist_unique_id() if rank == 0 else None]
             if dist is not None:
                 dist.broadcast_object_list(uid, src=0)
-            group = gcz.Group.rccl(ctx, rank, world, uid[0])
+            err = None
+            try:
+                group = gcz.Group.rccl(ctx, rank, world, uid[0])
+            except gcz.GczError as e:   # every rank learns of any rank's failure (gloo)
+                err = str(e)
+            failed = [err is not None]
+            if dist is not None:
+                flags = [None] * world
+                dist.all_gather_object(flags, failed[0])
+                failed = [any(flags)]
+            if failed[0]:
+                # RCCL could not form the communicator: the same build with host-staged
+                # exchanges (correct, slower), labelled in the line -- not a silent switch
+                print(f"bench: RCCL group failed ({err}); falling back to the shm transport", file=sys.stderr)
+                if group is not None:
+                    group.close()
+                name = [f"/gcz_bench_{os.getpid()}_{time.time_ns()}" if rank == 0 else None]
+                if dist is not None:
+                    dist.broadcast_object_list(name, src=0)
+                group = gcz.Group.shm(ctx, rank, world, name[0], args.shm_region_mb << 20)
+                transport_used = "shm (RCCL group creation failed)"
         prof_ctx = ctx
         run = lambda: group.build_device_bases([dev.ptr], S, L)  # noqa: E731
     elif mode == "virtual":
@@ -531,7 +553,7 @@ def main():
         text.free()
 
     weak_line = None
-    if mode == "dist" and args.mode == "strong" and not args.no_weak and cfg["kind"] != "file":
+    if mode == "dist" and world > 1 and args.mode == "strong" and not args.no_weak and cfg["kind"] != "file":
         weak_line = weak_run(gcz, ctx, group, dist, cfg, args, seed, L, world, rank, barrier)
 
     cpu = cpu_job.result() if cpu_job is not None else None
@@ -548,7 +570,7 @@ def main():
                        "parallelism": {"single": "1 GPU",
                                        "dist": f"dist{world}: one genome, strand ranges per GPU "
                                                f"({'1 config genome per GPU' if weak else 'config genome split'}), "
-                                               "owner-hashed RCCL all-to-all per level",
+                                               f"owner-hashed all-to-all per level over {transport_used}",
                                        "replicas": f"{world} independent genomes, one per GPU",
                                        "virtual": f"{args.virtual} virtual ranks on 1 GPU (overhead probe)"}[mode]},
             "roofline": roofline,

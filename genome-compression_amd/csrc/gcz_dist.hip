@@ -162,12 +162,14 @@ struct RcclApi {
 };
 
 // RCCL is loaded on first use; a process that already holds torch's RCCL
-// (same SONAME) shares it.
+// (same SONAME) shares it.  RTLD_LOCAL: a copy torch loads LATER (its own
+// librccl.so) must not bind its globals to ours -- with RTLD_GLOBAL both
+// copies' static destructors ran on one set of objects at exit (double free).
 RcclApi& rccl() {
   static RcclApi api = [] {
     RcclApi a;
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
     if (!h) return a;
 #define GCZ_SYM(field, name) a.field = reinterpret_cast<decltype(a.field)>(dlsym(h, name))
     GCZ_SYM(GetUniqueId, "ncclGetUniqueId");

@@ -49,3 +49,22 @@ def test_bench_multiprocess_shm(world):
     assert wk["golden"] == f"synth/uniform_{world * 100_000_003}"
     assert wk["nbases"] == world * 100_000_003 // 12 * 12
     assert wk["layer_sizes_match"] and wk["root_match"], wk
+
+
+@pytest.mark.gpu
+def test_bench_rccl_world1():
+    """The RCCL group path in one process (bench.py --rccl-world1): our librccl is
+    dlopen'd before torch loads its own copy; the process must also EXIT cleanly
+    (both copies resident: RTLD_GLOBAL once made their destructors double-free)."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--rccl-world1", "--config", "uniform_100m",
+           "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=REPO)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and lines, p.stdout[-2000:] + p.stderr[-4000:]
+    d = json.loads(lines[-1])
+    assert d["n_gpus"] == 1 and d["value"] > 0
+    assert d["config"]["parallelism"].endswith("over rccl"), d["config"]["parallelism"]
+    par = d["parity"]
+    for k in ("layers_sha256_match", "leaves_sha256_match", "root_match", "layer_sizes_match"):
+        assert par[k] is True, (k, par)
+    assert d["weak_scaling"] is None
