@@ -318,6 +318,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
+        # A collective that never completes (a peer that died inside RCCL, a fabric
+        # fault) would otherwise hold every rank until the launcher's own limit: after
+        # GCZ_BENCH_WATCHDOG_S seconds each rank dumps all thread stacks to stderr and exits with status 1.
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ.get("GCZ_BENCH_WATCHDOG_S", "900")), exit=True)
         # CPU-side rendezvous only (barrier, max-over-ranks).  torch is imported
         # before libgcz so the process holds a single HIP runtime; no GPU tensor
         # or collective is on the build path.

@@ -213,7 +213,6 @@ struct gcz_ctx {
   // last build
   gcz_info info{};
   std::vector<gcz_host::u64> layer_off;  // node offsets (in nodes) per layer within nodes_out
-  gcz_host::u64 leaf_cap_hint = 0;
   bool allow_packed = true;
   // profiling
   bool profile = false;
