@@ -582,7 +582,10 @@ def main():
             "build": {"device_ms": info["build_ms"], "hashed_pairs": info["hashed_pairs"],
                       "bucketed_pairs": info.get("bucketed_pairs", 0), "b_stream": b_stream, "b_table": b_table,
                       "hbm_frac_survey_formula": round(build_frac, 5), "n_leaves": info["n_leaves"],
-                      "n_layers": info["n_layers"]},
+                      "n_layers": info["n_layers"],
+                      # builds of the last step (> 1: a bucket / leaf-table overflow rebuilt it;
+                      # device_ms is the last attempt, device_ms_all every attempt's)
+                      "attempts": info.get("attempts", 1), "device_ms_all": info.get("build_ms_all")},
             "kernels": kernels,
             "rank_kernel_ms": rank_ms,
             "rank_timeline": rank_detail,
