@@ -322,7 +322,7 @@ def main():
         # fault) would otherwise hold every rank until the launcher's own limit: after
         # GCZ_BENCH_WATCHDOG_S seconds each rank dumps all thread stacks to stderr and exits with status 1.
         import faulthandler
-        faulthandler.dump_traceback_later(float(os.environ.get("GCZ_BENCH_WATCHDOG_S", "900")), exit=True)
+        faulthandler.dump_traceback_later(float(os.environ.get("GCZ_BENCH_WATCHDOG_S", "600")), exit=True)
         # CPU-side rendezvous only (barrier, max-over-ranks).  torch is imported
         # before libgcz so the process holds a single HIP runtime; no GPU tensor
         # or collective is on the build path.
