@@ -20,19 +20,6 @@
 
 namespace {
 
-std::string bytes_to_string(double size) {   // utility.h:200-216
-  constexpr std::array<const char*, 7> suffix{"B", "KB", "MB", "GB", "TB", "PB", "EB"};
-  std::size_t order = 0;
-  while (size >= 1000.0 && order < suffix.size() - 1) {
-    size /= 1000.0;
-    ++order;
-  }
-  std::stringstream s;
-  s.precision(3);
-  s << size << ' ' << suffix[order];
-  return s.str();
-}
-
 void print_input(const std::filesystem::path& input, std::uintmax_t file_size) {
   std::cout << "\n============================================================\n"
             << " Input\n"

@@ -39,6 +39,7 @@
 
 #include "dna.h"
 #include "fasta_reader.h"
+#include "utility.h"   // the reference's shared_tree.h:24 includes it too
 
 class pointer {
  public:

@@ -103,3 +103,70 @@ def test_compress_cli_gpus_errors(tmp_path, manifest):
                         os.path.join(GOLDEN, "fasta", "bad_symbol.fa")], capture_output=True, text=True,
                        cwd=str(tmp_path), env=env, timeout=240)
     assert r.returncode == 1 and r.stderr.strip() == exp["stderr"]
+
+
+# ---- the reference's own callers on the drop-in (include/utility.h, oracle/Makefile dropin) ----
+
+REF = "/root/reference"
+DROPIN_COMPRESS = os.path.join(REPO, "oracle", "_ref", "dropin_compress")
+DROPIN_TEST = os.path.join(REPO, "oracle", "_ref", "dropin_test")
+
+
+def test_utility_matches_reference(tmp_path):
+    """include/utility.h (our restatement) gives the reference utility.h's results on every
+    helper: compiled against both when /root/reference exists, otherwise against the output
+    the reference's header produced (tests/golden/utility_check.txt, same program)."""
+    src = os.path.join(REPO, "tests", "cxx", "utility_check.cpp")
+
+    def run(inc, name):
+        exe = str(tmp_path / name)
+        subprocess.run(["g++", "-std=c++17", "-O1", "-w", "-I" + inc, src, "-o", exe], check=True)
+        return subprocess.run([exe], capture_output=True, text=True, check=True).stdout
+
+    ours = run(os.path.join(REPO, "include"), "ours")
+    with open(os.path.join(GOLDEN, "utility_check.txt")) as f:
+        assert ours == f.read()
+    if os.path.isdir(os.path.join(REF, "include")):
+        assert ours == run(os.path.join(REF, "include"), "ref")
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="needs the reference sources")
+def test_reference_callers_compile():
+    """The reference's unmodified compress.cpp and tests/test.cpp compile against include/
+    and link to libgcz.so; the CLI's host-only paths behave."""
+    load_gcz()
+    subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "dropin"], check=True)
+    r = subprocess.run([DROPIN_COMPRESS, "--help"], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.startswith("Usage: compress")
+    r = subprocess.run([DROPIN_COMPRESS], capture_output=True, text=True)
+    assert r.returncode == 2 and "argument <file> required" in r.stdout
+    r = subprocess.run([DROPIN_COMPRESS, "/nonexistent/x"], capture_output=True, text=True)
+    assert r.returncode == 2 and "Invalid filename" in r.stdout
+
+
+@pytest.mark.gpu
+def test_reference_test_program_on_dropin():
+    """The reference's own test program (tests/test.cpp, every group) built on the drop-in
+    runs green on the GPU (it reads data/edited and data/chmpxx relative to its cwd)."""
+    if not os.path.exists(DROPIN_TEST):
+        pytest.skip("oracle/_ref/dropin_test not built (needs /root/reference at build time)")
+    r = subprocess.run([DROPIN_TEST], capture_output=True, text=True, cwd=GOLDEN, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out
+    assert out.count("Finished without errors") == 10 and "error" not in out.replace("without errors", ""), out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["chmpxx", "merged"])
+def test_reference_compress_on_dropin(name, tmp_path, manifest):
+    """The reference's own compress.cpp on the drop-in: same statistics and .dag bytes."""
+    if not os.path.exists(DROPIN_COMPRESS):
+        pytest.skip("oracle/_ref/dropin_compress not built (needs /root/reference at build time)")
+    exp = manifest[f"corpus/{name}"]["expect"]
+    out = tmp_path / f"{name}.dag"
+    r = subprocess.run([DROPIN_COMPRESS, "--statistics", f"--output={out}", os.path.join(GOLDEN, "data", name)],
+                       capture_output=True, text=True, cwd=str(tmp_path), timeout=300)
+    assert r.returncode == 0, r.stderr
+    f = r.stdout.strip().split(",")
+    assert f[0] == "12" and int(f[1]) == exp["width"] and f[2] == exp["ratio"] and int(f[4]) == exp["bytes"]
+    assert hashlib.sha256(out.read_bytes()).hexdigest() == exp["sha_dag"]
