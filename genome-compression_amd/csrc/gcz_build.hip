@@ -525,7 +525,8 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   if (L < 1 || L > 16) return fail(GCZ_ERR_ARG, "build", "leaf length L must be in 1..16");
   if (d_bases) S = nbases / u64(L);
   if (S == 0) return fail(GCZ_ERR_EMPTY, "build", "fewer than L bases: nothing to build");
-  if (S > u64(kIdx)) return fail(GCZ_ERR_CAPACITY, "build", "more than 2^29-1 strands");
+  // positions are 29-bit fields of the words: longer genomes run as virtual ranks
+  if (S > u64(kIdx) || split_min_strands < S) return gcz_split_build(this, d_bases, d_leaves, S, L);
   info.n_strands = S;
 
   // ---- plan: node layers, leaf chunks, scan descriptor regions ----
@@ -892,6 +893,8 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   if (const char* t = std::getenv("GCZ_FUSED")) c->use_fused = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_SMALL_CAP_SHIFT")) c->small_cap_shift = std::max(0, std::min(4, std::atoi(t)));
   if (const char* t = std::getenv("GCZ_SMALL_LEAF_SHIFT")) c->small_leaf_shift = std::max(0, std::min(4, std::atoi(t)));
+  if (const char* t = std::getenv("GCZ_SPLIT_MIN")) c->split_min_strands = std::strtoull(t, nullptr, 10);
+  if (const char* t = std::getenv("GCZ_SPLIT_SHARE")) c->split_share = std::max<u64>(1024, std::strtoull(t, nullptr, 10));
   if (const char* t = std::getenv("GCZ_LEAF_FIRST_LOG2")) c->leaf_first_log2 = std::max(1, std::min(20, std::atoi(t)));
   *out = c;
   return GCZ_OK;

@@ -195,6 +195,9 @@ struct GraphKey {
 struct gcz_dist_state;   // gcz_dist.hip
 struct gcz_sort_state;   // gcz_sort.hip
 struct gcz_ingest_state; // gcz_ingest.hip
+// Builds of more than 2^29 - 1 strands on one device (gcz_ctx::build): virtual ranks
+// whose slices are concatenated into the context's arrays (gcz_dist.hip).
+int gcz_split_build(struct gcz_ctx* c, const void* d_bases, const gcz_host::u64* d_leaves, gcz_host::u64 S, int L);
 
 struct gcz_ctx {
   int device = 0;
@@ -235,6 +238,10 @@ struct gcz_ctx {
   int small_cap_shift = 2;   // ... and tables 2^this times the usual size: short probe chains (GCZ_SMALL_CAP_SHIFT)
   int small_leaf_shift = -1; // ... the leaf table's own (GCZ_SMALL_LEAF_SHIFT; -1: small_cap_shift)
   int cap_boost = 0;         // (this build's node-table boost)
+  // builds of more strands than this run as virtual ranks (always above 2^29 - 1;
+  // GCZ_SPLIT_MIN lowers it for testing the split path on small genomes)
+  gcz_host::u64 split_min_strands = ~0ull;
+  gcz_host::u64 split_share = 1ull << 28;   // strands per virtual rank (GCZ_SPLIT_SHARE)
   gcz_host::DevBuf ftab;     // ... their node tables, three rotating regions
   gcz_host::DevBuf fsid;     // ... and slot -> id of each table's repeated keys, three regions
   gcz_host::DevBuf flkey, flsid;   // ... the leaf level's canonical keys by position, ids by slot
@@ -253,6 +260,7 @@ struct gcz_ctx {
   gcz_dist_state* dist = nullptr;   // multi-rank build state (gcz_dist.hip)
   gcz_sort_state* sortst = nullptr; // device sort / .dag writer state (gcz_sort.hip)
   gcz_ingest_state* ingest = nullptr; // device FASTA ingest state (gcz_ingest.hip)
+  gcz_group* split = nullptr;         // virtual ranks of builds beyond 2^29 - 1 strands (gcz_dist.hip)
 
   int fail(int code, const char* what, const char* detail) {
     last_error = std::string(what) + ": " + detail;

@@ -40,6 +40,10 @@ struct gcz_dist_state {
 };
 
 void gcz_dist_state_free(gcz_ctx* c) {
+  if (c->split) {
+    gcz_group_destroy(c->split);
+    c->split = nullptr;
+  }
   gcz_dist_state* d = c->dist;
   if (!d) return;
   for (DevBuf* b : {&d->dict, &d->scratch, &d->gnf, &d->gmul, &d->gid, &d->blockcnt, &d->bchunk, &d->skey, &d->sidx, &d->sflag,
@@ -1844,8 +1848,8 @@ void gcz_group_destroy(gcz_group* g) {
   for (gcz_ctx* c : g->ctx) (void)hipStreamSynchronize(c->stream);
   delete g->tr;
   if (g->owns_ctx) {
-    // virtual ranks > 0 borrowed rank 0's stream
-    for (size_t i = 1; i < g->ctx.size(); ++i) g->ctx[i]->stream = g->ctx[i]->own_stream;
+    // virtual ranks borrowed rank 0's stream (or, split builds, the parent context's)
+    for (size_t i = 0; i < g->ctx.size(); ++i) g->ctx[i]->stream = g->ctx[i]->own_stream;
     for (gcz_ctx* c : g->ctx) gcz_ctx_destroy(c);
   }
   delete g;
@@ -1934,3 +1938,93 @@ int gcz_group_fetch(gcz_group* g, gcz_tree* t) {
 }
 
 }  // extern "C"
+
+// ---- single-device builds beyond 2^29 - 1 strands ---------------------------------------
+// The single-device build keeps positions in the 29-bit index field of its words.  The
+// reference bounds only ids to 29 bits; its positions are size_t (src/shared_tree.cpp:630-672,
+// 743-763: segments of 2^25 strands), so it builds longer genomes, e.g. > 6.44 Gbase at
+// L = 12 or > 537 Mbase at L = 1.  Such a genome is built here by R virtual ranks on the
+// context's own device and stream (the multi-rank build above: rank-local positions, global
+// ids), and the rank slices are then concatenated into the context's arrays in the layout of
+// a single-device build, so copy-out, the device sort, the .dag writer and decompression see
+// one ordinary build.  The virtual ranks persist in the context for the next such build.
+#define SPLIT_HIP(x)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) return c->fail(GCZ_ERR_DEVICE, #x, hipGetErrorString(e_));  \
+  } while (0)
+int gcz_split_build(gcz_ctx* c, const void* d_bases, const u64* d_leaves, u64 S, int L) {
+  const u64 share = std::max<u64>(1024, std::min<u64>(c->split_share, u64(kIdx) / 2));
+  const int R = int(std::max<u64>(2, (S + share - 1) / share));
+  if (R > kMaxRanks)
+    return c->fail(GCZ_ERR_CAPACITY, "build", "genome too long for one device (more than 31 * 2^28 strands)");
+  gcz_group*& g = c->split;
+  if (g && g->world != R) {
+    gcz_group_destroy(g);
+    g = nullptr;
+  }
+  if (!g) {
+    if (int rc = gcz_group_create_local(c->device, R, &g)) return c->fail(rc, "build", "virtual ranks could not be created");
+    for (gcz_ctx* v : g->ctx) v->profile = false;
+  }
+  if (hipSetDevice(c->device) != hipSuccess) return c->fail(GCZ_ERR_DEVICE, "build", "hipSetDevice");
+  for (gcz_ctx* v : g->ctx) v->stream = c->stream;   // one stream orders ranks, copies and later calls
+  static_cast<LocalTransport*>(g->tr)->stream = c->stream;
+  if (!c->ev_start) {
+    SPLIT_HIP(hipEventCreate(&c->ev_start));
+    SPLIT_HIP(hipEventCreate(&c->ev_stop));
+  }
+  std::vector<const void*> bases(R, nullptr);
+  std::vector<const u64*> leaves(R, nullptr);
+  for (int r = 0; r < R; ++r) {
+    uint64_t s0 = 0, s1 = 0;
+    gcz_dist_plan(S, R, r, &s0, &s1, nullptr);
+    if (d_bases) bases[r] = static_cast<const unsigned char*>(d_bases) + s0 * u64(L);
+    if (d_leaves) leaves[r] = d_leaves + s0;
+  }
+  SPLIT_HIP(hipEventRecord(c->ev_start, c->stream));
+  const int rc = g->build(d_bases ? bases.data() : nullptr, d_leaves ? leaves.data() : nullptr, S, L);
+  if (rc) {
+    const gcz_info keep = g->info;
+    c->fail(rc, "build", g->last_error.c_str());
+    c->info = keep;
+    c->info.status = rc;
+    return rc;
+  }
+  // assemble: the layout of gcz_ctx::build (layer k stored at layer_off[k], ceil(n_k / 2) slots)
+  const gcz_info& gi = g->info;
+  const int D = gi.n_layers;
+  c->layer_off.assign(D + 1, 0);
+  u64 n = S;
+  for (int k = 0; k < D; ++k) {
+    const u64 p = (n + 1) / 2;
+    c->layer_off[k + 1] = c->layer_off[k] + p;
+    n = p;
+  }
+  if (int e = c->ensure(c->leaves_out, S * 8 + 16)) return e;
+  if (int e = c->ensure(c->nodes_out, c->layer_off[D] * 8 + 16)) return e;
+  for (int i = 0; i < R; ++i) {
+    gcz_ctx* v = g->ctx[i];
+    for (int layer = -1; layer < D; ++layer) {
+      uint64_t off = 0, cnt = 0;
+      if (gcz_group_slice(g, i, layer, &off, &cnt) || !cnt) continue;
+      void* dst = layer < 0 ? static_cast<void*>(c->leaves_out.as<u64>() + off)
+                            : static_cast<void*>(c->nodes_out.as<uint2>() + c->layer_off[layer] + off);
+      const void* src = layer < 0 ? v->leaves_out.ptr
+                                  : static_cast<const void*>(v->nodes_out.as<uint2>() + g->node_base[i][layer]);
+      SPLIT_HIP(hipMemcpyAsync(dst, src, cnt * 8, hipMemcpyDeviceToDevice, c->stream));
+    }
+  }
+  SPLIT_HIP(hipEventRecord(c->ev_stop, c->stream));
+  SPLIT_HIP(hipEventSynchronize(c->ev_stop));
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, c->ev_start, c->ev_stop);
+  c->info = gi;
+  c->info.status = GCZ_OK;
+  c->info.n_strands = S;
+  c->info.build_ms = ms;
+  c->info.build_ms_all = ms;
+  c->dense_used = gi.leaf_path == 1;
+  c->last_error.clear();
+  return GCZ_OK;
+}
