@@ -186,7 +186,9 @@ shared_tree::shared_tree(fasta_reader file, bool verbose) {
   std::lock_guard<std::mutex> lock(e.mu);
   {
     PhaseTimer t{"upload+build"};
-    check_build(gcz_build_host_fasta(e.ctx, file.raw_data(), file.raw_size(), int(dna::size())), e.ctx);
+    check_build(gcz_build_host_fasta_buffered(e.ctx, file.raw_data(), file.raw_size(), int(dna::size()),
+                                              file.buffer_strands(), file.strands_read()),
+                e.ctx);
   }
   build_from_gpu();
   if (verbose) std::cout << "\rConstructing subtrees: done.\n\rCombining subtrees: done.\n";
@@ -264,11 +266,15 @@ auto tree_constructor::reduce(const std::vector<dna>& data, bool verbose) -> poi
   return parent.root;
 }
 
+// every reader buffer of file.buffer_strands() strands its own subtree, the roots combined
+// (one global level loop for the default power-of-two buffers: the same tree)
 auto tree_constructor::reduce(fasta_reader& file, bool verbose) -> pointer {   // :719-736, on the GPU
   auto& e = engine();
   {
     std::lock_guard<std::mutex> lock(e.mu);
-    check_build(gcz_build_host_fasta(e.ctx, file.raw_data(), file.raw_size(), int(dna::size())), e.ctx);
+    check_build(gcz_build_host_fasta_buffered(e.ctx, file.raw_data(), file.raw_size(), int(dna::size()),
+                                              file.buffer_strands(), file.strands_read()),
+                e.ctx);
     parent.build_from_gpu();
   }
   if (verbose) std::cout << "\rConstructing subtrees: done.\n\rCombining subtrees: done.\n";

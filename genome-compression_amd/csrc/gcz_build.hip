@@ -330,8 +330,8 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     return GCZ_OK;
   }
   const Marks mk{knf, multi_set[cur]};
-  const unsigned char* pnf = a.prev_marks ? nf_set[prev] : nullptr;
-  const unsigned char* pmu = a.prev_marks ? multi_set[prev] : nullptr;
+  const unsigned char* pnf = a.prev_nf ? a.prev_nf : a.prev_marks ? nf_set[prev] : nullptr;
+  const unsigned char* pmu = a.prev_nf ? a.prev_multi : a.prev_marks ? multi_set[prev] : nullptr;
   Group* d_grp = grp.as<Group>();
   // bucketed insert (decided on the device: hdr->predup == 0) when the buckets average
   // <= 2560 pairs (the LDS dedupe holds 4608) and a record fits 8 bytes
@@ -525,14 +525,42 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   if (L < 1 || L > 16) return fail(GCZ_ERR_ARG, "build", "leaf length L must be in 1..16");
   if (d_bases) S = nbases / u64(L);
   if (S == 0) return fail(GCZ_ERR_EMPTY, "build", "fewer than L bases: nothing to build");
+  // reader-buffer segments of segB strands (one build only); a single buffer or a power of
+  // two >= 2 pairs exactly like the global level loop.  (Buffers of one strand
+  // are not: each strand becomes a unary layer-0 node of its own.)
+  u64 segB = segment_strands;
+  segment_strands = 0;
+  if (segB >= S || (segB >= 2 && (segB & (segB - 1)) == 0)) segB = 0;
   // positions are 29-bit fields of the words: longer genomes run as virtual ranks
-  if (S > u64(kIdx) || split_min_strands < S) return gcz_split_build(this, d_bases, d_leaves, S, L);
+  if (S > u64(kIdx) || split_min_strands < S) {
+    if (segB)
+      return fail(GCZ_ERR_CAPACITY, "build", "reader buffers that are not a power of two need at most 2^29-1 strands");
+    return gcz_split_build(this, d_bases, d_leaves, S, L);
+  }
   info.n_strands = S;
 
   // ---- plan: node layers, leaf chunks, scan descriptor regions ----
+  // Segmented levels k < seg_d (the depth of one full buffer's subtree): full segments hold
+  // seg_bk[k] input elements; where that is odd the input is expanded to seg_ne[k] elements
+  // (k_seg_expand), one null after every segment but the last.
+  int seg_d = 0;
+  u64 nseg = 0;
+  std::vector<u64> seg_bk, seg_ne;
+  if (segB) {
+    seg_d = std::max<int>(1, int(bit_width(segB - 1)));
+    nseg = (S + segB - 1) / segB;
+  }
   std::vector<u64> pk;                     // pairs per node layer
   for (u64 n = S;;) {
-    const u64 p = (n + 1) / 2;
+    u64 ne = n;
+    if (int(pk.size()) < seg_d) {
+      const int k = int(pk.size());
+      const u64 bk = (segB + (u64(1) << k) - 1) >> k;
+      if (bk & 1) ne = n + nseg - 1;
+      seg_bk.push_back(bk);
+      seg_ne.push_back(ne);
+    }
+    const u64 p = (ne + 1) / 2;
     pk.push_back(p);
     if (p == 1) break;
     n = p;
@@ -572,7 +600,12 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
 
   int rc;
   if ((rc = ensure(wa, S * 4 + 16))) return rc;
-  if ((rc = ensure(wb, ((S + 1) / 2) * 4 + 16))) return rc;
+  if ((rc = ensure(wb, (seg_d ? S : (S + 1) / 2) * 4 + 16))) return rc;
+  if (seg_d) {
+    const u64 ne_max = *std::max_element(seg_ne.begin(), seg_ne.end());
+    if ((rc = ensure(seg_w, ne_max * 4 + 16)) || (rc = ensure(seg_nf, ne_max + 16)) || (rc = ensure(seg_mu, ne_max + 16)))
+      return rc;
+  }
   if ((rc = ensure(grp, ((S + 63) / 64 + kGroupsPerTile) * sizeof(Group)))) return rc;
   if ((rc = ensure(desc, ntiles_total * 8 + 64))) return rc;
   if ((rc = ensure(leaves_out, S * 8 + 16))) return rc;
@@ -599,7 +632,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     if ((rc = ensure(tab, std::max(leaf_cap, node_cap0) * 16))) return rc;
     // small build, one leaf chunk, no bucketed level, no host look at a gate: two launches
     // per node level (FuseIn, gcz_device.h), the node tables in three regions of ftab
-    const bool fused = use_fused && !try_dense && C == 1 && pk[0] < kDirectCheckMin &&
+    const bool fused = use_fused && !seg_d && !try_dense && C == 1 && pk[0] < kDirectCheckMin &&
                        !(bucket_now && pk[0] >= bucket_min) && (S > u64(kTailMaxN) || !use_tail);
     const u64 fregion = node_cap0 * 16;
     if (fused && ((rc = ensure(ftab, 3 * fregion)) || (rc = ensure(fsid, 3 * node_cap0 * 4)) ||
@@ -673,7 +706,8 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
       bool prev_regular = false;   // the previous level ran node_level (its gate is written)
       bool table_only = false;     // hdr->predup seen on the host: no bucketed levels
       for (int k = 0; k < D; ++k) {
-        if (n <= u64(kTailMaxN) && use_tail) {   // the rest fits one workgroup: one launch
+        const bool segmented = k < seg_d;   // pairing inside reader buffers
+        if (n <= u64(kTailMaxN) && use_tail && !segmented) {   // the rest fits one workgroup: one launch
           const u64* pc = k == 0 ? &d_hdr->count[C - 1] : prev_regular ? &d_hdr->gate[k - 1]
                                                                          : &d_hdr->count[kLayerSlot + k - 1];
           TailSettle st{};
@@ -710,6 +744,20 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
         NodeLevel na;
         na.k = k;
         na.in = in; na.n = n; na.p = pk[k];
+        if (segmented && seg_ne[k] != n) {   // a null after every odd segment (and its marks)
+          const bool marks = k > 0;
+          hipLaunchKernelGGL(k_seg_expand, dim3(unsigned((seg_ne[k] + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
+                             in, marks ? nf_set[k & 1] : nullptr, marks ? multi_set[k & 1] : nullptr, seg_bk[k],
+                             seg_ne[k], seg_w.as<u32>(), marks ? seg_nf.as<unsigned char>() : nullptr,
+                             marks ? seg_mu.as<unsigned char>() : nullptr);
+          HIP_TRY(hipGetLastError());
+          na.in = seg_w.as<u32>();
+          na.n = seg_ne[k];
+          if (marks) {
+            na.prev_nf = seg_nf.as<unsigned char>();
+            na.prev_multi = seg_mu.as<unsigned char>();
+          }
+        }
         na.words = outw;
         na.out = nodes_out.as<uint2>() + layer_off[k];
         na.count = &d_hdr->count[kLayerSlot + k];
@@ -718,7 +766,9 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
         na.pcount = k == 0 ? &d_hdr->count[C - 1] : &d_hdr->gate[k - 1];
         na.desc = d_desc + desc_off[C + k];
         na.ticket = &d_hdr->ticket[kLayerSlot + k];
-        na.hashed_next = &d_hdr->hashed_next[k];   // look-ahead for layer k + 1 (its pairs' children are here)
+        // look-ahead for layer k + 1 (its pairs' children are here; not where that layer pairs
+        // inside reader buffers)
+        na.hashed_next = k + 1 < seg_d ? nullptr : &d_hdr->hashed_next[k];
         na.gate = &d_hdr->gate[k];
         na.allow_bucket = !table_only && !fused;
         if (fused) {
@@ -738,7 +788,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
         bound = pk[k];
         // a look at the device after layers 0 and 1: once a gate is open every later
         // level is direct and runs as direct subtrees (saves ~4 launches per level)
-        if (k <= 1 && use_direct && n >= kDirectCheckMin) {   // (a host round trip: only where levels are big)
+        if (k <= 1 && use_direct && n >= kDirectCheckMin && k + 1 >= seg_d) {   // (a host round trip: only where levels are big)
           u64 g = 0;
           u32 pd = 0;
           HIP_TRY(hipMemcpyAsync(&g, &d_hdr->gate[k], 8, hipMemcpyDeviceToHost, stream));
@@ -758,7 +808,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
     };
     // (a level that may take the bucketed path can allocate inside: never captured; a
     // shape is captured on its second build, once every buffer has its size)
-    const bool static_seq = use_graph && !profile && !try_dense && pk[0] < kDirectCheckMin &&
+    const bool static_seq = use_graph && !profile && !seg_d && !try_dense && pk[0] < kDirectCheckMin &&
                             !(use_bucket && pk[0] >= bucket_min);
     bool launched = false;
     if (static_seq) {
@@ -911,7 +961,8 @@ void gcz_ctx_destroy(gcz_ctx* c) {
                     &c->nf, &c->multi, &c->stats, &c->bkt_key, &c->bkt_cnt, &c->bkt_off, &c->bkt_tmp, &c->bkt_rec2, &c->dl_pw,
                     &c->dl_rec, &c->dl_idrec, &c->dl_cnt, &c->dl_off, &c->dl_fpg, &c->dl_fb, &c->dl_wpre,
                     &c->dl_desc, &c->dl_fl, &c->dl_fo, &c->dl_lh, &c->dl_pb, &c->dl_pbs, &c->dl_lower,
-                    &c->dl_pos, &c->dl_list, &c->dl_gid, &c->dl_recv, &c->dl_stage, &c->dl_seg})
+                    &c->dl_pos, &c->dl_list, &c->dl_gid, &c->dl_recv, &c->dl_stage, &c->dl_seg, &c->seg_w,
+                    &c->seg_nf, &c->seg_mu, &c->seg_in})
     if (b->ptr) (void)hipFree(b->ptr);
   if (c->h_hdr) (void)hipHostFree(c->h_hdr);
   if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);

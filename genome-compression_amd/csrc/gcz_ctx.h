@@ -143,6 +143,9 @@ struct NodeLevel {
   void* ftab_next = nullptr;        // ... and of the next level's
   gcz_host::u32* sid = nullptr;     // ids of this level's repeated keys by slot (flag scan -> next insert)
   const gcz_host::u32* sid_prev = nullptr;   // ... of the previous level
+  // reader-buffer segments: the previous level's marks as expanded with the input (k_seg_expand)
+  const unsigned char* prev_nf = nullptr;
+  const unsigned char* prev_multi = nullptr;
 };
 
 // One leaf level (all chunks).
@@ -242,6 +245,11 @@ struct gcz_ctx {
   // GCZ_SPLIT_MIN lowers it for testing the split path on small genomes)
   gcz_host::u64 split_min_strands = ~0ull;
   gcz_host::u64 split_share = 1ull << 28;   // strands per virtual rank (GCZ_SPLIT_SHARE)
+  // the next build's reader buffers of this many strands (gcz_build_*_fasta_buffered; 0: one
+  // global level loop, which equals any power-of-two buffer)
+  gcz_host::u64 segment_strands = 0;
+  gcz_host::DevBuf seg_w, seg_nf, seg_mu;   // a level's input expanded at the segment ends
+  gcz_host::DevBuf seg_in;                  // realigned bases after skipped reader buffers
   gcz_host::DevBuf ftab;     // ... their node tables, three rotating regions
   gcz_host::DevBuf fsid;     // ... and slot -> id of each table's repeated keys, three regions
   gcz_host::DevBuf flkey, flsid;   // ... the leaf level's canonical keys by position, ids by slot

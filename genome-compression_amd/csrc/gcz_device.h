@@ -555,6 +555,37 @@ __device__ __forceinline__ void load_pair(const u32* __restrict__ in, u64 n, u64
   }
 }
 
+// Reader-buffer segments (gcz_build_*_fasta_buffered): the reference reduces every
+// fasta_reader buffer of B strands to its own subtree, pairing inside the buffer only and an
+// odd buffer's last element with null, before it combines the roots
+// (src/shared_tree.cpp:719-736, reduce_segment include/shared_tree.h:305-316).  At a node
+// level whose full segments hold an odd number Bk of input elements, this copies the level's
+// input with a null element after every segment but the last, so that the ordinary (2j, 2j+1)
+// pairing of the copy pairs exactly like the reference.  The null slots are marked as repeated
+// (not singletons), so a pair (x, null) is hash-consed unless x itself is a singleton.
+[[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_seg_expand(const u32* __restrict__ in, const unsigned char* __restrict__ nf,
+                                                       const unsigned char* __restrict__ mu, u64 Bk, u64 nout,
+                                                       u32* __restrict__ out, unsigned char* __restrict__ onf,
+                                                       unsigned char* __restrict__ omu) {
+  const u64 o = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (o >= nout) return;
+  const u64 s = o / (Bk + 1), q = o - s * (Bk + 1);
+  if (q == Bk) {
+    out[o] = kNullWord;
+    if (onf) {
+      onf[o] = kNfNot;
+      omu[o] = 1;
+    }
+  } else {
+    const u64 i = s * Bk + q;
+    out[o] = in[i];
+    if (onf) {
+      onf[o] = nf[i];
+      omu[o] = mu[i];
+    }
+  }
+}
+
 // Node level, tree_constructor::emplace_node (src/shared_tree.cpp:662-672).
 //
 // Singleton propagation: a previous-level element that is the only occurrence

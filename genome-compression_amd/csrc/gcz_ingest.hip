@@ -403,6 +403,40 @@ int gcz_build_device_fasta(gcz_ctx* c, const void* d_file, uint64_t n, int L) {
   return c->build(b, nullptr, nb, 0, L);
 }
 
+int gcz_build_device_fasta_buffered(gcz_ctx* c, const void* d_file, uint64_t n, int L, uint64_t buffer_strands,
+                                    uint64_t first_strand) {
+  if (!c || (!d_file && n) || L < 1 || L > 16) return GCZ_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  // fasta_reader{path, buffer_strands}: buffers of B strands (src/fasta_reader.cpp:21-31)
+  const u64 B = gcz::reader_buffer_bytes(n, L, buffer_strands) / u64(L);
+  if (first_strand % B) return c->fail(GCZ_ERR_ARG, "gcz_build_device_fasta_buffered", "first_strand is not a buffer start");
+  const unsigned char* b = nullptr;
+  u64 nb = 0;
+  if (int rc = gcz_fasta_extract_on_device(c, static_cast<const unsigned char*>(d_file), n, L, buffer_strands, &b, &nb))
+    return rc;
+  // buffers already handed out by read_into are not part of the tree (src/shared_tree.cpp:722)
+  const u64 skip = std::min<u64>(nb / u64(L), first_strand) * u64(L);
+  b += skip;
+  nb -= skip;
+  if (skip & 3) {   // the leaf kernels stage with 4-B loads
+    if (int rc = c->ensure(c->seg_in, nb + 16)) return rc;
+    I_HIP(hipMemcpyAsync(c->seg_in.ptr, b, nb, hipMemcpyDeviceToDevice, c->stream));
+    b = c->seg_in.as<unsigned char>();
+  }
+  c->segment_strands = B;
+  return c->build(b, nullptr, nb, 0, L);
+}
+
+int gcz_build_host_fasta_buffered(gcz_ctx* c, const void* fasta, uint64_t nbytes, int L, uint64_t buffer_strands,
+                                  uint64_t first_strand) {
+  if (!c || (!fasta && nbytes)) return GCZ_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  if (int rc = c->ensure(c->input, nbytes + 16)) return rc;
+  if (nbytes && c->upload(c->input.ptr, fasta, nbytes))
+    return c->fail(GCZ_ERR_DEVICE, "gcz_build_host_fasta_buffered", "H2D copy failed");
+  return gcz_build_device_fasta_buffered(c, c->input.ptr, nbytes, L, buffer_strands, first_strand);
+}
+
 int gcz_fasta_extract_device(gcz_ctx* c, const void* d_file, uint64_t n, int L, uint64_t buffer_strands, void* d_out,
                              uint64_t cap, uint64_t* nbases) {
   if (!c || (!d_file && n) || !nbases) return GCZ_ERR_ARG;

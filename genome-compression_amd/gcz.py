@@ -61,6 +61,8 @@ _SIGS = {
     "gcz_build_device_bases": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
     "gcz_build_device_leaves": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
     "gcz_build_host_fasta": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
+    "gcz_build_host_fasta_buffered": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int, _U64, _U64]),
+    "gcz_build_device_fasta_buffered": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int, _U64, _U64]),
     "gcz_build_host_leaves": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
     "gcz_build_device_fasta": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
     "gcz_fasta_extract_device": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int, _U64, _P, _U64, ctypes.POINTER(_U64)]),
@@ -364,6 +366,17 @@ class Context:
     def build_fasta(self, data: bytes, L: int = 12) -> dict:
         buf = np.frombuffer(data, dtype=np.uint8)
         return self._check(_lib.gcz_build_host_fasta(self._h, _ptr(buf), len(data), L))
+
+    def build_fasta_buffered(self, data: bytes, L: int = 12, buffer_strands: int = 0, first_strand: int = 0) -> dict:
+        """shared_tree{fasta_reader{path, buffer_strands}}: every reader buffer its own subtree."""
+        buf = np.frombuffer(data, dtype=np.uint8)
+        return self._check(_lib.gcz_build_host_fasta_buffered(self._h, _ptr(buf), len(data), L, buffer_strands,
+                                                              first_strand))
+
+    def build_device_fasta_buffered(self, dev_ptr: int, nbytes: int, L: int = 12, buffer_strands: int = 0,
+                                    first_strand: int = 0) -> dict:
+        return self._check(_lib.gcz_build_device_fasta_buffered(self._h, ctypes.c_void_p(dev_ptr), nbytes, L,
+                                                                buffer_strands, first_strand))
 
     def build_leaves(self, leaves: np.ndarray, L: int = 12) -> dict:
         a = np.ascontiguousarray(leaves, dtype=np.uint64)

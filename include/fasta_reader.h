@@ -44,6 +44,11 @@ class fasta_reader {
   auto size() const -> std::size_t;      // file size in bytes (upper bound on bases)
   auto buffers() const -> std::size_t;   // approximate number of buffers
   auto path() const -> const std::filesystem::path& { return file_path; }
+  // Beyond the reference surface: the buffer size asked for (strands) and the strands that
+  // read_into has handed out, so that tree_constructor::reduce(*this) builds the buffers
+  // still to come, each its own subtree, like the reference (src/shared_tree.cpp:719-736).
+  auto buffer_strands() const -> std::size_t { return buffer_size; }
+  auto strands_read() const -> std::size_t { return next - (loaded ? back.size() : 0); }
 
   // Raw file bytes (read-only mapping) and the concatenated bases (FASTA contract applied).
   auto raw_data() const -> const std::uint8_t* { return bytes.get(); }

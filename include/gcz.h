@@ -112,6 +112,16 @@ GCZ_API int gcz_build_host_leaves(gcz_ctx *ctx, const uint64_t *leaves, uint64_t
 /* A FASTA file already in device memory: the line contract (headers, blank lines;
  * src/fasta_reader.cpp:40-68) runs on the device, then the build. */
 GCZ_API int gcz_build_device_fasta(gcz_ctx *ctx, const void *d_file, uint64_t n, int L);
+/* fasta_reader{path, buffer_strands} + tree_constructor::reduce(file) (src/fasta_reader.cpp:13-35,
+ * src/shared_tree.cpp:719-736): the reader's buffers of B = min(n / L + 1, buffer_strands)
+ * strands (0: the default 1 << 22) shape both the line contract (a line that crosses a buffer
+ * boundary) and the tree, every buffer being reduced to its own subtree before the roots are
+ * combined.  For a power-of-two B >= 2 (the default reader) the tree equals gcz_build_*_fasta's.
+ * first_strand (a multiple of B) skips the buffers read_into already handed out. */
+GCZ_API int gcz_build_host_fasta_buffered(gcz_ctx *ctx, const void *fasta, uint64_t nbytes, int L,
+                                          uint64_t buffer_strands, uint64_t first_strand);
+GCZ_API int gcz_build_device_fasta_buffered(gcz_ctx *ctx, const void *d_file, uint64_t n, int L,
+                                            uint64_t buffer_strands, uint64_t first_strand);
 /* The device line contract alone (as gcz_fasta_extract): bases of d_file into d_out
  * (cap bytes; null: count only). */
 GCZ_API int gcz_fasta_extract_device(gcz_ctx *ctx, const void *d_file, uint64_t n, int L, uint64_t buffer_strands,

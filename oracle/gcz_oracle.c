@@ -310,6 +310,80 @@ ORC_API orc_tree *orc_build(const uint64_t *leaves, uint64_t S, int L) {
   return tr;
 }
 
+/* Segmented build: tree_constructor::reduce(fasta_reader&) over reader buffers of B strands
+ * (src/shared_tree.cpp:719-736).  Each buffer goes through reduce_segment
+ * (include/shared_tree.h:305-316): reduce_leaves (:282-299), then reduce_nodes
+ * (src/shared_tree.cpp:697-712) while the layer holds more than one element or is shallower
+ * than the tree; its root is kept.  reduce_roots (:677-692) then pairs the roots upwards.
+ * Every layer's dictionary lives across the buffers, so ids are first-occurrence ranks in
+ * buffer order.  For a power-of-two B >= 2 this is orc_build's tree. */
+static void seg_reduce(orc_tree *tr, orc_map *maps, int layer, const uint32_t *in, uint64_t n, uint32_t *out) {
+  if (layer >= tr->n_layers) tr->n_layers = layer + 1;      /* add_layer (:701-704) */
+  for (uint64_t j = 0; 2 * j < n; ++j)                       /* foreach_pair, utility.h:17-29 */
+    out[j] = emplace_node(tr, layer, &maps[layer], in[2 * j], 2 * j + 1 < n ? in[2 * j + 1] : NULL_WORD);
+}
+
+ORC_API orc_tree *orc_build_segmented(const uint64_t *leaves, uint64_t S, int L, uint64_t B) {
+  if (S == 0 || L < 1 || L > 16 || B == 0) return NULL;
+  enum { MAXL = 64 };
+  /* node bound per layer: every buffer's layer k has ceil(len_k / 2) nodes; the roots above */
+  const uint64_t nseg = (S + B - 1) / B, last = S - (nseg - 1) * B;
+  uint64_t bound[MAXL] = {0};
+  int depth = 0;                                   /* layers of one full buffer's subtree */
+  for (uint64_t b = B; depth == 0 || b > 1; b = (b + 1) / 2) ++depth;
+  {
+    uint64_t b = B, e = last;
+    for (int k = 0; k < depth; ++k) {
+      bound[k] = (nseg - 1) * ((b + 1) / 2) + (e + 1) / 2;
+      b = (b + 1) / 2;
+      e = (e + 1) / 2;
+    }
+    int k = depth;
+    for (uint64_t r = nseg; r > 1; r = (r + 1) / 2) {
+      if (k >= MAXL) return NULL;
+      bound[k++] = (r + 1) / 2;
+    }
+  }
+  orc_tree *tr = calloc(1, sizeof *tr);
+  tr->L = L; tr->S = S;
+  tr->leaves = malloc(S * sizeof(uint64_t));
+  tr->layer_n = calloc(MAXL, sizeof(uint64_t));
+  tr->layer_words = calloc(MAXL, sizeof(uint32_t *));
+  orc_map lm, maps[MAXL];
+  map_init(&lm, S);
+  for (int k = 0; k < MAXL && bound[k]; ++k) {
+    tr->layer_words[k] = malloc(2 * bound[k] * sizeof(uint32_t));
+    map_init(&maps[k], bound[k]);
+  }
+  uint32_t *roots = malloc(nseg * sizeof(uint32_t));
+  uint32_t *a = malloc((B + 1) * sizeof(uint32_t)), *b = malloc((B + 1) * sizeof(uint32_t));
+  for (uint64_t s = 0; s < nseg; ++s) {
+    const uint64_t s0 = s * B, len = s + 1 < nseg ? B : last;
+    for (uint64_t i = 0; i < len; ++i) a[i] = emplace_leaf(tr, &lm, leaves[s0 + i]);
+    uint64_t n = len;
+    seg_reduce(tr, maps, 0, a, n, b);                        /* reduce_leaves */
+    n = (n + 1) / 2;
+    for (int index = 1; n > 1 || index < tr->n_layers; ++index) {   /* reduce_segment loop */
+      seg_reduce(tr, maps, index, b, n, a);
+      uint32_t *t = a; a = b; b = t;
+      n = (n + 1) / 2;
+    }
+    roots[s] = b[0];
+  }
+  uint64_t n = nseg;
+  uint32_t *r2 = malloc(nseg * sizeof(uint32_t));
+  for (int index = tr->n_layers; n > 1; ++index) {           /* reduce_roots */
+    seg_reduce(tr, maps, index, roots, n, r2);
+    uint32_t *t = roots; roots = r2; r2 = t;
+    n = (n + 1) / 2;
+  }
+  tr->root = roots[0];
+  free(roots); free(r2); free(a); free(b);
+  map_free(&lm);
+  for (int k = 0; k < MAXL && bound[k]; ++k) map_free(&maps[k]);
+  return tr;
+}
+
 ORC_API void orc_free(orc_tree *tr) {
   if (!tr) return;
   for (int i = 0; i < tr->n_layers; ++i) free(tr->layer_words[i]);

@@ -35,6 +35,7 @@ for name, res, args in [
     ("orc_fasta_extract", _U64, [_P, _U64, _I, _U64, _P]),
     ("orc_pack", ctypes.c_int64, [_P, _U64, _I, _P]),
     ("orc_build", _P, [_P, _U64, _I]),
+    ("orc_build_segmented", _P, [_P, _U64, _I, _U64]),
     ("orc_free", None, [_P]),
     ("orc_n_layers", _I, [_P]),
     ("orc_n_leaves", _U64, [_P]),
@@ -157,6 +158,28 @@ def build_leaves(leaves: np.ndarray, L: int) -> OracleTree:
 
 def build_fasta(data: bytes, L: int) -> OracleTree:
     return build_leaves(pack(fasta_extract(data, L), L), L)
+
+
+def build_leaves_segmented(leaves: np.ndarray, L: int, B: int) -> OracleTree:
+    """tree_constructor::reduce over buffers of B strands (every buffer its own subtree)."""
+    a = np.ascontiguousarray(leaves, dtype=np.uint64)
+    h = _lib.orc_build_segmented(_ptr(a), a.size, L, B)
+    if not h:
+        raise ValueError("empty input or bad L / B")
+    return OracleTree(h, L)
+
+
+def reader_buffer_strands(nbytes: int, L: int, buffer_strands: int = 0) -> int:
+    """fasta_reader's buffer size in strands (src/fasta_reader.cpp:21-31)."""
+    return min(nbytes // L + 1, buffer_strands or (1 << 22))
+
+
+def build_fasta_buffered(data: bytes, L: int, buffer_strands: int, first_strand: int = 0) -> OracleTree:
+    """shared_tree{fasta_reader{path, buffer_strands}}: the reader's line contract and its
+    buffers as subtrees (first_strand: buffers already read out)."""
+    B = reader_buffer_strands(len(data), L, buffer_strands)
+    leaves = pack(fasta_extract(data, L, buffer_strands), L)[first_strand:]
+    return build_leaves_segmented(leaves, L, B)
 
 
 def digest(tree) -> dict:

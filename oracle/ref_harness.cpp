@@ -9,6 +9,8 @@
 // Modes
 //   dump <fasta> <L> <prefix>        shared_tree{fasta_reader{path}} (compress.cpp:183)
 //   dumpleaves <u64.bin> <L> <prefix> shared_tree(std::vector<dna>&)  (shared_tree.cpp:212)
+//   dumpbuf <fasta> <L> <buffer> <prefix>  shared_tree{fasta_reader{path, buffer}}: the tree of
+//                                    reader buffers of `buffer` strands (shared_tree.cpp:719-736)
 //   time <kind> <nbases> <L> [reps]  synthetic genome (csrc/synth.h) -> vector<dna> -> build
 //   random <seed>                    prints dna::random(seed) (dna.cpp:92-96) as u64
 //   reader <fasta> <L> <buffer> <out> fasta_reader{path, buffer} (fasta_reader.cpp:13-35) read_into
@@ -139,6 +141,15 @@ int main(int argc, char** argv) {
     shared_tree tree{std::filesystem::path{argv[2]}};
     auto t1 = std::chrono::high_resolution_clock::now();
     dump_tree(tree, argv[4], std::filesystem::file_size(argv[2]),
+              std::chrono::duration<double, std::milli>(t1 - t0).count());
+    return 0;
+  }
+  if (mode == "dumpbuf" && argc == 6) {
+    dna::size(std::atoi(argv[3]));
+    auto t0 = std::chrono::high_resolution_clock::now();
+    shared_tree tree{fasta_reader{std::filesystem::path{argv[2]}, std::strtoull(argv[4], nullptr, 10)}};
+    auto t1 = std::chrono::high_resolution_clock::now();
+    dump_tree(tree, argv[5], std::filesystem::file_size(argv[2]),
               std::chrono::duration<double, std::milli>(t1 - t0).count());
     return 0;
   }

@@ -207,6 +207,43 @@ static void gpu_tree_constructor() {
   CHECK(cd.reduce(f) == gpu.root_pointer() && dump(d) == dump(gpu), "reduce(fasta_reader)");
 }
 
+// fasta_reader{path, B} with B not a power of two: every reader buffer is its own subtree
+// (src/shared_tree.cpp:719-736).  The GPU build (shared_tree{reader}, tree_constructor::
+// reduce(reader)) equals the element-wise constructor fed buffer by buffer; a reader whose
+// first buffers were already read out builds the rest.
+static void gpu_reader_segments() {
+  for (const std::size_t B : {std::size_t(1000), std::size_t(7), std::size_t(4095)}) {
+    shared_tree host;
+    tree_constructor ch{host};
+    fasta_reader hr{dir + "/data/chmpxx", B};
+    std::vector<dna> buf;
+    while (hr.read_into(buf)) ch.reduce_segment(buf);
+    const pointer root = ch.reduce_roots();
+    const shared_tree gpu{fasta_reader{dir + "/data/chmpxx", B}};
+    CHECK(gpu.root_pointer() == root && dump(gpu) == dump(host), "shared_tree{fasta_reader{path, B}} = buffer subtrees");
+    shared_tree d;
+    tree_constructor cd{d};
+    fasta_reader f{dir + "/data/chmpxx", B};
+    CHECK(cd.reduce(f) == root && dump(d) == dump(host), "tree_constructor::reduce(fasta_reader{path, B})");
+  }
+  // two buffers handed out before reduce(): the tree of the remaining ones
+  const std::size_t B = 1000;
+  fasta_reader hr{dir + "/data/chmpxx", B};
+  std::vector<dna> buf;
+  hr.read_into(buf);
+  hr.read_into(buf);
+  shared_tree host;
+  tree_constructor ch{host};
+  while (hr.read_into(buf)) ch.reduce_segment(buf);
+  const pointer root = ch.reduce_roots();
+  fasta_reader f{dir + "/data/chmpxx", B};
+  f.read_into(buf);
+  f.read_into(buf);
+  shared_tree d;
+  tree_constructor cd{d};
+  CHECK(cd.reduce(f) == root && dump(d) == dump(host), "reduce(reader) after two read_into calls");
+}
+
 int main(int argc, char** argv) {
   dir = argc > 1 ? argv[1] : "tests/golden";
   const bool gpu = argc > 2 && std::string(argv[2]) == "gpu";
@@ -217,6 +254,7 @@ int main(int argc, char** argv) {
   buffer_api();
   if (gpu) {
     gpu_tree_constructor();
+    gpu_reader_segments();
     gpu_transposition();
     gpu_frequency_sort();
     gpu_file_build();

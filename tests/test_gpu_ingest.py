@@ -49,7 +49,7 @@ def test_device_extract_random_line_soup(ctx, gcz):
 def _fasta_cases():
     with open(os.path.join(GOLDEN, "manifest.json")) as f:
         m = json.load(f)
-    return [n for n, c in sorted(m.items()) if c["kind"] == "fasta"]
+    return [n for n, c in sorted(m.items()) if c["kind"] == "fasta" and "buffer" not in c]
 
 
 @pytest.mark.parametrize("name", _fasta_cases())

@@ -18,7 +18,7 @@ def _names(max_bases):
         m = json.load(f)
     return [n for n, c in sorted(m.items())
             if c["expect"]["exit"] == 0 and not (c["kind"] == "synth" and c["nbases"] > max_bases)
-            and c["kind"] != "fastabig"]
+            and c["kind"] != "fastabig" and "buffer" not in c]
 
 
 @pytest.fixture(scope="module")

@@ -30,12 +30,16 @@ def test_oracle_matches_reference(oracle_case, manifest, oracle, gcz):
     case = manifest[oracle_case]
     exp = case["expect"]
     kind, payload, L = case_input(case, gcz)
+    buf = case.get("buffer")   # segbuf/: reader buffers of B strands, each its own subtree
     if exp["exit"] != 0:
         with pytest.raises(oracle.OracleError) as ei:
-            oracle.build_fasta(payload, L)
+            oracle.build_fasta(payload, L) if buf is None else oracle.build_fasta_buffered(payload, L, buf)
         assert str(ei.value) == exp["stderr"]
         return
-    tree = oracle.build_fasta(payload, L) if kind == "fasta" else oracle.build_leaves(payload, L)
+    if buf is not None:
+        tree = oracle.build_fasta_buffered(payload, L, buf)
+    else:
+        tree = oracle.build_fasta(payload, L) if kind == "fasta" else oracle.build_leaves(payload, L)
     got = oracle.digest(tree)
     assert compare_digest(got, exp) == {}
 
