@@ -16,7 +16,9 @@
 #include <sstream>
 #include <thread>
 
+#include <signal.h>
 #include <sys/mman.h>
+#include <sys/prctl.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -285,9 +287,64 @@ auto tree_constructor::reduce(fasta_reader& file, bool verbose) -> pointer {   /
 // ---- multi-GPU construction (compress --gpus=N) ------------------------------------
 namespace {
 
+constexpr int kMaxGpus = 31;    // the multi-rank build's rank limit (gcz_dist_device.h kMaxRanks)
+
 struct MultiShared {            // head of the shared result region
-  std::atomic<int> status[64];  // per rank: 0 running, 1 done, 2 failed
+  std::atomic<int> status[kMaxGpus];  // per rank: 0 running, 1 done, 2 failed (read by rank 0's watcher)
   gcz_info info;                // rank 0's whole-tree summary
+};
+
+// Rank 0's watcher: a rank that fails (its status, or an exit that is not a clean 0) ends
+// the whole job at once -- the other ranks may be blocked in an RCCL collective or in
+// communicator creation, which has no timeout -- by killing every child and exiting 1.
+// Children die with the parent (PR_SET_PDEATHSIG), so a failure of rank 0 ends them too.
+class RankWatcher {
+ public:
+  RankWatcher(MultiShared* ms, std::vector<pid_t> kids) : ms_{ms}, kids_{std::move(kids)}, st_(kids_.size(), -1) {
+    thread_ = std::thread([this] { run(); });
+  }
+  // Stops watching and reaps the children that are left: true iff every rank exited 0.
+  bool finish() {
+    done_.store(true);
+    thread_.join();
+    bool ok = true;
+    for (std::size_t i = 0; i < kids_.size(); ++i) {
+      if (st_[i] < 0) {
+        int st = 0;
+        st_[i] = ::waitpid(kids_[i], &st, 0) == kids_[i] && WIFEXITED(st) ? WEXITSTATUS(st) : 255;
+      }
+      ok = ok && st_[i] == 0;
+    }
+    return ok;
+  }
+
+ private:
+  void run() {
+    while (!done_.load()) {
+      for (std::size_t i = 0; i < kids_.size(); ++i) {
+        const int r = int(i) + 1;
+        bool failed = ms_->status[r].load() == 2;
+        if (st_[i] < 0) {
+          int st = 0;
+          if (::waitpid(kids_[i], &st, WNOHANG) == kids_[i]) {
+            st_[i] = WIFEXITED(st) ? WEXITSTATUS(st) : 255;
+            failed = failed || st_[i] != 0;
+          }
+        }
+        if (failed) {
+          for (pid_t p : kids_) ::kill(p, SIGKILL);
+          std::cerr << "libgcz: rank " << r << " of the multi-GPU build failed, stopping every rank\n";
+          std::_Exit(1);
+        }
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    }
+  }
+  MultiShared* ms_;
+  std::vector<pid_t> kids_;
+  std::vector<int> st_;   // exit status of a reaped child, -1 while running
+  std::atomic<bool> done_{false};
+  std::thread thread_;
 };
 
 // first byte of [0, n) that is not one of the 16 symbols (any case), or n; threads
@@ -338,7 +395,12 @@ auto shared_tree_on_gpus(const std::filesystem::path& path, int gpus) -> shared_
   }
   if (const auto bad = first_unknown(bases, S * L); bad < S * L)   // to_nac's message and exit(1)
     (void)dna{std::string_view{reinterpret_cast<const char*>(bases + bad), 1}};
-  gpus = std::max(1, std::min(gpus, 64));
+  if (gpus > kMaxGpus) {
+    std::cerr << "compress: --gpus=" << gpus << " is more than the " << kMaxGpus
+              << " ranks the multi-GPU build supports, aborting...\n";
+    std::exit(1);
+  }
+  gpus = std::max(1, gpus);
   // layer slots: every layer's ids are < its pair count
   std::vector<std::uint64_t> loff{0};
   for (std::uint64_t n = S;;) {
@@ -371,6 +433,8 @@ auto shared_tree_on_gpus(const std::filesystem::path& path, int gpus) -> shared_
     const pid_t pid = ::fork();
     if (pid < 0) { std::cerr << "libgcz: fork failed\n"; std::exit(1); }
     if (pid == 0) {
+      ::prctl(PR_SET_PDEATHSIG, SIGKILL);   // never outlive rank 0
+      if (::getppid() == 1) std::_Exit(1);
       rank = r;
       rd = fd[0];
       ::close(fd[1]);
@@ -381,6 +445,8 @@ auto shared_tree_on_gpus(const std::filesystem::path& path, int gpus) -> shared_
     wr[r] = fd[1];
     kids.push_back(pid);
   }
+  std::unique_ptr<RankWatcher> watch;
+  if (rank == 0 && !kids.empty()) watch = std::make_unique<RankWatcher>(ms, kids);
   gcz_ctx* ctx = nullptr;
   int rc = gcz_ctx_create(shm ? dev0 : dev0 + rank, &ctx);
   if (rc) rank_fail(ms, rank, "device context", rc, nullptr);
@@ -391,8 +457,13 @@ auto shared_tree_on_gpus(const std::filesystem::path& path, int gpus) -> shared_
     unsigned char id[128] = {};
     if (rank == 0) {
       if ((rc = gcz_dist_unique_id(id, sizeof id))) rank_fail(ms, 0, "RCCL unique id", rc, ctx);
+      // (a rank that already died closed its pipe: EPIPE, not SIGPIPE)
+      struct sigaction ign {}, old {};
+      ign.sa_handler = SIG_IGN;
+      ::sigaction(SIGPIPE, &ign, &old);
       for (int r = 1; r < gpus; ++r)
         if (::write(wr[r], id, sizeof id) != ssize_t(sizeof id)) rank_fail(ms, 0, "id pipe", -1, ctx);
+      ::sigaction(SIGPIPE, &old, nullptr);
     } else if (::read(rd, id, sizeof id) != ssize_t(sizeof id)) {
       rank_fail(ms, rank, "id pipe", -1, ctx);
     }
@@ -400,7 +471,7 @@ auto shared_tree_on_gpus(const std::filesystem::path& path, int gpus) -> shared_
   }
   if (rc) rank_fail(ms, rank, "group", rc, ctx);
   std::uint64_t s0 = 0, s1 = 0;
-  gcz_dist_plan(S, gpus, rank, &s0, &s1, nullptr);
+  if ((rc = gcz_dist_plan(S, gpus, rank, &s0, &s1, nullptr))) rank_fail(ms, rank, "partition plan", rc, ctx);
   void* d = gcz_dev_alloc(ctx, (s1 - s0) * std::uint64_t(L) + 16);
   if (!d) rank_fail(ms, rank, "device allocation", GCZ_ERR_DEVICE, ctx);
   if ((rc = gcz_memcpy_h2d(ctx, d, bases + s0 * std::uint64_t(L), (s1 - s0) * std::uint64_t(L))))
@@ -421,11 +492,7 @@ auto shared_tree_on_gpus(const std::filesystem::path& path, int gpus) -> shared_
   gcz_ctx_destroy(ctx);
   ms->status[rank].store(1);
   if (rank != 0) std::_Exit(0);
-  bool ok = true;
-  for (pid_t pid : kids) {
-    int st = 0;
-    if (::waitpid(pid, &st, 0) != pid || !WIFEXITED(st) || WEXITSTATUS(st) != 0) ok = false;
-  }
+  const bool ok = !watch || watch->finish();
   for (int r = 1; r < gpus; ++r) ::close(wr[r]);
   if (!ok) { std::cerr << "libgcz: a rank of the multi-GPU build failed\n"; std::exit(1); }
   shared_tree t;

@@ -170,3 +170,25 @@ def test_reference_compress_on_dropin(name, tmp_path, manifest):
     f = r.stdout.strip().split(",")
     assert f[0] == "12" and int(f[1]) == exp["width"] and f[2] == exp["ratio"] and int(f[4]) == exp["bytes"]
     assert hashlib.sha256(out.read_bytes()).hexdigest() == exp["sha_dag"]
+
+
+def test_compress_cli_gpus_over_rank_limit(tmp_path):
+    """--gpus beyond the multi-rank build's 31 ranks is refused up front (no device touched)."""
+    r = _compress(["--no-save", "--gpus=40", os.path.join(GOLDEN, "data", "chmpxx")], str(tmp_path))
+    assert r.returncode == 1 and "more than the 31 ranks" in r.stderr
+
+
+@pytest.mark.gpu
+def test_compress_cli_gpus_failing_rank_ends_job(tmp_path):
+    """A rank that cannot start (here: a device index past the box's GPUs, RCCL transport) ends
+    the whole job with exit 1 instead of leaving the other ranks blocked in RCCL."""
+    import time
+    env = dict(os.environ, GCZ_DEVICE="0", HIP_VISIBLE_DEVICES="0")   # one visible GPU: rank 1 has none
+    env.pop("GCZ_MULTI_TRANSPORT", None)
+    t0 = time.time()
+    r = subprocess.run([os.path.join(PKG, "compress"), "--no-save", "--gpus=2",
+                        os.path.join(GOLDEN, "data", "chmpxx")], capture_output=True, text=True,
+                       cwd=str(tmp_path), env=env, timeout=180)
+    assert r.returncode == 1, r.stderr
+    assert "failed" in r.stderr
+    assert time.time() - t0 < 170
