@@ -74,9 +74,12 @@ def load_gcz():
     return mod
 
 
-def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None, bucketed_pairs=0, two_pass=False):
+def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None, bucketed_pairs=0, two_pass=False,
+                      launches=None):
     """Algorithmic HBM bytes of all launches of `kernel` in one build:
-    streamed bytes + one 64-B sector per random table/group access."""
+    streamed bytes + one 64-B sector per random table/group access.  The per-level kernels
+    (flagscan_node, resolve_node) count only the levels they ran on: the first `launches`
+    node levels (the later ones are direct subtrees or the fused tail)."""
     pk = []
     n = S
     while True:
@@ -127,12 +130,15 @@ def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None, bu
         return 16 * S + S // 8 + 8 * U
     if kernel == "flagscan_leaf":   # not-first marks; firsts: word, slot sector, leaf out, slot->id sector
         return S + U * (4 + 64 + 8 + 64 + 4)
+    lv = list(zip(pk, layer_sizes))[:launches] if launches is not None else list(zip(pk, layer_sizes))
     if kernel == "flagscan_node":   # not-first marks, group records; firsts: pair re-read, node out, word
-        return sum(p + 16 * ((p + 63) // 64) + u * (8 + 8 + 4 + 4) for p, u in zip(pk, layer_sizes))
+        return sum(p + 16 * ((p + 63) // 64) + u * (8 + 8 + 4 + 4) for p, u in lv)
     if kernel == "resolve_leaf":    # marks; non-first: word, slot->id sector, word
         return S + (S - U) * (4 + 64 + 4)
-    if kernel == "resolve_node":    # marks; non-first: word, slot sector, group sector, word
-        return sum(p + (p - u) * (4 + 64 + 64 + 4) for p, u in zip(pk, layer_sizes))
+    if kernel == "resolve_node":    # marks; non-first: word in and out; the slot and group sectors
+        # of the repeated keys (at most min(repeats, uniques) distinct keys: a hot key's
+        # repeats share its two lines)
+        return sum(p + (p - u) * (4 + 4) + 128 * min(p - u, u) for p, u in lv)
     return 0
 
 
@@ -382,8 +388,10 @@ def main():
                 failed = [any(flags)]
             if failed[0]:
                 # RCCL could not form the communicator: the same build with host-staged
-                # exchanges (correct, slower), labelled in the line -- not a silent switch
+                # exchanges (correct, slower), labelled in the line ("transport") and the run
+                # exits 4 -- it is not an RCCL number
                 print(f"bench: RCCL group failed ({err}); falling back to the shm transport", file=sys.stderr)
+                exit_code[0] = 4
                 if group is not None:
                     group.close()
                 name = [f"/gcz_bench_{os.getpid()}_{time.time_ns()}" if rank == 0 else None]
@@ -463,7 +471,8 @@ def main():
         b = algorithmic_bytes(name, L, S, info["n_leaves"], info["layer_size"],
                               info["hashed_pairs"] if mode in ("single", "replicas") else None,
                               info.get("bucketed_pairs", 0),
-                              two_pass=prof.get("bucket_fine", {}).get("launches", 0) > 0) // share
+                              two_pass=prof.get("bucket_fine", {}).get("launches", 0) > 0,
+                              launches=p["launches"]) // share
         kernels[name] = {"launches": p["launches"], "total_ms": round(p["total_ms"], 4),
                          "avg_ms": p["total_ms"] / p["launches"], "alg_bytes": b,
                          "gbs": b / (p["total_ms"] * 1e-3) / 1e9 if p["total_ms"] > 0 else None}
@@ -569,6 +578,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "weak" if (args.mode in ("weak", "replicas") and mode != "virtual") else "strong",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "transport": transport_used if mode == "dist" else None,
             "config": {"workload": args.config, "nbases": nbases * (world if mode == "replicas" else 1),
                        "per_gpu_nbases": nbases // world if mode == "dist" else nbases, "L": L,
                        "strands": S * (world if mode == "replicas" else 1),

@@ -55,14 +55,19 @@ std::vector<u64> gcz_host::leaf_chunks(u64 S, int first_log2) {
   return chunk_start;
 }
 
-int gcz_ctx::ensure_marks(u64 S) {
-  const u64 full_b = (S + 16 + 255) / 256 * 256, half = ((S + 1) / 2 + 16 + 255) / 256 * 256;
-  if (int rc = ensure(nf, full_b + half)) return rc;       // [leaf / even layers: S][odd layers: S/2]
-  if (int rc = ensure(multi, 2 * half)) return rc;         // [even layers][odd layers]
+int gcz_ctx::ensure_marks(u64 S) { return ensure_marks(S, (S + 1) / 2); }
+
+// Set 0: the leaves and the outputs of odd node levels (n0 elements at most); set 1: the
+// outputs of even node levels (n1).  A global level loop has n1 = ceil(S / 2); reader-buffer
+// segments can make layer 0 longer (up to S pairs for one-strand buffers).
+int gcz_ctx::ensure_marks(u64 n0, u64 n1) {
+  const u64 b0 = (n0 + 16 + 255) / 256 * 256, b1 = (n1 + 16 + 255) / 256 * 256;
+  if (int rc = ensure(nf, b0 + b1)) return rc;             // [leaf / outputs of odd layers][of even layers]
+  if (int rc = ensure(multi, b0 + b1)) return rc;
   nf_set[0] = nf.as<unsigned char>();
-  nf_set[1] = nf.as<unsigned char>() + full_b;
+  nf_set[1] = nf.as<unsigned char>() + b0;
   multi_set[0] = multi.as<unsigned char>();
-  multi_set[1] = multi.as<unsigned char>() + half;
+  multi_set[1] = multi.as<unsigned char>() + b0;
   return GCZ_OK;
 }
 
@@ -284,7 +289,7 @@ int gcz_ctx::dense_phase_b(const LeafLevel& a, Header* d_hdr, const u32* gid, u6
   (void)d_hdr;
   const DensePlan& P = dl_plan;
   const int RBbytes = int((1u << P.IB) * 4);
-  const int words_bytes = int((kDC + 2 * kDNBMax + 1 + 16) * 4);
+  const int words_bytes = int((kDC + 2 * kDNBMax + 1 + 16 + kDC / 32) * 4);
   HIP_TRY(allow_lds(k_dl_ids, RBbytes));
   HIP_TRY(allow_lds(k_dl_words, words_bytes));
   hipEvent_t e0{};
@@ -294,9 +299,8 @@ int gcz_ctx::dense_phase_b(const LeafLevel& a, Header* d_hdr, const u32* gid, u6
   HIP_TRY(hipGetLastError());
   prof_end(KID_DL_IDS, e0);
   prof_begin(KID_DL_WORDS, e0);
-  hipLaunchKernelGGL(k_dl_words, dim3(P.nch), dim3(kDThreads), words_bytes, stream, dl_pw.as<u32>(),
-                     dl_rec.as<u32>(), dl_idrec.as<u32>(), dl_off.as<u32>(), P, dl_fb.as<unsigned long long>(),
-                     a.words, leaves);
+  hipLaunchKernelGGL(k_dl_words, dim3(P.nch), dim3(kDThreads), words_bytes, stream, dl_rec.as<u32>(),
+                     dl_idrec.as<u32>(), dl_off.as<u32>(), P, dl_fb.as<unsigned long long>(), a.words, leaves);
   HIP_TRY(hipGetLastError());
   prof_end(KID_DL_WORDS, e0);
   return GCZ_OK;
@@ -612,7 +616,11 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   if ((rc = ensure(nodes_out, layer_off[D] * 8 + 16))) return rc;
   if ((rc = ensure(hdr, sizeof(Header)))) return rc;
   if ((rc = ensure(stats, kStatBytes))) return rc;
-  if ((rc = ensure_marks(S))) return rc;
+  {   // marks of every level's output, by parity (k_clear / the flag scans write pk[k] of set (k + 1) & 1)
+    u64 n0 = S, n1 = 0;
+    for (int k = 0; k < D; ++k) (k & 1 ? n0 : n1) = std::max(k & 1 ? n0 : n1, pk[k]);
+    if ((rc = ensure_marks(n0, n1))) return rc;
+  }
   if (!h_hdr) HIP_TRY(hipHostMalloc((void**)&h_hdr, sizeof(Header), hipHostMallocDefault));
 
   Header* d_hdr = hdr.as<Header>();

@@ -333,6 +333,7 @@ struct gcz_ctx {
   }
   // Marks buffers for levels of up to S elements (sets aligned for uchar2 loads).
   int ensure_marks(gcz_host::u64 S);
+  int ensure_marks(gcz_host::u64 n0, gcz_host::u64 n1);   // set 0 / set 1 element counts
 
   int leaf_level(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr);
   // The dense leaf level (pure-ACGT strands, L <= 12); *used = false when a strand is

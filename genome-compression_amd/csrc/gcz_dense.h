@@ -222,7 +222,8 @@ template <int L, bool kBases>
   for (u32 b = tid; b < P.NB; b += kDThreads) cnt[u64(b) * P.nch + blockIdx.x] = s_hist[b];
 }
 
-// Scatter: records (h's low IB bits << kDLog | position in chunk) in runs
+// Scatter: records (h's low IB bits << kDLog | position in chunk, the pre-word's m/t/v in
+// bits 29-31) in runs
 // (chunk, bucket) at off[b * nch + chunk] of the bucket-ordered record array,
 // staged in LDS so every run is written contiguously.
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_scatter(const u32* __restrict__ pw, DensePlan P,
@@ -237,11 +238,11 @@ template <int L, bool kBases>
   const u32 ch = blockIdx.x;
   const u64 c0 = u64(ch) * kDC;
   const u32 n = u32(P.S - c0 < u64(kDC) ? P.S - c0 : u64(kDC));
-  u32 h[kDC / kDThreads];
+  u32 h[kDC / kDThreads];   // pre-words: hashed code | m/t/v
 #pragma unroll
   for (u32 j = 0; j < kDC / kDThreads; ++j) {   // every pre-word load in flight at once
     const u32 q = j * kDThreads + tid;
-    h[j] = q < n ? pw[c0 + q] & kIdx : 0u;
+    h[j] = q < n ? pw[c0 + q] : 0u;
   }
   chunk_runs(off, P, ch, s_base, s_dst, s_tmp);
   if (u32(tid) < P.NB) s_cur[tid] = s_base[tid];
@@ -251,8 +252,9 @@ template <int L, bool kBases>
   for (u32 j = 0; j < kDC / kDThreads; ++j) {
     const u32 q = j * kDThreads + tid;
     if (q < n) {
-      const u32 slot = atomicAdd(&s_cur[h[j] >> P.IB], 1u);
-      s_stage[slot] = ((h[j] & imask) << kDLog) | q;
+      const u32 hc = h[j] & kIdx;
+      const u32 slot = atomicAdd(&s_cur[hc >> P.IB], 1u);
+      s_stage[slot] = ((hc & imask) << kDLog) | q | (h[j] & kBits);   // (IB + 15 <= 29 bits, then m/t/v)
     }
   }
   __syncthreads();
@@ -321,7 +323,7 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
   for (u32 c = tid; c <= P.nch; c += kDThreads) s_cnt[c] = 0;
   __syncthreads();
   bucket_records(rec, off, P, b, [&](u32 x, u32, u32 pos) {
-    const u32 idx = x >> kDLog;
+    const u32 idx = (x & kIdx) >> kDLog;
     if (s_fp[idx] > pos) atomicMin(&s_fp[idx], pos);
   });
   __syncthreads();
@@ -398,7 +400,7 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
 }
 
 // Ids: per bucket, the id of each present code (rank of its first position)
-// in LDS, then one id per record in bucket order.
+// in LDS, then one final word (id | the record's m/t/v) per record in bucket order.
 // gid (multi-rank build): the GLOBAL id of every code present on this rank,
 // indexed by hashed code; null: ids are this build's first-occurrence ranks.
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_ids(const u32* __restrict__ rec, const u32* __restrict__ off,
@@ -435,71 +437,71 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
 #pragma unroll
     for (int j = 0; j < kDBatch; ++j) {
       const u32 rj = r + u32(j) * kDThreads;
-      if (rj < r1) idrec[rj] = s_id[x[j] >> kDLog];
+      if (rj < r1) idrec[rj] = s_id[(x[j] & kIdx) >> kDLog] | (x[j] & kBits);   // the final word
     }
   }
 }
 
-// Words: per chunk, the ids of its records back into position order (LDS), the
-// pre-word's m/t/v bits -> final words; first occurrences emit their leaf.
-[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_words(const u32* __restrict__ pw, const u32* __restrict__ rec,
+// Words: per chunk, the final words of its records (k_dl_ids, bucket order) back into
+// position order in LDS, written out coalesced.  A record at a first occurrence (the
+// chunk's first-occurrence bitmap, staged in LDS) emits its leaf from the record's code
+// (bucket | the record's low code bits); leaf ids are the first-occurrence ranks.
+[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_words(const u32* __restrict__ rec,
                                                         const u32* __restrict__ idrec, const u32* __restrict__ off,
                                                         DensePlan P, const unsigned long long* __restrict__ fb,
                                                         u32* __restrict__ words, u64* __restrict__ leaves_out) {
   extern __shared__ u32 s_dyn[];
-  u32* s_w = s_dyn;                  // kDC ids by position in the chunk
+  u32* s_w = s_dyn;                  // kDC final words by position in the chunk
   u32* s_base = s_dyn + kDC;         // NB + 1
   u32* s_dst = s_base + kDNBMax + 1; // NB
   u32* s_tmp = s_dst + kDNBMax;      // 16
+  u32* s_fb = s_tmp + 16;            // kDC / 32 first-occurrence bits of the chunk
   const int tid = threadIdx.x;
   const u32 ch = blockIdx.x;
   const u64 c0 = u64(ch) * kDC;
   const u32 n = u32(P.S - c0 < u64(kDC) ? P.S - c0 : u64(kDC));
+  if (leaves_out)
+    for (u32 w = tid; w < kDC / 64; w += kDThreads) {
+      const u64 m = (c0 + u64(w) * 64 < P.S) ? fb[(c0 >> 6) + w] : 0ull;
+      s_fb[2 * w] = u32(m);
+      s_fb[2 * w + 1] = u32(m >> 32);
+    }
   chunk_runs(off, P, ch, s_base, s_dst, s_tmp);
   const int lane = tid & 63, wave = tid >> 6;
+  const u32 IB = P.IB, imask = (1u << IB) - 1u;
   constexpr int RW = 8;   // runs per wave step (2 loads each in flight per lane)
   for (u32 b0 = wave; b0 < P.NB; b0 += (kDThreads / 64) * RW) {
-    u32 x[RW], id[RW], dst[RW], len[RW];
+    u32 x[RW], w[RW], dst[RW], len[RW];
 #pragma unroll
     for (int j = 0; j < RW; ++j) {
       const u32 b = b0 + u32(j) * (kDThreads / 64);
-      len[j] = 0; dst[j] = 0; x[j] = 0; id[j] = 0;
+      len[j] = 0; dst[j] = 0; x[j] = 0; w[j] = 0;
       if (b < P.NB) {
         dst[j] = s_dst[b];
         len[j] = s_base[b + 1] - s_base[b];
       }
       if (u32(lane) < len[j]) {
         x[j] = rec[dst[j] + lane];
-        id[j] = idrec[dst[j] + lane];
+        w[j] = idrec[dst[j] + lane];
       }
     }
 #pragma unroll
     for (int j = 0; j < RW; ++j) {
-      if (u32(lane) < len[j]) s_w[x[j] & (kDC - 1)] = id[j];
-      for (u32 l = lane + 64; l < len[j]; l += 64) s_w[rec[dst[j] + l] & (kDC - 1)] = idrec[dst[j] + l];
-    }
-  }
-  __syncthreads();
-  for (u32 q0 = 0; q0 < n; q0 += kDThreads * kDBatch) {
-    u32 p[kDBatch];
-#pragma unroll
-    for (int j = 0; j < kDBatch; ++j) {
-      const u32 q = q0 + u32(j) * kDThreads + tid;
-      p[j] = q < n ? pw[c0 + q] : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < kDBatch; ++j) {
-      const u32 q = q0 + u32(j) * kDThreads + tid;
-      if (q >= n) continue;
-      const u64 s = c0 + q;
-      const u32 id = s_w[q];
-      words[s] = id | (p[j] & kBits);
-      if (leaves_out && ((fb[s >> 6] >> (s & 63)) & 1ull)) {
-        const u32 h = p[j] & kIdx;
-        leaves_out[id] = code2_leaf((h * P.Kinv) & P.cmask, P.L);
+      const u32 b = b0 + u32(j) * (kDThreads / 64);
+      for (u32 l = lane; l < len[j]; l += 64) {
+        const u32 xr = l == u32(lane) ? x[j] : rec[dst[j] + l];
+        const u32 wr = l == u32(lane) ? w[j] : idrec[dst[j] + l];
+        const u32 q = xr & (kDC - 1);
+        s_w[q] = wr;
+        if (leaves_out && ((s_fb[q >> 5] >> (q & 31)) & 1u)) {
+          const u32 h = (b << IB) | (((xr & kIdx) >> kDLog) & imask);
+          leaves_out[wr & kIdx] = code2_leaf((h * P.Kinv) & P.cmask, P.L);
+        }
       }
     }
   }
+  __syncthreads();
+  for (u32 q = tid; q < n; q += kDThreads) words[c0 + q] = s_w[q];
 }
 
 // ---- multi-rank build (gcz_dist.hip): the leaf level of one rank ----------------

@@ -35,8 +35,8 @@ def _ctx_env(gcz, env):
 
 @pytest.fixture(scope="module")
 def ctx_split(gcz):
-    """Every build through the virtual-rank split, 2^14 strands per rank."""
-    c = _ctx_env(gcz, {"GCZ_SPLIT_MIN": "0", "GCZ_SPLIT_SHARE": "16384"})
+    """Every build through the virtual-rank split, 2^15 strands per rank (up to 26 ranks here)."""
+    c = _ctx_env(gcz, {"GCZ_SPLIT_MIN": "0", "GCZ_SPLIT_SHARE": "32768"})
     yield c
     c.close()
 
