@@ -289,7 +289,7 @@ int gcz_ctx::dense_phase_b(const LeafLevel& a, Header* d_hdr, const u32* gid, u6
   (void)d_hdr;
   const DensePlan& P = dl_plan;
   const int RBbytes = int((1u << P.IB) * 4);
-  const int words_bytes = int((kDC + 2 * kDNBMax + 1 + 16 + kDC / 32) * 4);
+  const int words_bytes = int((kDC + 2 * kDNBMax + 1 + 16 + kDC / 32 + kDNBMax) * 4);
   HIP_TRY(allow_lds(k_dl_ids, RBbytes));
   HIP_TRY(allow_lds(k_dl_words, words_bytes));
   hipEvent_t e0{};
@@ -317,7 +317,7 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   if (p == 0) return GCZ_OK;
   const u64 cap = node_cap(p);
   const u32 Bk = std::max<u32>(1, bit_width(a.bound));
-  LevelTab nt = plan_table(a.fused ? a.ftab : tab.ptr, cap, 2 * (Bk + 3), p, Bk, allow_packed, kMaxProbe);
+  LevelTab nt = plan_table(a.fused ? a.ftab : tab.ptr, cap, 2 * (Bk + 2), p, Bk, allow_packed, kMaxProbe);
   nt.pt.cas_first = cap_boost > 0;
   const int cur = (a.k + 1) & 1, prev = a.k & 1;
   unsigned char* knf = nf_set[cur];
@@ -341,11 +341,14 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   // <= 2560 pairs (the LDS dedupe holds 4608) and a record fits 8 bytes
   BktPlan bp{};
   bp.T = nt.pt;
-  bp.K = 2 * (Bk + 3);
-  while (bp.bb < u32(kBktMaxLog) && (p >> bp.bb) > 2560) ++bp.bb;
-  const u32 bkt = a.allow_bucket && bucket_now && nt.packed && p >= bucket_min && (p >> bp.bb) <= 2560 &&
-                  bp.K >= bp.bb && bp.K - bp.bb + kBktRP <= 64 &&
-                  p <= u64(kBktMaxG) * kBktChunk ? 1u : 0u;
+  bp.K = 2 * (Bk + 2);
+  // (up to 2^16 buckets through the two-pass partition: 256 coarse x 256 fine, e.g. 133 M pairs
+  // on layer 0 of a 3.2 Gbase genome; the single pass counts at most 2^14 in LDS)
+  const u32 bb_max = two_pass ? kPartMaxB1 + kFineMaxB2 : u32(kBktMaxLog);
+  while (bp.bb < bb_max && (p >> bp.bb) > 2560) ++bp.bb;
+  u32 bkt = a.allow_bucket && bucket_now && nt.packed && p >= bucket_min && (p >> bp.bb) <= 2560 &&
+            bp.K >= bp.bb && bp.K - bp.bb + kBktRP <= 64 &&
+            p <= u64(kBktMaxG) * kBktChunk ? 1u : 0u;
   const u32 bb = bp.bb;
   const u64 G = (p + kBktChunk - 1) / kBktChunk;
   const u64 ncnt = (u64(1) << bb) * G + 1;
@@ -365,6 +368,8 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   b2.nslice = u32((b2.G + b2.SC - 1) / b2.SC);
   const bool two = bkt && two_pass && b2.b2 <= u32(kFineMaxB2) && bp.K - b2.b1 + kPartLog <= 64 &&
                    bp.K - bb + b2.P <= 64 && mean_run * b2.SC <= u64(kFineCap) / 2 && b2.nslice <= 512;
+  if (two) bkt = 2;   // (the two-pass partition also takes repetitive data: kernels see bkt 2)
+  else if (a.repetitive || bb > u32(kBktMaxLog)) bkt = 0;   // (the single pass would skip on the device)
   if (two) {
     int rc;
     const u64 nfine = (u64(1) << b2.b1) * b2.nslice;
@@ -399,7 +404,7 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   if (two) {
     prof_begin(KID_BKT_SCATTER, e0);
     hipLaunchKernelGGL(k_bkt_part, dim3(unsigned(b2.G)), dim3(kBktThreads), size_t(kPartChunk) * 8, stream, a.in,
-                       n, p, pnf, pmu, b2, bkt_key.as<u64>(), bkt_cnt.as<u32>(), a.words, d_hdr, a.pcount,
+                       n, p, pnf, pmu, b2, bkt_key.as<u64>(), bkt_cnt.as<u32>(), a.words, mk, d_hdr, a.pcount,
                        stats.as<u64>());
     HIP_TRY(hipGetLastError());
     prof_end(KID_BKT_SCATTER, e0);
@@ -449,7 +454,7 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     if (a.p_next) {
       const u32 Bn = std::max<u32>(1, bit_width(p));
       fz.clear = static_cast<uint4*>(a.ftab_next);
-      fz.clear16 = plan_table(a.ftab_next, node_cap(a.p_next), 2 * (Bn + 3), a.p_next, Bn, allow_packed, kMaxProbe)
+      fz.clear16 = plan_table(a.ftab_next, node_cap(a.p_next), 2 * (Bn + 2), a.p_next, Bn, allow_packed, kMaxProbe)
                        .bytes() / 16;
       clr16 = (a.p_next + 15) / 16;
     }
@@ -475,7 +480,8 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   auto flagscan = [&](auto items) {
     hipLaunchKernelGGL((k_flagscan_node<decltype(items)::value>), gs, dim3(kBlock), 0, stream, a.words, p, a.in, n,
                        knf, d_grp, ndesc, a.ticket, a.out, a.count, a.pcount, mk.multi, a.hashed_next, clr_nf, clr_mu,
-                       clr16, a.fused && (!a.fused_last || a.tail_settles) ? a.sid : nullptr);
+                       clr16, a.fused && (!a.fused_last || a.tail_settles) ? a.sid : nullptr,
+                       bkt == 2 ? static_cast<const u32*>(&d_hdr->predup) : nullptr);
   };
   if (tile == u64(kTile)) flagscan(std::integral_constant<int, kItems>{});
   else if (tile == u64(kTileSmall)) flagscan(std::integral_constant<int, kItemsSmall>{});
@@ -671,7 +677,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
         if (fused) {   // level 0's table and marks
           const u32 B0 = std::max<u32>(1, bit_width(std::min(S, leaf_cap)));
           ip.ftab = static_cast<uint4*>(fregion_ptr(0));
-          ip.nftab16 = plan_table(ip.ftab, node_cap0, 2 * (B0 + 3), pk[0], B0, allow_packed, kMaxProbe).bytes() / 16;
+          ip.nftab16 = plan_table(ip.ftab, node_cap0, 2 * (B0 + 2), pk[0], B0, allow_packed, kMaxProbe).bytes() / 16;
           ip.fnf = reinterpret_cast<uint4*>(nf_set[1]);
           ip.fmulti = reinterpret_cast<uint4*>(multi_set[1]);
           ip.nfm16 = (pk[0] + 15) / 16;
@@ -778,7 +784,8 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
         // inside reader buffers)
         na.hashed_next = k + 1 < seg_d ? nullptr : &d_hdr->hashed_next[k];
         na.gate = &d_hdr->gate[k];
-        na.allow_bucket = !table_only && !fused;
+        na.allow_bucket = !fused;
+        na.repetitive = table_only;
         if (fused) {
           na.fused = true;
           na.ftab = fregion_ptr(k);
@@ -803,7 +810,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
           HIP_TRY(hipMemcpyAsync(&pd, &d_hdr->predup, 4, hipMemcpyDeviceToHost, stream));
           HIP_TRY(hipStreamSynchronize(stream));
           direct = g == n;
-          table_only = pd != 0;   // repetitive data: later levels skip the (gated-off) bucket launches
+          table_only = pd != 0;   // repetitive data: later levels skip the single-pass bucket launches
         }
       }
       if (!tail_done) {   // (the tail sums the statistics itself)

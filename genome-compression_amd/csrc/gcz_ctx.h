@@ -133,6 +133,7 @@ struct NodeLevel {
   u32* hashed_next = nullptr;       // single-device build: look ahead for the next level (null: off)
   u64* gate = nullptr;              // ... and open its gate (the next level's pcount)
   bool allow_bucket = false;        // single-device build: bucketed insert allowed (overflow -> rebuild)
+  bool repetitive = false;          // ... the host knows the data is repetitive (no single-pass buckets)
   // fused small-build levels (k_node_insert with a resolver, gcz_device.h): this level's
   // table lives in ftab region k % 3, its repeats are settled by the next level's insert
   // unless it is the last one before the tail (resolve launched here)

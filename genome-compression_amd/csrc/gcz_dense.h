@@ -456,6 +456,8 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
   u32* s_dst = s_base + kDNBMax + 1; // NB
   u32* s_tmp = s_dst + kDNBMax;      // 16
   u32* s_fb = s_tmp + 16;            // kDC / 32 first-occurrence bits of the chunk
+  u32* s_ex = s_fb + kDC / 32;       // NB + 1: exclusive prefix of the runs' records past the
+                                     // first 64 (skewed data: hot codes), walked by the block
   const int tid = threadIdx.x;
   const u32 ch = blockIdx.x;
   const u64 c0 = u64(ch) * kDC;
@@ -469,6 +471,14 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
   chunk_runs(off, P, ch, s_base, s_dst, s_tmp);
   const int lane = tid & 63, wave = tid >> 6;
   const u32 IB = P.IB, imask = (1u << IB) - 1u;
+  auto place = [&](u32 b, u32 xr, u32 wr) {   // one record: its word into position order, its leaf
+    const u32 q = xr & (kDC - 1);
+    s_w[q] = wr;
+    if (leaves_out && ((s_fb[q >> 5] >> (q & 31)) & 1u)) {
+      const u32 h = (b << IB) | (((xr & kIdx) >> kDLog) & imask);
+      leaves_out[wr & kIdx] = code2_leaf((h * P.Kinv) & P.cmask, P.L);
+    }
+  };
   constexpr int RW = 8;   // runs per wave step (2 loads each in flight per lane)
   for (u32 b0 = wave; b0 < P.NB; b0 += (kDThreads / 64) * RW) {
     u32 x[RW], w[RW], dst[RW], len[RW];
@@ -488,16 +498,21 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
 #pragma unroll
     for (int j = 0; j < RW; ++j) {
       const u32 b = b0 + u32(j) * (kDThreads / 64);
-      for (u32 l = lane; l < len[j]; l += 64) {
-        const u32 xr = l == u32(lane) ? x[j] : rec[dst[j] + l];
-        const u32 wr = l == u32(lane) ? w[j] : idrec[dst[j] + l];
-        const u32 q = xr & (kDC - 1);
-        s_w[q] = wr;
-        if (leaves_out && ((s_fb[q >> 5] >> (q & 31)) & 1u)) {
-          const u32 h = (b << IB) | (((xr & kIdx) >> kDLog) & imask);
-          leaves_out[wr & kIdx] = code2_leaf((h * P.Kinv) & P.cmask, P.L);
-        }
-      }
+      if (u32(lane) < len[j]) place(b, x[j], w[j]);
+    }
+  }
+  {   // the records past the first 64 of each run, flat over the block (none on uniform data)
+    const u32 b = u32(tid);
+    const u32 len = b < P.NB ? s_base[b + 1] - s_base[b] : 0u;
+    u32 total;
+    const u32 ex = block_excl(len > 64u ? len - 64u : 0u, s_tmp, &total);
+    if (b < P.NB) s_ex[b] = ex;
+    if (b == 0) s_ex[P.NB] = total;
+    __syncthreads();
+    for (u32 k = u32(tid); k < total; k += kDThreads) {
+      const u32 rb = run_of(s_ex, P.NB, k);
+      const u32 l = 64u + (k - s_ex[rb]), at = s_dst[rb] + l;
+      place(rb, rec[at], idrec[at]);
     }
   }
   __syncthreads();

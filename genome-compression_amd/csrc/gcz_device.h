@@ -210,15 +210,13 @@ __device__ __forceinline__ u32 slot_hash(u64 k) {
   return u32(k);
 }
 
-__device__ __forceinline__ u32 enc_child(u32 w, u32 B) {      // pointer word -> B+3 bits
+// pointer word -> B+2 bits: index code, mirror, transpose.  The invariant bit is left out:
+// it is a property of the child's id (src/shared_tree.cpp:670 gives every occurrence of a key
+// the same value), so keys stay distinct -- the same to_ulong key as node::operator==.
+__device__ __forceinline__ u32 enc_child(u32 w, u32 B) {
   const u32 idx = w & kIdx;
   const u32 code = idx == kIdx ? ((1u << B) - 1u) : idx;      // null index -> all-ones code
-  return (code << 3) | (((w >> 29) & 1u) << 2) | (((w >> 30) & 1u) << 1) | (w >> 31);
-}
-__device__ __forceinline__ u32 dec_child(u32 e, u32 B) {
-  const u32 code = e >> 3;
-  if (code == (1u << B) - 1u) return kNullWord;
-  return code | (((e >> 2) & 1u) << 29) | (((e >> 1) & 1u) << 30) | ((e & 1u) << 31);
+  return (code << 2) | (((w >> 29) & 1u) << 1) | ((w >> 30) & 1u);
 }
 
 // not-first marks: 0 = maybe first, 1 = not first (resolve through the slot),
@@ -226,6 +224,10 @@ __device__ __forceinline__ u32 dec_child(u32 e, u32 B) {
 // 3 = multi-rank leaf level: the key was seeded with its GLOBAL id (rank 0's dictionary,
 // gcz_dist.hip), the word already holds the final id
 constexpr unsigned char kNfMaybe = 0, kNfNot = 1, kNfDone = 2, kNfGlobal = 3;
+// 4 = a node pair collapsed onto an earlier repeat of its key in the same 4096-pair block of
+// the bucketed partition (k_bkt_part on repetitive data); its word holds that position until
+// the flag scan points it at the key's first occurrence
+constexpr unsigned char kNfDup = 4;
 __device__ __forceinline__ void mark(unsigned char* nf, u32 pos) { nf[pos] = kNfNot; }
 
 // Marks of one level: nf (not first) and, on node levels, multi (the key has
@@ -322,7 +324,7 @@ struct PackedTab {
   u64 kmask, c1, c2, c1i, c2i;
 
   __device__ __forceinline__ u64 node_key(u32 cl, u32 cr) const {
-    return (u64(enc_child(cl, B)) << (B + 3)) | enc_child(cr, B);
+    return (u64(enc_child(cl, B)) << (B + 2)) | enc_child(cr, B);
   }
   __device__ __forceinline__ u64 mix(u64 x) const {
     x ^= x >> sh; x = (x * c1) & kmask;
@@ -736,7 +738,9 @@ __global__ __launch_bounds__(kBlock) void k_node_insert(u32* __restrict__ in, u6
     for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < fz.clear16; i += u64(gridDim.x) * kBlock)
       fz.clear[i] = ones;
   }
-  if (bkt && !level_direct(prev_count, n) && hdr->predup == 0) return;   // k_bkt_* insert this level
+  // k_bkt_* insert this level (bkt 2: the two-pass partition, on any data; 1: the single pass,
+  // on non-repetitive data only)
+  if (bkt && !level_direct(prev_count, n) && (bkt == 2 || hdr->predup == 0)) return;
   // every load that depends on nothing goes out first: the pair, the previous level's
   // marks of its two children, the gate inputs
   const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
@@ -846,6 +850,11 @@ __global__ __launch_bounds__(kBlock) void k_node_insert(u32* __restrict__ in, u6
 }
 
 // ---- flag scan ------------------------------------------------------------------
+
+// Workgroup barrier that waits for LDS operations only (__syncthreads also drains the wave's
+// outstanding global loads and stores: vmcnt(0)), for loops that exchange data through LDS
+// while their global loads for the next step are in flight.
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ u64 wave_sum(u64 v) {
 #pragma unroll
@@ -1086,7 +1095,7 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
                                                          const unsigned char* __restrict__ multi,
                                                          u32* __restrict__ hashed_next, uint4* __restrict__ clr_nf,
                                                          uint4* __restrict__ clr_multi, u64 clr16,
-                                                         u32* __restrict__ sid) {
+                                                         u32* __restrict__ sid, const u32* __restrict__ dup_flag) {
   // fused small-build levels: clear the marks of the level after this one (its parity
   // set held the previous level's marks, last read by this level's insert)
   for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < clr16; i += u64(gridDim.x) * kBlock) {
@@ -1140,6 +1149,7 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
   tile_scan(ts, &s_tile, s_pre, nf, 0, p, 0, desc, ticket, count_out, fetch);
   const u64 lt = (1ull << lane) - 1;
   bool hashed = false;
+  const bool dups = dup_flag && *dup_flag != 0;   // block-collapsed repeats (k_bkt_part) exist
 #pragma unroll
   for (int e = 0; e < ITEMS; ++e) {
     const u64 j = ts.base + u64(e) * kBlock + tid;
@@ -1174,6 +1184,13 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
       w.x = cl; w.y = cr;
       out[id] = w;
       words[j] = make_word(id, m, t, ulw(l) == ulw(xf(r, 1, 0)));   // the insert's bits, recomputed
+    } else if (dups && j < p && nf[j] == kNfDup) {
+      // its block representative: the key's first occurrence itself, or a repeat whose word
+      // the bucket dedupe pointed at the first occurrence (only first occurrences' words
+      // change here, so that word is stable)
+      const u32 w = words[j];
+      const u32 rep = w & kIdx;
+      if (nf[rep] != kNfMaybe) words[j] = (words[rep] & kIdx) | (w & kBits);
     }
   }
   if (hashed_next) {
@@ -1209,11 +1226,11 @@ __global__ __launch_bounds__(kBlock) void k_resolve_node(u32* __restrict__ words
     *gate = (*count == p || (hashed_next && *hashed_next == 0)) ? p : ~0ull;
   if (level_direct(prev_count, n)) return;
   const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (j >= p || nf[j] != kNfNot) return;
+  if (j >= p || (nf[j] != kNfNot && nf[j] != kNfDup)) return;
   const u32 w = words[j];
   u64 key;
   u32 q;
-  if (bkt && hdr->predup == 0) q = w & kIdx;    // bucketed insert: the word holds it
+  if (bkt && (bkt == 2 || hdr->predup == 0)) q = w & kIdx;    // bucketed insert: the word holds it
   else T.read(w & kIdx, key, q);                // q = the key's first position
   const Group h = grp[q >> 6];
   const u32 id = h.prefix + u32(__popcll(h.mask & ((1ull << (q & 63)) - 1)));
@@ -1290,6 +1307,10 @@ __device__ __forceinline__ u64 bkt_chunk(u64 G) {
 
 __device__ __forceinline__ bool bkt_skip(const Header* hdr, const u64* prev_count, u64 n) {
   return hdr && (level_direct(prev_count, n) || hdr->predup != 0);   // (null: the multi-rank owner)
+}
+// the two-pass partition also takes repetitive data (k_bkt_part collapses block repeats)
+__device__ __forceinline__ bool bkt2_skip(const Header* hdr, const u64* prev_count, u64 n) {
+  return hdr && level_direct(prev_count, n);
 }
 
 // Column g of the count matrix: cnt[b * G + g] = hashed pairs of chunk g in bucket b.
@@ -1494,15 +1515,34 @@ __device__ __forceinline__ void lds_excl256(u32* c, u32 n) {
   }
 }
 
+// Repetitive data (hdr->predup): before partitioning, the repeats of a key inside each
+// block of 4096 consecutive pairs collapse onto the block's earliest occurrence of it (an LDS
+// table per block): only that representative is partitioned (marked multi), the others are
+// marked kNfDup with the representative's position in their word (k_flagscan_node then
+// points them at the key's first occurrence).  Hot keys -- tandem repeats -- thus reach the
+// buckets once per block instead of once per occurrence.
+constexpr u32 kColBlock = 4096;   // pairs per collapse block (4 of them per part chunk)
+constexpr u32 kColSlots = 8192;   // its LDS table (load <= 1/2), in the part's staging area
+
 [[maybe_unused]] static __global__ __launch_bounds__(kBktThreads) void k_bkt_part(
     const u32* __restrict__ in, u64 n, u64 p, const unsigned char* __restrict__ prev_nf,
     const unsigned char* __restrict__ prev_multi, Bkt2Plan bp, u64* __restrict__ seg, u32* __restrict__ rt,
-    u32* __restrict__ rec, Header* __restrict__ hdr, const u64* prev_count, u64* __restrict__ stats) {
-  if (bkt_skip(hdr, prev_count, n)) return;
+    u32* __restrict__ rec, Marks mk, Header* __restrict__ hdr, const u64* prev_count, u64* __restrict__ stats) {
+  if (bkt2_skip(hdr, prev_count, n)) return;
   extern __shared__ u64 stage[];   // kPartChunk records (dynamic)
   __shared__ u32 cur[(1u << kPartMaxB1) + 1];
+  const bool collapse = hdr && hdr->predup != 0;
   const u32 nb1 = 1u << bp.b1;
   for (u32 q = threadIdx.x; q <= nb1; q += kBktThreads) cur[q] = 0;
+  // the block table lives in the staging area until the records are staged: block q's
+  // entries carry the tag q + 1 (a slot of another tag is free: no clearing): key | tag << 58
+  // (K <= 58 on this path), the earliest offset as tag << 16 | 0xffff - offset (atomicMax),
+  // the repeat flag as the tag
+  unsigned long long* s_ck = reinterpret_cast<unsigned long long*>(stage);
+  u32* s_cp = reinterpret_cast<u32*>(stage + kColSlots);
+  unsigned char* s_cd = reinterpret_cast<unsigned char*>(stage + kColSlots + kColSlots / 2);
+  if (collapse)
+    for (u32 q = threadIdx.x; q < kColSlots + kColSlots / 2 + kColSlots / 8; q += kBktThreads) stage[q] = 0;
   __syncthreads();
   const u64 g = bkt_chunk(bp.G), j0 = g * kPartChunk;
   const u32 sh1 = bp.K - bp.b1;
@@ -1511,20 +1551,105 @@ __device__ __forceinline__ void lds_excl256(u32* c, u32 n) {
   u64 r[kPartItems];
   u32 slot[kPartItems];   // coarse bucket << 16 | rank in it; ~0: not hashed
   u32 hashed = 0;
+  auto place = [&](int e, u64 j, u64 key) {   // the record of a hashed pair into its coarse run
+    const u32 c = bp.b1 ? u32(key >> sh1) : 0u;
+    r[e] = ((key & lowmask) << kPartLog) | (j - j0);
+    slot[e] = (c << 16) | atomicAdd(&cur[c], 1u);
+    ++hashed;
+  };
+  if (!collapse) {
 #pragma unroll
-  for (int e = 0; e < kPartItems; ++e) {
-    const u64 j = j0 + u64(e) * kBktThreads + threadIdx.x;
-    slot[e] = ~0u;
-    if (j >= p) continue;
-    u64 key;
-    u32 bits;
-    if (bkt_pair(in, n, j, prev_nf, prev_multi, kp, key, bits)) {
-      const u32 c = bp.b1 ? u32(key >> sh1) : 0u;
-      r[e] = ((key & lowmask) << kPartLog) | (j - j0);
-      slot[e] = (c << 16) | atomicAdd(&cur[c], 1u);
-      ++hashed;
+    for (int e = 0; e < kPartItems; ++e) {
+      const u64 j = j0 + u64(e) * kBktThreads + threadIdx.x;
+      slot[e] = ~0u;
+      if (j >= p) continue;
+      u64 key;
+      u32 bits;
+      if (bkt_pair(in, n, j, prev_nf, prev_multi, kp, key, bits)) place(e, j, key);
+      rec[j] = bits;
     }
-    rec[j] = bits;
+  } else {
+    // each block's repeats onto its earliest occurrence of the key; the next block's pairs
+    // are loaded while this block hashes in LDS
+    constexpr int BI = kColBlock / kBktThreads;   // items per block
+    u64 kn[BI];
+    u32 bn[BI];
+    bool hn[BI];
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const u64 j = j0 + u64(i) * kBktThreads + threadIdx.x;
+      kn[i] = 0;
+      bn[i] = 0;
+      hn[i] = j < p && bkt_pair(in, n, j, prev_nf, prev_multi, kp, kn[i], bn[i]);
+    }
+#pragma unroll
+    for (int q = 0; q < kPartItems / BI; ++q) {
+      u64 key[BI];
+      u32 bits[BI], cs[BI];
+      bool h[BI];
+#pragma unroll
+      for (int i = 0; i < BI; ++i) {
+        key[i] = kn[i];
+        bits[i] = bn[i];
+        h[i] = hn[i];
+      }
+      if (q + 1 < kPartItems / BI)
+#pragma unroll
+        for (int i = 0; i < BI; ++i) {
+          const u64 j = j0 + u64((q + 1) * BI + i) * kBktThreads + threadIdx.x;
+          kn[i] = 0;
+          bn[i] = 0;
+          hn[i] = j < p && bkt_pair(in, n, j, prev_nf, prev_multi, kp, kn[i], bn[i]);
+        }
+      const u64 tag = u64(q + 1);
+#pragma unroll
+      for (int i = 0; i < BI; ++i) {   // claim (or find) the key's slot, the earliest offset, the flag
+        cs[i] = 0;
+        if (!h[i]) continue;
+        const u64 mk2 = (tag << 58) | key[i];
+        const u32 off = u32(i) * kBktThreads + threadIdx.x;
+        u32 s2 = u32((u64(u32(bkt_hash(key[i]))) * kColSlots) >> 32);
+        bool several = false;
+        for (;;) {
+          unsigned long long cv = s_ck[s2];
+          if ((cv >> 58) != tag) {   // free in this block: claim it
+            const unsigned long long old = atomicCAS(&s_ck[s2], cv, (unsigned long long)mk2);
+            if (old == cv) break;
+            cv = old;
+            if ((cv >> 58) != tag) continue;
+          }
+          if (cv == mk2) {
+            several = true;
+            break;
+          }
+          s2 = s2 + 1 == kColSlots ? 0u : s2 + 1;
+        }
+        if (several) s_cd[s2] = (unsigned char)tag;
+        atomicMax(&s_cp[s2], (u32(tag) << 16) | (0xffffu - off));
+        cs[i] = s2;
+      }
+      lds_sync();
+#pragma unroll
+      for (int i = 0; i < BI; ++i) {
+        const int e = q * BI + i;
+        const u64 j = j0 + u64(e) * kBktThreads + threadIdx.x;
+        slot[e] = ~0u;
+        bool dup = false;
+        if (h[i] && s_cd[cs[i]] == (unsigned char)tag) {
+          const u32 rep = u32(j0 + u64(q * BI) * kBktThreads) + (0xffffu - (s_cp[cs[i]] & 0xffffu));
+          if (rep != u32(j)) {   // collapsed: not partitioned
+            mk.nf[j] = kNfDup;
+            rec[j] = rep | bits[i];
+            dup = true;
+          } else {
+            mk.multi[j] = 1;
+          }
+        }
+        if (h[i] && !dup) place(e, j, key[i]);
+        if (j < p && !dup) rec[j] = bits[i];
+      }
+      lds_sync();   // (the next block's tag overwrites these slots; its pairs' loads stay in flight)
+    }
   }
   __syncthreads();
   lds_excl256(cur, nb1);
@@ -1548,7 +1673,7 @@ __device__ __forceinline__ void lds_excl256(u32* c, u32 n) {
 [[maybe_unused]] static __global__ __launch_bounds__(kBktThreads) void k_bkt_fine(
     const u64* __restrict__ seg, const u32* __restrict__ rt, Bkt2Plan bp, u64* __restrict__ out,
     u32* __restrict__ fo, Header* __restrict__ hdr, const u64* prev_count, u64 n, u32* __restrict__ ovf) {
-  if (bkt_skip(hdr, prev_count, n)) return;
+  if (bkt2_skip(hdr, prev_count, n)) return;
   extern __shared__ u64 stage[];   // kFineCap records (dynamic)
   __shared__ u32 s_pre[129], s_beg[128];   // runs of the slice's chunks (SC <= 128)
   __shared__ u32 s_w[2];
@@ -1628,7 +1753,7 @@ template <bool kOwner>
 __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
     const u64* __restrict__ recs, const u32* __restrict__ fo, Bkt2Plan bp, u32* __restrict__ rec, Marks mk,
     Header* __restrict__ hdr, const u64* prev_count, u64 n, u32* __restrict__ ovf) {
-  if (bkt_skip(hdr, prev_count, n)) return;
+  if (bkt2_skip(hdr, prev_count, n)) return;
   constexpr u32 TS = kBktSlots;
   __shared__ u64 s_key[TS];
   __shared__ u32 s_pos[TS];
@@ -1667,11 +1792,83 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
   for (u32 q = threadIdx.x; q < TS / 32; q += kBktThreads) s_dup[q] = 0;
   __syncthreads();
   const u32 total = s_pre[ns];
-  if (total > u32(kBktCap)) {   // a hot key: the table path handles this data
-    if (threadIdx.x == 0) *ovf = 1;
+  const u64 pmask = (1ull << bp.P) - 1;
+  auto record = [&](u32 i, u64& key, u32& pos) {   // record i of the bucket: its key bits and position
+    u32 lo = 0, hi = ns - 1;   // slice of record i: the last s with s_pre[s] <= i
+    while (lo < hi) {
+      const u32 mid = (lo + hi + 1) >> 1;
+      if (s_pre[mid] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    const u64 v = recs[u64(c * ns + lo) * kFineCap + s_beg[lo] + (i - s_pre[lo])];
+    key = v >> bp.P;
+    pos = u32(u64(lo) * bp.SC * kPartChunk + (v & pmask));
+  };
+  if (total > u32(kBktCap)) {
+    // More records than registers hold (hot keys: repeats beyond the block collapse): the
+    // same three steps in passes over the records, the LDS table kept across them.  Only
+    // more distinct keys than the table holds overflow (the host rebuilds with the table).
+    __shared__ u32 s_full;
+    if (threadIdx.x == 0) s_full = 0;
+    __syncthreads();
+    auto find = [&](u64 key, bool insert) -> u32 {   // slot of key (inserting), ~0 when full
+      u32 h = u32((u64(u32(bkt_hash(key))) * TS) >> 32);
+      for (u32 probe = 0; probe < TS; ++probe) {
+        unsigned long long cv = s_key[h];
+        if (cv == kEmpty && insert) cv = atomicCAS(&s_key[h], kEmpty, (unsigned long long)key);
+        if (cv == key) {
+          if (insert) atomicOr(&s_dup[h >> 5], 1u << (h & 31));
+          return h;
+        }
+        if (cv == kEmpty) return h;
+        h = h + 1 == TS ? 0u : h + 1;
+      }
+      return ~0u;
+    };
+    const u32 wlane = threadIdx.x & 63u;   // (every lane of a wave runs the same passes)
+    for (u32 i = threadIdx.x; i - wlane < total; i += kBktThreads) {
+      const bool act = i < total;
+      u64 key = kEmpty;
+      u32 pos = 0, sl = 0;
+      if (act) record(i, key, pos);
+      if (act) sl = find(key, true);
+      if (act && sl == ~0u) s_full = 1;
+    }
+    __syncthreads();
+    if (s_full) {
+      if (threadIdx.x == 0) *ovf = 1;
+      return;
+    }
+    for (int pass = 0; pass < 2; ++pass) {   // 0: first positions of repeated keys, 1: the marks
+      for (u32 i = threadIdx.x; i - wlane < total; i += kBktThreads) {
+        const bool act = i < total;
+        u64 key = kEmpty;
+        u32 pos = 0, sl = 0;
+        if (act) {
+          record(i, key, pos);
+          sl = find(key, false);
+        }
+        const bool dup = act && ((s_dup[sl >> 5] >> (sl & 31)) & 1u);
+        if (pass == 0) {
+          if (dup) atomicMin(&s_pos[sl], pos);
+          continue;
+        }
+        if (!dup) continue;
+        const u32 first = s_pos[sl];
+        if constexpr (kOwner) {
+          rec[pos] = first;
+          mk.nf[pos] = pos != first ? 7 : 6;
+        } else if (pos != first) {
+          mk.nf[pos] = kNfNot;
+          rec[pos] = first | (rec[pos] & kBits);
+        } else {
+          mk.multi[pos] = 1;
+        }
+      }
+      __syncthreads();
+    }
     return;
   }
-  const u64 pmask = (1ull << bp.P) - 1;
   u64 key[kBktCapItems];
   u32 pos[kBktCapItems], slot[kBktCapItems];
 #pragma unroll
@@ -1689,25 +1886,27 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
     key[e] = v >> bp.P;
     pos[e] = u32(u64(lo) * bp.SC * kPartChunk + (v & pmask));
   }
-#pragma unroll
-  for (int e = 0; e < kBktCapItems; ++e) {
-    if (key[e] == kEmpty) continue;
-    u32 h = u32((u64(u32(bkt_hash(key[e]))) * TS) >> 32);
+  auto insert = [&](u64 k, bool several) -> u32 {   // slot of k; a second holder sets its repeat bit
+    u32 h = u32((u64(u32(bkt_hash(k))) * TS) >> 32);
     for (;;) {
       unsigned long long cv = s_key[h];
-      if (cv == kEmpty) cv = atomicCAS(&s_key[h], kEmpty, (unsigned long long)key[e]);
-      if (cv == key[e]) atomicOr(&s_dup[h >> 5], 1u << (h & 31));   // another position holds it
-      if (cv == kEmpty || cv == key[e]) break;
+      if (cv == kEmpty) cv = atomicCAS(&s_key[h], kEmpty, (unsigned long long)k);
+      if (cv == k) several = true;   // another position holds it
+      if (cv == kEmpty || cv == k) break;
       h = h + 1 == TS ? 0u : h + 1;
     }
-    slot[e] = h;
+    if (several) atomicOr(&s_dup[h >> 5], 1u << (h & 31));
+    return h;
+  };
+#pragma unroll
+  for (int e = 0; e < kBktCapItems; ++e) {
+    slot[e] = 0;
+    if (key[e] != kEmpty) slot[e] = insert(key[e], false);
   }
   __syncthreads();
 #pragma unroll
-  for (int e = 0; e < kBktCapItems; ++e) {
-    if (key[e] == kEmpty || !((s_dup[slot[e] >> 5] >> (slot[e] & 31)) & 1u)) continue;
-    atomicMin(&s_pos[slot[e]], pos[e]);
-  }
+  for (int e = 0; e < kBktCapItems; ++e)
+    if (key[e] != kEmpty && ((s_dup[slot[e] >> 5] >> (slot[e] & 31)) & 1u)) atomicMin(&s_pos[slot[e]], pos[e]);
   __syncthreads();
 #pragma unroll
   for (int e = 0; e < kBktCapItems; ++e) {
@@ -2018,7 +2217,7 @@ __device__ unsigned long long gcz_tail_probe[64];
                                                  uint4* __restrict__ multi, u64 p16, const u64* prev_count,
                                                  u64 prev_n, const Header* __restrict__ hdr, u32 bkt) {
   if (level_direct(prev_count, prev_n)) return;
-  if (bkt && hdr->predup == 0) tab16 = 0;   // bucketed insert: no table
+  if (bkt == 2 || (bkt && hdr->predup == 0)) tab16 = 0;   // bucketed insert: no table
   const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u), zero = make_uint4(0, 0, 0, 0);
   const u64 stride = u64(gridDim.x) * kBlock;
   for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < tab16; i += stride) tab[i] = ones;

@@ -44,6 +44,19 @@ def ctx_bucket(gcz):
 
 
 @pytest.fixture(scope="module")
+def ctx_bucket_rep(gcz):
+    """The two-pass bucketed insert on every hashed level with the repetitive-data block
+    collapse forced on (k_bkt_part: repeats inside 1024-pair blocks collapse, kNfDup)."""
+    os.environ.update({"GCZ_BUCKET_MIN": "1", "GCZ_PREDUP": "1"})
+    try:
+        c = gcz.Context(0)
+    finally:
+        del os.environ["GCZ_BUCKET_MIN"], os.environ["GCZ_PREDUP"]
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
 def ctx_dense(gcz):
     """A context that runs the dense leaf level (gcz_dense.h) at every size."""
     os.environ["GCZ_DENSE"] = "2"
@@ -75,6 +88,31 @@ def test_gpu_bucketed_insert_goldens(name, ctx_bucket, gcz, manifest):
     kind, payload, L = case_input(case, gcz)
     _build(ctx_bucket, kind, payload, L)
     assert compare_digest(gcz.digest(ctx_bucket.tree()), case["expect"]) == {}
+
+
+@pytest.mark.parametrize("name", [n for n in _names(12_000_000) if not n.startswith("fasta/")])
+def test_gpu_bucketed_collapse_goldens(name, ctx_bucket_rep, gcz, manifest):
+    case = manifest[name]
+    kind, payload, L = case_input(case, gcz)
+    info = _build(ctx_bucket_rep, kind, payload, L)
+    assert compare_digest(gcz.digest(ctx_bucket_rep.tree()), case["expect"]) == {}
+    if info["hashed_pairs"]:
+        assert info["attempts"] == 1   # (no bucket overflow: hot keys collapse, big buckets loop)
+
+
+def test_gpu_bucketed_collapse_random(ctx_bucket_rep, gcz, oracle):
+    """Block collapse + looping dedupe on random leaf mixes from all-unique to a few hot keys
+    (the hot keys fill buckets far beyond the register batch), against the oracle."""
+    rng = np.random.default_rng(13)
+    for S, pool_div in [(5, 1), (4097, 1), (100_003, 7), (300_001, 50_000), (400_000, 200_000),
+                        (262_144, 4), (1_000_003, 333_334)]:
+        pool = rng.integers(0, 1 << 48, size=max(4, S // pool_div), dtype=np.uint64)
+        leaves = pool[rng.integers(0, pool.size, size=S)]
+        ctx_bucket_rep.build_leaves(leaves, 12)
+        g = ctx_bucket_rep.tree()
+        o = oracle.build_leaves(leaves, 12)
+        assert g.leaves_bin() == o.leaves_bin(), S
+        assert g.layers_bin() == o.layers_bin(), S
 
 
 @pytest.mark.parametrize("name", _names(12_000_000))
