@@ -23,6 +23,38 @@ constexpr u64 kScanTile = u64(kScanThreads) * kScanItems;   // 16 Ki elements (a
 
 __host__ __device__ inline u64 scan_tiles(u64 n) { return (n + kScanTile - 1) / kScanTile; }
 
+// Look-back of tile `tile` (taken in ticket order) whose own sum is agg, run by one whole
+// wave: publishes the aggregate, adds up the predecessors' values until an inclusive
+// prefix, publishes its own and returns the exclusive prefix (the same in every lane).
+__device__ __forceinline__ u64 tile_lookback(u64* __restrict__ desc, u64 tile, u64 agg) {
+  const int lane = threadIdx.x & 63;
+  if (tile == 0) {
+    if (lane == 0) __hip_atomic_store(&desc[0], kStP | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (lane == 0) __hip_atomic_store(&desc[tile], kStA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  u64 prefix = 0;
+  long long look = (long long)tile - 1;
+  for (;;) {
+    const long long idx = look - lane;
+    const u64 d = idx >= 0 ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    const u64 st = d >> 62;
+    const u64 pm = __ballot(st == 2);
+    const u64 zm = __ballot(st == 0 && idx >= 0);
+    const int firstP = pm ? __ffsll((long long)pm) - 1 : 64;
+    const u64 need = firstP >= 63 ? ~0ull : ((1ull << (firstP + 1)) - 1);
+    if (zm & need) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    prefix += wave_sum(lane <= firstP && idx >= 0 ? (d & kValMask) : 0ull);
+    if (firstP < 64 || look - 64 < 0) break;
+    look -= 64;
+  }
+  if (lane == 0) __hip_atomic_store(&desc[tile], kStP | (prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return prefix;
+}
+
 // In: u32 operator()(u64 i) const for i < n.
 template <class In, class Out = u32>
 __global__ __launch_bounds__(kScanThreads) void k_scan_excl(In in, u64 n, Out* __restrict__ out,
@@ -65,32 +97,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_excl(In in, u64 n, Out* _
   if (wave == 0) {
     u32 agg = 0;
     for (int w = 0; w < kScanThreads / 64; ++w) agg += s_wave[w];
-    u64 prefix = 0;
-    if (tile == 0) {
-      if (lane == 0) __hip_atomic_store(&desc[0], kStP | u64(agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      if (lane == 0) __hip_atomic_store(&desc[tile], kStA | u64(agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      long long look = (long long)tile - 1;
-      for (;;) {
-        const long long idx = look - lane;
-        const u64 d =
-            idx >= 0 ? __hip_atomic_load(&desc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-        const u64 st = d >> 62;
-        const u64 pm = __ballot(st == 2);
-        const u64 zm = __ballot(st == 0 && idx >= 0);
-        const int firstP = pm ? __ffsll((long long)pm) - 1 : 64;
-        const u64 need = firstP >= 63 ? ~0ull : ((1ull << (firstP + 1)) - 1);
-        if (zm & need) {
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        prefix += wave_sum(lane <= firstP && idx >= 0 ? (d & kValMask) : 0ull);
-        if (firstP < 64 || look - 64 < 0) break;
-        look -= 64;
-      }
-      if (lane == 0)
-        __hip_atomic_store(&desc[tile], kStP | (prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    const u64 prefix = tile_lookback(desc, tile, agg);
     if (lane == 0) {
       s_prefix = prefix;
       if (total && (tile + 1) * kScanTile >= n) *total = prefix + agg;

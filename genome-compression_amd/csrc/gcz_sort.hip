@@ -28,19 +28,22 @@ using namespace gcz_dev;
 using namespace gcz_host;
 
 struct gcz_sort_state {
-  DevBuf cnt, keys, keys2, vals, vals2, newpos, mm, tmp, sizes, pos, acc, dag, nodes2, leaves2, dw1, dw2, text;
+  DevBuf cnt, keys, keys2, vals, vals2, newpos, mm, acc, dag, nodes2, leaves2, dw1, dw2, text;
   DevBuf hmat, hoff, hrec, desc;   // partitioned histogram; scan descriptors
+  DevBuf hslot, hval, hbs;         // its records' positions per word, new children, bucket starts
   u32* h_mm = nullptr;
+  u64* h_tot = nullptr;
 };
 
 void gcz_sort_state_free(gcz_ctx* c) {
   gcz_sort_state* s = c->sortst;
   if (!s) return;
-  for (DevBuf* b : {&s->cnt, &s->keys, &s->keys2, &s->vals, &s->vals2, &s->newpos, &s->mm, &s->tmp, &s->sizes,
-                    &s->pos, &s->acc, &s->dag, &s->nodes2, &s->leaves2, &s->dw1, &s->dw2, &s->text, &s->hmat,
-                    &s->hoff, &s->hrec, &s->desc})
+  for (DevBuf* b : {&s->cnt, &s->keys, &s->keys2, &s->vals, &s->vals2, &s->newpos, &s->mm, &s->acc, &s->dag,
+                    &s->nodes2, &s->leaves2, &s->dw1, &s->dw2, &s->text, &s->hmat, &s->hoff, &s->hrec, &s->desc,
+                    &s->hslot, &s->hval, &s->hbs})
     if (b->ptr) (void)hipFree(b->ptr);
   if (s->h_mm) (void)hipHostFree(s->h_mm);
+  if (s->h_tot) (void)hipHostFree(s->h_tot);
   delete s;
   c->sortst = nullptr;
 }
@@ -76,20 +79,13 @@ __device__ __forceinline__ void put_be(unsigned char* o, u64 v, int nbytes) {   
   for (int i = nbytes - 1; i >= 0; --i) *o++ = (unsigned char)(v >> (8 * i));
 }
 
-// histogram (src/shared_tree.cpp:316-326): references of each child from the parent layer
-__global__ __launch_bounds__(kBlock) void k_hist(const u32* __restrict__ parent, u64 nwords, u32* __restrict__ cnt) {
-  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (i >= nwords) return;
-  const u32 w = parent[i];
-  if (!is_null(w)) atomicAdd(&cnt[w & kIdx], 1u);
-}
-
 // ---- partitioned histogram (parent layers of >= 2^20 words) ----
 // Buckets of 2^kHB child ids; chunks of kHChunk parent words (one count-matrix
 // column each, dealt to XCDs in contiguous runs like the build's bucket chunks).
 constexpr int kHThreads = 1024;
 constexpr int kHItems = 64;
 constexpr u64 kHChunk = u64(kHThreads) * kHItems;
+constexpr int kHBatch = 16;
 constexpr u32 kHB = 15;                 // ids per bucket: 2^15 (LDS counters, 128 KB)
 constexpr u32 kHMaxBuckets = 4096;      // child layers of <= 2^27 nodes (LDS cursors, 16 KB)
 
@@ -104,20 +100,26 @@ __global__ __launch_bounds__(kHThreads) void k_hcount(const u32* __restrict__ wo
   for (u32 q = threadIdx.x; q < nb; q += kHThreads) hist[q] = 0;
   __syncthreads();
   const u64 g = h_chunk(G), j0 = g * kHChunk;
-#pragma unroll 8
-  for (int e = 0; e < kHItems; ++e) {
-    const u64 j = j0 + u64(e) * kHThreads + threadIdx.x;
-    if (j >= nw) break;
-    const u32 w = words[j];
-    if (!is_null(w)) atomicAdd(&hist[(w & kIdx) >> kHB], 1u);
+  for (int e0 = 0; e0 < kHItems; e0 += kHBatch) {   // (a batch of loads in flight)
+    u32 wv[kHBatch];
+#pragma unroll
+    for (int e = 0; e < kHBatch; ++e) {
+      const u64 j = j0 + u64(e0 + e) * kHThreads + threadIdx.x;
+      wv[e] = j < nw ? words[j] : kIdx;
+    }
+#pragma unroll
+    for (int e = 0; e < kHBatch; ++e)
+      if (!is_null(wv[e])) atomicAdd(&hist[(wv[e] & kIdx) >> kHB], 1u);
   }
   __syncthreads();
   for (u32 q = threadIdx.x; q < nb; q += kHThreads) mat[u64(q) * G + g] = hist[q];
 }
 
+// slot != null: also each word's record position (the rewire reads its new child back
+// from there, k_hremap)
 __global__ __launch_bounds__(kHThreads) void k_hscatter(const u32* __restrict__ words, u64 nw, u32 nb, u64 G,
                                                         const u32* __restrict__ off,
-                                                        unsigned short* __restrict__ rec) {
+                                                        unsigned short* __restrict__ rec, u32* __restrict__ slot) {
   __shared__ u32 cur[kHMaxBuckets];
   const u64 g = h_chunk(G), j0 = g * kHChunk;
   for (u32 q = threadIdx.x; q < nb; q += kHThreads) cur[q] = off[u64(q) * G + g];
@@ -131,24 +133,107 @@ __global__ __launch_bounds__(kHThreads) void k_hscatter(const u32* __restrict__ 
     const u32 id = w & kIdx;
     const u32 d = atomicAdd(&cur[id >> kHB], 1u);
     rec[d] = (unsigned short)(id & ((1u << kHB) - 1));
+    if (slot) slot[j] = d;
   }
 }
 
-// One workgroup per bucket: LDS counters for its 2^kHB ids, written coalesced, and
-// the block's min / max folded into mm[0..1].
+// The same partition staged in LDS (buckets <= kHStagedMax): the chunk's records are
+// placed at their in-chunk rank (LDS cursors from the chunk's count column), then stored
+// as one contiguous run per bucket -- scattered 2-B stores become coalesced runs.
+constexpr u32 kHStagedMax = 2048;
+
+__global__ __launch_bounds__(kHThreads) void k_hscatter_lds(const u32* __restrict__ words, u64 nw, u32 nb, u64 G,
+                                                            const u32* __restrict__ mat, const u32* __restrict__ off,
+                                                            unsigned short* __restrict__ rec,
+                                                            u32* __restrict__ slot) {
+  __shared__ u32 s_cur[kHStagedMax];     // in-chunk starts, then cursors, then ends
+  __shared__ u32 s_delta[kHStagedMax];   // global start - in-chunk start, per bucket
+  __shared__ u32 s_wave[kHThreads / 64];
+  __shared__ unsigned short s_rec[kHChunk];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const u64 g = h_chunk(G), j0 = g * kHChunk;
+  // exclusive scan of the chunk's bucket counts (two per thread: nb <= 2048)
+  const u32 q0 = 2 * tid;
+  const u32 c0 = q0 < nb ? mat[u64(q0) * G + g] : 0u, c1 = q0 + 1 < nb ? mat[u64(q0 + 1) * G + g] : 0u;
+  const u32 o0 = q0 < nb ? off[u64(q0) * G + g] : 0u, o1 = q0 + 1 < nb ? off[u64(q0 + 1) * G + g] : 0u;
+  u32 incl = c0 + c1;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u32 y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) s_wave[wave] = incl;
+  __syncthreads();
+  u32 base = 0;
+  for (int w = 0; w < wave; ++w) base += s_wave[w];
+  const u32 st0 = base + incl - (c0 + c1), st1 = st0 + c0;
+  if (q0 < nb) { s_cur[q0] = st0; s_delta[q0] = o0 - st0; }
+  if (q0 + 1 < nb) { s_cur[q0 + 1] = st1; s_delta[q0 + 1] = o1 - st1; }
+  __syncthreads();
+  for (int e0 = 0; e0 < kHItems; e0 += kHBatch) {   // (a batch of loads in flight)
+    u32 wv[kHBatch];
+#pragma unroll
+    for (int e = 0; e < kHBatch; ++e) {
+      const u64 j = j0 + u64(e0 + e) * kHThreads + tid;
+      wv[e] = j < nw ? words[j] : kIdx;
+    }
+#pragma unroll
+    for (int e = 0; e < kHBatch; ++e) {
+      if (is_null(wv[e])) continue;
+      const u64 j = j0 + u64(e0 + e) * kHThreads + tid;
+      const u32 id = wv[e] & kIdx, q = id >> kHB;
+      const u32 d = atomicAdd(&s_cur[q], 1u);
+      s_rec[d] = (unsigned short)(id & ((1u << kHB) - 1));
+      if (slot) slot[j] = s_delta[q] + d;
+    }
+  }
+  __syncthreads();
+  // s_cur[q] is now bucket q's in-chunk end: record i belongs to the first q with end > i
+  const u32 nrec = s_cur[nb - 1];
+  for (u32 i = tid; i < nrec; i += kHThreads) {
+    u32 lo = 0, hi = nb - 1;
+    while (lo < hi) {
+      const u32 mid = (lo + hi) >> 1;
+      if (s_cur[mid] > i) hi = mid;
+      else lo = mid + 1;
+    }
+    rec[s_delta[lo] + i] = s_rec[i];
+  }
+}
+
+// S workgroups per bucket, each counting a slice of its records in LDS counters for the
+// bucket's 2^kHB ids.  S = 1: the counters are written coalesced and the block's min / max
+// folded into mm[0..1]; S > 1: added into cnt (zeroed) with coalesced atomics (the layer's
+// min / max taken afterwards).
 __global__ __launch_bounds__(kHThreads) void k_hbucket(const unsigned short* __restrict__ rec,
-                                                       const u32* __restrict__ off, u64 G, u64 nc,
-                                                       u32* __restrict__ cnt, u32* __restrict__ mm) {
+                                                       const u32* __restrict__ off, u64 G, u64 nc, u32 S,
+                                                       u32* __restrict__ cnt, u32* __restrict__ mm,
+                                                       u32* __restrict__ bstart) {
   extern __shared__ u32 c32[];   // 2^kHB counters (dynamic: 128 KB)
   __shared__ u32 smin[kHThreads / 64], smax[kHThreads / 64];
-  const u64 b = blockIdx.x;
+  const u64 b = blockIdx.x / S;
+  const u32 sub = blockIdx.x % S;
   for (u32 q = threadIdx.x; q < (1u << kHB); q += kHThreads) c32[q] = 0;
   __syncthreads();
   const u32 r0 = off[b * G], r1 = off[(b + 1) * G];
-  for (u32 i = r0 + threadIdx.x; i < r1; i += kHThreads) atomicAdd(&c32[rec[i]], 1u);
+  if (bstart && sub == 0 && threadIdx.x == 0) {   // (the records' bucket boundaries, kept for k_hremap)
+    bstart[b] = r0;
+    if (b + 1 == gridDim.x / S) bstart[b + 1] = r1;
+  }
+  const u32 len = r1 - r0;
+  const u32 s0 = r0 + u32(u64(len) * sub / S), s1 = r0 + u32(u64(len) * (sub + 1) / S);
+  for (u32 i = s0 + threadIdx.x; i < s1; i += kHThreads) atomicAdd(&c32[rec[i]], 1u);
   __syncthreads();
-  u32 lo = ~0u, hi = 0;
   const u64 id0 = b << kHB;
+  if (S > 1) {
+    for (u32 q = threadIdx.x; q < (1u << kHB); q += kHThreads) {
+      if (id0 + q >= nc) break;
+      const u32 v = c32[q];
+      if (v) atomicAdd(&cnt[id0 + q], v);
+    }
+    return;
+  }
+  u32 lo = ~0u, hi = 0;
   for (u32 q = threadIdx.x; q < (1u << kHB); q += kHThreads) {
     if (id0 + q >= nc) break;
     const u32 v = c32[q];
@@ -168,6 +253,23 @@ __global__ __launch_bounds__(kHThreads) void k_hbucket(const unsigned short* __r
     atomicMin(&mm[0], lo);
     atomicMax(&mm[1], hi);
   }
+}
+
+// The partitioned layer's new child positions in record order: one workgroup per bucket
+// with the bucket's 2^kHB new positions in LDS (a random gather into the whole newpos
+// array becomes an LDS lookup; the rewire then reads val[slot[j]], whose records for a
+// chunk of words sit in one short run per bucket).
+__global__ __launch_bounds__(kHThreads) void k_hremap(const unsigned short* __restrict__ rec,
+                                                      const u32* __restrict__ bstart, const u32* __restrict__ np,
+                                                      u64 nc, u32 S, u32* __restrict__ val) {
+  extern __shared__ u32 tab[];   // 2^kHB new positions (dynamic: 128 KB)
+  const u64 b = blockIdx.x / S, id0 = b << kHB;
+  const u32 sub = blockIdx.x % S;
+  for (u32 q = threadIdx.x; q < (1u << kHB); q += kHThreads) tab[q] = id0 + q < nc ? np[id0 + q] : 0u;
+  __syncthreads();
+  const u32 r0 = bstart[b], len = bstart[b + 1] - r0;
+  const u32 s0 = r0 + u32(u64(len) * sub / S), s1 = r0 + u32(u64(len) * (sub + 1) / S);
+  for (u32 i = s0 + threadIdx.x; i < s1; i += kHThreads) val[i] = tab[rec[i]];
 }
 
 // ---- stable counting sort by count, descending (LSD passes of <= 8 bits) ----
@@ -258,28 +360,6 @@ __global__ __launch_bounds__(kCsThreads) void k_cs_scatter(CsPass P, u64 ntiles,
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_minmax(const u32* __restrict__ cnt, u64 n, u32* __restrict__ mm) {
-  __shared__ u32 smin[kBlock / 64], smax[kBlock / 64];
-  u32 lo = ~0u, hi = 0;
-  for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < n; i += u64(gridDim.x) * kBlock) {
-    const u32 c = cnt[i];
-    lo = min(lo, c);
-    hi = max(hi, c);
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    lo = min(lo, u32(__shfl_xor(int(lo), o, 64)));
-    hi = max(hi, u32(__shfl_xor(int(hi), o, 64)));
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) { smin[wave] = lo; smax[wave] = hi; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < kBlock / 64; ++w) { lo = min(lo, smin[w]); hi = max(hi, smax[w]); }
-    atomicMin(&mm[0], lo);
-    atomicMax(&mm[1], hi);
-  }
-}
-
 __global__ void k_mm_init(u32* mm, int D) {
   for (int i = threadIdx.x; i < D; i += blockDim.x) { mm[2 * i] = ~0u; mm[2 * i + 1] = 0u; }
 }
@@ -290,30 +370,162 @@ __global__ __launch_bounds__(kBlock) void k_perm_leaves(const u64* __restrict__ 
   if (i < n) out[newpos[i]] = in[i];
 }
 
-// rewire_nodes (:383-403) with the child permutation and reorder_layer (:371-377) with
-// the own one, for every node layer in one launch (storage slot g of layer k).
-struct PermPlan {
-  u64 node[GCZ_MAX_LAYERS + 1];     // storage start of each layer (+ the end)
-  u64 count[GCZ_MAX_LAYERS];
-  long long child[GCZ_MAX_LAYERS];  // offset of the child layer's newpos, -1: identity
-  long long own[GCZ_MAX_LAYERS];    // offset of the layer's own newpos, -1: identity
+// ---- multi-layer launches: entry e of a plan owns blocks [b0[e], b0[e + 1]) ----
+struct RangePlan {
+  u64 lo[GCZ_MAX_LAYERS];    // first element of the entry's range
+  u64 n[GCZ_MAX_LAYERS];     // its elements
+  u64 aux[GCZ_MAX_LAYERS];   // counters' offset (hist) / layer (min-max)
+  u32 b0[GCZ_MAX_LAYERS + 1];
+  int m;
 };
 
-__global__ __launch_bounds__(kBlock) void k_perm_nodes(const uint2* __restrict__ in, u64 N, int D, PermPlan pp,
-                                                       const u32* __restrict__ newpos, uint2* __restrict__ out) {
-  const u64 g = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (g >= N) return;
-  int k = 0;
-  while (k + 1 < D && g >= pp.node[k + 1]) ++k;
-  const u64 i = g - pp.node[k];
-  if (i >= pp.count[k]) return;
-  uint2 w = in[g];
-  if (pp.child[k] >= 0) {
-    const u32* cn = newpos + pp.child[k];
-    if (!is_null(w.x)) w.x = (w.x & kBits) | cn[w.x & kIdx];
-    if (!is_null(w.y)) w.y = (w.y & kBits) | cn[w.y & kIdx];
+__device__ __forceinline__ int plan_entry(const RangePlan& p) {
+  int e = 0;
+  while (e + 1 < p.m && blockIdx.x >= p.b0[e + 1]) ++e;
+  return e;
+}
+
+// counters of the listed child layers to zero: cnt[lo, lo + n)
+__global__ __launch_bounds__(kBlock) void k_zero_ranges(RangePlan p, u32* __restrict__ cnt) {
+  const int e = plan_entry(p);
+  const u64 nb = p.b0[e + 1] - p.b0[e];
+  for (u64 i = (blockIdx.x - p.b0[e]) * u64(kBlock) + threadIdx.x; i < p.n[e]; i += nb * kBlock) cnt[p.lo[e] + i] = 0;
+}
+
+// pointer::serialize of w as a little-endian word of its bytes in output order, and
+// their count: the pointer's value (seg | t | m | offset) is written big-endian
+__device__ __forceinline__ u64 ptr_le(u32 w, u32& nbytes) {
+  const u32 idx = w & kIdx;
+  u32 seg, off;
+  if (idx == kIdx) { seg = 3; off = 0xfffffffu; }
+  else if (idx < kSegStart1) { seg = 0; off = idx; }
+  else if (idx < kSegStart2) { seg = 1; off = idx - kSegStart1; }
+  else if (idx < kSegStart3) { seg = 2; off = idx - kSegStart2; }
+  else { seg = 3; off = idx - kSegStart3; }
+  const u32 top = 8 * seg;
+  const u32 v = off | (((w >> 29) & 1u) << (top + 4)) | (((w >> 30) & 1u) << (top + 5)) | (seg << (top + 6));
+  nbytes = seg + 1;
+  return u64(__builtin_bswap32(v) >> (8 * (3 - seg)));
+}
+
+// len <= 8 bytes of v (first byte lowest) at byte o of a zeroed LDS buffer: ORed into its
+// aligned words, so neighbours that share a word need no ordering
+__device__ __forceinline__ void lds_emit(u32* __restrict__ buf, u32 o, u64 v, u32 len) {
+  const u32 r = o & 3, w0 = o >> 2;
+  atomicOr(&buf[w0], u32(v << (8 * r)));
+  if (r + len > 4) atomicOr(&buf[w0 + 1], u32(v >> (32 - 8 * r)));
+  if (r + len > 8) atomicOr(&buf[w0 + 2], u32(v >> (64 - 8 * r)));
+}
+
+// histogram (src/shared_tree.cpp:316-326) of the listed parent layers: words [lo, lo + n)
+// counted into cnt + aux (their references come in near id order: global atomics coalesce)
+__global__ __launch_bounds__(kBlock) void k_hist_ranges(RangePlan p, const u32* __restrict__ words,
+                                                        u32* __restrict__ cnt) {
+  const int e = plan_entry(p);
+  const u64 nb = p.b0[e + 1] - p.b0[e];
+  u32* c = cnt + p.aux[e];
+  for (u64 i = (blockIdx.x - p.b0[e]) * u64(kBlock) + threadIdx.x; i < p.n[e]; i += nb * kBlock) {
+    const u32 w = words[p.lo[e] + i];
+    if (!is_null(w)) atomicAdd(&c[w & kIdx], 1u);
   }
-  out[pp.node[k] + (pp.own[k] >= 0 ? newpos[pp.own[k] + i] : i)] = w;
+}
+
+// min / max count of the listed child layers: cnt[lo, lo + n) into mm[2 aux, 2 aux + 1]
+__global__ __launch_bounds__(kBlock) void k_minmax_ranges(RangePlan p, const u32* __restrict__ cnt,
+                                                          u32* __restrict__ mm) {
+  __shared__ u32 smin[kBlock / 64], smax[kBlock / 64];
+  const int e = plan_entry(p);
+  const u64 nb = p.b0[e + 1] - p.b0[e];
+  u32 lo = ~0u, hi = 0;
+  for (u64 i = (blockIdx.x - p.b0[e]) * u64(kBlock) + threadIdx.x; i < p.n[e]; i += nb * kBlock) {
+    const u32 v = cnt[p.lo[e] + i];
+    lo = min(lo, v);
+    hi = max(hi, v);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, u32(__shfl_xor(int(lo), o, 64)));
+    hi = max(hi, u32(__shfl_xor(int(hi), o, 64)));
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) { smin[wave] = lo; smax[wave] = hi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kBlock / 64; ++w) { lo = min(lo, smin[w]); hi = max(hi, smax[w]); }
+    atomicMin(&mm[2 * p.aux[e]], lo);
+    atomicMax(&mm[2 * p.aux[e] + 1], hi);
+  }
+}
+
+// rewire_nodes (:383-403) with the child permutation and reorder_layer (:371-377) with
+// the own one, for the listed node layers in one launch.  A layer whose own order
+// stays is rewired in place (out == in); a permuted one goes to out at the same slots.
+struct PermPlan {
+  u64 node[GCZ_MAX_LAYERS];         // storage start of the entry's layer
+  u64 count[GCZ_MAX_LAYERS];        // its nodes
+  long long child[GCZ_MAX_LAYERS];  // offset of the child layer's newpos, -1: identity
+  long long own[GCZ_MAX_LAYERS];    // offset of the layer's own newpos, -1: identity
+  int via_slot[GCZ_MAX_LAYERS];     // children from val[slot[word]] (k_hremap) instead
+  u32 b0[GCZ_MAX_LAYERS + 1];
+  int m;
+};
+constexpr int kPermItems = 4;
+
+__global__ __launch_bounds__(kBlock) void k_perm_nodes(const uint2* in, PermPlan pp, const u32* __restrict__ newpos,
+                                                       const u32* __restrict__ slot, const u32* __restrict__ val,
+                                                       uint2* inplace_or_out, uint2* out_perm) {
+  int e = 0;
+  while (e + 1 < pp.m && blockIdx.x >= pp.b0[e + 1]) ++e;
+  // a layer's blocks dealt to the XCDs in contiguous runs (the val runs a chunk of words
+  // reads stay in one L2)
+  const u32 nbk = pp.b0[e + 1] - pp.b0[e], lb = blockIdx.x - pp.b0[e], per = nbk / 8;
+  const u32 blk = lb < 8 * per ? (lb % 8) * per + lb / 8 : lb;
+  const u64 i0 = u64(blk) * (kBlock * kPermItems) + threadIdx.x;
+  const u64 node = pp.node[e], count = pp.count[e];
+  const long long child = pp.child[e], own = pp.own[e];
+  uint2 w[kPermItems];
+#pragma unroll
+  for (int q = 0; q < kPermItems; ++q) {
+    const u64 i = i0 + u64(q) * kBlock;
+    if (i < count) w[q] = in[node + i];
+  }
+  if (pp.via_slot[e]) {
+    u32 nx[kPermItems], ny[kPermItems];
+#pragma unroll
+    for (int q = 0; q < kPermItems; ++q) {
+      const u64 i = i0 + u64(q) * kBlock;
+      uint2 sl = make_uint2(0u, 0u);
+      if (i < count) sl = reinterpret_cast<const uint2*>(slot)[i];
+      nx[q] = i < count && !is_null(w[q].x) ? val[sl.x] : 0u;
+      ny[q] = i < count && !is_null(w[q].y) ? val[sl.y] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < kPermItems; ++q) {
+      if (!is_null(w[q].x)) w[q].x = (w[q].x & kBits) | nx[q];
+      if (!is_null(w[q].y)) w[q].y = (w[q].y & kBits) | ny[q];
+    }
+  } else if (child >= 0) {
+    const u32* cn = newpos + child;
+    u32 nx[kPermItems], ny[kPermItems];
+#pragma unroll
+    for (int q = 0; q < kPermItems; ++q) {   // every gather in flight before the first use
+      const u64 i = i0 + u64(q) * kBlock;
+      const bool ok = i < count;
+      nx[q] = ok && !is_null(w[q].x) ? cn[w[q].x & kIdx] : 0u;
+      ny[q] = ok && !is_null(w[q].y) ? cn[w[q].y & kIdx] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < kPermItems; ++q) {
+      if (!is_null(w[q].x)) w[q].x = (w[q].x & kBits) | nx[q];
+      if (!is_null(w[q].y)) w[q].y = (w[q].y & kBits) | ny[q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kPermItems; ++q) {
+    const u64 i = i0 + u64(q) * kBlock;
+    if (i >= count) continue;
+    if (own >= 0) out_perm[node + newpos[own + i]] = w[q];
+    else inplace_or_out[node + i] = w[q];
+  }
 }
 
 struct LayerStarts {
@@ -321,65 +533,225 @@ struct LayerStarts {
   u64 count[GCZ_MAX_LAYERS];      // nodes of each layer (storage holds ceil(n/2) slots, count <= that)
 };
 
-__device__ __forceinline__ int layer_of(const LayerStarts& ls, int D, u64 g) {
+// ---- bytes() and the .dag node section ----
+// Tiles of kDagTile storage slots, element e * kDagThreads + tid of a tile per thread
+// (coalesced 8-B loads); the tile's first layer is found once, each element steps on
+// from it.  A slot's size is its two pointers' bytes (0 past its layer's node count)
+// plus 8 for every layer count that is written right before it (the slot that starts
+// the layer).
+constexpr int kDagThreads = 256;
+constexpr int kDagItems = 8;
+constexpr u64 kDagTile = u64(kDagThreads) * kDagItems;       // 2 Ki slots (several workgroups per CU)
+constexpr int kDagGroups = kDagItems * (kDagThreads / 64);   // 64-slot groups of a tile
+constexpr int kDagPer = (kDagGroups + 63) / 64;              // groups per lane of the scanning wave
+constexpr u32 kDagBuf = (u32(kDagTile) * 8 + 8 * GCZ_MAX_LAYERS + 32 + 15) / 16 * 16;
+
+struct DagSlot {
+  uint2 w;
+  u32 meta;   // layer | layer counts written before it << 8 | a node (not padding) << 16
+  __device__ __forceinline__ int k() const { return int(meta & 0xff); }
+  __device__ __forceinline__ u32 nh() const { return (meta >> 8) & 0xff; }
+  __device__ __forceinline__ bool valid() const { return (meta >> 16) & 1u; }
+};
+
+__device__ __forceinline__ int tile_first_layer(const LayerStarts& ls, int D, u64 g0) {
   int k = 0;
-  while (k + 1 < D && g >= ls.node[k + 1]) ++k;
+  while (k + 1 < D && g0 >= ls.node[k + 1]) ++k;
   return k;
 }
 
-// Byte size of every storage slot (0 past a layer's node count) and their sum.
-__global__ __launch_bounds__(kBlock) void k_node_sizes(const uint2* __restrict__ nodes, u64 n, LayerStarts ls, int D,
-                                                       u32* __restrict__ sz, unsigned long long* __restrict__ acc) {
-  __shared__ u32 part[kBlock / 64];
-  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
-  u32 b = 0;
-  if (i < n) {
-    const int k = layer_of(ls, D, i);
-    if (i - ls.node[k] < ls.count[k]) {
-      const uint2 w = nodes[i];
-      b = ptr_bytes(w.x) + ptr_bytes(w.y);
+__device__ __forceinline__ u64 uniform64(u64 v) {   // (a wave-uniform value, into scalar registers)
+  return (u64(u32(__builtin_amdgcn_readfirstlane(int(v >> 32)))) << 32) | u32(__builtin_amdgcn_readfirstlane(int(v)));
+}
+
+// Slot g of the wave whose first slot of this item is gw (w: the slot's words, loaded by
+// the caller -- all of a thread's loads go out first).  The layer is looked up once per
+// wave on the scalar unit; only a wave that a layer start cuts walks per lane.
+__device__ __forceinline__ DagSlot dag_slot(uint2 w, const LayerStarts& ls, int D, int k0, u64 gw, u64 g) {
+  DagSlot s;
+  int k = k0;
+  while (k + 1 < D && gw >= ls.node[k + 1]) ++k;
+  const u64 nk = ls.node[k], nk1 = k + 1 < D ? ls.node[k + 1] : ~0ull, ck = ls.count[k];
+  u32 nh = 0;
+  bool valid;
+  if (g < nk1) {
+    if (g == nk) {
+      nh = 1;
+      for (int j = k - 1; j >= 0 && ls.node[j] == g; --j) ++nh;
     }
-    if (sz) sz[i] = b;
+    valid = g - nk < ck;
+  } else {   // (per lane)
+    while (k + 1 < D && g >= ls.node[k + 1]) ++k;
+    for (int j = k; j >= 0 && ls.node[j] == g; --j) ++nh;
+    valid = g - ls.node[k] < ls.count[k];
   }
-  for (int o = 32; o > 0; o >>= 1) b += u32(__shfl_xor(int(b), o, 64));
+  s.meta = u32(k) | (nh << 8) | (u32(valid) << 16);
+  s.w = w;
+  return s;
+}
+
+// a thread's kDagItems slots of tile g0 (slots past n: padding of no size)
+__device__ __forceinline__ void dag_load(const uint2* __restrict__ nodes, u64 n, const LayerStarts& ls, int D, u64 g0,
+                                         DagSlot (&sl)[kDagItems]) {
+  const int k0 = tile_first_layer(ls, D, g0);
+  uint2 w[kDagItems];
+#pragma unroll
+  for (int e = 0; e < kDagItems; ++e) {
+    const u64 g = g0 + u64(e) * kDagThreads + threadIdx.x;
+    w[e] = g < n ? nodes[g] : make_uint2(0u, 0u);
+  }
+#pragma unroll
+  for (int e = 0; e < kDagItems; ++e) {
+    const u64 gw = uniform64(g0 + u64(e) * kDagThreads + (threadIdx.x & ~63u));
+    const u64 g = gw + (threadIdx.x & 63u);
+    if (g < n) {
+      sl[e] = dag_slot(w[e], ls, D, k0, gw, g);
+    } else {
+      sl[e].meta = 0;
+      sl[e].w = w[e];
+    }
+  }
+}
+
+__device__ __forceinline__ u32 dag_size(const DagSlot& s) {
+  return 8 * s.nh() + (s.valid() ? ptr_bytes(s.w.x) + ptr_bytes(s.w.y) : 0u);
+}
+
+// Sum of the node section's pointer bytes (bytes(), src/shared_tree.cpp:488-496).
+__global__ __launch_bounds__(kDagThreads) void k_node_bytes(const uint2* __restrict__ nodes, u64 n, LayerStarts ls,
+                                                            int D, unsigned long long* __restrict__ acc) {
+  __shared__ u32 part[kDagThreads / 64];
+  DagSlot sl[kDagItems];
+  dag_load(nodes, n, ls, D, u64(blockIdx.x) * kDagTile, sl);
+  u32 b = 0;
+#pragma unroll
+  for (int e = 0; e < kDagItems; ++e)
+    if (sl[e].valid()) b += ptr_bytes(sl[e].w.x) + ptr_bytes(sl[e].w.y);
+  b = u32(wave_sum(u64(b)));
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = b;
   __syncthreads();
   if (threadIdx.x == 0) {   // line-padded shards (k_stats_sum): a few shared addresses would serialise
     u32 t = 0;
-    for (int w = 0; w < kBlock / 64; ++w) t += part[w];
+    for (int w = 0; w < kDagThreads / 64; ++w) t += part[w];
     if (t) atomicAdd(&acc[(blockIdx.x & (kStatShards - 1)) * kStatStride], (unsigned long long)t);
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_write_nodes(const uint2* __restrict__ nodes, u64 n,
-                                                        const u64* __restrict__ pos, LayerStarts ls, int D, u64 hdr,
-                                                        unsigned char* __restrict__ out) {
-  const u64 g = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (g >= n) return;
-  const int k = layer_of(ls, D, g);
-  if (g - ls.node[k] >= ls.count[k]) return;
-  unsigned char* o = out + hdr + 8 * u64(k + 1) + pos[g];
-  const uint2 w = nodes[g];
-  put_ptr(o, w.x);
-  put_ptr(o + ptr_bytes(w.x), w.y);
+// Per-tile byte counts of the node section (layer counts included): the tiles' prefixes
+// come from a scan of these (a look-back chain over thousands of tiles waits on
+// device-scope loads, which on this part cost more than a second read of the nodes).
+__global__ __launch_bounds__(kDagThreads) void k_dag_sizes(const uint2* __restrict__ nodes, u64 n, LayerStarts ls,
+                                                           int D, u32* __restrict__ tsum) {
+  __shared__ u32 part[kDagThreads / 64];
+  DagSlot sl[kDagItems];
+  dag_load(nodes, n, ls, D, u64(blockIdx.x) * kDagTile, sl);
+  u32 b = 0;
+#pragma unroll
+  for (int e = 0; e < kDagItems; ++e) b += dag_size(sl[e]);
+  b = u32(wave_sum(u64(b)));
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = b;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u32 t = 0;
+    for (int w = 0; w < kDagThreads / 64; ++w) t += part[w];
+    tsum[blockIdx.x] = t;
+  }
 }
 
-__global__ __launch_bounds__(kBlock) void k_write_leaves(const u64* __restrict__ leaves, u64 n, int lb, u64 base,
+// The node section (serialize, src/shared_tree.cpp:504-513), one tile per workgroup at
+// its prefix tpre[tile]: every slot's bytes (pointer::serialize, layer counts
+// big-endian) staged in LDS at the tile's output alignment, then stored as aligned
+// 16-B chunks (bytes at the two ends, which neighbouring tiles share).
+__global__ __launch_bounds__(kDagThreads) void k_dag_nodes(const uint2* __restrict__ nodes, u64 n, LayerStarts ls,
+                                                           int D, u64 hdr, const u64* __restrict__ tpre,
+                                                           unsigned char* __restrict__ out) {
+  __shared__ u32 s_grp[kDagGroups];
+  __shared__ __attribute__((aligned(16))) unsigned char s_out[kDagBuf];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const u64 tile = blockIdx.x;
+  DagSlot sl[kDagItems];
+  dag_load(nodes, n, ls, D, tile * kDagTile, sl);
+  for (u32 q = tid; q < kDagBuf / 16; q += kDagThreads)   // (the slots' bytes are ORed in)
+    reinterpret_cast<uint4*>(s_out)[q] = make_uint4(0u, 0u, 0u, 0u);
+  u32 ex[kDagItems];
+#pragma unroll
+  for (int e = 0; e < kDagItems; ++e) {
+    const u32 sz = dag_size(sl[e]);
+    u32 incl = sz;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const u32 y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    ex[e] = incl - sz;
+    if (lane == 63) s_grp[e * (kDagThreads / 64) + wave] = incl;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    u32 cs[kDagPer];
+    u32 c = 0;
+#pragma unroll
+    for (int q = 0; q < kDagPer; ++q) {
+      cs[q] = lane * kDagPer + q < kDagGroups ? s_grp[lane * kDagPer + q] : 0u;
+      c += cs[q];
+    }
+    u32 incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const u32 y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    u32 run = incl - c;
+#pragma unroll
+    for (int q = 0; q < kDagPer; ++q) {
+      if (lane * kDagPer + q < kDagGroups) s_grp[lane * kDagPer + q] = run;
+      run += cs[q];
+    }
+  }
+  __syncthreads();
+  const u64 obase = hdr + tpre[tile];
+  const u32 sh = u32(obase & 15);
+  u32* buf = reinterpret_cast<u32*>(s_out);
+#pragma unroll
+  for (int e = 0; e < kDagItems; ++e) {
+    u32 o = sh + s_grp[e * (kDagThreads / 64) + wave] + ex[e];
+    const DagSlot& s = sl[e];
+    const u32 nh = s.nh();
+    for (u32 h = 0; h < nh; ++h) {   // (layers that start here, in order)
+      const u64 cnt = ls.count[s.k() + 1 - int(nh) + int(h)];
+      lds_emit(buf, o, __builtin_bswap64(cnt), 8);
+      o += 8;
+    }
+    if (s.valid()) {
+      u32 nx, ny;
+      const u64 vx = ptr_le(s.w.x, nx), vy = ptr_le(s.w.y, ny);
+      lds_emit(buf, o, vx | (vy << (8 * nx)), nx + ny);
+    }
+  }
+  __syncthreads();
+  const u32 end = sh + u32(tpre[tile + 1] - tpre[tile]);
+  unsigned char* ob = out + (obase - sh);   // 16-B aligned (the buffer is)
+  for (u32 c = tid; c * 16 < end; c += kDagThreads) {
+    const u32 lo = c * 16, hi = lo + 16;
+    if (lo >= sh && hi <= end) {
+      *reinterpret_cast<uint4*>(ob + lo) = *reinterpret_cast<const uint4*>(s_out + lo);
+    } else {
+      for (u32 b = lo < sh ? sh : lo; b < hi && b < end; ++b) ob[b] = s_out[b];
+    }
+  }
+}
+
+// leaves (binary_write of each value, lb bytes); thread 0 also writes the root pointer
+// and the leaf count before them
+__global__ __launch_bounds__(kBlock) void k_write_leaves(const u64* __restrict__ leaves, u64 n, int lb, u32 root,
                                                          unsigned char* __restrict__ out) {
   const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (i < n) put_be(out + base + i * u64(lb), leaves[i], lb);
-}
-
-// root pointer, leaf count and every layer's count (its position needs the scan)
-__global__ void k_write_headers(u32 root, u64 n_leaves, LayerStarts ls, int D, u64 hdr,
-                                const u64* __restrict__ pos, const u32* __restrict__ sz, unsigned char* __restrict__ out) {
-  put_ptr(out, root);
-  put_be(out + ptr_bytes(root), n_leaves, 8);
-  for (int k = 0; k < D; ++k) {
-    const u64 g = ls.node[k];
-    const u64 before = g < ls.node[D] ? pos[g] : (pos[ls.node[D] - 1] + sz[ls.node[D] - 1]);
-    put_be(out + hdr + 8 * u64(k) + before, ls.count[k], 8);
+  const u64 base = ptr_bytes(root) + 8;
+  if (i == 0) {
+    put_ptr(out, root);
+    put_be(out + ptr_bytes(root), n, 8);
   }
+  if (i < n) put_be(out + base + i * u64(lb), leaves[i], lb);
 }
 
 // ---- decompression ---------------------------------------------
@@ -480,6 +852,11 @@ int gcz_sort_device(gcz_ctx* c) {
       matmax = std::max(matmax, nb * hG[cl] + 1);
     }
   }
+  // the partitioned layer with the most references keeps its records (histogrammed last):
+  // its rewire reads new children back through them (k_hremap)
+  int scl = -1;
+  for (int cl = 0; cl < D; ++cl)
+    if (hnb[cl] && (scl < 0 || c->info.layer_size[cl] > c->info.layer_size[scl])) scl = cl;
   const u64 cs_tiles = (nmax + kCsTile - 1) / kCsTile;
   matmax = std::max(matmax, 256 * cs_tiles + 1);
   tilemax = scan_tiles(matmax);
@@ -493,8 +870,14 @@ int gcz_sort_device(gcz_ctx* c) {
       (rc = c->ensure(s.hoff, matmax * 4 + 16)) || (rc = c->ensure(s.hrec, nwmax * 2 + 16)) ||
       (rc = c->ensure(s.desc, tilemax * 8 + 16)))
     return rc;
+  if (scl >= 0 && ((rc = c->ensure(s.hslot, 2 * c->info.layer_size[scl] * 4 + 16)) ||
+                   (rc = c->ensure(s.hval, 2 * c->info.layer_size[scl] * 4 + 16)) ||
+                   (rc = c->ensure(s.hbs, (u64(hnb[scl]) + 1) * 4 + 16))))
+    return rc;
   if (!s.h_mm) S_HIP(hipHostMalloc((void**)&s.h_mm, size_t(GCZ_MAX_LAYERS) * 8, hipHostMallocDefault));
   S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_hbucket), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            int((1u << kHB) * 4)));
+  S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_hremap), hipFuncAttributeMaxDynamicSharedMemorySize,
                             int((1u << kHB) * 4)));
   hipEvent_t e0{};
   c->prof_begin(KID_SORT, e0);
@@ -514,32 +897,79 @@ int gcz_sort_device(gcz_ctx* c) {
   };
   hipLaunchKernelGGL(k_mm_init, dim3(1), dim3(64), 0, c->stream, mm, D);   // [min, max] per child layer
   const uint2* nodes = c->nodes_out.as<uint2>();
+  // Every child is referenced at least once by its parent layer's stored words (each id
+  // occurs in the parent layer's input, and a pair stored or not holds the same ids as
+  // the node it is an instance of), so when the parent holds no more non-null words than
+  // there are children, every count is 1 and the order stays.  The parent's input pairs
+  // up with a null at its end when it is odd (reader-buffer builds hold more: the bound
+  // only grows), so 2 * nodes - (input & 1) bounds its non-null words from above.
+  std::vector<bool> once(D);
   for (int cl = 0; cl < D; ++cl) {
+    const u64 in = cl == 0 ? c->info.n_strands : c->layer_off[cl] - c->layer_off[cl - 1];
+    once[cl] = 2 * c->info.layer_size[cl] - (in & 1) <= n_of[cl];
+  }
+  // the other layers: partitioned (the leaves' parents) or atomics, zeroed / counted /
+  // reduced in one launch each for all of them
+  RangePlan zp{}, hp{}, mp{};
+  auto add = [](RangePlan& p, u64 lo, u64 n, u64 aux, u64 per_block) {
+    const u32 nb = u32(std::min<u64>(2048, std::max<u64>(1, (n + per_block - 1) / per_block)));
+    p.lo[p.m] = lo;
+    p.n[p.m] = n;
+    p.aux[p.m] = aux;
+    p.b0[p.m + 1] = p.b0[p.m] + nb;
+    ++p.m;
+  };
+  std::vector<int> order;
+  for (int cl = 0; cl < D; ++cl)
+    if (cl != scl) order.push_back(cl);
+  if (scl >= 0) order.push_back(scl);
+  // workgroups per bucket of a partitioned layer: enough to fill the part
+  std::vector<u32> hS(D, 1);
+  for (int cl : order) {
+    if (once[cl] || n_of[cl] == 0) continue;
     const u64 nw = 2 * c->info.layer_size[cl];   // words of parent layer cl
-    const u32* words = reinterpret_cast<const u32*>(nodes + c->layer_off[cl]);
     if (hnb[cl]) {
-      const u32 nb = hnb[cl];
-      const u64 G = hG[cl];
-      hipLaunchKernelGGL(k_hcount, dim3(unsigned(G)), dim3(kHThreads), 0, c->stream, words, nw, nb, G, mat);
-      if ((rc = scan(u64(nb) * G))) return rc;
-      hipLaunchKernelGGL(k_hscatter, dim3(unsigned(G)), dim3(kHThreads), 0, c->stream, words, nw, nb, G, off,
-                         s.hrec.as<unsigned short>());
-      hipLaunchKernelGGL(k_hbucket, dim3(nb), dim3(kHThreads), (1u << kHB) * 4, c->stream,
-                         s.hrec.as<unsigned short>(), off, G, n_of[cl], cnt + coff[cl], mm + 2 * cl);
+      hS[cl] = u32(std::max<u64>(1, std::min<u64>((1024 + hnb[cl] - 1) / hnb[cl], nw / (hnb[cl] * 32768ull))));
+      if (hS[cl] > 1) {
+        add(zp, coff[cl], n_of[cl], 0, u64(kBlock) * 8);
+        add(mp, coff[cl], n_of[cl], u64(cl), u64(kBlock) * 8);
+      }
     } else {
-      if (n_of[cl]) S_HIP(hipMemsetAsync(cnt + coff[cl], 0, n_of[cl] * 4, c->stream));
-      if (nw)
-        hipLaunchKernelGGL(k_hist, grid_of(nw), dim3(kBlock), 0, c->stream, words, nw, cnt + coff[cl]);
-      if (n_of[cl])
-        hipLaunchKernelGGL(k_minmax, dim3(unsigned(std::min<u64>(1024, (n_of[cl] + kBlock - 1) / kBlock))),
-                           dim3(kBlock), 0, c->stream, cnt + coff[cl], n_of[cl], mm + 2 * cl);
+      add(zp, coff[cl], n_of[cl], 0, u64(kBlock) * 8);
+      add(hp, 2 * c->layer_off[cl], nw, coff[cl], u64(kBlock) * 8);
+      add(mp, coff[cl], n_of[cl], u64(cl), u64(kBlock) * 8);
     }
+  }
+  if (zp.m) hipLaunchKernelGGL(k_zero_ranges, dim3(zp.b0[zp.m]), dim3(kBlock), 0, c->stream, zp, cnt);
+  for (int cl : order) {
+    if (once[cl] || n_of[cl] == 0 || !hnb[cl]) continue;
+    const u64 nw = 2 * c->info.layer_size[cl];
+    const u32* words = reinterpret_cast<const u32*>(nodes + c->layer_off[cl]);
+    const u32 nb = hnb[cl];
+    const u64 G = hG[cl];
+    const bool keep = cl == scl;
+    hipLaunchKernelGGL(k_hcount, dim3(unsigned(G)), dim3(kHThreads), 0, c->stream, words, nw, nb, G, mat);
+    if ((rc = scan(u64(nb) * G))) return rc;
+    if (nb <= kHStagedMax)
+      hipLaunchKernelGGL(k_hscatter_lds, dim3(unsigned(G)), dim3(kHThreads), 0, c->stream, words, nw, nb, G, mat,
+                         off, s.hrec.as<unsigned short>(), keep ? s.hslot.as<u32>() : nullptr);
+    else
+      hipLaunchKernelGGL(k_hscatter, dim3(unsigned(G)), dim3(kHThreads), 0, c->stream, words, nw, nb, G, off,
+                         s.hrec.as<unsigned short>(), keep ? s.hslot.as<u32>() : nullptr);
+    hipLaunchKernelGGL(k_hbucket, dim3(nb * hS[cl]), dim3(kHThreads), (1u << kHB) * 4, c->stream,
+                       s.hrec.as<unsigned short>(), off, G, n_of[cl], hS[cl], cnt + coff[cl], mm + 2 * cl,
+                       keep ? s.hbs.as<u32>() : nullptr);
     S_HIP(hipGetLastError());
   }
+  if (hp.m)
+    hipLaunchKernelGGL(k_hist_ranges, dim3(hp.b0[hp.m]), dim3(kBlock), 0, c->stream, hp,
+                       reinterpret_cast<const u32*>(nodes), cnt);
+  if (mp.m) hipLaunchKernelGGL(k_minmax_ranges, dim3(mp.b0[mp.m]), dim3(kBlock), 0, c->stream, mp, cnt, mm);
+  S_HIP(hipGetLastError());
   S_HIP(hipMemcpyAsync(s.h_mm, mm, size_t(D) * 8, hipMemcpyDeviceToHost, c->stream));
   S_HIP(hipStreamSynchronize(c->stream));
   std::vector<bool> ident(D);
-  for (int cl = 0; cl < D; ++cl) ident[cl] = n_of[cl] <= 1 || s.h_mm[2 * cl] == s.h_mm[2 * cl + 1];
+  for (int cl = 0; cl < D; ++cl) ident[cl] = once[cl] || n_of[cl] <= 1 || s.h_mm[2 * cl] == s.h_mm[2 * cl + 1];
   // stable descending sort of (count, index) per non-trivial child layer: newpos[old] = new
   for (int cl = 0; cl < D; ++cl) {
     if (ident[cl]) continue;
@@ -576,17 +1006,54 @@ int gcz_sort_device(gcz_ctx* c) {
                        s.newpos.as<u32>(), s.leaves2.as<u64>());
     std::swap(c->leaves_out, s.leaves2);
   }
-  PermPlan pp{};
-  for (int k = 0; k <= D; ++k) pp.node[k] = c->layer_off[k];
-  for (int k = 0; k < D; ++k) {
-    pp.count[k] = c->info.layer_size[k];
-    pp.child[k] = ident[k] ? -1 : (long long)coff[k];
-    pp.own[k] = (k + 1 < D && !ident[k + 1]) ? (long long)coff[k + 1] : -1;
+  const bool remap = scl >= 0 && !once[scl] && !ident[scl];
+  if (remap) {
+    const u32 S = u32(std::max<u64>(1, (1024 + hnb[scl] - 1) / hnb[scl]));
+    hipLaunchKernelGGL(k_hremap, dim3(hnb[scl] * S), dim3(kHThreads), (1u << kHB) * 4, c->stream,
+                       s.hrec.as<unsigned short>(), s.hbs.as<u32>(), s.newpos.as<u32>() + coff[scl], n_of[scl], S,
+                       s.hval.as<u32>());
+    S_HIP(hipGetLastError());
   }
-  hipLaunchKernelGGL(k_perm_nodes, grid_of(N), dim3(kBlock), 0, c->stream, nodes, N, D, pp, s.newpos.as<u32>(),
-                     s.nodes2.as<uint2>());
-  S_HIP(hipGetLastError());
-  std::swap(c->nodes_out, s.nodes2);
+  // node layers: rewired in place where their own order stays, permuted into nodes2 (and
+  // copied back) where it changes -- or, when that moves more bytes, every layer into
+  // nodes2 and the buffers swapped
+  u64 moved_inplace = 0, moved_swap = 0;
+  for (int k = 0; k < D; ++k) {
+    const bool child = !ident[k], own = k + 1 < D && !ident[k + 1];
+    const u64 n = c->info.layer_size[k];
+    moved_swap += 2 * n;
+    moved_inplace += own ? 4 * n : child ? 2 * n : 0;
+  }
+  const bool swap_all = moved_swap < moved_inplace;
+  PermPlan pp{};
+  for (int k = 0; k < D; ++k) {
+    const bool child = !ident[k], own = k + 1 < D && !ident[k + 1];
+    const u64 n = c->info.layer_size[k];
+    if (n == 0 || (!swap_all && !child && !own)) continue;
+    pp.node[pp.m] = c->layer_off[k];
+    pp.count[pp.m] = n;
+    pp.child[pp.m] = child ? (long long)coff[k] : -1;
+    pp.via_slot[pp.m] = child && remap && k == scl;
+    pp.own[pp.m] = own ? (long long)coff[k + 1] : -1;
+    pp.b0[pp.m + 1] = pp.b0[pp.m] + u32((n + kBlock * kPermItems - 1) / (kBlock * kPermItems));
+    ++pp.m;
+  }
+  if (pp.m) {
+    uint2* in = c->nodes_out.as<uint2>();
+    uint2* tmp = s.nodes2.as<uint2>();
+    hipLaunchKernelGGL(k_perm_nodes, dim3(pp.b0[pp.m]), dim3(kBlock), 0, c->stream, in, pp, s.newpos.as<u32>(),
+                       s.hslot.as<u32>(), s.hval.as<u32>(),
+                       swap_all ? tmp : in, tmp);
+    S_HIP(hipGetLastError());
+    if (swap_all) {
+      std::swap(c->nodes_out, s.nodes2);
+    } else {
+      for (int e = 0; e < pp.m; ++e)
+        if (pp.own[e] >= 0)
+          S_HIP(hipMemcpyAsync(in + pp.node[e], tmp + pp.node[e], pp.count[e] * 8, hipMemcpyDeviceToDevice,
+                               c->stream));
+    }
+  }
   c->prof_end(KID_SORT, e0);
   S_HIP(hipStreamSynchronize(c->stream));
   return GCZ_OK;
@@ -602,8 +1069,8 @@ int gcz_bytes_device(gcz_ctx* c, uint64_t* out) {
   const int D = c->info.n_layers;
   const u64 N = c->layer_off[D];
   const LayerStarts ls = layer_starts(c);
-  hipLaunchKernelGGL(k_node_sizes, grid_of(N), dim3(kBlock), 0, c->stream, c->nodes_out.as<uint2>(), N, ls, D,
-                     nullptr, s.acc.as<unsigned long long>());
+  hipLaunchKernelGGL(k_node_bytes, dim3(unsigned((N + kDagTile - 1) / kDagTile)), dim3(kDagThreads), 0, c->stream,
+                     c->nodes_out.as<uint2>(), N, ls, D, s.acc.as<unsigned long long>());
   u64* total = s.acc.as<u64>() + kStatBytes / 8;
   hipLaunchKernelGGL(k_stats_sum, dim3(1), dim3(1024), 0, c->stream, s.acc.as<u64>(), total);
   S_HIP(hipGetLastError());
@@ -619,40 +1086,43 @@ int gcz_bytes_device(gcz_ctx* c, uint64_t* out) {
 static int serialize_on_device(gcz_ctx* c, unsigned char** d_dag, uint64_t* written) {
   if (!c->sortst) c->sortst = new gcz_sort_state();
   gcz_sort_state& s = *c->sortst;
-  uint64_t total = 0;
-  if (int rc = gcz_bytes_device(c, &total)) return rc;
   const int D = c->info.n_layers;
   const u64 N = c->layer_off[D];
-  int rc;
-  if ((rc = c->ensure(s.sizes, N * 4 + 16)) || (rc = c->ensure(s.pos, N * 8 + 16)) ||
-      (rc = c->ensure(s.dag, total + 16)))
-    return rc;
-  hipEvent_t e0{};
-  c->prof_begin(KID_DAG, e0);
-  S_HIP(hipMemsetAsync(s.acc.ptr, 0, kStatBytes, c->stream));
-  const LayerStarts ls = layer_starts(c);
-  hipLaunchKernelGGL(k_node_sizes, grid_of(N), dim3(kBlock), 0, c->stream, c->nodes_out.as<uint2>(), N, ls, D,
-                     s.sizes.as<u32>(), s.acc.as<unsigned long long>());
-  const u64 t = scan_tiles(N);   // u64 byte offsets (tile sums <= 8 * kScanTile)
-  if ((rc = c->ensure(s.desc, std::max<u64>(s.desc.bytes, t * 8 + 16)))) return rc;
-  S_HIP(hipMemsetAsync(s.desc.ptr, 0, t * 8 + 16, c->stream));
-  hipLaunchKernelGGL((k_scan_excl<ScanU32, u64>), dim3(unsigned(std::max<u64>(t, 1))), dim3(kScanThreads), 0,
-                     c->stream, ScanU32{s.sizes.as<u32>(), N}, N, s.pos.as<u64>(), s.desc.as<u64>(),
-                     reinterpret_cast<u32*>(s.desc.as<u64>() + t), static_cast<u64*>(nullptr));
-  S_HIP(hipGetLastError());
+  for (int k = 0; k < D; ++k)   // (every layer count is written before its first slot)
+    if (c->layer_off[k + 1] <= c->layer_off[k]) return c->fail(GCZ_ERR_ARG, "serialize", "empty node layer");
   const int lb = (c->info.L + 1) / 2;
   const u64 hdr = host_ptr_bytes(c->info.root) + 8 + c->info.n_leaves * u64(lb);
+  const u64 cap = hdr + 8 * u64(D) + 8 * N;   // (pointers of at most 4 bytes)
+  const u64 t = (N + kDagTile - 1) / kDagTile;
+  const u64 st = scan_tiles(t + 1);
+  int rc;
+  if ((rc = c->ensure(s.dag, cap + 16)) || (rc = c->ensure(s.desc, std::max<u64>(s.desc.bytes, st * 8 + 16))) ||
+      (rc = c->ensure(s.cnt, std::max<u64>(s.cnt.bytes, t * 4 + 16))) ||
+      (rc = c->ensure(s.keys, std::max<u64>(s.keys.bytes, (t + 1) * 8 + 16))))
+    return rc;
+  if (!s.h_tot) S_HIP(hipHostMalloc((void**)&s.h_tot, 8, hipHostMallocDefault));
+  hipEvent_t e0{};
+  c->prof_begin(KID_DAG, e0);
+  const LayerStarts ls = layer_starts(c);
   unsigned char* out = s.dag.as<unsigned char>();
-  hipLaunchKernelGGL(k_write_headers, dim3(1), dim3(1), 0, c->stream, c->info.root, c->info.n_leaves, ls, D, hdr,
-                     s.pos.as<u64>(), s.sizes.as<u32>(), out);
+  u32* tsum = s.cnt.as<u32>();
+  u64* tpre = s.keys.as<u64>();   // t + 1 prefixes (the last: the section's size)
   hipLaunchKernelGGL(k_write_leaves, grid_of(c->info.n_leaves), dim3(kBlock), 0, c->stream,
-                     c->leaves_out.as<u64>(), c->info.n_leaves, lb, host_ptr_bytes(c->info.root) + 8, out);
-  hipLaunchKernelGGL(k_write_nodes, grid_of(N), dim3(kBlock), 0, c->stream, c->nodes_out.as<uint2>(), N,
-                     s.pos.as<u64>(), ls, D, hdr, out);
+                     c->leaves_out.as<u64>(), c->info.n_leaves, lb, c->info.root, out);
+  hipLaunchKernelGGL(k_dag_sizes, dim3(unsigned(t)), dim3(kDagThreads), 0, c->stream, c->nodes_out.as<uint2>(), N, ls,
+                     D, tsum);
+  S_HIP(hipMemsetAsync(s.desc.ptr, 0, st * 8 + 16, c->stream));
+  hipLaunchKernelGGL((k_scan_excl<ScanU32, u64>), dim3(unsigned(st)), dim3(kScanThreads), 0, c->stream,
+                     ScanU32{tsum, t}, t + 1, tpre, s.desc.as<u64>(), reinterpret_cast<u32*>(s.desc.as<u64>() + st),
+                     static_cast<u64*>(nullptr));
+  hipLaunchKernelGGL(k_dag_nodes, dim3(unsigned(t)), dim3(kDagThreads), 0, c->stream, c->nodes_out.as<uint2>(), N,
+                     ls, D, hdr, tpre, out);
   S_HIP(hipGetLastError());
+  S_HIP(hipMemcpyAsync(s.h_tot, tpre + t, 8, hipMemcpyDeviceToHost, c->stream));
   c->prof_end(KID_DAG, e0);
+  S_HIP(hipStreamSynchronize(c->stream));
   *d_dag = out;
-  *written = total;
+  *written = hdr + *s.h_tot;
   return GCZ_OK;
 }
 
