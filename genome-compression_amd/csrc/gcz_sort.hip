@@ -31,6 +31,7 @@ struct gcz_sort_state {
   DevBuf cnt, keys, keys2, vals, vals2, newpos, mm, acc, dag, nodes2, leaves2, dw1, dw2, text;
   DevBuf hmat, hoff, hrec, desc;   // partitioned histogram; scan descriptors
   DevBuf hslot, hval, hbs;         // its records' positions per word, new children, bucket starts
+  DevBuf hpart;                    // per-block (min, max) counts
   u32* h_mm = nullptr;
   u64* h_tot = nullptr;
 };
@@ -40,7 +41,7 @@ void gcz_sort_state_free(gcz_ctx* c) {
   if (!s) return;
   for (DevBuf* b : {&s->cnt, &s->keys, &s->keys2, &s->vals, &s->vals2, &s->newpos, &s->mm, &s->acc, &s->dag,
                     &s->nodes2, &s->leaves2, &s->dw1, &s->dw2, &s->text, &s->hmat, &s->hoff, &s->hrec, &s->desc,
-                    &s->hslot, &s->hval, &s->hbs})
+                    &s->hslot, &s->hval, &s->hbs, &s->hpart})
     if (b->ptr) (void)hipFree(b->ptr);
   if (s->h_mm) (void)hipHostFree(s->h_mm);
   if (s->h_tot) (void)hipHostFree(s->h_tot);
@@ -293,16 +294,32 @@ struct CsPass {
   __device__ __forceinline__ u32 digit(u32 k) const { return (k >> shift) & ((1u << bits) - 1u); }
 };
 
+// (equal digits of a wave counted once: the lowest lane of each match adds the match's size)
 __global__ __launch_bounds__(kCsThreads) void k_cs_count(CsPass P, u64 ntiles, u32* __restrict__ mat) {
   __shared__ u32 hist[256];
   const u32 R = 1u << P.bits;
   for (u32 q = threadIdx.x; q < R; q += kCsThreads) hist[q] = 0;
   __syncthreads();
   const u64 t = blockIdx.x, i0 = t * kCsTile;
+  const int lane = threadIdx.x & 63;
+  const u64 lt = (1ull << lane) - 1;
+  u32 key[kCsItems];
 #pragma unroll
   for (int e = 0; e < kCsItems; ++e) {
     const u64 i = i0 + u64(e) * kCsThreads + threadIdx.x;
-    if (i < P.n) atomicAdd(&hist[P.digit(P.key(i))], 1u);
+    key[e] = i < P.n ? P.key(i) : 0u;
+  }
+#pragma unroll
+  for (int e = 0; e < kCsItems; ++e) {
+    const u64 i = i0 + u64(e) * kCsThreads + threadIdx.x;
+    const bool ok = i < P.n;
+    const u32 d = P.digit(key[e]);
+    u64 m = __ballot(ok);
+    for (u32 b = 0; b < P.bits; ++b) {
+      const u64 bal = __ballot((d >> b) & 1u);
+      m &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    if (ok && (m & lt) == 0) atomicAdd(&hist[d], u32(__popcll(m)));
   }
   __syncthreads();
   for (u32 q = threadIdx.x; q < R; q += kCsThreads) mat[u64(q) * ntiles + t] = hist[q];
@@ -379,6 +396,8 @@ struct RangePlan {
   int m;
 };
 
+constexpr int kRangeBatch = 8;   // loads in flight per thread
+
 __device__ __forceinline__ int plan_entry(const RangePlan& p) {
   int e = 0;
   while (e + 1 < p.m && blockIdx.x >= p.b0[e + 1]) ++e;
@@ -392,29 +411,26 @@ __global__ __launch_bounds__(kBlock) void k_zero_ranges(RangePlan p, u32* __rest
   for (u64 i = (blockIdx.x - p.b0[e]) * u64(kBlock) + threadIdx.x; i < p.n[e]; i += nb * kBlock) cnt[p.lo[e] + i] = 0;
 }
 
-// pointer::serialize of w as a little-endian word of its bytes in output order, and
-// their count: the pointer's value (seg | t | m | offset) is written big-endian
-__device__ __forceinline__ u64 ptr_le(u32 w, u32& nbytes) {
-  const u32 idx = w & kIdx;
-  u32 seg, off;
-  if (idx == kIdx) { seg = 3; off = 0xfffffffu; }
-  else if (idx < kSegStart1) { seg = 0; off = idx; }
-  else if (idx < kSegStart2) { seg = 1; off = idx - kSegStart1; }
-  else if (idx < kSegStart3) { seg = 2; off = idx - kSegStart2; }
-  else { seg = 3; off = idx - kSegStart3; }
+// pointer::serialize of w as a word of its bytes in output order (the first byte lowest),
+// and their count: the pointer's value (seg | t | m | offset) written big-endian
+__device__ __forceinline__ u32 ptr_enc(u32 w, u32& nbytes) {
+  const u32 idx = w & kIdx;   // (null: idx = kIdx, segment 3 with offset 0xfffffff)
+  const u32 seg = u32(idx >= kSegStart1) + u32(idx >= kSegStart2) + u32(idx >= kSegStart3);
+  const u32 base = seg == 0 ? 0u : seg == 1 ? kSegStart1 : seg == 2 ? kSegStart2 : kSegStart3;
+  const u32 off = idx == kIdx ? 0xfffffffu : idx - base;
   const u32 top = 8 * seg;
-  const u32 v = off | (((w >> 29) & 1u) << (top + 4)) | (((w >> 30) & 1u) << (top + 5)) | (seg << (top + 6));
+  const u32 v = off | (((w >> 29) & 3u) << (top + 4)) | (seg << (top + 6));
   nbytes = seg + 1;
-  return u64(__builtin_bswap32(v) >> (8 * (3 - seg)));
+  return __builtin_bswap32(v) >> (24 - top);
 }
 
-// len <= 8 bytes of v (first byte lowest) at byte o of a zeroed LDS buffer: ORed into its
-// aligned words, so neighbours that share a word need no ordering
-__device__ __forceinline__ void lds_emit(u32* __restrict__ buf, u32 o, u64 v, u32 len) {
-  const u32 r = o & 3, w0 = o >> 2;
-  atomicOr(&buf[w0], u32(v << (8 * r)));
-  if (r + len > 4) atomicOr(&buf[w0 + 1], u32(v >> (32 - 8 * r)));
-  if (r + len > 8) atomicOr(&buf[w0 + 2], u32(v >> (64 - 8 * r)));
+// len <= 8 bytes (hi:lo, the first byte lowest) at byte o of a zeroed LDS buffer: ORed into
+// their aligned words, so neighbours that share a word need no ordering
+__device__ __forceinline__ void lds_emit(u32* __restrict__ buf, u32 o, u32 lo, u32 hi, u32 len) {
+  const u32 r = o & 3, w0 = o >> 2, sh = 8 * r;
+  atomicOr(&buf[w0], lo << sh);
+  if (r + len > 4) atomicOr(&buf[w0 + 1], r ? __builtin_amdgcn_alignbit(hi, lo, 32 - sh) : hi);
+  if (r + len > 8) atomicOr(&buf[w0 + 2], hi >> (32 - sh));
 }
 
 // histogram (src/shared_tree.cpp:316-326) of the listed parent layers: words [lo, lo + n)
@@ -422,25 +438,38 @@ __device__ __forceinline__ void lds_emit(u32* __restrict__ buf, u32 o, u64 v, u3
 __global__ __launch_bounds__(kBlock) void k_hist_ranges(RangePlan p, const u32* __restrict__ words,
                                                         u32* __restrict__ cnt) {
   const int e = plan_entry(p);
-  const u64 nb = p.b0[e + 1] - p.b0[e];
+  const u64 step = u64(p.b0[e + 1] - p.b0[e]) * kBlock, n = p.n[e];
+  const u32* wv = words + p.lo[e];
   u32* c = cnt + p.aux[e];
-  for (u64 i = (blockIdx.x - p.b0[e]) * u64(kBlock) + threadIdx.x; i < p.n[e]; i += nb * kBlock) {
-    const u32 w = words[p.lo[e] + i];
-    if (!is_null(w)) atomicAdd(&c[w & kIdx], 1u);
+  for (u64 i = (blockIdx.x - p.b0[e]) * u64(kBlock) + threadIdx.x; i < n; i += kRangeBatch * step) {
+    u32 w[kRangeBatch];
+#pragma unroll
+    for (int q = 0; q < kRangeBatch; ++q) w[q] = i + q * step < n ? wv[i + q * step] : kIdx;
+#pragma unroll
+    for (int q = 0; q < kRangeBatch; ++q)
+      if (!is_null(w[q])) atomicAdd(&c[w[q] & kIdx], 1u);
   }
 }
 
-// min / max count of the listed child layers: cnt[lo, lo + n) into mm[2 aux, 2 aux + 1]
+// min / max count of the listed child layers: cnt[lo, lo + n), one (min, max) per block
+// into part (device-scope atomics on two shared words would serialise thousands of blocks)
 __global__ __launch_bounds__(kBlock) void k_minmax_ranges(RangePlan p, const u32* __restrict__ cnt,
-                                                          u32* __restrict__ mm) {
+                                                          u32* __restrict__ part) {
   __shared__ u32 smin[kBlock / 64], smax[kBlock / 64];
   const int e = plan_entry(p);
   const u64 nb = p.b0[e + 1] - p.b0[e];
   u32 lo = ~0u, hi = 0;
-  for (u64 i = (blockIdx.x - p.b0[e]) * u64(kBlock) + threadIdx.x; i < p.n[e]; i += nb * kBlock) {
-    const u32 v = cnt[p.lo[e] + i];
-    lo = min(lo, v);
-    hi = max(hi, v);
+  const u64 step = nb * kBlock, n = p.n[e];
+  const u32* cv = cnt + p.lo[e];
+  for (u64 i = (blockIdx.x - p.b0[e]) * u64(kBlock) + threadIdx.x; i < n; i += kRangeBatch * step) {
+    u32 v[kRangeBatch];
+#pragma unroll
+    for (int q = 0; q < kRangeBatch; ++q) v[q] = i + q * step < n ? cv[i + q * step] : ~0u;
+#pragma unroll
+    for (int q = 0; q < kRangeBatch; ++q) {
+      lo = min(lo, v[q]);
+      if (v[q] != ~0u) hi = max(hi, v[q]);
+    }
   }
   for (int o = 32; o > 0; o >>= 1) {
     lo = min(lo, u32(__shfl_xor(int(lo), o, 64)));
@@ -451,8 +480,34 @@ __global__ __launch_bounds__(kBlock) void k_minmax_ranges(RangePlan p, const u32
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int w = 1; w < kBlock / 64; ++w) { lo = min(lo, smin[w]); hi = max(hi, smax[w]); }
-    atomicMin(&mm[2 * p.aux[e]], lo);
-    atomicMax(&mm[2 * p.aux[e] + 1], hi);
+    part[2 * blockIdx.x] = lo;
+    part[2 * blockIdx.x + 1] = hi;
+  }
+}
+
+// the blocks' (min, max) of each entry into mm[2 aux, 2 aux + 1] (one workgroup)
+__global__ __launch_bounds__(1024) void k_minmax_fold(RangePlan p, const u32* __restrict__ part,
+                                                      u32* __restrict__ mm) {
+  __shared__ u32 smin[16], smax[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int e = 0; e < p.m; ++e) {
+    u32 lo = ~0u, hi = 0;
+    for (u32 b = p.b0[e] + threadIdx.x; b < p.b0[e + 1]; b += 1024) {
+      lo = min(lo, part[2 * b]);
+      hi = max(hi, part[2 * b + 1]);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = min(lo, u32(__shfl_xor(int(lo), o, 64)));
+      hi = max(hi, u32(__shfl_xor(int(hi), o, 64)));
+    }
+    if (lane == 0) { smin[wave] = lo; smax[wave] = hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < 16; ++w) { lo = min(lo, smin[w]); hi = max(hi, smax[w]); }
+      mm[2 * p.aux[e]] = lo;
+      mm[2 * p.aux[e] + 1] = hi;
+    }
+    __syncthreads();
   }
 }
 
@@ -529,92 +584,80 @@ __global__ __launch_bounds__(kBlock) void k_perm_nodes(const uint2* in, PermPlan
 }
 
 struct LayerStarts {
-  u64 node[GCZ_MAX_LAYERS + 1];   // storage start of each layer within the node buffer (+ the end)
-  u64 count[GCZ_MAX_LAYERS];      // nodes of each layer (storage holds ceil(n/2) slots, count <= that)
+  u64 node[GCZ_MAX_LAYERS + 1];     // storage start of each layer within the node buffer (+ the end)
+  u64 count[GCZ_MAX_LAYERS];        // nodes of each layer (storage holds ceil(n/2) slots, count <= that)
+  u64 cstart[GCZ_MAX_LAYERS + 1];   // first node of each layer in the concatenation of the layers' nodes
 };
 
 // ---- bytes() and the .dag node section ----
-// Tiles of kDagTile storage slots, element e * kDagThreads + tid of a tile per thread
-// (coalesced 8-B loads); the tile's first layer is found once, each element steps on
-// from it.  A slot's size is its two pointers' bytes (0 past its layer's node count)
-// plus 8 for every layer count that is written right before it (the slot that starts
-// the layer).
+// The nodes of all layers, concatenated (storage padding skipped), in tiles of kDagTile,
+// element e * kDagThreads + tid of a tile per thread (coalesced 8-B loads).  A node's size
+// is its two pointers' bytes, plus 8 for the layer count written right before the first
+// node of each layer.  The layer is looked up once per wave on the scalar unit; only a
+// wave that a layer start cuts walks per lane.
 constexpr int kDagThreads = 256;
 constexpr int kDagItems = 8;
-constexpr u64 kDagTile = u64(kDagThreads) * kDagItems;       // 2 Ki slots (several workgroups per CU)
-constexpr int kDagGroups = kDagItems * (kDagThreads / 64);   // 64-slot groups of a tile
+constexpr u64 kDagTile = u64(kDagThreads) * kDagItems;       // 2 Ki nodes (several workgroups per CU)
+constexpr int kDagGroups = kDagItems * (kDagThreads / 64);   // 64-node groups of a tile
 constexpr int kDagPer = (kDagGroups + 63) / 64;              // groups per lane of the scanning wave
 constexpr u32 kDagBuf = (u32(kDagTile) * 8 + 8 * GCZ_MAX_LAYERS + 32 + 15) / 16 * 16;
 
 struct DagSlot {
-  uint2 w;
-  u32 meta;   // layer | layer counts written before it << 8 | a node (not padding) << 16
+  uint2 w;    // the node's words; after dag_encode, its bytes in output order (x: first four)
+  u32 meta;   // layer | starts its layer << 8 | a node (not past the end) << 16 | bytes << 20
   __device__ __forceinline__ int k() const { return int(meta & 0xff); }
   __device__ __forceinline__ u32 nh() const { return (meta >> 8) & 0xff; }
   __device__ __forceinline__ bool valid() const { return (meta >> 16) & 1u; }
+  __device__ __forceinline__ u32 len() const { return meta >> 20; }
 };
 
-__device__ __forceinline__ int tile_first_layer(const LayerStarts& ls, int D, u64 g0) {
-  int k = 0;
-  while (k + 1 < D && g0 >= ls.node[k + 1]) ++k;
-  return k;
+// the node's serialized bytes (two pointers: 2..8 bytes) in place of its words
+__device__ __forceinline__ void dag_encode(DagSlot& s) {
+  u32 nx, ny;
+  const u32 vx = ptr_enc(s.w.x, nx), vy = ptr_enc(s.w.y, ny);
+  const u32 sx = 8 * nx;
+  s.w.x = sx == 32 ? vx : vx | (vy << sx);
+  s.w.y = sx == 32 ? vy : vy >> (32 - sx);
+  s.meta |= (s.valid() ? nx + ny : 0u) << 20;
 }
 
 __device__ __forceinline__ u64 uniform64(u64 v) {   // (a wave-uniform value, into scalar registers)
   return (u64(u32(__builtin_amdgcn_readfirstlane(int(v >> 32)))) << 32) | u32(__builtin_amdgcn_readfirstlane(int(v)));
 }
 
-// Slot g of the wave whose first slot of this item is gw (w: the slot's words, loaded by
-// the caller -- all of a thread's loads go out first).  The layer is looked up once per
-// wave on the scalar unit; only a wave that a layer start cuts walks per lane.
-__device__ __forceinline__ DagSlot dag_slot(uint2 w, const LayerStarts& ls, int D, int k0, u64 gw, u64 g) {
-  DagSlot s;
-  int k = k0;
-  while (k + 1 < D && gw >= ls.node[k + 1]) ++k;
-  const u64 nk = ls.node[k], nk1 = k + 1 < D ? ls.node[k + 1] : ~0ull, ck = ls.count[k];
-  u32 nh = 0;
-  bool valid;
-  if (g < nk1) {
-    if (g == nk) {
-      nh = 1;
-      for (int j = k - 1; j >= 0 && ls.node[j] == g; --j) ++nh;
-    }
-    valid = g - nk < ck;
-  } else {   // (per lane)
-    while (k + 1 < D && g >= ls.node[k + 1]) ++k;
-    for (int j = k; j >= 0 && ls.node[j] == g; --j) ++nh;
-    valid = g - ls.node[k] < ls.count[k];
-  }
-  s.meta = u32(k) | (nh << 8) | (u32(valid) << 16);
-  s.w = w;
-  return s;
-}
-
-// a thread's kDagItems slots of tile g0 (slots past n: padding of no size)
-__device__ __forceinline__ void dag_load(const uint2* __restrict__ nodes, u64 n, const LayerStarts& ls, int D, u64 g0,
+// a thread's kDagItems nodes of the tile starting at node c0 (of m)
+__device__ __forceinline__ void dag_load(const uint2* __restrict__ nodes, u64 m, const LayerStarts& ls, int D, u64 c0,
                                          DagSlot (&sl)[kDagItems]) {
-  const int k0 = tile_first_layer(ls, D, g0);
-  uint2 w[kDagItems];
+  int k = 0;
+  while (k + 1 < D && c0 >= ls.cstart[k + 1]) ++k;
+  u64 kcs = ls.cstart[k], kend = ls.cstart[k + 1], knd = ls.node[k];   // (scalar registers)
+  u64 g[kDagItems];
 #pragma unroll
   for (int e = 0; e < kDagItems; ++e) {
-    const u64 g = g0 + u64(e) * kDagThreads + threadIdx.x;
-    w[e] = g < n ? nodes[g] : make_uint2(0u, 0u);
-  }
-#pragma unroll
-  for (int e = 0; e < kDagItems; ++e) {
-    const u64 gw = uniform64(g0 + u64(e) * kDagThreads + (threadIdx.x & ~63u));
-    const u64 g = gw + (threadIdx.x & 63u);
-    if (g < n) {
-      sl[e] = dag_slot(w[e], ls, D, k0, gw, g);
-    } else {
-      sl[e].meta = 0;
-      sl[e].w = w[e];
+    const u64 cw = uniform64(c0 + u64(e) * kDagThreads + (threadIdx.x & ~63u));
+    const u64 c = cw + (threadIdx.x & 63u);
+    if (cw >= kend && cw < m) {   // (the wave starts in a later layer)
+      while (k + 1 < D && cw >= ls.cstart[k + 1]) ++k;
+      kcs = ls.cstart[k];
+      kend = ls.cstart[k + 1];
+      knd = ls.node[k];
     }
+    int kk = k;
+    u64 cs = kcs, nd = knd;
+    if (c >= kend && c < m) {   // (a layer starts inside the wave: per lane)
+      while (kk + 1 < D && c >= ls.cstart[kk + 1]) ++kk;
+      cs = ls.cstart[kk];
+      nd = ls.node[kk];
+    }
+    g[e] = nd + (c - cs);
+    sl[e].meta = c < m ? u32(kk) | (u32(c == cs) << 8) | (1u << 16) : 0u;
   }
+#pragma unroll
+  for (int e = 0; e < kDagItems; ++e) sl[e].w = sl[e].valid() ? nodes[g[e]] : make_uint2(0u, 0u);
 }
 
 __device__ __forceinline__ u32 dag_size(const DagSlot& s) {
-  return 8 * s.nh() + (s.valid() ? ptr_bytes(s.w.x) + ptr_bytes(s.w.y) : 0u);
+  return s.valid() ? 8 * s.nh() + ptr_bytes(s.w.x) + ptr_bytes(s.w.y) : 0u;
 }
 
 // Sum of the node section's pointer bytes (bytes(), src/shared_tree.cpp:488-496).
@@ -676,7 +719,8 @@ __global__ __launch_bounds__(kDagThreads) void k_dag_nodes(const uint2* __restri
   u32 ex[kDagItems];
 #pragma unroll
   for (int e = 0; e < kDagItems; ++e) {
-    const u32 sz = dag_size(sl[e]);
+    dag_encode(sl[e]);
+    const u32 sz = 8 * sl[e].nh() + sl[e].len();
     u32 incl = sz;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -717,16 +761,12 @@ __global__ __launch_bounds__(kDagThreads) void k_dag_nodes(const uint2* __restri
     u32 o = sh + s_grp[e * (kDagThreads / 64) + wave] + ex[e];
     const DagSlot& s = sl[e];
     const u32 nh = s.nh();
-    for (u32 h = 0; h < nh; ++h) {   // (layers that start here, in order)
-      const u64 cnt = ls.count[s.k() + 1 - int(nh) + int(h)];
-      lds_emit(buf, o, __builtin_bswap64(cnt), 8);
+    if (nh) {   // (the layer's count, big-endian, before its first node)
+      const u64 cnt = ls.count[s.k()];
+      lds_emit(buf, o, __builtin_bswap32(u32(cnt >> 32)), __builtin_bswap32(u32(cnt)), 8);
       o += 8;
     }
-    if (s.valid()) {
-      u32 nx, ny;
-      const u64 vx = ptr_le(s.w.x, nx), vy = ptr_le(s.w.y, ny);
-      lds_emit(buf, o, vx | (vy << (8 * nx)), nx + ny);
-    }
+    if (s.valid()) lds_emit(buf, o, s.w.x, s.w.y, s.len());
   }
   __syncthreads();
   const u32 end = sh + u32(tpre[tile + 1] - tpre[tile]);
@@ -802,6 +842,7 @@ LayerStarts layer_starts(const gcz_ctx* c) {
   const int D = c->info.n_layers;
   for (int k = 0; k <= D; ++k) ls.node[k] = c->layer_off[k];
   for (int k = 0; k < D; ++k) ls.count[k] = c->info.layer_size[k];
+  for (int k = 0; k < D; ++k) ls.cstart[k + 1] = ls.cstart[k] + ls.count[k];
   return ls;
 }
 
@@ -870,6 +911,7 @@ int gcz_sort_device(gcz_ctx* c) {
       (rc = c->ensure(s.hoff, matmax * 4 + 16)) || (rc = c->ensure(s.hrec, nwmax * 2 + 16)) ||
       (rc = c->ensure(s.desc, tilemax * 8 + 16)))
     return rc;
+  if ((rc = c->ensure(s.hpart, size_t(2048) * GCZ_MAX_LAYERS * 8 + 16))) return rc;
   if (scl >= 0 && ((rc = c->ensure(s.hslot, 2 * c->info.layer_size[scl] * 4 + 16)) ||
                    (rc = c->ensure(s.hval, 2 * c->info.layer_size[scl] * 4 + 16)) ||
                    (rc = c->ensure(s.hbs, (u64(hnb[scl]) + 1) * 4 + 16))))
@@ -964,7 +1006,10 @@ int gcz_sort_device(gcz_ctx* c) {
   if (hp.m)
     hipLaunchKernelGGL(k_hist_ranges, dim3(hp.b0[hp.m]), dim3(kBlock), 0, c->stream, hp,
                        reinterpret_cast<const u32*>(nodes), cnt);
-  if (mp.m) hipLaunchKernelGGL(k_minmax_ranges, dim3(mp.b0[mp.m]), dim3(kBlock), 0, c->stream, mp, cnt, mm);
+  if (mp.m) {
+    hipLaunchKernelGGL(k_minmax_ranges, dim3(mp.b0[mp.m]), dim3(kBlock), 0, c->stream, mp, cnt, s.hpart.as<u32>());
+    hipLaunchKernelGGL(k_minmax_fold, dim3(1), dim3(1024), 0, c->stream, mp, s.hpart.as<u32>(), mm);
+  }
   S_HIP(hipGetLastError());
   S_HIP(hipMemcpyAsync(s.h_mm, mm, size_t(D) * 8, hipMemcpyDeviceToHost, c->stream));
   S_HIP(hipStreamSynchronize(c->stream));
@@ -1067,10 +1112,10 @@ int gcz_bytes_device(gcz_ctx* c, uint64_t* out) {
   if (int rc = c->ensure(s.acc, kStatBytes + 8)) return rc;
   S_HIP(hipMemsetAsync(s.acc.ptr, 0, kStatBytes, c->stream));
   const int D = c->info.n_layers;
-  const u64 N = c->layer_off[D];
   const LayerStarts ls = layer_starts(c);
-  hipLaunchKernelGGL(k_node_bytes, dim3(unsigned((N + kDagTile - 1) / kDagTile)), dim3(kDagThreads), 0, c->stream,
-                     c->nodes_out.as<uint2>(), N, ls, D, s.acc.as<unsigned long long>());
+  const u64 M = ls.cstart[D];
+  hipLaunchKernelGGL(k_node_bytes, dim3(unsigned(std::max<u64>(1, (M + kDagTile - 1) / kDagTile))), dim3(kDagThreads),
+                     0, c->stream, c->nodes_out.as<uint2>(), M, ls, D, s.acc.as<unsigned long long>());
   u64* total = s.acc.as<u64>() + kStatBytes / 8;
   hipLaunchKernelGGL(k_stats_sum, dim3(1), dim3(1024), 0, c->stream, s.acc.as<u64>(), total);
   S_HIP(hipGetLastError());
@@ -1087,13 +1132,14 @@ static int serialize_on_device(gcz_ctx* c, unsigned char** d_dag, uint64_t* writ
   if (!c->sortst) c->sortst = new gcz_sort_state();
   gcz_sort_state& s = *c->sortst;
   const int D = c->info.n_layers;
-  const u64 N = c->layer_off[D];
-  for (int k = 0; k < D; ++k)   // (every layer count is written before its first slot)
-    if (c->layer_off[k + 1] <= c->layer_off[k]) return c->fail(GCZ_ERR_ARG, "serialize", "empty node layer");
+  for (int k = 0; k < D; ++k)   // (every layer count is written before its first node)
+    if (c->info.layer_size[k] == 0) return c->fail(GCZ_ERR_ARG, "serialize", "empty node layer");
+  const LayerStarts ls = layer_starts(c);
+  const u64 M = ls.cstart[D];
   const int lb = (c->info.L + 1) / 2;
   const u64 hdr = host_ptr_bytes(c->info.root) + 8 + c->info.n_leaves * u64(lb);
-  const u64 cap = hdr + 8 * u64(D) + 8 * N;   // (pointers of at most 4 bytes)
-  const u64 t = (N + kDagTile - 1) / kDagTile;
+  const u64 cap = hdr + 8 * u64(D) + 8 * M;   // (pointers of at most 4 bytes)
+  const u64 t = (M + kDagTile - 1) / kDagTile;
   const u64 st = scan_tiles(t + 1);
   int rc;
   if ((rc = c->ensure(s.dag, cap + 16)) || (rc = c->ensure(s.desc, std::max<u64>(s.desc.bytes, st * 8 + 16))) ||
@@ -1103,19 +1149,18 @@ static int serialize_on_device(gcz_ctx* c, unsigned char** d_dag, uint64_t* writ
   if (!s.h_tot) S_HIP(hipHostMalloc((void**)&s.h_tot, 8, hipHostMallocDefault));
   hipEvent_t e0{};
   c->prof_begin(KID_DAG, e0);
-  const LayerStarts ls = layer_starts(c);
   unsigned char* out = s.dag.as<unsigned char>();
   u32* tsum = s.cnt.as<u32>();
   u64* tpre = s.keys.as<u64>();   // t + 1 prefixes (the last: the section's size)
   hipLaunchKernelGGL(k_write_leaves, grid_of(c->info.n_leaves), dim3(kBlock), 0, c->stream,
                      c->leaves_out.as<u64>(), c->info.n_leaves, lb, c->info.root, out);
-  hipLaunchKernelGGL(k_dag_sizes, dim3(unsigned(t)), dim3(kDagThreads), 0, c->stream, c->nodes_out.as<uint2>(), N, ls,
+  hipLaunchKernelGGL(k_dag_sizes, dim3(unsigned(t)), dim3(kDagThreads), 0, c->stream, c->nodes_out.as<uint2>(), M, ls,
                      D, tsum);
   S_HIP(hipMemsetAsync(s.desc.ptr, 0, st * 8 + 16, c->stream));
   hipLaunchKernelGGL((k_scan_excl<ScanU32, u64>), dim3(unsigned(st)), dim3(kScanThreads), 0, c->stream,
                      ScanU32{tsum, t}, t + 1, tpre, s.desc.as<u64>(), reinterpret_cast<u32*>(s.desc.as<u64>() + st),
                      static_cast<u64*>(nullptr));
-  hipLaunchKernelGGL(k_dag_nodes, dim3(unsigned(t)), dim3(kDagThreads), 0, c->stream, c->nodes_out.as<uint2>(), N,
+  hipLaunchKernelGGL(k_dag_nodes, dim3(unsigned(t)), dim3(kDagThreads), 0, c->stream, c->nodes_out.as<uint2>(), M,
                      ls, D, hdr, tpre, out);
   S_HIP(hipGetLastError());
   S_HIP(hipMemcpyAsync(s.h_tot, tpre + t, 8, hipMemcpyDeviceToHost, c->stream));
