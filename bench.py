@@ -91,11 +91,13 @@ def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None, bu
     U = n_leaves
     if kernel == "leaf_insert":     # ASCII in, provisional word out, one table sector per strand
         return S * L + 4 * S + 64 * S
-    if kernel == "node_insert":     # pair + child marks in, word out; table sector per hashed pair
+    if kernel == "node_insert":     # pair + child marks in, word out, a table sector: per pair it
+        # inserted (the hashed pairs that did not go through the buckets; bucketed levels
+        # and direct ones return at the gate)
         hashed = (hashed_pairs if hashed_pairs is not None else sum(pk)) - bucketed_pairs
         if hashed <= 0:             # every hashed level went through the buckets: gate-only launches
             return 0
-        return sum(8 * p + 4 * p + 4 * p for p in pk) + 64 * hashed
+        return (8 + 4 + 4 + 64) * hashed
     # bucketed node insert (non-repetitive data, levels of >= 2^20 pairs: layer 0 of
     # uniform_1g): bp = hashed pairs that went through the buckets
     bp = bucketed_pairs
@@ -136,9 +138,9 @@ def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None, bu
     if kernel == "resolve_leaf":    # marks; non-first: word, slot->id sector, word
         return S + (S - U) * (4 + 64 + 4)
     if kernel == "resolve_node":    # marks; non-first: word in and out; the slot and group sectors
-        # of the repeated keys (at most min(repeats, uniques) distinct keys: a hot key's
-        # repeats share its two lines)
-        return sum(p + (p - u) * (4 + 4) + 128 * min(p - u, u) for p, u in lv)
+        # of the repeated keys (at most min(repeats, uniques) distinct keys, and no more lines
+        # than the group array and the table hold: a hot key's repeats share its lines)
+        return sum(p + (p - u) * (4 + 4) + min(128 * min(p - u, u), 16 * ((p + 63) // 64) + 8 * p) for p, u in lv)
     return 0
 
 
@@ -307,6 +309,8 @@ def main():
     ap.add_argument("--config", default="uniform_1g", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--build-only", action="store_true",
+                    help="skip the ratio path and decompression (PMC captures of the build alone)")
     ap.add_argument("--no-weak", action="store_true", help="strong runs at N > 1: skip the weak-scaled timing")
     ap.add_argument("--mode", choices=["weak", "strong", "dist", "replicas"], default="strong",
                     help="N > 1: the config genome itself over N GPUs (strong, the default; 'dist' is an alias), "
@@ -479,11 +483,18 @@ def main():
     dom = max((k for k in kernels if k not in ("clear", "exchange", "dist_local")),
               key=lambda k: kernels[k]["total_ms"])
     dk = kernels[dom]
+    # HBM bytes from the committed PMC capture of this config (scripts/traffic_json.py): per
+    # build for each kernel name, and the whole build's
     traffic = None
+    counter_build = None
     tpath = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tpath) and mode in ("single", "replicas"):
         with open(tpath) as f:
-            traffic = json.load(f).get(dom)
+            tj = json.load(f)
+        per_build = tj.get("per_build", {})
+        if dom in per_build:
+            traffic = int(per_build[dom] / dk["launches"])
+        counter_build = tj.get("build_total")
     roofline = {"bound": "hbm", "kernel": dom,
                 "achieved": round(dk["alg_bytes"] / dk["launches"] / (dk["avg_ms"] * 1e-3) / 1e9, 2),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -492,6 +503,7 @@ def main():
                 "alg_bytes_per_launch": dk["alg_bytes"] // dk["launches"]}
     b_stream, b_table = build_bytes(L, S, info["n_leaves"], info["layer_size"])
     build_frac = (b_stream + b_table) / (info["build_ms"] * 1e-3) / (HBM_PEAK_GBS * 1e9)
+    counter_frac = (counter_build / (info["build_ms"] * 1e-3) / (HBM_PEAK_GBS * 1e9)) if counter_build else None
 
     parity = None
     tree = None
@@ -531,7 +543,7 @@ def main():
 
     # ratio path on the device: frequency sort + bytes() + .dag writer
     ratio_path = None
-    if mode in ("single", "replicas") and rank == 0:
+    if mode in ("single", "replicas") and rank == 0 and not args.build_only:
         # a cold pass (first-call allocations), then the same pass timed on a fresh build
         n = gcz._U64()
         ctx.sync()
@@ -591,7 +603,11 @@ def main():
             "roofline": roofline,
             "build": {"device_ms": info["build_ms"], "hashed_pairs": info["hashed_pairs"],
                       "bucketed_pairs": info.get("bucketed_pairs", 0), "b_stream": b_stream, "b_table": b_table,
-                      "hbm_frac_survey_formula": round(build_frac, 5), "n_leaves": info["n_leaves"],
+                      "hbm_frac_survey_formula": round(build_frac, 5),
+                      # counter HBM bytes of a whole build (PMC capture) over this build's time
+                      "counter_traffic_bytes": counter_build,
+                      "hbm_frac_counter": round(counter_frac, 5) if counter_frac else None,
+                      "n_leaves": info["n_leaves"],
                       "n_layers": info["n_layers"],
                       # builds of the last step (> 1: a bucket / leaf-table overflow rebuilt it;
                       # device_ms is the last attempt, device_ms_all every attempt's)

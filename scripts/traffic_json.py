@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""profiles/traffic_<config>.json from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE captures of
+`bench.py --config <config> --build-only` (scripts/gpu_evidence.sh): HBM bytes per build
+for each of bench.py's kernel names and for the whole build.
+
+usage: traffic_json.py <fetch_dir> <write_dir> <config> <out.json>
+Every launch in the capture belongs to a build (--build-only); builds are counted by
+k_build_init (one per build attempt).  gfx950 correction (MI355X_MICROARCH.md, HBM /
+rocprofv3 section): FETCH_SIZE tallies a 128-B read request as 64 B, so a kernel's bytes
+are 2 x FETCH_SIZE + WRITE_SIZE (both in KiB).
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+from pmc_summary import NAMES, short
+
+EXTRA = {"k_scan_excl": "scan", "k_seg_expand": "node_insert", "k_tail": "tail",
+         "__amd_rocclr_copyBuffer": "copy"}
+
+
+def load(d, counter):
+    acc = defaultdict(float)
+    inits = 0
+    for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
+        if r["Counter_Name"] != counter:
+            continue
+        s = short(r["Kernel_Name"])
+        if s == "k_build_init":
+            inits += 1
+        k = NAMES.get(s, EXTRA.get(s.split("<")[0], s))
+        acc[k] += float(r["Counter_Value"]) * 1024
+    return acc, inits
+
+
+def main():
+    f, nf = load(sys.argv[1], "FETCH_SIZE")
+    w, nw = load(sys.argv[2], "WRITE_SIZE")
+    builds = max(1, min(nf, nw))
+    per = {k: round((2 * f[k] + w[k]) / builds) for k in sorted(set(f) | set(w))}
+    out = {"config": sys.argv[3], "builds": builds, "per_build": per, "build_total": sum(per.values()),
+           "_note": "HBM bytes per build from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of "
+                    "bench.py --build-only (scripts/gpu_evidence.sh), 2 x FETCH_SIZE + WRITE_SIZE "
+                    "(gfx950: FETCH_SIZE tallies a 128-B read as 64 B)"}
+    with open(sys.argv[4], "w") as fo:
+        json.dump(out, fo, indent=1)
+    print(json.dumps({"builds": builds, "build_total": out["build_total"]}))
+
+
+if __name__ == "__main__":
+    main()
