@@ -516,12 +516,13 @@ void shared_tree::build_from_gpu() {
   gcz_info info{};
   gcz_info_get(ctx, &info);
   leaves.resize(info.n_leaves);
-  if (info.n_leaves) check_build(gcz_copy_leaves(ctx, reinterpret_cast<std::uint64_t*>(leaves.data())), ctx);
   nodes.resize(info.n_layers);   // keeps each layer's storage when a device sort refetches the same sizes
+  std::vector<std::uint32_t*> outs(info.n_layers);
   for (int k = 0; k < info.n_layers; ++k) {
     nodes[k].resize(info.layer_size[k]);
-    check_build(gcz_copy_layer(ctx, k, reinterpret_cast<std::uint32_t*>(nodes[k].data())), ctx);
+    outs[k] = reinterpret_cast<std::uint32_t*>(nodes[k].data());
   }
+  check_build(gcz_fetch_host(ctx, reinterpret_cast<std::uint64_t*>(leaves.data()), outs.data()), ctx);
   root = pointer::from_word(info.root);
   device_gen = ++engine().gen;
 }

@@ -1,6 +1,9 @@
 // MI355X (gfx950) shared_tree construction: host orchestration and the C ABI.
 // Device code and the algorithm description: gcz_device.h; the multi-rank
 // build: gcz_dist.hip.
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
 #include <thread>
 
 #include "gcz_ctx.h"
@@ -213,7 +216,7 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
       (rc = ensure(dl_wpre, (nfb + 1) * 4 + 16)) || (rc = ensure(dl_desc, (t_cnt + t_fb) * 8 + 16)) ||
       (rc = ensure(dl_fl, ncodes * 4 + 16)) || (rc = ensure(dl_fo, u64(P.NB) * (P.nch + 1) * 4 + 16)))
     return rc;
-  if (list && ((rc = ensure(dl_lh, std::min(S, ncodes) * 4 + 16)) || (rc = ensure(dl_pb, (ncodes / 64 + 1) * 8))))
+  if (list && ((rc = ensure(dl_fl2, ncodes * 2 + 16)) || (rc = ensure(dl_pb, (ncodes / 64 + 1) * 8))))
     return rc;
   u64* sdesc = dl_desc.as<u64>();
   u32* tickets = reinterpret_cast<u32*>(sdesc + t_cnt + t_fb);
@@ -265,10 +268,16 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
   if (list && (1u << P.IB) < 64) HIP_TRY(hipMemsetAsync(dl_pb.ptr, 0, (ncodes / 64 + 1) * 8, stream));
   hipLaunchKernelGGL(k_dl_first, dim3(P.NB), dim3(kDThreads), first_bytes, stream, dl_rec.as<u32>(), dl_off.as<u32>(),
                      P, list ? nullptr : dl_fpg.as<u32>(), dl_fl.as<u32>(), dl_fo.as<u32>(),
-                     list ? dl_pb.as<unsigned long long>() : nullptr);   // (multi-rank: ids come from gid)
+                     list ? dl_pb.as<unsigned long long>() : nullptr,   // (multi-rank: ids come from gid)
+                     list ? dl_fl2.as<unsigned short>() : nullptr);
   HIP_TRY(hipGetLastError());
+  if (list) {   // multi-rank: the bitmap of r-first keys follows the exchange (dense_rfirst)
+    prof_end(KID_DL_FIRST, e0);
+    return GCZ_OK;
+  }
   hipLaunchKernelGGL(k_dl_fb, dim3(P.nch), dim3(kDThreads), 0, stream, dl_fl.as<u32>(), dl_fo.as<u32>(), P,
-                     dl_fb.as<unsigned long long>());
+                     dl_fb.as<unsigned long long>(), static_cast<const unsigned short*>(nullptr),
+                     static_cast<const unsigned long long*>(nullptr));
   HIP_TRY(hipGetLastError());
   prof_end(KID_DL_FIRST, e0);
   prof_begin(KID_DL_FBSCAN, e0);
@@ -276,11 +285,33 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
                      ScanPopc{dl_fb.as<unsigned long long>()}, nfb, dl_wpre.as<u32>(), sdesc + t_cnt, &tickets[1],
                      ucount);
   HIP_TRY(hipGetLastError());
-  if (list) {
-    hipLaunchKernelGGL(k_dl_lh, dim3(unsigned((S + 255) / 256)), dim3(256), 0, stream, dl_pw.as<u32>(),
-                       dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), S, dl_lh.as<u32>());
-    HIP_TRY(hipGetLastError());
-  }
+  prof_end(KID_DL_FBSCAN, e0);
+  return GCZ_OK;
+}
+
+// Multi-rank (after the presence-bitmap exchange): the first-occurrence bitmap of this
+// rank's r-first keys only (lower = OR of the lower ranks' presence bitmaps), its popcount
+// prefix (*count = the rank's r-first keys) and their hashed codes in position order = global
+// id order (list).
+int gcz_ctx::dense_rfirst(const unsigned long long* lower, u64* count, u32* list) {
+  const DensePlan& P = dl_plan;
+  const u64 S = P.S, nfb = (S + 63) / 64;
+  const u64 t_cnt = scan_tiles(u64(P.NB) * P.nch + 1), t_fb = scan_tiles(nfb + 1);
+  u64* sdesc = dl_desc.as<u64>();
+  u32* tickets = reinterpret_cast<u32*>(sdesc + t_cnt + t_fb);
+  hipEvent_t e0{};
+  prof_begin(KID_DL_FIRST, e0);
+  hipLaunchKernelGGL(k_dl_fb, dim3(P.nch), dim3(kDThreads), 0, stream, dl_fl.as<u32>(), dl_fo.as<u32>(), P,
+                     dl_fb.as<unsigned long long>(), dl_fl2.as<unsigned short>(), lower);
+  HIP_TRY(hipGetLastError());
+  prof_end(KID_DL_FIRST, e0);
+  prof_begin(KID_DL_FBSCAN, e0);
+  hipLaunchKernelGGL(k_scan_excl<ScanPopc>, dim3(unsigned(t_fb)), dim3(kScanThreads), 0, stream,
+                     ScanPopc{dl_fb.as<unsigned long long>()}, nfb, dl_wpre.as<u32>(), sdesc + t_cnt, &tickets[1],
+                     count);
+  hipLaunchKernelGGL(k_dl_lh, dim3(unsigned((S + 255) / 256)), dim3(256), 0, stream, dl_pw.as<u32>(),
+                     dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), S, list);
+  HIP_TRY(hipGetLastError());
   prof_end(KID_DL_FBSCAN, e0);
   return GCZ_OK;
 }
@@ -975,11 +1006,14 @@ void gcz_ctx_destroy(gcz_ctx* c) {
   for (DevBuf* b : {&c->wa, &c->wb, &c->grp, &c->desc, &c->tab, &c->leaves_out, &c->nodes_out, &c->hdr, &c->input,
                     &c->nf, &c->multi, &c->stats, &c->bkt_key, &c->bkt_cnt, &c->bkt_off, &c->bkt_tmp, &c->bkt_rec2, &c->dl_pw,
                     &c->dl_rec, &c->dl_idrec, &c->dl_cnt, &c->dl_off, &c->dl_fpg, &c->dl_fb, &c->dl_wpre,
-                    &c->dl_desc, &c->dl_fl, &c->dl_fo, &c->dl_lh, &c->dl_pb, &c->dl_pbs, &c->dl_lower,
+                    &c->dl_desc, &c->dl_fl, &c->dl_fo, &c->dl_fl2, &c->dl_pb, &c->dl_pbs, &c->dl_lower,
                     &c->dl_pos, &c->dl_list, &c->dl_gid, &c->dl_recv, &c->dl_stage, &c->dl_seg, &c->seg_w,
                     &c->seg_nf, &c->seg_mu, &c->seg_in})
     if (b->ptr) (void)hipFree(b->ptr);
   if (c->h_hdr) (void)hipHostFree(c->h_hdr);
+  if (c->h_ring) (void)hipHostFree(c->h_ring);
+  for (hipEvent_t e : c->ring_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
@@ -1104,18 +1138,151 @@ const uint32_t* gcz_device_layer(gcz_ctx* c, int k) {
   return reinterpret_cast<const uint32_t*>(static_cast<uint2*>(c->nodes_out.ptr) + c->layer_off[k]);
 }
 
+// The whole DAG of the last build into caller-owned host memory (fresh, unpinned pages):
+// DMA into a pinned staging ring (kRingSlots slots of kRingChunk bytes, allocated once per
+// context) while host threads copy the previous slot out, each a slice -- the page faults of
+// the destination are taken by several threads at once and the DMA never waits for them.
+// The runtime's pageable D2H path copies and faults on one thread (~10 GB/s at 1 Gbase).
+namespace {
+constexpr u64 kRingChunk = u64(16) << 20;
+constexpr int kRingSlots = 4;
+
+struct CopyPool {   // T - 1 workers + the calling thread copy one chunk's slices, then meet
+  int T;
+  std::vector<std::thread> th;
+  std::mutex m;
+  std::condition_variable cv, done_cv;
+  const unsigned char* src = nullptr;
+  unsigned char* dst = nullptr;
+  u64 len = 0;
+  u64 gen = 0;
+  int pending = 0;
+  bool stop = false;
+  explicit CopyPool(int t) : T(t) {
+    for (int i = 1; i < T; ++i) th.emplace_back([this, i] { work(i); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(m);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& x : th) x.join();
+  }
+  void slice(int i) {
+    const u64 a = len * u64(i) / u64(T), b = len * u64(i + 1) / u64(T);
+    if (b > a) std::memcpy(dst + a, src + a, b - a);
+  }
+  void work(int i) {
+    u64 seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> lk(m);
+      cv.wait(lk, [&] { return stop || gen != seen; });
+      if (stop) return;
+      seen = gen;
+      lk.unlock();
+      slice(i);
+      lk.lock();
+      if (--pending == 0) done_cv.notify_one();
+    }
+  }
+  void copy(const unsigned char* s, unsigned char* d, u64 n) {
+    if (T == 1 || n < (u64(1) << 20)) {
+      std::memcpy(d, s, n);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(m);
+      src = s; dst = d; len = n;
+      pending = T - 1;
+      ++gen;
+    }
+    cv.notify_all();
+    slice(0);
+    std::unique_lock<std::mutex> lk(m);
+    done_cv.wait(lk, [&] { return pending == 0; });
+  }
+};
+}  // namespace
+
+int gcz_fetch_host(gcz_ctx* c, uint64_t* leaves_out, uint32_t* const* layers_out) {
+  if (!c || c->info.status != GCZ_OK) return GCZ_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  struct Piece { const unsigned char* src; unsigned char* dst; u64 len; };
+  std::vector<Piece> pieces;   // <= kRingChunk each
+  u64 total = 0;
+  auto add = [&](const void* src, void* dst, u64 len) {
+    if (len && !dst) return false;
+    for (u64 o = 0; o < len; o += kRingChunk)
+      pieces.push_back({static_cast<const unsigned char*>(src) + o, static_cast<unsigned char*>(dst) + o,
+                        std::min<u64>(kRingChunk, len - o)});
+    total += len;
+    return true;
+  };
+  if (!add(c->leaves_out.ptr, leaves_out, c->info.n_leaves * 8)) return GCZ_ERR_ARG;
+  for (int k = 0; k < c->info.n_layers; ++k)
+    if (!add(static_cast<uint2*>(c->nodes_out.ptr) + c->layer_off[k], layers_out ? layers_out[k] : nullptr,
+             c->info.layer_size[k] * 8))
+      return GCZ_ERR_ARG;
+  if (pieces.empty()) return GCZ_OK;
+  // a small DAG: one slot holding all of it; else kRingSlots slots of kRingChunk
+  const u64 need = total > kRingChunk ? u64(kRingSlots) * kRingChunk : (total + 4095) & ~u64(4095);
+  if (c->h_ring_bytes < need) {
+    if (c->h_ring) (void)hipHostFree(c->h_ring);
+    c->h_ring = nullptr;
+    c->h_ring_bytes = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_ring), need, hipHostMallocDefault) != hipSuccess)
+      return GCZ_ERR_DEVICE;
+    c->h_ring_bytes = need;
+  }
+  for (hipEvent_t& e : c->ring_ev)
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return GCZ_ERR_DEVICE;
+  const unsigned hc = std::thread::hardware_concurrency();
+  CopyPool pool(total >= (u64(8) << 20) ? int(std::min<unsigned>(8, std::max(1u, hc))) : 1);
+  if (total <= kRingChunk) {   // one D2H batch, then the host copies
+    u64 at = 0;
+    for (const Piece& p : pieces) {
+      if (hipMemcpyAsync(c->h_ring + at, p.src, p.len, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        return GCZ_ERR_DEVICE;
+      at += p.len;
+    }
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return GCZ_ERR_DEVICE;
+    at = 0;
+    for (const Piece& p : pieces) {
+      pool.copy(c->h_ring + at, p.dst, p.len);
+      at += p.len;
+    }
+    return GCZ_OK;
+  }
+  const size_t slots = kRingSlots;
+  auto stage_of = [&](size_t i) { return c->h_ring + (i % slots) * kRingChunk; };
+  auto issue = [&](size_t i) {
+    return hipMemcpyAsync(stage_of(i), pieces[i].src, pieces[i].len, hipMemcpyDeviceToHost, c->stream) ==
+               hipSuccess &&
+           hipEventRecord(c->ring_ev[i % slots], c->stream) == hipSuccess;
+  };
+  for (size_t i = 0; i < pieces.size() && i < slots; ++i)
+    if (!issue(i)) return GCZ_ERR_DEVICE;
+  for (size_t i = 0; i < pieces.size(); ++i) {
+    if (hipEventSynchronize(c->ring_ev[i % slots]) != hipSuccess) return GCZ_ERR_DEVICE;
+    pool.copy(stage_of(i), pieces[i].dst, pieces[i].len);
+    if (i + slots < pieces.size() && !issue(i + slots)) return GCZ_ERR_DEVICE;
+  }
+  return GCZ_OK;
+}
+
 int gcz_tree_fetch(gcz_ctx* c, gcz_tree* t) {
   if (!c || !t || c->info.status != GCZ_OK) return GCZ_ERR_ARG;
   t->L = c->info.L;
   t->root = c->info.root;
   t->leaves.resize(c->info.n_leaves);
-  if (int rc = gcz_copy_leaves(c, t->leaves.data())) return rc;
   t->layers.assign(c->info.n_layers, {});
+  std::vector<uint32_t*> outs(c->info.n_layers);
   for (int k = 0; k < c->info.n_layers; ++k) {
     t->layers[k].resize(2 * c->info.layer_size[k]);
-    if (int rc = gcz_copy_layer(c, k, t->layers[k].data())) return rc;
+    outs[k] = t->layers[k].data();
   }
-  return GCZ_OK;
+  return gcz_fetch_host(c, t->leaves.data(), outs.data());
 }
 
 int gcz_profile_enable(gcz_ctx* c, int on) {

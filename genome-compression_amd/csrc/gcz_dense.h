@@ -310,9 +310,11 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
 // first positions sorted by chunk: fl[b * RB + ...], with fo[ch * NB + b] the start
 // of chunk ch's (a counting sort in LDS; k_dl_fb gathers them per chunk).  pb
 // (multi-rank build, else null): the presence bitmap, bit h set iff hashed code h occurs.
+// fl2 (multi-rank, with pb): each fl entry's code within the bucket, for k_dl_fb's filter.
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_first(const u32* __restrict__ rec, const u32* __restrict__ off,
                                                         DensePlan P, u32* __restrict__ fpg, u32* __restrict__ fl,
-                                                        u32* __restrict__ fo, unsigned long long* __restrict__ pb) {
+                                                        u32* __restrict__ fo, unsigned long long* __restrict__ pb,
+                                                        unsigned short* __restrict__ fl2) {
   extern __shared__ u32 s_dyn[];
   u32* s_fp = s_dyn;                    // RB codes
   u32* s_cnt = s_dyn + (1u << P.IB);    // nch + 1 chunk counters
@@ -361,13 +363,21 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < PER; ++k)
-    if (fp[k] != ~0u) fl[u64(b) * RB + s_cnt[fp[k] >> kDLog] + rk[k]] = fp[k];
+    if (fp[k] != ~0u) {
+      const u64 at = u64(b) * RB + s_cnt[fp[k] >> kDLog] + rk[k];
+      fl[at] = fp[k];
+      if (fl2) fl2[at] = (unsigned short)(u32(k) * kDThreads + tid);
+    }
 }
 
 // First-occurrence bitmap of one chunk: its first positions from every bucket's
 // sorted list (k_dl_first), set in LDS, written as the chunk's 512 bitmap words.
+// lower (multi-rank): only the rank's r-first keys (held by no lower rank, fl2 gives each
+// entry's code) -- the bitmap's popcount ranks are then the r-first keys' local order.
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_fb(const u32* __restrict__ fl, const u32* __restrict__ fo,
-                                                     DensePlan P, unsigned long long* __restrict__ fb) {
+                                                     DensePlan P, unsigned long long* __restrict__ fb,
+                                                     const unsigned short* __restrict__ fl2,
+                                                     const unsigned long long* __restrict__ lower) {
   __shared__ u32 s_bits[kDC / 32];
   const int tid = threadIdx.x;
   const u32 ch = blockIdx.x, RB = 1u << P.IB;
@@ -379,6 +389,16 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
       u32 q[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) q[j] = k0 + j < o1 ? fl[u64(b) * RB + k0 + j] & (kDC - 1) : ~0u;
+      if (lower) {
+        u32 c[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) c[j] = q[j] != ~0u ? fl2[u64(b) * RB + k0 + j] : 0u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const u32 h = (b << P.IB) | c[j];
+          if (q[j] != ~0u && ((lower[h >> 6] >> (h & 63)) & 1ull)) q[j] = ~0u;
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (q[j] != ~0u) atomicOr(&s_bits[q[j] >> 5], 1u << (q[j] & 31));
@@ -529,8 +549,8 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
 // lists (hashed codes in id order) are exchanged so that every rank can look up the
 // global id of each key it holds; rank r's list is also its slice of the leaves.
 
-// Local key list: the hashed code of each first occurrence, in local-id order (the
-// ids of first occurrences increase with position, so the writes are contiguous).
+// Key list: the hashed code of each first occurrence in the bitmap fb (multi-rank: of the
+// r-first keys), in position order = id order (the writes are contiguous).
 [[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_lh(const u32* __restrict__ pw,
                                                      const unsigned long long* __restrict__ fb,
                                                      const u32* __restrict__ wpre, u64 S, u32* __restrict__ lh) {
@@ -540,41 +560,27 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
   if ((m >> (s & 63)) & 1ull) lh[wpre[s >> 6] + u32(__popcll(m & ((1ull << (s & 63)) - 1ull)))] = pw[s] & kIdx;
 }
 
-// (pure-ACGT failure flag, local uniques, repetitive-data flag) for the first exchange
+// (pure-ACGT failure flag, unused, repetitive-data flag) for the first exchange
 [[maybe_unused]] static __global__ void k_dl_vec(const Header* __restrict__ hdr, u64* __restrict__ vec) {
   vec[0] = hdr->dense_fail;
-  vec[1] = hdr->count[0];
+  vec[1] = 0;
   vec[2] = hdr->predup;
 }
 
-// lower = OR of the presence bitmaps of ranks 0 .. r-1 (pbs: R bitmaps of nw words)
-[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_lower(const unsigned long long* __restrict__ pbs, u64 nw, int r,
-                                                  unsigned long long* __restrict__ lower) {
+// the status words behind each rank's bitmap (exchange 1), rank-major into out[3 r + j]
+[[maybe_unused]] static __global__ void k_dl_vecs(const u64* __restrict__ pbs, u64 stride, u64 nw, int R,
+                                                 u64* __restrict__ out) {
+  for (int t = threadIdx.x; t < 3 * R; t += blockDim.x) out[t] = pbs[u64(t / 3) * stride + nw + t % 3];
+}
+
+// lower = OR of the presence bitmaps of ranks 0 .. r-1 (pbs: R blocks of stride words, bitmap first)
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_lower(const unsigned long long* __restrict__ pbs, u64 nw, u64 stride,
+                                                  int r, unsigned long long* __restrict__ lower) {
   const u64 w = u64(blockIdx.x) * 256 + threadIdx.x;
   if (w >= nw) return;
   unsigned long long x = 0;
-  for (int q = 0; q < r; ++q) x |= pbs[u64(q) * nw + w];
+  for (int q = 0; q < r; ++q) x |= pbs[u64(q) * stride + w];
   lower[w] = x;
-}
-
-struct ScanRFirst {   // local key j is r-first: no lower rank holds it
-  const u32* lh;
-  const unsigned long long* lower;
-  u64 n;
-  __device__ __forceinline__ u32 operator()(u64 j) const {
-    if (j >= n) return 0u;
-    const u32 h = lh[j];
-    return ((lower[h >> 6] >> (h & 63)) & 1ull) ? 0u : 1u;
-  }
-};
-
-// the r-first keys in local-id order (= global-id order)
-[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_compact(const u32* __restrict__ lh, const unsigned long long* __restrict__ lower,
-                                                    const u32* __restrict__ pos, u64 n, u32* __restrict__ list) {
-  const u64 j = u64(blockIdx.x) * 256 + threadIdx.x;
-  if (j >= n) return;
-  const u32 h = lh[j];
-  if (!((lower[h >> 6] >> (h & 63)) & 1ull)) list[pos[j]] = h;
 }
 
 // Global ids from the gathered lists: recv holds segments (start, len, global id of

@@ -1485,6 +1485,8 @@ struct Bkt2Plan {
   u32 K, b1, b2, P;    // key bits, coarse / fine bucket bits, position-in-slice bits (log2(SC) + 14)
   u32 SC, nslice;      // chunks per fine slice, slices per coarse bucket
   u64 G;               // part chunks
+  u32* olist;          // owner dedupe (kOwner): the not-first records' indices, appended ...
+  u32* ocnt;           // ... at this cursor (the D records, k_own_getid_list); null: none
 };
 
 // Exclusive prefix of n <= 256 LDS counters in place (one wave, 4 per lane); c[n] = the total.
@@ -1858,6 +1860,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
         if constexpr (kOwner) {
           rec[pos] = first;
           mk.nf[pos] = pos != first ? 7 : 6;
+          if (bp.olist && pos != first) bp.olist[atomicAdd(bp.ocnt, 1u)] = pos;
         } else if (pos != first) {
           mk.nf[pos] = kNfNot;
           rec[pos] = first | (rec[pos] & kBits);
@@ -1915,6 +1918,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
     if constexpr (kOwner) {
       rec[pos[e]] = first;
       mk.nf[pos[e]] = pos[e] != first ? 7 : 6;
+      if (bp.olist && pos[e] != first) bp.olist[atomicAdd(bp.ocnt, 1u)] = pos[e];
     } else if (pos[e] != first) {
       mk.nf[pos[e]] = kNfNot;
       rec[pos[e]] = first | (rec[pos[e]] & kBits);

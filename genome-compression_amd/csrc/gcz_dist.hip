@@ -28,9 +28,9 @@ using namespace gcz_dev;
 using namespace gcz_host;
 
 struct gcz_dist_state {
-  DevBuf scratch, gnf, gmul, gid, blockcnt, bchunk, skey, sidx, sflag, scval, sdval;   // sender side
+  DevBuf scratch, gnf, gmul, gid, blockcnt, bchunk, skey, sidx, sflag, scval, sdval, clist;   // sender side
   DevBuf dict;                                                                // rank 0's leaf dictionary
-  DevBuf rkey, oslot, rflag, rcval, rdval, owntab, oids, omin;                // owner side
+  DevBuf rkey, oslot, rflag, rcval, rdval, owntab, oids, omin, olist;         // owner side
   DevBuf ob_cnt, ob_off, ob_desc, ob_rec;                                      // owner bucketed dedupe
   DevBuf ob_seg, ob_rt, ob_rec2, ob_fo;                                        // ... as the two-pass partition
   DevBuf dhdr, gath, gath2, gathf, ddesc, tail_in;
@@ -47,7 +47,7 @@ void gcz_dist_state_free(gcz_ctx* c) {
   gcz_dist_state* d = c->dist;
   if (!d) return;
   for (DevBuf* b : {&d->dict, &d->scratch, &d->gnf, &d->gmul, &d->gid, &d->blockcnt, &d->bchunk, &d->skey, &d->sidx, &d->sflag,
-                    &d->scval, &d->sdval, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab, &d->oids,
+                    &d->scval, &d->sdval, &d->clist, &d->olist, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab, &d->oids,
                     &d->omin, &d->ob_cnt, &d->ob_off, &d->ob_desc, &d->ob_rec, &d->ob_seg, &d->ob_rt,
                     &d->ob_rec2, &d->ob_fo,
                     &d->dhdr, &d->gath, &d->gath2, &d->gathf, &d->ddesc, &d->tail_in})
@@ -500,6 +500,7 @@ struct RankLevel {
   bool counted = false;                   // k_node_keys wrote the bucketing's tile counts
   const unsigned char* gmark = nullptr;   // leaf level: kNfGlobal strands already hold global ids
   bool identity = false;                  // rank 0's leaf level: local ids are the global ids
+  bool keys_zeroed = false;               // k_node_keys zeroed gnf / gmul and the rank scan's descriptors
 };
 }  // namespace
 
@@ -621,6 +622,7 @@ int gcz_group::alloc(int i, u64 leaf_cap) {
   if ((rc = c->ensure(d.sflag, u))) return rc;
   if ((rc = c->ensure(d.scval, u * 8))) return rc;
   if ((rc = c->ensure(d.sdval, u * 8))) return rc;
+  if ((rc = c->ensure(d.clist, u * 4))) return rc;
   if ((rc = c->ensure(d.dhdr, sizeof(DistHdr)))) return rc;
   if ((rc = c->ensure(d.gath, size_t(world) * kSyncWords * 8))) return rc;
   if ((rc = c->ensure(d.gath2, size_t(world) * (2 + 2 * kMaxRanks) * 8))) return rc;
@@ -645,8 +647,14 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
   const DistPlan& P = plan;
   const u64 ncodes = u64(1) << (2 * L);
   const u64 nw = (ncodes + 63) / 64;   // presence bitmap words
+  const u64 nwb = nw + 4;               // + the rank's status words (vec) behind its bitmap
   std::vector<LeafLevel> las(NL);
-  // A. every rank's local first occurrences, key list and presence bitmap
+  // A. every rank's local first occurrences, key list and presence bitmap.  The status words
+  // (pure ACGT? / local uniques / repetitive?) ride behind the bitmap, so exchange 1 is one
+  // allgather; a rank that fails here still joins it with a failure word (vec[0] = 2), so its
+  // peers leave together instead of waiting in a collective it never enters (RCCL has no
+  // timeout).
+  int local_rc = 0;
   for (int i = 0; i < NL; ++i) {
     gcz_ctx* cx = ctx[i];
     LeafLevel& la = las[i];
@@ -655,66 +663,68 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
     la.S = P.count(rank[i], 0);
     la.L = L;
     la.words = cx->wa.as<u32>();
+    if (cx->ensure(cx->dl_seg, size_t(64 + 3 * R) * 8 + size_t(R) * R * sizeof(DlSeg) + 64) ||
+        cx->ensure(cx->dl_pb, nwb * 8) || cx->ensure(cx->dl_pbs, size_t(R) * nwb * 8 + 16) ||
+        cx->ensure(cx->dl_lower, nw * 8 + 16))
+      return dev_fail("dense leaf buffers");   // (no word to send: nothing else can be done)
+    u64* vec = cx->dl_pb.as<u64>() + nw;
     bool u = false;
     Header* h = cx->hdr.as<Header>();
-    if (int rc = cx->dense_phase_a(la, h, &h->count[0], false, true, &u)) return rc == GCZ_ERR_DEVICE ? dev_fail("dense leaves") : rc;
-    if (!u) return GCZ_OK;   // L or sizes outside the dense level (the same on every rank)
-    if (cx->ensure(cx->dl_seg, size_t(64 + 3 * R) * 8 + size_t(R) * R * sizeof(DlSeg) + 64) ||
-        cx->ensure(cx->dl_pbs, size_t(R) * nw * 8 + 16) || cx->ensure(cx->dl_lower, nw * 8 + 16))
-      return dev_fail("dense leaf buffers");
-    u64* vec = cx->dl_seg.as<u64>();
+    const int rc = cx->dense_phase_a(la, h, &h->count[0], false, true, &u);
+    if (!rc && !u) return GCZ_OK;   // L or sizes outside the dense level (the same on every rank)
+    if (rc) {
+      local_rc = rc;
+      static const u64 failed_vec[3] = {2, 0, 0};
+      G_HIP(hipMemcpyAsync(vec, failed_vec, sizeof(failed_vec), hipMemcpyHostToDevice, cx->stream));
+      continue;
+    }
     hipLaunchKernelGGL(k_dl_vec, dim3(1), dim3(1), 0, cx->stream, h, vec);
     G_HIP(hipGetLastError());
   }
-  // exchange 1: (pure ACGT?, local uniques, repetitive?) and the presence bitmaps
+  if (local_rc && NL == R) return local_rc == GCZ_ERR_DEVICE ? dev_fail("dense leaves") : local_rc;
+  // exchange 1: the presence bitmaps with the status words
   {
-    std::vector<const void*> s, s2;
-    std::vector<void*> rv, rv2;
+    std::vector<const void*> s;
+    std::vector<void*> rv;
     for (gcz_ctx* cx : ctx) {
-      s.push_back(cx->dl_seg.as<u64>());
-      rv.push_back(cx->dl_seg.as<u64>() + 8);
-      s2.push_back(cx->dl_pb.ptr);
-      rv2.push_back(cx->dl_pbs.ptr);
+      s.push_back(cx->dl_pb.ptr);
+      rv.push_back(cx->dl_pbs.ptr);
     }
     hipEvent_t e0{};
     ctx[0]->prof_begin(KID_EXCHANGE, e0);
-    G_RC(tr->allgather(24, s, rv));
-    G_RC(tr->allgather(nw * 8, s2, rv2));
+    G_RC(tr->allgather(nwb * 8, s, rv));
     ctx[0]->prof_end(KID_EXCHANGE, e0);
   }
   std::vector<u64> hv(size_t(3) * R + 8);
+  hipLaunchKernelGGL(k_dl_vecs, dim3(1), dim3(64), 0, ctx[0]->stream, ctx[0]->dl_pbs.as<u64>(), nwb, nw, R,
+                     ctx[0]->dl_seg.as<u64>() + 8);
+  G_HIP(hipGetLastError());
   G_HIP(hipMemcpyAsync(hv.data(), ctx[0]->dl_seg.as<u64>() + 8, size_t(3) * R * 8, hipMemcpyDeviceToHost,
                        ctx[0]->stream));
   for (gcz_ctx* cx : ctx) G_HIP(hipStreamSynchronize(cx->stream));
-  std::vector<u64> U(R);
+  for (int r = 0; r < R; ++r)
+    if (hv[3 * r] == 2) return local_rc && local_rc != GCZ_ERR_DEVICE ? local_rc : dev_fail("dense leaves (a rank failed)");
   bool pred = false;
   for (int r = 0; r < R; ++r) {
     if (hv[3 * r]) return GCZ_OK;   // some rank holds a non-ACGT strand: the hash-table leaf level
-    U[r] = hv[3 * r + 1];
     pred = pred || hv[3 * r + 2] != 0;
   }
   any_predup = pred;
-  // r-first keys (held by no lower rank) in local-id order = global-id order
+  // r-first keys (held by no lower rank): their first-occurrence bitmap, count and codes in
+  // position order = global-id order (rank 0: all its keys)
   for (int i = 0; i < NL; ++i) {
     gcz_ctx* cx = ctx[i];
     const int r = rank[i];
-    const u64 ur = U[r], t = scan_tiles(ur + 1);
-    ProfScope ps_(cx, KID_IDS);
-    if (cx->ensure(cx->dl_pos, (ur + 1) * 4 + t * 8 + 64) || cx->ensure(cx->dl_list, ur * 4 + 16))
-      return dev_fail("dense leaf lists");
-    u32* pos = cx->dl_pos.as<u32>();
-    u64* desc = reinterpret_cast<u64*>(pos + ((ur + 1 + 1) & ~u64(1)));
-    u32* ticket = reinterpret_cast<u32*>(desc + t);
-    G_HIP(hipMemsetAsync(desc, 0, t * 8 + 8, cx->stream));
-    hipLaunchKernelGGL(k_dl_lower, dim3(unsigned((nw + 255) / 256)), dim3(256), 0, cx->stream,
-                       cx->dl_pbs.as<unsigned long long>(), nw, r, cx->dl_lower.as<unsigned long long>());
-    hipLaunchKernelGGL(k_scan_excl<ScanRFirst>, dim3(unsigned(t)), dim3(kScanThreads), 0, cx->stream,
-                       ScanRFirst{cx->dl_lh.as<u32>(), cx->dl_lower.as<unsigned long long>(), ur}, ur + 1, pos, desc,
-                       ticket, cx->dl_seg.as<u64>() + 4);
-    if (ur)
-      hipLaunchKernelGGL(k_dl_compact, dim3(unsigned((ur + 255) / 256)), dim3(256), 0, cx->stream, cx->dl_lh.as<u32>(),
-                         cx->dl_lower.as<unsigned long long>(), pos, ur, cx->dl_list.as<u32>());
-    G_HIP(hipGetLastError());
+    if (cx->ensure(cx->dl_list, std::min<u64>(P.count(r, 0), ncodes) * 4 + 16)) return dev_fail("dense leaf lists");
+    if (r > 0) {
+      ProfScope ps_(cx, KID_IDS);
+      hipLaunchKernelGGL(k_dl_lower, dim3(unsigned((nw + 255) / 256)), dim3(256), 0, cx->stream,
+                         cx->dl_pbs.as<unsigned long long>(), nw, nwb, r, cx->dl_lower.as<unsigned long long>());
+      G_HIP(hipGetLastError());
+    }
+    if (cx->dense_rfirst(r > 0 ? cx->dl_lower.as<unsigned long long>() : nullptr, cx->dl_seg.as<u64>() + 4,
+                         cx->dl_list.as<u32>()))
+      return dev_fail("dense leaves (r-first keys)");
   }
   // exchange 2: r-first counts -> id offsets
   {
@@ -900,6 +910,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
   };
   std::vector<OwnTab> otab(NL);
   std::vector<LevelTab> opos(NL);
+  std::vector<char> olisted(NL, 0);   // the owner dedupe listed its not-first records (k_own_getid_list)
 
   auto send_displ_of = [&](int r) {   // destination segments of rank r's send buffer
     Displ D{};
@@ -921,7 +932,8 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       const u64 nr = recvd(rank[i]);
       int rc;
       if ((rc = cx->ensure(d.rkey, nr * 8 + 16)) || (rc = cx->ensure(d.oslot, nr * 4 + 16)) ||
-          (rc = cx->ensure(d.rflag, nr + 16)) || (rc = cx->ensure(d.rcval, nr * 8 + 16)) ||
+          (rc = cx->ensure(d.rflag, nr + 32)) || (rc = cx->ensure(d.rcval, nr * 8 + 16)) ||
+          (rc = cx->ensure(d.olist, nr * 4 + 16)) ||
           (rc = cx->ensure(d.rdval, nr * 8 + 16)))
         return dev_fail("exchange buffers");
       const u64 cap = std::max<u64>(256, next_pow2(2 * nr));
@@ -996,6 +1008,8 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
         b2.SC = 1u << log2_exact(b2.SC);
         b2.P = kPartLog + log2_exact(b2.SC);
         b2.nslice = u32((b2.G + b2.SC - 1) / b2.SC);
+        b2.olist = d.olist.as<u32>();
+        b2.ocnt = &d.dhdr.as<DistHdr>()->lcnt[1];
         use_ob2 = key_bits >= bb && b2.b2 <= u32(kFineMaxB2) && key_bits - b2.b1 + kPartLog <= 64 &&
                   key_bits - bb + b2.P <= 64 && mean_run * b2.SC <= u64(kFineCap) / 2 && b2.nslice <= 512;
       }
@@ -1005,8 +1019,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       if (opos[i].packed) {
         unsigned char* onf = d.omin.as<unsigned char>();
         unsigned char* omul = onf + nr + 32;
-        if (use_ob2) G_HIP(hipMemsetAsync(d.rflag.ptr, 0, nr + 16, cx->stream));   // (the reply, written directly)
-        else G_HIP(hipMemsetAsync(onf, 0, 2 * nr + 64, cx->stream));
+        if (!use_ob2) G_HIP(hipMemsetAsync(onf, 0, 2 * nr + 64, cx->stream));   // (ob2: k_ob_part zeroes the reply)
         if (use_ob2) {
           const u64 nfine = (u64(1) << b2.b1) * b2.nslice;
           if (cx->ensure(d.ob_seg, b2.G * kPartChunk * 8) || cx->ensure(d.ob_rt, b2.G * ((u64(1) << b2.b1) + 1) * 4 + 16) ||
@@ -1018,10 +1031,12 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
                                     hipFuncAttributeMaxDynamicSharedMemorySize, int(kFineCap * 8)));
           u32* ovf = &cx->hdr.as<Header>()->overflow;
           hipLaunchKernelGGL(k_ob_part, dim3(unsigned(b2.G)), dim3(kBktThreads), size_t(kPartChunk) * 8, cx->stream,
-                             d.rkey.as<u64>(), nr, b2, child_bits, d.ob_seg.as<u64>(), d.ob_rt.as<u32>());
+                             d.rkey.as<u64>(), nr, b2, child_bits, d.ob_seg.as<u64>(), d.ob_rt.as<u32>(),
+                             d.rflag.as<unsigned char>());
           hipLaunchKernelGGL(k_bkt_fine, dim3(unsigned(nfine)), dim3(kBktThreads), size_t(kFineCap) * 8, cx->stream,
                              d.ob_seg.as<u64>(), d.ob_rt.as<u32>(), b2, d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(),
                              static_cast<Header*>(nullptr), static_cast<const u64*>(nullptr), nr, ovf);
+          olisted[i] = 1;
           hipLaunchKernelGGL(k_bkt_dedupe2<true>, dim3(unsigned(u64(1) << (b2.b1 + b2.b2))), dim3(kBktThreads), 0,
                              cx->stream, d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(), b2, d.oslot.as<u32>(),
                              Marks{d.rflag.as<unsigned char>(), nullptr}, static_cast<Header*>(nullptr),
@@ -1081,20 +1096,22 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     const u64 ur = u[rank[i]];
     DistHdr* dh = d.dhdr.as<DistHdr>();
     ProfScope ps_(cx, KID_IDS);
-    G_HIP(hipMemsetAsync(d.gnf.ptr, 0, ur + 1, cx->stream));
-    G_HIP(hipMemsetAsync(d.gmul.ptr, 0, ur + 1, cx->stream));
+    if (!lv[i].keys_zeroed) {   // (k_node_keys zeroed them, and the rank scan's descriptors)
+      G_HIP(hipMemsetAsync(d.gnf.ptr, 0, ur + 1, cx->stream));
+      G_HIP(hipMemsetAsync(d.gmul.ptr, 0, ur + 1, cx->stream));
+    }
     if (records) {
       const u64 ns = sent(rank[i]);
       hipLaunchKernelGGL(k_dist_flags, tiles(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
                          d.sflag.as<unsigned char>(), d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(),
-                         send_displ_of(rank[i]), u32(R), &dh->sync2[1]);
+                         send_displ_of(rank[i]), u32(R), &dh->sync2[1], d.clist.as<u32>(), &dh->lcnt[0]);
       if (lookahead && nwords[i] > 0)
         hipLaunchKernelGGL(k_lookahead, blocks((nwords[i] + 1) / 2), dim3(kBlock), 0, cx->stream,
                            d.gmul.as<unsigned char>(), nwords[i], &dh->sync2[1 + 2 * R]);
       G_HIP(hipGetLastError());
     }
     const u64 tiles = std::max<u64>(1, tiles_of(ur));
-    G_HIP(hipMemsetAsync(d.ddesc.ptr, 0, tiles * 8, cx->stream));
+    if (!lv[i].keys_zeroed) G_HIP(hipMemsetAsync(d.ddesc.ptr, 0, tiles * 8, cx->stream));
     if (lv[i].leaves)
       hipLaunchKernelGGL((k_dist_rank<u64>), dim3(unsigned(tiles)), dim3(kBlock), 0, cx->stream,
                          d.gnf.as<unsigned char>(), lv[i].ucount, d.gid.as<u32>(), d.ddesc.as<u64>(), &dh->ticket,
@@ -1162,11 +1179,13 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     for (int i = 0; i < NL; ++i) {
       gcz_ctx* cx = ctx[i];
       gcz_dist_state& d = *cx->dist;
-      const u64 ns = sent(rank[i]);
       ProfScope ps_(cx, KID_IDS);
-      hipLaunchKernelGGL(k_dist_cvals, tiles(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
-                         send_displ_of(rank[i]), u32(R), d.sflag.as<unsigned char>(), d.gid.as<u32>(),
-                         u32(off[rank[i]]), d.dhdr.as<DistHdr>()->ccur, d.scval.as<u64>());
+      u64 nci = 0;   // this rank's C records (k_dist_flags' list)
+      for (int q = 0; q < R; ++q) nci += MC[size_t(rank[i]) * R + q];
+      if (nci)
+        hipLaunchKernelGGL(k_dist_cvals, blocks(nci), dim3(kBlock), 0, cx->stream, d.clist.as<u32>(), nci,
+                           d.sidx.as<u32>(), send_displ_of(rank[i]), u32(R), d.gid.as<u32>(), u32(off[rank[i]]),
+                           d.dhdr.as<DistHdr>()->ccur, d.scval.as<u64>());
       G_HIP(hipGetLastError());
       s.push_back(d.scval.ptr);
       rv.push_back(d.rcval.ptr);
@@ -1180,10 +1199,12 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     for (int i = 0; i < NL; ++i) {
       gcz_ctx* cx = ctx[i];
       gcz_dist_state& d = *cx->dist;
-      const u64 nr = recvd(rank[i]);
       ProfScope ps_(cx, KID_OWNER);
-      hipLaunchKernelGGL(k_own_setid, blocks(nr), dim3(kBlock), 0, cx->stream, d.rcval.as<u64>(), nr,
-                         displ_of(rank[i]), counts_from(MC, rank[i], true), u32(R), d.oslot.as<u32>(), otab[i]);
+      u64 nco = 0;   // C records for this owner
+      for (int q = 0; q < R; ++q) nco += MC[size_t(q) * R + rank[i]];
+      if (nco)
+        hipLaunchKernelGGL(k_own_setid, blocks(nco), dim3(kBlock), 0, cx->stream, d.rcval.as<u64>(), nco,
+                           displ_of(rank[i]), counts_from(MC, rank[i], true), u32(R), d.oslot.as<u32>(), otab[i]);
       G_HIP(hipGetLastError());
     }
   }
@@ -1195,9 +1216,18 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       gcz_dist_state& d = *cx->dist;
       const u64 nr = recvd(rank[i]);
       ProfScope ps_(cx, KID_OWNER);
-      hipLaunchKernelGGL(k_own_getid, tiles(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr,
-                         displ_of(rank[i]), u32(R), d.rflag.as<unsigned char>(), otab[i],
-                         d.dhdr.as<DistHdr>()->dcur, d.rdval.as<u64>());
+      u64 ndo = 0;   // D records from this owner
+      for (int q = 0; q < R; ++q) ndo += MD[size_t(q) * R + rank[i]];
+      if (olisted[i]) {
+        if (ndo)
+          hipLaunchKernelGGL(k_own_getid_list, blocks(ndo), dim3(kBlock), 0, cx->stream, d.olist.as<u32>(), ndo,
+                             d.oslot.as<u32>(), displ_of(rank[i]), u32(R), otab[i], d.dhdr.as<DistHdr>()->dcur,
+                             d.rdval.as<u64>());
+      } else {
+        hipLaunchKernelGGL(k_own_getid, tiles(nr), dim3(kBlock), 0, cx->stream, d.oslot.as<u32>(), nr,
+                           displ_of(rank[i]), u32(R), d.rflag.as<unsigned char>(), otab[i],
+                           d.dhdr.as<DistHdr>()->dcur, d.rdval.as<u64>());
+      }
       G_HIP(hipGetLastError());
       s.push_back(d.rdval.ptr);
       rv.push_back(d.sdval.ptr);
@@ -1211,11 +1241,13 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     for (int i = 0; i < NL; ++i) {
       gcz_ctx* cx = ctx[i];
       gcz_dist_state& d = *cx->dist;
-      const u64 ns = sent(rank[i]);
       ProfScope ps_(cx, KID_IDS);
-      hipLaunchKernelGGL(k_dist_dvals, blocks(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
-                         send_displ_of(rank[i]), counts_from(MD, rank[i], false), u32(R), d.sdval.as<u64>(),
-                         d.gid.as<u32>());
+      u64 ndi = 0;   // D records for this rank
+      for (int q = 0; q < R; ++q) ndi += MD[size_t(rank[i]) * R + q];
+      if (ndi)
+        hipLaunchKernelGGL(k_dist_dvals, blocks(ndi), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ndi,
+                           send_displ_of(rank[i]), counts_from(MD, rank[i], false), u32(R), d.sdval.as<u64>(),
+                           d.gid.as<u32>());
       G_HIP(hipGetLastError());
     }
   }
@@ -1299,10 +1331,13 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         G_HIP(hipEventCreate(&cx->ev_stop));
       }
       G_HIP(hipEventRecord(cx->ev_start, cx->stream));
-      Header* h = cx->hdr.as<Header>();
-      G_HIP(hipMemsetAsync(h, 0, sizeof(Header), cx->stream));
-      G_HIP(hipMemsetAsync(&h->err_offset, 0xff, 8, cx->stream));
-      G_HIP(hipMemsetAsync(cx->desc.ptr, 0, cx->desc.bytes, cx->stream));
+      InitPlan ip{};   // header (err_offset = ~0) and the look-back descriptors, one launch
+      ip.hdr = cx->hdr.as<Header>();
+      ip.desc = cx->desc.as<uint4>();
+      ip.ndesc16 = cx->desc.bytes / 16;
+      hipLaunchKernelGGL(k_build_init, dim3(unsigned(std::min<u64>(1024, std::max<u64>(1, (ip.ndesc16 + kBlock - 1) / kBlock)))),
+                         dim3(kBlock), 0, cx->stream, ip);
+      G_HIP(hipGetLastError());
     }
     // per-rank descriptor cursors
     std::vector<u64> dcur(NL, 0);
@@ -1562,7 +1597,10 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
           hipLaunchKernelGGL(k_node_keys, dim3(nb), dim3(kBlock), 0, cx->stream, cur_in[i], n, p, cur_out[i],
                              cx->dist->scratch.as<uint2>(), cx->nf_set[cs], cx->multi_set[cs], na.count,
                              tr ? cx->dist->gid.as<u32>() : nullptr, tr ? leaf_offs[i] : 0u, rl.src,
-                             cx->dist->blockcnt.as<u32>(), nb, tr ? leaf_gmark[i] : nullptr);
+                             cx->dist->blockcnt.as<u32>(), nb, tr ? leaf_gmark[i] : nullptr,
+                             cx->dist->gnf.as<unsigned char>(), cx->dist->gmul.as<unsigned char>(),
+                             cx->dist->ddesc.as<u64>());
+          rl.keys_zeroed = true;
           G_HIP(hipGetLastError());
         }
       }

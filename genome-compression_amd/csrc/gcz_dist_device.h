@@ -44,7 +44,8 @@ struct DistHdr {
   u64 tot[4];                           // selected counts of the four compaction scans
   u32 ticket;                           // look-back tickets of k_dist_rank
   u32 tick[4];                          // ... of the compaction scans
-  u32 pad[3];
+  u32 lcnt[2];                          // list lengths: C records (sender), D records (owner dedupe)
+  u32 pad;
   u32 ccur[kMaxRanks + 1];              // append cursors: C records per owner (sender side)
   u32 dcur[kMaxRanks + 1];              // ... D records per source (owner side)
   u64 cell[GCZ_MAX_LAYERS + 1];         // direct flags: n_local when the layer is direct, else ~0
@@ -495,12 +496,18 @@ struct OwnBkt {
 // h = T.mix(packed key) in LDS and writes the records back contiguously with the chunk's
 // run table -- whole runs instead of k_ob_scatter's scattered 8-B stores.
 static __global__ __launch_bounds__(kBktThreads) void k_ob_part(const u64* __restrict__ rkey, u64 nr, Bkt2Plan bp,
-                                                                u32 B, u64* __restrict__ seg, u32* __restrict__ rt) {
+                                                                u32 B, u64* __restrict__ seg, u32* __restrict__ rt,
+                                                                unsigned char* __restrict__ rflag) {
   extern __shared__ u64 stage[];   // kPartChunk records (dynamic)
   __shared__ u32 cur[(1u << kPartMaxB1) + 1];
   const u32 nb1 = 1u << bp.b1;
   for (u32 q = threadIdx.x; q <= nb1; q += kBktThreads) cur[q] = 0;
   const u64 g = blockIdx.x, j0 = g * kPartChunk;
+  {   // the reply flags of this chunk's records start at 0 (the dedupe writes the repeats'); 16 B a store
+    const u64 end = blockIdx.x + 1 == gridDim.x ? nr + 16 : j0 + kPartChunk;   // (rflag holds nr + 32 bytes)
+    const u64 e0 = j0 / 16, e1 = (end + 15) / 16;
+    for (u64 e = e0 + threadIdx.x; e < e1; e += kBktThreads) reinterpret_cast<uint4*>(rflag)[e] = make_uint4(0, 0, 0, 0);
+  }
   u64 x[kPartItems];
 #pragma unroll
   for (int e = 0; e < kPartItems; ++e) {
@@ -693,14 +700,19 @@ __device__ __forceinline__ u32 wave_append(u32* __restrict__ cur, u32 q, bool wa
 }
 
 // C at the owner: the first holder's global id of every shared key.  cnt.d[s] = C records
-// from source s, packed at the start of s's segment.
-static __global__ __launch_bounds__(kBlock) void k_own_setid(const u64* __restrict__ rc, u64 nrecv, Displ D,
+// from source s, packed at the start of s's segment; the grid covers their sum only.
+__device__ __forceinline__ u64 packed_at(const Displ& D, const Displ& cnt, u32 R, u64 i) {   // i-th packed record
+  u32 s = 0;
+  while (s + 1 < R && i >= cnt.d[s]) i -= cnt.d[s++];
+  return D.d[s] + i;
+}
+static __global__ __launch_bounds__(kBlock) void k_own_setid(const u64* __restrict__ rc, u64 ntot, Displ D,
                                                              Displ cnt, u32 R, const u32* __restrict__ oslot,
                                                              OwnTab T) {
-  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (k >= nrecv) return;
+  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= ntot) return;
+  const u64 k = packed_at(D, cnt, R, i);
   const u32 s = seg_of(D, R, k);
-  if (k - D.d[s] >= cnt.d[s]) return;
   const u64 v = rc[k];
   own_set_id(T, oslot[D.d[s] + u32(v)], u32(v >> 32));
 }
@@ -751,6 +763,20 @@ static __global__ __launch_bounds__(kBlock) void k_own_getid(const u32* __restri
       [&](u64 k, u32 s, u32 slot) { dval[D.d[s] + slot] = u64(k - D.d[s]) | (u64(own_id(T, oslot[k])) << 32); });
 }
 
+// ... the same from the owner dedupe's list of not-first records (k_bkt_dedupe2<true>), in
+// any order: the D records of a segment need no order.
+static __global__ __launch_bounds__(kBlock) void k_own_getid_list(const u32* __restrict__ list, u64 n,
+                                                                  const u32* __restrict__ oslot, Displ D, u32 R,
+                                                                  OwnTab T, u32* __restrict__ dcur,
+                                                                  u64* __restrict__ dval) {
+  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const u32 k = list[i];
+  const u32 s = seg_of(D, R, k);
+  const u32 slot = atomicAdd(&dcur[s], 1u);
+  dval[D.d[s] + slot] = u64(k - D.d[s]) | (u64(own_id(T, oslot[k])) << 32);
+}
+
 // ---- sender side ---------------------------------------------------------------
 
 // Reply flags -> per local unique (gnf: not globally first, gmul: repeats globally), and
@@ -760,7 +786,8 @@ static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restr
                                                               const unsigned char* __restrict__ sflag,
                                                               unsigned char* __restrict__ gnf,
                                                               unsigned char* __restrict__ gmul, Displ SD, u32 R,
-                                                              u64* __restrict__ cnt) {
+                                                              u64* __restrict__ cnt, u32* __restrict__ clist,
+                                                              u32* __restrict__ lcnt) {
   __shared__ u32 hc[kMaxRanks], hd[kMaxRanks];
   const int tid = threadIdx.x;
   if (tid < int(R)) { hc[tid] = 0; hd[tid] = 0; }
@@ -787,6 +814,8 @@ static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restr
       const u32 q = (want_c(f) || want_d(f)) ? seg_of(SD, R, k) : 0u;
       (void)wave_append(hc, q, k < nsent && want_c(f));
       (void)wave_append(hd, q, k < nsent && want_d(f));
+      const u32 cs = wave_append(lcnt, 0u, k < nsent && want_c(f));   // (k_dist_cvals' list)
+      if (k < nsent && want_c(f)) clist[cs] = u32(k);
     }
   }
   __syncthreads();
@@ -842,31 +871,29 @@ __global__ __launch_bounds__(kBlock) void k_dist_rank(const unsigned char* __res
   }
 }
 
-// C at the sender: the first holder of a shared key sends (segment index, global id).
-static __global__ __launch_bounds__(kBlock) void k_dist_cvals(const u32* __restrict__ sidx, u64 nsent, Displ SD,
-                                                              u32 R, const unsigned char* __restrict__ sflag,
+// C at the sender: the first holder of a shared key sends (segment index, global id); the
+// grid covers k_dist_flags' list of those records only.
+static __global__ __launch_bounds__(kBlock) void k_dist_cvals(const u32* __restrict__ clist, u64 n,
+                                                              const u32* __restrict__ sidx, Displ SD, u32 R,
                                                               const u32* __restrict__ gid, u32 off,
                                                               u32* __restrict__ ccur, u64* __restrict__ cval) {
-  tile_append(
-      nsent, R, ccur,
-      [&](u64 k, u32& q) {
-        if (!want_c(sflag[k])) return false;
-        q = seg_of(SD, R, k);
-        return true;
-      },
-      [&](u64 k, u32 q, u32 slot) {
-        cval[SD.d[q] + slot] = u64(k - SD.d[q]) | (u64(off + (gid[sidx[k]] & ~kLocalId)) << 32);
-      });
+  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const u32 k = clist[i];
+  const u32 q = seg_of(SD, R, k);
+  const u32 slot = atomicAdd(&ccur[q], 1u);
+  cval[SD.d[q] + slot] = u64(k - SD.d[q]) | (u64(off + (gid[sidx[k]] & ~kLocalId)) << 32);
 }
 
-// D at the sender: cnt.d[q] records from owner q, packed at the start of q's segment.
-static __global__ __launch_bounds__(kBlock) void k_dist_dvals(const u32* __restrict__ sidx, u64 nsent, Displ SD,
+// D at the sender: cnt.d[q] records from owner q, packed at the start of q's segment; the
+// grid covers their sum only.
+static __global__ __launch_bounds__(kBlock) void k_dist_dvals(const u32* __restrict__ sidx, u64 ntot, Displ SD,
                                                               Displ cnt, u32 R, const u64* __restrict__ dval,
                                                               u32* __restrict__ gid) {
-  const u64 k = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (k >= nsent) return;
+  const u64 i = u64(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= ntot) return;
+  const u64 k = packed_at(SD, cnt, R, i);
   const u32 q = seg_of(SD, R, k);
-  if (k - SD.d[q] >= cnt.d[q]) return;
   const u64 v = dval[k];
   gid[sidx[SD.d[q] + u32(v)]] = u32(v >> 32);
 }
@@ -919,9 +946,22 @@ static __global__ __launch_bounds__(kBlock) void k_node_keys(const u32* __restri
                                                              u64* __restrict__ count_out,
                                                              const u32* __restrict__ gid, u32 off, RecSrc rs,
                                                              u32* __restrict__ blockcnt, u32 nb,
-                                                             const unsigned char* __restrict__ gmark) {
+                                                             const unsigned char* __restrict__ gmark,
+                                                             unsigned char* __restrict__ gnf,
+                                                             unsigned char* __restrict__ gmul, u64* __restrict__ ddesc) {
   __shared__ u32 h[kMaxRanks];
   const int tid = threadIdx.x;
+  // what the exchange's sender side expects zeroed for this tile (local uniques = positions):
+  // the global flags (k_dist_flags sets the sent ones) and the rank scan's look-back word
+  if (gnf) {
+    const u64 end = blockIdx.x + 1 == gridDim.x ? p + 1 : std::min<u64>(u64(blockIdx.x + 1) * kTile, p + 1);
+    const u64 e0 = u64(blockIdx.x) * kTile / 16, e1 = (end + 15) / 16;
+    for (u64 e = e0 + tid; e < e1; e += kBlock) {
+      reinterpret_cast<uint4*>(gnf)[e] = make_uint4(0, 0, 0, 0);
+      reinterpret_cast<uint4*>(gmul)[e] = make_uint4(0, 0, 0, 0);
+    }
+    if (tid == 0) ddesc[blockIdx.x] = 0;
+  }
   if (blockcnt) {
     if (tid < int(rs.R)) h[tid] = 0;
     __syncthreads();

@@ -130,6 +130,15 @@ GCZ_API int gcz_fasta_extract_device(gcz_ctx *ctx, const void *d_file, uint64_t 
 GCZ_API int gcz_info_get(gcz_ctx *ctx, gcz_info *out);
 GCZ_API int gcz_copy_leaves(gcz_ctx *ctx, uint64_t *host_out);                /* n_leaves u64 */
 GCZ_API int gcz_copy_layer(gcz_ctx *ctx, int layer, uint32_t *host_out);      /* 2*layer_size words */
+/* The whole DAG in one call: leaves (n_leaves u64) and every layer (layers_out[k]: 2*layer_size
+ * words), through a pinned staging ring with parallel host copies -- the fast path into fresh,
+ * unpinned host memory (the reference's shared_tree containers). */
+GCZ_API int gcz_fetch_host(gcz_ctx *ctx, uint64_t *leaves_out, uint32_t *const *layers_out);
+/* Host storage for fetched trees (the shared_tree containers' allocator): arrays of >= 4 MB are
+ * 2 MB-aligned mappings advised as transparent huge pages (the fetch faults them in 2 MB steps
+ * on several threads); gcz_host_free takes the same byte count. */
+GCZ_API void *gcz_host_alloc(uint64_t bytes);
+GCZ_API void gcz_host_free(void *p, uint64_t bytes);
 
 /* Device pointers of the last build (valid until the next build). */
 GCZ_API const uint64_t *gcz_device_leaves(gcz_ctx *ctx);

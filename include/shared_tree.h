@@ -153,7 +153,11 @@ struct hash<node> {
 // Allocator of the tree's containers: resize() without a value leaves the
 // elements (plain 32/64-bit words with trivial destructors) uninitialised,
 // because a device copy or a full permutation fills them right after -- 0.6 GB
-// of value-initialisation and page faults otherwise.
+// of value-initialisation and page faults otherwise; large arrays are huge-page
+// mappings (gcz_host_alloc, include/gcz.h).
+extern "C" void* gcz_host_alloc(std::uint64_t bytes);              // libgcz (include/gcz.h)
+extern "C" void gcz_host_free(void* p, std::uint64_t bytes);
+
 template <class T>
 struct gcz_uninit_allocator : std::allocator<T> {
   template <class U>
@@ -163,6 +167,8 @@ struct gcz_uninit_allocator : std::allocator<T> {
   gcz_uninit_allocator() = default;
   template <class U>
   gcz_uninit_allocator(const gcz_uninit_allocator<U>&) noexcept {}
+  T* allocate(std::size_t n) { return static_cast<T*>(gcz_host_alloc(n * sizeof(T))); }
+  void deallocate(T* p, std::size_t n) noexcept { gcz_host_free(p, n * sizeof(T)); }
   template <class U>
   void construct(U*) noexcept {
     static_assert(std::is_trivially_destructible_v<U> && std::is_standard_layout_v<U>,
