@@ -176,6 +176,15 @@ fasta_reader open_with_engine(const std::filesystem::path& path) {
     (void)gcz_upload_reserve(engine().ctx, fsize);
   });
   fasta_reader f = [&] { PhaseTimer t{"map"}; return fasta_reader{path}; }();
+  if (!ec && fsize >= (std::uint64_t(64) << 20)) {
+    // ... and the tree's host storage is faulted in meanwhile (the runtime start leaves the
+    // host idle for ~0.1-0.25 s): a bound of the fetched arrays -- <= S nodes over all
+    // layers and <= S leaves, 8 B each, S <= file bytes / L -- capped at 2 GB; the fetch
+    // then copies into present pages (gcz_host_prefault, include/gcz.h)
+    PhaseTimer t{"prefault"};
+    const std::uint64_t S = fsize / std::max<std::size_t>(1, dna::size());
+    (void)gcz_host_prefault(std::min<std::uint64_t>(16 * S + (std::uint64_t(96) << 20), std::uint64_t(2) << 30), 8);
+  }
   init.join();
   return f;
 }
@@ -515,14 +524,23 @@ void shared_tree::build_from_gpu() {
   gcz_ctx* ctx = engine().ctx;
   gcz_info info{};
   gcz_info_get(ctx, &info);
-  leaves.resize(info.n_leaves);
-  nodes.resize(info.n_layers);   // keeps each layer's storage when a device sort refetches the same sizes
   std::vector<std::uint32_t*> outs(info.n_layers);
-  for (int k = 0; k < info.n_layers; ++k) {
-    nodes[k].resize(info.layer_size[k]);
-    outs[k] = reinterpret_cast<std::uint32_t*>(nodes[k].data());
+  {
+    PhaseTimer t2{"fetch-alloc"};
+    leaves.resize(info.n_leaves);
+    nodes.resize(info.n_layers);   // keeps each layer's storage when a device sort refetches the same sizes
+    for (int k = 0; k < info.n_layers; ++k) {
+      nodes[k].resize(info.layer_size[k]);
+      outs[k] = reinterpret_cast<std::uint32_t*>(nodes[k].data());
+    }
   }
-  check_build(gcz_fetch_host(ctx, reinterpret_cast<std::uint64_t*>(leaves.data()), outs.data()), ctx);
+  {
+    PhaseTimer t2{"fetch-copy"};
+    check_build(gcz_fetch_host(ctx, reinterpret_cast<std::uint64_t*>(leaves.data()), outs.data()), ctx);
+  }
+  // what the pre-faulted pool did not hold goes back on a side thread (unmapping ~0.6 GB of
+  // present pages takes ~25 ms)
+  gcz_host_pool_release(1);
   root = pointer::from_word(info.root);
   device_gen = ++engine().gen;
 }

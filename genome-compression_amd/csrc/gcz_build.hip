@@ -1,7 +1,10 @@
 // MI355X (gfx950) shared_tree construction: host orchestration and the C ABI.
 // Device code and the algorithm description: gcz_device.h; the multi-rank
 // build: gcz_dist.hip.
+#include <chrono>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -212,11 +215,12 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
   int rc;
   if ((rc = ensure(dl_pw, S * 4 + 16)) || (rc = ensure(dl_rec, S * 4 + 16)) || (rc = ensure(dl_idrec, S * 4 + 16)) ||
       (rc = ensure(dl_cnt, ncnt * 4 + 16)) || (rc = ensure(dl_off, (ncnt + 1) * 4 + 16)) ||
+      (rc = ensure(dl_offt, (ncnt + P.NB) * 4 + 16)) ||
       (rc = ensure(dl_fpg, ncodes * 4 + 16)) || (rc = ensure(dl_fb, nfb * 8 + 16)) ||
       (rc = ensure(dl_wpre, (nfb + 1) * 4 + 16)) || (rc = ensure(dl_desc, (t_cnt + t_fb) * 8 + 16)) ||
       (rc = ensure(dl_fl, ncodes * 4 + 16)) || (rc = ensure(dl_fo, u64(P.NB) * (P.nch + 1) * 4 + 16)))
     return rc;
-  if (list && ((rc = ensure(dl_fl2, ncodes * 2 + 16)) || (rc = ensure(dl_pb, (ncodes / 64 + 1) * 8))))
+  if (list && ((rc = ensure(dl_lh, std::min(S, ncodes) * 4 + 16)) || (rc = ensure(dl_pb, (ncodes / 64 + 1) * 8))))
     return rc;
   u64* sdesc = dl_desc.as<u64>();
   u32* tickets = reinterpret_cast<u32*>(sdesc + t_cnt + t_fb);
@@ -257,27 +261,23 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
   hipLaunchKernelGGL(k_scan_excl<ScanU32>, dim3(unsigned(t_cnt)), dim3(kScanThreads), 0, stream,
                      ScanU32{dl_cnt.as<u32>(), ncnt}, ncnt + 1, dl_off.as<u32>(), sdesc, &tickets[0],
                      static_cast<u64*>(nullptr));
+  hipLaunchKernelGGL(k_dl_offt, dim3((P.nch + 1 + 31) / 32, (P.NB + 31) / 32), dim3(256), 0, stream, dl_off.as<u32>(), P,
+                     dl_offt.as<u32>());
   HIP_TRY(hipGetLastError());
   prof_end(KID_DL_SCAN, e0);
   prof_begin(KID_DL_SCATTER, e0);
   hipLaunchKernelGGL(k_dl_scatter, dim3(P.nch), dim3(kDThreads), scat_bytes, stream, dl_pw.as<u32>(), P,
-                     dl_off.as<u32>(), dl_rec.as<u32>());
+                     dl_offt.as<u32>(), dl_rec.as<u32>());
   HIP_TRY(hipGetLastError());
   prof_end(KID_DL_SCATTER, e0);
   prof_begin(KID_DL_FIRST, e0);
   if (list && (1u << P.IB) < 64) HIP_TRY(hipMemsetAsync(dl_pb.ptr, 0, (ncodes / 64 + 1) * 8, stream));
   hipLaunchKernelGGL(k_dl_first, dim3(P.NB), dim3(kDThreads), first_bytes, stream, dl_rec.as<u32>(), dl_off.as<u32>(),
                      P, list ? nullptr : dl_fpg.as<u32>(), dl_fl.as<u32>(), dl_fo.as<u32>(),
-                     list ? dl_pb.as<unsigned long long>() : nullptr,   // (multi-rank: ids come from gid)
-                     list ? dl_fl2.as<unsigned short>() : nullptr);
+                     list ? dl_pb.as<unsigned long long>() : nullptr);   // (multi-rank: ids come from gid)
   HIP_TRY(hipGetLastError());
-  if (list) {   // multi-rank: the bitmap of r-first keys follows the exchange (dense_rfirst)
-    prof_end(KID_DL_FIRST, e0);
-    return GCZ_OK;
-  }
   hipLaunchKernelGGL(k_dl_fb, dim3(P.nch), dim3(kDThreads), 0, stream, dl_fl.as<u32>(), dl_fo.as<u32>(), P,
-                     dl_fb.as<unsigned long long>(), static_cast<const unsigned short*>(nullptr),
-                     static_cast<const unsigned long long*>(nullptr));
+                     dl_fb.as<unsigned long long>());
   HIP_TRY(hipGetLastError());
   prof_end(KID_DL_FIRST, e0);
   prof_begin(KID_DL_FBSCAN, e0);
@@ -285,33 +285,11 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
                      ScanPopc{dl_fb.as<unsigned long long>()}, nfb, dl_wpre.as<u32>(), sdesc + t_cnt, &tickets[1],
                      ucount);
   HIP_TRY(hipGetLastError());
-  prof_end(KID_DL_FBSCAN, e0);
-  return GCZ_OK;
-}
-
-// Multi-rank (after the presence-bitmap exchange): the first-occurrence bitmap of this
-// rank's r-first keys only (lower = OR of the lower ranks' presence bitmaps), its popcount
-// prefix (*count = the rank's r-first keys) and their hashed codes in position order = global
-// id order (list).
-int gcz_ctx::dense_rfirst(const unsigned long long* lower, u64* count, u32* list) {
-  const DensePlan& P = dl_plan;
-  const u64 S = P.S, nfb = (S + 63) / 64;
-  const u64 t_cnt = scan_tiles(u64(P.NB) * P.nch + 1), t_fb = scan_tiles(nfb + 1);
-  u64* sdesc = dl_desc.as<u64>();
-  u32* tickets = reinterpret_cast<u32*>(sdesc + t_cnt + t_fb);
-  hipEvent_t e0{};
-  prof_begin(KID_DL_FIRST, e0);
-  hipLaunchKernelGGL(k_dl_fb, dim3(P.nch), dim3(kDThreads), 0, stream, dl_fl.as<u32>(), dl_fo.as<u32>(), P,
-                     dl_fb.as<unsigned long long>(), dl_fl2.as<unsigned short>(), lower);
-  HIP_TRY(hipGetLastError());
-  prof_end(KID_DL_FIRST, e0);
-  prof_begin(KID_DL_FBSCAN, e0);
-  hipLaunchKernelGGL(k_scan_excl<ScanPopc>, dim3(unsigned(t_fb)), dim3(kScanThreads), 0, stream,
-                     ScanPopc{dl_fb.as<unsigned long long>()}, nfb, dl_wpre.as<u32>(), sdesc + t_cnt, &tickets[1],
-                     count);
-  hipLaunchKernelGGL(k_dl_lh, dim3(unsigned((S + 255) / 256)), dim3(256), 0, stream, dl_pw.as<u32>(),
-                     dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), S, list);
-  HIP_TRY(hipGetLastError());
+  if (list) {
+    hipLaunchKernelGGL(k_dl_lh, dim3(unsigned((S + 255) / 256)), dim3(256), 0, stream, dl_pw.as<u32>(),
+                       dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), S, dl_lh.as<u32>());
+    HIP_TRY(hipGetLastError());
+  }
   prof_end(KID_DL_FBSCAN, e0);
   return GCZ_OK;
 }
@@ -331,7 +309,7 @@ int gcz_ctx::dense_phase_b(const LeafLevel& a, Header* d_hdr, const u32* gid, u6
   prof_end(KID_DL_IDS, e0);
   prof_begin(KID_DL_WORDS, e0);
   hipLaunchKernelGGL(k_dl_words, dim3(P.nch), dim3(kDThreads), words_bytes, stream, dl_rec.as<u32>(),
-                     dl_idrec.as<u32>(), dl_off.as<u32>(), P, dl_fb.as<unsigned long long>(), a.words, leaves);
+                     dl_idrec.as<u32>(), dl_offt.as<u32>(), P, dl_fb.as<unsigned long long>(), a.words, leaves);
   HIP_TRY(hipGetLastError());
   prof_end(KID_DL_WORDS, e0);
   return GCZ_OK;
@@ -1005,8 +983,8 @@ void gcz_ctx_destroy(gcz_ctx* c) {
   gcz_ingest_state_free(c);
   for (DevBuf* b : {&c->wa, &c->wb, &c->grp, &c->desc, &c->tab, &c->leaves_out, &c->nodes_out, &c->hdr, &c->input,
                     &c->nf, &c->multi, &c->stats, &c->bkt_key, &c->bkt_cnt, &c->bkt_off, &c->bkt_tmp, &c->bkt_rec2, &c->dl_pw,
-                    &c->dl_rec, &c->dl_idrec, &c->dl_cnt, &c->dl_off, &c->dl_fpg, &c->dl_fb, &c->dl_wpre,
-                    &c->dl_desc, &c->dl_fl, &c->dl_fo, &c->dl_fl2, &c->dl_pb, &c->dl_pbs, &c->dl_lower,
+                    &c->dl_rec, &c->dl_idrec, &c->dl_cnt, &c->dl_off, &c->dl_offt, &c->dl_fpg, &c->dl_fb, &c->dl_wpre,
+                    &c->dl_desc, &c->dl_fl, &c->dl_fo, &c->dl_lh, &c->dl_pb, &c->dl_pbs, &c->dl_lower,
                     &c->dl_pos, &c->dl_list, &c->dl_gid, &c->dl_recv, &c->dl_stage, &c->dl_seg, &c->seg_w,
                     &c->seg_nf, &c->seg_mu, &c->seg_in})
     if (b->ptr) (void)hipFree(b->ptr);
@@ -1144,8 +1122,8 @@ const uint32_t* gcz_device_layer(gcz_ctx* c, int k) {
 // the destination are taken by several threads at once and the DMA never waits for them.
 // The runtime's pageable D2H path copies and faults on one thread (~10 GB/s at 1 Gbase).
 namespace {
-constexpr u64 kRingChunk = u64(16) << 20;
-constexpr int kRingSlots = 4;
+constexpr u64 kRingChunk = u64(8) << 20;   // (pinning costs ~0.25 ms per MB: a small ring)
+constexpr int kRingSlots = 3;
 
 struct CopyPool {   // T - 1 workers + the calling thread copy one chunk's slices, then meet
   int T;
@@ -1205,6 +1183,30 @@ struct CopyPool {   // T - 1 workers + the calling thread copy one chunk's slice
 };
 }  // namespace
 
+// The staging ring for a fetch of `total` bytes: one slot holding a small DAG, else kRingSlots
+// slots of kRingChunk; pinned once per context (hipHostMalloc pins at ~4 GB/s on the box, and
+// beside a running build it slows the upload as much as it saves, so it is not overlapped).
+int gcz_fetch_reserve(gcz_ctx* c, uint64_t total) {
+  if (!c) return GCZ_ERR_ARG;
+  const u64 need = total > kRingChunk ? u64(kRingSlots) * kRingChunk : (total + 4095) & ~u64(4095);
+  if (c->h_ring_bytes < need) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
+    if (c->h_ring) (void)hipHostFree(c->h_ring);
+    c->h_ring = nullptr;
+    c->h_ring_bytes = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_ring), need, hipHostMallocDefault) != hipSuccess)
+      return GCZ_ERR_DEVICE;
+    c->h_ring_bytes = need;
+    if (std::getenv("GCZ_TIMING"))
+      std::fprintf(stderr, "gcz-time ring-alloc %g\n",
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  }
+  for (hipEvent_t& e : c->ring_ev)
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return GCZ_ERR_DEVICE;
+  return GCZ_OK;
+}
+
 int gcz_fetch_host(gcz_ctx* c, uint64_t* leaves_out, uint32_t* const* layers_out) {
   if (!c || c->info.status != GCZ_OK) return GCZ_ERR_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
@@ -1225,18 +1227,7 @@ int gcz_fetch_host(gcz_ctx* c, uint64_t* leaves_out, uint32_t* const* layers_out
              c->info.layer_size[k] * 8))
       return GCZ_ERR_ARG;
   if (pieces.empty()) return GCZ_OK;
-  // a small DAG: one slot holding all of it; else kRingSlots slots of kRingChunk
-  const u64 need = total > kRingChunk ? u64(kRingSlots) * kRingChunk : (total + 4095) & ~u64(4095);
-  if (c->h_ring_bytes < need) {
-    if (c->h_ring) (void)hipHostFree(c->h_ring);
-    c->h_ring = nullptr;
-    c->h_ring_bytes = 0;
-    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_ring), need, hipHostMallocDefault) != hipSuccess)
-      return GCZ_ERR_DEVICE;
-    c->h_ring_bytes = need;
-  }
-  for (hipEvent_t& e : c->ring_ev)
-    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return GCZ_ERR_DEVICE;
+  if (int rc = gcz_fetch_reserve(c, total)) return rc;
   const unsigned hc = std::thread::hardware_concurrency();
   CopyPool pool(total >= (u64(8) << 20) ? int(std::min<unsigned>(8, std::max(1u, hc))) : 1);
   if (total <= kRingChunk) {   // one D2H batch, then the host copies

@@ -211,8 +211,8 @@ struct gcz_ctx {
   gcz_host::DevBuf wa, wb, grp, desc, tab, leaves_out, nodes_out, hdr, input, nf, multi;
   gcz_host::DevBuf stats;   // hashed-pair counter shards (k_node_insert), summed into hdr->hashed[0]
   gcz_host::DevBuf bkt_key, bkt_cnt, bkt_off, bkt_tmp, bkt_rec2;   // bucketed node insert (k_bkt_*)
-  gcz_host::DevBuf dl_pw, dl_rec, dl_idrec, dl_cnt, dl_off, dl_fpg, dl_fb, dl_wpre, dl_desc, dl_fl, dl_fo;   // dense leaf level
-  gcz_host::DevBuf dl_fl2, dl_pb, dl_pbs, dl_lower, dl_pos, dl_list, dl_gid, dl_recv, dl_stage, dl_seg;   // ... multi-rank
+  gcz_host::DevBuf dl_pw, dl_rec, dl_idrec, dl_cnt, dl_off, dl_offt, dl_fpg, dl_fb, dl_wpre, dl_desc, dl_fl, dl_fo;   // dense leaf level
+  gcz_host::DevBuf dl_lh, dl_pb, dl_pbs, dl_lower, dl_pos, dl_list, dl_gid, dl_recv, dl_stage, dl_seg;   // ... multi-rank
   gcz_dev::DensePlan dl_plan{};
   gcz_dev::Header* h_hdr = nullptr;   // pinned
   unsigned char* h_ring = nullptr;    // pinned D2H staging ring of the host fetch (gcz_fetch_host)
@@ -345,13 +345,11 @@ struct gcz_ctx {
   // unique count to *ucount.
   int leaf_level_dense(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr, gcz_host::u64* ucount, bool* used);
   // ... in two phases (gcz_dist.hip exchanges in between): A = local first occurrences
-  // (check: read the pure-ACGT flag on the host; list: the presence bitmap, the rank's
-  // first-occurrence bitmap and key list then come from dense_rfirst after the exchange),
-  // B = ids (gid: global ids by hashed code, or null: local) and words (leaves: write the
-  // unique leaves, or null).
+  // (check: read the pure-ACGT flag on the host; list: the local key list and presence
+  // bitmap), B = ids (gid: global ids by hashed code, or null: local) and words
+  // (leaves: write the unique leaves, or null).
   int dense_phase_a(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr, gcz_host::u64* ucount, bool check, bool list,
                     bool* used);
-  int dense_rfirst(const unsigned long long* lower, gcz_host::u64* count, gcz_host::u32* list);
   int dense_phase_b(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr, const gcz_host::u32* gid,
                     gcz_host::u64* leaves);
   int node_level(const gcz_host::NodeLevel& a, gcz_dev::Header* d_hdr);

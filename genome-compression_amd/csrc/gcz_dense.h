@@ -110,15 +110,16 @@ static __device__ __forceinline__ u32 block_excl(u32 x, u32* s_tmp, u32* total) 
 }
 
 // The runs (b, ch) of one chunk: s_base[b] = local exclusive offset (s_base[NB] = the
-// chunk's strands), s_dst[b] = the run's start in the record array.
-static __device__ __forceinline__ void chunk_runs(const u32* __restrict__ off, const DensePlan& P, u32 ch, u32* s_base,
+// chunk's strands), s_dst[b] = the run's start in the record array.  offt: the run starts
+// chunk-major (k_dl_offt), so a chunk reads two contiguous rows of NB words instead of a
+// strided column of the bucket-major scan output.
+static __device__ __forceinline__ void chunk_runs(const u32* __restrict__ offt, const DensePlan& P, u32 ch, u32* s_base,
                                            u32* s_dst, u32* s_tmp) {
   const u32 b = threadIdx.x;   // NB <= kDThreads
   u32 c = 0, d = 0;
   if (b < P.NB) {
-    const u64 k = u64(b) * P.nch + ch;   // run (b, ch) = [off[k], off[k + 1]) in the flat bucket-major order
-    d = off[k];
-    c = off[k + 1] - d;
+    d = offt[u64(ch) * P.NB + b];
+    c = offt[u64(ch + 1) * P.NB + b] - d;
   }
   u32 total;
   const u32 e = block_excl(c, s_tmp, &total);
@@ -128,6 +129,23 @@ static __device__ __forceinline__ void chunk_runs(const u32* __restrict__ off, c
   }
   if (b == 0) s_base[P.NB] = total;
   __syncthreads();
+}
+
+// offt[ch][b] = off[b * nch + ch] for ch in [0, nch] (column nch = the bucket's end = the
+// next bucket's start): a 32 x 32 tiled transpose through LDS, coalesced on both sides.
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_offt(const u32* __restrict__ off, DensePlan P,
+                                                 u32* __restrict__ offt) {
+  __shared__ u32 t[32][33];
+  const u32 c0 = blockIdx.x * 32, b0 = blockIdx.y * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (u32 r = ty; r < 32; r += 8) {   // rows b, columns ch
+    const u32 b = b0 + r, ch = c0 + tx;
+    if (b < P.NB && ch <= P.nch) t[r][tx] = off[u64(b) * P.nch + ch];
+  }
+  __syncthreads();
+  for (u32 r = ty; r < 32; r += 8) {   // rows ch, columns b
+    const u32 ch = c0 + r, b = b0 + tx;
+    if (b < P.NB && ch <= P.nch) offt[u64(ch) * P.NB + b] = t[tx][r];
+  }
 }
 
 // last bucket b with s_base[b] <= q (runs of zero length are skipped)
@@ -227,7 +245,7 @@ template <int L, bool kBases>
 // (chunk, bucket) at off[b * nch + chunk] of the bucket-ordered record array,
 // staged in LDS so every run is written contiguously.
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_scatter(const u32* __restrict__ pw, DensePlan P,
-                                                          const u32* __restrict__ off, u32* __restrict__ rec) {
+                                                          const u32* __restrict__ offt, u32* __restrict__ rec) {
   extern __shared__ u32 s_dyn[];
   u32* s_stage = s_dyn;                 // kDC records
   u32* s_base = s_dyn + kDC;            // NB + 1: local exclusive offsets of the runs
@@ -244,7 +262,7 @@ template <int L, bool kBases>
     const u32 q = j * kDThreads + tid;
     h[j] = q < n ? pw[c0 + q] : 0u;
   }
-  chunk_runs(off, P, ch, s_base, s_dst, s_tmp);
+  chunk_runs(offt, P, ch, s_base, s_dst, s_tmp);
   if (u32(tid) < P.NB) s_cur[tid] = s_base[tid];
   __syncthreads();
   const u32 imask = (1u << P.IB) - 1u;
@@ -310,11 +328,9 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
 // first positions sorted by chunk: fl[b * RB + ...], with fo[ch * NB + b] the start
 // of chunk ch's (a counting sort in LDS; k_dl_fb gathers them per chunk).  pb
 // (multi-rank build, else null): the presence bitmap, bit h set iff hashed code h occurs.
-// fl2 (multi-rank, with pb): each fl entry's code within the bucket, for k_dl_fb's filter.
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_first(const u32* __restrict__ rec, const u32* __restrict__ off,
                                                         DensePlan P, u32* __restrict__ fpg, u32* __restrict__ fl,
-                                                        u32* __restrict__ fo, unsigned long long* __restrict__ pb,
-                                                        unsigned short* __restrict__ fl2) {
+                                                        u32* __restrict__ fo, unsigned long long* __restrict__ pb) {
   extern __shared__ u32 s_dyn[];
   u32* s_fp = s_dyn;                    // RB codes
   u32* s_cnt = s_dyn + (1u << P.IB);    // nch + 1 chunk counters
@@ -363,21 +379,13 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < PER; ++k)
-    if (fp[k] != ~0u) {
-      const u64 at = u64(b) * RB + s_cnt[fp[k] >> kDLog] + rk[k];
-      fl[at] = fp[k];
-      if (fl2) fl2[at] = (unsigned short)(u32(k) * kDThreads + tid);
-    }
+    if (fp[k] != ~0u) fl[u64(b) * RB + s_cnt[fp[k] >> kDLog] + rk[k]] = fp[k];
 }
 
 // First-occurrence bitmap of one chunk: its first positions from every bucket's
 // sorted list (k_dl_first), set in LDS, written as the chunk's 512 bitmap words.
-// lower (multi-rank): only the rank's r-first keys (held by no lower rank, fl2 gives each
-// entry's code) -- the bitmap's popcount ranks are then the r-first keys' local order.
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_fb(const u32* __restrict__ fl, const u32* __restrict__ fo,
-                                                     DensePlan P, unsigned long long* __restrict__ fb,
-                                                     const unsigned short* __restrict__ fl2,
-                                                     const unsigned long long* __restrict__ lower) {
+                                                     DensePlan P, unsigned long long* __restrict__ fb) {
   __shared__ u32 s_bits[kDC / 32];
   const int tid = threadIdx.x;
   const u32 ch = blockIdx.x, RB = 1u << P.IB;
@@ -389,16 +397,6 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
       u32 q[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) q[j] = k0 + j < o1 ? fl[u64(b) * RB + k0 + j] & (kDC - 1) : ~0u;
-      if (lower) {
-        u32 c[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) c[j] = q[j] != ~0u ? fl2[u64(b) * RB + k0 + j] : 0u;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const u32 h = (b << P.IB) | c[j];
-          if (q[j] != ~0u && ((lower[h >> 6] >> (h & 63)) & 1ull)) q[j] = ~0u;
-        }
-      }
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (q[j] != ~0u) atomicOr(&s_bits[q[j] >> 5], 1u << (q[j] & 31));
@@ -467,7 +465,7 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
 // chunk's first-occurrence bitmap, staged in LDS) emits its leaf from the record's code
 // (bucket | the record's low code bits); leaf ids are the first-occurrence ranks.
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_words(const u32* __restrict__ rec,
-                                                        const u32* __restrict__ idrec, const u32* __restrict__ off,
+                                                        const u32* __restrict__ idrec, const u32* __restrict__ offt,
                                                         DensePlan P, const unsigned long long* __restrict__ fb,
                                                         u32* __restrict__ words, u64* __restrict__ leaves_out) {
   extern __shared__ u32 s_dyn[];
@@ -488,7 +486,7 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
       s_fb[2 * w] = u32(m);
       s_fb[2 * w + 1] = u32(m >> 32);
     }
-  chunk_runs(off, P, ch, s_base, s_dst, s_tmp);
+  chunk_runs(offt, P, ch, s_base, s_dst, s_tmp);
   const int lane = tid & 63, wave = tid >> 6;
   const u32 IB = P.IB, imask = (1u << IB) - 1u;
   auto place = [&](u32 b, u32 xr, u32 wr) {   // one record: its word into position order, its leaf
@@ -549,8 +547,8 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
 // lists (hashed codes in id order) are exchanged so that every rank can look up the
 // global id of each key it holds; rank r's list is also its slice of the leaves.
 
-// Key list: the hashed code of each first occurrence in the bitmap fb (multi-rank: of the
-// r-first keys), in position order = id order (the writes are contiguous).
+// Local key list: the hashed code of each first occurrence, in local-id order (the
+// ids of first occurrences increase with position, so the writes are contiguous).
 [[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_lh(const u32* __restrict__ pw,
                                                      const unsigned long long* __restrict__ fb,
                                                      const u32* __restrict__ wpre, u64 S, u32* __restrict__ lh) {
@@ -560,10 +558,10 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
   if ((m >> (s & 63)) & 1ull) lh[wpre[s >> 6] + u32(__popcll(m & ((1ull << (s & 63)) - 1ull)))] = pw[s] & kIdx;
 }
 
-// (pure-ACGT failure flag, unused, repetitive-data flag) for the first exchange
+// (pure-ACGT failure flag, local uniques, repetitive-data flag) for the first exchange
 [[maybe_unused]] static __global__ void k_dl_vec(const Header* __restrict__ hdr, u64* __restrict__ vec) {
   vec[0] = hdr->dense_fail;
-  vec[1] = 0;
+  vec[1] = hdr->count[0];
   vec[2] = hdr->predup;
 }
 
@@ -581,6 +579,26 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
   unsigned long long x = 0;
   for (int q = 0; q < r; ++q) x |= pbs[u64(q) * stride + w];
   lower[w] = x;
+}
+
+struct ScanRFirst {   // local key j is r-first: no lower rank holds it
+  const u32* lh;
+  const unsigned long long* lower;
+  u64 n;
+  __device__ __forceinline__ u32 operator()(u64 j) const {
+    if (j >= n) return 0u;
+    const u32 h = lh[j];
+    return ((lower[h >> 6] >> (h & 63)) & 1ull) ? 0u : 1u;
+  }
+};
+
+// the r-first keys in local-id order (= global-id order)
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_compact(const u32* __restrict__ lh, const unsigned long long* __restrict__ lower,
+                                                    const u32* __restrict__ pos, u64 n, u32* __restrict__ list) {
+  const u64 j = u64(blockIdx.x) * 256 + threadIdx.x;
+  if (j >= n) return;
+  const u32 h = lh[j];
+  if (!((lower[h >> 6] >> (h & 63)) & 1ull)) list[pos[j]] = h;
 }
 
 // Global ids from the gathered lists: recv holds segments (start, len, global id of

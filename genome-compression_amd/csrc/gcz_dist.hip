@@ -704,27 +704,35 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
   for (gcz_ctx* cx : ctx) G_HIP(hipStreamSynchronize(cx->stream));
   for (int r = 0; r < R; ++r)
     if (hv[3 * r] == 2) return local_rc && local_rc != GCZ_ERR_DEVICE ? local_rc : dev_fail("dense leaves (a rank failed)");
+  std::vector<u64> U(R);
   bool pred = false;
   for (int r = 0; r < R; ++r) {
     if (hv[3 * r]) return GCZ_OK;   // some rank holds a non-ACGT strand: the hash-table leaf level
+    U[r] = hv[3 * r + 1];
     pred = pred || hv[3 * r + 2] != 0;
   }
   any_predup = pred;
-  // r-first keys (held by no lower rank): their first-occurrence bitmap, count and codes in
-  // position order = global-id order (rank 0: all its keys)
+  // r-first keys (held by no lower rank) in local-id order = global-id order
   for (int i = 0; i < NL; ++i) {
     gcz_ctx* cx = ctx[i];
     const int r = rank[i];
-    if (cx->ensure(cx->dl_list, std::min<u64>(P.count(r, 0), ncodes) * 4 + 16)) return dev_fail("dense leaf lists");
-    if (r > 0) {
-      ProfScope ps_(cx, KID_IDS);
-      hipLaunchKernelGGL(k_dl_lower, dim3(unsigned((nw + 255) / 256)), dim3(256), 0, cx->stream,
-                         cx->dl_pbs.as<unsigned long long>(), nw, nwb, r, cx->dl_lower.as<unsigned long long>());
-      G_HIP(hipGetLastError());
-    }
-    if (cx->dense_rfirst(r > 0 ? cx->dl_lower.as<unsigned long long>() : nullptr, cx->dl_seg.as<u64>() + 4,
-                         cx->dl_list.as<u32>()))
-      return dev_fail("dense leaves (r-first keys)");
+    const u64 ur = U[r], t = scan_tiles(ur + 1);
+    ProfScope ps_(cx, KID_IDS);
+    if (cx->ensure(cx->dl_pos, (ur + 1) * 4 + t * 8 + 64) || cx->ensure(cx->dl_list, ur * 4 + 16))
+      return dev_fail("dense leaf lists");
+    u32* pos = cx->dl_pos.as<u32>();
+    u64* desc = reinterpret_cast<u64*>(pos + ((ur + 1 + 1) & ~u64(1)));
+    u32* ticket = reinterpret_cast<u32*>(desc + t);
+    G_HIP(hipMemsetAsync(desc, 0, t * 8 + 8, cx->stream));
+    hipLaunchKernelGGL(k_dl_lower, dim3(unsigned((nw + 255) / 256)), dim3(256), 0, cx->stream,
+                       cx->dl_pbs.as<unsigned long long>(), nw, nwb, r, cx->dl_lower.as<unsigned long long>());
+    hipLaunchKernelGGL(k_scan_excl<ScanRFirst>, dim3(unsigned(t)), dim3(kScanThreads), 0, cx->stream,
+                       ScanRFirst{cx->dl_lh.as<u32>(), cx->dl_lower.as<unsigned long long>(), ur}, ur + 1, pos, desc,
+                       ticket, cx->dl_seg.as<u64>() + 4);
+    if (ur)
+      hipLaunchKernelGGL(k_dl_compact, dim3(unsigned((ur + 255) / 256)), dim3(256), 0, cx->stream, cx->dl_lh.as<u32>(),
+                         cx->dl_lower.as<unsigned long long>(), pos, ur, cx->dl_list.as<u32>());
+    G_HIP(hipGetLastError());
   }
   // exchange 2: r-first counts -> id offsets
   {

@@ -4,8 +4,10 @@
 // these entry points work on machines without a GPU.
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <numeric>
 #include <thread>
+#include <vector>
 
 #include <sys/mman.h>
 
@@ -316,30 +318,89 @@ void gcz_synth_fill(char* out, int kind, uint64_t seed, uint64_t begin, uint64_t
 uint64_t gcz_synth_default_seed(void) { return GCZ_SYNTH_SEED; }
 
 // Host storage of the tree containers (include/shared_tree.h, gcz_uninit_allocator): large
-// arrays are their own 2 MB-aligned anonymous mappings advised as transparent huge pages, so
-// the fetch's first touch (gcz_fetch_host's parallel copies) faults 2 MB at a time on several
-// threads instead of 4 KB pages one after another (~46 ms of the 1 Gbase fetch's 60).
-void* gcz_host_alloc(uint64_t bytes) {
-  constexpr uint64_t kHuge = uint64_t(2) << 20;
-  if (bytes < (uint64_t(4) << 20)) return ::operator new(bytes ? bytes : 1);
-  const uint64_t sz = (bytes + kHuge - 1) & ~(kHuge - 1);
+// arrays are 2 MB-aligned anonymous mappings advised as transparent huge pages, carved from a
+// pre-faulted pool when one is there (gcz_host_prefault: the drop-in faults the pool in while
+// the HIP runtime starts, so the fetch's copies find their pages present), else mapped fresh.
+// Pieces are whole 2 MB units, so gcz_host_free unmaps exactly its piece, pool or not.
+namespace {
+constexpr uint64_t kHuge = uint64_t(2) << 20;
+constexpr uint64_t kBig = uint64_t(4) << 20;
+std::mutex g_pool_mu;
+uintptr_t g_pool_cur = 0, g_pool_end = 0;
+
+uint64_t huge_round(uint64_t b) { return (b + kHuge - 1) & ~(kHuge - 1); }
+
+void* map_huge(uint64_t sz) {   // sz: a multiple of kHuge
   void* m = ::mmap(nullptr, sz + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-  if (m == MAP_FAILED) throw std::bad_alloc();
+  if (m == MAP_FAILED) return nullptr;
   const uintptr_t base = reinterpret_cast<uintptr_t>(m), a = (base + kHuge - 1) & ~uintptr_t(kHuge - 1);
-  if (a > base) ::munmap(m, a - base);                                         // trim to [a, a + sz)
+  if (a > base) ::munmap(m, a - base);   // trim to [a, a + sz)
   if (base + sz + kHuge > a + sz) ::munmap(reinterpret_cast<void*>(a + sz), base + sz + kHuge - (a + sz));
   (void)::madvise(reinterpret_cast<void*>(a), sz, MADV_HUGEPAGE);
   return reinterpret_cast<void*>(a);
 }
+}  // namespace
+
+void* gcz_host_alloc(uint64_t bytes) {
+  if (bytes < kBig) return ::operator new(bytes ? bytes : 1);
+  const uint64_t sz = huge_round(bytes);
+  {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    if (g_pool_end - g_pool_cur >= sz) {
+      void* p = reinterpret_cast<void*>(g_pool_cur);
+      g_pool_cur += sz;
+      return p;
+    }
+  }
+  void* p = map_huge(sz);
+  if (!p) throw std::bad_alloc();
+  return p;
+}
 
 void gcz_host_free(void* p, uint64_t bytes) {
   if (!p) return;
-  constexpr uint64_t kHuge = uint64_t(2) << 20;
-  if (bytes < (uint64_t(4) << 20)) {
+  if (bytes < kBig) {
     ::operator delete(p);
     return;
   }
-  ::munmap(p, (bytes + kHuge - 1) & ~(kHuge - 1));
+  ::munmap(p, huge_round(bytes));
+}
+
+int gcz_host_prefault(uint64_t bytes, int threads) {
+  gcz_host_pool_release(0);
+  if (bytes < kBig) return GCZ_OK;
+  const uint64_t sz = huge_round(bytes);
+  void* p = map_huge(sz);
+  if (!p) return GCZ_ERR_DEVICE;
+  unsigned char* b = static_cast<unsigned char*>(p);
+  const int T = std::max(1, std::min(threads, 16));
+  auto touch = [&](int t) {   // one write per 4 KB page: the fault maps it (a huge page where THP allows)
+    const uint64_t lo = sz * uint64_t(t) / uint64_t(T) & ~uint64_t(4095), hi = sz * uint64_t(t + 1) / uint64_t(T);
+    for (uint64_t o = lo; o < hi; o += 4096) b[o] = 0;
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) th.emplace_back(touch, t);
+  touch(0);
+  for (auto& x : th) x.join();
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  g_pool_cur = reinterpret_cast<uintptr_t>(p);
+  g_pool_end = g_pool_cur + sz;
+  return GCZ_OK;
+}
+
+void gcz_host_pool_release(int async) {
+  uintptr_t a, b;
+  {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    a = g_pool_cur;
+    b = g_pool_end;
+    g_pool_cur = g_pool_end = 0;
+  }
+  if (b <= a) return;
+  if (async)   // (the range is no longer the pool's: a later prefault cannot be unmapped by this)
+    std::thread([a, b] { ::munmap(reinterpret_cast<void*>(a), b - a); }).detach();
+  else
+    ::munmap(reinterpret_cast<void*>(a), b - a);
 }
 
 }  // extern "C"

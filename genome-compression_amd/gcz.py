@@ -70,8 +70,11 @@ _SIGS = {
     "gcz_copy_leaves": (ctypes.c_int, [_P, _P]),
     "gcz_copy_layer": (ctypes.c_int, [_P, ctypes.c_int, _P]),
     "gcz_fetch_host": (ctypes.c_int, [_P, _P, _P]),
+    "gcz_fetch_reserve": (ctypes.c_int, [_P, _U64]),
     "gcz_host_alloc": (_P, [_U64]),
     "gcz_host_free": (None, [_P, _U64]),
+    "gcz_host_prefault": (ctypes.c_int, [_U64, ctypes.c_int]),
+    "gcz_host_pool_release": (None, [ctypes.c_int]),
     "gcz_device_leaves": (_P, [_P]),
     "gcz_device_layer": (_P, [_P, ctypes.c_int]),
     "gcz_profile_enable": (ctypes.c_int, [_P, ctypes.c_int]),

@@ -134,11 +134,19 @@ GCZ_API int gcz_copy_layer(gcz_ctx *ctx, int layer, uint32_t *host_out);      /*
  * words), through a pinned staging ring with parallel host copies -- the fast path into fresh,
  * unpinned host memory (the reference's shared_tree containers). */
 GCZ_API int gcz_fetch_host(gcz_ctx *ctx, uint64_t *leaves_out, uint32_t *const *layers_out);
+/* Pin the fetch's staging ring for a DAG of `total_bytes` ahead of time (24 MB at most, a few
+ * ms; gcz_fetch_host otherwise does it on its first call). */
+GCZ_API int gcz_fetch_reserve(gcz_ctx *ctx, uint64_t total_bytes);
 /* Host storage for fetched trees (the shared_tree containers' allocator): arrays of >= 4 MB are
  * 2 MB-aligned mappings advised as transparent huge pages (the fetch faults them in 2 MB steps
  * on several threads); gcz_host_free takes the same byte count. */
 GCZ_API void *gcz_host_alloc(uint64_t bytes);
 GCZ_API void gcz_host_free(void *p, uint64_t bytes);
+/* Pre-fault `bytes` of that storage (2 MB pages, `threads` host threads) as a pool the next
+ * large gcz_host_alloc calls are carved from -- the drop-in does it while the HIP runtime
+ * starts, so the fetch copies into present pages; gcz_host_pool_release unmaps what is left. */
+GCZ_API int gcz_host_prefault(uint64_t bytes, int threads);
+GCZ_API void gcz_host_pool_release(int async);   /* async: unmapped on a detached thread */
 
 /* Device pointers of the last build (valid until the next build). */
 GCZ_API const uint64_t *gcz_device_leaves(gcz_ctx *ctx);

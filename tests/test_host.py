@@ -26,6 +26,33 @@ def test_abi_exports_every_declared_symbol(gcz):
     assert sorted(set(gcz.EXPORTED)) == syms
 
 
+def test_host_storage_pool(gcz):
+    """The containers' host storage (gcz_host_alloc / free / prefault / pool_release): small
+    arrays from the heap, large ones as 2 MB-aligned mappings, carved from a pre-faulted pool
+    while it lasts, then mapped fresh; every piece unmaps alone."""
+    import ctypes
+    lib = gcz._lib
+    MB = 1 << 20
+    assert lib.gcz_host_prefault(64 * MB, 4) == 0
+    pieces = []
+    for nbytes in (1000, 5 * MB, 17 * MB + 3, 30 * MB, 40 * MB):   # the last one exceeds the pool's rest
+        p = lib.gcz_host_alloc(nbytes)
+        assert p
+        if nbytes >= 4 * MB:
+            assert p % (2 * MB) == 0
+        ctypes.memset(p, 0x5A, nbytes)
+        pieces.append((p, nbytes))
+    big = [p for p, n in pieces if n >= 4 * MB]
+    assert big[1] == big[0] + 6 * MB and big[2] == big[1] + 18 * MB   # carved back to back from the pool
+    for p, nbytes in pieces:
+        assert ctypes.string_at(p + nbytes - 1, 1) == b"Z"
+        lib.gcz_host_free(p, nbytes)
+    lib.gcz_host_pool_release(0)
+    lib.gcz_host_pool_release(1)   # (idempotent; async)
+    assert lib.gcz_host_prefault(8 * MB, 2) == 0
+    lib.gcz_host_pool_release(1)
+
+
 def test_fasta_extract_matches_oracle(gcz, oracle, manifest):
     for name, case in manifest.items():
         if case["kind"] != "fasta":
