@@ -174,6 +174,7 @@ fasta_reader open_with_engine(const std::filesystem::path& path) {
   std::thread init([fsize] {   // the context, the input buffer and a warm upload path, while the file maps
     PhaseTimer t{"context"};
     (void)gcz_upload_reserve(engine().ctx, fsize);
+    if (fsize >= (std::uint64_t(64) << 20)) (void)gcz_fetch_reserve(engine().ctx, fsize);   // the fetch's ring
   });
   fasta_reader f = [&] { PhaseTimer t{"map"}; return fasta_reader{path}; }();
   if (!ec && fsize >= (std::uint64_t(64) << 20)) {

@@ -134,8 +134,8 @@ GCZ_API int gcz_copy_layer(gcz_ctx *ctx, int layer, uint32_t *host_out);      /*
  * words), through a pinned staging ring with parallel host copies -- the fast path into fresh,
  * unpinned host memory (the reference's shared_tree containers). */
 GCZ_API int gcz_fetch_host(gcz_ctx *ctx, uint64_t *leaves_out, uint32_t *const *layers_out);
-/* Pin the fetch's staging ring for a DAG of `total_bytes` ahead of time (24 MB at most, a few
- * ms; gcz_fetch_host otherwise does it on its first call). */
+/* Pin the fetch's staging ring for a DAG of `total_bytes` ahead of time (64 MB at most, ~16 ms;
+ * gcz_fetch_host otherwise does it on its first call). */
 GCZ_API int gcz_fetch_reserve(gcz_ctx *ctx, uint64_t total_bytes);
 /* Host storage for fetched trees (the shared_tree containers' allocator): arrays of >= 4 MB are
  * 2 MB-aligned mappings advised as transparent huge pages (the fetch faults them in 2 MB steps

@@ -6,6 +6,9 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 G=genome-compression_amd
 o=gpurun_out/dropin_${1:-r03}.txt
+test -x tools/probe/init_probe || /opt/rocm/bin/hipcc -O2 -std=c++17 -Iinclude tools/probe/init_probe.cpp -L$G -lgcz \
+  -Wl,-rpath,'$ORIGIN/../../genome-compression_amd' -o tools/probe/init_probe || exit $?
+test -x oracle/_ref/ref_compress || { echo "oracle/_ref/ref_compress missing (make -C oracle ref)"; exit 2; }
 : > $o
 for i in 1 2 3; do
   echo "## ref_compress merged $i" >> $o
