@@ -261,8 +261,8 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
   hipLaunchKernelGGL(k_scan_excl<ScanU32>, dim3(unsigned(t_cnt)), dim3(kScanThreads), 0, stream,
                      ScanU32{dl_cnt.as<u32>(), ncnt}, ncnt + 1, dl_off.as<u32>(), sdesc, &tickets[0],
                      static_cast<u64*>(nullptr));
-  hipLaunchKernelGGL(k_dl_offt, dim3((P.nch + 1 + 31) / 32, (P.NB + 31) / 32), dim3(256), 0, stream, dl_off.as<u32>(), P,
-                     dl_offt.as<u32>());
+  hipLaunchKernelGGL(k_dl_tr, dim3((P.nch + 1 + 31) / 32, (P.NB + 31) / 32), dim3(256), 0, stream, dl_off.as<u32>(),
+                     P.NB, P.nch + 1, u64(P.nch), dl_offt.as<u32>());
   HIP_TRY(hipGetLastError());
   prof_end(KID_DL_SCAN, e0);
   prof_begin(KID_DL_SCATTER, e0);
@@ -1122,8 +1122,8 @@ const uint32_t* gcz_device_layer(gcz_ctx* c, int k) {
 // the destination are taken by several threads at once and the DMA never waits for them.
 // The runtime's pageable D2H path copies and faults on one thread (~10 GB/s at 1 Gbase).
 namespace {
-constexpr u64 kRingChunk = u64(8) << 20;   // (pinning costs ~0.25 ms per MB: a small ring)
-constexpr int kRingSlots = 3;
+constexpr u64 kRingChunk = u64(16) << 20;
+constexpr int kRingSlots = 4;
 
 struct CopyPool {   // T - 1 workers + the calling thread copy one chunk's slices, then meet
   int T;
@@ -1184,8 +1184,8 @@ struct CopyPool {   // T - 1 workers + the calling thread copy one chunk's slice
 }  // namespace
 
 // The staging ring for a fetch of `total` bytes: one slot holding a small DAG, else kRingSlots
-// slots of kRingChunk; pinned once per context (hipHostMalloc pins at ~4 GB/s on the box, and
-// beside a running build it slows the upload as much as it saves, so it is not overlapped).
+// slots of kRingChunk; pinned once per context (~16 ms for 64 MB on the box: the drop-in
+// reserves it while the context comes up; two slots or 8 MB ones were measured slower).
 int gcz_fetch_reserve(gcz_ctx* c, uint64_t total) {
   if (!c) return GCZ_ERR_ARG;
   const u64 need = total > kRingChunk ? u64(kRingSlots) * kRingChunk : (total + 4095) & ~u64(4095);

@@ -11,7 +11,8 @@
 //            h = c*K mod 4^L (a bijection, balances the buckets); writes the
 //            pre-word (h | m t v) per strand and a per-chunk histogram of the
 //            NB buckets (h's top bits) -> count matrix, bucket-major.
-//   scan     exclusive sum of the count matrix (gcz_scan.h).
+//   scan     exclusive sum of the count matrix (gcz_scan.h), and its chunk-major
+//            copy (k_dl_tr) for the per-chunk kernels.
 //   scatter  per chunk of 32 Ki strands: records (h's low bits, position in
 //            the chunk) staged in LDS by bucket, written as contiguous runs.
 //   first    one workgroup per bucket: LDS table of the bucket's RB codes,
@@ -111,7 +112,7 @@ static __device__ __forceinline__ u32 block_excl(u32 x, u32* s_tmp, u32* total) 
 
 // The runs (b, ch) of one chunk: s_base[b] = local exclusive offset (s_base[NB] = the
 // chunk's strands), s_dst[b] = the run's start in the record array.  offt: the run starts
-// chunk-major (k_dl_offt), so a chunk reads two contiguous rows of NB words instead of a
+// chunk-major (k_dl_tr), so a chunk reads two contiguous rows of NB words instead of a
 // strided column of the bucket-major scan output.
 static __device__ __forceinline__ void chunk_runs(const u32* __restrict__ offt, const DensePlan& P, u32 ch, u32* s_base,
                                            u32* s_dst, u32* s_tmp) {
@@ -131,20 +132,23 @@ static __device__ __forceinline__ void chunk_runs(const u32* __restrict__ offt, 
   __syncthreads();
 }
 
-// offt[ch][b] = off[b * nch + ch] for ch in [0, nch] (column nch = the bucket's end = the
-// next bucket's start): a 32 x 32 tiled transpose through LDS, coalesced on both sides.
-[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_offt(const u32* __restrict__ off, DensePlan P,
-                                                 u32* __restrict__ offt) {
+// dst[c * rows + r] = src[r * stride + c] (r < rows, c < cols): a 32 x 32 tiled transpose
+// through LDS, coalesced on both sides: the run starts, chunk-major copy of the scan's
+// bucket-major output (rows = NB, cols = nch + 1, stride = nch -- column nch is a bucket's end
+// = the next bucket's start).  (Tried for the pack's count matrix and k_dl_first's chunk
+// offsets too: neutral, not kept.)
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_tr(const u32* __restrict__ src, u32 rows, u32 cols,
+                                               u64 stride, u32* __restrict__ dst) {
   __shared__ u32 t[32][33];
-  const u32 c0 = blockIdx.x * 32, b0 = blockIdx.y * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (u32 r = ty; r < 32; r += 8) {   // rows b, columns ch
-    const u32 b = b0 + r, ch = c0 + tx;
-    if (b < P.NB && ch <= P.nch) t[r][tx] = off[u64(b) * P.nch + ch];
+  const u32 c0 = blockIdx.x * 32, r0 = blockIdx.y * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (u32 i = ty; i < 32; i += 8) {
+    const u32 r = r0 + i, c = c0 + tx;
+    if (r < rows && c < cols) t[i][tx] = src[u64(r) * stride + c];
   }
   __syncthreads();
-  for (u32 r = ty; r < 32; r += 8) {   // rows ch, columns b
-    const u32 ch = c0 + r, b = b0 + tx;
-    if (b < P.NB && ch <= P.nch) offt[u64(ch) * P.NB + b] = t[tx][r];
+  for (u32 i = ty; i < 32; i += 8) {
+    const u32 c = c0 + i, r = r0 + tx;
+    if (r < rows && c < cols) dst[u64(c) * rows + r] = t[tx][i];
   }
 }
 
