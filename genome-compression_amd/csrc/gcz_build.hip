@@ -414,7 +414,7 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     prof_begin(KID_BKT_SCATTER, e0);
     hipLaunchKernelGGL(k_bkt_part, dim3(unsigned(b2.G)), dim3(kBktThreads), size_t(kPartChunk) * 8, stream, a.in,
                        n, p, pnf, pmu, b2, bkt_key.as<u64>(), bkt_cnt.as<u32>(), a.words, mk, d_hdr, a.pcount,
-                       stats.as<u64>());
+                       stats.as<u64>(), a.out, a.count, a.id_off);
     HIP_TRY(hipGetLastError());
     prof_end(KID_BKT_SCATTER, e0);
     prof_begin(KID_BKT_FINE, e0);
@@ -476,8 +476,14 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     if (!a.fused) insert(T, NoRes{});
     else insert(T, SlotRes{nf_set[prev], a.sid_prev});   // (k = 0: the leaves' ids by slot)
   };
-  if (nt.packed) insert_settling(nt.pt);
-  else insert_settling(nt.wt);
+  if (two && !a.fused) {
+    // two-pass levels: k_bkt_part inserts (or, on a level that turned out direct, writes the
+    // words and nodes itself), so the insert would only launch p / 256 empty workgroups
+  } else if (nt.packed) {
+    insert_settling(nt.pt);
+  } else {
+    insert_settling(nt.wt);
+  }
   HIP_TRY(hipGetLastError());
   prof_end(KID_NODE, e0);
   uint4* clr_nf = reinterpret_cast<uint4*>(nf_set[prev]);

@@ -1214,7 +1214,9 @@ __global__ __launch_bounds__(kBlock) void k_resolve_leaf(u32* __restrict__ words
 }
 
 // Block 0 also opens the next level's gate: gate = p (the next level is direct)
-// when this level is all unique or none of the next level's pairs hashes.
+// when this level is all unique or none of the next level's pairs hashes.  One mark per
+// thread: 16 per thread (one 16-B load) was 34 us faster on uniform data but 0.15-0.4 ms
+// slower on tandem data (its repeats' dependent loads serialised per thread), not kept.
 template <class Tab>
 __global__ __launch_bounds__(kBlock) void k_resolve_node(u32* __restrict__ words, u64 p, Tab T,
                                                         const unsigned char* __restrict__ nf,
@@ -1529,8 +1531,23 @@ constexpr u32 kColSlots = 8192;   // its LDS table (load <= 1/2), in the part's 
 [[maybe_unused]] static __global__ __launch_bounds__(kBktThreads) void k_bkt_part(
     const u32* __restrict__ in, u64 n, u64 p, const unsigned char* __restrict__ prev_nf,
     const unsigned char* __restrict__ prev_multi, Bkt2Plan bp, u64* __restrict__ seg, u32* __restrict__ rt,
-    u32* __restrict__ rec, Marks mk, Header* __restrict__ hdr, const u64* prev_count, u64* __restrict__ stats) {
-  if (bkt2_skip(hdr, prev_count, n)) return;
+    u32* __restrict__ rec, Marks mk, Header* __restrict__ hdr, const u64* prev_count, u64* __restrict__ stats,
+    uint2* __restrict__ nodes, u64* __restrict__ count_out, u32 id_off) {
+  if (bkt2_skip(hdr, prev_count, n)) {
+    // the level turned out direct (every child unique): ids are positions; this launch writes
+    // the words and nodes k_node_insert's direct path would (the host launches no insert on
+    // two-pass levels, so its ~p/256 empty workgroups are not paid)
+    const u64 j0 = u64(blockIdx.x) * kPartChunk;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *count_out = p;
+    for (u64 j = j0 + threadIdx.x; j < p && j < j0 + kPartChunk; j += kBktThreads) {
+      u32 l, r, cl, cr, m, t;
+      load_pair(in, n, j, l, r);
+      node_canonical(l, r, cl, cr, m, t);
+      nodes[j] = make_uint2(cl, cr);
+      rec[j] = make_word(u32(j) + id_off, m, t, ulw(l) == ulw(xf(r, 1, 0)));
+    }
+    return;
+  }
   extern __shared__ u64 stage[];   // kPartChunk records (dynamic)
   __shared__ u32 cur[(1u << kPartMaxB1) + 1];
   const bool collapse = hdr && hdr->predup != 0;
