@@ -856,18 +856,25 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     cx->prof_begin(KID_DIST, eb);
     if (!L.counted)
       hipLaunchKernelGGL(k_bucket_count, dim3(nb), dim3(kBlock), 0, cx->stream, L.src, d.blockcnt.as<u32>(), nb);
-    const u32 cpr = (nb + kScanChunk - 1) / kScanChunk;
-    if (u64(R) * cpr > 1024) return fail(GCZ_ERR_CAPACITY, "bucket scan: too many chunks");
-    if (cx->ensure(d.bchunk, u64(R) * cpr * 4 + 64)) return dev_fail("bucket scan");
-    hipLaunchKernelGGL(k_bscan_sum, dim3(R * cpr), dim3(kBlock), 0, cx->stream, d.blockcnt.as<u32>(), nb, cpr,
-                       d.bchunk.as<u32>());
-    hipLaunchKernelGGL(k_bscan_top, dim3(1), dim3(1024), 0, cx->stream, d.bchunk.as<u32>(), u32(R), cpr, dh->sync);
-    hipLaunchKernelGGL(k_bscan_down, dim3(R * cpr), dim3(kBlock), 0, cx->stream, d.blockcnt.as<u32>(), nb, cpr,
-                       d.bchunk.as<u32>());
-    hipLaunchKernelGGL(k_bucket_scatter, dim3(nb), dim3(kBlock), 0, cx->stream, L.src, d.blockcnt.as<u32>(), nb,
-                       d.skey.as<u64>(), d.sidx.as<u32>());
-    hipLaunchKernelGGL(k_dist_pack, dim3(1), dim3(1), 0, cx->stream, cx->hdr.as<Header>(), L.ucount, L.bases, dh,
-                       u32(R));
+    if (u64(R) * nb <= kBscanSmall) {   // one block: the scan, the totals and the sync vector
+      hipLaunchKernelGGL(k_bscan_small, dim3(1), dim3(1024), 0, cx->stream, d.blockcnt.as<u32>(), u32(R), nb, dh->sync,
+                         cx->hdr.as<Header>(), L.ucount, L.bases);
+      hipLaunchKernelGGL(k_bucket_scatter, dim3(nb), dim3(kBlock), 0, cx->stream, L.src, d.blockcnt.as<u32>(), nb,
+                         d.skey.as<u64>(), d.sidx.as<u32>());
+    } else {
+      const u32 cpr = (nb + kScanChunk - 1) / kScanChunk;
+      if (u64(R) * cpr > 1024) return fail(GCZ_ERR_CAPACITY, "bucket scan: too many chunks");
+      if (cx->ensure(d.bchunk, u64(R) * cpr * 4 + 64)) return dev_fail("bucket scan");
+      hipLaunchKernelGGL(k_bscan_sum, dim3(R * cpr), dim3(kBlock), 0, cx->stream, d.blockcnt.as<u32>(), nb, cpr,
+                         d.bchunk.as<u32>());
+      hipLaunchKernelGGL(k_bscan_top, dim3(1), dim3(1024), 0, cx->stream, d.bchunk.as<u32>(), u32(R), cpr, dh->sync);
+      hipLaunchKernelGGL(k_bscan_down, dim3(R * cpr), dim3(kBlock), 0, cx->stream, d.blockcnt.as<u32>(), nb, cpr,
+                         d.bchunk.as<u32>());
+      hipLaunchKernelGGL(k_bucket_scatter, dim3(nb), dim3(kBlock), 0, cx->stream, L.src, d.blockcnt.as<u32>(), nb,
+                         d.skey.as<u64>(), d.sidx.as<u32>());
+      hipLaunchKernelGGL(k_dist_pack, dim3(1), dim3(1), 0, cx->stream, cx->hdr.as<Header>(), L.ucount, L.bases, dh,
+                         u32(R));
+    }
     G_HIP(hipGetLastError());
     cx->prof_end(KID_DIST, eb);
   }

@@ -225,6 +225,53 @@ static __global__ __launch_bounds__(1024) void k_bscan_top(u32* __restrict__ csu
   }
 }
 
+// The whole bucketing scan in one block when the count matrix is small (R x nb <= kBscanSmall
+// entries, e.g. 8 ranks x 636 tiles at 1 Gbase over 8 ranks): exclusive offsets in place in
+// destination-major order, the per-destination totals into tot[0, R) -- k_bscan_sum / top /
+// down in one launch -- and the rest of the sync vector (k_dist_pack's words, thread 0).
+constexpr u32 kBscanSmall = 16384;
+static __global__ __launch_bounds__(1024) void k_bscan_small(u32* __restrict__ a, u32 R, u32 nb, u64* __restrict__ tot,
+                                                             const Header* __restrict__ h,
+                                                             const u64* __restrict__ ucount,
+                                                             const unsigned char* __restrict__ bases) {
+  __shared__ u32 ws[1024 / 64];
+  __shared__ u32 rowst[kMaxRanks + 1];
+  const u32 n = R * nb, tid = threadIdx.x, per = (n + 1023) / 1024, j0 = tid * per;
+  const int lane = tid & 63;
+  u32 x[kBscanSmall / 1024];
+  u32 sum = 0;
+#pragma unroll
+  for (u32 i = 0; i < kBscanSmall / 1024; ++i) {
+    x[i] = i < per && j0 + i < n ? a[j0 + i] : 0u;
+    sum += x[i];
+  }
+  const u32 inc = wave_incl_scan(sum, lane);
+  if (lane == 63) ws[tid >> 6] = inc;
+  __syncthreads();
+  u32 run = inc - sum;
+  for (u32 w = 0; w < (tid >> 6); ++w) run += ws[w];
+#pragma unroll
+  for (u32 i = 0; i < kBscanSmall / 1024; ++i) {
+    if (i < per && j0 + i < n) {
+      const u32 j = j0 + i;
+      if (j % nb == 0) rowst[j / nb] = run;   // a destination row starts here
+      a[j] = run;
+    }
+    run += x[i];
+  }
+  if (tid == 1023) rowst[R] = run;   // (the last thread's run is the grand total)
+  __syncthreads();
+  if (tid < R) tot[tid] = u64(rowst[tid + 1] - rowst[tid]);
+  if (tid == 0) {
+    tot[R] = u64(h->overflow | h->leaf_overflow);
+    tot[R + 1] = ucount ? *ucount : 0ull;
+    const u64 e = h->err_offset;
+    tot[R + 2] = e;
+    tot[R + 3] = (e != ~0ull && bases) ? u64(bases[e]) : 0ull;
+    tot[R + 4] = u64(h->predup);
+  }
+}
+
 static __global__ __launch_bounds__(kBlock) void k_bscan_down(u32* __restrict__ a, u32 nb, u32 cpr,
                                                               const u32* __restrict__ coff) {
   constexpr int kPer = kScanChunk / kBlock;
