@@ -188,7 +188,8 @@ hipError_t allow_lds(F f, int bytes) {   // dynamic LDS above the default 64 KB
 
 }  // namespace
 
-int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool check, bool list, bool* used) {
+int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool check, bool list, bool* used,
+                           u64* vec) {
   *used = false;
   const u64 S = a.S;
   const u32 L = u32(a.L);
@@ -287,7 +288,8 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
   HIP_TRY(hipGetLastError());
   if (list) {
     hipLaunchKernelGGL(k_dl_lh, dim3(unsigned((S + 255) / 256)), dim3(256), 0, stream, dl_pw.as<u32>(),
-                       dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), S, dl_lh.as<u32>());
+                       dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), S, dl_lh.as<u32>(),
+                       static_cast<const Header*>(d_hdr), vec);
     HIP_TRY(hipGetLastError());
   }
   prof_end(KID_DL_FBSCAN, e0);

@@ -349,7 +349,7 @@ struct gcz_ctx {
   // bitmap), B = ids (gid: global ids by hashed code, or null: local) and words
   // (leaves: write the unique leaves, or null).
   int dense_phase_a(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr, gcz_host::u64* ucount, bool check, bool list,
-                    bool* used);
+                    bool* used, gcz_host::u64* vec = nullptr);   // vec (list): the first exchange's status words
   int dense_phase_b(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr, const gcz_host::u32* gid,
                     gcz_host::u64* leaves);
   int node_level(const gcz_host::NodeLevel& a, gcz_dev::Header* d_hdr);

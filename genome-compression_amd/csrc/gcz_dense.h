@@ -553,21 +553,23 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
 
 // Local key list: the hashed code of each first occurrence, in local-id order (the
 // ids of first occurrences increase with position, so the writes are contiguous).
+// vec (optional): the first exchange's status words (pure-ACGT failure flag, local uniques,
+// repetitive-data flag), all settled by the kernels before this one.
 [[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_lh(const u32* __restrict__ pw,
                                                      const unsigned long long* __restrict__ fb,
-                                                     const u32* __restrict__ wpre, u64 S, u32* __restrict__ lh) {
+                                                     const u32* __restrict__ wpre, u64 S, u32* __restrict__ lh,
+                                                     const Header* __restrict__ hdr, u64* __restrict__ vec) {
+  if (vec && blockIdx.x == 0 && threadIdx.x == 0) {
+    vec[0] = hdr->dense_fail;
+    vec[1] = hdr->count[0];
+    vec[2] = hdr->predup;
+  }
   const u64 s = u64(blockIdx.x) * 256 + threadIdx.x;
   if (s >= S) return;
   const unsigned long long m = fb[s >> 6];
   if ((m >> (s & 63)) & 1ull) lh[wpre[s >> 6] + u32(__popcll(m & ((1ull << (s & 63)) - 1ull)))] = pw[s] & kIdx;
 }
 
-// (pure-ACGT failure flag, local uniques, repetitive-data flag) for the first exchange
-[[maybe_unused]] static __global__ void k_dl_vec(const Header* __restrict__ hdr, u64* __restrict__ vec) {
-  vec[0] = hdr->dense_fail;
-  vec[1] = hdr->count[0];
-  vec[2] = hdr->predup;
-}
 
 // the status words behind each rank's bitmap (exchange 1), rank-major into out[3 r + j]
 [[maybe_unused]] static __global__ void k_dl_vecs(const u64* __restrict__ pbs, u64 stride, u64 nw, int R,

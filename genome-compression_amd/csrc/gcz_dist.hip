@@ -670,7 +670,7 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
     u64* vec = cx->dl_pb.as<u64>() + nw;
     bool u = false;
     Header* h = cx->hdr.as<Header>();
-    const int rc = cx->dense_phase_a(la, h, &h->count[0], false, true, &u);
+    const int rc = cx->dense_phase_a(la, h, &h->count[0], false, true, &u, vec);   // (writes vec too)
     if (!rc && !u) return GCZ_OK;   // L or sizes outside the dense level (the same on every rank)
     if (rc) {
       local_rc = rc;
@@ -678,8 +678,6 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
       G_HIP(hipMemcpyAsync(vec, failed_vec, sizeof(failed_vec), hipMemcpyHostToDevice, cx->stream));
       continue;
     }
-    hipLaunchKernelGGL(k_dl_vec, dim3(1), dim3(1), 0, cx->stream, h, vec);
-    G_HIP(hipGetLastError());
   }
   if (local_rc && NL == R) return local_rc == GCZ_ERR_DEVICE ? dev_fail("dense leaves") : local_rc;
   // exchange 1: the presence bitmaps with the status words
@@ -1567,7 +1565,8 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         DistHdr* dh = cx->dist->dhdr.as<DistHdr>();
         const int r = rank[i];
         const u64 n = P.count(r, k), p = P.count(r, k + 1);
-        hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, cx->stream, &dh->cell[k], direct ? n : ~0ull);
+        if (!(nolocal && !direct))   // (only node_level reads the cell: k_node_keys levels need none)
+          hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, cx->stream, &dh->cell[k], direct ? n : ~0ull);
         NodeLevel na;
         na.k = k;
         na.in = cur_in[i];

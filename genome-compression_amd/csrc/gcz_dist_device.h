@@ -299,72 +299,78 @@ static __global__ __launch_bounds__(kBlock) void k_bscan_down(u32* __restrict__ 
   }
 }
 
-// Stable: a block's records keep their order inside each destination segment (rounds
-// in order, waves in order within a round, lanes in order within a wave), so every
+// Stable: a block's records keep their order inside each destination segment (items
+// in order, waves in order within an item, lanes in order within a wave), so every
 // owner receives each source's records in the source's order.  Owners of levels that
 // skip the local dedupe rely on it: the first record of a key is its first occurrence.
 static __global__ __launch_bounds__(kBlock) void k_bucket_scatter(RecSrc s, const u32* __restrict__ boff, u32 nb,
                                                                   u64* __restrict__ skey, u32* __restrict__ sidx) {
   constexpr int kWaves = kBlock / 64;
+  // kPre items per round: their records loaded together (canonical-pair levels: straight-line,
+  // in flight at once), one ballot pass per item, then ONE block-wide exclusive prefix over
+  // the round's (item, wave, destination) counts -- two barriers per kPre items instead of
+  // three per item.  Double-buffered counts: a round zeroes the previous round's buffer.
+  constexpr int kPre = 8;
   __shared__ u32 cur[kMaxRanks];
-  __shared__ u32 wcnt[kWaves][kMaxRanks];
+  __shared__ u32 wcnt[2][kPre][kWaves][kMaxRanks];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid < int(s.R)) cur[tid] = boff[u64(tid) * nb + blockIdx.x];
-  for (int q = tid; q < kWaves * kMaxRanks; q += kBlock) (&wcnt[0][0])[q] = 0;
+  for (int q = tid; q < 2 * kPre * kWaves * kMaxRanks; q += kBlock) (&wcnt[0][0][0][0])[q] = 0;
   __syncthreads();
   const u64 lt = (1ull << lane) - 1;
-  // canonical-pair levels: the records of kPre items are loaded together (straight-line,
-  // in flight at once) instead of one dependent pair of loads per item
-  constexpr int kPre = 8;
   const bool pre = s.canon != nullptr && s.leaves == nullptr;
-  for (int e0 = 0; e0 < kItems; e0 += kPre) {
-    u64 pkey[kPre];
-    u32 plid[kPre];
-    bool pok[kPre];
+  int buf = 0;
+  for (int e0 = 0; e0 < kItems; e0 += kPre, buf ^= 1) {
+    u64 key[kPre];
+    u32 lid[kPre], d[kPre], before[kPre];
+    bool ok[kPre];
     if (pre) {
 #pragma unroll
       for (int q = 0; q < kPre; ++q)
-        pok[q] = rec_get_canon(s, u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid, pkey[q], plid[q]);
+        ok[q] = rec_get_canon(s, u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid, key[q], lid[q]);
     }
 #pragma unroll
     for (int q = 0; q < kPre; ++q) {
-      const u64 idx = u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid;
-      u64 key = 0;
-      u32 lid = 0;
-      bool ok;
-      if (pre) {
-        ok = pok[q];
-        key = pkey[q];
-        lid = plid[q];
-      } else {
-        ok = rec_get(s, idx, key, lid);
+      if (!pre) {
+        key[q] = 0;
+        lid[q] = 0;
+        ok[q] = rec_get(s, u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid, key[q], lid[q]);
       }
-      const u32 d = ok ? owner_of(rec_key(s, key), s.R) : 0u;
-      u32 before = 0;
-      u64 left = __ballot(ok);
+      d[q] = ok[q] ? owner_of(rec_key(s, key[q]), s.R) : 0u;
+      before[q] = 0;
+      u64 left = __ballot(ok[q]);
       while (left) {                                  // one ballot per distinct destination in the wave
         const int leader = __ffsll((long long)left) - 1;
-        const u32 dl = __shfl(d, leader, 64);
-        const u64 m = __ballot(ok && d == dl);
-        if (ok && d == dl) before = __popcll(m & lt);
-        if (lane == leader) wcnt[wave][dl] = u32(__popcll(m));
+        const u32 dl = __shfl(d[q], leader, 64);
+        const u64 m = __ballot(ok[q] && d[q] == dl);
+        if (ok[q] && d[q] == dl) before[q] = __popcll(m & lt);
+        if (lane == leader) wcnt[buf][q][wave][dl] = u32(__popcll(m));
         left &= ~m;
       }
-      __syncthreads();
-      if (ok) {
-        u32 o = cur[d] + before;
-        for (int w = 0; w < wave; ++w) o += wcnt[w][d];
-        skey[o] = key;
-        sidx[o] = lid;
-      }
-      __syncthreads();
-      if (tid < int(s.R)) {
-        u32 t = 0;
-        for (int w = 0; w < kWaves; ++w) { t += wcnt[w][tid]; wcnt[w][tid] = 0; }
-        cur[tid] += t;
-      }
-      __syncthreads();
     }
+    __syncthreads();   // this round's counts
+    if (tid < int(s.R)) {   // per destination: exclusive offsets in (item, wave) order
+#pragma unroll
+      for (int q = 0; q < kPre; ++q)
+        for (int w = 0; w < kWaves; ++w) wcnt[buf ^ 1][q][w][tid] = 0;   // (last round's, all read)
+      u32 run = cur[tid];
+#pragma unroll
+      for (int q = 0; q < kPre; ++q)
+        for (int w = 0; w < kWaves; ++w) {
+          const u32 c = wcnt[buf][q][w][tid];
+          wcnt[buf][q][w][tid] = run;
+          run += c;
+        }
+      cur[tid] = run;
+    }
+    __syncthreads();   // this round's offsets
+#pragma unroll
+    for (int q = 0; q < kPre; ++q)
+      if (ok[q]) {
+        const u32 o = wcnt[buf][q][wave][d[q]] + before[q];
+        skey[o] = key[q];
+        sidx[o] = lid[q];
+      }
   }
 }
 
