@@ -132,12 +132,14 @@ GCZ_API int gcz_copy_leaves(gcz_ctx *ctx, uint64_t *host_out);                /*
 GCZ_API int gcz_copy_layer(gcz_ctx *ctx, int layer, uint32_t *host_out);      /* 2*layer_size words */
 /* The whole DAG in one call: leaves (n_leaves u64) and every layer (layers_out[k]: 2*layer_size
  * words), through a pinned staging ring with parallel host copies -- the fast path into fresh,
- * unpinned host memory (the reference's shared_tree containers). */
+ * unpinned host memory.  Fills what the reference's tree_constructor appends to
+ * shared_tree::leaves / nodes (include/shared_tree.h:221-223, src/shared_tree.cpp:298-308). */
 GCZ_API int gcz_fetch_host(gcz_ctx *ctx, uint64_t *leaves_out, uint32_t *const *layers_out);
 /* Pin the fetch's staging ring for a DAG of `total_bytes` ahead of time (64 MB at most, ~16 ms;
  * gcz_fetch_host otherwise does it on its first call). */
 GCZ_API int gcz_fetch_reserve(gcz_ctx *ctx, uint64_t total_bytes);
-/* Host storage for fetched trees (the shared_tree containers' allocator): arrays of >= 4 MB are
+/* Host storage for fetched trees (the allocator of the drop-in's shared_tree containers, the
+ * reference's std::vector members at include/shared_tree.h:221-222): arrays of >= 4 MB are
  * 2 MB-aligned mappings advised as transparent huge pages (the fetch faults them in 2 MB steps
  * on several threads); gcz_host_free takes the same byte count. */
 GCZ_API void *gcz_host_alloc(uint64_t bytes);
