@@ -214,6 +214,7 @@ struct gcz_ctx {
   gcz_host::DevBuf dl_pw, dl_rec, dl_idrec, dl_cnt, dl_off, dl_offt, dl_fpg, dl_fb, dl_wpre, dl_desc, dl_fl, dl_fo;   // dense leaf level
   gcz_host::DevBuf dl_lh, dl_pb, dl_pbs, dl_lower, dl_pos, dl_list, dl_gid, dl_recv, dl_stage, dl_seg;   // ... multi-rank
   gcz_dev::DensePlan dl_plan{};
+  unsigned probe_ranks = 1;   // ranks sharing the repetitive-data probe (multi-rank dense leaf level)
   gcz_dev::Header* h_hdr = nullptr;   // pinned
   unsigned char* h_ring = nullptr;    // pinned D2H staging ring of the host fetch (gcz_fetch_host)
   gcz_host::u64 h_ring_bytes = 0;

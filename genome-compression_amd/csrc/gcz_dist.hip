@@ -670,7 +670,9 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
     u64* vec = cx->dl_pb.as<u64>() + nw;
     bool u = false;
     Header* h = cx->hdr.as<Header>();
+    cx->probe_ranks = unsigned(R);
     const int rc = cx->dense_phase_a(la, h, &h->count[0], false, true, &u, vec);   // (writes vec too)
+    cx->probe_ranks = 1;
     if (!rc && !u) return GCZ_OK;   // L or sizes outside the dense level (the same on every rank)
     if (rc) {
       local_rc = rc;
