@@ -250,16 +250,24 @@ LEAF_SCOPES = ("leaf_insert", "flagscan_leaf", "resolve_leaf", "dl_pack", "dl_sc
                "dl_fbscan", "dl_ids", "dl_words")
 
 
-def rank_summary(rank, build_ms, trace):
+def rank_summary(rank, build_ms, trace, xlog=None):
     """One rank's profiled build: busy kernel time, exchange scopes (transfer + wait for the
-    peers), host gaps, and when its leaf level ended (ms after the build's start event)."""
+    peers), host gaps, and when its leaf level ended (ms after the build's start event); with
+    the group's exchange log (gcz_group_xlog), every collective's name and the bytes this rank
+    sent to / received from the other ranks."""
     busy = sum(d for k, _, d in trace if k != "exchange")
     xch = [(round(t, 3), round(d, 3)) for k, t, d in trace if k == "exchange"]
     leaf_end = max((t + d for k, t, d in trace if k in LEAF_SCOPES), default=None)
     x = sum(d for _, d in xch)
-    return {"rank": rank, "build_ms": round(build_ms, 3), "busy_ms": round(busy, 3), "exchange_ms": round(x, 3),
-            "gap_ms": round(build_ms - busy - x, 3),
-            "leaf_end_ms": round(leaf_end, 3) if leaf_end is not None else None, "exchanges": xch}
+    out = {"rank": rank, "build_ms": round(build_ms, 3), "busy_ms": round(busy, 3), "exchange_ms": round(x, 3),
+           "gap_ms": round(build_ms - busy - x, 3),
+           "leaf_end_ms": round(leaf_end, 3) if leaf_end is not None else None, "exchanges": xch}
+    if xlog is not None:
+        out["collectives"] = len(xlog)
+        out["sent_bytes"] = sum(e["sent"] for e in xlog)
+        out["recvd_bytes"] = sum(e["recvd"] for e in xlog)
+        out["exchange_log"] = [[e["seq"], e["name"], e["sent"], e["recvd"]] for e in xlog]
+    return out
 
 
 def weak_run(gcz, ctx, group, dist, cfg, args, seed, L, world, rank, barrier):
@@ -455,13 +463,14 @@ def main():
     # wait for peers, host gaps) -- where a rank waits is invisible in the max-over-ranks time
     rank_detail = None
     if mode == "dist":
-        mine = rank_summary(rank, info["build_ms"], prof_ctx.profile_trace())
+        mine = rank_summary(rank, info["build_ms"], prof_ctx.profile_trace(), group.exchange_log(0))
         rank_detail = [mine]
         if dist is not None:
             rank_detail = [None] * world
             dist.all_gather_object(rank_detail, mine)
     elif mode == "virtual":
-        rank_detail = [rank_summary(r, info["build_ms"], c.profile_trace()) for r, c in enumerate(pctxs)]
+        rank_detail = [rank_summary(r, info["build_ms"], c.profile_trace(), group.exchange_log(r))
+                       for r, c in enumerate(pctxs)]
     for c in pctxs:
         c.profile(False)
     prof = tables[0]

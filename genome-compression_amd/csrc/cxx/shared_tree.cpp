@@ -69,6 +69,7 @@ struct PhaseTimer {
 
 void check_build(int rc, gcz_ctx* ctx) {
   if (rc == GCZ_OK) return;
+  gcz_host_pool_release(0);   // (a pre-faulted pool no fetch will use)
   gcz_info info{};
   gcz_info_get(ctx, &info);
   if (rc == GCZ_ERR_SYMBOL) {   // to_nac, src/dna.cpp:44-47
@@ -196,6 +197,9 @@ shared_tree::shared_tree(std::filesystem::path path) : shared_tree{open_with_eng
 shared_tree::shared_tree(fasta_reader file, bool verbose) {
   auto& e = engine();
   std::lock_guard<std::mutex> lock(e.mu);
+  struct PoolGuard {   // the pool open_with_engine faulted in goes whichever way this ends
+    ~PoolGuard() { gcz_host_pool_release(1); }
+  } pool_guard;
   {
     PhaseTimer t{"upload+build"};
     check_build(gcz_build_host_fasta_buffered(e.ctx, file.raw_data(), file.raw_size(), int(dna::size()),

@@ -251,8 +251,9 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
   }
   // repetitive data? (the node inserts' LDS pre-dedupe): in-block repeats of a sample's
   // hashed codes (equal codes <=> equal keys)
-  // (a rank of an R-rank build samples 1/R of that, at least 2^18: the decision is OR-ed
-  // over the ranks, so the whole genome's sample stays ~2^21)
+  // (a rank of an R-rank build samples the first 1/R of that, at least 2^18, of its own
+  // slice: R prefixes, not a spread over the genome; the decision is OR-ed over the ranks
+  // and written back into every rank's header before the node levels, gcz_dist.hip)
   const u64 ip = std::min<u64>(S, std::max<u64>(u64(1) << 18, (u64(1) << 21) / std::max(1u, probe_ranks)));
   hipLaunchKernelGGL(k_dup_probe, dim3(unsigned((ip + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream,
                      dl_pw.as<u32>(), u64(0), ip, d_hdr);

@@ -17,6 +17,11 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <thread>
 #include <rccl/rccl.h>   // types only: the functions are resolved with dlsym
 
@@ -60,6 +65,14 @@ void gcz_dist_state_free(gcz_ctx* c) {
 
 namespace {
 
+// Limit on one exchange (GCZ_DIST_TIMEOUT_S, default 180 s): the shm transport's barrier, the
+// RCCL watchdog (gcz_group::Watch).
+long dist_timeout_s() {
+  const char* e = std::getenv("GCZ_DIST_TIMEOUT_S");
+  const long v = e ? std::atol(e) : 180;
+  return v > 0 ? v : 180;
+}
+
 // ---- transports ------------------------------------------------------------------
 
 struct Transport {
@@ -95,6 +108,36 @@ u64 recv_displ(const std::vector<u64>& M, int R, bool rev, int d, int s) {
   u64 o = 0;
   for (int q = 0; q < s; ++q) o += mcount(M, R, rev, q, d);
   return o;
+}
+
+// One peer's share of rank `me`'s all-to-all, in bytes: what the point-to-point transport
+// (RcclTransport) sends to and receives from `peer` (peer == me: the local copy).  The counts
+// M[s * R + d] (reverse: transposed) place the segments back to back in peer order, or at
+// the explicit element displacements sd[s * R + d] (sender s) / rd[d * R + s] (receiver d).
+// Host tests drive this arithmetic through gcz_dist_p2p_plan against the transport contract.
+struct P2POp {
+  int peer;
+  u64 send_off, send_bytes, recv_off, recv_bytes;
+};
+std::vector<P2POp> p2p_plan(const std::vector<u64>& M, int R, int me, bool rev, size_t elem, const u64* sd,
+                            const u64* rd) {
+  std::vector<P2POp> ops;
+  ops.resize(size_t(R));
+  for (int q = 0; q < R; ++q) {
+    P2POp& o = ops[size_t(q)];
+    o.peer = q;
+    o.send_bytes = mcount(M, R, rev, me, q) * elem;
+    o.recv_bytes = mcount(M, R, rev, q, me) * elem;
+    o.send_off = (sd ? sd[size_t(me) * R + q] : send_displ(M, R, rev, me, q)) * elem;
+    o.recv_off = (rd ? rd[size_t(me) * R + q] : recv_displ(M, R, rev, me, q)) * elem;
+  }
+  return ops;
+}
+// gather to rank 0 = the all-to-all whose only nonzero column is rank 0's
+std::vector<u64> gather_matrix(const std::vector<u64>& cnt, int R) {
+  std::vector<u64> M(size_t(R) * R, 0);
+  for (int s = 0; s < R; ++s) M[size_t(s) * R] = cnt[size_t(s)];
+  return M;
 }
 
 // All ranks in this process on one stream: exchanges are device copies.
@@ -155,6 +198,7 @@ struct RcclApi {
   ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
   ncclResult_t (*GroupStart)() = nullptr;
   ncclResult_t (*GroupEnd)() = nullptr;
   ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
@@ -179,6 +223,7 @@ RcclApi& rccl() {
     GCZ_SYM(GetUniqueId, "ncclGetUniqueId");
     GCZ_SYM(CommInitRank, "ncclCommInitRank");
     GCZ_SYM(CommDestroy, "ncclCommDestroy");
+    GCZ_SYM(CommAbort, "ncclCommAbort");
     GCZ_SYM(GroupStart, "ncclGroupStart");
     GCZ_SYM(GroupEnd, "ncclGroupEnd");
     GCZ_SYM(Send, "ncclSend");
@@ -187,20 +232,26 @@ RcclApi& rccl() {
     GCZ_SYM(Broadcast, "ncclBroadcast");
     GCZ_SYM(GetErrorString, "ncclGetErrorString");
 #undef GCZ_SYM
-    a.ok = a.GetUniqueId && a.CommInitRank && a.CommDestroy && a.GroupStart && a.GroupEnd && a.Send && a.Recv &&
+    a.ok = a.GetUniqueId && a.CommInitRank && a.CommDestroy && a.CommAbort && a.GroupStart && a.GroupEnd && a.Send && a.Recv &&
            a.AllGather && a.Broadcast && a.GetErrorString;
     return a;
   }();
   return api;
 }
 
-// One rank of this process on its own GPU; peers are other processes.
+// One rank of this process on its own GPU; peers are other processes.  Every exchange is
+// one group of ncclSend / ncclRecv (or an ncclAllGather / ncclBroadcast) on the build stream,
+// its transfers planned by p2p_plan.  A collective that does not complete is bounded by the
+// group's watchdog (gcz_group::Watch), which aborts the communicator.
 struct RcclTransport : Transport {
   int me = 0;
-  ncclComm_t comm = nullptr;
+  std::atomic<ncclComm_t> comm{nullptr};
   hipStream_t stream = nullptr;
   ~RcclTransport() override {
-    if (comm) (void)rccl().CommDestroy(comm);
+    if (ncclComm_t c = comm.exchange(nullptr)) (void)rccl().CommDestroy(c);
+  }
+  void abort() {   // (from the watchdog thread: unblocks the stream and any blocked call)
+    if (ncclComm_t c = comm.exchange(nullptr)) (void)rccl().CommAbort(c);
   }
   int check(ncclResult_t r, const char* what) {
     if (r == ncclSuccess) return GCZ_OK;
@@ -214,82 +265,56 @@ struct RcclTransport : Transport {
     }
     return GCZ_OK;
   }
-  int alltoallv(const std::vector<u64>& M, bool rev, size_t elem, const std::vector<const void*>& send,
-                const std::vector<void*>& recv) override {
-    const auto* sb = static_cast<const char*>(send[0]);
-    auto* rb = static_cast<char*>(recv[0]);
-    if (int rc = self_copy(rb + recv_displ(M, world, rev, me, me) * elem,
-                           sb + send_displ(M, world, rev, me, me) * elem, mcount(M, world, rev, me, me) * elem))
-      return rc;
+  int run(const std::vector<P2POp>& ops, const void* send, void* recv) {
+    const auto* sb = static_cast<const char*>(send);
+    auto* rb = static_cast<char*>(recv);
+    ncclComm_t c = comm.load();
+    if (!c) {
+      err = "communicator aborted";
+      return GCZ_ERR_DEVICE;
+    }
+    const P2POp& self = ops[size_t(me)];
+    if (int rc = self_copy(rb + self.recv_off, sb + self.send_off, self.send_bytes)) return rc;
     RcclApi& a = rccl();
     if (int rc = check(a.GroupStart(), "ncclGroupStart")) return rc;
-    for (int q = 0; q < world; ++q) {
-      if (q == me) continue;
-      const u64 sc = mcount(M, world, rev, me, q), rcnt = mcount(M, world, rev, q, me);
-      if (sc) {
-        const ncclResult_t r =
-            a.Send(sb + send_displ(M, world, rev, me, q) * elem, sc * elem, ncclUint8, q, comm, stream);
+    for (const P2POp& o : ops) {
+      if (o.peer == me) continue;
+      if (o.send_bytes) {
+        const ncclResult_t r = a.Send(sb + o.send_off, o.send_bytes, ncclUint8, o.peer, c, stream);
         if (r != ncclSuccess) { (void)a.GroupEnd(); return check(r, "ncclSend"); }
       }
-      if (rcnt) {
-        const ncclResult_t r =
-            a.Recv(rb + recv_displ(M, world, rev, me, q) * elem, rcnt * elem, ncclUint8, q, comm, stream);
+      if (o.recv_bytes) {
+        const ncclResult_t r = a.Recv(rb + o.recv_off, o.recv_bytes, ncclUint8, o.peer, c, stream);
         if (r != ncclSuccess) { (void)a.GroupEnd(); return check(r, "ncclRecv"); }
       }
     }
     return check(a.GroupEnd(), "ncclGroupEnd");
+  }
+  int alltoallv(const std::vector<u64>& M, bool rev, size_t elem, const std::vector<const void*>& send,
+                const std::vector<void*>& recv) override {
+    return run(p2p_plan(M, world, me, rev, elem, nullptr, nullptr), send[0], recv[0]);
   }
   int alltoallv_at(const std::vector<u64>& M, bool rev, size_t elem, const std::vector<u64>& sd,
                    const std::vector<u64>& rd, const std::vector<const void*>& send,
                    const std::vector<void*>& recv) override {
-    const auto* sb = static_cast<const char*>(send[0]);
-    auto* rb = static_cast<char*>(recv[0]);
-    const size_t R = size_t(world);
-    if (int rc = self_copy(rb + rd[me * R + me] * elem, sb + sd[me * R + me] * elem,
-                           mcount(M, world, rev, me, me) * elem))
-      return rc;
-    RcclApi& a = rccl();
-    if (int rc = check(a.GroupStart(), "ncclGroupStart")) return rc;
-    for (int q = 0; q < world; ++q) {
-      if (q == me) continue;
-      const u64 sc = mcount(M, world, rev, me, q), rcnt = mcount(M, world, rev, q, me);
-      if (sc) {
-        const ncclResult_t r = a.Send(sb + sd[me * R + q] * elem, sc * elem, ncclUint8, q, comm, stream);
-        if (r != ncclSuccess) { (void)a.GroupEnd(); return check(r, "ncclSend"); }
-      }
-      if (rcnt) {
-        const ncclResult_t r = a.Recv(rb + rd[me * R + q] * elem, rcnt * elem, ncclUint8, q, comm, stream);
-        if (r != ncclSuccess) { (void)a.GroupEnd(); return check(r, "ncclRecv"); }
-      }
-    }
-    return check(a.GroupEnd(), "ncclGroupEnd");
+    return run(p2p_plan(M, world, me, rev, elem, sd.data(), rd.data()), send[0], recv[0]);
   }
   int allgather(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) override {
-    return check(rccl().AllGather(send[0], recv[0], bytes, ncclUint8, comm, stream), "ncclAllGather");
+    ncclComm_t c = comm.load();
+    if (!c) { err = "communicator aborted"; return GCZ_ERR_DEVICE; }
+    return check(rccl().AllGather(send[0], recv[0], bytes, ncclUint8, c, stream), "ncclAllGather");
   }
   int bcast0(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) override {
     if (!bytes) return GCZ_OK;
+    ncclComm_t c = comm.load();
+    if (!c) { err = "communicator aborted"; return GCZ_ERR_DEVICE; }
     void* buf = me == 0 ? const_cast<void*>(send[0]) : recv[0];   // in place on the root
-    return check(rccl().Broadcast(buf, buf, bytes, ncclUint8, 0, comm, stream), "ncclBroadcast");
+    return check(rccl().Broadcast(buf, buf, bytes, ncclUint8, 0, c, stream), "ncclBroadcast");
   }
   int gather0(const std::vector<u64>& cnt, size_t elem, const std::vector<const void*>& send,
               void* recv0) override {
-    RcclApi& a = rccl();
-    if (me != 0) {
-      if (!cnt[me]) return GCZ_OK;
-      return check(a.Send(send[0], cnt[me] * elem, ncclUint8, 0, comm, stream), "ncclSend");
-    }
-    if (int rc = self_copy(recv0, send[0], cnt[0] * elem)) return rc;
-    if (int rc = check(a.GroupStart(), "ncclGroupStart")) return rc;
-    u64 o = cnt[0];
-    for (int q = 1; q < world; ++q) {
-      if (cnt[q]) {
-        const ncclResult_t r = a.Recv(static_cast<char*>(recv0) + o * elem, cnt[q] * elem, ncclUint8, q, comm, stream);
-        if (r != ncclSuccess) { (void)a.GroupEnd(); return check(r, "ncclRecv"); }
-      }
-      o += cnt[q];
-    }
-    return check(a.GroupEnd(), "ncclGroupEnd");
+    return run(p2p_plan(gather_matrix(cnt, world), world, me, false, elem, nullptr, nullptr), send[0],
+               me == 0 ? recv0 : nullptr);
   }
 };
 
@@ -305,6 +330,7 @@ struct ShmTransport : Transport {
   };
   int me = 0;
   hipStream_t stream = nullptr;
+  long timeout_s = 120;       // barrier limit (GCZ_DIST_TIMEOUT_S)
   size_t cap = 0;             // bytes per rank region
   size_t map_bytes = 0;
   char* base = nullptr;
@@ -325,8 +351,8 @@ struct ShmTransport : Transport {
       const auto t0 = std::chrono::steady_clock::now();
       while (c->sense.load() != local_sense) {
         if (c->failed.load()) { err = "shm transport: a peer failed"; return GCZ_ERR_DEVICE; }
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) {
-          err = "shm transport: barrier timeout";
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(timeout_s)) {
+          err = "shm transport: no peer arrived within " + std::to_string(timeout_s) + " s";
           c->failed.store(1);
           return GCZ_ERR_DEVICE;
         }
@@ -511,6 +537,190 @@ struct gcz_group {
   bool owns_ctx = false;
   Transport* tr = nullptr;
   std::string last_error;
+
+  // ---- exchanges: numbered, logged with their bytes, bounded -------------------------
+  // Every collective of a build is #seq in a sequence every rank runs identically.  The log
+  // (gcz_group_xlog) gives each its bytes to / from the other ranks; GCZ_DIST_STALL =
+  // "rank:seq:seconds" makes that rank sleep before #seq (tests of the bounds below).
+  struct XRec {
+    const char* name;
+    int seq;
+    std::vector<u64> sent, recvd;   // per local rank
+    double t_us;                    // host enqueue time after the build began
+  };
+  std::vector<XRec> xlog;
+  std::chrono::steady_clock::time_point t_build{};
+  // RCCL has no timeout of its own: the watchdog thread is armed from a collective's enqueue
+  // until the host sync that waits for it.  Past GCZ_DIST_TIMEOUT_S it names the first
+  // collective that did not complete (events recorded behind each), prints it, aborts the
+  // communicator (the stream and any blocked call return) and, should the build still not
+  // return, ends the process.
+  struct Watch {
+    struct Pending {
+      int seq;
+      std::string what;
+      hipEvent_t done;   // null while the enqueue call itself runs
+    };
+    RcclTransport* tr;
+    int device, rank;
+    long limit_s = dist_timeout_s();
+    std::mutex mu;
+    std::condition_variable cv;
+    bool armed = false, stop = false;
+    std::atomic<bool> fired{false};
+    std::chrono::steady_clock::time_point deadline{};
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> pool;
+    size_t used = 0;
+    std::string msg;
+    std::thread th;
+    Watch(RcclTransport* t, int dev, int r) : tr(t), device(dev), rank(r) { th = std::thread([this] { loop(); }); }
+    ~Watch() {
+      {
+        std::lock_guard<std::mutex> g(mu);
+        stop = true;
+      }
+      cv.notify_all();
+      th.join();
+      for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+    }
+    void begin(int seq, std::string what) {   // before the enqueue call
+      std::lock_guard<std::mutex> g(mu);
+      if (!armed) {
+        armed = true;
+        deadline = std::chrono::steady_clock::now() + std::chrono::seconds(limit_s);
+        cv.notify_all();
+      }
+      pending.push_back({seq, std::move(what), nullptr});
+    }
+    void end(hipStream_t stream) {   // after it: an event behind the collective
+      std::lock_guard<std::mutex> g(mu);
+      if (used == pool.size()) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return;
+        pool.push_back(e);
+      }
+      hipEvent_t e = pool[used++];
+      if (hipEventRecord(e, stream) == hipSuccess && !pending.empty()) pending.back().done = e;
+    }
+    void disarm() {
+      std::lock_guard<std::mutex> g(mu);
+      armed = false;
+      pending.clear();
+      used = 0;
+      cv.notify_all();
+    }
+    void loop() {
+      (void)hipSetDevice(device);
+      std::unique_lock<std::mutex> lk(mu);
+      while (!stop) {
+        if (!armed) {
+          cv.wait(lk);
+          continue;
+        }
+        if (cv.wait_until(lk, deadline) != std::cv_status::timeout || !armed || stop) continue;
+        std::string what = "the host sync after the last collective";
+        for (const Pending& p : pending)
+          if (!p.done || hipEventQuery(p.done) == hipErrorNotReady) {
+            what = p.what + (p.done ? "" : " (inside the enqueue call)");
+            break;
+          }
+        msg = "rank " + std::to_string(rank) + ": " + what + " has not completed within " +
+              std::to_string(limit_s) + " s (GCZ_DIST_TIMEOUT_S): a peer stalled or failed; RCCL communicator aborted";
+        std::fprintf(stderr, "gcz watchdog: %s\n", msg.c_str());
+        std::fflush(stderr);
+        fired = true;
+        armed = false;
+        lk.unlock();
+        tr->abort();
+        lk.lock();
+        // the aborted collective lets the build return; if it does not, end the process
+        const auto grace = std::chrono::steady_clock::now() + std::chrono::seconds(30);
+        while (!stop && !armed && pending.size() && std::chrono::steady_clock::now() < grace)
+          cv.wait_until(lk, grace);
+        if (!stop && pending.size()) {
+          std::fprintf(stderr, "gcz watchdog: rank %d: the build did not return after the abort; exiting\n", rank);
+          std::fflush(stderr);
+          std::_Exit(70);
+        }
+      }
+    }
+  };
+  std::unique_ptr<Watch> watch;
+  int stall_rank = -1, stall_seq = -1, stall_s = 0;
+  gcz_group() {
+    if (const char* e = std::getenv("GCZ_DIST_STALL"))
+      if (std::sscanf(e, "%d:%d:%d", &stall_rank, &stall_seq, &stall_s) != 3) stall_rank = -1;
+  }
+  int xbegin(const char* name, std::vector<u64> sent, std::vector<u64> recvd) {
+    const int seq = int(xlog.size());
+    const double t = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_build).count();
+    for (int r : rank)
+      if (r == stall_rank && seq == stall_seq) std::this_thread::sleep_for(std::chrono::seconds(stall_s));
+    if (watch)
+      watch->begin(seq, "collective #" + std::to_string(seq) + " " + name + " (this rank sends " +
+                            std::to_string(sent[0]) + " B, receives " + std::to_string(recvd[0]) + " B)");
+    xlog.push_back({name, seq, std::move(sent), std::move(recvd), t});
+    return GCZ_OK;
+  }
+  int xend(int rc) {
+    if (watch) watch->end(ctx[0]->stream);
+    if (rc && tr) {
+      const XRec& x = xlog.back();
+      tr->err = "collective #" + std::to_string(x.seq) + " " + x.name + " (this rank sends " + std::to_string(x.sent[0]) +
+                " B, receives " + std::to_string(x.recvd[0]) + " B): " + tr->err;
+    }
+    return rc;
+  }
+  // the host waits for its streams (the exchanges' counts and status words)
+  int host_sync() {
+    for (gcz_ctx* cx : ctx) {
+      const hipError_t e = hipStreamSynchronize(cx->stream);
+      if (watch && watch->fired) return fail(GCZ_ERR_DEVICE, watch->msg);
+      if (e != hipSuccess) return dev_fail("hipStreamSynchronize");
+    }
+    if (watch) watch->disarm();
+    return GCZ_OK;
+  }
+  std::vector<u64> per_local(const std::function<u64(int)>& f) const {
+    std::vector<u64> v;
+    for (int r : rank) v.push_back(f(r));
+    return v;
+  }
+  int x_alltoallv(const char* name, const std::vector<u64>& M, bool rev, size_t elem, const std::vector<const void*>& s,
+                  const std::vector<void*>& r) {
+    const int R = world;
+    xbegin(name, per_local([&](int me) { u64 t = 0; for (int q = 0; q < R; ++q) if (q != me) t += mcount(M, R, rev, me, q); return t * elem; }),
+           per_local([&](int me) { u64 t = 0; for (int q = 0; q < R; ++q) if (q != me) t += mcount(M, R, rev, q, me); return t * elem; }));
+    return xend(tr->alltoallv(M, rev, elem, s, r));
+  }
+  int x_alltoallv_at(const char* name, const std::vector<u64>& M, bool rev, size_t elem, const std::vector<u64>& sd,
+                     const std::vector<u64>& rd, const std::vector<const void*>& s, const std::vector<void*>& r) {
+    const int R = world;
+    xbegin(name, per_local([&](int me) { u64 t = 0; for (int q = 0; q < R; ++q) if (q != me) t += mcount(M, R, rev, me, q); return t * elem; }),
+           per_local([&](int me) { u64 t = 0; for (int q = 0; q < R; ++q) if (q != me) t += mcount(M, R, rev, q, me); return t * elem; }));
+    return xend(tr->alltoallv_at(M, rev, elem, sd, rd, s, r));
+  }
+  int x_allgather(const char* name, size_t bytes, const std::vector<const void*>& s, const std::vector<void*>& r) {
+    xbegin(name, per_local([&](int) { return u64(bytes) * u64(world - 1); }),
+           per_local([&](int) { return u64(bytes) * u64(world - 1); }));
+    return xend(tr->allgather(bytes, s, r));
+  }
+  int x_bcast0(const char* name, size_t bytes, const std::vector<const void*>& s, const std::vector<void*>& r) {
+    xbegin(name, per_local([&](int me) { return me == 0 ? u64(bytes) * u64(world - 1) : u64(0); }),
+           per_local([&](int me) { return me == 0 ? u64(0) : u64(bytes); }));
+    return xend(tr->bcast0(bytes, s, r));
+  }
+  int x_gather0(const char* name, const std::vector<u64>& cnt, size_t elem, const std::vector<const void*>& s,
+                void* recv0) {
+    xbegin(name, per_local([&](int me) { return me == 0 ? u64(0) : cnt[size_t(me)] * elem; }),
+           per_local([&](int me) {
+             u64 t = 0;
+             if (me == 0) for (int q = 1; q < world; ++q) t += cnt[size_t(q)];
+             return t * elem;
+           }));
+    return xend(tr->gather0(cnt, elem, s, recv0));
+  }
   // last build
   gcz_info info{};
   DistPlan plan;
@@ -538,6 +748,7 @@ struct gcz_group {
   int fail(int code, const std::string& what) {
     last_error = what;
     info.status = code;
+    if (watch && !watch->fired) watch->disarm();   // (a failing rank's peers are bounded by their own)
     for (gcz_ctx* c : ctx) c->fail(code, "group build", what.c_str());
     return code;
   }
@@ -692,7 +903,7 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
     }
     hipEvent_t e0{};
     ctx[0]->prof_begin(KID_EXCHANGE, e0);
-    G_RC(tr->allgather(nwb * 8, s, rv));
+    G_RC(x_allgather("leaf presence bitmaps + status", nwb * 8, s, rv));
     ctx[0]->prof_end(KID_EXCHANGE, e0);
   }
   std::vector<u64> hv(size_t(3) * R + 8);
@@ -701,7 +912,7 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
   G_HIP(hipGetLastError());
   G_HIP(hipMemcpyAsync(hv.data(), ctx[0]->dl_seg.as<u64>() + 8, size_t(3) * R * 8, hipMemcpyDeviceToHost,
                        ctx[0]->stream));
-  for (gcz_ctx* cx : ctx) G_HIP(hipStreamSynchronize(cx->stream));
+  G_RC(host_sync());
   for (int r = 0; r < R; ++r)
     if (hv[3 * r] == 2) return local_rc && local_rc != GCZ_ERR_DEVICE ? local_rc : dev_fail("dense leaves (a rank failed)");
   std::vector<u64> U(R);
@@ -744,12 +955,12 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
     }
     hipEvent_t e0{};
     ctx[0]->prof_begin(KID_EXCHANGE, e0);
-    G_RC(tr->allgather(8, s, rv));
+    G_RC(x_allgather("leaf r-first counts", 8, s, rv));
     ctx[0]->prof_end(KID_EXCHANGE, e0);
   }
   G_HIP(hipMemcpyAsync(hv.data(), ctx[0]->dl_seg.as<u64>() + 8 + 3 * R, size_t(R) * 8, hipMemcpyDeviceToHost,
                        ctx[0]->stream));
-  for (gcz_ctx* cx : ctx) G_HIP(hipStreamSynchronize(cx->stream));
+  G_RC(host_sync());
   c.assign(R, 0);
   off.assign(R + 1, 0);
   for (int r = 0; r < R; ++r) {
@@ -798,14 +1009,14 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
     }
     hipEvent_t e0{};
     ctx[0]->prof_begin(KID_EXCHANGE, e0);
-    G_RC(tr->alltoallv(M1, false, 4, s, rv));
+    G_RC(x_alltoallv("leaf r-first lists, relay 1", M1, false, 4, s, rv));
     std::vector<const void*> s2;
     std::vector<void*> rv2;
     for (gcz_ctx* cx : ctx) {
       s2.push_back(cx->dl_stage.ptr);
       rv2.push_back(cx->dl_recv.ptr);
     }
-    G_RC(tr->alltoallv_at(M2, false, 4, sd2, rd2, s2, rv2));
+    G_RC(x_alltoallv_at("leaf r-first lists, relay 2", M2, false, 4, sd2, rd2, s2, rv2));
     ctx[0]->prof_end(KID_EXCHANGE, e0);
   }
   // global ids, then the words and this rank's slice of the leaves
@@ -887,12 +1098,12 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     }
     hipEvent_t e0{};
     ctx[0]->prof_begin(KID_EXCHANGE, e0);
-    G_RC(tr->allgather(kSyncWords * 8, s, r));
+    G_RC(x_allgather(lv[0].leaves ? "leaf owner counts" : "owner counts", kSyncWords * 8, s, r));
     ctx[0]->prof_end(KID_EXCHANGE, e0);
   }
   gcz_dist_state& d0 = *ctx[0]->dist;
   G_HIP(hipMemcpyAsync(d0.h_gath, d0.gath.ptr, size_t(R) * kSyncWords * 8, hipMemcpyDeviceToHost, ctx[0]->stream));
-  for (gcz_ctx* cx : ctx) G_HIP(hipStreamSynchronize(cx->stream));
+  G_RC(host_sync());
   const u64* gv = d0.h_gath;
   std::vector<u64> M(size_t(R) * R), u(R);
   u64 records = 0;
@@ -984,7 +1195,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     {
       hipEvent_t e0{};
       ctx[0]->prof_begin(KID_EXCHANGE, e0);
-      G_RC(tr->alltoallv(M, false, 8, s, rv));
+      G_RC(x_alltoallv(lv[0].leaves ? "leaf keys to owners" : "keys to owners", M, false, 8, s, rv));
       ctx[0]->prof_end(KID_EXCHANGE, e0);
     }
     s.clear();
@@ -1099,7 +1310,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     {
       hipEvent_t e0{};
       ctx[0]->prof_begin(KID_EXCHANGE, e0);
-      G_RC(tr->alltoallv(M, true, 1, s, rv));
+      G_RC(x_alltoallv("owner replies", M, true, 1, s, rv));
       ctx[0]->prof_end(KID_EXCHANGE, e0);
     }
   }
@@ -1151,11 +1362,11 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     {
       hipEvent_t e0{};
       ctx[0]->prof_begin(KID_EXCHANGE, e0);
-      G_RC(tr->allgather(W * 8, s, rv));
+      G_RC(x_allgather("first counts + C/D sizes", W * 8, s, rv));
       ctx[0]->prof_end(KID_EXCHANGE, e0);
     }
     G_HIP(hipMemcpyAsync(d0.h_gath2, d0.gath2.ptr, size_t(R) * W * 8, hipMemcpyDeviceToHost, ctx[0]->stream));
-    for (gcz_ctx* cx : ctx) G_HIP(hipStreamSynchronize(cx->stream));
+    G_RC(host_sync());
     for (int s2 = 0; s2 < R; ++s2) {
       const u64* v = d0.h_gath2 + size_t(s2) * W;
       c[s2] = v[0];
@@ -1208,7 +1419,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     {
       hipEvent_t e0{};
       ctx[0]->prof_begin(KID_EXCHANGE, e0);
-      G_RC(tr->alltoallv_at(MC, false, 8, SA, RA, s, rv));
+      G_RC(x_alltoallv_at("C ids to owners", MC, false, 8, SA, RA, s, rv));
       ctx[0]->prof_end(KID_EXCHANGE, e0);
     }
     for (int i = 0; i < NL; ++i) {
@@ -1250,7 +1461,7 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     {
       hipEvent_t e0{};
       ctx[0]->prof_begin(KID_EXCHANGE, e0);
-      G_RC(tr->alltoallv_at(MD, true, 8, RA, SA, s, rv));
+      G_RC(x_alltoallv_at("D ids to holders", MD, true, 8, RA, SA, s, rv));
       ctx[0]->prof_end(KID_EXCHANGE, e0);
     }
     for (int i = 0; i < NL; ++i) {
@@ -1295,6 +1506,8 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
   info.L = L;
   info.status = GCZ_OK;
   last_error.clear();
+  xlog.clear();
+  t_build = std::chrono::steady_clock::now();
   const int R = world, NL = int(ctx.size());
   if (L < 1 || L > 16) return fail(GCZ_ERR_ARG, "leaf length L must be in 1..16");
   if (S == 0) return fail(GCZ_ERR_EMPTY, "fewer than L bases: nothing to build");
@@ -1435,12 +1648,12 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
       {
         hipEvent_t e0{};
         ctx[0]->prof_begin(KID_EXCHANGE, e0);
-        G_RC(tr->allgather(8, sv, rv));
+        G_RC(x_allgather("leaf dictionary size", 8, sv, rv));
         ctx[0]->prof_end(KID_EXCHANGE, e0);
       }
       gcz_dist_state& d0 = *ctx[0]->dist;
       G_HIP(hipMemcpyAsync(d0.h_gath, d0.gath.ptr, 8, hipMemcpyDeviceToHost, ctx[0]->stream));
-      for (gcz_ctx* cx : ctx) G_HIP(hipStreamSynchronize(cx->stream));
+      G_RC(host_sync());
       const u64 U = std::min<u64>(d0.h_gath[0], chunks0[c0]);
       std::vector<const void*> ks(NL, nullptr);
       std::vector<void*> kr(NL, nullptr);
@@ -1460,7 +1673,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
       {
         hipEvent_t e0{};
         ctx[0]->prof_begin(KID_EXCHANGE, e0);
-        G_RC(tr->bcast0(U * 8, ks, kr));
+        G_RC(x_bcast0("leaf dictionary", U * 8, ks, kr));
         ctx[0]->prof_end(KID_EXCHANGE, e0);
       }
       for (int i = 0; i < NL; ++i) {
@@ -1524,6 +1737,13 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     for (int i = 0; i < NL; ++i) leaf_offs[i] = u32(off[rank[i]]);
     info.n_leaves = total;
     info.leaf_path = dense ? 1u : 0u;
+    // The repetitive-data decision is the OR over the ranks' probes (each sampled only a
+    // prefix of its own slice): every rank's node levels take the same path from here.
+    if (any_predup) {
+      static const u32 one = 1;
+      for (gcz_ctx* cx : ctx)
+        G_HIP(hipMemcpyAsync(&cx->hdr.as<Header>()->predup, &one, 4, hipMemcpyHostToDevice, cx->stream));
+    }
 
     // ---- distributed node levels ----
     // Without repetitive data the local dedupe of a node level finds almost nothing and
@@ -1658,7 +1878,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         if (rank[i] == 0) recv0 = ctx[i]->dist->tail_in.ptr;
       }
       if (!recv0) recv0 = ctx[0]->dist->tail_in.ptr;   // not used off rank 0
-      G_RC(tr->gather0(cnt, 4, sv, recv0));
+      G_RC(x_gather0("top words to rank 0", cnt, 4, sv, recv0));
     }
     for (int i = 0; i < NL; ++i) {
       gcz_ctx* cx = ctx[i];
@@ -1731,12 +1951,12 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         s.push_back(cx->dist->dhdr.as<DistHdr>()->final_vec);
         rv.push_back(cx->dist->gathf.ptr);
       }
-      G_RC(tr->allgather(kFinalWords * 8, s, rv));
+      G_RC(x_allgather("final vectors", kFinalWords * 8, s, rv));
     }
     gcz_dist_state& d0 = *ctx[0]->dist;
     G_HIP(hipMemcpyAsync(d0.h_gathf, d0.gathf.ptr, size_t(R) * kFinalWords * 8, hipMemcpyDeviceToHost,
                          ctx[0]->stream));
-    for (gcz_ctx* cx : ctx) G_HIP(hipStreamSynchronize(cx->stream));
+    G_RC(host_sync());
     int fo = 0;
     for (int s = 0; s < R; ++s) fo |= int(d0.h_gathf[size_t(s) * kFinalWords]);
     if (fo) {
@@ -1818,18 +2038,20 @@ int gcz_group_create_rccl(gcz_ctx* ctx, int rank, int world, const void* unique_
   t->stream = ctx->stream;
   ncclUniqueId id;
   std::memcpy(&id, unique_id, NCCL_UNIQUE_ID_BYTES);
-  const ncclResult_t r = a.CommInitRank(&t->comm, world, id, rank);
+  ncclComm_t comm = nullptr;
+  const ncclResult_t r = a.CommInitRank(&comm, world, id, rank);
   if (r != ncclSuccess) {
     ctx->last_error = std::string("ncclCommInitRank: ") + a.GetErrorString(r);
-    t->comm = nullptr;
     delete t;
     return GCZ_ERR_DEVICE;
   }
+  t->comm.store(comm);
   auto* g = new gcz_group();
   g->world = world;
   g->tr = t;
   g->ctx.push_back(ctx);
   g->rank.push_back(rank);
+  g->watch.reset(new gcz_group::Watch(t, ctx->device, rank));
   *out = g;
   return GCZ_OK;
 }
@@ -1878,6 +2100,7 @@ int gcz_group_create_shm(gcz_ctx* ctx, int rank, int world, const char* name, ui
   t->world = world;
   t->me = rank;
   t->stream = ctx->stream;
+  t->timeout_s = dist_timeout_s();
   t->cap = cap;
   t->map_bytes = bytes;
   t->base = static_cast<char*>(p);
@@ -1899,7 +2122,9 @@ int gcz_group_create_shm(gcz_ctx* ctx, int rank, int world, const char* name, ui
 
 void gcz_group_destroy(gcz_group* g) {
   if (!g) return;
+  if (g->watch && !g->watch->fired) g->watch->begin(-1, "teardown (collectives a failed build left queued)");
   for (gcz_ctx* c : g->ctx) (void)hipStreamSynchronize(c->stream);
+  g->watch.reset();
   delete g->tr;
   if (g->owns_ctx) {
     // virtual ranks borrowed rank 0's stream (or, split builds, the parent context's)
@@ -1907,6 +2132,47 @@ void gcz_group_destroy(gcz_group* g) {
     for (gcz_ctx* c : g->ctx) gcz_ctx_destroy(c);
   }
   delete g;
+}
+
+int gcz_group_xlog(const gcz_group* g, int local, uint64_t* rec, const char** names, int cap) {
+  if (!g || local < 0 || local >= int(g->ctx.size())) return -1;
+  const int n = int(g->xlog.size());
+  for (int i = 0; i < n && i < cap; ++i) {
+    const gcz_group::XRec& x = g->xlog[size_t(i)];
+    if (rec) {
+      rec[4 * i] = u64(x.seq);
+      rec[4 * i + 1] = x.sent[size_t(local)];
+      rec[4 * i + 2] = x.recvd[size_t(local)];
+      rec[4 * i + 3] = u64(x.t_us);
+    }
+    if (names) names[i] = x.name;
+  }
+  return n;
+}
+
+int gcz_dist_p2p_plan(int world, int me, const uint64_t* M, int reverse, uint64_t elem, const uint64_t* sd,
+                      const uint64_t* rd, uint64_t* out) {
+  if (world < 1 || world > kMaxRanks || me < 0 || me >= world || !M || !out) return GCZ_ERR_ARG;
+  const std::vector<u64> Mv(M, M + size_t(world) * size_t(world));   // (uint64_t -> u64)
+  const auto ops = p2p_plan(Mv, world, me, reverse != 0, size_t(elem), reinterpret_cast<const u64*>(sd),
+                            reinterpret_cast<const u64*>(rd));
+  for (int q = 0; q < world; ++q) {
+    const P2POp& o = ops[size_t(q)];
+    out[5 * q] = o.send_off;
+    out[5 * q + 1] = o.send_bytes;
+    out[5 * q + 2] = o.recv_off;
+    out[5 * q + 3] = o.recv_bytes;
+    out[5 * q + 4] = u64(o.peer);
+  }
+  return GCZ_OK;
+}
+
+int gcz_dist_gather_plan(int world, int me, const uint64_t* cnt, uint64_t elem, uint64_t* out) {
+  if (world < 1 || world > kMaxRanks || me < 0 || me >= world || !cnt || !out) return GCZ_ERR_ARG;
+  const std::vector<u64> c(cnt, cnt + world);
+  const std::vector<u64> Mu = gather_matrix(c, world);
+  const std::vector<uint64_t> M(Mu.begin(), Mu.end());
+  return gcz_dist_p2p_plan(world, me, M.data(), 0, elem, nullptr, nullptr, out);
 }
 
 int gcz_group_n_local(const gcz_group* g) { return g ? int(g->ctx.size()) : 0; }

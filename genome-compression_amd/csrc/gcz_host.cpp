@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstring>
 #include <mutex>
+#include <new>
 #include <numeric>
 #include <thread>
 #include <vector>
@@ -341,8 +342,10 @@ void* map_huge(uint64_t sz) {   // sz: a multiple of kHuge
 }
 }  // namespace
 
+// A C entry point: nullptr when the memory is not there (nothing may throw through the C ABI;
+// gcz_uninit_allocator turns nullptr into std::bad_alloc on the C++ side).
 void* gcz_host_alloc(uint64_t bytes) {
-  if (bytes < kBig) return ::operator new(bytes ? bytes : 1);
+  if (bytes < kBig) return ::operator new(bytes ? bytes : 1, std::nothrow);
   const uint64_t sz = huge_round(bytes);
   {
     std::lock_guard<std::mutex> g(g_pool_mu);
@@ -352,9 +355,7 @@ void* gcz_host_alloc(uint64_t bytes) {
       return p;
     }
   }
-  void* p = map_huge(sz);
-  if (!p) throw std::bad_alloc();
-  return p;
+  return map_huge(sz);
 }
 
 void gcz_host_free(void* p, uint64_t bytes) {

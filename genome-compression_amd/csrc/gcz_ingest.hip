@@ -414,7 +414,10 @@ int gcz_build_device_fasta_buffered(gcz_ctx* c, const void* d_file, uint64_t n, 
   u64 nb = 0;
   if (int rc = gcz_fasta_extract_on_device(c, static_cast<const unsigned char*>(d_file), n, L, buffer_strands, &b, &nb))
     return rc;
-  // buffers already handed out by read_into are not part of the tree (src/shared_tree.cpp:722)
+  // buffers already handed out by read_into are not part of the tree (src/shared_tree.cpp:722);
+  // none left is an empty root list there (reduce_roots' roots.front(): undefined), an error here
+  if (first_strand > 0 && first_strand >= nb / u64(L))
+    return c->fail(GCZ_ERR_ARG, "gcz_build_device_fasta_buffered", "every reader buffer was already read");
   const u64 skip = std::min<u64>(nb / u64(L), first_strand) * u64(L);
   b += skip;
   nb -= skip;

@@ -120,6 +120,12 @@ _SIGS = {
     "gcz_group_rank": (ctypes.c_int, [_P, ctypes.c_int]),
     "gcz_group_ctx": (_P, [_P, ctypes.c_int]),
     "gcz_group_last_error": (ctypes.c_char_p, [_P]),
+    "gcz_group_xlog": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_U64), ctypes.POINTER(ctypes.c_char_p),
+                                      ctypes.c_int]),
+    "gcz_dist_p2p_plan": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_U64), ctypes.c_int, _U64,
+                                         ctypes.POINTER(_U64), ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
+    "gcz_dist_gather_plan": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_U64), _U64,
+                                            ctypes.POINTER(_U64)]),
     "gcz_dist_plan": (ctypes.c_int, [_U64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_U64), ctypes.POINTER(_U64),
                                       ctypes.POINTER(ctypes.c_int)]),
     "gcz_group_build_device_bases": (ctypes.c_int, [_P, ctypes.POINTER(_P), _U64, ctypes.c_int]),
@@ -262,6 +268,41 @@ def dist_plan(S: int, world: int, rank: int):
     if rc != GCZ_OK:
         raise GczError(rc, "gcz_dist_plan: bad arguments")
     return int(s0.value), int(s1.value), int(g.value)
+
+
+def _u64s(a):
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    return a, a.ctypes.data_as(ctypes.POINTER(_U64))
+
+
+def p2p_plan(world: int, me: int, M, reverse: bool, elem: int, sd=None, rd=None) -> np.ndarray:
+    """The RCCL transport's transfers for rank `me` of an all-to-all (gcz_dist_p2p_plan):
+    rows q = {send offset, send bytes, receive offset, receive bytes, q} in bytes."""
+    Ma, Mp = _u64s(np.asarray(M).reshape(-1))
+    keep = [Ma]
+    sdp = rdp = None
+    if sd is not None:
+        a, sdp = _u64s(np.asarray(sd).reshape(-1))
+        keep.append(a)
+    if rd is not None:
+        a, rdp = _u64s(np.asarray(rd).reshape(-1))
+        keep.append(a)
+    out = np.zeros(5 * world, dtype=np.uint64)
+    rc = _lib.gcz_dist_p2p_plan(world, me, Mp, int(bool(reverse)), elem, sdp, rdp,
+                                out.ctypes.data_as(ctypes.POINTER(_U64)))
+    if rc != GCZ_OK:
+        raise GczError(rc, "gcz_dist_p2p_plan: bad arguments")
+    return out.reshape(world, 5)
+
+
+def gather_plan(world: int, me: int, cnt, elem: int) -> np.ndarray:
+    """The RCCL transport's transfers for rank `me` of the gather to rank 0 (same rows)."""
+    c, cp = _u64s(cnt)
+    out = np.zeros(5 * world, dtype=np.uint64)
+    rc = _lib.gcz_dist_gather_plan(world, me, cp, elem, out.ctypes.data_as(ctypes.POINTER(_U64)))
+    if rc != GCZ_OK:
+        raise GczError(rc, "gcz_dist_gather_plan: bad arguments")
+    return out.reshape(world, 5)
 
 
 def dist_unique_id() -> bytes:
@@ -576,6 +617,18 @@ class Group:
         if rc != GCZ_OK:
             raise GczError(rc, "gcz_group_copy_slice failed")
         return out
+
+    def exchange_log(self, i=0) -> list:
+        """The last build's exchanges as local rank i saw them (gcz_group_xlog): name, sequence
+        number, bytes sent to / received from the other ranks, host enqueue time (us)."""
+        n = _lib.gcz_group_xlog(self._h, i, None, None, 0)
+        if n <= 0:
+            return []
+        rec = (_U64 * (4 * n))()
+        names = (ctypes.c_char_p * n)()
+        _lib.gcz_group_xlog(self._h, i, rec, names, n)
+        return [{"seq": int(rec[4 * k]), "name": names[k].decode(), "sent": int(rec[4 * k + 1]),
+                 "recvd": int(rec[4 * k + 2]), "t_us": int(rec[4 * k + 3])} for k in range(n)]
 
     def tree(self) -> Tree:
         t = _lib.gcz_tree_new()

@@ -141,7 +141,8 @@ GCZ_API int gcz_fetch_reserve(gcz_ctx *ctx, uint64_t total_bytes);
 /* Host storage for fetched trees (the allocator of the drop-in's shared_tree containers, the
  * reference's std::vector members at include/shared_tree.h:221-222): arrays of >= 4 MB are
  * 2 MB-aligned mappings advised as transparent huge pages (the fetch faults them in 2 MB steps
- * on several threads); gcz_host_free takes the same byte count. */
+ * on several threads); gcz_host_free takes the same byte count.  NULL when the memory cannot be
+ * had (nothing throws through the C ABI). */
 GCZ_API void *gcz_host_alloc(uint64_t bytes);
 GCZ_API void gcz_host_free(void *p, uint64_t bytes);
 /* Pre-fault `bytes` of that storage (2 MB pages, `threads` host threads) as a pool the next
@@ -243,6 +244,24 @@ GCZ_API int gcz_group_n_local(const gcz_group *g);          /* ranks driven by t
 GCZ_API int gcz_group_rank(const gcz_group *g, int local);
 GCZ_API gcz_ctx *gcz_group_ctx(gcz_group *g, int local);
 GCZ_API const char *gcz_group_last_error(const gcz_group *g);
+/* The exchanges of the group's last build, in order (every rank runs the same sequence):
+ * returns their number; for i < cap, rec[4 i ..] = {sequence number, bytes local rank `local`
+ * sent to other ranks, bytes it received from them, host enqueue time in us after the build
+ * began}, names[i] = the exchange's name (static string).  Either array may be NULL.
+ * Bounds: GCZ_DIST_TIMEOUT_S (default 180) limits one exchange -- the RCCL watchdog names the
+ * collective that did not complete and aborts the communicator, the shm barrier fails;
+ * GCZ_DIST_STALL="rank:seq:seconds" makes a rank sleep before exchange #seq (testing). */
+GCZ_API int gcz_group_xlog(const gcz_group *g, int local, uint64_t *rec, const char **names, int cap);
+/* The point-to-point transfers rank `me` issues in an all-to-all of `world` ranks (the RCCL
+ * transport's own arithmetic, for host tests): counts M[s * world + d] elements of `elem` bytes
+ * (reverse != 0: the transposed exchange), segments packed in peer order or at the explicit
+ * element displacements sd[s * world + d] (sender s) / rd[d * world + s] (receiver d); NULL sd/rd
+ * = packed.  out[5 q ..] = {send offset, send bytes, receive offset, receive bytes, q} in bytes for
+ * peer q (q == me: the local copy).  gcz_dist_gather_plan: the gather of cnt[r] elements of every
+ * rank r to rank 0, concatenated in rank order. */
+GCZ_API int gcz_dist_p2p_plan(int world, int me, const uint64_t *M, int reverse, uint64_t elem, const uint64_t *sd,
+                              const uint64_t *rd, uint64_t *out);
+GCZ_API int gcz_dist_gather_plan(int world, int me, const uint64_t *cnt, uint64_t elem, uint64_t *out);
 /* Strands [s0, s1) of `rank` for an S-strand genome; G = distributed node levels. */
 GCZ_API int gcz_dist_plan(uint64_t S, int world, int rank, uint64_t *s0, uint64_t *s1, int *G);
 /* d_bases[i]: device ASCII bases of local rank i's strands ((s1 - s0) * L bytes). */

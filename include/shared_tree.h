@@ -31,6 +31,7 @@
 #include <filesystem>
 #include <iostream>
 #include <memory>
+#include <new>
 #include <tuple>
 #include <type_traits>
 #include <unordered_map>
@@ -167,7 +168,11 @@ struct gcz_uninit_allocator : std::allocator<T> {
   gcz_uninit_allocator() = default;
   template <class U>
   gcz_uninit_allocator(const gcz_uninit_allocator<U>&) noexcept {}
-  T* allocate(std::size_t n) { return static_cast<T*>(gcz_host_alloc(n * sizeof(T))); }
+  T* allocate(std::size_t n) {   // (the C entry point returns nullptr; the container throws)
+    void* p = gcz_host_alloc(n * sizeof(T));
+    if (!p) throw std::bad_alloc();
+    return static_cast<T*>(p);
+  }
   void deallocate(T* p, std::size_t n) noexcept { gcz_host_free(p, n * sizeof(T)); }
   template <class U>
   void construct(U*) noexcept {

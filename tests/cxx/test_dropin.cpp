@@ -244,9 +244,24 @@ static void gpu_reader_segments() {
   CHECK(cd.reduce(f) == root && dump(d) == dump(host), "reduce(reader) after two read_into calls");
 }
 
+// every buffer handed out before reduce(): nothing is left to build (the reference reduces an
+// empty root list, undefined); the drop-in prints libgcz's error and exits(1) like its other
+// build failures -- run as its own process ("exhausted"), the exit is the expected outcome
+static int gpu_reader_exhausted() {
+  fasta_reader f{dir + "/data/chmpxx", 1000};
+  std::vector<dna> buf;
+  while (f.read_into(buf)) {}
+  shared_tree d;
+  tree_constructor cd{d};
+  cd.reduce(f);
+  std::cout << "reduce() of an exhausted reader returned\n";
+  return 3;
+}
+
 int main(int argc, char** argv) {
   dir = argc > 1 ? argv[1] : "tests/golden";
   const bool gpu = argc > 2 && std::string(argv[2]) == "gpu";
+  if (argc > 2 && std::string(argv[2]) == "exhausted") return gpu_reader_exhausted();
   dna_ops();
   pointer_ops();
   canonical_invariance();

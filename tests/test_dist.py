@@ -317,3 +317,29 @@ def test_dist_owner_hot_pair_overflow(world, gcz, oracle):
         assert t.root == ref.root
     finally:
         g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_dist_skewed_repetitive_slice(world, gcz, groups):
+    """Repetitive data on the LAST rank only (uniform everywhere else): only that rank's probe
+    sees in-block repeats, the OR over the ranks turns the local dedupe on for every rank
+    (written back into each rank's header), and the tree equals the single-device build."""
+    n = 16_000_000
+    uni = gcz.synth(0, n).tobytes()
+    tan = gcz.synth(1, n).tobytes()
+    cut = n - n // (world * 2)           # inside the last rank's slice
+    data = uni[:cut] + tan[cut:]
+    ctx = gcz.Context(0)
+    try:
+        ctx.build_fasta(data, 12)
+        single = ctx.tree()
+        _dist_build(gcz, groups(world), "fasta", data, 12)
+        multi = groups(world).tree()
+        assert np.array_equal(single.leaves(), multi.leaves())
+        assert single.n_layers == multi.n_layers
+        for k in range(single.n_layers):
+            assert np.array_equal(single.layer(k), multi.layer(k)), k
+        assert single.root == multi.root
+    finally:
+        ctx.close()

@@ -34,6 +34,14 @@ def test_dropin_gpu_groups():
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+@pytest.mark.gpu
+def test_dropin_reader_exhausted():
+    """tree_constructor::reduce on a reader whose every buffer was read: libgcz's error, exit 1."""
+    r = subprocess.run([build_test_binary(), GOLDEN, "exhausted"], capture_output=True, text=True)
+    assert r.returncode == 1, r.stdout + r.stderr
+    assert "every reader buffer was already read" in r.stderr
+
+
 def _compress(args, cwd):
     exe = os.path.join(PKG, "compress")
     if not os.path.exists(exe):

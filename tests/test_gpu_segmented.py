@@ -107,3 +107,22 @@ def test_gpu_reader_power_of_two_is_global(gcz, manifest):
             assert compare_digest(gcz.digest(ctx.tree()), exp) == {}, B
     finally:
         ctx.close()
+
+
+def test_gpu_reader_all_buffers_read(gcz):
+    """A reader whose every buffer was already handed out (read_into) leaves no strand to
+    build: the reference reduces an empty root list (undefined); here a clear GCZ_ERR_ARG
+    naming it, and the context builds normally afterwards.  (Parity unpinned: no reference
+    output exists for this case.)"""
+    ctx = gcz.Context(0)
+    try:
+        data = b"ACGT" * 3000          # 1000 strands of 12
+        for B, first in ((100, 1000), (256, 1024), (7, 1001)):
+            with pytest.raises(gcz.GczError) as ei:
+                ctx.build_fasta_buffered(data, 12, B, first)
+            assert ei.value.code == gcz.GCZ_ERR_ARG
+            assert "already read" in str(ei.value)
+        info = ctx.build_fasta_buffered(data, 12, 100, 900)
+        assert info["n_strands"] == 100
+    finally:
+        ctx.close()

@@ -68,3 +68,28 @@ def test_bench_rccl_world1():
     for k in ("layers_sha256_match", "leaves_sha256_match", "root_match", "layer_sizes_match"):
         assert par[k] is True, (k, par)
     assert d["weak_scaling"] is None
+
+
+@pytest.mark.gpu
+def test_bench_multiprocess_stalled_rank_is_bounded():
+    """A rank that stalls before an exchange (GCZ_DIST_STALL = rank:seq:seconds) must not hold
+    the job: its peer leaves that exchange after GCZ_DIST_TIMEOUT_S, the run exits non-zero and
+    the error names the exchange (sequence number and name) -- the diagnosis an 8-GPU run that
+    hangs in RCCL gets from the watchdog (same exchange numbering, gcz_group::Watch)."""
+    import time
+    env = dict(os.environ, GCZ_DIST_STALL="1:2:60", GCZ_DIST_TIMEOUT_S="6")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
+           "--transport", "shm", "--shm-region-mb", "256", "--config", "uniform_100m", "--steps", "1",
+           "--warmup", "0", "--no-cpu-baseline", "--no-parity", "--no-weak"]
+    t0 = time.monotonic()
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=200, cwd=REPO, env=env)
+    dt = time.monotonic() - t0
+    out = p.stdout + p.stderr
+    assert p.returncode != 0, out[-3000:]
+    assert dt < 150, dt
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert lines, out[-3000:]
+    err = json.loads(lines[-1]).get("error", "")
+    assert "collective #2" in err and "leaf r-first lists, relay 1" in err, err
+    assert "no peer arrived within 6 s" in err, err
