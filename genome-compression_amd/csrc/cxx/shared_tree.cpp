@@ -415,21 +415,11 @@ auto shared_tree_on_gpus(const std::filesystem::path& path, int gpus) -> shared_
     std::exit(1);
   }
   gpus = std::max(1, gpus);
-  // layer slots: every layer's ids are < its pair count
-  std::vector<std::uint64_t> loff{0};
-  for (std::uint64_t n = S;;) {
-    const std::uint64_t p = (n + 1) / 2;
-    loff.push_back(loff.back() + p);
-    if (p == 1) break;
-    n = p;
-  }
-  const std::size_t head = (sizeof(MultiShared) + 4095) / 4096 * 4096;
-  const std::size_t rbytes = head + S * 8 + loff.back() * 8;
+  // the ranks' status words, shared across the fork (the tree itself is gathered on the device)
+  const std::size_t rbytes = (sizeof(MultiShared) + 4095) / 4096 * 4096;
   auto* region = static_cast<char*>(::mmap(nullptr, rbytes, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0));
-  if (region == MAP_FAILED) { std::cerr << "libgcz: no memory for the results\n"; std::exit(1); }
+  if (region == MAP_FAILED) { std::cerr << "libgcz: no memory for the rank status\n"; std::exit(1); }
   auto* ms = new (region) MultiShared{};
-  auto* out_leaves = reinterpret_cast<std::uint64_t*>(region + head);
-  auto* out_nodes = reinterpret_cast<std::uint32_t*>(region + head + S * 8);
   const bool shm = [] {
     const char* t = std::getenv("GCZ_MULTI_TRANSPORT");
     return t && std::string_view{t} == "shm";
@@ -492,15 +482,11 @@ auto shared_tree_on_gpus(const std::filesystem::path& path, int gpus) -> shared_
     rank_fail(ms, rank, "upload", rc, ctx);
   const void* dp = d;
   if ((rc = gcz_group_build_device_bases(g, &dp, S, L))) rank_fail(ms, rank, "build", rc, ctx);
-  gcz_info info{};
-  gcz_group_info(g, &info);
-  for (int layer = -1; layer < info.n_layers; ++layer) {   // the rank's slices into place
-    std::uint64_t off = 0, cnt = 0;
-    gcz_group_slice(g, 0, layer, &off, &cnt);
-    void* dst = layer < 0 ? static_cast<void*>(out_leaves + off) : static_cast<void*>(out_nodes + 2 * (loff[layer] + off));
-    if (cnt && (rc = gcz_group_copy_slice(g, 0, layer, dst))) rank_fail(ms, rank, "slice copy", rc, ctx);
-  }
-  if (rank == 0) ms->info = info;
+  // the whole tree gathered device to device into rank 0's engine context (gcz_group_assemble):
+  // there it is a device-resident tree like a one-GPU build's, so the frequency sort, bytes()
+  // and the .dag writer run on the GPU (sort_tree / serialize above)
+  gcz_ctx* dst = rank == 0 ? engine().ctx : nullptr;
+  if ((rc = gcz_group_assemble(g, dst))) rank_fail(ms, rank, "tree gather", rc, ctx);
   gcz_dev_free(ctx, d);
   gcz_group_destroy(g);
   gcz_ctx_destroy(ctx);
@@ -510,15 +496,11 @@ auto shared_tree_on_gpus(const std::filesystem::path& path, int gpus) -> shared_
   for (int r = 1; r < gpus; ++r) ::close(wr[r]);
   if (!ok) { std::cerr << "libgcz: a rank of the multi-GPU build failed\n"; std::exit(1); }
   shared_tree t;
-  const gcz_info& in = ms->info;
-  t.leaves.resize(in.n_leaves);
-  std::memcpy(t.leaves.data(), out_leaves, in.n_leaves * 8);
-  t.nodes.resize(in.n_layers);
-  for (int k = 0; k < in.n_layers; ++k) {
-    t.nodes[k].resize(in.layer_size[k]);
-    std::memcpy(static_cast<void*>(t.nodes[k].data()), out_nodes + 2 * loff[k], in.layer_size[k] * 8);
+  {
+    auto& e = engine();
+    std::lock_guard<std::mutex> lock(e.mu);
+    t.build_from_gpu();
   }
-  t.root = pointer::from_word(in.root);
   ::munmap(region, rbytes);
   ::munmap(bases, fsz + 16);
   return t;

@@ -217,12 +217,11 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
   if ((rc = ensure(dl_pw, S * 4 + 16)) || (rc = ensure(dl_rec, S * 4 + 16)) || (rc = ensure(dl_idrec, S * 4 + 16)) ||
       (rc = ensure(dl_cnt, ncnt * 4 + 16)) || (rc = ensure(dl_off, (ncnt + 1) * 4 + 16)) ||
       (rc = ensure(dl_offt, (ncnt + P.NB) * 4 + 16)) ||
-      (rc = ensure(dl_fpg, ncodes * 4 + 16)) || (rc = ensure(dl_fb, nfb * 8 + 16)) ||
+      (rc = ensure(dl_fpg, ncodes * 4 + 16)) || (rc = ensure(dl_fb, u64(P.nch) * (kDC / 64) * 8 + 16)) ||
       (rc = ensure(dl_wpre, (nfb + 1) * 4 + 16)) || (rc = ensure(dl_desc, (t_cnt + t_fb) * 8 + 16)) ||
       (rc = ensure(dl_fl, ncodes * 4 + 16)) || (rc = ensure(dl_fo, u64(P.NB) * (P.nch + 1) * 4 + 16)))
     return rc;
-  if (list && ((rc = ensure(dl_lh, std::min(S, ncodes) * 4 + 16)) || (rc = ensure(dl_pb, (ncodes / 64 + 1) * 8))))
-    return rc;
+  if (list && (rc = ensure(dl_pb, (ncodes / 64 + 1) * 8))) return rc;
   u64* sdesc = dl_desc.as<u64>();
   u32* tickets = reinterpret_cast<u32*>(sdesc + t_cnt + t_fb);
   const int first_bytes = int(((1u << P.IB) + P.nch + 1) * 4);
@@ -276,10 +275,17 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
   prof_end(KID_DL_SCATTER, e0);
   prof_begin(KID_DL_FIRST, e0);
   if (list && (1u << P.IB) < 64) HIP_TRY(hipMemsetAsync(dl_pb.ptr, 0, (ncodes / 64 + 1) * 8, stream));
+  // (multi-rank, list: first positions, the presence bitmap and the status words only -- the
+  // r-first filter, position bitmap and ranks follow the bitmap exchange, gcz_dist.hip)
   hipLaunchKernelGGL(k_dl_first, dim3(P.NB), dim3(kDThreads), first_bytes, stream, dl_rec.as<u32>(), dl_off.as<u32>(),
-                     P, list ? nullptr : dl_fpg.as<u32>(), dl_fl.as<u32>(), dl_fo.as<u32>(),
-                     list ? dl_pb.as<unsigned long long>() : nullptr);   // (multi-rank: ids come from gid)
+                     P, dl_fpg.as<u32>(), list ? nullptr : dl_fl.as<u32>(), dl_fo.as<u32>(),
+                     list ? dl_pb.as<unsigned long long>() : nullptr, static_cast<const Header*>(d_hdr),
+                     list ? vec : nullptr);
   HIP_TRY(hipGetLastError());
+  if (list) {
+    prof_end(KID_DL_FIRST, e0);
+    return GCZ_OK;
+  }
   hipLaunchKernelGGL(k_dl_fb, dim3(P.nch), dim3(kDThreads), 0, stream, dl_fl.as<u32>(), dl_fo.as<u32>(), P,
                      dl_fb.as<unsigned long long>());
   HIP_TRY(hipGetLastError());
@@ -289,17 +295,11 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
                      ScanPopc{dl_fb.as<unsigned long long>()}, nfb, dl_wpre.as<u32>(), sdesc + t_cnt, &tickets[1],
                      ucount);
   HIP_TRY(hipGetLastError());
-  if (list) {
-    hipLaunchKernelGGL(k_dl_lh, dim3(unsigned((S + 255) / 256)), dim3(256), 0, stream, dl_pw.as<u32>(),
-                       dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), S, dl_lh.as<u32>(),
-                       static_cast<const Header*>(d_hdr), vec);
-    HIP_TRY(hipGetLastError());
-  }
   prof_end(KID_DL_FBSCAN, e0);
   return GCZ_OK;
 }
 
-int gcz_ctx::dense_phase_b(const LeafLevel& a, Header* d_hdr, const u32* gid, u64* leaves) {
+int gcz_ctx::dense_phase_b(const LeafLevel& a, Header* d_hdr, const u32* gid, u64* leaves, bool ids_done) {
   (void)d_hdr;
   const DensePlan& P = dl_plan;
   const int RBbytes = int((1u << P.IB) * 4);
@@ -307,11 +307,13 @@ int gcz_ctx::dense_phase_b(const LeafLevel& a, Header* d_hdr, const u32* gid, u6
   HIP_TRY(allow_lds(k_dl_ids, RBbytes));
   HIP_TRY(allow_lds(k_dl_words, words_bytes));
   hipEvent_t e0{};
-  prof_begin(KID_DL_IDS, e0);
-  hipLaunchKernelGGL(k_dl_ids, dim3(P.NB), dim3(kDThreads), RBbytes, stream, dl_rec.as<u32>(), dl_off.as<u32>(), P,
-                     dl_fpg.as<u32>(), dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), gid, dl_idrec.as<u32>());
-  HIP_TRY(hipGetLastError());
-  prof_end(KID_DL_IDS, e0);
+  if (!ids_done) {   // (multi-rank: k_dl_ids_mr wrote the final words per record)
+    prof_begin(KID_DL_IDS, e0);
+    hipLaunchKernelGGL(k_dl_ids, dim3(P.NB), dim3(kDThreads), RBbytes, stream, dl_rec.as<u32>(), dl_off.as<u32>(), P,
+                       dl_fpg.as<u32>(), dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), gid, dl_idrec.as<u32>());
+    HIP_TRY(hipGetLastError());
+    prof_end(KID_DL_IDS, e0);
+  }
   prof_begin(KID_DL_WORDS, e0);
   hipLaunchKernelGGL(k_dl_words, dim3(P.nch), dim3(kDThreads), words_bytes, stream, dl_rec.as<u32>(),
                      dl_idrec.as<u32>(), dl_offt.as<u32>(), P, dl_fb.as<unsigned long long>(), a.words, leaves);

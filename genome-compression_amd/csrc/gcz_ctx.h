@@ -212,7 +212,9 @@ struct gcz_ctx {
   gcz_host::DevBuf stats;   // hashed-pair counter shards (k_node_insert), summed into hdr->hashed[0]
   gcz_host::DevBuf bkt_key, bkt_cnt, bkt_off, bkt_tmp, bkt_rec2;   // bucketed node insert (k_bkt_*)
   gcz_host::DevBuf dl_pw, dl_rec, dl_idrec, dl_cnt, dl_off, dl_offt, dl_fpg, dl_fb, dl_wpre, dl_desc, dl_fl, dl_fo;   // dense leaf level
-  gcz_host::DevBuf dl_lh, dl_pb, dl_pbs, dl_lower, dl_pos, dl_list, dl_gid, dl_recv, dl_stage, dl_seg;   // ... multi-rank
+  // ... multi-rank: rfc (dl_lh), presence bitmaps (own, gathered), bucket counts + exchange vector (dl_pos),
+  // gathered exchange vectors (dl_lower), G (dl_list), relay table (dl_gid), relay buffers, status words
+  gcz_host::DevBuf dl_lh, dl_pb, dl_pbs, dl_lower, dl_pos, dl_list, dl_gid, dl_recv, dl_stage, dl_seg;
   gcz_dev::DensePlan dl_plan{};
   unsigned probe_ranks = 1;   // ranks sharing the repetitive-data probe (multi-rank dense leaf level)
   gcz_dev::Header* h_hdr = nullptr;   // pinned
@@ -346,13 +348,14 @@ struct gcz_ctx {
   // unique count to *ucount.
   int leaf_level_dense(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr, gcz_host::u64* ucount, bool* used);
   // ... in two phases (gcz_dist.hip exchanges in between): A = local first occurrences
-  // (check: read the pure-ACGT flag on the host; list: the local key list and presence
-  // bitmap), B = ids (gid: global ids by hashed code, or null: local) and words
-  // (leaves: write the unique leaves, or null).
+  // (check: read the pure-ACGT flag on the host; list: first positions by code, the presence
+  // bitmap and the status words vec only), B = ids (gid: by hashed code, null: local;
+  // ids_done: the multi-rank ids kernel already wrote them) and words (leaves: write the
+  // unique leaves, or null).
   int dense_phase_a(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr, gcz_host::u64* ucount, bool check, bool list,
                     bool* used, gcz_host::u64* vec = nullptr);   // vec (list): the first exchange's status words
   int dense_phase_b(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr, const gcz_host::u32* gid,
-                    gcz_host::u64* leaves);
+                    gcz_host::u64* leaves, bool ids_done = false);
   int node_level(const gcz_host::NodeLevel& a, gcz_dev::Header* d_hdr);
   // Known-direct levels k0..k0+nlev-1 in one launch (gcz_device.h k_direct_levels).
   int direct_levels(const gcz_host::u32* in, int k0, int nlev, const gcz_dev::DirectPlan& dp, gcz_host::u32* out,

@@ -332,15 +332,25 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
 // first positions sorted by chunk: fl[b * RB + ...], with fo[ch * NB + b] the start
 // of chunk ch's (a counting sort in LDS; k_dl_fb gathers them per chunk).  pb
 // (multi-rank build, else null): the presence bitmap, bit h set iff hashed code h occurs.
+// fl null (multi-rank phase A): first positions and the presence bitmap only; block 0 also
+// writes the status words vec = {pure-ACGT failure, 0, repetitive data} (settled by the pack
+// and the probe before this launch).
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_first(const u32* __restrict__ rec, const u32* __restrict__ off,
                                                         DensePlan P, u32* __restrict__ fpg, u32* __restrict__ fl,
-                                                        u32* __restrict__ fo, unsigned long long* __restrict__ pb) {
+                                                        u32* __restrict__ fo, unsigned long long* __restrict__ pb,
+                                                        const Header* __restrict__ hdr = nullptr,
+                                                        u64* __restrict__ vec = nullptr) {
   extern __shared__ u32 s_dyn[];
   u32* s_fp = s_dyn;                    // RB codes
   u32* s_cnt = s_dyn + (1u << P.IB);    // nch + 1 chunk counters
   __shared__ u32 s_tmp[16];
   const int tid = threadIdx.x;
   const u32 b = blockIdx.x, RB = 1u << P.IB;
+  if (vec && b == 0 && tid == 0) {
+    vec[0] = hdr->dense_fail;
+    vec[1] = 0;
+    vec[2] = hdr->predup;
+  }
   for (u32 i = tid; i < RB; i += kDThreads) s_fp[i] = ~0u;
   for (u32 c = tid; c <= P.nch; c += kDThreads) s_cnt[c] = 0;
   __syncthreads();
@@ -356,7 +366,7 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
     const u32 i = u32(k) * kDThreads + tid;
     fp[k] = i < RB ? s_fp[i] : ~0u;
     if (fpg && i < RB) fpg[u64(b) * RB + i] = fp[k];
-    rk[k] = fp[k] != ~0u ? atomicAdd(&s_cnt[fp[k] >> kDLog], 1u) : 0u;
+    rk[k] = fl && fp[k] != ~0u ? atomicAdd(&s_cnt[fp[k] >> kDLog], 1u) : 0u;
     if (pb) {
       const u32 h = (b << P.IB) | i;
       if (RB >= 64) {
@@ -367,6 +377,7 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
       }
     }
   }
+  if (!fl) return;
   __syncthreads();
   // exclusive scan of the nch + 1 counters (a few per thread, in order)
   const u32 n1 = P.nch + 1, per = (n1 + kDThreads - 1) / kDThreads, c0 = tid * per;
@@ -543,33 +554,26 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
 
 // ---- multi-rank build (gcz_dist.hip): the leaf level of one rank ----------------
 //
-// Rank r's local dense level gives its keys' local first-occurrence order.  A key's
-// global first occurrence is on the lowest rank that holds it (rank order = position
-// order), so with every rank's presence bitmap (allgather) rank r knows its "r-first"
-// keys (held by no lower rank); their global ids are off_r + their order among
-// rank r's r-first keys, off_r = the r-first counts of lower ranks.  The r-first
-// lists (hashed codes in id order) are exchanged so that every rank can look up the
-// global id of each key it holds; rank r's list is also its slice of the leaves.
-
-// Local key list: the hashed code of each first occurrence, in local-id order (the
-// ids of first occurrences increase with position, so the writes are contiguous).
-// vec (optional): the first exchange's status words (pure-ACGT failure flag, local uniques,
-// repetitive-data flag), all settled by the kernels before this one.
-[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_lh(const u32* __restrict__ pw,
-                                                     const unsigned long long* __restrict__ fb,
-                                                     const u32* __restrict__ wpre, u64 S, u32* __restrict__ lh,
-                                                     const Header* __restrict__ hdr, u64* __restrict__ vec) {
-  if (vec && blockIdx.x == 0 && threadIdx.x == 0) {
-    vec[0] = hdr->dense_fail;
-    vec[1] = hdr->count[0];
-    vec[2] = hdr->predup;
-  }
-  const u64 s = u64(blockIdx.x) * 256 + threadIdx.x;
-  if (s >= S) return;
-  const unsigned long long m = fb[s >> 6];
-  if ((m >> (s & 63)) & 1ull) lh[wpre[s >> 6] + u32(__popcll(m & ((1ull << (s & 63)) - 1ull)))] = pw[s] & kIdx;
-}
-
+// A key's global first occurrence is on the lowest rank holding it (rank order = position
+// order), so with every rank's presence bitmap (one allgather) rank r knows its "r-first"
+// keys (held by no lower rank); their global ids are off_r + their rank among rank r's
+// r-first positions, off_r = the r-first counts of lower ranks.  Per code bucket:
+//
+//   phase A  pack, scan, scatter, first (local first position per code, presence bitmap)
+//   -- allgather the presence bitmaps (+ status words) --
+//   rfirst   per bucket: the r-first codes (present here, in no lower rank's bitmap), their
+//            first positions by chunk (fl/fo, as the single-device first) and in code order
+//            (rfc), and the bucket's count
+//   fb, scan the r-first position bitmap and its popcount prefix: local r-first ranks
+//   gq       per bucket: G[bucket prefix + j] = the local rank of the bucket's j-th r-first
+//            code in CODE order; the bucket prefixes ride in the exchange vector
+//   -- allgather the exchange vectors (r-first count + bucket prefixes); relay the G arrays --
+//   ids      per bucket: the global id of every code present here in LDS -- for each lower
+//            rank q (and r itself) the codes q holds first are present_q & ~(present_0 | ..
+//            | present_{q-1}); a code's index among them in the bucket is a popcount prefix of
+//            those bitmap words, so its id is off_q + G_q[prefix_q(b) + index]: no code-indexed
+//            id table, no list in id order -- then one final word per record
+//   words    as single-device; leaves: rank r's r-first codes in position order.
 
 // the status words behind each rank's bitmap (exchange 1), rank-major into out[3 r + j]
 [[maybe_unused]] static __global__ void k_dl_vecs(const u64* __restrict__ pbs, u64 stride, u64 nw, int R,
@@ -577,71 +581,179 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
   for (int t = threadIdx.x; t < 3 * R; t += blockDim.x) out[t] = pbs[u64(t / 3) * stride + nw + t % 3];
 }
 
-// lower = OR of the presence bitmaps of ranks 0 .. r-1 (pbs: R blocks of stride words, bitmap first)
-[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_lower(const unsigned long long* __restrict__ pbs, u64 nw, u64 stride,
-                                                  int r, unsigned long long* __restrict__ lower) {
-  const u64 w = u64(blockIdx.x) * 256 + threadIdx.x;
-  if (w >= nw) return;
-  unsigned long long x = 0;
-  for (int q = 0; q < r; ++q) x |= pbs[u64(q) * stride + w];
-  lower[w] = x;
+// Bits [64 lw, 64 lw + 64) of bucket b's codes in bitmap bm (RB < 64: the bucket's RB bits).
+static __device__ __forceinline__ u64 bucket_word(const unsigned long long* __restrict__ bm, u32 b, u32 IB, u32 lw) {
+  const u64 h0 = u64(b) << IB;
+  if (IB >= 6) return bm[(h0 >> 6) + lw];
+  return (bm[h0 >> 6] >> (h0 & 63)) & ((1ull << (1u << IB)) - 1ull);
 }
 
-struct ScanRFirst {   // local key j is r-first: no lower rank holds it
-  const u32* lh;
-  const unsigned long long* lower;
-  u64 n;
-  __device__ __forceinline__ u32 operator()(u64 j) const {
-    if (j >= n) return 0u;
-    const u32 h = lh[j];
-    return ((lower[h >> 6] >> (h & 63)) & 1ull) ? 0u : 1u;
-  }
-};
-
-// the r-first keys in local-id order (= global-id order)
-[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_compact(const u32* __restrict__ lh, const unsigned long long* __restrict__ lower,
-                                                    const u32* __restrict__ pos, u64 n, u32* __restrict__ list) {
-  const u64 j = u64(blockIdx.x) * 256 + threadIdx.x;
-  if (j >= n) return;
-  const u32 h = lh[j];
-  if (!((lower[h >> 6] >> (h & 63)) & 1ull)) list[pos[j]] = h;
-}
-
-// Global ids from the gathered lists: recv holds segments (start, len, global id of
-// the first element) in any order; gid[h] = that id + index.
-struct DlSeg {
-  u64 start, len, gbase;
-};
-// (pb, optional: this rank's presence bitmap -- only the codes it holds are looked up, so
-// the others' ids need not be written; measured slower at R = 8, 0.10 vs 0.08 ms: the
-// bitmap read puts a second dependent load in front of every store)
-[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_gid(const u32* __restrict__ recv, const DlSeg* __restrict__ seg, int nseg,
-                                                u64 n, u32* __restrict__ gid,
-                                                const unsigned long long* __restrict__ pb) {
-  __shared__ u64 s_start[1024], s_base[1024];   // segments sorted by start, nonempty
-  for (int q = threadIdx.x; q < nseg; q += 256) {
-    s_start[q] = seg[q].start;
-    s_base[q] = seg[q].gbase;
+// r-first codes of each bucket: fl/fo by chunk (k_dl_fb builds the position bitmap), rfc in
+// code order (rfc[b * RB + j]), bcnt[b].  pbs: the R gathered presence bitmaps (stride words).
+[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_rfirst(const u32* __restrict__ fpg, DensePlan P,
+                                                         const unsigned long long* __restrict__ pbs, u64 stride, int r,
+                                                         u32* __restrict__ fl, u32* __restrict__ fo,
+                                                         u32* __restrict__ rfc, u32* __restrict__ bcnt) {
+  extern __shared__ u32 s_cnt[];   // nch + 1 chunk counters
+  __shared__ u64 s_low[256];       // OR of the lower ranks' words of this bucket
+  __shared__ u32 s_tmp[16];
+  const int tid = threadIdx.x;
+  const u32 b = blockIdx.x, RB = 1u << P.IB, NW = RB >= 64 ? RB / 64 : 1u;
+  for (u32 c = tid; c <= P.nch; c += kDThreads) s_cnt[c] = 0;
+  for (u32 lw = tid; lw < NW; lw += kDThreads) {
+    u64 x = 0;
+    for (int q = 0; q < r; ++q) x |= bucket_word(pbs + u64(q) * stride, b, P.IB, lw);
+    s_low[lw] = x;
   }
   __syncthreads();
-  const u64 e = u64(blockIdx.x) * 256 + threadIdx.x;
-  if (e >= n) return;
-  const u32 h = recv[e];
-  if (pb && !((pb[h >> 6] >> (h & 63)) & 1ull)) return;
-  int lo = 0, hi = nseg - 1;   // last segment starting at or before e
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (s_start[mid] <= e) lo = mid;
-    else hi = mid - 1;
+  constexpr int PER = 16;   // codes per thread, contiguous (RB <= 16 Ki)
+  u32 fp[PER], rk[PER];
+  u32 nrf = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const u32 i = u32(tid) * PER + u32(k);
+    fp[k] = i < RB ? fpg[u64(b) * RB + i] : ~0u;
+    if (fp[k] != ~0u && ((s_low[i >> 6] >> (i & 63)) & 1ull)) fp[k] = ~0u;   // held by a lower rank
+    rk[k] = fp[k] != ~0u ? atomicAdd(&s_cnt[fp[k] >> kDLog], 1u) : 0u;
+    nrf += fp[k] != ~0u ? 1u : 0u;
   }
-  gid[h] = u32(s_base[lo] + (e - s_start[lo]));
+  u32 total;
+  u32 j = block_excl(nrf, s_tmp, &total);   // (its barrier also orders the counters)
+#pragma unroll
+  for (int k = 0; k < PER; ++k)
+    if (fp[k] != ~0u) rfc[u64(b) * RB + j++] = fp[k];
+  if (tid == 0) bcnt[b] = total;
+  // exclusive scan of the nch + 1 chunk counters (a few per thread, in order)
+  const u32 n1 = P.nch + 1, per = (n1 + kDThreads - 1) / kDThreads, c0 = tid * per;
+  u32 loc = 0;
+  for (u32 c = c0; c < c0 + per && c < n1; ++c) loc += s_cnt[c];
+  u32 run = block_excl(loc, s_tmp, &total);
+  for (u32 c = c0; c < c0 + per && c < n1; ++c) {
+    const u32 v = s_cnt[c];
+    s_cnt[c] = run;
+    fo[u64(c) * P.NB + b] = run;
+    run += v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PER; ++k)
+    if (fp[k] != ~0u) fl[u64(b) * RB + s_cnt[fp[k] >> kDLog] + rk[k]] = fp[k];
 }
 
-// This rank's slice of the unique leaves: its r-first list as dna values
-[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_leaves(const u32* __restrict__ list, u64 n, DensePlan P,
-                                                   u64* __restrict__ out) {
-  const u64 k = u64(blockIdx.x) * 256 + threadIdx.x;
-  if (k < n) out[k] = code2_leaf((list[k] * P.Kinv) & P.cmask, P.L);
+// G: per bucket, the local r-first rank of each r-first code in code order, at the bucket's
+// prefix; xv = the rank's exchange vector {r-first count, 0, prefix of bucket 0, 1, ...}.
+[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_gq(const u32* __restrict__ rfc, const u32* __restrict__ bcnt,
+                                                     DensePlan P, const unsigned long long* __restrict__ rfb,
+                                                     const u32* __restrict__ wpre, const u64* __restrict__ ucount,
+                                                     u32* __restrict__ G, u32* __restrict__ xv) {
+  __shared__ u32 s_tmp[16];
+  const int tid = threadIdx.x;
+  const u32 b = blockIdx.x, RB = 1u << P.IB;
+  u32 pre;   // sum over the buckets before b (NB <= kDThreads)
+  (void)block_excl(u32(tid) < b ? bcnt[tid] : 0u, s_tmp, &pre);
+  if (tid == 0) {
+    xv[2 + b] = pre;
+    if (b == 0) {
+      xv[0] = u32(*ucount);
+      xv[1] = 0;
+    }
+  }
+  const u32 n = bcnt[b];
+  for (u32 j = tid; j < n; j += kDThreads) G[pre + j] = fb_rank(rfb, wpre, rfc[u64(b) * RB + j]);
+}
+
+// Where the relay put list q's element j (gcz_dist.hip: piece p = [c_q p / R, c_q (p+1) / R) of
+// every list went through rank p; pos0[q * R + p] = that piece's start in the receive buffer).
+constexpr int kDlMaxRanks = 31;
+struct DlRelay {
+  u64 off[kDlMaxRanks + 1];            // global id offsets (r-first counts of lower ranks)
+  u64 c[kDlMaxRanks];                  // list lengths
+  u64 pos0[kDlMaxRanks * kDlMaxRanks];
+};
+static __device__ __forceinline__ u64 relay_pos(const DlRelay& T, int R, int q, u64 j) {
+  const u64 c = T.c[q];
+  u64 p = (j * u64(R)) / c;   // (j < c)
+  if (p >= u64(R)) p = R - 1;
+  while (p > 0 && c * p / u64(R) > j) --p;
+  while (p + 1 < u64(R) && c * (p + 1) / u64(R) <= j) ++p;
+  return T.pos0[u64(q) * R + p] + (j - c * p / u64(R));
+}
+
+// Global ids of every code present on rank r (LDS), then one final word per record.  pbs /
+// xvs: the gathered presence bitmaps (stride words) and exchange vectors (xstride u32);
+// recv: the relayed G arrays.
+[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_ids_mr(const u32* __restrict__ rec, const u32* __restrict__ off,
+                                                         DensePlan P, const unsigned long long* __restrict__ pbs,
+                                                         u64 stride, const u32* __restrict__ xvs, u64 xstride,
+                                                         const u32* __restrict__ recv, const DlRelay* __restrict__ T,
+                                                         int R, int r, u32* __restrict__ idrec) {
+  extern __shared__ u32 s_id[];    // RB
+  __shared__ u64 s_acc[256], s_rf[256], s_mine[256];
+  __shared__ u32 s_pf[256];
+  __shared__ u32 s_tmp[16];
+  const int tid = threadIdx.x;
+  const u32 b = blockIdx.x, RB = 1u << P.IB, NW = RB >= 64 ? RB / 64 : 1u;
+  for (u32 lw = tid; lw < NW; lw += kDThreads) {
+    s_acc[lw] = 0;
+    s_mine[lw] = bucket_word(pbs + u64(r) * stride, b, P.IB, lw);
+  }
+  for (int q = 0; q <= r; ++q) {
+    const unsigned long long* pq = pbs + u64(q) * stride;
+    u32 pc = 0;
+    if (u32(tid) < NW) {
+      const u64 w = bucket_word(pq, b, P.IB, tid);
+      const u64 rf = w & ~s_acc[tid];
+      s_rf[tid] = rf;
+      s_acc[tid] |= w;
+      pc = u32(__popcll(rf));
+    }
+    u32 total;
+    const u32 e = block_excl(pc, s_tmp, &total);   // (NW <= 256 < kDThreads)
+    if (u32(tid) < NW) s_pf[tid] = e;
+    __syncthreads();
+    if (total) {   // codes first held by q: id = off_q + G_q[prefix_q(b) + index in the bucket]
+      const u64 base = xvs[u64(q) * xstride + 2 + b];
+      for (u32 i = tid; i < RB; i += kDThreads) {
+        const u64 rf = s_rf[i >> 6] & s_mine[i >> 6];   // (codes not held here need no id)
+        if (!((rf >> (i & 63)) & 1ull)) continue;
+        const u64 k = base + s_pf[i >> 6] + u64(__popcll(s_rf[i >> 6] & ((1ull << (i & 63)) - 1ull)));
+        s_id[i] = u32(T->off[q] + recv[relay_pos(*T, R, q, k)]);
+      }
+    }
+    __syncthreads();
+  }
+  const u64 row = u64(b) * P.nch;
+  const u32 r0 = off[row], r1 = off[row + P.nch];
+  for (u32 x0 = r0 + tid; x0 < r1; x0 += kDThreads * kDBatch) {
+    u32 x[kDBatch];
+#pragma unroll
+    for (int j = 0; j < kDBatch; ++j) {
+      const u32 rj = x0 + u32(j) * kDThreads;
+      x[j] = rj < r1 ? rec[rj] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kDBatch; ++j) {
+      const u32 rj = x0 + u32(j) * kDThreads;
+      if (rj < r1) idrec[rj] = s_id[(x[j] & kIdx) >> kDLog] | (x[j] & kBits);
+    }
+  }
+}
+
+// This rank's slice of the unique leaves: its r-first codes in position order (= id order),
+// one thread per word of the r-first position bitmap.
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_rleaves(const unsigned long long* __restrict__ rfb,
+                                                    const u32* __restrict__ wpre, const u32* __restrict__ pw,
+                                                    DensePlan P, u64* __restrict__ out) {
+  const u64 w = u64(blockIdx.x) * 256 + threadIdx.x;
+  if (w >= (P.S + 63) / 64) return;
+  unsigned long long m = rfb[w];
+  u32 k = wpre[w];
+  while (m) {
+    const int bit = __ffsll(m) - 1;
+    m &= m - 1;
+    const u32 h = pw[w * 64 + u64(bit)] & kIdx;
+    out[k++] = code2_leaf((h * P.Kinv) & P.cmask, P.L);
+  }
 }
 
 }  // namespace gcz_dev

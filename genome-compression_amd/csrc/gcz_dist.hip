@@ -756,6 +756,7 @@ struct gcz_group {
     return fail(GCZ_ERR_DEVICE, std::string(what) + (tr && !tr->err.empty() ? ": " + tr->err : ""));
   }
   int build(const void* const* d_bases, const u64* const* d_leaves, u64 S, int L);
+  int assemble(gcz_ctx* dst);
   int alloc(int i, u64 leaf_cap);
   // The dense leaf level of every rank + the presence / r-first-list exchange
   // (gcz_dense.h); *used = false when some strand is not pure ACGT.
@@ -860,8 +861,8 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
   const u64 nw = (ncodes + 63) / 64;   // presence bitmap words
   const u64 nwb = nw + 4;               // + the rank's status words (vec) behind its bitmap
   std::vector<LeafLevel> las(NL);
-  // A. every rank's local first occurrences, key list and presence bitmap.  The status words
-  // (pure ACGT? / local uniques / repetitive?) ride behind the bitmap, so exchange 1 is one
+  // A. every rank's local first positions by code and presence bitmap.  The status words
+  // (pure ACGT? / 0 / repetitive?) ride behind the bitmap, so exchange 1 is one
   // allgather; a rank that fails here still joins it with a failure word (vec[0] = 2), so its
   // peers leave together instead of waiting in a collective it never enters (RCCL has no
   // timeout).
@@ -874,9 +875,8 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
     la.S = P.count(rank[i], 0);
     la.L = L;
     la.words = cx->wa.as<u32>();
-    if (cx->ensure(cx->dl_seg, size_t(64 + 3 * R) * 8 + size_t(R) * R * sizeof(DlSeg) + 64) ||
-        cx->ensure(cx->dl_pb, nwb * 8) || cx->ensure(cx->dl_pbs, size_t(R) * nwb * 8 + 16) ||
-        cx->ensure(cx->dl_lower, nw * 8 + 16))
+    if (cx->ensure(cx->dl_seg, size_t(64 + 3 * R) * 8 + 64) || cx->ensure(cx->dl_pb, nwb * 8) ||
+        cx->ensure(cx->dl_pbs, size_t(R) * nwb * 8 + 16))
       return dev_fail("dense leaf buffers");   // (no word to send: nothing else can be done)
     u64* vec = cx->dl_pb.as<u64>() + nw;
     bool u = false;
@@ -915,64 +915,80 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
   G_RC(host_sync());
   for (int r = 0; r < R; ++r)
     if (hv[3 * r] == 2) return local_rc && local_rc != GCZ_ERR_DEVICE ? local_rc : dev_fail("dense leaves (a rank failed)");
-  std::vector<u64> U(R);
   bool pred = false;
   for (int r = 0; r < R; ++r) {
     if (hv[3 * r]) return GCZ_OK;   // some rank holds a non-ACGT strand: the hash-table leaf level
-    U[r] = hv[3 * r + 1];
     pred = pred || hv[3 * r + 2] != 0;
   }
   any_predup = pred;
-  // r-first keys (held by no lower rank) in local-id order = global-id order
+  // B1: r-first codes (held by no lower rank), their position bitmap and local ranks, and G =
+  // those ranks in code order with the bucket prefixes in the exchange vector (gcz_dense.h)
+  const u32 NB = ctx[0]->dl_plan.NB, RB = 1u << ctx[0]->dl_plan.IB;
+  const u64 xw = (u64(NB) + 2 + 1) & ~u64(1);   // exchange vector words (u32), even
   for (int i = 0; i < NL; ++i) {
     gcz_ctx* cx = ctx[i];
     const int r = rank[i];
-    const u64 ur = U[r], t = scan_tiles(ur + 1);
-    ProfScope ps_(cx, KID_IDS);
-    if (cx->ensure(cx->dl_pos, (ur + 1) * 4 + t * 8 + 64) || cx->ensure(cx->dl_list, ur * 4 + 16))
-      return dev_fail("dense leaf lists");
-    u32* pos = cx->dl_pos.as<u32>();
-    u64* desc = reinterpret_cast<u64*>(pos + ((ur + 1 + 1) & ~u64(1)));
+    const DensePlan& DP = cx->dl_plan;
+    Header* h = cx->hdr.as<Header>();
+    const u64 nfb = (DP.S + 63) / 64, t = scan_tiles(nfb + 1);
+    if (cx->ensure(cx->dl_lh, ncodes * 4 + 16) || cx->ensure(cx->dl_list, std::min<u64>(DP.S, ncodes) * 4 + 16) ||
+        cx->ensure(cx->dl_pos, (u64(NB) + xw) * 4 + t * 8 + 64) || cx->ensure(cx->dl_lower, u64(R) * xw * 4 + 16))
+      return dev_fail("dense leaf buffers");
+    u32* bcnt = cx->dl_pos.as<u32>();
+    u32* xv = bcnt + NB;
+    u64* desc = reinterpret_cast<u64*>(xv + xw);
     u32* ticket = reinterpret_cast<u32*>(desc + t);
-    G_HIP(hipMemsetAsync(desc, 0, t * 8 + 8, cx->stream));
-    hipLaunchKernelGGL(k_dl_lower, dim3(unsigned((nw + 255) / 256)), dim3(256), 0, cx->stream,
-                       cx->dl_pbs.as<unsigned long long>(), nw, nwb, r, cx->dl_lower.as<unsigned long long>());
-    hipLaunchKernelGGL(k_scan_excl<ScanRFirst>, dim3(unsigned(t)), dim3(kScanThreads), 0, cx->stream,
-                       ScanRFirst{cx->dl_lh.as<u32>(), cx->dl_lower.as<unsigned long long>(), ur}, ur + 1, pos, desc,
-                       ticket, cx->dl_seg.as<u64>() + 4);
-    if (ur)
-      hipLaunchKernelGGL(k_dl_compact, dim3(unsigned((ur + 255) / 256)), dim3(256), 0, cx->stream, cx->dl_lh.as<u32>(),
-                         cx->dl_lower.as<unsigned long long>(), pos, ur, cx->dl_list.as<u32>());
-    G_HIP(hipGetLastError());
+    {
+      ProfScope ps_(cx, KID_DL_FIRST);
+      G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_rfirst), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                int((DP.nch + 1) * 4)));
+      hipLaunchKernelGGL(k_dl_rfirst, dim3(NB), dim3(kDThreads), (DP.nch + 1) * 4, cx->stream, cx->dl_fpg.as<u32>(), DP,
+                         cx->dl_pbs.as<unsigned long long>(), nwb, r, cx->dl_fl.as<u32>(), cx->dl_fo.as<u32>(),
+                         cx->dl_lh.as<u32>(), bcnt);
+      hipLaunchKernelGGL(k_dl_fb, dim3(DP.nch), dim3(kDThreads), 0, cx->stream, cx->dl_fl.as<u32>(), cx->dl_fo.as<u32>(),
+                         DP, cx->dl_fb.as<unsigned long long>());
+      G_HIP(hipGetLastError());
+    }
+    {
+      ProfScope ps_(cx, KID_DL_FBSCAN);
+      G_HIP(hipMemsetAsync(desc, 0, t * 8 + 8, cx->stream));
+      hipLaunchKernelGGL(k_scan_excl<ScanPopc>, dim3(unsigned(t)), dim3(kScanThreads), 0, cx->stream,
+                         ScanPopc{cx->dl_fb.as<unsigned long long>()}, nfb, cx->dl_wpre.as<u32>(), desc, ticket,
+                         &h->count[0]);
+      hipLaunchKernelGGL(k_dl_gq, dim3(NB), dim3(kDThreads), 0, cx->stream, cx->dl_lh.as<u32>(), bcnt, DP,
+                         cx->dl_fb.as<unsigned long long>(), cx->dl_wpre.as<u32>(),
+                         static_cast<const u64*>(&h->count[0]), cx->dl_list.as<u32>(), xv);
+      G_HIP(hipGetLastError());
+    }
   }
-  // exchange 2: r-first counts -> id offsets
+  // exchange 2: the exchange vectors (r-first counts -> id offsets; bucket prefixes)
   {
     std::vector<const void*> s;
     std::vector<void*> rv;
     for (gcz_ctx* cx : ctx) {
-      s.push_back(cx->dl_seg.as<u64>() + 4);
-      rv.push_back(cx->dl_seg.as<u64>() + 8 + 3 * R);
+      s.push_back(cx->dl_pos.as<u32>() + NB);
+      rv.push_back(cx->dl_lower.ptr);
     }
     hipEvent_t e0{};
     ctx[0]->prof_begin(KID_EXCHANGE, e0);
-    G_RC(x_allgather("leaf r-first counts", 8, s, rv));
+    G_RC(x_allgather("leaf r-first counts + bucket prefixes", xw * 4, s, rv));
     ctx[0]->prof_end(KID_EXCHANGE, e0);
   }
-  G_HIP(hipMemcpyAsync(hv.data(), ctx[0]->dl_seg.as<u64>() + 8 + 3 * R, size_t(R) * 8, hipMemcpyDeviceToHost,
-                       ctx[0]->stream));
+  std::vector<u32> hx(size_t(R) * xw);
+  G_HIP(hipMemcpyAsync(hx.data(), ctx[0]->dl_lower.ptr, hx.size() * 4, hipMemcpyDeviceToHost, ctx[0]->stream));
   G_RC(host_sync());
   c.assign(R, 0);
   off.assign(R + 1, 0);
   for (int r = 0; r < R; ++r) {
-    c[r] = hv[r];
+    c[r] = hx[size_t(r) * xw];
     off[r + 1] = off[r] + c[r];
   }
   total = off[R];
   if (total > u64(kIdx)) return fail(GCZ_ERR_CAPACITY, "more than 2^29-1 unique leaves");
-  // exchange 3: every rank gets every r-first list, relayed in two steps so no link
-  // carries rank 0's long list R - 1 times: piece q of list r goes to rank q, then each
-  // rank sends the pieces it holds to all ranks
-  auto pc = [&](int r, int q) { return c[r] * u64(q) / u64(R); };   // start of piece q of list r
+  // exchange 3: every rank gets every G array, relayed in two steps so no link carries rank
+  // 0's long one R - 1 times: piece q of array r goes to rank q, then each rank sends the
+  // pieces it holds to all ranks (k_dl_ids_mr finds an element through relay_pos)
+  auto pc = [&](int r, int q) { return c[r] * u64(q) / u64(R); };   // start of piece q of array r
   std::vector<u64> M1(size_t(R) * R), T(R, 0), M2(size_t(R) * R), sd2(size_t(R) * R, 0), rd2(size_t(R) * R);
   for (int r = 0; r < R; ++r)
     for (int q = 0; q < R; ++q) {
@@ -986,58 +1002,63 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
       for (int q2 = 0; q2 < q; ++q2) o += T[q2];
       rd2[size_t(d) * R + q] = o;
     }
-  std::vector<DlSeg> seg;   // (at most R^2 <= 961 nonempty pieces: k_dl_gid holds 1024)
+  DlRelay relay{};
   {
     u64 o = 0;
     for (int q = 0; q < R; ++q)
       for (int r = 0; r < R; ++r) {
-        const u64 len = M1[size_t(r) * R + q];
-        if (len) seg.push_back({o, len, off[r] + pc(r, q)});
-        o += len;
+        relay.pos0[size_t(r) * R + q] = o;
+        o += M1[size_t(r) * R + q];
       }
+    for (int r = 0; r <= R; ++r) relay.off[r] = off[r];
+    for (int r = 0; r < R; ++r) relay.c[r] = c[r];
   }
   {
     std::vector<const void*> s;
     std::vector<void*> rv;
     for (int i = 0; i < NL; ++i) {
       gcz_ctx* cx = ctx[i];
-      if (cx->ensure(cx->dl_stage, T[rank[i]] * 4 + 16) || cx->ensure(cx->dl_recv, total * 4 + 16) ||
-          cx->ensure(cx->dl_gid, ncodes * 4 + 16))
+      if (cx->ensure(cx->dl_stage, T[rank[i]] * 4 + 16) || cx->ensure(cx->dl_recv, total * 4 + 16))
         return dev_fail("dense leaf relay");
       s.push_back(cx->dl_list.ptr);
       rv.push_back(cx->dl_stage.ptr);
     }
     hipEvent_t e0{};
     ctx[0]->prof_begin(KID_EXCHANGE, e0);
-    G_RC(x_alltoallv("leaf r-first lists, relay 1", M1, false, 4, s, rv));
+    G_RC(x_alltoallv("leaf G arrays, relay 1", M1, false, 4, s, rv));
     std::vector<const void*> s2;
     std::vector<void*> rv2;
     for (gcz_ctx* cx : ctx) {
       s2.push_back(cx->dl_stage.ptr);
       rv2.push_back(cx->dl_recv.ptr);
     }
-    G_RC(x_alltoallv_at("leaf r-first lists, relay 2", M2, false, 4, sd2, rd2, s2, rv2));
+    G_RC(x_alltoallv_at("leaf G arrays, relay 2", M2, false, 4, sd2, rd2, s2, rv2));
     ctx[0]->prof_end(KID_EXCHANGE, e0);
   }
-  // global ids, then the words and this rank's slice of the leaves
+  // B2: the global id of every code held here and the final word per record, the words in
+  // position order, and this rank's slice of the leaves
   for (int i = 0; i < NL; ++i) {
     gcz_ctx* cx = ctx[i];
+    const int r = rank[i];
+    const DensePlan& DP = cx->dl_plan;
     Header* h = cx->hdr.as<Header>();
     {
       ProfScope ps_(cx, KID_IDS);
-      DlSeg* dseg = reinterpret_cast<DlSeg*>(cx->dl_seg.as<u64>() + 64 + 3 * R);
-      G_HIP(hipMemcpyAsync(dseg, seg.data(), seg.size() * sizeof(DlSeg), hipMemcpyHostToDevice, cx->stream));
-      if (total)
-        hipLaunchKernelGGL(k_dl_gid, dim3(unsigned((total + 255) / 256)), dim3(256), 0, cx->stream,
-                           cx->dl_recv.as<u32>(), dseg, int(seg.size()), total, cx->dl_gid.as<u32>(),
-                           static_cast<const unsigned long long*>(nullptr));   // (filtering by presence: slower)
-      const u64 cr = c[rank[i]];
+      if (cx->ensure(cx->dl_gid, sizeof(DlRelay) + 16)) return dev_fail("dense leaf relay table");
+      G_HIP(hipMemcpyAsync(cx->dl_gid.ptr, &relay, sizeof(DlRelay), hipMemcpyHostToDevice, cx->stream));
+      G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_ids_mr), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                int(RB * 4)));
+      hipLaunchKernelGGL(k_dl_ids_mr, dim3(NB), dim3(kDThreads), RB * 4, cx->stream, cx->dl_rec.as<u32>(),
+                         cx->dl_off.as<u32>(), DP, cx->dl_pbs.as<unsigned long long>(), nwb, cx->dl_lower.as<u32>(), xw,
+                         cx->dl_recv.as<u32>(), cx->dl_gid.as<DlRelay>(), R, r, cx->dl_idrec.as<u32>());
+      const u64 cr = c[r];
       if (cr)
-        hipLaunchKernelGGL(k_dl_leaves, dim3(unsigned((cr + 255) / 256)), dim3(256), 0, cx->stream,
-                           cx->dl_list.as<u32>(), cr, cx->dl_plan, cx->leaves_out.as<u64>());
+        hipLaunchKernelGGL(k_dl_rleaves, dim3(unsigned(((DP.S + 63) / 64 + 255) / 256)), dim3(256), 0, cx->stream,
+                           cx->dl_fb.as<unsigned long long>(), cx->dl_wpre.as<u32>(), cx->dl_pw.as<u32>(), DP,
+                           cx->leaves_out.as<u64>());
       G_HIP(hipGetLastError());
     }
-    if (int rc = cx->dense_phase_b(las[i], h, cx->dl_gid.as<u32>(), nullptr))
+    if (int rc = cx->dense_phase_b(las[i], h, nullptr, nullptr, true))
       return rc == GCZ_ERR_DEVICE ? dev_fail("dense leaves") : rc;
   }
   *used = true;
@@ -1987,7 +2008,75 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
   return GCZ_OK;
 }
 
+// The whole tree in dst's arrays in the single-device layout (gcz_ctx::build: layer k at
+// layer_off[k], ceil(n_k / 2) slots; leaves first), so dst's device sort, .dag writer,
+// decompression and host fetch run on it as on a one-GPU build (reference: sort_tree / bytes /
+// serialize, src/shared_tree.cpp:443-513).  Every layer is the rank-ordered concatenation of
+// the rank slices: all ranks local -> device copies; one rank per process -> one gather to
+// rank 0 per layer over the transport (dst: rank 0's context, a different one from the
+// group's; unused on the other ranks).
+int gcz_group::assemble(gcz_ctx* dst) {
+  const int R = world, NL = int(ctx.size());
+  const bool here = NL == R;   // every rank local
+  int i0 = -1;
+  for (int i = 0; i < NL; ++i)
+    if (rank[i] == 0) i0 = i;
+  const bool root = i0 >= 0;
+  if (root && !dst) return fail(GCZ_ERR_ARG, "assemble: rank 0 needs a destination context");
+  if (info.status != GCZ_OK || slice_cnt.empty()) return fail(GCZ_ERR_ARG, "assemble: no finished build");
+  const int D = info.n_layers;
+  const u64 S = info.n_strands;
+  std::vector<u64> loff(D + 1, 0);
+  {
+    u64 n = S;
+    for (int k = 0; k < D; ++k) {
+      const u64 p = (n + 1) / 2;
+      loff[k + 1] = loff[k] + p;
+      n = p;
+    }
+  }
+  hipStream_t st = ctx[0]->stream;
+  if (root) {
+    if (dst->ensure(dst->leaves_out, S * 8 + 16) || dst->ensure(dst->nodes_out, loff[D] * 8 + 16))
+      return dev_fail("assemble: destination arrays");
+    dst->layer_off = loff;
+    if (dst->stream != st) G_HIP(hipStreamSynchronize(dst->stream));   // (its earlier work on the arrays)
+  }
+  for (int layer = -1; layer < D; ++layer) {
+    auto src_of = [&](int i) -> const void* {
+      return layer < 0 ? ctx[i]->leaves_out.ptr : static_cast<const void*>(ctx[i]->nodes_out.as<uint2>() + node_base[i][layer]);
+    };
+    char* out = !root ? nullptr
+                      : layer < 0 ? reinterpret_cast<char*>(dst->leaves_out.as<u64>())
+                                  : reinterpret_cast<char*>(dst->nodes_out.as<uint2>() + loff[layer]);
+    if (here) {
+      for (int i = 0; i < NL; ++i) {
+        const u64 o = slice_off[layer + 1][rank[i]], n = slice_cnt[layer + 1][rank[i]];
+        if (n) G_HIP(hipMemcpyAsync(out + o * 8, src_of(i), n * 8, hipMemcpyDeviceToDevice, st));
+      }
+    } else {
+      std::vector<u64> cnt(R);
+      for (int r = 0; r < R; ++r) cnt[r] = slice_cnt[layer + 1][r];
+      G_RC(x_gather0(layer < 0 ? "leaves to rank 0" : "tree layer to rank 0", cnt, 8, {src_of(0)}, out));
+    }
+  }
+  G_RC(host_sync());
+  if (root) {
+    dst->info = info;
+    dst->info.status = GCZ_OK;
+    dst->dense_used = info.leaf_path == 1;
+    dst->last_error.clear();
+  }
+  return GCZ_OK;
+}
+
 extern "C" {
+
+int gcz_group_assemble(gcz_group* g, gcz_ctx* dst) {
+  if (!g) return GCZ_ERR_ARG;
+  if (hipSetDevice(g->ctx[0]->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  return g->assemble(dst);
+}
 
 int gcz_dist_unique_id(void* out, uint64_t cap) {
   if (!out || cap < NCCL_UNIQUE_ID_BYTES) return GCZ_ERR_ARG;
@@ -2311,29 +2400,11 @@ int gcz_split_build(gcz_ctx* c, const void* d_bases, const u64* d_leaves, u64 S,
     c->info.status = rc;
     return rc;
   }
-  // assemble: the layout of gcz_ctx::build (layer k stored at layer_off[k], ceil(n_k / 2) slots)
+  // assemble: the layout of gcz_ctx::build (one stream: the copies follow the build)
   const gcz_info& gi = g->info;
-  const int D = gi.n_layers;
-  c->layer_off.assign(D + 1, 0);
-  u64 n = S;
-  for (int k = 0; k < D; ++k) {
-    const u64 p = (n + 1) / 2;
-    c->layer_off[k + 1] = c->layer_off[k] + p;
-    n = p;
-  }
-  if (int e = c->ensure(c->leaves_out, S * 8 + 16)) return e;
-  if (int e = c->ensure(c->nodes_out, c->layer_off[D] * 8 + 16)) return e;
-  for (int i = 0; i < R; ++i) {
-    gcz_ctx* v = g->ctx[i];
-    for (int layer = -1; layer < D; ++layer) {
-      uint64_t off = 0, cnt = 0;
-      if (gcz_group_slice(g, i, layer, &off, &cnt) || !cnt) continue;
-      void* dst = layer < 0 ? static_cast<void*>(c->leaves_out.as<u64>() + off)
-                            : static_cast<void*>(c->nodes_out.as<uint2>() + c->layer_off[layer] + off);
-      const void* src = layer < 0 ? v->leaves_out.ptr
-                                  : static_cast<const void*>(v->nodes_out.as<uint2>() + g->node_base[i][layer]);
-      SPLIT_HIP(hipMemcpyAsync(dst, src, cnt * 8, hipMemcpyDeviceToDevice, c->stream));
-    }
+  if (int e = g->assemble(c)) {
+    c->fail(e, "build", g->last_error.c_str());
+    return e;
   }
   SPLIT_HIP(hipEventRecord(c->ev_stop, c->stream));
   SPLIT_HIP(hipEventSynchronize(c->ev_stop));

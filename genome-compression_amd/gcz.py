@@ -120,6 +120,7 @@ _SIGS = {
     "gcz_group_rank": (ctypes.c_int, [_P, ctypes.c_int]),
     "gcz_group_ctx": (_P, [_P, ctypes.c_int]),
     "gcz_group_last_error": (ctypes.c_char_p, [_P]),
+    "gcz_group_assemble": (ctypes.c_int, [_P, _P]),
     "gcz_group_xlog": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_U64), ctypes.POINTER(ctypes.c_char_p),
                                       ctypes.c_int]),
     "gcz_dist_p2p_plan": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_U64), ctypes.c_int, _U64,
@@ -617,6 +618,15 @@ class Group:
         if rc != GCZ_OK:
             raise GczError(rc, "gcz_group_copy_slice failed")
         return out
+
+    def assemble(self, dst: "Context" = None) -> dict:
+        """The last build's whole tree into `dst` (rank 0: a Context on its device other than
+        the group's; other ranks pass None) in the single-device layout, so dst's device sort,
+        .dag writer, decompression and tree() work on it (gcz_group_assemble)."""
+        rc = _lib.gcz_group_assemble(self._h, dst._h if dst is not None else None)
+        if rc != GCZ_OK:
+            raise GczError(rc, _lib.gcz_group_last_error(self._h).decode())
+        return dst.info() if dst is not None else {}
 
     def exchange_log(self, i=0) -> list:
         """The last build's exchanges as local rank i saw them (gcz_group_xlog): name, sequence

@@ -274,6 +274,14 @@ GCZ_API int gcz_group_slice(const gcz_group *g, int local, int layer, uint64_t *
 GCZ_API int gcz_group_copy_slice(gcz_group *g, int local, int layer, void *host_out);
 /* Whole tree to the host (every rank local, i.e. gcz_group_create_local). */
 GCZ_API int gcz_group_fetch(gcz_group *g, gcz_tree *t);
+/* The last build's whole tree into `dst` (rank 0's process: a context on rank 0's device other
+ * than the group's own; ignored elsewhere, every rank calls) in the single-device layout: each
+ * layer's rank slices gathered device to device (RCCL / shm gather to rank 0, or copies when all
+ * ranks are local).  Afterwards gcz_sort_device, gcz_device_dag / gcz_serialize_device,
+ * gcz_decompress_device and gcz_fetch_host work on dst as after a one-GPU build -- the device
+ * ratio path of a distributed tree (reference: sort_tree / bytes / serialize,
+ * src/shared_tree.cpp:443-513). */
+GCZ_API int gcz_group_assemble(gcz_group *g, gcz_ctx *dst);
 
 #ifdef __cplusplus
 }
