@@ -596,8 +596,10 @@ static __device__ __forceinline__ u64 bucket_word(const unsigned long long* __re
                                                          u32* __restrict__ rfc, u32* __restrict__ bcnt) {
   extern __shared__ u32 s_cnt[];   // nch + 1 chunk counters
   __shared__ u64 s_low[256];       // OR of the lower ranks' words of this bucket
+  __shared__ u32 s_wc[16 * (kDThreads / 64)];   // r-first codes per (k, wave), then their prefix
   __shared__ u32 s_tmp[16];
-  const int tid = threadIdx.x;
+  constexpr int PER = 16;          // codes per thread: i = k * kDThreads + tid (coalesced loads, RB <= 16 Ki)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const u32 b = blockIdx.x, RB = 1u << P.IB, NW = RB >= 64 ? RB / 64 : 1u;
   for (u32 c = tid; c <= P.nch; c += kDThreads) s_cnt[c] = 0;
   for (u32 lw = tid; lw < NW; lw += kDThreads) {
@@ -605,23 +607,32 @@ static __device__ __forceinline__ u64 bucket_word(const unsigned long long* __re
     for (int q = 0; q < r; ++q) x |= bucket_word(pbs + u64(q) * stride, b, P.IB, lw);
     s_low[lw] = x;
   }
-  __syncthreads();
-  constexpr int PER = 16;   // codes per thread, contiguous (RB <= 16 Ki)
-  u32 fp[PER], rk[PER];
-  u32 nrf = 0;
+  u32 fp[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    const u32 i = u32(tid) * PER + u32(k);
+    const u32 i = u32(k) * kDThreads + tid;
     fp[k] = i < RB ? fpg[u64(b) * RB + i] : ~0u;
+  }
+  __syncthreads();
+  u32 rk[PER];
+  u64 m[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const u32 i = u32(k) * kDThreads + tid;
     if (fp[k] != ~0u && ((s_low[i >> 6] >> (i & 63)) & 1ull)) fp[k] = ~0u;   // held by a lower rank
     rk[k] = fp[k] != ~0u ? atomicAdd(&s_cnt[fp[k] >> kDLog], 1u) : 0u;
-    nrf += fp[k] != ~0u ? 1u : 0u;
+    m[k] = __ballot(fp[k] != ~0u);
+    if (lane == 0) s_wc[k * (kDThreads / 64) + wave] = u32(__popcll(m[k]));
   }
-  u32 total;
-  u32 j = block_excl(nrf, s_tmp, &total);   // (its barrier also orders the counters)
+  __syncthreads();
+  u32 total;   // code order = (k, wave, lane): exclusive prefix of the 256 (k, wave) counts
+  const u32 e = block_excl(u32(tid) < 16u * (kDThreads / 64) ? s_wc[tid] : 0u, s_tmp, &total);
+  if (u32(tid) < 16u * (kDThreads / 64)) s_wc[tid] = e;
+  __syncthreads();
+  const u64 lt = (1ull << lane) - 1ull;
 #pragma unroll
   for (int k = 0; k < PER; ++k)
-    if (fp[k] != ~0u) rfc[u64(b) * RB + j++] = fp[k];
+    if (fp[k] != ~0u) rfc[u64(b) * RB + s_wc[k * (kDThreads / 64) + wave] + u32(__popcll(m[k] & lt))] = fp[k];
   if (tid == 0) bcnt[b] = total;
   // exclusive scan of the nch + 1 chunk counters (a few per thread, in order)
   const u32 n1 = P.nch + 1, per = (n1 + kDThreads - 1) / kDThreads, c0 = tid * per;
@@ -662,31 +673,31 @@ static __device__ __forceinline__ u64 bucket_word(const unsigned long long* __re
   for (u32 j = tid; j < n; j += kDThreads) G[pre + j] = fb_rank(rfb, wpre, rfc[u64(b) * RB + j]);
 }
 
-// Where the relay put list q's element j (gcz_dist.hip: piece p = [c_q p / R, c_q (p+1) / R) of
-// every list went through rank p; pos0[q * R + p] = that piece's start in the receive buffer).
+// The relay (gcz_dist.hip) leaves piece p = [c_q p / R, c_q (p+1) / R) of every list q at
+// seg_src[q R + p] of the receive buffer; k_dl_unrelay copies each piece to its list's place,
+// off_q + c_q p / R, so list q is contiguous at off_q (= the global id of its first code).
 constexpr int kDlMaxRanks = 31;
 struct DlRelay {
-  u64 off[kDlMaxRanks + 1];            // global id offsets (r-first counts of lower ranks)
-  u64 c[kDlMaxRanks];                  // list lengths
-  u64 pos0[kDlMaxRanks * kDlMaxRanks];
+  u64 off[kDlMaxRanks + 1];                     // global id offsets (r-first counts of lower ranks)
+  u64 seg_src[kDlMaxRanks * kDlMaxRanks];       // piece starts in the relay's receive buffer
+  u64 seg_dst[kDlMaxRanks * kDlMaxRanks];       // ... and in list order
+  u64 seg_len[kDlMaxRanks * kDlMaxRanks];
 };
-static __device__ __forceinline__ u64 relay_pos(const DlRelay& T, int R, int q, u64 j) {
-  const u64 c = T.c[q];
-  u64 p = (j * u64(R)) / c;   // (j < c)
-  if (p >= u64(R)) p = R - 1;
-  while (p > 0 && c * p / u64(R) > j) --p;
-  while (p + 1 < u64(R) && c * (p + 1) / u64(R) <= j) ++p;
-  return T.pos0[u64(q) * R + p] + (j - c * p / u64(R));
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_unrelay(const u32* __restrict__ recv,
+                                                    const DlRelay* __restrict__ T, u32* __restrict__ out) {
+  const u32 sg = blockIdx.x;
+  const u64 src = T->seg_src[sg], dst = T->seg_dst[sg], len = T->seg_len[sg];
+  for (u64 e = u64(blockIdx.y) * 256 + threadIdx.x; e < len; e += u64(gridDim.y) * 256) out[dst + e] = recv[src + e];
 }
 
 // Global ids of every code present on rank r (LDS), then one final word per record.  pbs /
-// xvs: the gathered presence bitmaps (stride words) and exchange vectors (xstride u32);
-// recv: the relayed G arrays.
+// xvs: the gathered presence bitmaps (stride words) and exchange vectors (xstride u32); gl: the
+// G arrays in list order (k_dl_unrelay).  Codes: 16 contiguous per thread (a quarter word).
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_ids_mr(const u32* __restrict__ rec, const u32* __restrict__ off,
                                                          DensePlan P, const unsigned long long* __restrict__ pbs,
                                                          u64 stride, const u32* __restrict__ xvs, u64 xstride,
-                                                         const u32* __restrict__ recv, const DlRelay* __restrict__ T,
-                                                         int R, int r, u32* __restrict__ idrec) {
+                                                         const u32* __restrict__ gl, const DlRelay* __restrict__ T,
+                                                         int r, u32* __restrict__ idrec) {
   extern __shared__ u32 s_id[];    // RB
   __shared__ u64 s_acc[256], s_rf[256], s_mine[256];
   __shared__ u32 s_pf[256];
@@ -697,11 +708,11 @@ static __device__ __forceinline__ u64 relay_pos(const DlRelay& T, int R, int q, 
     s_acc[lw] = 0;
     s_mine[lw] = bucket_word(pbs + u64(r) * stride, b, P.IB, lw);
   }
+  const u32 lw = u32(tid) >> 2, sh = (u32(tid) & 3u) * 16u;   // this thread's codes: 16 tid .. 16 tid + 15
   for (int q = 0; q <= r; ++q) {
-    const unsigned long long* pq = pbs + u64(q) * stride;
     u32 pc = 0;
     if (u32(tid) < NW) {
-      const u64 w = bucket_word(pq, b, P.IB, tid);
+      const u64 w = bucket_word(pbs + u64(q) * stride, b, P.IB, tid);
       const u64 rf = w & ~s_acc[tid];
       s_rf[tid] = rf;
       s_acc[tid] |= w;
@@ -711,13 +722,18 @@ static __device__ __forceinline__ u64 relay_pos(const DlRelay& T, int R, int q, 
     const u32 e = block_excl(pc, s_tmp, &total);   // (NW <= 256 < kDThreads)
     if (u32(tid) < NW) s_pf[tid] = e;
     __syncthreads();
-    if (total) {   // codes first held by q: id = off_q + G_q[prefix_q(b) + index in the bucket]
-      const u64 base = xvs[u64(q) * xstride + 2 + b];
-      for (u32 i = tid; i < RB; i += kDThreads) {
-        const u64 rf = s_rf[i >> 6] & s_mine[i >> 6];   // (codes not held here need no id)
-        if (!((rf >> (i & 63)) & 1ull)) continue;
-        const u64 k = base + s_pf[i >> 6] + u64(__popcll(s_rf[i >> 6] & ((1ull << (i & 63)) - 1ull)));
-        s_id[i] = u32(T->off[q] + recv[relay_pos(*T, R, q, k)]);
+    if (total && 16u * u32(tid) < RB) {   // codes first held by q: id = off_q + G_q[prefix_q(b) + index]
+      const u64 rfw = s_rf[lw];
+      u32 win = u32(rfw >> sh) & 0xffffu & u32(s_mine[lw] >> sh);   // (codes not held here need no id)
+      if (win) {
+        const u64 base = T->off[q] + xvs[u64(q) * xstride + 2 + b] + s_pf[lw];
+        const u32 q0 = u32(T->off[q]);
+        while (win) {
+          const u32 j = u32(__ffs(int(win))) - 1u;
+          win &= win - 1u;
+          const u32 bit = sh + j;
+          s_id[16u * u32(tid) + j] = q0 + gl[base + u64(__popcll(rfw & ((1ull << bit) - 1ull)))];
+        }
       }
     }
     __syncthreads();
@@ -740,20 +756,17 @@ static __device__ __forceinline__ u64 relay_pos(const DlRelay& T, int R, int q, 
 }
 
 // This rank's slice of the unique leaves: its r-first codes in position order (= id order),
-// one thread per word of the r-first position bitmap.
+// one thread per position of the r-first position bitmap (a wave shares one bitmap word).
 [[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_rleaves(const unsigned long long* __restrict__ rfb,
                                                     const u32* __restrict__ wpre, const u32* __restrict__ pw,
                                                     DensePlan P, u64* __restrict__ out) {
-  const u64 w = u64(blockIdx.x) * 256 + threadIdx.x;
-  if (w >= (P.S + 63) / 64) return;
-  unsigned long long m = rfb[w];
-  u32 k = wpre[w];
-  while (m) {
-    const int bit = __ffsll(m) - 1;
-    m &= m - 1;
-    const u32 h = pw[w * 64 + u64(bit)] & kIdx;
-    out[k++] = code2_leaf((h * P.Kinv) & P.cmask, P.L);
-  }
+  const u64 p = u64(blockIdx.x) * 256 + threadIdx.x;
+  if (p >= P.S) return;
+  const unsigned long long m = rfb[p >> 6];
+  if (!((m >> (p & 63)) & 1ull)) return;
+  const u32 k = wpre[p >> 6] + u32(__popcll(m & ((1ull << (p & 63)) - 1ull)));
+  const u32 h = pw[p] & kIdx;
+  out[k] = code2_leaf((h * P.Kinv) & P.cmask, P.L);
 }
 
 }  // namespace gcz_dev

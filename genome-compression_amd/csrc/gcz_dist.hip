@@ -987,7 +987,7 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
   if (total > u64(kIdx)) return fail(GCZ_ERR_CAPACITY, "more than 2^29-1 unique leaves");
   // exchange 3: every rank gets every G array, relayed in two steps so no link carries rank
   // 0's long one R - 1 times: piece q of array r goes to rank q, then each rank sends the
-  // pieces it holds to all ranks (k_dl_ids_mr finds an element through relay_pos)
+  // pieces it holds to all ranks; k_dl_unrelay then puts every piece in list order
   auto pc = [&](int r, int q) { return c[r] * u64(q) / u64(R); };   // start of piece q of array r
   std::vector<u64> M1(size_t(R) * R), T(R, 0), M2(size_t(R) * R), sd2(size_t(R) * R, 0), rd2(size_t(R) * R);
   for (int r = 0; r < R; ++r)
@@ -1003,15 +1003,19 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
       rd2[size_t(d) * R + q] = o;
     }
   DlRelay relay{};
+  u64 max_piece = 0;
   {
     u64 o = 0;
-    for (int q = 0; q < R; ++q)
+    for (int q = 0; q < R; ++q)   // (relay order: piece index outer, list inner)
       for (int r = 0; r < R; ++r) {
-        relay.pos0[size_t(r) * R + q] = o;
-        o += M1[size_t(r) * R + q];
+        const size_t sg = size_t(r) * R + q;
+        relay.seg_src[sg] = o;
+        relay.seg_dst[sg] = off[r] + pc(r, q);
+        relay.seg_len[sg] = M1[sg];
+        max_piece = std::max(max_piece, M1[sg]);
+        o += M1[sg];
       }
     for (int r = 0; r <= R; ++r) relay.off[r] = off[r];
-    for (int r = 0; r < R; ++r) relay.c[r] = c[r];
   }
   {
     std::vector<const void*> s;
@@ -1046,14 +1050,18 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
       ProfScope ps_(cx, KID_IDS);
       if (cx->ensure(cx->dl_gid, sizeof(DlRelay) + 16)) return dev_fail("dense leaf relay table");
       G_HIP(hipMemcpyAsync(cx->dl_gid.ptr, &relay, sizeof(DlRelay), hipMemcpyHostToDevice, cx->stream));
+      u32* gl = cx->dl_fl.as<u32>();   // (the first lists are consumed: total <= 4^L entries fit)
+      if (max_piece)
+        hipLaunchKernelGGL(k_dl_unrelay, dim3(unsigned(R * R), unsigned(std::min<u64>(64, (max_piece + 4095) / 4096))),
+                           dim3(256), 0, cx->stream, cx->dl_recv.as<u32>(), cx->dl_gid.as<DlRelay>(), gl);
       G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_ids_mr), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 int(RB * 4)));
       hipLaunchKernelGGL(k_dl_ids_mr, dim3(NB), dim3(kDThreads), RB * 4, cx->stream, cx->dl_rec.as<u32>(),
                          cx->dl_off.as<u32>(), DP, cx->dl_pbs.as<unsigned long long>(), nwb, cx->dl_lower.as<u32>(), xw,
-                         cx->dl_recv.as<u32>(), cx->dl_gid.as<DlRelay>(), R, r, cx->dl_idrec.as<u32>());
+                         static_cast<const u32*>(gl), cx->dl_gid.as<DlRelay>(), r, cx->dl_idrec.as<u32>());
       const u64 cr = c[r];
       if (cr)
-        hipLaunchKernelGGL(k_dl_rleaves, dim3(unsigned(((DP.S + 63) / 64 + 255) / 256)), dim3(256), 0, cx->stream,
+        hipLaunchKernelGGL(k_dl_rleaves, dim3(unsigned((DP.S + 255) / 256)), dim3(256), 0, cx->stream,
                            cx->dl_fb.as<unsigned long long>(), cx->dl_wpre.as<u32>(), cx->dl_pw.as<u32>(), DP,
                            cx->leaves_out.as<u64>());
       G_HIP(hipGetLastError());

@@ -343,3 +343,30 @@ def test_dist_skewed_repetitive_slice(world, gcz, groups):
         assert single.root == multi.root
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_dist_assemble_device_ratio_path(world, gcz, manifest, groups):
+    """A distributed tree gathered device to device into one context (gcz_group_assemble):
+    that context's frequency sort and .dag writer give the reference .dag (sort_tree / bytes /
+    serialize on the device, no host gather), its decompression gives the genome back, and the
+    fetched tree equals the golden dumps."""
+    import hashlib
+    ctx = gcz.Context(0)
+    try:
+        for name in ("corpus/chmpxx", "corpus/merged", "synth/uniform_10000000", "synth/tandem_10000000"):
+            case = manifest[name]
+            exp = case["expect"]
+            kind, payload, L = case_input(case, gcz)
+            _dist_build(gcz, groups(world), kind, payload, L)
+            groups(world).assemble(ctx)
+            assert compare_digest(gcz.digest(ctx.tree()), exp) == {}, name
+            if kind == "fasta":
+                bases = gcz.fasta_extract(payload)
+                bases = bases[:len(bases) // L * L].upper()
+                assert ctx.decompress() == bases, name
+            ctx.sort_device()
+            assert hashlib.sha256(ctx.serialize_device()).hexdigest() == exp["sha_dag"], name
+    finally:
+        ctx.close()
