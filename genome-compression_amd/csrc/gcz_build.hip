@@ -405,8 +405,15 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
       return rc;
     HIP_TRY(hipMemsetAsync(bkt_tmp.ptr, 0, t_scan * 8 + 16, stream));
   }
+  // two-pass levels: k_bkt_part writes every mark itself (the clear only zeroed marks there),
+  // and the dedupe lists the level's not-first positions for the sparse flag scan
+  b2.wmarks = two && part_marks ? 1u : 0u;
+  if (two && sparse_scan) {
+    if (int rc = ensure(nf_list, kNfListCap * 4 + 16)) return rc;
+    b2.nfl = nf_list.as<u32>();
+  }
   hipEvent_t e0{};
-  if (!a.fused) {
+  if (!a.fused && !b2.wmarks) {
     prof_begin(KID_MEMSET, e0);
     const u64 tab16 = nt.bytes() / 16, p16 = (p + 15) / 16;
     const u64 blocks = std::min<u64>(4096, (std::max(tab16, p16) + kBlock - 1) / kBlock);
@@ -503,7 +510,8 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     hipLaunchKernelGGL((k_flagscan_node<decltype(items)::value>), gs, dim3(kBlock), 0, stream, a.words, p, a.in, n,
                        knf, d_grp, ndesc, a.ticket, a.out, a.count, a.pcount, mk.multi, a.hashed_next, clr_nf, clr_mu,
                        clr16, a.fused && (!a.fused_last || a.tail_settles) ? a.sid : nullptr,
-                       bkt == 2 ? static_cast<const u32*>(&d_hdr->predup) : nullptr);
+                       bkt == 2 ? static_cast<const u32*>(&d_hdr->predup) : nullptr, b2.nfl,
+                       static_cast<const u32*>(&d_hdr->nnf));
   };
   if (tile == u64(kTile)) flagscan(std::integral_constant<int, kItems>{});
   else if (tile == u64(kTileSmall)) flagscan(std::integral_constant<int, kItemsSmall>{});
@@ -975,6 +983,8 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   if (const char* t = std::getenv("GCZ_BUCKET")) c->use_bucket = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_BUCKET_MIN")) c->bucket_min = std::strtoull(t, nullptr, 10);
   if (const char* t = std::getenv("GCZ_BUCKET_TWO")) c->two_pass = std::atoi(t) != 0;
+  if (const char* t = std::getenv("GCZ_PART_MARKS")) c->part_marks = std::atoi(t) != 0;
+  if (const char* t = std::getenv("GCZ_SPARSE_SCAN")) c->sparse_scan = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_DENSE")) c->dense_mode = std::atoi(t);
   if (const char* t = std::getenv("GCZ_GRAPH")) c->use_graph = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_FUSED")) c->use_fused = std::atoi(t) != 0;
@@ -999,7 +1009,7 @@ void gcz_ctx_destroy(gcz_ctx* c) {
                     &c->dl_rec, &c->dl_idrec, &c->dl_cnt, &c->dl_off, &c->dl_offt, &c->dl_fpg, &c->dl_fb, &c->dl_wpre,
                     &c->dl_desc, &c->dl_fl, &c->dl_fo, &c->dl_lh, &c->dl_pb, &c->dl_pbs, &c->dl_lower,
                     &c->dl_pos, &c->dl_list, &c->dl_gid, &c->dl_recv, &c->dl_stage, &c->dl_seg, &c->seg_w,
-                    &c->seg_nf, &c->seg_mu, &c->seg_in})
+                    &c->seg_nf, &c->seg_mu, &c->seg_in, &c->nf_list})
     if (b->ptr) (void)hipFree(b->ptr);
   if (c->h_hdr) (void)hipHostFree(c->h_hdr);
   if (c->h_ring) (void)hipHostFree(c->h_ring);

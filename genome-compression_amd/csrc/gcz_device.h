@@ -102,7 +102,13 @@ struct Header {
   u32 root;
   u32 bkt_overflow;         // a node-level bucket exceeded the LDS dedupe (k_bkt_dedupe)
   u32 dense_fail;           // a strand is not pure ACGT: the dense leaf level does not apply (gcz_dense.h)
+  u32 nnf;                  // two-pass level: its not-first positions (k_bkt_dedupe2), listed up to kNfListCap
 };
+
+// A two-pass level with at most this many repeats (e.g. 13 of 41.7 M pairs on layer 0 of
+// 1 Gbase uniform) is ranked without the look-back chain: id = position - repeats before it,
+// counted from the dedupe's list (k_flagscan_node's sparse path).
+constexpr u32 kNfListCap = 2048;
 
 // ---- word algebra: reference src/shared_tree.cpp:76-107 --------------------
 __device__ __forceinline__ u32 ulw(u32 w) { return w & 0x7fffffffu; }   // to_ulong
@@ -1095,7 +1101,9 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
                                                          const unsigned char* __restrict__ multi,
                                                          u32* __restrict__ hashed_next, uint4* __restrict__ clr_nf,
                                                          uint4* __restrict__ clr_multi, u64 clr16,
-                                                         u32* __restrict__ sid, const u32* __restrict__ dup_flag) {
+                                                         u32* __restrict__ sid, const u32* __restrict__ dup_flag,
+                                                         const u32* __restrict__ nfl = nullptr,
+                                                         const u32* __restrict__ nnf = nullptr) {
   // fused small-build levels: clear the marks of the level after this one (its parity
   // set held the previous level's marks, last read by this level's insert)
   for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < clr16; i += u64(gridDim.x) * kBlock) {
@@ -1135,6 +1143,82 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
   }
   if (level_direct(prev_count, n)) return;
   if (threadIdx.x == 0) s_hashed = 0;
+  if (nfl && !(dup_flag && *dup_flag != 0) && *nnf <= kNfListCap) {
+    // Sparse repeats (two-pass level, the dedupe listed every not-first position): tiles in
+    // block order, no look-back chain -- a position's id is itself minus the repeats before it.
+    constexpr u32 T = u32(kBlock) * ITEMS, NWB = T / 32;
+    __shared__ u32 s_bits[NWB], s_bpre[NWB], s_red[kBlock / 64];
+    const u64 base = u64(blockIdx.x) * T;
+    const u32 c = *nnf;
+    for (u32 w = u32(tid); w < NWB; w += kBlock) s_bits[w] = 0;
+    __syncthreads();
+    u32 before = 0;
+    for (u32 k = u32(tid); k < c; k += kBlock) {
+      const u64 q = nfl[k];
+      if (q < base) ++before;
+      else if (q < base + T) atomicOr(&s_bits[u32(q - base) >> 5], 1u << (u32(q - base) & 31));
+    }
+    before = u32(wave_sum(u64(before)));
+    if (lane == 0) s_red[wave] = before;
+    __syncthreads();
+    before = 0;
+    for (int w = 0; w < kBlock / 64; ++w) before += s_red[w];
+    {   // exclusive prefix of the tile's not-first bits per 32-bit word (NWB <= kBlock)
+      const u32 v = u32(tid) < NWB ? u32(__popc(s_bits[tid])) : 0u;
+      u32 inc = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const u32 y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+      }
+      __syncthreads();   // (s_red read by every thread above)
+      if (lane == 63) s_red[wave] = inc;
+      __syncthreads();
+      u32 pre = inc - v;
+      for (int w = 0; w < wave; ++w) pre += s_red[w];
+      if (u32(tid) < NWB) s_bpre[tid] = pre;
+    }
+    __syncthreads();
+    if (blockIdx.x == 0 && tid == 0) *count_out = p - c;
+    const u64 lt = (1ull << lane) - 1;
+    bool hashed = false;
+#pragma unroll
+    for (int e = 0; e < ITEMS; ++e) {
+      const u32 k = u32(e) * kBlock + u32(tid);
+      const u64 j = base + k;
+      const u32 bw = s_bits[k >> 5];
+      const bool is_first = j < p && !((bw >> (k & 31)) & 1u);
+      const u64 mask = __ballot(is_first);
+      const u64 nb = u64(before) + s_bpre[k >> 5] + u32(__popc(bw & ((1u << (k & 31)) - 1u)));
+      if (lane == 0) {
+        Group g;
+        g.mask = mask; g.prefix = u32(j - nb); g.pad = 0;
+        grp[(base >> 6) + u64(e) * 4 + wave] = g;
+      }
+      unsigned char me = 0;
+      if (hashed_next && is_first) me = multi[j];
+      if (hashed_next) {
+        const bool rep = j < p && (!is_first || me != 0);
+        const bool partner = __shfl_xor(int(rep), 1, 64) != 0;
+        if ((lane & 1) == 0 && rep && (j + 1 < p ? partner : true)) hashed = true;
+      }
+      if (is_first) {
+        const u32 id = u32(j - nb);
+        u32 l, r, cl, cr, m, t;
+        load_pair(in, n, j, l, r);
+        node_canonical(l, r, cl, cr, m, t);
+        out[id] = make_uint2(cl, cr);
+        words[j] = make_word(id, m, t, ulw(l) == ulw(xf(r, 1, 0)));
+      }
+    }
+    (void)lt;
+    if (hashed_next) {
+      if (__ballot(hashed) && lane == 0) s_hashed = 1;
+      __syncthreads();
+      if (threadIdx.x == 0 && s_hashed) *hashed_next = 1;
+    }
+    return;
+  }
   auto fetch = [&]() {
     if constexpr (kPre) {
       if (!early) {
@@ -1489,7 +1573,24 @@ struct Bkt2Plan {
   u64 G;               // part chunks
   u32* olist;          // owner dedupe (kOwner): the not-first records' indices, appended ...
   u32* ocnt;           // ... at this cursor (the D records, k_own_getid_list); null: none
+  u32 wmarks;          // k_bkt_part writes every pair's not-first / multi mark (no k_clear pass)
+  u32* nfl;            // k_bkt_dedupe2: the not-first positions (hdr->nnf counts them); null: none
 };
+
+// Append the not-first positions of a wave to bp.nfl (one atomic per wave; none once the
+// list is over its cap -- the count then only tells the flag scan to take the look-back path).
+__device__ __forceinline__ void nf_list_add(const Bkt2Plan& bp, Header* hdr, bool nf, u32 pos) {
+  const u64 m = __ballot(nf);
+  if (!m || !bp.nfl) return;
+  const int lane = int(threadIdx.x & 63), lead = __ffsll((long long)m) - 1;
+  u32 base = 0;
+  if (lane == lead)
+    base = *reinterpret_cast<volatile u32*>(&hdr->nnf) > kNfListCap ? ~0u : atomicAdd(&hdr->nnf, u32(__popcll(m)));
+  base = __shfl(base, lead, 64);
+  if (!nf || base == ~0u) return;
+  const u32 k = base + u32(__popcll(m & ((1ull << lane) - 1ull)));
+  if (k < kNfListCap) bp.nfl[k] = pos;
+}
 
 // Exclusive prefix of n <= 256 LDS counters in place (one wave, 4 per lane); c[n] = the total.
 __device__ __forceinline__ void lds_excl256(u32* c, u32 n) {
@@ -1550,6 +1651,7 @@ constexpr u32 kColSlots = 8192;   // its LDS table (load <= 1/2), in the part's 
   }
   extern __shared__ u64 stage[];   // kPartChunk records (dynamic)
   __shared__ u32 cur[(1u << kPartMaxB1) + 1];
+  if (bp.nfl && blockIdx.x == 0 && threadIdx.x == 0) hdr->nnf = 0;   // (the dedupe counts after this launch)
   const bool collapse = hdr && hdr->predup != 0;
   const u32 nb1 = 1u << bp.b1;
   for (u32 q = threadIdx.x; q <= nb1; q += kBktThreads) cur[q] = 0;
@@ -1576,11 +1678,21 @@ constexpr u32 kColSlots = 8192;   // its LDS table (load <= 1/2), in the part's 
     slot[e] = (c << 16) | atomicAdd(&cur[c], 1u);
     ++hashed;
   };
+  // bp.wmarks: every pair's marks written here (0, or the collapse's), whole lines per wave --
+  // the level needs no clearing pass; the bytes up to the next 16 are zeroed too (vector reads)
+  const u64 p16 = (p + 15) & ~u64(15);
+  auto marks = [&](u64 j, unsigned char nfv, unsigned char muv) {
+    if (bp.wmarks && j < p16) {
+      mk.nf[j] = nfv;
+      mk.multi[j] = muv;
+    }
+  };
   if (!collapse) {
 #pragma unroll
     for (int e = 0; e < kPartItems; ++e) {
       const u64 j = j0 + u64(e) * kBktThreads + threadIdx.x;
       slot[e] = ~0u;
+      marks(j, 0, 0);
       if (j >= p) continue;
       u64 key;
       u32 bits;
@@ -1621,9 +1733,41 @@ constexpr u32 kColSlots = 8192;   // its LDS table (load <= 1/2), in the part's 
           hn[i] = j < p && bkt_pair(in, n, j, prev_nf, prev_multi, kp, kn[i], bn[i]);
         }
       const u64 tag = u64(q + 1);
+      const int lane = int(threadIdx.x & 63);
 #pragma unroll
       for (int i = 0; i < BI; ++i) {   // claim (or find) the key's slot, the earliest offset, the flag
         cs[i] = 0;
+        // a wave whose hashed pairs all carry one key (a tandem repeat whose period divides the
+        // pair's span): only its first such lane -- the earliest offset -- touches the table
+        const u64 hm = __ballot(h[i]);
+        if (hm) {
+          const int lead = __ffsll((long long)hm) - 1;
+          const u64 k0 = __shfl(key[i], lead, 64);
+          if (__ballot(h[i] && key[i] == k0) == hm && __popcll(hm) > 1) {
+            u32 s0 = 0;
+            if (lane == lead) {
+              const u64 mk2 = (tag << 58) | key[i];
+              const u32 off = u32(i) * kBktThreads + threadIdx.x;
+              u32 s2 = u32((u64(u32(bkt_hash(key[i]))) * kColSlots) >> 32);
+              for (;;) {
+                unsigned long long cv = s_ck[s2];
+                if ((cv >> 58) != tag) {
+                  const unsigned long long old = atomicCAS(&s_ck[s2], cv, (unsigned long long)mk2);
+                  if (old == cv) break;
+                  cv = old;
+                  if ((cv >> 58) != tag) continue;
+                }
+                if (cv == mk2) break;
+                s2 = s2 + 1 == kColSlots ? 0u : s2 + 1;
+              }
+              s_cd[s2] = (unsigned char)tag;   // several: the other lanes
+              atomicMax(&s_cp[s2], (u32(tag) << 16) | (0xffffu - off));
+              s0 = s2;
+            }
+            cs[i] = __shfl(s0, lead, 64);
+            continue;
+          }
+        }
         if (!h[i]) continue;
         const u64 mk2 = (tag << 58) | key[i];
         const u32 off = u32(i) * kBktThreads + threadIdx.x;
@@ -1654,15 +1798,22 @@ constexpr u32 kColSlots = 8192;   // its LDS table (load <= 1/2), in the part's 
         const u64 j = j0 + u64(e) * kBktThreads + threadIdx.x;
         slot[e] = ~0u;
         bool dup = false;
+        unsigned char nfv = 0, muv = 0;
         if (h[i] && s_cd[cs[i]] == (unsigned char)tag) {
           const u32 rep = u32(j0 + u64(q * BI) * kBktThreads) + (0xffffu - (s_cp[cs[i]] & 0xffffu));
           if (rep != u32(j)) {   // collapsed: not partitioned
-            mk.nf[j] = kNfDup;
+            nfv = kNfDup;
             rec[j] = rep | bits[i];
             dup = true;
           } else {
-            mk.multi[j] = 1;
+            muv = 1;
           }
+        }
+        if (bp.wmarks) {
+          marks(j, nfv, muv);
+        } else {
+          if (nfv) mk.nf[j] = nfv;
+          if (muv) mk.multi[j] = muv;
         }
         if (h[i] && !dup) place(e, j, key[i]);
         if (j < p && !dup) rec[j] = bits[i];
@@ -1872,6 +2023,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
           if (dup) atomicMin(&s_pos[sl], pos);
           continue;
         }
+        if constexpr (!kOwner) nf_list_add(bp, hdr, dup && pos != s_pos[sl], pos);
         if (!dup) continue;
         const u32 first = s_pos[sl];
         if constexpr (kOwner) {
@@ -1930,7 +2082,9 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
   __syncthreads();
 #pragma unroll
   for (int e = 0; e < kBktCapItems; ++e) {
-    if (key[e] == kEmpty || !((s_dup[slot[e] >> 5] >> (slot[e] & 31)) & 1u)) continue;
+    const bool dup = key[e] != kEmpty && ((s_dup[slot[e] >> 5] >> (slot[e] & 31)) & 1u);
+    if constexpr (!kOwner) nf_list_add(bp, hdr, dup && pos[e] != s_pos[slot[e]], pos[e]);
+    if (!dup) continue;
     const u32 first = s_pos[slot[e]];
     if constexpr (kOwner) {
       rec[pos[e]] = first;
