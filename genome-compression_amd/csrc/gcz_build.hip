@@ -408,6 +408,7 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   // two-pass levels: k_bkt_part writes every mark itself (the clear only zeroed marks there),
   // and the dedupe lists the level's not-first positions for the sparse flag scan
   b2.wmarks = two && part_marks ? 1u : 0u;
+  b2.wave1 = part_wave ? 1u : 0u;
   if (two && sparse_scan) {
     if (int rc = ensure(nf_list, kNfListCap * 4 + 16)) return rc;
     b2.nfl = nf_list.as<u32>();
@@ -985,6 +986,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   if (const char* t = std::getenv("GCZ_BUCKET_TWO")) c->two_pass = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_PART_MARKS")) c->part_marks = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_SPARSE_SCAN")) c->sparse_scan = std::atoi(t) != 0;
+  if (const char* t = std::getenv("GCZ_PART_WAVE")) c->part_wave = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_DENSE")) c->dense_mode = std::atoi(t);
   if (const char* t = std::getenv("GCZ_GRAPH")) c->use_graph = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_FUSED")) c->use_fused = std::atoi(t) != 0;

@@ -568,6 +568,7 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
 //   gq       per bucket: G[bucket prefix + j] = the local rank of the bucket's j-th r-first
 //            code in CODE order; the bucket prefixes ride in the exchange vector
 //   -- allgather the exchange vectors (r-first count + bucket prefixes); relay the G arrays --
+//            (a rank with few r-first codes writes its leaves here too)
 //   ids      per bucket: the global id of every code present here in LDS -- for each lower
 //            rank q (and r itself) the codes q holds first are present_q & ~(present_0 | ..
 //            | present_{q-1}); a code's index among them in the bucket is a popcount prefix of
@@ -653,10 +654,14 @@ static __device__ __forceinline__ u64 bucket_word(const unsigned long long* __re
 
 // G: per bucket, the local r-first rank of each r-first code in code order, at the bucket's
 // prefix; xv = the rank's exchange vector {r-first count, 0, prefix of bucket 0, 1, ...}.
+// A rank with few r-first codes (dl_rleaves_sparse: count * 16 < S) writes its leaves here,
+// by rank (random stores of few entries), instead of a pass over every position (k_dl_rleaves).
+__host__ __device__ __forceinline__ bool dl_rleaves_sparse(u64 count, u64 S) { return count * 16 < S; }
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_gq(const u32* __restrict__ rfc, const u32* __restrict__ bcnt,
                                                      DensePlan P, const unsigned long long* __restrict__ rfb,
                                                      const u32* __restrict__ wpre, const u64* __restrict__ ucount,
-                                                     u32* __restrict__ G, u32* __restrict__ xv) {
+                                                     u32* __restrict__ G, u32* __restrict__ xv,
+                                                     const u32* __restrict__ pw, u64* __restrict__ leaves_out) {
   __shared__ u32 s_tmp[16];
   const int tid = threadIdx.x;
   const u32 b = blockIdx.x, RB = 1u << P.IB;
@@ -670,36 +675,39 @@ static __device__ __forceinline__ u64 bucket_word(const unsigned long long* __re
     }
   }
   const u32 n = bcnt[b];
-  for (u32 j = tid; j < n; j += kDThreads) G[pre + j] = fb_rank(rfb, wpre, rfc[u64(b) * RB + j]);
+  const bool lv = leaves_out && dl_rleaves_sparse(*ucount, P.S);
+  for (u32 j = tid; j < n; j += kDThreads) {
+    const u32 fp = rfc[u64(b) * RB + j];
+    const u32 k = fb_rank(rfb, wpre, fp);
+    G[pre + j] = k;
+    if (lv) leaves_out[k] = code2_leaf(((pw[fp] & kIdx) * P.Kinv) & P.cmask, P.L);
+  }
 }
 
 // The relay (gcz_dist.hip) leaves piece p = [c_q p / R, c_q (p+1) / R) of every list q at
-// seg_src[q R + p] of the receive buffer; k_dl_unrelay copies each piece to its list's place,
-// off_q + c_q p / R, so list q is contiguous at off_q (= the global id of its first code).
+// seg_src[q R + p] of the receive buffer; in global id order that piece starts at
+// seg_dst[q R + p] = off_q + c_q p / R.
 constexpr int kDlMaxRanks = 31;
 struct DlRelay {
   u64 off[kDlMaxRanks + 1];                     // global id offsets (r-first counts of lower ranks)
   u64 seg_src[kDlMaxRanks * kDlMaxRanks];       // piece starts in the relay's receive buffer
-  u64 seg_dst[kDlMaxRanks * kDlMaxRanks];       // ... and in list order
+  u64 seg_dst[kDlMaxRanks * kDlMaxRanks];       // ... and by global id
   u64 seg_len[kDlMaxRanks * kDlMaxRanks];
 };
-[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_unrelay(const u32* __restrict__ recv,
-                                                    const DlRelay* __restrict__ T, u32* __restrict__ out) {
-  const u32 sg = blockIdx.x;
-  const u64 src = T->seg_src[sg], dst = T->seg_dst[sg], len = T->seg_len[sg];
-  for (u64 e = u64(blockIdx.y) * 256 + threadIdx.x; e < len; e += u64(gridDim.y) * 256) out[dst + e] = recv[src + e];
-}
 
 // Global ids of every code present on rank r (LDS), then one final word per record.  pbs /
 // xvs: the gathered presence bitmaps (stride words) and exchange vectors (xstride u32); gl: the
-// G arrays in list order (k_dl_unrelay).  Codes: 16 contiguous per thread (a quarter word).
+// relay's receive buffer.  Codes: 16 contiguous per thread (a quarter word).
+// The G arrays are read where the relay left them (T's pieces: list q's element at global id
+// position off_q + k lies in the piece p with seg_dst <= off_q + k < seg_dst + seg_len).
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_ids_mr(const u32* __restrict__ rec, const u32* __restrict__ off,
                                                          DensePlan P, const unsigned long long* __restrict__ pbs,
                                                          u64 stride, const u32* __restrict__ xvs, u64 xstride,
                                                          const u32* __restrict__ gl, const DlRelay* __restrict__ T,
-                                                         int r, u32* __restrict__ idrec) {
+                                                         int R, int r, u32* __restrict__ idrec) {
   extern __shared__ u32 s_id[];    // RB
   __shared__ u64 s_acc[256], s_rf[256], s_mine[256];
+  __shared__ u64 s_sdst[kDlMaxRanks + 1], s_ssrc[kDlMaxRanks];
   __shared__ u32 s_pf[256];
   __shared__ u32 s_tmp[16];
   const int tid = threadIdx.x;
@@ -711,6 +719,11 @@ struct DlRelay {
   const u32 lw = u32(tid) >> 2, sh = (u32(tid) & 3u) * 16u;   // this thread's codes: 16 tid .. 16 tid + 15
   for (int q = 0; q <= r; ++q) {
     u32 pc = 0;
+    if (tid < R) {   // list q's pieces, by global id position
+      s_sdst[tid] = T->seg_dst[u64(q) * R + tid];
+      s_ssrc[tid] = T->seg_src[u64(q) * R + tid];
+    }
+    if (tid == 0) s_sdst[R] = T->off[q + 1];
     if (u32(tid) < NW) {
       const u64 w = bucket_word(pbs + u64(q) * stride, b, P.IB, tid);
       const u64 rf = w & ~s_acc[tid];
@@ -728,11 +741,15 @@ struct DlRelay {
       if (win) {
         const u64 base = T->off[q] + xvs[u64(q) * xstride + 2 + b] + s_pf[lw];
         const u32 q0 = u32(T->off[q]);
+        int pc2 = 0;   // the piece holding the window's first id position, then onwards
+        const u64 g0 = base + u64(__popcll(rfw & ((1ull << (sh + u32(__ffs(int(win))) - 1u)) - 1ull)));
+        while (pc2 + 1 < R && s_sdst[pc2 + 1] <= g0) ++pc2;
         while (win) {
           const u32 j = u32(__ffs(int(win))) - 1u;
           win &= win - 1u;
-          const u32 bit = sh + j;
-          s_id[16u * u32(tid) + j] = q0 + gl[base + u64(__popcll(rfw & ((1ull << bit) - 1ull)))];
+          const u64 g = base + u64(__popcll(rfw & ((1ull << (sh + j)) - 1ull)));
+          while (pc2 + 1 < R && s_sdst[pc2 + 1] <= g) ++pc2;
+          s_id[16u * u32(tid) + j] = q0 + gl[s_ssrc[pc2] + (g - s_sdst[pc2])];
         }
       }
     }

@@ -1091,6 +1091,57 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_leaf(u32* __restrict__ word
 // the next level goes through the table only if both its children repeat
 // (singleton propagation); if no such pair exists, every pair of the next level
 // is a first occurrence and that level is direct (k_resolve_node opens its gate).
+// Sparse ranking of one tile of T = kBlock * ITEMS positions [base, base + T) when the
+// level's not-first positions are few and listed (any order, c <= kNfListCap): a position's
+// rank among the first ones is itself minus the listed positions before it -- no look-back
+// chain.  LDS: the tile's listed positions as bits, their exclusive popcount per 32-bit word,
+// and the count of listed positions before the tile.
+template <int ITEMS>
+struct SparseTile {
+  static constexpr u32 T = u32(kBlock) * ITEMS, NWB = T / 32;
+  u32* bits;
+  u32* bpre;
+  u64 base, before;
+  __device__ __forceinline__ bool listed(u32 k) const { return (bits[k >> 5] >> (k & 31)) & 1u; }
+  __device__ __forceinline__ u64 nb(u32 k) const {   // listed positions before base + k
+    return before + bpre[k >> 5] + u32(__popc(bits[k >> 5] & ((1u << (k & 31)) - 1u)));
+  }
+};
+template <int ITEMS>
+__device__ __forceinline__ SparseTile<ITEMS> sparse_tile(const u32* __restrict__ list, u32 c, u64 base) {
+  using ST = SparseTile<ITEMS>;
+  __shared__ u32 s_bits[ST::NWB], s_bpre[ST::NWB], s_red[kBlock / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (u32 w = u32(tid); w < ST::NWB; w += kBlock) s_bits[w] = 0;
+  __syncthreads();
+  u32 before = 0;
+  for (u32 k = u32(tid); k < c; k += kBlock) {
+    const u64 q = list[k];
+    if (q < base) ++before;
+    else if (q < base + ST::T) atomicOr(&s_bits[u32(q - base) >> 5], 1u << (u32(q - base) & 31));
+  }
+  before = u32(wave_sum(u64(before)));
+  if (lane == 0) s_red[wave] = before;
+  __syncthreads();
+  before = 0;
+  for (int w = 0; w < kBlock / 64; ++w) before += s_red[w];
+  const u32 v = u32(tid) < ST::NWB ? u32(__popc(s_bits[tid])) : 0u;   // (NWB <= kBlock)
+  u32 inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u32 y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  __syncthreads();   // (s_red read by every thread above)
+  if (lane == 63) s_red[wave] = inc;
+  __syncthreads();
+  u32 pre = inc - v;
+  for (int w = 0; w < wave; ++w) pre += s_red[w];
+  if (u32(tid) < ST::NWB) s_bpre[tid] = pre;
+  __syncthreads();
+  return ST{s_bits, s_bpre, base, before};
+}
+
 template <int ITEMS>
 __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ words, u64 p,
                                                          const u32* __restrict__ in, u64 n,
@@ -1146,50 +1197,18 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
   if (nfl && !(dup_flag && *dup_flag != 0) && *nnf <= kNfListCap) {
     // Sparse repeats (two-pass level, the dedupe listed every not-first position): tiles in
     // block order, no look-back chain -- a position's id is itself minus the repeats before it.
-    constexpr u32 T = u32(kBlock) * ITEMS, NWB = T / 32;
-    __shared__ u32 s_bits[NWB], s_bpre[NWB], s_red[kBlock / 64];
-    const u64 base = u64(blockIdx.x) * T;
     const u32 c = *nnf;
-    for (u32 w = u32(tid); w < NWB; w += kBlock) s_bits[w] = 0;
-    __syncthreads();
-    u32 before = 0;
-    for (u32 k = u32(tid); k < c; k += kBlock) {
-      const u64 q = nfl[k];
-      if (q < base) ++before;
-      else if (q < base + T) atomicOr(&s_bits[u32(q - base) >> 5], 1u << (u32(q - base) & 31));
-    }
-    before = u32(wave_sum(u64(before)));
-    if (lane == 0) s_red[wave] = before;
-    __syncthreads();
-    before = 0;
-    for (int w = 0; w < kBlock / 64; ++w) before += s_red[w];
-    {   // exclusive prefix of the tile's not-first bits per 32-bit word (NWB <= kBlock)
-      const u32 v = u32(tid) < NWB ? u32(__popc(s_bits[tid])) : 0u;
-      u32 inc = v;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const u32 y = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += y;
-      }
-      __syncthreads();   // (s_red read by every thread above)
-      if (lane == 63) s_red[wave] = inc;
-      __syncthreads();
-      u32 pre = inc - v;
-      for (int w = 0; w < wave; ++w) pre += s_red[w];
-      if (u32(tid) < NWB) s_bpre[tid] = pre;
-    }
-    __syncthreads();
+    const SparseTile<ITEMS> st = sparse_tile<ITEMS>(nfl, c, u64(blockIdx.x) * (u32(kBlock) * ITEMS));
+    const u64 base = st.base;
     if (blockIdx.x == 0 && tid == 0) *count_out = p - c;
-    const u64 lt = (1ull << lane) - 1;
     bool hashed = false;
 #pragma unroll
     for (int e = 0; e < ITEMS; ++e) {
       const u32 k = u32(e) * kBlock + u32(tid);
       const u64 j = base + k;
-      const u32 bw = s_bits[k >> 5];
-      const bool is_first = j < p && !((bw >> (k & 31)) & 1u);
+      const bool is_first = j < p && !st.listed(k);
       const u64 mask = __ballot(is_first);
-      const u64 nb = u64(before) + s_bpre[k >> 5] + u32(__popc(bw & ((1u << (k & 31)) - 1u)));
+      const u64 nb = st.nb(k);
       if (lane == 0) {
         Group g;
         g.mask = mask; g.prefix = u32(j - nb); g.pad = 0;
@@ -1211,7 +1230,6 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
         words[j] = make_word(id, m, t, ulw(l) == ulw(xf(r, 1, 0)));
       }
     }
-    (void)lt;
     if (hashed_next) {
       if (__ballot(hashed) && lane == 0) s_hashed = 1;
       __syncthreads();
@@ -1575,13 +1593,15 @@ struct Bkt2Plan {
   u32* ocnt;           // ... at this cursor (the D records, k_own_getid_list); null: none
   u32 wmarks;          // k_bkt_part writes every pair's not-first / multi mark (no k_clear pass)
   u32* nfl;            // k_bkt_dedupe2: the not-first positions (hdr->nnf counts them); null: none
+  u32 wave1;           // k_bkt_part collapse: a wave of one key touches the table once (GCZ_PART_WAVE)
 };
 
 // Append the not-first positions of a wave to bp.nfl (one atomic per wave; none once the
 // list is over its cap -- the count then only tells the flag scan to take the look-back path).
 __device__ __forceinline__ void nf_list_add(const Bkt2Plan& bp, Header* hdr, bool nf, u32 pos) {
+  if (!bp.nfl) return;
   const u64 m = __ballot(nf);
-  if (!m || !bp.nfl) return;
+  if (!m) return;
   const int lane = int(threadIdx.x & 63), lead = __ffsll((long long)m) - 1;
   u32 base = 0;
   if (lane == lead)
@@ -1739,7 +1759,7 @@ constexpr u32 kColSlots = 8192;   // its LDS table (load <= 1/2), in the part's 
         cs[i] = 0;
         // a wave whose hashed pairs all carry one key (a tandem repeat whose period divides the
         // pair's span): only its first such lane -- the earliest offset -- touches the table
-        const u64 hm = __ballot(h[i]);
+        const u64 hm = bp.wave1 ? __ballot(h[i]) : 0ull;
         if (hm) {
           const int lead = __ffsll((long long)hm) - 1;
           const u64 k0 = __shfl(key[i], lead, 64);
@@ -1924,6 +1944,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
     const u64* __restrict__ recs, const u32* __restrict__ fo, Bkt2Plan bp, u32* __restrict__ rec, Marks mk,
     Header* __restrict__ hdr, const u64* prev_count, u64 n, u32* __restrict__ ovf) {
   if (bkt2_skip(hdr, prev_count, n)) return;
+  if (!kOwner && hdr->predup) bp.nfl = nullptr;   // (collapsed levels: the flag scan takes the look-back path)
   constexpr u32 TS = kBktSlots;
   __shared__ u64 s_key[TS];
   __shared__ u32 s_pos[TS];

@@ -38,7 +38,7 @@ struct gcz_dist_state {
   DevBuf rkey, oslot, rflag, rcval, rdval, owntab, oids, omin, olist;         // owner side
   DevBuf ob_cnt, ob_off, ob_desc, ob_rec;                                      // owner bucketed dedupe
   DevBuf ob_seg, ob_rt, ob_rec2, ob_fo;                                        // ... as the two-pass partition
-  DevBuf dhdr, gath, gath2, gathf, ddesc, tail_in;
+  DevBuf dhdr, gath, gath2, gathf, ddesc, tail_in, nfl;
   u64* h_gath = nullptr;    // pinned mirrors of the gathered vectors
   u64* h_gath2 = nullptr;
   u64* h_gathf = nullptr;
@@ -55,7 +55,7 @@ void gcz_dist_state_free(gcz_ctx* c) {
                     &d->scval, &d->sdval, &d->clist, &d->olist, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab, &d->oids,
                     &d->omin, &d->ob_cnt, &d->ob_off, &d->ob_desc, &d->ob_rec, &d->ob_seg, &d->ob_rt,
                     &d->ob_rec2, &d->ob_fo,
-                    &d->dhdr, &d->gath, &d->gath2, &d->gathf, &d->ddesc, &d->tail_in})
+                    &d->dhdr, &d->gath, &d->gath2, &d->gathf, &d->ddesc, &d->tail_in, &d->nfl})
     if (b->ptr) (void)hipFree(b->ptr);
   for (u64* h : {d->h_gath, d->h_gath2, d->h_gathf})
     if (h) (void)hipHostFree(h);
@@ -932,12 +932,15 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
     Header* h = cx->hdr.as<Header>();
     const u64 nfb = (DP.S + 63) / 64, t = scan_tiles(nfb + 1);
     if (cx->ensure(cx->dl_lh, ncodes * 4 + 16) || cx->ensure(cx->dl_list, std::min<u64>(DP.S, ncodes) * 4 + 16) ||
-        cx->ensure(cx->dl_pos, (u64(NB) + xw) * 4 + t * 8 + 64) || cx->ensure(cx->dl_lower, u64(R) * xw * 4 + 16))
+        cx->ensure(cx->dl_pos, (u64(NB) + xw) * 4 + 64) || cx->ensure(cx->dl_lower, u64(R) * xw * 4 + 16))
       return dev_fail("dense leaf buffers");
     u32* bcnt = cx->dl_pos.as<u32>();
     u32* xv = bcnt + NB;
-    u64* desc = reinterpret_cast<u64*>(xv + xw);
-    u32* ticket = reinterpret_cast<u32*>(desc + t);
+    // the popcount scan's descriptors and ticket: the ones dense_phase_a zeroed for the
+    // single-device first-occurrence scan, which list mode does not run
+    const u64 t_cnt = scan_tiles(u64(NB) * DP.nch + 1);
+    u64* desc = cx->dl_desc.as<u64>() + t_cnt;
+    u32* ticket = reinterpret_cast<u32*>(desc + t) + 1;
     {
       ProfScope ps_(cx, KID_DL_FIRST);
       G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_rfirst), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -951,13 +954,13 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
     }
     {
       ProfScope ps_(cx, KID_DL_FBSCAN);
-      G_HIP(hipMemsetAsync(desc, 0, t * 8 + 8, cx->stream));
       hipLaunchKernelGGL(k_scan_excl<ScanPopc>, dim3(unsigned(t)), dim3(kScanThreads), 0, cx->stream,
                          ScanPopc{cx->dl_fb.as<unsigned long long>()}, nfb, cx->dl_wpre.as<u32>(), desc, ticket,
                          &h->count[0]);
       hipLaunchKernelGGL(k_dl_gq, dim3(NB), dim3(kDThreads), 0, cx->stream, cx->dl_lh.as<u32>(), bcnt, DP,
                          cx->dl_fb.as<unsigned long long>(), cx->dl_wpre.as<u32>(),
-                         static_cast<const u64*>(&h->count[0]), cx->dl_list.as<u32>(), xv);
+                         static_cast<const u64*>(&h->count[0]), cx->dl_list.as<u32>(), xv, cx->dl_pw.as<u32>(),
+                         cx->leaves_out.as<u64>());
       G_HIP(hipGetLastError());
     }
   }
@@ -987,7 +990,7 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
   if (total > u64(kIdx)) return fail(GCZ_ERR_CAPACITY, "more than 2^29-1 unique leaves");
   // exchange 3: every rank gets every G array, relayed in two steps so no link carries rank
   // 0's long one R - 1 times: piece q of array r goes to rank q, then each rank sends the
-  // pieces it holds to all ranks; k_dl_unrelay then puts every piece in list order
+  // pieces it holds to all ranks; k_dl_ids_mr reads each element where its piece landed
   auto pc = [&](int r, int q) { return c[r] * u64(q) / u64(R); };   // start of piece q of array r
   std::vector<u64> M1(size_t(R) * R), T(R, 0), M2(size_t(R) * R), sd2(size_t(R) * R, 0), rd2(size_t(R) * R);
   for (int r = 0; r < R; ++r)
@@ -1003,7 +1006,6 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
       rd2[size_t(d) * R + q] = o;
     }
   DlRelay relay{};
-  u64 max_piece = 0;
   {
     u64 o = 0;
     for (int q = 0; q < R; ++q)   // (relay order: piece index outer, list inner)
@@ -1012,7 +1014,6 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
         relay.seg_src[sg] = o;
         relay.seg_dst[sg] = off[r] + pc(r, q);
         relay.seg_len[sg] = M1[sg];
-        max_piece = std::max(max_piece, M1[sg]);
         o += M1[sg];
       }
     for (int r = 0; r <= R; ++r) relay.off[r] = off[r];
@@ -1050,17 +1051,14 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
       ProfScope ps_(cx, KID_IDS);
       if (cx->ensure(cx->dl_gid, sizeof(DlRelay) + 16)) return dev_fail("dense leaf relay table");
       G_HIP(hipMemcpyAsync(cx->dl_gid.ptr, &relay, sizeof(DlRelay), hipMemcpyHostToDevice, cx->stream));
-      u32* gl = cx->dl_fl.as<u32>();   // (the first lists are consumed: total <= 4^L entries fit)
-      if (max_piece)
-        hipLaunchKernelGGL(k_dl_unrelay, dim3(unsigned(R * R), unsigned(std::min<u64>(64, (max_piece + 4095) / 4096))),
-                           dim3(256), 0, cx->stream, cx->dl_recv.as<u32>(), cx->dl_gid.as<DlRelay>(), gl);
       G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_ids_mr), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 int(RB * 4)));
       hipLaunchKernelGGL(k_dl_ids_mr, dim3(NB), dim3(kDThreads), RB * 4, cx->stream, cx->dl_rec.as<u32>(),
                          cx->dl_off.as<u32>(), DP, cx->dl_pbs.as<unsigned long long>(), nwb, cx->dl_lower.as<u32>(), xw,
-                         static_cast<const u32*>(gl), cx->dl_gid.as<DlRelay>(), r, cx->dl_idrec.as<u32>());
+                         static_cast<const u32*>(cx->dl_recv.as<u32>()), cx->dl_gid.as<DlRelay>(), R, r,
+                         cx->dl_idrec.as<u32>());
       const u64 cr = c[r];
-      if (cr)
+      if (cr && !dl_rleaves_sparse(cr, DP.S))   // (sparse: k_dl_gq wrote them)
         hipLaunchKernelGGL(k_dl_rleaves, dim3(unsigned((DP.S + 255) / 256)), dim3(256), 0, cx->stream,
                            cx->dl_fb.as<unsigned long long>(), cx->dl_wpre.as<u32>(), cx->dl_pw.as<u32>(), DP,
                            cx->leaves_out.as<u64>());
@@ -1357,9 +1355,11 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     }
     if (records) {
       const u64 ns = sent(rank[i]);
+      if (cx->ensure(d.nfl, kNfListCap * 4 + 16)) return dev_fail("not-first list");
       hipLaunchKernelGGL(k_dist_flags, tiles(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
                          d.sflag.as<unsigned char>(), d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(),
-                         send_displ_of(rank[i]), u32(R), &dh->sync2[1], d.clist.as<u32>(), &dh->lcnt[0]);
+                         send_displ_of(rank[i]), u32(R), &dh->sync2[1], d.clist.as<u32>(), &dh->lcnt[0],
+                         d.nfl.as<u32>(), &dh->nnf);
       if (lookahead && nwords[i] > 0)
         hipLaunchKernelGGL(k_lookahead, blocks((nwords[i] + 1) / 2), dim3(kBlock), 0, cx->stream,
                            d.gmul.as<unsigned char>(), nwords[i], &dh->sync2[1 + 2 * R]);
@@ -1367,14 +1367,19 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
     }
     const u64 tiles = std::max<u64>(1, tiles_of(ur));
     if (!lv[i].keys_zeroed) G_HIP(hipMemsetAsync(d.ddesc.ptr, 0, tiles * 8, cx->stream));
+    // (records crossed ranks: k_dist_flags listed the positions not globally first; sparse
+    // lists rank without the look-back chain)
+    const u32* nfl = records ? d.nfl.as<u32>() : nullptr;
     if (lv[i].leaves)
       hipLaunchKernelGGL((k_dist_rank<u64>), dim3(unsigned(tiles)), dim3(kBlock), 0, cx->stream,
                          d.gnf.as<unsigned char>(), lv[i].ucount, d.gid.as<u32>(), d.ddesc.as<u64>(), &dh->ticket,
-                         &dh->sync2[0], d.scratch.as<u64>(), static_cast<u64*>(lv[i].out));
+                         &dh->sync2[0], d.scratch.as<u64>(), static_cast<u64*>(lv[i].out), nfl,
+                         static_cast<const u32*>(&dh->nnf));
     else
       hipLaunchKernelGGL((k_dist_rank<uint2>), dim3(unsigned(tiles)), dim3(kBlock), 0, cx->stream,
                          d.gnf.as<unsigned char>(), lv[i].ucount, d.gid.as<u32>(), d.ddesc.as<u64>(), &dh->ticket,
-                         &dh->sync2[0], d.scratch.as<uint2>(), static_cast<uint2*>(lv[i].out));
+                         &dh->sync2[0], d.scratch.as<uint2>(), static_cast<uint2*>(lv[i].out), nfl,
+                         static_cast<const u32*>(&dh->nnf));
     G_HIP(hipGetLastError());
   }
   c.assign(R, 0);

@@ -45,7 +45,7 @@ struct DistHdr {
   u32 ticket;                           // look-back tickets of k_dist_rank
   u32 tick[4];                          // ... of the compaction scans
   u32 lcnt[2];                          // list lengths: C records (sender), D records (owner dedupe)
-  u32 pad;
+  u32 nnf;                              // positions not globally first (k_dist_flags; listed up to kNfListCap)
   u32 ccur[kMaxRanks + 1];              // append cursors: C records per owner (sender side)
   u32 dcur[kMaxRanks + 1];              // ... D records per source (owner side)
   u64 cell[GCZ_MAX_LAYERS + 1];         // direct flags: n_local when the layer is direct, else ~0
@@ -835,12 +835,16 @@ static __global__ __launch_bounds__(kBlock) void k_own_getid_list(const u32* __r
 // Reply flags -> per local unique (gnf: not globally first, gmul: repeats globally), and
 // the C / D record counts per owner (cnt[q], cnt[R + q]: the sync2 vector).  One tile of
 // kTile records per block.
+// gnf / gmul arrive zeroed (k_node_keys, or the exchange's memsets): only the set flags are
+// written.  nfl (optional): the positions not globally first, counted in *nnf and listed while
+// there are at most kNfListCap of them (k_dist_rank's sparse path).
 static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restrict__ sidx, u64 nsent,
                                                               const unsigned char* __restrict__ sflag,
                                                               unsigned char* __restrict__ gnf,
                                                               unsigned char* __restrict__ gmul, Displ SD, u32 R,
                                                               u64* __restrict__ cnt, u32* __restrict__ clist,
-                                                              u32* __restrict__ lcnt) {
+                                                              u32* __restrict__ lcnt, u32* __restrict__ nfl,
+                                                              u32* __restrict__ nnf) {
   __shared__ u32 hc[kMaxRanks], hd[kMaxRanks];
   const int tid = threadIdx.x;
   if (tid < int(R)) { hc[tid] = 0; hd[tid] = 0; }
@@ -861,8 +865,23 @@ static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restr
       const u64 k = k0 + u64(e0 + b) * kBlock + tid;
       const unsigned char f = fl[b];
       if (k < nsent) {
-        gnf[li[b]] = f & 1;
-        gmul[li[b]] = (f >> 1) & 1;
+        if (f & 1) gnf[li[b]] = 1;
+        if (f & 2) gmul[li[b]] = 1;
+      }
+      if (nfl) {   // (one atomic per wave with such records, none once the list is over its cap)
+        const bool nf = k < nsent && (f & 1);
+        const u64 m = __ballot(nf);
+        if (m) {
+          const int lane = tid & 63, lead = __ffsll((long long)m) - 1;
+          u32 base = 0;
+          if (lane == lead)
+            base = *reinterpret_cast<volatile u32*>(nnf) > kNfListCap ? ~0u : atomicAdd(nnf, u32(__popcll(m)));
+          base = __shfl(base, lead, 64);
+          if (nf && base != ~0u) {
+            const u32 i = base + u32(__popcll(m & ((1ull << lane) - 1ull)));
+            if (i < kNfListCap) nfl[i] = li[b];
+          }
+        }
       }
       const u32 q = (want_c(f) || want_d(f)) ? seg_of(SD, R, k) : 0u;
       (void)wave_append(hc, q, k < nsent && want_c(f));
@@ -897,16 +916,35 @@ static __global__ __launch_bounds__(kBlock) void k_lookahead(const unsigned char
 // rank tagged kLocalId (the global offset is known only after the count allgather and is
 // added where the id is used: k_dist_cvals, k_dist_remap).
 constexpr u32 kLocalId = 1u << 31;
+// nfl / nnf (optional): k_dist_flags' list of the positions not globally first; at most
+// kNfListCap of them: ranked without the look-back chain (SparseTile).
 template <class T>
 __global__ __launch_bounds__(kBlock) void k_dist_rank(const unsigned char* __restrict__ gnf,
                                                       const u64* __restrict__ ucount, u32* __restrict__ gid,
                                                       u64* __restrict__ desc, u32* __restrict__ ticket,
                                                       u64* __restrict__ count_out, const T* __restrict__ scratch,
-                                                      T* __restrict__ out) {
+                                                      T* __restrict__ out, const u32* __restrict__ nfl = nullptr,
+                                                      const u32* __restrict__ nnf = nullptr) {
   __shared__ u32 s_tile;
   __shared__ u32 s_pre[kGroupsPerTile];
   const u64 u = *ucount;
   if (u64(blockIdx.x) * kTile >= u) {          // grid sized for the capacity: surplus tiles leave
+    return;
+  }
+  if (nfl && *nnf <= kNfListCap) {
+    const u32 c = *nnf;
+    const SparseTile<kItems> st = sparse_tile<kItems>(nfl, c, u64(blockIdx.x) * kTile);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *count_out = u - c;
+#pragma unroll
+    for (int e = 0; e < kItems; ++e) {
+      const u32 k = u32(e) * kBlock + threadIdx.x;
+      const u64 j = st.base + k;
+      if (j < u && !st.listed(k)) {
+        const u32 r = u32(j - st.nb(k));
+        gid[j] = r | kLocalId;
+        out[r] = scratch[j];
+      }
+    }
     return;
   }
   TileScan<kItems> ts;

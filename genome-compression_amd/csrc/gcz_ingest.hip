@@ -409,7 +409,6 @@ int gcz_build_device_fasta_buffered(gcz_ctx* c, const void* d_file, uint64_t n, 
   if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
   // fasta_reader{path, buffer_strands}: buffers of B strands (src/fasta_reader.cpp:21-31)
   const u64 B = gcz::reader_buffer_bytes(n, L, buffer_strands) / u64(L);
-  if (first_strand % B) return c->fail(GCZ_ERR_ARG, "gcz_build_device_fasta_buffered", "first_strand is not a buffer start");
   const unsigned char* b = nullptr;
   u64 nb = 0;
   if (int rc = gcz_fasta_extract_on_device(c, static_cast<const unsigned char*>(d_file), n, L, buffer_strands, &b, &nb))
@@ -418,6 +417,7 @@ int gcz_build_device_fasta_buffered(gcz_ctx* c, const void* d_file, uint64_t n, 
   // none left is an empty root list there (reduce_roots' roots.front(): undefined), an error here
   if (first_strand > 0 && first_strand >= nb / u64(L))
     return c->fail(GCZ_ERR_ARG, "gcz_build_device_fasta_buffered", "every reader buffer was already read");
+  if (first_strand % B) return c->fail(GCZ_ERR_ARG, "gcz_build_device_fasta_buffered", "first_strand is not a buffer start");
   const u64 skip = std::min<u64>(nb / u64(L), first_strand) * u64(L);
   b += skip;
   nb -= skip;

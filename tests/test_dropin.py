@@ -90,10 +90,11 @@ def test_compress_cli_errors(tmp_path, manifest):
 def test_compress_cli_gpus(name, gpus, tmp_path, manifest):
     """compress --gpus=N (shared_tree_on_gpus): N processes, one rank each; on the one-GPU
     box every rank shares the device and exchanges host-staged (GCZ_MULTI_TRANSPORT=shm).
-    Same .dag and statistics as the reference."""
+    Same .dag and statistics as the reference; the tree is gathered device to device into rank
+    0's context (gcz_group_assemble), so the frequency sort runs on the GPU (GCZ_TIMING phase)."""
     exp = manifest[f"corpus/{name}"]["expect"]
     out = tmp_path / f"{name}.dag"
-    env = dict(os.environ, GCZ_MULTI_TRANSPORT="shm")
+    env = dict(os.environ, GCZ_MULTI_TRANSPORT="shm", GCZ_TIMING="1")
     exe = os.path.join(PKG, "compress")
     r = subprocess.run([exe, "--statistics", f"--gpus={gpus}", f"--output={out}", os.path.join(GOLDEN, "data", name)],
                        capture_output=True, text=True, cwd=str(tmp_path), env=env, timeout=240)
@@ -101,6 +102,7 @@ def test_compress_cli_gpus(name, gpus, tmp_path, manifest):
     f = r.stdout.strip().split(",")
     assert int(f[1]) == exp["width"] and f[2] == exp["ratio"] and int(f[4]) == exp["bytes"]
     assert hashlib.sha256(out.read_bytes()).hexdigest() == exp["sha_dag"]
+    assert "gcz-time device-sort" in r.stderr, r.stderr
 
 
 @pytest.mark.gpu
