@@ -241,7 +241,8 @@ struct gcz_ctx {
   bool two_pass = true;      // ... as the two-pass partition where records fit (GCZ_BUCKET_TWO=0: one pass)
   bool part_marks = true;    // ... whose partition writes every mark (no clearing pass; GCZ_PART_MARKS=0)
   bool sparse_scan = true;   // ... and whose few repeats are ranked without a look-back scan (GCZ_SPARSE_SCAN=0)
-  bool part_wave = true;     // ... and whose collapse inserts a one-key wave once (GCZ_PART_WAVE=0)
+  bool part_wave = false;    // ... and whose collapse inserts a one-key wave once (GCZ_PART_WAVE=1;
+                             // measured 0.14 ms slower on tandem_3g2, off)
   gcz_host::DevBuf nf_list;  // ... those repeats' positions (k_bkt_dedupe2)
   bool bucket_now = true;    // this build (cleared after a bucket overflow: rebuild with the table)
   int dense_mode = 1;        // dense leaf level (gcz_dense.h): 0 off, 1 on large pure-ACGT inputs, 2 any size (GCZ_DENSE)

@@ -706,50 +706,84 @@ struct DlRelay {
                                                          const u32* __restrict__ gl, const DlRelay* __restrict__ T,
                                                          int R, int r, u32* __restrict__ idrec) {
   extern __shared__ u32 s_id[];    // RB
-  __shared__ u64 s_acc[256], s_rf[256], s_mine[256];
-  __shared__ u64 s_sdst[kDlMaxRanks + 1], s_ssrc[kDlMaxRanks];
-  __shared__ u32 s_pf[256];
-  __shared__ u32 s_tmp[16];
-  const int tid = threadIdx.x;
+  // ranks q <= r in rounds of QB: their words, first-held words and prefixes loaded and
+  // scanned together (one load round trip and two barriers per round, not per rank)
+  constexpr int QB = 4;
+  __shared__ u64 s_rf[QB][256];
+  __shared__ u32 s_pf[QB][256];
+  __shared__ u64 s_sdst[QB][kDlMaxRanks + 1], s_ssrc[QB][kDlMaxRanks], s_base[QB];
+  __shared__ u32 s_wt[QB][4];
+  __shared__ u64 s_mine[256];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const u32 b = blockIdx.x, RB = 1u << P.IB, NW = RB >= 64 ? RB / 64 : 1u;
-  for (u32 lw = tid; lw < NW; lw += kDThreads) {
-    s_acc[lw] = 0;
-    s_mine[lw] = bucket_word(pbs + u64(r) * stride, b, P.IB, lw);
-  }
+  u64 acc = 0;   // (threads < NW: the OR of the words of the ranks before this round)
+  if (u32(tid) < NW) s_mine[tid] = bucket_word(pbs + u64(r) * stride, b, P.IB, tid);
   const u32 lw = u32(tid) >> 2, sh = (u32(tid) & 3u) * 16u;   // this thread's codes: 16 tid .. 16 tid + 15
-  for (int q = 0; q <= r; ++q) {
-    u32 pc = 0;
-    if (tid < R) {   // list q's pieces, by global id position
-      s_sdst[tid] = T->seg_dst[u64(q) * R + tid];
-      s_ssrc[tid] = T->seg_src[u64(q) * R + tid];
+  for (int q0 = 0; q0 <= r; q0 += QB) {
+    const int nq = r + 1 - q0 < QB ? r + 1 - q0 : QB;
+    if (tid < nq * R) {   // the lists' pieces, by global id position
+      const int i = tid / R, pp = tid % R;
+      s_sdst[i][pp] = T->seg_dst[u64(q0 + i) * R + pp];
+      s_ssrc[i][pp] = T->seg_src[u64(q0 + i) * R + pp];
     }
-    if (tid == 0) s_sdst[R] = T->off[q + 1];
+    if (tid < nq) {
+      s_sdst[tid][R] = T->off[q0 + tid + 1];
+      s_base[tid] = T->off[q0 + tid] + xvs[u64(q0 + tid) * xstride + 2 + b];
+    }
+    u32 pc[QB], inc[QB];
     if (u32(tid) < NW) {
-      const u64 w = bucket_word(pbs + u64(q) * stride, b, P.IB, tid);
-      const u64 rf = w & ~s_acc[tid];
-      s_rf[tid] = rf;
-      s_acc[tid] |= w;
-      pc = u32(__popcll(rf));
+      u64 w[QB];
+#pragma unroll
+      for (int i = 0; i < QB; ++i) w[i] = i < nq ? bucket_word(pbs + u64(q0 + i) * stride, b, P.IB, tid) : 0ull;
+#pragma unroll
+      for (int i = 0; i < QB; ++i) {
+        const u64 rf = w[i] & ~acc;
+        acc |= w[i];
+        s_rf[i][tid] = rf;
+        pc[i] = u32(__popcll(rf));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < QB; ++i) pc[i] = 0;
     }
-    u32 total;
-    const u32 e = block_excl(pc, s_tmp, &total);   // (NW <= 256 < kDThreads)
-    if (u32(tid) < NW) s_pf[tid] = e;
+    if (wave < 4) {   // (NW <= 256: the first four waves) inclusive wave scans, wave totals
+#pragma unroll
+      for (int i = 0; i < QB; ++i) {
+        u32 v = pc[i];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const u32 y = __shfl_up(v, o, 64);
+          if (lane >= o) v += y;
+        }
+        inc[i] = v;
+        if (lane == 63) s_wt[i][wave] = v;
+      }
+    }
     __syncthreads();
-    if (total && 16u * u32(tid) < RB) {   // codes first held by q: id = off_q + G_q[prefix_q(b) + index]
-      const u64 rfw = s_rf[lw];
-      u32 win = u32(rfw >> sh) & 0xffffu & u32(s_mine[lw] >> sh);   // (codes not held here need no id)
-      if (win) {
-        const u64 base = T->off[q] + xvs[u64(q) * xstride + 2 + b] + s_pf[lw];
-        const u32 q0 = u32(T->off[q]);
+    if (u32(tid) < NW) {
+#pragma unroll
+      for (int i = 0; i < QB; ++i) {
+        u32 pre = inc[i] - pc[i];
+        for (int w2 = 0; w2 < wave; ++w2) pre += s_wt[i][w2];
+        s_pf[i][tid] = pre;
+      }
+    }
+    __syncthreads();
+    if (16u * u32(tid) < RB) {   // codes first held by q: id = off_q + G_q[prefix_q(b) + index]
+      const u32 mw = u32(s_mine[lw] >> sh) & 0xffffu;   // (codes not held here need no id)
+      for (int i = 0; i < nq; ++i) {
+        const u64 rfw = s_rf[i][lw];
+        u32 win = u32(rfw >> sh) & mw;
+        if (!win) continue;
+        const u64 base = s_base[i] + s_pf[i][lw];
+        const u32 qo = u32(T->off[q0 + i]);
         int pc2 = 0;   // the piece holding the window's first id position, then onwards
-        const u64 g0 = base + u64(__popcll(rfw & ((1ull << (sh + u32(__ffs(int(win))) - 1u)) - 1ull)));
-        while (pc2 + 1 < R && s_sdst[pc2 + 1] <= g0) ++pc2;
         while (win) {
           const u32 j = u32(__ffs(int(win))) - 1u;
           win &= win - 1u;
           const u64 g = base + u64(__popcll(rfw & ((1ull << (sh + j)) - 1ull)));
-          while (pc2 + 1 < R && s_sdst[pc2 + 1] <= g) ++pc2;
-          s_id[16u * u32(tid) + j] = q0 + gl[s_ssrc[pc2] + (g - s_sdst[pc2])];
+          while (pc2 + 1 < R && s_sdst[i][pc2 + 1] <= g) ++pc2;
+          s_id[16u * u32(tid) + j] = qo + gl[s_ssrc[i][pc2] + (g - s_sdst[i][pc2])];
         }
       }
     }

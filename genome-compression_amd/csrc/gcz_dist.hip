@@ -485,14 +485,18 @@ struct DistPlan {
     if (G < 0) G = 0;
     const u64 g = 1ull << G;
     B = (T + g - 1) / g * g;
-    // Rank 0 also gathers the top and finishes it alone (~0.1 ms at 1 Gbase over 8 ranks
-    // against ~1.1 ms per rank, most of it not proportional to the share), so it takes a
-    // smaller share: 1000 - 25 R permille of B (0.80 at R = 8, 0.95 at R = 2), the rest
-    // spread over the others (GCZ_DIST_RANK0_PERMILLE overrides; 1000 = even shares).  Only
+    // Rank 0 also finishes the gathered top alone, and its leaf level ranks the whole
+    // dictionary (at 1 Gbase it first-holds 3.6-4.1 M of the 4.2 M leaves: their position
+    // bitmap, ranks and leaves), work that does not shrink with its share; so it takes a
+    // smaller share of B: 850 / 800 / 750 / 700 permille at R = 2 / 3 / 4 / >= 5, the rest
+    // spread over the others (measured on 1 Gbase over virtual ranks, scripts/gpu_share.sh:
+    // slowest rank 1.85 -> 1.81 ms at R = 2, 1.19 -> 1.07 at R = 4, 0.81 -> 0.77 at R = 8
+    // against the earlier 1000 - 25 R; GCZ_DIST_RANK0_PERMILLE overrides, 1000 = even shares).  Only
     // where the ranks hold >= 2^20 strands, so every share stays a multiple of 2^G far
     // above 256.
     const char* e0 = std::getenv("GCZ_DIST_RANK0_PERMILLE");
-    const u64 pm = e0 ? u64(std::max(500, std::min(1000, std::atoi(e0)))) : u64(std::max(700, 1000 - 25 * R));
+    const u64 pm = e0 ? u64(std::max(500, std::min(1000, std::atoi(e0))))
+                      : u64(R <= 2 ? 850 : R == 3 ? 800 : R == 4 ? 750 : 700);
     B0 = B1 = B;
     if (R > 1 && G > 0 && T >= (1ull << 20) && pm < 1000) {
       B0 = std::max<u64>(g, B * pm / 1000 / g * g);

@@ -319,6 +319,7 @@ static __global__ __launch_bounds__(kBlock) void k_bucket_scatter(RecSrc s, cons
   __syncthreads();
   const u64 lt = (1ull << lane) - 1;
   const bool pre = s.canon != nullptr && s.leaves == nullptr;
+  const u32 dbits = s.R > 1 ? 32u - u32(__clz(int(s.R - 1))) : 0u;   // bits of a destination
   int buf = 0;
   for (int e0 = 0; e0 < kItems; e0 += kPre, buf ^= 1) {
     u64 key[kPre];
@@ -337,16 +338,15 @@ static __global__ __launch_bounds__(kBlock) void k_bucket_scatter(RecSrc s, cons
         ok[q] = rec_get(s, u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid, key[q], lid[q]);
       }
       d[q] = ok[q] ? owner_of(rec_key(s, key[q]), s.R) : 0u;
-      before[q] = 0;
-      u64 left = __ballot(ok[q]);
-      while (left) {                                  // one ballot per distinct destination in the wave
-        const int leader = __ffsll((long long)left) - 1;
-        const u32 dl = __shfl(d[q], leader, 64);
-        const u64 m = __ballot(ok[q] && d[q] == dl);
-        if (ok[q] && d[q] == dl) before[q] = __popcll(m & lt);
-        if (lane == leader) wcnt[buf][q][wave][dl] = u32(__popcll(m));
-        left &= ~m;
+      // the lanes sharing this lane's destination: one ballot per destination bit
+      u64 m = __ballot(ok[q]);
+      for (u32 bit = 0; bit < dbits; ++bit) {
+        const bool set = (d[q] >> bit) & 1u;
+        const u64 bb = __ballot(ok[q] && set);
+        m &= set ? bb : ~bb;
       }
+      before[q] = u32(__popcll(m & lt));
+      if (ok[q] && before[q] == 0) wcnt[buf][q][wave][d[q]] = u32(__popcll(m));
     }
     __syncthreads();   // this round's counts
     if (tid < int(s.R)) {   // per destination: exclusive offsets in (item, wave) order
