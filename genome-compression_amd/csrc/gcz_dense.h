@@ -236,6 +236,8 @@ template <int L, bool kBases>
         const u32 h = (cc * P.K) & P.cmask;
         pw[s] = make_word(h, m, t, v);
         atomicAdd(&s_hist[h >> ib], 1u);
+      } else {
+        pw[s] = ~0u;   // (no pre-word is all ones: h < 2^24; the multi-rank scatter skips it)
       }
     }
   }
@@ -273,7 +275,7 @@ template <int L, bool kBases>
 #pragma unroll
   for (u32 j = 0; j < kDC / kDThreads; ++j) {
     const u32 q = j * kDThreads + tid;
-    if (q < n) {
+    if (q < n && h[j] != ~0u) {   // (a strand the pack rejected: the multi-rank build runs on to the exchange)
       const u32 hc = h[j] & kIdx;
       const u32 slot = atomicAdd(&s_cur[hc >> P.IB], 1u);
       s_stage[slot] = ((hc & imask) << kDLog) | q | (h[j] & kBits);   // (IB + 15 <= 29 bits, then m/t/v)
@@ -597,12 +599,6 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
 //            id table, no list in id order -- then one final word per record
 //   words    as single-device; leaves: rank r's r-first codes in position order.
 
-// the status words behind each rank's bitmap (exchange 1), rank-major into out[3 r + j]
-[[maybe_unused]] static __global__ void k_dl_vecs(const u64* __restrict__ pbs, u64 stride, u64 nw, int R,
-                                                 u64* __restrict__ out) {
-  for (int t = threadIdx.x; t < 3 * R; t += blockDim.x) out[t] = pbs[u64(t / 3) * stride + nw + t % 3];
-}
-
 // Bits [64 lw, 64 lw + 64) of bucket b's codes in bitmap bm (RB < 64: the bucket's RB bits).
 static __device__ __forceinline__ u64 bucket_word(const unsigned long long* __restrict__ bm, u32 b, u32 IB, u32 lw) {
   const u64 h0 = u64(b) << IB;
@@ -692,7 +688,8 @@ static __device__ __forceinline__ u64 bucket_word(const unsigned long long* __re
 }
 
 // G: per bucket, the local r-first rank of each r-first code in code order, at the bucket's
-// prefix; xv = the rank's exchange vector {r-first count, 0, prefix of bucket 0, 1, ...}.
+// prefix; xv = the rank's exchange vector {r-first count, status, prefix of bucket 0, 1, ...}
+// (status: bit 0 a non-ACGT strand, bit 1 repetitive data; the host adds bit 2, failed).
 // A rank with few r-first codes (dl_rleaves_sparse: count * 16 < S) writes its leaves here,
 // by rank (random stores of few entries), instead of a pass over every position (k_dl_rleaves).
 __host__ __device__ __forceinline__ bool dl_rleaves_sparse(u64 count, u64 S) { return count * 16 < S; }
@@ -700,7 +697,8 @@ __host__ __device__ __forceinline__ bool dl_rleaves_sparse(u64 count, u64 S) { r
                                                      DensePlan P, const unsigned long long* __restrict__ rfb,
                                                      const u32* __restrict__ wpre, const u64* __restrict__ ucount,
                                                      u32* __restrict__ G, u32* __restrict__ xv,
-                                                     const u32* __restrict__ pw, u64* __restrict__ leaves_out) {
+                                                     const u32* __restrict__ pw, u64* __restrict__ leaves_out,
+                                                     const u64* __restrict__ status) {
   __shared__ u32 s_tmp[16];
   const int tid = threadIdx.x;
   const u32 b = blockIdx.x, RB = 1u << P.IB;
@@ -708,9 +706,9 @@ __host__ __device__ __forceinline__ bool dl_rleaves_sparse(u64 count, u64 S) { r
   (void)block_excl(u32(tid) < b ? bcnt[tid] : 0u, s_tmp, &pre);
   if (tid == 0) {
     xv[2 + b] = pre;
-    if (b == 0) {
+    if (b == 0) {   // the r-first count and the phase-A status words (k_dl_first's vec)
       xv[0] = u32(*ucount);
-      xv[1] = 0;
+      xv[1] = (status[0] ? 1u : 0u) | (status[2] ? 2u : 0u);
     }
   }
   const u32 n = bcnt[b];

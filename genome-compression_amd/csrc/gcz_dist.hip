@@ -910,21 +910,9 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
     G_RC(x_allgather("leaf presence bitmaps + status", nwb * 8, s, rv));
     ctx[0]->prof_end(KID_EXCHANGE, e0);
   }
-  std::vector<u64> hv(size_t(3) * R + 8);
-  hipLaunchKernelGGL(k_dl_vecs, dim3(1), dim3(64), 0, ctx[0]->stream, ctx[0]->dl_pbs.as<u64>(), nwb, nw, R,
-                     ctx[0]->dl_seg.as<u64>() + 8);
-  G_HIP(hipGetLastError());
-  G_HIP(hipMemcpyAsync(hv.data(), ctx[0]->dl_seg.as<u64>() + 8, size_t(3) * R * 8, hipMemcpyDeviceToHost,
-                       ctx[0]->stream));
-  G_RC(host_sync());
-  for (int r = 0; r < R; ++r)
-    if (hv[3 * r] == 2) return local_rc && local_rc != GCZ_ERR_DEVICE ? local_rc : dev_fail("dense leaves (a rank failed)");
-  bool pred = false;
-  for (int r = 0; r < R; ++r) {
-    if (hv[3 * r]) return GCZ_OK;   // some rank holds a non-ACGT strand: the hash-table leaf level
-    pred = pred || hv[3 * r + 2] != 0;
-  }
-  any_predup = pred;
+  // (no host sync here: the status words travel on in the exchange vectors below; a rank
+  // with a non-ACGT strand runs B1 on in-bounds data -- its pack marked those strands -- and
+  // every rank learns of it after exchange 2)
   // B1: r-first codes (held by no lower rank), their position bitmap and local ranks, and G =
   // those ranks in code order with the bucket prefixes in the exchange vector (gcz_dense.h)
   const u32 NB = ctx[0]->dl_plan.NB, RB = 1u << ctx[0]->dl_plan.IB;
@@ -934,6 +922,12 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
     const int r = rank[i];
     const DensePlan& DP = cx->dl_plan;
     Header* h = cx->hdr.as<Header>();
+    if (cx->ensure(cx->dl_pos, (u64(NB) + xw) * 4 + 64)) return dev_fail("dense leaf buffers");
+    if (local_rc) {   // this rank's phase A failed: it joins exchange 2 with a failure word only
+      const u32 failed_xv[2] = {0, 4};
+      G_HIP(hipMemcpyAsync(cx->dl_pos.as<u32>() + NB, failed_xv, sizeof(failed_xv), hipMemcpyHostToDevice, cx->stream));
+      continue;
+    }
     const u64 nfb = (DP.S + 63) / 64, t = scan_tiles(nfb + 1);
     if (cx->ensure(cx->dl_lh, ncodes * 4 + 16) || cx->ensure(cx->dl_list, std::min<u64>(DP.S, ncodes) * 4 + 16) ||
         cx->ensure(cx->dl_pos, (u64(NB) + xw) * 4 + 64) || cx->ensure(cx->dl_lower, u64(R) * xw * 4 + 16))
@@ -964,7 +958,7 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
       hipLaunchKernelGGL(k_dl_gq, dim3(NB), dim3(kDThreads), 0, cx->stream, cx->dl_lh.as<u32>(), bcnt, DP,
                          cx->dl_fb.as<unsigned long long>(), cx->dl_wpre.as<u32>(),
                          static_cast<const u64*>(&h->count[0]), cx->dl_list.as<u32>(), xv, cx->dl_pw.as<u32>(),
-                         cx->leaves_out.as<u64>());
+                         cx->leaves_out.as<u64>(), static_cast<const u64*>(cx->dl_pb.as<u64>() + nw));
       G_HIP(hipGetLastError());
     }
   }
@@ -984,6 +978,13 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
   std::vector<u32> hx(size_t(R) * xw);
   G_HIP(hipMemcpyAsync(hx.data(), ctx[0]->dl_lower.ptr, hx.size() * 4, hipMemcpyDeviceToHost, ctx[0]->stream));
   G_RC(host_sync());
+  {   // status words (gcz_dense.h k_dl_gq): bit 0 a non-ACGT strand, bit 1 repetitive data, bit 2 failed
+    u32 any = 0;
+    for (int r = 0; r < R; ++r) any |= hx[size_t(r) * xw + 1];
+    if (any & 4) return local_rc && local_rc != GCZ_ERR_DEVICE ? local_rc : dev_fail("dense leaves (a rank failed)");
+    if (any & 1) return GCZ_OK;   // some rank holds a non-ACGT strand: the hash-table leaf level
+    any_predup = (any & 2) != 0;
+  }
   c.assign(R, 0);
   off.assign(R + 1, 0);
   for (int r = 0; r < R; ++r) {
