@@ -507,12 +507,27 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   const u64 tile = scan_tile(p);
   const dim3 gs(unsigned((p + tile - 1) / tile));
   u64* ndesc = p <= kSmallScanMax ? nullptr : a.desc;   // small levels: no look-back chain
+  // large levels: the tiles' prefixes counted ahead instead of the look-back (GCZ_TILE_COUNT)
+  u32* tpre = nullptr;
+  if (ndesc && tile_count && !a.fused) {
+    const u64 nt = (p + tile - 1) / tile;
+    const void* had = tcount.ptr;
+    if (int rc = ensure(tcount, nt * 4 + 64)) return rc;
+    if (tcount.ptr != had) HIP_TRY(hipMemsetAsync(tcount.ptr, 0, 64, stream));   // (the done counter, once)
+    tpre = tcount.as<u32>() + 16;
+    auto count = [&](auto items) {
+      hipLaunchKernelGGL((k_tile_count<decltype(items)::value>), gs, dim3(kBlock), 0, stream, knf, p, a.pcount, n,
+                         tpre, tcount.as<u32>());
+    };
+    if (tile == u64(kTile)) count(std::integral_constant<int, kItems>{});
+    else count(std::integral_constant<int, kItemsSmall>{});
+  }
   auto flagscan = [&](auto items) {
     hipLaunchKernelGGL((k_flagscan_node<decltype(items)::value>), gs, dim3(kBlock), 0, stream, a.words, p, a.in, n,
                        knf, d_grp, ndesc, a.ticket, a.out, a.count, a.pcount, mk.multi, a.hashed_next, clr_nf, clr_mu,
                        clr16, a.fused && (!a.fused_last || a.tail_settles) ? a.sid : nullptr,
                        bkt == 2 ? static_cast<const u32*>(&d_hdr->predup) : nullptr, b2.nfl,
-                       static_cast<const u32*>(&d_hdr->nnf));
+                       static_cast<const u32*>(&d_hdr->nnf), static_cast<const u32*>(tpre));
   };
   if (tile == u64(kTile)) flagscan(std::integral_constant<int, kItems>{});
   else if (tile == u64(kTileSmall)) flagscan(std::integral_constant<int, kItemsSmall>{});
@@ -987,6 +1002,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   if (const char* t = std::getenv("GCZ_PART_MARKS")) c->part_marks = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_SPARSE_SCAN")) c->sparse_scan = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_PART_WAVE")) c->part_wave = std::atoi(t) != 0;
+  if (const char* t = std::getenv("GCZ_TILE_COUNT")) c->tile_count = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_DENSE")) c->dense_mode = std::atoi(t);
   if (const char* t = std::getenv("GCZ_GRAPH")) c->use_graph = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_FUSED")) c->use_fused = std::atoi(t) != 0;
@@ -1011,7 +1027,7 @@ void gcz_ctx_destroy(gcz_ctx* c) {
                     &c->dl_rec, &c->dl_idrec, &c->dl_cnt, &c->dl_off, &c->dl_offt, &c->dl_fpg, &c->dl_fb, &c->dl_wpre,
                     &c->dl_desc, &c->dl_fl, &c->dl_fo, &c->dl_lh, &c->dl_pb, &c->dl_pbs, &c->dl_lower,
                     &c->dl_pos, &c->dl_list, &c->dl_gid, &c->dl_recv, &c->dl_stage, &c->dl_seg, &c->seg_w,
-                    &c->seg_nf, &c->seg_mu, &c->seg_in, &c->nf_list})
+                    &c->seg_nf, &c->seg_mu, &c->seg_in, &c->nf_list, &c->tcount})
     if (b->ptr) (void)hipFree(b->ptr);
   if (c->h_hdr) (void)hipHostFree(c->h_hdr);
   if (c->h_ring) (void)hipHostFree(c->h_ring);

@@ -904,18 +904,82 @@ struct NoPrefetch {
   __device__ __forceinline__ void operator()() const {}
 };
 
+// Tile prefixes ahead of a scan (the alternative to the look-back chain on large levels):
+// block t counts the first occurrences (zero marks) of tile t of T = kBlock * ITEMS positions,
+// and the last block to finish turns the counts into exclusive prefixes tpre[t] (and resets
+// the done counter for the next level).
+template <int ITEMS>
+__global__ __launch_bounds__(kBlock) void k_tile_count(const unsigned char* __restrict__ nf, u64 p,
+                                                       const u64* prev_count, u64 n, u32* __restrict__ tpre,
+                                                       u32* __restrict__ done) {
+  if (prev_count && level_direct(prev_count, n)) return;
+  constexpr u32 T = u32(kBlock) * ITEMS;
+  __shared__ u32 s_red[kBlock / 64];
+  __shared__ u32 s_last;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const u64 base = u64(blockIdx.x) * T;
+  u32 c = 0;
+  if (base + T <= p) {
+    const uint4* q = reinterpret_cast<const uint4*>(nf + base);
+    for (u32 i = u32(tid); i < T / 16; i += kBlock) {
+      const uint4 v = q[i];
+      c += zero_bytes(v.x) + zero_bytes(v.y) + zero_bytes(v.z) + zero_bytes(v.w);
+    }
+  } else {
+    for (u64 j = base + u64(tid); j < p; j += kBlock) c += nf[j] == kNfMaybe ? 1u : 0u;
+  }
+  c = u32(wave_sum(u64(c)));
+  if (lane == 0) s_red[wave] = c;
+  __syncthreads();
+  if (tid == 0) {
+    u32 t = 0;
+    for (int w = 0; w < kBlock / 64; ++w) t += s_red[w];
+    tpre[blockIdx.x] = t;
+    __threadfence();
+    s_last = atomicAdd(done, 1u) == gridDim.x - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  // the last block: exclusive scan of the gridDim.x tile counts, in place
+  const u32 nt = gridDim.x, per = (nt + kBlock - 1) / kBlock, t0 = u32(tid) * per;
+  u32 loc = 0;
+  for (u32 t = t0; t < t0 + per && t < nt; ++t) loc += __hip_atomic_load(&tpre[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  u32 inc = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u32 y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  __syncthreads();
+  if (lane == 63) s_red[wave] = inc;
+  __syncthreads();
+  u32 run = inc - loc;
+  for (int w = 0; w < wave; ++w) run += s_red[w];
+  for (u32 t = t0; t < t0 + per && t < nt; ++t) {
+    const u32 v = __hip_atomic_load(&tpre[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tpre[t] = run;
+    run += v;
+  }
+  if (tid == 0) *done = 0;
+}
+
 // after_marks() runs once the tile's marks are read and before the scan waits: loads
 // issued there (e.g. the first occurrences' input pairs) overlap the look-back.
+// tpre (optional, with desc): the tiles' prefixes, counted ahead (k_tile_count): tiles in
+// block order, no look-back chain.
 template <int ITEMS, class AfterMarks = NoPrefetch>
 __device__ __forceinline__ void tile_scan(TileScan<ITEMS>& ts, u32* s_tile, u32* s_pre,
                                           const unsigned char* __restrict__ nf, u64 j0, u64 p, u64 id0,
                                           u64* __restrict__ desc, u32* __restrict__ ticket,
-                                          u64* __restrict__ count_out, AfterMarks after_marks = {}) {
+                                          u64* __restrict__ count_out, AfterMarks after_marks = {},
+                                          const u32* __restrict__ tpre = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool direct = desc == nullptr;
-  if (tid == 0) *s_tile = direct ? 0u : atomicAdd(ticket, 1u);
+  const bool counted = tpre != nullptr;
+  if (tid == 0) *s_tile = direct || counted ? 0u : atomicAdd(ticket, 1u);
   __syncthreads();
-  const u64 tile = direct ? u64(blockIdx.x) : u64(*s_tile);
+  const u64 tile = direct || counted ? u64(blockIdx.x) : u64(*s_tile);
   ts.base = j0 + tile * (kBlock * ITEMS);
   // short tiles: the marks' loads go out before the prefix count's (long tiles read them
   // one ballot at a time: registers)
@@ -981,6 +1045,8 @@ __device__ __forceinline__ void tile_scan(TileScan<ITEMS>& ts, u32* s_tile, u32*
     u64 prefix = tile == 0 ? id0 : 0;   // descriptors' P values already include id0
     if (direct) {
       prefix = id0 + *s_tile;
+    } else if (counted) {
+      prefix = id0 + tpre[tile];
     } else if (tile == 0) {
       if (lane == 0) __hip_atomic_store(&desc[0], kStP | (id0 + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
@@ -1154,7 +1220,8 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
                                                          uint4* __restrict__ clr_multi, u64 clr16,
                                                          u32* __restrict__ sid, const u32* __restrict__ dup_flag,
                                                          const u32* __restrict__ nfl = nullptr,
-                                                         const u32* __restrict__ nnf = nullptr) {
+                                                         const u32* __restrict__ nnf = nullptr,
+                                                         const u32* __restrict__ tpre = nullptr) {
   // fused small-build levels: clear the marks of the level after this one (its parity
   // set held the previous level's marks, last read by this level's insert)
   for (u64 i = u64(blockIdx.x) * kBlock + threadIdx.x; i < clr16; i += u64(gridDim.x) * kBlock) {
@@ -1248,7 +1315,7 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
       }
     }
   };
-  tile_scan(ts, &s_tile, s_pre, nf, 0, p, 0, desc, ticket, count_out, fetch);
+  tile_scan(ts, &s_tile, s_pre, nf, 0, p, 0, desc, ticket, count_out, fetch, tpre);
   const u64 lt = (1ull << lane) - 1;
   bool hashed = false;
   const bool dups = dup_flag && *dup_flag != 0;   // block-collapsed repeats (k_bkt_part) exist
