@@ -463,6 +463,7 @@ struct ShmTransport : Transport {
 struct DistPlan {
   u64 S = 0;
   int R = 1, G = 0, D = 0;
+  int Gh = 0;   // hash-consed (non-direct) levels from Gh on are gathered to rank 0 (G >= Gh)
   u64 B = 0;
   std::vector<u64> nk;   // global input count of node level k (nk[0] = S); pairs of level k = nk[k+1]
 
@@ -473,16 +474,24 @@ struct DistPlan {
     while (nk.back() > 1 || nk.size() == 1) nk.push_back((nk.back() + 1) / 2);
     D = int(nk.size()) - 1;
     const u64 T = (S + R - 1) / R;
-    // >= 2^t elements per rank after G levels; rank 0 gathers the ~R * 2^t words left and
-    // finishes alone.  Every distributed hash-consed level pays an exchange round (two
-    // host syncs, four or five collectives) whatever its size, so the small levels go to
-    // rank 0: t = 23 - ceil(log2 R) (~2^23 words in the tail; GCZ_DIST_TAIL_LOG2 overrides).
+    // Levels 0 .. G-1 pair within a rank (>= 2^9 elements per rank after G levels); the words
+    // left are gathered to rank 0, which finishes alone.  A direct level (every element
+    // unique: ids are positions) costs no exchange, so direct levels stay distributed down to
+    // G; but every distributed hash-consed level pays an exchange round (two host syncs, four
+    // or five collectives) whatever its size, so a hash-consed level from Gh on -- ~2^23 words
+    // left, t = 23 - ceil(log2 R) -- is gathered instead (GCZ_DIST_TAIL_LOG2 overrides t).
+    // Uniform data: levels >= 1 are direct, the gather holds ~R * 2^9 words (round 3 gathered
+    // 2^23: 5.2 MB over every link into rank 0 at R = 8, and rank 0 ran their direct levels).
+    auto depth = [&](int t) {
+      int g = T < (2ull << t) ? 0 : int(bit_width(T)) - 1 - t;
+      g = std::min(g, 20);
+      g = std::min(g, D - 1);
+      return std::max(g, 0);
+    };
     const char* env = std::getenv("GCZ_DIST_TAIL_LOG2");
-    const int t = env ? std::atoi(env) : std::max(9, 23 - int(bit_width(u64(R) - 1)));
-    G = T < (2ull << t) ? 0 : int(bit_width(T)) - 1 - t;
-    G = std::min(G, 20);
-    G = std::min(G, D - 1);
-    if (G < 0) G = 0;
+    const int th = env ? std::atoi(env) : std::max(9, 23 - int(bit_width(u64(R) - 1)));
+    Gh = depth(th);
+    G = std::max(Gh, depth(9));
     const u64 g = 1ull << G;
     B = (T + g - 1) / g * g;
     // Rank 0 also finishes the gathered top alone, and its leaf level ranks the whole
@@ -794,24 +803,28 @@ int gcz_group::alloc(int i, u64 leaf_cap) {
   const int r = rank[i];
   const DistPlan& P = plan;
   const u64 S_r = P.count(r, 0);
-  const u64 nG = r == 0 ? P.nk[P.G] : 0;
+  const u64 nG = r == 0 ? P.nk[P.Gh] : 0;   // (the gather happens at a level in [Gh, G])
   const u64 wmax = std::max(S_r, nG);
   if (!c->dist) c->dist = new gcz_dist_state();
   gcz_dist_state& d = *c->dist;
-  // node storage: local slices of the distributed layers, then (rank 0) the tail layers
+  // node storage: local slices of the distributed layers; rank 0 holds every layer from Gh on
+  // whole (a gathered layer, or its slice at the region's start)
   node_base[i].assign(P.D + 1, 0);
   u64 nodes = 0;
   for (int k = 0; k < P.D; ++k) {
     node_base[i][k] = nodes;
-    if (k < P.G) nodes += P.count(r, k + 1);
-    else if (r == 0) nodes += P.nk[k + 1];
+    if (r == 0 && k >= P.Gh) nodes += P.nk[k + 1];
+    else if (k < P.G) nodes += P.count(r, k + 1);
   }
   node_base[i][P.D] = nodes;
   const auto chunks = leaf_chunks(S_r, leaf_first_log2);
   u64 tiles = 0;
   auto ntiles = [](u64 n) { return (n + scan_tile(n) - 1) / scan_tile(n); };
   for (size_t q = 0; q + 1 < chunks.size(); ++q) tiles += ntiles(chunks[q + 1] - chunks[q]);
-  for (int k = 0; k < P.D; ++k) tiles += ntiles(k < P.G ? P.count(r, k + 1) : (r == 0 ? P.nk[k + 1] : 0));
+  for (int k = 0; k < P.D; ++k) {
+    tiles += ntiles(k < P.G ? P.count(r, k + 1) : 0);
+    if (r == 0 && k >= P.Gh) tiles += ntiles(P.nk[k + 1]);
+  }
   int rc;
   if ((rc = c->ensure(c->wa, wmax * 4 + 16))) return rc;
   if ((rc = c->ensure(c->wb, wmax * 4 + 16))) return rc;
@@ -1747,7 +1760,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     // Without the local dedupe the leaf words are translated by layer 0's k_node_keys (one
     // pass instead of two), unless layer 0 turns out direct or is not distributed (exchange
     // decides once the leaf totals are known: leaf_deferred).
-    for (int i = 0; i < NL; ++i) lv[i].defer_remap = G > 0;
+    for (int i = 0; i < NL; ++i) lv[i].defer_remap = P.Gh > 0;   // (layer 0 is distributed then)
     if (!dense) {
       std::vector<u64> nw(NL);
       for (int i = 0; i < NL; ++i) nw[i] = P.count(rank[i], 0);
@@ -1793,7 +1806,12 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     bool retry = false;
     std::vector<u32*> cur_in(NL), cur_out(NL);
     for (int i = 0; i < NL; ++i) { cur_in[i] = ctx[i]->wa.as<u32>(); cur_out[i] = ctx[i]->wb.as<u32>(); }
+    int Gx = G;   // the level whose input is gathered to rank 0
     for (int k = 0; k < G && !retry; ++k) {
+      if (!direct && k >= P.Gh) {   // a small hash-consed level: rank 0 finishes from here
+        Gx = k;
+        break;
+      }
       if (direct) {   // host-known: direct subtrees, up to kDirectLog levels per launch, no exchange
         const int nlev = std::min(kDirectLog, G - k);
         for (int i = 0; i < NL; ++i) {
@@ -1909,7 +1927,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     // ---- gather the last distributed level to rank 0, finish the top there ----
     {
       std::vector<u64> cnt(R);
-      for (int s = 0; s < R; ++s) cnt[s] = P.count(s, G);
+      for (int s = 0; s < R; ++s) cnt[s] = P.count(s, Gx);
       std::vector<const void*> sv;
       void* recv0 = nullptr;
       for (int i = 0; i < NL; ++i) {
@@ -1928,13 +1946,13 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         u32* in = cx->dist->tail_in.as<u32>();
         u32* bufs[2] = {cx->wa.as<u32>(), cx->wb.as<u32>()};
         int nb = 0;
-        u64 n = P.nk[G];
-        hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, cx->stream, &dh->cell[G], direct ? n : ~0ull);
+        u64 n = P.nk[Gx];
+        hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, cx->stream, &dh->cell[Gx], direct ? n : ~0ull);
         u64 bound = prev_total;
         bool tail_done = false;
-        for (int k = G; k < D; ++k) {
+        for (int k = Gx; k < D; ++k) {
           if (n <= u64(kTailMaxN) && cx->use_tail) {   // the rest in one launch
-            const u64* pc = k == G ? &dh->cell[G] : &h->count[kLayerSlot + k - 1];
+            const u64* pc = k == Gx ? &dh->cell[Gx] : &h->count[kLayerSlot + k - 1];
             if (cx->tail_levels(in, n, pc, k, D, node_base[i], h)) return dev_fail("tail levels");
             tail_done = true;
             break;
@@ -1966,8 +1984,8 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
           na.out = cx->nodes_out.as<uint2>() + node_base[i][k];
           na.count = &h->count[kLayerSlot + k];
           na.bound = bound;
-          na.prev_marks = k > G;
-          na.pcount = k == G ? &dh->cell[G] : &h->count[kLayerSlot + k - 1];
+          na.prev_marks = k > Gx;
+          na.pcount = k == Gx ? &dh->cell[Gx] : &h->count[kLayerSlot + k - 1];
           na.desc = cx->desc.as<u64>() + dcur[i];
           dcur[i] += (na.p + scan_tile(na.p) - 1) / scan_tile(na.p);
           na.ticket = &h->ticket[kLayerSlot + k];
@@ -1979,7 +1997,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         }
         if (!tail_done) hipLaunchKernelGGL(k_root, dim3(1), dim3(1), 0, cx->stream, in, h);
       }
-      hipLaunchKernelGGL(k_dist_final, dim3(1), dim3(1), 0, cx->stream, h, dh, G, D, int(tail));
+      hipLaunchKernelGGL(k_dist_final, dim3(1), dim3(1), 0, cx->stream, h, dh, Gx, D, int(tail));
       G_HIP(hipGetLastError());
       G_HIP(hipEventRecord(cx->ev_stop, cx->stream));
     }
@@ -2004,7 +2022,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     }
     const u64* f0 = d0.h_gathf;   // rank 0's vector
     info.root = u32(f0[1]);
-    for (int k = G; k < D; ++k) {
+    for (int k = Gx; k < D; ++k) {
       info.layer_size[k] = f0[4 + k];
       slice_off[k + 1][0] = 0;
       slice_cnt[k + 1][0] = f0[4 + k];
