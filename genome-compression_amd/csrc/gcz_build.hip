@@ -517,7 +517,8 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     tpre = tcount.as<u32>() + 16;
     auto count = [&](auto items) {
       hipLaunchKernelGGL((k_tile_count<decltype(items)::value>), gs, dim3(kBlock), 0, stream, knf, p, a.pcount, n,
-                         tpre, tcount.as<u32>());
+                         tpre, tcount.as<u32>(), static_cast<const u32*>(b2.nfl), static_cast<const u32*>(&d_hdr->nnf),
+                         bkt == 2 ? static_cast<const u32*>(&d_hdr->predup) : nullptr);
     };
     if (tile == u64(kTile)) count(std::integral_constant<int, kItems>{});
     else count(std::integral_constant<int, kItemsSmall>{});

@@ -908,11 +908,14 @@ struct NoPrefetch {
 // block t counts the first occurrences (zero marks) of tile t of T = kBlock * ITEMS positions,
 // and the last block to finish turns the counts into exclusive prefixes tpre[t] (and resets
 // the done counter for the next level).
+// (nfl / nnf / dup_flag: the flag scan's sparse path will run instead -- nothing to count)
 template <int ITEMS>
 __global__ __launch_bounds__(kBlock) void k_tile_count(const unsigned char* __restrict__ nf, u64 p,
                                                        const u64* prev_count, u64 n, u32* __restrict__ tpre,
-                                                       u32* __restrict__ done) {
+                                                       u32* __restrict__ done, const u32* __restrict__ nfl,
+                                                       const u32* __restrict__ nnf, const u32* __restrict__ dup_flag) {
   if (prev_count && level_direct(prev_count, n)) return;
+  if (nfl && !(dup_flag && *dup_flag != 0) && *nnf <= kNfListCap) return;
   constexpr u32 T = u32(kBlock) * ITEMS;
   __shared__ u32 s_red[kBlock / 64];
   __shared__ u32 s_last;
