@@ -363,44 +363,23 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
   __syncthreads();
   constexpr int PER = 16;   // codes per thread (RB <= 16 Ki)
   u32 fp[PER], rk[PER];
-  u64 pm[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const u32 i = u32(k) * kDThreads + tid;
     fp[k] = i < RB ? s_fp[i] : ~0u;
-    if (fpg && fl && i < RB) fpg[u64(b) * RB + i] = fp[k];
+    if (fpg && i < RB) fpg[u64(b) * RB + i] = fp[k];
     rk[k] = fl && fp[k] != ~0u ? atomicAdd(&s_cnt[fp[k] >> kDLog], 1u) : 0u;
-    pm[k] = __ballot(fp[k] != ~0u);
     if (pb) {
       const u32 h = (b << P.IB) | i;
       if (RB >= 64) {
-        if ((tid & 63) == 0 && i < RB) pb[h >> 6] = pm[k];
+        const u64 m = __ballot(fp[k] != ~0u);
+        if ((tid & 63) == 0 && i < RB) pb[h >> 6] = m;
       } else if (fp[k] != ~0u) {
         atomicOr(&pb[h >> 6], 1ull << (h & 63));
       }
     }
   }
-  if (!fl) {
-    // multi-rank phase A: the present codes' first positions, compacted in code order at
-    // fpg[b * RB ...] (k_dl_rfirst finds a code's entry by a popcount of the presence bits)
-    if (fpg) {
-      __shared__ u32 s_wc[PER * (kDThreads / 64)];
-      const int lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-      for (int k = 0; k < PER; ++k)
-        if (lane == 0) s_wc[k * (kDThreads / 64) + wave] = u32(__popcll(pm[k]));
-      __syncthreads();
-      u32 total;
-      const u32 e = block_excl(u32(tid) < PER * (kDThreads / 64) ? s_wc[tid] : 0u, s_tmp, &total);
-      if (u32(tid) < PER * (kDThreads / 64)) s_wc[tid] = e;
-      __syncthreads();
-      const u64 lt = (1ull << lane) - 1ull;
-#pragma unroll
-      for (int k = 0; k < PER; ++k)
-        if (fp[k] != ~0u) fpg[u64(b) * RB + s_wc[k * (kDThreads / 64) + wave] + u32(__popcll(pm[k] & lt))] = fp[k];
-    }
-    return;
-  }
+  if (!fl) return;
   __syncthreads();
   // exclusive scan of the nch + 1 counters (a few per thread, in order)
   const u32 n1 = P.nch + 1, per = (n1 + kDThreads - 1) / kDThreads, c0 = tid * per;
@@ -625,31 +604,13 @@ static __device__ __forceinline__ u64 bucket_word(const unsigned long long* __re
     for (int q = 0; q < r; ++q) x |= bucket_word(pbs + u64(q) * stride, b, P.IB, lw);
     s_low[lw] = x;
   }
-  // this rank's present codes (its own bitmap) index the compact first positions (k_dl_first):
-  // code order = (k, wave, lane), so an entry's index is a (k, wave) prefix plus a lane popcount
-  const unsigned long long* mine = pbs + u64(r) * stride;
-  u64 pm[PER];
+  u32 fp[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const u32 i = u32(k) * kDThreads + tid;
-    const u64 w = i < RB ? bucket_word(mine, b, P.IB, i >> 6) : 0ull;
-    pm[k] = __ballot(i < RB && ((w >> (i & 63)) & 1ull));
-    if (lane == 0) s_wc[k * (kDThreads / 64) + wave] = u32(__popcll(pm[k]));
+    fp[k] = i < RB ? fpg[u64(b) * RB + i] : ~0u;
   }
   __syncthreads();
-  {
-    u32 tp;
-    const u32 e = block_excl(u32(tid) < 16u * (kDThreads / 64) ? s_wc[tid] : 0u, s_tmp, &tp);
-    if (u32(tid) < 16u * (kDThreads / 64)) s_wc[tid] = e;
-    __syncthreads();
-  }
-  u32 fp[PER];
-  const u64 lt0 = (1ull << lane) - 1ull;
-#pragma unroll
-  for (int k = 0; k < PER; ++k)
-    fp[k] = (pm[k] >> lane) & 1ull ? fpg[u64(b) * RB + s_wc[k * (kDThreads / 64) + wave] + u32(__popcll(pm[k] & lt0))]
-                                   : ~0u;
-  __syncthreads();   // (s_wc is reused below)
   u32 rk[PER];
   u64 m[PER];
 #pragma unroll
