@@ -244,7 +244,8 @@ struct gcz_ctx {
   bool part_wave = false;    // ... and whose collapse inserts a one-key wave once (GCZ_PART_WAVE=1;
                              // measured 0.14 ms slower on tandem_3g2, off)
   gcz_host::DevBuf nf_list;  // ... those repeats' positions (k_bkt_dedupe2)
-  bool tile_count = true;    // large flag scans: tile prefixes counted ahead, no look-back (GCZ_TILE_COUNT=0)
+  bool tile_count = false;   // large flag scans: tile prefixes counted ahead, no look-back (GCZ_TILE_COUNT=1;
+                             // measured 0.75 ms slower on tandem_3g2, neutral on uniform_1g: off)
   gcz_host::DevBuf tcount;   // ... done counter (zeroed once: the last block resets it) + the prefixes
   bool bucket_now = true;    // this build (cleared after a bucket overflow: rebuild with the table)
   int dense_mode = 1;        // dense leaf level (gcz_dense.h): 0 off, 1 on large pure-ACGT inputs, 2 any size (GCZ_DENSE)
