@@ -651,9 +651,10 @@ static __device__ __forceinline__ u64 bucket_word(const unsigned long long* __re
 // G: per bucket, the local r-first rank of each r-first code in code order, at the bucket's
 // prefix; xv = the rank's exchange vector {r-first count, status, prefix of bucket 0, 1, ...}
 // (status: bit 0 a non-ACGT strand, bit 1 repetitive data; the host adds bit 2, failed).
-// A rank with few r-first codes (dl_rleaves_sparse: count * 16 < S) writes its leaves here,
-// by rank (random stores of few entries), instead of a pass over every position (k_dl_rleaves).
-__host__ __device__ __forceinline__ bool dl_rleaves_sparse(u64 count, u64 S) { return count * 16 < S; }
+// A rank with few r-first codes (dl_rleaves_sparse: count * 4 < S) writes its leaves here,
+// by rank (random stores of few entries), instead of a pass over every position (k_dl_rleaves;
+// at 1 Gbase over 8 ranks rank 1 first-holds ~0.7 M of its 10.9 M strands' codes: 41 us there).
+__host__ __device__ __forceinline__ bool dl_rleaves_sparse(u64 count, u64 S) { return count * 4 < S; }
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_gq(const u32* __restrict__ rfc, const u32* __restrict__ bcnt,
                                                      DensePlan P, const unsigned long long* __restrict__ rfb,
                                                      const u32* __restrict__ wpre, const u64* __restrict__ ucount,
