@@ -549,12 +549,13 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   return GCZ_OK;
 }
 
-int gcz_ctx::direct_levels(const u32* in, int k0, int nlev, const DirectPlan& dp, u32* out, Header* d_hdr) {
+int gcz_ctx::direct_levels(const u32* in, int k0, int nlev, const DirectPlan& dp, u32* out, Header* d_hdr,
+                           const DirectRemap& rm) {
   hipEvent_t e0{};
   prof_begin(KID_DIRECT, e0);
   const u64 blocks = (dp.n[0] + kDirectChunk - 1) / kDirectChunk;
   hipLaunchKernelGGL(k_direct_levels, dim3(unsigned(blocks)), dim3(kBlock), 0, stream, in, k0, nlev,
-                     nodes_out.as<uint2>(), dp, out, d_hdr);
+                     nodes_out.as<uint2>(), dp, out, d_hdr, rm);
   HIP_TRY(hipGetLastError());
   prof_end(KID_DIRECT, e0);
   return GCZ_OK;

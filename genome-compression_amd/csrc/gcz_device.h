@@ -2205,13 +2205,29 @@ struct DirectPlan {
   u32 id_off[GCZ_MAX_LAYERS];      // id of local pair 0 of each level (multi-rank: the rank's first position)
 };
 
+// Multi-rank (gcz_dist.hip): the input words of the first level may still hold the previous
+// exchanged level's LOCAL ids -- gid[local id] = the global id, or the local rank tagged
+// kLocalIdBit to which the rank's offset is added (k_dist_remap's translation, done here
+// on the load instead of in a pass of its own).
+constexpr u32 kLocalIdBit = 1u << 31;
+struct DirectRemap {
+  const u32* gid;   // null: the words are global
+  u32 off;
+};
 [[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_direct_levels(
     const u32* __restrict__ in, int k0, int nlev, uint2* __restrict__ nodes, DirectPlan dp, u32* __restrict__ words_out,
-    Header* __restrict__ hdr) {
+    Header* __restrict__ hdr, DirectRemap rm = {}) {
   __shared__ u32 buf[2][kDirectChunk];
   const u64 base0 = u64(blockIdx.x) * kDirectChunk;
   u32 c = u32(dp.n[0] - base0 < u64(kDirectChunk) ? dp.n[0] - base0 : u64(kDirectChunk));
-  for (u32 e = threadIdx.x; e < c; e += kBlock) buf[0][e] = in[base0 + e];
+  for (u32 e = threadIdx.x; e < c; e += kBlock) {
+    u32 w = in[base0 + e];
+    if (rm.gid) {
+      const u32 g = rm.gid[w & kIdx];
+      w = ((g & kLocalIdBit) ? (g & ~kLocalIdBit) + rm.off : g) | (w & kBits);
+    }
+    buf[0][e] = w;
+  }
   __syncthreads();
   int cur = 0;
   for (int i = 0; i < nlev; ++i) {

@@ -779,6 +779,22 @@ struct gcz_group {
   // owners hash-cons levels without the local dedupe in LDS buckets (GCZ_OWNER_BUCKETS=0: the table)
   bool owner_buckets = !std::getenv("GCZ_OWNER_BUCKETS") || std::atoi(std::getenv("GCZ_OWNER_BUCKETS")) != 0;
   bool owner_two_pass = !std::getenv("GCZ_OWNER_TWO") || std::atoi(std::getenv("GCZ_OWNER_TWO")) != 0;
+  // A node level's words keep their local ids after exchange() when defer_node_remap is set:
+  // the next level's direct subtrees translate them on their load (DirectRemap), else
+  // remap_level runs k_dist_remap.
+  bool defer_node_remap = false;
+  std::vector<u32> remap_off;   // each local rank's id offset of the last exchanged level
+  int remap_level(std::vector<RankLevel>& lv, const std::vector<u64>& nwords) {
+    for (int i = 0; i < int(ctx.size()); ++i) {
+      gcz_ctx* cx = ctx[i];
+      ProfScope ps_(cx, KID_REMAP);
+      hipLaunchKernelGGL(k_dist_remap, dim3(unsigned(std::max<u64>(1, (nwords[i] + kBlock - 1) / kBlock))),
+                         dim3(kBlock), 0, cx->stream, lv[i].w, nwords[i], lv[i].nf, lv[i].multi,
+                         cx->dist->gid.as<u32>(), cx->dist->gmul.as<unsigned char>(), remap_off[i], lv[i].gmark);
+      if (hipGetLastError() != hipSuccess) return dev_fail("remap");
+    }
+    return GCZ_OK;
+  }
   int exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, u32 key_bits, u32 child_bits,
                std::vector<u64>& c, std::vector<u64>& off, u64& total, u64* err_global, int* err_sym,
                int* ovf_bits, bool nolocal = false, bool lookahead = false, u64* next_hashed_out = nullptr);
@@ -1540,8 +1556,11 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
       leaf_identity[i] = lv[i].identity;
     }
   }
+  remap_off.assign(NL, 0);
+  for (int i = 0; i < NL; ++i) remap_off[i] = u32(off[rank[i]]);
   for (int i = 0; i < NL; ++i) {
     if (leaf_deferred || lv[i].identity) continue;   // rank 0's leaf ids are already global
+    if (!lv[i].leaves && defer_node_remap) continue;   // (the caller remaps: remap_level / direct levels)
     gcz_ctx* cx = ctx[i];
     gcz_dist_state& d = *cx->dist;
     const u64 nw = nwords[i];
@@ -1807,6 +1826,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     std::vector<u32*> cur_in(NL), cur_out(NL);
     for (int i = 0; i < NL; ++i) { cur_in[i] = ctx[i]->wa.as<u32>(); cur_out[i] = ctx[i]->wb.as<u32>(); }
     int Gx = G;   // the level whose input is gathered to rank 0
+    bool remap_pending = false;   // the last exchanged level's words still hold local ids
     for (int k = 0; k < G && !retry; ++k) {
       if (!direct && k >= P.Gh) {   // a small hash-consed level: rank 0 finishes from here
         Gx = k;
@@ -1823,9 +1843,12 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
             dp.layer_off[k + q] = node_base[i][k + q];
             dp.id_off[k + q] = u32(P.start(r, k + q + 1));
           }
-          if (ctx[i]->direct_levels(cur_in[i], k, nlev, dp, cur_out[i], ctx[i]->hdr.as<Header>()))
+          DirectRemap rm{};
+          if (remap_pending) rm = DirectRemap{ctx[i]->dist->gid.as<u32>(), remap_off[i]};
+          if (ctx[i]->direct_levels(cur_in[i], k, nlev, dp, cur_out[i], ctx[i]->hdr.as<Header>(), rm))
             return dev_fail("direct levels");
         }
+        remap_pending = false;
         for (int q = 0; q < nlev; ++q) {
           for (int s = 0; s < R; ++s) {
             slice_off[k + q + 1][s] = P.start(s, k + q + 1);
@@ -1906,8 +1929,10 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         for (int i = 0; i < NL; ++i) nw[i] = P.count(rank[i], k + 1);
         const u32 cb = std::max<u32>(1, bit_width(prev_total));
         u64 next_hashed = ~0ull;
+        defer_node_remap = true;
         const int rc = exchange(lv, nw, 2 * (cb + 2), cb, c, off, total, &err_global, &err_sym, &ovf, nolocal,
                                 nolocal && k + 1 < G, &next_hashed);
+        defer_node_remap = false;
         if (rc == kRetry) {
           allow_packed = false;
           retry = true;
@@ -1919,6 +1944,9 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
         // all unique, or (look-ahead) every pair of the next level holds a singleton
         direct = total == P.nk[k + 1] || next_hashed == 0;
         prev_total = total;
+        // the level's words to global ids: on the next direct subtrees' load, else a pass
+        if (direct && k + 1 < G) remap_pending = true;
+        else if (int rc2 = remap_level(lv, nw)) return rc2;
       }
       for (int i = 0; i < NL; ++i) std::swap(cur_in[i], cur_out[i]);
     }

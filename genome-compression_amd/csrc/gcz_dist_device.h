@@ -915,7 +915,7 @@ static __global__ __launch_bounds__(kBlock) void k_lookahead(const unsigned char
 // Such a unique goes straight to its place in the rank's output slice; gid keeps its local
 // rank tagged kLocalId (the global offset is known only after the count allgather and is
 // added where the id is used: k_dist_cvals, k_dist_remap).
-constexpr u32 kLocalId = 1u << 31;
+constexpr u32 kLocalId = kLocalIdBit;
 // nfl / nnf (optional): k_dist_flags' list of the positions not globally first; at most
 // kNfListCap of them: ranked without the look-back chain (SparseTile).
 template <class T>

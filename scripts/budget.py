@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Exchange budget of the multi-rank build from a virtual-rank bench line.
 
-    python scripts/budget.py <bench --virtual R json> [single-GPU ms] [--link GB/s ...]
+    python scripts/budget.py <bench --virtual R json> [single-GPU ms per Gbase] [--weak] [--link GB/s ...]
+
+(--weak: the line is a weak-scaled probe, e.g. uniform_8g over 8 ranks = 1 Gbase per rank; the
+projected speedup is then genome Gbase x single-GPU ms / T_R, else single-GPU ms / T_R.)
 
 A `bench.py --virtual R` line carries each rank's kernel time (`rank_kernel_ms`, the device
 work of that rank alone -- on R GPUs the ranks run concurrently) and its exchange log
@@ -22,6 +25,8 @@ import sys
 
 def main():
     args = sys.argv[1:]
+    weak = "--weak" in args
+    args = [a for a in args if a != "--weak"]
     links = [50.0, 100.0]
     if "--link" in args:
         i = args.index("--link")
@@ -55,8 +60,9 @@ def main():
         line = (f"B = {B:.0f} GB/s: kernels {kern:.3f} + transfers {xfer:.3f} + {n} collectives / {nsync} syncs "
                 f"{lat:.3f} = {T:.3f} ms")
         if single:
-            total_work = d["config"]["nbases"] / 1e9
-            line += f" -> {single * total_work / T if 'weak' in sys.argv[0] else single / T:.2f}x of {single} ms"
+            gb = d["config"]["nbases"] / 1e9
+            line += (f" -> {single * gb / T:.2f}x ({gb:.0f} Gbase at {single} ms per Gbase on one GPU)" if weak
+                     else f" -> {single / T:.2f}x of {single} ms on one GPU")
         print(line)
 
 
