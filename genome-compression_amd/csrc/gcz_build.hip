@@ -538,12 +538,13 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   // the next level's insert (or the tail) settles the repeats
   if (a.fused && (!a.fused_last || a.tail_settles)) return GCZ_OK;
   prof_begin(KID_RESOLVE_NODE, e0);
+  const dim3 gr(resolve_grid ? unsigned(std::min<u64>(gi.x, resolve_grid)) : gi.x);
   if (nt.packed)
-    hipLaunchKernelGGL((k_resolve_node<PackedTab>), gi, dim3(kBlock), 0, stream, a.words, p, nt.pt, knf, d_grp,
-                       a.pcount, n, a.count, a.hashed_next, a.gate, d_hdr, bkt);
+    hipLaunchKernelGGL((k_resolve_node<PackedTab>), gr, dim3(kBlock), 0, stream, a.words, p, nt.pt, knf, d_grp,
+                       a.pcount, n, a.count, a.hashed_next, a.gate, d_hdr, bkt, b2.nfl ? 1u : 0u);
   else
-    hipLaunchKernelGGL((k_resolve_node<WideTab>), gi, dim3(kBlock), 0, stream, a.words, p, nt.wt, knf, d_grp,
-                       a.pcount, n, a.count, a.hashed_next, a.gate, d_hdr, bkt);
+    hipLaunchKernelGGL((k_resolve_node<WideTab>), gr, dim3(kBlock), 0, stream, a.words, p, nt.wt, knf, d_grp,
+                       a.pcount, n, a.count, a.hashed_next, a.gate, d_hdr, bkt, b2.nfl ? 1u : 0u);
   HIP_TRY(hipGetLastError());
   prof_end(KID_RESOLVE_NODE, e0);
   return GCZ_OK;
@@ -1005,6 +1006,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   if (const char* t = std::getenv("GCZ_SPARSE_SCAN")) c->sparse_scan = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_PART_WAVE")) c->part_wave = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_TILE_COUNT")) c->tile_count = std::atoi(t) != 0;
+  if (const char* t = std::getenv("GCZ_RESOLVE_GRID")) c->resolve_grid = u32(std::strtoul(t, nullptr, 10));
   if (const char* t = std::getenv("GCZ_DENSE")) c->dense_mode = std::atoi(t);
   if (const char* t = std::getenv("GCZ_GRAPH")) c->use_graph = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_FUSED")) c->use_fused = std::atoi(t) != 0;

@@ -246,6 +246,8 @@ struct gcz_ctx {
   gcz_host::DevBuf nf_list;  // ... those repeats' positions (k_bkt_dedupe2)
   bool tile_count = false;   // large flag scans: tile prefixes counted ahead, no look-back (GCZ_TILE_COUNT=1;
                              // measured 0.75 ms slower on tandem_3g2, neutral on uniform_1g: off)
+  unsigned resolve_grid = 2048;   // node resolve: at most this many workgroups, striding (GCZ_RESOLVE_GRID;
+                                 // 0: p / 256; 2048 measured -32 us uniform_1g, -0.25 ms tandem_3g2)
   gcz_host::DevBuf tcount;   // ... done counter (zeroed once: the last block resets it) + the prefixes
   bool bucket_now = true;    // this build (cleared after a bucket overflow: rebuild with the table)
   int dense_mode = 1;        // dense leaf level (gcz_dense.h): 0 off, 1 on large pure-ACGT inputs, 2 any size (GCZ_DENSE)

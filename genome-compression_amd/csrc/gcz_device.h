@@ -1272,32 +1272,55 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
     const u64 base = st.base;
     if (blockIdx.x == 0 && tid == 0) *count_out = p - c;
     bool hashed = false;
+    // EB items' pairs and marks loaded before any is used (the ranks need no scan here)
+    constexpr int EB = ITEMS < 8 ? ITEMS : 8;
 #pragma unroll
-    for (int e = 0; e < ITEMS; ++e) {
-      const u32 k = u32(e) * kBlock + u32(tid);
-      const u64 j = base + k;
-      const bool is_first = j < p && !st.listed(k);
-      const u64 mask = __ballot(is_first);
-      const u64 nb = st.nb(k);
-      if (lane == 0) {
-        Group g;
-        g.mask = mask; g.prefix = u32(j - nb); g.pad = 0;
-        grp[(base >> 6) + u64(e) * 4 + wave] = g;
+    for (int e0 = 0; e0 < ITEMS; e0 += EB) {
+      u32 bl[EB], br[EB];
+      unsigned char bm[EB];
+#pragma unroll
+      for (int q = 0; q < EB; ++q) {
+        const u64 j = base + u64(e0 + q) * kBlock + tid;
+        bl[q] = br[q] = 0;
+        bm[q] = 0;
+        if (j < p) {
+          load_pair(in, n, j, bl[q], br[q]);
+          if (hashed_next) bm[q] = multi[j];
+        }
       }
-      unsigned char me = 0;
-      if (hashed_next && is_first) me = multi[j];
-      if (hashed_next) {
-        const bool rep = j < p && (!is_first || me != 0);
-        const bool partner = __shfl_xor(int(rep), 1, 64) != 0;
-        if ((lane & 1) == 0 && rep && (j + 1 < p ? partner : true)) hashed = true;
-      }
-      if (is_first) {
-        const u32 id = u32(j - nb);
-        u32 l, r, cl, cr, m, t;
-        load_pair(in, n, j, l, r);
-        node_canonical(l, r, cl, cr, m, t);
-        out[id] = make_uint2(cl, cr);
-        words[j] = make_word(id, m, t, ulw(l) == ulw(xf(r, 1, 0)));
+#pragma unroll
+      for (int q = 0; q < EB; ++q) {
+        const u32 k = u32(e0 + q) * kBlock + u32(tid);
+        const u64 j = base + k;
+        const bool listed = j < p && st.listed(k);
+        const bool is_first = j < p && !listed;
+        const u64 mask = __ballot(is_first);
+        const u64 nb = st.nb(k);
+        if (lane == 0) {
+          Group g;
+          g.mask = mask; g.prefix = u32(j - nb); g.pad = 0;
+          grp[(base >> 6) + u64(e0 + q) * 4 + wave] = g;
+        }
+        if (hashed_next) {
+          const bool rep = j < p && (!is_first || bm[q] != 0);
+          const bool partner = __shfl_xor(int(rep), 1, 64) != 0;
+          if ((lane & 1) == 0 && rep && (j + 1 < p ? partner : true)) hashed = true;
+        }
+        if (is_first) {
+          const u32 id = u32(j - nb);
+          u32 cl, cr, m, t;
+          node_canonical(bl[q], br[q], cl, cr, m, t);
+          out[id] = make_uint2(cl, cr);
+          words[j] = make_word(id, m, t, ulw(bl[q]) == ulw(xf(br[q], 1, 0)));
+        } else if (listed) {
+          // a repeat (the resolve's work, done here: k_resolve_node skips sparse levels): its
+          // word holds its key's first position f, whose id is f minus the repeats before it
+          const u32 w = words[j];
+          const u32 f = w & kIdx;
+          u32 before = 0;
+          for (u32 i = 0; i < c; ++i) before += nfl[i] < f ? 1u : 0u;
+          words[j] = (f - before) | (w & kBits);
+        }
       }
     }
     if (hashed_next) {
@@ -1395,20 +1418,25 @@ __global__ __launch_bounds__(kBlock) void k_resolve_node(u32* __restrict__ words
                                                         const Group* __restrict__ grp, const u64* prev_count,
                                                         u64 n, const u64* __restrict__ count,
                                                         const u32* __restrict__ hashed_next, u64* __restrict__ gate,
-                                                        const Header* __restrict__ hdr, u32 bkt) {
+                                                        const Header* __restrict__ hdr, u32 bkt,
+                                                        u32 sparse = 0) {
   if (gate && blockIdx.x == 0 && threadIdx.x == 0)
     *gate = (*count == p || (hashed_next && *hashed_next == 0)) ? p : ~0ull;
   if (level_direct(prev_count, n)) return;
-  const u64 j = u64(blockIdx.x) * kBlock + threadIdx.x;
-  if (j >= p || (nf[j] != kNfNot && nf[j] != kNfDup)) return;
-  const u32 w = words[j];
-  u64 key;
-  u32 q;
-  if (bkt && (bkt == 2 || hdr->predup == 0)) q = w & kIdx;    // bucketed insert: the word holds it
-  else T.read(w & kIdx, key, q);                // q = the key's first position
-  const Group h = grp[q >> 6];
-  const u32 id = h.prefix + u32(__popcll(h.mask & ((1ull << (q & 63)) - 1)));
-  words[j] = id | (w & kBits);
+  // the flag scan's sparse path resolved the level's few repeats itself
+  if (sparse && bkt == 2 && hdr->predup == 0 && hdr->nnf <= kNfListCap) return;
+  // (a grid smaller than p / kBlock strides: fewer empty workgroups on levels without repeats)
+  for (u64 j = u64(blockIdx.x) * kBlock + threadIdx.x; j < p; j += u64(gridDim.x) * kBlock) {
+    if (nf[j] != kNfNot && nf[j] != kNfDup) continue;
+    const u32 w = words[j];
+    u64 key;
+    u32 q;
+    if (bkt && (bkt == 2 || hdr->predup == 0)) q = w & kIdx;    // bucketed insert: the word holds it
+    else T.read(w & kIdx, key, q);                // q = the key's first position
+    const Group h = grp[q >> 6];
+    const u32 id = h.prefix + u32(__popcll(h.mask & ((1ull << (q & 63)) - 1)));
+    words[j] = id | (w & kBits);
+  }
 }
 
 // ---- bucketed node insert (non-repetitive data) ---------------------------------------
