@@ -2245,16 +2245,32 @@ struct DirectRemap {
 [[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_direct_levels(
     const u32* __restrict__ in, int k0, int nlev, uint2* __restrict__ nodes, DirectPlan dp, u32* __restrict__ words_out,
     Header* __restrict__ hdr, DirectRemap rm = {}) {
-  __shared__ u32 buf[2][kDirectChunk];
+  __shared__ __align__(16) u32 buf[2][kDirectChunk];
   const u64 base0 = u64(blockIdx.x) * kDirectChunk;
   u32 c = u32(dp.n[0] - base0 < u64(kDirectChunk) ? dp.n[0] - base0 : u64(kDirectChunk));
-  for (u32 e = threadIdx.x; e < c; e += kBlock) {
-    u32 w = in[base0 + e];
+  auto remap = [&](u32 w) {
+    const u32 g = rm.gid[w & kIdx];
+    return ((g & kLocalIdBit) ? (g & ~kLocalIdBit) + rm.off : g) | (w & kBits);
+  };
+  if (c == u32(kDirectChunk) && (reinterpret_cast<uintptr_t>(in) & 15u) == 0) {   // a whole chunk: every 16-B load in flight first
+    constexpr int V = kDirectChunk / 4 / kBlock;
+    uint4 v[V];
+    const uint4* src = reinterpret_cast<const uint4*>(in + base0);
+#pragma unroll
+    for (int q = 0; q < V; ++q) v[q] = src[q * kBlock + threadIdx.x];
     if (rm.gid) {
-      const u32 g = rm.gid[w & kIdx];
-      w = ((g & kLocalIdBit) ? (g & ~kLocalIdBit) + rm.off : g) | (w & kBits);
+#pragma unroll
+      for (int q = 0; q < V; ++q) {
+        v[q].x = remap(v[q].x);
+        v[q].y = remap(v[q].y);
+        v[q].z = remap(v[q].z);
+        v[q].w = remap(v[q].w);
+      }
     }
-    buf[0][e] = w;
+#pragma unroll
+    for (int q = 0; q < V; ++q) reinterpret_cast<uint4*>(buf[0])[q * kBlock + threadIdx.x] = v[q];
+  } else {
+    for (u32 e = threadIdx.x; e < c; e += kBlock) buf[0][e] = rm.gid ? remap(in[base0 + e]) : in[base0 + e];
   }
   __syncthreads();
   int cur = 0;
