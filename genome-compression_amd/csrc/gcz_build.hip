@@ -226,7 +226,7 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
   u32* tickets = reinterpret_cast<u32*>(sdesc + t_cnt + t_fb);
   const int first_bytes = int(((1u << P.IB) + P.nch + 1) * 4);
   if (first_bytes > 160 * 1024) return GCZ_OK;   // (never at L <= 12, S < 2^29)
-  const int scat_bytes = int((kDC + 3 * kDNBMax + 1 + 16) * 4);
+  const int scat_bytes = int((kDC + 3 * kDNBMax + 1 + 16 + kDC / 64) * 4);
   HIP_TRY(allow_lds(k_dl_scatter, scat_bytes));
   HIP_TRY(allow_lds(k_dl_first, first_bytes));
   hipEvent_t e0{};
@@ -303,7 +303,7 @@ int gcz_ctx::dense_phase_b(const LeafLevel& a, Header* d_hdr, const u32* gid, u6
   (void)d_hdr;
   const DensePlan& P = dl_plan;
   const int RBbytes = int((1u << P.IB) * 4);
-  const int words_bytes = int((kDC + 2 * kDNBMax + 1 + 16 + kDC / 32 + kDNBMax) * 4);
+  const int words_bytes = int((kDC + 2 * kDNBMax + 1 + 16 + kDC / 32 + kDC / 64) * 4);
   HIP_TRY(allow_lds(k_dl_ids, RBbytes));
   HIP_TRY(allow_lds(k_dl_words, words_bytes));
   hipEvent_t e0{};

@@ -152,17 +152,6 @@ static __device__ __forceinline__ void chunk_runs(const u32* __restrict__ offt, 
   }
 }
 
-// last bucket b with s_base[b] <= q (runs of zero length are skipped)
-static __device__ __forceinline__ u32 run_of(const u32* s_base, u32 NB, u32 q) {
-  u32 lo = 0, hi = NB - 1;
-  while (lo < hi) {
-    const u32 mid = (lo + hi + 1) >> 1;
-    if (s_base[mid] <= q) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
-}
-
 constexpr int kDBatch = 8;   // strands / records in flight per thread
 
 // L bytes of strand s from 4-B aligned loads (no LDS staging)
@@ -281,11 +270,24 @@ template <int L, bool kBases>
       s_stage[slot] = ((hc & imask) << kDLog) | q | (h[j] & kBits);   // (IB + 15 <= 29 bits, then m/t/v)
     }
   }
-  __syncthreads();
   const int lane = tid & 63, wave = tid >> 6;
-  for (u32 b = wave; b < P.NB; b += kDThreads / 64) {   // one run per wave step: contiguous stores
-    const u32 st = s_base[b], len = s_base[b + 1] - st, dst = s_dst[b];
-    for (u32 l = lane; l < len; l += 64) rec[dst + l] = s_stage[st + l];
+  // the staged runs written as flat 64-record groups (k_dl_words' walk), every lane busy
+  {
+    u32* s_gs = s_tmp + 16;   // group g -> the run holding record 64 g
+    const u32 nrec = s_base[P.NB];
+    for (u32 b = u32(tid); b < P.NB; b += kDThreads) {
+      const u32 s1 = s_base[b + 1];
+      for (u32 g = (s_base[b] + 63) >> 6; (g << 6) < s1; ++g) s_gs[g] = b;
+    }
+    __syncthreads();
+    const u32 ng = (nrec + 63) >> 6;
+    for (u32 g = wave; g < ng; g += kDThreads / 64) {
+      const u32 k = (g << 6) + u32(lane);
+      if (k >= nrec) continue;
+      u32 b = s_gs[g];
+      while (s_base[b + 1] <= k) ++b;
+      rec[s_dst[b] + (k - s_base[b])] = s_stage[k];
+    }
   }
 }
 
@@ -491,8 +493,7 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
   u32* s_dst = s_base + kDNBMax + 1; // NB
   u32* s_tmp = s_dst + kDNBMax;      // 16
   u32* s_fb = s_tmp + 16;            // kDC / 32 first-occurrence bits of the chunk
-  u32* s_ex = s_fb + kDC / 32;       // NB + 1: exclusive prefix of the runs' records past the
-                                     // first 64 (skewed data: hot codes), walked by the block
+  u32* s_ex = s_fb + kDC / 32;       // kDC / 64: the run of each 64-record group's first record
   const int tid = threadIdx.x;
   const u32 ch = blockIdx.x;
   const u64 c0 = u64(ch) * kDC;
@@ -514,44 +515,41 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
       leaves_out[wr & kIdx] = code2_leaf((h * P.Kinv) & P.cmask, P.L);
     }
   };
-  constexpr int RW = 8;   // runs per wave step (2 loads each in flight per lane)
-  for (u32 b0 = wave; b0 < P.NB; b0 += (kDThreads / 64) * RW) {
-    u32 x[RW], w[RW], dst[RW], len[RW];
-#pragma unroll
-    for (int j = 0; j < RW; ++j) {
-      const u32 b = b0 + u32(j) * (kDThreads / 64);
-      len[j] = 0; dst[j] = 0; x[j] = 0; w[j] = 0;
-      if (b < P.NB) {
-        dst[j] = s_dst[b];
-        len[j] = s_base[b + 1] - s_base[b];
-      }
-      if (u32(lane) < len[j]) {
-        x[j] = rec[dst[j] + lane];
-        w[j] = idrec[dst[j] + lane];
-      }
+  // the chunk's records walked as one flat sequence of 64-record groups over the runs (every
+  // lane busy: a group spans 2-3 runs of ~32 records), a group's first run looked up in LDS
+  {
+    u32* s_gs = s_ex;   // group g -> the run holding record 64 g
+    const u32 nrec = s_base[P.NB];
+    for (u32 b = u32(tid); b < P.NB; b += kDThreads) {
+      const u32 s1 = s_base[b + 1];
+      for (u32 g = (s_base[b] + 63) >> 6; (g << 6) < s1; ++g) s_gs[g] = b;
     }
-#pragma unroll
-    for (int j = 0; j < RW; ++j) {
-      const u32 b = b0 + u32(j) * (kDThreads / 64);
-      if (u32(lane) < len[j]) place(b, x[j], w[j]);
-    }
-  }
-  {   // the records past the first 64 of each run, flat over the block (none on uniform data)
-    const u32 b = u32(tid);
-    const u32 len = b < P.NB ? s_base[b + 1] - s_base[b] : 0u;
-    u32 total;
-    const u32 ex = block_excl(len > 64u ? len - 64u : 0u, s_tmp, &total);
-    if (b < P.NB) s_ex[b] = ex;
-    if (b == 0) s_ex[P.NB] = total;
     __syncthreads();
-    for (u32 k = u32(tid); k < total; k += kDThreads) {
-      const u32 rb = run_of(s_ex, P.NB, k);
-      const u32 l = 64u + (k - s_ex[rb]), at = s_dst[rb] + l;
-      place(rb, rec[at], idrec[at]);
+    const u32 ng = (nrec + 63) >> 6;
+    constexpr int GW = 8;   // groups per wave step (2 loads each in flight per lane)
+    for (u32 g0 = wave; g0 < ng; g0 += (kDThreads / 64) * GW) {
+      u32 x[GW], w[GW], bq[GW];
+#pragma unroll
+      for (int q = 0; q < GW; ++q) {
+        const u32 g = g0 + u32(q) * (kDThreads / 64), k = (g << 6) + u32(lane);
+        bq[q] = ~0u;
+        x[q] = w[q] = 0;
+        if (g < ng && k < nrec) {
+          u32 b = s_gs[g];
+          while (s_base[b + 1] <= k) ++b;
+          const u32 at = s_dst[b] + (k - s_base[b]);
+          x[q] = rec[at];
+          w[q] = idrec[at];
+          bq[q] = b;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < GW; ++q)
+        if (bq[q] != ~0u) place(bq[q], x[q], w[q]);
     }
+    __syncthreads();
+    for (u32 q = tid; q < n; q += kDThreads) words[c0 + q] = s_w[q];
   }
-  __syncthreads();
-  for (u32 q = tid; q < n; q += kDThreads) words[c0 + q] = s_w[q];
 }
 
 // ---- multi-rank build (gcz_dist.hip): the leaf level of one rank ----------------
