@@ -2001,6 +2001,10 @@ constexpr u32 kColSlots = 8192;   // its LDS table (load <= 1/2), in the part's 
   }
   const u32 sh2 = bp.K - bp.b1 - bp.b2;   // key bits kept in the final record
   const u64 keep = sh2 >= 64 ? ~0ull : (1ull << sh2) - 1;
+  __shared__ u32 s_gs[kFineCap / 64];   // the run holding record 64 g
+  for (u32 t = threadIdx.x; t < nsc; t += kBktThreads)
+    for (u32 g = (s_pre[t] + 63) >> 6; (g << 6) < s_pre[t + 1]; ++g) s_gs[g] = t;
+  __syncthreads();
   u64 r[kFineItems];
   u32 slot[kFineItems];
 #pragma unroll
@@ -2008,7 +2012,9 @@ constexpr u32 kColSlots = 8192;   // its LDS table (load <= 1/2), in the part's 
     const u32 i = u32(e) * kBktThreads + threadIdx.x;
     slot[e] = ~0u;
     if (i >= total) continue;
-    u32 s = 0, hi = nsc - 1;   // run of record i: the last s with s_pre[s] <= i
+    // run of record i: the last s with s_pre[s] <= i, between the runs of its group's first
+    // record and the next group's (one or two steps unless the runs there are short)
+    u32 s = s_gs[i >> 6], hi = (i >> 6) + 1 < ((total + 63) >> 6) ? s_gs[(i >> 6) + 1] : nsc - 1;
     while (s < hi) {
       const u32 mid = (s + hi + 1) >> 1;
       if (s_pre[mid] <= i) s = mid;
@@ -2160,6 +2166,10 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
     }
     return;
   }
+  __shared__ u32 s_gs[(kBktCap + 63) / 64];   // the slice holding record 64 g
+  for (u32 t = threadIdx.x; t < ns; t += kBktThreads)
+    for (u32 g = (s_pre[t] + 63) >> 6; (g << 6) < s_pre[t + 1]; ++g) s_gs[g] = t;
+  __syncthreads();
   u64 key[kBktCapItems];
   u32 pos[kBktCapItems], slot[kBktCapItems];
 #pragma unroll
@@ -2167,7 +2177,9 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
     const u32 i = u32(e) * kBktThreads + threadIdx.x;
     key[e] = kEmpty;
     if (i >= total) continue;
-    u32 lo = 0, hi = ns - 1;   // slice of record i: the last s with s_pre[s] <= i
+    // slice of record i: the last s with s_pre[s] <= i, between the slices of its group's
+    // first record and the next group's
+    u32 lo = s_gs[i >> 6], hi = (i >> 6) + 1 < ((total + 63) >> 6) ? s_gs[(i >> 6) + 1] : ns - 1;
     while (lo < hi) {
       const u32 mid = (lo + hi + 1) >> 1;
       if (s_pre[mid] <= i) lo = mid;
