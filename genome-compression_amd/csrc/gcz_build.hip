@@ -240,10 +240,9 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
                           d_hdr);
   HIP_TRY(hipGetLastError());
   if (check) {   // single device: fall back at once (the multi-rank caller checks every rank's flag)
-    u32 dfail = 0;
-    HIP_TRY(hipMemcpyAsync(&dfail, &d_hdr->dense_fail, 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(&h_hdr->dense_fail, &d_hdr->dense_fail, 4, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
-    if (dfail) {
+    if (h_hdr->dense_fail) {
       prof_end(KID_DL_PACK, e0);
       return GCZ_OK;
     }
@@ -551,12 +550,12 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
 }
 
 int gcz_ctx::direct_levels(const u32* in, int k0, int nlev, const DirectPlan& dp, u32* out, Header* d_hdr,
-                           const DirectRemap& rm) {
+                           const DirectRemap& rm, const u64* guard, u64 expect) {
   hipEvent_t e0{};
   prof_begin(KID_DIRECT, e0);
   const u64 blocks = (dp.n[0] + kDirectChunk - 1) / kDirectChunk;
   hipLaunchKernelGGL(k_direct_levels, dim3(unsigned(blocks)), dim3(kBlock), 0, stream, in, k0, nlev,
-                     nodes_out.as<uint2>(), dp, out, d_hdr, rm);
+                     nodes_out.as<uint2>(), dp, out, d_hdr, rm, guard, expect);
   HIP_TRY(hipGetLastError());
   prof_end(KID_DIRECT, e0);
   return GCZ_OK;
@@ -853,13 +852,33 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
         // a look at the device after layers 0 and 1: once a gate is open every later
         // level is direct and runs as direct subtrees (saves ~4 launches per level)
         if (k <= 1 && use_direct && n >= kDirectCheckMin && k + 1 >= seg_d) {   // (a host round trip: only where levels are big)
-          u64 g = 0;
-          u32 pd = 0;
-          HIP_TRY(hipMemcpyAsync(&g, &d_hdr->gate[k], 8, hipMemcpyDeviceToHost, stream));
-          HIP_TRY(hipMemcpyAsync(&pd, &d_hdr->predup, 4, hipMemcpyDeviceToHost, stream));
+          // the next direct step is launched before the round trip, guarded on the device by
+          // the gate (all unique data: the wait overlaps it; otherwise it exits at once)
+          DirectPlan sdp{};
+          int snlev = 0;
+          u64 sm = n;
+          if (k + 1 < D && (n > u64(kTailMaxN) || !use_tail)) {
+            sdp.n[0] = n;
+            while (snlev < kDirectLog && k + 1 + snlev < D && (sm > u64(kTailMaxN) || !use_tail)) {
+              sdp.layer_off[k + 1 + snlev] = layer_off[k + 1 + snlev];
+              sm = pk[k + 1 + snlev];
+              sdp.n[++snlev] = sm;
+            }
+            if (snlev > 0 && (rc = direct_levels(in, k + 1, snlev, sdp, outw, d_hdr, DirectRemap{}, &d_hdr->gate[k], n)))
+              return rc;
+          }
+          HIP_TRY(hipMemcpyAsync(&h_hdr->gate[k], &d_hdr->gate[k], 8, hipMemcpyDeviceToHost, stream));
+          HIP_TRY(hipMemcpyAsync(&h_hdr->predup, &d_hdr->predup, 4, hipMemcpyDeviceToHost, stream));
           HIP_TRY(hipStreamSynchronize(stream));
-          direct = g == n;
-          table_only = pd != 0;   // repetitive data: later levels skip the single-pass bucket launches
+          direct = h_hdr->gate[k] == n;
+          table_only = h_hdr->predup != 0;   // repetitive data: later levels skip the single-pass bucket launches
+          if (direct && snlev > 0) {   // the speculative step ran: continue after it
+            prev_regular = false;
+            std::swap(in, outw);
+            n = sm;
+            bound = sm;
+            k += snlev;
+          }
         }
       }
       if (!tail_done) {   // (the tail sums the statistics itself)

@@ -369,7 +369,8 @@ struct gcz_ctx {
   int node_level(const gcz_host::NodeLevel& a, gcz_dev::Header* d_hdr);
   // Known-direct levels k0..k0+nlev-1 in one launch (gcz_device.h k_direct_levels).
   int direct_levels(const gcz_host::u32* in, int k0, int nlev, const gcz_dev::DirectPlan& dp, gcz_host::u32* out,
-                    gcz_dev::Header* d_hdr, const gcz_dev::DirectRemap& rm = {});
+                    gcz_dev::Header* d_hdr, const gcz_dev::DirectRemap& rm = {},
+                    const gcz_host::u64* guard = nullptr, gcz_host::u64 expect = 0);
   // Levels k0..D-1 in one launch (n0 <= kTailMaxN input words); writes counts and the root
   // (and, given the statistics shards, sums them: the build's last launch).
   int tail_levels(const gcz_host::u32* in, gcz_host::u64 n0, const gcz_host::u64* pcount, int k0, int D,

@@ -2256,7 +2256,10 @@ struct DirectRemap {
 };
 [[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_direct_levels(
     const u32* __restrict__ in, int k0, int nlev, uint2* __restrict__ nodes, DirectPlan dp, u32* __restrict__ words_out,
-    Header* __restrict__ hdr, DirectRemap rm = {}) {
+    Header* __restrict__ hdr, DirectRemap rm = {}, const u64* guard = nullptr, u64 expect = 0) {
+  // guard: a speculative launch (gcz_build.hip, ahead of the host's look at the gate) runs only
+  // when the gate says the level is direct
+  if (guard && *guard != expect) return;
   __shared__ __align__(16) u32 buf[2][kDirectChunk];
   const u64 base0 = u64(blockIdx.x) * kDirectChunk;
   u32 c = u32(dp.n[0] - base0 < u64(kDirectChunk) ? dp.n[0] - base0 : u64(kDirectChunk));
