@@ -239,13 +239,10 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
     launch_dl_pack<false>(int(L), dim3(P.nch), stream, nullptr, a.leaves, P, dl_pw.as<u32>(), dl_cnt.as<u32>(),
                           d_hdr);
   HIP_TRY(hipGetLastError());
-  if (check) {   // single device: fall back at once (the multi-rank caller checks every rank's flag)
+  if (check) {   // single device: the pure-ACGT verdict, read after the scatter is queued (below)
+    if (!ev_dfail) HIP_TRY(hipEventCreateWithFlags(&ev_dfail, hipEventDisableTiming));
     HIP_TRY(hipMemcpyAsync(&h_hdr->dense_fail, &d_hdr->dense_fail, 4, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    if (h_hdr->dense_fail) {
-      prof_end(KID_DL_PACK, e0);
-      return GCZ_OK;
-    }
+    HIP_TRY(hipEventRecord(ev_dfail, stream));
   }
   // repetitive data? (the node inserts' LDS pre-dedupe): in-block repeats of a sample's
   // hashed codes (equal codes <=> equal keys)
@@ -258,7 +255,6 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
   hipLaunchKernelGGL(k_dup_decide, dim3(1), dim3(1), 0, stream, d_hdr, ip, u32(predup_mode));
   HIP_TRY(hipGetLastError());
   prof_end(KID_DL_PACK, e0);
-  *used = true;
   prof_begin(KID_DL_SCAN, e0);
   hipLaunchKernelGGL(k_scan_excl<ScanU32>, dim3(unsigned(t_cnt)), dim3(kScanThreads), 0, stream,
                      ScanU32{dl_cnt.as<u32>(), ncnt}, ncnt + 1, dl_off.as<u32>(), sdesc, &tickets[0],
@@ -272,6 +268,16 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
                      dl_offt.as<u32>(), dl_rec.as<u32>());
   HIP_TRY(hipGetLastError());
   prof_end(KID_DL_SCATTER, e0);
+  if (check) {
+    // the host waits for the pack's verdict only, while the scan and scatter (harmless on a
+    // failed pack: rejected strands carry no record) keep the device busy
+    HIP_TRY(hipEventSynchronize(ev_dfail));
+    if (h_hdr->dense_fail) {   // the hash-table leaf level follows: no repetitive-data verdict from here
+      HIP_TRY(hipMemsetAsync(&d_hdr->predup, 0, sizeof(d_hdr->predup), stream));
+      return GCZ_OK;
+    }
+  }
+  *used = true;
   prof_begin(KID_DL_FIRST, e0);
   if (list && (1u << P.IB) < 64) HIP_TRY(hipMemsetAsync(dl_pb.ptr, 0, (ncodes / 64 + 1) * 8, stream));
   // (multi-rank, list: first positions, the presence bitmap and the status words only -- the
@@ -1058,6 +1064,7 @@ void gcz_ctx_destroy(gcz_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
+  if (c->ev_dfail) (void)hipEventDestroy(c->ev_dfail);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
   if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);

@@ -282,6 +282,7 @@ struct gcz_ctx {
   double prof_ms[gcz_host::KID_COUNT] = {};
   std::vector<float> prof_trace;   // (kid, start ms after ev_start, duration ms) per profiled scope
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+  hipEvent_t ev_dfail = nullptr;   // the dense pack's verdict copied to the pinned header
   gcz_dist_state* dist = nullptr;   // multi-rank build state (gcz_dist.hip)
   gcz_sort_state* sortst = nullptr; // device sort / .dag writer state (gcz_sort.hip)
   gcz_ingest_state* ingest = nullptr; // device FASTA ingest state (gcz_ingest.hip)
