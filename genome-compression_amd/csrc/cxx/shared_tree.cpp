@@ -523,7 +523,15 @@ void shared_tree::build_from_gpu() {
   }
   {
     PhaseTimer t2{"fetch-copy"};
-    check_build(gcz_fetch_host(ctx, reinterpret_cast<std::uint64_t*>(leaves.data()), outs.data()), ctx);
+    // a large tree's frequency-sort buffers are allocated beside the copy (compress sorts next;
+    // its first device sort at 1 Gbase otherwise starts with ~40 ms of allocation)
+    std::uint64_t total = info.n_leaves;
+    for (int k = 0; k < info.n_layers; ++k) total += info.layer_size[k];
+    std::thread reserve;
+    if (total >= (std::uint64_t(1) << 22)) reserve = std::thread([ctx] { (void)gcz_sort_reserve(ctx); });
+    const int rc = gcz_fetch_host(ctx, reinterpret_cast<std::uint64_t*>(leaves.data()), outs.data());
+    if (reserve.joinable()) reserve.join();
+    check_build(rc, ctx);
   }
   // what the pre-faulted pool did not hold goes back on a side thread (unmapping ~0.6 GB of
   // present pages takes ~25 ms)

@@ -1196,6 +1196,26 @@ namespace {
 constexpr u64 kRingChunk = u64(16) << 20;
 constexpr int kRingSlots = 4;
 
+// A small DAG (one ring slot) is gathered into the pinned ring by a kernel of this library's
+// own instead of one runtime D2H copy per layer: the runtime's first device-to-host copy in a
+// process pays a one-time start-up of its copy path (~17 ms measured on merged's 1.2 MB tree,
+// profiles/r03 and r04 compress_e2e), a kernel launch from an already loaded module does not.
+// Stores go to host memory directly (vector stores; the ring is pinned and device-visible).
+constexpr int kGatherMax = 64;
+struct HostGather {
+  const u64* src[kGatherMax];
+  u64 off[kGatherMax];   // destination word offset in the ring
+  u64 len[kGatherMax];   // words (pieces are whole u64 / uint2 arrays)
+  u32 n;
+};
+static __global__ __launch_bounds__(256) void k_gather_host(HostGather g, u64* __restrict__ ring) {
+  const u32 i = blockIdx.y;
+  if (i >= g.n) return;
+  const u64* __restrict__ s = g.src[i];
+  u64* d = ring + g.off[i];
+  for (u64 k = u64(blockIdx.x) * 256 + threadIdx.x; k < g.len[i]; k += u64(gridDim.x) * 256) d[k] = s[k];
+}
+
 struct CopyPool {   // T - 1 workers + the calling thread copy one chunk's slices, then meet
   int T;
   std::vector<std::thread> th;
@@ -1303,10 +1323,26 @@ int gcz_fetch_host(gcz_ctx* c, uint64_t* leaves_out, uint32_t* const* layers_out
   CopyPool pool(total >= (u64(8) << 20) ? int(std::min<unsigned>(8, std::max(1u, hc))) : 1);
   if (total <= kRingChunk) {   // one D2H batch, then the host copies
     u64 at = 0;
-    for (const Piece& p : pieces) {
-      if (hipMemcpyAsync(c->h_ring + at, p.src, p.len, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
-        return GCZ_ERR_DEVICE;
-      at += p.len;
+    if (pieces.size() <= size_t(kGatherMax)) {   // one gather kernel into the ring (see k_gather_host)
+      HostGather g{};
+      u64 mx = 0;
+      for (const Piece& p : pieces) {
+        g.src[g.n] = reinterpret_cast<const u64*>(p.src);
+        g.off[g.n] = at / 8;
+        g.len[g.n] = p.len / 8;
+        mx = std::max(mx, p.len / 8);
+        ++g.n;
+        at += p.len;
+      }
+      const dim3 grid(unsigned(std::min<u64>(64, (mx + 255) / 256)), g.n);
+      hipLaunchKernelGGL(k_gather_host, grid, dim3(256), 0, c->stream, g, reinterpret_cast<u64*>(c->h_ring));
+      if (hipGetLastError() != hipSuccess) return GCZ_ERR_DEVICE;
+    } else {
+      for (const Piece& p : pieces) {
+        if (hipMemcpyAsync(c->h_ring + at, p.src, p.len, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+          return GCZ_ERR_DEVICE;
+        at += p.len;
+      }
     }
     if (hipStreamSynchronize(c->stream) != hipSuccess) return GCZ_ERR_DEVICE;
     at = 0;

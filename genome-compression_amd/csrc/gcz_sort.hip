@@ -28,6 +28,7 @@ using namespace gcz_dev;
 using namespace gcz_host;
 
 struct gcz_sort_state {
+  bool warm = false;   // k_sort_warm launched (gcz_sort_reserve)
   DevBuf cnt, keys, keys2, vals, vals2, newpos, mm, acc, dag, nodes2, leaves2, dw1, dw2, text;
   DevBuf hmat, hoff, hrec, desc;   // partitioned histogram; scan descriptors
   DevBuf hslot, hval, hbs;         // its records' positions per word, new children, bucket starts
@@ -860,12 +861,68 @@ u32 host_ptr_bytes(u32 w) {
     if (e_ != hipSuccess) return c->fail(GCZ_ERR_DEVICE, #x, hipGetErrorString(e_));     \
   } while (0)
 
+static __global__ void k_sort_warm() {}
+
 extern "C" {
 
-int gcz_sort_device(gcz_ctx* c) {
+// The sort's device buffers for the current tree, allocated ahead (the drop-in reserves them on
+// a side thread while the tree is fetched: a first sort at 1 Gbase otherwise pays ~40 ms of
+// allocation, profiles/r04/compress_e2e.txt); gcz_sort_device calls it too (then a no-op).
+int gcz_sort_reserve(gcz_ctx* c) {
   if (!c || c->info.status != GCZ_OK || c->info.n_layers < 1) return GCZ_ERR_ARG;
   S_HIP(hipSetDevice(c->device));
   if (!c->sortst) c->sortst = new gcz_sort_state();
+  gcz_sort_state& s = *c->sortst;
+  const int D = c->info.n_layers;
+  const u64 nl = c->info.n_leaves;
+  std::vector<u64> n_of(D), coff(D + 1, 0);
+  for (int cl = 0; cl < D; ++cl) {
+    n_of[cl] = cl == 0 ? nl : c->info.layer_size[cl - 1];
+    coff[cl + 1] = coff[cl] + n_of[cl];
+  }
+  u64 nmax = 0, nwmax = 0, matmax = 0;
+  std::vector<u32> hnb(D, 0);
+  for (int cl = 0; cl < D; ++cl) {
+    nmax = std::max(nmax, n_of[cl]);
+    const u64 nw = 2 * c->info.layer_size[cl];
+    const u64 nb = (n_of[cl] + (1ull << kHB) - 1) >> kHB;
+    if (nw >= (1ull << 20) && nw >= 4 * n_of[cl] && nb >= 1 && nb <= kHMaxBuckets) {   // (as gcz_sort_device)
+      hnb[cl] = u32(nb);
+      nwmax = std::max(nwmax, nw);
+      matmax = std::max(matmax, nb * ((nw + kHChunk - 1) / kHChunk) + 1);
+    }
+  }
+  int scl = -1;
+  for (int cl = 0; cl < D; ++cl)
+    if (hnb[cl] && (scl < 0 || c->info.layer_size[cl] > c->info.layer_size[scl])) scl = cl;
+  matmax = std::max(matmax, 256 * ((nmax + kCsTile - 1) / kCsTile) + 1);
+  const u64 tilemax = scan_tiles(matmax);
+  const u64 N = c->layer_off[D];
+  int rc;
+  if ((rc = c->ensure(s.cnt, coff[D] * 4 + 16)) || (rc = c->ensure(s.newpos, coff[D] * 4 + 16)) ||
+      (rc = c->ensure(s.keys, nmax * 4 + 16)) || (rc = c->ensure(s.keys2, nmax * 4 + 16)) ||
+      (rc = c->ensure(s.vals, nmax * 4 + 16)) || (rc = c->ensure(s.vals2, nmax * 4 + 16)) ||
+      (rc = c->ensure(s.mm, size_t(D) * 8 + 16)) || (rc = c->ensure(s.nodes2, N * 8 + 16)) ||
+      (rc = c->ensure(s.leaves2, nl * 8 + 16)) || (rc = c->ensure(s.hmat, matmax * 4 + 16)) ||
+      (rc = c->ensure(s.hoff, matmax * 4 + 16)) || (rc = c->ensure(s.hrec, nwmax * 2 + 16)) ||
+      (rc = c->ensure(s.desc, tilemax * 8 + 16)))
+    return rc;
+  if ((rc = c->ensure(s.hpart, size_t(2048) * GCZ_MAX_LAYERS * 8 + 16))) return rc;
+  if (scl >= 0 && ((rc = c->ensure(s.hslot, 2 * c->info.layer_size[scl] * 4 + 16)) ||
+                   (rc = c->ensure(s.hval, 2 * c->info.layer_size[scl] * 4 + 16)) ||
+                   (rc = c->ensure(s.hbs, (u64(hnb[scl]) + 1) * 4 + 16))))
+    return rc;
+  if (!s.h_mm) S_HIP(hipHostMalloc((void**)&s.h_mm, size_t(GCZ_MAX_LAYERS) * 8, hipHostMallocDefault));
+  if (!s.warm) {   // this file's code object loaded now, not at the first sort's first launch
+    hipLaunchKernelGGL(k_sort_warm, dim3(1), dim3(64), 0, c->stream);
+    S_HIP(hipGetLastError());
+    s.warm = true;
+  }
+  return GCZ_OK;
+}
+
+int gcz_sort_device(gcz_ctx* c) {
+  if (int rc = gcz_sort_reserve(c)) return rc;
   gcz_sort_state& s = *c->sortst;
   const int D = c->info.n_layers;
   const u64 nl = c->info.n_leaves;
@@ -875,7 +932,7 @@ int gcz_sort_device(gcz_ctx* c) {
     n_of[cl] = cl == 0 ? nl : c->info.layer_size[cl - 1];
     coff[cl + 1] = coff[cl] + n_of[cl];
   }
-  u64 nmax = 0, nwmax = 0, matmax = 0, tilemax = 0;
+  u64 nmax = 0, nwmax = 0, matmax = 0;
   // per parent layer: partitioned histogram (nb buckets x G chunks) or global atomics (nb = 0)
   std::vector<u32> hnb(D, 0);
   std::vector<u64> hG(D, 0);
@@ -900,23 +957,7 @@ int gcz_sort_device(gcz_ctx* c) {
     if (hnb[cl] && (scl < 0 || c->info.layer_size[cl] > c->info.layer_size[scl])) scl = cl;
   const u64 cs_tiles = (nmax + kCsTile - 1) / kCsTile;
   matmax = std::max(matmax, 256 * cs_tiles + 1);
-  tilemax = scan_tiles(matmax);
-  const u64 N = c->layer_off[D];
-  int rc;
-  if ((rc = c->ensure(s.cnt, coff[D] * 4 + 16)) || (rc = c->ensure(s.newpos, coff[D] * 4 + 16)) ||
-      (rc = c->ensure(s.keys, nmax * 4 + 16)) || (rc = c->ensure(s.keys2, nmax * 4 + 16)) ||
-      (rc = c->ensure(s.vals, nmax * 4 + 16)) || (rc = c->ensure(s.vals2, nmax * 4 + 16)) ||
-      (rc = c->ensure(s.mm, size_t(D) * 8 + 16)) || (rc = c->ensure(s.nodes2, N * 8 + 16)) ||
-      (rc = c->ensure(s.leaves2, nl * 8 + 16)) || (rc = c->ensure(s.hmat, matmax * 4 + 16)) ||
-      (rc = c->ensure(s.hoff, matmax * 4 + 16)) || (rc = c->ensure(s.hrec, nwmax * 2 + 16)) ||
-      (rc = c->ensure(s.desc, tilemax * 8 + 16)))
-    return rc;
-  if ((rc = c->ensure(s.hpart, size_t(2048) * GCZ_MAX_LAYERS * 8 + 16))) return rc;
-  if (scl >= 0 && ((rc = c->ensure(s.hslot, 2 * c->info.layer_size[scl] * 4 + 16)) ||
-                   (rc = c->ensure(s.hval, 2 * c->info.layer_size[scl] * 4 + 16)) ||
-                   (rc = c->ensure(s.hbs, (u64(hnb[scl]) + 1) * 4 + 16))))
-    return rc;
-  if (!s.h_mm) S_HIP(hipHostMalloc((void**)&s.h_mm, size_t(GCZ_MAX_LAYERS) * 8, hipHostMallocDefault));
+  int rc;   // (the buffers: gcz_sort_reserve, same sizes)
   S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_hbucket), hipFuncAttributeMaxDynamicSharedMemorySize,
                             int((1u << kHB) * 4)));
   S_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_hremap), hipFuncAttributeMaxDynamicSharedMemorySize,

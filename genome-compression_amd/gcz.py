@@ -104,6 +104,7 @@ _SIGS = {
     "gcz_synth_fill": (None, [_P, ctypes.c_int, _U64, _U64, _U64]),
     "gcz_synth_default_seed": (_U64, []),
     "gcz_sort_device": (ctypes.c_int, [_P]),
+    "gcz_sort_reserve": (ctypes.c_int, [_P]),
     "gcz_bytes_device": (ctypes.c_int, [_P, ctypes.POINTER(_U64)]),
     "gcz_serialize_device": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
     "gcz_device_dag": (_P, [_P, ctypes.POINTER(_U64)]),

@@ -208,6 +208,9 @@ GCZ_API uint64_t gcz_synth_default_seed(void);
  * gcz_tree_bytes / gcz_tree_serialize on the fetched tree (reference
  * shared_tree::sort_tree, bytes, serialize: src/shared_tree.cpp:443-513). */
 GCZ_API int gcz_sort_device(gcz_ctx *ctx);
+/* The device buffers gcz_sort_device needs for the last build, allocated ahead (callable on
+ * another thread while the tree is fetched; gcz_sort_device then finds them in place). */
+GCZ_API int gcz_sort_reserve(gcz_ctx *ctx);
 GCZ_API int gcz_bytes_device(gcz_ctx *ctx, uint64_t *out);
 /* .dag bytes into host_buf (cap >= *written, else GCZ_ERR_ARG with *written set). */
 GCZ_API int gcz_serialize_device(gcz_ctx *ctx, uint8_t *host_buf, uint64_t cap, uint64_t *written);
