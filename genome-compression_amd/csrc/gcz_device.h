@@ -1345,10 +1345,12 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
   const u64 lt = (1ull << lane) - 1;
   bool hashed = false;
   const bool dups = dup_flag && *dup_flag != 0;   // block-collapsed repeats (k_bkt_part) exist
+  u32 nfirst = 0;   // this thread's items that are not first occurrences (the dups pass below)
 #pragma unroll
   for (int e = 0; e < ITEMS; ++e) {
     const u64 j = ts.base + u64(e) * kBlock + tid;
     const bool is_first = j < p && ((ts.mask[e] >> lane) & 1ull);
+    if (!is_first) nfirst |= 1u << e;
     unsigned char me = 0;   // multi mark: needed for first occurrences only
     if ((hashed_next || sid) && is_first) me = early ? mu[e] : multi[j];
     if (hashed_next) {   // next-level pair (j, j+1): both children repeat?  (first <=> mask bit)
@@ -1379,13 +1381,32 @@ __global__ __launch_bounds__(kBlock) void k_flagscan_node(u32* __restrict__ word
       w.x = cl; w.y = cr;
       out[id] = w;
       words[j] = make_word(id, m, t, ulw(l) == ulw(xf(r, 1, 0)));   // the insert's bits, recomputed
-    } else if (dups && j < p && nf[j] == kNfDup) {
-      // its block representative: the key's first occurrence itself, or a repeat whose word
-      // the bucket dedupe pointed at the first occurrence (only first occurrences' words
-      // change here, so that word is stable)
-      const u32 w = words[j];
-      const u32 rep = w & kIdx;
-      if (nf[rep] != kNfMaybe) words[j] = (words[rep] & kIdx) | (w & kBits);
+    }
+  }
+  if (dups) {
+    // collapsed repeats (nf = kNfDup, k_bkt_part): their word holds the block representative,
+    // the key's first occurrence itself or a repeat whose word the bucket dedupe pointed at the
+    // first occurrence (only first occurrences' words change in this kernel, so that word is
+    // stable); the latter's first position is copied here.  Eight items at a time, each step's
+    // loads issued together (a dependent chain of four per repeat otherwise).
+    constexpr int DB = ITEMS < 8 ? ITEMS : 8;
+#pragma unroll
+    for (int e0 = 0; e0 < ITEMS; e0 += DB) {
+      unsigned char f[DB];
+      u32 w[DB], g[DB];
+#pragma unroll
+      for (int q = 0; q < DB; ++q) {
+        const u64 j = ts.base + u64(e0 + q) * kBlock + tid;
+        f[q] = j < p && ((nfirst >> (e0 + q)) & 1u) ? nf[j] : kNfMaybe;
+      }
+#pragma unroll
+      for (int q = 0; q < DB; ++q) w[q] = f[q] == kNfDup ? words[ts.base + u64(e0 + q) * kBlock + tid] : 0u;
+#pragma unroll
+      for (int q = 0; q < DB; ++q) g[q] = f[q] == kNfDup ? u32(nf[w[q] & kIdx]) : 0u;
+#pragma unroll
+      for (int q = 0; q < DB; ++q)
+        if (f[q] == kNfDup && g[q] != kNfMaybe)
+          words[ts.base + u64(e0 + q) * kBlock + tid] = (words[w[q] & kIdx] & kIdx) | (w[q] & kBits);
     }
   }
   if (hashed_next) {
