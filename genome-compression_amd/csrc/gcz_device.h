@@ -1446,17 +1446,39 @@ __global__ __launch_bounds__(kBlock) void k_resolve_node(u32* __restrict__ words
   if (level_direct(prev_count, n)) return;
   // the flag scan's sparse path resolved the level's few repeats itself
   if (sparse && bkt == 2 && hdr->predup == 0 && hdr->nnf <= kNfListCap) return;
-  // (a grid smaller than p / kBlock strides: fewer empty workgroups on levels without repeats)
-  for (u64 j = u64(blockIdx.x) * kBlock + threadIdx.x; j < p; j += u64(gridDim.x) * kBlock) {
-    if (nf[j] != kNfNot && nf[j] != kNfDup) continue;
-    const u32 w = words[j];
-    u64 key;
-    u32 q;
-    if (bkt && (bkt == 2 || hdr->predup == 0)) q = w & kIdx;    // bucketed insert: the word holds it
-    else T.read(w & kIdx, key, q);                // q = the key's first position
-    const Group h = grp[q >> 6];
-    const u32 id = h.prefix + u32(__popcll(h.mask & ((1ull << (q & 63)) - 1)));
-    words[j] = id | (w & kBits);
+  // (a grid smaller than p / kBlock strides: fewer empty workgroups on levels without repeats;
+  // four elements per step, each step's loads issued together: mark, word, group record)
+  const bool bucketed = bkt && (bkt == 2 || hdr->predup == 0);   // the word holds the first position
+  const u64 S = u64(gridDim.x) * kBlock;
+  constexpr int RB = 4;
+  for (u64 j0 = u64(blockIdx.x) * kBlock + threadIdx.x; j0 < p; j0 += RB * S) {
+    bool rep[RB];
+    u32 w[RB], q[RB];
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      const u64 j = j0 + u64(k) * S;
+      const unsigned char f = j < p ? nf[j] : kNfMaybe;
+      rep[k] = f == kNfNot || f == kNfDup;
+    }
+#pragma unroll
+    for (int k = 0; k < RB; ++k) w[k] = rep[k] ? words[j0 + u64(k) * S] : 0u;
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      q[k] = 0;
+      if (!rep[k]) continue;
+      u64 key;
+      if (bucketed) q[k] = w[k] & kIdx;
+      else T.read(w[k] & kIdx, key, q[k]);   // q = the key's first position
+    }
+    Group h[RB];
+#pragma unroll
+    for (int k = 0; k < RB; ++k)
+      if (rep[k]) h[k] = grp[q[k] >> 6];
+#pragma unroll
+    for (int k = 0; k < RB; ++k)
+      if (rep[k])
+        words[j0 + u64(k) * S] =
+            (h[k].prefix + u32(__popcll(h[k].mask & ((1ull << (q[k] & 63)) - 1)))) | (w[k] & kBits);
   }
 }
 
