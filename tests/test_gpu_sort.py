@@ -53,6 +53,23 @@ def test_device_sort_and_dag_match_reference(name, ctx, gcz, manifest):
     assert dev.root == host.root
 
 
+@pytest.mark.parametrize("name", ["corpus/merged", "synth/uniform_10000000"])
+def test_device_sort_after_reserve(name, gcz, manifest):
+    """gcz_sort_reserve (the drop-in calls it on a side thread during the fetch) then the sort
+    in a fresh context: same .dag as the reference; reserving twice is a no-op."""
+    case = manifest[name]
+    kind, payload, L = case_input(case, gcz)
+    c = gcz.Context(0)
+    try:
+        _build(c, kind, payload, L)
+        assert gcz._lib.gcz_sort_reserve(c._h) == 0
+        assert gcz._lib.gcz_sort_reserve(c._h) == 0
+        c.sort_device()
+        assert hashlib.sha256(c.serialize_device()).hexdigest() == case["expect"]["sha_dag"]
+    finally:
+        c.close()
+
+
 def test_device_sort_idempotent_and_unsorted_dag(ctx, gcz, manifest):
     case = manifest["corpus/hehcmv"]
     kind, payload, L = case_input(case, gcz)
