@@ -168,11 +168,12 @@ namespace {
 
 template <bool kBases>
 void launch_dl_pack(int L, dim3 g, hipStream_t st, const unsigned char* b, const u64* lv, const DensePlan& P,
-                    u32* pw, u32* cnt, Header* hdr) {
+                    u32* pw, u32* cnt, Header* hdr, uint4* zdesc, u64 nz16) {
   switch (L) {
 #define GCZ_CASE(X)                                                                                          \
   case X:                                                                                                    \
-    hipLaunchKernelGGL((k_dl_pack<X, kBases>), g, dim3(kDThreads), 0, st, b, lv, P, pw, cnt, hdr);         \
+    hipLaunchKernelGGL((k_dl_pack<X, kBases>), g, dim3(kDThreads), 0, st, b, lv, P, pw, cnt, hdr, zdesc,   \
+                       nz16);                                                                                \
     break;
     GCZ_CASE(1) GCZ_CASE(2) GCZ_CASE(3) GCZ_CASE(4) GCZ_CASE(5) GCZ_CASE(6) GCZ_CASE(7) GCZ_CASE(8)
     GCZ_CASE(9) GCZ_CASE(10) GCZ_CASE(11) GCZ_CASE(12)
@@ -218,7 +219,7 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
       (rc = ensure(dl_cnt, ncnt * 4 + 16)) || (rc = ensure(dl_off, (ncnt + 1) * 4 + 16)) ||
       (rc = ensure(dl_offt, (ncnt + P.NB) * 4 + 16)) ||
       (rc = ensure(dl_fpg, ncodes * 4 + 16)) || (rc = ensure(dl_fb, u64(P.nch) * (kDC / 64) * 8 + 16)) ||
-      (rc = ensure(dl_wpre, (nfb + 1) * 4 + 16)) || (rc = ensure(dl_desc, (t_cnt + t_fb) * 8 + 16)) ||
+      (rc = ensure(dl_wpre, (nfb + 1) * 4 + 16)) || (rc = ensure(dl_desc, (t_cnt + t_fb) * 8 + 32)) ||
       (rc = ensure(dl_fl, ncodes * 4 + 16)) || (rc = ensure(dl_fo, u64(P.NB) * (P.nch + 1) * 4 + 16)))
     return rc;
   if (list && (rc = ensure(dl_pb, (ncodes / 64 + 1) * 8))) return rc;
@@ -231,13 +232,13 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
   HIP_TRY(allow_lds(k_dl_first, first_bytes));
   hipEvent_t e0{};
   prof_begin(KID_DL_PACK, e0);
-  HIP_TRY(hipMemsetAsync(dl_desc.ptr, 0, (t_cnt + t_fb) * 8 + 16, stream));
+  const u64 nz16 = ((t_cnt + t_fb) * 8 + 16 + 15) / 16;   // (the descriptors and the two tickets; dl_desc holds 16 B more)
   if (a.bases)
     launch_dl_pack<true>(int(L), dim3(P.nch), stream, static_cast<const unsigned char*>(a.bases), nullptr, P,
-                         dl_pw.as<u32>(), dl_cnt.as<u32>(), d_hdr);
+                         dl_pw.as<u32>(), dl_cnt.as<u32>(), d_hdr, static_cast<uint4*>(dl_desc.ptr), nz16);
   else
     launch_dl_pack<false>(int(L), dim3(P.nch), stream, nullptr, a.leaves, P, dl_pw.as<u32>(), dl_cnt.as<u32>(),
-                          d_hdr);
+                          d_hdr, static_cast<uint4*>(dl_desc.ptr), nz16);
   HIP_TRY(hipGetLastError());
   if (check) {   // single device: the pure-ACGT verdict, read after the scatter is queued (below)
     if (!ev_dfail) HIP_TRY(hipEventCreateWithFlags(&ev_dfail, hipEventDisableTiming));

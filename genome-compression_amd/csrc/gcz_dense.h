@@ -166,14 +166,18 @@ static __device__ __forceinline__ void load_strand(const unsigned char* __restri
 
 // Pack: the strand's pre-word make_word(h, m, t, v) and the chunk's bucket histogram.
 // Bases: L bytes per strand (dna::dna(string_view), src/dna.cpp:79-84); leaves: u64.
+// (zdesc / nz16: the dense level's scan descriptors, cleared here -- no memset launch)
 template <int L, bool kBases>
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_pack(const unsigned char* __restrict__ bases,
                                                        const u64* __restrict__ leaves, DensePlan P,
                                                        u32* __restrict__ pw, u32* __restrict__ cnt,
-                                                       Header* __restrict__ hdr) {
+                                                       Header* __restrict__ hdr, uint4* __restrict__ zdesc,
+                                                       u64 nz16) {
   __shared__ u32 s_hist[kDNBMax];
   __shared__ signed char s_lut[256];
   const int tid = threadIdx.x;
+  for (u64 i = u64(blockIdx.x) * kDThreads + tid; i < nz16; i += u64(gridDim.x) * kDThreads)
+    zdesc[i] = make_uint4(0, 0, 0, 0);
   if (tid < 256) s_lut[tid] = (signed char)acgt_code(tid);
   for (u32 b = tid; b < P.NB; b += kDThreads) s_hist[b] = 0;
   const u64 c0 = u64(blockIdx.x) * kDC;
