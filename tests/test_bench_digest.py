@@ -8,6 +8,7 @@ streamed hashes must equal the hashes of the whole dump -- the format the
 reference goldens are stored in (tests/golden/manifest.json).
 """
 import hashlib
+import json
 import importlib.util
 import os
 import socket
@@ -114,3 +115,25 @@ def test_stream_digest_virtual_ranks():
     info = {"n_layers": tree.n_layers, "layer_size": [w.size // 2 for w in layers]}
     d = bench.stream_digest(SliceGroup(leaves, layers, 4, [0, 1, 2, 3]), None, 0, 1, info)
     assert (d["sha_leaves_bin"], d["sha_layers_bin"]) == _expected(tree)
+
+
+def test_exchange_budget_script_on_committed_probe():
+    """scripts/budget.py (DESIGN.md §7's projection) reads a committed virtual-rank line and
+    prints, per assumed link bandwidth, T_R = kernels + transfers + collective latency; the
+    printed sum and speed-up follow from the line's own numbers."""
+    import re
+    import subprocess
+    import sys
+    line = os.path.join(REPO, "profiles", "r04", "strong_virtual8.json")
+    out = subprocess.run([sys.executable, os.path.join(REPO, "scripts", "budget.py"), line, "2.5"],
+                         capture_output=True, text=True, check=True).stdout
+    with open(line) as f:
+        d = json.loads(f.read().strip().splitlines()[-1])
+    rows = re.findall(r"B = ([\d.]+) GB/s: kernels ([\d.]+) \+ transfers ([\d.]+) \+ (\d+) collectives / (\d+) syncs "
+                      r"([\d.]+) = ([\d.]+) ms -> ([\d.]+)x", out)
+    assert len(rows) == 2
+    assert float(rows[0][1]) == round(max(d["rank_kernel_ms"]), 3)
+    assert int(rows[0][3]) == len(d["rank_timeline"][0]["exchange_log"])
+    for _, k, x, _, _, lat, tot, sp in rows:
+        assert abs(float(k) + float(x) + float(lat) - float(tot)) < 2e-3
+        assert abs(2.5 / float(tot) - float(sp)) < 0.01
