@@ -159,7 +159,7 @@ template <int L>
 static __device__ __forceinline__ void load_strand(const unsigned char* __restrict__ bases, u64 s, u32 (&w)[4]) {
   const u64 a = s * L;
   const u32* p = reinterpret_cast<const u32*>(bases + (a & ~3ull));
-  constexpr int NW = (L + 3 + 3) / 4;
+  constexpr int NW = L % 4 == 0 ? L / 4 : (L + 3 + 3) / 4;   // (L % 4 == 0: every strand is 4-B aligned)
 #pragma unroll
   for (int i = 0; i < 4; ++i) w[i] = i < NW ? p[i] : 0u;
 }
@@ -203,7 +203,7 @@ template <int L, bool kBases>
       u32 x = 0;
       bool ok = true;
       if constexpr (kBases) {
-        const u32 sh = u32(s * L) & 3u;
+        const u32 sh = L % 4 == 0 ? 0u : u32(s * L) & 3u;   // (0: each base's byte a compile-time index)
 #pragma unroll
         for (int c = 0; c < L; ++c) {
           const u32 byte_i = sh + u32(c);
