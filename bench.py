@@ -144,6 +144,51 @@ def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None, bu
     return 0
 
 
+def dist_rank_bytes(kernel, L, Sr, r, R, c_r, u_r, n_leaves):
+    """Algorithmic HBM bytes of one RANK's launches of `kernel` in a multi-rank build (the
+    profiled rank r: Sr strands, pr = ceil(Sr / 2) layer-0 pairs, c_r leaves it holds first, u_r
+    layer-0 uniques it emits; R ranks).  Streamed bytes + one 64-B sector per random access,
+    like algorithmic_bytes, but over what this rank's launches touch: its own strands and pairs,
+    the owner side's received records (~pr, owners balance by hash), the code-space passes over
+    all 4^L codes and the R gathered presence bitmaps (gcz_dense.h, gcz_dist_fast.h).  Scopes
+    without HBM work of their own (exchange, tail) count 0."""
+    pr = (Sr + 1) // 2
+    C = 4 ** L
+    NB = min(1024, C)
+    nch = (Sr + 32767) // 32768
+    if kernel == "dl_pack":         # bases in, pre-word out, per-chunk bucket counts
+        return Sr * L + 4 * Sr + 4 * NB * nch
+    if kernel == "dl_scan":
+        return 8 * NB * nch
+    if kernel == "dl_scatter":      # pre-word in, record out
+        return 8 * Sr
+    if kernel == "dl_first":        # k_dl_first (records, first position per code, bitmap), the
+        # r-first counts over the R gathered bitmaps, k_dl_rfirst (first positions, the lower
+        # ranks' bitmaps, r-first lists), k_dl_fb (lists in, position bitmap out)
+        return 4 * Sr + 8 * C + C // 8 + R * C // 8 + r * C // 8 + 12 * c_r + Sr // 8
+    if kernel == "dl_fbscan":       # popcount scan; k_dl_gq: one rank lookup (a sector) per r-first code
+        return Sr // 8 + Sr // 16 + 72 * c_r
+    if kernel == "dl_ids":          # bitmaps of ranks <= r, relayed G reads per held code, record -> word
+        return (r + 1) * C // 8 + 4 * min(n_leaves, Sr) + 8 * Sr + (Sr // 8 + 8 * c_r)
+    if kernel == "dl_words":        # record, id in; word out
+        return 16 * Sr + Sr // 8
+    if kernel == "node_insert":     # k_node_keys: pre-word pairs in; canonical pair, word, marks out
+        return 24 * pr
+    if kernel == "dist_bucket":     # canonical pair, marks, word in; key and index out
+        return 26 * pr
+    if kernel == "dist_owner":      # ~pr received keys: partition, fine pass, LDS dedupe
+        return 41 * pr
+    if kernel == "dist_ids":        # reply flags -> global flags, look-ahead, the rank scan
+        return 11 * pr
+    if kernel == "dist_remap":
+        return 8 * pr
+    if kernel == "dist_l0":         # leaf word pairs, flags, ids in; words and unique nodes out
+        return 17 * pr + 8 * u_r
+    if kernel == "direct_levels":   # level-1 words in, the subtrees' nodes out (inner levels in LDS)
+        return 12 * pr
+    return 0
+
+
 def build_bytes(L, S, n_leaves, layer_sizes):
     """Whole-build algorithmic bytes, SURVEY §8(d): B_stream + B_table."""
     pk = []
@@ -475,22 +520,30 @@ def main():
         c.profile(False)
     prof = tables[0]
     rank_ms = [round(sum(v["total_ms"] for k, v in t.items() if k != "exchange"), 3) for t in tables]
-    share = world if mode == "dist" else (args.virtual if mode == "virtual" else 1)
     kernels = {}
+    rank_model = None
+    if mode in ("dist", "virtual"):   # the profiled rank's own launches (rank 0 of the virtual ranks)
+        R = world if mode == "dist" else args.virtual
+        me = rank if mode == "dist" else 0
+        r0, r1, _ = gcz.dist_plan(S, R, me)
+        rank_model = {"rank": me, "strands": r1 - r0, "pairs": (r1 - r0 + 1) // 2,
+                      "first_leaves": group.slice(0, -1)[1], "layer0_uniques": group.slice(0, 0)[1]}
     for name, p in prof.items():
         if p["launches"] == 0:
             continue
-        # per-rank share of the algorithmic bytes (rank 0 profiled); exchange/dist phases carry none
-        b = algorithmic_bytes(name, L, S, info["n_leaves"], info["layer_size"],
-                              info["hashed_pairs"] if mode in ("single", "replicas") else None,
-                              info.get("bucketed_pairs", 0),
-                              two_pass=prof.get("bucket_fine", {}).get("launches", 0) > 0,
-                              launches=p["launches"]) // share
+        if rank_model:
+            b = dist_rank_bytes(name, L, rank_model["strands"], rank_model["rank"], R, rank_model["first_leaves"],
+                                rank_model["layer0_uniques"], info["n_leaves"])
+        else:
+            b = algorithmic_bytes(name, L, S, info["n_leaves"], info["layer_size"], info["hashed_pairs"],
+                                  info.get("bucketed_pairs", 0),
+                                  two_pass=prof.get("bucket_fine", {}).get("launches", 0) > 0,
+                                  launches=p["launches"])
         kernels[name] = {"launches": p["launches"], "total_ms": round(p["total_ms"], 4),
                          "avg_ms": p["total_ms"] / p["launches"], "alg_bytes": b,
                          "gbs": b / (p["total_ms"] * 1e-3) / 1e9 if p["total_ms"] > 0 else None}
-    dom = max((k for k in kernels if k not in ("clear", "exchange", "dist_local")),
-              key=lambda k: kernels[k]["total_ms"])
+    # the dominant kernel: the most device time among kernels that move algorithmic bytes
+    dom = max((k for k in kernels if kernels[k]["alg_bytes"] > 0), key=lambda k: kernels[k]["total_ms"])
     dk = kernels[dom]
     # HBM bytes from the committed PMC capture of this config (scripts/traffic_json.py): per
     # build for each kernel name, and the whole build's
@@ -656,6 +709,7 @@ def main():
                       # device_ms is the last attempt, device_ms_all every attempt's)
                       "attempts": info.get("attempts", 1), "device_ms_all": info.get("build_ms_all")},
             "kernels": kernels,
+            "rank_byte_model": rank_model,
             "rank_kernel_ms": rank_ms,
             "rank_timeline": rank_detail,
             "ratio_path": ratio_path,

@@ -274,7 +274,11 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
     // failed pack: rejected strands carry no record) keep the device busy
     HIP_TRY(hipEventSynchronize(ev_dfail));
     if (h_hdr->dense_fail) {   // the hash-table leaf level follows: no repetitive-data verdict from here
-      HIP_TRY(hipMemsetAsync(&d_hdr->predup, 0, sizeof(d_hdr->predup), stream));
+      // (the probe's counts too: they were taken over the rejected pack's pre-words, and the
+      // hash-table level's own probe adds into the same shards; dupstat sits right before predup)
+      static_assert(offsetof(Header, predup) == offsetof(Header, dupstat) + sizeof(Header::dupstat),
+                    "dupstat and predup are cleared as one range");
+      HIP_TRY(hipMemsetAsync(&d_hdr->dupstat[0], 0, sizeof(d_hdr->dupstat) + sizeof(d_hdr->predup), stream));
       return GCZ_OK;
     }
   }
@@ -973,6 +977,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   for (int i = 0; i < 64; ++i) info.hashed_pairs += h_hdr->hashed[i];
   info.bucketed_pairs = h_hdr->hashed[1];
   info.leaf_path = dense_used ? 1u : 0u;
+  info.repetitive = h_hdr->predup;
   return GCZ_OK;
 }
 

@@ -99,7 +99,7 @@ enum KernelId {
   KID_LEAF, KID_NODE, KID_FLAGSCAN_LEAF, KID_FLAGSCAN_NODE, KID_RESOLVE_LEAF, KID_RESOLVE_NODE, KID_MEMSET,
   KID_EXCHANGE, KID_DIST, KID_OWNER, KID_IDS, KID_REMAP, KID_TAIL, KID_SORT, KID_DAG, KID_DIRECT,
   KID_BKT_COUNT, KID_BKT_SCAN, KID_BKT_SCATTER, KID_BKT_DEDUPE, KID_BKT_FINE,
-  KID_DL_PACK, KID_DL_SCAN, KID_DL_SCATTER, KID_DL_FIRST, KID_DL_FBSCAN, KID_DL_IDS, KID_DL_WORDS, KID_COUNT
+  KID_DL_PACK, KID_DL_SCAN, KID_DL_SCATTER, KID_DL_FIRST, KID_DL_FBSCAN, KID_DL_IDS, KID_DL_WORDS, KID_L0, KID_COUNT
 };
 inline const char* kernel_name(int k) {
   static const char* names[KID_COUNT] = {"leaf_insert", "node_insert", "flagscan_leaf", "flagscan_node",
@@ -107,7 +107,7 @@ inline const char* kernel_name(int k) {
                                          "dist_owner", "dist_ids", "dist_remap", "tail", "sort", "dag_write", "direct_levels",
                                          "bucket_count", "bucket_scan", "bucket_scatter", "bucket_dedupe", "bucket_fine",
                                          "dl_pack", "dl_scan", "dl_scatter", "dl_first", "dl_fbscan", "dl_ids",
-                                         "dl_words"};
+                                         "dl_words", "dist_l0"};
   return names[k];
 }
 
@@ -304,6 +304,19 @@ struct gcz_ctx {
     HIP_TRY(hipMalloc(&b.ptr, bytes ? bytes : 16));
     b.bytes = bytes ? bytes : 16;
     return GCZ_OK;
+  }
+  // ensure() that leaves last_error / info.status alone: for work on a side thread beside
+  // another call on this context (gcz_sort_reserve during gcz_fetch_host)
+  hipError_t ensure_quiet(gcz_host::DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes && b.ptr) return hipSuccess;
+    if (b.ptr) {
+      if (hipError_t e = hipStreamSynchronize(stream)) return e;
+      if (hipError_t e = hipFree(b.ptr)) return e;
+      b.ptr = nullptr; b.bytes = 0;
+    }
+    if (hipError_t e = hipMalloc(&b.ptr, bytes ? bytes : 16)) return e;
+    b.bytes = bytes ? bytes : 16;
+    return hipSuccess;
   }
 
   hipEvent_t next_event() {

@@ -27,6 +27,7 @@
 
 #include "gcz_ctx.h"
 #include "gcz_dist_device.h"
+#include "gcz_dist_fast.h"
 #include "gcz_scan.h"
 
 using namespace gcz_dev;
@@ -42,6 +43,9 @@ struct gcz_dist_state {
   u64* h_gath = nullptr;    // pinned mirrors of the gathered vectors
   u64* h_gath2 = nullptr;
   u64* h_gathf = nullptr;
+  DlRelay* h_relay = nullptr;   // pinned staging of the dense leaf relay table (H2D, stream-ordered)
+  DevBuf fl_cntb, fl_mid, fl_g3, fl_g4;   // fused schedule: r-first counts per bucket, the mid-build
+  u64* h_mid = nullptr;                   // vector (+ pinned mirror), R3's / R4's gathered vectors
 };
 
 void gcz_dist_state_free(gcz_ctx* c) {
@@ -54,11 +58,13 @@ void gcz_dist_state_free(gcz_ctx* c) {
   for (DevBuf* b : {&d->dict, &d->scratch, &d->gnf, &d->gmul, &d->gid, &d->blockcnt, &d->bchunk, &d->skey, &d->sidx, &d->sflag,
                     &d->scval, &d->sdval, &d->clist, &d->olist, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab, &d->oids,
                     &d->omin, &d->ob_cnt, &d->ob_off, &d->ob_desc, &d->ob_rec, &d->ob_seg, &d->ob_rt,
-                    &d->ob_rec2, &d->ob_fo,
+                    &d->ob_rec2, &d->ob_fo, &d->fl_cntb, &d->fl_mid, &d->fl_g3, &d->fl_g4,
                     &d->dhdr, &d->gath, &d->gath2, &d->gathf, &d->ddesc, &d->tail_in, &d->nfl})
     if (b->ptr) (void)hipFree(b->ptr);
   for (u64* h : {d->h_gath, d->h_gath2, d->h_gathf})
     if (h) (void)hipHostFree(h);
+  if (d->h_relay) (void)hipHostFree(d->h_relay);
+  if (d->h_mid) (void)hipHostFree(d->h_mid);
   delete d;
   c->dist = nullptr;
 }
@@ -89,6 +95,22 @@ struct Transport {
                            const std::vector<u64>& rd, const std::vector<const void*>& send,
                            const std::vector<void*>& recv) = 0;
   virtual int allgather(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) = 0;
+  // Several exchanges as ONE group (RCCL: one ncclGroupStart/End, a single launch whose
+  // transfers proceed together; the other transports run them one after the other).  Each op
+  // is an alltoallv_at; an allgather is the op whose every count is its size, every send
+  // displacement 0 and receive displacement s * size (XOp::allgather).
+  struct XOp {
+    std::vector<u64> M, sd, rd;
+    bool rev = false;
+    size_t elem = 1;
+    std::vector<const void*> send;
+    std::vector<void*> recv;
+  };
+  virtual int group(const std::vector<XOp>& ops) {
+    for (const XOp& o : ops)
+      if (int rc = alltoallv_at(o.M, o.rev, o.elem, o.sd, o.rd, o.send, o.recv)) return rc;
+    return 0;
+  }
   // rank 0's `bytes` at send[i of rank 0] to recv[i] of every other rank
   virtual int bcast0(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) = 0;
   // rank 0 receives cnt[r] elements from every rank r, concatenated in rank order
@@ -293,6 +315,41 @@ struct RcclTransport : Transport {
   int alltoallv(const std::vector<u64>& M, bool rev, size_t elem, const std::vector<const void*>& send,
                 const std::vector<void*>& recv) override {
     return run(p2p_plan(M, world, me, rev, elem, nullptr, nullptr), send[0], recv[0]);
+  }
+  // every op's self copy first, then all their sends / receives in one group (NCCL matches a
+  // pair's several sends and receives in issue order)
+  int group(const std::vector<XOp>& ops) override {
+    ncclComm_t c = comm.load();
+    if (!c) {
+      err = "communicator aborted";
+      return GCZ_ERR_DEVICE;
+    }
+    std::vector<std::vector<P2POp>> plans;
+    for (const XOp& o : ops) {
+      plans.push_back(p2p_plan(o.M, world, me, o.rev, o.elem, o.sd.data(), o.rd.data()));
+      const P2POp& self = plans.back()[size_t(me)];
+      if (int rc = self_copy(static_cast<char*>(o.recv[0]) + self.recv_off,
+                             static_cast<const char*>(o.send[0]) + self.send_off, self.send_bytes))
+        return rc;
+    }
+    RcclApi& a = rccl();
+    if (int rc = check(a.GroupStart(), "ncclGroupStart")) return rc;
+    for (size_t k = 0; k < ops.size(); ++k) {
+      const auto* sb = static_cast<const char*>(ops[k].send[0]);
+      auto* rb = static_cast<char*>(ops[k].recv[0]);
+      for (const P2POp& o : plans[k]) {
+        if (o.peer == me) continue;
+        if (o.send_bytes) {
+          const ncclResult_t r = a.Send(sb + o.send_off, o.send_bytes, ncclUint8, o.peer, c, stream);
+          if (r != ncclSuccess) { (void)a.GroupEnd(); return check(r, "ncclSend"); }
+        }
+        if (o.recv_bytes) {
+          const ncclResult_t r = a.Recv(rb + o.recv_off, o.recv_bytes, ncclUint8, o.peer, c, stream);
+          if (r != ncclSuccess) { (void)a.GroupEnd(); return check(r, "ncclRecv"); }
+        }
+      }
+    }
+    return check(a.GroupEnd(), "ncclGroupEnd");
   }
   int alltoallv_at(const std::vector<u64>& M, bool rev, size_t elem, const std::vector<u64>& sd,
                    const std::vector<u64>& rd, const std::vector<const void*>& send,
@@ -577,6 +634,7 @@ struct gcz_group {
     RcclTransport* tr;
     int device, rank;
     long limit_s = dist_timeout_s();
+    long grace_s = 30;   // after the abort: the build's return, else the process ends
     std::mutex mu;
     std::condition_variable cv;
     bool armed = false, stop = false;
@@ -624,7 +682,7 @@ struct gcz_group {
       cv.notify_all();
     }
     void loop() {
-      (void)hipSetDevice(device);
+      if (device >= 0) (void)hipSetDevice(device);
       std::unique_lock<std::mutex> lk(mu);
       while (!stop) {
         if (!armed) {
@@ -647,8 +705,9 @@ struct gcz_group {
         lk.unlock();
         tr->abort();
         lk.lock();
-        // the aborted collective lets the build return; if it does not, end the process
-        const auto grace = std::chrono::steady_clock::now() + std::chrono::seconds(30);
+        // the aborted collective lets the build return (gcz_group::fail -> disarm clears
+        // `pending`); if it does not, end the process
+        const auto grace = std::chrono::steady_clock::now() + std::chrono::seconds(grace_s);
         while (!stop && !armed && pending.size() && std::chrono::steady_clock::now() < grace)
           cv.wait_until(lk, grace);
         if (!stop && pending.size()) {
@@ -714,6 +773,19 @@ struct gcz_group {
            per_local([&](int me) { u64 t = 0; for (int q = 0; q < R; ++q) if (q != me) t += mcount(M, R, rev, q, me); return t * elem; }));
     return xend(tr->alltoallv_at(M, rev, elem, sd, rd, s, r));
   }
+  // One group of exchanges (Transport::group), logged as one collective with the ops' bytes.
+  int x_group(const char* name, const std::vector<Transport::XOp>& ops) {
+    const int R = world;
+    auto tot = [&](int me, bool sent) {
+      u64 t = 0;
+      for (const Transport::XOp& o : ops)
+        for (int q = 0; q < R; ++q)
+          if (q != me) t += (sent ? mcount(o.M, R, o.rev, me, q) : mcount(o.M, R, o.rev, q, me)) * o.elem;
+      return t;
+    };
+    xbegin(name, per_local([&](int me) { return tot(me, true); }), per_local([&](int me) { return tot(me, false); }));
+    return xend(tr->group(ops));
+  }
   int x_allgather(const char* name, size_t bytes, const std::vector<const void*>& s, const std::vector<void*>& r) {
     xbegin(name, per_local([&](int) { return u64(bytes) * u64(world - 1); }),
            per_local([&](int) { return u64(bytes) * u64(world - 1); }));
@@ -761,7 +833,10 @@ struct gcz_group {
   int fail(int code, const std::string& what) {
     last_error = what;
     info.status = code;
-    if (watch && !watch->fired) watch->disarm();   // (a failing rank's peers are bounded by their own)
+    // the build returns: nothing of it is pending any more -- also after the watchdog fired, whose
+    // thread would otherwise take the build for hung and end the process after its grace period
+    // (a failing rank's peers are bounded by their own watchdogs)
+    if (watch) watch->disarm();
     for (gcz_ctx* c : ctx) c->fail(code, "group build", what.c_str());
     return code;
   }
@@ -795,6 +870,16 @@ struct gcz_group {
     }
     return GCZ_OK;
   }
+  int finish_top(int Gx, bool direct, u64 prev_total, const std::vector<u32*>& cur_in, std::vector<u64>& dcur,
+                 bool fl, bool* failed);
+  // The fused leaf + layer-0 schedule (gcz_dist_fast.h); *taken = false: not applicable to this
+  // genome, or the attempt was discarded on every rank -- the general schedule follows.
+  int build_fast(const std::vector<const unsigned char*>& bases, const u64* const* d_leaves, int L,
+                 const std::vector<u64>& leaf_cap, bool* taken);
+  int fast_mode = std::getenv("GCZ_DIST_FAST") ? std::atoi(std::getenv("GCZ_DIST_FAST")) : 1;   // 0: off
+  hipEvent_t ev_mid = nullptr;   // the fused schedule's mid-build read (status, counts)
+  int event_sync(hipEvent_t e);
+  int build_done();
   int exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, u32 key_bits, u32 child_bits,
                std::vector<u64>& c, std::vector<u64>& off, u64& total, u64* err_global, int* err_sym,
                int* ovf_bits, bool nolocal = false, bool lookahead = false, u64* next_hashed_out = nullptr);
@@ -953,7 +1038,7 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
     Header* h = cx->hdr.as<Header>();
     if (cx->ensure(cx->dl_pos, (u64(NB) + xw) * 4 + 64)) return dev_fail("dense leaf buffers");
     if (local_rc) {   // this rank's phase A failed: it joins exchange 2 with a failure word only
-      const u32 failed_xv[2] = {0, 4};
+      static const u32 failed_xv[2] = {0, 4};   // (static: the async copy may read it after this scope)
       G_HIP(hipMemcpyAsync(cx->dl_pos.as<u32>() + NB, failed_xv, sizeof(failed_xv), hipMemcpyHostToDevice, cx->stream));
       continue;
     }
@@ -1082,9 +1167,15 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
     const DensePlan& DP = cx->dl_plan;
     Header* h = cx->hdr.as<Header>();
     {
-      ProfScope ps_(cx, KID_IDS);
+      ProfScope ps_(cx, KID_DL_IDS);
       if (cx->ensure(cx->dl_gid, sizeof(DlRelay) + 16)) return dev_fail("dense leaf relay table");
-      G_HIP(hipMemcpyAsync(cx->dl_gid.ptr, &relay, sizeof(DlRelay), hipMemcpyHostToDevice, cx->stream));
+      // staged in pinned memory the context owns (the copy is asynchronous; the previous build's
+      // copy has completed: every build ends with a host sync)
+      gcz_dist_state& ds = *cx->dist;
+      if (!ds.h_relay && hipHostMalloc((void**)&ds.h_relay, sizeof(DlRelay), hipHostMallocDefault) != hipSuccess)
+        return dev_fail("dense leaf relay staging");
+      *ds.h_relay = relay;
+      G_HIP(hipMemcpyAsync(cx->dl_gid.ptr, ds.h_relay, sizeof(DlRelay), hipMemcpyHostToDevice, cx->stream));
       G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_ids_mr), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 int(RB * 4)));
       hipLaunchKernelGGL(k_dl_ids_mr, dim3(NB), dim3(kDThreads), RB * 4, cx->stream, cx->dl_rec.as<u32>(),
@@ -1572,6 +1663,730 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
   return GCZ_OK;
 }
 
+// ---- the fused leaf + layer-0 schedule (gcz_dist_fast.h) -----------------------------------
+
+namespace {
+// The owner's two-pass dedupe of nr received layer-0 records with K-bit keys (exchange()'s
+// k_ob_part / k_bkt_fine / k_bkt_dedupe2<true> path); false: the records do not fit it.
+bool owner_two_pass_plan(u64 nr, u32 K, Bkt2Plan& b2) {
+  u32 obb = 0;   // (exchange()'s single-pass precondition holds too)
+  while (obb < 12 && (nr >> obb) > 4096) ++obb;
+  const u64 nch = (nr + kDC - 1) / kDC;
+  if (nr < 2 || K < obb || K - obb + kDLog > 64 || nch > 8192) return false;
+  u32 bb = 0;
+  while (bb < u32(kBktMaxLog) && (nr >> bb) > 2560) ++bb;
+  b2 = Bkt2Plan{};
+  b2.K = K;
+  b2.b1 = std::min<u32>(bb, kPartMaxB1);
+  b2.b2 = bb - b2.b1;
+  b2.G = (nr + kPartChunk - 1) / kPartChunk;
+  const u64 mean_run = std::max<u64>(1, std::min<u64>(nr, kPartChunk) >> b2.b1);
+  b2.SC = u32(std::max<u64>(1, std::min<u64>(128, u64(kFineCap / 2) / mean_run)));
+  b2.SC = 1u << log2_exact(b2.SC);
+  b2.P = kPartLog + log2_exact(b2.SC);
+  b2.nslice = u32((b2.G + b2.SC - 1) / b2.SC);
+  return K >= bb && b2.b2 <= u32(kFineMaxB2) && K - b2.b1 + kPartLog <= 64 && K - bb + b2.P <= 64 &&
+         mean_run * b2.SC <= u64(kFineCap) / 2 && b2.nslice <= 512;
+}
+
+Transport::XOp xop_a2a(const std::vector<u64>& M, int R, bool rev, size_t elem, std::vector<const void*> send,
+                       std::vector<void*> recv) {
+  Transport::XOp o;
+  o.M = M;
+  o.rev = rev;
+  o.elem = elem;
+  o.sd.assign(size_t(R) * R, 0);
+  o.rd.assign(size_t(R) * R, 0);
+  for (int s = 0; s < R; ++s)
+    for (int d = 0; d < R; ++d) {
+      o.sd[size_t(s) * R + d] = send_displ(M, R, rev, s, d);
+      o.rd[size_t(d) * R + s] = recv_displ(M, R, rev, d, s);
+    }
+  o.send = std::move(send);
+  o.recv = std::move(recv);
+  return o;
+}
+// every rank's `n` elements to every rank, concatenated in rank order
+Transport::XOp xop_allgather(int R, u64 n, size_t elem, std::vector<const void*> send, std::vector<void*> recv) {
+  Transport::XOp o;
+  o.M.assign(size_t(R) * R, n);
+  o.elem = elem;
+  o.sd.assign(size_t(R) * R, 0);
+  o.rd.assign(size_t(R) * R, 0);
+  for (int d = 0; d < R; ++d)
+    for (int s = 0; s < R; ++s) o.rd[size_t(d) * R + s] = u64(s) * n;
+  o.send = std::move(send);
+  o.recv = std::move(recv);
+  return o;
+}
+// segment d (of `seg` elements) of every rank's buffer to rank d, landing at segment s
+Transport::XOp xop_fixed(int R, u64 seg, size_t elem, std::vector<const void*> send, std::vector<void*> recv) {
+  Transport::XOp o;
+  o.M.assign(size_t(R) * R, seg);
+  o.elem = elem;
+  o.sd.assign(size_t(R) * R, 0);
+  o.rd.assign(size_t(R) * R, 0);
+  for (int s = 0; s < R; ++s)
+    for (int d = 0; d < R; ++d) {
+      o.sd[size_t(s) * R + d] = u64(d) * seg;
+      o.rd[size_t(d) * R + s] = u64(s) * seg;
+    }
+  o.send = std::move(send);
+  o.recv = std::move(recv);
+  return o;
+}
+}  // namespace
+
+// The host waits for one event (the build goes on queued behind it); every collective enqueued
+// before it has completed then, so the watchdog is disarmed.
+int gcz_group::event_sync(hipEvent_t e) {
+  const hipError_t rc = hipEventSynchronize(e);
+  if (watch && watch->fired) return fail(GCZ_ERR_DEVICE, watch->msg);
+  if (rc != hipSuccess) return dev_fail("hipEventSynchronize");
+  if (watch) watch->disarm();
+  return GCZ_OK;
+}
+
+int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const u64* const* d_leaves, int L,
+                          const std::vector<u64>& leaf_cap, bool* taken) {
+  *taken = false;
+  const int R = world, NL = int(ctx.size());
+  const DistPlan& P = plan;
+  const int G = P.G, D = P.D;
+  // applicable: several ranks with distributed levels to spare (G >= 2; the general schedule
+  // gathers a small hash-consed layer 0 to rank 0 instead -- here its exchange rides in the leaf
+  // level's collective groups, so it stays distributed), every rank with pairs of its own, the
+  // dense leaf level's codes
+  if (!fast_mode || R < 2 || L > 12 || G < 2 || dense_mode == 0) return GCZ_OK;
+  for (int s = 0; s < R; ++s)
+    if (P.count(s, 1) < 2) return GCZ_OK;
+  const u64 ncodes = u64(1) << (2 * L), nw = (ncodes + 63) / 64;
+  const u64 nwb = nw + 4 + u64(R);   // bitmap, status words, layer-0 records per owner
+  const u32 child_bits = 2 * u32(L);  // hashed code labels (< 4^L; the null pair is not exchanged)
+  const u32 key_bits = 2 * (child_bits + 2);
+  FlPairs pairs{};
+  for (int s = 0; s < R; ++s) pairs.p[s] = P.count(s, 1);
+  std::vector<LeafLevel> las(NL);
+  std::vector<u64> dcur(NL, 0);
+  // ---- phase A: the dense pack / sort / first positions, the presence bitmap, and layer 0's
+  // keys from the pre-words (hashed codes as labels), bucketed by owner
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    const int r = rank[i];
+    if (int rc = alloc(i, leaf_cap[i])) return rc == GCZ_ERR_DEVICE ? dev_fail("allocation") : rc;
+    gcz_dist_state& d = *cx->dist;
+    if (!cx->ev_start) {
+      G_HIP(hipEventCreate(&cx->ev_start));
+      G_HIP(hipEventCreate(&cx->ev_stop));
+    }
+    G_HIP(hipEventRecord(cx->ev_start, cx->stream));
+    InitPlan ip{};
+    ip.hdr = cx->hdr.as<Header>();
+    ip.desc = cx->desc.as<uint4>();
+    ip.ndesc16 = cx->desc.bytes / 16;
+    hipLaunchKernelGGL(k_build_init, dim3(unsigned(std::min<u64>(1024, std::max<u64>(1, (ip.ndesc16 + kBlock - 1) / kBlock)))),
+                       dim3(kBlock), 0, cx->stream, ip);
+    G_HIP(hipGetLastError());
+    Header* h = cx->hdr.as<Header>();
+    DistHdr* dh = d.dhdr.as<DistHdr>();
+    G_HIP(hipMemsetAsync(dh, 0, sizeof(DistHdr), cx->stream));
+    LeafLevel& la = las[i];
+    la.bases = bases[i];
+    la.leaves = d_leaves ? d_leaves[i] : nullptr;
+    la.S = P.count(r, 0);
+    la.L = L;
+    la.words = cx->wa.as<u32>();
+    if (cx->ensure(cx->dl_seg, size_t(64 + 3 * R) * 8 + 64) || cx->ensure(cx->dl_pb, nwb * 8) ||
+        cx->ensure(cx->dl_pbs, size_t(R) * nwb * 8 + 16))
+      return dev_fail("dense leaf buffers");
+    bool used = false;
+    cx->probe_ranks = unsigned(R);
+    const int rc = cx->dense_phase_a(la, h, &h->count[0], false, true, &used, cx->dl_pb.as<u64>() + nw);
+    cx->probe_ranks = 1;
+    if (rc) return rc == GCZ_ERR_DEVICE ? dev_fail("dense leaves") : rc;
+    if (!used) return GCZ_OK;   // (sizes outside the dense level: the same on every rank)
+    const u64 n = la.S, p = P.count(r, 1);
+    const u32 nb = u32(std::max<u64>(1, (p + kTile - 1) / kTile));
+    if (u64(R) * nb > kBscanSmall) return GCZ_OK;   // (>= 2^29 pairs per rank; not here)
+    RecSrc rs{};
+    rs.in = cx->dl_pw.as<u32>();
+    rs.n = n;
+    rs.p = p;
+    rs.words = cx->wb.as<u32>();
+    rs.nf = cx->nf_set[1];
+    rs.multi = cx->multi_set[1];
+    rs.canon = d.scratch.as<uint2>();
+    rs.R = u32(R);
+    {
+      ProfScope ps_(cx, KID_NODE);
+      hipLaunchKernelGGL(k_node_keys, dim3(nb), dim3(kBlock), 0, cx->stream, rs.in, n, p, cx->wb.as<u32>(),
+                         d.scratch.as<uint2>(), cx->nf_set[1], cx->multi_set[1], &h->count[kLayerSlot], static_cast<const u32*>(nullptr), 0u, rs,
+                         d.blockcnt.as<u32>(), nb, static_cast<const unsigned char*>(nullptr),
+                         d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(), d.ddesc.as<u64>(), 1u);
+      G_HIP(hipGetLastError());
+    }
+    {
+      ProfScope ps_(cx, KID_DIST);
+      hipLaunchKernelGGL(k_bscan_small, dim3(1), dim3(1024), 0, cx->stream, d.blockcnt.as<u32>(), u32(R), nb, dh->sync,
+                         static_cast<const Header*>(h), static_cast<const u64*>(nullptr),
+                         static_cast<const unsigned char*>(nullptr));
+      hipLaunchKernelGGL(k_bucket_scatter, dim3(nb), dim3(kBlock), 0, cx->stream, rs, d.blockcnt.as<u32>(), nb,
+                         d.skey.as<u64>(), d.sidx.as<u32>());
+      G_HIP(hipGetLastError());
+      // the owner counts ride behind the bitmap and the status words
+      G_HIP(hipMemcpyAsync(cx->dl_pb.as<u64>() + nw + 4, dh->sync, size_t(R) * 8, hipMemcpyDeviceToDevice, cx->stream));
+    }
+  }
+  // ---- R1: presence bitmaps + status words + owner counts
+  {
+    std::vector<const void*> s;
+    std::vector<void*> rv;
+    for (gcz_ctx* cx : ctx) {
+      s.push_back(cx->dl_pb.ptr);
+      rv.push_back(cx->dl_pbs.ptr);
+    }
+    hipEvent_t e0{};
+    ctx[0]->prof_begin(KID_EXCHANGE, e0);
+    G_RC(x_allgather("R1 leaf presence bitmaps + status + layer-0 owner counts", nwb * 8, s, rv));
+    ctx[0]->prof_end(KID_EXCHANGE, e0);
+  }
+  // every rank's r-first counts and bucket prefixes from the bitmaps; the host's one mid-build
+  // read (status, owner counts, r-first counts) queued ahead of the leaf level's r-first work
+  const u32 NB = ctx[0]->dl_plan.NB, RB = 1u << ctx[0]->dl_plan.IB;
+  const u64 xw = (u64(NB) + 2 + 1) & ~u64(1);
+  const u64 nmid = u64(R) * (4 + R) + R;
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    gcz_dist_state& d = *cx->dist;
+    const DensePlan& DP = cx->dl_plan;
+    if (cx->ensure(d.fl_cntb, u64(R) * NB * 4 + 16) || cx->ensure(d.fl_mid, nmid * 8 + 16) ||
+        cx->ensure(cx->dl_lower, u64(R) * xw * 4 + 16))
+      return dev_fail("fused schedule buffers");
+    ProfScope ps_(cx, KID_DL_FIRST);
+    hipLaunchKernelGGL(k_fl_counts, dim3(NB), dim3(256), 0, cx->stream, cx->dl_pbs.as<unsigned long long>(), nwb, R, DP,
+                       d.fl_cntb.as<u32>());
+    hipLaunchKernelGGL(k_fl_prefix, dim3(1), dim3(kDThreads), 0, cx->stream, static_cast<const u32*>(d.fl_cntb.as<u32>()),
+                       R, DP, xw, cx->dl_lower.as<u32>(), static_cast<const unsigned long long*>(cx->dl_pbs.as<unsigned long long>()),
+                       nwb, nw, d.fl_mid.as<u64>());
+    G_HIP(hipGetLastError());
+  }
+  {
+    gcz_dist_state& d0 = *ctx[0]->dist;
+    if (!d0.h_mid && hipHostMalloc((void**)&d0.h_mid, size_t(kMaxRanks) * (kMaxRanks + 5) * 8, hipHostMallocDefault) != hipSuccess)
+      return dev_fail("fused schedule staging");
+    if (!ev_mid) G_HIP(hipEventCreateWithFlags(&ev_mid, hipEventDisableTiming));
+    G_HIP(hipMemcpyAsync(d0.h_mid, d0.fl_mid.ptr, nmid * 8, hipMemcpyDeviceToHost, ctx[0]->stream));
+    G_HIP(hipEventRecord(ev_mid, ctx[0]->stream));
+  }
+  // B1 (as dense_leaves): the r-first codes, their position bitmap and local ranks, G in code order
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    const int r = rank[i];
+    const DensePlan& DP = cx->dl_plan;
+    Header* h = cx->hdr.as<Header>();
+    const u64 nfb = (DP.S + 63) / 64, t = scan_tiles(nfb + 1);
+    if (cx->ensure(cx->dl_lh, ncodes * 4 + 16) || cx->ensure(cx->dl_list, std::min<u64>(DP.S, ncodes) * 4 + 16) ||
+        cx->ensure(cx->dl_pos, (u64(NB) + xw) * 4 + 64))
+      return dev_fail("dense leaf buffers");
+    u32* bcnt = cx->dl_pos.as<u32>();
+    u32* xv = bcnt + NB;   // (k_dl_gq's own exchange vector: unused by this schedule)
+    const u64 t_cnt = scan_tiles(u64(NB) * DP.nch + 1);
+    u64* desc = cx->dl_desc.as<u64>() + t_cnt;
+    u32* ticket = reinterpret_cast<u32*>(desc + t) + 1;
+    {
+      ProfScope ps_(cx, KID_DL_FIRST);
+      G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_rfirst), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                int((DP.nch + 1) * 4)));
+      hipLaunchKernelGGL(k_dl_rfirst, dim3(NB), dim3(kDThreads), (DP.nch + 1) * 4, cx->stream, cx->dl_fpg.as<u32>(), DP,
+                         cx->dl_pbs.as<unsigned long long>(), nwb, r, cx->dl_fl.as<u32>(), cx->dl_fo.as<u32>(),
+                         cx->dl_lh.as<u32>(), bcnt);
+      hipLaunchKernelGGL(k_dl_fb, dim3(DP.nch), dim3(kDThreads), 0, cx->stream, cx->dl_fl.as<u32>(), cx->dl_fo.as<u32>(),
+                         DP, cx->dl_fb.as<unsigned long long>());
+      G_HIP(hipGetLastError());
+    }
+    {
+      ProfScope ps_(cx, KID_DL_FBSCAN);
+      hipLaunchKernelGGL(k_scan_excl<ScanPopc>, dim3(unsigned(t)), dim3(kScanThreads), 0, cx->stream,
+                         ScanPopc{cx->dl_fb.as<unsigned long long>()}, nfb, cx->dl_wpre.as<u32>(), desc, ticket,
+                         &h->count[0]);
+      hipLaunchKernelGGL(k_dl_gq, dim3(NB), dim3(kDThreads), 0, cx->stream, cx->dl_lh.as<u32>(), bcnt, DP,
+                         cx->dl_fb.as<unsigned long long>(), cx->dl_wpre.as<u32>(),
+                         static_cast<const u64*>(&h->count[0]), cx->dl_list.as<u32>(), xv, cx->dl_pw.as<u32>(),
+                         cx->leaves_out.as<u64>(), static_cast<const u64*>(cx->dl_pb.as<u64>() + nw));
+      G_HIP(hipGetLastError());
+    }
+  }
+  // ---- the mid-build read: the path, the all-to-all sizes, the relay plan
+  G_RC(event_sync(ev_mid));
+  const u64* hm = ctx[0]->dist->h_mid;
+  std::vector<u64> M(size_t(R) * R), c(R), off(R + 1, 0);
+  {
+    u64 st = 0;
+    for (int s = 0; s < R; ++s) {
+      const u64* v = hm + size_t(s) * (4 + R);
+      st |= v[0] | v[2];   // a non-ACGT strand (the dense level does not apply), repetitive data
+      for (int q = 0; q < R; ++q) M[size_t(s) * R + q] = v[4 + q];
+      c[s] = hm[size_t(R) * (4 + R) + s];
+      off[s + 1] = off[s] + c[s];
+    }
+    if (st) return GCZ_OK;   // every rank decides alike from the same words: the general schedule
+  }
+  const u64 total = off[R];
+  if (total > u64(kIdx)) return fail(GCZ_ERR_CAPACITY, "more than 2^29-1 unique leaves");
+  auto sent = [&](int r) { u64 t = 0; for (int q = 0; q < R; ++q) t += M[size_t(r) * R + q]; return t; };
+  auto recvd = [&](int r) { u64 t = 0; for (int q = 0; q < R; ++q) t += M[size_t(q) * R + r]; return t; };
+  std::vector<Bkt2Plan> b2(R);
+  for (int s = 0; s < R; ++s)
+    if (!owner_two_pass_plan(recvd(s), key_bits, b2[s])) return GCZ_OK;   // (every rank sees every owner's size)
+  auto displ_recv = [&](int r) {   // source segments of owner r's receive buffer
+    Displ Dd{};
+    u64 o = 0;
+    for (int q = 0; q < R; ++q) { Dd.d[q] = o; o += M[size_t(q) * R + r]; }
+    for (int q = R; q <= kMaxRanks; ++q) Dd.d[q] = o;
+    return Dd;
+  };
+  auto displ_send = [&](int r) {   // destination segments of rank r's send buffer
+    Displ Dd{};
+    u64 o = 0;
+    for (int q = 0; q < R; ++q) { Dd.d[q] = o; o += M[size_t(r) * R + q]; }
+    for (int q = R; q <= kMaxRanks; ++q) Dd.d[q] = o;
+    return Dd;
+  };
+  // the leaf relay (dense_leaves): piece q of every G array to rank q, then everyone's pieces to all
+  auto pc = [&](int r, int q) { return c[r] * u64(q) / u64(R); };
+  std::vector<u64> M1(size_t(R) * R), T(R, 0), M2(size_t(R) * R), sd2(size_t(R) * R, 0), rd2(size_t(R) * R);
+  for (int r = 0; r < R; ++r)
+    for (int q = 0; q < R; ++q) {
+      M1[size_t(r) * R + q] = pc(r, q + 1) - pc(r, q);
+      T[q] += M1[size_t(r) * R + q];
+    }
+  for (int q = 0; q < R; ++q)
+    for (int dd = 0; dd < R; ++dd) {
+      M2[size_t(q) * R + dd] = T[q];
+      u64 o = 0;
+      for (int q2 = 0; q2 < q; ++q2) o += T[q2];
+      rd2[size_t(dd) * R + q] = o;
+    }
+  DlRelay relay{};
+  {
+    u64 o = 0;
+    for (int q = 0; q < R; ++q)
+      for (int r = 0; r < R; ++r) {
+        const size_t sg = size_t(r) * R + q;
+        relay.seg_src[sg] = o;
+        relay.seg_dst[sg] = off[r] + pc(r, q);
+        relay.seg_len[sg] = M1[sg];
+        o += M1[sg];
+      }
+    for (int r = 0; r <= R; ++r) relay.off[r] = off[r];
+  }
+  // owner-side tables and buffers
+  std::vector<OwnTab> otab(NL);
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    gcz_dist_state& d = *cx->dist;
+    const int r = rank[i];
+    const u64 nr = recvd(r);
+    const u64 cap = std::max<u64>(256, next_pow2(2 * nr));
+    const LevelTab lt = plan_table(d.owntab.ptr, cap, key_bits, std::max<u64>(nr, 2), child_bits, true, 0);
+    if (!lt.packed) return fail(GCZ_ERR_CAPACITY, "fused schedule: owner keys do not pack");
+    Bkt2Plan& bp = b2[r];
+    bp.T = lt.pt;
+    const u64 nfine = (u64(1) << bp.b1) * bp.nslice;
+    const size_t cd = size_t(R) * kFlSeg * 8;
+    if (cx->ensure(d.rkey, nr * 8 + 16) || cx->ensure(d.oslot, nr * 4 + 16) || cx->ensure(d.rflag, nr + 32) ||
+        cx->ensure(d.olist, nr * 4 + 16) || cx->ensure(d.owntab, cap * 8) || cx->ensure(d.oids, cap * 4) ||
+        cx->ensure(d.ob_seg, bp.G * kPartChunk * 8) || cx->ensure(d.ob_rt, bp.G * ((u64(1) << bp.b1) + 1) * 4 + 16) ||
+        cx->ensure(d.ob_rec2, nfine * kFineCap * 8) || cx->ensure(d.ob_fo, nfine * ((u64(1) << bp.b2) + 1) * 4 + 16) ||
+        cx->ensure(d.scval, cd) || cx->ensure(d.rcval, cd) || cx->ensure(d.rdval, cd) || cx->ensure(d.sdval, cd) ||
+        cx->ensure(d.fl_g3, size_t(R) * kMaxRanks * 8 + 16) || cx->ensure(d.fl_g4, size_t(R) * 2 * 8 + 16) ||
+        cx->ensure(d.nfl, kNfListCap * 4 + 16) || cx->ensure(cx->dl_stage, T[r] * 4 + 16) ||
+        cx->ensure(cx->dl_recv, total * 4 + 16) || cx->ensure(cx->dl_gid, sizeof(DlRelay) + 16))
+      return dev_fail("fused schedule buffers");
+    bp.T.tab = d.owntab.as<u64>();
+    bp.olist = d.olist.as<u32>();
+    bp.ocnt = &d.dhdr.as<DistHdr>()->lcnt[1];
+    OwnTab& ot = otab[i];
+    ot = OwnTab{};
+    ot.tab = d.owntab.as<Slot>();
+    ot.ptab = d.owntab.as<u64>();
+    ot.ids = d.oids.as<u32>();
+    ot.mask = u32(cap - 1);
+    ot.packed = 1;
+    ot.R = u32(R);
+    ot.B = child_bits;
+    ot.sh = u32(R) + 2;
+    ot.nolocal = 1;
+    G_HIP(hipMemsetAsync(d.scval.ptr, 0, cd, cx->stream));   // C / D slot counts (and records)
+    G_HIP(hipMemsetAsync(d.rdval.ptr, 0, cd, cx->stream));
+    // the relay table, staged in pinned memory the context owns
+    if (!d.h_relay && hipHostMalloc((void**)&d.h_relay, sizeof(DlRelay), hipHostMallocDefault) != hipSuccess)
+      return dev_fail("dense leaf relay staging");
+    *d.h_relay = relay;
+    G_HIP(hipMemcpyAsync(cx->dl_gid.ptr, d.h_relay, sizeof(DlRelay), hipMemcpyHostToDevice, cx->stream));
+  }
+  // ---- R2: layer-0 keys to their owners | leaf G arrays, relay 1
+  {
+    std::vector<const void*> sk, sg;
+    std::vector<void*> rk, rg;
+    for (gcz_ctx* cx : ctx) {
+      sk.push_back(cx->dist->skey.ptr);
+      rk.push_back(cx->dist->rkey.ptr);
+      sg.push_back(cx->dl_list.ptr);
+      rg.push_back(cx->dl_stage.ptr);
+    }
+    hipEvent_t e0{};
+    ctx[0]->prof_begin(KID_EXCHANGE, e0);
+    G_RC(x_group("R2 layer-0 keys to owners | leaf G arrays, relay 1",
+                 {xop_a2a(M, R, false, 8, sk, rk), xop_a2a(M1, R, false, 4, sg, rg)}));
+    ctx[0]->prof_end(KID_EXCHANGE, e0);
+  }
+  // owners: the two-pass hash-cons of their records (first = lowest receive index: the sources
+  // send in position order and arrive in rank order), then their not-first counts per source
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    gcz_dist_state& d = *cx->dist;
+    const int r = rank[i];
+    const u64 nr = recvd(r);
+    const Bkt2Plan& bp = b2[r];
+    const u64 nfine = (u64(1) << bp.b1) * bp.nslice;
+    u32* ovf = &cx->hdr.as<Header>()->overflow;
+    ProfScope ps_(cx, KID_OWNER);
+    G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_ob_part), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              int(kPartChunk * 8)));
+    G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_bkt_fine), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              int(kFineCap * 8)));
+    hipLaunchKernelGGL(k_ob_part, dim3(unsigned(bp.G)), dim3(kBktThreads), size_t(kPartChunk) * 8, cx->stream,
+                       d.rkey.as<u64>(), nr, bp, child_bits, d.ob_seg.as<u64>(), d.ob_rt.as<u32>(), d.rflag.as<unsigned char>());
+    hipLaunchKernelGGL(k_bkt_fine, dim3(unsigned(nfine)), dim3(kBktThreads), size_t(kFineCap) * 8, cx->stream,
+                       d.ob_seg.as<u64>(), d.ob_rt.as<u32>(), bp, d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(),
+                       static_cast<Header*>(nullptr), static_cast<const u64*>(nullptr), nr, ovf);
+    hipLaunchKernelGGL(k_bkt_dedupe2<true>, dim3(unsigned(u64(1) << (bp.b1 + bp.b2))), dim3(kBktThreads), 0, cx->stream,
+                       d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(), bp, d.oslot.as<u32>(),
+                       Marks{d.rflag.as<unsigned char>(), nullptr}, static_cast<Header*>(nullptr),
+                       static_cast<const u64*>(nullptr), nr, ovf);
+    DistHdr* dh = d.dhdr.as<DistHdr>();
+    hipLaunchKernelGGL(k_fl_ownnf, dim3(64), dim3(256), 0, cx->stream, static_cast<const u32*>(d.olist.as<u32>()),
+                       static_cast<const u32*>(&dh->lcnt[1]), displ_recv(r), u32(R), dh->fl_onf);
+    G_HIP(hipGetLastError());
+  }
+  // ---- R3: owner replies | leaf G arrays, relay 2 | the owners' not-first counts
+  {
+    std::vector<const void*> sf, sg, sn;
+    std::vector<void*> rf, rg, rn;
+    for (gcz_ctx* cx : ctx) {
+      gcz_dist_state& d = *cx->dist;
+      sf.push_back(d.rflag.ptr);
+      rf.push_back(d.sflag.ptr);
+      sg.push_back(cx->dl_stage.ptr);
+      rg.push_back(cx->dl_recv.ptr);
+      sn.push_back(d.dhdr.as<DistHdr>()->fl_onf);
+      rn.push_back(d.fl_g3.ptr);
+    }
+    Transport::XOp relay2;
+    relay2.M = M2;
+    relay2.elem = 4;
+    relay2.sd = sd2;
+    relay2.rd = rd2;
+    relay2.send = sg;
+    relay2.recv = rg;
+    hipEvent_t e0{};
+    ctx[0]->prof_begin(KID_EXCHANGE, e0);
+    G_RC(x_group("R3 owner replies | leaf G arrays, relay 2 | not-first counts",
+                 {xop_a2a(M, R, true, 1, sf, rf), relay2, xop_allgather(R, u64(R), 8, sn, rn)}));
+    ctx[0]->prof_end(KID_EXCHANGE, e0);
+  }
+  // senders: layer-0 id offsets, the replies -> global flags, look-ahead, local ranks of the
+  // globally-first pairs, C records of the shared keys
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    gcz_dist_state& d = *cx->dist;
+    const int r = rank[i];
+    Header* h = cx->hdr.as<Header>();
+    DistHdr* dh = d.dhdr.as<DistHdr>();
+    const u64 ns = sent(r), p = P.count(r, 1);
+    const Displ SD = displ_send(r);
+    ProfScope ps_(cx, KID_IDS);
+    hipLaunchKernelGGL(k_fl_offs, dim3(1), dim3(64), 0, cx->stream, static_cast<const u64*>(d.fl_g3.as<u64>()), u32(R),
+                       pairs, u32(r), dh->fl_offs);
+    auto tiles = [](u64 x) { return dim3(unsigned(std::max<u64>(1, (x + kTile - 1) / kTile))); };
+    hipLaunchKernelGGL(k_dist_flags, tiles(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
+                       d.sflag.as<unsigned char>(), d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(), SD, u32(R),
+                       &dh->sync2[1], d.clist.as<u32>(), &dh->lcnt[0], d.nfl.as<u32>(), &dh->nnf);
+    hipLaunchKernelGGL(k_lookahead, dim3(unsigned(std::max<u64>(1, ((p + 1) / 2 + kBlock - 1) / kBlock))), dim3(kBlock), 0,
+                       cx->stream, static_cast<const unsigned char*>(d.gmul.as<unsigned char>()), p, &dh->fl_r4[0]);
+    hipLaunchKernelGGL((k_dist_rank<uint2>), tiles(p), dim3(kBlock), 0, cx->stream, d.gnf.as<unsigned char>(),
+                       static_cast<const u64*>(&h->count[kLayerSlot]), d.gid.as<u32>(), d.ddesc.as<u64>(), &dh->ticket,
+                       &dh->sync2[0], static_cast<const uint2*>(nullptr), static_cast<uint2*>(nullptr),
+                       static_cast<const u32*>(d.nfl.as<u32>()), static_cast<const u32*>(&dh->nnf));
+    hipLaunchKernelGGL(k_fl_cvals, dim3(16), dim3(256), 0, cx->stream, static_cast<const u32*>(d.clist.as<u32>()),
+                       static_cast<const u32*>(&dh->lcnt[0]), static_cast<const u32*>(d.sidx.as<u32>()), SD, u32(R),
+                       static_cast<const u32*>(d.gid.as<u32>()), static_cast<const u64*>(dh->fl_offs), u32(r),
+                       d.scval.as<u64>(), &dh->fl_bad);
+    // R4's vector {look-ahead pairs, failure}: the failure word so far (a C slot overflow)
+    hipLaunchKernelGGL(k_fl_r4pack, dim3(1), dim3(1), 0, cx->stream, dh);
+    G_HIP(hipGetLastError());
+  }
+  // ---- R4: C (first holders' ids to owners) | look-ahead + failures
+  {
+    std::vector<const void*> sc, sv;
+    std::vector<void*> rc, rv;
+    for (gcz_ctx* cx : ctx) {
+      gcz_dist_state& d = *cx->dist;
+      sc.push_back(d.scval.ptr);
+      rc.push_back(d.rcval.ptr);
+      sv.push_back(d.dhdr.as<DistHdr>()->fl_r4);
+      rv.push_back(d.fl_g4.ptr);
+    }
+    hipEvent_t e0{};
+    ctx[0]->prof_begin(KID_EXCHANGE, e0);
+    G_RC(x_group("R4 C ids to owners | look-ahead + status",
+                 {xop_fixed(R, kFlSeg, 8, sc, rc), xop_allgather(R, 2, 8, sv, rv)}));
+    ctx[0]->prof_end(KID_EXCHANGE, e0);
+  }
+  // the leaf level's global ids and words (the relay has landed); owners: C -> D records
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    gcz_dist_state& d = *cx->dist;
+    const int r = rank[i];
+    const DensePlan& DP = cx->dl_plan;
+    Header* h = cx->hdr.as<Header>();
+    DistHdr* dh = d.dhdr.as<DistHdr>();
+    hipLaunchKernelGGL(k_fl_guard, dim3(1), dim3(1), 0, cx->stream, static_cast<const u64*>(d.fl_g4.as<u64>()), u32(R),
+                       &dh->fl_guard);
+    {
+      ProfScope ps_(cx, KID_DL_IDS);
+      G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_ids_mr), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                int(RB * 4)));
+      hipLaunchKernelGGL(k_dl_ids_mr, dim3(NB), dim3(kDThreads), RB * 4, cx->stream, cx->dl_rec.as<u32>(),
+                         cx->dl_off.as<u32>(), DP, cx->dl_pbs.as<unsigned long long>(), nwb, cx->dl_lower.as<u32>(), xw,
+                         static_cast<const u32*>(cx->dl_recv.as<u32>()), cx->dl_gid.as<DlRelay>(), R, r,
+                         cx->dl_idrec.as<u32>());
+      if (c[r] && !dl_rleaves_sparse(c[r], DP.S))   // (sparse: k_dl_gq wrote them)
+        hipLaunchKernelGGL(k_dl_rleaves, dim3(unsigned((DP.S + 255) / 256)), dim3(256), 0, cx->stream,
+                           cx->dl_fb.as<unsigned long long>(), cx->dl_wpre.as<u32>(), cx->dl_pw.as<u32>(), DP,
+                           cx->leaves_out.as<u64>());
+      G_HIP(hipGetLastError());
+    }
+    if (int rc = cx->dense_phase_b(las[i], h, nullptr, nullptr, true))
+      return rc == GCZ_ERR_DEVICE ? dev_fail("dense leaves") : rc;
+    ProfScope ps_(cx, KID_OWNER);
+    const Displ RD = displ_recv(r);
+    hipLaunchKernelGGL(k_fl_setid, dim3(16), dim3(256), 0, cx->stream, static_cast<const u64*>(d.rcval.as<u64>()), RD,
+                       u32(R), static_cast<const u32*>(d.oslot.as<u32>()), otab[i], &dh->fl_bad);
+    hipLaunchKernelGGL(k_fl_getid, dim3(64), dim3(256), 0, cx->stream, static_cast<const u32*>(d.olist.as<u32>()),
+                       static_cast<const u32*>(&dh->lcnt[1]), static_cast<const u32*>(d.oslot.as<u32>()), RD, u32(R),
+                       otab[i], d.rdval.as<u64>(), &dh->fl_bad);
+    G_HIP(hipGetLastError());
+  }
+  // ---- R5: D (owners forward the ids to the other holders)
+  {
+    std::vector<const void*> sd;
+    std::vector<void*> rd;
+    for (gcz_ctx* cx : ctx) {
+      sd.push_back(cx->dist->rdval.ptr);
+      rd.push_back(cx->dist->sdval.ptr);
+    }
+    hipEvent_t e0{};
+    ctx[0]->prof_begin(KID_EXCHANGE, e0);
+    G_RC(x_group("R5 D ids to holders", {xop_fixed(R, kFlSeg, 8, sd, rd)}));
+    ctx[0]->prof_end(KID_EXCHANGE, e0);
+  }
+  // layer 0 with the global leaf ids, then the direct subtrees of levels 1 .. G-1 (guarded: they
+  // run only when layer 1 is direct everywhere and no rank failed)
+  std::vector<u32*> cur_in(NL), cur_out(NL);
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    gcz_dist_state& d = *cx->dist;
+    const int r = rank[i];
+    DistHdr* dh = d.dhdr.as<DistHdr>();
+    const u64 n = P.count(r, 0), p = P.count(r, 1);
+    {
+      ProfScope ps_(cx, KID_IDS);
+      hipLaunchKernelGGL(k_fl_dvals, dim3(16), dim3(256), 0, cx->stream, static_cast<const u64*>(d.sdval.as<u64>()),
+                         displ_send(r), u32(R), static_cast<const u32*>(d.sidx.as<u32>()), d.gid.as<u32>(), &dh->fl_bad);
+      G_HIP(hipGetLastError());
+    }
+    {
+      ProfScope ps_(cx, KID_L0);
+      hipLaunchKernelGGL(k_fl_l0, dim3(unsigned(std::max<u64>(1, (p + 4 * kBlock - 1) / (4 * kBlock)))), dim3(kBlock), 0,
+                         cx->stream, static_cast<const u32*>(cx->wa.as<u32>()), n, p,
+                         static_cast<const unsigned char*>(d.gnf.as<unsigned char>()),
+                         static_cast<const u32*>(d.gid.as<u32>()), static_cast<const u64*>(dh->fl_offs), u32(r),
+                         cx->nodes_out.as<uint2>() + node_base[i][0], cx->wb.as<u32>());
+      G_HIP(hipGetLastError());
+    }
+    cur_in[i] = cx->wb.as<u32>();
+    cur_out[i] = cx->wa.as<u32>();
+  }
+  slice_off.assign(D + 1, std::vector<u64>(R, 0));
+  slice_cnt.assign(D + 1, std::vector<u64>(R, 0));
+  for (int s = 0; s < R; ++s) { slice_off[0][s] = off[s]; slice_cnt[0][s] = c[s]; }
+  for (int k = 1; k < G;) {
+    const int nlev = std::min(kDirectLog, G - k);
+    for (int i = 0; i < NL; ++i) {
+      const int r = rank[i];
+      if (P.count(r, k) == 0) continue;
+      DirectPlan dp{};
+      for (int q = 0; q <= nlev; ++q) dp.n[q] = P.count(r, k + q);
+      for (int q = 0; q < nlev; ++q) {
+        dp.layer_off[k + q] = node_base[i][k + q];
+        dp.id_off[k + q] = u32(P.start(r, k + q + 1));
+      }
+      if (ctx[i]->direct_levels(cur_in[i], k, nlev, dp, cur_out[i], ctx[i]->hdr.as<Header>(), DirectRemap{},
+                                &ctx[i]->dist->dhdr.as<DistHdr>()->fl_guard, 0))
+        return dev_fail("direct levels");
+    }
+    for (int q = 0; q < nlev; ++q) {
+      for (int s = 0; s < R; ++s) {
+        slice_off[k + q + 1][s] = P.start(s, k + q + 1);
+        slice_cnt[k + q + 1][s] = P.count(s, k + q + 1);
+      }
+      info.layer_size[k + q] = P.nk[k + q + 1];
+    }
+    for (int i = 0; i < NL; ++i) std::swap(cur_in[i], cur_out[i]);
+    k += nlev;
+  }
+  // ---- R6 / R7: the top on rank 0, the final vectors; any failure discards the attempt
+  bool failed = false;
+  G_RC(finish_top(G, true, P.nk[G], cur_in, dcur, true, &failed));
+  if (failed) return GCZ_OK;   // (the general schedule rebuilds from scratch)
+  const u64* gf = ctx[0]->dist->h_gathf;
+  u64 l0 = 0;
+  for (int s = 0; s < R; ++s) {
+    slice_off[1][s] = l0;
+    slice_cnt[1][s] = gf[size_t(s) * kFinalWords + 3];
+    l0 += slice_cnt[1][s];
+  }
+  info.layer_size[0] = l0;
+  info.n_leaves = total;
+  info.leaf_path = 1;
+  info.repetitive = 0;
+  *taken = true;
+  return GCZ_OK;
+}
+
+// The top of the tree (every build schedule): the words of level Gx gathered to rank 0, which
+// runs the remaining levels (direct subtrees, hash-consed levels, the fused tail), then the
+// final vectors allgathered and the one host sync of the build's end.  *failed: some rank's
+// final vector flags a table overflow (general schedule: rebuild with wide tables) or, with fl
+// (the fused schedule: its failure words in the vector), a failed attempt of that schedule.
+int gcz_group::finish_top(int Gx, bool direct, u64 prev_total, const std::vector<u32*>& cur_in, std::vector<u64>& dcur,
+                          bool fl, bool* failed) {
+  const int R = world, NL = int(ctx.size());
+  const DistPlan& P = plan;
+  const int D = P.D;
+  *failed = false;
+  // ---- gather the last distributed level to rank 0, finish the top there ----
+  {
+    std::vector<u64> cnt(R);
+    for (int s = 0; s < R; ++s) cnt[s] = P.count(s, Gx);
+    std::vector<const void*> sv;
+    void* recv0 = nullptr;
+    for (int i = 0; i < NL; ++i) {
+      sv.push_back(cur_in[i]);
+      if (rank[i] == 0) recv0 = ctx[i]->dist->tail_in.ptr;
+    }
+    if (!recv0) recv0 = ctx[0]->dist->tail_in.ptr;   // not used off rank 0
+    G_RC(x_gather0("top words to rank 0", cnt, 4, sv, recv0));
+  }
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    Header* h = cx->hdr.as<Header>();
+    DistHdr* dh = cx->dist->dhdr.as<DistHdr>();
+    const bool tail = rank[i] == 0;
+    if (tail) {
+      u32* in = cx->dist->tail_in.as<u32>();
+      u32* bufs[2] = {cx->wa.as<u32>(), cx->wb.as<u32>()};
+      int nb = 0;
+      u64 n = P.nk[Gx];
+      hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, cx->stream, &dh->cell[Gx], direct ? n : ~0ull);
+      u64 bound = prev_total;
+      bool tail_done = false;
+      for (int k = Gx; k < D; ++k) {
+        if (n <= u64(kTailMaxN) && cx->use_tail) {   // the rest in one launch
+          const u64* pc = k == Gx ? &dh->cell[Gx] : &h->count[kLayerSlot + k - 1];
+          if (cx->tail_levels(in, n, pc, k, D, node_base[i], h)) return dev_fail("tail levels");
+          tail_done = true;
+          break;
+        }
+        if (direct) {   // host-known (every later level too): direct subtrees, ids = positions
+          DirectPlan dp{};
+          int nlev = 0;
+          u64 m = n;
+          dp.n[0] = n;
+          while (nlev < kDirectLog && k + nlev < D && (m > u64(kTailMaxN) || !cx->use_tail)) {
+            dp.layer_off[k + nlev] = node_base[i][k + nlev];
+            m = P.nk[k + nlev + 1];
+            dp.n[++nlev] = m;
+          }
+          if (cx->direct_levels(in, k, nlev, dp, bufs[nb], h)) return dev_fail("tail direct levels");
+          in = bufs[nb];
+          nb ^= 1;
+          n = m;
+          bound = m;
+          k += nlev - 1;
+          continue;
+        }
+        NodeLevel na;
+        na.k = k;
+        na.in = in;
+        na.n = n;
+        na.p = P.nk[k + 1];
+        na.words = bufs[nb];
+        na.out = cx->nodes_out.as<uint2>() + node_base[i][k];
+        na.count = &h->count[kLayerSlot + k];
+        na.bound = bound;
+        na.prev_marks = k > Gx;
+        na.pcount = k == Gx ? &dh->cell[Gx] : &h->count[kLayerSlot + k - 1];
+        na.desc = cx->desc.as<u64>() + dcur[i];
+        dcur[i] += (na.p + scan_tile(na.p) - 1) / scan_tile(na.p);
+        na.ticket = &h->ticket[kLayerSlot + k];
+        if (cx->node_level(na, h)) return dev_fail("tail level");
+        in = bufs[nb];
+        nb ^= 1;
+        n = na.p;
+        bound = na.p;
+      }
+      if (!tail_done) hipLaunchKernelGGL(k_root, dim3(1), dim3(1), 0, cx->stream, in, h);
+    }
+    if (fl)
+      hipLaunchKernelGGL(k_fl_final, dim3(1), dim3(1), 0, cx->stream, h, dh, Gx, D, int(tail), &dh->fl_bad,
+                         &dh->fl_guard, dh->fl_offs, u32(R));
+    else
+      hipLaunchKernelGGL(k_dist_final, dim3(1), dim3(1), 0, cx->stream, h, dh, Gx, D, int(tail));
+    G_HIP(hipGetLastError());
+    G_HIP(hipEventRecord(cx->ev_stop, cx->stream));
+  }
+  {
+    std::vector<const void*> s;
+    std::vector<void*> rv;
+    for (gcz_ctx* cx : ctx) {
+      s.push_back(cx->dist->dhdr.as<DistHdr>()->final_vec);
+      rv.push_back(cx->dist->gathf.ptr);
+    }
+    G_RC(x_allgather("final vectors", kFinalWords * 8, s, rv));
+  }
+  gcz_dist_state& d0 = *ctx[0]->dist;
+  G_HIP(hipMemcpyAsync(d0.h_gathf, d0.gathf.ptr, size_t(R) * kFinalWords * 8, hipMemcpyDeviceToHost,
+                       ctx[0]->stream));
+  G_RC(host_sync());
+  int fo = 0;
+  for (int s = 0; s < R; ++s) fo |= int(d0.h_gathf[size_t(s) * kFinalWords]);
+  if (fo) {
+    *failed = true;
+    return GCZ_OK;
+  }
+  const u64* f0 = d0.h_gathf;   // rank 0's vector
+  info.root = u32(f0[1]);
+  for (int k = Gx; k < D; ++k) {
+    info.layer_size[k] = f0[4 + k];
+    slice_off[k + 1][0] = 0;
+    slice_cnt[k + 1][0] = f0[4 + k];
+  }
+  return GCZ_OK;
+}
+
 int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64 S, int L) {
   info = gcz_info{};
   info.L = L;
@@ -1618,6 +2433,13 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     }
   }
 
+  // the fused leaf + layer-0 schedule where it applies (the general schedule below otherwise,
+  // and after an attempt of it that some rank had to discard)
+  {
+    bool taken = false;
+    G_RC(build_fast(bases, d_leaves, L, leaf_cap, &taken));
+    if (taken) return build_done();
+  }
   std::vector<RankLevel> lv(NL);
   for (int attempt = 0;; ++attempt) {
     if (attempt > 8) return fail(GCZ_ERR_CAPACITY, "hash table overflow persists");
@@ -1808,6 +2630,7 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     for (int i = 0; i < NL; ++i) leaf_offs[i] = u32(off[rank[i]]);
     info.n_leaves = total;
     info.leaf_path = dense ? 1u : 0u;
+    info.repetitive = any_predup ? 1u : 0u;
     // The repetitive-data decision is the OR over the ranks' probes (each sampled only a
     // prefix of its own slice): every rank's node levels take the same path from here.
     if (any_predup) {
@@ -1953,111 +2776,20 @@ int gcz_group::build(const void* const* d_bases, const u64* const* d_leaves, u64
     if (retry) continue;
 
     // ---- gather the last distributed level to rank 0, finish the top there ----
-    {
-      std::vector<u64> cnt(R);
-      for (int s = 0; s < R; ++s) cnt[s] = P.count(s, Gx);
-      std::vector<const void*> sv;
-      void* recv0 = nullptr;
-      for (int i = 0; i < NL; ++i) {
-        sv.push_back(cur_in[i]);
-        if (rank[i] == 0) recv0 = ctx[i]->dist->tail_in.ptr;
-      }
-      if (!recv0) recv0 = ctx[0]->dist->tail_in.ptr;   // not used off rank 0
-      G_RC(x_gather0("top words to rank 0", cnt, 4, sv, recv0));
-    }
-    for (int i = 0; i < NL; ++i) {
-      gcz_ctx* cx = ctx[i];
-      Header* h = cx->hdr.as<Header>();
-      DistHdr* dh = cx->dist->dhdr.as<DistHdr>();
-      const bool tail = rank[i] == 0;
-      if (tail) {
-        u32* in = cx->dist->tail_in.as<u32>();
-        u32* bufs[2] = {cx->wa.as<u32>(), cx->wb.as<u32>()};
-        int nb = 0;
-        u64 n = P.nk[Gx];
-        hipLaunchKernelGGL(k_set_u64, dim3(1), dim3(1), 0, cx->stream, &dh->cell[Gx], direct ? n : ~0ull);
-        u64 bound = prev_total;
-        bool tail_done = false;
-        for (int k = Gx; k < D; ++k) {
-          if (n <= u64(kTailMaxN) && cx->use_tail) {   // the rest in one launch
-            const u64* pc = k == Gx ? &dh->cell[Gx] : &h->count[kLayerSlot + k - 1];
-            if (cx->tail_levels(in, n, pc, k, D, node_base[i], h)) return dev_fail("tail levels");
-            tail_done = true;
-            break;
-          }
-          if (direct) {   // host-known (every later level too): direct subtrees, ids = positions
-            DirectPlan dp{};
-            int nlev = 0;
-            u64 m = n;
-            dp.n[0] = n;
-            while (nlev < kDirectLog && k + nlev < D && (m > u64(kTailMaxN) || !cx->use_tail)) {
-              dp.layer_off[k + nlev] = node_base[i][k + nlev];
-              m = P.nk[k + nlev + 1];
-              dp.n[++nlev] = m;
-            }
-            if (cx->direct_levels(in, k, nlev, dp, bufs[nb], h)) return dev_fail("tail direct levels");
-            in = bufs[nb];
-            nb ^= 1;
-            n = m;
-            bound = m;
-            k += nlev - 1;
-            continue;
-          }
-          NodeLevel na;
-          na.k = k;
-          na.in = in;
-          na.n = n;
-          na.p = P.nk[k + 1];
-          na.words = bufs[nb];
-          na.out = cx->nodes_out.as<uint2>() + node_base[i][k];
-          na.count = &h->count[kLayerSlot + k];
-          na.bound = bound;
-          na.prev_marks = k > Gx;
-          na.pcount = k == Gx ? &dh->cell[Gx] : &h->count[kLayerSlot + k - 1];
-          na.desc = cx->desc.as<u64>() + dcur[i];
-          dcur[i] += (na.p + scan_tile(na.p) - 1) / scan_tile(na.p);
-          na.ticket = &h->ticket[kLayerSlot + k];
-          if (cx->node_level(na, h)) return dev_fail("tail level");
-          in = bufs[nb];
-          nb ^= 1;
-          n = na.p;
-          bound = na.p;
-        }
-        if (!tail_done) hipLaunchKernelGGL(k_root, dim3(1), dim3(1), 0, cx->stream, in, h);
-      }
-      hipLaunchKernelGGL(k_dist_final, dim3(1), dim3(1), 0, cx->stream, h, dh, Gx, D, int(tail));
-      G_HIP(hipGetLastError());
-      G_HIP(hipEventRecord(cx->ev_stop, cx->stream));
-    }
-    {
-      std::vector<const void*> s;
-      std::vector<void*> rv;
-      for (gcz_ctx* cx : ctx) {
-        s.push_back(cx->dist->dhdr.as<DistHdr>()->final_vec);
-        rv.push_back(cx->dist->gathf.ptr);
-      }
-      G_RC(x_allgather("final vectors", kFinalWords * 8, s, rv));
-    }
-    gcz_dist_state& d0 = *ctx[0]->dist;
-    G_HIP(hipMemcpyAsync(d0.h_gathf, d0.gathf.ptr, size_t(R) * kFinalWords * 8, hipMemcpyDeviceToHost,
-                         ctx[0]->stream));
-    G_RC(host_sync());
-    int fo = 0;
-    for (int s = 0; s < R; ++s) fo |= int(d0.h_gathf[size_t(s) * kFinalWords]);
+    bool fo = false;
+    G_RC(finish_top(Gx, direct, prev_total, cur_in, dcur, false, &fo));
     if (fo) {
       allow_packed = false;
       continue;
     }
-    const u64* f0 = d0.h_gathf;   // rank 0's vector
-    info.root = u32(f0[1]);
-    for (int k = Gx; k < D; ++k) {
-      info.layer_size[k] = f0[4 + k];
-      slice_off[k + 1][0] = 0;
-      slice_cnt[k + 1][0] = f0[4 + k];
-    }
     break;
   }
-  info.n_layers = D;
+  return build_done();
+}
+
+// The summary of a finished build (any schedule) into the group's and every context's info.
+int gcz_group::build_done() {
+  info.n_layers = plan.D;
   double ms = 0;
   for (gcz_ctx* cx : ctx) {
     float t = 0.f;
@@ -2086,7 +2818,7 @@ int gcz_group::assemble(gcz_ctx* dst) {
   for (int i = 0; i < NL; ++i)
     if (rank[i] == 0) i0 = i;
   const bool root = i0 >= 0;
-  if (root && !dst) return fail(GCZ_ERR_ARG, "assemble: rank 0 needs a destination context");
+  // (every rank has the same build status: the build's failures are decided collectively)
   if (info.status != GCZ_OK || slice_cnt.empty()) return fail(GCZ_ERR_ARG, "assemble: no finished build");
   const int D = info.n_layers;
   const u64 S = info.n_strands;
@@ -2100,11 +2832,39 @@ int gcz_group::assemble(gcz_ctx* dst) {
     }
   }
   hipStream_t st = ctx[0]->stream;
+  // rank 0's destination (a context, its arrays) is settled before any gather, and with one rank
+  // per process every rank learns the outcome from one status allgather first: a rank 0 that
+  // cannot take the tree fails the call on every rank instead of leaving the others blocked in
+  // a gather it never joins
+  int root_rc = GCZ_OK;
+  std::string root_why;
   if (root) {
-    if (dst->ensure(dst->leaves_out, S * 8 + 16) || dst->ensure(dst->nodes_out, loff[D] * 8 + 16))
-      return dev_fail("assemble: destination arrays");
-    dst->layer_off = loff;
-    if (dst->stream != st) G_HIP(hipStreamSynchronize(dst->stream));   // (its earlier work on the arrays)
+    if (!dst) {
+      root_rc = GCZ_ERR_ARG;
+      root_why = "assemble: rank 0 needs a destination context";
+    } else if (dst->ensure(dst->leaves_out, S * 8 + 16) || dst->ensure(dst->nodes_out, loff[D] * 8 + 16)) {
+      root_rc = GCZ_ERR_DEVICE;
+      root_why = "assemble: destination arrays";
+    } else {
+      dst->layer_off = loff;
+      if (dst->stream != st && hipStreamSynchronize(dst->stream) != hipSuccess) {   // (its earlier work on the arrays)
+        root_rc = GCZ_ERR_DEVICE;
+        root_why = "assemble: destination stream";
+      }
+    }
+  }
+  if (!here) {
+    gcz_dist_state& d0 = *ctx[0]->dist;
+    u64* word = &d0.dhdr.as<DistHdr>()->final_vec[0];
+    static_assert(kFinalWords >= 1, "status word");
+    G_HIP(hipMemsetAsync(word, root_rc ? 0xff : 0, 8, st));
+    G_RC(x_allgather("assemble status", 8, {word}, {d0.gath.ptr}));
+    G_HIP(hipMemcpyAsync(d0.h_gath, d0.gath.ptr, size_t(R) * 8, hipMemcpyDeviceToHost, st));
+    G_RC(host_sync());
+    for (int r = 0; r < R; ++r)
+      if (d0.h_gath[r]) return root_rc ? fail(root_rc, root_why) : fail(GCZ_ERR_DEVICE, "assemble: rank 0 cannot take the tree");
+  } else if (root_rc) {
+    return fail(root_rc, root_why);
   }
   for (int layer = -1; layer < D; ++layer) {
     auto src_of = [&](int i) -> const void* {
@@ -2301,6 +3061,26 @@ int gcz_group_xlog(const gcz_group* g, int local, uint64_t* rec, const char** na
     if (names) names[i] = x.name;
   }
   return n;
+}
+
+// The RCCL watchdog's lifecycle without a GPU or a communicator (tests/test_transport_plan.py):
+// a collective is marked pending, the watchdog fires after limit_s, then -- when build_returns --
+// the build's failure path runs (gcz_group::fail's disarm) and the process must still be alive
+// grace_s + 1 s later.  Returns 0 when it fired and the process survived (it ends with exit code
+// 70 when the build never returns, which is the other half of the contract).
+int gcz_dist_watch_selftest(int limit_s, int grace_s, int build_returns) {
+  RcclTransport t;
+  gcz_group::Watch w(&t, -1, 0);
+  w.limit_s = limit_s;
+  w.grace_s = grace_s;
+  w.begin(0, "collective #0 selftest");
+  const auto t0 = std::chrono::steady_clock::now();
+  while (!w.fired && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(limit_s + 10))
+    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  if (!w.fired) return 1;
+  if (build_returns) w.disarm();
+  std::this_thread::sleep_for(std::chrono::seconds(grace_s + 1));
+  return 0;
 }
 
 int gcz_dist_p2p_plan(int world, int me, const uint64_t* M, int reverse, uint64_t elem, const uint64_t* sd,

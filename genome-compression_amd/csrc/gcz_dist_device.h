@@ -50,6 +50,12 @@ struct DistHdr {
   u32 dcur[kMaxRanks + 1];              // ... D records per source (owner side)
   u64 cell[GCZ_MAX_LAYERS + 1];         // direct flags: n_local when the layer is direct, else ~0
   u64 final_vec[kFinalWords];           // [0] overflow, [1] root, [2] tail first layer, [4 + k] tail counts
+  // fused leaf + layer-0 schedule (gcz_dist_fast.h)
+  u64 fl_onf[kMaxRanks];                // this owner's not-first layer-0 records per source (R3's allgather)
+  u64 fl_r4[2];                         // {layer-1 pairs with two repeated children, failure} (R4's allgather)
+  u64 fl_offs[kMaxRanks + 2];           // layer-0 id offsets, [R] total, [R + 1] this rank's uniques
+  u64 fl_guard;                         // 0: layer 1 is direct on every rank and none failed
+  u32 fl_bad;                           // a C / D slot overflowed
 };
 
 struct Displ {   // segment starts of the R source (or destination) ranks in a buffer, plus the end
@@ -942,7 +948,7 @@ __global__ __launch_bounds__(kBlock) void k_dist_rank(const unsigned char* __res
       if (j < u && !st.listed(k)) {
         const u32 r = u32(j - st.nb(k));
         gid[j] = r | kLocalId;
-        out[r] = scratch[j];
+        if (out) out[r] = scratch[j];
       }
     }
     return;
@@ -957,7 +963,7 @@ __global__ __launch_bounds__(kBlock) void k_dist_rank(const unsigned char* __res
     if (j < u && ((ts.mask[e] >> lane) & 1ull)) {
       const u32 r = s_pre[e * 4 + wave] + u32(__popcll(ts.mask[e] & lt));
       gid[j] = r | kLocalId;
-      out[r] = scratch[j];
+      if (out) out[r] = scratch[j];   // (null: the fused schedule writes the nodes later, k_fl_l0)
     }
   }
 }
@@ -1039,7 +1045,8 @@ static __global__ __launch_bounds__(kBlock) void k_node_keys(const u32* __restri
                                                              u32* __restrict__ blockcnt, u32 nb,
                                                              const unsigned char* __restrict__ gmark,
                                                              unsigned char* __restrict__ gnf,
-                                                             unsigned char* __restrict__ gmul, u64* __restrict__ ddesc) {
+                                                             unsigned char* __restrict__ gmul, u64* __restrict__ ddesc,
+                                                             u32 skip_null = 0) {
   __shared__ u32 h[kMaxRanks];
   const int tid = threadIdx.x;
   // what the exchange's sender side expects zeroed for this tile (local uniques = positions):
@@ -1119,9 +1126,13 @@ static __global__ __launch_bounds__(kBlock) void k_node_keys(const u32* __restri
       const u32 v = ulw(l) == ulw(xf(r, 1, 0));
       pairs[j] = make_uint2(cl, cr);
       words[j] = make_word(u32(j), m, t, v);
-      nf[j] = kNfMaybe;
+      // skip_null (the fused schedule, whose keys carry code labels without a null code): the
+      // genome's last pair, with the null child, is the only pair of its class -- globally
+      // first and unique without an exchange
+      const bool lone = skip_null && (r & kIdx) == kIdx;
+      nf[j] = lone ? kNfDone : kNfMaybe;
       multi[j] = 0;
-      if (blockcnt) {
+      if (blockcnt && !lone) {
         const bool single = rs.prev_nf && ((pf[q].x == 0 && pm[q].x == 0) || (pf[q].y == 0 && pm[q].y == 0));
         if (!single) atomicAdd(&h[owner_of((u64(ulw(cl)) << 31) | ulw(cr), rs.R)], 1u);
       }

@@ -868,9 +868,20 @@ extern "C" {
 // The sort's device buffers for the current tree, allocated ahead (the drop-in reserves them on
 // a side thread while the tree is fetched: a first sort at 1 Gbase otherwise pays ~40 ms of
 // allocation, profiles/r04/compress_e2e.txt); gcz_sort_device calls it too (then a no-op).
-int gcz_sort_reserve(gcz_ctx* c) {
-  if (!c || c->info.status != GCZ_OK || c->info.n_layers < 1) return GCZ_ERR_ARG;
-  S_HIP(hipSetDevice(c->device));
+//
+// It runs beside gcz_fetch_host on the same context, so it reads only the tree's shape and
+// writes nothing the fetch reads: no last_error / info.status -- a failure comes back as a code
+// (and *why), and gcz_sort_device, the only caller that goes on to use the buffers, reports it.
+static int sort_reserve(gcz_ctx* c, const char** why) {
+#define R_HIP(x)                       \
+  do {                                 \
+    if ((x) != hipSuccess) {           \
+      *why = #x;                       \
+      return GCZ_ERR_DEVICE;           \
+    }                                  \
+  } while (0)
+  if (c->info.n_layers < 1) return GCZ_ERR_ARG;
+  R_HIP(hipSetDevice(c->device));
   if (!c->sortst) c->sortst = new gcz_sort_state();
   gcz_sort_state& s = *c->sortst;
   const int D = c->info.n_layers;
@@ -898,31 +909,49 @@ int gcz_sort_reserve(gcz_ctx* c) {
   matmax = std::max(matmax, 256 * ((nmax + kCsTile - 1) / kCsTile) + 1);
   const u64 tilemax = scan_tiles(matmax);
   const u64 N = c->layer_off[D];
-  int rc;
-  if ((rc = c->ensure(s.cnt, coff[D] * 4 + 16)) || (rc = c->ensure(s.newpos, coff[D] * 4 + 16)) ||
-      (rc = c->ensure(s.keys, nmax * 4 + 16)) || (rc = c->ensure(s.keys2, nmax * 4 + 16)) ||
-      (rc = c->ensure(s.vals, nmax * 4 + 16)) || (rc = c->ensure(s.vals2, nmax * 4 + 16)) ||
-      (rc = c->ensure(s.mm, size_t(D) * 8 + 16)) || (rc = c->ensure(s.nodes2, N * 8 + 16)) ||
-      (rc = c->ensure(s.leaves2, nl * 8 + 16)) || (rc = c->ensure(s.hmat, matmax * 4 + 16)) ||
-      (rc = c->ensure(s.hoff, matmax * 4 + 16)) || (rc = c->ensure(s.hrec, nwmax * 2 + 16)) ||
-      (rc = c->ensure(s.desc, tilemax * 8 + 16)))
-    return rc;
-  if ((rc = c->ensure(s.hpart, size_t(2048) * GCZ_MAX_LAYERS * 8 + 16))) return rc;
-  if (scl >= 0 && ((rc = c->ensure(s.hslot, 2 * c->info.layer_size[scl] * 4 + 16)) ||
-                   (rc = c->ensure(s.hval, 2 * c->info.layer_size[scl] * 4 + 16)) ||
-                   (rc = c->ensure(s.hbs, (u64(hnb[scl]) + 1) * 4 + 16))))
-    return rc;
-  if (!s.h_mm) S_HIP(hipHostMalloc((void**)&s.h_mm, size_t(GCZ_MAX_LAYERS) * 8, hipHostMallocDefault));
+  R_HIP(c->ensure_quiet(s.cnt, coff[D] * 4 + 16));
+  R_HIP(c->ensure_quiet(s.newpos, coff[D] * 4 + 16));
+  R_HIP(c->ensure_quiet(s.keys, nmax * 4 + 16));
+  R_HIP(c->ensure_quiet(s.keys2, nmax * 4 + 16));
+  R_HIP(c->ensure_quiet(s.vals, nmax * 4 + 16));
+  R_HIP(c->ensure_quiet(s.vals2, nmax * 4 + 16));
+  R_HIP(c->ensure_quiet(s.mm, size_t(D) * 8 + 16));
+  R_HIP(c->ensure_quiet(s.nodes2, N * 8 + 16));
+  R_HIP(c->ensure_quiet(s.leaves2, nl * 8 + 16));
+  R_HIP(c->ensure_quiet(s.hmat, matmax * 4 + 16));
+  R_HIP(c->ensure_quiet(s.hoff, matmax * 4 + 16));
+  R_HIP(c->ensure_quiet(s.hrec, nwmax * 2 + 16));
+  R_HIP(c->ensure_quiet(s.desc, tilemax * 8 + 16));
+  R_HIP(c->ensure_quiet(s.hpart, size_t(2048) * GCZ_MAX_LAYERS * 8 + 16));
+  if (scl >= 0) {
+    R_HIP(c->ensure_quiet(s.hslot, 2 * c->info.layer_size[scl] * 4 + 16));
+    R_HIP(c->ensure_quiet(s.hval, 2 * c->info.layer_size[scl] * 4 + 16));
+    R_HIP(c->ensure_quiet(s.hbs, (u64(hnb[scl]) + 1) * 4 + 16));
+  }
+  if (!s.h_mm) R_HIP(hipHostMalloc((void**)&s.h_mm, size_t(GCZ_MAX_LAYERS) * 8, hipHostMallocDefault));
   if (!s.warm) {   // this file's code object loaded now, not at the first sort's first launch
     hipLaunchKernelGGL(k_sort_warm, dim3(1), dim3(64), 0, c->stream);
-    S_HIP(hipGetLastError());
+    R_HIP(hipGetLastError());
     s.warm = true;
   }
   return GCZ_OK;
+#undef R_HIP
 }
 
+int gcz_sort_reserve(gcz_ctx* c) {
+  if (!c) return GCZ_ERR_ARG;
+  const char* why = nullptr;
+  return sort_reserve(c, &why);
+}
+
+
+
 int gcz_sort_device(gcz_ctx* c) {
-  if (int rc = gcz_sort_reserve(c)) return rc;
+  if (!c || c->info.status != GCZ_OK) return GCZ_ERR_ARG;
+  {
+    const char* why = "";
+    if (int rc = sort_reserve(c, &why)) return rc == GCZ_ERR_DEVICE ? c->fail(rc, "sort buffers", why) : rc;
+  }
   gcz_sort_state& s = *c->sortst;
   const int D = c->info.n_layers;
   const u64 nl = c->info.n_leaves;

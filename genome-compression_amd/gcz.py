@@ -36,7 +36,7 @@ class _Info(ctypes.Structure):
                 ("layer_size", ctypes.c_uint64 * MAX_LAYERS), ("error_offset", ctypes.c_uint64),
                 ("error_symbol", ctypes.c_int), ("build_ms", ctypes.c_double), ("hashed_pairs", ctypes.c_uint64),
                 ("bucketed_pairs", ctypes.c_uint64), ("leaf_path", ctypes.c_uint32), ("attempts", ctypes.c_uint32),
-                ("build_ms_all", ctypes.c_double)]
+                ("build_ms_all", ctypes.c_double), ("repetitive", ctypes.c_uint32)]
 
 
 if not os.path.exists(LIB_PATH):
@@ -128,6 +128,7 @@ _SIGS = {
                                          ctypes.POINTER(_U64), ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
     "gcz_dist_gather_plan": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_U64), _U64,
                                             ctypes.POINTER(_U64)]),
+    "gcz_dist_watch_selftest": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "gcz_dist_plan": (ctypes.c_int, [_U64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_U64), ctypes.POINTER(_U64),
                                       ctypes.POINTER(ctypes.c_int)]),
     "gcz_group_build_device_bases": (ctypes.c_int, [_P, ctypes.POINTER(_P), _U64, ctypes.c_int]),
@@ -320,7 +321,7 @@ def _info_dict(i):
             "n_strands": i.n_strands, "n_leaves": i.n_leaves,
             "layer_size": [int(i.layer_size[k]) for k in range(i.n_layers)],
             "error_offset": i.error_offset, "error_symbol": i.error_symbol, "build_ms": i.build_ms,
-            "hashed_pairs": i.hashed_pairs, "bucketed_pairs": i.bucketed_pairs, "leaf_path": i.leaf_path,
+            "hashed_pairs": i.hashed_pairs, "bucketed_pairs": i.bucketed_pairs, "leaf_path": i.leaf_path, "repetitive": i.repetitive,
             "attempts": i.attempts, "build_ms_all": i.build_ms_all}
 
 

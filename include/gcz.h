@@ -69,6 +69,8 @@ typedef struct {
   uint32_t attempts;                 /* device builds this call ran: > 1 after a rebuild (a bucket
                                         overflow, leaf-table regrowth or the wide-table fallback) */
   double build_ms_all;               /* device time of every attempt (build_ms: the last one) */
+  uint32_t repetitive;               /* the node levels took the repetitive-data path (LDS pre-dedupe;
+                                        decided by a probe of the first leaf chunk) */
 } gcz_info;
 
 /* ---- device context ---------------------------------------------------- */
@@ -265,6 +267,10 @@ GCZ_API int gcz_group_xlog(const gcz_group *g, int local, uint64_t *rec, const c
 GCZ_API int gcz_dist_p2p_plan(int world, int me, const uint64_t *M, int reverse, uint64_t elem, const uint64_t *sd,
                               const uint64_t *rd, uint64_t *out);
 GCZ_API int gcz_dist_gather_plan(int world, int me, const uint64_t *cnt, uint64_t elem, uint64_t *out);
+/* The RCCL watchdog's lifecycle without a GPU (tests): a pending collective, the watchdog fires
+ * after limit_s; build_returns != 0: the build's failure path runs and the process is still alive
+ * grace_s + 1 s later (returns 0); build_returns == 0: the process ends with exit code 70. */
+GCZ_API int gcz_dist_watch_selftest(int limit_s, int grace_s, int build_returns);
 /* Strands [s0, s1) of `rank` for an S-strand genome; G = distributed node levels. */
 GCZ_API int gcz_dist_plan(uint64_t S, int world, int rank, uint64_t *s0, uint64_t *s1, int *G);
 /* d_bases[i]: device ASCII bases of local rank i's strands ((s1 - s0) * L bytes). */

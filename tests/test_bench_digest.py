@@ -137,3 +137,52 @@ def test_exchange_budget_script_on_committed_probe():
     for _, k, x, _, _, lat, tot, sp in rows:
         assert abs(float(k) + float(x) + float(lat) - float(tot)) < 2e-3
         assert abs(2.5 / float(tot) - float(sp)) < 0.01
+
+
+def _committed_lines(min_round=5):
+    """(path, line) of every committed bench line under profiles/r05 and later (rounds 1-4 used
+    a per-build byte model that charged distributed ranks for the whole genome's pairs)."""
+    import glob
+    import re
+    out = []
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r0*", "**", "*.json"), recursive=True)):
+        m = re.search(r"profiles/r(\d+)", path)
+        if not m or int(m.group(1)) < min_round:
+            continue
+        with open(path) as f:
+            for ln in f.read().splitlines():
+                if ln.startswith("{") and '"kernels"' in ln:
+                    out.append((path, json.loads(ln)))
+    return out
+
+
+def test_committed_profiles_stay_below_peak():
+    """no kernel of a committed bench line is credited above the 8 TB/s HBM peak,
+    and the line's roofline names a kernel that moves bytes, with frac <= 1."""
+    for path, d in _committed_lines():
+        for name, k in d["kernels"].items():
+            assert k["gbs"] is None or k["gbs"] <= 8000.0, (path, name, k["gbs"])
+        rf = d["roofline"]
+        assert rf["alg_bytes_per_launch"] > 0, path
+        assert 0.0 < rf["frac"] <= 1.0, (path, rf["frac"])
+
+
+def test_rank_byte_model_on_the_r04_probes():
+    """The per-rank byte model (bench.dist_rank_bytes) over the r04 virtual-rank probes' own
+    kernel times: every kernel of rank 0 stays below the HBM peak (the r04 lines credited
+    node_insert with 23.9 / 44.4 TB/s by charging a rank for every pair of the genome)."""
+    bench = _load_bench()
+    for name, S, R in (("strong_virtual8.json", 83_333_333, 8), ("weak_virtual8_uniform_8g.json", 666_666_666, 8),
+                       ("strong_virtual2.json", 83_333_333, 2)):
+        with open(os.path.join(REPO, "profiles", "r04", name)) as f:
+            d = json.loads(f.read().strip().splitlines()[-1])
+        # rank 0's strands as the r04 partition gave them: 700 / 850 permille shares
+        g = 1 << 9
+        T = (S + R - 1) // R
+        B = (T + g - 1) // g * g
+        Sr = max(g, B * (700 if R >= 5 else 850) // 1000 // g * g)
+        c0 = int(d["build"]["n_leaves"] * 0.9)
+        for kname, k in d["kernels"].items():
+            b = bench.dist_rank_bytes(kname, 12, Sr, 0, R, c0, (Sr + 1) // 2, d["build"]["n_leaves"])
+            if b and k["total_ms"] > 0:
+                assert b / (k["total_ms"] * 1e-3) / 1e9 <= 8000.0, (name, kname)

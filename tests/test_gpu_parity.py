@@ -357,3 +357,32 @@ def test_gpu_fused_small_levels_random(env, gcz, oracle):
                 assert g.layers_bin() == o.layers_bin(), (env, S, pool_div, rep)
     finally:
         c.close()
+
+
+def test_gpu_repetitive_decision_after_failed_dense_pack(gcz):
+    """a genome the dense pack rejects (one IUPAC 'N', past the probe's sample) falls
+    back to the hash-table leaf level, whose own repetitive-data probe must decide alone -- the
+    dense probe's counts over the rejected pre-words are cleared.  With 3.5 % in-block repeats
+    (below the 5 % threshold) both probes together would read 7 % and flip the decision; the
+    verdict (gcz_info.repetitive) and the tree must equal those of a build that never tries the
+    dense level."""
+    rng = np.random.default_rng(5)
+    L, S = 12, 1 << 22
+    strands = rng.integers(0, 4, size=(S, L), dtype=np.uint8)
+    blocks = strands.reshape(S // 256, 256, L)
+    for j in range(9):                                   # 9 of 256 strands repeat one earlier in the block
+        blocks[:, 200 + j] = blocks[:, 10 + j]
+    bases = np.frombuffer(b"ACGT", np.uint8)[strands].tobytes()
+    data = b">x\n" + bases[:-1] + b"N\n"               # the last strand: not pure ACGT (N is valid IUPAC)
+    got = {}
+    for env in ({}, {"GCZ_DENSE": "0"}):
+        c = _ctx_env(gcz, env)
+        try:
+            info = c.build_fasta(data, L)
+            assert info["status"] == 0
+            got[bool(env)] = (info["repetitive"], info["leaf_path"], gcz.digest(c.tree())["sha_dag"])
+        finally:
+            c.close()
+    assert got[False][1] == got[True][1] == 0, got       # both took the hash-table leaf level
+    assert got[False][0] == got[True][0] == 0, got
+    assert got[False][2] == got[True][2], got

@@ -113,3 +113,32 @@ def test_plan_rejects_bad_arguments(gcz):
         gcz.p2p_plan(2, 2, np.zeros(4), False, 1)
     with pytest.raises(gcz.GczError):
         gcz.p2p_plan(40, 0, np.zeros(1600), False, 1)
+
+
+def _watch_run(build_returns):
+    """gcz_dist_watch_selftest in a child process: (exit code, stderr)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = (
+        "import ctypes, sys\n"
+        f"lib = ctypes.CDLL({os.path.join(here, '..', 'genome-compression_amd', 'libgcz.so')!r})\n"
+        f"sys.exit(lib.gcz_dist_watch_selftest(1, 2, {int(build_returns)}))\n")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    return p.returncode, p.stderr
+
+
+def test_watchdog_spares_a_build_that_returned():
+    """ADVICE r04: after the watchdog fired and the build returned its error (gcz_group::fail),
+    the process must outlive the watchdog's grace period and keep its own exit code."""
+    rc, err = _watch_run(True)
+    assert rc == 0, err
+    assert "has not completed within 1 s" in err and "collective #0 selftest" in err
+    assert "did not return after the abort" not in err
+
+
+def test_watchdog_ends_a_build_that_never_returns():
+    rc, err = _watch_run(False)
+    assert rc == 70, (rc, err)
+    assert "did not return after the abort; exiting" in err
