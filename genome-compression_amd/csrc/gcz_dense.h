@@ -486,12 +486,15 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
 // Words: per chunk, the final words of its records (k_dl_ids, bucket order) back into
 // position order in LDS, written out coalesced.  A record at a first occurrence (the
 // chunk's first-occurrence bitmap, staged in LDS) emits its leaf from the record's code
-// (bucket | the record's low code bits); leaf ids are the first-occurrence ranks.
-[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_words(const u32* __restrict__ rec,
-                                                        const u32* __restrict__ idrec, const u32* __restrict__ offt,
-                                                        DensePlan P, const unsigned long long* __restrict__ fb,
-                                                        u32* __restrict__ words, u64* __restrict__ leaves_out) {
-  extern __shared__ u32 s_dyn[];
+// (bucket | the record's low code bits) at leaves_out[id - leaf_off]; leaf ids are the
+// first-occurrence ranks (the multi-rank build: rank r's r-first positions, ids from off_r).
+// dl_words_chunk does it all but the write-out: emit(s_w, n, c0) gets the chunk's n words in
+// position order in LDS (after a barrier).
+template <class Emit>
+static __device__ __forceinline__ void dl_words_chunk(const u32* __restrict__ rec, const u32* __restrict__ idrec,
+                                               const u32* __restrict__ offt, const DensePlan& P,
+                                               const unsigned long long* __restrict__ fb, u64* __restrict__ leaves_out,
+                                               u32 leaf_off, u32* s_dyn, Emit emit) {
   u32* s_w = s_dyn;                  // kDC final words by position in the chunk
   u32* s_base = s_dyn + kDC;         // NB + 1
   u32* s_dst = s_base + kDNBMax + 1; // NB
@@ -516,7 +519,7 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
     s_w[q] = wr;
     if (leaves_out && ((s_fb[q >> 5] >> (q & 31)) & 1u)) {
       const u32 h = (b << IB) | (((xr & kIdx) >> kDLog) & imask);
-      leaves_out[wr & kIdx] = code2_leaf((h * P.Kinv) & P.cmask, P.L);
+      leaves_out[(wr & kIdx) - leaf_off] = code2_leaf((h * P.Kinv) & P.cmask, P.L);
     }
   };
   // the chunk's records walked as one flat sequence of 64-record groups over the runs (every
@@ -552,8 +555,19 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
         if (bq[q] != ~0u) place(bq[q], x[q], w[q]);
     }
     __syncthreads();
-    for (u32 q = tid; q < n; q += kDThreads) words[c0 + q] = s_w[q];
+    emit(s_w, n, c0);
   }
+}
+
+[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_words(const u32* __restrict__ rec,
+                                                        const u32* __restrict__ idrec, const u32* __restrict__ offt,
+                                                        DensePlan P, const unsigned long long* __restrict__ fb,
+                                                        u32* __restrict__ words, u64* __restrict__ leaves_out,
+                                                        u32 leaf_off = 0) {
+  extern __shared__ u32 s_dyn[];
+  dl_words_chunk(rec, idrec, offt, P, fb, leaves_out, leaf_off, s_dyn, [&](const u32* s_w, u32 n, u64 c0) {
+    for (u32 q = threadIdx.x; q < n; q += kDThreads) words[c0 + q] = s_w[q];
+  });
 }
 
 // ---- multi-rank build (gcz_dist.hip): the leaf level of one rank ----------------

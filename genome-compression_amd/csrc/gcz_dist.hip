@@ -878,6 +878,7 @@ struct gcz_group {
                  const std::vector<u64>& leaf_cap, bool* taken);
   int fast_mode = std::getenv("GCZ_DIST_FAST") ? std::atoi(std::getenv("GCZ_DIST_FAST")) : 1;   // 0: off
   hipEvent_t ev_mid = nullptr;   // the fused schedule's mid-build read (status, counts)
+  FlPairs fl_pairs{};            // ... and every rank's layer-0 pairs
   int event_sync(hipEvent_t e);
   int build_done();
   int exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, u32 key_bits, u32 child_bits,
@@ -1764,7 +1765,8 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
   const u64 nwb = nw + 4 + u64(R);   // bitmap, status words, layer-0 records per owner
   const u32 child_bits = 2 * u32(L);  // hashed code labels (< 4^L; the null pair is not exchanged)
   const u32 key_bits = 2 * (child_bits + 2);
-  FlPairs pairs{};
+  FlPairs& pairs = fl_pairs;
+  pairs = FlPairs{};
   for (int s = 0; s < R; ++s) pairs.p[s] = P.count(s, 1);
   std::vector<LeafLevel> las(NL);
   std::vector<u64> dcur(NL, 0);
@@ -1807,29 +1809,29 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     if (!used) return GCZ_OK;   // (sizes outside the dense level: the same on every rank)
     const u64 n = la.S, p = P.count(r, 1);
     const u32 nb = u32(std::max<u64>(1, (p + kTile - 1) / kTile));
-    if (u64(R) * nb > kBscanSmall) return GCZ_OK;   // (>= 2^29 pairs per rank; not here)
+    const u32 cpr = (nb + kScanChunk - 1) / kScanChunk;   // (the three-pass scan of large levels)
+    if (u64(R) * nb > kBscanSmall && u64(R) * cpr > 1024) return fail(GCZ_ERR_CAPACITY, "bucket scan: too many chunks");
     RecSrc rs{};
-    rs.in = cx->dl_pw.as<u32>();
+    rs.pre = cx->dl_pw.as<u32>();
     rs.n = n;
     rs.p = p;
-    rs.words = cx->wb.as<u32>();
-    rs.nf = cx->nf_set[1];
-    rs.multi = cx->multi_set[1];
-    rs.canon = d.scratch.as<uint2>();
     rs.R = u32(R);
     {
-      ProfScope ps_(cx, KID_NODE);
-      hipLaunchKernelGGL(k_node_keys, dim3(nb), dim3(kBlock), 0, cx->stream, rs.in, n, p, cx->wb.as<u32>(),
-                         d.scratch.as<uint2>(), cx->nf_set[1], cx->multi_set[1], &h->count[kLayerSlot], static_cast<const u32*>(nullptr), 0u, rs,
-                         d.blockcnt.as<u32>(), nb, static_cast<const unsigned char*>(nullptr),
-                         d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(), d.ddesc.as<u64>(), 1u);
-      G_HIP(hipGetLastError());
-    }
-    {
       ProfScope ps_(cx, KID_DIST);
-      hipLaunchKernelGGL(k_bscan_small, dim3(1), dim3(1024), 0, cx->stream, d.blockcnt.as<u32>(), u32(R), nb, dh->sync,
-                         static_cast<const Header*>(h), static_cast<const u64*>(nullptr),
-                         static_cast<const unsigned char*>(nullptr));
+      hipLaunchKernelGGL(k_fl_count, dim3(nb), dim3(kBlock), 0, cx->stream, rs, d.blockcnt.as<u32>(), nb,
+                         d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(), d.ddesc.as<u64>(), &h->count[kLayerSlot]);
+      if (u64(R) * nb <= kBscanSmall) {
+        hipLaunchKernelGGL(k_bscan_small, dim3(1), dim3(1024), 0, cx->stream, d.blockcnt.as<u32>(), u32(R), nb, dh->sync,
+                           static_cast<const Header*>(h), static_cast<const u64*>(nullptr),
+                           static_cast<const unsigned char*>(nullptr));
+      } else {
+        if (cx->ensure(d.bchunk, u64(R) * cpr * 4 + 64)) return dev_fail("bucket scan");
+        hipLaunchKernelGGL(k_bscan_sum, dim3(R * cpr), dim3(kBlock), 0, cx->stream, d.blockcnt.as<u32>(), nb, cpr,
+                           d.bchunk.as<u32>());
+        hipLaunchKernelGGL(k_bscan_top, dim3(1), dim3(1024), 0, cx->stream, d.bchunk.as<u32>(), u32(R), cpr, dh->sync);
+        hipLaunchKernelGGL(k_bscan_down, dim3(R * cpr), dim3(kBlock), 0, cx->stream, d.blockcnt.as<u32>(), nb, cpr,
+                           static_cast<const u32*>(d.bchunk.as<u32>()));
+      }
       hipLaunchKernelGGL(k_bucket_scatter, dim3(nb), dim3(kBlock), 0, cx->stream, rs, d.blockcnt.as<u32>(), nb,
                          d.skey.as<u64>(), d.sidx.as<u32>());
       G_HIP(hipGetLastError());
@@ -1912,7 +1914,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       hipLaunchKernelGGL(k_dl_gq, dim3(NB), dim3(kDThreads), 0, cx->stream, cx->dl_lh.as<u32>(), bcnt, DP,
                          cx->dl_fb.as<unsigned long long>(), cx->dl_wpre.as<u32>(),
                          static_cast<const u64*>(&h->count[0]), cx->dl_list.as<u32>(), xv, cx->dl_pw.as<u32>(),
-                         cx->leaves_out.as<u64>(), static_cast<const u64*>(cx->dl_pb.as<u64>() + nw));
+                         static_cast<u64*>(nullptr), static_cast<const u64*>(cx->dl_pb.as<u64>() + nw));
       G_HIP(hipGetLastError());
     }
   }
@@ -2107,8 +2109,6 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     const u64 ns = sent(r), p = P.count(r, 1);
     const Displ SD = displ_send(r);
     ProfScope ps_(cx, KID_IDS);
-    hipLaunchKernelGGL(k_fl_offs, dim3(1), dim3(64), 0, cx->stream, static_cast<const u64*>(d.fl_g3.as<u64>()), u32(R),
-                       pairs, u32(r), dh->fl_offs);
     auto tiles = [](u64 x) { return dim3(unsigned(std::max<u64>(1, (x + kTile - 1) / kTile))); };
     hipLaunchKernelGGL(k_dist_flags, tiles(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
                        d.sflag.as<unsigned char>(), d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(), SD, u32(R),
@@ -2119,12 +2119,11 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
                        static_cast<const u64*>(&h->count[kLayerSlot]), d.gid.as<u32>(), d.ddesc.as<u64>(), &dh->ticket,
                        &dh->sync2[0], static_cast<const uint2*>(nullptr), static_cast<uint2*>(nullptr),
                        static_cast<const u32*>(d.nfl.as<u32>()), static_cast<const u32*>(&dh->nnf));
+    // (R4's vector {look-ahead pairs, failure}: k_lookahead and a C slot overflow write it)
     hipLaunchKernelGGL(k_fl_cvals, dim3(16), dim3(256), 0, cx->stream, static_cast<const u32*>(d.clist.as<u32>()),
                        static_cast<const u32*>(&dh->lcnt[0]), static_cast<const u32*>(d.sidx.as<u32>()), SD, u32(R),
-                       static_cast<const u32*>(d.gid.as<u32>()), static_cast<const u64*>(dh->fl_offs), u32(r),
-                       d.scval.as<u64>(), &dh->fl_bad);
-    // R4's vector {look-ahead pairs, failure}: the failure word so far (a C slot overflow)
-    hipLaunchKernelGGL(k_fl_r4pack, dim3(1), dim3(1), 0, cx->stream, dh);
+                       static_cast<const u32*>(d.gid.as<u32>()), static_cast<const u64*>(d.fl_g3.as<u64>()), pairs,
+                       u32(r), d.scval.as<u64>(), dh->fl_r4);
     G_HIP(hipGetLastError());
   }
   // ---- R4: C (first holders' ids to owners) | look-ahead + failures
@@ -2150,10 +2149,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     gcz_dist_state& d = *cx->dist;
     const int r = rank[i];
     const DensePlan& DP = cx->dl_plan;
-    Header* h = cx->hdr.as<Header>();
     DistHdr* dh = d.dhdr.as<DistHdr>();
-    hipLaunchKernelGGL(k_fl_guard, dim3(1), dim3(1), 0, cx->stream, static_cast<const u64*>(d.fl_g4.as<u64>()), u32(R),
-                       &dh->fl_guard);
     {
       ProfScope ps_(cx, KID_DL_IDS);
       G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_ids_mr), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2162,21 +2158,13 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
                          cx->dl_off.as<u32>(), DP, cx->dl_pbs.as<unsigned long long>(), nwb, cx->dl_lower.as<u32>(), xw,
                          static_cast<const u32*>(cx->dl_recv.as<u32>()), cx->dl_gid.as<DlRelay>(), R, r,
                          cx->dl_idrec.as<u32>());
-      if (c[r] && !dl_rleaves_sparse(c[r], DP.S))   // (sparse: k_dl_gq wrote them)
-        hipLaunchKernelGGL(k_dl_rleaves, dim3(unsigned((DP.S + 255) / 256)), dim3(256), 0, cx->stream,
-                           cx->dl_fb.as<unsigned long long>(), cx->dl_wpre.as<u32>(), cx->dl_pw.as<u32>(), DP,
-                           cx->leaves_out.as<u64>());
       G_HIP(hipGetLastError());
     }
-    if (int rc = cx->dense_phase_b(las[i], h, nullptr, nullptr, true))
-      return rc == GCZ_ERR_DEVICE ? dev_fail("dense leaves") : rc;
     ProfScope ps_(cx, KID_OWNER);
-    const Displ RD = displ_recv(r);
-    hipLaunchKernelGGL(k_fl_setid, dim3(16), dim3(256), 0, cx->stream, static_cast<const u64*>(d.rcval.as<u64>()), RD,
-                       u32(R), static_cast<const u32*>(d.oslot.as<u32>()), otab[i], &dh->fl_bad);
-    hipLaunchKernelGGL(k_fl_getid, dim3(64), dim3(256), 0, cx->stream, static_cast<const u32*>(d.olist.as<u32>()),
-                       static_cast<const u32*>(&dh->lcnt[1]), static_cast<const u32*>(d.oslot.as<u32>()), RD, u32(R),
-                       otab[i], d.rdval.as<u64>(), &dh->fl_bad);
+    hipLaunchKernelGGL(k_fl_cd, dim3(1), dim3(1024), 0, cx->stream, static_cast<const u64*>(d.rcval.as<u64>()),
+                       displ_recv(r), u32(R), static_cast<const u32*>(d.oslot.as<u32>()), otab[i],
+                       static_cast<const u32*>(d.olist.as<u32>()), static_cast<const u32*>(&dh->lcnt[1]),
+                       d.rdval.as<u64>(), &dh->fl_bad);
     G_HIP(hipGetLastError());
   }
   // ---- R5: D (owners forward the ids to the other holders)
@@ -2200,20 +2188,33 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     gcz_dist_state& d = *cx->dist;
     const int r = rank[i];
     DistHdr* dh = d.dhdr.as<DistHdr>();
-    const u64 n = P.count(r, 0), p = P.count(r, 1);
     {
       ProfScope ps_(cx, KID_IDS);
       hipLaunchKernelGGL(k_fl_dvals, dim3(16), dim3(256), 0, cx->stream, static_cast<const u64*>(d.sdval.as<u64>()),
                          displ_send(r), u32(R), static_cast<const u32*>(d.sidx.as<u32>()), d.gid.as<u32>(), &dh->fl_bad);
       G_HIP(hipGetLastError());
     }
-    {
+    {   // the leaf words (global ids) into layer 0 in LDS, chunk by chunk; the rank's leaves
       ProfScope ps_(cx, KID_L0);
-      hipLaunchKernelGGL(k_fl_l0, dim3(unsigned(std::max<u64>(1, (p + 4 * kBlock - 1) / (4 * kBlock)))), dim3(kBlock), 0,
-                         cx->stream, static_cast<const u32*>(cx->wa.as<u32>()), n, p,
-                         static_cast<const unsigned char*>(d.gnf.as<unsigned char>()),
-                         static_cast<const u32*>(d.gid.as<u32>()), static_cast<const u64*>(dh->fl_offs), u32(r),
-                         cx->nodes_out.as<uint2>() + node_base[i][0], cx->wb.as<u32>());
+      const DensePlan& DP = cx->dl_plan;
+      const int words_bytes = int((kDC + 2 * kDNBMax + 1 + 16 + kDC / 32 + kDC / 64) * 4);
+      G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_fl_words_l0), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                words_bytes));
+      FlL0 a{};
+      a.gnf = d.gnf.as<unsigned char>();
+      a.gid = d.gid.as<u32>();
+      a.gonf = d.fl_g3.as<u64>();
+      a.g4 = d.fl_g4.as<u64>();
+      a.pp = pairs;
+      a.R = u32(R);
+      a.me = u32(r);
+      a.leaf_off = u32(off[r]);
+      a.nodes = cx->nodes_out.as<uint2>() + node_base[i][0];
+      a.words0 = cx->wb.as<u32>();
+      a.guard = &dh->fl_guard;
+      hipLaunchKernelGGL(k_fl_words_l0, dim3(DP.nch), dim3(kDThreads), words_bytes, cx->stream, cx->dl_rec.as<u32>(),
+                         cx->dl_idrec.as<u32>(), cx->dl_offt.as<u32>(), DP, cx->dl_fb.as<unsigned long long>(),
+                         static_cast<const u32*>(cx->dl_pw.as<u32>()), cx->leaves_out.as<u64>(), a);
       G_HIP(hipGetLastError());
     }
     cur_in[i] = cx->wb.as<u32>();
@@ -2351,8 +2352,9 @@ int gcz_group::finish_top(int Gx, bool direct, u64 prev_total, const std::vector
       if (!tail_done) hipLaunchKernelGGL(k_root, dim3(1), dim3(1), 0, cx->stream, in, h);
     }
     if (fl)
-      hipLaunchKernelGGL(k_fl_final, dim3(1), dim3(1), 0, cx->stream, h, dh, Gx, D, int(tail), &dh->fl_bad,
-                         &dh->fl_guard, dh->fl_offs, u32(R));
+      hipLaunchKernelGGL(k_fl_final, dim3(1), dim3(1), 0, cx->stream, h, dh, Gx, D, int(tail),
+                         static_cast<const u32*>(&dh->fl_bad), static_cast<const u64*>(cx->dist->fl_g4.as<u64>()),
+                         static_cast<const u64*>(cx->dist->fl_g3.as<u64>()), fl_pairs, u32(R), u32(rank[i]));
     else
       hipLaunchKernelGGL(k_dist_final, dim3(1), dim3(1), 0, cx->stream, h, dh, Gx, D, int(tail));
     G_HIP(hipGetLastError());

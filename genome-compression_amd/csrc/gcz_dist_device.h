@@ -53,7 +53,6 @@ struct DistHdr {
   // fused leaf + layer-0 schedule (gcz_dist_fast.h)
   u64 fl_onf[kMaxRanks];                // this owner's not-first layer-0 records per source (R3's allgather)
   u64 fl_r4[2];                         // {layer-1 pairs with two repeated children, failure} (R4's allgather)
-  u64 fl_offs[kMaxRanks + 2];           // layer-0 id offsets, [R] total, [R + 1] this rank's uniques
   u64 fl_guard;                         // 0: layer 1 is direct on every rank and none failed
   u32 fl_bad;                           // a C / D slot overflowed
 };
@@ -93,6 +92,9 @@ struct RecSrc {
   const unsigned char* prev_multi;
   const uint2* canon;                  // levels without the local dedupe: canonical pairs (k_node_keys)
   u32 R;
+  // the fused schedule's layer 0 (gcz_dist_fast.h): pairs of the dense pack's pre-words (code
+  // labels), canonicalised on the fly; every pair but the null one is a record, lid = position
+  const u32* pre;
 };
 
 __device__ __forceinline__ bool rec_get(const RecSrc& s, u64 e, u64& key, u32& lid) {
@@ -134,6 +136,14 @@ __device__ __forceinline__ u64 rec_key(const RecSrc& s, u64 key) { return s.leav
 // rec_get for levels without the local dedupe (canonical pairs given): every load of the
 // record issued at once, none behind the not-first mark.
 __device__ __forceinline__ bool rec_get_canon(const RecSrc& s, u64 e, u64& key, u32& lid) {
+  if (s.pre) {
+    u32 l = kNullWord, r = kNullWord, cl, cr, m, t;
+    if (e < s.p) load_pair(s.pre, s.n, e, l, r);
+    node_canonical(l, r, cl, cr, m, t);
+    key = (u64(ulw(cl)) << 31) | ulw(cr);
+    lid = u32(e);
+    return e < s.p && (r & kIdx) != kIdx;
+  }
   const u64 es = e < s.p ? e : 0;   // (in bounds; used only when e < p)
   const unsigned char f = s.nf[es], mu = s.multi[es];
   const uint2 c = s.canon[es];
@@ -324,7 +334,7 @@ static __global__ __launch_bounds__(kBlock) void k_bucket_scatter(RecSrc s, cons
   for (int q = tid; q < 2 * kPre * kWaves * kMaxRanks; q += kBlock) (&wcnt[0][0][0][0])[q] = 0;
   __syncthreads();
   const u64 lt = (1ull << lane) - 1;
-  const bool pre = s.canon != nullptr && s.leaves == nullptr;
+  const bool pre = (s.canon != nullptr || s.pre != nullptr) && s.leaves == nullptr;
   const u32 dbits = s.R > 1 ? 32u - u32(__clz(int(s.R - 1))) : 0u;   // bits of a destination
   int buf = 0;
   for (int e0 = 0; e0 < kItems; e0 += kPre, buf ^= 1) {

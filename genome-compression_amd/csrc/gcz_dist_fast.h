@@ -115,69 +115,90 @@ struct FlPairs {   // layer-0 pairs of every rank (host-known from the plan)
   u64 p[kMaxRanks];
 };
 
-// Layer-0 id offsets from the gathered not-first counts (gonf[o * R + s] = owner o's
-// not-first records of source s): u_s = p_s - sum_o gonf[o R + s], off[s] = u_0 + .. + u_{s-1};
-// offs[R + 1] = this rank's u.
-[[maybe_unused]] static __global__ void k_fl_offs(const u64* __restrict__ gonf, u32 R, FlPairs pp, u32 me,
-                                                  u64* __restrict__ offs) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// This rank's layer-0 id offset (and its unique count) from R3's gathered not-first counts
+// (gonf[o * R + s] = owner o's not-first records of source s): u_s = p_s - sum_o gonf[o R + s].
+// R^2 loads (L2-resident): recomputed where it is needed rather than a launch of its own.
+__device__ __forceinline__ u64 fl_offset(const u64* __restrict__ gonf, u32 R, const FlPairs& pp, u32 me, u64* u_me) {
   u64 o = 0;
-  for (u32 s = 0; s < R; ++s) {
+  for (u32 s = 0; s <= me; ++s) {
     u64 nf = 0;
     for (u32 q = 0; q < R; ++q) nf += gonf[u64(q) * R + s];
     const u64 u = pp.p[s] - nf;
-    offs[s] = o;
-    if (s == me) offs[R + 1] = u;
+    if (s == me) {
+      if (u_me) *u_me = u;
+      return o;
+    }
     o += u;
   }
-  offs[R] = o;
+  return o;
 }
 
-// C at a first holder: (index within its segment to owner q, global id) into q's slot.
-[[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_cvals(const u32* __restrict__ clist,
-                                                      const u32* __restrict__ ccount, const u32* __restrict__ sidx,
-                                                      Displ SD, u32 R, const u32* __restrict__ gid,
-                                                      const u64* __restrict__ offs, u32 me, u64* __restrict__ cbuf,
-                                                      u32* __restrict__ bad) {
-  const u32 n = *ccount;
-  for (u32 i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const u32 k = clist[i];
-    const u32 q = seg_of(SD, R, k);
-    const u64 slot = atomicAdd(reinterpret_cast<unsigned long long*>(&cbuf[u64(q) * kFlSeg]), 1ull);
-    if (slot >= kFlCap) {
-      atomicOr(bad, 1u);
-      continue;
+// R4's gathered {look-ahead pairs, failure} of every rank -> 0 when layer 1 is direct on
+// every rank and none failed (the direct subtrees' guard)
+__device__ __forceinline__ u64 fl_guard(const u64* __restrict__ g4, u32 R) {
+  u64 t = 0;
+  for (u32 s = 0; s < R; ++s) t += g4[2 * s] + g4[2 * s + 1];
+  return t;
+}
+
+// Layer 0's records per owner, per tile of kTile pairs (the bucketing's count pass over the
+// pre-words: k_bucket_scatter with RecSrc::pre follows), and what the exchange expects zeroed:
+// the global flags and the rank scan's look-back words; count_out = the pairs.
+[[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_fl_count(RecSrc rs, u32* __restrict__ blockcnt, u32 nb,
+                                                         unsigned char* __restrict__ gnf,
+                                                         unsigned char* __restrict__ gmul, u64* __restrict__ ddesc,
+                                                         u64* __restrict__ count_out) {
+  __shared__ u32 h[kMaxRanks];
+  const int tid = threadIdx.x;
+  const u64 p = rs.p;
+  {
+    const u64 end = blockIdx.x + 1 == gridDim.x ? p + 1 : std::min<u64>(u64(blockIdx.x + 1) * kTile, p + 1);
+    const u64 e0 = u64(blockIdx.x) * kTile / 16, e1 = (end + 15) / 16;
+    for (u64 e = e0 + tid; e < e1; e += kBlock) {
+      reinterpret_cast<uint4*>(gnf)[e] = make_uint4(0, 0, 0, 0);
+      reinterpret_cast<uint4*>(gmul)[e] = make_uint4(0, 0, 0, 0);
     }
-    const u32 id = u32(offs[me] + (gid[sidx[k]] & ~kLocalId));
-    cbuf[u64(q) * kFlSeg + 1 + slot] = u64(k - SD.d[q]) | (u64(id) << 32);
+    if (tid == 0) ddesc[blockIdx.x] = 0;
   }
+  if (tid < int(rs.R)) h[tid] = 0;
+  if (blockIdx.x == 0 && tid == 0) *count_out = p;
+  __syncthreads();
+  constexpr int kB = 8;
+  for (int e0 = 0; e0 < kItems; e0 += kB) {
+    u64 key[kB];
+    u32 lid[kB];
+    bool ok[kB];
+#pragma unroll
+    for (int q = 0; q < kB; ++q) ok[q] = rec_get_canon(rs, u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid, key[q], lid[q]);
+#pragma unroll
+    for (int q = 0; q < kB; ++q)
+      if (ok[q]) atomicAdd(&h[owner_of(key[q], rs.R)], 1u);
+  }
+  __syncthreads();
+  if (tid < int(rs.R)) blockcnt[u64(tid) * nb + blockIdx.x] = h[tid];
 }
 
-// C at the owner: the first holder's global id of each shared key into the key's id slot.
-[[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_setid(const u64* __restrict__ rc, Displ D, u32 R,
-                                                      const u32* __restrict__ oslot, OwnTab T,
-                                                      u32* __restrict__ bad) {
+// C and D at the owner, one block: the first holders' ids into the keys' id slots, then every
+// not-first record's id into the slot of its source (the C / D counts of this schedule are
+// bounded by the slots: kFlCap per pair).
+[[maybe_unused]] static __global__ __launch_bounds__(1024) void k_fl_cd(const u64* __restrict__ rc, Displ D, u32 R,
+                                                    const u32* __restrict__ oslot, OwnTab T,
+                                                    const u32* __restrict__ olist, const u32* __restrict__ ocnt,
+                                                    u64* __restrict__ dbuf, u32* __restrict__ bad) {
   for (u32 s = 0; s < R; ++s) {
     const u64 n = rc[u64(s) * kFlSeg];
     if (n > kFlCap) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(bad, 1u);
+      if (threadIdx.x == 0) atomicOr(bad, 1u);
       continue;
     }
-    for (u64 i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    for (u64 i = threadIdx.x; i < n; i += 1024) {
       const u64 v = rc[u64(s) * kFlSeg + 1 + i];
       own_set_id(T, oslot[D.d[s] + u32(v)], u32(v >> 32));
     }
   }
-}
-
-// D at the owner: every not-first record (the dedupe's list) gets its key's id back, into the
-// slot of the record's source.
-[[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_getid(const u32* __restrict__ olist,
-                                                      const u32* __restrict__ ocnt, const u32* __restrict__ oslot,
-                                                      Displ D, u32 R, OwnTab T, u64* __restrict__ dbuf,
-                                                      u32* __restrict__ bad) {
+  __syncthreads();
   const u32 n = *ocnt;
-  for (u32 i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+  for (u32 i = threadIdx.x; i < n; i += 1024) {
     const u32 k = olist[i];
     const u32 s = seg_of(D, R, k);
     const u64 slot = atomicAdd(reinterpret_cast<unsigned long long*>(&dbuf[u64(s) * kFlSeg]), 1ull);
@@ -186,6 +207,29 @@ struct FlPairs {   // layer-0 pairs of every rank (host-known from the plan)
       continue;
     }
     dbuf[u64(s) * kFlSeg + 1 + slot] = u64(k - D.d[s]) | (u64(own_id(T, oslot[k])) << 32);
+  }
+}
+
+// C at a first holder: (index within its segment to owner q, global id) into q's slot.
+// (a slot overflow goes straight into this rank's R4 vector: r4[1])
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_cvals(const u32* __restrict__ clist,
+                                                      const u32* __restrict__ ccount, const u32* __restrict__ sidx,
+                                                      Displ SD, u32 R, const u32* __restrict__ gid,
+                                                      const u64* __restrict__ gonf, FlPairs pp, u32 me,
+                                                      u64* __restrict__ cbuf, u64* __restrict__ r4) {
+  const u32 n = *ccount;
+  if (n == 0) return;
+  const u64 off = fl_offset(gonf, R, pp, me, nullptr);
+  for (u32 i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const u32 k = clist[i];
+    const u32 q = seg_of(SD, R, k);
+    const u64 slot = atomicAdd(reinterpret_cast<unsigned long long*>(&cbuf[u64(q) * kFlSeg]), 1ull);
+    if (slot >= kFlCap) {
+      atomicOr(reinterpret_cast<unsigned long long*>(&r4[1]), 1ull);
+      continue;
+    }
+    const u32 id = u32(off + (gid[sidx[k]] & ~kLocalId));
+    cbuf[u64(q) * kFlSeg + 1 + slot] = u64(k - SD.d[q]) | (u64(id) << 32);
   }
 }
 
@@ -206,73 +250,85 @@ struct FlPairs {   // layer-0 pairs of every rank (host-known from the plan)
   }
 }
 
-// R4's vector of this rank: {look-ahead pairs (k_lookahead added them), failure so far}
-[[maybe_unused]] static __global__ void k_fl_r4pack(DistHdr* __restrict__ dh) { dh->fl_r4[1] = dh->fl_bad; }
-
-// R4's gathered vectors {look-ahead pairs, failure flags} of every rank -> one word: 0 when
-// layer 1 is direct everywhere and no rank failed (the direct subtrees' guard).
-[[maybe_unused]] static __global__ void k_fl_guard(const u64* __restrict__ g4, u32 R, u64* __restrict__ guard) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  u64 t = 0;
-  for (u32 s = 0; s < R; ++s) t += g4[2 * s] + g4[2 * s + 1];
-  *guard = t;
-}
-
-// Layer 0 with the global leaf ids (emplace_node, src/shared_tree.cpp:662-672): the pair's
-// canonical node and bits; a globally-first pair takes id off + its local rank and writes its
-// node at that rank in the rank's slice; the others take the id D delivered.  Four pairs per
-// thread, their loads issued together.
-[[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_fl_l0(const u32* __restrict__ in, u64 n, u64 p,
-                                                      const unsigned char* __restrict__ gnf,
-                                                      const u32* __restrict__ gid, const u64* __restrict__ offs,
-                                                      u32 me, uint2* __restrict__ nodes, u32* __restrict__ words) {
-  constexpr int kB = 4;
-  const u64 j0 = (u64(blockIdx.x) * kBlock * kB) + threadIdx.x;
-  u32 l[kB], r[kB], g[kB];
-  unsigned char f[kB];
-#pragma unroll
-  for (int q = 0; q < kB; ++q) {
-    const u64 j = j0 + u64(q) * kBlock;
-    l[q] = r[q] = kNullWord;
-    g[q] = 0;
-    f[q] = 0;
-    if (j < p) {
-      load_pair(in, n, j, l[q], r[q]);
-      g[q] = gid[j];
-      f[q] = gnf[j];
-    }
-  }
-  const u32 off = u32(offs[me]);
-#pragma unroll
-  for (int q = 0; q < kB; ++q) {
-    const u64 j = j0 + u64(q) * kBlock;
-    if (j >= p) continue;
-    u32 cl, cr, m, t;
-    node_canonical(l[q], r[q], cl, cr, m, t);
-    const u32 v = ulw(l[q]) == ulw(xf(r[q], 1, 0));
-    u32 id = g[q];
-    if (!f[q]) {
-      const u32 lr = g[q] & ~kLocalId;
-      nodes[lr] = make_uint2(cl, cr);
-      id = off + lr;
-    }
-    words[j] = make_word(id, m, t, v);
-  }
-}
-
 // The final vector of a fast-schedule rank: the general one (k_dist_final) plus failure bit 2
 // (a C/D overflow, a look-ahead that found layer 1 not direct) and [3] = this rank's layer-0
 // uniques.
 [[maybe_unused]] static __global__ void k_fl_final(const Header* __restrict__ h, DistHdr* __restrict__ dh, int tail0,
                                                    int D, int has_tail, const u32* __restrict__ bad,
-                                                   const u64* __restrict__ guard, const u64* __restrict__ offs,
-                                                   u32 R) {
-  dh->final_vec[0] = u64(h->overflow | h->leaf_overflow) | ((*bad || *guard) ? 2ull : 0ull);
+                                                   const u64* __restrict__ g4, const u64* __restrict__ gonf,
+                                                   FlPairs pp, u32 R, u32 me) {
+  u64 u = 0;
+  (void)fl_offset(gonf, R, pp, me, &u);
+  dh->final_vec[0] = u64(h->overflow | h->leaf_overflow) | ((*bad || fl_guard(g4, R)) ? 2ull : 0ull);
   dh->final_vec[1] = has_tail ? u64(h->root) : 0ull;
   dh->final_vec[2] = u64(tail0);
-  dh->final_vec[3] = offs[R + 1];
+  dh->final_vec[3] = u;
   for (int k = 0; k < GCZ_MAX_LAYERS; ++k)
     dh->final_vec[4 + k] = (has_tail && k >= tail0 && k < D) ? h->count[kLayerSlot + k] : 0ull;
+}
+
+}  // namespace gcz_dev
+
+namespace gcz_dev {
+
+// Layer 0 with the global leaf ids (emplace_node, src/shared_tree.cpp:662-672), fused into the
+// dense level's words pass (k_dl_words): the chunk's leaf words never leave LDS.  Each pair of
+// the chunk gets its canonical node and bits; a globally-first pair takes id off + its local
+// rank and writes its node at that rank of the rank's slice, the others take the id D
+// delivered.  The chunk's first positions (the rank's r-first codes) write their leaves.
+// Block 0 also settles the direct subtrees' guard from R4's vectors.
+struct FlL0 {
+  const unsigned char* gnf;   // per pair: not globally first
+  const u32* gid;             // per pair: local rank | kLocalId (first), else the global id
+  const u64* gonf;            // R3's gathered not-first counts
+  const u64* g4;              // R4's gathered {look-ahead, failure}
+  FlPairs pp;
+  u32 R, me, leaf_off;
+  uint2* nodes;               // the rank's slice of layer 0
+  u32* words0;                // layer-0 words (the direct subtrees' input)
+  u64* guard;
+};
+// The leaves go out in position order (= id order) from the pre-words: coalesced stores, where
+// k_dl_words' record-order stores scatter (at 1 Gbase over 8 ranks rank 0 first-holds ~47 % of
+// its strands' codes).
+[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_fl_words_l0(const u32* __restrict__ rec,
+                                                           const u32* __restrict__ idrec, const u32* __restrict__ offt,
+                                                           DensePlan P, const unsigned long long* __restrict__ fb,
+                                                           const u32* __restrict__ pw, u64* __restrict__ leaves_out,
+                                                           FlL0 a) {
+  extern __shared__ u32 s_dyn[];
+  __shared__ u32 s_off;
+  if (threadIdx.x == 0) {
+    s_off = u32(fl_offset(a.gonf, a.R, a.pp, a.me, nullptr));
+    if (blockIdx.x == 0) *a.guard = fl_guard(a.g4, a.R);
+  }
+  dl_words_chunk(rec, idrec, offt, P, fb, nullptr, 0, s_dyn, [&](const u32* s_w, u32 n, u64 c0) {
+    const u64 j0 = c0 / 2;
+    const u32 np = (n + 1) / 2, off = s_off;
+#pragma unroll 4
+    for (u32 jj = threadIdx.x; jj < np; jj += kDThreads) {
+      const u64 j = j0 + jj;
+      const unsigned char f = a.gnf[j];
+      const u32 g = a.gid[j];
+      const u64 fw = fb[(c0 + 2 * jj) >> 6];   // (the pair's two positions share a word)
+      const u32 sh = u32(c0 + 2 * jj) & 63u;
+      const u32 l = s_w[2 * jj], r = 2 * jj + 1 < n ? s_w[2 * jj + 1] : kNullWord;
+      if ((fw >> sh) & 1ull)
+        leaves_out[(l & kIdx) - a.leaf_off] = code2_leaf(((pw[c0 + 2 * jj] & kIdx) * P.Kinv) & P.cmask, P.L);
+      if (2 * jj + 1 < n && ((fw >> (sh + 1)) & 1ull))
+        leaves_out[(r & kIdx) - a.leaf_off] = code2_leaf(((pw[c0 + 2 * jj + 1] & kIdx) * P.Kinv) & P.cmask, P.L);
+      u32 cl, cr, m, t;
+      node_canonical(l, r, cl, cr, m, t);
+      const u32 v = ulw(l) == ulw(xf(r, 1, 0));
+      u32 id = g;
+      if (!f) {
+        const u32 lr = g & ~kLocalId;
+        a.nodes[lr] = make_uint2(cl, cr);
+        id = off + lr;
+      }
+      a.words0[j] = make_word(id, m, t, v);
+    }
+  });
 }
 
 }  // namespace gcz_dev
