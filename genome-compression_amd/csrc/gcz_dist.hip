@@ -44,6 +44,7 @@ struct gcz_dist_state {
   u64* h_gath2 = nullptr;
   u64* h_gathf = nullptr;
   DlRelay* h_relay = nullptr;   // pinned staging of the dense leaf relay table (H2D, stream-ordered)
+  DevBuf skey_hi, rkey_hi;   // fused schedule: the 6-byte records' high 16 bits
   DevBuf fl_cntb, fl_mid, fl_g3, fl_g4;   // fused schedule: r-first counts per bucket, the mid-build
   u64* h_mid = nullptr;                   // vector (+ pinned mirror), R3's / R4's gathered vectors
 };
@@ -58,7 +59,8 @@ void gcz_dist_state_free(gcz_ctx* c) {
   for (DevBuf* b : {&d->dict, &d->scratch, &d->gnf, &d->gmul, &d->gid, &d->blockcnt, &d->bchunk, &d->skey, &d->sidx, &d->sflag,
                     &d->scval, &d->sdval, &d->clist, &d->olist, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab, &d->oids,
                     &d->omin, &d->ob_cnt, &d->ob_off, &d->ob_desc, &d->ob_rec, &d->ob_seg, &d->ob_rt,
-                    &d->ob_rec2, &d->ob_fo, &d->fl_cntb, &d->fl_mid, &d->fl_g3, &d->fl_g4,
+                    &d->ob_rec2, &d->ob_fo, &d->fl_cntb, &d->fl_mid, &d->fl_g3, &d->fl_g4, &d->skey_hi,
+                    &d->rkey_hi,
                     &d->dhdr, &d->gath, &d->gath2, &d->gathf, &d->ddesc, &d->tail_in, &d->nfl})
     if (b->ptr) (void)hipFree(b->ptr);
   for (u64* h : {d->h_gath, d->h_gath2, d->h_gathf})
@@ -1763,8 +1765,14 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     if (P.count(s, 1) < 2) return GCZ_OK;
   const u64 ncodes = u64(1) << (2 * L), nw = (ncodes + 63) / 64;
   const u64 nwb = nw + 4 + u64(R);   // bitmap, status words, layer-0 records per owner
-  const u32 child_bits = 2 * u32(L);  // hashed code labels (< 4^L; the null pair is not exchanged)
-  const u32 key_bits = 2 * (child_bits + 2);
+  // Layer-0 records: R a power of two -> 6 bytes (PreKey: canonical-code ranks, the owner in
+  // the mixed key's top bits); else the raw canonical pair in hashed-code labels, 8 bytes
+  const u32 lgR = (R & (R - 1)) == 0 ? log2_exact(u64(R)) : 0u;
+  const bool split = lgR > 0;
+  const u32 Bc = 2 * u32(L) - 1;   // (a canonical code's top bit is 0: PreKey)
+  const u32 child_bits = 2 * u32(L);  // (8-byte records: hashed code labels; the null pair is not exchanged)
+  const u32 key_bits = split ? 2 * Bc + 3 - lgR : 2 * (child_bits + 2);
+  if (split && key_bits > 48) return GCZ_OK;
   FlPairs& pairs = fl_pairs;
   pairs = FlPairs{};
   for (int s = 0; s < R; ++s) pairs.p[s] = P.count(s, 1);
@@ -1816,6 +1824,21 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     rs.n = n;
     rs.p = p;
     rs.R = u32(R);
+    if (split) {
+      const DensePlan& DP = cx->dl_plan;
+      const LevelTab mt = plan_table(nullptr, 256, 2 * Bc + 3, 2, Bc, true, 0);   // (its mix only)
+      rs.pk.on = 1;
+      rs.pk.Kinv = DP.Kinv;
+      rs.pk.cmask = DP.cmask;
+      rs.pk.Bc = Bc;
+      rs.pk.K = 2 * Bc + 3;
+      rs.pk.lgR = lgR;
+      rs.pk.sh = mt.pt.sh;
+      rs.pk.kmask = mt.pt.kmask;
+      rs.pk.c1 = mt.pt.c1;
+      rs.pk.c2 = mt.pt.c2;
+      if (cx->ensure(d.skey_hi, p * 2 + 16)) return dev_fail("fused schedule buffers");
+    }
     {
       ProfScope ps_(cx, KID_DIST);
       hipLaunchKernelGGL(k_fl_count, dim3(nb), dim3(kBlock), 0, cx->stream, rs, d.blockcnt.as<u32>(), nb,
@@ -1833,7 +1856,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
                            static_cast<const u32*>(d.bchunk.as<u32>()));
       }
       hipLaunchKernelGGL(k_bucket_scatter, dim3(nb), dim3(kBlock), 0, cx->stream, rs, d.blockcnt.as<u32>(), nb,
-                         d.skey.as<u64>(), d.sidx.as<u32>());
+                         d.skey.as<u64>(), d.sidx.as<u32>(), split ? d.skey_hi.as<unsigned short>() : nullptr);
       G_HIP(hipGetLastError());
       // the owner counts ride behind the bitmap and the status words
       G_HIP(hipMemcpyAsync(cx->dl_pb.as<u64>() + nw + 4, dh->sync, size_t(R) * 8, hipMemcpyDeviceToDevice, cx->stream));
@@ -1947,6 +1970,16 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     for (int q = R; q <= kMaxRanks; ++q) Dd.d[q] = o;
     return Dd;
   };
+  // the replies packed 2 bits per record: ceil(count / 4) bytes per segment
+  std::vector<u64> M4(size_t(R) * R);
+  for (size_t q = 0; q < M4.size(); ++q) M4[q] = (M[q] + 3) / 4;
+  auto displ4 = [&](int r, bool as_owner) {   // packed segments: owner r's per source / sender r's per owner
+    Displ Dd{};
+    u64 o = 0;
+    for (int q = 0; q < R; ++q) { Dd.d[q] = o; o += as_owner ? M4[size_t(q) * R + r] : M4[size_t(r) * R + q]; }
+    for (int q = R; q <= kMaxRanks; ++q) Dd.d[q] = o;
+    return Dd;
+  };
   auto displ_send = [&](int r) {   // destination segments of rank r's send buffer
     Displ Dd{};
     u64 o = 0;
@@ -2003,6 +2036,8 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
         cx->ensure(d.scval, cd) || cx->ensure(d.rcval, cd) || cx->ensure(d.rdval, cd) || cx->ensure(d.sdval, cd) ||
         cx->ensure(d.fl_g3, size_t(R) * kMaxRanks * 8 + 16) || cx->ensure(d.fl_g4, size_t(R) * 2 * 8 + 16) ||
         cx->ensure(d.nfl, kNfListCap * 4 + 16) || cx->ensure(cx->dl_stage, T[r] * 4 + 16) ||
+        cx->ensure(d.omin, nr / 4 + u64(R) + 64) ||   // (the packed replies)
+        (split && cx->ensure(d.rkey_hi, nr * 2 + 16)) ||
         cx->ensure(cx->dl_recv, total * 4 + 16) || cx->ensure(cx->dl_gid, sizeof(DlRelay) + 16))
       return dev_fail("fused schedule buffers");
     bp.T.tab = d.owntab.as<u64>();
@@ -2029,18 +2064,27 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
   }
   // ---- R2: layer-0 keys to their owners | leaf G arrays, relay 1
   {
-    std::vector<const void*> sk, sg;
-    std::vector<void*> rk, rg;
+    std::vector<const void*> sk, sh, sg;
+    std::vector<void*> rk, rh, rg;
     for (gcz_ctx* cx : ctx) {
       sk.push_back(cx->dist->skey.ptr);
       rk.push_back(cx->dist->rkey.ptr);
+      sh.push_back(cx->dist->skey_hi.ptr);
+      rh.push_back(cx->dist->rkey_hi.ptr);
       sg.push_back(cx->dl_list.ptr);
       rg.push_back(cx->dl_stage.ptr);
     }
+    std::vector<Transport::XOp> ops;
+    if (split) {   // 6-byte records: low 32 bits | high 16 bits
+      ops.push_back(xop_a2a(M, R, false, 4, sk, rk));
+      ops.push_back(xop_a2a(M, R, false, 2, sh, rh));
+    } else {
+      ops.push_back(xop_a2a(M, R, false, 8, sk, rk));
+    }
+    ops.push_back(xop_a2a(M1, R, false, 4, sg, rg));
     hipEvent_t e0{};
     ctx[0]->prof_begin(KID_EXCHANGE, e0);
-    G_RC(x_group("R2 layer-0 keys to owners | leaf G arrays, relay 1",
-                 {xop_a2a(M, R, false, 8, sk, rk), xop_a2a(M1, R, false, 4, sg, rg)}));
+    G_RC(x_group("R2 layer-0 keys to owners | leaf G arrays, relay 1", ops));
     ctx[0]->prof_end(KID_EXCHANGE, e0);
   }
   // owners: the two-pass hash-cons of their records (first = lowest receive index: the sources
@@ -2059,7 +2103,8 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_bkt_fine), hipFuncAttributeMaxDynamicSharedMemorySize,
                               int(kFineCap * 8)));
     hipLaunchKernelGGL(k_ob_part, dim3(unsigned(bp.G)), dim3(kBktThreads), size_t(kPartChunk) * 8, cx->stream,
-                       d.rkey.as<u64>(), nr, bp, child_bits, d.ob_seg.as<u64>(), d.ob_rt.as<u32>(), d.rflag.as<unsigned char>());
+                       d.rkey.as<u64>(), nr, bp, child_bits, d.ob_seg.as<u64>(), d.ob_rt.as<u32>(), d.rflag.as<unsigned char>(),
+                       split ? static_cast<const unsigned short*>(d.rkey_hi.as<unsigned short>()) : nullptr);
     hipLaunchKernelGGL(k_bkt_fine, dim3(unsigned(nfine)), dim3(kBktThreads), size_t(kFineCap) * 8, cx->stream,
                        d.ob_seg.as<u64>(), d.ob_rt.as<u32>(), bp, d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(),
                        static_cast<Header*>(nullptr), static_cast<const u64*>(nullptr), nr, ovf);
@@ -2070,6 +2115,10 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     DistHdr* dh = d.dhdr.as<DistHdr>();
     hipLaunchKernelGGL(k_fl_ownnf, dim3(64), dim3(256), 0, cx->stream, static_cast<const u32*>(d.olist.as<u32>()),
                        static_cast<const u32*>(&dh->lcnt[1]), displ_recv(r), u32(R), dh->fl_onf);
+    const Displ P4 = displ4(r, true);
+    hipLaunchKernelGGL(k_fl_pack2, dim3(unsigned(std::max<u64>(1, (P4.d[R] + 255) / 256))), dim3(256), 0, cx->stream,
+                       static_cast<const unsigned char*>(d.rflag.as<unsigned char>()), displ_recv(r), P4, u32(R),
+                       d.omin.as<unsigned char>());
     G_HIP(hipGetLastError());
   }
   // ---- R3: owner replies | leaf G arrays, relay 2 | the owners' not-first counts
@@ -2078,7 +2127,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     std::vector<void*> rf, rg, rn;
     for (gcz_ctx* cx : ctx) {
       gcz_dist_state& d = *cx->dist;
-      sf.push_back(d.rflag.ptr);
+      sf.push_back(d.omin.ptr);   // (the packed replies)
       rf.push_back(d.sflag.ptr);
       sg.push_back(cx->dl_stage.ptr);
       rg.push_back(cx->dl_recv.ptr);
@@ -2095,7 +2144,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     hipEvent_t e0{};
     ctx[0]->prof_begin(KID_EXCHANGE, e0);
     G_RC(x_group("R3 owner replies | leaf G arrays, relay 2 | not-first counts",
-                 {xop_a2a(M, R, true, 1, sf, rf), relay2, xop_allgather(R, u64(R), 8, sn, rn)}));
+                 {xop_a2a(M4, R, true, 1, sf, rf), relay2, xop_allgather(R, u64(R), 8, sn, rn)}));
     ctx[0]->prof_end(KID_EXCHANGE, e0);
   }
   // senders: layer-0 id offsets, the replies -> global flags, look-ahead, local ranks of the
@@ -2112,7 +2161,8 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     auto tiles = [](u64 x) { return dim3(unsigned(std::max<u64>(1, (x + kTile - 1) / kTile))); };
     hipLaunchKernelGGL(k_dist_flags, tiles(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
                        d.sflag.as<unsigned char>(), d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(), SD, u32(R),
-                       &dh->sync2[1], d.clist.as<u32>(), &dh->lcnt[0], d.nfl.as<u32>(), &dh->nnf);
+                       &dh->sync2[1], d.clist.as<u32>(), &dh->lcnt[0], d.nfl.as<u32>(), &dh->nnf,
+                       static_cast<const unsigned char*>(d.sflag.as<unsigned char>()), displ4(r, false));
     hipLaunchKernelGGL(k_lookahead, dim3(unsigned(std::max<u64>(1, ((p + 1) / 2 + kBlock - 1) / kBlock))), dim3(kBlock), 0,
                        cx->stream, static_cast<const unsigned char*>(d.gmul.as<unsigned char>()), p, &dh->fl_r4[0]);
     hipLaunchKernelGGL((k_dist_rank<uint2>), tiles(p), dim3(kBlock), 0, cx->stream, d.gnf.as<unsigned char>(),

@@ -77,6 +77,30 @@ __device__ __forceinline__ u32 owner_of(u64 key, u32 R) {
 
 constexpr u64 kLocalMulti = 1ull << 63;
 
+// The fused schedule's 6-byte layer-0 records (gcz_dist_fast.h): the canonical pair re-labelled
+// by the children's canonical 2-bit codes -- a dna::canonical code is the minimum of its orbit,
+// which holds a code and its complement (x ^ mask), so its top bit is 0: Bc = 2L - 1 bits --
+// left child code | m, right child code | m | t (a canonical node's left child never carries t,
+// include/shared_tree.h:119-126) = K = 2 Bc + 3 bits, mixed by a K-bit bijection h;
+// owner = h's top lgR bits, record = the K - lgR bits below (<= 48).
+struct PreKey {
+  u32 on;                            // 0: 8-B raw keys
+  u32 Kinv, cmask;                   // hashed code -> code
+  u32 Bc, K, lgR;
+  u32 sh;
+  u64 kmask, c1, c2;                 // the mix (PackedTab::mix's form)
+  __device__ __forceinline__ u64 mix(u64 x) const {
+    x ^= x >> sh; x = (x * c1) & kmask;
+    x ^= x >> sh; x = (x * c2) & kmask;
+    x ^= x >> sh;
+    return x;
+  }
+  __device__ __forceinline__ u64 label(u32 w) const {   // a child word -> code << 2 | m << 1 | t
+    const u32 c = ((w & kIdx) * Kinv) & cmask;
+    return (u64(c) << 2) | (((w >> 29) & 1u) << 1) | ((w >> 30) & 1u);   // (bit 29 mirror, 30 transpose)
+  }
+};
+
 // The elements of a level that send a record.
 struct RecSrc {
   // leaf levels: local unique ids [0, *ucount), key = leaves[lid]
@@ -95,7 +119,10 @@ struct RecSrc {
   // the fused schedule's layer 0 (gcz_dist_fast.h): pairs of the dense pack's pre-words (code
   // labels), canonicalised on the fly; every pair but the null one is a record, lid = position
   const u32* pre;
+  PreKey pk;     // ... with pk.on: 6-byte records, the key = owner << 48 | record
 };
+
+
 
 __device__ __forceinline__ bool rec_get(const RecSrc& s, u64 e, u64& key, u32& lid) {
   if (s.leaves) {
@@ -133,6 +160,11 @@ __device__ __forceinline__ bool rec_get(const RecSrc& s, u64 e, u64& key, u32& l
 
 __device__ __forceinline__ u64 rec_key(const RecSrc& s, u64 key) { return s.leaves ? key : (key & ~kLocalMulti); }
 
+// destination rank of a record's key
+__device__ __forceinline__ u32 rec_dest(const RecSrc& s, u64 key) {
+  return s.pre && s.pk.on ? u32(key >> 48) : owner_of(rec_key(s, key), s.R);
+}
+
 // rec_get for levels without the local dedupe (canonical pairs given): every load of the
 // record issued at once, none behind the not-first mark.
 __device__ __forceinline__ bool rec_get_canon(const RecSrc& s, u64 e, u64& key, u32& lid) {
@@ -140,9 +172,21 @@ __device__ __forceinline__ bool rec_get_canon(const RecSrc& s, u64 e, u64& key, 
     u32 l = kNullWord, r = kNullWord, cl, cr, m, t;
     if (e < s.p) load_pair(s.pre, s.n, e, l, r);
     node_canonical(l, r, cl, cr, m, t);
-    key = (u64(ulw(cl)) << 31) | ulw(cr);
     lid = u32(e);
-    return e < s.p && (r & kIdx) != kIdx;
+    const bool ok = e < s.p && (r & kIdx) != kIdx;
+    if (s.pk.on) {
+      if (!ok) {
+        key = 0;
+        return false;
+      }
+      const u64 k = ((s.pk.label(cl) >> 1) << (s.pk.Bc + 2)) | s.pk.label(cr);   // (cl's t bit is 0)
+      const u64 h = s.pk.mix(k);
+      const u32 sh = s.pk.K - s.pk.lgR;
+      key = ((h >> sh) << 48) | (h & ((1ull << sh) - 1ull));
+      return true;
+    }
+    key = (u64(ulw(cl)) << 31) | ulw(cr);
+    return ok;
   }
   const u64 es = e < s.p ? e : 0;   // (in bounds; used only when e < p)
   const unsigned char f = s.nf[es], mu = s.multi[es];
@@ -319,8 +363,11 @@ static __global__ __launch_bounds__(kBlock) void k_bscan_down(u32* __restrict__ 
 // in order, waves in order within an item, lanes in order within a wave), so every
 // owner receives each source's records in the source's order.  Owners of levels that
 // skip the local dedupe rely on it: the first record of a key is its first occurrence.
+// split (the fused schedule's 6-byte records): record low 32 bits to skey as u32 [0, n), the
+// high 16 to the u16 array `split`.
 static __global__ __launch_bounds__(kBlock) void k_bucket_scatter(RecSrc s, const u32* __restrict__ boff, u32 nb,
-                                                                  u64* __restrict__ skey, u32* __restrict__ sidx) {
+                                                                  u64* __restrict__ skey, u32* __restrict__ sidx,
+                                                                  unsigned short* __restrict__ split = nullptr) {
   constexpr int kWaves = kBlock / 64;
   // kPre items per round: their records loaded together (canonical-pair levels: straight-line,
   // in flight at once), one ballot pass per item, then ONE block-wide exclusive prefix over
@@ -353,7 +400,7 @@ static __global__ __launch_bounds__(kBlock) void k_bucket_scatter(RecSrc s, cons
         lid[q] = 0;
         ok[q] = rec_get(s, u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid, key[q], lid[q]);
       }
-      d[q] = ok[q] ? owner_of(rec_key(s, key[q]), s.R) : 0u;
+      d[q] = ok[q] ? rec_dest(s, key[q]) : 0u;
       // the lanes sharing this lane's destination: one ballot per destination bit
       u64 m = __ballot(ok[q]);
       for (u32 bit = 0; bit < dbits; ++bit) {
@@ -384,7 +431,12 @@ static __global__ __launch_bounds__(kBlock) void k_bucket_scatter(RecSrc s, cons
     for (int q = 0; q < kPre; ++q)
       if (ok[q]) {
         const u32 o = wcnt[buf][q][wave][d[q]] + before[q];
-        skey[o] = key[q];
+        if (split) {
+          reinterpret_cast<u32*>(skey)[o] = u32(key[q]);
+          split[o] = (unsigned short)(key[q] >> 32);
+        } else {
+          skey[o] = key[q];
+        }
         sidx[o] = lid[q];
       }
   }
@@ -564,9 +616,12 @@ struct OwnBkt {
 // follow): pass 1 sorts each chunk of kPartChunk receive indices by the b1 coarse bits of
 // h = T.mix(packed key) in LDS and writes the records back contiguously with the chunk's
 // run table -- whole runs instead of k_ob_scatter's scattered 8-B stores.
+// hi != null (the fused schedule's 6-byte records): rkey holds the records' low 32 bits as u32,
+// hi their high 16; the record IS the key's mix (h's bits below the owner's), no own_pack_key.
 static __global__ __launch_bounds__(kBktThreads) void k_ob_part(const u64* __restrict__ rkey, u64 nr, Bkt2Plan bp,
                                                                 u32 B, u64* __restrict__ seg, u32* __restrict__ rt,
-                                                                unsigned char* __restrict__ rflag) {
+                                                                unsigned char* __restrict__ rflag,
+                                                                const unsigned short* __restrict__ hi = nullptr) {
   extern __shared__ u64 stage[];   // kPartChunk records (dynamic)
   __shared__ u32 cur[(1u << kPartMaxB1) + 1];
   const u32 nb1 = 1u << bp.b1;
@@ -581,7 +636,7 @@ static __global__ __launch_bounds__(kBktThreads) void k_ob_part(const u64* __res
 #pragma unroll
   for (int e = 0; e < kPartItems; ++e) {
     const u64 j = j0 + u64(e) * kBktThreads + threadIdx.x;
-    x[e] = j < nr ? rkey[j] : 0ull;
+    x[e] = j >= nr ? 0ull : hi ? u64(reinterpret_cast<const u32*>(rkey)[j]) | (u64(hi[j]) << 32) : rkey[j];
   }
   __syncthreads();
   const u32 sh1 = bp.K - bp.b1;
@@ -593,7 +648,7 @@ static __global__ __launch_bounds__(kBktThreads) void k_ob_part(const u64* __res
     const u64 j = j0 + u64(e) * kBktThreads + threadIdx.x;
     slot[e] = ~0u;
     if (j >= nr) continue;
-    const u64 h = bp.T.mix(own_pack_key(x[e] & ~kLocalMulti, 0, B));
+    const u64 h = hi ? x[e] : bp.T.mix(own_pack_key(x[e] & ~kLocalMulti, 0, B));
     const u32 c = bp.b1 ? u32(h >> sh1) : 0u;
     r[e] = ((h & lowmask) << kPartLog) | (j - j0);
     slot[e] = (c << 16) | atomicAdd(&cur[c], 1u);
@@ -854,19 +909,43 @@ static __global__ __launch_bounds__(kBlock) void k_own_getid_list(const u32* __r
 // gnf / gmul arrive zeroed (k_node_keys, or the exchange's memsets): only the set flags are
 // written.  nfl (optional): the positions not globally first, counted in *nnf and listed while
 // there are at most kNfListCap of them (k_dist_rank's sparse path).
+// Owner replies packed 2 bits per record (the fused schedule, gcz_dist_fast.h): per source
+// segment s of the owner's receive layout D, ceil(n_s / 4) bytes at P4.d[s]; codes 0 (a single
+// key), 1 (the first of a repeated key: reply 6), 2 (not first: reply 7).
+// (sd / p4: the two Displ's starts staged in LDS -- a kernel argument indexed by a register
+// would go through scratch)
+__device__ __forceinline__ unsigned char reply_unpack2(const unsigned char* __restrict__ p2, const u64* sd,
+                                                       const u64* p4, u32 R, u64 k, u32& q) {
+  while (q + 1 < R && k >= sd[q + 1]) ++q;   // (k only grows along a thread's records)
+  const u64 i = k - sd[q];
+  const u32 c = (p2[p4[q] + (i >> 2)] >> (2 * (i & 3))) & 3u;
+  return c == 0 ? 0 : c == 1 ? 6 : 7;
+}
+
+// p2 != null: the replies arrive packed (reply_unpack2, P4 the packed segment starts), sflag unused.
 static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restrict__ sidx, u64 nsent,
                                                               const unsigned char* __restrict__ sflag,
                                                               unsigned char* __restrict__ gnf,
                                                               unsigned char* __restrict__ gmul, Displ SD, u32 R,
                                                               u64* __restrict__ cnt, u32* __restrict__ clist,
                                                               u32* __restrict__ lcnt, u32* __restrict__ nfl,
-                                                              u32* __restrict__ nnf) {
+                                                              u32* __restrict__ nnf,
+                                                              const unsigned char* __restrict__ p2 = nullptr,
+                                                              Displ P4 = {}) {
   __shared__ u32 hc[kMaxRanks], hd[kMaxRanks];
+  __shared__ u64 s_sd[kMaxRanks + 1], s_p4[kMaxRanks + 1];
   const int tid = threadIdx.x;
   if (tid < int(R)) { hc[tid] = 0; hd[tid] = 0; }
+  if (tid <= kMaxRanks) {
+    s_sd[tid] = SD.d[tid];
+    s_p4[tid] = P4.d[tid];
+  }
   __syncthreads();
   const u64 k0 = u64(blockIdx.x) * kTile;
   constexpr int kB = 8;   // records whose index and flag are loaded together
+  u32 q2 = 0;   // the packed replies' segment of this thread's records
+  if (p2)
+    while (q2 + 1 < R && k0 >= s_sd[q2 + 1]) ++q2;
   for (int e0 = 0; e0 < kItems; e0 += kB) {
     u32 li[kB];
     unsigned char fl[kB];
@@ -874,7 +953,7 @@ static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restr
     for (int b = 0; b < kB; ++b) {
       const u64 k = k0 + u64(e0 + b) * kBlock + tid;
       li[b] = k < nsent ? sidx[k] : 0u;
-      fl[b] = k < nsent ? sflag[k] : 0;
+      fl[b] = k >= nsent ? 0 : p2 ? reply_unpack2(p2, s_sd, s_p4, R, k, q2) : sflag[k];
     }
 #pragma unroll
     for (int b = 0; b < kB; ++b) {

@@ -111,6 +111,24 @@ constexpr u32 kFlSeg = kFlCap + 1;
     atomicAdd(reinterpret_cast<unsigned long long*>(&onf[threadIdx.x]), (unsigned long long)s_c[threadIdx.x]);
 }
 
+// The owner's replies (k_bkt_dedupe2<true>: 0, 6 first of a repeated key, 7 not first) packed
+// 2 bits per record, segment by segment (reply_unpack2 reads them): one thread per output byte.
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_pack2(const unsigned char* __restrict__ rflag,
+                                                      Displ D, Displ P4, u32 R, unsigned char* __restrict__ out) {
+  const u64 t = u64(blockIdx.x) * 256 + threadIdx.x;
+  if (t >= P4.d[R]) return;
+  const u32 s = seg_of(P4, R, t);
+  const u64 i0 = (t - P4.d[s]) * 4, n = D.d[s + 1] - D.d[s];
+  u32 b = 0;
+#pragma unroll
+  for (u32 j = 0; j < 4; ++j)
+    if (i0 + j < n) {
+      const unsigned char f = rflag[D.d[s] + i0 + j];
+      b |= u32(f == 0 ? 0 : f == 6 ? 1 : 2) << (2 * j);
+    }
+  out[t] = (unsigned char)b;
+}
+
 struct FlPairs {   // layer-0 pairs of every rank (host-known from the plan)
   u64 p[kMaxRanks];
 };
@@ -172,7 +190,7 @@ __device__ __forceinline__ u64 fl_guard(const u64* __restrict__ g4, u32 R) {
     for (int q = 0; q < kB; ++q) ok[q] = rec_get_canon(rs, u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid, key[q], lid[q]);
 #pragma unroll
     for (int q = 0; q < kB; ++q)
-      if (ok[q]) atomicAdd(&h[owner_of(key[q], rs.R)], 1u);
+      if (ok[q]) atomicAdd(&h[rec_dest(rs, key[q])], 1u);
   }
   __syncthreads();
   if (tid < int(rs.R)) blockcnt[u64(tid) * nb + blockIdx.x] = h[tid];

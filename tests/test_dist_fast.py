@@ -161,3 +161,35 @@ def test_fast_declines_repetitive_and_iupac(world, gcz, manifest):
         assert gcz.digest(g.tree()) == _single(gcz, iu)
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_fast_equals_general_symmetric_variants(world, gcz):
+    """Pairs next to their symmetric variants: (A, B) with (A mirrored, B), (A transposed, B),
+    (A, B mirrored), the mirrored node (B~, A~), the transposed node (A', B') and palindromic
+    leaves -- every child bit the 6-byte records re-label (canonical-code rank, m, t) must keep
+    distinct classes apart and equal ones together."""
+    rng = np.random.default_rng(40 + world)
+    L = 12
+    comp = np.array([3, 2, 1, 0], np.uint8)      # A<->T, C<->G on codes 0..3 = A,C,G,T
+    base = rng.integers(0, 4, size=(1_000_000, L), dtype=np.uint8)
+    pal = base[:1000, :6]
+    base[:1000] = np.concatenate([pal, pal[:, ::-1]], axis=1)   # mirror-invariant leaves
+    a, b = base[0::2], base[1::2]
+    variants = [(a, b), (a[:, ::-1], b), (comp[a], b), (a, b[:, ::-1]), (b[:, ::-1], a[:, ::-1]),
+                (comp[a], comp[b]), (comp[b][:, ::-1], comp[a][:, ::-1]), (a, comp[b])]
+    pairs = []
+    for x, y in variants:
+        pairs.append(np.stack([x, y], axis=1))
+    strands = np.concatenate(pairs).reshape(-1, L)
+    order = rng.permutation(strands.shape[0] // 2)
+    strands = strands.reshape(-1, 2, L)[order].reshape(-1, L)
+    bases = np.frombuffer(b"ACGT", np.uint8)[strands].reshape(-1).copy()
+    ref = _single(gcz, bases)
+    g = _group(gcz, world)
+    try:
+        _build(gcz, g, bases)
+        assert _schedule(g) in ("fast", "fast, discarded")
+        assert gcz.digest(g.tree()) == ref
+    finally:
+        g.close()
