@@ -190,7 +190,7 @@ hipError_t allow_lds(F f, int bytes) {   // dynamic LDS above the default 64 KB
 }  // namespace
 
 int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool check, bool list, bool* used,
-                           u64* vec) {
+                           u64* vec, bool pack_only) {
   *used = false;
   const u64 S = a.S;
   const u32 L = u32(a.L);
@@ -223,8 +223,6 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
       (rc = ensure(dl_fl, ncodes * 4 + 16)) || (rc = ensure(dl_fo, u64(P.NB) * (P.nch + 1) * 4 + 16)))
     return rc;
   if (list && (rc = ensure(dl_pb, (ncodes / 64 + 1) * 8))) return rc;
-  u64* sdesc = dl_desc.as<u64>();
-  u32* tickets = reinterpret_cast<u32*>(sdesc + t_cnt + t_fb);
   const int first_bytes = int(((1u << P.IB) + P.nch + 1) * 4);
   if (first_bytes > 160 * 1024) return GCZ_OK;   // (never at L <= 12, S < 2^29)
   const int scat_bytes = int((kDC + 3 * kDNBMax + 1 + 16 + kDC / 64) * 4);
@@ -256,19 +254,11 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
   hipLaunchKernelGGL(k_dup_decide, dim3(1), dim3(1), 0, stream, d_hdr, ip, u32(predup_mode));
   HIP_TRY(hipGetLastError());
   prof_end(KID_DL_PACK, e0);
-  prof_begin(KID_DL_SCAN, e0);
-  hipLaunchKernelGGL(k_scan_excl<ScanU32>, dim3(unsigned(t_cnt)), dim3(kScanThreads), 0, stream,
-                     ScanU32{dl_cnt.as<u32>(), ncnt}, ncnt + 1, dl_off.as<u32>(), sdesc, &tickets[0],
-                     static_cast<u64*>(nullptr));
-  hipLaunchKernelGGL(k_dl_tr, dim3((P.nch + 1 + 31) / 32, (P.NB + 31) / 32), dim3(256), 0, stream, dl_off.as<u32>(),
-                     P.NB, P.nch + 1, u64(P.nch), dl_offt.as<u32>());
-  HIP_TRY(hipGetLastError());
-  prof_end(KID_DL_SCAN, e0);
-  prof_begin(KID_DL_SCATTER, e0);
-  hipLaunchKernelGGL(k_dl_scatter, dim3(P.nch), dim3(kDThreads), scat_bytes, stream, dl_pw.as<u32>(), P,
-                     dl_offt.as<u32>(), dl_rec.as<u32>());
-  HIP_TRY(hipGetLastError());
-  prof_end(KID_DL_SCATTER, e0);
+  if (pack_only) {   // (the fused multi-rank schedule queues its own work before the rest)
+    *used = true;
+    return GCZ_OK;
+  }
+  if (int rc2 = dense_phase_a2(a)) return rc2;
   if (check) {
     // the host waits for the pack's verdict only, while the scan and scatter (harmless on a
     // failed pack: rejected strands carry no record) keep the device busy
@@ -283,10 +273,49 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
     }
   }
   *used = true;
+  return dense_phase_a3(d_hdr, ucount, list, vec);
+}
+
+// scan of the (bucket, chunk) counts and the records' scatter into bucket order
+int gcz_ctx::dense_phase_a2(const LeafLevel& a) {
+  (void)a;
+  const DensePlan& P = dl_plan;
+  const u64 ncnt = u64(P.NB) * P.nch, nfb = (P.S + 63) / 64;
+  const u64 t_cnt = scan_tiles(ncnt + 1), t_fb = scan_tiles(nfb + 1);
+  u64* sdesc = dl_desc.as<u64>();
+  u32* tickets = reinterpret_cast<u32*>(sdesc + t_cnt + t_fb);
+  const int scat_bytes = int((kDC + 3 * kDNBMax + 1 + 16 + kDC / 64) * 4);
+  hipEvent_t e0{};
+  prof_begin(KID_DL_SCAN, e0);
+  hipLaunchKernelGGL(k_scan_excl<ScanU32>, dim3(unsigned(t_cnt)), dim3(kScanThreads), 0, stream,
+                     ScanU32{dl_cnt.as<u32>(), ncnt}, ncnt + 1, dl_off.as<u32>(), sdesc, &tickets[0],
+                     static_cast<u64*>(nullptr));
+  hipLaunchKernelGGL(k_dl_tr, dim3((P.nch + 1 + 31) / 32, (P.NB + 31) / 32), dim3(256), 0, stream, dl_off.as<u32>(),
+                     P.NB, P.nch + 1, u64(P.nch), dl_offt.as<u32>());
+  HIP_TRY(hipGetLastError());
+  prof_end(KID_DL_SCAN, e0);
+  prof_begin(KID_DL_SCATTER, e0);
+  hipLaunchKernelGGL(k_dl_scatter, dim3(P.nch), dim3(kDThreads), scat_bytes, stream, dl_pw.as<u32>(), P,
+                     dl_offt.as<u32>(), dl_rec.as<u32>());
+  HIP_TRY(hipGetLastError());
+  prof_end(KID_DL_SCATTER, e0);
+  return GCZ_OK;
+}
+
+// first positions; single device: + the first bitmap and its popcount scan (the unique count);
+// multi-rank (list): + the presence bitmap and the status words only -- the r-first filter,
+// position bitmap and ranks follow the bitmap exchange (gcz_dist.hip)
+int gcz_ctx::dense_phase_a3(Header* d_hdr, u64* ucount, bool list, u64* vec) {
+  const DensePlan& P = dl_plan;
+  const u64 ncnt = u64(P.NB) * P.nch, nfb = (P.S + 63) / 64;
+  const u64 t_cnt = scan_tiles(ncnt + 1), t_fb = scan_tiles(nfb + 1);
+  const u64 ncodes = u64(1) << (2 * P.L);
+  u64* sdesc = dl_desc.as<u64>();
+  u32* tickets = reinterpret_cast<u32*>(sdesc + t_cnt + t_fb);
+  const int first_bytes = int(((1u << P.IB) + P.nch + 1) * 4);
+  hipEvent_t e0{};
   prof_begin(KID_DL_FIRST, e0);
   if (list && (1u << P.IB) < 64) HIP_TRY(hipMemsetAsync(dl_pb.ptr, 0, (ncodes / 64 + 1) * 8, stream));
-  // (multi-rank, list: first positions, the presence bitmap and the status words only -- the
-  // r-first filter, position bitmap and ranks follow the bitmap exchange, gcz_dist.hip)
   hipLaunchKernelGGL(k_dl_first, dim3(P.NB), dim3(kDThreads), first_bytes, stream, dl_rec.as<u32>(), dl_off.as<u32>(),
                      P, dl_fpg.as<u32>(), list ? nullptr : dl_fl.as<u32>(), dl_fo.as<u32>(),
                      list ? dl_pb.as<unsigned long long>() : nullptr, static_cast<const Header*>(d_hdr),

@@ -99,7 +99,8 @@ enum KernelId {
   KID_LEAF, KID_NODE, KID_FLAGSCAN_LEAF, KID_FLAGSCAN_NODE, KID_RESOLVE_LEAF, KID_RESOLVE_NODE, KID_MEMSET,
   KID_EXCHANGE, KID_DIST, KID_OWNER, KID_IDS, KID_REMAP, KID_TAIL, KID_SORT, KID_DAG, KID_DIRECT,
   KID_BKT_COUNT, KID_BKT_SCAN, KID_BKT_SCATTER, KID_BKT_DEDUPE, KID_BKT_FINE,
-  KID_DL_PACK, KID_DL_SCAN, KID_DL_SCATTER, KID_DL_FIRST, KID_DL_FBSCAN, KID_DL_IDS, KID_DL_WORDS, KID_L0, KID_COUNT
+  KID_DL_PACK, KID_DL_SCAN, KID_DL_SCATTER, KID_DL_FIRST, KID_DL_FBSCAN, KID_DL_IDS, KID_DL_WORDS, KID_L0, KID_MARK,
+  KID_COUNT
 };
 inline const char* kernel_name(int k) {
   static const char* names[KID_COUNT] = {"leaf_insert", "node_insert", "flagscan_leaf", "flagscan_node",
@@ -107,7 +108,7 @@ inline const char* kernel_name(int k) {
                                          "dist_owner", "dist_ids", "dist_remap", "tail", "sort", "dag_write", "direct_levels",
                                          "bucket_count", "bucket_scan", "bucket_scatter", "bucket_dedupe", "bucket_fine",
                                          "dl_pack", "dl_scan", "dl_scatter", "dl_first", "dl_fbscan", "dl_ids",
-                                         "dl_words", "dist_l0"};
+                                         "dl_words", "dist_l0", "mark"};
   return names[k];
 }
 
@@ -377,7 +378,12 @@ struct gcz_ctx {
   // ids_done: the multi-rank ids kernel already wrote them) and words (leaves: write the
   // unique leaves, or null).
   int dense_phase_a(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr, gcz_host::u64* ucount, bool check, bool list,
-                    bool* used, gcz_host::u64* vec = nullptr);   // vec (list): the first exchange's status words
+                    bool* used, gcz_host::u64* vec = nullptr,    // vec (list): the first exchange's status words
+                    bool pack_only = false);                     // ... stop after the pack (dense_phase_a2 goes on)
+  // the rest of phase A after a pack_only call: scan + scatter (a2), first positions (a3; list:
+  // the presence bitmap and status words instead of the first bitmap and its scan)
+  int dense_phase_a2(const gcz_host::LeafLevel& a);
+  int dense_phase_a3(gcz_dev::Header* d_hdr, gcz_host::u64* ucount, bool list, gcz_host::u64* vec);
   int dense_phase_b(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr, const gcz_host::u32* gid,
                     gcz_host::u64* leaves, bool ids_done = false);
   int node_level(const gcz_host::NodeLevel& a, gcz_dev::Header* d_hdr);

@@ -113,6 +113,10 @@ struct Transport {
       if (int rc = alltoallv_at(o.M, o.rev, o.elem, o.sd, o.rd, o.send, o.recv)) return rc;
     return 0;
   }
+  // A bulk group on the transport's second stream (and communicator), beside the build's own:
+  // bulk_stream() null = the build's stream (the testing transports run bulk groups in line).
+  virtual hipStream_t bulk_stream() { return nullptr; }
+  virtual int group_bulk(const std::vector<XOp>& ops) { return group(ops); }
   // rank 0's `bytes` at send[i of rank 0] to recv[i] of every other rank
   virtual int bcast0(size_t bytes, const std::vector<const void*>& send, const std::vector<void*>& recv) = 0;
   // rank 0 receives cnt[r] elements from every rank r, concatenated in rank order
@@ -229,6 +233,7 @@ struct RcclApi {
   ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*Broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*CommSplit)(ncclComm_t, int, int, ncclComm_t*, ncclConfig_t*) = nullptr;   // (optional)
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
   bool ok = false;
 };
@@ -255,6 +260,7 @@ RcclApi& rccl() {
     GCZ_SYM(AllGather, "ncclAllGather");
     GCZ_SYM(Broadcast, "ncclBroadcast");
     GCZ_SYM(GetErrorString, "ncclGetErrorString");
+    GCZ_SYM(CommSplit, "ncclCommSplit");
 #undef GCZ_SYM
     a.ok = a.GetUniqueId && a.CommInitRank && a.CommDestroy && a.CommAbort && a.GroupStart && a.GroupEnd && a.Send && a.Recv &&
            a.AllGather && a.Broadcast && a.GetErrorString;
@@ -271,19 +277,32 @@ struct RcclTransport : Transport {
   int me = 0;
   std::atomic<ncclComm_t> comm{nullptr};
   hipStream_t stream = nullptr;
+  // bulk groups: a second communicator (ncclCommSplit of the first: its own channels) on its own
+  // stream, so a large all-to-all runs beside the build's kernels and small collectives
+  std::atomic<ncclComm_t> comm2{nullptr};
+  hipStream_t stream2 = nullptr;
   ~RcclTransport() override {
+    if (ncclComm_t c = comm2.exchange(nullptr)) (void)rccl().CommDestroy(c);
     if (ncclComm_t c = comm.exchange(nullptr)) (void)rccl().CommDestroy(c);
+    if (stream2) (void)hipStreamDestroy(stream2);
   }
-  void abort() {   // (from the watchdog thread: unblocks the stream and any blocked call)
+  void abort() {   // (from the watchdog thread: unblocks the streams and any blocked call)
+    if (ncclComm_t c = comm2.exchange(nullptr)) (void)rccl().CommAbort(c);
     if (ncclComm_t c = comm.exchange(nullptr)) (void)rccl().CommAbort(c);
+  }
+  hipStream_t bulk_stream() override { return comm2.load() ? stream2 : nullptr; }
+  int group_bulk(const std::vector<XOp>& ops) override {
+    ncclComm_t c2 = comm2.load();
+    if (!c2) return group(ops);
+    return run_group(ops, c2, stream2);
   }
   int check(ncclResult_t r, const char* what) {
     if (r == ncclSuccess) return GCZ_OK;
     err = std::string(what) + ": " + rccl().GetErrorString(r);
     return GCZ_ERR_DEVICE;
   }
-  int self_copy(void* dst, const void* src, size_t bytes) {
-    if (bytes && hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream) != hipSuccess) {
+  int self_copy(void* dst, const void* src, size_t bytes, hipStream_t st = nullptr) {
+    if (bytes && hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st ? st : stream) != hipSuccess) {
       err = "rccl transport self copy failed";
       return GCZ_ERR_DEVICE;
     }
@@ -320,8 +339,8 @@ struct RcclTransport : Transport {
   }
   // every op's self copy first, then all their sends / receives in one group (NCCL matches a
   // pair's several sends and receives in issue order)
-  int group(const std::vector<XOp>& ops) override {
-    ncclComm_t c = comm.load();
+  int group(const std::vector<XOp>& ops) override { return run_group(ops, comm.load(), stream); }
+  int run_group(const std::vector<XOp>& ops, ncclComm_t c, hipStream_t st) {
     if (!c) {
       err = "communicator aborted";
       return GCZ_ERR_DEVICE;
@@ -331,7 +350,7 @@ struct RcclTransport : Transport {
       plans.push_back(p2p_plan(o.M, world, me, o.rev, o.elem, o.sd.data(), o.rd.data()));
       const P2POp& self = plans.back()[size_t(me)];
       if (int rc = self_copy(static_cast<char*>(o.recv[0]) + self.recv_off,
-                             static_cast<const char*>(o.send[0]) + self.send_off, self.send_bytes))
+                             static_cast<const char*>(o.send[0]) + self.send_off, self.send_bytes, st))
         return rc;
     }
     RcclApi& a = rccl();
@@ -342,11 +361,11 @@ struct RcclTransport : Transport {
       for (const P2POp& o : plans[k]) {
         if (o.peer == me) continue;
         if (o.send_bytes) {
-          const ncclResult_t r = a.Send(sb + o.send_off, o.send_bytes, ncclUint8, o.peer, c, stream);
+          const ncclResult_t r = a.Send(sb + o.send_off, o.send_bytes, ncclUint8, o.peer, c, st);
           if (r != ncclSuccess) { (void)a.GroupEnd(); return check(r, "ncclSend"); }
         }
         if (o.recv_bytes) {
-          const ncclResult_t r = a.Recv(rb + o.recv_off, o.recv_bytes, ncclUint8, o.peer, c, stream);
+          const ncclResult_t r = a.Recv(rb + o.recv_off, o.recv_bytes, ncclUint8, o.peer, c, st);
           if (r != ncclSuccess) { (void)a.GroupEnd(); return check(r, "ncclRecv"); }
         }
       }
@@ -737,8 +756,8 @@ struct gcz_group {
     xlog.push_back({name, seq, std::move(sent), std::move(recvd), t});
     return GCZ_OK;
   }
-  int xend(int rc) {
-    if (watch) watch->end(ctx[0]->stream);
+  int xend(int rc, hipStream_t st = nullptr) {
+    if (watch) watch->end(st ? st : ctx[0]->stream);
     if (rc && tr) {
       const XRec& x = xlog.back();
       tr->err = "collective #" + std::to_string(x.seq) + " " + x.name + " (this rank sends " + std::to_string(x.sent[0]) +
@@ -787,6 +806,46 @@ struct gcz_group {
     };
     xbegin(name, per_local([&](int me) { return tot(me, true); }), per_local([&](int me) { return tot(me, false); }));
     return xend(tr->group(ops));
+  }
+  // A bulk group (Transport::group_bulk) on the transport's second stream: it starts once the
+  // build's stream reaches the last bulk_mark() (or the call itself); bulk_done() makes the
+  // build's stream wait for it.
+  hipEvent_t ev_bulk_in = nullptr, ev_bulk_out = nullptr;
+  bool bulk_marked = false;
+  int bulk_mark() {
+    if (!tr->bulk_stream()) return GCZ_OK;
+    if (!ev_bulk_in && (hipEventCreateWithFlags(&ev_bulk_in, hipEventDisableTiming) != hipSuccess ||
+                        hipEventCreateWithFlags(&ev_bulk_out, hipEventDisableTiming) != hipSuccess))
+      return dev_fail("bulk events");
+    if (hipEventRecord(ev_bulk_in, ctx[0]->stream) != hipSuccess) return dev_fail("bulk stream order");
+    bulk_marked = true;
+    return GCZ_OK;
+  }
+  int x_group_bulk(const char* name, const std::vector<Transport::XOp>& ops) {
+    hipStream_t bs = tr->bulk_stream();
+    if (bs) {
+      if (!bulk_marked)
+        if (int rc = bulk_mark()) return rc;
+      bulk_marked = false;
+      if (hipStreamWaitEvent(bs, ev_bulk_in, 0) != hipSuccess) return dev_fail("bulk stream order");
+    }
+    const int R = world;
+    auto tot = [&](int me, bool sent) {
+      u64 t = 0;
+      for (const Transport::XOp& o : ops)
+        for (int q = 0; q < R; ++q)
+          if (q != me) t += (sent ? mcount(o.M, R, o.rev, me, q) : mcount(o.M, R, o.rev, q, me)) * o.elem;
+      return t;
+    };
+    xbegin(name, per_local([&](int me) { return tot(me, true); }), per_local([&](int me) { return tot(me, false); }));
+    const int rc = xend(tr->group_bulk(ops), bs);
+    if (!rc && bs && hipEventRecord(ev_bulk_out, bs) != hipSuccess) return dev_fail("bulk stream order");
+    return rc;
+  }
+  int bulk_done() {
+    hipStream_t bs = tr->bulk_stream();
+    if (bs && hipStreamWaitEvent(ctx[0]->stream, ev_bulk_out, 0) != hipSuccess) return dev_fail("bulk stream order");
+    return GCZ_OK;
   }
   int x_allgather(const char* name, size_t bytes, const std::vector<const void*>& s, const std::vector<void*>& r) {
     xbegin(name, per_local([&](int) { return u64(bytes) * u64(world - 1); }),
@@ -881,6 +940,15 @@ struct gcz_group {
   int fast_mode = std::getenv("GCZ_DIST_FAST") ? std::atoi(std::getenv("GCZ_DIST_FAST")) : 1;   // 0: off
   hipEvent_t ev_mid = nullptr;   // the fused schedule's mid-build read (status, counts)
   FlPairs fl_pairs{};            // ... and every rank's layer-0 pairs
+  RecSrc fl_rs[kMaxRanks] = {};  // ... each local rank's layer-0 record source
+  // segment boundaries of the fused schedule's compute stream, a zero-length profiled scope on
+  // every local rank (bench.py splits each rank's kernel time at them: scripts/budget.py's model)
+  void fl_mark(const char*) {
+    for (gcz_ctx* cx : ctx) {
+      ProfScope ps_(cx, KID_MARK);
+    }
+  }
+  Header* cx_hdr(int i) { return ctx[i]->hdr.as<Header>(); }
   int event_sync(hipEvent_t e);
   int build_done();
   int exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwords, u32 key_bits, u32 child_bits,
@@ -1764,7 +1832,6 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
   for (int s = 0; s < R; ++s)
     if (P.count(s, 1) < 2) return GCZ_OK;
   const u64 ncodes = u64(1) << (2 * L), nw = (ncodes + 63) / 64;
-  const u64 nwb = nw + 4 + u64(R);   // bitmap, status words, layer-0 records per owner
   // Layer-0 records: R a power of two -> 6 bytes (PreKey: canonical-code ranks, the owner in
   // the mixed key's top bits); else the raw canonical pair in hashed-code labels, 8 bytes
   const u32 lgR = (R & (R - 1)) == 0 ? log2_exact(u64(R)) : 0u;
@@ -1778,8 +1845,19 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
   for (int s = 0; s < R; ++s) pairs.p[s] = P.count(s, 1);
   std::vector<LeafLevel> las(NL);
   std::vector<u64> dcur(NL, 0);
-  // ---- phase A: the dense pack / sort / first positions, the presence bitmap, and layer 0's
-  // keys from the pre-words (hashed codes as labels), bucketed by owner
+  // fixed capacities of the leaf relay's pieces (a list holds at most min(strands, canonical
+  // 2-bit codes) entries: dna::canonical orbits, Burnside over {id, transpose, mirror, inversion})
+  u64 ncanon = ncodes + (u64(1) << (2 * ((L + 1) / 2)));
+  if (L % 2 == 0) ncanon += u64(1) << L;
+  ncanon /= 4;
+  u64 smax = 0;
+  for (int s = 0; s < R; ++s) smax = std::max(smax, P.count(s, 0));
+  const u64 cap1 = std::min(smax, ncanon) / u64(R) + 2, cap2 = std::min(P.S, ncanon) / u64(R) + u64(R) + 2;
+  const u32 NB0 = u32(std::min<u64>(kDNBMax, ncodes));
+  const u64 xw = (u64(NB0) + 2 + 1) & ~u64(1);
+  const u32 syncw = u32(R) + 6;   // R1a's vector: owner counts, overflow, uniques, symbol, .., predup, non-ACGT
+  // ---- C1 (+ C2, C3 queued before the mid-build read): the dense pack; layer 0's keys from the
+  // pre-words counted per owner; R1a; the keys scattered by owner; the dense sort and presence
   for (int i = 0; i < NL; ++i) {
     gcz_ctx* cx = ctx[i];
     const int r = rank[i];
@@ -1806,12 +1884,12 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     la.S = P.count(r, 0);
     la.L = L;
     la.words = cx->wa.as<u32>();
-    if (cx->ensure(cx->dl_seg, size_t(64 + 3 * R) * 8 + 64) || cx->ensure(cx->dl_pb, nwb * 8) ||
-        cx->ensure(cx->dl_pbs, size_t(R) * nwb * 8 + 16))
+    if (cx->ensure(cx->dl_seg, size_t(64 + 3 * R) * 8 + 64) || cx->ensure(cx->dl_pb, (nw + 4) * 8) ||
+        cx->ensure(cx->dl_pbs, size_t(R) * nw * 8 + 16))
       return dev_fail("dense leaf buffers");
     bool used = false;
     cx->probe_ranks = unsigned(R);
-    const int rc = cx->dense_phase_a(la, h, &h->count[0], false, true, &used, cx->dl_pb.as<u64>() + nw);
+    const int rc = cx->dense_phase_a(la, h, &h->count[0], false, true, &used, cx->dl_pb.as<u64>() + nw, true);
     cx->probe_ranks = 1;
     if (rc) return rc == GCZ_ERR_DEVICE ? dev_fail("dense leaves") : rc;
     if (!used) return GCZ_OK;   // (sizes outside the dense level: the same on every rank)
@@ -1819,7 +1897,8 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     const u32 nb = u32(std::max<u64>(1, (p + kTile - 1) / kTile));
     const u32 cpr = (nb + kScanChunk - 1) / kScanChunk;   // (the three-pass scan of large levels)
     if (u64(R) * nb > kBscanSmall && u64(R) * cpr > 1024) return fail(GCZ_ERR_CAPACITY, "bucket scan: too many chunks");
-    RecSrc rs{};
+    RecSrc& rs = fl_rs[i];
+    rs = RecSrc{};
     rs.pre = cx->dl_pw.as<u32>();
     rs.n = n;
     rs.p = p;
@@ -1839,125 +1918,74 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       rs.pk.c2 = mt.pt.c2;
       if (cx->ensure(d.skey_hi, p * 2 + 16)) return dev_fail("fused schedule buffers");
     }
-    {
-      ProfScope ps_(cx, KID_DIST);
-      hipLaunchKernelGGL(k_fl_count, dim3(nb), dim3(kBlock), 0, cx->stream, rs, d.blockcnt.as<u32>(), nb,
-                         d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(), d.ddesc.as<u64>(), &h->count[kLayerSlot]);
-      if (u64(R) * nb <= kBscanSmall) {
-        hipLaunchKernelGGL(k_bscan_small, dim3(1), dim3(1024), 0, cx->stream, d.blockcnt.as<u32>(), u32(R), nb, dh->sync,
-                           static_cast<const Header*>(h), static_cast<const u64*>(nullptr),
-                           static_cast<const unsigned char*>(nullptr));
-      } else {
-        if (cx->ensure(d.bchunk, u64(R) * cpr * 4 + 64)) return dev_fail("bucket scan");
-        hipLaunchKernelGGL(k_bscan_sum, dim3(R * cpr), dim3(kBlock), 0, cx->stream, d.blockcnt.as<u32>(), nb, cpr,
-                           d.bchunk.as<u32>());
-        hipLaunchKernelGGL(k_bscan_top, dim3(1), dim3(1024), 0, cx->stream, d.bchunk.as<u32>(), u32(R), cpr, dh->sync);
-        hipLaunchKernelGGL(k_bscan_down, dim3(R * cpr), dim3(kBlock), 0, cx->stream, d.blockcnt.as<u32>(), nb, cpr,
-                           static_cast<const u32*>(d.bchunk.as<u32>()));
-      }
-      hipLaunchKernelGGL(k_bucket_scatter, dim3(nb), dim3(kBlock), 0, cx->stream, rs, d.blockcnt.as<u32>(), nb,
-                         d.skey.as<u64>(), d.sidx.as<u32>(), split ? d.skey_hi.as<unsigned short>() : nullptr);
-      G_HIP(hipGetLastError());
-      // the owner counts ride behind the bitmap and the status words
-      G_HIP(hipMemcpyAsync(cx->dl_pb.as<u64>() + nw + 4, dh->sync, size_t(R) * 8, hipMemcpyDeviceToDevice, cx->stream));
+    ProfScope ps_(cx, KID_DIST);
+    hipLaunchKernelGGL(k_fl_count, dim3(nb), dim3(kBlock), 0, cx->stream, rs, d.blockcnt.as<u32>(), nb,
+                       d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(), d.ddesc.as<u64>(), &h->count[kLayerSlot]);
+    if (u64(R) * nb <= kBscanSmall) {
+      hipLaunchKernelGGL(k_bscan_small, dim3(1), dim3(1024), 0, cx->stream, d.blockcnt.as<u32>(), u32(R), nb, dh->sync,
+                         static_cast<const Header*>(h), static_cast<const u64*>(nullptr),
+                         static_cast<const unsigned char*>(nullptr));
+    } else {
+      if (cx->ensure(d.bchunk, u64(R) * cpr * 4 + 64)) return dev_fail("bucket scan");
+      hipLaunchKernelGGL(k_bscan_sum, dim3(R * cpr), dim3(kBlock), 0, cx->stream, d.blockcnt.as<u32>(), nb, cpr,
+                         d.bchunk.as<u32>());
+      hipLaunchKernelGGL(k_bscan_top, dim3(1), dim3(1024), 0, cx->stream, d.bchunk.as<u32>(), u32(R), cpr, dh->sync);
+      hipLaunchKernelGGL(k_bscan_down, dim3(R * cpr), dim3(kBlock), 0, cx->stream, d.blockcnt.as<u32>(), nb, cpr,
+                         static_cast<const u32*>(d.bchunk.as<u32>()));
+      hipLaunchKernelGGL(k_dist_pack, dim3(1), dim3(1), 0, cx->stream, static_cast<const Header*>(h),
+                         static_cast<const u64*>(nullptr), static_cast<const unsigned char*>(nullptr), dh, u32(R));
     }
+    G_HIP(hipGetLastError());
   }
-  // ---- R1: presence bitmaps + status words + owner counts
+  fl_mark("C1");
+  // ---- R1a: status words + owner counts; the host reads them while C2 / C3 run
   {
     std::vector<const void*> s;
     std::vector<void*> rv;
     for (gcz_ctx* cx : ctx) {
-      s.push_back(cx->dl_pb.ptr);
-      rv.push_back(cx->dl_pbs.ptr);
+      s.push_back(cx->dist->dhdr.as<DistHdr>()->sync);
+      rv.push_back(cx->dist->gath.ptr);
     }
     hipEvent_t e0{};
     ctx[0]->prof_begin(KID_EXCHANGE, e0);
-    G_RC(x_allgather("R1 leaf presence bitmaps + status + layer-0 owner counts", nwb * 8, s, rv));
+    G_RC(x_allgather("R1a status + layer-0 owner counts", size_t(syncw) * 8, s, rv));
     ctx[0]->prof_end(KID_EXCHANGE, e0);
-  }
-  // every rank's r-first counts and bucket prefixes from the bitmaps; the host's one mid-build
-  // read (status, owner counts, r-first counts) queued ahead of the leaf level's r-first work
-  const u32 NB = ctx[0]->dl_plan.NB, RB = 1u << ctx[0]->dl_plan.IB;
-  const u64 xw = (u64(NB) + 2 + 1) & ~u64(1);
-  const u64 nmid = u64(R) * (4 + R) + R;
-  for (int i = 0; i < NL; ++i) {
-    gcz_ctx* cx = ctx[i];
-    gcz_dist_state& d = *cx->dist;
-    const DensePlan& DP = cx->dl_plan;
-    if (cx->ensure(d.fl_cntb, u64(R) * NB * 4 + 16) || cx->ensure(d.fl_mid, nmid * 8 + 16) ||
-        cx->ensure(cx->dl_lower, u64(R) * xw * 4 + 16))
-      return dev_fail("fused schedule buffers");
-    ProfScope ps_(cx, KID_DL_FIRST);
-    hipLaunchKernelGGL(k_fl_counts, dim3(NB), dim3(256), 0, cx->stream, cx->dl_pbs.as<unsigned long long>(), nwb, R, DP,
-                       d.fl_cntb.as<u32>());
-    hipLaunchKernelGGL(k_fl_prefix, dim3(1), dim3(kDThreads), 0, cx->stream, static_cast<const u32*>(d.fl_cntb.as<u32>()),
-                       R, DP, xw, cx->dl_lower.as<u32>(), static_cast<const unsigned long long*>(cx->dl_pbs.as<unsigned long long>()),
-                       nwb, nw, d.fl_mid.as<u64>());
-    G_HIP(hipGetLastError());
-  }
-  {
     gcz_dist_state& d0 = *ctx[0]->dist;
-    if (!d0.h_mid && hipHostMalloc((void**)&d0.h_mid, size_t(kMaxRanks) * (kMaxRanks + 5) * 8, hipHostMallocDefault) != hipSuccess)
-      return dev_fail("fused schedule staging");
     if (!ev_mid) G_HIP(hipEventCreateWithFlags(&ev_mid, hipEventDisableTiming));
-    G_HIP(hipMemcpyAsync(d0.h_mid, d0.fl_mid.ptr, nmid * 8, hipMemcpyDeviceToHost, ctx[0]->stream));
+    G_HIP(hipMemcpyAsync(d0.h_gath, d0.gath.ptr, size_t(R) * syncw * 8, hipMemcpyDeviceToHost, ctx[0]->stream));
     G_HIP(hipEventRecord(ev_mid, ctx[0]->stream));
   }
-  // B1 (as dense_leaves): the r-first codes, their position bitmap and local ranks, G in code order
-  for (int i = 0; i < NL; ++i) {
+  for (int i = 0; i < NL; ++i) {   // C2: the keys scattered by owner (K2's input)
     gcz_ctx* cx = ctx[i];
-    const int r = rank[i];
-    const DensePlan& DP = cx->dl_plan;
-    Header* h = cx->hdr.as<Header>();
-    const u64 nfb = (DP.S + 63) / 64, t = scan_tiles(nfb + 1);
-    if (cx->ensure(cx->dl_lh, ncodes * 4 + 16) || cx->ensure(cx->dl_list, std::min<u64>(DP.S, ncodes) * 4 + 16) ||
-        cx->ensure(cx->dl_pos, (u64(NB) + xw) * 4 + 64))
-      return dev_fail("dense leaf buffers");
-    u32* bcnt = cx->dl_pos.as<u32>();
-    u32* xv = bcnt + NB;   // (k_dl_gq's own exchange vector: unused by this schedule)
-    const u64 t_cnt = scan_tiles(u64(NB) * DP.nch + 1);
-    u64* desc = cx->dl_desc.as<u64>() + t_cnt;
-    u32* ticket = reinterpret_cast<u32*>(desc + t) + 1;
-    {
-      ProfScope ps_(cx, KID_DL_FIRST);
-      G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_rfirst), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                int((DP.nch + 1) * 4)));
-      hipLaunchKernelGGL(k_dl_rfirst, dim3(NB), dim3(kDThreads), (DP.nch + 1) * 4, cx->stream, cx->dl_fpg.as<u32>(), DP,
-                         cx->dl_pbs.as<unsigned long long>(), nwb, r, cx->dl_fl.as<u32>(), cx->dl_fo.as<u32>(),
-                         cx->dl_lh.as<u32>(), bcnt);
-      hipLaunchKernelGGL(k_dl_fb, dim3(DP.nch), dim3(kDThreads), 0, cx->stream, cx->dl_fl.as<u32>(), cx->dl_fo.as<u32>(),
-                         DP, cx->dl_fb.as<unsigned long long>());
-      G_HIP(hipGetLastError());
-    }
-    {
-      ProfScope ps_(cx, KID_DL_FBSCAN);
-      hipLaunchKernelGGL(k_scan_excl<ScanPopc>, dim3(unsigned(t)), dim3(kScanThreads), 0, cx->stream,
-                         ScanPopc{cx->dl_fb.as<unsigned long long>()}, nfb, cx->dl_wpre.as<u32>(), desc, ticket,
-                         &h->count[0]);
-      hipLaunchKernelGGL(k_dl_gq, dim3(NB), dim3(kDThreads), 0, cx->stream, cx->dl_lh.as<u32>(), bcnt, DP,
-                         cx->dl_fb.as<unsigned long long>(), cx->dl_wpre.as<u32>(),
-                         static_cast<const u64*>(&h->count[0]), cx->dl_list.as<u32>(), xv, cx->dl_pw.as<u32>(),
-                         static_cast<u64*>(nullptr), static_cast<const u64*>(cx->dl_pb.as<u64>() + nw));
-      G_HIP(hipGetLastError());
-    }
+    gcz_dist_state& d = *cx->dist;
+    const u64 p = P.count(rank[i], 1);
+    const u32 nb = u32(std::max<u64>(1, (p + kTile - 1) / kTile));
+    ProfScope ps_(cx, KID_DIST);
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(nb), dim3(kBlock), 0, cx->stream, fl_rs[i], d.blockcnt.as<u32>(), nb,
+                       d.skey.as<u64>(), d.sidx.as<u32>(), split ? d.skey_hi.as<unsigned short>() : nullptr);
+    G_HIP(hipGetLastError());
   }
-  // ---- the mid-build read: the path, the all-to-all sizes, the relay plan
+  fl_mark("C2");
+  G_RC(bulk_mark());   // (K2 waits for the keys only, not for C3)
+  for (int i = 0; i < NL; ++i) {   // C3: the dense sort, first positions and the presence bitmap
+    int rc = ctx[i]->dense_phase_a2(las[i]);
+    if (!rc) rc = ctx[i]->dense_phase_a3(cx_hdr(i), nullptr, true, ctx[i]->dl_pb.as<u64>() + nw);
+    if (rc) return rc == GCZ_ERR_DEVICE ? dev_fail("dense leaves") : rc;
+  }
+  fl_mark("C3");
+  // ---- the mid-build read: the path, the keys' all-to-all sizes
   G_RC(event_sync(ev_mid));
-  const u64* hm = ctx[0]->dist->h_mid;
-  std::vector<u64> M(size_t(R) * R), c(R), off(R + 1, 0);
+  std::vector<u64> M(size_t(R) * R);
   {
+    const u64* gv = ctx[0]->dist->h_gath;
     u64 st = 0;
     for (int s = 0; s < R; ++s) {
-      const u64* v = hm + size_t(s) * (4 + R);
-      st |= v[0] | v[2];   // a non-ACGT strand (the dense level does not apply), repetitive data
-      for (int q = 0; q < R; ++q) M[size_t(s) * R + q] = v[4 + q];
-      c[s] = hm[size_t(R) * (4 + R) + s];
-      off[s + 1] = off[s] + c[s];
+      const u64* v = gv + size_t(s) * syncw;
+      st |= v[R] | v[R + 4] | v[R + 5];   // an overflow, repetitive data, a strand that is not pure ACGT
+      for (int q = 0; q < R; ++q) M[size_t(s) * R + q] = v[q];
     }
     if (st) return GCZ_OK;   // every rank decides alike from the same words: the general schedule
   }
-  const u64 total = off[R];
-  if (total > u64(kIdx)) return fail(GCZ_ERR_CAPACITY, "more than 2^29-1 unique leaves");
   auto sent = [&](int r) { u64 t = 0; for (int q = 0; q < R; ++q) t += M[size_t(r) * R + q]; return t; };
   auto recvd = [&](int r) { u64 t = 0; for (int q = 0; q < R; ++q) t += M[size_t(q) * R + r]; return t; };
   std::vector<Bkt2Plan> b2(R);
@@ -1987,34 +2015,6 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     for (int q = R; q <= kMaxRanks; ++q) Dd.d[q] = o;
     return Dd;
   };
-  // the leaf relay (dense_leaves): piece q of every G array to rank q, then everyone's pieces to all
-  auto pc = [&](int r, int q) { return c[r] * u64(q) / u64(R); };
-  std::vector<u64> M1(size_t(R) * R), T(R, 0), M2(size_t(R) * R), sd2(size_t(R) * R, 0), rd2(size_t(R) * R);
-  for (int r = 0; r < R; ++r)
-    for (int q = 0; q < R; ++q) {
-      M1[size_t(r) * R + q] = pc(r, q + 1) - pc(r, q);
-      T[q] += M1[size_t(r) * R + q];
-    }
-  for (int q = 0; q < R; ++q)
-    for (int dd = 0; dd < R; ++dd) {
-      M2[size_t(q) * R + dd] = T[q];
-      u64 o = 0;
-      for (int q2 = 0; q2 < q; ++q2) o += T[q2];
-      rd2[size_t(dd) * R + q] = o;
-    }
-  DlRelay relay{};
-  {
-    u64 o = 0;
-    for (int q = 0; q < R; ++q)
-      for (int r = 0; r < R; ++r) {
-        const size_t sg = size_t(r) * R + q;
-        relay.seg_src[sg] = o;
-        relay.seg_dst[sg] = off[r] + pc(r, q);
-        relay.seg_len[sg] = M1[sg];
-        o += M1[sg];
-      }
-    for (int r = 0; r <= R; ++r) relay.off[r] = off[r];
-  }
   // owner-side tables and buffers
   std::vector<OwnTab> otab(NL);
   for (int i = 0; i < NL; ++i) {
@@ -2035,10 +2035,13 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
         cx->ensure(d.ob_rec2, nfine * kFineCap * 8) || cx->ensure(d.ob_fo, nfine * ((u64(1) << bp.b2) + 1) * 4 + 16) ||
         cx->ensure(d.scval, cd) || cx->ensure(d.rcval, cd) || cx->ensure(d.rdval, cd) || cx->ensure(d.sdval, cd) ||
         cx->ensure(d.fl_g3, size_t(R) * kMaxRanks * 8 + 16) || cx->ensure(d.fl_g4, size_t(R) * 2 * 8 + 16) ||
-        cx->ensure(d.nfl, kNfListCap * 4 + 16) || cx->ensure(cx->dl_stage, T[r] * 4 + 16) ||
-        cx->ensure(d.omin, nr / 4 + u64(R) + 64) ||   // (the packed replies)
+        cx->ensure(d.nfl, kNfListCap * 4 + 16) || cx->ensure(d.omin, nr / 4 + u64(R) + 64) ||   // (packed replies)
         (split && cx->ensure(d.rkey_hi, nr * 2 + 16)) ||
-        cx->ensure(cx->dl_recv, total * 4 + 16) || cx->ensure(cx->dl_gid, sizeof(DlRelay) + 16))
+        cx->ensure(cx->dl_stage, (2 * u64(R) * cap1 + cap2) * 4 + 16) || cx->ensure(cx->dl_recv, u64(R) * cap2 * 4 + 16) ||
+        cx->ensure(cx->dl_gid, sizeof(DlRelay) + 16) || cx->ensure(d.fl_cntb, u64(R) * NB0 * 4 + 16) ||
+        cx->ensure(cx->dl_lower, u64(R) * xw * 4 + 16) || cx->ensure(cx->dl_lh, ncodes * 4 + 16) ||
+        cx->ensure(cx->dl_list, std::min<u64>(P.count(r, 0), ncodes) * 4 + 16) ||
+        cx->ensure(cx->dl_pos, (u64(NB0) + xw) * 4 + 64))
       return dev_fail("fused schedule buffers");
     bp.T.tab = d.owntab.as<u64>();
     bp.olist = d.olist.as<u32>();
@@ -2056,23 +2059,16 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     ot.nolocal = 1;
     G_HIP(hipMemsetAsync(d.scval.ptr, 0, cd, cx->stream));   // C / D slot counts (and records)
     G_HIP(hipMemsetAsync(d.rdval.ptr, 0, cd, cx->stream));
-    // the relay table, staged in pinned memory the context owns
-    if (!d.h_relay && hipHostMalloc((void**)&d.h_relay, sizeof(DlRelay), hipHostMallocDefault) != hipSuccess)
-      return dev_fail("dense leaf relay staging");
-    *d.h_relay = relay;
-    G_HIP(hipMemcpyAsync(cx->dl_gid.ptr, d.h_relay, sizeof(DlRelay), hipMemcpyHostToDevice, cx->stream));
   }
-  // ---- R2: layer-0 keys to their owners | leaf G arrays, relay 1
+  // ---- K2: layer-0 keys to their owners, a bulk group beside the build's stream
   {
-    std::vector<const void*> sk, sh, sg;
-    std::vector<void*> rk, rh, rg;
+    std::vector<const void*> sk, sh;
+    std::vector<void*> rk, rh;
     for (gcz_ctx* cx : ctx) {
       sk.push_back(cx->dist->skey.ptr);
       rk.push_back(cx->dist->rkey.ptr);
       sh.push_back(cx->dist->skey_hi.ptr);
       rh.push_back(cx->dist->rkey_hi.ptr);
-      sg.push_back(cx->dl_list.ptr);
-      rg.push_back(cx->dl_stage.ptr);
     }
     std::vector<Transport::XOp> ops;
     if (split) {   // 6-byte records: low 32 bits | high 16 bits
@@ -2081,14 +2077,90 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     } else {
       ops.push_back(xop_a2a(M, R, false, 8, sk, rk));
     }
-    ops.push_back(xop_a2a(M1, R, false, 4, sg, rg));
     hipEvent_t e0{};
     ctx[0]->prof_begin(KID_EXCHANGE, e0);
-    G_RC(x_group("R2 layer-0 keys to owners | leaf G arrays, relay 1", ops));
+    G_RC(x_group_bulk("K2 [bulk] layer-0 keys to owners", ops));
     ctx[0]->prof_end(KID_EXCHANGE, e0);
   }
-  // owners: the two-pass hash-cons of their records (first = lowest receive index: the sources
-  // send in position order and arrive in rank order), then their not-first counts per source
+  // ---- R1b: the presence bitmaps
+  {
+    std::vector<const void*> s;
+    std::vector<void*> rv;
+    for (gcz_ctx* cx : ctx) {
+      s.push_back(cx->dl_pb.ptr);
+      rv.push_back(cx->dl_pbs.ptr);
+    }
+    hipEvent_t e0{};
+    ctx[0]->prof_begin(KID_EXCHANGE, e0);
+    G_RC(x_allgather("R1b leaf presence bitmaps", nw * 8, s, rv));
+    ctx[0]->prof_end(KID_EXCHANGE, e0);
+  }
+  // ---- C4: every rank's r-first counts and bucket prefixes from the bitmaps, the relay table;
+  // this rank's r-first codes, their position bitmap and local ranks, G in code order, relay 1 out
+  const u32 RB = 1u << ctx[0]->dl_plan.IB;
+  for (int i = 0; i < NL; ++i) {
+    gcz_ctx* cx = ctx[i];
+    gcz_dist_state& d = *cx->dist;
+    const int r = rank[i];
+    const DensePlan& DP = cx->dl_plan;
+    Header* h = cx->hdr.as<Header>();
+    DistHdr* dh = d.dhdr.as<DistHdr>();
+    const u32 NB = DP.NB;
+    const u64 nfb = (DP.S + 63) / 64, t = scan_tiles(nfb + 1);
+    u32* bcnt = cx->dl_pos.as<u32>();
+    u32* xv = bcnt + NB;   // (k_dl_gq's own exchange vector: unused by this schedule)
+    const u64 t_cnt = scan_tiles(u64(NB) * DP.nch + 1);
+    u64* desc = cx->dl_desc.as<u64>() + t_cnt;
+    u32* ticket = reinterpret_cast<u32*>(desc + t) + 1;
+    {
+      ProfScope ps_(cx, KID_DL_FIRST);
+      hipLaunchKernelGGL(k_fl_counts, dim3(NB), dim3(256), 0, cx->stream, cx->dl_pbs.as<unsigned long long>(), nw, R, DP,
+                         d.fl_cntb.as<u32>());
+      hipLaunchKernelGGL(k_fl_prefix, dim3(1), dim3(kDThreads), 0, cx->stream, static_cast<const u32*>(d.fl_cntb.as<u32>()),
+                         R, DP, xw, cx->dl_lower.as<u32>());
+      hipLaunchKernelGGL(k_fl_relay, dim3(1), dim3(1), 0, cx->stream, static_cast<const u32*>(cx->dl_lower.as<u32>()), xw,
+                         u32(R), u32(r), cap2, cx->dl_gid.as<DlRelay>(), dh->fl_leaf);
+      G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_rfirst), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                int((DP.nch + 1) * 4)));
+      hipLaunchKernelGGL(k_dl_rfirst, dim3(NB), dim3(kDThreads), (DP.nch + 1) * 4, cx->stream, cx->dl_fpg.as<u32>(), DP,
+                         cx->dl_pbs.as<unsigned long long>(), nw, r, cx->dl_fl.as<u32>(), cx->dl_fo.as<u32>(),
+                         cx->dl_lh.as<u32>(), bcnt);
+      hipLaunchKernelGGL(k_dl_fb, dim3(DP.nch), dim3(kDThreads), 0, cx->stream, cx->dl_fl.as<u32>(), cx->dl_fo.as<u32>(),
+                         DP, cx->dl_fb.as<unsigned long long>());
+      G_HIP(hipGetLastError());
+    }
+    {
+      ProfScope ps_(cx, KID_DL_FBSCAN);
+      hipLaunchKernelGGL(k_scan_excl<ScanPopc>, dim3(unsigned(t)), dim3(kScanThreads), 0, cx->stream,
+                         ScanPopc{cx->dl_fb.as<unsigned long long>()}, nfb, cx->dl_wpre.as<u32>(), desc, ticket,
+                         &h->count[0]);
+      hipLaunchKernelGGL(k_dl_gq, dim3(NB), dim3(kDThreads), 0, cx->stream, cx->dl_lh.as<u32>(), bcnt, DP,
+                         cx->dl_fb.as<unsigned long long>(), cx->dl_wpre.as<u32>(),
+                         static_cast<const u64*>(&h->count[0]), cx->dl_list.as<u32>(), xv, cx->dl_pw.as<u32>(),
+                         static_cast<u64*>(nullptr), static_cast<const u64*>(cx->dl_pb.as<u64>() + nw));
+      hipLaunchKernelGGL(k_fl_relay_out, dim3(256), dim3(256), 0, cx->stream, static_cast<const u32*>(cx->dl_list.as<u32>()),
+                         static_cast<const u64*>(dh->fl_leaf), u32(R), cap1, cx->dl_stage.as<u32>());
+      G_HIP(hipGetLastError());
+    }
+  }
+  fl_mark("C4");
+  // ---- R2: leaf G arrays, relay 1 (fixed-capacity slots)
+  {
+    std::vector<const void*> s;
+    std::vector<void*> rv;
+    for (gcz_ctx* cx : ctx) {
+      s.push_back(cx->dl_stage.ptr);
+      rv.push_back(cx->dl_stage.as<u32>() + u64(R) * cap1);
+    }
+    hipEvent_t e0{};
+    ctx[0]->prof_begin(KID_EXCHANGE, e0);
+    G_RC(x_group("R2 leaf G arrays, relay 1", {xop_fixed(R, cap1, 4, s, rv)}));
+    ctx[0]->prof_end(KID_EXCHANGE, e0);
+  }
+  // ---- C5 (after K2): owners hash-cons their records (first = lowest receive index: the
+  // sources send in position order and arrive in rank order), count their not-first records per
+  // source, pack the replies; relay 2 staged
+  G_RC(bulk_done());
   for (int i = 0; i < NL; ++i) {
     gcz_ctx* cx = ctx[i];
     gcz_dist_state& d = *cx->dist;
@@ -2097,30 +2169,42 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     const Bkt2Plan& bp = b2[r];
     const u64 nfine = (u64(1) << bp.b1) * bp.nslice;
     u32* ovf = &cx->hdr.as<Header>()->overflow;
-    ProfScope ps_(cx, KID_OWNER);
-    G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_ob_part), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              int(kPartChunk * 8)));
-    G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_bkt_fine), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              int(kFineCap * 8)));
-    hipLaunchKernelGGL(k_ob_part, dim3(unsigned(bp.G)), dim3(kBktThreads), size_t(kPartChunk) * 8, cx->stream,
-                       d.rkey.as<u64>(), nr, bp, child_bits, d.ob_seg.as<u64>(), d.ob_rt.as<u32>(), d.rflag.as<unsigned char>(),
-                       split ? static_cast<const unsigned short*>(d.rkey_hi.as<unsigned short>()) : nullptr);
-    hipLaunchKernelGGL(k_bkt_fine, dim3(unsigned(nfine)), dim3(kBktThreads), size_t(kFineCap) * 8, cx->stream,
-                       d.ob_seg.as<u64>(), d.ob_rt.as<u32>(), bp, d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(),
-                       static_cast<Header*>(nullptr), static_cast<const u64*>(nullptr), nr, ovf);
-    hipLaunchKernelGGL(k_bkt_dedupe2<true>, dim3(unsigned(u64(1) << (bp.b1 + bp.b2))), dim3(kBktThreads), 0, cx->stream,
-                       d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(), bp, d.oslot.as<u32>(),
-                       Marks{d.rflag.as<unsigned char>(), nullptr}, static_cast<Header*>(nullptr),
-                       static_cast<const u64*>(nullptr), nr, ovf);
     DistHdr* dh = d.dhdr.as<DistHdr>();
-    hipLaunchKernelGGL(k_fl_ownnf, dim3(64), dim3(256), 0, cx->stream, static_cast<const u32*>(d.olist.as<u32>()),
-                       static_cast<const u32*>(&dh->lcnt[1]), displ_recv(r), u32(R), dh->fl_onf);
-    const Displ P4 = displ4(r, true);
-    hipLaunchKernelGGL(k_fl_pack2, dim3(unsigned(std::max<u64>(1, (P4.d[R] + 255) / 256))), dim3(256), 0, cx->stream,
-                       static_cast<const unsigned char*>(d.rflag.as<unsigned char>()), displ_recv(r), P4, u32(R),
-                       d.omin.as<unsigned char>());
-    G_HIP(hipGetLastError());
+    {
+      ProfScope ps_(cx, KID_OWNER);
+      G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_ob_part), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                int(kPartChunk * 8)));
+      G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_bkt_fine), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                int(kFineCap * 8)));
+      hipLaunchKernelGGL(k_ob_part, dim3(unsigned(bp.G)), dim3(kBktThreads), size_t(kPartChunk) * 8, cx->stream,
+                         d.rkey.as<u64>(), nr, bp, child_bits, d.ob_seg.as<u64>(), d.ob_rt.as<u32>(),
+                         d.rflag.as<unsigned char>(),
+                         split ? static_cast<const unsigned short*>(d.rkey_hi.as<unsigned short>()) : nullptr);
+      hipLaunchKernelGGL(k_bkt_fine, dim3(unsigned(nfine)), dim3(kBktThreads), size_t(kFineCap) * 8, cx->stream,
+                         d.ob_seg.as<u64>(), d.ob_rt.as<u32>(), bp, d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(),
+                         static_cast<Header*>(nullptr), static_cast<const u64*>(nullptr), nr, ovf);
+      hipLaunchKernelGGL(k_bkt_dedupe2<true>, dim3(unsigned(u64(1) << (bp.b1 + bp.b2))), dim3(kBktThreads), 0,
+                         cx->stream, d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(), bp, d.oslot.as<u32>(),
+                         Marks{d.rflag.as<unsigned char>(), nullptr}, static_cast<Header*>(nullptr),
+                         static_cast<const u64*>(nullptr), nr, ovf);
+      hipLaunchKernelGGL(k_fl_ownnf, dim3(64), dim3(256), 0, cx->stream, static_cast<const u32*>(d.olist.as<u32>()),
+                         static_cast<const u32*>(&dh->lcnt[1]), displ_recv(r), u32(R), dh->fl_onf);
+      const Displ P4 = displ4(r, true);
+      hipLaunchKernelGGL(k_fl_pack2, dim3(unsigned(std::max<u64>(1, (P4.d[R] + 255) / 256))), dim3(256), 0, cx->stream,
+                         static_cast<const unsigned char*>(d.rflag.as<unsigned char>()), displ_recv(r), P4, u32(R),
+                         d.omin.as<unsigned char>());
+      G_HIP(hipGetLastError());
+    }
+    {
+      ProfScope ps_(cx, KID_DL_FBSCAN);
+      hipLaunchKernelGGL(k_fl_relay_mid, dim3(256), dim3(256), 0, cx->stream,
+                         static_cast<const u32*>(cx->dl_stage.as<u32>() + u64(R) * cap1),
+                         static_cast<const u32*>(cx->dl_lower.as<u32>()), xw, u32(R), u32(r), cap1,
+                         cx->dl_stage.as<u32>() + 2 * u64(R) * cap1);
+      G_HIP(hipGetLastError());
+    }
   }
+  fl_mark("C5");
   // ---- R3: owner replies | leaf G arrays, relay 2 | the owners' not-first counts
   {
     std::vector<const void*> sf, sg, sn;
@@ -2129,26 +2213,20 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       gcz_dist_state& d = *cx->dist;
       sf.push_back(d.omin.ptr);   // (the packed replies)
       rf.push_back(d.sflag.ptr);
-      sg.push_back(cx->dl_stage.ptr);
+      sg.push_back(cx->dl_stage.as<u32>() + 2 * u64(R) * cap1);
       rg.push_back(cx->dl_recv.ptr);
       sn.push_back(d.dhdr.as<DistHdr>()->fl_onf);
       rn.push_back(d.fl_g3.ptr);
     }
-    Transport::XOp relay2;
-    relay2.M = M2;
-    relay2.elem = 4;
-    relay2.sd = sd2;
-    relay2.rd = rd2;
-    relay2.send = sg;
-    relay2.recv = rg;
     hipEvent_t e0{};
     ctx[0]->prof_begin(KID_EXCHANGE, e0);
     G_RC(x_group("R3 owner replies | leaf G arrays, relay 2 | not-first counts",
-                 {xop_a2a(M4, R, true, 1, sf, rf), relay2, xop_allgather(R, u64(R), 8, sn, rn)}));
+                 {xop_a2a(M4, R, true, 1, sf, rf), xop_allgather(R, cap2, 4, sg, rg),
+                  xop_allgather(R, u64(R), 8, sn, rn)}));
     ctx[0]->prof_end(KID_EXCHANGE, e0);
   }
-  // senders: layer-0 id offsets, the replies -> global flags, look-ahead, local ranks of the
-  // globally-first pairs, C records of the shared keys
+  // ---- C6: senders: the replies -> global flags, look-ahead, local ranks of the globally-first
+  // pairs, C records of the shared keys
   for (int i = 0; i < NL; ++i) {
     gcz_ctx* cx = ctx[i];
     gcz_dist_state& d = *cx->dist;
@@ -2176,6 +2254,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
                        u32(r), d.scval.as<u64>(), dh->fl_r4);
     G_HIP(hipGetLastError());
   }
+  fl_mark("C6");
   // ---- R4: C (first holders' ids to owners) | look-ahead + failures
   {
     std::vector<const void*> sc, sv;
@@ -2193,7 +2272,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
                  {xop_fixed(R, kFlSeg, 8, sc, rc), xop_allgather(R, 2, 8, sv, rv)}));
     ctx[0]->prof_end(KID_EXCHANGE, e0);
   }
-  // the leaf level's global ids and words (the relay has landed); owners: C -> D records
+  // ---- C7: the leaf level's global ids (the relay has landed); owners: C -> D records
   for (int i = 0; i < NL; ++i) {
     gcz_ctx* cx = ctx[i];
     gcz_dist_state& d = *cx->dist;
@@ -2204,8 +2283,8 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       ProfScope ps_(cx, KID_DL_IDS);
       G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_ids_mr), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 int(RB * 4)));
-      hipLaunchKernelGGL(k_dl_ids_mr, dim3(NB), dim3(kDThreads), RB * 4, cx->stream, cx->dl_rec.as<u32>(),
-                         cx->dl_off.as<u32>(), DP, cx->dl_pbs.as<unsigned long long>(), nwb, cx->dl_lower.as<u32>(), xw,
+      hipLaunchKernelGGL(k_dl_ids_mr, dim3(DP.NB), dim3(kDThreads), RB * 4, cx->stream, cx->dl_rec.as<u32>(),
+                         cx->dl_off.as<u32>(), DP, cx->dl_pbs.as<unsigned long long>(), nw, cx->dl_lower.as<u32>(), xw,
                          static_cast<const u32*>(cx->dl_recv.as<u32>()), cx->dl_gid.as<DlRelay>(), R, r,
                          cx->dl_idrec.as<u32>());
       G_HIP(hipGetLastError());
@@ -2217,6 +2296,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
                        d.rdval.as<u64>(), &dh->fl_bad);
     G_HIP(hipGetLastError());
   }
+  fl_mark("C7");
   // ---- R5: D (owners forward the ids to the other holders)
   {
     std::vector<const void*> sd;
@@ -2230,8 +2310,8 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     G_RC(x_group("R5 D ids to holders", {xop_fixed(R, kFlSeg, 8, sd, rd)}));
     ctx[0]->prof_end(KID_EXCHANGE, e0);
   }
-  // layer 0 with the global leaf ids, then the direct subtrees of levels 1 .. G-1 (guarded: they
-  // run only when layer 1 is direct everywhere and no rank failed)
+  // ---- C8: layer 0 with the global leaf ids, then the direct subtrees of levels 1 .. G-1
+  // (guarded: they run only when layer 1 is direct everywhere and no rank failed)
   std::vector<u32*> cur_in(NL), cur_out(NL);
   for (int i = 0; i < NL; ++i) {
     gcz_ctx* cx = ctx[i];
@@ -2258,7 +2338,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       a.pp = pairs;
       a.R = u32(R);
       a.me = u32(r);
-      a.leaf_off = u32(off[r]);
+      a.leaf = dh->fl_leaf;
       a.nodes = cx->nodes_out.as<uint2>() + node_base[i][0];
       a.words0 = cx->wb.as<u32>();
       a.guard = &dh->fl_guard;
@@ -2272,7 +2352,6 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
   }
   slice_off.assign(D + 1, std::vector<u64>(R, 0));
   slice_cnt.assign(D + 1, std::vector<u64>(R, 0));
-  for (int s = 0; s < R; ++s) { slice_off[0][s] = off[s]; slice_cnt[0][s] = c[s]; }
   for (int k = 1; k < G;) {
     const int nlev = std::min(kDirectLog, G - k);
     for (int i = 0; i < NL; ++i) {
@@ -2298,19 +2377,24 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     for (int i = 0; i < NL; ++i) std::swap(cur_in[i], cur_out[i]);
     k += nlev;
   }
+  fl_mark("C8");
   // ---- R6 / R7: the top on rank 0, the final vectors; any failure discards the attempt
   bool failed = false;
   G_RC(finish_top(G, true, P.nk[G], cur_in, dcur, true, &failed));
   if (failed) return GCZ_OK;   // (the general schedule rebuilds from scratch)
   const u64* gf = ctx[0]->dist->h_gathf;
-  u64 l0 = 0;
+  u64 l0 = 0, lv = 0;
   for (int s = 0; s < R; ++s) {
+    slice_off[0][s] = lv;
+    slice_cnt[0][s] = gf[size_t(s) * kFinalWords + 2];
+    lv += slice_cnt[0][s];
     slice_off[1][s] = l0;
     slice_cnt[1][s] = gf[size_t(s) * kFinalWords + 3];
     l0 += slice_cnt[1][s];
   }
+  if (lv > u64(kIdx)) return fail(GCZ_ERR_CAPACITY, "more than 2^29-1 unique leaves");
   info.layer_size[0] = l0;
-  info.n_leaves = total;
+  info.n_leaves = lv;
   info.leaf_path = 1;
   info.repetitive = 0;
   *taken = true;
@@ -3011,6 +3095,15 @@ int gcz_group_create_rccl(gcz_ctx* ctx, int rank, int world, const void* unique_
     return GCZ_ERR_DEVICE;
   }
   t->comm.store(comm);
+  // the bulk communicator and stream (every rank makes the same call; without ncclCommSplit,
+  // bulk groups run on the first communicator and stream)
+  if (a.CommSplit && world > 1) {
+    ncclComm_t c2 = nullptr;
+    if (a.CommSplit(comm, 0, rank, &c2, nullptr) == ncclSuccess && c2) {
+      if (hipStreamCreateWithFlags(&t->stream2, hipStreamNonBlocking) == hipSuccess) t->comm2.store(c2);
+      else (void)a.CommDestroy(c2);
+    }
+  }
   auto* g = new gcz_group();
   g->world = world;
   g->tr = t;
@@ -3087,6 +3180,8 @@ int gcz_group_create_shm(gcz_ctx* ctx, int rank, int world, const char* name, ui
 
 void gcz_group_destroy(gcz_group* g) {
   if (!g) return;
+  for (hipEvent_t e : {g->ev_mid, g->ev_bulk_in, g->ev_bulk_out})
+    if (e) (void)hipEventDestroy(e);
   if (g->watch && !g->watch->fired) g->watch->begin(-1, "teardown (collectives a failed build left queued)");
   for (gcz_ctx* c : g->ctx) (void)hipStreamSynchronize(c->stream);
   g->watch.reset();

@@ -29,13 +29,13 @@
 namespace gcz_dev {
 
 constexpr int kMaxRanks = 31;              // owner slot state: one bit per rank + local-multi bit
-constexpr int kSyncWords = kMaxRanks + 5;  // per-rank sync vector (see DistHdr)
+constexpr int kSyncWords = kMaxRanks + 6;  // per-rank sync vector (see DistHdr)
 constexpr int kFinalWords = 4 + GCZ_MAX_LAYERS;
 
 struct DistHdr {
   // per-level sync vector: [0, R) records per owner, [R] overflow, [R+1] local uniques,
   // [R+2] first bad symbol offset (local bytes), [R+3] that symbol, [R+4] repetitive
-  // data (the leaf probe's pre-dedupe decision)
+  // data (the leaf probe's pre-dedupe decision), [R+5] a strand that is not pure ACGT
   u64 sync[kSyncWords];
   // second sync vector: [0] globally-first local uniques, [1, 1+R) C records per owner,
   // [1+R, 1+2R) D records per owner, [1+2R] pairs of the next level with two repeated
@@ -54,6 +54,7 @@ struct DistHdr {
   u64 fl_onf[kMaxRanks];                // this owner's not-first layer-0 records per source (R3's allgather)
   u64 fl_r4[2];                         // {layer-1 pairs with two repeated children, failure} (R4's allgather)
   u64 fl_guard;                         // 0: layer 1 is direct on every rank and none failed
+  u64 fl_leaf[3];                       // this rank's leaf id offset, r-first count, all ranks' total
   u32 fl_bad;                           // a C / D slot overflowed
 };
 
@@ -329,6 +330,7 @@ static __global__ __launch_bounds__(1024) void k_bscan_small(u32* __restrict__ a
     tot[R + 2] = e;
     tot[R + 3] = (e != ~0ull && bases) ? u64(bases[e]) : 0ull;
     tot[R + 4] = u64(h->predup);
+    tot[R + 5] = u64(h->dense_fail);
   }
 }
 
@@ -1114,6 +1116,7 @@ static __global__ void k_dist_pack(const Header* __restrict__ h, const u64* __re
   dh->sync[R + 2] = e;
   dh->sync[R + 3] = (e != ~0ull && bases) ? u64(bases[e]) : 0ull;
   dh->sync[R + 4] = u64(h->predup);
+  dh->sync[R + 5] = u64(h->dense_fail);
 }
 
 // A node level without the local dedupe: every pair is its own local unique (local id =

@@ -12,11 +12,15 @@
 // BEFORE the leaves' global ids exist.  The layer-0 key exchange therefore rides in the same
 // collective groups as the leaf-id exchange instead of after it:
 //
-//   R1  allgather: presence bitmaps + status words + layer-0 owner counts
-//       (the one mid-build host read: status -> path, counts -> exact all-to-all sizes)
-//   R2  keys to owners (code labels) | leaf G arrays, relay 1
-//   R3  owner replies | leaf G arrays, relay 2 | allgather of the owners' not-first counts
-//       per source (-> every rank's layer-0 id offset, no count round of its own)
+//   R1a allgather: status words + layer-0 owner counts (right after the pack and the keys'
+//       count: the one mid-build host read -- the path, the keys' all-to-all sizes)
+//   K2  keys to owners (code labels): one all-to-all on a second stream and communicator, so
+//       it runs beside the leaf level's sort and the next collectives (RCCL; the testing
+//       transports run it in line)
+//   R1b allgather: presence bitmaps
+//   R2  leaf G arrays, relay 1 (fixed-capacity pieces: no host read of the r-first counts)
+//   R3  owner replies (2 bits per record) | leaf G arrays, relay 2 | allgather of the owners'
+//       not-first counts per source (-> every rank's layer-0 id offset, no count round)
 //   R4  C: first holders' ids to owners (fixed-capacity slots) | allgather: look-ahead, status
 //   R5  D: owners forward them to the other holders (fixed-capacity slots)
 //   R6  top words to rank 0 (gather)              R7  final vectors (allgather, host sync)
@@ -73,13 +77,9 @@ constexpr u32 kFlSeg = kFlCap + 1;
 
 // One block: per rank q the exclusive prefix of its per-bucket counts into the layout of the
 // general schedule's gathered exchange vectors (xvs[q * xw + 2 + b], k_dl_ids_mr reads them)
-// with the total at xvs[q * xw]; and the compact vector the host reads at the mid-build sync:
-// mid[q * (4 + R) + j] = rank q's status words and owner counts (behind its bitmap in pbs),
-// mid[R * (4 + R) + q] = c_q.
+// with the total, c_q, at xvs[q * xw].
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_fl_prefix(const u32* __restrict__ cntb, int R, DensePlan P,
-                                                         u64 xw, u32* __restrict__ xvs,
-                                                         const unsigned long long* __restrict__ pbs, u64 stride,
-                                                         u64 nw, u64* __restrict__ mid) {
+                                                         u64 xw, u32* __restrict__ xvs) {
   __shared__ u32 s_tmp[16];
   const int tid = threadIdx.x;
   for (int q = 0; q < R; ++q) {
@@ -90,9 +90,7 @@ constexpr u32 kFlSeg = kFlCap + 1;
     if (tid == 0) {
       xvs[u64(q) * xw] = total;
       xvs[u64(q) * xw + 1] = 0;
-      mid[u64(R) * (4 + R) + q] = total;
     }
-    if (tid < 4 + R) mid[u64(q) * (4 + R) + tid] = pbs[u64(q) * stride + nw + tid];
   }
 }
 
@@ -127,6 +125,76 @@ constexpr u32 kFlSeg = kFlCap + 1;
       b |= u32(f == 0 ? 0 : f == 6 ? 1 : 2) << (2 * j);
     }
   out[t] = (unsigned char)b;
+}
+
+// ---- the leaf relay with fixed-capacity pieces --------------------------------------------
+// Rank s's G list (c_s elements, k_dl_gq) is cut into R pieces, piece q = [c_s q / R,
+// c_s (q + 1) / R) -> rank q (relay 1: slot s of rank q's buffer, cap1 elements per slot); rank
+// q concatenates the pieces it got (relay 2: cap2 elements to every rank, slot q).  The c_s come
+// from the gathered bitmaps (k_fl_prefix: xvs[s * xw]), so every rank computes the layout and
+// k_dl_ids_mr's table itself.
+__device__ __forceinline__ u64 fl_piece(u64 c, u32 q, u32 R) { return c * q / R; }
+
+// one thread: the relay table (DlRelay, k_dl_ids_mr reads where each piece landed) and this
+// rank's leaf id offset, r-first count and the total
+[[maybe_unused]] static __global__ void k_fl_relay(const u32* __restrict__ xvs, u64 xw, u32 R, u32 me, u64 cap2,
+                                                   DlRelay* __restrict__ T, u64* __restrict__ leaf) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  u64 o = 0;
+  for (u32 s = 0; s < R; ++s) {
+    T->off[s] = o;
+    o += xvs[u64(s) * xw];
+  }
+  T->off[R] = o;
+  leaf[0] = T->off[me];
+  leaf[1] = T->off[me + 1] - T->off[me];
+  leaf[2] = o;
+  for (u32 q = 0; q < R; ++q) {
+    u64 at = u64(q) * cap2;   // rank q's block of the relay-2 buffer
+    for (u32 s = 0; s < R; ++s) {
+      const u64 c = xvs[u64(s) * xw], a = fl_piece(c, q, R), len = fl_piece(c, q + 1, R) - a;
+      const u64 sg = u64(s) * R + q;
+      T->seg_src[sg] = at;
+      T->seg_dst[sg] = T->off[s] + a;
+      T->seg_len[sg] = len;
+      at += len;
+    }
+  }
+}
+
+// relay 1, sender side: the rank's G list into slot q of the staging buffer, piece by piece
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_relay_out(const u32* __restrict__ G,
+                                                          const u64* __restrict__ leaf, u32 R, u64 cap1,
+                                                          u32* __restrict__ stage) {
+  const u64 c = leaf[1];
+  for (u64 j = u64(blockIdx.x) * 256 + threadIdx.x; j < c; j += u64(gridDim.x) * 256) {
+    u32 q = u32((j * R) / c);   // (a first guess; exact below)
+    while (q + 1 < R && fl_piece(c, q + 1, R) <= j) ++q;
+    while (q > 0 && fl_piece(c, q, R) > j) --q;
+    stage[u64(q) * cap1 + (j - fl_piece(c, q, R))] = G[j];
+  }
+}
+
+// relay 2, sender side (rank me): the pieces it received (slot s: piece me of list s) back to back
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_relay_mid(const u32* __restrict__ got,
+                                                          const u32* __restrict__ xvs, u64 xw, u32 R, u32 me,
+                                                          u64 cap1, u32* __restrict__ out) {
+  __shared__ u64 s_len[kMaxRanks + 1];
+  if (threadIdx.x == 0) {
+    u64 o = 0;
+    for (u32 s = 0; s < R; ++s) {
+      s_len[s] = o;
+      const u64 c = xvs[u64(s) * xw];
+      o += fl_piece(c, me + 1, R) - fl_piece(c, me, R);
+    }
+    s_len[R] = o;
+  }
+  __syncthreads();
+  for (u64 j = u64(blockIdx.x) * 256 + threadIdx.x; j < s_len[R]; j += u64(gridDim.x) * 256) {
+    u32 s = 0;
+    while (s + 1 < R && s_len[s + 1] <= j) ++s;
+    out[j] = got[u64(s) * cap1 + (j - s_len[s])];
+  }
 }
 
 struct FlPairs {   // layer-0 pairs of every rank (host-known from the plan)
@@ -277,10 +345,11 @@ __device__ __forceinline__ u64 fl_guard(const u64* __restrict__ g4, u32 R) {
                                                    FlPairs pp, u32 R, u32 me) {
   u64 u = 0;
   (void)fl_offset(gonf, R, pp, me, &u);
+  (void)tail0;
   dh->final_vec[0] = u64(h->overflow | h->leaf_overflow) | ((*bad || fl_guard(g4, R)) ? 2ull : 0ull);
   dh->final_vec[1] = has_tail ? u64(h->root) : 0ull;
-  dh->final_vec[2] = u64(tail0);
-  dh->final_vec[3] = u;
+  dh->final_vec[2] = dh->fl_leaf[1];   // this rank's r-first leaves
+  dh->final_vec[3] = u;                // ... and layer-0 uniques
   for (int k = 0; k < GCZ_MAX_LAYERS; ++k)
     dh->final_vec[4 + k] = (has_tail && k >= tail0 && k < D) ? h->count[kLayerSlot + k] : 0ull;
 }
@@ -301,7 +370,8 @@ struct FlL0 {
   const u64* gonf;            // R3's gathered not-first counts
   const u64* g4;              // R4's gathered {look-ahead, failure}
   FlPairs pp;
-  u32 R, me, leaf_off;
+  u32 R, me;
+  const u64* leaf;            // k_fl_relay's {leaf offset, r-first count, total}
   uint2* nodes;               // the rank's slice of layer 0
   u32* words0;                // layer-0 words (the direct subtrees' input)
   u64* guard;
@@ -315,9 +385,10 @@ struct FlL0 {
                                                            const u32* __restrict__ pw, u64* __restrict__ leaves_out,
                                                            FlL0 a) {
   extern __shared__ u32 s_dyn[];
-  __shared__ u32 s_off;
+  __shared__ u32 s_off, s_loff;
   if (threadIdx.x == 0) {
     s_off = u32(fl_offset(a.gonf, a.R, a.pp, a.me, nullptr));
+    s_loff = u32(a.leaf[0]);
     if (blockIdx.x == 0) *a.guard = fl_guard(a.g4, a.R);
   }
   dl_words_chunk(rec, idrec, offt, P, fb, nullptr, 0, s_dyn, [&](const u32* s_w, u32 n, u64 c0) {
@@ -332,9 +403,9 @@ struct FlL0 {
       const u32 sh = u32(c0 + 2 * jj) & 63u;
       const u32 l = s_w[2 * jj], r = 2 * jj + 1 < n ? s_w[2 * jj + 1] : kNullWord;
       if ((fw >> sh) & 1ull)
-        leaves_out[(l & kIdx) - a.leaf_off] = code2_leaf(((pw[c0 + 2 * jj] & kIdx) * P.Kinv) & P.cmask, P.L);
+        leaves_out[(l & kIdx) - s_loff] = code2_leaf(((pw[c0 + 2 * jj] & kIdx) * P.Kinv) & P.cmask, P.L);
       if (2 * jj + 1 < n && ((fw >> (sh + 1)) & 1ull))
-        leaves_out[(r & kIdx) - a.leaf_off] = code2_leaf(((pw[c0 + 2 * jj + 1] & kIdx) * P.Kinv) & P.cmask, P.L);
+        leaves_out[(r & kIdx) - s_loff] = code2_leaf(((pw[c0 + 2 * jj + 1] & kIdx) * P.Kinv) & P.cmask, P.L);
       u32 cl, cr, m, t;
       node_canonical(l, r, cl, cr, m, t);
       const u32 v = ulw(l) == ulw(xf(r, 1, 0));

@@ -44,7 +44,7 @@ def main():
              "final vectors", "leaf dictionary size"}
     # the fused schedule (gcz_dist_fast.h): one collective group per row; its mid-build read
     # waits on an event behind R1 (the r-first work stays queued behind it) -- counted as a sync
-    is_sync = lambda name: name in syncs or name.startswith("R1 ")  # noqa: E731
+    is_sync = lambda name: name in syncs or name.startswith("R1a ")  # noqa: E731
     rows = []
     for k in range(n):
         name = logs[0][k][1]

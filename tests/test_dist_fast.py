@@ -45,7 +45,7 @@ def _build(gcz, g, bases, L=12):
 def _schedule(g):
     """'fast' / 'general' / 'fast, discarded' from the last build's exchange log."""
     names = [e["name"] for e in g.exchange_log(0)]
-    fast = any(n.startswith("R1 ") for n in names)
+    fast = any(n.startswith("R1a ") for n in names)
     general = any(n in ("keys to owners", "leaf presence bitmaps + status") for n in names)
     return "fast, discarded" if fast and general else "fast" if fast else "general"
 
@@ -69,7 +69,7 @@ def uniform_100m(gcz, manifest):
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
 @pytest.mark.parametrize("tail", ["9", None])
 def test_fast_schedule_uniform_golden(world, tail, gcz, uniform_100m, monkeypatch):
-    """100 Mbase uniform ACGT: the fused schedule is taken (7 collective groups) and the tree
+    """100 Mbase uniform ACGT: the fused schedule is taken (9 collective groups, K2 on the bulk stream) and the tree
     equals the compiled reference's, at the deep and at the default partition depth."""
     if tail:
         monkeypatch.setenv("GCZ_DIST_TAIL_LOG2", tail)
@@ -79,7 +79,7 @@ def test_fast_schedule_uniform_golden(world, tail, gcz, uniform_100m, monkeypatc
         _build(gcz, g, bases)
         assert _schedule(g) == "fast"
         log = g.exchange_log(0)
-        assert len(log) == 7, [e["name"] for e in log]
+        assert len(log) == 9, [e["name"] for e in log]
         assert compare_digest(gcz.digest(g.tree()), exp) == {}
     finally:
         g.close()
