@@ -115,7 +115,8 @@ def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None, bu
         return 8 * bp + 128 * max(0, bp - (layer_sizes[0] if layer_sizes else bp))
     # dense leaf level (pure ACGT, L <= 12; gcz_dense.h): streamed bytes per pass
     nch = (S + 32767) // 32768
-    NB = min(1024, 4 ** L)
+    C = 2 ** (2 * L - 1)            # the code space: canonical codes (top bit 0, gcz_dense.h)
+    NB = min(1024, C)
     if kernel == "dl_pack":         # bases in, pre-word out, per-chunk bucket counts
         return S * L + 4 * S + 4 * NB * nch
     if kernel == "dl_scan":         # exclusive scan of the count matrix
@@ -123,11 +124,11 @@ def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None, bu
     if kernel == "dl_scatter":      # pre-word in, record out
         return 8 * S
     if kernel == "dl_first":        # records in, first position per code out, sorted first lists, bitmap
-        return 4 * S + 4 * 4 ** L + 8 * U + S // 8
+        return 4 * S + 4 * C + 8 * U + S // 8
     if kernel == "dl_fbscan":       # bitmap in, per-word prefix out
         return S // 8 + S // 16
     if kernel == "dl_ids":          # first positions in, two random rank reads per key, id per record out
-        return 4 * 4 ** L + 8 * S + 128 * U
+        return 4 * C + 8 * S + 128 * U
     if kernel == "dl_words":        # record, id, pre-word, bitmap in; word and the leaves out
         return 16 * S + S // 8 + 8 * U
     if kernel == "flagscan_leaf":   # not-first marks; firsts: word, slot sector, leaf out, slot->id sector
@@ -150,10 +151,10 @@ def dist_rank_bytes(kernel, L, Sr, r, R, c_r, u_r, n_leaves):
     layer-0 uniques it emits; R ranks).  Streamed bytes + one 64-B sector per random access,
     like algorithmic_bytes, but over what this rank's launches touch: its own strands and pairs,
     the owner side's received records (~pr, owners balance by hash), the code-space passes over
-    all 4^L codes and the R gathered presence bitmaps (gcz_dense.h, gcz_dist_fast.h).  Scopes
+    all 2^(2L-1) canonical codes and the R gathered presence bitmaps (gcz_dense.h, gcz_dist_fast.h).  Scopes
     without HBM work of their own (exchange, tail) count 0."""
     pr = (Sr + 1) // 2
-    C = 4 ** L
+    C = 2 ** (2 * L - 1)
     NB = min(1024, C)
     nch = (Sr + 32767) // 32768
     if kernel == "dl_pack":         # bases in, pre-word out, per-chunk bucket counts
@@ -300,13 +301,24 @@ def rank_summary(rank, build_ms, trace, xlog=None):
     peers), host gaps, and when its leaf level ended (ms after the build's start event); with
     the group's exchange log (gcz_group_xlog), every collective's name and the bytes this rank
     sent to / received from the other ranks."""
-    busy = sum(d for k, _, d in trace if k != "exchange")
+    busy = sum(d for k, _, d in trace if k not in ("exchange", "mark"))
     xch = [(round(t, 3), round(d, 3)) for k, t, d in trace if k == "exchange"]
     leaf_end = max((t + d for k, t, d in trace if k in LEAF_SCOPES), default=None)
     x = sum(d for _, d in xch)
     out = {"rank": rank, "build_ms": round(build_ms, 3), "busy_ms": round(busy, 3), "exchange_ms": round(x, 3),
            "gap_ms": round(build_ms - busy - x, 3),
            "leaf_end_ms": round(leaf_end, 3) if leaf_end is not None else None, "exchanges": xch}
+    if any(k == "mark" for k, _, _ in trace):
+        # the fused schedule's compute segments (gcz_group::build_fast's fl_mark boundaries):
+        # kernel time between consecutive marks, the last segment after the last mark
+        segs, acc = [], 0.0
+        for k, _, d in trace:
+            if k == "mark":
+                segs.append(round(acc, 4))
+                acc = 0.0
+            elif k != "exchange":
+                acc += d
+        out["segments_ms"] = segs + [round(acc, 4)]
     if xlog is not None:
         out["collectives"] = len(xlog)
         out["sent_bytes"] = sum(e["sent"] for e in xlog)
@@ -519,7 +531,7 @@ def main():
     for c in pctxs:
         c.profile(False)
     prof = tables[0]
-    rank_ms = [round(sum(v["total_ms"] for k, v in t.items() if k != "exchange"), 3) for t in tables]
+    rank_ms = [round(sum(v["total_ms"] for k, v in t.items() if k not in ("exchange", "mark")), 3) for t in tables]
     kernels = {}
     rank_model = None
     if mode in ("dist", "virtual"):   # the profiled rank's own launches (rank 0 of the virtual ranks)
@@ -529,7 +541,7 @@ def main():
         rank_model = {"rank": me, "strands": r1 - r0, "pairs": (r1 - r0 + 1) // 2,
                       "first_leaves": group.slice(0, -1)[1], "layer0_uniques": group.slice(0, 0)[1]}
     for name, p in prof.items():
-        if p["launches"] == 0:
+        if p["launches"] == 0 or name == "mark":
             continue
         if rank_model:
             b = dist_rank_bytes(name, L, rank_model["strands"], rank_model["rank"], R, rank_model["first_leaves"],

@@ -201,15 +201,16 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
   P.L = L;
   P.nch = u32((S + kDC - 1) / kDC);
   P.cmask = u32((1ull << (2 * L)) - 1);
-  const u32 cbits = 2 * L;
+  const u32 cbits = dense_code_bits(L);
+  P.hmask = u32((1ull << cbits) - 1);
   // 1024 buckets: LDS tables of RB = 2^14 codes (64 KB, two workgroups per CU) at L = 12
   P.NB = u32(std::min<u64>(kDNBMax, 1ull << cbits));
   P.IB = cbits - log2_exact(P.NB);
   const u32 kmul = 0x5bd1e995u;                     // odd: a bijection mod 4^L
   u32 Ki = kmul;
   for (int i = 0; i < 5; ++i) Ki *= 2u - kmul * Ki;   // inverse mod 2^32 (hence mod 4^L)
-  P.K = kmul & P.cmask;
-  P.Kinv = Ki & P.cmask;
+  P.K = kmul & P.hmask;   // (odd: a bijection mod 2^cbits)
+  P.Kinv = Ki & P.hmask;
   const u64 ncnt = u64(P.NB) * P.nch;
   const u64 nfb = (S + 63) / 64;
   const u64 t_cnt = scan_tiles(ncnt + 1), t_fb = scan_tiles(nfb + 1);
@@ -309,7 +310,7 @@ int gcz_ctx::dense_phase_a3(Header* d_hdr, u64* ucount, bool list, u64* vec) {
   const DensePlan& P = dl_plan;
   const u64 ncnt = u64(P.NB) * P.nch, nfb = (P.S + 63) / 64;
   const u64 t_cnt = scan_tiles(ncnt + 1), t_fb = scan_tiles(nfb + 1);
-  const u64 ncodes = u64(1) << (2 * P.L);
+  const u64 ncodes = u64(1) << dense_code_bits(P.L);
   u64* sdesc = dl_desc.as<u64>();
   u32* tickets = reinterpret_cast<u32*>(sdesc + t_cnt + t_fb);
   const int first_bytes = int(((1u << P.IB) + P.nch + 1) * 4);

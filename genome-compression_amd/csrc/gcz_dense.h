@@ -41,11 +41,16 @@ constexpr u32 kDC = 1u << kDLog;     // strands per chunk (positions in a chunk 
 constexpr int kDThreads = 1024;
 constexpr u32 kDNBMax = 1024;        // buckets (h's top bits)
 
+// Bits of the level's code space: a canonical 2-bit code is the minimum of an orbit that holds
+// the code and its complement (x ^ cmask), which differ in the top bit, so its top bit is 0.
+__host__ __device__ __forceinline__ u32 dense_code_bits(u32 L) { return 2 * L - 1; }
+
 struct DensePlan {
   u64 S;
   u32 nch;     // chunks of kDC strands
   u32 L;
-  u32 cmask;   // 4^L - 1
+  u32 cmask;   // 4^L - 1 (the complement's mask)
+  u32 hmask;   // 2^(2L-1) - 1: hashed codes (a canonical code's top bit is 0, dense_code_bits)
   u32 NB;      // buckets, power of two <= kDNBMax
   u32 IB;      // log2(codes per bucket) <= kDLog
   u32 K, Kinv; // odd multiplier mod 4^L and its inverse
@@ -226,7 +231,7 @@ template <int L, bool kBases>
       if (ok) {
         u32 m, t, v;
         const u32 cc = canon2(x, L, P.cmask, m, t, v);
-        const u32 h = (cc * P.K) & P.cmask;
+        const u32 h = (cc * P.K) & P.hmask;
         pw[s] = make_word(h, m, t, v);
         atomicAdd(&s_hist[h >> ib], 1u);
       } else {
@@ -519,7 +524,7 @@ static __device__ __forceinline__ void dl_words_chunk(const u32* __restrict__ re
     s_w[q] = wr;
     if (leaves_out && ((s_fb[q >> 5] >> (q & 31)) & 1u)) {
       const u32 h = (b << IB) | (((xr & kIdx) >> kDLog) & imask);
-      leaves_out[(wr & kIdx) - leaf_off] = code2_leaf((h * P.Kinv) & P.cmask, P.L);
+      leaves_out[(wr & kIdx) - leaf_off] = code2_leaf((h * P.Kinv) & P.hmask, P.L);
     }
   };
   // the chunk's records walked as one flat sequence of 64-record groups over the runs (every
@@ -695,7 +700,7 @@ __host__ __device__ __forceinline__ bool dl_rleaves_sparse(u64 count, u64 S) { r
     const u32 fp = rfc[u64(b) * RB + j];
     const u32 k = fb_rank(rfb, wpre, fp);
     G[pre + j] = k;
-    if (lv) leaves_out[k] = code2_leaf(((pw[fp] & kIdx) * P.Kinv) & P.cmask, P.L);
+    if (lv) leaves_out[k] = code2_leaf(((pw[fp] & kIdx) * P.Kinv) & P.hmask, P.L);
   }
 }
 
@@ -715,11 +720,12 @@ struct DlRelay {
 // relay's receive buffer.  Codes: 16 contiguous per thread (a quarter word).
 // The G arrays are read where the relay left them (T's pieces: list q's element at global id
 // position off_q + k lies in the piece p with seg_dst <= off_q + k < seg_dst + seg_len).
-[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_ids_mr(const u32* __restrict__ rec, const u32* __restrict__ off,
-                                                         DensePlan P, const unsigned long long* __restrict__ pbs,
-                                                         u64 stride, const u32* __restrict__ xvs, u64 xstride,
-                                                         const u32* __restrict__ gl, const DlRelay* __restrict__ T,
-                                                         int R, int r, u32* __restrict__ idrec) {
+// (dl_ids_mr_block: one workgroup's bucket b; k_dl_ids_mr launches one per bucket)
+static __device__ __forceinline__ void dl_ids_mr_block(const u32* __restrict__ rec, const u32* __restrict__ off,
+                                                       const DensePlan& P, const unsigned long long* __restrict__ pbs,
+                                                       u64 stride, const u32* __restrict__ xvs, u64 xstride,
+                                                       const u32* __restrict__ gl, const DlRelay* __restrict__ T,
+                                                       int R, int r, u32* __restrict__ idrec, u32 b) {
   extern __shared__ u32 s_id[];    // RB
   // ranks q <= r in rounds of QB: their words, first-held words and prefixes loaded and
   // scanned together (one load round trip and two barriers per round, not per rank)
@@ -730,7 +736,7 @@ struct DlRelay {
   __shared__ u32 s_wt[QB][4];
   __shared__ u64 s_mine[256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const u32 b = blockIdx.x, RB = 1u << P.IB, NW = RB >= 64 ? RB / 64 : 1u;
+  const u32 RB = 1u << P.IB, NW = RB >= 64 ? RB / 64 : 1u;
   u64 acc = 0;   // (threads < NW: the OR of the words of the ranks before this round)
   if (u32(tid) < NW) s_mine[tid] = bucket_word(pbs + u64(r) * stride, b, P.IB, tid);
   const u32 lw = u32(tid) >> 2, sh = (u32(tid) & 3u) * 16u;   // this thread's codes: 16 tid .. 16 tid + 15
@@ -821,6 +827,14 @@ struct DlRelay {
   }
 }
 
+[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_ids_mr(const u32* __restrict__ rec, const u32* __restrict__ off,
+                                                         DensePlan P, const unsigned long long* __restrict__ pbs,
+                                                         u64 stride, const u32* __restrict__ xvs, u64 xstride,
+                                                         const u32* __restrict__ gl, const DlRelay* __restrict__ T,
+                                                         int R, int r, u32* __restrict__ idrec) {
+  dl_ids_mr_block(rec, off, P, pbs, stride, xvs, xstride, gl, T, R, r, idrec, blockIdx.x);
+}
+
 // This rank's slice of the unique leaves: its r-first codes in position order (= id order),
 // one thread per position of the r-first position bitmap (a wave shares one bitmap word).
 [[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_rleaves(const unsigned long long* __restrict__ rfb,
@@ -832,7 +846,7 @@ struct DlRelay {
   if (!((m >> (p & 63)) & 1ull)) return;
   const u32 k = wpre[p >> 6] + u32(__popcll(m & ((1ull << (p & 63)) - 1ull)));
   const u32 h = pw[p] & kIdx;
-  out[k] = code2_leaf((h * P.Kinv) & P.cmask, P.L);
+  out[k] = code2_leaf((h * P.Kinv) & P.hmask, P.L);
 }
 
 }  // namespace gcz_dev

@@ -956,14 +956,16 @@ struct gcz_group {
                int* ovf_bits, bool nolocal = false, bool lookahead = false, u64* next_hashed_out = nullptr);
 };
 
-#define G_HIP(x)                                                   \
-  do {                                                             \
-    if ((x) != hipSuccess) return dev_fail(#x);                    \
+#define G_HIP(x)                                                                   \
+  do {                                                                             \
+    const hipError_t e_ = (x);                                                     \
+    if (e_ != hipSuccess) return dev_fail((std::string(#x) + ": " + hipGetErrorString(e_)).c_str()); \
   } while (0)
-#define G_RC(x)                                                    \
-  do {                                                             \
-    int rc_ = (x);                                                 \
-    if (rc_) return rc_ == GCZ_ERR_DEVICE ? dev_fail(#x) : rc_;    \
+// (a device failure keeps the inner message: "outer <- inner")
+#define G_RC(x)                                                                    \
+  do {                                                                             \
+    int rc_ = (x);                                                                 \
+    if (rc_) return rc_ == GCZ_ERR_DEVICE ? fail(rc_, std::string(#x) + " <- " + last_error) : rc_; \
   } while (0)
 
 namespace {
@@ -1046,7 +1048,7 @@ int gcz_group::dense_leaves(const std::vector<const unsigned char*>& bases, cons
   *used = false;
   const int R = world, NL = int(ctx.size());
   const DistPlan& P = plan;
-  const u64 ncodes = u64(1) << (2 * L);
+  const u64 ncodes = u64(1) << dense_code_bits(u32(L));
   const u64 nw = (ncodes + 63) / 64;   // presence bitmap words
   const u64 nwb = nw + 4;               // + the rank's status words (vec) behind its bitmap
   std::vector<LeafLevel> las(NL);
@@ -1831,7 +1833,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
   if (!fast_mode || R < 2 || L > 12 || G < 2 || dense_mode == 0) return GCZ_OK;
   for (int s = 0; s < R; ++s)
     if (P.count(s, 1) < 2) return GCZ_OK;
-  const u64 ncodes = u64(1) << (2 * L), nw = (ncodes + 63) / 64;
+  const u64 ncodes = u64(1) << dense_code_bits(u32(L)), nw = (ncodes + 63) / 64;
   // Layer-0 records: R a power of two -> 6 bytes (PreKey: canonical-code ranks, the owner in
   // the mixed key's top bits); else the raw canonical pair in hashed-code labels, 8 bytes
   const u32 lgR = (R & (R - 1)) == 0 ? log2_exact(u64(R)) : 0u;
@@ -1847,7 +1849,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
   std::vector<u64> dcur(NL, 0);
   // fixed capacities of the leaf relay's pieces (a list holds at most min(strands, canonical
   // 2-bit codes) entries: dna::canonical orbits, Burnside over {id, transpose, mirror, inversion})
-  u64 ncanon = ncodes + (u64(1) << (2 * ((L + 1) / 2)));
+  u64 ncanon = (u64(1) << (2 * L)) + (u64(1) << (2 * ((L + 1) / 2)));
   if (L % 2 == 0) ncanon += u64(1) << L;
   ncanon /= 4;
   u64 smax = 0;
@@ -1908,7 +1910,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       const LevelTab mt = plan_table(nullptr, 256, 2 * Bc + 3, 2, Bc, true, 0);   // (its mix only)
       rs.pk.on = 1;
       rs.pk.Kinv = DP.Kinv;
-      rs.pk.cmask = DP.cmask;
+      rs.pk.cmask = DP.hmask;
       rs.pk.Bc = Bc;
       rs.pk.K = 2 * Bc + 3;
       rs.pk.lgR = lgR;
@@ -2114,12 +2116,16 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     u32* ticket = reinterpret_cast<u32*>(desc + t) + 1;
     {
       ProfScope ps_(cx, KID_DL_FIRST);
+      FlRelayOut fo{};
+      fo.xvs = cx->dl_lower.as<u32>();
+      fo.xw = xw;
+      fo.me = u32(r);
+      fo.cap2 = cap2;
+      fo.T = cx->dl_gid.as<DlRelay>();
+      fo.leaf = dh->fl_leaf;
+      fo.ticket = &dh->fl_ticket;
       hipLaunchKernelGGL(k_fl_counts, dim3(NB), dim3(256), 0, cx->stream, cx->dl_pbs.as<unsigned long long>(), nw, R, DP,
-                         d.fl_cntb.as<u32>());
-      hipLaunchKernelGGL(k_fl_prefix, dim3(1), dim3(kDThreads), 0, cx->stream, static_cast<const u32*>(d.fl_cntb.as<u32>()),
-                         R, DP, xw, cx->dl_lower.as<u32>());
-      hipLaunchKernelGGL(k_fl_relay, dim3(1), dim3(1), 0, cx->stream, static_cast<const u32*>(cx->dl_lower.as<u32>()), xw,
-                         u32(R), u32(r), cap2, cx->dl_gid.as<DlRelay>(), dh->fl_leaf);
+                         d.fl_cntb.as<u32>(), fo);
       G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_rfirst), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 int((DP.nch + 1) * 4)));
       hipLaunchKernelGGL(k_dl_rfirst, dim3(NB), dim3(kDThreads), (DP.nch + 1) * 4, cx->stream, cx->dl_fpg.as<u32>(), DP,
@@ -2187,20 +2193,23 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
                          cx->stream, d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(), bp, d.oslot.as<u32>(),
                          Marks{d.rflag.as<unsigned char>(), nullptr}, static_cast<Header*>(nullptr),
                          static_cast<const u64*>(nullptr), nr, ovf);
-      hipLaunchKernelGGL(k_fl_ownnf, dim3(64), dim3(256), 0, cx->stream, static_cast<const u32*>(d.olist.as<u32>()),
-                         static_cast<const u32*>(&dh->lcnt[1]), displ_recv(r), u32(R), dh->fl_onf);
       const Displ P4 = displ4(r, true);
-      hipLaunchKernelGGL(k_fl_pack2, dim3(unsigned(std::max<u64>(1, (P4.d[R] + 255) / 256))), dim3(256), 0, cx->stream,
-                         static_cast<const unsigned char*>(d.rflag.as<unsigned char>()), displ_recv(r), P4, u32(R),
-                         d.omin.as<unsigned char>());
-      G_HIP(hipGetLastError());
-    }
-    {
-      ProfScope ps_(cx, KID_DL_FBSCAN);
-      hipLaunchKernelGGL(k_fl_relay_mid, dim3(256), dim3(256), 0, cx->stream,
-                         static_cast<const u32*>(cx->dl_stage.as<u32>() + u64(R) * cap1),
-                         static_cast<const u32*>(cx->dl_lower.as<u32>()), xw, u32(R), u32(r), cap1,
-                         cx->dl_stage.as<u32>() + 2 * u64(R) * cap1);
+      FlC5 c{};
+      c.olist = d.olist.as<u32>();
+      c.ocnt = &dh->lcnt[1];
+      c.D = displ_recv(r);
+      c.P4 = P4;
+      c.onf = dh->fl_onf;
+      c.rflag = d.rflag.as<unsigned char>();
+      c.packed = d.omin.as<unsigned char>();
+      c.npack = u32(std::max<u64>(1, (P4.d[R] + 255) / 256));
+      c.got = cx->dl_stage.as<u32>() + u64(R) * cap1;
+      c.xvs = cx->dl_lower.as<u32>();
+      c.xw = xw;
+      c.cap1 = cap1;
+      c.me = u32(r);
+      c.relay2 = cx->dl_stage.as<u32>() + 2 * u64(R) * cap1;
+      hipLaunchKernelGGL(k_fl_c5, dim3(c.npack + 64 + 256), dim3(256), 0, cx->stream, c, u32(R));
       G_HIP(hipGetLastError());
     }
   }
@@ -2281,20 +2290,23 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     DistHdr* dh = d.dhdr.as<DistHdr>();
     {
       ProfScope ps_(cx, KID_DL_IDS);
-      G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_ids_mr), hipFuncAttributeMaxDynamicSharedMemorySize,
+      FlCd c{};
+      c.rc = d.rcval.as<u64>();
+      c.D = displ_recv(r);
+      c.oslot = d.oslot.as<u32>();
+      c.T = otab[i];
+      c.olist = d.olist.as<u32>();
+      c.ocnt = &dh->lcnt[1];
+      c.dbuf = d.rdval.as<u64>();
+      c.bad = &dh->fl_bad;
+      G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_fl_ids_cd), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 int(RB * 4)));
-      hipLaunchKernelGGL(k_dl_ids_mr, dim3(DP.NB), dim3(kDThreads), RB * 4, cx->stream, cx->dl_rec.as<u32>(),
+      hipLaunchKernelGGL(k_fl_ids_cd, dim3(DP.NB + 1), dim3(kDThreads), RB * 4, cx->stream, cx->dl_rec.as<u32>(),
                          cx->dl_off.as<u32>(), DP, cx->dl_pbs.as<unsigned long long>(), nw, cx->dl_lower.as<u32>(), xw,
                          static_cast<const u32*>(cx->dl_recv.as<u32>()), cx->dl_gid.as<DlRelay>(), R, r,
-                         cx->dl_idrec.as<u32>());
+                         cx->dl_idrec.as<u32>(), c);
       G_HIP(hipGetLastError());
     }
-    ProfScope ps_(cx, KID_OWNER);
-    hipLaunchKernelGGL(k_fl_cd, dim3(1), dim3(1024), 0, cx->stream, static_cast<const u64*>(d.rcval.as<u64>()),
-                       displ_recv(r), u32(R), static_cast<const u32*>(d.oslot.as<u32>()), otab[i],
-                       static_cast<const u32*>(d.olist.as<u32>()), static_cast<const u32*>(&dh->lcnt[1]),
-                       d.rdval.as<u64>(), &dh->fl_bad);
-    G_HIP(hipGetLastError());
   }
   fl_mark("C7");
   // ---- R5: D (owners forward the ids to the other holders)
@@ -2318,12 +2330,6 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     gcz_dist_state& d = *cx->dist;
     const int r = rank[i];
     DistHdr* dh = d.dhdr.as<DistHdr>();
-    {
-      ProfScope ps_(cx, KID_IDS);
-      hipLaunchKernelGGL(k_fl_dvals, dim3(16), dim3(256), 0, cx->stream, static_cast<const u64*>(d.sdval.as<u64>()),
-                         displ_send(r), u32(R), static_cast<const u32*>(d.sidx.as<u32>()), d.gid.as<u32>(), &dh->fl_bad);
-      G_HIP(hipGetLastError());
-    }
     {   // the leaf words (global ids) into layer 0 in LDS, chunk by chunk; the rank's leaves
       ProfScope ps_(cx, KID_L0);
       const DensePlan& DP = cx->dl_plan;
@@ -2342,6 +2348,10 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       a.nodes = cx->nodes_out.as<uint2>() + node_base[i][0];
       a.words0 = cx->wb.as<u32>();
       a.guard = &dh->fl_guard;
+      a.rd = d.sdval.as<u64>();
+      a.SD = displ_send(r);
+      a.sidx = d.sidx.as<u32>();
+      a.bad = &dh->fl_bad;
       hipLaunchKernelGGL(k_fl_words_l0, dim3(DP.nch), dim3(kDThreads), words_bytes, cx->stream, cx->dl_rec.as<u32>(),
                          cx->dl_idrec.as<u32>(), cx->dl_offt.as<u32>(), DP, cx->dl_fb.as<unsigned long long>(),
                          static_cast<const u32*>(cx->dl_pw.as<u32>()), cx->leaves_out.as<u64>(), a);
@@ -2486,7 +2496,7 @@ int gcz_group::finish_top(int Gx, bool direct, u64 prev_total, const std::vector
       if (!tail_done) hipLaunchKernelGGL(k_root, dim3(1), dim3(1), 0, cx->stream, in, h);
     }
     if (fl)
-      hipLaunchKernelGGL(k_fl_final, dim3(1), dim3(1), 0, cx->stream, h, dh, Gx, D, int(tail),
+      hipLaunchKernelGGL(k_fl_final, dim3(1), dim3(64), 0, cx->stream, h, dh, Gx, D, int(tail),
                          static_cast<const u32*>(&dh->fl_bad), static_cast<const u64*>(cx->dist->fl_g4.as<u64>()),
                          static_cast<const u64*>(cx->dist->fl_g3.as<u64>()), fl_pairs, u32(R), u32(rank[i]));
     else

@@ -56,6 +56,7 @@ struct DistHdr {
   u64 fl_guard;                         // 0: layer 1 is direct on every rank and none failed
   u64 fl_leaf[3];                       // this rank's leaf id offset, r-first count, all ranks' total
   u32 fl_bad;                           // a C / D slot overflowed
+  u32 fl_ticket;                        // k_fl_counts' last-block ticket
 };
 
 struct Displ {   // segment starts of the R source (or destination) ranks in a buffer, plus the end
@@ -916,15 +917,19 @@ static __global__ __launch_bounds__(kBlock) void k_own_getid_list(const u32* __r
 // key), 1 (the first of a repeated key: reply 6), 2 (not first: reply 7).
 // (sd / p4: the two Displ's starts staged in LDS -- a kernel argument indexed by a register
 // would go through scratch)
-__device__ __forceinline__ unsigned char reply_unpack2(const unsigned char* __restrict__ p2, const u64* sd,
-                                                       const u64* p4, u32 R, u64 k, u32& q) {
+// (the segment search first, for every record of a round, then the loads together)
+__device__ __forceinline__ u64 reply_at2(const u64* sd, const u64* p4, u32 R, u64 k, u32& q, u32& sh) {
   while (q + 1 < R && k >= sd[q + 1]) ++q;   // (k only grows along a thread's records)
   const u64 i = k - sd[q];
-  const u32 c = (p2[p4[q] + (i >> 2)] >> (2 * (i & 3))) & 3u;
+  sh = 2 * u32(i & 3);
+  return p4[q] + (i >> 2);
+}
+__device__ __forceinline__ unsigned char reply_code2(unsigned char byte, u32 sh) {
+  const u32 c = (u32(byte) >> sh) & 3u;
   return c == 0 ? 0 : c == 1 ? 6 : 7;
 }
 
-// p2 != null: the replies arrive packed (reply_unpack2, P4 the packed segment starts), sflag unused.
+// p2 != null: the replies arrive packed (reply_at2 / reply_code2, P4 the packed segment starts), sflag unused.
 static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restrict__ sidx, u64 nsent,
                                                               const unsigned char* __restrict__ sflag,
                                                               unsigned char* __restrict__ gnf,
@@ -951,11 +956,25 @@ static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restr
   for (int e0 = 0; e0 < kItems; e0 += kB) {
     u32 li[kB];
     unsigned char fl[kB];
+    u64 at[kB];
+    u32 sh[kB];
+    if (p2) {
+#pragma unroll
+      for (int b = 0; b < kB; ++b) {
+        const u64 k = k0 + u64(e0 + b) * kBlock + tid;
+        sh[b] = 0;
+        at[b] = k < nsent ? reply_at2(s_sd, s_p4, R, k, q2, sh[b]) : 0ull;
+      }
+    }
 #pragma unroll
     for (int b = 0; b < kB; ++b) {
       const u64 k = k0 + u64(e0 + b) * kBlock + tid;
       li[b] = k < nsent ? sidx[k] : 0u;
-      fl[b] = k >= nsent ? 0 : p2 ? reply_unpack2(p2, s_sd, s_p4, R, k, q2) : sflag[k];
+      fl[b] = k >= nsent ? 0 : p2 ? p2[at[b]] : sflag[k];
+    }
+    if (p2) {
+#pragma unroll
+      for (int b = 0; b < kB; ++b) fl[b] = reply_code2(fl[b], sh[b]);   // (k >= nsent: byte 0 -> 0)
     }
 #pragma unroll
     for (int b = 0; b < kB; ++b) {

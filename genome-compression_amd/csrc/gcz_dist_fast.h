@@ -44,11 +44,67 @@ constexpr u32 kFlSeg = kFlCap + 1;
 
 // Per (bucket, rank q): the codes rank q holds first (present_q & ~(present_0 | ... |
 // present_{q-1})), counted from the gathered presence bitmaps -- every rank derives every
-// rank's r-first counts itself (the general schedule allgathers them).  One block per bucket.
+// rank's r-first counts itself (the general schedule allgathers them).  One block per bucket;
+// the last block to finish (a ticket) then writes, per rank q, the exclusive prefix of its
+// per-bucket counts into the layout of the general schedule's gathered exchange vectors
+// (xvs[q * xw + 2 + b], k_dl_ids_mr reads them) with the total, c_q, at xvs[q * xw], and the
+// leaf relay's table (fl_relay_table).
+// the leaf relay's piece q of a list of c elements: [c q / R, c (q + 1) / R) (see below)
+__device__ __forceinline__ u64 fl_piece(u64 c, u32 q, u32 R) { return c * q / R; }
+
+struct FlRelayOut {
+  u32* xvs;
+  u64 xw;
+  u32 me;
+  u64 cap2;
+  DlRelay* T;
+  u64* leaf;      // {leaf offset, r-first count, total}
+  u32* ticket;    // zero before the launch; the last block leaves it zero
+};
+
+// one block of 256 threads: the relay table from the r-first totals c[0, R) (LDS)
+static __device__ void fl_relay_table(const u64* s_c, u32 R, const FlRelayOut& o) {
+  __shared__ u64 s_off[kDlMaxRanks + 1];
+  __shared__ u64 s_len[kDlMaxRanks * kDlMaxRanks];
+  const u32 t0 = threadIdx.x;
+  if (t0 == 0) {
+    u64 x = 0;
+    for (u32 s = 0; s < R; ++s) {
+      s_off[s] = x;
+      x += s_c[s];
+    }
+    s_off[R] = x;
+  }
+  for (u32 t = t0; t < R * R; t += blockDim.x) {   // piece q of list s
+    const u32 q = t / R, s = t % R;
+    s_len[t] = fl_piece(s_c[s], q + 1, R) - fl_piece(s_c[s], q, R);
+  }
+  __syncthreads();
+  if (t0 <= R) o.T->off[t0] = s_off[t0];
+  if (t0 == 0) {
+    o.leaf[0] = s_off[o.me];
+    o.leaf[1] = s_c[o.me];
+    o.leaf[2] = s_off[R];
+  }
+  for (u32 t = t0; t < R * R; t += blockDim.x) {
+    const u32 q = t / R, s = t % R;
+    u64 at = u64(q) * o.cap2;   // rank q's block of the relay-2 buffer: lists 0 .. s-1's pieces q first
+    for (u32 s2 = 0; s2 < s; ++s2) at += s_len[q * R + s2];
+    const u64 sg = u64(s) * R + q;
+    o.T->seg_src[sg] = at;
+    o.T->seg_dst[sg] = s_off[s] + fl_piece(s_c[s], q, R);
+    o.T->seg_len[sg] = s_len[t];
+  }
+}
+
 [[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_counts(const unsigned long long* __restrict__ pbs,
-                                                       u64 stride, int R, DensePlan P, u32* __restrict__ cntb) {
+                                                       u64 stride, int R, DensePlan P, u32* __restrict__ cntb,
+                                                       FlRelayOut o) {
   __shared__ u32 s_c[kMaxRanks];
-  const int tid = threadIdx.x;
+  __shared__ u32 s_last;
+  __shared__ u32 s_w[4];
+  __shared__ u64 s_tot[kDlMaxRanks];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const u32 b = blockIdx.x, RB = 1u << P.IB, NW = RB >= 64 ? RB / 64 : 1u;
   if (tid < R) s_c[tid] = 0;
   __syncthreads();
@@ -69,51 +125,76 @@ constexpr u32 kFlSeg = kFlCap + 1;
   for (int q = 0; q < kMaxRanks; ++q)
     if (q < R) {
       const u32 v = u32(wave_sum(u64(c[q])));
-      if ((tid & 63) == 0 && v) atomicAdd(&s_c[q], v);
+      if (lane == 0 && v) atomicAdd(&s_c[q], v);
     }
   __syncthreads();
   if (tid < R) cntb[u64(tid) * P.NB + b] = s_c[tid];
-}
-
-// One block: per rank q the exclusive prefix of its per-bucket counts into the layout of the
-// general schedule's gathered exchange vectors (xvs[q * xw + 2 + b], k_dl_ids_mr reads them)
-// with the total, c_q, at xvs[q * xw].
-[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_fl_prefix(const u32* __restrict__ cntb, int R, DensePlan P,
-                                                         u64 xw, u32* __restrict__ xvs) {
-  __shared__ u32 s_tmp[16];
-  const int tid = threadIdx.x;
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) s_last = atomicAdd(o.ticket, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  // the last block: per rank, the exclusive prefix over the NB <= 1024 buckets (4 per thread)
   for (int q = 0; q < R; ++q) {
-    u32 total;
-    const u32 x = u32(tid) < P.NB ? cntb[u64(q) * P.NB + tid] : 0u;
-    const u32 e = block_excl(x, s_tmp, &total);
-    if (u32(tid) < P.NB) xvs[u64(q) * xw + 2 + tid] = e;
-    if (tid == 0) {
-      xvs[u64(q) * xw] = total;
-      xvs[u64(q) * xw + 1] = 0;
+    u32 x[4], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const u32 bb = 4 * u32(tid) + u32(k);
+      x[k] = bb < P.NB ? __hip_atomic_load(&cntb[u64(q) * P.NB + bb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      sum += x[k];
     }
+    u32 inc = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const u32 y = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += y;
+    }
+    if (lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    u32 run = inc - sum, all = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      run += w < wave ? s_w[w] : 0u;
+      all += s_w[w];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const u32 bb = 4 * u32(tid) + u32(k);
+      if (bb < P.NB) o.xvs[u64(q) * o.xw + 2 + bb] = run;
+      run += x[k];
+    }
+    if (tid == 0) {
+      o.xvs[u64(q) * o.xw] = all;
+      o.xvs[u64(q) * o.xw + 1] = 0;
+      s_tot[q] = all;
+    }
+    __syncthreads();   // (s_w reused by the next rank)
   }
+  fl_relay_table(s_tot, u32(R), o);
+  if (tid == 0) *o.ticket = 0;
 }
 
 // The owner's not-first records counted per source rank (its dedupe's list): a source's
 // globally-first layer-0 pairs are its pairs minus the not-first ones at every owner.
-[[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_ownnf(const u32* __restrict__ olist,
-                                                      const u32* __restrict__ ocnt, Displ D, u32 R,
-                                                      u64* __restrict__ onf) {
+// (C5's device functions take their workgroup's index and count within the launch: k_fl_c5)
+static __device__ __forceinline__ void fl_ownnf(const u32* __restrict__ olist, const u32* __restrict__ ocnt,
+                                                const Displ& D, u32 R, u64* __restrict__ onf, u32 bx, u32 gx) {
   __shared__ u32 s_c[kMaxRanks];
   if (threadIdx.x < R) s_c[threadIdx.x] = 0;
   __syncthreads();
   const u32 n = *ocnt;
-  for (u32 i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) atomicAdd(&s_c[seg_of(D, R, olist[i])], 1u);
+  for (u32 i = bx * 256 + threadIdx.x; i < n; i += gx * 256) atomicAdd(&s_c[seg_of(D, R, olist[i])], 1u);
   __syncthreads();
   if (threadIdx.x < R && s_c[threadIdx.x])
     atomicAdd(reinterpret_cast<unsigned long long*>(&onf[threadIdx.x]), (unsigned long long)s_c[threadIdx.x]);
 }
 
 // The owner's replies (k_bkt_dedupe2<true>: 0, 6 first of a repeated key, 7 not first) packed
-// 2 bits per record, segment by segment (reply_unpack2 reads them): one thread per output byte.
-[[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_pack2(const unsigned char* __restrict__ rflag,
-                                                      Displ D, Displ P4, u32 R, unsigned char* __restrict__ out) {
-  const u64 t = u64(blockIdx.x) * 256 + threadIdx.x;
+// 2 bits per record, segment by segment (k_dist_flags' reply_code2 reads them): one thread per output byte.
+static __device__ __forceinline__ void fl_pack2(const unsigned char* __restrict__ rflag, const Displ& D,
+                                                const Displ& P4, u32 R, unsigned char* __restrict__ out, u32 bx) {
+  const u64 t = u64(bx) * 256 + threadIdx.x;
   if (t >= P4.d[R]) return;
   const u32 s = seg_of(P4, R, t);
   const u64 i0 = (t - P4.d[s]) * 4, n = D.d[s + 1] - D.d[s];
@@ -131,55 +212,29 @@ constexpr u32 kFlSeg = kFlCap + 1;
 // Rank s's G list (c_s elements, k_dl_gq) is cut into R pieces, piece q = [c_s q / R,
 // c_s (q + 1) / R) -> rank q (relay 1: slot s of rank q's buffer, cap1 elements per slot); rank
 // q concatenates the pieces it got (relay 2: cap2 elements to every rank, slot q).  The c_s come
-// from the gathered bitmaps (k_fl_prefix: xvs[s * xw]), so every rank computes the layout and
+// from the gathered bitmaps (k_fl_counts: xvs[s * xw]), so every rank computes the layout and
 // k_dl_ids_mr's table itself.
-__device__ __forceinline__ u64 fl_piece(u64 c, u32 q, u32 R) { return c * q / R; }
-
-// one thread: the relay table (DlRelay, k_dl_ids_mr reads where each piece landed) and this
-// rank's leaf id offset, r-first count and the total
-[[maybe_unused]] static __global__ void k_fl_relay(const u32* __restrict__ xvs, u64 xw, u32 R, u32 me, u64 cap2,
-                                                   DlRelay* __restrict__ T, u64* __restrict__ leaf) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  u64 o = 0;
-  for (u32 s = 0; s < R; ++s) {
-    T->off[s] = o;
-    o += xvs[u64(s) * xw];
-  }
-  T->off[R] = o;
-  leaf[0] = T->off[me];
-  leaf[1] = T->off[me + 1] - T->off[me];
-  leaf[2] = o;
-  for (u32 q = 0; q < R; ++q) {
-    u64 at = u64(q) * cap2;   // rank q's block of the relay-2 buffer
-    for (u32 s = 0; s < R; ++s) {
-      const u64 c = xvs[u64(s) * xw], a = fl_piece(c, q, R), len = fl_piece(c, q + 1, R) - a;
-      const u64 sg = u64(s) * R + q;
-      T->seg_src[sg] = at;
-      T->seg_dst[sg] = T->off[s] + a;
-      T->seg_len[sg] = len;
-      at += len;
-    }
-  }
-}
 
 // relay 1, sender side: the rank's G list into slot q of the staging buffer, piece by piece
+// (the piece bounds in LDS: no division per element)
 [[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_relay_out(const u32* __restrict__ G,
                                                           const u64* __restrict__ leaf, u32 R, u64 cap1,
                                                           u32* __restrict__ stage) {
+  __shared__ u64 s_b[kDlMaxRanks + 1];
   const u64 c = leaf[1];
+  if (threadIdx.x <= R) s_b[threadIdx.x] = fl_piece(c, threadIdx.x, R);
+  __syncthreads();
   for (u64 j = u64(blockIdx.x) * 256 + threadIdx.x; j < c; j += u64(gridDim.x) * 256) {
-    u32 q = u32((j * R) / c);   // (a first guess; exact below)
-    while (q + 1 < R && fl_piece(c, q + 1, R) <= j) ++q;
-    while (q > 0 && fl_piece(c, q, R) > j) --q;
-    stage[u64(q) * cap1 + (j - fl_piece(c, q, R))] = G[j];
+    u32 q = 0;
+    while (q + 1 < R && s_b[q + 1] <= j) ++q;
+    stage[u64(q) * cap1 + (j - s_b[q])] = G[j];
   }
 }
 
 // relay 2, sender side (rank me): the pieces it received (slot s: piece me of list s) back to back
-[[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_relay_mid(const u32* __restrict__ got,
-                                                          const u32* __restrict__ xvs, u64 xw, u32 R, u32 me,
-                                                          u64 cap1, u32* __restrict__ out) {
-  __shared__ u64 s_len[kMaxRanks + 1];
+static __device__ __forceinline__ void fl_relay_mid(const u32* __restrict__ got, const u32* __restrict__ xvs, u64 xw,
+                                                    u32 R, u32 me, u64 cap1, u32* __restrict__ out, u32 bx, u32 gx) {
+  __shared__ u64 s_len[kDlMaxRanks + 1];
   if (threadIdx.x == 0) {
     u64 o = 0;
     for (u32 s = 0; s < R; ++s) {
@@ -190,10 +245,37 @@ __device__ __forceinline__ u64 fl_piece(u64 c, u32 q, u32 R) { return c * q / R;
     s_len[R] = o;
   }
   __syncthreads();
-  for (u64 j = u64(blockIdx.x) * 256 + threadIdx.x; j < s_len[R]; j += u64(gridDim.x) * 256) {
+  for (u64 j = u64(bx) * 256 + threadIdx.x; j < s_len[R]; j += u64(gx) * 256) {
     u32 s = 0;
     while (s + 1 < R && s_len[s + 1] <= j) ++s;
     out[j] = got[u64(s) * cap1 + (j - s_len[s])];
+  }
+}
+
+// C5's tail in one launch (after the owner's dedupe): workgroups [0, npack) pack the replies,
+// the next 64 count the not-first records per source, the last 256 stage relay 2
+struct FlC5 {
+  const u32* olist;
+  const u32* ocnt;
+  Displ D, P4;
+  u64* onf;
+  const unsigned char* rflag;
+  unsigned char* packed;
+  u32 npack;
+  const u32* got;
+  const u32* xvs;
+  u64 xw, cap1;
+  u32 me;
+  u32* relay2;
+};
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_c5(FlC5 a, u32 R) {
+  const u32 b = blockIdx.x;
+  if (b < a.npack) {
+    fl_pack2(a.rflag, a.D, a.P4, R, a.packed, b);
+  } else if (b < a.npack + 64) {
+    fl_ownnf(a.olist, a.ocnt, a.D, R, a.onf, b - a.npack, 64);
+  } else {
+    fl_relay_mid(a.got, a.xvs, a.xw, R, a.me, a.cap1, a.relay2, b - a.npack - 64, 256);
   }
 }
 
@@ -249,7 +331,11 @@ __device__ __forceinline__ u64 fl_guard(const u64* __restrict__ g4, u32 R) {
   if (tid < int(rs.R)) h[tid] = 0;
   if (blockIdx.x == 0 && tid == 0) *count_out = p;
   __syncthreads();
+  // one LDS atomic per (wave, item, destination): the lanes sharing a destination found by a
+  // ballot per destination bit (R <= 8 addresses: per-lane atomics would serialize on them)
   constexpr int kB = 8;
+  const u32 dbits = rs.R > 1 ? 32u - u32(__clz(int(rs.R - 1))) : 0u;
+  const u64 lt = (1ull << (tid & 63)) - 1ull;
   for (int e0 = 0; e0 < kItems; e0 += kB) {
     u64 key[kB];
     u32 lid[kB];
@@ -257,8 +343,16 @@ __device__ __forceinline__ u64 fl_guard(const u64* __restrict__ g4, u32 R) {
 #pragma unroll
     for (int q = 0; q < kB; ++q) ok[q] = rec_get_canon(rs, u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid, key[q], lid[q]);
 #pragma unroll
-    for (int q = 0; q < kB; ++q)
-      if (ok[q]) atomicAdd(&h[rec_dest(rs, key[q])], 1u);
+    for (int q = 0; q < kB; ++q) {
+      const u32 d = ok[q] ? rec_dest(rs, key[q]) : 0u;
+      u64 m = __ballot(ok[q]);
+      for (u32 bit = 0; bit < dbits; ++bit) {
+        const bool set = (d >> bit) & 1u;
+        const u64 bb = __ballot(ok[q] && set);
+        m &= set ? bb : ~bb;
+      }
+      if (ok[q] && (m & lt) == 0) atomicAdd(&h[d], u32(__popcll(m)));
+    }
   }
   __syncthreads();
   if (tid < int(rs.R)) blockcnt[u64(tid) * nb + blockIdx.x] = h[tid];
@@ -267,10 +361,11 @@ __device__ __forceinline__ u64 fl_guard(const u64* __restrict__ g4, u32 R) {
 // C and D at the owner, one block: the first holders' ids into the keys' id slots, then every
 // not-first record's id into the slot of its source (the C / D counts of this schedule are
 // bounded by the slots: kFlCap per pair).
-[[maybe_unused]] static __global__ __launch_bounds__(1024) void k_fl_cd(const u64* __restrict__ rc, Displ D, u32 R,
-                                                    const u32* __restrict__ oslot, OwnTab T,
-                                                    const u32* __restrict__ olist, const u32* __restrict__ ocnt,
-                                                    u64* __restrict__ dbuf, u32* __restrict__ bad) {
+// (one workgroup of 1024 threads; k_fl_ids_cd runs it beside the leaf ids' buckets)
+static __device__ __forceinline__ void fl_cd_block(const u64* __restrict__ rc, const Displ& D, u32 R,
+                                                   const u32* __restrict__ oslot, const OwnTab& T,
+                                                   const u32* __restrict__ olist, const u32* __restrict__ ocnt,
+                                                   u64* __restrict__ dbuf, u32* __restrict__ bad) {
   for (u32 s = 0; s < R; ++s) {
     const u64 n = rc[u64(s) * kFlSeg];
     if (n > kFlCap) {
@@ -296,6 +391,30 @@ __device__ __forceinline__ u64 fl_guard(const u64* __restrict__ g4, u32 R) {
   }
 }
 
+// C7 in one launch: blocks [0, NB) the leaf level's global ids (dl_ids_mr_block, gcz_dense.h),
+// block NB the owner's C -> D records (fl_cd_block)
+struct FlCd {
+  const u64* rc;
+  Displ D;
+  const u32* oslot;
+  OwnTab T;
+  const u32* olist;
+  const u32* ocnt;
+  u64* dbuf;
+  u32* bad;
+};
+[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_fl_ids_cd(const u32* __restrict__ rec, const u32* __restrict__ off,
+                                                         DensePlan P, const unsigned long long* __restrict__ pbs,
+                                                         u64 stride, const u32* __restrict__ xvs, u64 xstride,
+                                                         const u32* __restrict__ gl, const DlRelay* __restrict__ T,
+                                                         int R, int r, u32* __restrict__ idrec, FlCd c) {
+  if (blockIdx.x < P.NB) {
+    dl_ids_mr_block(rec, off, P, pbs, stride, xvs, xstride, gl, T, R, r, idrec, blockIdx.x);
+    return;
+  }
+  fl_cd_block(c.rc, c.D, u32(R), c.oslot, c.T, c.olist, c.ocnt, c.dbuf, c.bad);
+}
+
 // C at a first holder: (index within its segment to owner q, global id) into q's slot.
 // (a slot overflow goes straight into this rank's R4 vector: r4[1])
 [[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_cvals(const u32* __restrict__ clist,
@@ -319,39 +438,30 @@ __device__ __forceinline__ u64 fl_guard(const u64* __restrict__ g4, u32 R) {
   }
 }
 
-// D at a holder: the global id of each of its not-first pairs.
-[[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_dvals(const u64* __restrict__ rd, Displ SD, u32 R,
-                                                      const u32* __restrict__ sidx, u32* __restrict__ gid,
-                                                      u32* __restrict__ bad) {
-  for (u32 q = 0; q < R; ++q) {
-    const u64 n = rd[u64(q) * kFlSeg];
-    if (n > kFlCap) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(bad, 1u);
-      continue;
-    }
-    for (u64 i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-      const u64 v = rd[u64(q) * kFlSeg + 1 + i];
-      gid[sidx[SD.d[q] + u32(v)]] = u32(v >> 32);
-    }
-  }
-}
-
 // The final vector of a fast-schedule rank: the general one (k_dist_final) plus failure bit 2
-// (a C/D overflow, a look-ahead that found layer 1 not direct) and [3] = this rank's layer-0
-// uniques.
-[[maybe_unused]] static __global__ void k_fl_final(const Header* __restrict__ h, DistHdr* __restrict__ dh, int tail0,
-                                                   int D, int has_tail, const u32* __restrict__ bad,
-                                                   const u64* __restrict__ g4, const u64* __restrict__ gonf,
-                                                   FlPairs pp, u32 R, u32 me) {
-  u64 u = 0;
-  (void)fl_offset(gonf, R, pp, me, &u);
-  (void)tail0;
-  dh->final_vec[0] = u64(h->overflow | h->leaf_overflow) | ((*bad || fl_guard(g4, R)) ? 2ull : 0ull);
-  dh->final_vec[1] = has_tail ? u64(h->root) : 0ull;
-  dh->final_vec[2] = dh->fl_leaf[1];   // this rank's r-first leaves
-  dh->final_vec[3] = u;                // ... and layer-0 uniques
-  for (int k = 0; k < GCZ_MAX_LAYERS; ++k)
-    dh->final_vec[4 + k] = (has_tail && k >= tail0 && k < D) ? h->count[kLayerSlot + k] : 0ull;
+// (a C/D overflow, a look-ahead that found layer 1 not direct), [2] = this rank's r-first
+// leaves and [3] = its layer-0 uniques.
+// (one wave: lane k < GCZ_MAX_LAYERS copies layer k's count, lane s < R sums source s's
+// not-first counts and its look-ahead / status words)
+[[maybe_unused]] static __global__ __launch_bounds__(64) void k_fl_final(const Header* __restrict__ h,
+                                                         DistHdr* __restrict__ dh, int tail0, int D, int has_tail,
+                                                         const u32* __restrict__ bad, const u64* __restrict__ g4,
+                                                         const u64* __restrict__ gonf, FlPairs pp, u32 R, u32 me) {
+  const u32 t = threadIdx.x;
+  for (u32 k = t; k < GCZ_MAX_LAYERS; k += 64)
+    dh->final_vec[4 + k] = (has_tail && int(k) >= tail0 && int(k) < D) ? h->count[kLayerSlot + k] : 0ull;
+  u64 nf = 0, gv = 0;
+  if (t < R) {
+    for (u32 q = 0; q < R; ++q) nf += gonf[u64(q) * R + t];
+    gv = g4[2 * t] + g4[2 * t + 1];
+  }
+  const u64 gsum = wave_sum(gv);
+  if (t == me) dh->final_vec[3] = pp.p[t] - nf;   // this rank's layer-0 uniques
+  if (t == 0) {
+    dh->final_vec[0] = u64(h->overflow | h->leaf_overflow) | ((*bad || gsum) ? 2ull : 0ull);
+    dh->final_vec[1] = has_tail ? u64(h->root) : 0ull;
+    dh->final_vec[2] = dh->fl_leaf[1];   // this rank's r-first leaves
+  }
 }
 
 }  // namespace gcz_dev
@@ -366,15 +476,21 @@ namespace gcz_dev {
 // Block 0 also settles the direct subtrees' guard from R4's vectors.
 struct FlL0 {
   const unsigned char* gnf;   // per pair: not globally first
-  const u32* gid;             // per pair: local rank | kLocalId (first), else the global id
+  u32* gid;                   // per pair: local rank | kLocalId (first), else the global id
   const u64* gonf;            // R3's gathered not-first counts
   const u64* g4;              // R4's gathered {look-ahead, failure}
   FlPairs pp;
   u32 R, me;
-  const u64* leaf;            // k_fl_relay's {leaf offset, r-first count, total}
+  const u64* leaf;            // k_fl_counts' {leaf offset, r-first count, total}
   uint2* nodes;               // the rank's slice of layer 0
   u32* words0;                // layer-0 words (the direct subtrees' input)
   u64* guard;
+  // R5's D records (the owners' ids of this rank's not-first pairs): each
+  // block writes the ones of its own pairs into gid before reading them
+  const u64* rd;
+  Displ SD;
+  const u32* sidx;
+  u32* bad;
 };
 // The leaves go out in position order (= id order) from the pre-words: coalesced stores, where
 // k_dl_words' record-order stores scatter (at 1 Gbase over 8 ranks rank 0 first-holds ~47 % of
@@ -391,21 +507,52 @@ struct FlL0 {
     s_loff = u32(a.leaf[0]);
     if (blockIdx.x == 0) *a.guard = fl_guard(a.g4, a.R);
   }
+  constexpr int kPP = kDC / 2 / kDThreads;
+  const u64 cc0 = u64(blockIdx.x) * kDC;
+  const u32 npp = u32((std::min<u64>(P.S - cc0, kDC) + 1) / 2);
+  {   // D: the ids of this chunk's not-first pairs whose first holder is another rank
+    const u64 j0 = cc0 / 2, j1 = j0 + npp;
+    for (u32 q = 0; q < a.R; ++q) {
+      const u64 n = a.rd[u64(q) * kFlSeg];
+      if (n > kFlCap) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.bad, 1u);
+        continue;
+      }
+      for (u64 i = threadIdx.x; i < n; i += kDThreads) {
+        const u64 v = a.rd[u64(q) * kFlSeg + 1 + i];
+        const u32 j = a.sidx[a.SD.d[q] + u32(v)];
+        if (j >= j0 && j < j1) a.gid[j] = u32(v >> 32);
+      }
+    }
+    __threadfence();
+    __syncthreads();
+  }
+  // the chunk's pair flags and ids loaded up front: in flight while the records are placed
+  u32 gp[kPP];
+  unsigned char fp[kPP];
+#pragma unroll
+  for (int k = 0; k < kPP; ++k) {
+    const u32 jj = u32(k) * kDThreads + threadIdx.x;
+    gp[k] = jj < npp ? a.gid[cc0 / 2 + jj] : 0u;
+    fp[k] = jj < npp ? a.gnf[cc0 / 2 + jj] : (unsigned char)1;
+  }
   dl_words_chunk(rec, idrec, offt, P, fb, nullptr, 0, s_dyn, [&](const u32* s_w, u32 n, u64 c0) {
     const u64 j0 = c0 / 2;
     const u32 np = (n + 1) / 2, off = s_off;
-#pragma unroll 4
-    for (u32 jj = threadIdx.x; jj < np; jj += kDThreads) {
+#pragma unroll
+    for (int k = 0; k < kPP; ++k) {
+      const u32 jj = u32(k) * kDThreads + threadIdx.x;
+      if (jj >= np) continue;
       const u64 j = j0 + jj;
-      const unsigned char f = a.gnf[j];
-      const u32 g = a.gid[j];
+      const unsigned char f = fp[k];
+      const u32 g = gp[k];
       const u64 fw = fb[(c0 + 2 * jj) >> 6];   // (the pair's two positions share a word)
       const u32 sh = u32(c0 + 2 * jj) & 63u;
       const u32 l = s_w[2 * jj], r = 2 * jj + 1 < n ? s_w[2 * jj + 1] : kNullWord;
       if ((fw >> sh) & 1ull)
-        leaves_out[(l & kIdx) - s_loff] = code2_leaf(((pw[c0 + 2 * jj] & kIdx) * P.Kinv) & P.cmask, P.L);
+        leaves_out[(l & kIdx) - s_loff] = code2_leaf(((pw[c0 + 2 * jj] & kIdx) * P.Kinv) & P.hmask, P.L);
       if (2 * jj + 1 < n && ((fw >> (sh + 1)) & 1ull))
-        leaves_out[(r & kIdx) - s_loff] = code2_leaf(((pw[c0 + 2 * jj + 1] & kIdx) * P.Kinv) & P.cmask, P.L);
+        leaves_out[(r & kIdx) - s_loff] = code2_leaf(((pw[c0 + 2 * jj + 1] & kIdx) * P.Kinv) & P.hmask, P.L);
       u32 cl, cr, m, t;
       node_canonical(l, r, cl, cr, m, t);
       const u32 v = ulw(l) == ulw(xf(r, 1, 0));
