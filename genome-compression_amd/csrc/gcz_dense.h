@@ -696,11 +696,30 @@ __host__ __device__ __forceinline__ bool dl_rleaves_sparse(u64 count, u64 S) { r
   }
   const u32 n = bcnt[b];
   const bool lv = leaves_out && dl_rleaves_sparse(*ucount, P.S);
-  for (u32 j = tid; j < n; j += kDThreads) {
-    const u32 fp = rfc[u64(b) * RB + j];
-    const u32 k = fb_rank(rfb, wpre, fp);
-    G[pre + j] = k;
-    if (lv) leaves_out[k] = code2_leaf(((pw[fp] & kIdx) * P.Kinv) & P.hmask, P.L);
+  constexpr int kQ = 4;   // codes per thread in flight (the rank lookups are random L2 reads)
+  for (u32 j0 = tid; j0 < n; j0 += kQ * kDThreads) {
+    u32 fp[kQ];
+    unsigned long long w[kQ];
+    u32 wp[kQ];
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const u32 j = j0 + u32(q) * kDThreads;
+      fp[q] = j < n ? rfc[u64(b) * RB + j] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const u32 j = j0 + u32(q) * kDThreads;
+      w[q] = j < n ? rfb[fp[q] >> 6] : 0ull;
+      wp[q] = j < n ? wpre[fp[q] >> 6] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const u32 j = j0 + u32(q) * kDThreads;
+      if (j >= n) continue;
+      const u32 k = wp[q] + u32(__popcll(w[q] & ((1ull << (fp[q] & 63)) - 1ull)));   // fb_rank
+      G[pre + j] = k;
+      if (lv) leaves_out[k] = code2_leaf(((pw[fp[q]] & kIdx) * P.Kinv) & P.hmask, P.L);
+    }
   }
 }
 

@@ -45,6 +45,7 @@ struct gcz_dist_state {
   u64* h_gathf = nullptr;
   DlRelay* h_relay = nullptr;   // pinned staging of the dense leaf relay table (H2D, stream-ordered)
   DevBuf skey_hi, rkey_hi;   // fused schedule: the 6-byte records' high 16 bits
+  DevBuf fl_pkey;            // fused schedule: layer 0's mixed keys (k_fl_count -> k_bucket_scatter)
   DevBuf fl_cntb, fl_mid, fl_g3, fl_g4;   // fused schedule: r-first counts per bucket, the mid-build
   u64* h_mid = nullptr;                   // vector (+ pinned mirror), R3's / R4's gathered vectors
 };
@@ -60,7 +61,7 @@ void gcz_dist_state_free(gcz_ctx* c) {
                     &d->scval, &d->sdval, &d->clist, &d->olist, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab, &d->oids,
                     &d->omin, &d->ob_cnt, &d->ob_off, &d->ob_desc, &d->ob_rec, &d->ob_seg, &d->ob_rt,
                     &d->ob_rec2, &d->ob_fo, &d->fl_cntb, &d->fl_mid, &d->fl_g3, &d->fl_g4, &d->skey_hi,
-                    &d->rkey_hi,
+                    &d->rkey_hi, &d->fl_pkey,
                     &d->dhdr, &d->gath, &d->gath2, &d->gathf, &d->ddesc, &d->tail_in, &d->nfl})
     if (b->ptr) (void)hipFree(b->ptr);
   for (u64* h : {d->h_gath, d->h_gath2, d->h_gathf})
@@ -904,6 +905,12 @@ struct gcz_group {
   int dev_fail(const char* what) {
     return fail(GCZ_ERR_DEVICE, std::string(what) + (tr && !tr->err.empty() ? ": " + tr->err : ""));
   }
+  // a callee's device failure, its message kept: "what <- inner" (inner: the callee's own
+  // message, else the transport's)
+  int chain_fail(const char* what) {
+    const std::string inner = !last_error.empty() ? last_error : tr ? tr->err : std::string();
+    return fail(GCZ_ERR_DEVICE, std::string(what) + " <- " + inner);
+  }
   int build(const void* const* d_bases, const u64* const* d_leaves, u64 S, int L);
   int assemble(gcz_ctx* dst);
   int alloc(int i, u64 leaf_cap);
@@ -965,7 +972,7 @@ struct gcz_group {
 #define G_RC(x)                                                                    \
   do {                                                                             \
     int rc_ = (x);                                                                 \
-    if (rc_) return rc_ == GCZ_ERR_DEVICE ? fail(rc_, std::string(#x) + " <- " + last_error) : rc_; \
+    if (rc_) return rc_ == GCZ_ERR_DEVICE ? chain_fail(#x) : rc_;                 \
   } while (0)
 
 namespace {
@@ -1920,6 +1927,9 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       rs.pk.c2 = mt.pt.c2;
       if (cx->ensure(d.skey_hi, p * 2 + 16)) return dev_fail("fused schedule buffers");
     }
+    if (cx->ensure(d.fl_pkey, p * 8 + 16)) return dev_fail("fused schedule buffers");
+    rs.pkey = d.fl_pkey.as<u64>();
+    rs.pkey_in = 0;
     ProfScope ps_(cx, KID_DIST);
     hipLaunchKernelGGL(k_fl_count, dim3(nb), dim3(kBlock), 0, cx->stream, rs, d.blockcnt.as<u32>(), nb,
                        d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(), d.ddesc.as<u64>(), &h->count[kLayerSlot]);
@@ -1963,6 +1973,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     const u64 p = P.count(rank[i], 1);
     const u32 nb = u32(std::max<u64>(1, (p + kTile - 1) / kTile));
     ProfScope ps_(cx, KID_DIST);
+    fl_rs[i].pkey_in = 1;   // (the count pass left the keys)
     hipLaunchKernelGGL(k_bucket_scatter, dim3(nb), dim3(kBlock), 0, cx->stream, fl_rs[i], d.blockcnt.as<u32>(), nb,
                        d.skey.as<u64>(), d.sidx.as<u32>(), split ? d.skey_hi.as<unsigned short>() : nullptr);
     G_HIP(hipGetLastError());
@@ -2123,9 +2134,10 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       fo.cap2 = cap2;
       fo.T = cx->dl_gid.as<DlRelay>();
       fo.leaf = dh->fl_leaf;
-      fo.ticket = &dh->fl_ticket;
       hipLaunchKernelGGL(k_fl_counts, dim3(NB), dim3(256), 0, cx->stream, cx->dl_pbs.as<unsigned long long>(), nw, R, DP,
-                         d.fl_cntb.as<u32>(), fo);
+                         d.fl_cntb.as<u32>());
+      hipLaunchKernelGGL(k_fl_prefix_relay, dim3(1), dim3(kDThreads), 0, cx->stream,
+                         static_cast<const u32*>(d.fl_cntb.as<u32>()), R, DP, fo);
       G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_rfirst), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 int((DP.nch + 1) * 4)));
       hipLaunchKernelGGL(k_dl_rfirst, dim3(NB), dim3(kDThreads), (DP.nch + 1) * 4, cx->stream, cx->dl_fpg.as<u32>(), DP,
@@ -2144,7 +2156,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
                          cx->dl_fb.as<unsigned long long>(), cx->dl_wpre.as<u32>(),
                          static_cast<const u64*>(&h->count[0]), cx->dl_list.as<u32>(), xv, cx->dl_pw.as<u32>(),
                          static_cast<u64*>(nullptr), static_cast<const u64*>(cx->dl_pb.as<u64>() + nw));
-      hipLaunchKernelGGL(k_fl_relay_out, dim3(256), dim3(256), 0, cx->stream, static_cast<const u32*>(cx->dl_list.as<u32>()),
+      hipLaunchKernelGGL(k_fl_relay_out, dim3(2048), dim3(256), 0, cx->stream, static_cast<const u32*>(cx->dl_list.as<u32>()),
                          static_cast<const u64*>(dh->fl_leaf), u32(R), cap1, cx->dl_stage.as<u32>());
       G_HIP(hipGetLastError());
     }

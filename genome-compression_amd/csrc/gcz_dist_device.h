@@ -56,7 +56,6 @@ struct DistHdr {
   u64 fl_guard;                         // 0: layer 1 is direct on every rank and none failed
   u64 fl_leaf[3];                       // this rank's leaf id offset, r-first count, all ranks' total
   u32 fl_bad;                           // a C / D slot overflowed
-  u32 fl_ticket;                        // k_fl_counts' last-block ticket
 };
 
 struct Displ {   // segment starts of the R source (or destination) ranks in a buffer, plus the end
@@ -122,6 +121,9 @@ struct RecSrc {
   // labels), canonicalised on the fly; every pair but the null one is a record, lid = position
   const u32* pre;
   PreKey pk;     // ... with pk.on: 6-byte records, the key = owner << 48 | record
+  u64* pkey;     // ... the keys as k_fl_count computed them (~0: no record): written by the
+                 // count pass (pkey_out), read by the scatter (pkey_in) instead of recomputed
+  u32 pkey_in;
 };
 
 
@@ -170,6 +172,11 @@ __device__ __forceinline__ u32 rec_dest(const RecSrc& s, u64 key) {
 // rec_get for levels without the local dedupe (canonical pairs given): every load of the
 // record issued at once, none behind the not-first mark.
 __device__ __forceinline__ bool rec_get_canon(const RecSrc& s, u64 e, u64& key, u32& lid) {
+  if (s.pre && s.pkey_in) {
+    lid = u32(e);
+    key = e < s.p ? s.pkey[e] : ~0ull;
+    return key != ~0ull;
+  }
   if (s.pre) {
     u32 l = kNullWord, r = kNullWord, cl, cr, m, t;
     if (e < s.p) load_pair(s.pre, s.n, e, l, r);

@@ -45,10 +45,10 @@ constexpr u32 kFlSeg = kFlCap + 1;
 // Per (bucket, rank q): the codes rank q holds first (present_q & ~(present_0 | ... |
 // present_{q-1})), counted from the gathered presence bitmaps -- every rank derives every
 // rank's r-first counts itself (the general schedule allgathers them).  One block per bucket;
-// the last block to finish (a ticket) then writes, per rank q, the exclusive prefix of its
-// per-bucket counts into the layout of the general schedule's gathered exchange vectors
-// (xvs[q * xw + 2 + b], k_dl_ids_mr reads them) with the total, c_q, at xvs[q * xw], and the
-// leaf relay's table (fl_relay_table).
+// k_fl_prefix_relay then writes, per rank q, the exclusive prefix of its per-bucket counts into
+// the layout of the general schedule's gathered exchange vectors (xvs[q * xw + 2 + b],
+// k_dl_ids_mr reads them) with the total, c_q, at xvs[q * xw], and the leaf relay's table
+// (fl_relay_table).
 // the leaf relay's piece q of a list of c elements: [c q / R, c (q + 1) / R) (see below)
 __device__ __forceinline__ u64 fl_piece(u64 c, u32 q, u32 R) { return c * q / R; }
 
@@ -59,10 +59,9 @@ struct FlRelayOut {
   u64 cap2;
   DlRelay* T;
   u64* leaf;      // {leaf offset, r-first count, total}
-  u32* ticket;    // zero before the launch; the last block leaves it zero
 };
 
-// one block of 256 threads: the relay table from the r-first totals c[0, R) (LDS)
+// one block: the relay table from the r-first totals c[0, R) (LDS)
 static __device__ void fl_relay_table(const u64* s_c, u32 R, const FlRelayOut& o) {
   __shared__ u64 s_off[kDlMaxRanks + 1];
   __shared__ u64 s_len[kDlMaxRanks * kDlMaxRanks];
@@ -98,13 +97,9 @@ static __device__ void fl_relay_table(const u64* s_c, u32 R, const FlRelayOut& o
 }
 
 [[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_counts(const unsigned long long* __restrict__ pbs,
-                                                       u64 stride, int R, DensePlan P, u32* __restrict__ cntb,
-                                                       FlRelayOut o) {
+                                                       u64 stride, int R, DensePlan P, u32* __restrict__ cntb) {
   __shared__ u32 s_c[kMaxRanks];
-  __shared__ u32 s_last;
-  __shared__ u32 s_w[4];
-  __shared__ u64 s_tot[kDlMaxRanks];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
   const u32 b = blockIdx.x, RB = 1u << P.IB, NW = RB >= 64 ? RB / 64 : 1u;
   if (tid < R) s_c[tid] = 0;
   __syncthreads();
@@ -129,50 +124,29 @@ static __device__ void fl_relay_table(const u64* s_c, u32 R, const FlRelayOut& o
     }
   __syncthreads();
   if (tid < R) cntb[u64(tid) * P.NB + b] = s_c[tid];
-  __threadfence();
-  __syncthreads();
-  if (tid == 0) s_last = atomicAdd(o.ticket, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();
-  // the last block: per rank, the exclusive prefix over the NB <= 1024 buckets (4 per thread)
+}
+
+// One block of kDThreads (NB <= 1024 buckets): the prefixes and totals into xvs, then the relay
+// table.  (A separate launch: a last-block ticket in k_fl_counts needs a device-scope fence per
+// block, an L2 write-back on this part.)
+[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_fl_prefix_relay(const u32* __restrict__ cntb, int R,
+                                                               DensePlan P, FlRelayOut o) {
+  __shared__ u32 s_tmp[16];
+  __shared__ u64 s_tot[kDlMaxRanks];
+  const int tid = threadIdx.x;
   for (int q = 0; q < R; ++q) {
-    u32 x[4], sum = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const u32 bb = 4 * u32(tid) + u32(k);
-      x[k] = bb < P.NB ? __hip_atomic_load(&cntb[u64(q) * P.NB + bb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-      sum += x[k];
-    }
-    u32 inc = sum;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const u32 y = __shfl_up(inc, d, 64);
-      if (lane >= d) inc += y;
-    }
-    if (lane == 63) s_w[wave] = inc;
-    __syncthreads();
-    u32 run = inc - sum, all = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      run += w < wave ? s_w[w] : 0u;
-      all += s_w[w];
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const u32 bb = 4 * u32(tid) + u32(k);
-      if (bb < P.NB) o.xvs[u64(q) * o.xw + 2 + bb] = run;
-      run += x[k];
-    }
+    u32 total;
+    const u32 x = u32(tid) < P.NB ? cntb[u64(q) * P.NB + tid] : 0u;
+    const u32 e = block_excl(x, s_tmp, &total);
+    if (u32(tid) < P.NB) o.xvs[u64(q) * o.xw + 2 + tid] = e;
     if (tid == 0) {
-      o.xvs[u64(q) * o.xw] = all;
+      o.xvs[u64(q) * o.xw] = total;
       o.xvs[u64(q) * o.xw + 1] = 0;
-      s_tot[q] = all;
+      s_tot[q] = total;
     }
-    __syncthreads();   // (s_w reused by the next rank)
   }
+  __syncthreads();
   fl_relay_table(s_tot, u32(R), o);
-  if (tid == 0) *o.ticket = 0;
 }
 
 // The owner's not-first records counted per source rank (its dedupe's list): a source's
@@ -310,8 +284,9 @@ __device__ __forceinline__ u64 fl_guard(const u64* __restrict__ g4, u32 R) {
 }
 
 // Layer 0's records per owner, per tile of kTile pairs (the bucketing's count pass over the
-// pre-words: k_bucket_scatter with RecSrc::pre follows), and what the exchange expects zeroed:
-// the global flags and the rank scan's look-back words; count_out = the pairs.
+// pre-words: k_bucket_scatter with RecSrc::pre follows and reads the keys this pass leaves in
+// rs.pkey), and what the exchange expects zeroed: the global flags and the rank scan's
+// look-back words; count_out = the pairs.
 [[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_fl_count(RecSrc rs, u32* __restrict__ blockcnt, u32 nb,
                                                          unsigned char* __restrict__ gnf,
                                                          unsigned char* __restrict__ gmul, u64* __restrict__ ddesc,
@@ -341,7 +316,11 @@ __device__ __forceinline__ u64 fl_guard(const u64* __restrict__ g4, u32 R) {
     u32 lid[kB];
     bool ok[kB];
 #pragma unroll
-    for (int q = 0; q < kB; ++q) ok[q] = rec_get_canon(rs, u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid, key[q], lid[q]);
+    for (int q = 0; q < kB; ++q) {
+      const u64 e = u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid;
+      ok[q] = rec_get_canon(rs, e, key[q], lid[q]);
+      if (e < p) rs.pkey[e] = ok[q] ? key[q] : ~0ull;
+    }
 #pragma unroll
     for (int q = 0; q < kB; ++q) {
       const u32 d = ok[q] ? rec_dest(rs, key[q]) : 0u;
@@ -507,7 +486,6 @@ struct FlL0 {
     s_loff = u32(a.leaf[0]);
     if (blockIdx.x == 0) *a.guard = fl_guard(a.g4, a.R);
   }
-  constexpr int kPP = kDC / 2 / kDThreads;
   const u64 cc0 = u64(blockIdx.x) * kDC;
   const u32 npp = u32((std::min<u64>(P.S - cc0, kDC) + 1) / 2);
   {   // D: the ids of this chunk's not-first pairs whose first holder is another rank
@@ -524,28 +502,17 @@ struct FlL0 {
         if (j >= j0 && j < j1) a.gid[j] = u32(v >> 32);
       }
     }
-    __threadfence();
+    __threadfence_block();   // (this workgroup reads them back: no device-scope fence, an L2 write-back)
     __syncthreads();
-  }
-  // the chunk's pair flags and ids loaded up front: in flight while the records are placed
-  u32 gp[kPP];
-  unsigned char fp[kPP];
-#pragma unroll
-  for (int k = 0; k < kPP; ++k) {
-    const u32 jj = u32(k) * kDThreads + threadIdx.x;
-    gp[k] = jj < npp ? a.gid[cc0 / 2 + jj] : 0u;
-    fp[k] = jj < npp ? a.gnf[cc0 / 2 + jj] : (unsigned char)1;
   }
   dl_words_chunk(rec, idrec, offt, P, fb, nullptr, 0, s_dyn, [&](const u32* s_w, u32 n, u64 c0) {
     const u64 j0 = c0 / 2;
     const u32 np = (n + 1) / 2, off = s_off;
-#pragma unroll
-    for (int k = 0; k < kPP; ++k) {
-      const u32 jj = u32(k) * kDThreads + threadIdx.x;
-      if (jj >= np) continue;
+#pragma unroll 4
+    for (u32 jj = threadIdx.x; jj < np; jj += kDThreads) {
       const u64 j = j0 + jj;
-      const unsigned char f = fp[k];
-      const u32 g = gp[k];
+      const unsigned char f = a.gnf[j];
+      const u32 g = a.gid[j];
       const u64 fw = fb[(c0 + 2 * jj) >> 6];   // (the pair's two positions share a word)
       const u32 sh = u32(c0 + 2 * jj) & 63u;
       const u32 l = s_w[2 * jj], r = 2 * jj + 1 < n ? s_w[2 * jj + 1] : kNullWord;

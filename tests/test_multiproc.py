@@ -91,5 +91,5 @@ def test_bench_multiprocess_stalled_rank_is_bounded():
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert lines, out[-3000:]
     err = json.loads(lines[-1]).get("error", "")
-    assert "collective #2" in err and "leaf G arrays, relay 1" in err, err
+    assert "collective #2" in err and "R1b leaf presence bitmaps" in err, err
     assert "no peer arrived within 6 s" in err, err
