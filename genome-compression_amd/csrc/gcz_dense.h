@@ -85,10 +85,17 @@ static __device__ __forceinline__ u32 canon2(u32 x, u32 L, u32 cmask, u32& m, u3
 }
 
 // 2-bit code -> nibble-packed dna value (A,C,G,T = 1,2,4,8 at bits 4i, include/dna.h:20-32)
+// (branch-free: the 2-bit groups spread to 4-bit slots, then one-hot per slot -- a loop over
+// the L bases inside the words passes' divergent first-leaf branch cost ~30 us per launch)
 static __device__ __forceinline__ u64 code2_leaf(u32 c, u32 L) {
-  u64 v = 0;
-  for (u32 i = 0; i < L; ++i) v |= u64(1u << ((c >> (2 * i)) & 3u)) << (4 * i);
-  return v;
+  u64 x = c;
+  x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+  x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x << 2)) & 0x3333333333333333ull;   // base i's 2 bits at bits 4i, 4i + 1
+  const u64 M = 0x1111111111111111ull, lo = x & M, hi = (x >> 1) & M;
+  const u64 v = (~hi & ~lo & M) | ((~hi & lo & M) << 1) | ((hi & ~lo & M) << 2) | ((hi & lo & M) << 3);
+  return L >= 16 ? v : v & ((1ull << (4 * L)) - 1ull);
 }
 
 // Block-wide exclusive scan of one u32 per thread (kDThreads threads); returns

@@ -2155,7 +2155,8 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       hipLaunchKernelGGL(k_dl_gq, dim3(NB), dim3(kDThreads), 0, cx->stream, cx->dl_lh.as<u32>(), bcnt, DP,
                          cx->dl_fb.as<unsigned long long>(), cx->dl_wpre.as<u32>(),
                          static_cast<const u64*>(&h->count[0]), cx->dl_list.as<u32>(), xv, cx->dl_pw.as<u32>(),
-                         static_cast<u64*>(nullptr), static_cast<const u64*>(cx->dl_pb.as<u64>() + nw));
+                         r > 0 ? cx->leaves_out.as<u64>() : nullptr,   // (k_fl_words_l0: rank 0's)
+                         static_cast<const u64*>(cx->dl_pb.as<u64>() + nw));
       hipLaunchKernelGGL(k_fl_relay_out, dim3(2048), dim3(256), 0, cx->stream, static_cast<const u32*>(cx->dl_list.as<u32>()),
                          static_cast<const u64*>(dh->fl_leaf), u32(R), cap1, cx->dl_stage.as<u32>());
       G_HIP(hipGetLastError());

@@ -471,9 +471,10 @@ struct FlL0 {
   const u32* sidx;
   u32* bad;
 };
-// The leaves go out in position order (= id order) from the pre-words: coalesced stores, where
-// k_dl_words' record-order stores scatter (at 1 Gbase over 8 ranks rank 0 first-holds ~47 % of
-// its strands' codes).
+// Rank 0's leaves and those of a rank whose r-first positions are dense go out here in
+// position order (= id order) from the pre-words: coalesced stores, where k_dl_words'
+// record-order stores scatter (at 1 Gbase over 8 ranks rank 0 first-holds ~47 % of its strands'
+// codes); k_dl_gq writes the others'.
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_fl_words_l0(const u32* __restrict__ rec,
                                                            const u32* __restrict__ idrec, const u32* __restrict__ offt,
                                                            DensePlan P, const unsigned long long* __restrict__ fb,
@@ -508,12 +509,17 @@ struct FlL0 {
   dl_words_chunk(rec, idrec, offt, P, fb, nullptr, 0, s_dyn, [&](const u32* s_w, u32 n, u64 c0) {
     const u64 j0 = c0 / 2;
     const u32 np = (n + 1) / 2, off = s_off;
+    // a rank > 0 whose r-first positions are sparse had k_dl_gq write its leaves (by rank, in
+    // the segment where rank 0's r-first work sets the pace): measured at 1 Gbase over 8 ranks,
+    // rank 1's 0.67 M leaves cost ~50 us here against ~27 us there; rank 0 writes here, where it
+    // is the lightest rank (its 4.2 M leaves over 8 Gbase: ~60 us here, ~140 us there)
+    const bool dense = a.me == 0 || !dl_rleaves_sparse(a.leaf[1], P.S);
 #pragma unroll 4
     for (u32 jj = threadIdx.x; jj < np; jj += kDThreads) {
       const u64 j = j0 + jj;
       const unsigned char f = a.gnf[j];
       const u32 g = a.gid[j];
-      const u64 fw = fb[(c0 + 2 * jj) >> 6];   // (the pair's two positions share a word)
+      const u64 fw = dense ? fb[(c0 + 2 * jj) >> 6] : 0ull;   // (the pair's two positions share a word)
       const u32 sh = u32(c0 + 2 * jj) & 63u;
       const u32 l = s_w[2 * jj], r = 2 * jj + 1 < n ? s_w[2 * jj + 1] : kNullWord;
       if ((fw >> sh) & 1ull)
