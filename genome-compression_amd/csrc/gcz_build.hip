@@ -306,7 +306,7 @@ int gcz_ctx::dense_phase_a2(const LeafLevel& a) {
 // first positions; single device: + the first bitmap and its popcount scan (the unique count);
 // multi-rank (list): + the presence bitmap and the status words only -- the r-first filter,
 // position bitmap and ranks follow the bitmap exchange (gcz_dist.hip)
-int gcz_ctx::dense_phase_a3(Header* d_hdr, u64* ucount, bool list, u64* vec) {
+int gcz_ctx::dense_phase_a3(Header* d_hdr, u64* ucount, bool list, u64* vec, u32* rfc, u32* bcnt) {
   const DensePlan& P = dl_plan;
   const u64 ncnt = u64(P.NB) * P.nch, nfb = (P.S + 63) / 64;
   const u64 t_cnt = scan_tiles(ncnt + 1), t_fb = scan_tiles(nfb + 1);
@@ -318,9 +318,9 @@ int gcz_ctx::dense_phase_a3(Header* d_hdr, u64* ucount, bool list, u64* vec) {
   prof_begin(KID_DL_FIRST, e0);
   if (list && (1u << P.IB) < 64) HIP_TRY(hipMemsetAsync(dl_pb.ptr, 0, (ncodes / 64 + 1) * 8, stream));
   hipLaunchKernelGGL(k_dl_first, dim3(P.NB), dim3(kDThreads), first_bytes, stream, dl_rec.as<u32>(), dl_off.as<u32>(),
-                     P, dl_fpg.as<u32>(), list ? nullptr : dl_fl.as<u32>(), dl_fo.as<u32>(),
+                     P, rfc ? nullptr : dl_fpg.as<u32>(), (list && !rfc) ? nullptr : dl_fl.as<u32>(), dl_fo.as<u32>(),
                      list ? dl_pb.as<unsigned long long>() : nullptr, static_cast<const Header*>(d_hdr),
-                     list ? vec : nullptr);
+                     list ? vec : nullptr, rfc, bcnt);
   HIP_TRY(hipGetLastError());
   if (list) {
     prof_end(KID_DL_FIRST, e0);

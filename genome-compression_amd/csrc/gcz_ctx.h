@@ -383,7 +383,9 @@ struct gcz_ctx {
   // the rest of phase A after a pack_only call: scan + scatter (a2), first positions (a3; list:
   // the presence bitmap and status words instead of the first bitmap and its scan)
   int dense_phase_a2(const gcz_host::LeafLevel& a);
-  int dense_phase_a3(gcz_dev::Header* d_hdr, gcz_host::u64* ucount, bool list, gcz_host::u64* vec);
+  // (rfc / bcnt: the fused schedule's rank 0 -- its r-first lists straight from the first pass)
+  int dense_phase_a3(gcz_dev::Header* d_hdr, gcz_host::u64* ucount, bool list, gcz_host::u64* vec,
+                     gcz_host::u32* rfc = nullptr, gcz_host::u32* bcnt = nullptr);
   int dense_phase_b(const gcz_host::LeafLevel& a, gcz_dev::Header* d_hdr, const gcz_host::u32* gid,
                     gcz_host::u64* leaves, bool ids_done = false);
   int node_level(const gcz_host::NodeLevel& a, gcz_dev::Header* d_hdr);

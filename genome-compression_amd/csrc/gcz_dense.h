@@ -56,6 +56,38 @@ struct DensePlan {
   u32 K, Kinv; // odd multiplier mod 4^L and its inverse
 };
 
+// The fused schedule's 6-byte layer-0 records (gcz_dist_fast.h): the canonical pair re-labelled
+// by the children's canonical 2-bit codes -- a dna::canonical code is the minimum of its orbit,
+// which holds a code and its complement (x ^ mask), so its top bit is 0: Bc = 2L - 1 bits --
+// left child code | m, right child code | m | t (a canonical node's left child never carries t,
+// include/shared_tree.h:119-126) = K = 2 Bc + 3 bits, mixed by a K-bit bijection h;
+// owner = h's top lgR bits, record = the K - lgR bits below (<= 48).
+struct PreKey {
+  u32 on;                            // 0: 8-B raw keys
+  u32 Kinv, cmask;                   // hashed code -> code
+  u32 Bc, K, lgR;
+  u32 sh;
+  u64 kmask, c1, c2;                 // the mix (PackedTab::mix's form)
+  __device__ __forceinline__ u64 mix(u64 x) const {
+    x ^= x >> sh; x = (x * c1) & kmask;
+    x ^= x >> sh; x = (x * c2) & kmask;
+    x ^= x >> sh;
+    return x;
+  }
+  __device__ __forceinline__ u64 label(u32 w) const {   // a child word -> code << 2 | m << 1 | t
+    const u32 c = ((w & kIdx) * Kinv) & cmask;
+    return (u64(c) << 2) | (((w >> 29) & 1u) << 1) | ((w >> 30) & 1u);   // (bit 29 mirror, 30 transpose)
+  }
+};
+
+// the record key of a canonical pair (cl, cr) of pre-words: owner << 48 | the K - lgR bits
+__device__ __forceinline__ void pre_key_of(const PreKey& pk, u32 cl, u32 cr, u64& key) {
+  const u64 k = ((pk.label(cl) >> 1) << (pk.Bc + 2)) | pk.label(cr);   // (cl's t bit is 0)
+  const u64 h = pk.mix(k);
+  const u32 sh = pk.K - pk.lgR;
+  key = ((h >> sh) << 48) | (h & ((1ull << sh) - 1ull));
+}
+
 // ACGT (any case) -> 0..3; other valid IUPAC symbols -> 4; unknown -> 5
 static __device__ __forceinline__ int acgt_code(int c) {
   const int u = (c >= 'a' && c <= 'z') ? c - 32 : c;
@@ -355,11 +387,14 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
 // fl null (multi-rank phase A): first positions and the presence bitmap only; block 0 also
 // writes the status words vec = {pure-ACGT failure, 0, repetitive data} (settled by the pack
 // and the probe before this launch).
+// rfc (rank 0 of the fused multi-rank schedule, whose r-first codes are all its codes): also
+// k_dl_rfirst's code-order list and per-bucket count (rfc[b * RB + j], bcnt[b]); fpg may be null.
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_first(const u32* __restrict__ rec, const u32* __restrict__ off,
                                                         DensePlan P, u32* __restrict__ fpg, u32* __restrict__ fl,
                                                         u32* __restrict__ fo, unsigned long long* __restrict__ pb,
                                                         const Header* __restrict__ hdr = nullptr,
-                                                        u64* __restrict__ vec = nullptr) {
+                                                        u64* __restrict__ vec = nullptr, u32* __restrict__ rfc = nullptr,
+                                                        u32* __restrict__ bcnt = nullptr) {
   extern __shared__ u32 s_dyn[];
   u32* s_fp = s_dyn;                    // RB codes
   u32* s_cnt = s_dyn + (1u << P.IB);    // nch + 1 chunk counters
@@ -396,6 +431,26 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
         atomicOr(&pb[h >> 6], 1ull << (h & 63));
       }
     }
+  }
+  if (rfc) {   // code order = (k, wave, lane): exclusive prefix of the 256 (k, wave) counts
+    __shared__ u32 s_wc[16 * (kDThreads / 64)];
+    const int lane = tid & 63, wave = tid >> 6;
+    u64 m[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      m[k] = __ballot(fp[k] != ~0u);
+      if (lane == 0) s_wc[k * (kDThreads / 64) + wave] = u32(__popcll(m[k]));
+    }
+    __syncthreads();
+    u32 total;
+    const u32 e = block_excl(u32(tid) < 16u * (kDThreads / 64) ? s_wc[tid] : 0u, s_tmp, &total);
+    if (u32(tid) < 16u * (kDThreads / 64)) s_wc[tid] = e;
+    __syncthreads();
+    const u64 lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (fp[k] != ~0u) rfc[u64(b) * RB + s_wc[k * (kDThreads / 64) + wave] + u32(__popcll(m[k] & lt))] = fp[k];
+    if (tid == 0) bcnt[b] = total;
   }
   if (!fl) return;
   __syncthreads();

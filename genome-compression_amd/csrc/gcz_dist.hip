@@ -771,7 +771,7 @@ struct gcz_group {
     for (gcz_ctx* cx : ctx) {
       const hipError_t e = hipStreamSynchronize(cx->stream);
       if (watch && watch->fired) return fail(GCZ_ERR_DEVICE, watch->msg);
-      if (e != hipSuccess) return dev_fail("hipStreamSynchronize");
+      if (e != hipSuccess) return dev_fail((std::string("hipStreamSynchronize: ") + hipGetErrorString(e)).c_str());
     }
     if (watch) watch->disarm();
     return GCZ_OK;
@@ -950,9 +950,16 @@ struct gcz_group {
   RecSrc fl_rs[kMaxRanks] = {};  // ... each local rank's layer-0 record source
   // segment boundaries of the fused schedule's compute stream, a zero-length profiled scope on
   // every local rank (bench.py splits each rank's kernel time at them: scripts/budget.py's model)
-  void fl_mark(const char*) {
+  // (GCZ_FL_CHECK=1: every segment synchronised and its first device error printed -- debugging)
+  bool fl_check = std::getenv("GCZ_FL_CHECK") != nullptr;
+  void fl_mark(const char* name) {
     for (gcz_ctx* cx : ctx) {
       ProfScope ps_(cx, KID_MARK);
+      if (fl_check) {
+        const hipError_t e = hipStreamSynchronize(cx->stream), e2 = hipGetLastError();
+        if (e != hipSuccess || e2 != hipSuccess)
+          std::fprintf(stderr, "gcz fused schedule: segment %s: %s / %s\n", name, hipGetErrorString(e), hipGetErrorString(e2));
+      }
     }
   }
   Header* cx_hdr(int i) { return ctx[i]->hdr.as<Header>(); }
@@ -1932,7 +1939,8 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     rs.pkey_in = 0;
     ProfScope ps_(cx, KID_DIST);
     hipLaunchKernelGGL(k_fl_count, dim3(nb), dim3(kBlock), 0, cx->stream, rs, d.blockcnt.as<u32>(), nb,
-                       d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(), d.ddesc.as<u64>(), &h->count[kLayerSlot]);
+                       d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(), d.ddesc.as<u64>(),
+                       &h->count[kLayerSlot]);
     if (u64(R) * nb <= kBscanSmall) {
       hipLaunchKernelGGL(k_bscan_small, dim3(1), dim3(1024), 0, cx->stream, d.blockcnt.as<u32>(), u32(R), nb, dh->sync,
                          static_cast<const Header*>(h), static_cast<const u64*>(nullptr),
@@ -1982,7 +1990,16 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
   G_RC(bulk_mark());   // (K2 waits for the keys only, not for C3)
   for (int i = 0; i < NL; ++i) {   // C3: the dense sort, first positions and the presence bitmap
     int rc = ctx[i]->dense_phase_a2(las[i]);
-    if (!rc) rc = ctx[i]->dense_phase_a3(cx_hdr(i), nullptr, true, ctx[i]->dl_pb.as<u64>() + nw);
+    // (rank 0 first-holds every code it holds: its r-first lists come from this pass, before
+    // the bitmaps' exchange, where it has slack; the other ranks' from k_dl_rfirst after it)
+    if (!rc && rank[i] == 0)
+      rc = ctx[i]->ensure(ctx[i]->dl_lh, ncodes * 4 + 16) || ctx[i]->ensure(ctx[i]->dl_pos, (u64(NB0) + xw) * 4 + 64)
+               ? GCZ_ERR_DEVICE
+               : 0;
+    if (!rc)
+      rc = ctx[i]->dense_phase_a3(cx_hdr(i), nullptr, true, ctx[i]->dl_pb.as<u64>() + nw,
+                                  rank[i] == 0 ? ctx[i]->dl_lh.as<u32>() : nullptr,
+                                  rank[i] == 0 ? ctx[i]->dl_pos.as<u32>() : nullptr);
     if (rc) return rc == GCZ_ERR_DEVICE ? dev_fail("dense leaves") : rc;
   }
   fl_mark("C3");
@@ -2138,11 +2155,13 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
                          d.fl_cntb.as<u32>());
       hipLaunchKernelGGL(k_fl_prefix_relay, dim3(1), dim3(kDThreads), 0, cx->stream,
                          static_cast<const u32*>(d.fl_cntb.as<u32>()), R, DP, fo);
-      G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_rfirst), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                int((DP.nch + 1) * 4)));
-      hipLaunchKernelGGL(k_dl_rfirst, dim3(NB), dim3(kDThreads), (DP.nch + 1) * 4, cx->stream, cx->dl_fpg.as<u32>(), DP,
-                         cx->dl_pbs.as<unsigned long long>(), nw, r, cx->dl_fl.as<u32>(), cx->dl_fo.as<u32>(),
-                         cx->dl_lh.as<u32>(), bcnt);
+      if (r > 0) {   // (rank 0's lists: k_dl_first, C3)
+        G_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_dl_rfirst), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  int((DP.nch + 1) * 4)));
+        hipLaunchKernelGGL(k_dl_rfirst, dim3(NB), dim3(kDThreads), (DP.nch + 1) * 4, cx->stream, cx->dl_fpg.as<u32>(), DP,
+                           cx->dl_pbs.as<unsigned long long>(), nw, r, cx->dl_fl.as<u32>(), cx->dl_fo.as<u32>(),
+                           cx->dl_lh.as<u32>(), bcnt);
+      }
       hipLaunchKernelGGL(k_dl_fb, dim3(DP.nch), dim3(kDThreads), 0, cx->stream, cx->dl_fl.as<u32>(), cx->dl_fo.as<u32>(),
                          DP, cx->dl_fb.as<unsigned long long>());
       G_HIP(hipGetLastError());

@@ -78,29 +78,7 @@ __device__ __forceinline__ u32 owner_of(u64 key, u32 R) {
 
 constexpr u64 kLocalMulti = 1ull << 63;
 
-// The fused schedule's 6-byte layer-0 records (gcz_dist_fast.h): the canonical pair re-labelled
-// by the children's canonical 2-bit codes -- a dna::canonical code is the minimum of its orbit,
-// which holds a code and its complement (x ^ mask), so its top bit is 0: Bc = 2L - 1 bits --
-// left child code | m, right child code | m | t (a canonical node's left child never carries t,
-// include/shared_tree.h:119-126) = K = 2 Bc + 3 bits, mixed by a K-bit bijection h;
-// owner = h's top lgR bits, record = the K - lgR bits below (<= 48).
-struct PreKey {
-  u32 on;                            // 0: 8-B raw keys
-  u32 Kinv, cmask;                   // hashed code -> code
-  u32 Bc, K, lgR;
-  u32 sh;
-  u64 kmask, c1, c2;                 // the mix (PackedTab::mix's form)
-  __device__ __forceinline__ u64 mix(u64 x) const {
-    x ^= x >> sh; x = (x * c1) & kmask;
-    x ^= x >> sh; x = (x * c2) & kmask;
-    x ^= x >> sh;
-    return x;
-  }
-  __device__ __forceinline__ u64 label(u32 w) const {   // a child word -> code << 2 | m << 1 | t
-    const u32 c = ((w & kIdx) * Kinv) & cmask;
-    return (u64(c) << 2) | (((w >> 29) & 1u) << 1) | ((w >> 30) & 1u);   // (bit 29 mirror, 30 transpose)
-  }
-};
+// (PreKey, the fused schedule's layer-0 record keys: gcz_dense.h)
 
 // The elements of a level that send a record.
 struct RecSrc {
@@ -188,10 +166,7 @@ __device__ __forceinline__ bool rec_get_canon(const RecSrc& s, u64 e, u64& key, 
         key = 0;
         return false;
       }
-      const u64 k = ((s.pk.label(cl) >> 1) << (s.pk.Bc + 2)) | s.pk.label(cr);   // (cl's t bit is 0)
-      const u64 h = s.pk.mix(k);
-      const u32 sh = s.pk.K - s.pk.lgR;
-      key = ((h >> sh) << 48) | (h & ((1ull << sh) - 1ull));
+      pre_key_of(s.pk, cl, cr, key);
       return true;
     }
     key = (u64(ulw(cl)) << 31) | ulw(cr);

@@ -167,10 +167,14 @@ def test_dist_equals_single_device_tandem(gcz, groups):
 
 @pytest.mark.gpu
 @pytest.mark.slow
-@pytest.mark.parametrize("world,names", [(2, ("synth/uniform_100000003", "synth/tandem_100000000")),
+@pytest.mark.parametrize("world,names", [(2, ("synth/uniform_100000003", "synth/tandem_100000000",
+                                              "synth/uniform_1000000000")),
+                                         (4, ("synth/uniform_1000000000",)),
                                          (8, ("synth/uniform_100000003", "synth/tandem_100000000",
                                               "synth/uniform_1000000000", "synth/tandem_3200000000"))])
 def test_dist_synth_large(world, names, gcz, manifest, groups):
+    """The benchmark's genome (1 Gbase uniform: the fused schedule) at 2, 4 and 8 virtual ranks and
+    the synthetic goldens around it, against the compiled reference."""
     for name in names:
         case = manifest[name]
         kind, payload, L = case_input(case, gcz)
