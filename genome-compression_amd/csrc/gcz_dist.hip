@@ -45,7 +45,7 @@ struct gcz_dist_state {
   u64* h_gathf = nullptr;
   DlRelay* h_relay = nullptr;   // pinned staging of the dense leaf relay table (H2D, stream-ordered)
   DevBuf skey_hi, rkey_hi;   // fused schedule: the 6-byte records' high 16 bits
-  DevBuf fl_pkey;            // fused schedule: layer 0's mixed keys (k_fl_count -> k_bucket_scatter)
+  DevBuf fl_desc;            // fused schedule: k_fl_scatter's look-back descriptors + ticket
   DevBuf fl_cntb, fl_mid, fl_g3, fl_g4;   // fused schedule: r-first counts per bucket, the mid-build
   u64* h_mid = nullptr;                   // vector (+ pinned mirror), R3's / R4's gathered vectors
 };
@@ -61,7 +61,7 @@ void gcz_dist_state_free(gcz_ctx* c) {
                     &d->scval, &d->sdval, &d->clist, &d->olist, &d->rkey, &d->oslot, &d->rflag, &d->rcval, &d->rdval, &d->owntab, &d->oids,
                     &d->omin, &d->ob_cnt, &d->ob_off, &d->ob_desc, &d->ob_rec, &d->ob_seg, &d->ob_rt,
                     &d->ob_rec2, &d->ob_fo, &d->fl_cntb, &d->fl_mid, &d->fl_g3, &d->fl_g4, &d->skey_hi,
-                    &d->rkey_hi, &d->fl_pkey,
+                    &d->rkey_hi, &d->fl_desc,
                     &d->dhdr, &d->gath, &d->gath2, &d->gathf, &d->ddesc, &d->tail_in, &d->nfl})
     if (b->ptr) (void)hipFree(b->ptr);
   for (u64* h : {d->h_gath, d->h_gath2, d->h_gathf})
@@ -1755,6 +1755,14 @@ int gcz_group::exchange(std::vector<RankLevel>& lv, const std::vector<u64>& nwor
 namespace {
 // The owner's two-pass dedupe of nr received layer-0 records with K-bit keys (exchange()'s
 // k_ob_part / k_bkt_fine / k_bkt_dedupe2<true> path); false: the records do not fit it.
+// Records per owner region of the fused schedule's send buffer (k_fl_scatter): the mean p / R
+// plus 16 standard deviations of the binomial count (hashed owners) and a margin; a region that
+// overflows all the same sends the attempt to the general schedule (status bit 4).
+u64 fl_cap(u64 p, int R) {
+  const double m = double(p) / double(R);
+  return u64(m + 16.0 * std::sqrt(m) + 1024.0);
+}
+
 bool owner_two_pass_plan(u64 nr, u32 K, Bkt2Plan& b2) {
   u32 obb = 0;   // (exchange()'s single-pass precondition holds too)
   while (obb < 12 && (nr >> obb) > 4096) ++obb;
@@ -1840,11 +1848,11 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
   const int R = world, NL = int(ctx.size());
   const DistPlan& P = plan;
   const int G = P.G, D = P.D;
-  // applicable: several ranks with distributed levels to spare (G >= 2; the general schedule
+  // applicable: several ranks of one node (k_fl_scatter's owner fields) with distributed levels to spare (G >= 2; the general schedule
   // gathers a small hash-consed layer 0 to rank 0 instead -- here its exchange rides in the leaf
   // level's collective groups, so it stays distributed), every rank with pairs of its own, the
   // dense leaf level's codes
-  if (!fast_mode || R < 2 || L > 12 || G < 2 || dense_mode == 0) return GCZ_OK;
+  if (!fast_mode || R < 2 || R > kFlMaxRanks || L > 12 || G < 2 || dense_mode == 0) return GCZ_OK;
   for (int s = 0; s < R; ++s)
     if (P.count(s, 1) < 2) return GCZ_OK;
   const u64 ncodes = u64(1) << dense_code_bits(u32(L)), nw = (ncodes + 63) / 64;
@@ -1911,14 +1919,13 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     if (!used) return GCZ_OK;   // (sizes outside the dense level: the same on every rank)
     const u64 n = la.S, p = P.count(r, 1);
     const u32 nb = u32(std::max<u64>(1, (p + kTile - 1) / kTile));
-    const u32 cpr = (nb + kScanChunk - 1) / kScanChunk;   // (the three-pass scan of large levels)
-    if (u64(R) * nb > kBscanSmall && u64(R) * cpr > 1024) return fail(GCZ_ERR_CAPACITY, "bucket scan: too many chunks");
     RecSrc& rs = fl_rs[i];
     rs = RecSrc{};
     rs.pre = cx->dl_pw.as<u32>();
     rs.n = n;
     rs.p = p;
     rs.R = u32(R);
+    const u64 cap = fl_cap(p, R);
     if (split) {
       const DensePlan& DP = cx->dl_plan;
       const LevelTab mt = plan_table(nullptr, 256, 2 * Bc + 3, 2, Bc, true, 0);   // (its mix only)
@@ -1932,33 +1939,40 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       rs.pk.kmask = mt.pt.kmask;
       rs.pk.c1 = mt.pt.c1;
       rs.pk.c2 = mt.pt.c2;
-      if (cx->ensure(d.skey_hi, p * 2 + 16)) return dev_fail("fused schedule buffers");
+      if (cx->ensure(d.skey_hi, u64(R) * cap * 2 + 16)) return dev_fail("fused schedule buffers");
     }
-    if (cx->ensure(d.fl_pkey, p * 8 + 16)) return dev_fail("fused schedule buffers");
-    rs.pkey = d.fl_pkey.as<u64>();
-    rs.pkey_in = 0;
-    ProfScope ps_(cx, KID_DIST);
-    hipLaunchKernelGGL(k_fl_count, dim3(nb), dim3(kBlock), 0, cx->stream, rs, d.blockcnt.as<u32>(), nb,
-                       d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(), d.ddesc.as<u64>(),
-                       &h->count[kLayerSlot]);
-    if (u64(R) * nb <= kBscanSmall) {
-      hipLaunchKernelGGL(k_bscan_small, dim3(1), dim3(1024), 0, cx->stream, d.blockcnt.as<u32>(), u32(R), nb, dh->sync,
-                         static_cast<const Header*>(h), static_cast<const u64*>(nullptr),
-                         static_cast<const unsigned char*>(nullptr));
-    } else {
-      if (cx->ensure(d.bchunk, u64(R) * cpr * 4 + 64)) return dev_fail("bucket scan");
-      hipLaunchKernelGGL(k_bscan_sum, dim3(R * cpr), dim3(kBlock), 0, cx->stream, d.blockcnt.as<u32>(), nb, cpr,
-                         d.bchunk.as<u32>());
-      hipLaunchKernelGGL(k_bscan_top, dim3(1), dim3(1024), 0, cx->stream, d.bchunk.as<u32>(), u32(R), cpr, dh->sync);
-      hipLaunchKernelGGL(k_bscan_down, dim3(R * cpr), dim3(kBlock), 0, cx->stream, d.blockcnt.as<u32>(), nb, cpr,
-                         static_cast<const u32*>(d.bchunk.as<u32>()));
-      hipLaunchKernelGGL(k_dist_pack, dim3(1), dim3(1), 0, cx->stream, static_cast<const Header*>(h),
-                         static_cast<const u64*>(nullptr), static_cast<const unsigned char*>(nullptr), dh, u32(R));
-    }
-    G_HIP(hipGetLastError());
+    // the send buffer: R regions of cap records; the look-back descriptors and their ticket
+    if (cx->ensure(d.skey, u64(R) * cap * 8 + 16) || cx->ensure(d.sidx, u64(R) * cap * 4 + 16) ||
+        cx->ensure(d.fl_desc, u64(nb) * R * 8 + 64))
+      return dev_fail("fused schedule buffers");
+    G_HIP(hipMemsetAsync(d.fl_desc.ptr, 0, u64(nb) * R * 8 + 64, cx->stream));
   }
   fl_mark("C1");
-  // ---- R1a: status words + owner counts; the host reads them while C2 / C3 run
+  for (int i = 0; i < NL; ++i) {   // C2: the keys scattered by owner (K2's input), the owner totals
+    gcz_ctx* cx = ctx[i];
+    gcz_dist_state& d = *cx->dist;
+    const u64 p = P.count(rank[i], 1);
+    const u32 nb = u32(std::max<u64>(1, (p + kTile - 1) / kTile));
+    FlScatter a{};
+    a.skey = d.skey.as<u64>();
+    a.sidx = d.sidx.as<u32>();
+    a.skey_hi = split ? d.skey_hi.as<unsigned short>() : nullptr;
+    a.cap = fl_cap(p, R);
+    a.desc = d.fl_desc.as<u64>();
+    a.nb = nb;
+    a.tot = d.dhdr.as<DistHdr>()->sync;
+    a.h = cx->hdr.as<Header>();
+    a.gnf = d.gnf.as<unsigned char>();
+    a.gmul = d.gmul.as<unsigned char>();
+    a.ddesc = d.ddesc.as<u64>();
+    a.count_out = &cx->hdr.as<Header>()->count[kLayerSlot];
+    ProfScope ps_(cx, KID_DIST);
+    hipLaunchKernelGGL(k_fl_scatter, dim3(nb), dim3(kFsThreads), 0, cx->stream, fl_rs[i], a);
+    G_HIP(hipGetLastError());
+  }
+  fl_mark("C2");
+  G_RC(bulk_mark());   // (K2 waits for the keys only, not for R1a or C3)
+  // ---- R1a: status words + owner totals; the host reads them while C3 runs
   {
     std::vector<const void*> s;
     std::vector<void*> rv;
@@ -1975,19 +1989,6 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     G_HIP(hipMemcpyAsync(d0.h_gath, d0.gath.ptr, size_t(R) * syncw * 8, hipMemcpyDeviceToHost, ctx[0]->stream));
     G_HIP(hipEventRecord(ev_mid, ctx[0]->stream));
   }
-  for (int i = 0; i < NL; ++i) {   // C2: the keys scattered by owner (K2's input)
-    gcz_ctx* cx = ctx[i];
-    gcz_dist_state& d = *cx->dist;
-    const u64 p = P.count(rank[i], 1);
-    const u32 nb = u32(std::max<u64>(1, (p + kTile - 1) / kTile));
-    ProfScope ps_(cx, KID_DIST);
-    fl_rs[i].pkey_in = 1;   // (the count pass left the keys)
-    hipLaunchKernelGGL(k_bucket_scatter, dim3(nb), dim3(kBlock), 0, cx->stream, fl_rs[i], d.blockcnt.as<u32>(), nb,
-                       d.skey.as<u64>(), d.sidx.as<u32>(), split ? d.skey_hi.as<unsigned short>() : nullptr);
-    G_HIP(hipGetLastError());
-  }
-  fl_mark("C2");
-  G_RC(bulk_mark());   // (K2 waits for the keys only, not for C3)
   for (int i = 0; i < NL; ++i) {   // C3: the dense sort, first positions and the presence bitmap
     int rc = ctx[i]->dense_phase_a2(las[i]);
     // (rank 0 first-holds every code it holds: its r-first lists come from this pass, before
@@ -2016,7 +2017,6 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     }
     if (st) return GCZ_OK;   // every rank decides alike from the same words: the general schedule
   }
-  auto sent = [&](int r) { u64 t = 0; for (int q = 0; q < R; ++q) t += M[size_t(r) * R + q]; return t; };
   auto recvd = [&](int r) { u64 t = 0; for (int q = 0; q < R; ++q) t += M[size_t(q) * R + r]; return t; };
   std::vector<Bkt2Plan> b2(R);
   for (int s = 0; s < R; ++s)
@@ -2038,11 +2038,17 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     for (int q = R; q <= kMaxRanks; ++q) Dd.d[q] = o;
     return Dd;
   };
-  auto displ_send = [&](int r) {   // destination segments of rank r's send buffer
+  // rank r's send buffer: owner q's records at [q cap_r, q cap_r + M[r][q]) (k_fl_scatter)
+  auto displ_send = [&](int r) {
     Displ Dd{};
-    u64 o = 0;
-    for (int q = 0; q < R; ++q) { Dd.d[q] = o; o += M[size_t(r) * R + q]; }
-    for (int q = R; q <= kMaxRanks; ++q) Dd.d[q] = o;
+    const u64 cap = fl_cap(P.count(r, 1), R);
+    for (int q = 0; q <= kMaxRanks; ++q) Dd.d[q] = u64(std::min(q, R)) * cap;
+    return Dd;
+  };
+  auto displ_send_end = [&](int r) {
+    Displ Dd{};
+    const u64 cap = fl_cap(P.count(r, 1), R);
+    for (int q = 0; q <= kMaxRanks; ++q) Dd.d[q] = q < R ? u64(q) * cap + M[size_t(r) * R + q] : u64(R) * cap;
     return Dd;
   };
   // owner-side tables and buffers
@@ -2101,11 +2107,18 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       rh.push_back(cx->dist->rkey_hi.ptr);
     }
     std::vector<Transport::XOp> ops;
+    // (sources send from their owner regions, owners receive back to back in source order)
+    auto gapped = [&](size_t elem, const std::vector<const void*>& snd, const std::vector<void*>& rcv) {
+      Transport::XOp o = xop_a2a(M, R, false, elem, snd, rcv);
+      for (int s2 = 0; s2 < R; ++s2)
+        for (int q = 0; q < R; ++q) o.sd[size_t(s2) * R + q] = displ_send(s2).d[q];
+      return o;
+    };
     if (split) {   // 6-byte records: low 32 bits | high 16 bits
-      ops.push_back(xop_a2a(M, R, false, 4, sk, rk));
-      ops.push_back(xop_a2a(M, R, false, 2, sh, rh));
+      ops.push_back(gapped(4, sk, rk));
+      ops.push_back(gapped(2, sh, rh));
     } else {
-      ops.push_back(xop_a2a(M, R, false, 8, sk, rk));
+      ops.push_back(gapped(8, sk, rk));
     }
     hipEvent_t e0{};
     ctx[0]->prof_begin(KID_EXCHANGE, e0);
@@ -2274,14 +2287,15 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     const int r = rank[i];
     Header* h = cx->hdr.as<Header>();
     DistHdr* dh = d.dhdr.as<DistHdr>();
-    const u64 ns = sent(r), p = P.count(r, 1);
     const Displ SD = displ_send(r);
+    const u64 ns = SD.d[R], p = P.count(r, 1);   // (the owner regions, gaps included)
     ProfScope ps_(cx, KID_IDS);
     auto tiles = [](u64 x) { return dim3(unsigned(std::max<u64>(1, (x + kTile - 1) / kTile))); };
     hipLaunchKernelGGL(k_dist_flags, tiles(ns), dim3(kBlock), 0, cx->stream, d.sidx.as<u32>(), ns,
                        d.sflag.as<unsigned char>(), d.gnf.as<unsigned char>(), d.gmul.as<unsigned char>(), SD, u32(R),
                        &dh->sync2[1], d.clist.as<u32>(), &dh->lcnt[0], d.nfl.as<u32>(), &dh->nnf,
-                       static_cast<const unsigned char*>(d.sflag.as<unsigned char>()), displ4(r, false));
+                       static_cast<const unsigned char*>(d.sflag.as<unsigned char>()), displ4(r, false),
+                       displ_send_end(r));
     hipLaunchKernelGGL(k_lookahead, dim3(unsigned(std::max<u64>(1, ((p + 1) / 2 + kBlock - 1) / kBlock))), dim3(kBlock), 0,
                        cx->stream, static_cast<const unsigned char*>(d.gmul.as<unsigned char>()), p, &dh->fl_r4[0]);
     hipLaunchKernelGGL((k_dist_rank<uint2>), tiles(p), dim3(kBlock), 0, cx->stream, d.gnf.as<unsigned char>(),

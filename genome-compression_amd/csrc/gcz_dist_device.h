@@ -99,9 +99,6 @@ struct RecSrc {
   // labels), canonicalised on the fly; every pair but the null one is a record, lid = position
   const u32* pre;
   PreKey pk;     // ... with pk.on: 6-byte records, the key = owner << 48 | record
-  u64* pkey;     // ... the keys as k_fl_count computed them (~0: no record): written by the
-                 // count pass (pkey_out), read by the scatter (pkey_in) instead of recomputed
-  u32 pkey_in;
 };
 
 
@@ -149,28 +146,30 @@ __device__ __forceinline__ u32 rec_dest(const RecSrc& s, u64 key) {
 
 // rec_get for levels without the local dedupe (canonical pairs given): every load of the
 // record issued at once, none behind the not-first mark.
-__device__ __forceinline__ bool rec_get_canon(const RecSrc& s, u64 e, u64& key, u32& lid) {
-  if (s.pre && s.pkey_in) {
-    lid = u32(e);
-    key = e < s.p ? s.pkey[e] : ~0ull;
-    return key != ~0ull;
-  }
-  if (s.pre) {
-    u32 l = kNullWord, r = kNullWord, cl, cr, m, t;
-    if (e < s.p) load_pair(s.pre, s.n, e, l, r);
-    node_canonical(l, r, cl, cr, m, t);
-    lid = u32(e);
-    const bool ok = e < s.p && (r & kIdx) != kIdx;
-    if (s.pk.on) {
-      if (!ok) {
-        key = 0;
-        return false;
-      }
-      pre_key_of(s.pk, cl, cr, key);
-      return true;
+// the record of a pre-word pair (l, r) (in: a pair of the level); false: no record (the null
+// pair, or out of the level)
+__device__ __forceinline__ bool pre_rec(const RecSrc& s, u32 l, u32 r, bool in, u64& key) {
+  u32 cl, cr, m, t;
+  node_canonical(l, r, cl, cr, m, t);
+  const bool ok = in && (r & kIdx) != kIdx;
+  if (s.pk.on) {
+    if (!ok) {
+      key = 0;
+      return false;
     }
-    key = (u64(ulw(cl)) << 31) | ulw(cr);
-    return ok;
+    pre_key_of(s.pk, cl, cr, key);
+    return true;
+  }
+  key = (u64(ulw(cl)) << 31) | ulw(cr);
+  return ok;
+}
+
+__device__ __forceinline__ bool rec_get_canon(const RecSrc& s, u64 e, u64& key, u32& lid) {
+  if (s.pre) {
+    u32 l = kNullWord, r = kNullWord;
+    if (e < s.p) load_pair(s.pre, s.n, e, l, r);
+    lid = u32(e);
+    return pre_rec(s, l, r, e < s.p, key);
   }
   const u64 es = e < s.p ? e : 0;   // (in bounds; used only when e < p)
   const unsigned char f = s.nf[es], mu = s.multi[es];
@@ -911,7 +910,8 @@ __device__ __forceinline__ unsigned char reply_code2(unsigned char byte, u32 sh)
   return c == 0 ? 0 : c == 1 ? 6 : 7;
 }
 
-// p2 != null: the replies arrive packed (reply_at2 / reply_code2, P4 the packed segment starts), sflag unused.
+// p2 != null: the replies arrive packed (reply_at2 / reply_code2, P4 the packed segment starts), sflag unused;
+// the send buffer's segments may have gaps: owner q's records are [SD.d[q], SE.d[q]).
 static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restrict__ sidx, u64 nsent,
                                                               const unsigned char* __restrict__ sflag,
                                                               unsigned char* __restrict__ gnf,
@@ -920,14 +920,15 @@ static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restr
                                                               u32* __restrict__ lcnt, u32* __restrict__ nfl,
                                                               u32* __restrict__ nnf,
                                                               const unsigned char* __restrict__ p2 = nullptr,
-                                                              Displ P4 = {}) {
+                                                              Displ P4 = {}, Displ SE = {}) {
   __shared__ u32 hc[kMaxRanks], hd[kMaxRanks];
-  __shared__ u64 s_sd[kMaxRanks + 1], s_p4[kMaxRanks + 1];
+  __shared__ u64 s_sd[kMaxRanks + 1], s_p4[kMaxRanks + 1], s_se[kMaxRanks + 1];
   const int tid = threadIdx.x;
   if (tid < int(R)) { hc[tid] = 0; hd[tid] = 0; }
   if (tid <= kMaxRanks) {
     s_sd[tid] = SD.d[tid];
     s_p4[tid] = P4.d[tid];
+    s_se[tid] = SE.d[tid];
   }
   __syncthreads();
   const u64 k0 = u64(blockIdx.x) * kTile;
@@ -940,34 +941,39 @@ static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restr
     unsigned char fl[kB];
     u64 at[kB];
     u32 sh[kB];
+    bool ok[kB];   // a record (p2: segments with gaps -- [SD.d[q], SE.d[q]) holds owner q's records)
     if (p2) {
 #pragma unroll
       for (int b = 0; b < kB; ++b) {
         const u64 k = k0 + u64(e0 + b) * kBlock + tid;
         sh[b] = 0;
         at[b] = k < nsent ? reply_at2(s_sd, s_p4, R, k, q2, sh[b]) : 0ull;
+        ok[b] = k < nsent && k < s_se[q2];
       }
+    } else {
+#pragma unroll
+      for (int b = 0; b < kB; ++b) ok[b] = k0 + u64(e0 + b) * kBlock + tid < nsent;
     }
 #pragma unroll
     for (int b = 0; b < kB; ++b) {
       const u64 k = k0 + u64(e0 + b) * kBlock + tid;
-      li[b] = k < nsent ? sidx[k] : 0u;
-      fl[b] = k >= nsent ? 0 : p2 ? p2[at[b]] : sflag[k];
+      li[b] = ok[b] ? sidx[k] : 0u;
+      fl[b] = !ok[b] ? 0 : p2 ? p2[at[b]] : sflag[k];
     }
     if (p2) {
 #pragma unroll
-      for (int b = 0; b < kB; ++b) fl[b] = reply_code2(fl[b], sh[b]);   // (k >= nsent: byte 0 -> 0)
+      for (int b = 0; b < kB; ++b) fl[b] = reply_code2(fl[b], sh[b]);   // (no record: byte 0 -> 0)
     }
 #pragma unroll
     for (int b = 0; b < kB; ++b) {
       const u64 k = k0 + u64(e0 + b) * kBlock + tid;
       const unsigned char f = fl[b];
-      if (k < nsent) {
+      if (ok[b]) {
         if (f & 1) gnf[li[b]] = 1;
         if (f & 2) gmul[li[b]] = 1;
       }
       if (nfl) {   // (one atomic per wave with such records, none once the list is over its cap)
-        const bool nf = k < nsent && (f & 1);
+        const bool nf = ok[b] && (f & 1);
         const u64 m = __ballot(nf);
         if (m) {
           const int lane = tid & 63, lead = __ffsll((long long)m) - 1;
@@ -982,10 +988,10 @@ static __global__ __launch_bounds__(kBlock) void k_dist_flags(const u32* __restr
         }
       }
       const u32 q = (want_c(f) || want_d(f)) ? seg_of(SD, R, k) : 0u;
-      (void)wave_append(hc, q, k < nsent && want_c(f));
-      (void)wave_append(hd, q, k < nsent && want_d(f));
-      const u32 cs = wave_append(lcnt, 0u, k < nsent && want_c(f));   // (k_dist_cvals' list)
-      if (k < nsent && want_c(f)) clist[cs] = u32(k);
+      (void)wave_append(hc, q, ok[b] && want_c(f));
+      (void)wave_append(hd, q, ok[b] && want_d(f));
+      const u32 cs = wave_append(lcnt, 0u, ok[b] && want_c(f));   // (k_dist_cvals' list)
+      if (ok[b] && want_c(f)) clist[cs] = u32(k);
     }
   }
   __syncthreads();

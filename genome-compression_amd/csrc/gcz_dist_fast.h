@@ -283,58 +283,226 @@ __device__ __forceinline__ u64 fl_guard(const u64* __restrict__ g4, u32 R) {
   return t;
 }
 
-// Layer 0's records per owner, per tile of kTile pairs (the bucketing's count pass over the
-// pre-words: k_bucket_scatter with RecSrc::pre follows and reads the keys this pass leaves in
-// rs.pkey), and what the exchange expects zeroed: the global flags and the rank scan's
-// look-back words; count_out = the pairs.
-[[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_fl_count(RecSrc rs, u32* __restrict__ blockcnt, u32 nb,
-                                                         unsigned char* __restrict__ gnf,
-                                                         unsigned char* __restrict__ gmul, u64* __restrict__ ddesc,
-                                                         u64* __restrict__ count_out) {
-  __shared__ u32 h[kMaxRanks];
-  const int tid = threadIdx.x;
-  const u64 p = rs.p;
+// Layer 0's records bucketed by owner in ONE pass over the pre-words (no count pass, no scan):
+// owner q's records go to the fixed-capacity region [q cap, (q + 1) cap) of the send buffer,
+// each tile's place in it found by a decoupled look-back over the tiles' per-owner counts
+// (tiles taken in dispatch order by a ticket, so a tile waits only on tiles already running).
+// Stable: within a region the records keep position order, so owners see each source's records
+// in order (the first record of a key is its first occurrence).  A thread takes kFsItems
+// consecutive pairs, counts them per owner in 16-bit fields of two registers (owners 0-3 | 4-7:
+// a tile's count fits), one block scan of those gives every record its place in the tile's
+// owner-sorted copy in LDS, and the tile leaves LDS as R contiguous runs (coalesced stores).
+// A region that would overflow drops its surplus (never written out of bounds) and the status
+// word R gets bit 4: every rank then runs the general schedule (the mid-build read).  The last
+// tile writes the owner totals and the status words (R1a's vector, as k_bscan_small does).  Also
+// what the exchange expects zeroed: the global flags and the rank scan's look-back words;
+// count_out = the pairs.
+struct FlScatter {
+  u64* skey;               // low 32 bits of the 6-byte records (split) or 8-byte keys
+  u32* sidx;
+  unsigned short* skey_hi; // (split) the high 16 bits
+  u64 cap;                 // records per owner region
+  u64* desc;               // nb x R look-back descriptors, zeroed, then the ticket
+  u32 nb;
+  u64* tot;                // [0, R): owner totals, [R, R + 6): status words
+  const Header* h;
+  unsigned char* gnf;
+  unsigned char* gmul;
+  u64* ddesc;
+  u64* count_out;
+};
+constexpr u32 kFlSpinCap = 1u << 22;   // look-back polls before a tile gives up (status bit 8)
+constexpr int kFsThreads = 512, kFsItems = kTile / kFsThreads;   // 16 consecutive pairs a thread
+constexpr int kFlMaxRanks = 8;   // the fused schedule's ranks at most (one node)
+static_assert(kFlMaxRanks <= kFsThreads / 64 && kTile <= 65535, "one look-back wave per owner, 16-bit fields");
+
+__device__ __forceinline__ u32 fs_field(u64 lo, u64 hi, u32 d) {
+  return u32(((d < 4 ? lo : hi) >> (16 * (d & 3))) & 0xffffu);
+}
+
+[[maybe_unused]] static __global__ __launch_bounds__(kFsThreads) void k_fl_scatter(RecSrc s, FlScatter a) {
+  constexpr int kW = kFsThreads / 64;
+  __shared__ u64 s_key[kTile];
+  __shared__ unsigned short s_pos[kTile];
+  __shared__ u64 s_wl[kW], s_wh[kW];
+  __shared__ u32 s_start[kMaxRanks + 1];
+  __shared__ u64 s_base[kMaxRanks];
+  __shared__ u32 s_tile, s_bad;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const u32 R = s.R;
+  u32* ticket = reinterpret_cast<u32*>(a.desc + u64(a.nb) * R);
+  if (tid == 0) {
+    s_tile = atomicAdd(ticket, 1u);
+    s_bad = 0;
+  }
+  __syncthreads();
+  const u32 tile = s_tile;
+  const u64 p = s.p, e_base = u64(tile) * kTile;
+  {   // the flags and the look-back word of this tile's pairs, zeroed for the exchange
+    const u64 end = tile + 1 == a.nb ? p + 1 : std::min<u64>(e_base + kTile, p + 1);
+    for (u64 q = e_base / 16 + tid; q < (end + 15) / 16; q += kFsThreads) {
+      reinterpret_cast<uint4*>(a.gnf)[q] = make_uint4(0, 0, 0, 0);
+      reinterpret_cast<uint4*>(a.gmul)[q] = make_uint4(0, 0, 0, 0);
+    }
+    if (tid == 0) a.ddesc[tile] = 0;
+    if (tile == 0 && tid == 0) *a.count_out = p;
+  }
+  // this thread's kFsItems pairs: keys, owners, counts per owner
+  const u64 j0 = e_base + u64(tid) * kFsItems;
+  u64 key[kFsItems];
+  u32 okm = 0;
+  u64 cl = 0, ch = 0;
+  if (2 * (j0 + kFsItems) <= s.n) {   // every pair whole: 16-byte loads
+    const uint4* w4 = reinterpret_cast<const uint4*>(s.pre) + j0 / 2;
+    uint4 w[kFsItems / 2];
+#pragma unroll
+    for (int k = 0; k < kFsItems / 2; ++k) w[k] = w4[k];
+#pragma unroll
+    for (int k = 0; k < kFsItems / 2; ++k) {
+      if (pre_rec(s, w[k].x, w[k].y, true, key[2 * k])) okm |= 1u << (2 * k);
+      if (pre_rec(s, w[k].z, w[k].w, true, key[2 * k + 1])) okm |= 2u << (2 * k);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < kFsItems; ++e) {
+      u32 l = kNullWord, r = kNullWord;
+      const bool in = j0 + e < p;
+      if (in) load_pair(s.pre, s.n, j0 + e, l, r);
+      if (pre_rec(s, l, r, in, key[e])) okm |= 1u << e;
+    }
+  }
+  u32 dst[kFsItems / 8];   // owners, 4 bits each
+#pragma unroll
+  for (int k = 0; k < kFsItems / 8; ++k) dst[k] = 0;
+#pragma unroll
+  for (int e = 0; e < kFsItems; ++e) {
+    const u32 d = rec_dest(s, key[e]);
+    dst[e / 8] |= d << (4 * (e % 8));
+    const u64 inc = ((okm >> e) & 1u) ? 1ull << (16 * (d & 3)) : 0ull;
+    if (d < 4) cl += inc; else ch += inc;
+  }
+  // the block scan of the packed counts: this thread's first place per owner
+  u64 il = cl, ih = ch;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u64 tl = __shfl_up(il, o, 64), th = __shfl_up(ih, o, 64);
+    if (lane >= o) { il += tl; ih += th; }
+  }
+  if (lane == 63) { s_wl[wave] = il; s_wh[wave] = ih; }
+  __syncthreads();
+  u64 bl = 0, bh = 0, tl = 0, th = 0;
+#pragma unroll
+  for (int w = 0; w < kW; ++w) {
+    const u64 vl = s_wl[w], vh = s_wh[w];
+    if (w < wave) { bl += vl; bh += vh; }
+    tl += vl; th += vh;
+  }
+  // tile totals per owner -> bucket starts; every owner's aggregate published at once
+  u64 sl = 0, sh = 0;   // the buckets' starts, packed
   {
-    const u64 end = blockIdx.x + 1 == gridDim.x ? p + 1 : std::min<u64>(u64(blockIdx.x + 1) * kTile, p + 1);
-    const u64 e0 = u64(blockIdx.x) * kTile / 16, e1 = (end + 15) / 16;
-    for (u64 e = e0 + tid; e < e1; e += kBlock) {
-      reinterpret_cast<uint4*>(gnf)[e] = make_uint4(0, 0, 0, 0);
-      reinterpret_cast<uint4*>(gmul)[e] = make_uint4(0, 0, 0, 0);
+    u32 run = 0;
+    for (u32 q = 0; q < R; ++q) {
+      if (q < 4) sl |= u64(run) << (16 * q); else sh |= u64(run) << (16 * (q - 4));
+      run += fs_field(tl, th, q);
     }
-    if (tid == 0) ddesc[blockIdx.x] = 0;
+    if (tid <= int(R)) {
+      u32 st = 0;
+      for (u32 q = 0; q < u32(tid); ++q) st += fs_field(tl, th, q);
+      s_start[tid] = st;
+    }
   }
-  if (tid < int(rs.R)) h[tid] = 0;
-  if (blockIdx.x == 0 && tid == 0) *count_out = p;
-  __syncthreads();
-  // one LDS atomic per (wave, item, destination): the lanes sharing a destination found by a
-  // ballot per destination bit (R <= 8 addresses: per-lane atomics would serialize on them)
-  constexpr int kB = 8;
-  const u32 dbits = rs.R > 1 ? 32u - u32(__clz(int(rs.R - 1))) : 0u;
-  const u64 lt = (1ull << (tid & 63)) - 1ull;
-  for (int e0 = 0; e0 < kItems; e0 += kB) {
-    u64 key[kB];
-    u32 lid[kB];
-    bool ok[kB];
+  if (tid < int(R))
+    __hip_atomic_store(&a.desc[u64(tile) * R + tid], (tile == 0 ? kStP : kStA) | u64(fs_field(tl, th, u32(tid))),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the records into the owner-sorted copy
+  u64 curl = sl + bl + il - cl, curh = sh + bh + ih - ch;
 #pragma unroll
-    for (int q = 0; q < kB; ++q) {
-      const u64 e = u64(blockIdx.x) * kTile + u64(e0 + q) * kBlock + tid;
-      ok[q] = rec_get_canon(rs, e, key[q], lid[q]);
-      if (e < p) rs.pkey[e] = ok[q] ? key[q] : ~0ull;
+  for (int e = 0; e < kFsItems; ++e) {
+    const u32 d = (dst[e / 8] >> (4 * (e % 8))) & 15u;
+    if ((okm >> e) & 1u) {
+      const u32 at = fs_field(curl, curh, d);
+      s_key[at] = key[e];
+      s_pos[at] = (unsigned short)(tid * kFsItems + e);
+      const u64 inc = 1ull << (16 * (d & 3));
+      if (d < 4) curl += inc; else curh += inc;
     }
-#pragma unroll
-    for (int q = 0; q < kB; ++q) {
-      const u32 d = ok[q] ? rec_dest(rs, key[q]) : 0u;
-      u64 m = __ballot(ok[q]);
-      for (u32 bit = 0; bit < dbits; ++bit) {
-        const bool set = (d >> bit) & 1u;
-        const u64 bb = __ballot(ok[q] && set);
-        m &= set ? bb : ~bb;
+  }
+  // the look-back: owner q by wave q (64 predecessors per poll)
+  if (u32(wave) < R) {
+    const u32 q = u32(wave);
+    const u64 agg = fs_field(tl, th, q);
+    u64 prefix = 0;
+    if (tile > 0) {
+      long long look = (long long)tile - 1;
+      u32 polls = 0;
+      for (;;) {
+        const long long idx = look - lane;
+        const u64 dv = idx >= 0 ? __hip_atomic_load(&a.desc[u64(idx) * R + q], __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT)
+                                : 0ull;
+        const u64 st = dv >> 62;
+        const u64 pm = __ballot(st == 2);
+        const u64 zm = __ballot(idx >= 0 && st == 0);
+        const int firstP = pm ? __ffsll((long long)pm) - 1 : 64;
+        const u64 need = firstP >= 63 ? ~0ull : ((1ull << (firstP + 1)) - 1);
+        if (zm & need) {
+          if (++polls > kFlSpinCap) {   // (bounded: a tile never waits forever)
+            if (lane == 0) s_bad = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        prefix += wave_sum(lane <= firstP && idx >= 0 ? (dv & kValMask) : 0ull);
+        if (firstP < 64 || look < 64) break;
+        look -= 64;
       }
-      if (ok[q] && (m & lt) == 0) atomicAdd(&h[d], u32(__popcll(m)));
+      if (lane == 0)
+        __hip_atomic_store(&a.desc[u64(tile) * R + q], kStP | (prefix + agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (lane == 0) s_base[q] = prefix;
   }
   __syncthreads();
-  if (tid < int(rs.R)) blockcnt[u64(tid) * nb + blockIdx.x] = h[tid];
+  if (tile + 1 == a.nb && tid <= int(R) + 5) {   // the last tile: owner totals and status words
+    if (tid < int(R)) {
+      const u64 t = s_base[tid] + fs_field(tl, th, u32(tid));
+      a.tot[tid] = t > a.cap ? a.cap : t;
+    } else {
+      const u32 w = u32(tid) - R;
+      u64 v = 0;
+      if (w == 0) {
+        u32 over = 0;
+        for (u32 q = 0; q < R; ++q) over |= s_base[q] + fs_field(tl, th, q) > a.cap ? 1u : 0u;
+        v = u64(a.h->overflow | a.h->leaf_overflow) | (over ? 16ull : 0ull) | (s_bad ? 256ull : 0ull);
+      } else if (w == 2) {
+        v = a.h->err_offset;
+      } else if (w == 4) {
+        v = u64(a.h->predup);
+      } else if (w == 5) {
+        v = u64(a.h->dense_fail);
+      }
+      a.tot[tid] = v;
+    }
+  }
+  // the owner-sorted copy out: R contiguous runs
+  const u32 nt = s_start[R];
+  for (u32 i = u32(tid); i < nt; i += kFsThreads) {
+    u32 q = 0;
+    while (q + 1 < R && i >= s_start[q + 1]) ++q;
+    const u64 o = s_base[q] + (i - s_start[q]);
+    if (o < a.cap) {   // (a surplus record is dropped: status bit 4, the general schedule)
+      const u64 at = u64(q) * a.cap + o;
+      const u64 k = s_key[i];
+      if (a.skey_hi) {
+        reinterpret_cast<u32*>(a.skey)[at] = u32(k);
+        a.skey_hi[at] = (unsigned short)(k >> 32);
+      } else {
+        a.skey[at] = k;
+      }
+      a.sidx[at] = u32(e_base + s_pos[i]);
+    }
+  }
 }
 
 // C and D at the owner, one block: the first holders' ids into the keys' id slots, then every

@@ -20,7 +20,7 @@ overlap (the fused schedule, gcz_group::build_fast): the line also carries each 
 segments (`rank_timeline[r].segments_ms`, kernel time between the schedule's fl_mark points
 C1 .. C8 and the tail after C8), and the model replays the schedule's dependencies:
 
-    C1 | R1a | C2 [bulk mark] C3 | (host: R1a + t_sync) R1b | C4 | R2 | (wait K2) C5 | R3 | C6 | R4 |
+    C1 C2 [bulk mark] | R1a | C3 | (host: R1a + t_sync) R1b | C4 | R2 | (wait K2) C5 | R3 | C6 | R4 |
     C7 | R5 | C8 tail | top gather | final vectors | t_sync
 
 A collective starts when every rank has reached it (its end is common to all ranks); K2, the
@@ -124,10 +124,10 @@ def overlap_model(segs, names, xb, B, verbose=False):
         return t1
 
     comp(0)
-    r1a = coll("R1a", None)
-    host = r1a + sync                      # the mid-build read
     comp(1)
     c2_end = max(ready)
+    r1a = coll("R1a", None)
+    host = r1a + sync                      # the mid-build read
     bulk = Bulk(max(c2_end, host), lat, xb[idx["K2"]])
     comp(2)
     coll("R1b", bulk, host)
