@@ -1967,7 +1967,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     a.ddesc = d.ddesc.as<u64>();
     a.count_out = &cx->hdr.as<Header>()->count[kLayerSlot];
     ProfScope ps_(cx, KID_DIST);
-    hipLaunchKernelGGL(k_fl_scatter, dim3(nb), dim3(kFsThreads), 0, cx->stream, fl_rs[i], a);
+    hipLaunchKernelGGL(k_fl_scatter, dim3(std::min<u32>(nb, kFsGrid)), dim3(kFsThreads), 0, cx->stream, fl_rs[i], a);
     G_HIP(hipGetLastError());
   }
   fl_mark("C2");

@@ -302,7 +302,7 @@ struct FlScatter {
   u32* sidx;
   unsigned short* skey_hi; // (split) the high 16 bits
   u64 cap;                 // records per owner region
-  u64* desc;               // nb x R look-back descriptors, zeroed, then the ticket
+  u64* desc;               // R x nb look-back descriptors (owner-major: a poll reads 512 B), zeroed, then the ticket
   u32 nb;
   u64* tot;                // [0, R): owner totals, [R, R + 6): status words
   const Header* h;
@@ -313,6 +313,7 @@ struct FlScatter {
 };
 constexpr u32 kFlSpinCap = 1u << 22;   // look-back polls before a tile gives up (status bit 8)
 constexpr int kFsThreads = 512, kFsItems = kTile / kFsThreads;   // 16 consecutive pairs a thread
+constexpr u32 kFsGrid = 512;     // persistent blocks: two per CU (80 KB of LDS each) on 256 CUs
 constexpr int kFlMaxRanks = 8;   // the fused schedule's ranks at most (one node)
 static_assert(kFlMaxRanks <= kFsThreads / 64 && kTile <= 65535, "one look-back wave per owner, 16-bit fields");
 
@@ -320,6 +321,26 @@ __device__ __forceinline__ u32 fs_field(u64 lo, u64 hi, u32 d) {
   return u32(((d < 4 ? lo : hi) >> (16 * (d & 3))) & 0xffffu);
 }
 
+// this thread's kFsItems pairs of tile `tile` (pairs past the level: null words)
+__device__ __forceinline__ void fs_load(const RecSrc& s, u32 tile, uint4 (&w)[kFsItems / 2]) {
+  const u64 j0 = u64(tile) * kTile + u64(threadIdx.x) * kFsItems;
+  if (2 * (j0 + kFsItems) <= s.n) {   // every pair whole: 16-byte loads
+    const uint4* w4 = reinterpret_cast<const uint4*>(s.pre) + j0 / 2;
+#pragma unroll
+    for (int k = 0; k < kFsItems / 2; ++k) w[k] = w4[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < kFsItems / 2; ++k) {
+      u32 l0 = kNullWord, r0 = kNullWord, l1 = kNullWord, r1 = kNullWord;
+      if (j0 + 2 * k < s.p) load_pair(s.pre, s.n, j0 + 2 * k, l0, r0);
+      if (j0 + 2 * k + 1 < s.p) load_pair(s.pre, s.n, j0 + 2 * k + 1, l1, r1);
+      w[k] = make_uint4(l0, r0, l1, r1);
+    }
+  }
+}
+
+// Persistent: a block takes tiles by the ticket until none is left; the next tile's pre-words
+// are in flight while the block waits on its look-back and writes the current tile out.
 [[maybe_unused]] static __global__ __launch_bounds__(kFsThreads) void k_fl_scatter(RecSrc s, FlScatter a) {
   constexpr int kW = kFsThreads / 64;
   __shared__ u64 s_key[kTile];
@@ -327,181 +348,182 @@ __device__ __forceinline__ u32 fs_field(u64 lo, u64 hi, u32 d) {
   __shared__ u64 s_wl[kW], s_wh[kW];
   __shared__ u32 s_start[kMaxRanks + 1];
   __shared__ u64 s_base[kMaxRanks];
-  __shared__ u32 s_tile, s_bad;
+  __shared__ u32 s_tile[2], s_bad;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const u32 R = s.R;
   u32* ticket = reinterpret_cast<u32*>(a.desc + u64(a.nb) * R);
   if (tid == 0) {
-    s_tile = atomicAdd(ticket, 1u);
+    s_tile[0] = atomicAdd(ticket, 1u);
     s_bad = 0;
   }
   __syncthreads();
-  const u32 tile = s_tile;
-  const u64 p = s.p, e_base = u64(tile) * kTile;
-  {   // the flags and the look-back word of this tile's pairs, zeroed for the exchange
-    const u64 end = tile + 1 == a.nb ? p + 1 : std::min<u64>(e_base + kTile, p + 1);
-    for (u64 q = e_base / 16 + tid; q < (end + 15) / 16; q += kFsThreads) {
-      reinterpret_cast<uint4*>(a.gnf)[q] = make_uint4(0, 0, 0, 0);
-      reinterpret_cast<uint4*>(a.gmul)[q] = make_uint4(0, 0, 0, 0);
+  u32 tile = s_tile[0];
+  uint4 w[kFsItems / 2];
+  if (tile < a.nb) fs_load(s, tile, w);
+  for (int it = 0; tile < a.nb; ++it) {
+    const u64 p = s.p, e_base = u64(tile) * kTile;
+    {   // the flags and the look-back word of this tile's pairs, zeroed for the exchange
+      const u64 end = tile + 1 == a.nb ? p + 1 : std::min<u64>(e_base + kTile, p + 1);
+      for (u64 q = e_base / 16 + tid; q < (end + 15) / 16; q += kFsThreads) {
+        reinterpret_cast<uint4*>(a.gnf)[q] = make_uint4(0, 0, 0, 0);
+        reinterpret_cast<uint4*>(a.gmul)[q] = make_uint4(0, 0, 0, 0);
+      }
+      if (tid == 0) {
+        a.ddesc[tile] = 0;
+        if (tile == 0) *a.count_out = p;
+        s_tile[(it + 1) & 1] = atomicAdd(ticket, 1u);   // (read after the next barrier)
+      }
     }
-    if (tid == 0) a.ddesc[tile] = 0;
-    if (tile == 0 && tid == 0) *a.count_out = p;
-  }
-  // this thread's kFsItems pairs: keys, owners, counts per owner
-  const u64 j0 = e_base + u64(tid) * kFsItems;
-  u64 key[kFsItems];
-  u32 okm = 0;
-  u64 cl = 0, ch = 0;
-  if (2 * (j0 + kFsItems) <= s.n) {   // every pair whole: 16-byte loads
-    const uint4* w4 = reinterpret_cast<const uint4*>(s.pre) + j0 / 2;
-    uint4 w[kFsItems / 2];
-#pragma unroll
-    for (int k = 0; k < kFsItems / 2; ++k) w[k] = w4[k];
+    // keys, owners, counts per owner
+    const u64 j0 = e_base + u64(tid) * kFsItems;
+    u64 key[kFsItems];
+    u32 okm = 0;
 #pragma unroll
     for (int k = 0; k < kFsItems / 2; ++k) {
-      if (pre_rec(s, w[k].x, w[k].y, true, key[2 * k])) okm |= 1u << (2 * k);
-      if (pre_rec(s, w[k].z, w[k].w, true, key[2 * k + 1])) okm |= 2u << (2 * k);
+      if (pre_rec(s, w[k].x, w[k].y, j0 + 2 * k < p, key[2 * k])) okm |= 1u << (2 * k);
+      if (pre_rec(s, w[k].z, w[k].w, j0 + 2 * k + 1 < p, key[2 * k + 1])) okm |= 2u << (2 * k);
     }
-  } else {
+    u64 cl = 0, ch = 0;
+    u32 dst[kFsItems / 8];   // owners, 4 bits each
+#pragma unroll
+    for (int k = 0; k < kFsItems / 8; ++k) dst[k] = 0;
 #pragma unroll
     for (int e = 0; e < kFsItems; ++e) {
-      u32 l = kNullWord, r = kNullWord;
-      const bool in = j0 + e < p;
-      if (in) load_pair(s.pre, s.n, j0 + e, l, r);
-      if (pre_rec(s, l, r, in, key[e])) okm |= 1u << e;
+      const u32 d = rec_dest(s, key[e]);
+      dst[e / 8] |= d << (4 * (e % 8));
+      const u64 inc = ((okm >> e) & 1u) ? 1ull << (16 * (d & 3)) : 0ull;
+      if (d < 4) cl += inc; else ch += inc;
     }
-  }
-  u32 dst[kFsItems / 8];   // owners, 4 bits each
+    // the block scan of the packed counts: this thread's first place per owner
+    u64 il = cl, ih = ch;
 #pragma unroll
-  for (int k = 0; k < kFsItems / 8; ++k) dst[k] = 0;
-#pragma unroll
-  for (int e = 0; e < kFsItems; ++e) {
-    const u32 d = rec_dest(s, key[e]);
-    dst[e / 8] |= d << (4 * (e % 8));
-    const u64 inc = ((okm >> e) & 1u) ? 1ull << (16 * (d & 3)) : 0ull;
-    if (d < 4) cl += inc; else ch += inc;
-  }
-  // the block scan of the packed counts: this thread's first place per owner
-  u64 il = cl, ih = ch;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const u64 tl = __shfl_up(il, o, 64), th = __shfl_up(ih, o, 64);
-    if (lane >= o) { il += tl; ih += th; }
-  }
-  if (lane == 63) { s_wl[wave] = il; s_wh[wave] = ih; }
-  __syncthreads();
-  u64 bl = 0, bh = 0, tl = 0, th = 0;
-#pragma unroll
-  for (int w = 0; w < kW; ++w) {
-    const u64 vl = s_wl[w], vh = s_wh[w];
-    if (w < wave) { bl += vl; bh += vh; }
-    tl += vl; th += vh;
-  }
-  // tile totals per owner -> bucket starts; every owner's aggregate published at once
-  u64 sl = 0, sh = 0;   // the buckets' starts, packed
-  {
-    u32 run = 0;
-    for (u32 q = 0; q < R; ++q) {
-      if (q < 4) sl |= u64(run) << (16 * q); else sh |= u64(run) << (16 * (q - 4));
-      run += fs_field(tl, th, q);
+    for (int o = 1; o < 64; o <<= 1) {
+      const u64 tl = __shfl_up(il, o, 64), th = __shfl_up(ih, o, 64);
+      if (lane >= o) { il += tl; ih += th; }
     }
-    if (tid <= int(R)) {
-      u32 st = 0;
-      for (u32 q = 0; q < u32(tid); ++q) st += fs_field(tl, th, q);
-      s_start[tid] = st;
-    }
-  }
-  if (tid < int(R))
-    __hip_atomic_store(&a.desc[u64(tile) * R + tid], (tile == 0 ? kStP : kStA) | u64(fs_field(tl, th, u32(tid))),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // the records into the owner-sorted copy
-  u64 curl = sl + bl + il - cl, curh = sh + bh + ih - ch;
+    if (lane == 63) { s_wl[wave] = il; s_wh[wave] = ih; }
+    __syncthreads();
+    const u32 next = s_tile[(it + 1) & 1];
+    u64 bl = 0, bh = 0, tl = 0, th = 0;
 #pragma unroll
-  for (int e = 0; e < kFsItems; ++e) {
-    const u32 d = (dst[e / 8] >> (4 * (e % 8))) & 15u;
-    if ((okm >> e) & 1u) {
-      const u32 at = fs_field(curl, curh, d);
-      s_key[at] = key[e];
-      s_pos[at] = (unsigned short)(tid * kFsItems + e);
-      const u64 inc = 1ull << (16 * (d & 3));
-      if (d < 4) curl += inc; else curh += inc;
+    for (int w2 = 0; w2 < kW; ++w2) {
+      const u64 vl = s_wl[w2], vh = s_wh[w2];
+      if (w2 < wave) { bl += vl; bh += vh; }
+      tl += vl; th += vh;
     }
-  }
-  // the look-back: owner q by wave q (64 predecessors per poll)
-  if (u32(wave) < R) {
-    const u32 q = u32(wave);
-    const u64 agg = fs_field(tl, th, q);
-    u64 prefix = 0;
-    if (tile > 0) {
-      long long look = (long long)tile - 1;
-      u32 polls = 0;
-      for (;;) {
-        const long long idx = look - lane;
-        const u64 dv = idx >= 0 ? __hip_atomic_load(&a.desc[u64(idx) * R + q], __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT)
-                                : 0ull;
-        const u64 st = dv >> 62;
-        const u64 pm = __ballot(st == 2);
-        const u64 zm = __ballot(idx >= 0 && st == 0);
-        const int firstP = pm ? __ffsll((long long)pm) - 1 : 64;
-        const u64 need = firstP >= 63 ? ~0ull : ((1ull << (firstP + 1)) - 1);
-        if (zm & need) {
-          if (++polls > kFlSpinCap) {   // (bounded: a tile never waits forever)
-            if (lane == 0) s_bad = 1;
-            break;
+    // tile totals per owner -> bucket starts; every owner's aggregate published at once
+    u64 sl = 0, sh = 0;   // the buckets' starts, packed
+    {
+      u32 run = 0;
+      for (u32 q = 0; q < R; ++q) {
+        if (q < 4) sl |= u64(run) << (16 * q); else sh |= u64(run) << (16 * (q - 4));
+        run += fs_field(tl, th, q);
+      }
+      if (tid <= int(R)) {
+        u32 st = 0;
+        for (u32 q = 0; q < u32(tid); ++q) st += fs_field(tl, th, q);
+        s_start[tid] = st;
+      }
+    }
+    if (tid < int(R))
+      __hip_atomic_store(&a.desc[u64(tid) * a.nb + tile], (tile == 0 ? kStP : kStA) | u64(fs_field(tl, th, u32(tid))),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the records into the owner-sorted copy
+    u64 curl = sl + bl + il - cl, curh = sh + bh + ih - ch;
+#pragma unroll
+    for (int e = 0; e < kFsItems; ++e) {
+      const u32 d = (dst[e / 8] >> (4 * (e % 8))) & 15u;
+      if ((okm >> e) & 1u) {
+        const u32 at = fs_field(curl, curh, d);
+        s_key[at] = key[e];
+        s_pos[at] = (unsigned short)(tid * kFsItems + e);
+        const u64 inc = 1ull << (16 * (d & 3));
+        if (d < 4) curl += inc; else curh += inc;
+      }
+    }
+    if (next < a.nb) fs_load(s, next, w);   // (in flight through the look-back and the write-out)
+    // the look-back: owner q by wave q (64 predecessors per poll)
+    if (u32(wave) < R) {
+      const u32 q = u32(wave);
+      const u64 agg = fs_field(tl, th, q);
+      u64 prefix = 0;
+      if (tile > 0) {
+        long long look = (long long)tile - 1;
+        u32 polls = 0;
+        for (;;) {
+          const long long idx = look - lane;
+          const u64 dv = idx >= 0 ? __hip_atomic_load(&a.desc[u64(q) * a.nb + u64(idx)], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT)
+                                  : 0ull;
+          const u64 st = dv >> 62;
+          const u64 pm = __ballot(st == 2);
+          const u64 zm = __ballot(idx >= 0 && st == 0);
+          const int firstP = pm ? __ffsll((long long)pm) - 1 : 64;
+          const u64 need = firstP >= 63 ? ~0ull : ((1ull << (firstP + 1)) - 1);
+          if (zm & need) {
+            if (++polls > kFlSpinCap) {   // (bounded: a tile never waits forever)
+              if (lane == 0) s_bad = 1;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
           }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
+          prefix += wave_sum(lane <= firstP && idx >= 0 ? (dv & kValMask) : 0ull);
+          if (firstP < 64 || look < 64) break;
+          look -= 64;
         }
-        prefix += wave_sum(lane <= firstP && idx >= 0 ? (dv & kValMask) : 0ull);
-        if (firstP < 64 || look < 64) break;
-        look -= 64;
+        if (lane == 0)
+          __hip_atomic_store(&a.desc[u64(q) * a.nb + tile], kStP | (prefix + agg), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (lane == 0)
-        __hip_atomic_store(&a.desc[u64(tile) * R + q], kStP | (prefix + agg), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) s_base[q] = prefix;
     }
-    if (lane == 0) s_base[q] = prefix;
-  }
-  __syncthreads();
-  if (tile + 1 == a.nb && tid <= int(R) + 5) {   // the last tile: owner totals and status words
-    if (tid < int(R)) {
-      const u64 t = s_base[tid] + fs_field(tl, th, u32(tid));
-      a.tot[tid] = t > a.cap ? a.cap : t;
-    } else {
-      const u32 w = u32(tid) - R;
-      u64 v = 0;
-      if (w == 0) {
-        u32 over = 0;
-        for (u32 q = 0; q < R; ++q) over |= s_base[q] + fs_field(tl, th, q) > a.cap ? 1u : 0u;
-        v = u64(a.h->overflow | a.h->leaf_overflow) | (over ? 16ull : 0ull) | (s_bad ? 256ull : 0ull);
-      } else if (w == 2) {
-        v = a.h->err_offset;
-      } else if (w == 4) {
-        v = u64(a.h->predup);
-      } else if (w == 5) {
-        v = u64(a.h->dense_fail);
-      }
-      a.tot[tid] = v;
-    }
-  }
-  // the owner-sorted copy out: R contiguous runs
-  const u32 nt = s_start[R];
-  for (u32 i = u32(tid); i < nt; i += kFsThreads) {
-    u32 q = 0;
-    while (q + 1 < R && i >= s_start[q + 1]) ++q;
-    const u64 o = s_base[q] + (i - s_start[q]);
-    if (o < a.cap) {   // (a surplus record is dropped: status bit 4, the general schedule)
-      const u64 at = u64(q) * a.cap + o;
-      const u64 k = s_key[i];
-      if (a.skey_hi) {
-        reinterpret_cast<u32*>(a.skey)[at] = u32(k);
-        a.skey_hi[at] = (unsigned short)(k >> 32);
+    __syncthreads();
+    if (tile + 1 == a.nb && tid <= int(R) + 5) {   // the last tile: owner totals and status words
+      if (tid < int(R)) {
+        const u64 t = s_base[tid] + fs_field(tl, th, u32(tid));
+        a.tot[tid] = t > a.cap ? a.cap : t;
       } else {
-        a.skey[at] = k;
+        const u32 w2 = u32(tid) - R;
+        u64 v = 0;
+        if (w2 == 0) {
+          u32 over = 0;
+          for (u32 q = 0; q < R; ++q) over |= s_base[q] + fs_field(tl, th, q) > a.cap ? 1u : 0u;
+          v = u64(a.h->overflow | a.h->leaf_overflow) | (over ? 16ull : 0ull) | (s_bad ? 256ull : 0ull);
+        } else if (w2 == 2) {
+          v = a.h->err_offset;
+        } else if (w2 == 4) {
+          v = u64(a.h->predup);
+        } else if (w2 == 5) {
+          v = u64(a.h->dense_fail);
+        }
+        a.tot[tid] = v;
       }
-      a.sidx[at] = u32(e_base + s_pos[i]);
     }
+    // the owner-sorted copy out: R contiguous runs
+    u32 st[kFlMaxRanks + 1];
+#pragma unroll
+    for (int q = 0; q <= kFlMaxRanks; ++q) st[q] = s_start[q <= int(R) ? q : int(R)];
+    const u32 nt = st[kFlMaxRanks];
+    for (u32 i = u32(tid); i < nt; i += kFsThreads) {
+      u32 q = 0;
+#pragma unroll
+      for (int k = 1; k < kFlMaxRanks; ++k) q += i >= st[k] ? 1u : 0u;   // (empty buckets: equal starts)
+      const u64 o = s_base[q] + (i - s_start[q]);
+      if (o < a.cap) {   // (a surplus record is dropped: status bit 4, the general schedule)
+        const u64 at = u64(q) * a.cap + o;
+        const u64 k = s_key[i];
+        if (a.skey_hi) {
+          reinterpret_cast<u32*>(a.skey)[at] = u32(k);
+          a.skey_hi[at] = (unsigned short)(k >> 32);
+        } else {
+          a.skey[at] = k;
+        }
+        a.sidx[at] = u32(e_base + s_pos[i]);
+      }
+    }
+    __syncthreads();   // (the copy, the starts and the bases are the next tile's)
+    tile = next;
   }
 }
 
