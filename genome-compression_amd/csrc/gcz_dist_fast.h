@@ -465,7 +465,9 @@ __device__ __forceinline__ void fs_load(const RecSrc& s, u32 tile, uint4 (&w)[kF
               if (lane == 0) s_bad = 1;
               break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            // back off (the polls are uncached loads: a tight spin of every waiting tile costs
+            // the chip's memory bandwidth)
+            for (u32 z = 0; z < std::min<u32>(polls, 8u); ++z) __builtin_amdgcn_s_sleep(16);
             continue;
           }
           prefix += wave_sum(lane <= firstP && idx >= 0 ? (dv & kValMask) : 0ull);
