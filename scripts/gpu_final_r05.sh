@@ -1,12 +1,12 @@
-# Round-4 evidence at HEAD: full GPU suite + smoke, the default bench (CPU baseline
+# Round-5 evidence at HEAD: full GPU suite + smoke, the default bench (CPU baseline
 # included), the rocprof / PMC passes of uniform_1g and tandem (part 1); the tandem and
 # corpus bench lines, strong virtual-rank probes (uniform 8/4/2, tandem 8), the weak-scaled
 # probe (8 Gbase over 8 virtual ranks = 1 Gbase per rank), the drop-in latency probe (part 2).
-# usage: bash scripts/gpu_final_r04.sh <tag> [1|2|all]   (one gpurun call per part fits its limit)
+# usage: bash scripts/gpu_final_r05.sh <tag> [1|2|all]   (one gpurun call per part fits its limit)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-tag=${1:-r04f}; part=${2:-all}
+tag=${1:-r05f}; part=${2:-all}
 mkdir -p gpurun_out
 if [ "$part" = 1 ] || [ "$part" = all ]; then
   timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$tag.txt 2>&1 &&
