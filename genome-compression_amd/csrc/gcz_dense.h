@@ -54,6 +54,9 @@ struct DensePlan {
   u32 NB;      // buckets, power of two <= kDNBMax
   u32 IB;      // log2(codes per bucket) <= kDLog
   u32 K, Kinv; // odd multiplier mod 4^L and its inverse
+  // the fused multi-rank schedule's sort and first pass, queued before its mid-build read: they
+  // return at once when the pack found repetitive or non-ACGT data (that attempt is discarded)
+  const Header* gate;
 };
 
 // The fused schedule's 6-byte layer-0 records (gcz_dist_fast.h): the canonical pair re-labelled
@@ -289,6 +292,7 @@ template <int L, bool kBases>
 // staged in LDS so every run is written contiguously.
 [[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_scatter(const u32* __restrict__ pw, DensePlan P,
                                                           const u32* __restrict__ offt, u32* __restrict__ rec) {
+  if (P.gate && (P.gate->predup | P.gate->dense_fail)) return;
   extern __shared__ u32 s_dyn[];
   u32* s_stage = s_dyn;                 // kDC records
   u32* s_base = s_dyn + kDC;            // NB + 1: local exclusive offsets of the runs
@@ -395,6 +399,7 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
                                                         const Header* __restrict__ hdr = nullptr,
                                                         u64* __restrict__ vec = nullptr, u32* __restrict__ rfc = nullptr,
                                                         u32* __restrict__ bcnt = nullptr) {
+  if (P.gate && (P.gate->predup | P.gate->dense_fail)) return;
   extern __shared__ u32 s_dyn[];
   u32* s_fp = s_dyn;                    // RB codes
   u32* s_cnt = s_dyn + (1u << P.IB);    // nch + 1 chunk counters

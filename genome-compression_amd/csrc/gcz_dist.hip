@@ -1990,6 +1990,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     G_HIP(hipEventRecord(ev_mid, ctx[0]->stream));
   }
   for (int i = 0; i < NL; ++i) {   // C3: the dense sort, first positions and the presence bitmap
+    ctx[i]->dl_plan.gate = cx_hdr(i);   // (skipped on the device when the pack found repetitive data)
     int rc = ctx[i]->dense_phase_a2(las[i]);
     // (rank 0 first-holds every code it holds: its r-first lists come from this pass, before
     // the bitmaps' exchange, where it has slack; the other ranks' from k_dl_rfirst after it)
@@ -2001,6 +2002,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       rc = ctx[i]->dense_phase_a3(cx_hdr(i), nullptr, true, ctx[i]->dl_pb.as<u64>() + nw,
                                   rank[i] == 0 ? ctx[i]->dl_lh.as<u32>() : nullptr,
                                   rank[i] == 0 ? ctx[i]->dl_pos.as<u32>() : nullptr);
+    ctx[i]->dl_plan.gate = nullptr;
     if (rc) return rc == GCZ_ERR_DEVICE ? dev_fail("dense leaves") : rc;
   }
   fl_mark("C3");

@@ -351,6 +351,17 @@ __device__ __forceinline__ void fs_load(const RecSrc& s, u32 tile, uint4 (&w)[kF
   __shared__ u32 s_tile[2], s_bad;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const u32 R = s.R;
+  if (a.h->predup | a.h->dense_fail) {   // repetitive or not pure ACGT (the pack said so): the
+    // general schedule runs instead, so only R1a's vector is written (no scatter to waste)
+    if (blockIdx.x == 0 && tid <= int(R) + 5)
+      a.tot[tid] = tid < int(R) ? 0ull
+                 : tid == int(R)     ? u64(a.h->overflow | a.h->leaf_overflow)
+                 : tid == int(R) + 2 ? a.h->err_offset
+                 : tid == int(R) + 4 ? u64(a.h->predup)
+                 : tid == int(R) + 5 ? u64(a.h->dense_fail)
+                                     : 0ull;
+    return;
+  }
   u32* ticket = reinterpret_cast<u32*>(a.desc + u64(a.nb) * R);
   if (tid == 0) {
     s_tile[0] = atomicAdd(ticket, 1u);
