@@ -2396,10 +2396,9 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       a.nodes = cx->nodes_out.as<uint2>() + node_base[i][0];
       a.words0 = cx->wb.as<u32>();
       a.guard = &dh->fl_guard;
-      a.rd = d.sdval.as<u64>();
-      a.SD = displ_send(r);
-      a.sidx = d.sidx.as<u32>();
-      a.bad = &dh->fl_bad;
+      hipLaunchKernelGGL(k_fl_dpatch, dim3(unsigned((u64(R) * kFlCap + 255) / 256)), dim3(256), 0, cx->stream,
+                         static_cast<const u64*>(d.sdval.as<u64>()), displ_send(r), u32(R),
+                         static_cast<const u32*>(d.sidx.as<u32>()), d.gid.as<u32>(), &dh->fl_bad);
       hipLaunchKernelGGL(k_fl_words_l0, dim3(DP.nch), dim3(kDThreads), words_bytes, cx->stream, cx->dl_rec.as<u32>(),
                          cx->dl_idrec.as<u32>(), cx->dl_offt.as<u32>(), DP, cx->dl_fb.as<unsigned long long>(),
                          static_cast<const u32*>(cx->dl_pw.as<u32>()), cx->leaves_out.as<u64>(), a);

@@ -667,13 +667,27 @@ struct FlL0 {
   uint2* nodes;               // the rank's slice of layer 0
   u32* words0;                // layer-0 words (the direct subtrees' input)
   u64* guard;
-  // R5's D records (the owners' ids of this rank's not-first pairs): each
-  // block writes the ones of its own pairs into gid before reading them
-  const u64* rd;
-  Displ SD;
-  const u32* sidx;
-  u32* bad;
 };
+
+// R5's D records (the owners' ids of this rank's not-first pairs whose first holder is another
+// rank) into gid, one thread a slot, before k_fl_words_l0 reads them (a few hundred records: in
+// every words block, the R dependent segment reads cost each workgroup several microseconds)
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_fl_dpatch(const u64* __restrict__ rd, Displ SD, u32 R,
+                                                                          const u32* __restrict__ sidx,
+                                                                          u32* __restrict__ gid, u32* __restrict__ bad) {
+  const u64 t = u64(blockIdx.x) * 256 + threadIdx.x;
+  const u32 q = u32(t / kFlCap), i = u32(t % kFlCap);
+  if (q >= R) return;
+  const u64 n = rd[u64(q) * kFlSeg];
+  if (n > kFlCap) {
+    if (i == 0) atomicOr(bad, 1u);
+    return;
+  }
+  if (i < n) {
+    const u64 v = rd[u64(q) * kFlSeg + 1 + i];
+    gid[sidx[SD.d[q] + u32(v)]] = u32(v >> 32);
+  }
+}
 // Rank 0's leaves and those of a rank whose r-first positions are dense go out here in
 // position order (= id order) from the pre-words: coalesced stores, where k_dl_words'
 // record-order stores scatter (at 1 Gbase over 8 ranks rank 0 first-holds ~47 % of its strands'
@@ -689,25 +703,6 @@ struct FlL0 {
     s_off = u32(fl_offset(a.gonf, a.R, a.pp, a.me, nullptr));
     s_loff = u32(a.leaf[0]);
     if (blockIdx.x == 0) *a.guard = fl_guard(a.g4, a.R);
-  }
-  const u64 cc0 = u64(blockIdx.x) * kDC;
-  const u32 npp = u32((std::min<u64>(P.S - cc0, kDC) + 1) / 2);
-  {   // D: the ids of this chunk's not-first pairs whose first holder is another rank
-    const u64 j0 = cc0 / 2, j1 = j0 + npp;
-    for (u32 q = 0; q < a.R; ++q) {
-      const u64 n = a.rd[u64(q) * kFlSeg];
-      if (n > kFlCap) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(a.bad, 1u);
-        continue;
-      }
-      for (u64 i = threadIdx.x; i < n; i += kDThreads) {
-        const u64 v = a.rd[u64(q) * kFlSeg + 1 + i];
-        const u32 j = a.sidx[a.SD.d[q] + u32(v)];
-        if (j >= j0 && j < j1) a.gid[j] = u32(v >> 32);
-      }
-    }
-    __threadfence_block();   // (this workgroup reads them back: no device-scope fence, an L2 write-back)
-    __syncthreads();
   }
   dl_words_chunk(rec, idrec, offt, P, fb, nullptr, 0, s_dyn, [&](const u32* s_w, u32 n, u64 c0) {
     const u64 j0 = c0 / 2;
