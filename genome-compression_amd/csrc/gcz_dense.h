@@ -249,8 +249,20 @@ template <int L, bool kBases>
       if (s >= P.S) continue;
       u32 x = 0;
       bool ok = true;
-      if constexpr (kBases) {
-        const u32 sh = L % 4 == 0 ? 0u : u32(s * L) & 3u;   // (0: each base's byte a compile-time index)
+      if constexpr (kBases && L % 4 == 0) {
+        // four bases a word in registers: code = ((b >> 1) ^ (b >> 2)) & 3 maps A C G T (either
+        // case) to 0 1 2 3; the byte is ACGT iff (b | 0x20) is the lower-case letter of its code
+        // (one byte permute of "acgt" by the codes)
+#pragma unroll
+        for (int q = 0; q < L / 4; ++q) {
+          const u32 b = w[j][q];
+          const u32 k = ((b >> 1) ^ (b >> 2)) & 0x03030303u;
+          ok &= (b | 0x20202020u) == __builtin_amdgcn_perm(0u, 0x74676361u, k);
+          const u32 t = k | (k >> 6);
+          x |= ((t & 0xfu) | ((t >> 12) & 0xf0u)) << (8 * q);
+        }
+      } else if constexpr (kBases) {
+        const u32 sh = u32(s * L) & 3u;
 #pragma unroll
         for (int c = 0; c < L; ++c) {
           const u32 byte_i = sh + u32(c);
