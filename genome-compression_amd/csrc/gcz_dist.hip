@@ -1760,6 +1760,9 @@ namespace {
 // overflows all the same sends the attempt to the general schedule (status bit 4).
 u64 fl_cap(u64 p, int R) {
   const double m = double(p) / double(R);
+  // GCZ_FL_CAP_PERMILLE (tests): regions of that fraction of the mean, so that they overflow
+  if (const char* e = std::getenv("GCZ_FL_CAP_PERMILLE"))
+    if (const int pm = std::atoi(e); pm > 0) return std::max<u64>(1, u64(m * pm / 1000.0));
   return u64(m + 16.0 * std::sqrt(m) + 1024.0);
 }
 

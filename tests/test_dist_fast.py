@@ -140,6 +140,24 @@ def test_fast_discards_and_falls_back(world, shape, gcz):
         g.close()
 
 
+@pytest.mark.parametrize("world", [2, 8])
+def test_fast_owner_region_overflow_falls_back(world, gcz, monkeypatch):
+    """Owner regions of the keys' scatter (k_fl_scatter) too small for their records: the surplus
+    is dropped in bounds, status bit 4 reaches every rank in R1a, and the general schedule
+    builds the same tree as one device."""
+    monkeypatch.setenv("GCZ_FL_CAP_PERMILLE", "900")
+    rng = np.random.default_rng(300 + world)
+    bases = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, size=24_000_000 + 12 * 3)].copy()
+    ref = _single(gcz, bases)
+    g = _group(gcz, world)
+    try:
+        _build(gcz, g, bases)
+        assert _schedule(g) == "fast, discarded"
+        assert gcz.digest(g.tree()) == ref
+    finally:
+        g.close()
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_fast_declines_repetitive_and_iupac(world, gcz, manifest):
     """Inputs outside the fused schedule decide at the mid-build read (R1's status words):
