@@ -139,6 +139,40 @@ def test_exchange_budget_script_on_committed_probe():
         assert abs(2.5 / float(tot) - float(sp)) < 0.01
 
 
+def test_exchange_budget_overlap_model_on_r05_probes():
+    """The overlap model (scripts/budget.py, the fused schedule's dependencies replayed) on the
+    committed r05 probes: a projection never below the slowest rank's summed segments plus the
+    schedule's latencies, never above the additive model's, and faster links never slower; the
+    K2 bulk transfer starts at or after R1a's read."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("budget", os.path.join(REPO, "scripts", "budget.py"))
+    budget = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(budget)
+    for name in ("strong_virtual8.json", "strong_virtual4.json", "strong_virtual2.json", "weak_virtual8_uniform_8g.json"):
+        with open(os.path.join(REPO, "profiles", "r05", name)) as f:
+            d = json.loads(f.read().strip().splitlines()[-1])
+        tl = d["rank_timeline"]
+        R = len(tl)
+        logs = [r["exchange_log"] for r in tl]
+        names = [e[1] for e in logs[0]]
+        xb = budget.busiest_bytes(logs, R)
+        segs = [r["segments_ms"] for r in tl]
+        assert all(len(s) == 9 for s in segs), name
+        lat = (len(names) * budget.LAT_US + 2 * budget.SYNC_US) * 1e-3
+        floor = max(sum(s) for s in segs) + lat - budget.LAT_US * 1e-3   # (K2's latency overlaps)
+        prev = None
+        for B in (25.0, 50.0, 100.0):
+            T, ev = budget.overlap_model(segs, names, xb, B * 1e9)
+            T *= 1e3
+            additive = max(d["rank_kernel_ms"]) + sum(xb) / (B * 1e9) * 1e3 + lat
+            assert floor - 1e-6 <= T <= additive + 1e-6, (name, B, floor, T, additive)
+            if prev is not None:
+                assert T <= prev + 1e-9, (name, B)
+            prev = T
+            ends = {f: (t0, t1) for f, t0, t1 in ev}
+            assert ends["K2 (bulk)"][0] >= ends["R1a"][1] - 1e-12, name
+
+
 def _committed_lines(min_round=5):
     """(path, line) of every committed bench line under profiles/r05 and later (rounds 1-4 used
     a per-build byte model that charged distributed ranks for the whole genome's pairs)."""
