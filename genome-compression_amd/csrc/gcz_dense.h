@@ -71,10 +71,9 @@ struct PreKey {
   u32 Bc, K, lgR;
   u32 sh;
   u64 kmask, c1, c2;                 // the mix (PackedTab::mix's form)
-  __device__ __forceinline__ u64 mix(u64 x) const {
-    x ^= x >> sh; x = (x * c1) & kmask;
-    x ^= x >> sh; x = (x * c2) & kmask;
-    x ^= x >> sh;
+  __device__ __forceinline__ u64 mix(u64 x) const {   // (one multiply round: a bijection on K bits
+    x ^= x >> sh; x = (x * c1) & kmask;                // that spreads the owner and partition bits;
+    x ^= x >> sh;                                      // the owner's table mixes again on its own)
     return x;
   }
   __device__ __forceinline__ u64 label(u32 w) const {   // a child word -> code << 2 | m << 1 | t
