@@ -13,7 +13,8 @@
 // collective groups as the leaf-id exchange instead of after it:
 //
 //   R1a allgather: status words + layer-0 owner counts (right after the pack and the keys'
-//       count: the one mid-build host read -- the path, the keys' all-to-all sizes)
+//       one-pass scatter into owner regions, k_fl_scatter: the one mid-build host read --
+//       the path, the keys' all-to-all sizes)
 //   K2  keys to owners (code labels): one all-to-all on a second stream and communicator, so
 //       it runs beside the leaf level's sort and the next collectives (RCCL; the testing
 //       transports run it in line)
@@ -25,11 +26,12 @@
 //   R5  D: owners forward them to the other holders (fixed-capacity slots)
 //   R6  top words to rank 0 (gather)              R7  final vectors (allgather, host sync)
 //
-// Only then are the layer-0 nodes written, canonicalised with the global leaf ids (k_fl_l0).
-// Any surprise (a non-ACGT strand or repetitive data at R1, an owner that cannot take the
-// two-pass dedupe, a C/D slot overflow, a look-ahead that finds layer 1 not direct, an owner
-// bucket overflow) makes every rank discard the attempt together and run the general schedule
-// (gcz_group::build's exchange loop), which handles every input.
+// Only then are the layer-0 nodes written, canonicalised with the global leaf ids
+// (k_fl_words_l0).  Any surprise (a non-ACGT strand or repetitive data at R1a -- the scatter and
+// the dense sort then return at once on the device --, an owner region overflow, an owner that
+// cannot take the two-pass dedupe, a C/D slot overflow, a look-ahead that finds layer 1 not
+// direct, an owner bucket overflow) makes every rank discard the attempt together and run the
+// general schedule (gcz_group::build's exchange loop), which handles every input.
 #pragma once
 
 #include "gcz_dist_device.h"
