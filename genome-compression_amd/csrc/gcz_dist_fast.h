@@ -475,7 +475,10 @@ __device__ __forceinline__ void fs_load(const RecSrc& s, u32 tile, uint4 (&w)[kF
           const u64 need = firstP >= 63 ? ~0ull : ((1ull << (firstP + 1)) - 1);
           if (zm & need) {
             if (++polls > kFlSpinCap) {   // (bounded: a tile never waits forever)
-              if (lane == 0) s_bad = 1;
+              if (lane == 0) {   // (any block: the status word, OR-ed -- the last tile may be another's)
+                s_bad = 1;
+                atomicOr(reinterpret_cast<unsigned long long*>(&a.tot[R]), 256ull);
+              }
               break;
             }
             // back off (the polls are uncached loads: a tight spin of every waiting tile costs
@@ -512,7 +515,10 @@ __device__ __forceinline__ void fs_load(const RecSrc& s, u32 tile, uint4 (&w)[kF
         } else if (w2 == 5) {
           v = u64(a.h->dense_fail);
         }
-        a.tot[tid] = v;
+        if (w2 == 0)
+          atomicOr(reinterpret_cast<unsigned long long*>(&a.tot[tid]), (unsigned long long)v);   // (R1a's word: zeroed)
+        else
+          a.tot[tid] = v;
       }
     }
     // the owner-sorted copy out: R contiguous runs
