@@ -1054,6 +1054,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
     return GCZ_ERR_DEVICE;
   }
   c->stream = c->own_stream;
+  if (const char* t = std::getenv("GCZ_CANARY")) c->canary = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_TABLE")) c->force_wide = std::strcmp(t, "wide") == 0;
   if (const char* t = std::getenv("GCZ_NODE_CAP_SHIFT")) c->node_cap_shift = std::atoi(t);
   if (const char* t = std::getenv("GCZ_LEAF_CAP_LOG2")) c->leaf_cap_log2 = std::atoi(t);
@@ -1105,6 +1106,65 @@ void gcz_ctx_destroy(gcz_ctx* c) {
   if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
+}
+
+// The guard bands of GCZ_CANARY=1 (gcz_ctx::ensure): the buffers whose band is not all
+// kCanaryByte any more, named where they are context members.
+extern "C++" int gcz_canary_scan(gcz_ctx* c, std::string& out) {
+  if (!c->canary) return -1;
+  if (hipStreamSynchronize(c->stream) != hipSuccess) {
+    out += "stream synchronisation failed; ";
+    return 1;
+  }
+  static const std::pair<DevBuf gcz_ctx::*, const char*> names[] = {
+      {&gcz_ctx::wa, "wa"}, {&gcz_ctx::wb, "wb"}, {&gcz_ctx::grp, "grp"}, {&gcz_ctx::desc, "desc"},
+      {&gcz_ctx::tab, "tab"}, {&gcz_ctx::leaves_out, "leaves_out"}, {&gcz_ctx::nodes_out, "nodes_out"},
+      {&gcz_ctx::hdr, "hdr"}, {&gcz_ctx::input, "input"}, {&gcz_ctx::nf, "nf"}, {&gcz_ctx::multi, "multi"},
+      {&gcz_ctx::stats, "stats"}, {&gcz_ctx::bkt_key, "bkt_key"}, {&gcz_ctx::bkt_cnt, "bkt_cnt"},
+      {&gcz_ctx::bkt_off, "bkt_off"}, {&gcz_ctx::bkt_tmp, "bkt_tmp"}, {&gcz_ctx::bkt_rec2, "bkt_rec2"},
+      {&gcz_ctx::dl_pw, "dl_pw"}, {&gcz_ctx::dl_rec, "dl_rec"}, {&gcz_ctx::dl_idrec, "dl_idrec"},
+      {&gcz_ctx::dl_cnt, "dl_cnt"}, {&gcz_ctx::dl_off, "dl_off"}, {&gcz_ctx::dl_offt, "dl_offt"},
+      {&gcz_ctx::dl_fpg, "dl_fpg"}, {&gcz_ctx::dl_fb, "dl_fb"}, {&gcz_ctx::dl_wpre, "dl_wpre"},
+      {&gcz_ctx::dl_desc, "dl_desc"}, {&gcz_ctx::dl_fl, "dl_fl"}, {&gcz_ctx::dl_fo, "dl_fo"},
+      {&gcz_ctx::dl_lh, "dl_lh"}, {&gcz_ctx::dl_pb, "dl_pb"}, {&gcz_ctx::dl_pbs, "dl_pbs"},
+      {&gcz_ctx::dl_lower, "dl_lower"}, {&gcz_ctx::dl_pos, "dl_pos"}, {&gcz_ctx::dl_list, "dl_list"},
+      {&gcz_ctx::dl_gid, "dl_gid"}, {&gcz_ctx::dl_recv, "dl_recv"}, {&gcz_ctx::dl_stage, "dl_stage"},
+      {&gcz_ctx::dl_seg, "dl_seg"}, {&gcz_ctx::seg_w, "seg_w"}, {&gcz_ctx::seg_nf, "seg_nf"},
+      {&gcz_ctx::seg_mu, "seg_mu"}, {&gcz_ctx::seg_in, "seg_in"}, {&gcz_ctx::nf_list, "nf_list"},
+      {&gcz_ctx::tcount, "tcount"}, {&gcz_ctx::ftab, "ftab"}, {&gcz_ctx::fsid, "fsid"},
+      {&gcz_ctx::flkey, "flkey"}, {&gcz_ctx::flsid, "flsid"}};
+  std::vector<unsigned char> band(gcz_ctx::kCanaryBytes);
+  int bad = 0;
+  for (size_t k = 0; k < c->canary_bufs.size(); ++k) {
+    DevBuf* b = c->canary_bufs[k];
+    if (!b->ptr) continue;
+    if (hipMemcpy(band.data(), static_cast<char*>(b->ptr) + b->bytes, band.size(), hipMemcpyDeviceToHost) != hipSuccess) {
+      out += "band copy failed; ";
+      return bad + 1;
+    }
+    size_t first = band.size();
+    for (size_t j = 0; j < band.size(); ++j)
+      if (band[j] != gcz_ctx::kCanaryByte) {
+        first = j;
+        break;
+      }
+    if (first == band.size()) continue;
+    ++bad;
+    std::string name = "buffer #" + std::to_string(k) + " (not a context member: multi-rank / sort / ingest state)";
+    for (const auto& nm : names)
+      if (&(c->*(nm.first)) == b) name = nm.second;
+    out += name + " of " + std::to_string(b->bytes) + " B: guard byte +" + std::to_string(first) + " overwritten; ";
+  }
+  return bad;
+}
+
+int gcz_ctx_canary_check(gcz_ctx* c, char* msg, uint64_t cap) {
+  if (!c) return GCZ_ERR_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  std::string out;
+  const int n = gcz_canary_scan(c, out);
+  if (msg && cap) std::snprintf(msg, size_t(cap), "%s", out.c_str());
+  return n;
 }
 
 int gcz_ctx_set_stream(gcz_ctx* c, void* s) {

@@ -203,6 +203,8 @@ struct gcz_ingest_state; // gcz_ingest.hip
 // Builds of more than 2^29 - 1 strands on one device (gcz_ctx::build): virtual ranks
 // whose slices are concatenated into the context's arrays (gcz_dist.hip).
 int gcz_split_build(struct gcz_ctx* c, const void* d_bases, const gcz_host::u64* d_leaves, gcz_host::u64 S, int L);
+// GCZ_CANARY=1: the overwritten guard bands of c's buffers, described into `out` (gcz_build.hip)
+int gcz_canary_scan(struct gcz_ctx* c, std::string& out);
 
 struct gcz_ctx {
   int device = 0;
@@ -295,6 +297,13 @@ struct gcz_ctx {
     return code;
   }
 
+  // GCZ_CANARY=1 (testing): every ensure()d buffer is allocated kCanaryBytes longer and the
+  // extra bytes hold kCanaryByte; gcz_ctx_canary_check finds the bands a kernel overwrote (a GPU
+  // store past a buffer's size, which faults only past the allocation's granule otherwise).
+  static constexpr size_t kCanaryBytes = 4096;
+  static constexpr unsigned char kCanaryByte = 0xA5;
+  bool canary = false;
+  std::vector<gcz_host::DevBuf*> canary_bufs;
   int ensure(gcz_host::DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes && b.ptr) return GCZ_OK;
     if (b.ptr) {
@@ -302,8 +311,13 @@ struct gcz_ctx {
       HIP_TRY(hipFree(b.ptr));
       b.ptr = nullptr; b.bytes = 0;
     }
-    HIP_TRY(hipMalloc(&b.ptr, bytes ? bytes : 16));
-    b.bytes = bytes ? bytes : 16;
+    const size_t n = bytes ? bytes : 16;
+    HIP_TRY(hipMalloc(&b.ptr, n + (canary ? kCanaryBytes : 0)));
+    b.bytes = n;
+    if (canary) {
+      HIP_TRY(hipMemsetAsync(static_cast<char*>(b.ptr) + n, kCanaryByte, kCanaryBytes, stream));
+      if (std::find(canary_bufs.begin(), canary_bufs.end(), &b) == canary_bufs.end()) canary_bufs.push_back(&b);
+    }
     return GCZ_OK;
   }
   // ensure() that leaves last_error / info.status alone: for work on a side thread beside

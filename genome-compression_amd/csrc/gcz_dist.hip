@@ -169,12 +169,27 @@ std::vector<u64> gather_matrix(const std::vector<u64>& cnt, int R) {
   return M;
 }
 
-// All ranks in this process on one stream: exchanges are device copies.
+// All ranks in this process on one stream: exchanges are device copies.  GCZ_LOCAL_BULK=1 gives
+// it a second stream for bulk groups (RcclTransport's second stream and communicator): their
+// copies then run there, ordered only by the schedule's bulk events (gcz_group::x_group_bulk /
+// bulk_done), as K2 runs beside the build on RCCL.
 struct LocalTransport : Transport {
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;   // (GCZ_LOCAL_BULK=1)
+  hipStream_t cur = nullptr;       // the copies' stream: `stream`, or stream2 inside group_bulk
+  ~LocalTransport() override {
+    if (stream2) (void)hipStreamDestroy(stream2);
+  }
+  hipStream_t bulk_stream() override { return stream2; }
+  int group_bulk(const std::vector<XOp>& ops) override {
+    cur = stream2;
+    const int rc = group(ops);
+    cur = nullptr;
+    return rc;
+  }
   int copy(void* dst, const void* src, size_t bytes) {
     if (!bytes) return GCZ_OK;
-    if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream) != hipSuccess) {
+    if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, cur ? cur : stream) != hipSuccess) {
       err = "local transport copy failed";
       return GCZ_ERR_DEVICE;
     }
@@ -776,6 +791,45 @@ struct gcz_group {
     if (watch) watch->disarm();
     return GCZ_OK;
   }
+  // Every rank's flag, allgathered on the RCCL communicator under the watchdog (group creation):
+  // *all = 1 when each rank passed a nonzero `mine`.
+  int agree(const char* what, int mine, int* all) {
+    *all = 0;
+    auto* rt = static_cast<RcclTransport*>(tr);
+    hipStream_t st = ctx[0]->stream;
+    std::vector<int> h(size_t(world) + 1, 0);
+    h[0] = mine;
+    void* d = nullptr;
+    if (hipMalloc(&d, h.size() * 4) != hipSuccess) {
+      last_error = std::string(what) + ": hipMalloc failed";
+      return GCZ_ERR_DEVICE;
+    }
+    int rc = hipMemcpyAsync(d, h.data(), 4, hipMemcpyHostToDevice, st) == hipSuccess ? GCZ_OK : GCZ_ERR_DEVICE;
+    if (!rc) {
+      watch->begin(-1, what);
+      ncclComm_t c = rt->comm.load();
+      if (!c || rccl().AllGather(d, static_cast<int*>(d) + 1, 4, ncclUint8, c, st) != ncclSuccess) rc = GCZ_ERR_DEVICE;
+      watch->end(st);
+      if (!rc && hipMemcpyAsync(h.data() + 1, static_cast<int*>(d) + 1, size_t(world) * 4, hipMemcpyDeviceToHost, st) !=
+                     hipSuccess)
+        rc = GCZ_ERR_DEVICE;
+      if (hipStreamSynchronize(st) != hipSuccess) rc = GCZ_ERR_DEVICE;
+      if (watch->fired) {
+        last_error = watch->msg;
+        rc = GCZ_ERR_DEVICE;
+      }
+      watch->disarm();
+    }
+    (void)hipFree(d);
+    if (rc) {
+      if (last_error.empty()) last_error = std::string(what) + ": allgather failed";
+      return rc;
+    }
+    int a = 1;
+    for (int r = 0; r < world; ++r) a &= h[size_t(r) + 1] != 0 ? 1 : 0;
+    *all = a;
+    return GCZ_OK;
+  }
   std::vector<u64> per_local(const std::function<u64(int)>& f) const {
     std::vector<u64> v;
     for (int r : rank) v.push_back(f(r));
@@ -822,13 +876,16 @@ struct gcz_group {
     bulk_marked = true;
     return GCZ_OK;
   }
-  int x_group_bulk(const char* name, const std::vector<Transport::XOp>& ops) {
+  // (name: in line on the build's stream; name2: on the second stream -- the log says which ran)
+  bool bulk_pending = false;   // a bulk group is queued that bulk_done() has not ordered yet
+  int x_group_bulk(const char* name, const char* name2, const std::vector<Transport::XOp>& ops) {
     hipStream_t bs = tr->bulk_stream();
     if (bs) {
       if (!bulk_marked)
         if (int rc = bulk_mark()) return rc;
       bulk_marked = false;
       if (hipStreamWaitEvent(bs, ev_bulk_in, 0) != hipSuccess) return dev_fail("bulk stream order");
+      name = name2;
     }
     const int R = world;
     auto tot = [&](int me, bool sent) {
@@ -840,12 +897,14 @@ struct gcz_group {
     };
     xbegin(name, per_local([&](int me) { return tot(me, true); }), per_local([&](int me) { return tot(me, false); }));
     const int rc = xend(tr->group_bulk(ops), bs);
-    if (!rc && bs && hipEventRecord(ev_bulk_out, bs) != hipSuccess) return dev_fail("bulk stream order");
+    if (bs && hipEventRecord(ev_bulk_out, bs) != hipSuccess) return dev_fail("bulk stream order");
+    bulk_pending = bs != nullptr;
     return rc;
   }
   int bulk_done() {
     hipStream_t bs = tr->bulk_stream();
     if (bs && hipStreamWaitEvent(ctx[0]->stream, ev_bulk_out, 0) != hipSuccess) return dev_fail("bulk stream order");
+    bulk_pending = false;
     return GCZ_OK;
   }
   int x_allgather(const char* name, size_t bytes, const std::vector<const void*>& s, const std::vector<void*>& r) {
@@ -899,6 +958,13 @@ struct gcz_group {
     // thread would otherwise take the build for hung and end the process after its grace period
     // (a failing rank's peers are bounded by their own watchdogs)
     if (watch) watch->disarm();
+    // a bulk group still queued on the second stream is ordered before whatever the build's
+    // stream runs next, so every later sync of that stream (the next build's buffer growth, the
+    // teardown) also covers it
+    if (bulk_pending) {
+      bulk_pending = false;
+      if (ev_bulk_out) (void)hipStreamWaitEvent(ctx[0]->stream, ev_bulk_out, 0);
+    }
     for (gcz_ctx* c : ctx) c->fail(code, "group build", what.c_str());
     return code;
   }
@@ -945,6 +1011,10 @@ struct gcz_group {
   int build_fast(const std::vector<const unsigned char*>& bases, const u64* const* d_leaves, int L,
                  const std::vector<u64>& leaf_cap, bool* taken);
   int fast_mode = std::getenv("GCZ_DIST_FAST") ? std::atoi(std::getenv("GCZ_DIST_FAST")) : 1;   // 0: off
+  // k_fl_scatter's look-back polls before a tile gives up (GCZ_FL_SPIN_CAP, testing; 0: every
+  // tile after the first gives up at once -- the attempt is discarded on every rank)
+  u32 fl_spin_cap = std::getenv("GCZ_FL_SPIN_CAP") ? u32(std::strtoul(std::getenv("GCZ_FL_SPIN_CAP"), nullptr, 10))
+                                                   : kFlSpinCap;
   hipEvent_t ev_mid = nullptr;   // the fused schedule's mid-build read (status, counts)
   FlPairs fl_pairs{};            // ... and every rank's layer-0 pairs
   RecSrc fl_rs[kMaxRanks] = {};  // ... each local rank's layer-0 record source
@@ -1969,6 +2039,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     a.gmul = d.gmul.as<unsigned char>();
     a.ddesc = d.ddesc.as<u64>();
     a.count_out = &cx->hdr.as<Header>()->count[kLayerSlot];
+    a.spin_cap = fl_spin_cap;
     ProfScope ps_(cx, KID_DIST);
     hipLaunchKernelGGL(k_fl_scatter, dim3(std::min<u32>(nb, kFsGrid)), dim3(kFsThreads), 0, cx->stream, fl_rs[i], a);
     G_HIP(hipGetLastError());
@@ -2023,9 +2094,17 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     if (st) return GCZ_OK;   // every rank decides alike from the same words: the general schedule
   }
   auto recvd = [&](int r) { u64 t = 0; for (int q = 0; q < R; ++q) t += M[size_t(q) * R + r]; return t; };
+  // every rank decides for every owner from the gathered counts: an owner whose records do not
+  // take the two-pass dedupe or whose key table would not pack sends EVERY rank to the general
+  // schedule together (a rank that failed alone would leave its peers waiting in K2)
   std::vector<Bkt2Plan> b2(R);
-  for (int s = 0; s < R; ++s)
-    if (!owner_two_pass_plan(recvd(s), key_bits, b2[s])) return GCZ_OK;   // (every rank sees every owner's size)
+  for (int s = 0; s < R; ++s) {
+    const u64 nr = recvd(s);
+    if (!owner_two_pass_plan(nr, key_bits, b2[s])) return GCZ_OK;
+    if (!plan_table(nullptr, std::max<u64>(256, next_pow2(2 * nr)), key_bits, std::max<u64>(nr, 2), child_bits, true, 0)
+             .packed)
+      return GCZ_OK;
+  }
   auto displ_recv = [&](int r) {   // source segments of owner r's receive buffer
     Displ Dd{};
     u64 o = 0;
@@ -2065,7 +2144,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     const u64 nr = recvd(r);
     const u64 cap = std::max<u64>(256, next_pow2(2 * nr));
     const LevelTab lt = plan_table(d.owntab.ptr, cap, key_bits, std::max<u64>(nr, 2), child_bits, true, 0);
-    if (!lt.packed) return fail(GCZ_ERR_CAPACITY, "fused schedule: owner keys do not pack");
+    if (!lt.packed) return fail(GCZ_ERR_CAPACITY, "fused schedule: owner keys do not pack");   // (decided above for every owner)
     Bkt2Plan& bp = b2[r];
     bp.T = lt.pt;
     const u64 nfine = (u64(1) << bp.b1) * bp.nslice;
@@ -2127,7 +2206,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     }
     hipEvent_t e0{};
     ctx[0]->prof_begin(KID_EXCHANGE, e0);
-    G_RC(x_group_bulk("K2 [bulk] layer-0 keys to owners", ops));
+    G_RC(x_group_bulk("K2 [bulk] layer-0 keys to owners", "K2 [bulk, second stream] layer-0 keys to owners", ops));
     ctx[0]->prof_end(KID_EXCHANGE, e0);
   }
   // ---- R1b: the presence bitmaps
@@ -3128,6 +3207,12 @@ int gcz_group_create_local(int device, int world, gcz_group** out) {
     g->rank.push_back(r);
   }
   t->stream = g->ctx[0]->stream;
+  if (const char* e = std::getenv("GCZ_LOCAL_BULK"); e && std::atoi(e) != 0 && world > 1)
+    if (hipStreamCreateWithFlags(&t->stream2, hipStreamNonBlocking) != hipSuccess) {
+      t->stream2 = nullptr;
+      gcz_group_destroy(g);
+      return GCZ_ERR_DEVICE;
+    }
   *out = g;
   return GCZ_OK;
 }
@@ -3155,21 +3240,51 @@ int gcz_group_create_rccl(gcz_ctx* ctx, int rank, int world, const void* unique_
     return GCZ_ERR_DEVICE;
   }
   t->comm.store(comm);
-  // the bulk communicator and stream (every rank makes the same call; without ncclCommSplit,
-  // bulk groups run on the first communicator and stream)
-  if (a.CommSplit && world > 1) {
-    ncclComm_t c2 = nullptr;
-    if (a.CommSplit(comm, 0, rank, &c2, nullptr) == ncclSuccess && c2) {
-      if (hipStreamCreateWithFlags(&t->stream2, hipStreamNonBlocking) == hipSuccess) t->comm2.store(c2);
-      else (void)a.CommDestroy(c2);
-    }
-  }
   auto* g = new gcz_group();
   g->world = world;
   g->tr = t;
   g->ctx.push_back(ctx);
   g->rank.push_back(rank);
   g->watch.reset(new gcz_group::Watch(t, ctx->device, rank));
+  // The bulk communicator and stream, agreed by every rank: ncclCommSplit is collective over
+  // `comm`, so it runs only where every rank wants it (GCZ_FL_BULK=0 on any rank, or an RCCL
+  // without the entry point: none splits), and comm2 is kept only where every rank got both the
+  // communicator and the stream -- else every rank drops it and bulk groups run in line on `comm`
+  // and the build's stream, the path the tests cover.  Both agreements are allgathers on `comm`
+  // under the watchdog (a peer that never arrives aborts the communicator after
+  // GCZ_DIST_TIMEOUT_S, and creation fails).  (Also at world 1, where no build uses it: the
+  // one-GPU tests run the split, the agreement and the second stream on the real library.)
+  {
+    const char* eb = std::getenv("GCZ_FL_BULK");
+    const int want = a.CommSplit && !(eb && std::atoi(eb) == 0) ? 1 : 0;
+    int all_want = 0;
+    int rc = g->agree("group creation: bulk communicator wanted", want, &all_want);
+    ncclComm_t c2 = nullptr;
+    int have = 0;
+    if (!rc && all_want) {
+      g->watch->begin(-1, "group creation: ncclCommSplit");
+      if (a.CommSplit(comm, 0, rank, &c2, nullptr) == ncclSuccess && c2)
+        have = hipStreamCreateWithFlags(&t->stream2, hipStreamNonBlocking) == hipSuccess ? 1 : 0;
+      g->watch->disarm();
+      int all_have = 0;
+      rc = g->agree("group creation: bulk communicator ready", have, &all_have);
+      if (!rc && all_have) {
+        t->comm2.store(c2);
+        c2 = nullptr;
+      }
+    }
+    if (c2) (void)a.CommDestroy(c2);
+    if (!t->comm2.load() && t->stream2) {
+      (void)hipStreamDestroy(t->stream2);
+      t->stream2 = nullptr;
+    }
+    if (rc || g->watch->fired) {
+      ctx->last_error = "group creation: " + (g->last_error.empty() ? std::string("the bulk communicator agreement failed")
+                                                                    : g->last_error);
+      gcz_group_destroy(g);
+      return GCZ_ERR_DEVICE;
+    }
+  }
   *out = g;
   return GCZ_OK;
 }
@@ -3240,11 +3355,13 @@ int gcz_group_create_shm(gcz_ctx* ctx, int rank, int world, const char* name, ui
 
 void gcz_group_destroy(gcz_group* g) {
   if (!g) return;
-  for (hipEvent_t e : {g->ev_mid, g->ev_bulk_in, g->ev_bulk_out})
-    if (e) (void)hipEventDestroy(e);
   if (g->watch && !g->watch->fired) g->watch->begin(-1, "teardown (collectives a failed build left queued)");
   for (gcz_ctx* c : g->ctx) (void)hipStreamSynchronize(c->stream);
+  if (g->tr)   // (a bulk group a failed build left on the second stream, under the same watchdog)
+    if (hipStream_t bs = g->tr->bulk_stream()) (void)hipStreamSynchronize(bs);
   g->watch.reset();
+  for (hipEvent_t e : {g->ev_mid, g->ev_bulk_in, g->ev_bulk_out})   // (after the streams that wait on them)
+    if (e) (void)hipEventDestroy(e);
   delete g->tr;
   if (g->owns_ctx) {
     // virtual ranks borrowed rank 0's stream (or, split builds, the parent context's)
@@ -3318,6 +3435,24 @@ int gcz_dist_gather_plan(int world, int me, const uint64_t* cnt, uint64_t elem, 
 int gcz_group_n_local(const gcz_group* g) { return g ? int(g->ctx.size()) : 0; }
 int gcz_group_rank(const gcz_group* g, int i) { return g && i >= 0 && i < int(g->ctx.size()) ? g->rank[i] : -1; }
 int gcz_group_world(const gcz_group* g) { return g ? g->world : 0; }
+int gcz_group_canary_check(gcz_group* g, char* msg, uint64_t cap) {
+  if (!g) return GCZ_ERR_ARG;
+  if (hipSetDevice(g->ctx[0]->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  if (g->tr)
+    if (hipStream_t bs = g->tr->bulk_stream()) (void)hipStreamSynchronize(bs);
+  std::string out;
+  int n = 0;
+  for (size_t i = 0; i < g->ctx.size(); ++i) {
+    std::string o;
+    const int k = gcz_canary_scan(g->ctx[i], o);
+    if (k < 0) return -1;
+    if (k) out += "local rank " + std::to_string(i) + ": " + o;
+    n += k;
+  }
+  if (msg && cap) std::snprintf(msg, size_t(cap), "%s", out.c_str());
+  return n;
+}
+int gcz_group_has_bulk(gcz_group* g) { return g && g->tr && g->tr->bulk_stream() ? 1 : 0; }
 gcz_ctx* gcz_group_ctx(gcz_group* g, int i) { return g && i >= 0 && i < int(g->ctx.size()) ? g->ctx[i] : nullptr; }
 const char* gcz_group_last_error(const gcz_group* g) { return g ? g->last_error.c_str() : "null group"; }
 

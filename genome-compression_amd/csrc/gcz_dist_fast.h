@@ -312,6 +312,7 @@ struct FlScatter {
   unsigned char* gmul;
   u64* ddesc;
   u64* count_out;
+  u32 spin_cap;            // look-back polls before a tile gives up (kFlSpinCap; 0: at once, testing)
 };
 constexpr u32 kFlSpinCap = 1u << 22;   // look-back polls before a tile gives up (status bit 8)
 constexpr int kFsThreads = 512, kFsItems = kTile / kFsThreads;   // 16 consecutive pairs a thread
@@ -473,8 +474,8 @@ __device__ __forceinline__ void fs_load(const RecSrc& s, u32 tile, uint4 (&w)[kF
           const u64 zm = __ballot(idx >= 0 && st == 0);
           const int firstP = pm ? __ffsll((long long)pm) - 1 : 64;
           const u64 need = firstP >= 63 ? ~0ull : ((1ull << (firstP + 1)) - 1);
-          if (zm & need) {
-            if (++polls > kFlSpinCap) {   // (bounded: a tile never waits forever)
+          if ((zm & need) || a.spin_cap == 0) {
+            if (++polls > a.spin_cap) {   // (bounded: a tile never waits forever)
               if (lane == 0) {   // (any block: the status word, OR-ed -- the last tile may be another's)
                 s_bad = 1;
                 atomicOr(reinterpret_cast<unsigned long long*>(&a.tot[R]), 256ull);

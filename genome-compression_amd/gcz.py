@@ -117,6 +117,9 @@ _SIGS = {
     "gcz_group_create_local": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
     "gcz_group_destroy": (None, [_P]),
     "gcz_group_world": (ctypes.c_int, [_P]),
+    "gcz_group_has_bulk": (ctypes.c_int, [_P]),
+    "gcz_ctx_canary_check": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_uint64]),
+    "gcz_group_canary_check": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_uint64]),
     "gcz_group_n_local": (ctypes.c_int, [_P]),
     "gcz_group_rank": (ctypes.c_int, [_P, ctypes.c_int]),
     "gcz_group_ctx": (_P, [_P, ctypes.c_int]),
@@ -342,6 +345,14 @@ def digest(tree: Tree) -> dict:
 
 
 # ---- device context -----------------------------------------------------------
+def _canary(fn, h) -> str:
+    msg = ctypes.create_string_buffer(2048)
+    n = fn(h, msg, len(msg))
+    if n < 0:
+        raise GczError(n, "canary check: the context was created without GCZ_CANARY=1")
+    return msg.value.decode() if n else ""
+
+
 class DeviceBuffer:
     """Device allocation made through libgcz (no other GPU runtime needed)."""
 
@@ -374,6 +385,11 @@ class Context:
         if rc != GCZ_OK:
             raise GczError(rc, f"gcz_ctx_create(device={device}) failed")
         self._h = h
+
+    def canary_check(self) -> str:
+        """'' when every guard band of this context's buffers is intact (GCZ_CANARY=1 at
+        creation), else a description of the overwritten ones."""
+        return _canary(_lib.gcz_ctx_canary_check, self._h)
 
     def close(self):
         if getattr(self, "_h", None) and getattr(self, "_owned", True):
@@ -580,6 +596,16 @@ class Group:
     @property
     def n_local(self):
         return _lib.gcz_group_n_local(self._h)
+
+    @property
+    def has_bulk(self) -> bool:
+        """Bulk groups run on a second stream (gcz_group_has_bulk)."""
+        return bool(_lib.gcz_group_has_bulk(self._h))
+
+    def canary_check(self) -> str:
+        """'' when every guard band of every local rank's buffers is intact (GCZ_CANARY=1 at
+        creation), else a description of the overwritten ones."""
+        return _canary(_lib.gcz_group_canary_check, self._h)
 
     def rank(self, i=0):
         return _lib.gcz_group_rank(self._h, i)

@@ -249,6 +249,17 @@ GCZ_API int gcz_group_n_local(const gcz_group *g);          /* ranks driven by t
 GCZ_API int gcz_group_rank(const gcz_group *g, int local);
 GCZ_API gcz_ctx *gcz_group_ctx(gcz_group *g, int local);
 GCZ_API const char *gcz_group_last_error(const gcz_group *g);
+/* 1 when the group runs bulk groups (the fused schedule's layer-0 key all-to-all) on a second
+ * stream: RCCL groups whose ranks all created the split communicator and its stream (agreed at
+ * creation; GCZ_FL_BULK=0 on any rank turns it off everywhere), local groups with
+ * GCZ_LOCAL_BULK=1 (testing). */
+GCZ_API int gcz_group_has_bulk(gcz_group *g);
+/* GCZ_CANARY=1 at context creation (testing): every device buffer the library sizes ends in a
+ * 4 KB guard band of 0xA5 bytes; the checks synchronise and return the number of buffers whose
+ * band was overwritten (an out-of-bounds store), describing the first ones in msg (may be
+ * NULL), or -1 when the context was created without canaries. */
+GCZ_API int gcz_ctx_canary_check(gcz_ctx *ctx, char *msg, uint64_t cap);
+GCZ_API int gcz_group_canary_check(gcz_group *g, char *msg, uint64_t cap);
 /* The exchanges of the group's last build, in order (every rank runs the same sequence):
  * returns their number; for i < cap, rec[4 i ..] = {sequence number, bytes local rank `local`
  * sent to other ranks, bytes it received from them, host enqueue time in us after the build

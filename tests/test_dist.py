@@ -188,6 +188,8 @@ def test_dist_rccl_world1(gcz, manifest):
     ctx = gcz.Context(0)
     try:
         g = gcz.Group.rccl(ctx, 0, 1, gcz.dist_unique_id())
+        # the bulk communicator (ncclCommSplit), its stream and the two creation agreements ran
+        assert g.has_bulk
         for name in ("corpus/chmpxx", "corpus/merged"):
             case = manifest[name]
             kind, payload, L = case_input(case, gcz)
@@ -198,6 +200,20 @@ def test_dist_rccl_world1(gcz, manifest):
             finally:
                 buf.free()
             assert compare_digest(gcz.digest(g.tree()), case["expect"]) == {}
+        g.close()
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_dist_rccl_bulk_kill_switch(gcz, monkeypatch):
+    """GCZ_FL_BULK=0: the creation agreement finds a rank that does not want the bulk
+    communicator, so no rank splits and bulk groups run in line (the path every test covers)."""
+    monkeypatch.setenv("GCZ_FL_BULK", "0")
+    ctx = gcz.Context(0)
+    try:
+        g = gcz.Group.rccl(ctx, 0, 1, gcz.dist_unique_id())
+        assert not g.has_bulk
         g.close()
     finally:
         ctx.close()

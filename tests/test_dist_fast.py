@@ -211,3 +211,115 @@ def test_fast_equals_general_symmetric_variants(world, gcz):
         assert gcz.digest(g.tree()) == ref
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_fast_schedule_bulk_second_stream(world, gcz, uniform_100m):
+    """K2 on a real second stream (GCZ_LOCAL_BULK=1: the local transport's bulk copies run
+    there, ordered only by the schedule's ev_bulk_in / ev_bulk_out, as RCCL's communicator 2
+    runs them): the tree equals the reference's, and a discarded attempt after K2 (a copied
+    block: layer 1 not direct) falls back to the same tree as one device."""
+    bases, exp = uniform_100m
+    g = _group(gcz, world, {"GCZ_LOCAL_BULK": "1"})
+    try:
+        assert g.has_bulk
+        for _ in range(2):   # (the second build reuses the events and buffers)
+            _build(gcz, g, bases)
+            names = [e["name"] for e in g.exchange_log(0)]
+            assert _schedule(g) == "fast" and len(names) == 9, names
+            assert any("second stream" in n for n in names), names
+            assert compare_digest(gcz.digest(g.tree()), exp) == {}
+        rng = np.random.default_rng(500 + world)
+        rep = _with_repeats(rng, 24_000_000, 12, 16_384, False)
+        _build(gcz, g, rep)
+        assert _schedule(g) == "fast, discarded"
+        assert gcz.digest(g.tree()) == _single(gcz, rep)
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("cap", ["0", "1"])
+def test_fast_lookback_give_up(world, cap, gcz, uniform_100m, monkeypatch):
+    """k_fl_scatter's look-back gives up (GCZ_FL_SPIN_CAP; 0: every tile after the first at
+    once): the tile publishes a partial prefix and sets status bit 256, the records it misplaces
+    stay inside their regions, every rank runs the general schedule and the tree equals the
+    reference's.  cap 1: whichever tiles happen to give up -- the same tree either way."""
+    monkeypatch.setenv("GCZ_FL_SPIN_CAP", cap)
+    bases, exp = uniform_100m
+    g = _group(gcz, world)
+    try:
+        _build(gcz, g, bases)
+        if cap == "0":
+            assert _schedule(g) == "fast, discarded"
+        assert compare_digest(gcz.digest(g.tree()), exp) == {}
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("L", [8, 9, 11])
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_fast_equals_general_other_L(L, world, gcz):
+    """Strand lengths other than 12: Bc = 2L - 1 code bits, the 6-byte record's key bits, the
+    relay slots' bound (canonical orbits of 2L-bit codes) and small bucket words -- fused
+    schedule, general schedule and one device byte-identical."""
+    rng = np.random.default_rng(1000 * L + world)
+    nbases = 12_000_000 // L * L + L * 5
+    bases = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, size=nbases)].copy()
+    ref = _single(gcz, bases, L)
+    got = {}
+    for mode in ("1", "0"):
+        g = _group(gcz, world, {"GCZ_DIST_FAST": mode})
+        try:
+            _build(gcz, g, bases, L)
+            got[mode] = (_schedule(g), gcz.digest(g.tree()))
+        finally:
+            g.close()
+    assert got["0"][0] == "general"
+    assert got["1"][0] == "fast" if L >= 9 else got["1"][0] in ("fast", "fast, discarded"), got["1"][0]
+    assert got["1"][1] == ref, (L, world)
+    assert got["0"][1] == ref, (L, world)
+
+
+@pytest.mark.parametrize("world,tail", [(2, "9"), (2, None), (3, "9"), (8, "9"), (8, None)])
+def test_fast_schedule_guard_bands(world, tail, gcz, uniform_100m, monkeypatch):
+    """No kernel of the fused schedule stores past a buffer (GCZ_CANARY=1: a 4 KB guard band
+    after every buffer the library sizes, checked after each build), at the shape of round 5's
+    illegal accesses (world 2, GCZ_DIST_TAIL_LOG2=9: rank 0's level buffers sized by its own
+    3.5 M strands instead of the whole genome) and around it; first build of fresh contexts
+    (every buffer allocated by that build) and a second one."""
+    if tail:
+        monkeypatch.setenv("GCZ_DIST_TAIL_LOG2", tail)
+    bases, exp = uniform_100m
+    g = _group(gcz, world, {"GCZ_CANARY": "1"})
+    try:
+        for _ in range(2):
+            _build(gcz, g, bases)
+            assert _schedule(g) == "fast"
+            assert g.canary_check() == ""
+        assert compare_digest(gcz.digest(g.tree()), exp) == {}
+        rng = np.random.default_rng(77)
+        rep = _with_repeats(rng, 24_000_000, 12, 16_384, True)   # discarded: the general schedule too
+        _build(gcz, g, rep)
+        assert g.canary_check() == ""
+    finally:
+        g.close()
+
+
+def test_single_device_guard_bands(gcz, manifest):
+    """The one-device build (dense leaf level, bucketed layer 0, direct subtrees, tail; tandem:
+    the hash-table levels with the block pre-dedupe) stores nothing past its buffers."""
+    os.environ["GCZ_CANARY"] = "1"
+    try:
+        c = gcz.Context(0)
+    finally:
+        del os.environ["GCZ_CANARY"]
+    try:
+        for name in ("synth/uniform_100000003", "synth/tandem_100000000", "corpus/merged"):
+            case = manifest[name]
+            kind, payload, L = case_input(case, gcz)
+            c.build_fasta(payload, L)
+            assert c.canary_check() == "", name
+            assert compare_digest(gcz.digest(c.tree()), case["expect"]) == {}, name
+    finally:
+        c.close()
