@@ -1167,6 +1167,24 @@ int gcz_ctx_canary_check(gcz_ctx* c, char* msg, uint64_t cap) {
   return n;
 }
 
+// The check itself (tests): a scratch buffer of 1000 bytes sized by ensure(), one byte stored
+// right past it; returns 0 when the scan reports exactly that buffer.
+int gcz_ctx_canary_selftest(gcz_ctx* c) {
+  if (!c) return GCZ_ERR_ARG;
+  if (!c->canary) return -1;
+  if (hipSetDevice(c->device) != hipSuccess) return GCZ_ERR_DEVICE;
+  DevBuf b;
+  if (c->ensure(b, 1000)) return GCZ_ERR_DEVICE;
+  std::string out;
+  int rc = gcz_canary_scan(c, out) == 0 ? 0 : 1;   // (nothing overwritten yet)
+  if (!rc && hipMemsetAsync(static_cast<char*>(b.ptr) + 1000, 0x5A, 1, c->stream) != hipSuccess) rc = 2;
+  out.clear();
+  if (!rc) rc = gcz_canary_scan(c, out) == 1 && out.find("+0 overwritten") != std::string::npos ? 0 : 3;
+  c->canary_bufs.erase(std::remove(c->canary_bufs.begin(), c->canary_bufs.end(), &b), c->canary_bufs.end());
+  (void)hipFree(b.ptr);
+  return rc;
+}
+
 int gcz_ctx_set_stream(gcz_ctx* c, void* s) {
   if (!c) return GCZ_ERR_ARG;
   c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;

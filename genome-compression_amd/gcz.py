@@ -120,6 +120,7 @@ _SIGS = {
     "gcz_group_has_bulk": (ctypes.c_int, [_P]),
     "gcz_ctx_canary_check": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_uint64]),
     "gcz_group_canary_check": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_uint64]),
+    "gcz_ctx_canary_selftest": (ctypes.c_int, [_P]),
     "gcz_group_n_local": (ctypes.c_int, [_P]),
     "gcz_group_rank": (ctypes.c_int, [_P, ctypes.c_int]),
     "gcz_group_ctx": (_P, [_P, ctypes.c_int]),

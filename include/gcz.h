@@ -260,6 +260,8 @@ GCZ_API int gcz_group_has_bulk(gcz_group *g);
  * NULL), or -1 when the context was created without canaries. */
 GCZ_API int gcz_ctx_canary_check(gcz_ctx *ctx, char *msg, uint64_t cap);
 GCZ_API int gcz_group_canary_check(gcz_group *g, char *msg, uint64_t cap);
+/* The guard-band check finds a planted store one byte past a 1000-byte buffer: 0 = it does. */
+GCZ_API int gcz_ctx_canary_selftest(gcz_ctx *ctx);
 /* The exchanges of the group's last build, in order (every rank runs the same sequence):
  * returns their number; for i < cap, rec[4 i ..] = {sequence number, bytes local rank `local`
  * sent to other ranks, bytes it received from them, host enqueue time in us after the build

@@ -315,6 +315,7 @@ def test_single_device_guard_bands(gcz, manifest):
     finally:
         del os.environ["GCZ_CANARY"]
     try:
+        assert gcz._lib.gcz_ctx_canary_selftest(c._h) == 0   # (the check sees a planted overwrite)
         for name in ("synth/uniform_100000003", "synth/tandem_100000000", "corpus/merged"):
             case = manifest[name]
             kind, payload, L = case_input(case, gcz)
