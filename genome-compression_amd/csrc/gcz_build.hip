@@ -203,8 +203,10 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
   P.cmask = u32((1ull << (2 * L)) - 1);
   const u32 cbits = dense_code_bits(L);
   P.hmask = u32((1ull << cbits) - 1);
-  // 1024 buckets: LDS tables of RB = 2^14 codes (64 KB, two workgroups per CU) at L = 12
-  P.NB = u32(std::min<u64>(kDNBMax, 1ull << cbits));
+  // dense_nb buckets (GCZ_DENSE_NB; a power of two <= kDNBMax), at least enough that a bucket's
+  // LDS table holds at most 2^14 codes (k_dl_first's 16 codes per thread)
+  P.NB = u32(std::min<u64>(std::max<u64>({u64(dense_nb), (1ull << cbits) >> 14, 1}), 1ull << cbits));
+  P.NB = std::min<u32>(1u << log2_exact(P.NB), kDNBMax);
   P.IB = cbits - log2_exact(P.NB);
   const u32 kmul = 0x5bd1e995u;                     // odd: a bijection mod 4^L
   u32 Ki = kmul;
@@ -1055,6 +1057,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   }
   c->stream = c->own_stream;
   if (const char* t = std::getenv("GCZ_CANARY")) c->canary = std::atoi(t) != 0;
+  if (const char* t = std::getenv("GCZ_DENSE_NB")) c->dense_nb = u32(std::strtoul(t, nullptr, 10));
   if (const char* t = std::getenv("GCZ_TABLE")) c->force_wide = std::strcmp(t, "wide") == 0;
   if (const char* t = std::getenv("GCZ_NODE_CAP_SHIFT")) c->node_cap_shift = std::atoi(t);
   if (const char* t = std::getenv("GCZ_LEAF_CAP_LOG2")) c->leaf_cap_log2 = std::atoi(t);

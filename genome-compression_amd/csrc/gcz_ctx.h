@@ -256,6 +256,7 @@ struct gcz_ctx {
   int dense_mode = 1;        // dense leaf level (gcz_dense.h): 0 off, 1 on large pure-ACGT inputs, 2 any size (GCZ_DENSE)
   gcz_host::u64 dense_min = 1ull << 21;   // ... from this many strands (mode 1)
   bool dense_used = false;   // the last build's leaf level ran dense
+  gcz_host::u32 dense_nb = gcz_dev::kDNBMax;   // ... its code buckets (GCZ_DENSE_NB, testing)
   bool use_graph = true;     // small builds as a replayed HIP graph       (GCZ_GRAPH=0 disables)
   bool use_fused = true;     // small builds: two launches per node level  (GCZ_FUSED=0 disables)
   int small_cap_shift = 2;   // ... and tables 2^this times the usual size: short probe chains (GCZ_SMALL_CAP_SHIFT)
