@@ -74,6 +74,12 @@ def load_gcz():
     return mod
 
 
+def dense_buckets(C):
+    """The dense leaf level's code buckets for a code space of C codes (gcz_ctx::dense_nb = 512,
+    at least C / 2^14: a bucket's LDS table holds <= 2^14 codes)."""
+    return min(C, max(512, C >> 14))
+
+
 def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None, bucketed_pairs=0, two_pass=False,
                       launches=None):
     """Algorithmic HBM bytes of all launches of `kernel` in one build:
@@ -116,7 +122,7 @@ def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None, bu
     # dense leaf level (pure ACGT, L <= 12; gcz_dense.h): streamed bytes per pass
     nch = (S + 32767) // 32768
     C = 2 ** (2 * L - 1)            # the code space: canonical codes (top bit 0, gcz_dense.h)
-    NB = min(1024, C)
+    NB = dense_buckets(C)
     if kernel == "dl_pack":         # bases in, pre-word out, per-chunk bucket counts
         return S * L + 4 * S + 4 * NB * nch
     if kernel == "dl_scan":         # exclusive scan of the count matrix
@@ -155,7 +161,7 @@ def dist_rank_bytes(kernel, L, Sr, r, R, c_r, u_r, n_leaves):
     without HBM work of their own (exchange, tail) count 0."""
     pr = (Sr + 1) // 2
     C = 2 ** (2 * L - 1)
-    NB = min(1024, C)
+    NB = dense_buckets(C)
     nch = (Sr + 32767) // 32768
     if kernel == "dl_pack":         # bases in, pre-word out, per-chunk bucket counts
         return Sr * L + 4 * Sr + 4 * NB * nch

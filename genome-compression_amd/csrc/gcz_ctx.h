@@ -256,7 +256,10 @@ struct gcz_ctx {
   int dense_mode = 1;        // dense leaf level (gcz_dense.h): 0 off, 1 on large pure-ACGT inputs, 2 any size (GCZ_DENSE)
   gcz_host::u64 dense_min = 1ull << 21;   // ... from this many strands (mode 1)
   bool dense_used = false;   // the last build's leaf level ran dense
-  gcz_host::u32 dense_nb = gcz_dev::kDNBMax;   // ... its code buckets (GCZ_DENSE_NB, testing)
+  // ... its code buckets (GCZ_DENSE_NB): 512 at L = 12 -- 2^14 codes per bucket (64 KB LDS tables,
+  // two workgroups per CU) and runs of ~64 records per (chunk, bucket); 1024 measured 2.576 vs
+  // 2.460 ms per 1 Gbase build (words 0.336 -> 0.308, first 0.257 -> 0.214, scatter 0.239 -> 0.208)
+  gcz_host::u32 dense_nb = 512;
   bool use_graph = true;     // small builds as a replayed HIP graph       (GCZ_GRAPH=0 disables)
   bool use_fused = true;     // small builds: two launches per node level  (GCZ_FUSED=0 disables)
   int small_cap_shift = 2;   // ... and tables 2^this times the usual size: short probe chains (GCZ_SMALL_CAP_SHIFT)
