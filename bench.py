@@ -211,6 +211,19 @@ def build_bytes(L, S, n_leaves, layer_sizes):
     return b_stream, b_table
 
 
+def traffic_file(config):
+    """The newest round's PMC capture of a config: profiles/rNN/pmc_traffic_<config>.json with the
+    highest NN (scripts/traffic_json.py writes it from the final evidence run of that round)."""
+    import glob
+    import re
+    best = None
+    for p in glob.glob(os.path.join(REPO, "profiles", "r*", f"pmc_traffic_{config}.json")):
+        m = re.search(r"[/\\]r(\d+)[/\\]pmc_traffic_", p)
+        if m and (best is None or int(m.group(1)) > best[0]):
+            best = (int(m.group(1)), p)
+    return best[1] if best else None
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -567,10 +580,12 @@ def main():
     # build for each kernel name, and the whole build's
     traffic = None
     counter_build = None
-    tpath = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
-    if os.path.exists(tpath) and mode in ("single", "replicas"):
+    tpath = traffic_file(args.config)
+    traffic_src = None
+    if tpath and mode in ("single", "replicas"):
         with open(tpath) as f:
             tj = json.load(f)
+        traffic_src = {"file": os.path.relpath(tpath, REPO), "code_head": tj.get("code_head")}
         per_build = tj.get("per_build", {})
         if dom in per_build:
             traffic = int(per_build[dom] / dk["launches"])
@@ -720,6 +735,7 @@ def main():
                       "hbm_frac_survey_formula": round(build_frac, 5),
                       # counter HBM bytes of a whole build (PMC capture) over this build's time
                       "counter_traffic_bytes": counter_build,
+                      "counter_traffic_source": traffic_src,
                       "hbm_frac_counter": round(counter_frac, 5) if counter_frac else None,
                       "n_leaves": info["n_leaves"],
                       "n_layers": info["n_layers"],

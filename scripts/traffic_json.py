@@ -3,7 +3,8 @@
 `bench.py --config <config> --build-only` (scripts/gpu_evidence.sh): HBM bytes per build
 for each of bench.py's kernel names and for the whole build.
 
-usage: traffic_json.py <fetch_dir> <write_dir> <config> <out.json>
+usage: traffic_json.py <fetch_dir> <write_dir> <config> <out.json> [code_head]
+(out.json: profiles/rNN/pmc_traffic_<config>.json -- bench.py reads the newest round's)
 Every launch in the capture belongs to a build (--build-only); builds are counted by
 k_build_init (one per build attempt).  gfx950 correction (MI355X_MICROARCH.md, HBM /
 rocprofv3 section): FETCH_SIZE tallies a 128-B read request as 64 B, so a kernel's bytes
@@ -39,7 +40,8 @@ def main():
     w, nw = load(sys.argv[2], "WRITE_SIZE")
     builds = max(1, min(nf, nw))
     per = {k: round((2 * f[k] + w[k]) / builds) for k in sorted(set(f) | set(w))}
-    out = {"config": sys.argv[3], "builds": builds, "per_build": per, "build_total": sum(per.values()),
+    out = {"config": sys.argv[3], "code_head": sys.argv[5] if len(sys.argv) > 5 else None,
+           "builds": builds, "per_build": per, "build_total": sum(per.values()),
            "_note": "HBM bytes per build from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of "
                     "bench.py --build-only (scripts/gpu_evidence.sh), 2 x FETCH_SIZE + WRITE_SIZE "
                     "(gfx950: FETCH_SIZE tallies a 128-B read as 64 B)"}

@@ -220,3 +220,22 @@ def test_rank_byte_model_on_the_r04_probes():
             b = bench.dist_rank_bytes(kname, 12, Sr, 0, R, c0, (Sr + 1) // 2, d["build"]["n_leaves"])
             if b and k["total_ms"] > 0:
                 assert b / (k["total_ms"] * 1e-3) / 1e9 <= 8000.0, (name, kname)
+
+
+def test_bench_reads_the_newest_traffic_capture():
+    """The bench line's counter bytes come from the newest round's PMC capture of its config
+    (profiles/rNN/pmc_traffic_<config>.json, written by scripts/traffic_json.py from the round's
+    final evidence run); no stale copy elsewhere can shadow it, and the capture's total is the
+    sum of its kernels."""
+    import glob
+    import re
+    bench = _load_bench()
+    assert not glob.glob(os.path.join(REPO, "profiles", "traffic_*.json"))
+    for cfg in ("uniform_1g", "tandem_3g2"):
+        files = glob.glob(os.path.join(REPO, "profiles", "r*", f"pmc_traffic_{cfg}.json"))
+        newest = max(files, key=lambda p: int(re.search(r"[/\\]r(\d+)[/\\]", p).group(1)))
+        assert bench.traffic_file(cfg) == newest
+        with open(newest) as f:
+            tj = json.load(f)
+        assert tj["build_total"] == sum(tj["per_build"].values())
+        assert tj["config"] == cfg
