@@ -39,9 +39,13 @@ def main():
     f, nf = load(sys.argv[1], "FETCH_SIZE")
     w, nw = load(sys.argv[2], "WRITE_SIZE")
     builds = max(1, min(nf, nw))
-    per = {k: round((2 * f[k] + w[k]) / builds) for k in sorted(set(f) | set(w))}
+    keys = sorted(set(f) | set(w))
+    per = {k: round((2 * f[k] + w[k]) / builds) for k in keys}
     out = {"config": sys.argv[3], "code_head": sys.argv[5] if len(sys.argv) > 5 else None,
            "builds": builds, "per_build": per, "build_total": sum(per.values()),
+           # the two sides apart: read bytes (2 x FETCH_SIZE) and written bytes (WRITE_SIZE)
+           "per_build_read": {k: round(2 * f[k] / builds) for k in keys},
+           "per_build_write": {k: round(w[k] / builds) for k in keys},
            "_note": "HBM bytes per build from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of "
                     "bench.py --build-only (scripts/gpu_evidence.sh), 2 x FETCH_SIZE + WRITE_SIZE "
                     "(gfx950: FETCH_SIZE tallies a 128-B read as 64 B)"}
