@@ -111,8 +111,14 @@ def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None, bu
         return 8 * bp + 4 * (bp // 3072 + 1) * ((bp >> 16) + 1)
     if kernel == "bucket_scan":     # exclusive scan of the count matrix
         return 8 * (bp // 3072 + 1) * ((bp >> 16) + 1)
-    if two_pass and kernel == "bucket_scatter":   # two-pass partition, pass 1: pair + child marks in,
-        return (8 + 4 + 4 + 8) * bp                 # word out, 8-B record appended to a coarse-bucket run
+    if two_pass and kernel == "bucket_scatter":   # two-pass partition, pass 1 (k_bkt_part): EVERY pair of
+        # the levels it ran on streams through it -- pair (8) and both children's marks (4) in, the
+        # provisional word (4) and its own two marks (2) out -- and each bucketed pair appends an 8-B
+        # record to a coarse run (round 5 charged the records' pairs only, which made the
+        # repetitive config's counter bytes look 2.6x the algorithmic ones: the read / write split
+        # of profiles/r06 matches the stream below)
+        pp = sum(pk[:launches]) if launches is not None else bp
+        return 18 * max(pp, bp) + 8 * bp
     if kernel == "bucket_fine":     # pass 2: records in, re-encoded records out (LDS-sorted slices)
         return 16 * bp
     if kernel == "bucket_scatter":  # pair in, word out, one 8-B record store (a 64-B sector) per pair
