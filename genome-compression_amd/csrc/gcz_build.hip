@@ -241,11 +241,6 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
     launch_dl_pack<false>(int(L), dim3(P.nch), stream, nullptr, a.leaves, P, dl_pw.as<u32>(), dl_cnt.as<u32>(),
                           d_hdr, static_cast<uint4*>(dl_desc.ptr), nz16);
   HIP_TRY(hipGetLastError());
-  if (check) {   // single device: the pure-ACGT verdict, read after the scatter is queued (below)
-    if (!ev_dfail) HIP_TRY(hipEventCreateWithFlags(&ev_dfail, hipEventDisableTiming));
-    HIP_TRY(hipMemcpyAsync(&h_hdr->dense_fail, &d_hdr->dense_fail, 4, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipEventRecord(ev_dfail, stream));
-  }
   // repetitive data? (the node inserts' LDS pre-dedupe): in-block repeats of a sample's
   // hashed codes (equal codes <=> equal keys)
   // (a rank of an R-rank build samples the first 1/R of that, at least 2^18, of its own
@@ -256,6 +251,12 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
                      dl_pw.as<u32>(), u64(0), ip, d_hdr);
   hipLaunchKernelGGL(k_dup_decide, dim3(1), dim3(1), 0, stream, d_hdr, ip, u32(predup_mode));
   HIP_TRY(hipGetLastError());
+  if (check) {   // single device: the pure-ACGT verdict and the probe's, read after the scatter is queued (below)
+    if (!ev_dfail) HIP_TRY(hipEventCreateWithFlags(&ev_dfail, hipEventDisableTiming));
+    HIP_TRY(hipMemcpyAsync(&h_hdr->dense_fail, &d_hdr->dense_fail, 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(&h_hdr->predup, &d_hdr->predup, 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipEventRecord(ev_dfail, stream));
+  }
   prof_end(KID_DL_PACK, e0);
   if (pack_only) {   // (the fused multi-rank schedule queues its own work before the rest)
     *used = true;
@@ -276,6 +277,7 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
     }
   }
   *used = true;
+  dense_nonrep = check && h_hdr->predup == 0;
   return dense_phase_a3(d_hdr, ucount, list, vec);
 }
 
@@ -481,8 +483,12 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     HIP_TRY(hipGetLastError());
     prof_end(KID_BKT_FINE, e0);
     prof_begin(KID_BKT_DEDUPE, e0);
-    hipLaunchKernelGGL(k_bkt_dedupe2<false>, dim3(1u << bb), dim3(kBktThreads), 0, stream, bkt_rec2.as<u64>(),
-                       bkt_off.as<u32>(), b2, a.words, mk, d_hdr, a.pcount, n, &d_hdr->bkt_overflow);
+    if (a.nonrep && dedupe_bm)
+      hipLaunchKernelGGL(k_bkt_dedupe_bm, dim3(1u << bb), dim3(kBmThreads), 0, stream, bkt_rec2.as<u64>(),
+                         bkt_off.as<u32>(), b2, a.words, mk, d_hdr, a.pcount, n, &d_hdr->bkt_overflow);
+    else
+      hipLaunchKernelGGL(k_bkt_dedupe2<false>, dim3(1u << bb), dim3(kBktThreads), 0, stream, bkt_rec2.as<u64>(),
+                         bkt_off.as<u32>(), b2, a.words, mk, d_hdr, a.pcount, n, &d_hdr->bkt_overflow);
     HIP_TRY(hipGetLastError());
     prof_end(KID_BKT_DEDUPE, e0);
   } else if (bkt) {
@@ -877,6 +883,7 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
         na.gate = &d_hdr->gate[k];
         na.allow_bucket = !fused;
         na.repetitive = table_only;
+        na.nonrep = dense_used && dense_nonrep;
         if (fused) {
           na.fused = true;
           na.ftab = fregion_ptr(k);
@@ -1057,6 +1064,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   }
   c->stream = c->own_stream;
   if (const char* t = std::getenv("GCZ_CANARY")) c->canary = std::atoi(t) != 0;
+  if (const char* t = std::getenv("GCZ_DEDUPE_BM")) c->dedupe_bm = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_DENSE_NB")) c->dense_nb = u32(std::strtoul(t, nullptr, 10));
   if (const char* t = std::getenv("GCZ_TABLE")) c->force_wide = std::strcmp(t, "wide") == 0;
   if (const char* t = std::getenv("GCZ_NODE_CAP_SHIFT")) c->node_cap_shift = std::atoi(t);

@@ -2273,6 +2273,160 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
   }
 }
 
+// The dedupe of non-repetitive data (the host read hdr->predup == 0 with the dense pack's verdict,
+// so the block collapse is off and a bucket's keys are nearly all distinct): k_bkt_dedupe2<false>'s
+// output from a quarter of its workgroup and a third of its LDS, so a CU holds six buckets in
+// flight instead of two (each bucket is a chain of dependent round trips: run offsets, records).
+// Equal keys share their low kBmLog bits (the record keys are bits of the level's key mix), so
+// only records whose bits another record of the bucket also set -- the "twice" bitmap, ~2 % of
+// them -- are hash-consed exactly, in a table of kBmSlots keys.  A bucket of more than
+// kBmItems * kBmThreads records or more such keys than the table holds sets the overflow flag
+// (the host rebuilds with the table path; non-repetitive data does not get there).
+constexpr int kBmThreads = 256;
+constexpr int kBmLog = 15;                   // seen / twice bitmaps of 2^15 bits (4 KB each)
+constexpr u32 kBmSlots = 1024;               // the candidates' keys (12 KB)
+constexpr int kBmItems = kBktCap / kBmThreads;   // records per thread (a bucket <= kBktCap)
+static_assert(kBmItems * kBmThreads == kBktCap, "the bucket capacity of the table path");
+
+[[maybe_unused]] static __global__ __launch_bounds__(kBmThreads) void k_bkt_dedupe_bm(const u64* __restrict__ recs, const u32* __restrict__ fo,
+                                                             Bkt2Plan bp, u32* __restrict__ rec, Marks mk,
+                                                             Header* __restrict__ hdr, const u64* prev_count, u64 n,
+                                                             u32* __restrict__ ovf) {
+  if (bkt2_skip(hdr, prev_count, n)) return;
+  __shared__ u32 s_seen[(1u << kBmLog) / 32], s_twice[(1u << kBmLog) / 32];
+  __shared__ u64 s_key[kBmSlots];
+  __shared__ u32 s_pos[kBmSlots];
+  __shared__ u32 s_dup[kBmSlots / 32];
+  __shared__ u32 s_pre[513], s_beg[512];   // slices per coarse bucket <= 512
+  __shared__ u32 s_gs[(kBktCap + 63) / 64];
+  __shared__ u32 s_wt[kBmThreads / 64];
+  __shared__ u32 s_full;
+  const u32 nb2 = 1u << bp.b2;
+  const u32 c = blockIdx.x >> bp.b2, f = blockIdx.x & (nb2 - 1);
+  const u32 ns = bp.nslice;
+  const u32 t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  {   // this bucket's run in every slice (two slices a thread), block exclusive scan of the lengths
+    u32 len[2] = {0, 0};
+#pragma unroll
+    for (u32 k = 0; k < 2; ++k) {
+      const u32 s2 = 2 * t + k;
+      if (s2 < ns) {
+        const u32* fs = fo + u64(c * ns + s2) * (nb2 + 1);
+        const u32 a = fs[f];
+        len[k] = fs[f + 1] - a;
+        s_beg[s2] = a;
+      }
+    }
+    const u32 sum = len[0] + len[1];
+    u32 inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const u32 y = __shfl_up(inc, o, 64);
+      if (int(lane) >= o) inc += y;
+    }
+    if (lane == 63) s_wt[wave] = inc;
+    for (u32 q = t; q < (1u << kBmLog) / 32; q += kBmThreads) {
+      s_seen[q] = 0;
+      s_twice[q] = 0;
+    }
+    for (u32 q = t; q < kBmSlots; q += kBmThreads) {
+      s_key[q] = kEmpty;
+      s_pos[q] = ~0u;
+    }
+    for (u32 q = t; q < kBmSlots / 32; q += kBmThreads) s_dup[q] = 0;
+    if (t == 0) s_full = 0;
+    __syncthreads();
+    u32 pre = 0;
+    for (u32 w = 0; w < wave; ++w) pre += s_wt[w];
+    pre += inc - sum;
+    if (2 * t < ns) s_pre[2 * t] = pre;
+    if (2 * t + 1 < ns) s_pre[2 * t + 1] = pre + len[0];
+    if (t == kBmThreads - 1) s_pre[ns] = pre + sum;
+  }
+  __syncthreads();
+  const u32 total = s_pre[ns];
+  if (total > u32(kBktCap)) {
+    if (t == 0) *ovf = 1;
+    return;
+  }
+  for (u32 s2 = t; s2 < ns; s2 += kBmThreads)
+    for (u32 g = (s_pre[s2] + 63) >> 6; (g << 6) < s_pre[s2 + 1]; ++g) s_gs[g] = s2;
+  __syncthreads();
+  const u64 pmask = (1ull << bp.P) - 1;
+  u64 key[kBmItems];
+  u32 pos[kBmItems];
+#pragma unroll
+  for (int e = 0; e < kBmItems; ++e) {
+    const u32 i = u32(e) * kBmThreads + t;
+    key[e] = kEmpty;
+    pos[e] = 0;
+    if (i >= total) continue;
+    u32 lo = s_gs[i >> 6], hi = (i >> 6) + 1 < ((total + 63) >> 6) ? s_gs[(i >> 6) + 1] : ns - 1;
+    while (lo < hi) {
+      const u32 mid = (lo + hi + 1) >> 1;
+      if (s_pre[mid] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    const u64 v = recs[u64(c * ns + lo) * kFineCap + s_beg[lo] + (i - s_pre[lo])];
+    key[e] = v >> bp.P;
+    pos[e] = u32(u64(lo) * bp.SC * kPartChunk + (v & pmask));
+  }
+  constexpr u32 bmask = (1u << kBmLog) - 1u;
+#pragma unroll
+  for (int e = 0; e < kBmItems; ++e) {   // seen once / twice by the key's low bits
+    if (key[e] == kEmpty) continue;
+    const u32 b = u32(key[e]) & bmask, m = 1u << (b & 31);
+    if (atomicOr(&s_seen[b >> 5], m) & m) atomicOr(&s_twice[b >> 5], m);
+  }
+  __syncthreads();
+  auto cand = [&](u64 k) { return k != kEmpty && ((s_twice[(u32(k) & bmask) >> 5] >> (u32(k) & 31)) & 1u); };
+  u32 slot[kBmItems];
+#pragma unroll
+  for (int e = 0; e < kBmItems; ++e) {   // the candidates into the table; a second holder marks its key
+    slot[e] = ~0u;
+    if (!cand(key[e])) continue;
+    const u64 k = key[e];
+    u32 h = u32((u64(u32(bkt_hash(k))) * kBmSlots) >> 32);
+    bool several = false;
+    for (u32 probe = 0;; ++probe) {
+      if (probe == kBmSlots) {
+        s_full = 1;
+        h = ~0u;
+        break;
+      }
+      unsigned long long cv = s_key[h];
+      if (cv == kEmpty) cv = atomicCAS(&s_key[h], kEmpty, (unsigned long long)k);
+      if (cv == k) several = true;
+      if (cv == kEmpty || cv == k) break;
+      h = h + 1 == kBmSlots ? 0u : h + 1;
+    }
+    slot[e] = h;
+    if (several && h != ~0u) atomicOr(&s_dup[h >> 5], 1u << (h & 31));
+  }
+  __syncthreads();
+  if (s_full) {
+    if (t == 0) *ovf = 1;
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < kBmItems; ++e)
+    if (slot[e] != ~0u && ((s_dup[slot[e] >> 5] >> (slot[e] & 31)) & 1u)) atomicMin(&s_pos[slot[e]], pos[e]);
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < kBmItems; ++e) {
+    const bool dup = slot[e] != ~0u && ((s_dup[slot[e] >> 5] >> (slot[e] & 31)) & 1u);
+    const u32 first = dup ? s_pos[slot[e]] : 0u;
+    nf_list_add(bp, hdr, dup && pos[e] != first, pos[e]);
+    if (!dup) continue;
+    if (pos[e] != first) {
+      mk.nf[pos[e]] = kNfNot;
+      rec[pos[e]] = first | (rec[pos[e]] & kBits);
+    } else {
+      mk.multi[pos[e]] = 1;
+    }
+  }
+}
+
 // ---- direct subtrees ----------------------------------------------------------------
 // Once level k0 is known to be direct (every element of level k0-1 unique), every
 // later level is too and ids are positions.  Each workgroup takes an aligned chunk
