@@ -484,7 +484,7 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     prof_end(KID_BKT_FINE, e0);
     prof_begin(KID_BKT_DEDUPE, e0);
     if (a.nonrep && dedupe_bm)
-      hipLaunchKernelGGL(k_bkt_dedupe_bm, dim3(1u << bb), dim3(kBmThreads), 0, stream, bkt_rec2.as<u64>(),
+      hipLaunchKernelGGL(k_bkt_dedupe_bm<false>, dim3(1u << bb), dim3(kBmThreads), 0, stream, bkt_rec2.as<u64>(),
                          bkt_off.as<u32>(), b2, a.words, mk, d_hdr, a.pcount, n, &d_hdr->bkt_overflow);
     else
       hipLaunchKernelGGL(k_bkt_dedupe2<false>, dim3(1u << bb), dim3(kBktThreads), 0, stream, bkt_rec2.as<u64>(),

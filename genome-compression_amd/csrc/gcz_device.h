@@ -2288,11 +2288,15 @@ constexpr u32 kBmSlots = 1024;               // the candidates' keys (12 KB)
 constexpr int kBmItems = kBktCap / kBmThreads;   // records per thread (a bucket <= kBktCap)
 static_assert(kBmItems * kBmThreads == kBktCap, "the bucket capacity of the table path");
 
-[[maybe_unused]] static __global__ __launch_bounds__(kBmThreads) void k_bkt_dedupe_bm(const u64* __restrict__ recs, const u32* __restrict__ fo,
+// kOwner: the fused multi-rank schedule's owner dedupe (k_bkt_dedupe2<true>'s outputs; its records
+// are non-repetitive data by construction: that schedule declines repetitive genomes).
+template <bool kOwner>
+__global__ __launch_bounds__(kBmThreads) void k_bkt_dedupe_bm(const u64* __restrict__ recs, const u32* __restrict__ fo,
                                                              Bkt2Plan bp, u32* __restrict__ rec, Marks mk,
                                                              Header* __restrict__ hdr, const u64* prev_count, u64 n,
                                                              u32* __restrict__ ovf) {
   if (bkt2_skip(hdr, prev_count, n)) return;
+  if (!kOwner && hdr->predup) bp.nfl = nullptr;   // (as k_bkt_dedupe2: collapsed levels take the look-back path)
   __shared__ u32 s_seen[(1u << kBmLog) / 32], s_twice[(1u << kBmLog) / 32];
   __shared__ u64 s_key[kBmSlots];
   __shared__ u32 s_pos[kBmSlots];
@@ -2416,9 +2420,13 @@ static_assert(kBmItems * kBmThreads == kBktCap, "the bucket capacity of the tabl
   for (int e = 0; e < kBmItems; ++e) {
     const bool dup = slot[e] != ~0u && ((s_dup[slot[e] >> 5] >> (slot[e] & 31)) & 1u);
     const u32 first = dup ? s_pos[slot[e]] : 0u;
-    nf_list_add(bp, hdr, dup && pos[e] != first, pos[e]);
+    if constexpr (!kOwner) nf_list_add(bp, hdr, dup && pos[e] != first, pos[e]);
     if (!dup) continue;
-    if (pos[e] != first) {
+    if constexpr (kOwner) {
+      rec[pos[e]] = first;
+      mk.nf[pos[e]] = pos[e] != first ? 7 : 6;
+      if (bp.olist && pos[e] != first) bp.olist[atomicAdd(bp.ocnt, 1u)] = pos[e];
+    } else if (pos[e] != first) {
       mk.nf[pos[e]] = kNfNot;
       rec[pos[e]] = first | (rec[pos[e]] & kBits);
     } else {

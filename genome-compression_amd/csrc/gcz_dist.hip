@@ -2318,10 +2318,18 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       hipLaunchKernelGGL(k_bkt_fine, dim3(unsigned(nfine)), dim3(kBktThreads), size_t(kFineCap) * 8, cx->stream,
                          d.ob_seg.as<u64>(), d.ob_rt.as<u32>(), bp, d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(),
                          static_cast<Header*>(nullptr), static_cast<const u64*>(nullptr), nr, ovf);
-      hipLaunchKernelGGL(k_bkt_dedupe2<true>, dim3(unsigned(u64(1) << (bp.b1 + bp.b2))), dim3(kBktThreads), 0,
-                         cx->stream, d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(), bp, d.oslot.as<u32>(),
-                         Marks{d.rflag.as<unsigned char>(), nullptr}, static_cast<Header*>(nullptr),
-                         static_cast<const u64*>(nullptr), nr, ovf);
+      // (the schedule takes non-repetitive data only: the bitmap dedupe, six buckets per CU in flight;
+      // a bucket over its capacity sets the overflow word and every rank falls back)
+      if (cx->dedupe_bm)
+        hipLaunchKernelGGL(k_bkt_dedupe_bm<true>, dim3(unsigned(u64(1) << (bp.b1 + bp.b2))), dim3(kBmThreads), 0,
+                           cx->stream, d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(), bp, d.oslot.as<u32>(),
+                           Marks{d.rflag.as<unsigned char>(), nullptr}, static_cast<Header*>(nullptr),
+                           static_cast<const u64*>(nullptr), nr, ovf);
+      else
+        hipLaunchKernelGGL(k_bkt_dedupe2<true>, dim3(unsigned(u64(1) << (bp.b1 + bp.b2))), dim3(kBktThreads), 0,
+                           cx->stream, d.ob_rec2.as<u64>(), d.ob_fo.as<u32>(), bp, d.oslot.as<u32>(),
+                           Marks{d.rflag.as<unsigned char>(), nullptr}, static_cast<Header*>(nullptr),
+                           static_cast<const u64*>(nullptr), nr, ovf);
       const Displ P4 = displ4(r, true);
       FlC5 c{};
       c.olist = d.olist.as<u32>();
