@@ -386,3 +386,55 @@ def test_gpu_repetitive_decision_after_failed_dense_pack(gcz):
     assert got[False][1] == got[True][1] == 0, got       # both took the hash-table leaf level
     assert got[False][0] == got[True][0] == 0, got
     assert got[False][2] == got[True][2], got
+
+
+@pytest.fixture(scope="module")
+def ctx_dense_bucket(gcz):
+    """Dense leaf level at every size and the two-pass bucketed insert on every hashed level:
+    on data the dense probe finds non-repetitive, layer 0 and up take the bitmap-filtered dedupe
+    (k_bkt_dedupe_bm); GCZ_PREDUP=2 keeps the block collapse off whatever the probe says."""
+    os.environ.update({"GCZ_DENSE": "2", "GCZ_BUCKET_MIN": "1", "GCZ_PREDUP": "2"})
+    try:
+        c = gcz.Context(0)
+    finally:
+        for k in ("GCZ_DENSE", "GCZ_BUCKET_MIN", "GCZ_PREDUP"):
+            del os.environ[k]
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("name", [n for n in _names(12_000_000) if not n.startswith("fasta/")])
+def test_gpu_bitmap_dedupe_goldens(name, ctx_dense_bucket, gcz, manifest):
+    """Every golden through the dense level + bitmap dedupe (or, for IUPAC / L > 12, the table
+    levels): the reference's tree bit for bit."""
+    case = manifest[name]
+    exp = case["expect"]
+    kind, payload, L = case_input(case, gcz)
+    if exp["exit"] != 0:
+        return
+    _build(ctx_dense_bucket, kind, payload, L)
+    assert compare_digest(gcz.digest(ctx_dense_bucket.tree()), exp) == {}
+
+
+@pytest.mark.parametrize("dups", [0, 200, 20_000, 400_000])
+def test_gpu_bitmap_dedupe_repeats_oracle(dups, ctx_dense_bucket, gcz, oracle):
+    """Random ACGT leaves with `dups` copied layer-0 pairs spread over the genome (true repeats
+    the bitmaps must route to the exact table: first occurrence, multi, not-first ids) -- up to
+    buckets whose repeated keys overflow the candidates' table (the overflow flag: the host
+    rebuilds with the table path).  Equal to the C oracle."""
+    rng = np.random.default_rng(900 + dups)
+    L, S = 12, 2_400_002
+    acgt = np.array([1, 2, 4, 8], dtype=np.uint64)
+    codes = rng.integers(0, 4, size=(S, L))
+    leaves = (acgt[codes] << (4 * np.arange(L, dtype=np.uint64))).sum(axis=1).astype(np.uint64)
+    if dups:
+        src = rng.integers(0, S // 2, size=dups)
+        dst = rng.integers(0, S // 2, size=dups)
+        leaves[2 * dst] = leaves[2 * src]
+        leaves[2 * dst + 1] = leaves[2 * src + 1]
+    ctx_dense_bucket.build_leaves(leaves, L)
+    g = ctx_dense_bucket.tree()
+    o = oracle.build_leaves(leaves, L)
+    assert g.leaves_bin() == o.leaves_bin(), dups
+    assert g.layers_bin() == o.layers_bin(), dups
+    assert g.root == o.root, dups
