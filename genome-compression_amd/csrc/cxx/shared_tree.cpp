@@ -34,10 +34,14 @@ namespace {
 
 // One libgcz context per process (device GCZ_DEVICE, default 0), created on
 // first use.  Builds are serialised, matching the reference's single build thread.
+std::atomic<bool> engine_alive{false};
+
 struct Engine {
   gcz_ctx* ctx = nullptr;
   std::mutex mu;
   std::uint64_t gen = 0;   // generation of the tree the device arrays hold (bumped by builds and device sorts)
+  // the device sort whose sorted arrays no tree has copied in yet (at most one: the device holds one tree)
+  std::shared_ptr<gcz_lazy_copy> pending;
   Engine() {
     const char* d = std::getenv("GCZ_DEVICE");
     const int rc = gcz_ctx_create(d ? std::atoi(d) : 0, &ctx);
@@ -45,8 +49,12 @@ struct Engine {
       std::cerr << "libgcz: no usable MI355X device (code " << rc << "), aborting...\n";
       std::exit(1);
     }
+    engine_alive.store(true);
   }
-  ~Engine() { gcz_ctx_destroy(ctx); }
+  ~Engine() {
+    engine_alive.store(false);
+    gcz_ctx_destroy(ctx);
+  }
 };
 
 Engine& engine() {
@@ -82,6 +90,29 @@ void check_build(int rc, gcz_ctx* ctx) {
     std::cerr << "libgcz build failed (code " << rc << "): " << gcz_ctx_last_error(ctx) << '\n';
   }
   std::exit(1);
+}
+
+}  // namespace
+
+// The destination of a device sort's arrays (shared_tree::lazy): the tree's containers keep their
+// sizes across the sort (a permutation), so raw pointers to their storage stay valid while the
+// tree lives -- also across a move, which takes the storage along.  Flags under the engine mutex.
+struct gcz_lazy_copy {
+  std::atomic<bool> pending{true};
+  bool dead = false;   // the tree went away or its containers are being replaced
+  std::uint64_t* leaves = nullptr;
+  std::vector<std::uint32_t*> layers;
+};
+
+namespace {
+// Before the engine's device arrays change (a build, a sort, a gather into its context): the
+// pending sorted arrays into their tree.  (e.mu held)
+void flush_pending(Engine& e) {
+  std::shared_ptr<gcz_lazy_copy> p = std::move(e.pending);
+  if (!p || !p->pending.load() || p->dead) return;
+  PhaseTimer t{"fetch-sorted"};
+  check_build(gcz_fetch_host(e.ctx, p->leaves, p->layers.data()), e.ctx);
+  p->pending.store(false);
 }
 
 // pointer compression, src/shared_tree.cpp:25-67
@@ -174,8 +205,11 @@ fasta_reader open_with_engine(const std::filesystem::path& path) {
   const auto fsize = std::filesystem::file_size(path, ec);
   std::thread init([fsize] {   // the context, the input buffer and a warm upload path, while the file maps
     PhaseTimer t{"context"};
-    (void)gcz_upload_reserve(engine().ctx, fsize);
-    if (fsize >= (std::uint64_t(64) << 20)) (void)gcz_fetch_reserve(engine().ctx, fsize);   // the fetch's ring
+    auto& e = engine();
+    std::lock_guard<std::mutex> lock(e.mu);
+    flush_pending(e);   // (another tree's sorted arrays still in HBM, before the reservations)
+    (void)gcz_upload_reserve(e.ctx, fsize);
+    if (fsize >= (std::uint64_t(64) << 20)) (void)gcz_fetch_reserve(e.ctx, fsize);   // the fetch's ring
   });
   fasta_reader f = [&] { PhaseTimer t{"map"}; return fasta_reader{path}; }();
   if (!ec && fsize >= (std::uint64_t(64) << 20)) {
@@ -197,6 +231,7 @@ shared_tree::shared_tree(std::filesystem::path path) : shared_tree{open_with_eng
 shared_tree::shared_tree(fasta_reader file, bool verbose) {
   auto& e = engine();
   std::lock_guard<std::mutex> lock(e.mu);
+  flush_pending(e);
   struct PoolGuard {   // the pool open_with_engine faulted in goes whichever way this ends
     ~PoolGuard() { gcz_host_pool_release(1); }
   } pool_guard;
@@ -214,6 +249,7 @@ shared_tree::shared_tree(std::vector<dna>& data, bool verbose) {
   static_assert(sizeof(dna) == 8, "dna is one 64-bit word");
   auto& e = engine();
   std::lock_guard<std::mutex> lock(e.mu);
+  flush_pending(e);
   check_build(gcz_build_host_leaves(e.ctx, reinterpret_cast<const std::uint64_t*>(data.data()), data.size(),
                                     int(dna::size())),
               e.ctx);
@@ -272,6 +308,8 @@ auto tree_constructor::reduce(const std::vector<dna>& data, bool verbose) -> poi
   auto& e = engine();
   {
     std::lock_guard<std::mutex> lock(e.mu);
+    parent.drop_lazy();
+    flush_pending(e);
     check_build(gcz_build_host_leaves(e.ctx, reinterpret_cast<const std::uint64_t*>(data.data()), data.size(),
                                       int(dna::size())),
                 e.ctx);
@@ -288,6 +326,8 @@ auto tree_constructor::reduce(fasta_reader& file, bool verbose) -> pointer {   /
   auto& e = engine();
   {
     std::lock_guard<std::mutex> lock(e.mu);
+    parent.drop_lazy();
+    flush_pending(e);
     check_build(gcz_build_host_fasta_buffered(e.ctx, file.raw_data(), file.raw_size(), int(dna::size()),
                                               file.buffer_strands(), file.strands_read()),
                 e.ctx);
@@ -486,6 +526,11 @@ auto shared_tree_on_gpus(const std::filesystem::path& path, int gpus) -> shared_
   // there it is a device-resident tree like a one-GPU build's, so the frequency sort, bytes()
   // and the .dag writer run on the GPU (sort_tree / serialize above)
   gcz_ctx* dst = rank == 0 ? engine().ctx : nullptr;
+  if (rank == 0) {   // (another tree's sorted arrays still in HBM: the gather overwrites them)
+    auto& e = engine();
+    std::lock_guard<std::mutex> lock(e.mu);
+    flush_pending(e);
+  }
   if ((rc = gcz_group_assemble(g, dst))) rank_fail(ms, rank, "tree gather", rc, ctx);
   gcz_dev_free(ctx, d);
   gcz_group_destroy(g);
@@ -508,6 +553,7 @@ auto shared_tree_on_gpus(const std::filesystem::path& path, int gpus) -> shared_
 
 void shared_tree::build_from_gpu() {
   PhaseTimer t{"fetch"};
+  drop_lazy();   // (the containers are refilled)
   gcz_ctx* ctx = engine().ctx;
   gcz_info info{};
   gcz_info_get(ctx, &info);
@@ -542,9 +588,79 @@ void shared_tree::build_from_gpu() {
 
 bool shared_tree::on_device() const { return device_gen != 0 && device_gen == engine().gen; }
 
+// ---- the lazy host copy of a device sort -----------------------------------------------
+void shared_tree::materialize() const {
+  if (!lazy || !lazy->pending.load(std::memory_order_acquire)) return;
+  auto& e = engine();
+  std::lock_guard<std::mutex> lock(e.mu);
+  if (!lazy->pending.load() || lazy->dead) return;
+  PhaseTimer t{"fetch-sorted"};
+  check_build(gcz_fetch_host(e.ctx, lazy->leaves, lazy->layers.data()), e.ctx);
+  lazy->pending.store(false, std::memory_order_release);
+  if (e.pending == lazy) e.pending.reset();
+}
+
+void shared_tree::drop_lazy() {   // (e.mu held by every caller but the destructor / assignments)
+  if (lazy) lazy->dead = true;
+  lazy.reset();
+}
+
+shared_tree::~shared_tree() {
+  if (lazy && engine_alive.load()) {
+    auto& e = engine();
+    std::lock_guard<std::mutex> lock(e.mu);
+    lazy->dead = true;
+  }
+}
+
+shared_tree::shared_tree(const shared_tree& o) {
+  o.materialize();
+  nodes = o.nodes;
+  leaves = o.leaves;
+  root = o.root;
+  device_gen = o.device_gen;
+}
+
+shared_tree::shared_tree(shared_tree&& o) noexcept
+    : lazy(std::move(o.lazy)), nodes(std::move(o.nodes)), leaves(std::move(o.leaves)), root(o.root),
+      device_gen(o.device_gen) {}
+
+auto shared_tree::operator=(const shared_tree& o) -> shared_tree& {
+  if (this == &o) return *this;
+  o.materialize();
+  if (lazy && engine_alive.load()) {
+    std::lock_guard<std::mutex> lock(engine().mu);
+    drop_lazy();
+  }
+  nodes = o.nodes;
+  leaves = o.leaves;
+  root = o.root;
+  device_gen = o.device_gen;
+  return *this;
+}
+
+auto shared_tree::operator=(shared_tree&& o) noexcept -> shared_tree& {
+  if (this == &o) return *this;
+  if (lazy && engine_alive.load()) {
+    std::lock_guard<std::mutex> lock(engine().mu);
+    drop_lazy();
+  }
+  nodes = std::move(o.nodes);
+  leaves = std::move(o.leaves);
+  root = o.root;
+  device_gen = o.device_gen;
+  lazy = std::move(o.lazy);
+  return *this;
+}
+
 // ---- accessors -----------------------------------------------------------------
 auto shared_tree::width() const -> std::size_t {
   assert(nodes.back().size() == 1);
+  if (on_device()) {   // a tree of the device build: the strands it was built from (gcz_info)
+    gcz_info info{};
+    if (gcz_info_get(engine().ctx, &info) == GCZ_OK) return std::size_t(info.n_strands);
+  }
+  materialize();
   return gcz::view_width(view(nodes, leaves, root));
 }
 
@@ -562,6 +678,7 @@ auto shared_tree::node_count() const -> std::size_t {
 }
 
 auto shared_tree::access_leaf(pointer p) const -> dna {   // :231-236
+  materialize();
   auto leaf = leaves[p.index()];
   if (p.is_mirrored()) leaf = leaf.mirrored();
   if (p.is_transposed()) leaf = leaf.transposed();
@@ -589,6 +706,7 @@ auto shared_tree::operator[](std::uint64_t index) const -> dna {   // :268-291
 // ---- frequency sort (:316-483) ------------------------------------------------------
 auto shared_tree::histogram(std::size_t layer) const -> std::vector<std::size_t> {
   assert(layer < nodes.size());
+  materialize();
   std::vector<std::size_t> result(layer == 0 ? leaves.size() : nodes[layer - 1].size(), 0);
   for (const auto& n : nodes[layer]) {
     if (auto l = n.left(); l) ++result[l.index()];
@@ -611,6 +729,7 @@ void shared_tree::store_histogram(std::filesystem::path path) const {
 }
 
 void shared_tree::rewire_nodes(std::size_t layer, const std::vector<std::size_t>& indices) {
+  materialize();
   device_gen = 0;
   auto rewire = [&](pointer old) {
     if (old.empty()) return old;
@@ -647,15 +766,31 @@ void shared_tree::sort_nodes(std::size_t layer) {
 }
 
 void shared_tree::sort_tree(bool verbose) {
-  if (on_device()) {   // the arrays are still in HBM: sort there, copy the result back
+  if (on_device()) {   // the arrays are still in HBM: sort there; the host copy waits for its first read
     auto& e = engine();
     std::lock_guard<std::mutex> lock(e.mu);
+    if (e.pending != lazy) flush_pending(e);   // (another tree's sorted arrays: none while this one is on the device)
     {
       PhaseTimer t{"device-sort"};
       check_build(gcz_sort_device(e.ctx), e.ctx);
     }
-    build_from_gpu();
+    if (!lazy) {   // (sorting again a tree whose copy is still pending: the same destination)
+      gcz_info info{};
+      gcz_info_get(e.ctx, &info);
+      auto lz = std::make_shared<gcz_lazy_copy>();
+      lz->leaves = reinterpret_cast<std::uint64_t*>(leaves.data());
+      for (int k = 0; k < info.n_layers; ++k) lz->layers.push_back(reinterpret_cast<std::uint32_t*>(nodes[k].data()));
+      lazy = std::move(lz);
+    }
+    e.pending = lazy;
+    root = [&] {
+      gcz_info info{};
+      gcz_info_get(e.ctx, &info);
+      return pointer::from_word(info.root);
+    }();
+    device_gen = ++e.gen;
   } else {
+    materialize();
     auto v = view(nodes, leaves, root);   // all layers at once, in parallel (same net effect)
     gcz::view_sort(v);
   }
@@ -668,6 +803,7 @@ auto shared_tree::bytes() const noexcept -> std::size_t {
     std::uint64_t b = 0;
     if (gcz_bytes_device(engine().ctx, &b) == GCZ_OK) return b;
   }
+  materialize();
   return gcz::view_bytes(view(nodes, leaves, root));
 }
 
@@ -682,6 +818,7 @@ void shared_tree::serialize(std::ostream& os) const {
       }
     }
   }
+  materialize();
   const auto v = view(nodes, leaves, root);
   std::vector<std::uint8_t> buf(gcz::view_bytes(v));
   gcz::view_serialize(v, buf.data(), buf.size());

@@ -185,9 +185,19 @@ struct gcz_uninit_allocator : std::allocator<T> {
   }
 };
 
+// The sorted arrays of a device sort, not yet copied into a tree's containers (shared_tree.cpp).
+struct gcz_lazy_copy;
+
 class shared_tree {
  public:
   shared_tree() = default;
+  // (explicit for the lazy host copy after a device sort: a copy reads the sorted arrays first, a
+  // destroyed or overwritten tree cancels its pending copy)
+  ~shared_tree();
+  shared_tree(const shared_tree& other);
+  shared_tree(shared_tree&& other) noexcept;
+  auto operator=(const shared_tree& other) -> shared_tree&;
+  auto operator=(shared_tree&& other) noexcept -> shared_tree&;
   shared_tree(std::filesystem::path path);
   shared_tree(fasta_reader file, bool verbose = false);
   shared_tree(std::vector<dna>& data, bool verbose = false);
@@ -201,12 +211,24 @@ class shared_tree {
   auto leaf_count() const noexcept { return leaves.size(); }
 
   auto access_leaf(pointer p) const -> dna;
-  auto access_node(std::size_t layer, pointer p) const -> node { return nodes[layer][p.index()]; }
+  auto access_node(std::size_t layer, pointer p) const -> node {
+    materialize();
+    return nodes[layer][p.index()];
+  }
   auto operator[](std::uint64_t index) const -> dna;
 
-  void add_layer() { nodes.emplace_back(); }
-  void emplace_node(std::size_t layer, node n) { nodes[layer].emplace_back(n); }
-  void emplace_leaf(dna leaf) { leaves.emplace_back(leaf); }
+  void add_layer() {
+    materialize();   // (a pending copy's destination must not move)
+    nodes.emplace_back();
+  }
+  void emplace_node(std::size_t layer, node n) {
+    materialize();
+    nodes[layer].emplace_back(n);
+  }
+  void emplace_leaf(dna leaf) {
+    materialize();
+    leaves.emplace_back(leaf);
+  }
 
   auto histogram(std::size_t layer) const -> std::vector<std::size_t>;
   void store_histogram(std::filesystem::path) const;
@@ -252,6 +274,12 @@ class shared_tree {
   friend auto shared_tree_on_gpus(const std::filesystem::path& path, int gpus) -> shared_tree;
   void build_from_gpu();   // copies the last libgcz build of this thread into the containers
   bool on_device() const;  // the engine's device arrays still hold exactly this tree
+  // After a device sort the containers keep their sizes but not yet the sorted contents: those
+  // stay in HBM (compress writes its .dag from there and never reads them on the host) and are
+  // copied in by the first host read (materialize), or before the engine's next build or sort.
+  std::shared_ptr<gcz_lazy_copy> lazy;
+  void materialize() const;
+  void drop_lazy();        // the containers are about to be replaced: no copy
 
   using layer_vector = std::vector<node, gcz_uninit_allocator<node>>;
   using leaf_vector = std::vector<dna, gcz_uninit_allocator<dna>>;
@@ -262,6 +290,7 @@ class shared_tree {
 };
 
 inline auto operator<<(std::ostream& os, const shared_tree& tree) -> std::ostream& {
+  tree.materialize();
   os << "Leaves (" << tree.leaves.size() << "):";
   for (const auto& leaf : tree.leaves) os << ' ' << leaf;
   os << '\n';

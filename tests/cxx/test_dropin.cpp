@@ -146,6 +146,69 @@ static void gpu_file_build() {
   CHECK(same_sequence(load, data), "deserialized tree decompresses");
 }
 
+// The host copy a device sort defers to the first host read (shared_tree::materialize): every
+// way a pending tree can be read, copied, moved, overwritten or outlived by the engine's next
+// build gives the sorted tree -- the one the host-only sort of the same build produces.
+static void gpu_lazy_sorted_copy() {
+  const auto data = read_genome(dir + "/data/hehcmv");
+  const auto other = read_genome(dir + "/data/chmpxx");
+  auto reference_sorted = [&] {   // the host frequency sort of a copy (no device sort)
+    shared_tree t{const_cast<std::vector<dna>&>(data)};
+    shared_tree h = t;        // a copy: on the device too, but the sort below is the host's
+    shared_tree unrelated{const_cast<std::vector<dna>&>(other)};   // the engine moves on: h is host-only
+    h.sort_tree();
+    std::stringstream s;
+    h.serialize(s);
+    return s.str();
+  }();
+  auto dump = [](const shared_tree& t) {
+    std::stringstream s;
+    t.serialize(s);
+    return s.str();
+  };
+  {   // read right after the sort (iterator, operator[], access_node via width's traversal)
+    shared_tree t{const_cast<std::vector<dna>&>(data)};
+    t.sort_tree();
+    CHECK(same_sequence(t, data), "pending tree decompresses");
+    CHECK(dump(t) == reference_sorted, "pending tree serializes as the host sort");
+  }
+  {   // the engine's next build copies the pending arrays in first
+    shared_tree t{const_cast<std::vector<dna>&>(data)};
+    t.sort_tree();
+    shared_tree u{const_cast<std::vector<dna>&>(other)};
+    CHECK(same_sequence(t, data), "pending tree read after another build");
+    CHECK(dump(t) == reference_sorted, "pending tree after another build: sorted contents");
+    CHECK(same_sequence(u, other), "the other build");
+  }
+  {   // moved, then copied, while pending; a pending tree destroyed before the next build
+    shared_tree t{const_cast<std::vector<dna>&>(data)};
+    t.sort_tree();
+    shared_tree m{std::move(t)};
+    shared_tree c = m;
+    CHECK(dump(c) == reference_sorted, "copy of a moved pending tree");
+    CHECK(dump(m) == reference_sorted, "moved pending tree");
+    {
+      shared_tree gone{const_cast<std::vector<dna>&>(other)};
+      gone.sort_tree();
+    }
+    shared_tree next{const_cast<std::vector<dna>&>(data)};
+    CHECK(same_sequence(next, data), "a build after a destroyed pending tree");
+  }
+  {   // sorted twice on the device, then assigned over while pending
+    shared_tree t{const_cast<std::vector<dna>&>(data)};
+    t.sort_tree();
+    t.sort_tree();
+    CHECK(dump(t) == reference_sorted, "sorted twice");
+    shared_tree a{const_cast<std::vector<dna>&>(other)};
+    a.sort_tree();
+    a = shared_tree{const_cast<std::vector<dna>&>(data)};
+    CHECK(same_sequence(a, data), "assigned over a pending tree");
+    tree_constructor tc{a};
+    tc.reduce(data);
+    CHECK(same_sequence(a, data), "tree_constructor::reduce into a tree");
+  }
+}
+
 // fasta_reader's buffer API (include/fasta_reader.h:31-33): load_buffer + read_into
 // hand out the same strands as read_genome; swap_buffers exchanges the buffers.
 static void buffer_api() {
@@ -273,6 +336,7 @@ int main(int argc, char** argv) {
     gpu_transposition();
     gpu_frequency_sort();
     gpu_file_build();
+    gpu_lazy_sorted_copy();
   }
   std::cout << (failures ? "FAILED " : "OK ") << failures << '\n';
   return failures ? 1 : 0;
