@@ -483,7 +483,7 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     HIP_TRY(hipGetLastError());
     prof_end(KID_BKT_FINE, e0);
     prof_begin(KID_BKT_DEDUPE, e0);
-    if (a.nonrep && dedupe_bm)
+    if (dedupe_bm && (a.nonrep || dedupe_bm_all))
       hipLaunchKernelGGL(k_bkt_dedupe_bm<false>, dim3(1u << bb), dim3(kBmThreads), 0, stream, bkt_rec2.as<u64>(),
                          bkt_off.as<u32>(), b2, a.words, mk, d_hdr, a.pcount, n, &d_hdr->bkt_overflow);
     else
@@ -1064,7 +1064,10 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   }
   c->stream = c->own_stream;
   if (const char* t = std::getenv("GCZ_CANARY")) c->canary = std::atoi(t) != 0;
-  if (const char* t = std::getenv("GCZ_DEDUPE_BM")) c->dedupe_bm = std::atoi(t) != 0;
+  if (const char* t = std::getenv("GCZ_DEDUPE_BM")) {
+    c->dedupe_bm = std::atoi(t) != 0;
+    c->dedupe_bm_all = std::atoi(t) == 2;
+  }
   if (const char* t = std::getenv("GCZ_DENSE_NB")) c->dense_nb = u32(std::strtoul(t, nullptr, 10));
   if (const char* t = std::getenv("GCZ_TABLE")) c->force_wide = std::strcmp(t, "wide") == 0;
   if (const char* t = std::getenv("GCZ_NODE_CAP_SHIFT")) c->node_cap_shift = std::atoi(t);

@@ -259,6 +259,7 @@ struct gcz_ctx {
   bool dense_used = false;   // the last build's leaf level ran dense
   bool dense_nonrep = false; // ... and its probe found the data not repetitive (read with its verdict)
   bool dedupe_bm = true;     // two-pass levels of such data: k_bkt_dedupe_bm (GCZ_DEDUPE_BM=0: k_bkt_dedupe2)
+  bool dedupe_bm_all = false; // ... on every two-pass level, repetitive data too (GCZ_DEDUPE_BM=2, testing)
   // ... its code buckets (GCZ_DENSE_NB): 512 at L = 12 -- 2^14 codes per bucket (64 KB LDS tables,
   // two workgroups per CU) and runs of ~64 records per (chunk, bucket); 1024 measured 2.576 vs
   // 2.460 ms per 1 Gbase build (words 0.336 -> 0.308, first 0.257 -> 0.214, scatter 0.239 -> 0.208)
