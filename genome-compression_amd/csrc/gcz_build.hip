@@ -251,10 +251,9 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
                      dl_pw.as<u32>(), u64(0), ip, d_hdr);
   hipLaunchKernelGGL(k_dup_decide, dim3(1), dim3(1), 0, stream, d_hdr, ip, u32(predup_mode));
   HIP_TRY(hipGetLastError());
-  if (check) {   // single device: the pure-ACGT verdict and the probe's, read after the scatter is queued (below)
+  if (check) {   // single device: the pure-ACGT verdict, read after the scatter is queued (below)
     if (!ev_dfail) HIP_TRY(hipEventCreateWithFlags(&ev_dfail, hipEventDisableTiming));
     HIP_TRY(hipMemcpyAsync(&h_hdr->dense_fail, &d_hdr->dense_fail, 4, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipMemcpyAsync(&h_hdr->predup, &d_hdr->predup, 4, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipEventRecord(ev_dfail, stream));
   }
   prof_end(KID_DL_PACK, e0);
@@ -277,7 +276,6 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
     }
   }
   *used = true;
-  dense_nonrep = check && h_hdr->predup == 0;
   return dense_phase_a3(d_hdr, ucount, list, vec);
 }
 
@@ -483,10 +481,19 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
     HIP_TRY(hipGetLastError());
     prof_end(KID_BKT_FINE, e0);
     prof_begin(KID_BKT_DEDUPE, e0);
-    if (dedupe_bm && (a.nonrep || dedupe_bm_all))
+    if (dedupe_bm) {
+      // the bitmap dedupe; buckets over its capacity (hot keys of repetitive data) go to
+      // k_bkt_dedupe2 in a second launch of a few workgroups that takes them from a list (empty:
+      // they exit at once)
+      if (int rc = ensure(bkt_redo, (u64(1) << kBktMaxLog) * 4 + 16)) return rc;
+      Bkt2Plan bm = b2;
+      bm.redo = bkt_redo.as<u32>();
+      bm.redo_cnt = &d_hdr->redo[a.k];
       hipLaunchKernelGGL(k_bkt_dedupe_bm<false>, dim3(1u << bb), dim3(kBmThreads), 0, stream, bkt_rec2.as<u64>(),
-                         bkt_off.as<u32>(), b2, a.words, mk, d_hdr, a.pcount, n, &d_hdr->bkt_overflow);
-    else
+                         bkt_off.as<u32>(), bm, a.words, mk, d_hdr, a.pcount, n, &d_hdr->bkt_overflow);
+      hipLaunchKernelGGL(k_bkt_dedupe2_redo, dim3(64), dim3(kBktThreads), 0, stream, bkt_rec2.as<u64>(),
+                         bkt_off.as<u32>(), bm, a.words, mk, d_hdr, a.pcount, n, &d_hdr->bkt_overflow);
+    } else
       hipLaunchKernelGGL(k_bkt_dedupe2<false>, dim3(1u << bb), dim3(kBktThreads), 0, stream, bkt_rec2.as<u64>(),
                          bkt_off.as<u32>(), b2, a.words, mk, d_hdr, a.pcount, n, &d_hdr->bkt_overflow);
     HIP_TRY(hipGetLastError());
@@ -883,7 +890,6 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
         na.gate = &d_hdr->gate[k];
         na.allow_bucket = !fused;
         na.repetitive = table_only;
-        na.nonrep = dense_used && dense_nonrep;
         if (fused) {
           na.fused = true;
           na.ftab = fregion_ptr(k);
@@ -1064,10 +1070,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   }
   c->stream = c->own_stream;
   if (const char* t = std::getenv("GCZ_CANARY")) c->canary = std::atoi(t) != 0;
-  if (const char* t = std::getenv("GCZ_DEDUPE_BM")) {
-    c->dedupe_bm = std::atoi(t) != 0;
-    c->dedupe_bm_all = std::atoi(t) == 2;
-  }
+  if (const char* t = std::getenv("GCZ_DEDUPE_BM")) c->dedupe_bm = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_DENSE_NB")) c->dense_nb = u32(std::strtoul(t, nullptr, 10));
   if (const char* t = std::getenv("GCZ_TABLE")) c->force_wide = std::strcmp(t, "wide") == 0;
   if (const char* t = std::getenv("GCZ_NODE_CAP_SHIFT")) c->node_cap_shift = std::atoi(t);
@@ -1107,7 +1110,7 @@ void gcz_ctx_destroy(gcz_ctx* c) {
                     &c->dl_rec, &c->dl_idrec, &c->dl_cnt, &c->dl_off, &c->dl_offt, &c->dl_fpg, &c->dl_fb, &c->dl_wpre,
                     &c->dl_desc, &c->dl_fl, &c->dl_fo, &c->dl_lh, &c->dl_pb, &c->dl_pbs, &c->dl_lower,
                     &c->dl_pos, &c->dl_list, &c->dl_gid, &c->dl_recv, &c->dl_stage, &c->dl_seg, &c->seg_w,
-                    &c->seg_nf, &c->seg_mu, &c->seg_in, &c->nf_list, &c->tcount})
+                    &c->seg_nf, &c->seg_mu, &c->seg_in, &c->nf_list, &c->tcount, &c->bkt_redo})
     if (b->ptr) (void)hipFree(b->ptr);
   if (c->h_hdr) (void)hipHostFree(c->h_hdr);
   if (c->h_ring) (void)hipHostFree(c->h_ring);
@@ -1145,7 +1148,7 @@ extern "C++" int gcz_canary_scan(gcz_ctx* c, std::string& out) {
       {&gcz_ctx::dl_gid, "dl_gid"}, {&gcz_ctx::dl_recv, "dl_recv"}, {&gcz_ctx::dl_stage, "dl_stage"},
       {&gcz_ctx::dl_seg, "dl_seg"}, {&gcz_ctx::seg_w, "seg_w"}, {&gcz_ctx::seg_nf, "seg_nf"},
       {&gcz_ctx::seg_mu, "seg_mu"}, {&gcz_ctx::seg_in, "seg_in"}, {&gcz_ctx::nf_list, "nf_list"},
-      {&gcz_ctx::tcount, "tcount"}, {&gcz_ctx::ftab, "ftab"}, {&gcz_ctx::fsid, "fsid"},
+      {&gcz_ctx::tcount, "tcount"}, {&gcz_ctx::bkt_redo, "bkt_redo"}, {&gcz_ctx::ftab, "ftab"}, {&gcz_ctx::fsid, "fsid"},
       {&gcz_ctx::flkey, "flkey"}, {&gcz_ctx::flsid, "flsid"}};
   std::vector<unsigned char> band(gcz_ctx::kCanaryBytes);
   int bad = 0;

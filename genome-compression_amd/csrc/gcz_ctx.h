@@ -135,7 +135,6 @@ struct NodeLevel {
   u64* gate = nullptr;              // ... and open its gate (the next level's pcount)
   bool allow_bucket = false;        // single-device build: bucketed insert allowed (overflow -> rebuild)
   bool repetitive = false;          // ... the host knows the data is repetitive (no single-pass buckets)
-  bool nonrep = false;              // ... or not (the dense pack's probe): the bitmap dedupe (k_bkt_dedupe_bm)
   // fused small-build levels (k_node_insert with a resolver, gcz_device.h): this level's
   // table lives in ftab region k % 3, its repeats are settled by the next level's insert
   // unless it is the last one before the tail (resolve launched here)
@@ -248,6 +247,7 @@ struct gcz_ctx {
   bool part_wave = false;    // ... and whose collapse inserts a one-key wave once (GCZ_PART_WAVE=1;
                              // measured 0.14 ms slower on tandem_3g2, off)
   gcz_host::DevBuf nf_list;  // ... those repeats' positions (k_bkt_dedupe2)
+  gcz_host::DevBuf bkt_redo; // ... the buckets the bitmap dedupe hands to k_bkt_dedupe2 (k_bkt_dedupe_bm)
   bool tile_count = false;   // large flag scans: tile prefixes counted ahead, no look-back (GCZ_TILE_COUNT=1;
                              // measured 0.75 ms slower on tandem_3g2, neutral on uniform_1g: off)
   unsigned resolve_grid = 2048;   // node resolve: at most this many workgroups, striding (GCZ_RESOLVE_GRID;
@@ -257,9 +257,8 @@ struct gcz_ctx {
   int dense_mode = 1;        // dense leaf level (gcz_dense.h): 0 off, 1 on large pure-ACGT inputs, 2 any size (GCZ_DENSE)
   gcz_host::u64 dense_min = 1ull << 21;   // ... from this many strands (mode 1)
   bool dense_used = false;   // the last build's leaf level ran dense
-  bool dense_nonrep = false; // ... and its probe found the data not repetitive (read with its verdict)
-  bool dedupe_bm = true;     // two-pass levels of such data: k_bkt_dedupe_bm (GCZ_DEDUPE_BM=0: k_bkt_dedupe2)
-  bool dedupe_bm_all = false; // ... on every two-pass level, repetitive data too (GCZ_DEDUPE_BM=2, testing)
+  bool dedupe_bm = true;     // two-pass levels: the bitmap dedupe k_bkt_dedupe_bm (+ k_bkt_dedupe2 for the
+                             // buckets it hands back; GCZ_DEDUPE_BM=0: k_bkt_dedupe2 alone)
   // ... its code buckets (GCZ_DENSE_NB): 512 at L = 12 -- 2^14 codes per bucket (64 KB LDS tables,
   // two workgroups per CU) and runs of ~64 records per (chunk, bucket); 1024 measured 2.576 vs
   // 2.460 ms per 1 Gbase build (words 0.336 -> 0.308, first 0.257 -> 0.214, scatter 0.239 -> 0.208)

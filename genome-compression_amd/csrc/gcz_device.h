@@ -103,6 +103,7 @@ struct Header {
   u32 bkt_overflow;         // a node-level bucket exceeded the LDS dedupe (k_bkt_dedupe)
   u32 dense_fail;           // a strand is not pure ACGT: the dense leaf level does not apply (gcz_dense.h)
   u32 nnf;                  // two-pass level: its not-first positions (k_bkt_dedupe2), listed up to kNfListCap
+  u32 redo[GCZ_MAX_LAYERS]; // level k: buckets the bitmap dedupe handed to k_bkt_dedupe2 (k_bkt_dedupe_bm)
 };
 
 // A two-pass level with at most this many repeats (e.g. 13 of 41.7 M pairs on layer 0 of
@@ -1735,6 +1736,8 @@ struct Bkt2Plan {
   u32 wmarks;          // k_bkt_part writes every pair's not-first / multi mark (no k_clear pass)
   u32* nfl;            // k_bkt_dedupe2: the not-first positions (hdr->nnf counts them); null: none
   u32 wave1;           // k_bkt_part collapse: a wave of one key touches the table once (GCZ_PART_WAVE)
+  u32* redo;           // k_bkt_dedupe_bm: buckets over its capacity, for k_bkt_dedupe2_redo (null: the
+  u32* redo_cnt;       // overflow flag instead), appended at this cursor
 };
 
 // Append the not-first positions of a wave to bp.nfl (one atomic per wave; none once the
@@ -2086,12 +2089,12 @@ constexpr u32 kColSlots = 8192;   // its LDS table (load <= 1/2), in the part's 
 // positions = receive indices): every record of a repeated key gets the key's first index
 // in oslot (`rec`), instead of the not-first words pointing at it, and mk.nf is the reply
 // itself (k_own_reply_marks' flags: 7 not first, 6 the first of a repeated key, 0 else).
+// (dedupe2_bucket: the workgroup's bucket `bucket`; k_bkt_dedupe2 takes bucket = blockIdx.x,
+// k_bkt_dedupe2_redo the buckets the bitmap dedupe handed back)
 template <bool kOwner>
-__global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
-    const u64* __restrict__ recs, const u32* __restrict__ fo, Bkt2Plan bp, u32* __restrict__ rec, Marks mk,
-    Header* __restrict__ hdr, const u64* prev_count, u64 n, u32* __restrict__ ovf) {
-  if (bkt2_skip(hdr, prev_count, n)) return;
-  if (!kOwner && hdr->predup) bp.nfl = nullptr;   // (collapsed levels: the flag scan takes the look-back path)
+__device__ __forceinline__ void dedupe2_bucket(u32 bucket, const u64* __restrict__ recs, const u32* __restrict__ fo,
+                                               Bkt2Plan bp, u32* __restrict__ rec, Marks mk, Header* __restrict__ hdr,
+                                               u32* __restrict__ ovf) {
   constexpr u32 TS = kBktSlots;
   __shared__ u64 s_key[TS];
   __shared__ u32 s_pos[TS];
@@ -2099,7 +2102,7 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
   __shared__ u32 s_pre[513], s_beg[512];   // slices per coarse bucket <= 512
   __shared__ u32 s_wt[kBktThreads / 64];
   const u32 nb2 = 1u << bp.b2;
-  const u32 c = blockIdx.x >> bp.b2, f = blockIdx.x & (nb2 - 1);
+  const u32 c = bucket >> bp.b2, f = bucket & (nb2 - 1);
   const u32 ns = bp.nslice;
   {   // this bucket's run in every slice: loaded in parallel, block exclusive scan of the lengths
     const u32 t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -2273,15 +2276,39 @@ __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
   }
 }
 
-// The dedupe of non-repetitive data (the host read hdr->predup == 0 with the dense pack's verdict,
-// so the block collapse is off and a bucket's keys are nearly all distinct): k_bkt_dedupe2<false>'s
-// output from a quarter of its workgroup and a third of its LDS, so a CU holds six buckets in
-// flight instead of two (each bucket is a chain of dependent round trips: run offsets, records).
-// Equal keys share their low kBmLog bits (the record keys are bits of the level's key mix), so
-// only records whose bits another record of the bucket also set -- the "twice" bitmap, ~2 % of
-// them -- are hash-consed exactly, in a table of kBmSlots keys.  A bucket of more than
-// kBmItems * kBmThreads records or more such keys than the table holds sets the overflow flag
-// (the host rebuilds with the table path; non-repetitive data does not get there).
+template <bool kOwner>
+__global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2(
+    const u64* __restrict__ recs, const u32* __restrict__ fo, Bkt2Plan bp, u32* __restrict__ rec, Marks mk,
+    Header* __restrict__ hdr, const u64* prev_count, u64 n, u32* __restrict__ ovf) {
+  if (bkt2_skip(hdr, prev_count, n)) return;
+  if (!kOwner && hdr->predup) bp.nfl = nullptr;   // (collapsed levels: the flag scan takes the look-back path)
+  dedupe2_bucket<kOwner>(blockIdx.x, recs, fo, bp, rec, mk, hdr, ovf);
+}
+
+// The buckets k_bkt_dedupe_bm handed back (more records or repeated keys than it holds: hot keys
+// of repetitive data), each workgroup taking list entries in turn; an empty list exits at once.
+[[maybe_unused]] static __global__ __launch_bounds__(kBktThreads) void k_bkt_dedupe2_redo(
+    const u64* __restrict__ recs, const u32* __restrict__ fo, Bkt2Plan bp, u32* __restrict__ rec, Marks mk,
+    Header* __restrict__ hdr, const u64* prev_count, u64 n, u32* __restrict__ ovf) {
+  if (bkt2_skip(hdr, prev_count, n)) return;
+  const u32 cnt = *reinterpret_cast<volatile u32*>(bp.redo_cnt);
+  if (blockIdx.x >= cnt) return;
+  if (hdr->predup) bp.nfl = nullptr;
+  for (u32 i = blockIdx.x; i < cnt; i += gridDim.x) {
+    dedupe2_bucket<false>(bp.redo[i], recs, fo, bp, rec, mk, hdr, ovf);
+    __syncthreads();   // (the LDS table is the next bucket's)
+  }
+}
+
+// The two-pass levels' dedupe in a quarter of k_bkt_dedupe2's workgroup and a third of its LDS,
+// so a CU holds six buckets in flight instead of two (each bucket is a chain of dependent round
+// trips: run offsets, records).  Equal keys share their low kBmLog bits (the record keys are bits
+// of the level's key mix), so only records whose bits another record of the bucket also set --
+// the "twice" bitmap, ~2 % of them on non-repetitive data -- are hash-consed exactly, in a table
+// of kBmSlots keys.  A bucket of more than kBmItems * kBmThreads records or with more such keys
+// than the table holds (hot keys of repetitive data) is handed back untouched: to
+// k_bkt_dedupe2_redo through bp.redo (single device), else through the overflow flag (the fused
+// multi-rank schedule's owners: every rank falls back to the general schedule).
 constexpr int kBmThreads = 256;
 constexpr int kBmLog = 15;                   // seen / twice bitmaps of 2^15 bits (4 KB each)
 constexpr u32 kBmSlots = 1024;               // the candidates' keys (12 KB)
@@ -2349,8 +2376,14 @@ __global__ __launch_bounds__(kBmThreads) void k_bkt_dedupe_bm(const u64* __restr
   }
   __syncthreads();
   const u32 total = s_pre[ns];
+  auto hand_back = [&] {   // (nothing of this bucket written yet)
+    if (t == 0) {
+      if (!kOwner && bp.redo) bp.redo[atomicAdd(bp.redo_cnt, 1u)] = blockIdx.x;
+      else *ovf = 1;
+    }
+  };
   if (total > u32(kBktCap)) {
-    if (t == 0) *ovf = 1;
+    hand_back();
     return;
   }
   for (u32 s2 = t; s2 < ns; s2 += kBmThreads)
@@ -2409,7 +2442,7 @@ __global__ __launch_bounds__(kBmThreads) void k_bkt_dedupe_bm(const u64* __restr
   }
   __syncthreads();
   if (s_full) {
-    if (t == 0) *ovf = 1;
+    hand_back();
     return;
   }
 #pragma unroll
