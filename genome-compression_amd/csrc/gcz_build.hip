@@ -1023,6 +1023,8 @@ int gcz_ctx::build(const void* d_bases, const u64* d_leaves, u64 nbases, u64 S, 
   info.bucketed_pairs = h_hdr->hashed[1];
   info.leaf_path = dense_used ? 1u : 0u;
   info.repetitive = h_hdr->predup;
+  info.handed_back = 0;
+  for (int k = 0; k < GCZ_MAX_LAYERS; ++k) info.handed_back += h_hdr->redo[k];
   return GCZ_OK;
 }
 

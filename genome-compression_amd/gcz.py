@@ -36,7 +36,8 @@ class _Info(ctypes.Structure):
                 ("layer_size", ctypes.c_uint64 * MAX_LAYERS), ("error_offset", ctypes.c_uint64),
                 ("error_symbol", ctypes.c_int), ("build_ms", ctypes.c_double), ("hashed_pairs", ctypes.c_uint64),
                 ("bucketed_pairs", ctypes.c_uint64), ("leaf_path", ctypes.c_uint32), ("attempts", ctypes.c_uint32),
-                ("build_ms_all", ctypes.c_double), ("repetitive", ctypes.c_uint32)]
+                ("build_ms_all", ctypes.c_double), ("repetitive", ctypes.c_uint32),
+                ("handed_back", ctypes.c_uint32)]
 
 
 if not os.path.exists(LIB_PATH):
@@ -325,7 +326,7 @@ def _info_dict(i):
             "n_strands": i.n_strands, "n_leaves": i.n_leaves,
             "layer_size": [int(i.layer_size[k]) for k in range(i.n_layers)],
             "error_offset": i.error_offset, "error_symbol": i.error_symbol, "build_ms": i.build_ms,
-            "hashed_pairs": i.hashed_pairs, "bucketed_pairs": i.bucketed_pairs, "leaf_path": i.leaf_path, "repetitive": i.repetitive,
+            "hashed_pairs": i.hashed_pairs, "bucketed_pairs": i.bucketed_pairs, "leaf_path": i.leaf_path, "repetitive": i.repetitive, "handed_back": i.handed_back,
             "attempts": i.attempts, "build_ms_all": i.build_ms_all}
 
 

@@ -71,6 +71,8 @@ typedef struct {
   double build_ms_all;               /* device time of every attempt (build_ms: the last one) */
   uint32_t repetitive;               /* the node levels took the repetitive-data path (LDS pre-dedupe;
                                         decided by a probe of the first leaf chunk) */
+  uint32_t handed_back;              /* dedupe buckets the bitmap kernel handed to the table kernel
+                                        (hot keys; all levels of the last attempt) */
 } gcz_info;
 
 /* ---- device context ---------------------------------------------------- */
