@@ -418,24 +418,29 @@ def test_gpu_bitmap_dedupe_goldens(name, ctx_dense_bucket, gcz, manifest):
     assert compare_digest(gcz.digest(ctx_dense_bucket.tree()), exp) == {}
 
 
-@pytest.mark.parametrize("dups", [0, 200, 20_000, 400_000])
+@pytest.mark.parametrize("dups", [0, 200, 20_000, 400_000, 700_000, "hot"])
 def test_gpu_bitmap_dedupe_repeats_oracle(dups, ctx_dense_bucket, gcz, oracle):
     """Random ACGT leaves with `dups` copied layer-0 pairs spread over the genome (true repeats
     the bitmaps must route to the exact table: first occurrence, multi, not-first ids) -- up to
-    buckets whose repeated keys overflow the candidates' table (the overflow flag: the host
-    rebuilds with the table path).  Equal to the C oracle."""
-    rng = np.random.default_rng(900 + dups)
+    buckets with more repeated keys than the candidates' table holds (700 K) and one pair copied
+    6000 times (a bucket over the kernel's record capacity): those buckets are handed to
+    k_bkt_dedupe2 in the same build (no rebuild).  Equal to the C oracle."""
+    rng = np.random.default_rng(900 + (dups if dups != "hot" else 1))
     L, S = 12, 2_400_002
     acgt = np.array([1, 2, 4, 8], dtype=np.uint64)
     codes = rng.integers(0, 4, size=(S, L))
     leaves = (acgt[codes] << (4 * np.arange(L, dtype=np.uint64))).sum(axis=1).astype(np.uint64)
-    if dups:
+    if dups == "hot":
+        dst = rng.choice(S // 2, size=6000, replace=False)
+        leaves[2 * dst] = leaves[0]
+        leaves[2 * dst + 1] = leaves[1]
+    elif dups:
         src = rng.integers(0, S // 2, size=dups)
         dst = rng.integers(0, S // 2, size=dups)
         leaves[2 * dst] = leaves[2 * src]
         leaves[2 * dst + 1] = leaves[2 * src + 1]
     info = ctx_dense_bucket.build_leaves(leaves, L)
-    if dups == 400_000:   # (~800 repeated keys a bucket: the bitmap kernel hands buckets back)
+    if dups in (700_000, "hot"):   # (the bitmap kernel hands buckets back; no rebuild)
         assert info["handed_back"] > 0 and info["attempts"] == 1, info
     g = ctx_dense_bucket.tree()
     o = oracle.build_leaves(leaves, L)
