@@ -422,16 +422,16 @@ def test_gpu_bitmap_dedupe_goldens(name, ctx_dense_bucket, gcz, manifest):
 def test_gpu_bitmap_dedupe_repeats_oracle(dups, ctx_dense_bucket, gcz, oracle):
     """Random ACGT leaves with `dups` copied layer-0 pairs spread over the genome (true repeats
     the bitmaps must route to the exact table: first occurrence, multi, not-first ids) -- up to
-    ~700 repeated keys a bucket (700 K) and one pair copied 6000 times (a bucket over the kernel's
-    record capacity: handed to k_bkt_dedupe2 in the same build, no rebuild).  Equal to the C
-    oracle."""
+    ~700 repeated keys a bucket (700 K) and one pair copied 4000 times (a bucket over the kernel's
+    record capacity: handed to k_bkt_dedupe2 in the same build, no rebuild; 6000 copies overflow
+    a fine-pass slice, which rebuilds with the table as before).  Equal to the C oracle."""
     rng = np.random.default_rng(900 + (dups if dups != "hot" else 1))
     L, S = 12, 2_400_002
     acgt = np.array([1, 2, 4, 8], dtype=np.uint64)
     codes = rng.integers(0, 4, size=(S, L))
     leaves = (acgt[codes] << (4 * np.arange(L, dtype=np.uint64))).sum(axis=1).astype(np.uint64)
     if dups == "hot":
-        dst = rng.choice(S // 2, size=6000, replace=False)
+        dst = rng.choice(S // 2, size=4000, replace=False)
         leaves[2 * dst] = leaves[0]
         leaves[2 * dst + 1] = leaves[1]
     elif dups:
