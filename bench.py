@@ -141,8 +141,9 @@ def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None, bu
         return S // 8 + S // 16
     if kernel == "dl_ids":          # first positions in, two random rank reads per key, id per record out
         return 4 * C + 8 * S + 128 * U
-    if kernel == "dl_words":        # record, id, pre-word, bitmap in; word and the leaves out
-        return 16 * S + S // 8 + 8 * U
+    if kernel == "dl_words":        # record and id in (k_dl_ids' final word), the chunk's first-occurrence
+        # bitmap in; word and the leaves out (no pre-word: rounds 2-5 charged 4 B per strand for one)
+        return 12 * S + S // 8 + 8 * U
     if kernel == "flagscan_leaf":   # not-first marks; firsts: word, slot sector, leaf out, slot->id sector
         return S + U * (4 + 64 + 8 + 64 + 4)
     lv = list(zip(pk, layer_sizes))[:launches] if launches is not None else list(zip(pk, layer_sizes))
@@ -184,7 +185,7 @@ def dist_rank_bytes(kernel, L, Sr, r, R, c_r, u_r, n_leaves):
     if kernel == "dl_ids":          # bitmaps of ranks <= r, relayed G reads per held code, record -> word
         return (r + 1) * C // 8 + 4 * min(n_leaves, Sr) + 8 * Sr + (Sr // 8 + 8 * c_r)
     if kernel == "dl_words":        # record, id in; word out
-        return 16 * Sr + Sr // 8
+        return 12 * Sr + Sr // 8
     if kernel == "node_insert":     # k_node_keys: pre-word pairs in; canonical pair, word, marks out
         return 24 * pr
     if kernel == "dist_bucket":     # canonical pair, marks, word in; key and index out
