@@ -318,7 +318,7 @@ def stream_digest(group, dist, rank, world, info):
     return {"sha_leaves_bin": h_leaves.hexdigest(), "sha_layers_bin": h_layers.hexdigest()}
 
 
-LEAF_SCOPES = ("leaf_insert", "flagscan_leaf", "resolve_leaf", "dl_pack", "dl_scan", "dl_scatter", "dl_first",
+LEAF_SCOPES = ("leaf_insert", "flagscan_leaf", "resolve_leaf", "dl_pack", "dl_probe", "dl_scan", "dl_scatter", "dl_first",
                "dl_fbscan", "dl_ids", "dl_words")
 
 

@@ -100,6 +100,7 @@ enum KernelId {
   KID_EXCHANGE, KID_DIST, KID_OWNER, KID_IDS, KID_REMAP, KID_TAIL, KID_SORT, KID_DAG, KID_DIRECT,
   KID_BKT_COUNT, KID_BKT_SCAN, KID_BKT_SCATTER, KID_BKT_DEDUPE, KID_BKT_FINE,
   KID_DL_PACK, KID_DL_SCAN, KID_DL_SCATTER, KID_DL_FIRST, KID_DL_FBSCAN, KID_DL_IDS, KID_DL_WORDS, KID_L0, KID_MARK,
+  KID_DL_PROBE,
   KID_COUNT
 };
 inline const char* kernel_name(int k) {
@@ -108,7 +109,7 @@ inline const char* kernel_name(int k) {
                                          "dist_owner", "dist_ids", "dist_remap", "tail", "sort", "dag_write", "direct_levels",
                                          "bucket_count", "bucket_scan", "bucket_scatter", "bucket_dedupe", "bucket_fine",
                                          "dl_pack", "dl_scan", "dl_scatter", "dl_first", "dl_fbscan", "dl_ids",
-                                         "dl_words", "dist_l0", "mark"};
+                                         "dl_words", "dist_l0", "mark", "dl_probe"};
   return names[k];
 }
 

@@ -28,10 +28,11 @@ def short(name):
 NAMES = {"k_leaf_bases": "leaf_insert", "k_leaf_packed": "leaf_insert", "k_node_insert": "node_insert",
          "k_flagscan_leaf": "flagscan_leaf", "k_flagscan_node": "flagscan_node", "k_resolve_leaf": "resolve_leaf",
          "k_resolve_node": "resolve_node", "k_clear": "clear", "__amd_rocclr_fillBufferAligned": "clear",
-         "k_tail": "tail", "k_direct_levels": "direct_levels", "k_dup_probe": "leaf_insert",
-         "k_dup_decide": "leaf_insert", "k_bkt_count": "bucket_count", "k_bkt_scatter": "bucket_scatter",
+         "k_tail": "tail", "k_direct_levels": "direct_levels", "k_dup_probe": "dl_probe",
+         "k_dup_decide": "dl_probe", "k_bkt_count": "bucket_count", "k_bkt_scatter": "bucket_scatter",
          "k_bkt_dedupe": "bucket_dedupe", "k_bkt_part": "bucket_scatter", "k_bkt_fine": "bucket_fine",
-         "k_bkt_dedupe2": "bucket_dedupe", "k_build_init": "clear", "k_build_finish": "clear",
+         "k_bkt_dedupe2": "bucket_dedupe", "k_bkt_dedupe_bm": "bucket_dedupe", "k_bkt_dedupe2_redo": "bucket_dedupe",
+         "k_build_init": "clear", "k_build_finish": "clear",
          "k_dl_pack": "dl_pack", "k_dl_scatter": "dl_scatter", "k_dl_first": "dl_first", "k_dl_fb": "dl_first",
          "k_dl_ids": "dl_ids", "k_dl_words": "dl_words"}
 
