@@ -199,6 +199,7 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
   P = DensePlan{};
   P.S = S;
   P.L = L;
+  P.xcd = dl_xcd;
   P.nch = u32((S + kDC - 1) / kDC);
   P.cmask = u32((1ull << (2 * L)) - 1);
   const u32 cbits = dense_code_bits(L);
@@ -241,6 +242,8 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
     launch_dl_pack<false>(int(L), dim3(P.nch), stream, nullptr, a.leaves, P, dl_pw.as<u32>(), dl_cnt.as<u32>(),
                           d_hdr, static_cast<uint4*>(dl_desc.ptr), nz16);
   HIP_TRY(hipGetLastError());
+  prof_end(KID_DL_PACK, e0);
+  prof_begin(KID_DL_PROBE, e0);
   // repetitive data? (the node inserts' LDS pre-dedupe): in-block repeats of a sample's
   // hashed codes (equal codes <=> equal keys)
   // (a rank of an R-rank build samples the first 1/R of that, at least 2^18, of its own
@@ -256,7 +259,7 @@ int gcz_ctx::dense_phase_a(const LeafLevel& a, Header* d_hdr, u64* ucount, bool 
     HIP_TRY(hipMemcpyAsync(&h_hdr->dense_fail, &d_hdr->dense_fail, 4, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipEventRecord(ev_dfail, stream));
   }
-  prof_end(KID_DL_PACK, e0);
+  prof_end(KID_DL_PROBE, e0);
   if (pack_only) {   // (the fused multi-rank schedule queues its own work before the rest)
     *used = true;
     return GCZ_OK;
@@ -1073,6 +1076,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   c->stream = c->own_stream;
   if (const char* t = std::getenv("GCZ_CANARY")) c->canary = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_DEDUPE_BM")) c->dedupe_bm = std::atoi(t) != 0;
+  if (const char* t = std::getenv("GCZ_DL_XCD")) c->dl_xcd = u32(std::strtoul(t, nullptr, 10));
   if (const char* t = std::getenv("GCZ_DENSE_NB")) c->dense_nb = u32(std::strtoul(t, nullptr, 10));
   if (const char* t = std::getenv("GCZ_TABLE")) c->force_wide = std::strcmp(t, "wide") == 0;
   if (const char* t = std::getenv("GCZ_NODE_CAP_SHIFT")) c->node_cap_shift = std::atoi(t);

@@ -264,6 +264,10 @@ struct gcz_ctx {
   // two workgroups per CU) and runs of ~64 records per (chunk, bucket); 1024 measured 2.576 vs
   // 2.460 ms per 1 Gbase build (words 0.336 -> 0.308, first 0.257 -> 0.214, scatter 0.239 -> 0.208)
   gcz_host::u32 dense_nb = 512;
+  // ... its chunk kernels walking XCD-contiguous chunk runs (GCZ_DL_XCD: DensePlan::xcd bits): the
+  // scatter only -- measured 0.193 against 0.207 ms; words 0.488 against 0.307 and first (whose
+  // input the scatter writes) 0.296 against 0.213 ms with every chunk kernel mapped
+  gcz_host::u32 dl_xcd = 2;
   bool use_graph = true;     // small builds as a replayed HIP graph       (GCZ_GRAPH=0 disables)
   bool use_fused = true;     // small builds: two launches per node level  (GCZ_FUSED=0 disables)
   int small_cap_shift = 2;   // ... and tables 2^this times the usual size: short probe chains (GCZ_SMALL_CAP_SHIFT)

@@ -57,7 +57,19 @@ struct DensePlan {
   // the fused multi-rank schedule's sort and first pass, queued before its mid-build read: they
   // return at once when the pack found repetitive or non-ACGT data (that attempt is discarded)
   const Header* gate;
+  u32 xcd;     // chunk kernels taking the XCD-contiguous chunk order (dl_chunk): bit 0 pack,
+               // 1 scatter, 2 fb, 3 words; clear: chunk = block
 };
+
+// Chunk of a chunk kernel's workgroup (grid = nch).  Workgroups are dealt round-robin over the
+// 8 XCDs, so with P.xcd each XCD takes a contiguous run of chunks, walked in order: the runs
+// (chunk, bucket) and (chunk + 1, bucket) that share a line at their boundary, and the pack's
+// count-matrix entries of neighbouring chunks, meet in one XCD's L2 instead of two.
+template <u32 kBit>
+__device__ __forceinline__ u32 dl_chunk(const DensePlan& P) {
+  const u32 b = blockIdx.x, per = P.nch / 8;
+  return (P.xcd & kBit) && b < 8 * per ? (b % 8) * per + b / 8 : b;
+}
 
 // The fused schedule's 6-byte layer-0 records (gcz_dist_fast.h): the canonical pair re-labelled
 // by the children's canonical 2-bit codes -- a dna::canonical code is the minimum of its orbit,
@@ -226,7 +238,8 @@ template <int L, bool kBases>
     zdesc[i] = make_uint4(0, 0, 0, 0);
   if (tid < 256) s_lut[tid] = (signed char)acgt_code(tid);
   for (u32 b = tid; b < P.NB; b += kDThreads) s_hist[b] = 0;
-  const u64 c0 = u64(blockIdx.x) * kDC;
+  const u32 ch = dl_chunk<1>(P);
+  const u64 c0 = u64(ch) * kDC;
   const u32 ib = P.IB;
   bool fail = false;
   __syncthreads();
@@ -294,7 +307,7 @@ template <int L, bool kBases>
   }
   if (__ballot(fail) && (tid & 63) == 0) atomicOr(&hdr->dense_fail, 1u);
   __syncthreads();
-  for (u32 b = tid; b < P.NB; b += kDThreads) cnt[u64(b) * P.nch + blockIdx.x] = s_hist[b];
+  for (u32 b = tid; b < P.NB; b += kDThreads) cnt[u64(b) * P.nch + ch] = s_hist[b];
 }
 
 // Scatter: records (h's low IB bits << kDLog | position in chunk, the pre-word's m/t/v in
@@ -311,7 +324,7 @@ template <int L, bool kBases>
   u32* s_dst = s_cur + kDNBMax;         // NB: global run starts
   u32* s_tmp = s_dst + kDNBMax;         // 16
   const int tid = threadIdx.x;
-  const u32 ch = blockIdx.x;
+  const u32 ch = dl_chunk<2>(P);
   const u64 c0 = u64(ch) * kDC;
   const u32 n = u32(P.S - c0 < u64(kDC) ? P.S - c0 : u64(kDC));
   u32 h[kDC / kDThreads];   // pre-words: hashed code | m/t/v
@@ -494,7 +507,7 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
                                                      DensePlan P, unsigned long long* __restrict__ fb) {
   __shared__ u32 s_bits[kDC / 32];
   const int tid = threadIdx.x;
-  const u32 ch = blockIdx.x, RB = 1u << P.IB;
+  const u32 ch = dl_chunk<4>(P), RB = 1u << P.IB;
   for (u32 w = tid; w < kDC / 32; w += kDThreads) s_bits[w] = 0;
   __syncthreads();
   for (u32 b = tid; b < P.NB; b += kDThreads) {
@@ -585,7 +598,7 @@ static __device__ __forceinline__ void dl_words_chunk(const u32* __restrict__ re
   u32* s_fb = s_tmp + 16;            // kDC / 32 first-occurrence bits of the chunk
   u32* s_ex = s_fb + kDC / 32;       // kDC / 64: the run of each 64-record group's first record
   const int tid = threadIdx.x;
-  const u32 ch = blockIdx.x;
+  const u32 ch = dl_chunk<8>(P);
   const u64 c0 = u64(ch) * kDC;
   const u32 n = u32(P.S - c0 < u64(kDC) ? P.S - c0 : u64(kDC));
   if (leaves_out)
