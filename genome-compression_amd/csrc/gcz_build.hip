@@ -340,6 +340,12 @@ int gcz_ctx::dense_phase_a3(Header* d_hdr, u64* ucount, bool list, u64* vec, u32
                      ScanPopc{dl_fb.as<unsigned long long>()}, nfb, dl_wpre.as<u32>(), sdesc + t_cnt, &tickets[1],
                      ucount);
   HIP_TRY(hipGetLastError());
+  if (dl_fbw_on) {
+    if (int rc = ensure(dl_fbw, nfb * 16 + 16)) return rc;
+    hipLaunchKernelGGL(k_dl_fbw, dim3(unsigned((nfb + 255) / 256)), dim3(256), 0, stream, dl_fb.as<unsigned long long>(),
+                       dl_wpre.as<u32>(), nfb, static_cast<uint4*>(dl_fbw.ptr));
+    HIP_TRY(hipGetLastError());
+  }
   prof_end(KID_DL_FBSCAN, e0);
   return GCZ_OK;
 }
@@ -355,7 +361,8 @@ int gcz_ctx::dense_phase_b(const LeafLevel& a, Header* d_hdr, const u32* gid, u6
   if (!ids_done) {   // (multi-rank: k_dl_ids_mr wrote the final words per record)
     prof_begin(KID_DL_IDS, e0);
     hipLaunchKernelGGL(k_dl_ids, dim3(P.NB), dim3(kDThreads), RBbytes, stream, dl_rec.as<u32>(), dl_off.as<u32>(), P,
-                       dl_fpg.as<u32>(), dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), gid, dl_idrec.as<u32>());
+                       dl_fpg.as<u32>(), dl_fb.as<unsigned long long>(), dl_wpre.as<u32>(), gid, dl_idrec.as<u32>(),
+                       dl_fbw_on && !gid ? static_cast<const uint4*>(dl_fbw.ptr) : nullptr);
     HIP_TRY(hipGetLastError());
     prof_end(KID_DL_IDS, e0);
   }
@@ -1076,6 +1083,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   c->stream = c->own_stream;
   if (const char* t = std::getenv("GCZ_CANARY")) c->canary = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_DEDUPE_BM")) c->dedupe_bm = std::atoi(t) != 0;
+  if (const char* t = std::getenv("GCZ_DL_FBW")) c->dl_fbw_on = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_DL_XCD")) c->dl_xcd = u32(std::strtoul(t, nullptr, 10));
   if (const char* t = std::getenv("GCZ_DENSE_NB")) c->dense_nb = u32(std::strtoul(t, nullptr, 10));
   if (const char* t = std::getenv("GCZ_TABLE")) c->force_wide = std::strcmp(t, "wide") == 0;
@@ -1113,7 +1121,7 @@ void gcz_ctx_destroy(gcz_ctx* c) {
   gcz_ingest_state_free(c);
   for (DevBuf* b : {&c->wa, &c->wb, &c->grp, &c->desc, &c->tab, &c->leaves_out, &c->nodes_out, &c->hdr, &c->input,
                     &c->nf, &c->multi, &c->stats, &c->bkt_key, &c->bkt_cnt, &c->bkt_off, &c->bkt_tmp, &c->bkt_rec2, &c->dl_pw,
-                    &c->dl_rec, &c->dl_idrec, &c->dl_cnt, &c->dl_off, &c->dl_offt, &c->dl_fpg, &c->dl_fb, &c->dl_wpre,
+                    &c->dl_rec, &c->dl_idrec, &c->dl_cnt, &c->dl_off, &c->dl_offt, &c->dl_fpg, &c->dl_fb, &c->dl_wpre, &c->dl_fbw,
                     &c->dl_desc, &c->dl_fl, &c->dl_fo, &c->dl_lh, &c->dl_pb, &c->dl_pbs, &c->dl_lower,
                     &c->dl_pos, &c->dl_list, &c->dl_gid, &c->dl_recv, &c->dl_stage, &c->dl_seg, &c->seg_w,
                     &c->seg_nf, &c->seg_mu, &c->seg_in, &c->nf_list, &c->tcount, &c->bkt_redo})
@@ -1147,7 +1155,7 @@ extern "C++" int gcz_canary_scan(gcz_ctx* c, std::string& out) {
       {&gcz_ctx::bkt_off, "bkt_off"}, {&gcz_ctx::bkt_tmp, "bkt_tmp"}, {&gcz_ctx::bkt_rec2, "bkt_rec2"},
       {&gcz_ctx::dl_pw, "dl_pw"}, {&gcz_ctx::dl_rec, "dl_rec"}, {&gcz_ctx::dl_idrec, "dl_idrec"},
       {&gcz_ctx::dl_cnt, "dl_cnt"}, {&gcz_ctx::dl_off, "dl_off"}, {&gcz_ctx::dl_offt, "dl_offt"},
-      {&gcz_ctx::dl_fpg, "dl_fpg"}, {&gcz_ctx::dl_fb, "dl_fb"}, {&gcz_ctx::dl_wpre, "dl_wpre"},
+      {&gcz_ctx::dl_fpg, "dl_fpg"}, {&gcz_ctx::dl_fb, "dl_fb"}, {&gcz_ctx::dl_wpre, "dl_wpre"}, {&gcz_ctx::dl_fbw, "dl_fbw"},
       {&gcz_ctx::dl_desc, "dl_desc"}, {&gcz_ctx::dl_fl, "dl_fl"}, {&gcz_ctx::dl_fo, "dl_fo"},
       {&gcz_ctx::dl_lh, "dl_lh"}, {&gcz_ctx::dl_pb, "dl_pb"}, {&gcz_ctx::dl_pbs, "dl_pbs"},
       {&gcz_ctx::dl_lower, "dl_lower"}, {&gcz_ctx::dl_pos, "dl_pos"}, {&gcz_ctx::dl_list, "dl_list"},

@@ -216,6 +216,7 @@ struct gcz_ctx {
   gcz_host::DevBuf stats;   // hashed-pair counter shards (k_node_insert), summed into hdr->hashed[0]
   gcz_host::DevBuf bkt_key, bkt_cnt, bkt_off, bkt_tmp, bkt_rec2;   // bucketed node insert (k_bkt_*)
   gcz_host::DevBuf dl_pw, dl_rec, dl_idrec, dl_cnt, dl_off, dl_offt, dl_fpg, dl_fb, dl_wpre, dl_desc, dl_fl, dl_fo;   // dense leaf level
+  gcz_host::DevBuf dl_fbw;   // ... the bitmap interleaved with its prefix (k_dl_fbw; single device)
   // ... multi-rank: rfc (dl_lh), presence bitmaps (own, gathered), bucket counts + exchange vector (dl_pos),
   // gathered exchange vectors (dl_lower), G (dl_list), relay table (dl_gid), relay buffers, status words
   gcz_host::DevBuf dl_lh, dl_pb, dl_pbs, dl_lower, dl_pos, dl_list, dl_gid, dl_recv, dl_stage, dl_seg;
@@ -268,6 +269,8 @@ struct gcz_ctx {
   // scatter only -- measured 0.193 against 0.207 ms; words 0.488 against 0.307 and first (whose
   // input the scatter writes) 0.296 against 0.213 ms with every chunk kernel mapped
   gcz_host::u32 dl_xcd = 2;
+  bool dl_fbw_on = true;      // k_dl_ids ranks through the interleaved bitmap (GCZ_DL_FBW=0: two lines a rank;
+                              // measured ids 0.182 -> 0.164 ms for +7 us of interleaving)
   bool use_graph = true;     // small builds as a replayed HIP graph       (GCZ_GRAPH=0 disables)
   bool use_fused = true;     // small builds: two launches per node level  (GCZ_FUSED=0 disables)
   int small_cap_shift = 2;   // ... and tables 2^this times the usual size: short probe chains (GCZ_SMALL_CAP_SHIFT)

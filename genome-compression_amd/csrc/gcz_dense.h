@@ -443,20 +443,27 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
     if (s_fp[idx] > pos) atomicMin(&s_fp[idx], pos);
   });
   __syncthreads();
-  constexpr int PER = 16;   // codes per thread (RB <= 16 Ki)
-  u32 fp[PER], rk[PER];
+  // 16 codes per thread (RB <= 16 Ki).  The first positions stay in LDS (s_fp is only read from
+  // here on) and each code's rank among the bucket's first positions of its chunk (< kDC) takes
+  // half a register: the kernel fits 64 VGPRs, two workgroups per CU (fp[16] and rk[16] in
+  // registers took 78, one per CU; measured the same 0.210 ms at 1 Gbase either way)
+  constexpr int PER = 16;
+  auto fp_of = [&](int k) { const u32 i = u32(k) * kDThreads + tid; return i < RB ? s_fp[i] : ~0u; };
+  u32 rk2[PER / 2];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const u32 i = u32(k) * kDThreads + tid;
-    fp[k] = i < RB ? s_fp[i] : ~0u;
-    if (fpg && i < RB) fpg[u64(b) * RB + i] = fp[k];
-    rk[k] = fl && fp[k] != ~0u ? atomicAdd(&s_cnt[fp[k] >> kDLog], 1u) : 0u;
+    const u32 fp = fp_of(k);
+    if (fpg && i < RB) fpg[u64(b) * RB + i] = fp;
+    const u32 rk = fl && fp != ~0u ? atomicAdd(&s_cnt[fp >> kDLog], 1u) : 0u;
+    if (k & 1) rk2[k >> 1] |= rk << 16;
+    else rk2[k >> 1] = rk;
     if (pb) {
       const u32 h = (b << P.IB) | i;
       if (RB >= 64) {
-        const u64 m = __ballot(fp[k] != ~0u);
+        const u64 m = __ballot(fp != ~0u);
         if ((tid & 63) == 0 && i < RB) pb[h >> 6] = m;
-      } else if (fp[k] != ~0u) {
+      } else if (fp != ~0u) {
         atomicOr(&pb[h >> 6], 1ull << (h & 63));
       }
     }
@@ -467,7 +474,7 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
     u64 m[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      m[k] = __ballot(fp[k] != ~0u);
+      m[k] = __ballot(fp_of(k) != ~0u);
       if (lane == 0) s_wc[k * (kDThreads / 64) + wave] = u32(__popcll(m[k]));
     }
     __syncthreads();
@@ -477,8 +484,10 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
     __syncthreads();
     const u64 lt = (1ull << lane) - 1ull;
 #pragma unroll
-    for (int k = 0; k < PER; ++k)
-      if (fp[k] != ~0u) rfc[u64(b) * RB + s_wc[k * (kDThreads / 64) + wave] + u32(__popcll(m[k] & lt))] = fp[k];
+    for (int k = 0; k < PER; ++k) {
+      const u32 fp = fp_of(k);
+      if (fp != ~0u) rfc[u64(b) * RB + s_wc[k * (kDThreads / 64) + wave] + u32(__popcll(m[k] & lt))] = fp;
+    }
     if (tid == 0) bcnt[b] = total;
   }
   if (!fl) return;
@@ -497,8 +506,10 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < PER; ++k)
-    if (fp[k] != ~0u) fl[u64(b) * RB + s_cnt[fp[k] >> kDLog] + rk[k]] = fp[k];
+  for (int k = 0; k < PER; ++k) {
+    const u32 fp = fp_of(k);
+    if (fp != ~0u) fl[u64(b) * RB + s_cnt[fp >> kDLog] + ((rk2[k >> 1] >> (16 * (k & 1))) & 0xffffu)] = fp;
+  }
 }
 
 // First-occurrence bitmap of one chunk: its first positions from every bucket's
@@ -536,6 +547,22 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
   return wpre[p >> 6] + u32(__popcll(w & ((1ull << (p & 63)) - 1ull)));
 }
 
+// The first-occurrence bitmap word and its popcount prefix side by side (16 B per 64 positions:
+// {word lo, word hi, prefix, 0}), so a rank is one random line instead of two (k_dl_ids).
+[[maybe_unused]] static __global__ __launch_bounds__(256) void k_dl_fbw(const unsigned long long* __restrict__ fb,
+                                                                       const u32* __restrict__ wpre, u64 nfb,
+                                                                       uint4* __restrict__ fbw) {
+  const u64 w = u64(blockIdx.x) * 256 + threadIdx.x;
+  if (w >= nfb) return;
+  const unsigned long long b = fb[w];
+  fbw[w] = make_uint4(u32(b), u32(b >> 32), wpre[w], 0u);
+}
+static __device__ __forceinline__ u32 fbw_rank(const uint4* __restrict__ fbw, u32 p) {
+  const uint4 v = fbw[p >> 6];
+  const unsigned long long w = (u64(v.y) << 32) | v.x;
+  return v.z + u32(__popcll(w & ((1ull << (p & 63)) - 1ull)));
+}
+
 // Ids: per bucket, the id of each present code (rank of its first position)
 // in LDS, then one final word (id | the record's m/t/v) per record in bucket order.
 // gid (multi-rank build): the GLOBAL id of every code present on this rank,
@@ -544,7 +571,7 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
                                                       DensePlan P, const u32* __restrict__ fpg,
                                                       const unsigned long long* __restrict__ fb,
                                                       const u32* __restrict__ wpre, const u32* __restrict__ gid,
-                                                      u32* __restrict__ idrec) {
+                                                      u32* __restrict__ idrec, const uint4* __restrict__ fbw = nullptr) {
   extern __shared__ u32 s_id[];
   const int tid = threadIdx.x;
   const u32 b = blockIdx.x, RB = 1u << P.IB;
@@ -558,7 +585,7 @@ static __device__ __forceinline__ u32 fb_rank(const unsigned long long* __restri
 #pragma unroll
     for (int j = 0; j < kDBatch; ++j) {
       const u32 i = i0 + u32(j) * kDThreads + tid;
-      if (i < RB) s_id[i] = gid ? fp[j] : fp[j] != ~0u ? fb_rank(fb, wpre, fp[j]) : 0u;
+      if (i < RB) s_id[i] = gid ? fp[j] : fp[j] == ~0u ? 0u : fbw ? fbw_rank(fbw, fp[j]) : fb_rank(fb, wpre, fp[j]);
     }
   }
   __syncthreads();
@@ -629,7 +656,7 @@ static __device__ __forceinline__ void dl_words_chunk(const u32* __restrict__ re
     }
     __syncthreads();
     const u32 ng = (nrec + 63) >> 6;
-    constexpr int GW = 8;   // groups per wave step (2 loads each in flight per lane)
+    constexpr int GW = 8;   // groups per wave step (2 loads each in flight per lane; 16: -4 us, 32: +14 us)
     for (u32 g0 = wave; g0 < ng; g0 += (kDThreads / 64) * GW) {
       u32 x[GW], w[GW], bq[GW];
 #pragma unroll
