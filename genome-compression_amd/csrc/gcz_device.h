@@ -644,6 +644,9 @@ struct InitPlan {
   // fused small-build levels: the first node level's table (ones) and marks (zero)
   uint4* ftab;  u64 nftab16;
   uint4* fnf;   uint4* fmulti; u64 nfm16;
+  // further zeroed regions (the fused multi-rank schedule's header, look-back words and C / D
+  // slots: no memset launch each)
+  uint4* zero[4]; u64 nzero16[4];
 };
 
 [[maybe_unused]] static __global__ __launch_bounds__(kBlock) void k_build_init(InitPlan ip) {
@@ -663,6 +666,9 @@ struct InitPlan {
     ip.fnf[i] = z;
     ip.fmulti[i] = z;
   }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    for (u64 i = t; i < ip.nzero16[k]; i += st) ip.zero[k][i] = z;
 }
 
 // Build end in one launch: the root word (when the level loop, not k_tail, ended the

@@ -1110,7 +1110,7 @@ int gcz_group::alloc(int i, u64 leaf_cap) {
   if ((rc = c->ensure(d.scval, u * 8))) return rc;
   if ((rc = c->ensure(d.sdval, u * 8))) return rc;
   if ((rc = c->ensure(d.clist, u * 4))) return rc;
-  if ((rc = c->ensure(d.dhdr, sizeof(DistHdr)))) return rc;
+  if ((rc = c->ensure(d.dhdr, kDistHdrBytes))) return rc;
   if ((rc = c->ensure(d.gath, size_t(world) * kSyncWords * 8))) return rc;
   if ((rc = c->ensure(d.gath2, size_t(world) * (2 + 2 * kMaxRanks) * 8))) return rc;
   if ((rc = c->ensure(d.gathf, size_t(world) * kFinalWords * 8))) return rc;
@@ -1965,16 +1965,30 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       G_HIP(hipEventCreate(&cx->ev_stop));
     }
     G_HIP(hipEventRecord(cx->ev_start, cx->stream));
+    // the build's zeroed state in one launch: the header and look-back descriptors, the schedule's
+    // header, K2's look-back words and the C / D slots (their sizes are the plan's)
+    const u64 p = P.count(r, 1);
+    const u32 nb = u32(std::max<u64>(1, (p + kTile - 1) / kTile));
+    const size_t cd = (size_t(R) * kFlSeg * 8 + 15) & ~size_t(15), fd = (u64(nb) * R * 8 + 64 + 15) & ~u64(15);
+    if (cx->ensure(d.fl_desc, fd) || cx->ensure(d.scval, cd) || cx->ensure(d.rdval, cd))
+      return dev_fail("fused schedule buffers");
     InitPlan ip{};
     ip.hdr = cx->hdr.as<Header>();
     ip.desc = cx->desc.as<uint4>();
     ip.ndesc16 = cx->desc.bytes / 16;
-    hipLaunchKernelGGL(k_build_init, dim3(unsigned(std::min<u64>(1024, std::max<u64>(1, (ip.ndesc16 + kBlock - 1) / kBlock)))),
+    ip.zero[0] = d.dhdr.as<uint4>();
+    ip.nzero16[0] = kDistHdrBytes / 16;
+    ip.zero[1] = d.fl_desc.as<uint4>();
+    ip.nzero16[1] = fd / 16;
+    ip.zero[2] = d.scval.as<uint4>();
+    ip.nzero16[2] = cd / 16;
+    ip.zero[3] = d.rdval.as<uint4>();
+    ip.nzero16[3] = cd / 16;
+    const u64 big = std::max<u64>({ip.ndesc16, ip.nzero16[1], ip.nzero16[2]});
+    hipLaunchKernelGGL(k_build_init, dim3(unsigned(std::min<u64>(1024, std::max<u64>(1, (big + kBlock - 1) / kBlock)))),
                        dim3(kBlock), 0, cx->stream, ip);
     G_HIP(hipGetLastError());
     Header* h = cx->hdr.as<Header>();
-    DistHdr* dh = d.dhdr.as<DistHdr>();
-    G_HIP(hipMemsetAsync(dh, 0, sizeof(DistHdr), cx->stream));
     LeafLevel& la = las[i];
     la.bases = bases[i];
     la.leaves = d_leaves ? d_leaves[i] : nullptr;
@@ -1990,8 +2004,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     cx->probe_ranks = 1;
     if (rc) return rc == GCZ_ERR_DEVICE ? dev_fail("dense leaves") : rc;
     if (!used) return GCZ_OK;   // (sizes outside the dense level: the same on every rank)
-    const u64 n = la.S, p = P.count(r, 1);
-    const u32 nb = u32(std::max<u64>(1, (p + kTile - 1) / kTile));
+    const u64 n = la.S;
     RecSrc& rs = fl_rs[i];
     rs = RecSrc{};
     rs.pre = cx->dl_pw.as<u32>();
@@ -2015,10 +2028,8 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
       if (cx->ensure(d.skey_hi, u64(R) * cap * 2 + 16)) return dev_fail("fused schedule buffers");
     }
     // the send buffer: R regions of cap records; the look-back descriptors and their ticket
-    if (cx->ensure(d.skey, u64(R) * cap * 8 + 16) || cx->ensure(d.sidx, u64(R) * cap * 4 + 16) ||
-        cx->ensure(d.fl_desc, u64(nb) * R * 8 + 64))
+    if (cx->ensure(d.skey, u64(R) * cap * 8 + 16) || cx->ensure(d.sidx, u64(R) * cap * 4 + 16))
       return dev_fail("fused schedule buffers");
-    G_HIP(hipMemsetAsync(d.fl_desc.ptr, 0, u64(nb) * R * 8 + 64, cx->stream));
   }
   fl_mark("C1");
   for (int i = 0; i < NL; ++i) {   // C2: the keys scattered by owner (K2's input), the owner totals
@@ -2177,8 +2188,7 @@ int gcz_group::build_fast(const std::vector<const unsigned char*>& bases, const 
     ot.B = child_bits;
     ot.sh = u32(R) + 2;
     ot.nolocal = 1;
-    G_HIP(hipMemsetAsync(d.scval.ptr, 0, cd, cx->stream));   // C / D slot counts (and records)
-    G_HIP(hipMemsetAsync(d.rdval.ptr, 0, cd, cx->stream));
+    // (the C / D slot counts and records, scval and rdval, were zeroed by C1's k_build_init)
   }
   // ---- K2: layer-0 keys to their owners, a bulk group beside the build's stream
   {

@@ -57,6 +57,7 @@ struct DistHdr {
   u64 fl_leaf[3];                       // this rank's leaf id offset, r-first count, all ranks' total
   u32 fl_bad;                           // a C / D slot overflowed
 };
+constexpr size_t kDistHdrBytes = (sizeof(DistHdr) + 15) & ~size_t(15);   // (its buffer: whole 16-B stores)
 
 struct Displ {   // segment starts of the R source (or destination) ranks in a buffer, plus the end
   u64 d[kMaxRanks + 1];
