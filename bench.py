@@ -81,7 +81,7 @@ def dense_buckets(C):
 
 
 def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None, bucketed_pairs=0, two_pass=False,
-                      launches=None):
+                      launches=None, repetitive=False):
     """Algorithmic HBM bytes of all launches of `kernel` in one build:
     streamed bytes + one 64-B sector per random table/group access.  The per-level kernels
     (flagscan_node, resolve_node) count only the levels they ran on: the first `launches`
@@ -112,13 +112,13 @@ def algorithmic_bytes(kernel, L, S, n_leaves, layer_sizes, hashed_pairs=None, bu
     if kernel == "bucket_scan":     # exclusive scan of the count matrix
         return 8 * (bp // 3072 + 1) * ((bp >> 16) + 1)
     if two_pass and kernel == "bucket_scatter":   # two-pass partition, pass 1 (k_bkt_part): EVERY pair of
-        # the levels it ran on streams through it -- pair (8) and both children's marks (4) in, the
-        # provisional word (4) and its own two marks (2) out -- and each bucketed pair appends an 8-B
-        # record to a coarse run (round 5 charged the records' pairs only, which made the
-        # repetitive config's counter bytes look 2.6x the algorithmic ones: the read / write split
-        # of profiles/r06 matches the stream below)
-        pp = sum(pk[:launches]) if launches is not None else bp
-        return 18 * max(pp, bp) + 8 * bp
+        # the levels it ran on streams through it -- pair (8) and, above layer 0, both children's
+        # marks (4) in; with the block collapse (repetitive data) the provisional word (4), and its
+        # own two marks (2) out -- and each bucketed pair appends an 8-B record to a coarse run
+        # (round 5 charged the records' pairs only, which made the repetitive config's counter bytes
+        # look 2.6x the algorithmic ones: the read / write split of profiles/r06 matches this stream)
+        lv = pk[:launches] if launches is not None else pk[:1]
+        return sum(p * (8 + (4 if k else 0) + (4 if repetitive else 0) + 2) for k, p in enumerate(lv)) + 8 * bp
     if kernel == "bucket_fine":     # pass 2: records in, re-encoded records out (LDS-sorted slices)
         return 16 * bp
     if kernel == "bucket_scatter":  # pair in, word out, one 8-B record store (a 64-B sector) per pair
@@ -576,7 +576,7 @@ def main():
             b = algorithmic_bytes(name, L, S, info["n_leaves"], info["layer_size"], info["hashed_pairs"],
                                   info.get("bucketed_pairs", 0),
                                   two_pass=prof.get("bucket_fine", {}).get("launches", 0) > 0,
-                                  launches=p["launches"])
+                                  launches=p["launches"], repetitive=bool(info.get("repetitive")))
         kernels[name] = {"launches": p["launches"], "total_ms": round(p["total_ms"], 4),
                          "avg_ms": p["total_ms"] / p["launches"], "alg_bytes": b,
                          "gbs": b / (p["total_ms"] * 1e-3) / 1e9 if p["total_ms"] > 0 else None}

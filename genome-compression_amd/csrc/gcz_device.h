@@ -1744,7 +1744,21 @@ struct Bkt2Plan {
   u32 wave1;           // k_bkt_part collapse: a wave of one key touches the table once (GCZ_PART_WAVE)
   u32* redo;           // k_bkt_dedupe_bm: buckets over its capacity, for k_bkt_dedupe2_redo (null: the
   u32* redo_cnt;       // overflow flag instead), appended at this cursor
+  // single device (not the owners): the level's input words.  Without the block collapse
+  // (hdr->predup == 0) k_bkt_part writes no provisional word; the dedupes take a repeat's
+  // m / t / v bits from its pair instead (first occurrences get theirs from the flag scan)
+  const u32* in;
+  u64 n;
 };
+
+// m / t / v bits of repeat `pos` of a two-pass level, for its word (first position | bits)
+__device__ __forceinline__ u32 repeat_bits(const Bkt2Plan& bp, const u32* rec, u32 pos, bool collapse) {
+  if (!bp.in || collapse) return rec[pos] & kBits;
+  u32 l, r, cl, cr, m, t;
+  load_pair(bp.in, bp.n, pos, l, r);
+  node_canonical(l, r, cl, cr, m, t);
+  return make_word(0, m, t, ulw(l) == ulw(xf(r, 1, 0)));
+}
 
 // Append the not-first positions of a wave to bp.nfl (one atomic per wave; none once the
 // list is over its cap -- the count then only tells the flag scan to take the look-back path).
@@ -1867,7 +1881,7 @@ constexpr u32 kColSlots = 8192;   // its LDS table (load <= 1/2), in the part's 
       u64 key;
       u32 bits;
       if (bkt_pair(in, n, j, prev_nf, prev_multi, kp, key, bits)) place(e, j, key);
-      rec[j] = bits;
+      if (!bp.in) rec[j] = bits;
     }
   } else {
     // each block's repeats onto its earliest occurrence of the key; the next block's pairs
@@ -2102,6 +2116,7 @@ __device__ __forceinline__ void dedupe2_bucket(u32 bucket, const u64* __restrict
                                                Bkt2Plan bp, u32* __restrict__ rec, Marks mk, Header* __restrict__ hdr,
                                                u32* __restrict__ ovf) {
   constexpr u32 TS = kBktSlots;
+  const bool collapse = !kOwner && hdr && hdr->predup != 0;   // (repeat_bits: the provisional words exist)
   __shared__ u64 s_key[TS];
   __shared__ u32 s_pos[TS];
   __shared__ u32 s_dup[TS / 32];
@@ -2209,7 +2224,7 @@ __device__ __forceinline__ void dedupe2_bucket(u32 bucket, const u64* __restrict
           if (bp.olist && pos != first) bp.olist[atomicAdd(bp.ocnt, 1u)] = pos;
         } else if (pos != first) {
           mk.nf[pos] = kNfNot;
-          rec[pos] = first | (rec[pos] & kBits);
+          rec[pos] = first | repeat_bits(bp, rec, pos, collapse);
         } else {
           mk.multi[pos] = 1;
         }
@@ -2275,7 +2290,7 @@ __device__ __forceinline__ void dedupe2_bucket(u32 bucket, const u64* __restrict
       if (bp.olist && pos[e] != first) bp.olist[atomicAdd(bp.ocnt, 1u)] = pos[e];
     } else if (pos[e] != first) {
       mk.nf[pos[e]] = kNfNot;
-      rec[pos[e]] = first | (rec[pos[e]] & kBits);
+      rec[pos[e]] = first | repeat_bits(bp, rec, pos[e], collapse);
     } else {
       mk.multi[pos[e]] = 1;
     }
@@ -2330,6 +2345,7 @@ __global__ __launch_bounds__(kBmThreads) void k_bkt_dedupe_bm(const u64* __restr
                                                              u32* __restrict__ ovf) {
   if (bkt2_skip(hdr, prev_count, n)) return;
   if (!kOwner && hdr->predup) bp.nfl = nullptr;   // (as k_bkt_dedupe2: collapsed levels take the look-back path)
+  const bool collapse = !kOwner && hdr->predup != 0;   // (repeat_bits: the provisional words exist)
   __shared__ u32 s_seen[(1u << kBmLog) / 32], s_twice[(1u << kBmLog) / 32];
   __shared__ u64 s_key[kBmSlots];
   __shared__ u32 s_pos[kBmSlots];
@@ -2467,7 +2483,7 @@ __global__ __launch_bounds__(kBmThreads) void k_bkt_dedupe_bm(const u64* __restr
       if (bp.olist && pos[e] != first) bp.olist[atomicAdd(bp.ocnt, 1u)] = pos[e];
     } else if (pos[e] != first) {
       mk.nf[pos[e]] = kNfNot;
-      rec[pos[e]] = first | (rec[pos[e]] & kBits);
+      rec[pos[e]] = first | repeat_bits(bp, rec, pos[e], collapse);
     } else {
       mk.multi[pos[e]] = 1;
     }
