@@ -461,6 +461,7 @@ int gcz_ctx::node_level(const NodeLevel& a, Header* d_hdr) {
   // and the dedupe lists the level's not-first positions for the sparse flag scan
   b2.wmarks = two && part_marks ? 1u : 0u;
   b2.wave1 = part_wave ? 1u : 0u;
+  b2.xcd = bkt_xcd;
   if (two && !a.fused && part_words_off) {   // (no provisional words on collapse-free levels)
     b2.in = a.in;
     b2.n = n;
@@ -1089,6 +1090,7 @@ int gcz_ctx_create(int device, gcz_ctx** out) {
   if (const char* t = std::getenv("GCZ_DEDUPE_BM")) c->dedupe_bm = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_DL_FBW")) c->dl_fbw_on = std::atoi(t) != 0;
   if (const char* t = std::getenv("GCZ_PART_WORDS")) c->part_words_off = std::atoi(t) == 0;
+  if (const char* t = std::getenv("GCZ_BKT_XCD")) c->bkt_xcd = u32(std::strtoul(t, nullptr, 10));
   if (const char* t = std::getenv("GCZ_DL_XCD")) c->dl_xcd = u32(std::strtoul(t, nullptr, 10));
   if (const char* t = std::getenv("GCZ_DENSE_NB")) c->dense_nb = u32(std::strtoul(t, nullptr, 10));
   if (const char* t = std::getenv("GCZ_TABLE")) c->force_wide = std::strcmp(t, "wide") == 0;

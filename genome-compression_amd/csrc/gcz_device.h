@@ -1749,6 +1749,7 @@ struct Bkt2Plan {
   // m / t / v bits from its pair instead (first occurrences get theirs from the flag scan)
   const u32* in;
   u64 n;
+  u32 xcd;             // XCD-contiguous workgroup order: bit 1 k_bkt_dedupe_bm, bit 2 k_bkt_fine (GCZ_BKT_XCD)
 };
 
 // m / t / v bits of repeat `pos` of a two-pass level, for its word (first position | bits)
@@ -2033,7 +2034,19 @@ constexpr u32 kColSlots = 8192;   // its LDS table (load <= 1/2), in the part's 
   __shared__ u32 s_w[2];
   __shared__ u32 hist[(1u << kFineMaxB2) + 1];
   const u32 nb1 = 1u << bp.b1, nb2 = 1u << bp.b2;
-  const u32 c = blockIdx.x / bp.nslice, sl = blockIdx.x % bp.nslice;
+  // bp.xcd bit 2: workgroups taken slice-major in XCD-contiguous runs, so the coarse buckets c and
+  // c + 1 of one slice -- adjacent runs of the same chunks, run-table entries on one line -- are
+  // read through one L2 (the output stays at (c * nslice + slice))
+  u32 c, sl;
+  if (bp.xcd & 2u) {
+    const u32 b = u32(bkt_chunk(gridDim.x));
+    sl = b / nb1;
+    c = b % nb1;
+  } else {
+    c = blockIdx.x / bp.nslice;
+    sl = blockIdx.x % bp.nslice;
+  }
+  const u64 wg = u64(c) * bp.nslice + sl;
   const u64 g0 = u64(sl) * bp.SC;
   const u32 nsc = u32(g0 + bp.SC <= bp.G ? bp.SC : bp.G - g0);
   {   // run (chunk g0 + t, bucket c): one lane each, a two-wave scan of the lengths
@@ -2059,7 +2072,7 @@ constexpr u32 kColSlots = 8192;   // its LDS table (load <= 1/2), in the part's 
   for (u32 q = threadIdx.x; q < nb2; q += kBktThreads) hist[q] = 0;
   __syncthreads();
   const u32 total = s_pre[nsc];
-  u32* fos = fo + u64(blockIdx.x) * (nb2 + 1);
+  u32* fos = fo + wg * (nb2 + 1);
   if (total > u32(kFineCap)) {   // a hot key the probe missed: the table path handles this data
     if (threadIdx.x == 0) *ovf = 1;
     for (u32 q = threadIdx.x; q <= nb2; q += kBktThreads) fos[q] = 0;
@@ -2101,7 +2114,7 @@ constexpr u32 kColSlots = 8192;   // its LDS table (load <= 1/2), in the part's 
     if (slot[e] != ~0u) stage[hist[slot[e] >> 16] + (slot[e] & 0xffffu)] = r[e];
   for (u32 q = threadIdx.x; q <= nb2; q += kBktThreads) fos[q] = hist[q];
   __syncthreads();
-  u64* o = out + u64(blockIdx.x) * kFineCap;
+  u64* o = out + wg * kFineCap;
   for (u32 i = threadIdx.x; i < total; i += kBktThreads) o[i] = stage[i];
 }
 
@@ -2355,7 +2368,11 @@ __global__ __launch_bounds__(kBmThreads) void k_bkt_dedupe_bm(const u64* __restr
   __shared__ u32 s_wt[kBmThreads / 64];
   __shared__ u32 s_full;
   const u32 nb2 = 1u << bp.b2;
-  const u32 c = blockIdx.x >> bp.b2, f = blockIdx.x & (nb2 - 1);
+  // bp.xcd: the 8 XCDs (workgroups dealt round-robin) each take a contiguous run of buckets, so
+  // neighbouring buckets -- whose fine offsets share lines and whose runs meet in every slice --
+  // are read through one L2
+  const u32 bucket = (bp.xcd & 1u) ? u32(bkt_chunk(gridDim.x)) : u32(blockIdx.x);
+  const u32 c = bucket >> bp.b2, f = bucket & (nb2 - 1);
   const u32 ns = bp.nslice;
   const u32 t = threadIdx.x, lane = t & 63, wave = t >> 6;
   {   // this bucket's run in every slice (two slices a thread), block exclusive scan of the lengths
@@ -2400,7 +2417,7 @@ __global__ __launch_bounds__(kBmThreads) void k_bkt_dedupe_bm(const u64* __restr
   const u32 total = s_pre[ns];
   auto hand_back = [&] {   // (nothing of this bucket written yet)
     if (t == 0) {
-      if (!kOwner && bp.redo) bp.redo[atomicAdd(bp.redo_cnt, 1u)] = blockIdx.x;
+      if (!kOwner && bp.redo) bp.redo[atomicAdd(bp.redo_cnt, 1u)] = bucket;
       else *ovf = 1;
     }
   };

@@ -262,7 +262,8 @@ def test_gpu_large_synth_goldens(name, ctx, gcz, manifest):
                                  {"GCZ_DENSE_NB": "1024"}, {"GCZ_DENSE_NB": "1024", "GCZ_DENSE": "2"},
                                  {"GCZ_DENSE": "2", "GCZ_DL_XCD": "0"}, {"GCZ_DENSE": "2", "GCZ_DL_XCD": "15"},
                                  {"GCZ_DENSE": "2", "GCZ_DL_FBW": "0"}, {"GCZ_PART_WORDS": "1", "GCZ_BUCKET_MIN": "1"},
-                                 {"GCZ_BUCKET_MIN": "1", "GCZ_PREDUP": "2", "GCZ_DEDUPE_BM": "0"}])
+                                 {"GCZ_BUCKET_MIN": "1", "GCZ_PREDUP": "2", "GCZ_DEDUPE_BM": "0"},
+                                 {"GCZ_BUCKET_MIN": "1", "GCZ_BKT_XCD": "0"}])
 def test_gpu_schedule_knobs_same_tree(env, gcz, manifest):
     """The per-level fallbacks (no direct subtrees, no fused top, tight tables, a leaf
     table that overflows and regrows) build the same tree as the default schedule."""
