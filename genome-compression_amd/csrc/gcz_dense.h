@@ -377,10 +377,17 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int G = 16;   // chunks per wave step
   const u64 row = u64(b) * P.nch;
+  // run starts of chunks ch0.., and the end; the next step's are loaded with this step's records
+  auto starts = [&](u32 ch0) {
+    const u32 nc = P.nch - ch0 < u32(G) ? P.nch - ch0 : u32(G);
+    return lane <= int(nc) ? off[row + ch0 + lane] : 0u;
+  };
+  u32 bnd = u32(wave) * G < P.nch ? starts(u32(wave) * G) : 0u;
   for (u32 ch0 = u32(wave) * G; ch0 < P.nch; ch0 += (kDThreads / 64) * G) {
     const u32 nc = P.nch - ch0 < u32(G) ? P.nch - ch0 : u32(G);
-    const u32 bnd = lane <= int(nc) ? off[row + ch0 + lane] : 0u;   // run starts of chunks ch0.., and the end
     const u32 r0 = __shfl(bnd, 0, 64), r1 = __shfl(bnd, int(nc), 64);
+    const u32 nxt = ch0 + (kDThreads / 64) * G;
+    const u32 bnd_next = nxt < P.nch ? starts(nxt) : 0u;
     u32 st[G];   // run starts of the group's chunks (past nc: never <= a record index)
 #pragma unroll
     for (int g = 1; g < G; ++g) {
@@ -404,6 +411,7 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
         f(x[j], rj, ((ch0 + c) << kDLog) | (x[j] & (kDC - 1)));
       }
     }
+    bnd = bnd_next;
   }
 }
 
@@ -417,7 +425,7 @@ static __device__ __forceinline__ void bucket_records(const u32* __restrict__ re
 // and the probe before this launch).
 // rfc (rank 0 of the fused multi-rank schedule, whose r-first codes are all its codes): also
 // k_dl_rfirst's code-order list and per-bucket count (rfc[b * RB + j], bcnt[b]); fpg may be null.
-[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) void k_dl_first(const u32* __restrict__ rec, const u32* __restrict__ off,
+[[maybe_unused]] static __global__ __launch_bounds__(kDThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_dl_first(const u32* __restrict__ rec, const u32* __restrict__ off,
                                                         DensePlan P, u32* __restrict__ fpg, u32* __restrict__ fl,
                                                         u32* __restrict__ fo, unsigned long long* __restrict__ pb,
                                                         const Header* __restrict__ hdr = nullptr,
