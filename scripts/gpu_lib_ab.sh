@@ -1,6 +1,6 @@
 # A/B of two builds of libgcz on the default bench (per-kernel times from the line's hipEvent
 # profile): ab/libgcz_base.so (a saved earlier build) against the tree's libgcz.so, two runs each.
-# usage: bash scripts/gpu_lib_ab.sh <tag> [bench args]
+# usage: bash scripts/gpu_lib_ab.sh <tag> [bench args]; AB_EXTRA="x y" also runs ab/libgcz_x.so ...
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -8,8 +8,8 @@ tag=$1; shift
 mkdir -p gpurun_out
 lib=genome-compression_amd/libgcz.so
 cp $lib /tmp/libgcz_new.so
-for v in base new; do
-  if [ $v = base ]; then cp ab/libgcz_base.so $lib; else cp /tmp/libgcz_new.so $lib; fi
+for v in base new $AB_EXTRA; do
+  if [ $v = new ]; then cp /tmp/libgcz_new.so $lib; else cp ab/libgcz_$v.so $lib; fi
   for rep in 1 2; do
     timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --build-only "$@" > gpurun_out/lab_${tag}_${v}_$rep.json 2> gpurun_out/lab_${tag}_${v}_$rep.err || { tail -5 gpurun_out/lab_${tag}_${v}_$rep.err; cp /tmp/libgcz_new.so $lib; exit 1; }
     python3 - "$v" gpurun_out/lab_${tag}_${v}_$rep.json <<'PY'
