@@ -583,17 +583,33 @@ static __device__ __forceinline__ u32 fbw_rank(const uint4* __restrict__ fbw, u3
   extern __shared__ u32 s_id[];
   const int tid = threadIdx.x;
   const u32 b = blockIdx.x, RB = 1u << P.IB;
-  for (u32 i0 = 0; i0 < RB; i0 += kDThreads * kDBatch) {
-    u32 fp[kDBatch];
+  constexpr int kFill = 16;   // codes per thread in flight (RB <= 16 Ki: one step)
+  for (u32 i0 = 0; i0 < RB; i0 += kDThreads * kFill) {
+    u32 fp[kFill];
 #pragma unroll
-    for (int j = 0; j < kDBatch; ++j) {
+    for (int j = 0; j < kFill; ++j) {
       const u32 i = i0 + u32(j) * kDThreads + tid;
       fp[j] = i < RB ? (gid ? gid : fpg)[u64(b) * RB + i] : ~0u;
     }
+    if (fbw && !gid) {   // 8 ranks' lines in flight before the first is used (absent: line 0, unused)
 #pragma unroll
-    for (int j = 0; j < kDBatch; ++j) {
+      for (int h = 0; h < kFill; h += 8) {
+        uint4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fbw[fp[h + j] == ~0u ? 0u : fp[h + j] >> 6];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const u32 i = i0 + u32(h + j) * kDThreads + tid, p = fp[h + j];
+          const unsigned long long w = (u64(v[j].y) << 32) | v[j].x;
+          if (i < RB) s_id[i] = p == ~0u ? 0u : v[j].z + u32(__popcll(w & ((1ull << (p & 63)) - 1ull)));
+        }
+      }
+      continue;
+    }
+#pragma unroll
+    for (int j = 0; j < kFill; ++j) {
       const u32 i = i0 + u32(j) * kDThreads + tid;
-      if (i < RB) s_id[i] = gid ? fp[j] : fp[j] == ~0u ? 0u : fbw ? fbw_rank(fbw, fp[j]) : fb_rank(fb, wpre, fp[j]);
+      if (i < RB) s_id[i] = gid ? fp[j] : fp[j] == ~0u ? 0u : fb_rank(fb, wpre, fp[j]);
     }
   }
   __syncthreads();
@@ -645,10 +661,9 @@ static __device__ __forceinline__ void dl_words_chunk(const u32* __restrict__ re
   chunk_runs(offt, P, ch, s_base, s_dst, s_tmp);
   const int lane = tid & 63, wave = tid >> 6;
   const u32 IB = P.IB, imask = (1u << IB) - 1u;
-  auto place = [&](u32 b, u32 xr, u32 wr) {   // one record: its word into position order, its leaf
+  auto leaf = [&](u32 b, u32 xr, u32 wr) {   // one record at a first occurrence: its leaf
     const u32 q = xr & (kDC - 1);
-    s_w[q] = wr;
-    if (leaves_out && ((s_fb[q >> 5] >> (q & 31)) & 1u)) {
+    if ((s_fb[q >> 5] >> (q & 31)) & 1u) {
       const u32 h = (b << IB) | (((xr & kIdx) >> kDLog) & imask);
       leaves_out[(wr & kIdx) - leaf_off] = code2_leaf((h * P.Kinv) & P.hmask, P.L);
     }
@@ -681,9 +696,17 @@ static __device__ __forceinline__ void dl_words_chunk(const u32* __restrict__ re
           bq[q] = b;
         }
       }
+      // the loads waited for once, unconditionally: waits inside the per-record branches below
+      // also waited for the leaf stores issued before them (one vmcnt for loads and stores)
+#pragma unroll
+      for (int q = 0; q < GW; ++q) asm volatile("" ::"v"(x[q]), "v"(w[q]));
 #pragma unroll
       for (int q = 0; q < GW; ++q)
-        if (bq[q] != ~0u) place(bq[q], x[q], w[q]);
+        if (bq[q] != ~0u) s_w[x[q] & (kDC - 1)] = w[q];
+      if (leaves_out)
+#pragma unroll
+        for (int q = 0; q < GW; ++q)
+          if (bq[q] != ~0u) leaf(bq[q], x[q], w[q]);
     }
     __syncthreads();
     emit(s_w, n, c0);
